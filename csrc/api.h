@@ -1,0 +1,78 @@
+// Host-side launch API of the fluxmpi_amd native library (no ATen dependency:
+// raw device pointers + a hipStream_t, so callers can launch on any PyTorch
+// stream, inside or outside HIP-graph capture).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <vector>
+
+namespace fluxmpi {
+
+// ---- multi-tensor copy / cast / scale (pack, unpack, scale) -----------------
+// dst[i][k] = (Tout)(src[i][k] * scale) for k < numel[i]. src[i] may equal dst[i]
+// (in-place scale / cast is not allowed when the element sizes differ).
+void mt_copy(const std::vector<uintptr_t>& src, const std::vector<uintptr_t>& dst,
+             const std::vector<int64_t>& numel, int in_dtype, int out_dtype, float scale,
+             hipStream_t stream);
+
+// Fill every tensor with `value` (zeroing flat grad buckets).
+void mt_fill(const std::vector<uintptr_t>& dst, const std::vector<int64_t>& numel, int dtype,
+             float value, hipStream_t stream);
+
+// Sum of squares of all tensors into out[0] (fp32, atomically accumulated; out must be
+// zeroed by the caller). Used by ClipNorm and by debug checksums.
+void mt_sumsq(const std::vector<uintptr_t>& src, const std::vector<int64_t>& numel, int dtype,
+              float* out, hipStream_t stream);
+
+// ---- fused optimisers ---------------------------------------------------------
+struct AdamHyper {
+  float lr, beta1, beta2, eps;
+  float bc1, bc2;     // 1 - beta1^t, 1 - beta2^t (host mode)
+  float weight_decay;  // Optimisers.jl WeightDecay after Adam (AdamW = chain)
+  float grad_scale;    // multiplies the incoming gradient (e.g. 1/world for mean)
+  const float* dev;    // optional device hyper block {lr, beta1^t, beta2^t} (graph mode)
+  const float* dev_gscale;  // optional device gradient scale (e.g. 1/loss_scale)
+};
+
+// master: optional fp32 master weights (mixed precision); when given, param is
+// the low-precision copy that is re-written from the master after the update.
+void mt_adam(const std::vector<uintptr_t>& param, const std::vector<uintptr_t>& grad,
+             const std::vector<uintptr_t>& m, const std::vector<uintptr_t>& v,
+             const std::vector<uintptr_t>& master, const std::vector<int64_t>& numel,
+             int p_dtype, int g_dtype, int s_dtype, const AdamHyper& h, hipStream_t stream);
+
+// dev[1] *= beta1, dev[2] *= beta2 (advance the bias-correction powers on device).
+void adam_advance(float* dev, float beta1, float beta2, hipStream_t stream);
+
+struct SgdHyper {
+  float lr, momentum, weight_decay, grad_scale;
+  int nesterov;  // 0: heavy ball (Optimisers.Momentum), 1: Optimisers.Nesterov
+  const float* dev_lr;
+};
+// buf: momentum buffers (ignored when momentum == 0 -> Optimisers.Descent).
+void mt_sgd(const std::vector<uintptr_t>& param, const std::vector<uintptr_t>& grad,
+            const std::vector<uintptr_t>& buf, const std::vector<uintptr_t>& master,
+            const std::vector<int64_t>& numel, int p_dtype, int g_dtype, int s_dtype,
+            const SgdHyper& h, hipStream_t stream);
+
+// ---- BatchNorm (NHWC, channels innermost) + ReLU / residual-add fusions ----------
+// Training forward: per-channel batch statistics over rows = N*H*W, then
+//   y = act(x * scale_c + shift_c [+ residual]).
+// Writes mean/invstd (fp32 [C]) for the backward and updates running stats.
+void bn_fwd_train(const void* x, void* y, const void* residual, const float* weight,
+                  const float* bias, float* running_mean, float* running_var, float* save_mean,
+                  float* save_invstd, float* workspace, int64_t rows, int64_t C, float momentum,
+                  float eps, int relu, int dtype, hipStream_t stream);
+// Backward: given dy (and y when relu, to mask), computes dx, dweight, dbias and
+// (when residual was fused) d_residual = masked dy.
+void bn_bwd(const void* dy, const void* x, const void* y, const float* weight,
+            const float* save_mean, const float* save_invstd, void* dx, void* dres,
+            float* dweight, float* dbias, float* workspace, int64_t rows, int64_t C, int relu,
+            int dtype, hipStream_t stream);
+size_t bn_workspace_floats(int64_t rows, int64_t C);
+// Inference: y = act(x * scale + shift [+ residual]) from running statistics.
+void bn_fwd_infer(const void* x, void* y, const void* residual, const float* weight,
+                  const float* bias, const float* running_mean, const float* running_var,
+                  int64_t rows, int64_t C, float eps, int relu, int dtype, hipStream_t stream);
+
+}  // namespace fluxmpi

@@ -1,0 +1,84 @@
+// pybind11 bindings of the fluxmpi_amd native library -> module `fluxmpi_amd._C`.
+//
+// Pointers and streams cross the boundary as integers (tensor.data_ptr(),
+// torch.cuda.Stream.cuda_stream), which keeps this module independent of the
+// ATen C++ ABI and lets it launch on any stream, including during HIP-graph
+// capture.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "api.h"
+#include "comm/rccl_comm.h"
+
+namespace py = pybind11;
+using namespace fluxmpi;
+
+static hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "fluxmpi_amd native library: gfx950 HIP kernels + RCCL communicator";
+
+  m.def("mt_copy",
+        [](const std::vector<uintptr_t>& src, const std::vector<uintptr_t>& dst, const std::vector<int64_t>& numel,
+           int in_dtype, int out_dtype, float scale, uintptr_t stream) {
+          mt_copy(src, dst, numel, in_dtype, out_dtype, scale, S(stream));
+        },
+        py::arg("src"), py::arg("dst"), py::arg("numel"), py::arg("in_dtype"), py::arg("out_dtype"),
+        py::arg("scale"), py::arg("stream"));
+  m.def("mt_fill",
+        [](const std::vector<uintptr_t>& dst, const std::vector<int64_t>& numel, int dtype, float value,
+           uintptr_t stream) { mt_fill(dst, numel, dtype, value, S(stream)); });
+  m.def("mt_sumsq",
+        [](const std::vector<uintptr_t>& src, const std::vector<int64_t>& numel, int dtype, uintptr_t out,
+           uintptr_t stream) { mt_sumsq(src, numel, dtype, reinterpret_cast<float*>(out), S(stream)); });
+
+  m.def("mt_adam",
+        [](const std::vector<uintptr_t>& p, const std::vector<uintptr_t>& g, const std::vector<uintptr_t>& mm,
+           const std::vector<uintptr_t>& vv, const std::vector<uintptr_t>& master, const std::vector<int64_t>& numel,
+           int p_dtype, int g_dtype, int s_dtype, float lr, float beta1, float beta2, float eps, float bc1,
+           float bc2, float weight_decay, float grad_scale, uintptr_t dev_hyper, uintptr_t dev_gscale,
+           uintptr_t stream) {
+          AdamHyper h{lr, beta1, beta2, eps, bc1, bc2, weight_decay, grad_scale,
+                      reinterpret_cast<const float*>(dev_hyper), reinterpret_cast<const float*>(dev_gscale)};
+          mt_adam(p, g, mm, vv, master, numel, p_dtype, g_dtype, s_dtype, h, S(stream));
+        },
+        py::arg("param"), py::arg("grad"), py::arg("m"), py::arg("v"), py::arg("master"), py::arg("numel"),
+        py::arg("p_dtype"), py::arg("g_dtype"), py::arg("s_dtype"), py::arg("lr"), py::arg("beta1"),
+        py::arg("beta2"), py::arg("eps"), py::arg("bc1"), py::arg("bc2"), py::arg("weight_decay"),
+        py::arg("grad_scale"), py::arg("dev_hyper"), py::arg("dev_gscale"), py::arg("stream"));
+  m.def("adam_advance", [](uintptr_t dev, float b1, float b2, uintptr_t stream) {
+    adam_advance(reinterpret_cast<float*>(dev), b1, b2, S(stream));
+  });
+  m.def("mt_sgd",
+        [](const std::vector<uintptr_t>& p, const std::vector<uintptr_t>& g, const std::vector<uintptr_t>& buf,
+           const std::vector<uintptr_t>& master, const std::vector<int64_t>& numel, int p_dtype, int g_dtype,
+           int s_dtype, float lr, float momentum, float weight_decay, float grad_scale, int nesterov,
+           uintptr_t dev_lr, uintptr_t stream) {
+          SgdHyper h{lr, momentum, weight_decay, grad_scale, nesterov, reinterpret_cast<const float*>(dev_lr)};
+          mt_sgd(p, g, buf, master, numel, p_dtype, g_dtype, s_dtype, h, S(stream));
+        },
+        py::arg("param"), py::arg("grad"), py::arg("buf"), py::arg("master"), py::arg("numel"),
+        py::arg("p_dtype"), py::arg("g_dtype"), py::arg("s_dtype"), py::arg("lr"), py::arg("momentum"),
+        py::arg("weight_decay"), py::arg("grad_scale"), py::arg("nesterov"), py::arg("dev_lr"),
+        py::arg("stream"));
+
+  // ---- RCCL ----------------------------------------------------------------
+  m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
+  m.def("rccl_version", &rccl_version);
+  py::class_<RcclComm>(m, "RcclComm")
+      .def(py::init<const std::string&, int, int, int>(), py::call_guard<py::gil_scoped_release>())
+      .def("allreduce", &RcclComm::allreduce, py::call_guard<py::gil_scoped_release>())
+      .def("allreduce_many", &RcclComm::allreduce_many, py::call_guard<py::gil_scoped_release>())
+      .def("broadcast", &RcclComm::broadcast, py::call_guard<py::gil_scoped_release>())
+      .def("reduce", &RcclComm::reduce, py::call_guard<py::gil_scoped_release>())
+      .def("allgather", &RcclComm::allgather, py::call_guard<py::gil_scoped_release>())
+      .def("reduce_scatter", &RcclComm::reduce_scatter, py::call_guard<py::gil_scoped_release>())
+      .def("alltoall", &RcclComm::alltoall, py::call_guard<py::gil_scoped_release>())
+      .def("async_error", &RcclComm::async_error)
+      .def_static("error_string", &RcclComm::error_string)
+      .def("abort", &RcclComm::abort, py::call_guard<py::gil_scoped_release>())
+      .def("destroy", &RcclComm::destroy, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("size", &RcclComm::size)
+      .def_property_readonly("device", &RcclComm::device);
+}

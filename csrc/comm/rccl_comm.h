@@ -1,0 +1,45 @@
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace fluxmpi {
+
+std::string rccl_unique_id();
+int rccl_version();
+
+// Thin owner of an ncclComm_t; all operations are stream-ordered and async.
+class RcclComm {
+ public:
+  RcclComm(const std::string& uid, int rank, int size, int device);
+  ~RcclComm();
+  RcclComm(const RcclComm&) = delete;
+  RcclComm& operator=(const RcclComm&) = delete;
+
+  void allreduce(uintptr_t send, uintptr_t recv, size_t count, int dtype, int op, uintptr_t stream);
+  void allreduce_many(const std::vector<uintptr_t>& bufs, const std::vector<size_t>& counts,
+                      const std::vector<int>& dtypes, int op, uintptr_t stream);
+  void broadcast(uintptr_t send, uintptr_t recv, size_t count, int dtype, int root, uintptr_t stream);
+  void reduce(uintptr_t send, uintptr_t recv, size_t count, int dtype, int op, int root, uintptr_t stream);
+  void allgather(uintptr_t send, uintptr_t recv, size_t sendcount, int dtype, uintptr_t stream);
+  void reduce_scatter(uintptr_t send, uintptr_t recv, size_t recvcount, int dtype, int op, uintptr_t stream);
+  void alltoall(uintptr_t send, uintptr_t recv, size_t count_per_peer, int dtype, uintptr_t stream);
+  int async_error() const;
+  static std::string error_string(int code);
+  void abort();
+  void destroy();
+
+  int rank() const { return rank_; }
+  int size() const { return size_; }
+  int device() const { return device_; }
+
+ private:
+  void check_open() const;
+  static size_t dtype_size(int dtype);
+  void* comm_ = nullptr;
+  int rank_, size_, device_;
+};
+
+}  // namespace fluxmpi

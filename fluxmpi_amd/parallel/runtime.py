@@ -1,0 +1,308 @@
+"""Runtime / process group (L4 of SURVEY §1).
+
+Reference: ``src/common.jl`` — ``Init``, ``Initialized``, ``local_rank``,
+``total_workers`` and the rank-ordered ``fluxmpi_print[ln]``.
+
+MI355X design: one process per GPU. ``Init`` bootstraps from the launcher's
+environment (``torch.distributed.run``/our ``fluxmpi_amd.launch``: ``RANK``,
+``WORLD_SIZE``, ``LOCAL_RANK``; Open MPI / MPICH / Slurm variables are also
+understood so ``mpiexec -n N python script.py`` works like ``mpiexecjl``),
+pins the process to its GPU by *node-local* rank, and creates
+
+* a CPU ``gloo`` process group (host barriers, rank-ordered printing, CPU
+  tensors — the reference's CPU MPI path that its CI exercises), and
+* the device communicator: the native RCCL communicator (default) or a
+  ``torch.distributed`` RCCL group.
+
+Differences from the reference, on purpose:
+
+* Q3/Q4 (``src/common.jl:32-36``): the reference picks GPU
+  ``(global_rank + 1) % ndev``. We pick ``node_local_rank % ndev`` so rank 0
+  uses GPU 0 and multi-node jobs map correctly. ``gpu_devices`` still
+  overrides the choice exactly like the reference (``gpu_devices[rank]``).
+* ``local_rank()`` keeps the reference's meaning: the **global** rank.
+"""
+from __future__ import annotations
+
+import datetime as _dt
+import logging
+import os
+import socket
+import sys
+import threading
+import warnings
+from dataclasses import dataclass, field
+
+import torch
+import torch.distributed as dist
+
+from ..utils.config import get_config
+from ..utils.errors import FluxMPINotInitializedError
+from . import comm as _comm
+
+log = logging.getLogger("fluxmpi_amd")
+
+
+@dataclass
+class _State:
+    initialized: bool = False  # C1: never reset, even by Finalize (reference semantics)
+    finalized: bool = False
+    rank: int = 0
+    size: int = 1
+    node_rank: int = 0
+    node_size: int = 1
+    device: torch.device = field(default_factory=lambda: torch.device("cpu"))
+    owns_pg: bool = False
+    cpu_comm: _comm.Communicator | None = None
+    dev_comm: _comm.Communicator | None = None
+    backend: str = "cpu"
+    lock: threading.Lock = field(default_factory=threading.Lock)
+
+
+_S = _State()
+
+
+def _env_int(*names, default=None):
+    for n in names:
+        v = os.environ.get(n)
+        if v not in (None, ""):
+            try:
+                return int(v)
+            except ValueError:
+                pass
+    return default
+
+
+def _discover():
+    rank = _env_int("RANK", "OMPI_COMM_WORLD_RANK", "PMI_RANK", "PMIX_RANK", "MV2_COMM_WORLD_RANK",
+                    "SLURM_PROCID", default=0)
+    size = _env_int("WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE", "MV2_COMM_WORLD_SIZE",
+                    "SLURM_NTASKS", default=1)
+    node_rank = _env_int("LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID", "MV2_COMM_WORLD_LOCAL_RANK",
+                         "SLURM_LOCALID", default=None)
+    node_size = _env_int("LOCAL_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_SIZE", "MPI_LOCALNRANKS",
+                         "MV2_COMM_WORLD_LOCAL_SIZE", default=None)
+    if node_rank is None:
+        node_rank = rank  # single node assumption
+    if node_size is None:
+        node_size = size
+    return rank, size, node_rank, node_size
+
+
+def _is_loopback(addr: str) -> bool:
+    return addr in ("127.0.0.1", "localhost", "::1")
+
+
+def Initialized() -> bool:
+    """Has ``Init`` been called? (reference ``src/common.jl:6``)"""
+    return _S.initialized
+
+
+def Init(gpu_devices: list[int] | None = None, verbose: bool = False, backend: str | None = None,
+         timeout_s: float | None = None) -> None:
+    """Set up the process group and device (reference ``src/common.jl:16-45``).
+
+    Idempotent. ``gpu_devices[rank]`` selects the GPU explicitly; otherwise the
+    node-local rank round-robins over the visible GPUs. ``backend`` overrides
+    ``FLUXMPI_BACKEND`` (``auto``/``rccl``/``torch``/``gloo``).
+    """
+    if _S.initialized and not _S.finalized:
+        if verbose:
+            fluxmpi_println("FluxMPI already initialized; Skipping...")
+        return
+    cfg = get_config()
+    backend = (backend or cfg.backend or "auto").lower()
+    timeout = _dt.timedelta(seconds=timeout_s or cfg.timeout_s)
+    rank, size, node_rank, node_size = _discover()
+
+    # ---- host process group (gloo) ------------------------------------------
+    owns = False
+    if dist.is_available() and dist.is_initialized():
+        rank, size = dist.get_rank(), dist.get_world_size()
+        cpu_group = None
+        if dist.get_backend() != "gloo":
+            cpu_group = dist.new_group(backend="gloo")
+        cpu_comm = _comm.TorchComm(cpu_group, rank, size, "gloo")
+    elif size > 1:
+        addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+        port = os.environ.get("MASTER_PORT", "29500")
+        if _is_loopback(addr):
+            os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+        dist.init_process_group("gloo", init_method=f"tcp://{addr}:{port}", rank=rank, world_size=size,
+                                timeout=timeout)
+        owns = True
+        cpu_comm = _comm.TorchComm(None, rank, size, "gloo")
+    else:
+        cpu_comm = _comm.SelfComm()
+
+    _S.rank, _S.size, _S.node_rank, _S.node_size = rank, size, node_rank, node_size
+    _S.owns_pg = owns
+    _S.cpu_comm = cpu_comm
+    _S.initialized = True
+    _S.finalized = False
+
+    if verbose and size == 1:
+        warnings.warn("Using FluxMPI with only 1 worker. It might be faster to run the code without MPI",
+                      stacklevel=2)
+
+    # ---- device ------------------------------------------------------------
+    use_gpu = backend != "gloo" and torch.cuda.is_available() and torch.cuda.device_count() > 0
+    if use_gpu:
+        ndev = torch.cuda.device_count()
+        dev_index = gpu_devices[rank] if gpu_devices is not None else node_rank % ndev
+        torch.cuda.set_device(dev_index)
+        _S.device = torch.device("cuda", dev_index)
+        if verbose:
+            fluxmpi_println(f"Using GPU {dev_index}")
+        _S.dev_comm, _S.backend = _make_device_comm(backend, cfg, rank, size, _S.device, cpu_comm)
+    else:
+        _S.device = torch.device("cpu")
+        _S.dev_comm, _S.backend = None, "gloo" if size > 1 else "self"
+        if verbose:
+            fluxmpi_println("Using CPU")
+    log.info("fluxmpi_amd: rank %d/%d device %s backend %s", rank, size, _S.device, _S.backend)
+
+
+def _make_device_comm(backend, cfg, rank, size, device, cpu_comm):
+    if cfg.host_staged:
+        log.info("Device-direct collectives disabled using LocalPreferences.toml (host-staged path).")
+        return _comm.HostStagedComm(cpu_comm), "host-staged"
+    store = None
+    if size > 1:
+        store = dist.distributed_c10d._get_default_store()
+    if backend in ("auto", "rccl"):
+        try:
+            c = _comm.RcclComm(rank, size, device, store)
+            return c, "rccl"
+        except Exception as e:  # extension missing / RCCL init failure
+            if backend == "rccl":
+                raise
+            log.warning("native RCCL communicator unavailable (%r); using torch.distributed nccl", e)
+    if size == 1:
+        return _comm.SelfComm(), "self"
+    grp = dist.new_group(backend="nccl")
+    return _comm.TorchComm(grp, rank, size, "nccl"), "torch-nccl"
+
+
+def Finalize() -> None:
+    """Tear down communicators (``MPI.Finalize`` analogue).
+
+    Like the reference, :func:`Initialized` keeps returning ``True``
+    afterwards (``src/FluxMPI.jl:7``: nothing ever resets the flag).
+    """
+    if not _S.initialized or _S.finalized:
+        return
+    if _S.dev_comm is not None:
+        try:
+            _S.dev_comm.destroy()
+        except Exception as e:  # pragma: no cover
+            log.warning("error destroying device communicator: %r", e)
+    if _S.owns_pg and dist.is_initialized():
+        dist.destroy_process_group()
+    _S.finalized = True
+
+
+def Finalized() -> bool:
+    return _S.finalized
+
+
+def _require():
+    if not _S.initialized:
+        raise FluxMPINotInitializedError()
+
+
+def local_rank() -> int:
+    """Rank of this process in the world (reference ``src/common.jl:52-55``; *global* rank, Q4)."""
+    _require()
+    return _S.rank
+
+
+def total_workers() -> int:
+    """Number of processes (reference ``src/common.jl:64-67``)."""
+    _require()
+    return _S.size
+
+
+def node_local_rank() -> int:
+    _require()
+    return _S.node_rank
+
+
+def device() -> torch.device:
+    """The device this rank computes on (``cuda:k`` or ``cpu``)."""
+    _require()
+    return _S.device
+
+
+def backend_name() -> str:
+    _require()
+    return _S.backend
+
+
+def cpu_comm() -> _comm.Communicator:
+    _require()
+    return _S.cpu_comm
+
+
+def device_comm() -> _comm.Communicator:
+    _require()
+    return _S.dev_comm if _S.dev_comm is not None else _S.cpu_comm
+
+
+def comm_for(t) -> _comm.Communicator:
+    """Pick the communicator for a tensor's device."""
+    _require()
+    if _S.finalized:
+        raise RuntimeError("fluxmpi_amd has been finalized")
+    if isinstance(t, torch.Tensor) and t.is_cuda:
+        if _S.dev_comm is None:
+            if _S.size == 1:
+                return _comm.SelfComm()
+            raise RuntimeError("GPU tensor passed but fluxmpi_amd was initialised without a device backend")
+        return _S.dev_comm
+    return _S.cpu_comm
+
+
+def barrier() -> None:
+    _require()
+    _S.cpu_comm.barrier()
+
+
+# --------------------------------------------------------------------------- printing
+def _now() -> str:
+    # Julia's Dates.now(): 2024-01-31T12:34:56.789
+    return _dt.datetime.now().isoformat(timespec="milliseconds")
+
+
+def _fluxmpi_print(newline: bool, *args, **kwargs) -> None:
+    end = kwargs.pop("end", "\n" if newline else "")
+    sep = kwargs.pop("sep", "")  # Julia's print concatenates its arguments
+    file = kwargs.pop("file", sys.stdout)
+    if not _S.initialized:
+        print(f"{_now()} ", *args, sep=sep, end=end, file=file, **kwargs)
+        return
+    rank, size = _S.rank, _S.size
+    if size == 1:
+        print(*args, sep=sep, end=end, file=file, **kwargs)
+        return
+    # Rank-ordered output: `size` barriers per call, exactly like src/common.jl:86-92.
+    # This is a collective: every rank must call it (Q7).
+    for r in range(size):
+        if r == rank:
+            print(f"{_now()} [{rank} / {size}] ", *args, sep=sep, end=end, file=file, **kwargs)
+            file.flush()
+        _S.cpu_comm.barrier()
+
+
+def fluxmpi_println(*args, **kwargs) -> None:
+    """Print with a timestamp and ``[rank / size]`` prefix, in rank order (collective)."""
+    _fluxmpi_print(True, *args, **kwargs)
+
+
+def fluxmpi_print(*args, **kwargs) -> None:
+    """Like :func:`fluxmpi_println` without the trailing newline."""
+    _fluxmpi_print(False, *args, **kwargs)
+
+
+def hostname() -> str:
+    return socket.gethostname()

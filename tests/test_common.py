@@ -1,0 +1,43 @@
+"""Mirror of reference test/test_common.jl (Init / rank / size / printing / Finalize)."""
+import pytest
+
+
+def worker():
+    import fluxmpi_amd as FluxMPI
+
+    assert not FluxMPI.Initialized()
+    try:
+        FluxMPI.local_rank()
+        raise AssertionError("local_rank before Init must raise")
+    except FluxMPI.FluxMPINotInitializedError as e:
+        assert "FluxMPI.init" in str(e)
+    FluxMPI.Init(verbose=True)
+    assert FluxMPI.Initialized()
+    assert FluxMPI.local_rank() < FluxMPI.total_workers()
+    assert FluxMPI.total_workers() >= 2
+    FluxMPI.fluxmpi_println("Printing from Rank ", FluxMPI.local_rank())
+    FluxMPI.fluxmpi_print("Printing from Rank ", FluxMPI.local_rank(), "\n")
+    FluxMPI.Init(verbose=True)  # idempotent: "already initialized; Skipping..."
+    FluxMPI.Finalize()
+    assert FluxMPI.Finalized()
+    assert FluxMPI.Initialized()  # reference: the flag is never reset
+
+
+def test_common(spmd):
+    spmd("tests.test_common:worker")
+
+
+def test_single_process_world(capsys):
+    """world == 1 path without a launcher (no process group needed)."""
+    import fluxmpi_amd as FluxMPI
+    from fluxmpi_amd.parallel import runtime
+
+    FluxMPI.fluxmpi_println("before init")  # prints a timestamp prefix, no error
+    out = capsys.readouterr().out
+    assert "before init" in out and out[:4].isdigit()
+    if not runtime.Initialized():
+        with pytest.warns(UserWarning, match="only 1 worker"):
+            FluxMPI.Init(verbose=True, backend="gloo")
+    assert FluxMPI.total_workers() == 1 and FluxMPI.local_rank() == 0
+    FluxMPI.fluxmpi_println("hello ", 1)
+    assert capsys.readouterr().out.endswith("hello 1\n")

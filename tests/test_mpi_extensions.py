@@ -1,0 +1,95 @@
+"""Mirror of reference test/test_mpi_extensions.jl (comm primitives), plus extras."""
+import numpy as np
+
+
+def _rank_array(shape, root_rank=0):
+    import torch
+    import fluxmpi_amd as FluxMPI
+    return torch.ones(shape, dtype=torch.float64) if FluxMPI.local_rank() == root_rank else torch.zeros(
+        shape, dtype=torch.float64)
+
+
+def worker():
+    import torch
+    import fluxmpi_amd as FluxMPI
+    from fluxmpi_amd import COMM_WORLD
+
+    FluxMPI.Init(verbose=True)
+    W = FluxMPI.total_workers()
+    r = FluxMPI.local_rank()
+
+    # --- Iallreduce! (out of place)
+    x = torch.ones(4, dtype=torch.float64)
+    y = torch.empty_like(x)
+    y, req = FluxMPI.Iallreduce(x, y, "+", COMM_WORLD)
+    FluxMPI.Wait(req)
+    assert torch.equal(y, x * W)
+    y = torch.empty_like(x)
+    y, req = FluxMPI.Iallreduce(x, y, "*")
+    req.wait()
+    assert torch.equal(y, x)
+    # in place form
+    z = torch.full((3,), float(r + 1))
+    z, req = FluxMPI.Iallreduce(z, max)
+    FluxMPI.Waitall([req])
+    assert torch.equal(z, torch.full((3,), float(W)))
+
+    # --- Ibcast!
+    x = _rank_array((2, 3), 0)
+    y, req = FluxMPI.Ibcast(x, 0, COMM_WORLD)
+    FluxMPI.Wait(req)
+    assert torch.equal(y, torch.ones(2, 3, dtype=torch.float64))
+
+    # --- blocking wrappers
+    x = torch.ones(4)
+    assert torch.equal(FluxMPI.allreduce(x.clone(), "+", COMM_WORLD), x * W)
+    assert torch.equal(FluxMPI.allreduce(x.clone(), "*", COMM_WORLD), x)
+    x = _rank_array((2, 3), 0)
+    assert torch.equal(FluxMPI.bcast(x.clone(), 0, COMM_WORLD), torch.ones(2, 3, dtype=torch.float64))
+    x = torch.ones(4)
+    y = FluxMPI.reduce(x.clone(), "+", 0, COMM_WORLD)
+    if r == 0:
+        assert torch.equal(y, x * W)
+    else:
+        assert torch.equal(y, x)
+
+    # --- extras: numpy buffers (in place), scalars, min/avg, ints, non-contiguous
+    a = np.ones(5, dtype=np.float32)
+    FluxMPI.allreduce(a, "+")
+    assert np.all(a == W)
+    assert FluxMPI.allreduce(float(r), "+") == sum(range(W))
+    assert FluxMPI.allreduce([r, 1], "+") == [sum(range(W)), W]
+    assert torch.equal(FluxMPI.allreduce(torch.tensor([r]), min), torch.tensor([0]))
+    assert torch.allclose(FluxMPI.allreduce(torch.tensor([float(r)]), "avg"), torch.tensor([(W - 1) / 2]))
+    m = torch.ones(4, 4)[:, ::2]
+    FluxMPI.allreduce(m, "+")
+    assert torch.equal(m, torch.full((4, 2), float(W)))
+    g = FluxMPI.allgather(torch.tensor([float(r)]))
+    assert torch.equal(g.reshape(-1), torch.arange(W, dtype=torch.float32))
+    rs = FluxMPI.reduce_scatter(torch.ones(W * 2))
+    assert torch.equal(rs, torch.full((2,), float(W)))
+    FluxMPI.Finalize()
+
+
+def test_mpi_extensions(spmd):
+    spmd("tests.test_mpi_extensions:worker")
+
+
+def worker_four():
+    worker()
+
+
+def test_mpi_extensions_4ranks(spmd):
+    spmd("tests.test_mpi_extensions:worker_four", nprocs=4)
+
+
+def test_op_coercion():
+    import operator
+    from fluxmpi_amd.parallel.comm import ReduceOp, to_op
+    assert to_op(operator.add) == ReduceOp.SUM
+    assert to_op("+") == ReduceOp.SUM
+    assert to_op(operator.mul) == ReduceOp.PROD
+    assert to_op(max) == ReduceOp.MAX and to_op(min) == ReduceOp.MIN
+    import pytest
+    with pytest.raises(ValueError):
+        to_op("xor")
