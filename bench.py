@@ -1,0 +1,122 @@
+#!/usr/bin/env python
+"""North-star benchmark: ResNet-50 data-parallel training throughput (images/s).
+
+``python bench.py --gpus N --steps K --warmup W`` — for N > 1 launched by the
+driver as ``torch.distributed.run --nproc-per-node N`` (one rank per GPU,
+RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* from the environment).
+
+Workload (BASELINE.json: "images/sec ResNet50 Lux.jl DDP at 1/2/4/8 MI355X"):
+ResNet-50 (25.6 M params, torchvision v1.5 layout), bf16 compute with fp32
+master weights + fp32 Adam moments (BatchNorm parameters fp32), channels_last,
+synthetic ImageNet batches (224x224x3, 1000 classes, random-init weights),
+per-GPU batch fixed as N grows (weak scaling). Every timed step runs the full
+forward, cross-entropy loss, backward with bucketed RCCL allreduce overlapped
+on a side stream (N > 1), and the fused HIP Adam update of every parameter.
+
+Timing: W untimed warmup steps, barrier + device sync, K timed steps, barrier
++ device sync; the max elapsed time over ranks is reported. Rank 0 prints one
+JSON line; ``value`` is the whole-job images/s.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.nn.functional as F
+
+METRIC = "images/sec ResNet50 Lux.jl DDP at 1/2/4/8 MI355X; scaling efficiency"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("BENCH_BATCH", "256")), help="per-GPU batch")
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--conv", default=os.environ.get("BENCH_CONV", "gemm"), choices=["gemm", "miopen"])
+    ap.add_argument("--norm", default=os.environ.get("BENCH_NORM", "torch"), choices=["torch", "fused"])
+    ap.add_argument("--optimizer", default="adam", choices=["adam", "momentum"])
+    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--graph", action="store_true", help="capture the step in a HIP graph")
+    ap.add_argument("--profile-steps", type=int, default=0)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import fluxmpi_amd as FluxMPI
+    from fluxmpi_amd import optimisers as O
+    from fluxmpi_amd.models import build_model
+    from fluxmpi_amd.parallel.ddp import DDP
+
+    torch.backends.cudnn.benchmark = False
+    FluxMPI.Init()
+    rank, world = FluxMPI.local_rank(), FluxMPI.total_workers()
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but world size {world}", file=sys.stderr)
+    dev = FluxMPI.device()
+    if dev.type != "cuda":
+        print("bench.py needs a GPU", file=sys.stderr)
+        return 2
+
+    torch.manual_seed(1234 + rank)
+    model = build_model(args.model, conv_impl=args.conv, norm=args.norm)
+    model = model.to(dev, memory_format=torch.channels_last)
+    # bf16 compute; BatchNorm affine params + running stats stay fp32
+    for m in model.modules():
+        is_norm = isinstance(m, torch.nn.modules.batchnorm._BatchNorm) or type(m).__name__ == "FusedBatchNorm2d"
+        if not is_norm:
+            for p in m.parameters(recurse=False):
+                p.data = p.data.to(torch.bfloat16)
+    rule = O.Adam(1e-3) if args.optimizer == "adam" else O.Momentum(0.1, 0.9)
+    ddp = DDP(model, rule, average=True, overlap=not args.no_overlap)
+
+    B = args.batch
+    gx = torch.Generator(device=dev).manual_seed(rank)
+    x = torch.randn(B, 3, args.image, args.image, device=dev, generator=gx).to(torch.bfloat16)
+    x = x.contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 1000, (B,), device=dev, generator=gx)
+
+    def step():
+        out = ddp(x)
+        loss = F.cross_entropy(out.float(), y)
+        loss.backward()
+        ddp.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    FluxMPI.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    FluxMPI.barrier()
+    dt = time.perf_counter() - t0
+    dt_max = FluxMPI.allreduce(torch.tensor([dt], dtype=torch.float64), max).item() if world > 1 else dt
+    lval = float(loss.item())
+    if rank == 0:
+        ips = world * B * args.steps / dt_max
+        rec = {
+            "metric": METRIC, "value": round(ips, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1000 * dt_max / args.steps, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            "config": {"model": "ResNet50", "global_batch": world * B, "per_gpu_batch": B, "seq_len": None,
+                       "image_size": args.image, "parallelism": f"dp{world}", "optimizer": args.optimizer,
+                       "conv": args.conv, "norm": args.norm, "backend": FluxMPI.backend_name(),
+                       "overlap": not args.no_overlap, "loss": round(lval, 4)},
+        }
+        print(json.dumps(rec), flush=True)
+    FluxMPI.Finalize()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,136 @@
+"""ResNet-50 (He et al. 2016; torchvision layout) for the north-star benchmark.
+
+The reference's headline workload is the Lux.jl ImageNet ResNet-50 example
+(``README.md:74-78``, ``BASELINE.json`` "ResNet50 Lux.jl DDP"). There is no
+torchvision in this image, so the architecture is written out here:
+7x7/2 stem -> 3x3/2 max-pool -> bottleneck stages [3, 4, 6, 3] (width 64..512,
+expansion 4, stride on the 3x3 conv, "ResNet v1.5") -> global average pool ->
+1000-way FC. 25.56 M parameters, 161 parameter tensors.
+
+MI355X choices:
+
+* activations in ``channels_last`` (NHWC): channels innermost is what the
+  conv kernels and our NHWC BatchNorm kernels want, and it makes every 1x1
+  convolution a plain GEMM ``[N*H*W, Cin] x [Cin, Cout]``;
+* ``conv_impl="gemm"`` routes 1x1 convolutions (36 of the 53 convs) to
+  hipBLASLt matmuls on that NHWC view instead of MIOpen;
+* ``norm="fused"`` uses the hand-written gfx950 NHWC BatchNorm kernels with
+  the ReLU (and the residual add of each block) fused into the normalisation
+  pass (``fluxmpi_amd.ops.batchnorm``); ``norm="torch"`` uses ``nn.BatchNorm2d``.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class Conv1x1(nn.Module):
+    """1x1 convolution computed as a GEMM on the NHWC view (hipBLASLt)."""
+
+    def __init__(self, cin: int, cout: int, stride: int = 1):
+        super().__init__()
+        self.stride = stride
+        self.weight = nn.Parameter(torch.empty(cout, cin, 1, 1))
+        nn.init.kaiming_normal_(self.weight, mode="fan_out", nonlinearity="relu")
+
+    def forward(self, x):
+        if self.stride != 1:
+            x = x[:, :, ::self.stride, ::self.stride]
+        n, c, h, w = x.shape
+        # NHWC memory -> [N*H*W, C] without a copy when x is channels_last
+        xm = x.permute(0, 2, 3, 1).reshape(n * h * w, c)
+        y = torch.matmul(xm, self.weight.view(self.weight.shape[0], c).t())
+        return y.view(n, h, w, -1).permute(0, 3, 1, 2)
+
+
+def conv1x1(cin, cout, stride=1, impl="gemm"):
+    if impl == "gemm":
+        return Conv1x1(cin, cout, stride)
+    return nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
+
+
+def _norm(c, kind):
+    if kind == "fused":
+        from ..ops.batchnorm import FusedBatchNorm2d
+        return FusedBatchNorm2d(c)
+    return nn.BatchNorm2d(c)
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin, width, stride=1, downsample=None, conv_impl="gemm", norm="torch"):
+        super().__init__()
+        cout = width * self.expansion
+        self.conv1 = conv1x1(cin, width, 1, conv_impl)
+        self.bn1 = _norm(width, norm)
+        self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)
+        self.bn2 = _norm(width, norm)
+        self.conv3 = conv1x1(width, cout, 1, conv_impl)
+        self.bn3 = _norm(cout, norm)
+        self.downsample = downsample
+        self.fused = norm == "fused"
+
+    def forward(self, x):
+        identity = x if self.downsample is None else self.downsample(x)
+        if self.fused:
+            out = self.bn1(self.conv1(x), relu=True)
+            out = self.bn2(self.conv2(out), relu=True)
+            return self.bn3(self.conv3(out), relu=True, residual=identity)
+        out = F.relu(self.bn1(self.conv1(x)))
+        out = F.relu(self.bn2(self.conv2(out)))
+        out = self.bn3(self.conv3(out))
+        return F.relu(out + identity)
+
+
+class ResNet(nn.Module):
+    def __init__(self, layers=(3, 4, 6, 3), num_classes=1000, conv_impl="gemm", norm="torch", zero_init_residual=False):
+        super().__init__()
+        self.conv_impl, self.norm_kind = conv_impl, norm
+        self.inplanes = 64
+        self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+        self.bn1 = _norm(64, norm)
+        self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
+        self.layer1 = self._make(64, layers[0], 1)
+        self.layer2 = self._make(128, layers[1], 2)
+        self.layer3 = self._make(256, layers[2], 2)
+        self.layer4 = self._make(512, layers[3], 2)
+        self.fc = nn.Linear(512 * Bottleneck.expansion, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+        if zero_init_residual:
+            for m in self.modules():
+                if isinstance(m, Bottleneck):
+                    nn.init.zeros_(m.bn3.weight)
+
+    def _make(self, width, blocks, stride):
+        down = None
+        cout = width * Bottleneck.expansion
+        if stride != 1 or self.inplanes != cout:
+            down = nn.Sequential(conv1x1(self.inplanes, cout, stride, self.conv_impl), _norm(cout, self.norm_kind))
+        mods = [Bottleneck(self.inplanes, width, stride, down, self.conv_impl, self.norm_kind)]
+        self.inplanes = cout
+        for _ in range(1, blocks):
+            mods.append(Bottleneck(cout, width, 1, None, self.conv_impl, self.norm_kind))
+        return nn.Sequential(*mods)
+
+    def forward(self, x):
+        if self.norm_kind == "fused":
+            x = self.bn1(self.conv1(x), relu=True)
+        else:
+            x = F.relu(self.bn1(self.conv1(x)))
+        x = self.maxpool(x)
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+        return self.fc(x)
+
+
+def resnet50(num_classes=1000, **kw) -> ResNet:
+    return ResNet((3, 4, 6, 3), num_classes, **kw)
+
+
+def resnet18ish(num_classes=10, **kw) -> ResNet:
+    """Small bottleneck ResNet ([1,1,1,1]) for fast tests."""
+    return ResNet((1, 1, 1, 1), num_classes, **kw)

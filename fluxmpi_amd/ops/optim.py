@@ -60,6 +60,11 @@ def adam_(params, grads, exp_avgs, exp_avg_sqs, *, lr: float, beta1: float, beta
                       dev_hyper.data_ptr() if dev_hyper is not None else 0,
                       dev_gscale.data_ptr() if dev_gscale is not None else 0, stream)
         return
+    if dev_hyper is not None:
+        h = dev_hyper.tolist()
+        lr, bc1, bc2 = h[0], 1.0 - float(torch.tensor(h[1])), 1.0 - float(torch.tensor(h[2]))
+    if dev_gscale is not None:
+        grad_scale = grad_scale * float(dev_gscale)
     adam_reference_(params, grads, exp_avgs, exp_avg_sqs, lr=lr, beta1=beta1, beta2=beta2, eps=eps, bc1=bc1,
                     bc2=bc2, weight_decay=weight_decay, grad_scale=grad_scale, masters=masters)
 
@@ -119,6 +124,8 @@ def sgd_(params, grads, bufs, *, lr: float, momentum: float = 0.0, nesterov: boo
                      float(lr), float(momentum), float(weight_decay), float(grad_scale), int(bool(nesterov)),
                      dev_lr.data_ptr() if dev_lr is not None else 0, stream)
         return
+    if dev_lr is not None:
+        lr = float(dev_lr.reshape(-1)[0])
     sgd_reference_(params, grads, bufs, lr=lr, momentum=momentum, nesterov=nesterov, weight_decay=weight_decay,
                    grad_scale=grad_scale, masters=masters)
 
