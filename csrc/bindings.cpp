@@ -62,6 +62,36 @@ PYBIND11_MODULE(_C, m) {
         py::arg("weight_decay"), py::arg("grad_scale"), py::arg("nesterov"), py::arg("dev_lr"),
         py::arg("stream"));
 
+  // ---- fused NHWC BatchNorm ------------------------------------------------
+  m.def("bn_fwd_train",
+        [](uintptr_t x, uintptr_t y, uintptr_t res, uintptr_t w, uintptr_t b, uintptr_t rm, uintptr_t rv,
+           uintptr_t sm, uintptr_t si, uintptr_t ws, int64_t rows, int64_t C, float momentum, float eps, int relu,
+           int dtype, uintptr_t stream) {
+          bn_fwd_train(reinterpret_cast<const void*>(x), reinterpret_cast<void*>(y), reinterpret_cast<const void*>(res),
+                       reinterpret_cast<const float*>(w), reinterpret_cast<const float*>(b),
+                       reinterpret_cast<float*>(rm), reinterpret_cast<float*>(rv), reinterpret_cast<float*>(sm),
+                       reinterpret_cast<float*>(si), reinterpret_cast<float*>(ws), rows, C, momentum, eps, relu, dtype,
+                       S(stream));
+        });
+  m.def("bn_fwd_infer",
+        [](uintptr_t x, uintptr_t y, uintptr_t res, uintptr_t w, uintptr_t b, uintptr_t rm, uintptr_t rv,
+           int64_t rows, int64_t C, float eps, int relu, int dtype, uintptr_t stream) {
+          bn_fwd_infer(reinterpret_cast<const void*>(x), reinterpret_cast<void*>(y), reinterpret_cast<const void*>(res),
+                       reinterpret_cast<const float*>(w), reinterpret_cast<const float*>(b),
+                       reinterpret_cast<const float*>(rm), reinterpret_cast<const float*>(rv), rows, C, eps, relu,
+                       dtype, S(stream));
+        });
+  m.def("bn_bwd",
+        [](uintptr_t dy, uintptr_t x, uintptr_t y, uintptr_t w, uintptr_t sm, uintptr_t si, uintptr_t dx,
+           uintptr_t dres, uintptr_t dw, uintptr_t db, uintptr_t ws, int64_t rows, int64_t C, int relu, int dtype,
+           uintptr_t stream) {
+          bn_bwd(reinterpret_cast<const void*>(dy), reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(y),
+                 reinterpret_cast<const float*>(w), reinterpret_cast<const float*>(sm),
+                 reinterpret_cast<const float*>(si), reinterpret_cast<void*>(dx), reinterpret_cast<void*>(dres),
+                 reinterpret_cast<float*>(dw), reinterpret_cast<float*>(db), reinterpret_cast<float*>(ws), rows, C,
+                 relu, dtype, S(stream));
+        });
+
   // ---- RCCL ----------------------------------------------------------------
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
   m.def("rccl_version", &rccl_version);

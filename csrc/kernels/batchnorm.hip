@@ -1,0 +1,455 @@
+// Fused NHWC BatchNorm (+ReLU, +residual add) for gfx950.
+//
+// ResNet-50's non-GEMM time is dominated by memory passes over activations:
+// eager BatchNorm + ReLU + residual add + ReLU costs ~7 passes forward and
+// ~10 backward. These kernels cut that to 2 forward (stats read; normalise
+// read + write) and 2 backward (reduce read; dx read + write) passes.
+//
+// Layout: x is [R, C] row-major (R = N*H*W, channels innermost = NHWC /
+// channels_last), C % 8 == 0. Each lane owns 8 consecutive channels of one
+// row (one 16 B vector for bf16/fp16), so every access is a full-width
+// coalesced global_load_dwordx4.
+//
+// Reductions: a workgroup accumulates fp32 per-channel partials over its rows
+// in registers, reduces the lanes that share a channel vector through LDS and
+// adds its partial to a [2][C] fp32 accumulator with global float atomics
+// (zeroed by hipMemsetAsync first). The grid is sized so each workgroup
+// streams >= 64K elements: atomic traffic stays a few % of the data traffic.
+// The consumer kernels derive per-channel coefficients from the accumulator in
+// an LDS prologue, so no separate "finalize" launch is needed.
+#include <stdexcept>
+#include <string>
+
+#include "../api.h"
+#include "common.h"
+
+namespace fluxmpi {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxC = 2048;
+
+template <typename T>
+struct V8 {
+  T v[8];
+};
+
+template <typename T>
+__device__ __forceinline__ void ld8f(const T* __restrict__ p, float (&f)[8]) {
+  T t[8];
+  load8(p, t);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = static_cast<float>(t[j]);
+}
+
+template <typename T>
+__device__ __forceinline__ void st8f(T* __restrict__ p, const float (&f)[8]) {
+  T t[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) t[j] = static_cast<T>(f[j]);
+  store8(p, t);
+}
+
+struct Geo {
+  int cv;    // channel vectors per row (C / 8)
+  int rpi;   // rows handled concurrently by a workgroup (kThreads / cv)
+  int64_t rows_per_block;
+  int blocks;
+};
+
+Geo geometry(int64_t rows, int64_t C) {
+  Geo g;
+  g.cv = static_cast<int>(C / 8);
+  g.rpi = kThreads / g.cv;
+  if (g.rpi < 1) g.rpi = 1;
+  // >= 64K elements per workgroup, at most 2048 workgroups
+  int64_t min_rows = (65536 + C - 1) / C;
+  int64_t blocks = (rows + min_rows - 1) / min_rows;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  int64_t rpb = (rows + blocks - 1) / blocks;
+  rpb = (rpb + g.rpi - 1) / g.rpi * g.rpi;
+  g.rows_per_block = rpb;
+  g.blocks = static_cast<int>((rows + rpb - 1) / rpb);
+  return g;
+}
+
+// Block-level reduction of two 8-float accumulators over lanes sharing a
+// channel vector, then one atomic per channel per workgroup.
+__device__ __forceinline__ void block_reduce_atomic(float (&a)[8], float (&b)[8], int cv, int rpi, int C,
+                                                    float* __restrict__ acc, float* smem) {
+  const int t = threadIdx.x;
+  const int r0 = t / cv, c8 = t % cv;
+  const bool active = r0 < rpi;
+  // smem layout: [rpi][C] for a, then [rpi][C] for b
+  float* sa = smem;
+  float* sb = smem + rpi * C;
+  if (active) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sa[r0 * C + c8 * 8 + j] = a[j];
+      sb[r0 * C + c8 * 8 + j] = b[j];
+    }
+  }
+  __syncthreads();
+  // every thread reduces some channels over the rpi rows
+  for (int c = t; c < C; c += kThreads) {
+    float x = 0.f, y = 0.f;
+    for (int r = 0; r < rpi; ++r) {
+      x += sa[r * C + c];
+      y += sb[r * C + c];
+    }
+    atomicAdd(acc + c, x);
+    atomicAdd(acc + C + c, y);
+  }
+}
+
+// ---------------------------------------------------------------- forward
+template <typename T>
+__global__ __launch_bounds__(kThreads) void bn_stats_kernel(const T* __restrict__ x, int64_t rows, int C, Geo g,
+                                                            float* __restrict__ acc) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int t = threadIdx.x;
+  const int r0 = t / g.cv, c8 = t % g.cv;
+  float s[8] = {0}, q[8] = {0};
+  if (r0 < g.rpi) {
+    const int64_t start = static_cast<int64_t>(blockIdx.x) * g.rows_per_block;
+    int64_t end = start + g.rows_per_block;
+    if (end > rows) end = rows;
+    int64_t r = start + r0;
+    // 4 rows in flight per lane
+    for (; r + 3 * g.rpi < end; r += 4 * g.rpi) {
+      float f[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) ld8f(x + (r + u * g.rpi) * C + c8 * 8, f[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s[j] += f[u][j];
+          q[j] = fmaf(f[u][j], f[u][j], q[j]);
+        }
+    }
+    for (; r < end; r += g.rpi) {
+      float f[8];
+      ld8f(x + r * C + c8 * 8, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s[j] += f[j];
+        q[j] = fmaf(f[j], f[j], q[j]);
+      }
+    }
+  }
+  block_reduce_atomic(s, q, g.cv, g.rpi, C, acc, smem);
+}
+
+// y = act(x*scale + shift [+ res]); scale/shift derived in the prologue.
+// Block 0 also writes save_mean/save_invstd and updates the running stats.
+template <typename T, bool RELU, bool RES>
+__global__ __launch_bounds__(kThreads) void bn_norm_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                           const T* __restrict__ res, const float* __restrict__ w,
+                                                           const float* __restrict__ b, const float* __restrict__ acc,
+                                                           float* __restrict__ rmean, float* __restrict__ rvar,
+                                                           float* __restrict__ smean, float* __restrict__ sinv,
+                                                           int64_t rows, int C, float momentum, float eps, int train,
+                                                           int64_t nvec) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* scale = smem;
+  float* shift = smem + C;
+  const float inv_n = 1.f / static_cast<float>(rows);
+  for (int c = threadIdx.x; c < C; c += kThreads) {
+    float mean, invstd;
+    if (train) {
+      mean = acc[c] * inv_n;
+      float var = acc[C + c] * inv_n - mean * mean;
+      var = var > 0.f ? var : 0.f;
+      invstd = rsqrtf(var + eps);
+      if (blockIdx.x == 0) {
+        smean[c] = mean;
+        sinv[c] = invstd;
+        if (rmean != nullptr) {
+          const float unbiased = rows > 1 ? var * static_cast<float>(rows) / static_cast<float>(rows - 1) : var;
+          rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+          rvar[c] = (1.f - momentum) * rvar[c] + momentum * unbiased;
+        }
+      }
+    } else {
+      mean = rmean[c];
+      invstd = rsqrtf(rvar[c] + eps);
+    }
+    const float sc = (w ? w[c] : 1.f) * invstd;
+    scale[c] = sc;
+    shift[c] = (b ? b[c] : 0.f) - mean * sc;
+  }
+  __syncthreads();
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  for (int64_t v = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; v < nvec; v += stride) {
+    const int64_t e = v * 8;
+    const int c0 = static_cast<int>(e % C);
+    float f[8];
+    ld8f(x + e, f);
+    float rr[8];
+    if (RES) ld8f(res + e, rr);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float o = fmaf(f[j], scale[c0 + j], shift[c0 + j]);
+      if (RES) o += rr[j];
+      if (RELU) o = o > 0.f ? o : 0.f;
+      f[j] = o;
+    }
+    st8f(y + e, f);
+  }
+}
+
+// ---------------------------------------------------------------- backward
+// acc[0:C] += sum(dy_eff), acc[C:2C] += sum(dy_eff * xhat)
+template <typename T, bool RELU>
+__global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                                 const T* __restrict__ y,
+                                                                 const float* __restrict__ smean,
+                                                                 const float* __restrict__ sinv, int64_t rows, int C,
+                                                                 Geo g, float* __restrict__ acc) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int t = threadIdx.x;
+  const int r0 = t / g.cv, c8 = t % g.cv;
+  float s[8] = {0}, q[8] = {0};
+  if (r0 < g.rpi) {
+    float mu[8], is[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      mu[j] = smean[c8 * 8 + j];
+      is[j] = sinv[c8 * 8 + j];
+    }
+    const int64_t start = static_cast<int64_t>(blockIdx.x) * g.rows_per_block;
+    int64_t end = start + g.rows_per_block;
+    if (end > rows) end = rows;
+    int64_t r = start + r0;
+    for (; r + g.rpi < end; r += 2 * g.rpi) {
+      float d[2][8], xv[2][8], yv[2][8];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int64_t off = (r + u * g.rpi) * C + c8 * 8;
+        ld8f(dy + off, d[u]);
+        ld8f(x + off, xv[u]);
+        if (RELU) ld8f(y + off, yv[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float dd = d[u][j];
+          if (RELU) dd = yv[u][j] > 0.f ? dd : 0.f;
+          s[j] += dd;
+          q[j] = fmaf(dd, (xv[u][j] - mu[j]) * is[j], q[j]);
+        }
+    }
+    for (; r < end; r += g.rpi) {
+      const int64_t off = r * C + c8 * 8;
+      float d[8], xv[8], yv[8];
+      ld8f(dy + off, d);
+      ld8f(x + off, xv);
+      if (RELU) ld8f(y + off, yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float dd = d[j];
+        if (RELU) dd = yv[j] > 0.f ? dd : 0.f;
+        s[j] += dd;
+        q[j] = fmaf(dd, (xv[j] - mu[j]) * is[j], q[j]);
+      }
+    }
+  }
+  block_reduce_atomic(s, q, g.cv, g.rpi, C, acc, smem);
+}
+
+// dx = w*invstd * (dy_eff - sum_dy/R - xhat * sum_dy_xhat/R); dres = dy_eff
+template <typename T, bool RELU, bool DRES>
+__global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                             const T* __restrict__ y, const float* __restrict__ w,
+                                                             const float* __restrict__ smean,
+                                                             const float* __restrict__ sinv,
+                                                             const float* __restrict__ acc, T* __restrict__ dx,
+                                                             T* __restrict__ dres, float* __restrict__ dw,
+                                                             float* __restrict__ db, int64_t rows, int C,
+                                                             int64_t nvec) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* k1 = smem;          // w*invstd
+  float* k2 = smem + C;      // mean(dy_eff)
+  float* k3 = smem + 2 * C;  // mean(dy_eff*xhat)
+  float* mu = smem + 3 * C;
+  float* is = smem + 4 * C;
+  const float inv_n = 1.f / static_cast<float>(rows);
+  for (int c = threadIdx.x; c < C; c += kThreads) {
+    const float iv = sinv[c];
+    k1[c] = (w ? w[c] : 1.f) * iv;
+    k2[c] = acc[c] * inv_n;
+    k3[c] = acc[C + c] * inv_n;
+    mu[c] = smean[c];
+    is[c] = iv;
+    if (blockIdx.x == 0) {
+      if (dw) dw[c] = acc[C + c];
+      if (db) db[c] = acc[c];
+    }
+  }
+  __syncthreads();
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  for (int64_t v = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; v < nvec; v += stride) {
+    const int64_t e = v * 8;
+    const int c0 = static_cast<int>(e % C);
+    float d[8], xv[8], yv[8];
+    ld8f(dy + e, d);
+    ld8f(x + e, xv);
+    if (RELU) ld8f(y + e, yv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + j;
+      float dd = d[j];
+      if (RELU) dd = yv[j] > 0.f ? dd : 0.f;
+      d[j] = dd;
+      const float xh = (xv[j] - mu[c]) * is[c];
+      xv[j] = k1[c] * (dd - k2[c] - xh * k3[c]);
+    }
+    st8f(dx + e, xv);
+    if (DRES) st8f(dres + e, d);
+  }
+}
+
+int elementwise_blocks(int64_t nvec) {
+  int64_t b = (nvec + kThreads - 1) / kThreads;
+  if (b > 2048) b = 2048;
+  if (b < 1) b = 1;
+  return static_cast<int>(b);
+}
+
+void check(int64_t C) {
+  if (C % 8 != 0 || C > kMaxC || C < 8)
+    throw std::runtime_error("fused batchnorm: need C % 8 == 0 and 8 <= C <= 2048 (got " + std::to_string(C) + ")");
+}
+
+size_t reduce_smem(const Geo& g, int64_t C) { return static_cast<size_t>(2 * g.rpi * C) * sizeof(float); }
+
+template <typename T>
+void fwd_train_t(const void* x, void* y, const void* res, const float* w, const float* b, float* rm, float* rv,
+                 float* sm, float* si, float* ws, int64_t rows, int64_t C, float momentum, float eps, int relu,
+                 hipStream_t s) {
+  Geo g = geometry(rows, C);
+  FLUXMPI_HIP_CHECK(hipMemsetAsync(ws, 0, 2 * C * sizeof(float), s));
+  bn_stats_kernel<T><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(static_cast<const T*>(x), rows, (int)C, g, ws);
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+  const int64_t nvec = rows * C / 8;
+  const int nb = elementwise_blocks(nvec);
+  const size_t sm2 = 2 * C * sizeof(float);
+  const T* xr = static_cast<const T*>(x);
+  T* yr = static_cast<T*>(y);
+  const T* rr = static_cast<const T*>(res);
+#define LAUNCH(RELU, RES)                                                                                        \
+  bn_norm_kernel<T, RELU, RES><<<nb, kThreads, sm2, s>>>(xr, yr, rr, w, b, ws, rm, rv, sm, si, rows, (int)C, \
+                                                         momentum, eps, 1, nvec)
+  if (relu && res) LAUNCH(true, true);
+  else if (relu) LAUNCH(true, false);
+  else if (res) LAUNCH(false, true);
+  else LAUNCH(false, false);
+#undef LAUNCH
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+}
+
+template <typename T>
+void fwd_infer_t(const void* x, void* y, const void* res, const float* w, const float* b, const float* rm,
+                 const float* rv, int64_t rows, int64_t C, float eps, int relu, hipStream_t s) {
+  const int64_t nvec = rows * C / 8;
+  const int nb = elementwise_blocks(nvec);
+  const size_t sm2 = 2 * C * sizeof(float);
+  const T* xr = static_cast<const T*>(x);
+  T* yr = static_cast<T*>(y);
+  const T* rr = static_cast<const T*>(res);
+  float* rmm = const_cast<float*>(rm);
+  float* rvv = const_cast<float*>(rv);
+#define LAUNCH(RELU, RES)                                                                                     \
+  bn_norm_kernel<T, RELU, RES><<<nb, kThreads, sm2, s>>>(xr, yr, rr, w, b, nullptr, rmm, rvv, nullptr, nullptr, \
+                                                         rows, (int)C, 0.f, eps, 0, nvec)
+  if (relu && res) LAUNCH(true, true);
+  else if (relu) LAUNCH(true, false);
+  else if (res) LAUNCH(false, true);
+  else LAUNCH(false, false);
+#undef LAUNCH
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+}
+
+template <typename T>
+void bwd_t(const void* dy, const void* x, const void* y, const float* w, const float* sm, const float* si, void* dx,
+           void* dres, float* dw, float* db, float* ws, int64_t rows, int64_t C, int relu, hipStream_t s) {
+  Geo g = geometry(rows, C);
+  FLUXMPI_HIP_CHECK(hipMemsetAsync(ws, 0, 2 * C * sizeof(float), s));
+  const T* dyr = static_cast<const T*>(dy);
+  const T* xr = static_cast<const T*>(x);
+  const T* yr = static_cast<const T*>(y);
+  if (relu)
+    bn_bwd_reduce_kernel<T, true><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(dyr, xr, yr, sm, si, rows, (int)C, g, ws);
+  else
+    bn_bwd_reduce_kernel<T, false><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(dyr, xr, yr, sm, si, rows, (int)C, g, ws);
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+  const int64_t nvec = rows * C / 8;
+  const int nb = elementwise_blocks(nvec);
+  const size_t sm5 = 5 * C * sizeof(float);
+  T* dxr = static_cast<T*>(dx);
+  T* drr = static_cast<T*>(dres);
+#define LAUNCH(RELU, DRES)                                                                                         \
+  bn_bwd_dx_kernel<T, RELU, DRES><<<nb, kThreads, sm5, s>>>(dyr, xr, yr, w, sm, si, ws, dxr, drr, dw, db, rows, \
+                                                            (int)C, nvec)
+  if (relu && dres) LAUNCH(true, true);
+  else if (relu) LAUNCH(true, false);
+  else if (dres) LAUNCH(false, true);
+  else LAUNCH(false, false);
+#undef LAUNCH
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace
+
+size_t bn_workspace_floats(int64_t rows, int64_t C) {
+  (void)rows;
+  return static_cast<size_t>(2 * C);
+}
+
+void bn_fwd_train(const void* x, void* y, const void* residual, const float* weight, const float* bias,
+                  float* running_mean, float* running_var, float* save_mean, float* save_invstd, float* workspace,
+                  int64_t rows, int64_t C, float momentum, float eps, int relu, int dtype, hipStream_t stream) {
+  check(C);
+  switch (dtype) {
+    case kBF16: fwd_train_t<bf16>(x, y, residual, weight, bias, running_mean, running_var, save_mean, save_invstd,
+                                  workspace, rows, C, momentum, eps, relu, stream); break;
+    case kF16: fwd_train_t<f16>(x, y, residual, weight, bias, running_mean, running_var, save_mean, save_invstd,
+                                workspace, rows, C, momentum, eps, relu, stream); break;
+    case kF32: fwd_train_t<float>(x, y, residual, weight, bias, running_mean, running_var, save_mean, save_invstd,
+                                  workspace, rows, C, momentum, eps, relu, stream); break;
+    default: throw std::runtime_error("fused batchnorm: unsupported dtype");
+  }
+}
+
+void bn_fwd_infer(const void* x, void* y, const void* residual, const float* weight, const float* bias,
+                  const float* running_mean, const float* running_var, int64_t rows, int64_t C, float eps, int relu,
+                  int dtype, hipStream_t stream) {
+  check(C);
+  switch (dtype) {
+    case kBF16: fwd_infer_t<bf16>(x, y, residual, weight, bias, running_mean, running_var, rows, C, eps, relu, stream); break;
+    case kF16: fwd_infer_t<f16>(x, y, residual, weight, bias, running_mean, running_var, rows, C, eps, relu, stream); break;
+    case kF32: fwd_infer_t<float>(x, y, residual, weight, bias, running_mean, running_var, rows, C, eps, relu, stream); break;
+    default: throw std::runtime_error("fused batchnorm: unsupported dtype");
+  }
+}
+
+void bn_bwd(const void* dy, const void* x, const void* y, const float* weight, const float* save_mean,
+            const float* save_invstd, void* dx, void* dres, float* dweight, float* dbias, float* workspace,
+            int64_t rows, int64_t C, int relu, int dtype, hipStream_t stream) {
+  check(C);
+  switch (dtype) {
+    case kBF16: bwd_t<bf16>(dy, x, y, weight, save_mean, save_invstd, dx, dres, dweight, dbias, workspace, rows, C,
+                            relu, stream); break;
+    case kF16: bwd_t<f16>(dy, x, y, weight, save_mean, save_invstd, dx, dres, dweight, dbias, workspace, rows, C,
+                          relu, stream); break;
+    case kF32: bwd_t<float>(dy, x, y, weight, save_mean, save_invstd, dx, dres, dweight, dbias, workspace, rows, C,
+                            relu, stream); break;
+    default: throw std::runtime_error("fused batchnorm: unsupported dtype");
+  }
+}
+
+}  // namespace fluxmpi

@@ -1,0 +1,116 @@
+"""Deep Equilibrium Model (Bai et al. 2019; the FastDEQ.jl example of the reference README).
+
+``z* = f(z*, x)`` is found by Anderson-accelerated fixed-point iteration
+without building a graph; the backward pass uses implicit differentiation:
+the incoming gradient ``g`` is replaced by the solution of
+``u = J_f(z*)^T u + g`` (solved by fixed-point iteration on
+vector-Jacobian products), so memory is independent of the solver depth.
+
+For the DDP layer this is the "irregular gradient tree" config: parameters of
+the implicit layer receive gradients only through the adjoint solve, and the
+number of solver iterations differs across ranks, which must not desync
+collectives (bucket plans are built from the parameter list, not from
+gradient arrival order).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0):
+    """Anderson acceleration for ``x = f(x)`` over batch-flattened tensors. Returns (x, iters, rel_residual)."""
+    bsz = x0.shape[0]
+    shape = x0.shape
+    d = x0[0].numel()
+    X = torch.zeros(bsz, m, d, dtype=x0.dtype, device=x0.device)
+    Fv = torch.zeros_like(X)
+    X[:, 0], Fv[:, 0] = x0.reshape(bsz, -1), f(x0).reshape(bsz, -1)
+    X[:, 1], Fv[:, 1] = Fv[:, 0], f(Fv[:, 0].reshape(shape)).reshape(bsz, -1)
+    H = torch.zeros(bsz, m + 1, m + 1, dtype=x0.dtype, device=x0.device)
+    H[:, 0, 1:] = H[:, 1:, 0] = 1
+    y = torch.zeros(bsz, m + 1, 1, dtype=x0.dtype, device=x0.device)
+    y[:, 0] = 1
+    res = float("inf")
+    k = 1
+    for k in range(2, max_iter):
+        n = min(k, m)
+        G = Fv[:, :n] - X[:, :n]
+        H[:, 1:n + 1, 1:n + 1] = torch.bmm(G, G.transpose(1, 2)) + lam * torch.eye(n, dtype=x0.dtype,
+                                                                                   device=x0.device)[None]
+        alpha = torch.linalg.solve(H[:, :n + 1, :n + 1], y[:, :n + 1])[:, 1:n + 1, 0]
+        X[:, k % m] = beta * (alpha[:, None] @ Fv[:, :n])[:, 0] + (1 - beta) * (alpha[:, None] @ X[:, :n])[:, 0]
+        Fv[:, k % m] = f(X[:, k % m].reshape(shape)).reshape(bsz, -1)
+        res = float((Fv[:, k % m] - X[:, k % m]).norm() / (1e-5 + Fv[:, k % m].norm()))
+        if res < tol:
+            break
+    return X[:, k % m].reshape(shape), k, res
+
+
+class DEQFixedPoint(nn.Module):
+    def __init__(self, f: nn.Module, max_iter=30, tol=1e-4, bwd_iter=30, bwd_tol=1e-4):
+        super().__init__()
+        self.f = f
+        self.max_iter, self.tol, self.bwd_iter, self.bwd_tol = max_iter, tol, bwd_iter, bwd_tol
+        self.last_iters = 0
+
+    def forward(self, x):
+        with torch.no_grad():
+            z, self.last_iters, _ = anderson(lambda z: self.f(z, x), torch.zeros_like(x), max_iter=self.max_iter,
+                                             tol=self.tol)
+        z = self.f(z, x)  # one differentiable step re-engages autograd at z*
+        if not torch.is_grad_enabled():
+            return z
+        z0 = z.clone().detach().requires_grad_()
+        f0 = self.f(z0, x)
+
+        def backward_hook(grad):
+            u = grad
+            for _ in range(self.bwd_iter):  # u = J^T u + grad
+                u_new = torch.autograd.grad(f0, z0, u, retain_graph=True)[0] + grad
+                if (u_new - u).norm() <= self.bwd_tol * (grad.norm() + 1e-9):
+                    u = u_new
+                    break
+                u = u_new
+            return u
+
+        if z.requires_grad:
+            z.register_hook(backward_hook)
+        return z
+
+
+class ResidualCell(nn.Module):
+    """f(z, x) = GN(relu(z + GN(conv2(GN(relu(conv1 z))) + x)))  (MDEQ-style cell)."""
+
+    def __init__(self, ch=48, groups=8):
+        super().__init__()
+        self.conv1 = nn.Conv2d(ch, ch, 3, padding=1, bias=False)
+        self.conv2 = nn.Conv2d(ch, ch, 3, padding=1, bias=False)
+        self.n1, self.n2, self.n3 = nn.GroupNorm(groups, ch), nn.GroupNorm(groups, ch), nn.GroupNorm(groups, ch)
+        for c in (self.conv1, self.conv2):
+            nn.init.normal_(c.weight, 0, 0.01)
+
+    def forward(self, z, x):
+        y = self.n1(F.relu(self.conv1(z)))
+        return self.n3(F.relu(z + self.n2(x + self.conv2(y))))
+
+
+class DEQClassifier(nn.Module):
+    def __init__(self, cin=1, ch=48, num_classes=10, **solver):
+        super().__init__()
+        self.inj = nn.Conv2d(cin, ch, 3, padding=1, bias=False)
+        self.inj_norm = nn.BatchNorm2d(ch)
+        self.deq = DEQFixedPoint(ResidualCell(ch), **solver)
+        self.out_norm = nn.BatchNorm2d(ch)
+        self.head = nn.Linear(ch * 4 * 4, num_classes)
+
+    def forward(self, x):
+        x = self.inj_norm(self.inj(x))
+        z = self.out_norm(self.deq(x))
+        z = F.adaptive_avg_pool2d(z, 4).flatten(1)
+        return self.head(z)
+
+
+def deq_mnist(num_classes=10, **kw) -> DEQClassifier:
+    return DEQClassifier(1, 48, num_classes, **kw)

@@ -1,0 +1,80 @@
+"""ViT-Base/16 (Dosovitskiy et al. 2021) — BASELINE.json config "ViT-Base/16 Lux.jl DDP bf16".
+
+224x224 input, 16x16 patches (196 tokens + [CLS] = 197), width 768, depth 12,
+12 heads, MLP 3072, pre-LayerNorm, learned position embeddings, 1000-way
+head: 86.6 M parameters in 152 tensors — large gradient buckets, which is the
+point of this config for the DDP layer (bucketing + backward/comm overlap).
+
+Attention uses ``F.scaled_dot_product_attention`` (the flash-attention
+kernels PyTorch-ROCm ships for gfx950); the patch embedding is a GEMM on the
+unfolded patches.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class PatchEmbed(nn.Module):
+    def __init__(self, img=224, patch=16, cin=3, dim=768):
+        super().__init__()
+        self.patch = patch
+        self.n = (img // patch) ** 2
+        self.proj = nn.Linear(cin * patch * patch, dim)
+
+    def forward(self, x):
+        n, c, h, w = x.shape
+        p = self.patch
+        x = x.reshape(n, c, h // p, p, w // p, p).permute(0, 2, 4, 1, 3, 5).reshape(n, (h // p) * (w // p), c * p * p)
+        return self.proj(x)
+
+
+class Block(nn.Module):
+    def __init__(self, dim, heads, mlp):
+        super().__init__()
+        self.heads = heads
+        self.ln1 = nn.LayerNorm(dim, eps=1e-6)
+        self.qkv = nn.Linear(dim, 3 * dim)
+        self.proj = nn.Linear(dim, dim)
+        self.ln2 = nn.LayerNorm(dim, eps=1e-6)
+        self.fc1 = nn.Linear(dim, mlp)
+        self.fc2 = nn.Linear(mlp, dim)
+
+    def forward(self, x):
+        b, t, d = x.shape
+        h = self.heads
+        q, k, v = self.qkv(self.ln1(x)).view(b, t, 3, h, d // h).permute(2, 0, 3, 1, 4)
+        a = F.scaled_dot_product_attention(q, k, v)
+        x = x + self.proj(a.transpose(1, 2).reshape(b, t, d))
+        return x + self.fc2(F.gelu(self.fc1(self.ln2(x))))
+
+
+class ViT(nn.Module):
+    def __init__(self, img=224, patch=16, dim=768, depth=12, heads=12, mlp=3072, num_classes=1000):
+        super().__init__()
+        self.embed = PatchEmbed(img, patch, 3, dim)
+        self.cls = nn.Parameter(torch.zeros(1, 1, dim))
+        self.pos = nn.Parameter(torch.randn(1, self.embed.n + 1, dim) * 0.02)
+        self.blocks = nn.ModuleList([Block(dim, heads, mlp) for _ in range(depth)])
+        self.ln = nn.LayerNorm(dim, eps=1e-6)
+        self.head = nn.Linear(dim, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Linear):
+                nn.init.trunc_normal_(m.weight, std=0.02)
+                nn.init.zeros_(m.bias)
+
+    def forward(self, x):
+        x = self.embed(x)
+        x = torch.cat([self.cls.expand(x.shape[0], -1, -1).to(x.dtype), x], 1) + self.pos.to(x.dtype)
+        for blk in self.blocks:
+            x = blk(x)
+        return self.head(self.ln(x)[:, 0])
+
+
+def vit_b16(num_classes=1000, img=224, **kw) -> ViT:
+    return ViT(img=img, num_classes=num_classes, **kw)
+
+
+def vit_tiny(num_classes=10, img=32) -> ViT:
+    return ViT(img=img, patch=8, dim=64, depth=2, heads=4, mlp=128, num_classes=num_classes)

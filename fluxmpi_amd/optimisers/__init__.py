@@ -240,7 +240,7 @@ def _adam_batch(rule: Adam, items, weight_decay: float):
         for i in idx:
             leaf, x = items[i][0], items[i][1]
             m, v, b = leaf.state
-            leaf.state = (m, v, (_T(x, b[0] * rule.beta[0]), _T(x, b[1] * rule.beta[1])))
+            leaf.state = (m, v, (_T(x, b[0] * _T(x, rule.beta[0])), _T(x, b[1] * _T(x, rule.beta[1]))))
             out[i] = None
     return out
 
