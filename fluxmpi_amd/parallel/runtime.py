@@ -128,8 +128,9 @@ def Init(gpu_devices: list[int] | None = None, verbose: bool = False, backend: s
         port = os.environ.get("MASTER_PORT", "29500")
         if _is_loopback(addr):
             os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
-        dist.init_process_group("gloo", init_method=f"tcp://{addr}:{port}", rank=rank, world_size=size,
-                                timeout=timeout)
+        # env:// also handles torchrun's agent-hosted store (TORCHELASTIC_USE_AGENT_STORE)
+        os.environ["MASTER_ADDR"], os.environ["MASTER_PORT"] = addr, port
+        dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=size, timeout=timeout)
         owns = True
         cpu_comm = _comm.TorchComm(None, rank, size, "gloo")
     else:
