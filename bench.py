@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--optimizer", default="adam", choices=["adam", "momentum"])
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--graph", action="store_true", help="capture the step in a HIP graph")
-    ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--miopen-find", type=int, default=int(os.environ.get("BENCH_MIOPEN_FIND", "0")))
     return ap.parse_args()
 
 
@@ -55,7 +55,8 @@ def main():
     from fluxmpi_amd.models import build_model
     from fluxmpi_amd.parallel.ddp import DDP
 
-    torch.backends.cudnn.benchmark = False
+    # MIOpen find mode (exhaustive per-shape kernel search) when requested; immediate mode otherwise
+    torch.backends.cudnn.benchmark = bool(args.miopen_find)
     FluxMPI.Init()
     rank, world = FluxMPI.local_rank(), FluxMPI.total_workers()
     if world != args.gpus and rank == 0:
@@ -111,7 +112,7 @@ def main():
             "config": {"model": "ResNet50", "global_batch": world * B, "per_gpu_batch": B, "seq_len": None,
                        "image_size": args.image, "parallelism": f"dp{world}", "optimizer": args.optimizer,
                        "conv": args.conv, "norm": args.norm, "backend": FluxMPI.backend_name(),
-                       "overlap": not args.no_overlap, "loss": round(lval, 4)},
+                       "overlap": not args.no_overlap, "miopen_find": bool(args.miopen_find), "loss": round(lval, 4)},
         }
         print(json.dumps(rec), flush=True)
     FluxMPI.Finalize()

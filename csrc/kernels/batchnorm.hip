@@ -63,7 +63,7 @@ Geo geometry(int64_t rows, int64_t C) {
   g.rpi = kThreads / g.cv;
   if (g.rpi < 1) g.rpi = 1;
   // >= 64K elements per workgroup, at most 2048 workgroups
-  int64_t min_rows = (65536 + C - 1) / C;
+  int64_t min_rows = (32768 + C - 1) / C;
   int64_t blocks = (rows + min_rows - 1) / min_rows;
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
@@ -117,17 +117,19 @@ __global__ __launch_bounds__(kThreads) void bn_stats_kernel(const T* __restrict_
     int64_t end = start + g.rows_per_block;
     if (end > rows) end = rows;
     int64_t r = start + r0;
-    // 4 rows in flight per lane
-    for (; r + 3 * g.rpi < end; r += 4 * g.rpi) {
-      float f[4][8];
+    // 8 rows (8 x 16 B) in flight per lane: the reduction is latency bound otherwise
+    constexpr int U = 8;
+    for (; r + (U - 1) * g.rpi < end; r += U * g.rpi) {
+      T raw[U][8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) ld8f(x + (r + u * g.rpi) * C + c8 * 8, f[u]);
+      for (int u = 0; u < U; ++u) load8(x + (r + u * g.rpi) * C + c8 * 8, raw[u]);
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          s[j] += f[u][j];
-          q[j] = fmaf(f[u][j], f[u][j], q[j]);
+          const float f = static_cast<float>(raw[u][j]);
+          s[j] += f;
+          q[j] = fmaf(f, f, q[j]);
         }
     }
     for (; r < end; r += g.rpi) {
@@ -224,23 +226,24 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const T* __rest
     int64_t end = start + g.rows_per_block;
     if (end > rows) end = rows;
     int64_t r = start + r0;
-    for (; r + g.rpi < end; r += 2 * g.rpi) {
-      float d[2][8], xv[2][8], yv[2][8];
+    constexpr int U = 4;  // 4 rows x 3 tensors = 12 x 16 B loads in flight per lane
+    for (; r + (U - 1) * g.rpi < end; r += U * g.rpi) {
+      T d[U][8], xv[U][8], yv[U][8];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int64_t off = (r + u * g.rpi) * C + c8 * 8;
-        ld8f(dy + off, d[u]);
-        ld8f(x + off, xv[u]);
-        if (RELU) ld8f(y + off, yv[u]);
+        load8(dy + off, d[u]);
+        load8(x + off, xv[u]);
+        if (RELU) load8(y + off, yv[u]);
       }
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
+      for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          float dd = d[u][j];
-          if (RELU) dd = yv[u][j] > 0.f ? dd : 0.f;
+          float dd = static_cast<float>(d[u][j]);
+          if (RELU) dd = static_cast<float>(yv[u][j]) > 0.f ? dd : 0.f;
           s[j] += dd;
-          q[j] = fmaf(dd, (xv[u][j] - mu[j]) * is[j], q[j]);
+          q[j] = fmaf(dd, (static_cast<float>(xv[u][j]) - mu[j]) * is[j], q[j]);
         }
     }
     for (; r < end; r += g.rpi) {
