@@ -43,6 +43,8 @@ from .. import optimisers as O
 from ..ops import multi_tensor as mt
 from ..ops import optim as fused
 from ..utils.config import get_config
+from ..utils import profiling
+from ..utils.debug import Watchdog, check_replicas, check_same_structure
 from . import runtime
 from .comm import Communicator, ReduceOp
 
@@ -103,7 +105,7 @@ class DDP:
                  bucket_mb: float | None = None, first_bucket_mb: float | None = None,
                  master_weights: bool = True, average: bool = False, overlap: bool | None = None,
                  broadcast: bool = True, root_rank: int = 0, comm: Communicator | None = None,
-                 comm_dtype: torch.dtype | None = None):
+                 comm_dtype: torch.dtype | None = None, watchdog: bool | None = None):
         cfg = get_config()
         self.module = module
         self.rule = rule if rule is not None else O.Adam()
@@ -133,6 +135,14 @@ class DDP:
             for p in params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad_ready))
         self._setup_optimizer()
+        self.debug_checks = cfg.debug_checks
+        self.watchdog = None
+        if self.world > 1 and runtime.Initialized():
+            # every rank must build the same bucket plan, or collectives would mismatch
+            check_same_structure([(str(b.dtype), b.numel, len(b.params)) for b in self.buckets],
+                                 comm=runtime.cpu_comm(), what="DDP bucket plan")
+            if watchdog if watchdog is not None else cfg.extra.get("watchdog", True):
+                self.watchdog = Watchdog(comm, timeout_s=cfg.timeout_s)
         if broadcast and self.world > 1:
             self.broadcast_parameters(root_rank)
         self._next_launch = 0
@@ -260,7 +270,10 @@ class DDP:
         b.launched = True
         if self.world == 1:
             return
-        b.work = self.comm.allreduce(b.flat_grad, ReduceOp.SUM, async_op=True)
+        with profiling.range(f"fluxmpi.allreduce.bucket{b.index}"):
+            b.work = self.comm.allreduce(b.flat_grad, ReduceOp.SUM, async_op=True)
+        if self.watchdog is not None:
+            self.watchdog.track(b.work, f"allreduce of gradient bucket {b.index} ({b.numel} elements)")
 
     # ------------------------------------------------------------------ public
     def __call__(self, *args, **kw):
@@ -306,6 +319,10 @@ class DDP:
         if self.kind == "adam":
             fused.adam_advance_(self.hyper, self.adam.beta[0], self.adam.beta[1])
         self.step_count += 1
+        if self.watchdog is not None:
+            self.watchdog.check()
+        if self.debug_checks and self.world > 1:
+            check_replicas(self.module, comm=runtime.cpu_comm())
         if zero_grad:
             self.zero_grad()
 

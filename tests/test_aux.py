@@ -1,0 +1,123 @@
+"""Aux subsystems: replica/structure checks, watchdog, checkpointing, profiling."""
+import time
+
+import pytest
+import torch
+
+
+def worker_checks():
+    import fluxmpi_amd as FluxMPI
+    from fluxmpi_amd.utils.debug import (CollectiveMismatchError, ReplicaDivergenceError, check_replicas,
+                                         check_same_structure)
+    FluxMPI.Init()
+    r = FluxMPI.local_rank()
+    tree = {"w": torch.full((3, 3), float(r)), "b": torch.ones(2)}
+    try:
+        check_replicas(tree)
+        raise AssertionError("divergence not detected")
+    except ReplicaDivergenceError:
+        pass
+    tree = FluxMPI.synchronize(tree)
+    check_replicas(tree)
+    check_same_structure({"a": torch.ones(2)})
+    bad = {"a": torch.ones(2)} if r == 0 else {"a": torch.ones(3)}
+    try:
+        check_same_structure(bad)
+        raise AssertionError("structure mismatch not detected")
+    except CollectiveMismatchError:
+        pass
+    FluxMPI.Finalize()
+
+
+def test_replica_and_structure_checks(spmd):
+    spmd("tests.test_aux:worker_checks", nprocs=2)
+
+
+def test_watchdog_detects_async_error():
+    from fluxmpi_amd.utils.debug import Watchdog
+
+    class FakeComm:
+        def __init__(self):
+            self.fail = False
+
+        def check_async_error(self):
+            if self.fail:
+                raise RuntimeError("RCCL asynchronous error 3")
+
+    c = FakeComm()
+    wd = Watchdog(c, timeout_s=100, interval_s=0.01)
+    wd.check()
+    c.fail = True
+    time.sleep(0.2)
+    with pytest.raises(RuntimeError, match="watchdog"):
+        wd.check()
+    wd.stop()
+
+
+def test_watchdog_timeout():
+    from fluxmpi_amd.parallel.comm import Work
+    from fluxmpi_amd.utils.debug import Watchdog
+
+    class Never(Work):
+        def is_completed(self):
+            return False
+
+    class OK:
+        def check_async_error(self):
+            pass
+
+    wd = Watchdog(OK(), timeout_s=0.05, interval_s=0.01)
+    wd.track(Never(), "allreduce bucket 0")
+    time.sleep(0.3)
+    with pytest.raises(RuntimeError, match="did not complete"):
+        wd.check()
+
+
+def test_checkpoint_roundtrip(tmp_path):
+    from fluxmpi_amd import optimisers as O
+    from fluxmpi_amd.utils import checkpoint
+    ps = {"a": torch.randn(3, 4), "nested": (torch.randn(2), 5, "name")}
+    st = O.setup(O.Adam(1e-3), ps)
+    st, ps = O.update(st, ps, {"a": torch.ones(3, 4), "nested": (torch.ones(2), None, None)})
+    path = str(tmp_path / "ck.pt")
+    checkpoint.save(path, {"ps": ps, "st": st, "step": 7})
+    ps2 = {"a": torch.zeros(3, 4), "nested": (torch.zeros(2), 0, "x")}
+    st2 = O.setup(O.Adam(1e-3), ps2)
+    out = checkpoint.load(path, like={"ps": ps2, "st": st2, "step": 0})
+    assert torch.equal(ps2["a"], ps["a"]) and out["step"] == 7
+    assert torch.equal(st2["a"].state[0], st["a"].state[0])
+    assert out["st"]["a"].state[2] == st["a"].state[2]
+    raw = torch.load(path, weights_only=True)  # loadable without unpickling code
+    assert "ps" in raw
+
+
+def test_ddp_state_dict_roundtrip(tmp_path):
+    from fluxmpi_amd import optimisers as O
+    from fluxmpi_amd.parallel.ddp import DDP
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(4, 8), torch.nn.Linear(8, 1))
+    ddp = DDP(m, O.Adam(1e-2))
+    x = torch.randn(5, 4)
+    m(x).sum().backward()
+    ddp.step()
+    sd = ddp.state_dict()
+    torch.save(sd, tmp_path / "d.pt")
+    m2 = torch.nn.Sequential(torch.nn.Linear(4, 8), torch.nn.Linear(8, 1))
+    ddp2 = DDP(m2, O.Adam(1e-2))
+    ddp2.load_state_dict(torch.load(tmp_path / "d.pt", weights_only=True))
+    for a, b in zip(m.parameters(), m2.parameters()):
+        assert torch.equal(a, b)
+    m(x).sum().backward(); ddp.step()
+    m2(x).sum().backward(); ddp2.step()
+    for a, b in zip(m.parameters(), m2.parameters()):
+        assert torch.equal(a, b)
+
+
+def test_step_timer_and_ranges():
+    from fluxmpi_amd.utils.profiling import StepTimer, range as prange
+    t = StepTimer(torch.device("cpu"))
+    with t.phase("fwd"):
+        with prange("fwd", force=True):
+            torch.randn(100, 100) @ torch.randn(100, 100)
+    s = t.summary()
+    assert "fwd" in s and s["fwd"] >= 0
