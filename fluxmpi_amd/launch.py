@@ -33,6 +33,8 @@ def launch(nprocs: int, argv: list[str], env: dict | None = None, timeout: float
     port = master_port or free_port()
     procs = []
     base = dict(os.environ)
+    # like torchrun: avoid nprocs x all-cores OpenMP oversubscription on CPU ranks
+    base.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // max(1, nprocs))))
     if env:
         base.update(env)
     for r in range(nprocs):
