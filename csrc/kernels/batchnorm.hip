@@ -12,11 +12,11 @@
 //
 // Reductions: a workgroup accumulates fp32 per-channel partials over its rows
 // in registers, reduces the lanes that share a channel vector through LDS and
-// adds its partial to a [2][C] fp32 accumulator with global float atomics
-// (zeroed by hipMemsetAsync first). The grid is sized so each workgroup
-// streams >= 64K elements: atomic traffic stays a few % of the data traffic.
-// The consumer kernels derive per-channel coefficients from the accumulator in
-// an LDS prologue, so no separate "finalize" launch is needed.
+// adds its partial to one of 16 shards of a [16][2][C] fp32 accumulator with
+// global float atomics. A tiny finalize kernel sums the shards into the
+// per-channel statistics (and re-zeroes them, so the persistent workspace
+// needs no memset per call); the consumer kernels derive their per-channel
+// coefficients from those statistics in an LDS prologue.
 #include <stdexcept>
 #include <string>
 
@@ -75,13 +75,17 @@ Geo geometry(int64_t rows, int64_t C) {
 }
 
 // Block-level reduction of two 8-float accumulators over lanes sharing a
-// channel vector, then one atomic per channel per workgroup.
+// channel vector, then one atomic per channel per workgroup into shard
+// (blockIdx % kShards) of acc[kShards][2][C]. Sharding keeps the number of
+// same-address atomics per line ~blocks/kShards: float atomics execute at the
+// memory side, and thousands of workgroups adding into ONE line serialise.
+constexpr int kShards = 16;
+
 __device__ __forceinline__ void block_reduce_atomic(float (&a)[8], float (&b)[8], int cv, int rpi, int C,
                                                     float* __restrict__ acc, float* smem) {
   const int t = threadIdx.x;
   const int r0 = t / cv, c8 = t % cv;
   const bool active = r0 < rpi;
-  // smem layout: [rpi][C] for a, then [rpi][C] for b
   float* sa = smem;
   float* sb = smem + rpi * C;
   if (active) {
@@ -92,16 +96,61 @@ __device__ __forceinline__ void block_reduce_atomic(float (&a)[8], float (&b)[8]
     }
   }
   __syncthreads();
-  // every thread reduces some channels over the rpi rows
+  float* shard = acc + static_cast<size_t>(blockIdx.x % kShards) * 2 * C;
   for (int c = t; c < C; c += kThreads) {
     float x = 0.f, y = 0.f;
     for (int r = 0; r < rpi; ++r) {
       x += sa[r * C + c];
       y += sb[r * C + c];
     }
-    atomicAdd(acc + c, x);
-    atomicAdd(acc + C + c, y);
+    atomicAdd(shard + c, x);
+    atomicAdd(shard + C + c, y);
   }
+}
+
+// Sum the shards of channel c and re-zero them (the workspace is left zeroed
+// for the next call, so no memset is needed per launch).
+__device__ __forceinline__ void take_shards(float* __restrict__ acc, int C, int c, float& a, float& b) {
+  a = 0.f;
+  b = 0.f;
+#pragma unroll
+  for (int k = 0; k < kShards; ++k) {
+    float* sh = acc + static_cast<size_t>(k) * 2 * C;
+    a += sh[c];
+    b += sh[C + c];
+    sh[c] = 0.f;
+    sh[C + c] = 0.f;
+  }
+}
+
+__global__ void bn_finalize_fwd_kernel(float* __restrict__ acc, int C, int64_t rows, float momentum, float eps,
+                                       float* __restrict__ smean, float* __restrict__ sinv,
+                                       float* __restrict__ rmean, float* __restrict__ rvar) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s, q;
+  take_shards(acc, C, c, s, q);
+  const float inv_n = 1.f / static_cast<float>(rows);
+  const float mean = s * inv_n;
+  float var = q * inv_n - mean * mean;
+  var = var > 0.f ? var : 0.f;
+  smean[c] = mean;
+  sinv[c] = rsqrtf(var + eps);
+  if (rmean != nullptr) {
+    const float unbiased = rows > 1 ? var * static_cast<float>(rows) / static_cast<float>(rows - 1) : var;
+    rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * unbiased;
+  }
+}
+
+__global__ void bn_finalize_bwd_kernel(float* __restrict__ acc, int C, float* __restrict__ dw,
+                                       float* __restrict__ db) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s, q;
+  take_shards(acc, C, c, s, q);
+  db[c] = s;  // sum(dy_eff)
+  dw[c] = q;  // sum(dy_eff * xhat)
 }
 
 // ---------------------------------------------------------------- forward
@@ -145,40 +194,21 @@ __global__ __launch_bounds__(kThreads) void bn_stats_kernel(const T* __restrict_
   block_reduce_atomic(s, q, g.cv, g.rpi, C, acc, smem);
 }
 
-// y = act(x*scale + shift [+ res]); scale/shift derived in the prologue.
-// Block 0 also writes save_mean/save_invstd and updates the running stats.
+// y = act(x*scale + shift [+ res]); scale/shift derived in the LDS prologue from
+// (mean, invstd) = batch statistics (training) or running statistics (eval).
 template <typename T, bool RELU, bool RES>
 __global__ __launch_bounds__(kThreads) void bn_norm_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                            const T* __restrict__ res, const float* __restrict__ w,
-                                                           const float* __restrict__ b, const float* __restrict__ acc,
-                                                           float* __restrict__ rmean, float* __restrict__ rvar,
-                                                           float* __restrict__ smean, float* __restrict__ sinv,
-                                                           int64_t rows, int C, float momentum, float eps, int train,
-                                                           int64_t nvec) {
+                                                           const float* __restrict__ b,
+                                                           const float* __restrict__ mean_in,
+                                                           const float* __restrict__ stat2, int C, float eps,
+                                                           int train, int64_t nvec) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* scale = smem;
   float* shift = smem + C;
-  const float inv_n = 1.f / static_cast<float>(rows);
   for (int c = threadIdx.x; c < C; c += kThreads) {
-    float mean, invstd;
-    if (train) {
-      mean = acc[c] * inv_n;
-      float var = acc[C + c] * inv_n - mean * mean;
-      var = var > 0.f ? var : 0.f;
-      invstd = rsqrtf(var + eps);
-      if (blockIdx.x == 0) {
-        smean[c] = mean;
-        sinv[c] = invstd;
-        if (rmean != nullptr) {
-          const float unbiased = rows > 1 ? var * static_cast<float>(rows) / static_cast<float>(rows - 1) : var;
-          rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
-          rvar[c] = (1.f - momentum) * rvar[c] + momentum * unbiased;
-        }
-      }
-    } else {
-      mean = rmean[c];
-      invstd = rsqrtf(rvar[c] + eps);
-    }
+    const float mean = mean_in[c];
+    const float invstd = train ? stat2[c] : rsqrtf(stat2[c] + eps);  // save_invstd | running_var
     const float sc = (w ? w[c] : 1.f) * invstd;
     scale[c] = sc;
     shift[c] = (b ? b[c] : 0.f) - mean * sc;
@@ -265,14 +295,15 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const T* __rest
 }
 
 // dx = w*invstd * (dy_eff - sum_dy/R - xhat * sum_dy_xhat/R); dres = dy_eff
+// (sum_dy = db, sum_dy_xhat = dw, produced by bn_finalize_bwd_kernel)
 template <typename T, bool RELU, bool DRES>
 __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                              const T* __restrict__ y, const float* __restrict__ w,
                                                              const float* __restrict__ smean,
                                                              const float* __restrict__ sinv,
-                                                             const float* __restrict__ acc, T* __restrict__ dx,
-                                                             T* __restrict__ dres, float* __restrict__ dw,
-                                                             float* __restrict__ db, int64_t rows, int C,
+                                                             const float* __restrict__ dw,
+                                                             const float* __restrict__ db, T* __restrict__ dx,
+                                                             T* __restrict__ dres, int64_t rows, int C,
                                                              int64_t nvec) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* k1 = smem;          // w*invstd
@@ -284,14 +315,10 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const T* __restrict
   for (int c = threadIdx.x; c < C; c += kThreads) {
     const float iv = sinv[c];
     k1[c] = (w ? w[c] : 1.f) * iv;
-    k2[c] = acc[c] * inv_n;
-    k3[c] = acc[C + c] * inv_n;
+    k2[c] = db[c] * inv_n;
+    k3[c] = dw[c] * inv_n;
     mu[c] = smean[c];
     is[c] = iv;
-    if (blockIdx.x == 0) {
-      if (dw) dw[c] = acc[C + c];
-      if (db) db[c] = acc[c];
-    }
   }
   __syncthreads();
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
@@ -330,58 +357,44 @@ void check(int64_t C) {
 
 size_t reduce_smem(const Geo& g, int64_t C) { return static_cast<size_t>(2 * g.rpi * C) * sizeof(float); }
 
+#define FLUXMPI_BN_DISPATCH2(F, A, B, ...) \
+  if ((A) && (B)) F(true, true, __VA_ARGS__);  \
+  else if (A) F(true, false, __VA_ARGS__);    \
+  else if (B) F(false, true, __VA_ARGS__);    \
+  else F(false, false, __VA_ARGS__);
+
 template <typename T>
-void fwd_train_t(const void* x, void* y, const void* res, const float* w, const float* b, float* rm, float* rv,
-                 float* sm, float* si, float* ws, int64_t rows, int64_t C, float momentum, float eps, int relu,
-                 hipStream_t s) {
-  Geo g = geometry(rows, C);
-  FLUXMPI_HIP_CHECK(hipMemsetAsync(ws, 0, 2 * C * sizeof(float), s));
-  bn_stats_kernel<T><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(static_cast<const T*>(x), rows, (int)C, g, ws);
-  FLUXMPI_HIP_CHECK(hipGetLastError());
+void norm_t(const void* x, void* y, const void* res, const float* w, const float* b, const float* mean,
+            const float* stat2, int64_t rows, int64_t C, float eps, int train, int relu, hipStream_t s) {
   const int64_t nvec = rows * C / 8;
   const int nb = elementwise_blocks(nvec);
   const size_t sm2 = 2 * C * sizeof(float);
   const T* xr = static_cast<const T*>(x);
   T* yr = static_cast<T*>(y);
   const T* rr = static_cast<const T*>(res);
-#define LAUNCH(RELU, RES)                                                                                        \
-  bn_norm_kernel<T, RELU, RES><<<nb, kThreads, sm2, s>>>(xr, yr, rr, w, b, ws, rm, rv, sm, si, rows, (int)C, \
-                                                         momentum, eps, 1, nvec)
-  if (relu && res) LAUNCH(true, true);
-  else if (relu) LAUNCH(true, false);
-  else if (res) LAUNCH(false, true);
-  else LAUNCH(false, false);
+#define LAUNCH(RELU, RES, _)                                                                                  \
+  bn_norm_kernel<T, RELU, RES><<<nb, kThreads, sm2, s>>>(xr, yr, rr, w, b, mean, stat2, (int)C, eps, train, nvec)
+  FLUXMPI_BN_DISPATCH2(LAUNCH, relu, res != nullptr, 0)
 #undef LAUNCH
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
 
 template <typename T>
-void fwd_infer_t(const void* x, void* y, const void* res, const float* w, const float* b, const float* rm,
-                 const float* rv, int64_t rows, int64_t C, float eps, int relu, hipStream_t s) {
-  const int64_t nvec = rows * C / 8;
-  const int nb = elementwise_blocks(nvec);
-  const size_t sm2 = 2 * C * sizeof(float);
-  const T* xr = static_cast<const T*>(x);
-  T* yr = static_cast<T*>(y);
-  const T* rr = static_cast<const T*>(res);
-  float* rmm = const_cast<float*>(rm);
-  float* rvv = const_cast<float*>(rv);
-#define LAUNCH(RELU, RES)                                                                                     \
-  bn_norm_kernel<T, RELU, RES><<<nb, kThreads, sm2, s>>>(xr, yr, rr, w, b, nullptr, rmm, rvv, nullptr, nullptr, \
-                                                         rows, (int)C, 0.f, eps, 0, nvec)
-  if (relu && res) LAUNCH(true, true);
-  else if (relu) LAUNCH(true, false);
-  else if (res) LAUNCH(false, true);
-  else LAUNCH(false, false);
-#undef LAUNCH
+void fwd_train_t(const void* x, void* y, const void* res, const float* w, const float* b, float* rm, float* rv,
+                 float* sm, float* si, float* ws, int64_t rows, int64_t C, float momentum, float eps, int relu,
+                 hipStream_t s) {
+  Geo g = geometry(rows, C);
+  bn_stats_kernel<T><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(static_cast<const T*>(x), rows, (int)C, g, ws);
   FLUXMPI_HIP_CHECK(hipGetLastError());
+  bn_finalize_fwd_kernel<<<(int)((C + 255) / 256), 256, 0, s>>>(ws, (int)C, rows, momentum, eps, sm, si, rm, rv);
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+  norm_t<T>(x, y, res, w, b, sm, si, rows, C, eps, 1, relu, s);
 }
 
 template <typename T>
 void bwd_t(const void* dy, const void* x, const void* y, const float* w, const float* sm, const float* si, void* dx,
            void* dres, float* dw, float* db, float* ws, int64_t rows, int64_t C, int relu, hipStream_t s) {
   Geo g = geometry(rows, C);
-  FLUXMPI_HIP_CHECK(hipMemsetAsync(ws, 0, 2 * C * sizeof(float), s));
   const T* dyr = static_cast<const T*>(dy);
   const T* xr = static_cast<const T*>(x);
   const T* yr = static_cast<const T*>(y);
@@ -390,18 +403,17 @@ void bwd_t(const void* dy, const void* x, const void* y, const float* w, const f
   else
     bn_bwd_reduce_kernel<T, false><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(dyr, xr, yr, sm, si, rows, (int)C, g, ws);
   FLUXMPI_HIP_CHECK(hipGetLastError());
+  bn_finalize_bwd_kernel<<<(int)((C + 255) / 256), 256, 0, s>>>(ws, (int)C, dw, db);
+  FLUXMPI_HIP_CHECK(hipGetLastError());
   const int64_t nvec = rows * C / 8;
   const int nb = elementwise_blocks(nvec);
   const size_t sm5 = 5 * C * sizeof(float);
   T* dxr = static_cast<T*>(dx);
   T* drr = static_cast<T*>(dres);
-#define LAUNCH(RELU, DRES)                                                                                         \
-  bn_bwd_dx_kernel<T, RELU, DRES><<<nb, kThreads, sm5, s>>>(dyr, xr, yr, w, sm, si, ws, dxr, drr, dw, db, rows, \
-                                                            (int)C, nvec)
-  if (relu && dres) LAUNCH(true, true);
-  else if (relu) LAUNCH(true, false);
-  else if (dres) LAUNCH(false, true);
-  else LAUNCH(false, false);
+#define LAUNCH(RELU, DRES, _)                                                                                    \
+  bn_bwd_dx_kernel<T, RELU, DRES><<<nb, kThreads, sm5, s>>>(dyr, xr, yr, w, sm, si, dw, db, dxr, drr, rows, (int)C, \
+                                                            nvec)
+  FLUXMPI_BN_DISPATCH2(LAUNCH, relu, dres != nullptr, 0)
 #undef LAUNCH
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
@@ -410,7 +422,7 @@ void bwd_t(const void* dy, const void* x, const void* y, const float* w, const f
 
 size_t bn_workspace_floats(int64_t rows, int64_t C) {
   (void)rows;
-  return static_cast<size_t>(2 * C);
+  return static_cast<size_t>(kShards) * 2 * static_cast<size_t>(C);
 }
 
 void bn_fwd_train(const void* x, void* y, const void* residual, const float* weight, const float* bias,
@@ -433,9 +445,9 @@ void bn_fwd_infer(const void* x, void* y, const void* residual, const float* wei
                   int dtype, hipStream_t stream) {
   check(C);
   switch (dtype) {
-    case kBF16: fwd_infer_t<bf16>(x, y, residual, weight, bias, running_mean, running_var, rows, C, eps, relu, stream); break;
-    case kF16: fwd_infer_t<f16>(x, y, residual, weight, bias, running_mean, running_var, rows, C, eps, relu, stream); break;
-    case kF32: fwd_infer_t<float>(x, y, residual, weight, bias, running_mean, running_var, rows, C, eps, relu, stream); break;
+    case kBF16: norm_t<bf16>(x, y, residual, weight, bias, running_mean, running_var, rows, C, eps, 0, relu, stream); break;
+    case kF16: norm_t<f16>(x, y, residual, weight, bias, running_mean, running_var, rows, C, eps, 0, relu, stream); break;
+    case kF32: norm_t<float>(x, y, residual, weight, bias, running_mean, running_var, rows, C, eps, 0, relu, stream); break;
     default: throw std::runtime_error("fused batchnorm: unsupported dtype");
   }
 }

@@ -33,6 +33,26 @@ def _nhwc(x: torch.Tensor) -> torch.Tensor:
     return x.contiguous()
 
 
+_WS: dict = {}
+_SHARDS = 16
+_MAXC = 2048
+
+
+def _workspace(x: torch.Tensor) -> torch.Tensor:
+    """Persistent zeroed [16][2][2048] fp32 accumulator per (device, stream).
+
+    The kernels leave it zeroed after every call (the finalize kernel re-zeroes
+    the shards it consumes), so there is no memset per BatchNorm launch.
+    """
+    stream = torch.cuda.current_stream(x.device)
+    key = (x.device.index, stream.cuda_stream)
+    ws = _WS.get(key)
+    if ws is None:
+        ws = torch.zeros(_SHARDS * 2 * _MAXC, device=x.device, dtype=torch.float32)
+        _WS[key] = ws
+    return ws
+
+
 def kernel_supported(x: torch.Tensor) -> bool:
     if not x.is_cuda or x.dtype not in (torch.bfloat16, torch.float16, torch.float32):
         return False
@@ -54,7 +74,7 @@ class _FusedBN(torch.autograd.Function):
         b32 = bias.float() if bias is not None else None
         save_mean = torch.empty(ch, device=x.device, dtype=torch.float32)
         save_inv = torch.empty(ch, device=x.device, dtype=torch.float32)
-        ws = torch.empty(2 * ch, device=x.device, dtype=torch.float32)
+        ws = _workspace(x)
         stream = torch.cuda.current_stream(x.device).cuda_stream
         C.bn_fwd_train(x.data_ptr(), y.data_ptr(), res.data_ptr() if res is not None else 0,
                        w32.data_ptr() if w32 is not None else 0, b32.data_ptr() if b32 is not None else 0,
@@ -77,18 +97,22 @@ class _FusedBN(torch.autograd.Function):
         rows, ch = _rows_c(x)
         dx = torch.empty_like(x)
         dres = torch.empty_like(x) if ctx.has_res else None
-        dw = torch.empty(ch, device=x.device, dtype=torch.float32) if w32 is not None else None
-        db = torch.empty(ch, device=x.device, dtype=torch.float32) if ctx.has_bias else None
-        ws = torch.empty(2 * ch, device=x.device, dtype=torch.float32)
+        # the finalize kernel always produces both reductions (they feed dx)
+        dw = torch.empty(ch, device=x.device, dtype=torch.float32)
+        db = torch.empty(ch, device=x.device, dtype=torch.float32)
+        ws = _workspace(x)
         stream = torch.cuda.current_stream(x.device).cuda_stream
         C.bn_bwd(dy.data_ptr(), x.data_ptr(), y.data_ptr() if y is not None else 0,
                  w32.data_ptr() if w32 is not None else 0, save_mean.data_ptr(), save_inv.data_ptr(), dx.data_ptr(),
-                 dres.data_ptr() if dres is not None else 0, dw.data_ptr() if dw is not None else 0,
-                 db.data_ptr() if db is not None else 0, ws.data_ptr(), rows, ch, int(ctx.relu),
-                 DTYPE_CODE[x.dtype], stream)
-        if dw is not None and ctx.wdtype != torch.float32:
+                 dres.data_ptr() if dres is not None else 0, dw.data_ptr(), db.data_ptr(), ws.data_ptr(), rows, ch,
+                 int(ctx.relu), DTYPE_CODE[x.dtype], stream)
+        if w32 is None:
+            dw = None
+        elif ctx.wdtype != torch.float32:
             dw = dw.to(ctx.wdtype)
-        if db is not None and ctx.wdtype != torch.float32:
+        if not ctx.has_bias:
+            db = None
+        elif ctx.wdtype != torch.float32:
             db = db.to(ctx.wdtype)
         return dx, dw, db, dres, None, None, None, None, None
 
