@@ -65,7 +65,8 @@ void bn_fwd_train(const void* x, void* y, const void* residual, const float* wei
                   float eps, int relu, int dtype, hipStream_t stream);
 // Backward: given dy (and y when relu, to mask), computes dx, dweight, dbias and
 // (when residual was fused) d_residual = masked dy.
-void bn_bwd(const void* dy, const void* x, const void* y, const float* weight,
+// y == nullptr with relu: the ReLU mask is recomputed from x (bit-identical to forward).
+void bn_bwd(const void* dy, const void* x, const void* y, const float* weight, const float* bias,
             const float* save_mean, const float* save_invstd, void* dx, void* dres,
             float* dweight, float* dbias, float* workspace, int64_t rows, int64_t C, int relu,
             int dtype, hipStream_t stream);

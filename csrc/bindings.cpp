@@ -82,11 +82,11 @@ PYBIND11_MODULE(_C, m) {
                        dtype, S(stream));
         });
   m.def("bn_bwd",
-        [](uintptr_t dy, uintptr_t x, uintptr_t y, uintptr_t w, uintptr_t sm, uintptr_t si, uintptr_t dx,
+        [](uintptr_t dy, uintptr_t x, uintptr_t y, uintptr_t w, uintptr_t b, uintptr_t sm, uintptr_t si, uintptr_t dx,
            uintptr_t dres, uintptr_t dw, uintptr_t db, uintptr_t ws, int64_t rows, int64_t C, int relu, int dtype,
            uintptr_t stream) {
           bn_bwd(reinterpret_cast<const void*>(dy), reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(y),
-                 reinterpret_cast<const float*>(w), reinterpret_cast<const float*>(sm),
+                 reinterpret_cast<const float*>(w), reinterpret_cast<const float*>(b), reinterpret_cast<const float*>(sm),
                  reinterpret_cast<const float*>(si), reinterpret_cast<void*>(dx), reinterpret_cast<void*>(dres),
                  reinterpret_cast<float*>(dw), reinterpret_cast<float*>(db), reinterpret_cast<float*>(ws), rows, C,
                  relu, dtype, S(stream));

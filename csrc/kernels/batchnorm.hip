@@ -211,7 +211,7 @@ __global__ __launch_bounds__(kThreads) void bn_norm_kernel(const T* __restrict__
     const float invstd = train ? stat2[c] : rsqrtf(stat2[c] + eps);  // save_invstd | running_var
     const float sc = (w ? w[c] : 1.f) * invstd;
     scale[c] = sc;
-    shift[c] = (b ? b[c] : 0.f) - mean * sc;
+    shift[c] = fmaf(-mean, sc, b ? b[c] : 0.f);  // explicit fma: backward recomputes it bit-identically
   }
   __syncthreads();
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
@@ -235,9 +235,14 @@ __global__ __launch_bounds__(kThreads) void bn_norm_kernel(const T* __restrict__
 
 // ---------------------------------------------------------------- backward
 // acc[0:C] += sum(dy_eff), acc[C:2C] += sum(dy_eff * xhat)
-template <typename T, bool RELU>
+// RM (ReLU mode): 0 none; 1 mask from the saved output y (needed when a residual
+// was added before the ReLU); 2 mask recomputed from x as fmaf(x, scale, shift) > 0
+// with scale/shift computed bit-identically to the forward prologue, so y is
+// neither saved nor re-read (one fewer activation read per element, both passes).
+template <typename T, int RM>
 __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x,
-                                                                 const T* __restrict__ y,
+                                                                 const T* __restrict__ y, const float* __restrict__ w,
+                                                                 const float* __restrict__ b,
                                                                  const float* __restrict__ smean,
                                                                  const float* __restrict__ sinv, int64_t rows, int C,
                                                                  Geo g, float* __restrict__ acc) {
@@ -246,17 +251,20 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const T* __rest
   const int r0 = t / g.cv, c8 = t % g.cv;
   float s[8] = {0}, q[8] = {0};
   if (r0 < g.rpi) {
-    float mu[8], is[8];
+    float mu[8], is[8], sc[8], sh[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      mu[j] = smean[c8 * 8 + j];
-      is[j] = sinv[c8 * 8 + j];
+      const int c = c8 * 8 + j;
+      mu[j] = smean[c];
+      is[j] = sinv[c];
+      sc[j] = (w ? w[c] : 1.f) * is[j];
+      sh[j] = fmaf(-mu[j], sc[j], b ? b[c] : 0.f);
     }
     const int64_t start = static_cast<int64_t>(blockIdx.x) * g.rows_per_block;
     int64_t end = start + g.rows_per_block;
     if (end > rows) end = rows;
     int64_t r = start + r0;
-    constexpr int U = 4;  // 4 rows x 3 tensors = 12 x 16 B loads in flight per lane
+    constexpr int U = 4;  // 4 rows x (2|3) tensors of 16 B loads in flight per lane
     for (; r + (U - 1) * g.rpi < end; r += U * g.rpi) {
       T d[U][8], xv[U][8], yv[U][8];
 #pragma unroll
@@ -264,16 +272,18 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const T* __rest
         const int64_t off = (r + u * g.rpi) * C + c8 * 8;
         load8(dy + off, d[u]);
         load8(x + off, xv[u]);
-        if (RELU) load8(y + off, yv[u]);
+        if (RM == 1) load8(y + off, yv[u]);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           float dd = static_cast<float>(d[u][j]);
-          if (RELU) dd = static_cast<float>(yv[u][j]) > 0.f ? dd : 0.f;
+          const float xf = static_cast<float>(xv[u][j]);
+          if (RM == 1) dd = static_cast<float>(yv[u][j]) > 0.f ? dd : 0.f;
+          if (RM == 2) dd = fmaf(xf, sc[j], sh[j]) > 0.f ? dd : 0.f;
           s[j] += dd;
-          q[j] = fmaf(dd, (static_cast<float>(xv[u][j]) - mu[j]) * is[j], q[j]);
+          q[j] = fmaf(dd, (xf - mu[j]) * is[j], q[j]);
         }
     }
     for (; r < end; r += g.rpi) {
@@ -281,11 +291,12 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const T* __rest
       float d[8], xv[8], yv[8];
       ld8f(dy + off, d);
       ld8f(x + off, xv);
-      if (RELU) ld8f(y + off, yv);
+      if (RM == 1) ld8f(y + off, yv);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float dd = d[j];
-        if (RELU) dd = yv[j] > 0.f ? dd : 0.f;
+        if (RM == 1) dd = yv[j] > 0.f ? dd : 0.f;
+        if (RM == 2) dd = fmaf(xv[j], sc[j], sh[j]) > 0.f ? dd : 0.f;
         s[j] += dd;
         q[j] = fmaf(dd, (xv[j] - mu[j]) * is[j], q[j]);
       }
@@ -296,9 +307,10 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const T* __rest
 
 // dx = w*invstd * (dy_eff - sum_dy/R - xhat * sum_dy_xhat/R); dres = dy_eff
 // (sum_dy = db, sum_dy_xhat = dw, produced by bn_finalize_bwd_kernel)
-template <typename T, bool RELU, bool DRES>
+template <typename T, int RM, bool DRES>
 __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                              const T* __restrict__ y, const float* __restrict__ w,
+                                                             const float* __restrict__ bias,
                                                              const float* __restrict__ smean,
                                                              const float* __restrict__ sinv,
                                                              const float* __restrict__ dw,
@@ -306,19 +318,23 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const T* __restrict
                                                              T* __restrict__ dres, int64_t rows, int C,
                                                              int64_t nvec) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* k1 = smem;          // w*invstd
+  float* k1 = smem;          // w*invstd (== forward scale)
   float* k2 = smem + C;      // mean(dy_eff)
   float* k3 = smem + 2 * C;  // mean(dy_eff*xhat)
   float* mu = smem + 3 * C;
   float* is = smem + 4 * C;
+  float* sh = smem + 5 * C;  // forward shift (RM == 2)
   const float inv_n = 1.f / static_cast<float>(rows);
   for (int c = threadIdx.x; c < C; c += kThreads) {
     const float iv = sinv[c];
-    k1[c] = (w ? w[c] : 1.f) * iv;
+    const float m = smean[c];
+    const float sc = (w ? w[c] : 1.f) * iv;
+    k1[c] = sc;
     k2[c] = db[c] * inv_n;
     k3[c] = dw[c] * inv_n;
-    mu[c] = smean[c];
+    mu[c] = m;
     is[c] = iv;
+    sh[c] = fmaf(-m, sc, bias ? bias[c] : 0.f);
   }
   __syncthreads();
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
@@ -328,12 +344,13 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const T* __restrict
     float d[8], xv[8], yv[8];
     ld8f(dy + e, d);
     ld8f(x + e, xv);
-    if (RELU) ld8f(y + e, yv);
+    if (RM == 1) ld8f(y + e, yv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int c = c0 + j;
       float dd = d[j];
-      if (RELU) dd = yv[j] > 0.f ? dd : 0.f;
+      if (RM == 1) dd = yv[j] > 0.f ? dd : 0.f;
+      if (RM == 2) dd = fmaf(xv[j], k1[c], sh[c]) > 0.f ? dd : 0.f;
       d[j] = dd;
       const float xh = (xv[j] - mu[c]) * is[c];
       xv[j] = k1[c] * (dd - k2[c] - xh * k3[c]);
@@ -392,28 +409,37 @@ void fwd_train_t(const void* x, void* y, const void* res, const float* w, const 
 }
 
 template <typename T>
-void bwd_t(const void* dy, const void* x, const void* y, const float* w, const float* sm, const float* si, void* dx,
-           void* dres, float* dw, float* db, float* ws, int64_t rows, int64_t C, int relu, hipStream_t s) {
+void bwd_t(const void* dy, const void* x, const void* y, const float* w, const float* b, const float* sm,
+           const float* si, void* dx, void* dres, float* dw, float* db, float* ws, int64_t rows, int64_t C, int relu,
+           hipStream_t s) {
   Geo g = geometry(rows, C);
   const T* dyr = static_cast<const T*>(dy);
   const T* xr = static_cast<const T*>(x);
   const T* yr = static_cast<const T*>(y);
-  if (relu)
-    bn_bwd_reduce_kernel<T, true><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(dyr, xr, yr, sm, si, rows, (int)C, g, ws);
+  // relu: 0 none, 1 mask from y, 2 mask recomputed from x (y == nullptr)
+  const int rm = relu == 0 ? 0 : (y != nullptr ? 1 : 2);
+  const size_t rsm = reduce_smem(g, C);
+  if (rm == 0)
+    bn_bwd_reduce_kernel<T, 0><<<g.blocks, kThreads, rsm, s>>>(dyr, xr, yr, w, b, sm, si, rows, (int)C, g, ws);
+  else if (rm == 1)
+    bn_bwd_reduce_kernel<T, 1><<<g.blocks, kThreads, rsm, s>>>(dyr, xr, yr, w, b, sm, si, rows, (int)C, g, ws);
   else
-    bn_bwd_reduce_kernel<T, false><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(dyr, xr, yr, sm, si, rows, (int)C, g, ws);
+    bn_bwd_reduce_kernel<T, 2><<<g.blocks, kThreads, rsm, s>>>(dyr, xr, yr, w, b, sm, si, rows, (int)C, g, ws);
   FLUXMPI_HIP_CHECK(hipGetLastError());
   bn_finalize_bwd_kernel<<<(int)((C + 255) / 256), 256, 0, s>>>(ws, (int)C, dw, db);
   FLUXMPI_HIP_CHECK(hipGetLastError());
   const int64_t nvec = rows * C / 8;
   const int nb = elementwise_blocks(nvec);
-  const size_t sm5 = 5 * C * sizeof(float);
+  const size_t sm6 = 6 * C * sizeof(float);
   T* dxr = static_cast<T*>(dx);
   T* drr = static_cast<T*>(dres);
-#define LAUNCH(RELU, DRES, _)                                                                                    \
-  bn_bwd_dx_kernel<T, RELU, DRES><<<nb, kThreads, sm5, s>>>(dyr, xr, yr, w, sm, si, dw, db, dxr, drr, rows, (int)C, \
-                                                            nvec)
-  FLUXMPI_BN_DISPATCH2(LAUNCH, relu, dres != nullptr, 0)
+#define LAUNCH(RM, DRES)                                                                                    \
+  bn_bwd_dx_kernel<T, RM, DRES><<<nb, kThreads, sm6, s>>>(dyr, xr, yr, w, b, sm, si, dw, db, dxr, drr, rows, \
+                                                          (int)C, nvec)
+  const bool has_dres = dres != nullptr;
+  if (rm == 0) { if (has_dres) LAUNCH(0, true); else LAUNCH(0, false); }
+  else if (rm == 1) { if (has_dres) LAUNCH(1, true); else LAUNCH(1, false); }
+  else { if (has_dres) LAUNCH(2, true); else LAUNCH(2, false); }
 #undef LAUNCH
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
@@ -452,16 +478,16 @@ void bn_fwd_infer(const void* x, void* y, const void* residual, const float* wei
   }
 }
 
-void bn_bwd(const void* dy, const void* x, const void* y, const float* weight, const float* save_mean,
+void bn_bwd(const void* dy, const void* x, const void* y, const float* weight, const float* bias, const float* save_mean,
             const float* save_invstd, void* dx, void* dres, float* dweight, float* dbias, float* workspace,
             int64_t rows, int64_t C, int relu, int dtype, hipStream_t stream) {
   check(C);
   switch (dtype) {
-    case kBF16: bwd_t<bf16>(dy, x, y, weight, save_mean, save_invstd, dx, dres, dweight, dbias, workspace, rows, C,
+    case kBF16: bwd_t<bf16>(dy, x, y, weight, bias, save_mean, save_invstd, dx, dres, dweight, dbias, workspace, rows, C,
                             relu, stream); break;
-    case kF16: bwd_t<f16>(dy, x, y, weight, save_mean, save_invstd, dx, dres, dweight, dbias, workspace, rows, C,
+    case kF16: bwd_t<f16>(dy, x, y, weight, bias, save_mean, save_invstd, dx, dres, dweight, dbias, workspace, rows, C,
                           relu, stream); break;
-    case kF32: bwd_t<float>(dy, x, y, weight, save_mean, save_invstd, dx, dres, dweight, dbias, workspace, rows, C,
+    case kF32: bwd_t<float>(dy, x, y, weight, bias, save_mean, save_invstd, dx, dres, dweight, dbias, workspace, rows, C,
                             relu, stream); break;
     default: throw std::runtime_error("fused batchnorm: unsupported dtype");
   }

@@ -86,13 +86,15 @@ class _FusedBN(torch.autograd.Function):
         ctx.has_res = residual is not None
         ctx.wdtype = weight.dtype if weight is not None else None
         ctx.has_bias = bias is not None
-        ctx.save_for_backward(x, y if relu else None, w32, save_mean, save_inv)
+        # Without a residual the ReLU mask is recomputed from x in the backward
+        # kernels (bit-identical to the forward), so y is neither saved nor re-read.
+        ctx.save_for_backward(x, y if (relu and residual is not None) else None, w32, b32, save_mean, save_inv)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         C = _ext.get(required=True)
-        x, y, w32, save_mean, save_inv = ctx.saved_tensors
+        x, y, w32, b32, save_mean, save_inv = ctx.saved_tensors
         dy = _nhwc(dy)
         rows, ch = _rows_c(x)
         dx = torch.empty_like(x)
@@ -103,7 +105,8 @@ class _FusedBN(torch.autograd.Function):
         ws = _workspace(x)
         stream = torch.cuda.current_stream(x.device).cuda_stream
         C.bn_bwd(dy.data_ptr(), x.data_ptr(), y.data_ptr() if y is not None else 0,
-                 w32.data_ptr() if w32 is not None else 0, save_mean.data_ptr(), save_inv.data_ptr(), dx.data_ptr(),
+                 w32.data_ptr() if w32 is not None else 0, b32.data_ptr() if b32 is not None else 0,
+                 save_mean.data_ptr(), save_inv.data_ptr(), dx.data_ptr(),
                  dres.data_ptr() if dres is not None else 0, dw.data_ptr(), db.data_ptr(), ws.data_ptr(), rows, ch,
                  int(ctx.relu), DTYPE_CODE[x.dtype], stream)
         if w32 is None:

@@ -1,7 +1,7 @@
 # shared helpers for GPU sessions: `source scripts/gpu_lib.sh`
 set -o pipefail
 ROOT="${GRAFT_REPO_ROOT:-$(cd "$(dirname "${BASH_SOURCE[0]}")/.." && pwd)}"
-cd "$ROOT"; OUT="$ROOT/gpurun_out"; mkdir -p "$OUT"; export TMPDIR=/tmp
+cd "$ROOT"; OUT="$ROOT/gpurun_out"; mkdir -p "$OUT"; export TMPDIR=/tmp PYTHONPATH="$ROOT${PYTHONPATH:+:$PYTHONPATH}"
 # step <name> <timeout_s> <allow_test_failure 0|1> cmd...
 step() { local name=$1 t=$2 allow=$3; shift 3; echo "[$(date +%T)] $name" | tee -a "$OUT/steps.log"
   timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1; local rc=$?
