@@ -492,7 +492,10 @@ class RcclComm(Communicator):
         return self._exit(list(tensors), list(tensors), async_op)
 
     def check_async_error(self):
-        code = self._h.async_error()
+        h = self._h
+        if h is None:  # destroyed (Finalize) — nothing left to watch
+            return
+        code = h.async_error()
         if code != 0:
             raise RuntimeError(f"RCCL asynchronous error {code}: {self._h.error_string(code)}")
 

@@ -67,6 +67,7 @@ class _Bucket:
     launched: bool = False
     work: object = None
     names: list = field(default_factory=list)
+    comm_buf: torch.Tensor | None = None
 
 
 def _strided_view(flat: torch.Tensor, like: torch.Tensor, offset: int) -> torch.Tensor:
@@ -120,6 +121,9 @@ class DDP:
             comm = runtime.comm_for(params[0]) if runtime.Initialized() else None
         self.comm = comm
         self.world = comm.size if comm is not None else 1
+        if comm_dtype is None:
+            comm_dtype = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16,
+                          "bfloat16": torch.bfloat16, "fp16": torch.float16}.get(cfg.comm_dtype)
         self.comm_dtype = comm_dtype
         bb = int((bucket_mb if bucket_mb is not None else cfg.bucket_mb) * (1 << 20))
         fb = int((first_bucket_mb if first_bucket_mb is not None else cfg.first_bucket_mb) * (1 << 20))
@@ -270,8 +274,15 @@ class DDP:
         b.launched = True
         if self.world == 1:
             return
+        buf = b.flat_grad
+        if self.comm_dtype is not None and self.comm_dtype != b.dtype:
+            # K5: cast the bucket to the wire dtype (e.g. fp32 grads sent as bf16) in one launch
+            if b.comm_buf is None:
+                b.comm_buf = torch.empty(b.numel, dtype=self.comm_dtype, device=b.device)
+            mt.pack([b.flat_grad], b.comm_buf, [0])
+            buf = b.comm_buf
         with profiling.range(f"fluxmpi.allreduce.bucket{b.index}"):
-            b.work = self.comm.allreduce(b.flat_grad, ReduceOp.SUM, async_op=True)
+            b.work = self.comm.allreduce(buf, ReduceOp.SUM, async_op=True)
         if self.watchdog is not None:
             self.watchdog.track(b.work, f"allreduce of gradient bucket {b.index} ({b.numel} elements)")
 
@@ -300,9 +311,15 @@ class DDP:
             b.ready = True
         self._launch_ready()
         for b in self.buckets:
-            if b.work is not None:
-                b.work.wait()
-                b.work = None
+            self._finish(b)
+
+    def _finish(self, b: _Bucket):
+        """Make the compute stream wait for bucket ``b``'s allreduce (and cast it back)."""
+        if b.work is not None:
+            b.work.wait()
+            b.work = None
+            if b.comm_buf is not None and self.comm_dtype != b.dtype:
+                mt.unpack(b.comm_buf, [b.flat_grad], [0])
 
     def step(self, zero_grad: bool = True):
         """Finish the gradient allreduces and apply the fused optimiser to every bucket."""
@@ -312,9 +329,7 @@ class DDP:
                 b.ready = True
         self._launch_ready()
         for b in self.buckets:
-            if b.work is not None:
-                b.work.wait()
-                b.work = None
+            self._finish(b)
             self._apply(b, gscale)
         if self.kind == "adam":
             fused.adam_advance_(self.hyper, self.adam.beta[0], self.adam.beta[1])

@@ -80,6 +80,16 @@ def worker_ddp():
         ((ddp(x[:4]) - y[:4]) ** 2).sum().backward()
     ((ddp(x[4:]) - y[4:]) ** 2).sum().backward()
     ddp.step()
+
+    # low-precision wire format (K5 cast): same result within bf16 rounding
+    m_a, m_b = _mlp(7), _mlp(7)
+    d_a = DDP(m_a, O.Descent(0.1), comm_dtype=torch.bfloat16)
+    d_b = DDP(m_b, O.Descent(0.1))
+    for d in (d_a, d_b):
+        ((d(x) - y) ** 2).mean().backward()
+        d.step()
+    for p, q in zip(m_a.parameters(), m_b.parameters()):
+        torch.testing.assert_close(p, q, rtol=2e-2, atol=2e-3)
     FluxMPI.Finalize()
 
 
