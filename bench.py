@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--optimizer", default="adam", choices=["adam", "momentum"])
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--graph", action="store_true", help="capture the step in a HIP graph")
-    ap.add_argument("--miopen-find", type=int, default=int(os.environ.get("BENCH_MIOPEN_FIND", "0")))
+    ap.add_argument("--miopen-find", type=int, default=int(os.environ.get("BENCH_MIOPEN_FIND", "1")))
     return ap.parse_args()
 
 
@@ -55,9 +55,14 @@ def main():
     from fluxmpi_amd.models import build_model
     from fluxmpi_amd.parallel.ddp import DDP
 
-    # MIOpen find mode (exhaustive per-shape kernel search) when requested; immediate mode otherwise
-    torch.backends.cudnn.benchmark = bool(args.miopen_find)
     FluxMPI.Init()
+    # MIOpen find mode, seeded with the tuning db recorded on MI355X (tuning/miopen): the
+    # per-shape solver choice without the ~3.5 min search. --miopen-find 0: immediate mode.
+    if args.miopen_find:
+        from fluxmpi_amd.utils.miopen import install_tuned_db
+
+        install_tuned_db(rank=int(os.environ.get("LOCAL_RANK", "0")))
+    torch.backends.cudnn.benchmark = bool(args.miopen_find)
     rank, world = FluxMPI.local_rank(), FluxMPI.total_workers()
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but world size {world}", file=sys.stderr)
@@ -91,6 +96,12 @@ def main():
         ddp.step()
         return loss
 
+    if args.graph:
+        from fluxmpi_amd.parallel.graph import GraphedStep
+
+        graphed = GraphedStep(ddp, lambda d, xx, yy: F.cross_entropy(d(xx).float(), yy), x, y)
+        step = lambda: graphed(x, y)  # noqa: E731
+
     for _ in range(args.warmup):
         step()
     FluxMPI.barrier()
@@ -112,7 +123,7 @@ def main():
             "config": {"model": "ResNet50", "global_batch": world * B, "per_gpu_batch": B, "seq_len": None,
                        "image_size": args.image, "parallelism": f"dp{world}", "optimizer": args.optimizer,
                        "conv": args.conv, "norm": args.norm, "backend": FluxMPI.backend_name(),
-                       "overlap": not args.no_overlap, "miopen_find": bool(args.miopen_find), "loss": round(lval, 4)},
+                       "overlap": not args.no_overlap, "miopen_find": bool(args.miopen_find), "hip_graph": bool(args.graph), "loss": round(lval, 4)},
         }
         print(json.dumps(rec), flush=True)
     FluxMPI.Finalize()
