@@ -76,4 +76,26 @@ void bn_fwd_infer(const void* x, void* y, const void* residual, const float* wei
                   const float* bias, const float* running_mean, const float* running_var,
                   int64_t rows, int64_t C, float eps, int relu, int dtype, hipStream_t stream);
 
+// ---- MFMA bf16 GEMM with BatchNorm fusions (1x1 convolutions) --------------------
+// C[M,N] = A[M,K] * B[N,K]^T. a_kmajor: A stored [M][lda] (K contiguous), else [K][lda]
+// (M contiguous); b_kmajor likewise for B. mode 0: C bf16; mode 1: C bf16 + per-column
+// sum/sumsq into stats[16][2][N] (sharded, caller-zeroed); mode 2: C fp32 += (atomics,
+// allows split-K over `splits`). a_scale/a_shift: relu(A*s+t) per k applied on load
+// (K-major A); b_scale/b_shift: per n on load (N-major B).
+struct GemmProblem {
+  const void* a;
+  const void* b;
+  void* c;
+  int64_t lda, ldb, ldc, M, N, K;
+  bool a_kmajor, b_kmajor;
+  int mode, splits;
+  const float* a_scale;
+  const float* a_shift;
+  const float* b_scale;
+  const float* b_shift;
+  float* stats;
+  int tile_m, tile_n;  // 0 = auto, 64 forces the 64 tile
+};
+void gemm_bf16(const GemmProblem& g, hipStream_t stream);
+
 }  // namespace fluxmpi

@@ -1,0 +1,350 @@
+// MFMA bf16 GEMM for 1x1 convolutions (NHWC) with BatchNorm fusions — gfx950.
+//
+// C[M,N] = A[M,K] · B[N,K]^T, fp32 accumulation on v_mfma_f32_16x16x32_bf16.
+// Each operand is stored either K-major ([rows][K], K contiguous) or
+// row-major along M/N ([K][rows], rows contiguous); the three 1x1-conv passes
+// map onto it as
+//
+//   forward  Y[m,co]  = X[m,:] · W[co,:]^T        A = X  (K-major)  B = W (K-major)
+//   dgrad    dX[m,ci] = dY[m,:] · W[:,ci]         A = dY (K-major)  B = W (N-major)
+//   wgrad    dW[co,ci]= dY[:,co]^T · X[:,ci]      A = dY (M-major)  B = X (N-major), split-K
+//
+// Staging is global -> registers -> LDS in the operand's natural orientation
+// (16 B per lane, coalesced). K-major tiles are read as MFMA fragments with
+// ds_read_b128; M/N-major tiles with two ds_read_b64_tr_b16 (gfx950 transposed
+// LDS read), so no operand is ever transposed in memory.
+//
+// Fusions that remove whole activation passes of ResNet-50:
+//  * prologue: an optional per-channel affine + ReLU (the previous BatchNorm,
+//    y = relu(x*scale + shift), bit-identical to the fused-BN kernels) applied
+//    to the A operand (forward, per k) or the B operand (wgrad, per n) while
+//    staging, so the normalised activation is never written to HBM;
+//  * epilogue: bf16 store + per-column sum / sum-of-squares of the stored bf16
+//    values into a sharded fp32 accumulator (the next BatchNorm's statistics,
+//    so its stats pass disappears); or fp32 atomic accumulation (split-K).
+//
+// Tiles: 256 threads = 4 waves (2 x 2), BM x BN x 32 with BM, BN in {64, 128};
+// LDS double buffer, next tile's global loads issued before the MFMAs of the
+// current one. Blocks are mapped XCD-aware (consecutive tiles of one XCD share
+// the A panel in its L2).
+#include <stdexcept>
+#include <string>
+
+#include "../api.h"
+#include "common.h"
+
+namespace fluxmpi {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kThreads = 256;
+constexpr int BK = 32;
+constexpr int kShards = 16;  // must match batchnorm.hip
+
+struct GemmArgs {
+  const bf16* a;
+  const bf16* b;
+  void* c;
+  int64_t lda, ldb, ldc;  // row strides of the stored matrices (elements)
+  int64_t M, N, K;
+  int64_t k_per_split;  // K range per blockIdx.z
+  const float* a_scale;  // prologue affine on A (per k) — forward
+  const float* a_shift;
+  const float* b_scale;  // prologue affine on B (per n) — wgrad
+  const float* b_shift;
+  float* stats;  // [kShards][2][N] sharded per-column sum / sumsq (epilogue mode 1)
+  int mode;      // 0: store bf16; 1: store bf16 + stats; 2: fp32 atomic add into c
+  int tiles_m, tiles_n;
+};
+
+template <int ROWS, bool KMAJOR>
+struct Tile {
+  // K-major image: [ROWS][BK + 8] (80 B rows: conflict-free 16-row b128 reads)
+  // rows-major image: [BK][ROWS + 16] (row stride == 8 dwords mod 64 for tr reads)
+  static constexpr int kStride = KMAJOR ? (BK + 8) : (ROWS + 16);
+  static constexpr int kElems = KMAJOR ? ROWS * kStride : BK * kStride;
+  static constexpr int kChunks = ROWS * BK / 8;  // 16 B chunks per tile
+};
+
+__device__ __forceinline__ void affine_relu8(uint4& v, const float* __restrict__ sc, const float* __restrict__ sh,
+                                             int64_t c0) {
+  bf16 e[8];
+  __builtin_memcpy(e, &v, 16);
+  const float4 s0 = *reinterpret_cast<const float4*>(sc + c0);
+  const float4 s1 = *reinterpret_cast<const float4*>(sc + c0 + 4);
+  const float4 h0 = *reinterpret_cast<const float4*>(sh + c0);
+  const float4 h1 = *reinterpret_cast<const float4*>(sh + c0 + 4);
+  const float s[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+  const float h[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float o = fmaf(static_cast<float>(e[j]), s[j], h[j]);
+    e[j] = static_cast<bf16>(o > 0.f ? o : 0.f);
+  }
+  __builtin_memcpy(&v, e, 16);
+}
+
+// Load this thread's share of one operand tile into registers.
+// KMAJOR: tile rows r0..r0+ROWS of [rows][K] storage, k range k0..k0+BK.
+// !KMAJOR: k rows k0..k0+BK of [K][rows] storage, columns r0..r0+ROWS.
+template <int ROWS, bool KMAJOR, int CPT>
+__device__ __forceinline__ void stage_load(uint4 (&reg)[CPT],
+                                           const bf16* __restrict__ g, int64_t ld, int64_t rows, int64_t r0,
+                                           int64_t k0, const float* __restrict__ sc, const float* __restrict__ sh,
+                                           bool affine_on_k) {
+  static_assert(CPT == ROWS * BK / 8 / kThreads, "chunks per thread");
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int idx = threadIdx.x + i * kThreads;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (KMAJOR) {
+      const int r = idx / (BK / 8), kc = idx % (BK / 8);
+      const int64_t row = r0 + r;
+      if (row < rows) {
+        v = *reinterpret_cast<const uint4*>(g + row * ld + k0 + kc * 8);
+        if (sc != nullptr) affine_relu8(v, sc, sh, k0 + kc * 8);
+      }
+    } else {
+      const int kr = idx / (ROWS / 8), rc = idx % (ROWS / 8);
+      const int64_t col = r0 + rc * 8;
+      if (col < rows) {
+        v = *reinterpret_cast<const uint4*>(g + (k0 + kr) * ld + col);
+        if (sc != nullptr) affine_relu8(v, sc, sh, col);  // per-row-channel affine (wgrad B = X)
+      }
+    }
+    reg[i] = v;
+  }
+  (void)affine_on_k;
+}
+
+template <int ROWS, bool KMAJOR, int CPT>
+__device__ __forceinline__ void stage_store(bf16* __restrict__ lds, const uint4 (&reg)[CPT]) {
+  constexpr int S = Tile<ROWS, KMAJOR>::kStride;
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int idx = threadIdx.x + i * kThreads;
+    if (KMAJOR) {
+      const int r = idx / (BK / 8), kc = idx % (BK / 8);
+      *reinterpret_cast<uint4*>(lds + r * S + kc * 8) = reg[i];
+    } else {
+      const int kr = idx / (ROWS / 8), rc = idx % (ROWS / 8);
+      *reinterpret_cast<uint4*>(lds + kr * S + rc * 8) = reg[i];
+    }
+  }
+}
+
+// Fragment of a 16-row slice starting at tile row `r0` for the 16x16x32 MFMA:
+// lane l gets rows (r0 + (l&15)), k = 8*(l>>4) .. +7.
+template <int ROWS, bool KMAJOR>
+__device__ __forceinline__ bf16x8 read_frag(const bf16* __restrict__ lds, int r0) {
+  const int l = threadIdx.x & 63;
+  constexpr int S = Tile<ROWS, KMAJOR>::kStride;
+  if (KMAJOR) {
+    return *reinterpret_cast<const bf16x8*>(lds + (r0 + (l & 15)) * S + 8 * (l >> 4));
+  } else {
+    // ds_read_b64_tr_b16: in each 16-lane group g, lane 4q+p addresses row (k) q of a
+    // 4-row block, columns 4p..4p+3; lane i receives column i of the 4 rows.
+    const int g = l >> 4, li = l & 15, q = li >> 2, p = li & 3;
+    const bf16* base0 = lds + (8 * g + q) * S + r0 + 4 * p;
+    const bf16* base1 = base0 + 4 * S;
+    typedef short short4v __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) short4v lds_short4v;
+    short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(base0));
+    short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(base1));
+    bf16x8 out;
+    __builtin_memcpy(&out, &lo, 8);
+    __builtin_memcpy(reinterpret_cast<char*>(&out) + 8, &hi, 8);
+    return out;
+  }
+}
+
+template <int BM, int BN, bool AK, bool BKM>
+__global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs p) {
+  using TA = Tile<BM, AK>;
+  using TB = Tile<BN, BKM>;
+  constexpr int WM = BM / 2, WN = BN / 2;  // per-wave tile
+  constexpr int FM = WM / 16, FN = WN / 16;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (TA::kElems + TB::kElems)];
+  // buffer b of A at smem + b*kElemsA, of B at smem + 2*kElemsA + b*kElemsB
+  auto la = [&](int b) { return smem + b * TA::kElems; };
+  auto lb = [&](int b) { return smem + 2 * TA::kElems + b * TB::kElems; };
+
+  // XCD-aware tile order: blocks b and b+8 share an XCD; give each XCD a contiguous
+  // range of tiles (n fastest) so neighbouring tiles share A rows in that L2.
+  const int nt = p.tiles_m * p.tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int q = nt / 8, r = nt % 8, xcd = bid % 8, pos = bid / 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+  }
+  const int tm = bid / p.tiles_n, tn = bid % p.tiles_n;
+  const int64_t m0 = static_cast<int64_t>(tm) * BM, n0 = static_cast<int64_t>(tn) * BN;
+  const int64_t kbeg = static_cast<int64_t>(blockIdx.z) * p.k_per_split;
+  int64_t kend = kbeg + p.k_per_split;
+  if (kend > p.K) kend = p.K;
+
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 ra[TA::kChunks / kThreads], rb[TB::kChunks / kThreads];
+  const int64_t nk = (kend - kbeg) / BK;
+  if (nk > 0) {
+    stage_load<BM, AK>(ra, p.a, p.lda, p.M, m0, kbeg, p.a_scale, p.a_shift, true);
+    stage_load<BN, BKM>(rb, p.b, p.ldb, p.N, n0, kbeg, p.b_scale, p.b_shift, false);
+    stage_store<BM, AK>(la(0), ra);
+    stage_store<BN, BKM>(lb(0), rb);
+  }
+  __syncthreads();
+  for (int64_t t = 0; t < nk; ++t) {
+    const int cur = t & 1;
+    const bool more = t + 1 < nk;
+    if (more) {  // issue next tile's global loads before this tile's MFMAs
+      const int64_t k1 = kbeg + (t + 1) * BK;
+      stage_load<BM, AK>(ra, p.a, p.lda, p.M, m0, k1, p.a_scale, p.a_shift, true);
+      stage_load<BN, BKM>(rb, p.b, p.ldb, p.N, n0, k1, p.b_scale, p.b_shift, false);
+    }
+    bf16x8 fa[FM], fb[FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) fa[i] = read_frag<BM, AK>(la(cur), wm * WM + i * 16);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) fb[j] = read_frag<BN, BKM>(lb(cur), wn * WN + j * 16);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    if (more) {
+      stage_store<BM, AK>(la(cur ^ 1), ra);
+      stage_store<BN, BKM>(lb(cur ^ 1), rb);
+    }
+    __syncthreads();
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  // acc[i][j][r]: row m0 + wm*WM + i*16 + 4*(lane>>4) + r, col n0 + wn*WN + j*16 + (lane&15)
+  const int col_in = lane & 15, rq = 4 * (lane >> 4);
+  if (p.mode == 2) {
+    float* c = static_cast<float*>(p.c);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int64_t n = n0 + wn * WN + j * 16 + col_in;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t m = m0 + wm * WM + i * 16 + rq + r;
+          if (m < p.M && n < p.N) atomicAdd(c + m * p.ldc + n, acc[i][j][r]);
+        }
+      }
+    return;
+  }
+  bf16* c = static_cast<bf16*>(p.c);
+  float cs[FN], cq[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    cs[j] = 0.f;
+    cq[j] = 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int64_t n = n0 + wn * WN + j * 16 + col_in;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = m0 + wm * WM + i * 16 + rq + r;
+        if (m < p.M && n < p.N) {
+          const bf16 v = static_cast<bf16>(acc[i][j][r]);
+          c[m * p.ldc + n] = v;
+          const float f = static_cast<float>(v);
+          cs[j] += f;
+          cq[j] = fmaf(f, f, cq[j]);
+        }
+      }
+    }
+  if (p.mode == 1) {
+    // reduce over the 4 lane groups holding the same column, then over the 2 waves in M
+    __shared__ float red[2][2][BN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      cs[j] += __shfl_xor(cs[j], 16, 64);
+      cs[j] += __shfl_xor(cs[j], 32, 64);
+      cq[j] += __shfl_xor(cq[j], 16, 64);
+      cq[j] += __shfl_xor(cq[j], 32, 64);
+    }
+    if (lane < 16) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        red[wm][0][wn * WN + j * 16 + lane] = cs[j];
+        red[wm][1][wn * WN + j * 16 + lane] = cq[j];
+      }
+    }
+    __syncthreads();
+    float* shard = p.stats + static_cast<size_t>(blockIdx.x % kShards) * 2 * p.N;
+    for (int c2 = threadIdx.x; c2 < BN; c2 += kThreads) {
+      const int64_t n = n0 + c2;
+      if (n < p.N) {
+        atomicAdd(shard + n, red[0][0][c2] + red[1][0][c2]);
+        atomicAdd(shard + p.N + n, red[0][1][c2] + red[1][1][c2]);
+      }
+    }
+  }
+}
+
+template <int BM, int BN, bool AK, bool BKM>
+void launch(const GemmArgs& a0, int splits, hipStream_t s) {
+  GemmArgs a = a0;
+  a.tiles_m = static_cast<int>((a.M + BM - 1) / BM);
+  a.tiles_n = static_cast<int>((a.N + BN - 1) / BN);
+  dim3 grid(a.tiles_m * a.tiles_n, 1, splits);
+  gemm_kernel<BM, BN, AK, BKM><<<grid, kThreads, 0, s>>>(a);
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace
+
+void gemm_bf16(const GemmProblem& g, hipStream_t stream) {
+  if (g.K % BK != 0) throw std::runtime_error("gemm_bf16: K must be a multiple of 32");
+  if ((g.a_kmajor ? g.lda : g.lda) % 8 != 0 || g.ldb % 8 != 0)
+    throw std::runtime_error("gemm_bf16: leading dimensions must be multiples of 8");
+  if (g.mode == 1 && g.stats == nullptr) throw std::runtime_error("gemm_bf16: stats buffer required");
+  if ((g.a_scale != nullptr) && !g.a_kmajor) throw std::runtime_error("gemm_bf16: A affine needs K-major A");
+  if ((g.b_scale != nullptr) && g.b_kmajor) throw std::runtime_error("gemm_bf16: B affine needs N-major B");
+  GemmArgs a{};
+  a.a = static_cast<const bf16*>(g.a);
+  a.b = static_cast<const bf16*>(g.b);
+  a.c = g.c;
+  a.lda = g.lda; a.ldb = g.ldb; a.ldc = g.ldc;
+  a.M = g.M; a.N = g.N; a.K = g.K;
+  int splits = g.splits < 1 ? 1 : g.splits;
+  int64_t kps = (g.K / BK + splits - 1) / splits * BK;
+  splits = static_cast<int>((g.K + kps - 1) / kps);
+  a.k_per_split = kps;
+  a.a_scale = g.a_scale; a.a_shift = g.a_shift;
+  a.b_scale = g.b_scale; a.b_shift = g.b_shift;
+  a.stats = g.stats;
+  a.mode = g.mode;
+  if (splits > 1 && g.mode != 2) throw std::runtime_error("gemm_bf16: split-K needs mode 2 (fp32 atomics)");
+  const bool bm128 = g.M >= 128 && g.tile_m != 64;
+  const bool bn128 = g.N >= 128 && g.tile_n != 64;
+#define DISPATCH(AK, BKM)                                            \
+  if (bm128 && bn128) launch<128, 128, AK, BKM>(a, splits, stream);  \
+  else if (bm128) launch<128, 64, AK, BKM>(a, splits, stream);       \
+  else if (bn128) launch<64, 128, AK, BKM>(a, splits, stream);       \
+  else launch<64, 64, AK, BKM>(a, splits, stream);
+  if (g.a_kmajor && g.b_kmajor) { DISPATCH(true, true) }
+  else if (g.a_kmajor && !g.b_kmajor) { DISPATCH(true, false) }
+  else if (!g.a_kmajor && !g.b_kmajor) { DISPATCH(false, false) }
+  else { DISPATCH(false, true) }
+#undef DISPATCH
+}
+
+}  // namespace fluxmpi
