@@ -62,11 +62,13 @@ void mt_sgd(const std::vector<uintptr_t>& param, const std::vector<uintptr_t>& g
 void bn_fwd_train(const void* x, void* y, const void* residual, const float* weight,
                   const float* bias, float* running_mean, float* running_var, float* save_mean,
                   float* save_invstd, float* workspace, int64_t rows, int64_t C, float momentum,
-                  float eps, int relu, int dtype, hipStream_t stream);
+                  float eps, int relu, uint8_t* relu_mask, int dtype, hipStream_t stream);
 // Backward: given dy (and y when relu, to mask), computes dx, dweight, dbias and
 // (when residual was fused) d_residual = masked dy.
 // y == nullptr with relu: the ReLU mask is recomputed from x (bit-identical to forward).
-void bn_bwd(const void* dy, const void* x, const void* y, const float* weight, const float* bias,
+// relu_mask (optional): the 1-bit-per-element mask written by bn_fwd_train.
+void bn_bwd(const void* dy, const void* x, const void* y, const uint8_t* relu_mask, const float* weight,
+            const float* bias,
             const float* save_mean, const float* save_invstd, void* dx, void* dres,
             float* dweight, float* dbias, float* workspace, int64_t rows, int64_t C, int relu,
             int dtype, hipStream_t stream);

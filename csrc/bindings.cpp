@@ -66,12 +66,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_fwd_train",
         [](uintptr_t x, uintptr_t y, uintptr_t res, uintptr_t w, uintptr_t b, uintptr_t rm, uintptr_t rv,
            uintptr_t sm, uintptr_t si, uintptr_t ws, int64_t rows, int64_t C, float momentum, float eps, int relu,
-           int dtype, uintptr_t stream) {
+           uintptr_t mask, int dtype, uintptr_t stream) {
           bn_fwd_train(reinterpret_cast<const void*>(x), reinterpret_cast<void*>(y), reinterpret_cast<const void*>(res),
                        reinterpret_cast<const float*>(w), reinterpret_cast<const float*>(b),
                        reinterpret_cast<float*>(rm), reinterpret_cast<float*>(rv), reinterpret_cast<float*>(sm),
-                       reinterpret_cast<float*>(si), reinterpret_cast<float*>(ws), rows, C, momentum, eps, relu, dtype,
-                       S(stream));
+                       reinterpret_cast<float*>(si), reinterpret_cast<float*>(ws), rows, C, momentum, eps, relu,
+                       reinterpret_cast<uint8_t*>(mask), dtype, S(stream));
         });
   m.def("bn_fwd_infer",
         [](uintptr_t x, uintptr_t y, uintptr_t res, uintptr_t w, uintptr_t b, uintptr_t rm, uintptr_t rv,
@@ -82,10 +82,12 @@ PYBIND11_MODULE(_C, m) {
                        dtype, S(stream));
         });
   m.def("bn_bwd",
-        [](uintptr_t dy, uintptr_t x, uintptr_t y, uintptr_t w, uintptr_t b, uintptr_t sm, uintptr_t si, uintptr_t dx,
+        [](uintptr_t dy, uintptr_t x, uintptr_t y, uintptr_t mask, uintptr_t w, uintptr_t b, uintptr_t sm, uintptr_t si,
+           uintptr_t dx,
            uintptr_t dres, uintptr_t dw, uintptr_t db, uintptr_t ws, int64_t rows, int64_t C, int relu, int dtype,
            uintptr_t stream) {
           bn_bwd(reinterpret_cast<const void*>(dy), reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(y),
+                 reinterpret_cast<const uint8_t*>(mask),
                  reinterpret_cast<const float*>(w), reinterpret_cast<const float*>(b), reinterpret_cast<const float*>(sm),
                  reinterpret_cast<const float*>(si), reinterpret_cast<void*>(dx), reinterpret_cast<void*>(dres),
                  reinterpret_cast<float*>(dw), reinterpret_cast<float*>(db), reinterpret_cast<float*>(ws), rows, C,

@@ -202,7 +202,10 @@ __global__ __launch_bounds__(kThreads) void bn_norm_kernel(const T* __restrict__
                                                            const float* __restrict__ b,
                                                            const float* __restrict__ mean_in,
                                                            const float* __restrict__ stat2, int C, float eps,
-                                                           int train, int64_t nvec) {
+                                                           int train, int64_t nvec, uint8_t* __restrict__ mask) {
+  // mask (optional, RELU only): bit j of byte v = (element 8v+j > 0). One byte per
+  // 8 elements lets the backward apply the ReLU of a residual block without
+  // re-reading y (2 B/element -> 1/8 B/element).
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* scale = smem;
   float* shift = smem + C;
@@ -222,14 +225,19 @@ __global__ __launch_bounds__(kThreads) void bn_norm_kernel(const T* __restrict__
     ld8f(x + e, f);
     float rr[8];
     if (RES) ld8f(res + e, rr);
+    unsigned bits = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float o = fmaf(f[j], scale[c0 + j], shift[c0 + j]);
       if (RES) o += rr[j];
-      if (RELU) o = o > 0.f ? o : 0.f;
+      if (RELU) {
+        bits |= (o > 0.f ? 1u : 0u) << j;
+        o = o > 0.f ? o : 0.f;
+      }
       f[j] = o;
     }
     st8f(y + e, f);
+    if (RELU && mask != nullptr) mask[v] = static_cast<uint8_t>(bits);
   }
 }
 
@@ -241,7 +249,9 @@ __global__ __launch_bounds__(kThreads) void bn_norm_kernel(const T* __restrict__
 // neither saved nor re-read (one fewer activation read per element, both passes).
 template <typename T, int RM>
 __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x,
-                                                                 const T* __restrict__ y, const float* __restrict__ w,
+                                                                 const T* __restrict__ y,
+                                                                 const uint8_t* __restrict__ mask,
+                                                                 const float* __restrict__ w,
                                                                  const float* __restrict__ b,
                                                                  const float* __restrict__ smean,
                                                                  const float* __restrict__ sinv, int64_t rows, int C,
@@ -267,12 +277,14 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const T* __rest
     constexpr int U = 4;  // 4 rows x (2|3) tensors of 16 B loads in flight per lane
     for (; r + (U - 1) * g.rpi < end; r += U * g.rpi) {
       T d[U][8], xv[U][8], yv[U][8];
+      unsigned mb[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t off = (r + u * g.rpi) * C + c8 * 8;
         load8(dy + off, d[u]);
         load8(x + off, xv[u]);
         if (RM == 1) load8(y + off, yv[u]);
+        if (RM == 3) mb[u] = mask[off >> 3];
       }
 #pragma unroll
       for (int u = 0; u < U; ++u)
@@ -282,6 +294,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const T* __rest
           const float xf = static_cast<float>(xv[u][j]);
           if (RM == 1) dd = static_cast<float>(yv[u][j]) > 0.f ? dd : 0.f;
           if (RM == 2) dd = fmaf(xf, sc[j], sh[j]) > 0.f ? dd : 0.f;
+          if (RM == 3) dd = (mb[u] >> j) & 1u ? dd : 0.f;
           s[j] += dd;
           q[j] = fmaf(dd, (xf - mu[j]) * is[j], q[j]);
         }
@@ -292,11 +305,13 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const T* __rest
       ld8f(dy + off, d);
       ld8f(x + off, xv);
       if (RM == 1) ld8f(y + off, yv);
+      const unsigned mbs = RM == 3 ? mask[off >> 3] : 0u;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float dd = d[j];
         if (RM == 1) dd = yv[j] > 0.f ? dd : 0.f;
         if (RM == 2) dd = fmaf(xv[j], sc[j], sh[j]) > 0.f ? dd : 0.f;
+        if (RM == 3) dd = (mbs >> j) & 1u ? dd : 0.f;
         s[j] += dd;
         q[j] = fmaf(dd, (xv[j] - mu[j]) * is[j], q[j]);
       }
@@ -309,7 +324,9 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const T* __rest
 // (sum_dy = db, sum_dy_xhat = dw, produced by bn_finalize_bwd_kernel)
 template <typename T, int RM, bool DRES>
 __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const T* __restrict__ dy, const T* __restrict__ x,
-                                                             const T* __restrict__ y, const float* __restrict__ w,
+                                                             const T* __restrict__ y,
+                                                             const uint8_t* __restrict__ mask,
+                                                             const float* __restrict__ w,
                                                              const float* __restrict__ bias,
                                                              const float* __restrict__ smean,
                                                              const float* __restrict__ sinv,
@@ -345,11 +362,13 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const T* __restrict
     ld8f(dy + e, d);
     ld8f(x + e, xv);
     if (RM == 1) ld8f(y + e, yv);
+    const unsigned mbs = RM == 3 ? mask[v] : 0u;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int c = c0 + j;
       float dd = d[j];
       if (RM == 1) dd = yv[j] > 0.f ? dd : 0.f;
+      if (RM == 3) dd = (mbs >> j) & 1u ? dd : 0.f;
       if (RM == 2) dd = fmaf(xv[j], k1[c], sh[c]) > 0.f ? dd : 0.f;
       d[j] = dd;
       const float xh = (xv[j] - mu[c]) * is[c];
@@ -382,15 +401,17 @@ size_t reduce_smem(const Geo& g, int64_t C) { return static_cast<size_t>(2 * g.r
 
 template <typename T>
 void norm_t(const void* x, void* y, const void* res, const float* w, const float* b, const float* mean,
-            const float* stat2, int64_t rows, int64_t C, float eps, int train, int relu, hipStream_t s) {
+            const float* stat2, int64_t rows, int64_t C, float eps, int train, int relu, uint8_t* mask,
+            hipStream_t s) {
   const int64_t nvec = rows * C / 8;
   const int nb = elementwise_blocks(nvec);
   const size_t sm2 = 2 * C * sizeof(float);
   const T* xr = static_cast<const T*>(x);
   T* yr = static_cast<T*>(y);
   const T* rr = static_cast<const T*>(res);
-#define LAUNCH(RELU, RES, _)                                                                                  \
-  bn_norm_kernel<T, RELU, RES><<<nb, kThreads, sm2, s>>>(xr, yr, rr, w, b, mean, stat2, (int)C, eps, train, nvec)
+#define LAUNCH(RELU, RES, _)                                                                                     \
+  bn_norm_kernel<T, RELU, RES><<<nb, kThreads, sm2, s>>>(xr, yr, rr, w, b, mean, stat2, (int)C, eps, train, nvec, \
+                                                         mask)
   FLUXMPI_BN_DISPATCH2(LAUNCH, relu, res != nullptr, 0)
 #undef LAUNCH
   FLUXMPI_HIP_CHECK(hipGetLastError());
@@ -399,32 +420,33 @@ void norm_t(const void* x, void* y, const void* res, const float* w, const float
 template <typename T>
 void fwd_train_t(const void* x, void* y, const void* res, const float* w, const float* b, float* rm, float* rv,
                  float* sm, float* si, float* ws, int64_t rows, int64_t C, float momentum, float eps, int relu,
-                 hipStream_t s) {
+                 uint8_t* mask, hipStream_t s) {
   Geo g = geometry(rows, C);
   bn_stats_kernel<T><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(static_cast<const T*>(x), rows, (int)C, g, ws);
   FLUXMPI_HIP_CHECK(hipGetLastError());
   bn_finalize_fwd_kernel<<<(int)((C + 255) / 256), 256, 0, s>>>(ws, (int)C, rows, momentum, eps, sm, si, rm, rv);
   FLUXMPI_HIP_CHECK(hipGetLastError());
-  norm_t<T>(x, y, res, w, b, sm, si, rows, C, eps, 1, relu, s);
+  norm_t<T>(x, y, res, w, b, sm, si, rows, C, eps, 1, relu, mask, s);
 }
 
 template <typename T>
-void bwd_t(const void* dy, const void* x, const void* y, const float* w, const float* b, const float* sm,
-           const float* si, void* dx, void* dres, float* dw, float* db, float* ws, int64_t rows, int64_t C, int relu,
-           hipStream_t s) {
+void bwd_t(const void* dy, const void* x, const void* y, const uint8_t* mask, const float* w, const float* b,
+           const float* sm, const float* si, void* dx, void* dres, float* dw, float* db, float* ws, int64_t rows,
+           int64_t C, int relu, hipStream_t s) {
   Geo g = geometry(rows, C);
   const T* dyr = static_cast<const T*>(dy);
   const T* xr = static_cast<const T*>(x);
   const T* yr = static_cast<const T*>(y);
-  // relu: 0 none, 1 mask from y, 2 mask recomputed from x (y == nullptr)
-  const int rm = relu == 0 ? 0 : (y != nullptr ? 1 : 2);
+  // relu: 0 none; 1 mask from y; 2 mask recomputed from x (no residual); 3 mask from saved bits
+  const int rm = relu == 0 ? 0 : (mask != nullptr ? 3 : (y != nullptr ? 1 : 2));
   const size_t rsm = reduce_smem(g, C);
-  if (rm == 0)
-    bn_bwd_reduce_kernel<T, 0><<<g.blocks, kThreads, rsm, s>>>(dyr, xr, yr, w, b, sm, si, rows, (int)C, g, ws);
-  else if (rm == 1)
-    bn_bwd_reduce_kernel<T, 1><<<g.blocks, kThreads, rsm, s>>>(dyr, xr, yr, w, b, sm, si, rows, (int)C, g, ws);
-  else
-    bn_bwd_reduce_kernel<T, 2><<<g.blocks, kThreads, rsm, s>>>(dyr, xr, yr, w, b, sm, si, rows, (int)C, g, ws);
+#define RED(RM) \
+  bn_bwd_reduce_kernel<T, RM><<<g.blocks, kThreads, rsm, s>>>(dyr, xr, yr, mask, w, b, sm, si, rows, (int)C, g, ws)
+  if (rm == 0) RED(0);
+  else if (rm == 1) RED(1);
+  else if (rm == 2) RED(2);
+  else RED(3);
+#undef RED
   FLUXMPI_HIP_CHECK(hipGetLastError());
   bn_finalize_bwd_kernel<<<(int)((C + 255) / 256), 256, 0, s>>>(ws, (int)C, dw, db);
   FLUXMPI_HIP_CHECK(hipGetLastError());
@@ -433,13 +455,14 @@ void bwd_t(const void* dy, const void* x, const void* y, const float* w, const f
   const size_t sm6 = 6 * C * sizeof(float);
   T* dxr = static_cast<T*>(dx);
   T* drr = static_cast<T*>(dres);
-#define LAUNCH(RM, DRES)                                                                                    \
-  bn_bwd_dx_kernel<T, RM, DRES><<<nb, kThreads, sm6, s>>>(dyr, xr, yr, w, b, sm, si, dw, db, dxr, drr, rows, \
+#define LAUNCH(RM, DRES)                                                                                          \
+  bn_bwd_dx_kernel<T, RM, DRES><<<nb, kThreads, sm6, s>>>(dyr, xr, yr, mask, w, b, sm, si, dw, db, dxr, drr, rows, \
                                                           (int)C, nvec)
   const bool has_dres = dres != nullptr;
   if (rm == 0) { if (has_dres) LAUNCH(0, true); else LAUNCH(0, false); }
   else if (rm == 1) { if (has_dres) LAUNCH(1, true); else LAUNCH(1, false); }
-  else { if (has_dres) LAUNCH(2, true); else LAUNCH(2, false); }
+  else if (rm == 2) { if (has_dres) LAUNCH(2, true); else LAUNCH(2, false); }
+  else { if (has_dres) LAUNCH(3, true); else LAUNCH(3, false); }
 #undef LAUNCH
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
@@ -453,15 +476,16 @@ size_t bn_workspace_floats(int64_t rows, int64_t C) {
 
 void bn_fwd_train(const void* x, void* y, const void* residual, const float* weight, const float* bias,
                   float* running_mean, float* running_var, float* save_mean, float* save_invstd, float* workspace,
-                  int64_t rows, int64_t C, float momentum, float eps, int relu, int dtype, hipStream_t stream) {
+                  int64_t rows, int64_t C, float momentum, float eps, int relu, uint8_t* relu_mask, int dtype,
+                  hipStream_t stream) {
   check(C);
   switch (dtype) {
     case kBF16: fwd_train_t<bf16>(x, y, residual, weight, bias, running_mean, running_var, save_mean, save_invstd,
-                                  workspace, rows, C, momentum, eps, relu, stream); break;
+                                  workspace, rows, C, momentum, eps, relu, relu_mask, stream); break;
     case kF16: fwd_train_t<f16>(x, y, residual, weight, bias, running_mean, running_var, save_mean, save_invstd,
-                                workspace, rows, C, momentum, eps, relu, stream); break;
+                                workspace, rows, C, momentum, eps, relu, relu_mask, stream); break;
     case kF32: fwd_train_t<float>(x, y, residual, weight, bias, running_mean, running_var, save_mean, save_invstd,
-                                  workspace, rows, C, momentum, eps, relu, stream); break;
+                                  workspace, rows, C, momentum, eps, relu, relu_mask, stream); break;
     default: throw std::runtime_error("fused batchnorm: unsupported dtype");
   }
 }
@@ -471,23 +495,24 @@ void bn_fwd_infer(const void* x, void* y, const void* residual, const float* wei
                   int dtype, hipStream_t stream) {
   check(C);
   switch (dtype) {
-    case kBF16: norm_t<bf16>(x, y, residual, weight, bias, running_mean, running_var, rows, C, eps, 0, relu, stream); break;
-    case kF16: norm_t<f16>(x, y, residual, weight, bias, running_mean, running_var, rows, C, eps, 0, relu, stream); break;
-    case kF32: norm_t<float>(x, y, residual, weight, bias, running_mean, running_var, rows, C, eps, 0, relu, stream); break;
+    case kBF16: norm_t<bf16>(x, y, residual, weight, bias, running_mean, running_var, rows, C, eps, 0, relu, nullptr, stream); break;
+    case kF16: norm_t<f16>(x, y, residual, weight, bias, running_mean, running_var, rows, C, eps, 0, relu, nullptr, stream); break;
+    case kF32: norm_t<float>(x, y, residual, weight, bias, running_mean, running_var, rows, C, eps, 0, relu, nullptr, stream); break;
     default: throw std::runtime_error("fused batchnorm: unsupported dtype");
   }
 }
 
-void bn_bwd(const void* dy, const void* x, const void* y, const float* weight, const float* bias, const float* save_mean,
+void bn_bwd(const void* dy, const void* x, const void* y, const uint8_t* relu_mask, const float* weight,
+            const float* bias, const float* save_mean,
             const float* save_invstd, void* dx, void* dres, float* dweight, float* dbias, float* workspace,
             int64_t rows, int64_t C, int relu, int dtype, hipStream_t stream) {
   check(C);
   switch (dtype) {
-    case kBF16: bwd_t<bf16>(dy, x, y, weight, bias, save_mean, save_invstd, dx, dres, dweight, dbias, workspace, rows, C,
+    case kBF16: bwd_t<bf16>(dy, x, y, relu_mask, weight, bias, save_mean, save_invstd, dx, dres, dweight, dbias, workspace, rows, C,
                             relu, stream); break;
-    case kF16: bwd_t<f16>(dy, x, y, weight, bias, save_mean, save_invstd, dx, dres, dweight, dbias, workspace, rows, C,
+    case kF16: bwd_t<f16>(dy, x, y, relu_mask, weight, bias, save_mean, save_invstd, dx, dres, dweight, dbias, workspace, rows, C,
                           relu, stream); break;
-    case kF32: bwd_t<float>(dy, x, y, weight, bias, save_mean, save_invstd, dx, dres, dweight, dbias, workspace, rows, C,
+    case kF32: bwd_t<float>(dy, x, y, relu_mask, weight, bias, save_mean, save_invstd, dx, dres, dweight, dbias, workspace, rows, C,
                             relu, stream); break;
     default: throw std::runtime_error("fused batchnorm: unsupported dtype");
   }

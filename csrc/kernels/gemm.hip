@@ -246,54 +246,73 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs p) {
       }
     return;
   }
-  bf16* c = static_cast<bf16*>(p.c);
-  float cs[FN], cq[FN];
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    cs[j] = 0.f;
-    cq[j] = 0.f;
-  }
+  // bf16 output: stage the tile through LDS (the operand buffers are free after the
+  // loop's final barrier) so every lane stores 16 contiguous bytes; the BatchNorm
+  // statistics are taken from the same staged bf16 values.
+  constexpr int CS = BN + 8;  // padded row (bf16 elements)
+  static_assert(BM * CS <= 2 * (TA::kElems + TB::kElems), "C tile must fit the operand LDS");
+  bf16* cl = smem;
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int64_t n = n0 + wn * WN + j * 16 + col_in;
+    for (int j = 0; j < FN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t m = m0 + wm * WM + i * 16 + rq + r;
-        if (m < p.M && n < p.N) {
-          const bf16 v = static_cast<bf16>(acc[i][j][r]);
-          c[m * p.ldc + n] = v;
-          const float f = static_cast<float>(v);
-          cs[j] += f;
-          cq[j] = fmaf(f, f, cq[j]);
-        }
+      for (int r = 0; r < 4; ++r)
+        cl[(wm * WM + i * 16 + rq + r) * CS + wn * WN + j * 16 + col_in] = static_cast<bf16>(acc[i][j][r]);
+  __syncthreads();
+  constexpr int CPR = BN / 8;            // 16 B chunks per row
+  constexpr int RPI = kThreads / CPR;    // rows per pass
+  const int cc = threadIdx.x % CPR, r0 = threadIdx.x / CPR;
+  const int64_t n = n0 + cc * 8;
+  const bool ncol_ok = n + 8 <= p.N;
+  bf16* c = static_cast<bf16*>(p.c);
+  float cs[8], cq[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    cs[e] = 0.f;
+    cq[e] = 0.f;
+  }
+  for (int r = r0; r < BM; r += RPI) {
+    const int64_t m = m0 + r;
+    if (m >= p.M) break;
+    const uint4 v = *reinterpret_cast<const uint4*>(cl + r * CS + cc * 8);
+    if (ncol_ok) {
+      *reinterpret_cast<uint4*>(c + m * p.ldc + n) = v;
+    } else {
+      const bf16* e8 = reinterpret_cast<const bf16*>(&v);
+      for (int e = 0; e < 8 && n + e < p.N; ++e) c[m * p.ldc + n + e] = e8[e];
+    }
+    if (p.mode == 1) {
+      bf16 e8[8];
+      __builtin_memcpy(e8, &v, 16);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float f = static_cast<float>(e8[e]);
+        cs[e] += f;
+        cq[e] = fmaf(f, f, cq[e]);
       }
     }
+  }
   if (p.mode == 1) {
-    // reduce over the 4 lane groups holding the same column, then over the 2 waves in M
-    __shared__ float red[2][2][BN];
+    // threads with equal cc (= same 8 columns) are RPI apart: reduce through LDS
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [RPI][2][BN]
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      cs[j] += __shfl_xor(cs[j], 16, 64);
-      cs[j] += __shfl_xor(cs[j], 32, 64);
-      cq[j] += __shfl_xor(cq[j], 16, 64);
-      cq[j] += __shfl_xor(cq[j], 32, 64);
-    }
-    if (lane < 16) {
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        red[wm][0][wn * WN + j * 16 + lane] = cs[j];
-        red[wm][1][wn * WN + j * 16 + lane] = cq[j];
-      }
+    for (int e = 0; e < 8; ++e) {
+      red[(r0 * 2 + 0) * BN + cc * 8 + e] = cs[e];
+      red[(r0 * 2 + 1) * BN + cc * 8 + e] = cq[e];
     }
     __syncthreads();
     float* shard = p.stats + static_cast<size_t>(blockIdx.x % kShards) * 2 * p.N;
-    for (int c2 = threadIdx.x; c2 < BN; c2 += kThreads) {
-      const int64_t n = n0 + c2;
-      if (n < p.N) {
-        atomicAdd(shard + n, red[0][0][c2] + red[1][0][c2]);
-        atomicAdd(shard + p.N + n, red[0][1][c2] + red[1][1][c2]);
+    for (int col = threadIdx.x; col < BN; col += kThreads) {
+      float s = 0.f, q = 0.f;
+      for (int k = 0; k < RPI; ++k) {
+        s += red[(k * 2 + 0) * BN + col];
+        q += red[(k * 2 + 1) * BN + col];
+      }
+      if (n0 + col < p.N) {
+        atomicAdd(shard + n0 + col, s);
+        atomicAdd(shard + p.N + n0 + col, q);
       }
     }
   }

@@ -75,26 +75,30 @@ class _FusedBN(torch.autograd.Function):
         save_mean = torch.empty(ch, device=x.device, dtype=torch.float32)
         save_inv = torch.empty(ch, device=x.device, dtype=torch.float32)
         ws = _workspace(x)
+        # ReLU after a residual add: keep a 1-bit mask (1/16 of y's bytes) for the backward
+        mask = torch.empty(x.numel() // 8, device=x.device, dtype=torch.uint8) if (relu and res is not None) \
+            else None
         stream = torch.cuda.current_stream(x.device).cuda_stream
         C.bn_fwd_train(x.data_ptr(), y.data_ptr(), res.data_ptr() if res is not None else 0,
                        w32.data_ptr() if w32 is not None else 0, b32.data_ptr() if b32 is not None else 0,
                        running_mean.data_ptr() if running_mean is not None else 0,
                        running_var.data_ptr() if running_var is not None else 0,
                        save_mean.data_ptr(), save_inv.data_ptr(), ws.data_ptr(), rows, ch, float(momentum),
-                       float(eps), int(relu), DTYPE_CODE[x.dtype], stream)
+                       float(eps), int(relu), mask.data_ptr() if mask is not None else 0, DTYPE_CODE[x.dtype], stream)
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.wdtype = weight.dtype if weight is not None else None
         ctx.has_bias = bias is not None
         # Without a residual the ReLU mask is recomputed from x in the backward
-        # kernels (bit-identical to the forward), so y is neither saved nor re-read.
-        ctx.save_for_backward(x, y if (relu and residual is not None) else None, w32, b32, save_mean, save_inv)
+        # kernels (bit-identical to the forward); with one, the 1-bit mask is used.
+        # Either way y is neither saved nor re-read.
+        ctx.save_for_backward(x, mask, w32, b32, save_mean, save_inv)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         C = _ext.get(required=True)
-        x, y, w32, b32, save_mean, save_inv = ctx.saved_tensors
+        x, mask, w32, b32, save_mean, save_inv = ctx.saved_tensors
         dy = _nhwc(dy)
         rows, ch = _rows_c(x)
         dx = torch.empty_like(x)
@@ -104,7 +108,7 @@ class _FusedBN(torch.autograd.Function):
         db = torch.empty(ch, device=x.device, dtype=torch.float32)
         ws = _workspace(x)
         stream = torch.cuda.current_stream(x.device).cuda_stream
-        C.bn_bwd(dy.data_ptr(), x.data_ptr(), y.data_ptr() if y is not None else 0,
+        C.bn_bwd(dy.data_ptr(), x.data_ptr(), 0, mask.data_ptr() if mask is not None else 0,
                  w32.data_ptr() if w32 is not None else 0, b32.data_ptr() if b32 is not None else 0,
                  save_mean.data_ptr(), save_inv.data_ptr(), dx.data_ptr(),
                  dres.data_ptr() if dres is not None else 0, dw.data_ptr(), db.data_ptr(), ws.data_ptr(), rows, ch,

@@ -4,7 +4,7 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-SHAPES = [(4096, 64, 256), (1000, 96, 72), (512, 256, 64), (2048, 512, 1024), (200, 32, 8)]
+SHAPES = [(4096, 64, 256), (1000, 96, 160), (512, 256, 64), (2048, 512, 1024), (200, 32, 32), (777, 64, 192)]
 
 
 def _rand(*s):
