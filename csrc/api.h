@@ -73,6 +73,17 @@ void bn_bwd(const void* dy, const void* x, const void* y, const uint8_t* relu_ma
             float* dweight, float* dbias, float* workspace, int64_t rows, int64_t C, int relu,
             int dtype, hipStream_t stream);
 size_t bn_workspace_floats(int64_t rows, int64_t C);
+// Split forward for producer/consumer fusion with the GEMM:
+// bn_stats_finalize: [stats pass over x unless stats_ready (a GEMM epilogue already
+// accumulated them into ws)] + finalize (mean/invstd, running stats, and optionally the
+// per-channel scale/shift a consumer GEMM applies on load). bn_apply: the normalise pass.
+void bn_stats_finalize(const void* x, const float* w, const float* b, float* running_mean,
+                       float* running_var, float* save_mean, float* save_invstd, float* scale,
+                       float* shift, float* workspace, int64_t rows, int64_t C, float momentum,
+                       float eps, int stats_ready, int dtype, hipStream_t stream);
+void bn_apply(const void* x, void* y, const void* residual, const float* w, const float* b,
+              const float* save_mean, const float* save_invstd, int64_t rows, int64_t C, int relu,
+              uint8_t* relu_mask, int dtype, hipStream_t stream);
 // Inference: y = act(x * scale + shift [+ residual]) from running statistics.
 void bn_fwd_infer(const void* x, void* y, const void* residual, const float* weight,
                   const float* bias, const float* running_mean, const float* running_var,

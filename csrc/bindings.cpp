@@ -94,6 +94,25 @@ PYBIND11_MODULE(_C, m) {
                  relu, dtype, S(stream));
         });
 
+  m.def("bn_stats_finalize",
+        [](uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t rm, uintptr_t rv, uintptr_t sm, uintptr_t si,
+           uintptr_t scale, uintptr_t shift, uintptr_t ws, int64_t rows, int64_t C, float momentum, float eps,
+           int stats_ready, int dtype, uintptr_t stream) {
+          bn_stats_finalize(reinterpret_cast<const void*>(x), reinterpret_cast<const float*>(w),
+                            reinterpret_cast<const float*>(b), reinterpret_cast<float*>(rm),
+                            reinterpret_cast<float*>(rv), reinterpret_cast<float*>(sm), reinterpret_cast<float*>(si),
+                            reinterpret_cast<float*>(scale), reinterpret_cast<float*>(shift),
+                            reinterpret_cast<float*>(ws), rows, C, momentum, eps, stats_ready, dtype, S(stream));
+        });
+  m.def("bn_apply",
+        [](uintptr_t x, uintptr_t y, uintptr_t res, uintptr_t w, uintptr_t b, uintptr_t sm, uintptr_t si,
+           int64_t rows, int64_t C, int relu, uintptr_t mask, int dtype, uintptr_t stream) {
+          bn_apply(reinterpret_cast<const void*>(x), reinterpret_cast<void*>(y), reinterpret_cast<const void*>(res),
+                   reinterpret_cast<const float*>(w), reinterpret_cast<const float*>(b),
+                   reinterpret_cast<const float*>(sm), reinterpret_cast<const float*>(si), rows, C, relu,
+                   reinterpret_cast<uint8_t*>(mask), dtype, S(stream));
+        });
+
   // ---- MFMA GEMM (1x1 conv) -------------------------------------------------
   m.def("gemm_bf16",
         [](uintptr_t a, uintptr_t b, uintptr_t c, int64_t lda, int64_t ldb, int64_t ldc, int64_t M, int64_t N,

@@ -125,7 +125,9 @@ __device__ __forceinline__ void take_shards(float* __restrict__ acc, int C, int 
 
 __global__ void bn_finalize_fwd_kernel(float* __restrict__ acc, int C, int64_t rows, float momentum, float eps,
                                        float* __restrict__ smean, float* __restrict__ sinv,
-                                       float* __restrict__ rmean, float* __restrict__ rvar) {
+                                       float* __restrict__ rmean, float* __restrict__ rvar,
+                                       const float* __restrict__ w, const float* __restrict__ b,
+                                       float* __restrict__ scale, float* __restrict__ shift) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   float s, q;
@@ -134,8 +136,14 @@ __global__ void bn_finalize_fwd_kernel(float* __restrict__ acc, int C, int64_t r
   const float mean = s * inv_n;
   float var = q * inv_n - mean * mean;
   var = var > 0.f ? var : 0.f;
+  const float invstd = rsqrtf(var + eps);
   smean[c] = mean;
-  sinv[c] = rsqrtf(var + eps);
+  sinv[c] = invstd;
+  if (scale != nullptr) {  // the affine a consumer GEMM applies on load (bit-identical to bn_norm_kernel)
+    const float sc = (w ? w[c] : 1.f) * invstd;
+    scale[c] = sc;
+    shift[c] = fmaf(-mean, sc, b ? b[c] : 0.f);
+  }
   if (rmean != nullptr) {
     const float unbiased = rows > 1 ? var * static_cast<float>(rows) / static_cast<float>(rows - 1) : var;
     rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
@@ -424,7 +432,8 @@ void fwd_train_t(const void* x, void* y, const void* res, const float* w, const 
   Geo g = geometry(rows, C);
   bn_stats_kernel<T><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(static_cast<const T*>(x), rows, (int)C, g, ws);
   FLUXMPI_HIP_CHECK(hipGetLastError());
-  bn_finalize_fwd_kernel<<<(int)((C + 255) / 256), 256, 0, s>>>(ws, (int)C, rows, momentum, eps, sm, si, rm, rv);
+  bn_finalize_fwd_kernel<<<(int)((C + 255) / 256), 256, 0, s>>>(ws, (int)C, rows, momentum, eps, sm, si, rm, rv,
+                                                                 nullptr, nullptr, nullptr, nullptr);
   FLUXMPI_HIP_CHECK(hipGetLastError());
   norm_t<T>(x, y, res, w, b, sm, si, rows, C, eps, 1, relu, mask, s);
 }
@@ -486,6 +495,36 @@ void bn_fwd_train(const void* x, void* y, const void* residual, const float* wei
                                 workspace, rows, C, momentum, eps, relu, relu_mask, stream); break;
     case kF32: fwd_train_t<float>(x, y, residual, weight, bias, running_mean, running_var, save_mean, save_invstd,
                                   workspace, rows, C, momentum, eps, relu, relu_mask, stream); break;
+    default: throw std::runtime_error("fused batchnorm: unsupported dtype");
+  }
+}
+
+void bn_stats_finalize(const void* x, const float* w, const float* b, float* rm, float* rv, float* sm, float* si,
+                       float* scale, float* shift, float* ws, int64_t rows, int64_t C, float momentum, float eps,
+                       int stats_ready, int dtype, hipStream_t s) {
+  check(C);
+  if (!stats_ready) {
+    Geo g = geometry(rows, C);
+    switch (dtype) {
+      case kBF16: bn_stats_kernel<bf16><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(static_cast<const bf16*>(x), rows, (int)C, g, ws); break;
+      case kF16: bn_stats_kernel<f16><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(static_cast<const f16*>(x), rows, (int)C, g, ws); break;
+      case kF32: bn_stats_kernel<float><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(static_cast<const float*>(x), rows, (int)C, g, ws); break;
+      default: throw std::runtime_error("fused batchnorm: unsupported dtype");
+    }
+    FLUXMPI_HIP_CHECK(hipGetLastError());
+  }
+  bn_finalize_fwd_kernel<<<(int)((C + 255) / 256), 256, 0, s>>>(ws, (int)C, rows, momentum, eps, sm, si, rm, rv, w, b,
+                                                                 scale, shift);
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+}
+
+void bn_apply(const void* x, void* y, const void* res, const float* w, const float* b, const float* sm,
+              const float* si, int64_t rows, int64_t C, int relu, uint8_t* mask, int dtype, hipStream_t s) {
+  check(C);
+  switch (dtype) {
+    case kBF16: norm_t<bf16>(x, y, res, w, b, sm, si, rows, C, 0.f, 1, relu, mask, s); break;
+    case kF16: norm_t<f16>(x, y, res, w, b, sm, si, rows, C, 0.f, 1, relu, mask, s); break;
+    case kF32: norm_t<float>(x, y, res, w, b, sm, si, rows, C, 0.f, 1, relu, mask, s); break;
     default: throw std::runtime_error("fused batchnorm: unsupported dtype");
   }
 }

@@ -63,6 +63,12 @@ class Bottleneck(nn.Module):
     def __init__(self, cin, width, stride=1, downsample=None, conv_impl="gemm", norm="torch"):
         super().__init__()
         cout = width * self.expansion
+        # "fused": 1x1 convs run on our MFMA GEMM with BatchNorm producer/consumer fusion
+        # (fluxmpi_amd.ops.fused_block); parameters are plain Conv2d/BatchNorm modules.
+        self.gemm_fused = conv_impl == "fused"
+        if self.gemm_fused:
+            conv_impl, norm = "miopen", "fused"
+        self.dims = (cin, width, cout)
         self.conv1 = conv1x1(cin, width, 1, conv_impl)
         self.bn1 = _norm(width, norm)
         self.conv2 = nn.Conv2d(width, width, 3, stride=stride, padding=1, bias=False)
@@ -74,6 +80,14 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         identity = x if self.downsample is None else self.downsample(x)
+        if self.gemm_fused and self.training:
+            from ..ops import fused_block as fb
+            if fb.supported(x, *self.dims):
+                c1 = fb.conv1x1_stats(x, self.conv1.weight)          # + bn1 statistics (GEMM epilogue)
+                a1 = fb.bn_from_stats(c1, self.bn1, relu=True)
+                c2 = self.conv2(a1)
+                c3 = fb.bn_relu_conv1x1(c2, self.bn2, self.conv3.weight)  # bn2+relu fused into the A load
+                return fb.bn_from_stats(c3, self.bn3, relu=True, residual=identity)
         if self.fused:
             out = self.bn1(self.conv1(x), relu=True)
             out = self.bn2(self.conv2(out), relu=True)
@@ -87,6 +101,8 @@ class Bottleneck(nn.Module):
 class ResNet(nn.Module):
     def __init__(self, layers=(3, 4, 6, 3), num_classes=1000, conv_impl="gemm", norm="torch", zero_init_residual=False):
         super().__init__()
+        if conv_impl == "fused":
+            norm = "fused"
         self.conv_impl, self.norm_kind = conv_impl, norm
         self.inplanes = 64
         self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
@@ -109,7 +125,8 @@ class ResNet(nn.Module):
         down = None
         cout = width * Bottleneck.expansion
         if stride != 1 or self.inplanes != cout:
-            down = nn.Sequential(conv1x1(self.inplanes, cout, stride, self.conv_impl), _norm(cout, self.norm_kind))
+            impl = "miopen" if self.conv_impl == "fused" else self.conv_impl
+            down = nn.Sequential(conv1x1(self.inplanes, cout, stride, impl), _norm(cout, self.norm_kind))
         mods = [Bottleneck(self.inplanes, width, stride, down, self.conv_impl, self.norm_kind)]
         self.inplanes = cout
         for _ in range(1, blocks):

@@ -1,0 +1,203 @@
+"""Producer/consumer fusion of 1x1 convolutions with BatchNorm for bottleneck blocks.
+
+Built on the MFMA GEMM (``csrc/kernels/gemm.hip``) and the split fused-BN
+kernels (``csrc/kernels/batchnorm.hip``). Per ResNet bottleneck:
+
+=========================  ===================================================
+op                         what disappears compared with conv -> BN -> ReLU
+=========================  ===================================================
+``conv1x1_stats``          the BatchNorm statistics pass over the conv output
+                           (sums come from the GEMM epilogue)
+``bn_relu_conv1x1``        the normalised activation: BN + ReLU are applied to
+                           the GEMM's A operand while staging (forward) and to
+                           the wgrad B operand (backward); never written to HBM
+``bn_from_stats``          (consumer of the above) finalize + normalise pass only
+=========================  ===================================================
+
+All three are autograd Functions; activations are bf16 NHWC (channels_last),
+weights bf16, BatchNorm parameters / statistics fp32. Numerics: the BN affine
+applied inside the GEMM is computed exactly like the fused-BN kernels'
+(``scale = w * invstd``, ``shift = fma(-mean, scale, b)``), so ReLU masks
+recomputed in the backward match the forward bit for bit.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _ext
+from .batchnorm import _workspace
+from .gemm import conv1x1_dgrad, conv1x1_wgrad, gemm
+from .multi_tensor import DTYPE_CODE
+
+
+def _stream(t):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _p(t):
+    return t.data_ptr() if t is not None else 0
+
+
+def _nhwc2d(x: torch.Tensor) -> torch.Tensor:
+    """[N,C,H,W] channels_last -> [N*H*W, C] view (copy if not channels_last)."""
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        x = x.contiguous(memory_format=torch.channels_last)
+    n, c, h, w = x.shape
+    return x.permute(0, 2, 3, 1).reshape(n * h * w, c)
+
+
+def _empty_nhwc(n, c, h, w, like):
+    return torch.empty(n, h, w, c, device=like.device, dtype=like.dtype).permute(0, 3, 1, 2)
+
+
+def _bn_bwd(dy, x, mask, w32, b32, mean, inv, relu, has_res):
+    """Shared fused-BN backward; returns (dx, dres, dw, db) (fp32 dw/db)."""
+    C = _ext.get(required=True)
+    rows, ch = x.numel() // x.shape[1], x.shape[1]
+    dx = torch.empty_like(x)
+    dres = torch.empty_like(x) if has_res else None
+    dw = torch.empty(ch, device=x.device, dtype=torch.float32)
+    db = torch.empty(ch, device=x.device, dtype=torch.float32)
+    ws = _workspace(x)
+    C.bn_bwd(dy.data_ptr(), x.data_ptr(), 0, _p(mask), _p(w32), _p(b32), mean.data_ptr(), inv.data_ptr(),
+             dx.data_ptr(), _p(dres), dw.data_ptr(), db.data_ptr(), ws.data_ptr(), rows, ch, int(relu),
+             DTYPE_CODE[x.dtype], _stream(x))
+    return dx, dres, dw, db
+
+
+class _Conv1x1Stats(torch.autograd.Function):
+    """c = conv1x1(x, W); the output's per-channel sum/sumsq go to the BN workspace."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        x = x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
+        n, ci, h, w = x.shape
+        co = weight.shape[0]
+        w2 = weight.reshape(co, ci)
+        c = _empty_nhwc(n, co, h, w, x)
+        ws = _workspace(x)
+        gemm(_nhwc2d(x), w2, c, M=n * h * w, N=co, K=ci, lda=ci, ldb=ci, ldc=co, a_kmajor=True, b_kmajor=True,
+             mode=1, stats=ws)
+        ctx.save_for_backward(x, weight)
+        return c
+
+    @staticmethod
+    def backward(ctx, dc):
+        x, weight = ctx.saved_tensors
+        co, ci = weight.shape[0], weight.shape[1]
+        dc2 = _nhwc2d(dc)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            n, _, h, w = x.shape
+            dx = _empty_nhwc(n, ci, h, w, x)
+            gemm(dc2, weight.reshape(co, ci), dx, M=n * h * w, N=ci, K=co, lda=co, ldb=ci, ldc=ci, a_kmajor=True,
+                 b_kmajor=False)
+        dw = conv1x1_wgrad(dc2, _nhwc2d(x)).to(weight.dtype).view_as(weight)
+        return dx, dw
+
+
+class _BNFromStats(torch.autograd.Function):
+    """BatchNorm(+residual)(+ReLU) whose batch statistics are already in the workspace
+    (``stats_ready``) or are computed by the stats pass here."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, momentum, eps, relu, stats_ready):
+        C = _ext.get(required=True)
+        ch = x.shape[1]
+        rows = x.numel() // ch
+        w32 = weight.float()
+        b32 = bias.float()
+        mean = torch.empty(ch, device=x.device, dtype=torch.float32)
+        inv = torch.empty(ch, device=x.device, dtype=torch.float32)
+        ws = _workspace(x)
+        C.bn_stats_finalize(x.data_ptr(), w32.data_ptr(), b32.data_ptr(), _p(running_mean), _p(running_var),
+                            mean.data_ptr(), inv.data_ptr(), 0, 0, ws.data_ptr(), rows, ch, float(momentum),
+                            float(eps), int(stats_ready), DTYPE_CODE[x.dtype], _stream(x))
+        res = None
+        if residual is not None:
+            res = residual if residual.is_contiguous(memory_format=torch.channels_last) else \
+                residual.contiguous(memory_format=torch.channels_last)
+        y = torch.empty_like(x)
+        mask = torch.empty(x.numel() // 8, device=x.device, dtype=torch.uint8) if (relu and res is not None) \
+            else None
+        C.bn_apply(x.data_ptr(), y.data_ptr(), _p(res), w32.data_ptr(), b32.data_ptr(), mean.data_ptr(),
+                   inv.data_ptr(), rows, ch, int(relu), _p(mask), DTYPE_CODE[x.dtype], _stream(x))
+        ctx.relu, ctx.has_res, ctx.wdtype = relu, residual is not None, weight.dtype
+        ctx.save_for_backward(x, mask, w32, b32, mean, inv)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mask, w32, b32, mean, inv = ctx.saved_tensors
+        if not dy.is_contiguous(memory_format=torch.channels_last):
+            dy = dy.contiguous(memory_format=torch.channels_last)
+        dx, dres, dw, db = _bn_bwd(dy, x, mask, w32, b32, mean, inv, ctx.relu, ctx.has_res)
+        return dx, dw.to(ctx.wdtype), db.to(ctx.wdtype), dres, None, None, None, None, None, None
+
+
+class _BNReluConv1x1(torch.autograd.Function):
+    """c3 = conv1x1(relu(BN(c2)), W) without materialising relu(BN(c2)); c3's statistics
+    go to the workspace (consumed by the next ``bn_from_stats``)."""
+
+    @staticmethod
+    def forward(ctx, c2, bn_weight, bn_bias, running_mean, running_var, weight, momentum, eps):
+        C = _ext.get(required=True)
+        if not c2.is_contiguous(memory_format=torch.channels_last):
+            c2 = c2.contiguous(memory_format=torch.channels_last)
+        n, ch, h, w = c2.shape
+        rows = n * h * w
+        w32, b32 = bn_weight.float(), bn_bias.float()
+        mean = torch.empty(ch, device=c2.device, dtype=torch.float32)
+        inv = torch.empty_like(mean)
+        scale = torch.empty_like(mean)
+        shift = torch.empty_like(mean)
+        ws = _workspace(c2)
+        C.bn_stats_finalize(c2.data_ptr(), w32.data_ptr(), b32.data_ptr(), _p(running_mean), _p(running_var),
+                            mean.data_ptr(), inv.data_ptr(), scale.data_ptr(), shift.data_ptr(), ws.data_ptr(),
+                            rows, ch, float(momentum), float(eps), 0, DTYPE_CODE[c2.dtype], _stream(c2))
+        co = weight.shape[0]
+        c3 = _empty_nhwc(n, co, h, w, c2)
+        gemm(_nhwc2d(c2), weight.reshape(co, ch), c3, M=rows, N=co, K=ch, lda=ch, ldb=ch, ldc=co, a_kmajor=True,
+             b_kmajor=True, mode=1, stats=ws, a_affine=(scale, shift))
+        ctx.bn_wdtype = bn_weight.dtype
+        ctx.save_for_backward(c2, w32, b32, mean, inv, scale, shift, weight)
+        return c3
+
+    @staticmethod
+    def backward(ctx, dc3):
+        c2, w32, b32, mean, inv, scale, shift, weight = ctx.saved_tensors
+        n, ch, h, w = c2.shape
+        co = weight.shape[0]
+        dc3_2d = _nhwc2d(dc3)
+        c2_2d = _nhwc2d(c2)
+        # dW = dc3^T @ relu(bn(c2))  — the activation is rebuilt on the fly in the B-operand load
+        dw = conv1x1_wgrad(dc3_2d, c2_2d, in_affine=(scale, shift)).to(weight.dtype).view_as(weight)
+        # d(relu(bn(c2))) = dc3 @ W, then the BN backward with the ReLU mask recomputed from c2
+        da = conv1x1_dgrad(dc3_2d, weight.reshape(co, ch)).view(n, h, w, ch).permute(0, 3, 1, 2)
+        dc2, _, dbw, dbb = _bn_bwd(da, c2, None, w32, b32, mean, inv, True, False)
+        return dc2, dbw.to(ctx.bn_wdtype), dbb.to(ctx.bn_wdtype), None, None, dw, None, None
+
+
+def conv1x1_stats(x, weight):
+    return _Conv1x1Stats.apply(x, weight)
+
+
+def bn_from_stats(x, bn, relu=False, residual=None, stats_ready=True):
+    if bn.training and bn.track_running_stats:
+        bn.num_batches_tracked.add_(1)
+    mom = 0.1 if bn.momentum is None else bn.momentum
+    return _BNFromStats.apply(x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, mom, bn.eps, relu,
+                              stats_ready)
+
+
+def bn_relu_conv1x1(c2, bn, weight):
+    if bn.training and bn.track_running_stats:
+        bn.num_batches_tracked.add_(1)
+    mom = 0.1 if bn.momentum is None else bn.momentum
+    return _BNReluConv1x1.apply(c2, bn.weight, bn.bias, bn.running_mean, bn.running_var, weight, mom, bn.eps)
+
+
+def supported(x: torch.Tensor, *channels: int) -> bool:
+    """Shapes the fused path handles (bf16 NHWC on GPU, channels % 32 == 0, <= 2048)."""
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
+            and all(c % 32 == 0 and 32 <= c <= 2048 for c in channels))
