@@ -94,30 +94,29 @@ template <int ROWS, bool KMAJOR, int CPT>
 __device__ __forceinline__ void stage_load(uint4 (&reg)[CPT],
                                            const bf16* __restrict__ g, int64_t ld, int64_t rows, int64_t r0,
                                            int64_t k0, const float* __restrict__ sc, const float* __restrict__ sh,
-                                           bool affine_on_k) {
+                                           int64_t kend) {
   static_assert(CPT == ROWS * BK / 8 / kThreads, "chunks per thread");
 #pragma unroll
   for (int i = 0; i < CPT; ++i) {
     const int idx = threadIdx.x + i * kThreads;
-    uint4 v = make_uint4(0, 0, 0, 0);
+    uint4 v = make_uint4(0, 0, 0, 0);  // zero fill: out-of-range rows / k contribute nothing
     if (KMAJOR) {
       const int r = idx / (BK / 8), kc = idx % (BK / 8);
       const int64_t row = r0 + r;
-      if (row < rows) {
+      if (row < rows && k0 + kc * 8 < kend) {  // K % 8 == 0 for K-major operands (host-checked)
         v = *reinterpret_cast<const uint4*>(g + row * ld + k0 + kc * 8);
         if (sc != nullptr) affine_relu8(v, sc, sh, k0 + kc * 8);
       }
     } else {
       const int kr = idx / (ROWS / 8), rc = idx % (ROWS / 8);
       const int64_t col = r0 + rc * 8;
-      if (col < rows) {
+      if (col < rows && k0 + kr < kend) {
         v = *reinterpret_cast<const uint4*>(g + (k0 + kr) * ld + col);
         if (sc != nullptr) affine_relu8(v, sc, sh, col);  // per-row-channel affine (wgrad B = X)
       }
     }
     reg[i] = v;
   }
-  (void)affine_on_k;
 }
 
 template <int ROWS, bool KMAJOR, int CPT>
@@ -196,10 +195,10 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs p) {
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   uint4 ra[TA::kChunks / kThreads], rb[TB::kChunks / kThreads];
-  const int64_t nk = (kend - kbeg) / BK;
+  const int64_t nk = (kend - kbeg + BK - 1) / BK;  // last K-tile may be partial (zero-filled)
   if (nk > 0) {
-    stage_load<BM, AK>(ra, p.a, p.lda, p.M, m0, kbeg, p.a_scale, p.a_shift, true);
-    stage_load<BN, BKM>(rb, p.b, p.ldb, p.N, n0, kbeg, p.b_scale, p.b_shift, false);
+    stage_load<BM, AK>(ra, p.a, p.lda, p.M, m0, kbeg, p.a_scale, p.a_shift, kend);
+    stage_load<BN, BKM>(rb, p.b, p.ldb, p.N, n0, kbeg, p.b_scale, p.b_shift, kend);
     stage_store<BM, AK>(la(0), ra);
     stage_store<BN, BKM>(lb(0), rb);
   }
@@ -209,8 +208,8 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs p) {
     const bool more = t + 1 < nk;
     if (more) {  // issue next tile's global loads before this tile's MFMAs
       const int64_t k1 = kbeg + (t + 1) * BK;
-      stage_load<BM, AK>(ra, p.a, p.lda, p.M, m0, k1, p.a_scale, p.a_shift, true);
-      stage_load<BN, BKM>(rb, p.b, p.ldb, p.N, n0, k1, p.b_scale, p.b_shift, false);
+      stage_load<BM, AK>(ra, p.a, p.lda, p.M, m0, k1, p.a_scale, p.a_shift, kend);
+      stage_load<BN, BKM>(rb, p.b, p.ldb, p.N, n0, k1, p.b_scale, p.b_shift, kend);
     }
     bf16x8 fa[FM], fb[FN];
 #pragma unroll
@@ -331,7 +330,7 @@ void launch(const GemmArgs& a0, int splits, hipStream_t s) {
 }  // namespace
 
 void gemm_bf16(const GemmProblem& g, hipStream_t stream) {
-  if (g.K % BK != 0) throw std::runtime_error("gemm_bf16: K must be a multiple of 32");
+  if ((g.a_kmajor || g.b_kmajor) && g.K % 8 != 0) throw std::runtime_error("gemm_bf16: K-major operands need K % 8 == 0");
   if ((g.a_kmajor ? g.lda : g.lda) % 8 != 0 || g.ldb % 8 != 0)
     throw std::runtime_error("gemm_bf16: leading dimensions must be multiples of 8");
   if (g.mode == 1 && g.stats == nullptr) throw std::runtime_error("gemm_bf16: stats buffer required");
@@ -344,7 +343,7 @@ void gemm_bf16(const GemmProblem& g, hipStream_t stream) {
   a.lda = g.lda; a.ldb = g.ldb; a.ldc = g.ldc;
   a.M = g.M; a.N = g.N; a.K = g.K;
   int splits = g.splits < 1 ? 1 : g.splits;
-  int64_t kps = (g.K / BK + splits - 1) / splits * BK;
+  int64_t kps = ((g.K + BK - 1) / BK + splits - 1) / splits * BK;
   splits = static_cast<int>((g.K + kps - 1) / kps);
   a.k_per_split = kps;
   a.a_scale = g.a_scale; a.a_shift = g.a_shift;
