@@ -79,7 +79,7 @@ Geo geometry(int64_t rows, int64_t C) {
 // (blockIdx % kShards) of acc[kShards][2][C]. Sharding keeps the number of
 // same-address atomics per line ~blocks/kShards: float atomics execute at the
 // memory side, and thousands of workgroups adding into ONE line serialise.
-constexpr int kShards = 16;
+constexpr int kShards = 64;  // <= ~200 same-address atomics even for 12k-block GEMM grids
 
 __device__ __forceinline__ void block_reduce_atomic(float (&a)[8], float (&b)[8], int cv, int rpi, int C,
                                                     float* __restrict__ acc, float* smem) {

@@ -42,7 +42,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kThreads = 256;
 constexpr int BK = 32;
-constexpr int kShards = 16;  // must match batchnorm.hip
+constexpr int kShards = 64;  // must match batchnorm.hip
 
 struct GemmArgs {
   const bf16* a;

@@ -34,7 +34,7 @@ def _nhwc(x: torch.Tensor) -> torch.Tensor:
 
 
 _WS: dict = {}
-_SHARDS = 16
+_SHARDS = 64  # == kShards in csrc/kernels/{batchnorm,gemm}.hip
 _MAXC = 2048
 
 

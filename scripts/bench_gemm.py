@@ -45,6 +45,7 @@ def main():
         dwbuf = torch.zeros(co, ci, device="cuda")
         r = {"H": H, "Cin": ci, "Cout": co}
         r["ours_fwd"] = bench(lambda: conv1x1_fwd(x2, w2, None, stats))
+        r["ours_fwd_nostats"] = bench(lambda: conv1x1_fwd(x2, w2, None, None))
         r["miopen_fwd"] = bench(lambda: torch.nn.functional.conv2d(x4, w4))
         r["ours_dgrad"] = bench(lambda: conv1x1_dgrad(dy2, w2))
         r["ours_wgrad"] = bench(lambda: conv1x1_wgrad(dy2, x2, None, dwbuf))

@@ -24,15 +24,21 @@ def _models():
 
 
 def test_fused_resnet_matches_unfused(gpu_ext):
+    """Both bf16 pipelines are compared with an fp32 model holding the same (bf16-rounded)
+    weights: the fused pipeline must be about as accurate as the unfused one."""
+    from fluxmpi_amd.models.resnet import ResNet
     ref, fus = _models()
+    f32 = ResNet((2, 1, 1, 1), 10, conv_impl="miopen", norm="fused").cuda().to(memory_format=torch.channels_last)
+    f32.load_state_dict({k: v.float() if v.is_floating_point() else v for k, v in ref.state_dict().items()})
     x = torch.randn(8, 3, 64, 64, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
-    ya, yb = ref(x), fus(x)
-    assert _rel(yb, ya) < 3e-2
-    g = torch.randn_like(ya)
-    (ya.float() * g.float()).sum().backward()
-    (yb.float() * g.float()).sum().backward()
-    for (n, p), q in zip(ref.named_parameters(), fus.parameters()):
-        assert _rel(q.grad, p.grad) < 5e-2, n
+    ya, yb, yc = ref(x), fus(x), f32(x.float())
+    assert _rel(yb, yc) < 2 * _rel(ya, yc) + 1e-2
+    g = torch.randn_like(yc)
+    for y, m in ((ya, ref), (yb, fus), (yc, f32)):
+        (y.float() * g).sum().backward()
+    for (n, pa), pb, pc in zip(ref.named_parameters(), fus.parameters(), f32.parameters()):
+        ea, eb = _rel(pa.grad, pc.grad), _rel(pb.grad, pc.grad)
+        assert eb < 2 * ea + 2e-2, f"{n}: fused {eb:.3e} vs unfused {ea:.3e}"
     for (n, b), c in zip(ref.named_buffers(), fus.buffers()):
         if b.dtype.is_floating_point:
             assert _rel(c, b) < 2e-2, n

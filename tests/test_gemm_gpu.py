@@ -19,7 +19,9 @@ def _act(x, aff):
     if aff is None:
         return x.float()
     s, t = aff
-    return torch.relu(x.float() * s + t).to(torch.bfloat16).float()
+    # the kernel computes fmaf(x, s, t): emulate the single rounding in fp64
+    y = (x.double() * s.double() + t.double()).float()
+    return torch.relu(y).to(torch.bfloat16).float()
 
 
 @pytest.mark.parametrize("M,K,N", SHAPES)
