@@ -48,6 +48,7 @@ class GraphedStep:
                 self.static_loss = self._eager()
         finally:
             ddp.watchdog = wd
+        ddp.step_count -= 1  # capture records the step but executes nothing
         self.replays = 0
 
     def _eager(self):
