@@ -85,9 +85,10 @@ def main():
 
     B = args.batch
     gx = torch.Generator(device=dev).manual_seed(rank)
-    x = torch.randn(B, 3, args.image, args.image, device=dev, generator=gx).to(torch.bfloat16)
+    cin, ncls = (1, 10) if args.model == "deq" else (3, 1000)  # DEQ: MNIST-shaped (FastDEQ example)
+    x = torch.randn(B, cin, args.image, args.image, device=dev, generator=gx).to(torch.bfloat16)
     x = x.contiguous(memory_format=torch.channels_last)
-    y = torch.randint(0, 1000, (B,), device=dev, generator=gx)
+    y = torch.randint(0, ncls, (B,), device=dev, generator=gx)
 
     def step():
         out = ddp(x)
@@ -116,11 +117,14 @@ def main():
     lval = float(loss.item())
     if rank == 0:
         ips = world * B * args.steps / dt_max
+        names = {"resnet50": "ResNet50", "vit_b16": "ViT-B/16", "deq": "DEQ"}
+        mname = names.get(args.model, args.model)
+        metric = METRIC if args.model == "resnet50" else METRIC.replace("ResNet50 Lux.jl", f"{mname}")
         rec = {
-            "metric": METRIC, "value": round(ips, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+            "metric": metric, "value": round(ips, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000 * dt_max / args.steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
-            "config": {"model": "ResNet50", "global_batch": world * B, "per_gpu_batch": B, "seq_len": None,
+            "config": {"model": mname, "global_batch": world * B, "per_gpu_batch": B, "seq_len": None,
                        "image_size": args.image, "parallelism": f"dp{world}", "optimizer": args.optimizer,
                        "conv": args.conv, "norm": args.norm, "backend": FluxMPI.backend_name(),
                        "overlap": not args.no_overlap, "miopen_find": bool(args.miopen_find), "hip_graph": bool(args.graph), "loss": round(lval, 4)},

@@ -92,7 +92,7 @@ void bn_fwd_infer(const void* x, void* y, const void* residual, const float* wei
 // ---- MFMA bf16 GEMM with BatchNorm fusions (1x1 convolutions) --------------------
 // C[M,N] = A[M,K] * B[N,K]^T. a_kmajor: A stored [M][lda] (K contiguous), else [K][lda]
 // (M contiguous); b_kmajor likewise for B. mode 0: C bf16; mode 1: C bf16 + per-column
-// sum/sumsq into stats[16][2][N] (sharded, caller-zeroed); mode 2: C fp32 += (atomics,
+// sum/sumsq into stats[64][2][N] (sharded, caller-zeroed); mode 2: C fp32 += (atomics,
 // allows split-K over `splits`). a_scale/a_shift: relu(A*s+t) per k applied on load
 // (K-major A); b_scale/b_shift: per n on load (N-major B).
 struct GemmProblem {
@@ -108,6 +108,7 @@ struct GemmProblem {
   const float* b_shift;
   float* stats;
   int tile_m, tile_n;  // 0 = auto, 64 forces the 64 tile
+  int nbuf;            // LDS buffers: 0 = auto (1 for K per split <= 128), 1, 2
 };
 void gemm_bf16(const GemmProblem& g, hipStream_t stream);
 

@@ -160,16 +160,20 @@ __device__ __forceinline__ bf16x8 read_frag(const bf16* __restrict__ lds, int r0
   }
 }
 
-template <int BM, int BN, bool AK, bool BKM>
+// NBUF = 2: double-buffered LDS, the next K-tile's loads overlap this tile's MFMAs
+// (compute-bound shapes). NBUF = 1: half the LDS, so twice the workgroups per CU —
+// for short K (memory-bound 1x1 convs) other workgroups' loads hide the latency.
+template <int BM, int BN, bool AK, bool BKM, int NBUF>
 __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs p) {
   using TA = Tile<BM, AK>;
   using TB = Tile<BN, BKM>;
   constexpr int WM = BM / 2, WN = BN / 2;  // per-wave tile
   constexpr int FM = WM / 16, FN = WN / 16;
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * (TA::kElems + TB::kElems)];
-  // buffer b of A at smem + b*kElemsA, of B at smem + 2*kElemsA + b*kElemsB
+  constexpr int kSmem = NBUF * (TA::kElems + TB::kElems);
+  __shared__ __attribute__((aligned(16))) bf16 smem[kSmem];
+  // buffer b of A at smem + b*kElemsA, of B at smem + NBUF*kElemsA + b*kElemsB
   auto la = [&](int b) { return smem + b * TA::kElems; };
-  auto lb = [&](int b) { return smem + 2 * TA::kElems + b * TB::kElems; };
+  auto lb = [&](int b) { return smem + NBUF * TA::kElems + b * TB::kElems; };
 
   // XCD-aware tile order: blocks b and b+8 share an XCD; give each XCD a contiguous
   // range of tiles (n fastest) so neighbouring tiles share A rows in that L2.
@@ -204,8 +208,14 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs p) {
   }
   __syncthreads();
   for (int64_t t = 0; t < nk; ++t) {
-    const int cur = t & 1;
+    const int cur = NBUF == 2 ? (t & 1) : 0;
     const bool more = t + 1 < nk;
+    if (NBUF == 1 && t > 0) {  // single buffer: refill after every wave finished reading it
+      __syncthreads();
+      stage_store<BM, AK>(la(0), ra);
+      stage_store<BN, BKM>(lb(0), rb);
+      __syncthreads();
+    }
     if (more) {  // issue next tile's global loads before this tile's MFMAs
       const int64_t k1 = kbeg + (t + 1) * BK;
       stage_load<BM, AK>(ra, p.a, p.lda, p.M, m0, k1, p.a_scale, p.a_shift, kend);
@@ -220,12 +230,15 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs p) {
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-    if (more) {
-      stage_store<BM, AK>(la(cur ^ 1), ra);
-      stage_store<BN, BKM>(lb(cur ^ 1), rb);
+    if (NBUF == 2) {
+      if (more) {
+        stage_store<BM, AK>(la(cur ^ 1), ra);
+        stage_store<BN, BKM>(lb(cur ^ 1), rb);
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
+  if (NBUF == 1) __syncthreads();
 
   // ---------------------------------------------------------------- epilogue
   // acc[i][j][r]: row m0 + wm*WM + i*16 + 4*(lane>>4) + r, col n0 + wn*WN + j*16 + (lane&15)
@@ -249,18 +262,14 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs p) {
   // loop's final barrier) so every lane stores 16 contiguous bytes; the BatchNorm
   // statistics are taken from the same staged bf16 values.
   constexpr int CS = BN + 8;  // padded row (bf16 elements)
-  static_assert(BM * CS <= 2 * (TA::kElems + TB::kElems), "C tile must fit the operand LDS");
-  bf16* cl = smem;
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        cl[(wm * WM + i * 16 + rq + r) * CS + wn * WN + j * 16 + col_in] = static_cast<bf16>(acc[i][j][r]);
-  __syncthreads();
+  // the C tile is staged in NP passes of BM/NP rows when it exceeds the operand LDS
+  constexpr int NP = (BM * CS <= kSmem) ? 1 : 2;
+  static_assert(NP == 1 || (BM / 2) * CS <= kSmem, "C half tile must fit the operand LDS");
+  static_assert(NP == 1 || WM == BM / 2, "pass split follows the wave rows");
+  constexpr int PR = BM / NP;            // rows per pass
   constexpr int CPR = BN / 8;            // 16 B chunks per row
-  constexpr int RPI = kThreads / CPR;    // rows per pass
+  constexpr int RPI = kThreads / CPR;    // rows per store sweep
+  bf16* cl = smem;
   const int cc = threadIdx.x % CPR, r0 = threadIdx.x / CPR;
   const int64_t n = n0 + cc * 8;
   const bool ncol_ok = n + 8 <= p.N;
@@ -271,44 +280,67 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs p) {
     cs[e] = 0.f;
     cq[e] = 0.f;
   }
-  for (int r = r0; r < BM; r += RPI) {
-    const int64_t m = m0 + r;
-    if (m >= p.M) break;
-    const uint4 v = *reinterpret_cast<const uint4*>(cl + r * CS + cc * 8);
-    if (ncol_ok) {
-      *reinterpret_cast<uint4*>(c + m * p.ldc + n) = v;
-    } else {
-      const bf16* e8 = reinterpret_cast<const bf16*>(&v);
-      for (int e = 0; e < 8 && n + e < p.N; ++e) c[m * p.ldc + n + e] = e8[e];
-    }
-    if (p.mode == 1) {
-      bf16 e8[8];
-      __builtin_memcpy(e8, &v, 16);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float f = static_cast<float>(e8[e]);
-        cs[e] += f;
-        cq[e] = fmaf(f, f, cq[e]);
+  for (int h = 0; h < NP; ++h) {
+    if (h > 0) __syncthreads();  // previous pass fully read
+    if (NP == 1 || wm == h) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            cl[(wm * WM - h * PR + i * 16 + rq + r) * CS + wn * WN + j * 16 + col_in] =
+                static_cast<bf16>(acc[i][j][r]);
+    }
+    __syncthreads();
+    for (int r = r0; r < PR; r += RPI) {
+      const int64_t m = m0 + h * PR + r;
+      if (m >= p.M) break;
+      const uint4 v = *reinterpret_cast<const uint4*>(cl + r * CS + cc * 8);
+      if (ncol_ok) {
+        *reinterpret_cast<uint4*>(c + m * p.ldc + n) = v;
+      } else {
+        const bf16* e8 = reinterpret_cast<const bf16*>(&v);
+        for (int e = 0; e < 8 && n + e < p.N; ++e) c[m * p.ldc + n + e] = e8[e];
+      }
+      if (p.mode == 1) {
+        bf16 e8[8];
+        __builtin_memcpy(e8, &v, 16);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float f = static_cast<float>(e8[e]);
+          cs[e] += f;
+          cq[e] = fmaf(f, f, cq[e]);
+        }
       }
     }
   }
   if (p.mode == 1) {
-    // threads with equal cc (= same 8 columns) are RPI apart: reduce through LDS
-    __syncthreads();
-    float* red = reinterpret_cast<float*>(smem);  // [RPI][2][BN]
+    // lanes of a wave with equal cc differ in the bits above log2(CPR): butterfly them,
+    // then combine the 4 waves through LDS and add one atomic per column per block.
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      red[(r0 * 2 + 0) * BN + cc * 8 + e] = cs[e];
-      red[(r0 * 2 + 1) * BN + cc * 8 + e] = cq[e];
+    for (int off = CPR; off < 64; off <<= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        cs[e] += __shfl_xor(cs[e], off, 64);
+        cq[e] += __shfl_xor(cq[e], off, 64);
+      }
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [4 waves][2][BN]
+    static_assert(4 * 2 * BN * 4 <= kSmem * 2, "stats scratch");
+    if (lane < CPR) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(wave * 2 + 0) * BN + cc * 8 + e] = cs[e];
+        red[(wave * 2 + 1) * BN + cc * 8 + e] = cq[e];
+      }
     }
     __syncthreads();
     float* shard = p.stats + static_cast<size_t>(blockIdx.x % kShards) * 2 * p.N;
     for (int col = threadIdx.x; col < BN; col += kThreads) {
-      float s = 0.f, q = 0.f;
-      for (int k = 0; k < RPI; ++k) {
-        s += red[(k * 2 + 0) * BN + col];
-        q += red[(k * 2 + 1) * BN + col];
-      }
+      const float s = red[0 * BN + col] + red[2 * BN + col] + red[4 * BN + col] + red[6 * BN + col];
+      const float q = red[1 * BN + col] + red[3 * BN + col] + red[5 * BN + col] + red[7 * BN + col];
       if (n0 + col < p.N) {
         atomicAdd(shard + n0 + col, s);
         atomicAdd(shard + p.N + n0 + col, q);
@@ -317,13 +349,13 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs p) {
   }
 }
 
-template <int BM, int BN, bool AK, bool BKM>
+template <int BM, int BN, bool AK, bool BKM, int NBUF>
 void launch(const GemmArgs& a0, int splits, hipStream_t s) {
   GemmArgs a = a0;
   a.tiles_m = static_cast<int>((a.M + BM - 1) / BM);
   a.tiles_n = static_cast<int>((a.N + BN - 1) / BN);
   dim3 grid(a.tiles_m * a.tiles_n, 1, splits);
-  gemm_kernel<BM, BN, AK, BKM><<<grid, kThreads, 0, s>>>(a);
+  gemm_kernel<BM, BN, AK, BKM, NBUF><<<grid, kThreads, 0, s>>>(a);
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
 
@@ -353,15 +385,20 @@ void gemm_bf16(const GemmProblem& g, hipStream_t stream) {
   if (splits > 1 && g.mode != 2) throw std::runtime_error("gemm_bf16: split-K needs mode 2 (fp32 atomics)");
   const bool bm128 = g.M >= 128 && g.tile_m != 64;
   const bool bn128 = g.N >= 128 && g.tile_n != 64;
-#define DISPATCH(AK, BKM)                                            \
-  if (bm128 && bn128) launch<128, 128, AK, BKM>(a, splits, stream);  \
-  else if (bm128) launch<128, 64, AK, BKM>(a, splits, stream);       \
-  else if (bn128) launch<64, 128, AK, BKM>(a, splits, stream);       \
-  else launch<64, 64, AK, BKM>(a, splits, stream);
+#define DISPATCH2(AK, BKM, NB)                                          \
+  if (bm128 && bn128) launch<128, 128, AK, BKM, NB>(a, splits, stream);  \
+  else if (bm128) launch<128, 64, AK, BKM, NB>(a, splits, stream);       \
+  else if (bn128) launch<64, 128, AK, BKM, NB>(a, splits, stream);       \
+  else launch<64, 64, AK, BKM, NB>(a, splits, stream);
+#define DISPATCH(AK, BKM) \
+  if (single) { DISPATCH2(AK, BKM, 1) } else { DISPATCH2(AK, BKM, 2) }
+  // short K per workgroup: single-buffered (occupancy); long K: double-buffered (overlap)
+  const bool single = g.nbuf == 1 || (g.nbuf == 0 && a.k_per_split <= 128);
   if (g.a_kmajor && g.b_kmajor) { DISPATCH(true, true) }
   else if (g.a_kmajor && !g.b_kmajor) { DISPATCH(true, false) }
   else if (!g.a_kmajor && !g.b_kmajor) { DISPATCH(false, false) }
   else { DISPATCH(false, true) }
+#undef DISPATCH2
 #undef DISPATCH
 }
 

@@ -10,11 +10,15 @@ given: the previous BatchNorm + ReLU applied on the fly (never stored).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _ext
 
 SHARDS = 64  # == kShards in csrc/kernels/{batchnorm,gemm}.hip
+# LDS buffering of the GEMM main loop: 0 = per-shape choice in the kernel launcher, 1 or 2 forces it
+NBUF = int(os.environ.get("FLUXMPI_GEMM_NBUF", "0"))
 
 
 def _stream(t):
@@ -26,12 +30,12 @@ def _ptr(t):
 
 
 def gemm(a, b, c, *, M, N, K, lda, ldb, ldc, a_kmajor=True, b_kmajor=True, mode=0, splits=1, a_affine=None,
-         b_affine=None, stats=None, tile_m=0, tile_n=0):
+         b_affine=None, stats=None, tile_m=0, tile_n=0, nbuf=0):
     C = _ext.get(required=True)
     asc, ash = a_affine if a_affine is not None else (None, None)
     bsc, bsh = b_affine if b_affine is not None else (None, None)
     C.gemm_bf16(a.data_ptr(), b.data_ptr(), c.data_ptr(), lda, ldb, ldc, M, N, K, a_kmajor, b_kmajor, mode, splits,
-                _ptr(asc), _ptr(ash), _ptr(bsc), _ptr(bsh), _ptr(stats), tile_m, tile_n, _stream(c))
+                _ptr(asc), _ptr(ash), _ptr(bsc), _ptr(bsh), _ptr(stats), tile_m, tile_n, _stream(c), nbuf or NBUF)
     return c
 
 

@@ -10,6 +10,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fluxmpi_amd.ops.gemm import SHARDS, conv1x1_dgrad, conv1x1_fwd, conv1x1_wgrad  # noqa: E402
 from fluxmpi_amd.utils.miopen import install_tuned_db  # noqa: E402
+import fluxmpi_amd.ops.gemm as G  # noqa: E402
 
 
 def bench(fn, iters=20):
@@ -32,7 +33,8 @@ def main():
     # (H, Cin, Cout) of the stride-1 1x1 convolutions of ResNet-50
     shapes = [(56, 64, 64), (56, 64, 256), (56, 256, 64), (56, 256, 128), (28, 128, 512), (28, 512, 128),
               (28, 512, 256), (14, 256, 1024), (14, 1024, 256), (14, 1024, 512), (7, 512, 2048), (7, 2048, 512)]
-    tot = {"ours_fwd": 0, "miopen_fwd": 0, "ours_dgrad": 0, "miopen_dgrad": 0, "ours_wgrad": 0, "miopen_wgrad": 0}
+    tot = {"ours_fwd": 0, "miopen_fwd": 0, "ours_dgrad": 0, "miopen_dgrad": 0, "ours_wgrad": 0, "miopen_wgrad": 0,
+           "fwd_nb1": 0, "fwd_nb2": 0, "dgrad_nb1": 0, "dgrad_nb2": 0, "wgrad_nb1": 0, "wgrad_nb2": 0}
     for H, ci, co in shapes:
         M = B * H * H
         x4 = torch.randn(B, ci, H, H, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
@@ -46,6 +48,12 @@ def main():
         r = {"H": H, "Cin": ci, "Cout": co}
         r["ours_fwd"] = bench(lambda: conv1x1_fwd(x2, w2, None, stats))
         r["ours_fwd_nostats"] = bench(lambda: conv1x1_fwd(x2, w2, None, None))
+        for nb in (1, 2):  # forced LDS buffering variants
+            G.NBUF = nb
+            r[f"fwd_nb{nb}"] = bench(lambda: conv1x1_fwd(x2, w2, None, stats))
+            r[f"dgrad_nb{nb}"] = bench(lambda: conv1x1_dgrad(dy2, w2))
+            r[f"wgrad_nb{nb}"] = bench(lambda: conv1x1_wgrad(dy2, x2, None, dwbuf))
+        G.NBUF = 0
         r["miopen_fwd"] = bench(lambda: torch.nn.functional.conv2d(x4, w4))
         r["ours_dgrad"] = bench(lambda: conv1x1_dgrad(dy2, w2))
         r["ours_wgrad"] = bench(lambda: conv1x1_wgrad(dy2, x2, None, dwbuf))

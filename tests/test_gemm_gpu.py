@@ -7,6 +7,14 @@ pytestmark = pytest.mark.gpu
 SHAPES = [(4096, 64, 256), (1000, 96, 160), (512, 256, 64), (2048, 512, 1024), (200, 32, 32), (777, 64, 192)]
 
 
+@pytest.fixture(params=[0, 1, 2], ids=["nbuf_auto", "nbuf1", "nbuf2"], autouse=True)
+def nbuf(request, monkeypatch):
+    """Every case runs with the launcher's choice and with both LDS buffering variants forced."""
+    from fluxmpi_amd.ops import gemm
+    monkeypatch.setattr(gemm, "NBUF", request.param)
+    return request.param
+
+
 def _rand(*s):
     return torch.randn(*s, device="cuda").to(torch.bfloat16)
 
