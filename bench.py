@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=int(os.environ.get("BENCH_BATCH", "256")), help="per-GPU batch")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--image", type=int, default=224)
-    ap.add_argument("--conv", default=os.environ.get("BENCH_CONV", "miopen"), choices=["gemm", "miopen", "fused"])
+    ap.add_argument("--conv", default=os.environ.get("BENCH_CONV", "miopen"), choices=["gemm", "miopen", "fused", "hybrid"])
     ap.add_argument("--norm", default=os.environ.get("BENCH_NORM", "fused"), choices=["torch", "fused"])
     ap.add_argument("--optimizer", default="adam", choices=["adam", "momentum"])
     ap.add_argument("--no-overlap", action="store_true")
@@ -115,6 +115,16 @@ def main():
     dt = time.perf_counter() - t0
     dt_max = FluxMPI.allreduce(torch.tensor([dt], dtype=torch.float64), max).item() if world > 1 else dt
     lval = float(loss.item())
+    exposed = None
+    if world > 1 and not args.graph:
+        # after the timed region: a few steps with event timing around the gradient-allreduce
+        # wait (exposed = not hidden behind backward), max over ranks
+        ddp.timing = True
+        for _ in range(3):
+            step()
+        ddp.timing = False
+        e = ddp.exposed_comm_ms()
+        exposed = FluxMPI.allreduce(torch.tensor([e or 0.0], dtype=torch.float64), max).item()
     if rank == 0:
         ips = world * B * args.steps / dt_max
         names = {"resnet50": "ResNet50", "vit_b16": "ViT-B/16", "deq": "DEQ"}
@@ -127,7 +137,8 @@ def main():
             "config": {"model": mname, "global_batch": world * B, "per_gpu_batch": B, "seq_len": None,
                        "image_size": args.image, "parallelism": f"dp{world}", "optimizer": args.optimizer,
                        "conv": args.conv, "norm": args.norm, "backend": FluxMPI.backend_name(),
-                       "overlap": not args.no_overlap, "miopen_find": bool(args.miopen_find), "hip_graph": bool(args.graph), "loss": round(lval, 4)},
+                       "overlap": not args.no_overlap, "miopen_find": bool(args.miopen_find), "hip_graph": bool(args.graph), "loss": round(lval, 4),
+                       "exposed_comm_ms": None if exposed is None else round(exposed, 3)},
         }
         print(json.dumps(rec), flush=True)
     FluxMPI.Finalize()

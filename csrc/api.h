@@ -93,7 +93,7 @@ void bn_fwd_infer(const void* x, void* y, const void* residual, const float* wei
 // C[M,N] = A[M,K] * B[N,K]^T. a_kmajor: A stored [M][lda] (K contiguous), else [K][lda]
 // (M contiguous); b_kmajor likewise for B. mode 0: C bf16; mode 1: C bf16 + per-column
 // sum/sumsq into stats[64][2][N] (sharded, caller-zeroed); mode 2: C fp32 += (atomics,
-// allows split-K over `splits`). a_scale/a_shift: relu(A*s+t) per k applied on load
+// allows split-K over `splits`); mode 3: split s stores its fp32 partial to C + s*M*ldc. a_scale/a_shift: relu(A*s+t) per k applied on load
 // (K-major A); b_scale/b_shift: per n on load (N-major B).
 struct GemmProblem {
   const void* a;
@@ -108,8 +108,12 @@ struct GemmProblem {
   const float* b_shift;
   float* stats;
   int tile_m, tile_n;  // 0 = auto, 64 forces the 64 tile
-  int nbuf;            // LDS buffers: 0 = auto (1 for K per split <= 128), 1, 2
+  int nbuf;            // LDS buffers: 0 = auto (2), 1, 2
+  const void* res;     // optional bf16 residual [M][ldr] added in the epilogue (modes 0/1)
+  int64_t ldr;
 };
 void gemm_bf16(const GemmProblem& g, hipStream_t stream);
+// out[e] = sum over s < splits of ws[s*n + e] (mode-3 split-K partials); out fp32 or bf16 (dtype code)
+void gemm_splitk_reduce(const float* ws, int splits, int64_t n, void* out, int out_dtype, hipStream_t stream);
 
 }  // namespace fluxmpi

@@ -117,18 +117,27 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_bf16",
         [](uintptr_t a, uintptr_t b, uintptr_t c, int64_t lda, int64_t ldb, int64_t ldc, int64_t M, int64_t N,
            int64_t K, bool a_kmajor, bool b_kmajor, int mode, int splits, uintptr_t a_scale, uintptr_t a_shift,
-           uintptr_t b_scale, uintptr_t b_shift, uintptr_t stats, int tile_m, int tile_n, uintptr_t stream, int nbuf) {
+           uintptr_t b_scale, uintptr_t b_shift, uintptr_t stats, int tile_m, int tile_n, uintptr_t stream, int nbuf, uintptr_t res, int64_t ldr) {
           GemmProblem g{reinterpret_cast<const void*>(a), reinterpret_cast<const void*>(b),
                         reinterpret_cast<void*>(c), lda, ldb, ldc, M, N, K, a_kmajor, b_kmajor, mode, splits,
                         reinterpret_cast<const float*>(a_scale), reinterpret_cast<const float*>(a_shift),
                         reinterpret_cast<const float*>(b_scale), reinterpret_cast<const float*>(b_shift),
-                        reinterpret_cast<float*>(stats), tile_m, tile_n, nbuf};
+                        reinterpret_cast<float*>(stats), tile_m, tile_n, nbuf,
+                        reinterpret_cast<const void*>(res), ldr};
           gemm_bf16(g, S(stream));
         },
         py::arg("a"), py::arg("b"), py::arg("c"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("M"),
         py::arg("N"), py::arg("K"), py::arg("a_kmajor"), py::arg("b_kmajor"), py::arg("mode"), py::arg("splits"),
         py::arg("a_scale"), py::arg("a_shift"), py::arg("b_scale"), py::arg("b_shift"), py::arg("stats"),
-        py::arg("tile_m"), py::arg("tile_n"), py::arg("stream"), py::arg("nbuf") = 0);
+        py::arg("tile_m"), py::arg("tile_n"), py::arg("stream"), py::arg("nbuf") = 0, py::arg("res") = 0,
+        py::arg("ldr") = 0);
+
+  m.def("gemm_splitk_reduce",
+        [](uintptr_t ws, int splits, int64_t n, uintptr_t out, int out_dtype, uintptr_t stream) {
+          gemm_splitk_reduce(reinterpret_cast<const float*>(ws), splits, n, reinterpret_cast<void*>(out), out_dtype,
+                             S(stream));
+        },
+        py::arg("ws"), py::arg("splits"), py::arg("n"), py::arg("out"), py::arg("out_dtype"), py::arg("stream"));
 
   // ---- RCCL ----------------------------------------------------------------
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });

@@ -65,8 +65,11 @@ class Bottleneck(nn.Module):
         cout = width * self.expansion
         # "fused": 1x1 convs run on our MFMA GEMM with BatchNorm producer/consumer fusion
         # (fluxmpi_amd.ops.fused_block); parameters are plain Conv2d/BatchNorm modules.
+        # "hybrid": MIOpen forward/wgrad for the 1x1 convs, our dgrad GEMM with the block's
+        # residual gradient added in its epilogue (fluxmpi_amd.ops.fused_block.conv1x1_hybrid)
         self.gemm_fused = conv_impl == "fused"
-        if self.gemm_fused:
+        self.hybrid = conv_impl == "hybrid"
+        if self.gemm_fused or self.hybrid:
             conv_impl, norm = "miopen", "fused"
         self.dims = (cin, width, cout)
         self.conv1 = conv1x1(cin, width, 1, conv_impl)
@@ -80,14 +83,22 @@ class Bottleneck(nn.Module):
 
     def forward(self, x):
         identity = x if self.downsample is None else self.downsample(x)
-        if self.gemm_fused and self.training:
+        if (self.gemm_fused or self.hybrid) and self.training:
             from ..ops import fused_block as fb
             if fb.supported(x, *self.dims):
-                c1 = fb.conv1x1_stats(x, self.conv1.weight)          # + bn1 statistics (GEMM epilogue)
+                # identity blocks: bn3's residual gradient goes straight into conv1's dgrad epilogue
+                link = fb.GradLink() if (self.downsample is None and x.requires_grad
+                                         and torch.is_grad_enabled()) else None
+                if self.hybrid:
+                    a1 = self.bn1(fb.conv1x1_hybrid(x, self.conv1.weight, link), relu=True)
+                    a2 = self.bn2(self.conv2(a1), relu=True)
+                    return self.bn3(fb.conv1x1_hybrid(a2, self.conv3.weight), relu=True, residual=identity,
+                                    link=link)
+                c1 = fb.conv1x1_stats(x, self.conv1.weight, link)    # + bn1 statistics (GEMM epilogue)
                 a1 = fb.bn_from_stats(c1, self.bn1, relu=True)
                 c2 = self.conv2(a1)
                 c3 = fb.bn_relu_conv1x1(c2, self.bn2, self.conv3.weight)  # bn2+relu fused into the A load
-                return fb.bn_from_stats(c3, self.bn3, relu=True, residual=identity)
+                return fb.bn_from_stats(c3, self.bn3, relu=True, residual=identity, link=link)
         if self.fused:
             out = self.bn1(self.conv1(x), relu=True)
             out = self.bn2(self.conv2(out), relu=True)
@@ -101,7 +112,7 @@ class Bottleneck(nn.Module):
 class ResNet(nn.Module):
     def __init__(self, layers=(3, 4, 6, 3), num_classes=1000, conv_impl="gemm", norm="torch", zero_init_residual=False):
         super().__init__()
-        if conv_impl == "fused":
+        if conv_impl in ("fused", "hybrid"):
             norm = "fused"
         self.conv_impl, self.norm_kind = conv_impl, norm
         self.inplanes = 64
@@ -125,7 +136,7 @@ class ResNet(nn.Module):
         down = None
         cout = width * Bottleneck.expansion
         if stride != 1 or self.inplanes != cout:
-            impl = "miopen" if self.conv_impl == "fused" else self.conv_impl
+            impl = "miopen" if self.conv_impl in ("fused", "hybrid") else self.conv_impl
             down = nn.Sequential(conv1x1(self.inplanes, cout, stride, impl), _norm(cout, self.norm_kind))
         mods = [Bottleneck(self.inplanes, width, stride, down, self.conv_impl, self.norm_kind)]
         self.inplanes = cout

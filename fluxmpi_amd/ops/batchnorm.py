@@ -62,9 +62,32 @@ def kernel_supported(x: torch.Tensor) -> bool:
     return c % 8 == 0 and 8 <= c <= 2048 and x.numel() > 0
 
 
+class GradLink:
+    """Hands the residual-branch gradient of a block from the BatchNorm that adds the
+    residual straight to the 1x1 convolution that also consumes the block input.
+
+    Without it autograd sums the two gradients of the block input with a separate add
+    kernel (a read-read-write pass over the largest activation of the block); with it
+    the BatchNorm backward deposits ``dres`` here and the convolution's dgrad GEMM adds
+    it in its epilogue. Autograd's data dependencies guarantee the order (the conv's
+    backward needs gradients that pass through the BatchNorm's backward).
+    """
+
+    __slots__ = ("grad",)
+
+    def __init__(self):
+        self.grad = None
+
+    def take(self) -> torch.Tensor:
+        g, self.grad = self.grad, None
+        if g is None:
+            raise RuntimeError("GradLink: the residual gradient was not produced before its consumer ran")
+        return g
+
+
 class _FusedBN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, running_mean, running_var, momentum, eps, relu):
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, momentum, eps, relu, link=None):
         C = _ext.get(required=True)
         x = _nhwc(x)
         res = _nhwc(residual) if residual is not None else None
@@ -87,6 +110,7 @@ class _FusedBN(torch.autograd.Function):
                        float(eps), int(relu), mask.data_ptr() if mask is not None else 0, DTYPE_CODE[x.dtype], stream)
         ctx.relu = relu
         ctx.has_res = residual is not None
+        ctx.link = link if residual is not None else None
         ctx.wdtype = weight.dtype if weight is not None else None
         ctx.has_bias = bias is not None
         # Without a residual the ReLU mask is recomputed from x in the backward
@@ -121,7 +145,9 @@ class _FusedBN(torch.autograd.Function):
             db = None
         elif ctx.wdtype != torch.float32:
             db = db.to(ctx.wdtype)
-        return dx, dw, db, dres, None, None, None, None, None
+        if ctx.link is not None:
+            ctx.link.grad, dres = dres, None
+        return dx, dw, db, dres, None, None, None, None, None, None
 
 
 def batch_norm_reference(x, weight, bias, running_mean, running_var, training, momentum, eps, relu=False,
@@ -137,9 +163,11 @@ def batch_norm_reference(x, weight, bias, running_mean, running_var, training, m
 
 
 def fused_batch_norm(x, weight, bias, running_mean, running_var, training=True, momentum=0.1, eps=1e-5,
-                     relu=False, residual=None):
+                     relu=False, residual=None, link: GradLink | None = None):
+    """``link``: deliver the residual's gradient through a :class:`GradLink` instead of
+    returning it to autograd (training with the fused kernels only; otherwise ignored)."""
     if training and kernel_supported(x):
-        return _FusedBN.apply(x, weight, bias, residual, running_mean, running_var, momentum, eps, relu)
+        return _FusedBN.apply(x, weight, bias, residual, running_mean, running_var, momentum, eps, relu, link)
     if (not training) and kernel_supported(x) and not torch.is_grad_enabled():
         C = _ext.get(required=True)
         x = _nhwc(x)
@@ -158,7 +186,7 @@ def fused_batch_norm(x, weight, bias, running_mean, running_var, training=True, 
 class FusedBatchNorm2d(nn.BatchNorm2d):
     """``nn.BatchNorm2d`` with optional fused ReLU / residual add (NHWC HIP kernels on GPU)."""
 
-    def forward(self, x, relu: bool = False, residual: torch.Tensor | None = None):
+    def forward(self, x, relu: bool = False, residual: torch.Tensor | None = None, link: GradLink | None = None):
         if self.training and self.track_running_stats:
             self.num_batches_tracked.add_(1)
         mom = 0.1 if self.momentum is None else self.momentum
@@ -166,4 +194,4 @@ class FusedBatchNorm2d(nn.BatchNorm2d):
         return fused_batch_norm(x, self.weight, self.bias,
                                 self.running_mean if self.track_running_stats else None,
                                 self.running_var if self.track_running_stats else None,
-                                use_batch, mom, self.eps, relu, residual)
+                                use_batch, mom, self.eps, relu, residual, link)

@@ -12,6 +12,10 @@ op                         what disappears compared with conv -> BN -> ReLU
                            the GEMM's A operand while staging (forward) and to
                            the wgrad B operand (backward); never written to HBM
 ``bn_from_stats``          (consumer of the above) finalize + normalise pass only
+``GradLink``               the residual-gradient add of the block input: the
+                           BN backward hands ``dres`` to the conv1 dgrad GEMM,
+                           which adds it in its epilogue
+``conv1x1_hybrid``         MIOpen forward/wgrad, our dgrad (+ linked residual)
 =========================  ===================================================
 
 All three are autograd Functions; activations are bf16 NHWC (channels_last),
@@ -25,7 +29,7 @@ from __future__ import annotations
 import torch
 
 from . import _ext
-from .batchnorm import _workspace
+from .batchnorm import GradLink, _workspace  # noqa: F401 (GradLink re-exported)
 from .gemm import conv1x1_dgrad, conv1x1_wgrad, gemm
 from .multi_tensor import DTYPE_CODE
 
@@ -69,8 +73,9 @@ class _Conv1x1Stats(torch.autograd.Function):
     """c = conv1x1(x, W); the output's per-channel sum/sumsq go to the BN workspace."""
 
     @staticmethod
-    def forward(ctx, x, weight):
+    def forward(ctx, x, weight, link=None):
         x = x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
+        ctx.link = link
         n, ci, h, w = x.shape
         co = weight.shape[0]
         w2 = weight.reshape(co, ci)
@@ -86,14 +91,44 @@ class _Conv1x1Stats(torch.autograd.Function):
         x, weight = ctx.saved_tensors
         co, ci = weight.shape[0], weight.shape[1]
         dc2 = _nhwc2d(dc)
-        dx = None
-        if ctx.needs_input_grad[0]:
-            n, _, h, w = x.shape
-            dx = _empty_nhwc(n, ci, h, w, x)
-            gemm(dc2, weight.reshape(co, ci), dx, M=n * h * w, N=ci, K=co, lda=co, ldb=ci, ldc=ci, a_kmajor=True,
-                 b_kmajor=False)
-        dw = conv1x1_wgrad(dc2, _nhwc2d(x)).to(weight.dtype).view_as(weight)
-        return dx, dw
+        dx = _dgrad_nhwc(dc2, weight, x, ctx.link) if ctx.needs_input_grad[0] else None
+        dw = conv1x1_wgrad(dc2, _nhwc2d(x), out_dtype=weight.dtype).view_as(weight)
+        return dx, dw, None
+
+
+def _dgrad_nhwc(dc2, weight, x, link):
+    """dX (NHWC, x's shape) = dC @ W [+ the residual gradient delivered through ``link``]."""
+    co, ci = weight.shape[0], weight.shape[1]
+    n, _, h, w = x.shape
+    dx = _empty_nhwc(n, ci, h, w, x)
+    res = _nhwc2d(link.take()) if link is not None else None
+    conv1x1_dgrad(dc2, weight.reshape(co, ci), residual=res, out=_nhwc2d(dx))
+    return dx
+
+
+class _Conv1x1Hybrid(torch.autograd.Function):
+    """1x1 convolution: forward and weight gradient on MIOpen (fastest there), input
+    gradient on our MFMA GEMM (faster than MIOpen's on every ResNet-50 shape measured)
+    with the block's residual gradient added in its epilogue (``link``)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, link=None):
+        x = x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
+        ctx.link = link
+        ctx.save_for_backward(x, weight)
+        return torch.nn.functional.conv2d(x, weight)
+
+    @staticmethod
+    def backward(ctx, dc):
+        x, weight = ctx.saved_tensors
+        if not dc.is_contiguous(memory_format=torch.channels_last):
+            dc = dc.contiguous(memory_format=torch.channels_last)
+        dx = _dgrad_nhwc(_nhwc2d(dc), weight, x, ctx.link) if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = torch.ops.aten.convolution_backward(dc, x, weight, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+                                                     [False, True, False])[1]
+        return dx, dw, None
 
 
 class _BNFromStats(torch.autograd.Function):
@@ -101,7 +136,8 @@ class _BNFromStats(torch.autograd.Function):
     (``stats_ready``) or are computed by the stats pass here."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, running_mean, running_var, momentum, eps, relu, stats_ready):
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, momentum, eps, relu, stats_ready,
+                link=None):
         C = _ext.get(required=True)
         ch = x.shape[1]
         rows = x.numel() // ch
@@ -123,6 +159,7 @@ class _BNFromStats(torch.autograd.Function):
         C.bn_apply(x.data_ptr(), y.data_ptr(), _p(res), w32.data_ptr(), b32.data_ptr(), mean.data_ptr(),
                    inv.data_ptr(), rows, ch, int(relu), _p(mask), DTYPE_CODE[x.dtype], _stream(x))
         ctx.relu, ctx.has_res, ctx.wdtype = relu, residual is not None, weight.dtype
+        ctx.link = link if residual is not None else None
         ctx.save_for_backward(x, mask, w32, b32, mean, inv)
         return y
 
@@ -132,7 +169,9 @@ class _BNFromStats(torch.autograd.Function):
         if not dy.is_contiguous(memory_format=torch.channels_last):
             dy = dy.contiguous(memory_format=torch.channels_last)
         dx, dres, dw, db = _bn_bwd(dy, x, mask, w32, b32, mean, inv, ctx.relu, ctx.has_res)
-        return dx, dw.to(ctx.wdtype), db.to(ctx.wdtype), dres, None, None, None, None, None, None
+        if ctx.link is not None:
+            ctx.link.grad, dres = dres, None
+        return dx, dw.to(ctx.wdtype), db.to(ctx.wdtype), dres, None, None, None, None, None, None, None
 
 
 class _BNReluConv1x1(torch.autograd.Function):
@@ -171,23 +210,27 @@ class _BNReluConv1x1(torch.autograd.Function):
         dc3_2d = _nhwc2d(dc3)
         c2_2d = _nhwc2d(c2)
         # dW = dc3^T @ relu(bn(c2))  — the activation is rebuilt on the fly in the B-operand load
-        dw = conv1x1_wgrad(dc3_2d, c2_2d, in_affine=(scale, shift)).to(weight.dtype).view_as(weight)
+        dw = conv1x1_wgrad(dc3_2d, c2_2d, in_affine=(scale, shift), out_dtype=weight.dtype).view_as(weight)
         # d(relu(bn(c2))) = dc3 @ W, then the BN backward with the ReLU mask recomputed from c2
         da = conv1x1_dgrad(dc3_2d, weight.reshape(co, ch)).view(n, h, w, ch).permute(0, 3, 1, 2)
         dc2, _, dbw, dbb = _bn_bwd(da, c2, None, w32, b32, mean, inv, True, False)
         return dc2, dbw.to(ctx.bn_wdtype), dbb.to(ctx.bn_wdtype), None, None, dw, None, None
 
 
-def conv1x1_stats(x, weight):
-    return _Conv1x1Stats.apply(x, weight)
+def conv1x1_stats(x, weight, link=None):
+    return _Conv1x1Stats.apply(x, weight, link)
 
 
-def bn_from_stats(x, bn, relu=False, residual=None, stats_ready=True):
+def conv1x1_hybrid(x, weight, link=None):
+    return _Conv1x1Hybrid.apply(x, weight, link)
+
+
+def bn_from_stats(x, bn, relu=False, residual=None, stats_ready=True, link=None):
     if bn.training and bn.track_running_stats:
         bn.num_batches_tracked.add_(1)
     mom = 0.1 if bn.momentum is None else bn.momentum
     return _BNFromStats.apply(x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, mom, bn.eps, relu,
-                              stats_ready)
+                              stats_ready, link)
 
 
 def bn_relu_conv1x1(c2, bn, weight):

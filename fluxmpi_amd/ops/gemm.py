@@ -30,12 +30,13 @@ def _ptr(t):
 
 
 def gemm(a, b, c, *, M, N, K, lda, ldb, ldc, a_kmajor=True, b_kmajor=True, mode=0, splits=1, a_affine=None,
-         b_affine=None, stats=None, tile_m=0, tile_n=0, nbuf=0):
+         b_affine=None, stats=None, tile_m=0, tile_n=0, nbuf=0, residual=None):
     C = _ext.get(required=True)
     asc, ash = a_affine if a_affine is not None else (None, None)
     bsc, bsh = b_affine if b_affine is not None else (None, None)
     C.gemm_bf16(a.data_ptr(), b.data_ptr(), c.data_ptr(), lda, ldb, ldc, M, N, K, a_kmajor, b_kmajor, mode, splits,
-                _ptr(asc), _ptr(ash), _ptr(bsc), _ptr(bsh), _ptr(stats), tile_m, tile_n, _stream(c), nbuf or NBUF)
+                _ptr(asc), _ptr(ash), _ptr(bsc), _ptr(bsh), _ptr(stats), tile_m, tile_n, _stream(c), nbuf or NBUF,
+                _ptr(residual), residual.stride(0) if residual is not None else 0)
     return c
 
 
@@ -52,37 +53,68 @@ def conv1x1_fwd(x2d: torch.Tensor, w2d: torch.Tensor, in_affine=None, stats: tor
     return y
 
 
-def conv1x1_dgrad(dy2d: torch.Tensor, w2d: torch.Tensor):
-    """``dy2d`` [M, Cout], ``w2d`` [Cout, Cin] -> dX [M, Cin] bf16."""
+def conv1x1_dgrad(dy2d: torch.Tensor, w2d: torch.Tensor, residual: torch.Tensor | None = None,
+                  out: torch.Tensor | None = None):
+    """``dy2d`` [M, Cout], ``w2d`` [Cout, Cin] -> dX [M, Cin] bf16 (``+ residual`` [M, Cin] bf16 fused
+    into the epilogue: the gradient of a residual block's input in one pass)."""
     M, Co = dy2d.shape
     Ci = w2d.shape[1]
-    dx = torch.empty(M, Ci, device=dy2d.device, dtype=torch.bfloat16)
-    gemm(dy2d, w2d, dx, M=M, N=Ci, K=Co, lda=dy2d.stride(0), ldb=w2d.stride(0), ldc=Ci, a_kmajor=True,
-         b_kmajor=False)
+    dx = out if out is not None else torch.empty(M, Ci, device=dy2d.device, dtype=torch.bfloat16)
+    if residual is not None:
+        assert residual.shape == (M, Ci) and residual.dtype == torch.bfloat16 and residual.stride(1) == 1
+    gemm(dy2d, w2d, dx, M=M, N=Ci, K=Co, lda=dy2d.stride(0), ldb=w2d.stride(0), ldc=dx.stride(0), a_kmajor=True,
+         b_kmajor=False, residual=residual)
     return dx
+
+
+BK = 32  # K tile of the kernel (split boundaries are multiples of it)
 
 
 def wgrad_splits(M: int, co: int, ci: int) -> int:
     """Split-K factor for the weight gradient (K = M pixels).
 
-    Every split adds a whole fp32 ``co x ci`` tile with float atomics, which run
-    at ~1.3 TB/s chip-wide (vs ~6 TB/s for plain streams): keep the atomic bytes
-    under 1/8 of the operand bytes, and use just enough splits to put ~512
-    workgroups on the 256 CUs.
+    Splits write fp32 partials with plain stores (a [splits, co, ci] workspace, then one
+    reduce pass), so their cost is ~2 x splits x co*ci*4 bytes of streaming traffic: aim
+    at ~1024 workgroups for the 256 CUs, keep >= 256 pixels per split and the partial
+    traffic under half of the operand bytes.
     """
     tiles = max(1, (co + 127) // 128) * max(1, (ci + 127) // 128)
     in_bytes = M * (co + ci) * 2
     out_bytes = co * ci * 4
-    s_bw = max(1, in_bytes // (8 * out_bytes))
-    s_occ = max(1, -(-512 // tiles))
-    return int(max(1, min(s_bw, s_occ, max(1, M // 256))))
+    s_occ = -(-1024 // tiles)
+    s_bw = max(1, in_bytes // (4 * out_bytes))
+    return int(max(1, min(s_occ, s_bw, M // 256)))
 
 
-def conv1x1_wgrad(dy2d: torch.Tensor, x2d: torch.Tensor, in_affine=None, out: torch.Tensor | None = None):
-    """``dy2d`` [M, Cout], ``x2d`` [M, Cin] -> dW [Cout, Cin] fp32 (accumulated into ``out`` if given)."""
+def _actual_splits(K: int, splits: int) -> int:
+    """The kernel launcher rounds the per-split K range up to whole K tiles."""
+    nk = -(-K // BK)
+    kps = -(-nk // splits) * BK
+    return -(-K // kps)
+
+
+def conv1x1_wgrad(dy2d: torch.Tensor, x2d: torch.Tensor, in_affine=None, out: torch.Tensor | None = None,
+                  out_dtype: torch.dtype = torch.float32, splits: int | None = None):
+    """``dy2d`` [M, Cout], ``x2d`` [M, Cin] -> dW [Cout, Cin] (``out_dtype``, fp32 accumulation).
+
+    Written into ``out`` (overwritten) if given. One split: the GEMM stores dW directly
+    (bf16 through the staged epilogue, fp32 plainly); several: fp32 partials + one reduce
+    launch that also casts to the output dtype.
+    """
     M, Co = dy2d.shape
     Ci = x2d.shape[1]
-    dw = out if out is not None else torch.zeros(Co, Ci, device=dy2d.device, dtype=torch.float32)
-    gemm(dy2d, x2d, dw, M=Co, N=Ci, K=M, lda=dy2d.stride(0), ldb=x2d.stride(0), ldc=Ci, a_kmajor=False,
-         b_kmajor=False, mode=2, splits=wgrad_splits(M, Co, Ci), b_affine=in_affine)
+    if out is not None:
+        out_dtype = out.dtype
+    dw = out if out is not None else torch.empty(Co, Ci, device=dy2d.device, dtype=out_dtype)
+    s = _actual_splits(M, splits or wgrad_splits(M, Co, Ci))
+    common = dict(M=Co, N=Ci, K=M, lda=dy2d.stride(0), ldb=x2d.stride(0), ldc=Ci, a_kmajor=False, b_kmajor=False,
+                  b_affine=in_affine)
+    if s == 1:
+        gemm(dy2d, x2d, dw, mode=0 if dw.dtype == torch.bfloat16 else 3, splits=1, **common)
+        return dw
+    ws = torch.empty(s, Co, Ci, device=dy2d.device, dtype=torch.float32)
+    gemm(dy2d, x2d, ws, mode=3, splits=s, **common)
+    C = _ext.get(required=True)
+    C.gemm_splitk_reduce(ws.data_ptr(), s, Co * Ci, dw.data_ptr(), 9 if dw.dtype == torch.bfloat16 else 7,
+                         _stream(dw))
     return dw

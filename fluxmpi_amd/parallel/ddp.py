@@ -41,6 +41,7 @@ import torch
 
 from .. import optimisers as O
 from ..ops import multi_tensor as mt
+from ..ops import _ext
 from ..ops import optim as fused
 from ..utils.config import get_config
 from ..utils import profiling
@@ -65,6 +66,7 @@ class _Bucket:
     pending: int = 0
     ready: bool = False
     launched: bool = False
+    packed: bool = False
     work: object = None
     names: list = field(default_factory=list)
     comm_buf: torch.Tensor | None = None
@@ -73,6 +75,11 @@ class _Bucket:
 def _strided_view(flat: torch.Tensor, like: torch.Tensor, offset: int) -> torch.Tensor:
     """A view of ``flat[offset:offset+numel]`` with ``like``'s sizes and (dense) strides."""
     return flat.as_strided(like.size(), like.stride(), flat.storage_offset() + offset)
+
+
+def _same_layout(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Same shape and the same strides on every dimension of size > 1 (memory order)."""
+    return a.shape == b.shape and all(sa == sb for n, sa, sb in zip(a.shape, a.stride(), b.stride()) if n > 1)
 
 
 def _is_dense(t: torch.Tensor) -> bool:
@@ -106,8 +113,15 @@ class DDP:
                  bucket_mb: float | None = None, first_bucket_mb: float | None = None,
                  master_weights: bool = True, average: bool = False, overlap: bool | None = None,
                  broadcast: bool = True, root_rank: int = 0, comm: Communicator | None = None,
-                 comm_dtype: torch.dtype | None = None, watchdog: bool | None = None):
+                 comm_dtype: torch.dtype | None = None, watchdog: bool | None = None,
+                 grad_mode: str | None = None):
         cfg = get_config()
+        # "steal": autograd hands over each freshly produced gradient (no in-place accumulate
+        # kernel per parameter, no zero fill) and one multi-tensor launch per bucket packs them
+        # into the flat buffer; "view": p.grad is a view into the flat buffer (autograd adds in).
+        self.grad_mode = grad_mode or cfg.extra.get("grad_mode", "steal")
+        if self.grad_mode not in ("steal", "view"):
+            raise ValueError(f"DDP: grad_mode must be 'steal' or 'view', got {self.grad_mode!r}")
         self.module = module
         self.rule = rule if rule is not None else O.Adam()
         self.average = average
@@ -152,6 +166,9 @@ class DDP:
         self._next_launch = 0
         self.zero_grad()
         self.step_count = 0
+        # exposed-communication timing (off by default: event timing costs a little)
+        self.timing = bool(cfg.profile)
+        self._comm_events: list = []
 
     # ------------------------------------------------------------------ setup
     def _build_buckets(self, params, bucket_bytes, first_bytes, names):
@@ -194,7 +211,8 @@ class DDP:
                 v = _strided_view(flat_p, p, o)
                 v.copy_(p.data)
                 p.data = v
-                p.grad = _strided_view(flat_g, p, o)
+                if self.grad_mode == "view":
+                    p.grad = _strided_view(flat_g, p, o)
         return _Bucket(idx, dtype, dev, list(params), offs, total, flat_p, flat_g,
                        names=[names.get(id(p), "?") for p in params])
 
@@ -274,6 +292,7 @@ class DDP:
         b.launched = True
         if self.world == 1:
             return
+        self._pack(b)
         buf = b.flat_grad
         if self.comm_dtype is not None and self.comm_dtype != b.dtype:
             # K5: cast the bucket to the wire dtype (e.g. fp32 grads sent as bf16) in one launch
@@ -293,17 +312,55 @@ class DDP:
     forward = __call__
 
     def zero_grad(self):
-        """Zero every flat gradient buffer (one fill launch per dtype) and re-arm the hooks."""
-        mt.fill_([b.flat_grad for b in self.buckets], 0.0)
+        """Reset the gradients and re-arm the hooks. "view" mode zeroes the flat buffers (one
+        fill launch per dtype); "steal" mode drops the per-step gradient tensors."""
+        if self.grad_mode == "view":
+            mt.fill_([b.flat_grad for b in self.buckets], 0.0)
         for b in self.buckets:
             b.pending = len(b.params)
-            b.ready = b.launched = False
+            b.ready = b.launched = b.packed = False
             b.work = None
-            # if someone replaced .grad (e.g. set_to_none), restore the views
             for p, o in zip(b.params, b.offsets):
-                if p.grad is None or p.grad.data_ptr() != b.flat_grad.data_ptr() + o * b.flat_grad.element_size():
+                if self.grad_mode == "steal":
+                    p.grad = None
+                elif p.grad is None or p.grad.data_ptr() != b.flat_grad.data_ptr() + o * b.flat_grad.element_size():
+                    # someone replaced .grad (e.g. set_to_none): restore the view
                     p.grad = _strided_view(b.flat_grad, p, o)
         self._next_launch = 0
+
+    def _pack(self, b: _Bucket):
+        """"steal" mode: copy the bucket's gradients into its flat buffer, one multi-tensor launch.
+
+        Autograd's layout contract gives every gradient its parameter's (dense) strides, and the
+        flat slice is a view with the same strides, so a raw copy of ``numel`` elements is exact.
+        Parameters that received no gradient get zeros.
+        """
+        if self.grad_mode != "steal" or b.packed:
+            return
+        b.packed = True
+        srcs, offs = [], []
+        for p, o in zip(b.params, b.offsets):
+            g = p.grad
+            dst = _strided_view(b.flat_grad, p, o)
+            if g is None:
+                dst.zero_()
+            elif g.data_ptr() == dst.data_ptr() and _same_layout(g, dst):
+                continue  # already in place (e.g. user set p.grad to the view)
+            elif g.is_cuda and g.dtype == b.dtype and _same_layout(g, p) and _is_dense(g):
+                srcs.append(g)
+                offs.append(o)
+            else:
+                dst.copy_(g)
+        if srcs:
+            C = _ext.get(required=True)
+            es = b.flat_grad.element_size()
+            base = b.flat_grad.data_ptr()
+            code = mt.DTYPE_CODE[b.dtype]
+            C.mt_copy([g.data_ptr() for g in srcs], [base + o * es for o in offs], [g.numel() for g in srcs],
+                      code, code, 1.0, torch.cuda.current_stream(b.device).cuda_stream)
+        # from here on p.grad aliases the (soon reduced) flat buffer, as in "view" mode
+        for p, o in zip(b.params, b.offsets):
+            p.grad = _strided_view(b.flat_grad, p, o)
 
     def reduce_gradients(self):
         """Make sure every bucket has been allreduced (launch the rest, in order) and wait."""
@@ -311,6 +368,7 @@ class DDP:
             b.ready = True
         self._launch_ready()
         for b in self.buckets:
+            self._pack(b)
             self._finish(b)
 
     def _finish(self, b: _Bucket):
@@ -328,9 +386,24 @@ class DDP:
             if not b.launched:
                 b.ready = True
         self._launch_ready()
-        for b in self.buckets:
-            self._finish(b)
-            self._apply(b, gscale)
+        if self.timing and self.device.type == "cuda":
+            # exposed communication: from the end of backward (all grads produced on the
+            # compute stream) until the compute stream may consume the last reduced bucket
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for b in self.buckets:
+                self._pack(b)
+                self._finish(b)
+            e1.record()
+            self._comm_events.append((e0, e1))
+            for b in self.buckets:
+                self._apply(b, gscale)
+        else:
+            for b in self.buckets:
+                self._pack(b)
+                self._finish(b)
+                self._apply(b, gscale)
         if self.kind == "adam":
             fused.adam_advance_(self.hyper, self.adam.beta[0], self.adam.beta[1])
         self.step_count += 1
@@ -340,6 +413,17 @@ class DDP:
             check_replicas(self.module, comm=runtime.cpu_comm())
         if zero_grad:
             self.zero_grad()
+
+    def exposed_comm_ms(self, reset: bool = True) -> float | None:
+        """Mean exposed (not overlapped with backward) allreduce time per step, in ms,
+        over the steps run with ``timing=True`` since the last reset; None if none."""
+        if not self._comm_events:
+            return None
+        torch.cuda.synchronize(self.device)
+        ms = [a.elapsed_time(b) for a, b in self._comm_events]
+        if reset:
+            self._comm_events.clear()
+        return sum(ms) / len(ms)
 
     def _apply(self, b: _Bucket, gscale: float):
         masters = [b.master] if b.master is not None else None

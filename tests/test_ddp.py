@@ -15,8 +15,9 @@ def _data(rank):
     return x, x.sum(1, keepdim=True) ** 2
 
 
+@pytest.mark.parametrize("grad_mode", ["steal", "view"])
 @pytest.mark.parametrize("rule_name", ["adam", "adamw", "descent", "momentum", "nesterov"])
-def test_ddp_world1_matches_functional(rule_name):
+def test_ddp_world1_matches_functional(rule_name, grad_mode):
     from fluxmpi_amd import optimisers as O
     from fluxmpi_amd.parallel.ddp import DDP
 
@@ -25,7 +26,7 @@ def test_ddp_world1_matches_functional(rule_name):
                 "momentum": O.Momentum(0.05, 0.9), "nesterov": O.Nesterov(0.05, 0.9)}[rule_name]
 
     m1, m2 = _mlp(0), _mlp(0)
-    ddp = DDP(m1, rule(), bucket_mb=0.001, first_bucket_mb=0.0005)  # several tiny buckets
+    ddp = DDP(m1, rule(), bucket_mb=0.001, first_bucket_mb=0.0005, grad_mode=grad_mode)  # several tiny buckets
     assert len(ddp.buckets) > 1
     ps = {n: p.detach().clone() for n, p in m2.named_parameters()}
     st = O.setup(rule(), ps)
@@ -48,13 +49,21 @@ def test_ddp_world1_matches_functional(rule_name):
 
 def worker_ddp():
     import fluxmpi_amd as FluxMPI
+
+    FluxMPI.Init()
+    for mode in ("steal", "view"):
+        _ddp_checks(mode)
+    FluxMPI.Finalize()
+
+
+def _ddp_checks(grad_mode):
+    import fluxmpi_amd as FluxMPI
     from fluxmpi_amd import optimisers as O
     from fluxmpi_amd.parallel.ddp import DDP
 
-    FluxMPI.Init()
     r, W = FluxMPI.local_rank(), FluxMPI.total_workers()
     model = _mlp(1000 + r)  # different init per rank: DDP must broadcast rank 0's
-    ddp = DDP(model, O.Descent(0.1), bucket_mb=0.001, first_bucket_mb=0.0005, overlap=True)
+    ddp = DDP(model, O.Descent(0.1), bucket_mb=0.001, first_bucket_mb=0.0005, overlap=True, grad_mode=grad_mode)
     ref = _mlp(1000)
     x, y = _data(r)
     for step in range(3):
@@ -79,18 +88,24 @@ def worker_ddp():
     with ddp.no_sync():
         ((ddp(x[:4]) - y[:4]) ** 2).sum().backward()
     ((ddp(x[4:]) - y[4:]) ** 2).sum().backward()
+    ddp.reduce_gradients()
+    acc = [p.grad.clone() for p in model.parameters()]
+    ddp.zero_grad()
+    ((ddp(x) - y) ** 2).sum().backward()
+    ddp.reduce_gradients()
+    for a, p in zip(acc, model.parameters()):
+        torch.testing.assert_close(a, p.grad, rtol=1e-5, atol=1e-5)
     ddp.step()
 
     # low-precision wire format (K5 cast): same result within bf16 rounding
     m_a, m_b = _mlp(7), _mlp(7)
-    d_a = DDP(m_a, O.Descent(0.1), comm_dtype=torch.bfloat16)
-    d_b = DDP(m_b, O.Descent(0.1))
+    d_a = DDP(m_a, O.Descent(0.1), comm_dtype=torch.bfloat16, grad_mode=grad_mode)
+    d_b = DDP(m_b, O.Descent(0.1), grad_mode=grad_mode)
     for d in (d_a, d_b):
         ((d(x) - y) ** 2).mean().backward()
         d.step()
     for p, q in zip(m_a.parameters(), m_b.parameters()):
         torch.testing.assert_close(p, q, rtol=2e-2, atol=2e-3)
-    FluxMPI.Finalize()
 
 
 def test_ddp_gloo(spmd):

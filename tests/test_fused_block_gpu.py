@@ -9,11 +9,11 @@ def _rel(a, b):
     return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
 
 
-def _models():
+def _models(impl="fused"):
     from fluxmpi_amd.models.resnet import ResNet
     torch.manual_seed(0)
     ref = ResNet((2, 1, 1, 1), 10, conv_impl="miopen", norm="fused").cuda().to(memory_format=torch.channels_last)
-    fus = ResNet((2, 1, 1, 1), 10, conv_impl="fused").cuda().to(memory_format=torch.channels_last)
+    fus = ResNet((2, 1, 1, 1), 10, conv_impl=impl).cuda().to(memory_format=torch.channels_last)
     fus.load_state_dict(ref.state_dict())
     for m in (ref, fus):
         for mod in m.modules():
@@ -23,11 +23,13 @@ def _models():
     return ref, fus
 
 
-def test_fused_resnet_matches_unfused(gpu_ext):
+@pytest.mark.parametrize("impl", ["fused", "hybrid"])
+def test_fused_resnet_matches_unfused(gpu_ext, impl):
     """Both bf16 pipelines are compared with an fp32 model holding the same (bf16-rounded)
-    weights: the fused pipeline must be about as accurate as the unfused one."""
+    weights: the fused pipeline must be about as accurate as the unfused one. Layer 1 has an
+    identity block, so the GradLink residual-gradient hand-off is exercised."""
     from fluxmpi_amd.models.resnet import ResNet
-    ref, fus = _models()
+    ref, fus = _models(impl)
     f32 = ResNet((2, 1, 1, 1), 10, conv_impl="miopen", norm="fused").cuda().to(memory_format=torch.channels_last)
     f32.load_state_dict({k: v.float() if v.is_floating_point() else v for k, v in ref.state_dict().items()})
     x = torch.randn(8, 3, 64, 64, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
@@ -78,3 +80,26 @@ def test_fused_ops_individually(gpu_ext):
     (zb.float() * g).sum().backward()
     assert _rel(xb.grad, xa.grad) < 3e-2 and _rel(w3b.grad, w3a.grad) < 3e-2
     assert _rel(bn2b.weight.grad, bn2a.weight.grad) < 3e-2
+
+
+def test_hybrid_conv_with_link(gpu_ext):
+    """relu(bn(conv1x1_hybrid(x)) + x) with the residual gradient handed over by a GradLink
+    == the same block with autograd summing the two input gradients."""
+    from fluxmpi_amd.ops import fused_block as fb
+    from fluxmpi_amd.ops.batchnorm import FusedBatchNorm2d
+    torch.manual_seed(2)
+    x = torch.randn(4, 128, 14, 14, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(128, 128, 1, 1, device="cuda") * 0.1).bfloat16()
+    bn_a, bn_b = FusedBatchNorm2d(128).cuda(), FusedBatchNorm2d(128).cuda()
+    xa, xb = x.clone().requires_grad_(), x.clone().requires_grad_()
+    wa, wb = w.clone().requires_grad_(), w.clone().requires_grad_()
+    ya = bn_a(torch.nn.functional.conv2d(xa, wa), relu=True, residual=xa)
+    link = fb.GradLink()
+    yb = bn_b(fb.conv1x1_hybrid(xb, wb, link), relu=True, residual=xb, link=link)
+    assert torch.equal(ya, yb)
+    g = torch.randn_like(ya)
+    (ya.float() * g).sum().backward()
+    (yb.float() * g).sum().backward()
+    assert link.grad is None  # consumed
+    assert _rel(xb.grad, xa.grad) < 1e-2 and _rel(wb.grad, wa.grad) < 1e-2
+    assert _rel(bn_b.weight.grad, bn_a.weight.grad) < 1e-4  # float atomics: order-dependent rounding

@@ -57,13 +57,26 @@ def test_dgrad(gpu_ext, M, K, N):
 
 @pytest.mark.parametrize("M,K,N", SHAPES)
 @pytest.mark.parametrize("use_aff", [False, True])
-def test_wgrad(gpu_ext, M, K, N, use_aff):
+@pytest.mark.parametrize("splits", [None, 1, 7])
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+def test_wgrad(gpu_ext, M, K, N, use_aff, splits, out_dtype):
     from fluxmpi_amd.ops.gemm import conv1x1_wgrad
     dy, x = _rand(M, N), _rand(M, K)
     aff = _affine(K) if use_aff else None
-    dw = conv1x1_wgrad(dy, x, aff)
+    dw = conv1x1_wgrad(dy, x, aff, out_dtype=out_dtype, splits=splits)
+    assert dw.dtype == out_dtype
     ref = dy.float().t() @ _act(x, aff)
-    torch.testing.assert_close(dw, ref, rtol=1e-2, atol=5e-2)
+    tol = dict(rtol=1e-2, atol=5e-2) if out_dtype == torch.float32 else dict(rtol=2e-2, atol=1e-1)
+    torch.testing.assert_close(dw.float(), ref, **tol)
+
+
+@pytest.mark.parametrize("M,K,N", SHAPES)
+def test_dgrad_residual(gpu_ext, M, K, N):
+    from fluxmpi_amd.ops.gemm import conv1x1_dgrad
+    dy, w, r = _rand(M, N), _rand(N, K), _rand(M, K)
+    dx = conv1x1_dgrad(dy, w, residual=r)
+    ref = (dy.float() @ w.float()).to(torch.bfloat16).float() + r.float()
+    torch.testing.assert_close(dx.float(), ref, rtol=2e-2, atol=2e-2)
 
 
 def test_asymmetric_identity(gpu_ext):
