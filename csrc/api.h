@@ -89,6 +89,14 @@ void bn_fwd_infer(const void* x, void* y, const void* residual, const float* wei
                   const float* bias, const float* running_mean, const float* running_var,
                   int64_t rows, int64_t C, float eps, int relu, int dtype, hipStream_t stream);
 
+// ---- fused stem: BN affine + ReLU + max-pool (NHWC) ---------------------------------
+// y = relu(max over KxK/S window (pad P) of x*scale+shift), idx = window index (0xFF: max <= 0)
+void bn_relu_maxpool_fwd(const void* x, const float* scale, const float* shift, void* y, uint8_t* idx, int64_t N,
+                         int64_t H, int64_t W, int64_t C, int K, int S, int P, int dtype, hipStream_t stream);
+// dx[n,h,w,c] = sum of dy over the windows whose idx points at (h,w) (gather; dx fully written)
+void maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, int64_t N, int64_t H, int64_t W, int64_t C, int K,
+                 int S, int P, int dtype, hipStream_t stream);
+
 // ---- MFMA bf16 GEMM with BatchNorm fusions (1x1 convolutions) --------------------
 // C[M,N] = A[M,K] * B[N,K]^T. a_kmajor: A stored [M][lda] (K contiguous), else [K][lda]
 // (M contiguous); b_kmajor likewise for B. mode 0: C bf16; mode 1: C bf16 + per-column

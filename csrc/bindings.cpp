@@ -113,6 +113,20 @@ PYBIND11_MODULE(_C, m) {
                    reinterpret_cast<uint8_t*>(mask), dtype, S(stream));
         });
 
+  // ---- fused stem pool -------------------------------------------------------
+  m.def("bn_relu_maxpool_fwd",
+        [](uintptr_t x, uintptr_t scale, uintptr_t shift, uintptr_t y, uintptr_t idx, int64_t N, int64_t H, int64_t W,
+           int64_t C, int K, int S, int P, int dtype, uintptr_t stream) {
+          bn_relu_maxpool_fwd(reinterpret_cast<const void*>(x), reinterpret_cast<const float*>(scale),
+                              reinterpret_cast<const float*>(shift), reinterpret_cast<void*>(y),
+                              reinterpret_cast<uint8_t*>(idx), N, H, W, C, K, S, P, dtype, reinterpret_cast<hipStream_t>(stream));
+        });
+  m.def("maxpool_bwd", [](uintptr_t dy, uintptr_t idx, uintptr_t dx, int64_t N, int64_t H, int64_t W, int64_t C,
+                          int K, int S, int P, int dtype, uintptr_t stream) {
+    maxpool_bwd(reinterpret_cast<const void*>(dy), reinterpret_cast<const uint8_t*>(idx), reinterpret_cast<void*>(dx),
+                N, H, W, C, K, S, P, dtype, reinterpret_cast<hipStream_t>(stream));
+  });
+
   // ---- MFMA GEMM (1x1 conv) -------------------------------------------------
   m.def("gemm_bf16",
         [](uintptr_t a, uintptr_t b, uintptr_t c, int64_t lda, int64_t ldb, int64_t ldc, int64_t M, int64_t N,

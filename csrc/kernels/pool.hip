@@ -1,0 +1,209 @@
+// Fused BatchNorm-affine + ReLU + max-pool (the ResNet stem) and its backward — gfx950.
+//
+// Unfused, the stem writes the normalised 112x112x64 activation, re-reads it in
+// the max-pool, and the pool stores int64 argmax indices (8 B per pooled
+// element); its backward zero-fills and scatters into a full-resolution tensor.
+// Here:
+//   forward   p = relu(max_{window} (x*scale + shift)) read straight from the conv
+//             output x (the per-channel scale/shift come from the BN statistics
+//             pass), plus a 1-byte window index per pooled element (0xFF when the
+//             max is <= 0: the ReLU blocks the gradient);
+//   backward  dz[h,w] = sum of dp over the (at most ceil(K/S)^2) windows whose
+//             recorded argmax is (h,w) — a gather, every dz element written once,
+//             no zero fill, no atomics. dz is the gradient of the pre-ReLU BN output
+//             and feeds the plain BatchNorm backward.
+// Layout NHWC, 8 channels (16 B) per lane; consecutive lanes walk channels, then
+// output columns, so a wave reads whole contiguous pixel rows.
+#include <stdexcept>
+#include <string>
+
+#include "../api.h"
+#include "common.h"
+
+namespace fluxmpi {
+namespace {
+
+constexpr int kThreads = 256;
+
+struct PoolGeo {
+  int64_t N, H, W, C, OH, OW;
+  int K, S, P;
+};
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void bn_relu_maxpool_fwd_kernel(const T* __restrict__ x,
+                                                                       const float* __restrict__ scale,
+                                                                       const float* __restrict__ shift,
+                                                                       T* __restrict__ y, uint8_t* __restrict__ idx,
+                                                                       PoolGeo g, int64_t nvec) {
+  const int cv = static_cast<int>(g.C / 8);
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  for (int64_t v = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; v < nvec; v += stride) {
+    const int c8 = static_cast<int>(v % cv);
+    int64_t pix = v / cv;  // (n, oh, ow)
+    const int64_t ow = pix % g.OW;
+    pix /= g.OW;
+    const int64_t oh = pix % g.OH;
+    const int64_t n = pix / g.OH;
+    const int c0 = c8 * 8;
+    float sc[8], sh[8], best[8];
+    int arg[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sc[j] = scale[c0 + j];
+      sh[j] = shift[c0 + j];
+      best[j] = -INFINITY;
+      arg[j] = 0;
+    }
+    const int64_t h0 = oh * g.S - g.P, w0 = ow * g.S - g.P;
+    for (int kh = 0; kh < g.K; ++kh) {
+      const int64_t h = h0 + kh;
+      if (h < 0 || h >= g.H) continue;
+      for (int kw = 0; kw < g.K; ++kw) {
+        const int64_t w = w0 + kw;
+        if (w < 0 || w >= g.W) continue;
+        T raw[8];
+        load8(x + ((n * g.H + h) * g.W + w) * g.C + c0, raw);
+        const int k = kh * g.K + kw;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          // bit-identical to bn_norm_kernel's fmaf(x, scale, shift); first max wins on ties
+          const float z = fmaf(static_cast<float>(raw[j]), sc[j], sh[j]);
+          if (z > best[j]) {
+            best[j] = z;
+            arg[j] = k;
+          }
+        }
+      }
+    }
+    T out[8];
+    uint8_t a8[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bool pos = best[j] > 0.f;
+      out[j] = static_cast<T>(pos ? best[j] : 0.f);
+      a8[j] = pos ? static_cast<uint8_t>(arg[j]) : static_cast<uint8_t>(0xFF);
+    }
+    store8(y + v * 8, out);
+    uint2 packed;
+    __builtin_memcpy(&packed, a8, 8);
+    *reinterpret_cast<uint2*>(idx + v * 8) = packed;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void maxpool_bwd_gather_kernel(const T* __restrict__ dy,
+                                                                      const uint8_t* __restrict__ idx,
+                                                                      T* __restrict__ dx, PoolGeo g, int64_t nvec) {
+  const int cv = static_cast<int>(g.C / 8);
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  for (int64_t v = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; v < nvec; v += stride) {
+    const int c8 = static_cast<int>(v % cv);
+    int64_t pix = v / cv;  // (n, h, w) of the input
+    const int64_t w = pix % g.W;
+    pix /= g.W;
+    const int64_t h = pix % g.H;
+    const int64_t n = pix / g.H;
+    // windows oh with oh*S - P <= h <= oh*S - P + K - 1
+    int64_t oh_lo = h + g.P - g.K + 1;
+    oh_lo = oh_lo <= 0 ? 0 : (oh_lo + g.S - 1) / g.S;
+    int64_t oh_hi = (h + g.P) / g.S;
+    if (oh_hi > g.OH - 1) oh_hi = g.OH - 1;
+    int64_t ow_lo = w + g.P - g.K + 1;
+    ow_lo = ow_lo <= 0 ? 0 : (ow_lo + g.S - 1) / g.S;
+    int64_t ow_hi = (w + g.P) / g.S;
+    if (ow_hi > g.OW - 1) ow_hi = g.OW - 1;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int64_t oh = oh_lo; oh <= oh_hi; ++oh) {
+      const int kh = static_cast<int>(h - (oh * g.S - g.P));
+      for (int64_t ow = ow_lo; ow <= ow_hi; ++ow) {
+        const int k = kh * g.K + static_cast<int>(w - (ow * g.S - g.P));
+        const int64_t o = ((n * g.OH + oh) * g.OW + ow) * g.C + c8 * 8;
+        const uint2 packed = *reinterpret_cast<const uint2*>(idx + o);
+        uint8_t a8[8];
+        __builtin_memcpy(a8, &packed, 8);
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) any |= a8[j] == k;
+        if (!any) continue;
+        T d[8];
+        load8(dy + o, d);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (a8[j] == k) acc[j] += static_cast<float>(d[j]);
+      }
+    }
+    T out[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[j] = static_cast<T>(acc[j]);
+    store8(dx + v * 8, out);
+  }
+}
+
+int grid_for(int64_t nvec) {
+  int64_t b = (nvec + kThreads - 1) / kThreads;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  return static_cast<int>(b);
+}
+
+PoolGeo make_geo(int64_t N, int64_t H, int64_t W, int64_t C, int K, int S, int P) {
+  if (C % 8 != 0) throw std::runtime_error("maxpool: C % 8 == 0 required (got " + std::to_string(C) + ")");
+  if (K < 1 || K * K > 255 || S < 1 || P < 0 || P >= K)
+    throw std::runtime_error("maxpool: need 1 <= K, K*K <= 255, S >= 1, 0 <= P < K");
+  PoolGeo g{N, H, W, C, (H + 2 * P - K) / S + 1, (W + 2 * P - K) / S + 1, K, S, P};
+  if (g.OH < 1 || g.OW < 1) throw std::runtime_error("maxpool: empty output");
+  return g;
+}
+
+}  // namespace
+
+void bn_relu_maxpool_fwd(const void* x, const float* scale, const float* shift, void* y, uint8_t* idx, int64_t N,
+                         int64_t H, int64_t W, int64_t C, int K, int S, int P, int dtype, hipStream_t s) {
+  const PoolGeo g = make_geo(N, H, W, C, K, S, P);
+  const int64_t nvec = N * g.OH * g.OW * C / 8;
+  const int nb = grid_for(nvec);
+  switch (dtype) {
+    case kBF16:
+      bn_relu_maxpool_fwd_kernel<bf16><<<nb, kThreads, 0, s>>>(static_cast<const bf16*>(x), scale, shift,
+                                                               static_cast<bf16*>(y), idx, g, nvec);
+      break;
+    case kF16:
+      bn_relu_maxpool_fwd_kernel<f16><<<nb, kThreads, 0, s>>>(static_cast<const f16*>(x), scale, shift,
+                                                              static_cast<f16*>(y), idx, g, nvec);
+      break;
+    case kF32:
+      bn_relu_maxpool_fwd_kernel<float><<<nb, kThreads, 0, s>>>(static_cast<const float*>(x), scale, shift,
+                                                                static_cast<float*>(y), idx, g, nvec);
+      break;
+    default:
+      throw std::runtime_error("bn_relu_maxpool_fwd: unsupported dtype");
+  }
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+}
+
+void maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, int64_t N, int64_t H, int64_t W, int64_t C, int K,
+                 int S, int P, int dtype, hipStream_t s) {
+  const PoolGeo g = make_geo(N, H, W, C, K, S, P);
+  const int64_t nvec = N * H * W * C / 8;
+  const int nb = grid_for(nvec);
+  switch (dtype) {
+    case kBF16:
+      maxpool_bwd_gather_kernel<bf16><<<nb, kThreads, 0, s>>>(static_cast<const bf16*>(dy), idx,
+                                                              static_cast<bf16*>(dx), g, nvec);
+      break;
+    case kF16:
+      maxpool_bwd_gather_kernel<f16><<<nb, kThreads, 0, s>>>(static_cast<const f16*>(dy), idx,
+                                                             static_cast<f16*>(dx), g, nvec);
+      break;
+    case kF32:
+      maxpool_bwd_gather_kernel<float><<<nb, kThreads, 0, s>>>(static_cast<const float*>(dy), idx,
+                                                               static_cast<float*>(dx), g, nvec);
+      break;
+    default:
+      throw std::runtime_error("maxpool_bwd: unsupported dtype");
+  }
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace fluxmpi

@@ -146,10 +146,15 @@ class ResNet(nn.Module):
 
     def forward(self, x):
         if self.norm_kind == "fused":
-            x = self.bn1(self.conv1(x), relu=True)
+            from ..ops import pool
+            c = self.conv1(x)
+            if self.training and pool.supported(c):
+                # BN + ReLU + 3x3/2 max-pool in one pass over the stem output
+                x = pool.bn_relu_maxpool(c, self.bn1, 3, 2, 1)
+            else:
+                x = self.maxpool(self.bn1(c, relu=True))
         else:
-            x = F.relu(self.bn1(self.conv1(x)))
-        x = self.maxpool(x)
+            x = self.maxpool(F.relu(self.bn1(self.conv1(x))))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
         return self.fc(x)

@@ -102,3 +102,47 @@ def test_resnet_fused_vs_torch_norm(gpu_ext):
         # deep-chain gradients accumulate fp32 rounding differences elementwise; compare norms
         rel = float((p.grad - q.grad).norm() / q.grad.norm().clamp_min(1e-12))
         assert rel < 5e-3, f"{n}: relative grad error {rel:.2e}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,k,s,p", [((4, 64, 32, 32), 3, 2, 1), ((2, 16, 17, 15), 3, 2, 1),
+                                          ((2, 32, 12, 12), 2, 2, 0), ((3, 8, 9, 11), 3, 1, 1)])
+def test_bn_relu_maxpool_vs_reference(gpu_ext, shape, k, s, p):
+    """Fused stem tail vs max_pool2d(relu(batch_norm(x))) in fp32 on the same bf16 input."""
+    import torch.nn.functional as F
+    from fluxmpi_amd.ops.batchnorm import FusedBatchNorm2d
+    from fluxmpi_amd.ops.pool import bn_relu_maxpool
+    torch.manual_seed(3)
+    n, c, h, w = shape
+    x = torch.randn(shape, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    bn = FusedBatchNorm2d(c).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(-1.5, 1.5)  # negative scales: the max must be taken after the affine
+        bn.bias.uniform_(-0.5, 0.5)
+    ref_bn = torch.nn.BatchNorm2d(c).cuda()
+    ref_bn.load_state_dict(bn.state_dict())
+    xa = x.clone().requires_grad_()
+    xr = x.float().clone().requires_grad_()
+    y = bn_relu_maxpool(xa, bn, k, s, p)
+    yr = F.max_pool2d(F.relu(ref_bn(xr)), k, s, p)
+    torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(bn.running_mean, ref_bn.running_mean, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(bn.running_var, ref_bn.running_var, rtol=1e-3, atol=1e-4)
+    g = torch.randn_like(yr)
+    (y.float() * g).sum().backward()
+    (yr * g).sum().backward()
+    rel = lambda a, b: float((a.float() - b.float()).norm() / b.float().norm())  # noqa: E731
+    assert rel(xa.grad, xr.grad) < 3e-2
+    assert rel(bn.weight.grad, ref_bn.weight.grad) < 2e-2
+    assert rel(bn.bias.grad, ref_bn.bias.grad) < 2e-2
+
+
+def test_bn_relu_maxpool_cpu_fallback():
+    import torch.nn.functional as F
+    from fluxmpi_amd.ops.pool import bn_relu_maxpool
+    x = torch.randn(2, 8, 10, 10)
+    bn = torch.nn.BatchNorm2d(8)
+    ref = torch.nn.BatchNorm2d(8)
+    y = bn_relu_maxpool(x, bn)
+    torch.testing.assert_close(y, F.max_pool2d(F.relu(ref(x)), 3, 2, 1))
+    torch.testing.assert_close(bn.running_mean, ref.running_mean)
