@@ -121,7 +121,7 @@ struct GemmProblem {
   int64_t ldr;
 };
 void gemm_bf16(const GemmProblem& g, hipStream_t stream);
-// out[e] = sum over s < splits of ws[s*n + e] (mode-3 split-K partials); out fp32 or bf16 (dtype code)
+// out[e] = sum over s < splits of ws[s*n + e] (mode-3 split-K partials; ws is clobbered); out fp32 or bf16
 void gemm_splitk_reduce(const float* ws, int splits, int64_t n, void* out, int out_dtype, hipStream_t stream);
 
 }  // namespace fluxmpi

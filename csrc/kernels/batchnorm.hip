@@ -12,11 +12,12 @@
 //
 // Reductions: a workgroup accumulates fp32 per-channel partials over its rows
 // in registers, reduces the lanes that share a channel vector through LDS and
-// adds its partial to one of 16 shards of a [16][2][C] fp32 accumulator with
+// adds its partial to one of 64 shards of a [64][2][C] fp32 accumulator with
 // global float atomics. A tiny finalize kernel sums the shards into the
 // per-channel statistics (and re-zeroes them, so the persistent workspace
 // needs no memset per call); the consumer kernels derive their per-channel
-// coefficients from those statistics in an LDS prologue.
+// coefficients from those statistics (registers, or LDS when C/8 does not divide
+// the workgroup). Grids are one full round of resident workgroups (occupancy x CUs).
 #include <stdexcept>
 #include <string>
 
@@ -57,15 +58,15 @@ struct Geo {
   int blocks;
 };
 
-Geo geometry(int64_t rows, int64_t C) {
+Geo geometry(int64_t rows, int64_t C, int64_t max_blocks = 2048) {
   Geo g;
   g.cv = static_cast<int>(C / 8);
   g.rpi = kThreads / g.cv;
   if (g.rpi < 1) g.rpi = 1;
-  // >= 64K elements per workgroup, at most 2048 workgroups
+  // >= 32K elements per workgroup, at most one full round of resident workgroups
   int64_t min_rows = (32768 + C - 1) / C;
   int64_t blocks = (rows + min_rows - 1) / min_rows;
-  if (blocks > 2048) blocks = 2048;
+  if (blocks > max_blocks) blocks = max_blocks;
   if (blocks < 1) blocks = 1;
   int64_t rpb = (rows + blocks - 1) / blocks;
   rpb = (rpb + g.rpi - 1) / g.rpi * g.rpi;
@@ -202,9 +203,29 @@ __global__ __launch_bounds__(kThreads) void bn_stats_kernel(const T* __restrict_
   block_reduce_atomic(s, q, g.cv, g.rpi, C, acc, smem);
 }
 
-// y = act(x*scale + shift [+ res]); scale/shift derived in the LDS prologue from
-// (mean, invstd) = batch statistics (training) or running statistics (eval).
+// y = act(x*scale + shift [+ res]); scale/shift derived from (mean, invstd) = batch
+// statistics (training) or running statistics (eval).
+// FIXED (C/8 divides the 256-lane workgroup): the grid stride is a multiple of C/8, so
+// every lane keeps the same 8 channels for the whole kernel and holds its coefficients
+// in registers; otherwise they are staged in LDS and indexed per vector.
+// Two vectors per lane per iteration (loads of both issued before any math).
 template <typename T, bool RELU, bool RES>
+__device__ __forceinline__ void norm_vec(float (&f)[8], const float (&rr)[8], const float* sc, const float* sh,
+                                         unsigned& bits) {
+  bits = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float o = fmaf(f[j], sc[j], sh[j]);  // explicit fma: backward recomputes it bit-identically
+    if (RES) o += rr[j];
+    if (RELU) {
+      bits |= (o > 0.f ? 1u : 0u) << j;
+      o = o > 0.f ? o : 0.f;
+    }
+    f[j] = o;
+  }
+}
+
+template <typename T, bool RELU, bool RES, bool FIXED>
 __global__ __launch_bounds__(kThreads) void bn_norm_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                            const T* __restrict__ res, const float* __restrict__ w,
                                                            const float* __restrict__ b,
@@ -215,37 +236,53 @@ __global__ __launch_bounds__(kThreads) void bn_norm_kernel(const T* __restrict__
   // 8 elements lets the backward apply the ReLU of a residual block without
   // re-reading y (2 B/element -> 1/8 B/element).
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* scale = smem;
-  float* shift = smem + C;
-  for (int c = threadIdx.x; c < C; c += kThreads) {
+  auto coef = [&](int c, float& sc, float& sh) {
     const float mean = mean_in[c];
     const float invstd = train ? stat2[c] : rsqrtf(stat2[c] + eps);  // save_invstd | running_var
-    const float sc = (w ? w[c] : 1.f) * invstd;
-    scale[c] = sc;
-    shift[c] = fmaf(-mean, sc, b ? b[c] : 0.f);  // explicit fma: backward recomputes it bit-identically
-  }
-  __syncthreads();
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
-  for (int64_t v = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; v < nvec; v += stride) {
-    const int64_t e = v * 8;
-    const int c0 = static_cast<int>(e % C);
-    float f[8];
-    ld8f(x + e, f);
-    float rr[8];
-    if (RES) ld8f(res + e, rr);
-    unsigned bits = 0;
+    sc = (w ? w[c] : 1.f) * invstd;
+    sh = fmaf(-mean, sc, b ? b[c] : 0.f);
+  };
+  float rsc[8], rsh[8];
+  if (FIXED) {
+    const int c0 = (threadIdx.x % (C / 8)) * 8;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float o = fmaf(f[j], scale[c0 + j], shift[c0 + j]);
-      if (RES) o += rr[j];
-      if (RELU) {
-        bits |= (o > 0.f ? 1u : 0u) << j;
-        o = o > 0.f ? o : 0.f;
-      }
-      f[j] = o;
+    for (int j = 0; j < 8; ++j) coef(c0 + j, rsc[j], rsh[j]);
+  } else {
+    for (int c = threadIdx.x; c < C; c += kThreads) coef(c, smem[c], smem[C + c]);
+    __syncthreads();
+  }
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  int64_t v = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  for (; v + stride < nvec; v += 2 * stride) {
+    float f0[8], f1[8], r0[8], r1[8];
+    ld8f(x + v * 8, f0);
+    ld8f(x + (v + stride) * 8, f1);
+    if (RES) {
+      ld8f(res + v * 8, r0);
+      ld8f(res + (v + stride) * 8, r1);
     }
-    st8f(y + e, f);
-    if (RELU && mask != nullptr) mask[v] = static_cast<uint8_t>(bits);
+    const float* sc0 = FIXED ? rsc : smem + (v * 8) % C;
+    const float* sh0 = FIXED ? rsh : smem + C + (v * 8) % C;
+    const float* sc1 = FIXED ? rsc : smem + ((v + stride) * 8) % C;
+    const float* sh1 = FIXED ? rsh : smem + C + ((v + stride) * 8) % C;
+    unsigned b0, b1;
+    norm_vec<T, RELU, RES>(f0, r0, sc0, sh0, b0);
+    norm_vec<T, RELU, RES>(f1, r1, sc1, sh1, b1);
+    st8f(y + v * 8, f0);
+    st8f(y + (v + stride) * 8, f1);
+    if (RELU && mask != nullptr) {
+      mask[v] = static_cast<uint8_t>(b0);
+      mask[v + stride] = static_cast<uint8_t>(b1);
+    }
+  }
+  if (v < nvec) {
+    float f0[8], r0[8];
+    ld8f(x + v * 8, f0);
+    if (RES) ld8f(res + v * 8, r0);
+    unsigned b0;
+    norm_vec<T, RELU, RES>(f0, r0, FIXED ? rsc : smem + (v * 8) % C, FIXED ? rsh : smem + C + (v * 8) % C, b0);
+    st8f(y + v * 8, f0);
+    if (RELU && mask != nullptr) mask[v] = static_cast<uint8_t>(b0);
   }
 }
 
@@ -329,8 +366,43 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const T* __rest
 }
 
 // dx = w*invstd * (dy_eff - sum_dy/R - xhat * sum_dy_xhat/R); dres = dy_eff
-// (sum_dy = db, sum_dy_xhat = dw, produced by bn_finalize_bwd_kernel)
+// (sum_dy = db, sum_dy_xhat = dw, produced by bn_finalize_bwd_kernel), evaluated as
+// dx = A*dy_eff + B*x + D with per-channel A = w*invstd, B = -A*invstd*mean(dy_eff*xhat),
+// D = A*(mean*invstd*mean(dy_eff*xhat) - mean(dy_eff)). Coefficients in registers
+// (FIXED) or LDS as in bn_norm_kernel; two vectors per lane per iteration.
+struct DxCoef {
+  float a, b, d, sh;  // sh: forward shift (RM == 2 mask recompute, with a == forward scale)
+};
+
+__device__ __forceinline__ DxCoef dx_coef(int c, const float* __restrict__ w, const float* __restrict__ bias,
+                                          const float* __restrict__ smean, const float* __restrict__ sinv,
+                                          const float* __restrict__ dw, const float* __restrict__ db, float inv_n) {
+  const float iv = sinv[c], m = smean[c];
+  const float sc = (w ? w[c] : 1.f) * iv;
+  const float k2 = db[c] * inv_n, k3 = dw[c] * inv_n;
+  DxCoef k;
+  k.a = sc;
+  k.b = -sc * iv * k3;
+  k.d = sc * (m * iv * k3 - k2);
+  k.sh = fmaf(-m, sc, bias ? bias[c] : 0.f);
+  return k;
+}
+
 template <typename T, int RM, bool DRES>
+__device__ __forceinline__ void dx_vec(float (&d)[8], float (&xv)[8], const float (&yv)[8], unsigned mbs,
+                                       const DxCoef* k) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float dd = d[j];
+    if (RM == 1) dd = yv[j] > 0.f ? dd : 0.f;
+    if (RM == 3) dd = (mbs >> j) & 1u ? dd : 0.f;
+    if (RM == 2) dd = fmaf(xv[j], k[j].a, k[j].sh) > 0.f ? dd : 0.f;
+    d[j] = dd;
+    xv[j] = fmaf(k[j].a, dd, fmaf(k[j].b, xv[j], k[j].d));
+  }
+}
+
+template <typename T, int RM, bool DRES, bool FIXED>
 __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                              const T* __restrict__ y,
                                                              const uint8_t* __restrict__ mask,
@@ -342,57 +414,62 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const T* __restrict
                                                              const float* __restrict__ db, T* __restrict__ dx,
                                                              T* __restrict__ dres, int64_t rows, int C,
                                                              int64_t nvec) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* k1 = smem;          // w*invstd (== forward scale)
-  float* k2 = smem + C;      // mean(dy_eff)
-  float* k3 = smem + 2 * C;  // mean(dy_eff*xhat)
-  float* mu = smem + 3 * C;
-  float* is = smem + 4 * C;
-  float* sh = smem + 5 * C;  // forward shift (RM == 2)
+  extern __shared__ __attribute__((aligned(16))) DxCoef ksm[];
   const float inv_n = 1.f / static_cast<float>(rows);
-  for (int c = threadIdx.x; c < C; c += kThreads) {
-    const float iv = sinv[c];
-    const float m = smean[c];
-    const float sc = (w ? w[c] : 1.f) * iv;
-    k1[c] = sc;
-    k2[c] = db[c] * inv_n;
-    k3[c] = dw[c] * inv_n;
-    mu[c] = m;
-    is[c] = iv;
-    sh[c] = fmaf(-m, sc, bias ? bias[c] : 0.f);
-  }
-  __syncthreads();
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
-  for (int64_t v = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; v < nvec; v += stride) {
-    const int64_t e = v * 8;
-    const int c0 = static_cast<int>(e % C);
-    float d[8], xv[8], yv[8];
-    ld8f(dy + e, d);
-    ld8f(x + e, xv);
-    if (RM == 1) ld8f(y + e, yv);
-    const unsigned mbs = RM == 3 ? mask[v] : 0u;
+  DxCoef rk[8];
+  if (FIXED) {
+    const int c0 = (threadIdx.x % (C / 8)) * 8;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = c0 + j;
-      float dd = d[j];
-      if (RM == 1) dd = yv[j] > 0.f ? dd : 0.f;
-      if (RM == 3) dd = (mbs >> j) & 1u ? dd : 0.f;
-      if (RM == 2) dd = fmaf(xv[j], k1[c], sh[c]) > 0.f ? dd : 0.f;
-      d[j] = dd;
-      const float xh = (xv[j] - mu[c]) * is[c];
-      xv[j] = k1[c] * (dd - k2[c] - xh * k3[c]);
+    for (int j = 0; j < 8; ++j) rk[j] = dx_coef(c0 + j, w, bias, smean, sinv, dw, db, inv_n);
+  } else {
+    for (int c = threadIdx.x; c < C; c += kThreads) ksm[c] = dx_coef(c, w, bias, smean, sinv, dw, db, inv_n);
+    __syncthreads();
+  }
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  int64_t v = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  for (; v + stride < nvec; v += 2 * stride) {
+    const int64_t v1 = v + stride;
+    float d0[8], x0[8], y0[8], d1[8], x1[8], y1[8];
+    ld8f(dy + v * 8, d0);
+    ld8f(x + v * 8, x0);
+    ld8f(dy + v1 * 8, d1);
+    ld8f(x + v1 * 8, x1);
+    if (RM == 1) {
+      ld8f(y + v * 8, y0);
+      ld8f(y + v1 * 8, y1);
     }
-    st8f(dx + e, xv);
-    if (DRES) st8f(dres + e, d);
+    const unsigned m0 = RM == 3 ? mask[v] : 0u, m1 = RM == 3 ? mask[v1] : 0u;
+    dx_vec<T, RM, DRES>(d0, x0, y0, m0, FIXED ? rk : ksm + (v * 8) % C);
+    dx_vec<T, RM, DRES>(d1, x1, y1, m1, FIXED ? rk : ksm + (v1 * 8) % C);
+    st8f(dx + v * 8, x0);
+    st8f(dx + v1 * 8, x1);
+    if (DRES) {
+      st8f(dres + v * 8, d0);
+      st8f(dres + v1 * 8, d1);
+    }
+  }
+  if (v < nvec) {
+    float d0[8], x0[8], y0[8];
+    ld8f(dy + v * 8, d0);
+    ld8f(x + v * 8, x0);
+    if (RM == 1) ld8f(y + v * 8, y0);
+    const unsigned m0 = RM == 3 ? mask[v] : 0u;
+    dx_vec<T, RM, DRES>(d0, x0, y0, m0, FIXED ? rk : ksm + (v * 8) % C);
+    st8f(dx + v * 8, x0);
+    if (DRES) st8f(dres + v * 8, d0);
   }
 }
 
-int elementwise_blocks(int64_t nvec) {
+// one full round of resident workgroups (or fewer if the tensor is small)
+int elementwise_grid(const void* kernel, size_t smem, int64_t nvec) {
   int64_t b = (nvec + kThreads - 1) / kThreads;
-  if (b > 2048) b = 2048;
+  const int64_t cap = resident_blocks(kernel, kThreads, smem);
+  if (b > cap) b = cap;
   if (b < 1) b = 1;
   return static_cast<int>(b);
 }
+
+bool fixed_channels(int64_t C) { return kThreads % (C / 8) == 0; }
 
 void check(int64_t C) {
   if (C % 8 != 0 || C > kMaxC || C < 8)
@@ -401,26 +478,40 @@ void check(int64_t C) {
 
 size_t reduce_smem(const Geo& g, int64_t C) { return static_cast<size_t>(2 * g.rpi * C) * sizeof(float); }
 
-#define FLUXMPI_BN_DISPATCH2(F, A, B, ...) \
-  if ((A) && (B)) F(true, true, __VA_ARGS__);  \
-  else if (A) F(true, false, __VA_ARGS__);    \
-  else if (B) F(false, true, __VA_ARGS__);    \
-  else F(false, false, __VA_ARGS__);
+// Geometry of a row-reduction kernel capped at one full round of its resident workgroups.
+Geo reduce_geometry(const void* kernel, int64_t rows, int64_t C) {
+  const Geo g0 = geometry(rows, C);
+  return geometry(rows, C, resident_blocks(kernel, kThreads, reduce_smem(g0, C)));
+}
+
 
 template <typename T>
 void norm_t(const void* x, void* y, const void* res, const float* w, const float* b, const float* mean,
             const float* stat2, int64_t rows, int64_t C, float eps, int train, int relu, uint8_t* mask,
             hipStream_t s) {
   const int64_t nvec = rows * C / 8;
-  const int nb = elementwise_blocks(nvec);
-  const size_t sm2 = 2 * C * sizeof(float);
   const T* xr = static_cast<const T*>(x);
   T* yr = static_cast<T*>(y);
   const T* rr = static_cast<const T*>(res);
-#define LAUNCH(RELU, RES, _)                                                                                     \
-  bn_norm_kernel<T, RELU, RES><<<nb, kThreads, sm2, s>>>(xr, yr, rr, w, b, mean, stat2, (int)C, eps, train, nvec, \
-                                                         mask)
-  FLUXMPI_BN_DISPATCH2(LAUNCH, relu, res != nullptr, 0)
+  const bool fixed = fixed_channels(C);
+#define LAUNCH(RELU, RES, FX)                                                                                   \
+  {                                                                                                            \
+    const size_t sm = FX ? 0 : 2 * C * sizeof(float);                                                          \
+    auto k = bn_norm_kernel<T, RELU, RES, FX>;                                                                 \
+    k<<<elementwise_grid(reinterpret_cast<const void*>(k), sm, nvec), kThreads, sm, s>>>(                      \
+        xr, yr, rr, w, b, mean, stat2, (int)C, eps, train, nvec, mask);                                        \
+  }
+#define LAUNCH_F(RELU, RES)                \
+  {                                        \
+    if (fixed) LAUNCH(RELU, RES, true)     \
+    else LAUNCH(RELU, RES, false)          \
+  }
+  const bool has_res = res != nullptr;
+  if (relu && has_res) LAUNCH_F(true, true)
+  else if (relu) LAUNCH_F(true, false)
+  else if (has_res) LAUNCH_F(false, true)
+  else LAUNCH_F(false, false)
+#undef LAUNCH_F
 #undef LAUNCH
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
@@ -429,7 +520,7 @@ template <typename T>
 void fwd_train_t(const void* x, void* y, const void* res, const float* w, const float* b, float* rm, float* rv,
                  float* sm, float* si, float* ws, int64_t rows, int64_t C, float momentum, float eps, int relu,
                  uint8_t* mask, hipStream_t s) {
-  Geo g = geometry(rows, C);
+  const Geo g = reduce_geometry(reinterpret_cast<const void*>(bn_stats_kernel<T>), rows, C);
   bn_stats_kernel<T><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(static_cast<const T*>(x), rows, (int)C, g, ws);
   FLUXMPI_HIP_CHECK(hipGetLastError());
   bn_finalize_fwd_kernel<<<(int)((C + 255) / 256), 256, 0, s>>>(ws, (int)C, rows, momentum, eps, sm, si, rm, rv,
@@ -442,36 +533,47 @@ template <typename T>
 void bwd_t(const void* dy, const void* x, const void* y, const uint8_t* mask, const float* w, const float* b,
            const float* sm, const float* si, void* dx, void* dres, float* dw, float* db, float* ws, int64_t rows,
            int64_t C, int relu, hipStream_t s) {
-  Geo g = geometry(rows, C);
   const T* dyr = static_cast<const T*>(dy);
   const T* xr = static_cast<const T*>(x);
   const T* yr = static_cast<const T*>(y);
   // relu: 0 none; 1 mask from y; 2 mask recomputed from x (no residual); 3 mask from saved bits
   const int rm = relu == 0 ? 0 : (mask != nullptr ? 3 : (y != nullptr ? 1 : 2));
-  const size_t rsm = reduce_smem(g, C);
-#define RED(RM) \
-  bn_bwd_reduce_kernel<T, RM><<<g.blocks, kThreads, rsm, s>>>(dyr, xr, yr, mask, w, b, sm, si, rows, (int)C, g, ws)
-  if (rm == 0) RED(0);
-  else if (rm == 1) RED(1);
-  else if (rm == 2) RED(2);
-  else RED(3);
+#define RED(RM)                                                                                                  \
+  {                                                                                                             \
+    const Geo g = reduce_geometry(reinterpret_cast<const void*>(bn_bwd_reduce_kernel<T, RM>), rows, C);          \
+    bn_bwd_reduce_kernel<T, RM><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(dyr, xr, yr, mask, w, b, sm, si,   \
+                                                                              rows, (int)C, g, ws);             \
+  }
+  if (rm == 0) RED(0)
+  else if (rm == 1) RED(1)
+  else if (rm == 2) RED(2)
+  else RED(3)
 #undef RED
   FLUXMPI_HIP_CHECK(hipGetLastError());
   bn_finalize_bwd_kernel<<<(int)((C + 255) / 256), 256, 0, s>>>(ws, (int)C, dw, db);
   FLUXMPI_HIP_CHECK(hipGetLastError());
   const int64_t nvec = rows * C / 8;
-  const int nb = elementwise_blocks(nvec);
-  const size_t sm6 = 6 * C * sizeof(float);
   T* dxr = static_cast<T*>(dx);
   T* drr = static_cast<T*>(dres);
-#define LAUNCH(RM, DRES)                                                                                          \
-  bn_bwd_dx_kernel<T, RM, DRES><<<nb, kThreads, sm6, s>>>(dyr, xr, yr, mask, w, b, sm, si, dw, db, dxr, drr, rows, \
-                                                          (int)C, nvec)
+  const bool fixed = fixed_channels(C);
+#define LAUNCH(RM, DRES, FX)                                                                                    \
+  {                                                                                                            \
+    const size_t lds = FX ? 0 : C * sizeof(DxCoef);                                                            \
+    auto k = bn_bwd_dx_kernel<T, RM, DRES, FX>;                                                                \
+    k<<<elementwise_grid(reinterpret_cast<const void*>(k), lds, nvec), kThreads, lds, s>>>(                    \
+        dyr, xr, yr, mask, w, b, sm, si, dw, db, dxr, drr, rows, (int)C, nvec);                                \
+  }
+#define LAUNCH_F(RM, DRES)             \
+  {                                    \
+    if (fixed) LAUNCH(RM, DRES, true)  \
+    else LAUNCH(RM, DRES, false)       \
+  }
   const bool has_dres = dres != nullptr;
-  if (rm == 0) { if (has_dres) LAUNCH(0, true); else LAUNCH(0, false); }
-  else if (rm == 1) { if (has_dres) LAUNCH(1, true); else LAUNCH(1, false); }
-  else if (rm == 2) { if (has_dres) LAUNCH(2, true); else LAUNCH(2, false); }
-  else { if (has_dres) LAUNCH(3, true); else LAUNCH(3, false); }
+  if (rm == 0) { if (has_dres) LAUNCH_F(0, true) else LAUNCH_F(0, false) }
+  else if (rm == 1) { if (has_dres) LAUNCH_F(1, true) else LAUNCH_F(1, false) }
+  else if (rm == 2) { if (has_dres) LAUNCH_F(2, true) else LAUNCH_F(2, false) }
+  else { if (has_dres) LAUNCH_F(3, true) else LAUNCH_F(3, false) }
+#undef LAUNCH_F
 #undef LAUNCH
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
@@ -504,13 +606,18 @@ void bn_stats_finalize(const void* x, const float* w, const float* b, float* rm,
                        int stats_ready, int dtype, hipStream_t s) {
   check(C);
   if (!stats_ready) {
-    Geo g = geometry(rows, C);
+#define STATS(T)                                                                                              \
+  {                                                                                                          \
+    const Geo g = reduce_geometry(reinterpret_cast<const void*>(bn_stats_kernel<T>), rows, C);               \
+    bn_stats_kernel<T><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(static_cast<const T*>(x), rows, (int)C, g, ws); \
+  }
     switch (dtype) {
-      case kBF16: bn_stats_kernel<bf16><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(static_cast<const bf16*>(x), rows, (int)C, g, ws); break;
-      case kF16: bn_stats_kernel<f16><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(static_cast<const f16*>(x), rows, (int)C, g, ws); break;
-      case kF32: bn_stats_kernel<float><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(static_cast<const float*>(x), rows, (int)C, g, ws); break;
+      case kBF16: STATS(bf16) break;
+      case kF16: STATS(f16) break;
+      case kF32: STATS(float) break;
       default: throw std::runtime_error("fused batchnorm: unsupported dtype");
     }
+#undef STATS
     FLUXMPI_HIP_CHECK(hipGetLastError());
   }
   bn_finalize_fwd_kernel<<<(int)((C + 255) / 256), 256, 0, s>>>(ws, (int)C, rows, momentum, eps, sm, si, rm, rv, w, b,

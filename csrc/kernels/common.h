@@ -10,7 +10,13 @@
 //  * grids of thousands of workgroups for the 256 CUs / 8 XCDs.
 #pragma once
 #include <hip/hip_runtime.h>
+
 #include <cstdint>
+#include <map>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <tuple>
 
 namespace fluxmpi {
 
@@ -70,6 +76,29 @@ __device__ __forceinline__ int find_tensor(const int32_t (&start)[N], int n, int
 }
 
 }  // namespace fluxmpi
+
+// Workgroups of `threads` lanes (with `smem` bytes of dynamic LDS) that one dispatch of
+// `kernel` keeps resident on the current device: occupancy x CUs. Grid-stride kernels
+// launched with exactly this many workgroups run as one full round — no partial last
+// round of workgroups (a 2048-block grid on a 7-block/CU kernel is 1.14 rounds: the
+// 0.14 tail costs as much as a whole round).
+inline int resident_blocks(const void* kernel, int threads, size_t smem) {
+  static std::mutex mu;
+  static std::map<std::tuple<const void*, int, size_t, int>, int> cache;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const auto key = std::make_tuple(kernel, threads, smem, dev);
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, smem) != hipSuccess || per_cu < 1)
+    per_cu = 1;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+  const int n = per_cu * cus;
+  cache.emplace(key, n);
+  return n;
+}
 
 #define FLUXMPI_HIP_CHECK(expr)                                                        \
   do {                                                                                 \

@@ -369,27 +369,54 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs p) {
   }
 }
 
-// out[e] = sum_s ws[s][e] (fp32 or bf16 out), 4 elements per lane per step
-template <typename TO>
-__global__ __launch_bounds__(kThreads) void splitk_reduce_kernel(const float* __restrict__ ws, int splits, int64_t n,
-                                                                 TO* __restrict__ out) {
+// Split-K reduction as a G-ary tree over the [splits][n] fp32 partials: level l sums
+// groups of G logical slices (slice i lives at ws + i*step*n) in parallel over
+// (element chunk, group) and writes each group's sum over its first slice (in place:
+// every lane reads and writes only its own elements); the last level (<= G slices)
+// writes the output dtype. Parallel over splits, so thousands of tiny partial slices
+// (small dW, huge K) reduce in a few microseconds.
+constexpr int kReduceGroup = 16;
+
+template <typename TO, bool FINAL>
+__global__ __launch_bounds__(kThreads) void splitk_reduce_kernel(float* __restrict__ ws, int cs, int64_t step,
+                                                                 int64_t n, TO* __restrict__ out) {
+  const int g = blockIdx.y;
+  const int i0 = g * kReduceGroup;
+  int cnt = cs - i0;
+  if (cnt > kReduceGroup) cnt = kReduceGroup;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads * 4;
   for (int64_t e = (static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x) * 4; e < n; e += stride) {
-    if ((n & 3) == 0 && e + 4 <= n) {  // 16 B aligned slices
-      float4 acc = *reinterpret_cast<const float4*>(ws + e);
-      for (int s = 1; s < splits; ++s) {
-        const float4 v = *reinterpret_cast<const float4*>(ws + s * n + e);
+    float* base = ws + static_cast<int64_t>(i0) * step * n;
+    if ((n & 3) == 0) {  // 16 B aligned slices: 4 independent loads per step
+      float4 acc = *reinterpret_cast<const float4*>(base + e);
+      int i = 1;
+      for (; i + 3 < cnt; i += 4) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(base + (i + u) * step * n + e);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+        }
+      }
+      for (; i < cnt; ++i) {
+        const float4 v = *reinterpret_cast<const float4*>(base + i * step * n + e);
         acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
       }
-      out[e] = static_cast<TO>(acc.x);
-      out[e + 1] = static_cast<TO>(acc.y);
-      out[e + 2] = static_cast<TO>(acc.z);
-      out[e + 3] = static_cast<TO>(acc.w);
+      if (FINAL) {
+        out[e] = static_cast<TO>(acc.x);
+        out[e + 1] = static_cast<TO>(acc.y);
+        out[e + 2] = static_cast<TO>(acc.z);
+        out[e + 3] = static_cast<TO>(acc.w);
+      } else {
+        *reinterpret_cast<float4*>(base + e) = acc;
+      }
     } else {
       for (int64_t k = e; k < e + 4 && k < n; ++k) {
         float a = 0.f;
-        for (int s = 0; s < splits; ++s) a += ws[s * n + k];
-        out[k] = static_cast<TO>(a);
+        for (int i = 0; i < cnt; ++i) a += base[i * step * n + k];
+        if (FINAL) out[k] = static_cast<TO>(a);
+        else base[k] = a;
       }
     }
   }
@@ -454,16 +481,32 @@ void gemm_bf16(const GemmProblem& g, hipStream_t stream) {
 #undef DISPATCH
 }
 
-void gemm_splitk_reduce(const float* ws, int splits, int64_t n, void* out, int out_dtype, hipStream_t stream) {
-  int64_t blocks = (n / 4 + kThreads - 1) / kThreads;
-  if (blocks > 4096) blocks = 4096;
-  if (blocks < 1) blocks = 1;
-  if (out_dtype == static_cast<int>(kF32))
-    splitk_reduce_kernel<float><<<(int)blocks, kThreads, 0, stream>>>(ws, splits, n, static_cast<float*>(out));
-  else if (out_dtype == static_cast<int>(kBF16))
-    splitk_reduce_kernel<bf16><<<(int)blocks, kThreads, 0, stream>>>(ws, splits, n, static_cast<bf16*>(out));
-  else
+void gemm_splitk_reduce(const float* ws_c, int splits, int64_t n, void* out, int out_dtype, hipStream_t stream) {
+  if (out_dtype != static_cast<int>(kF32) && out_dtype != static_cast<int>(kBF16))
     throw std::runtime_error("gemm_splitk_reduce: out dtype must be fp32 or bf16");
+  float* ws = const_cast<float*>(ws_c);  // intermediate tree levels are written in place
+  int64_t bx = (n / 4 + kThreads - 1) / kThreads;
+  int cs = splits < 1 ? 1 : splits;
+  int64_t step = 1;
+  while (cs > kReduceGroup) {
+    const int groups = (cs + kReduceGroup - 1) / kReduceGroup;
+    int64_t gx = bx;
+    // ~2048 workgroups per level in total
+    const int64_t cap = (2048 + groups - 1) / groups;
+    if (gx > cap) gx = cap;
+    if (gx < 1) gx = 1;
+    splitk_reduce_kernel<float, false><<<dim3((unsigned)gx, (unsigned)groups), kThreads, 0, stream>>>(
+        ws, cs, step, n, nullptr);
+    FLUXMPI_HIP_CHECK(hipGetLastError());
+    cs = groups;
+    step *= kReduceGroup;
+  }
+  int64_t gx = bx > 4096 ? 4096 : (bx < 1 ? 1 : bx);
+  if (out_dtype == static_cast<int>(kF32))
+    splitk_reduce_kernel<float, true><<<(unsigned)gx, kThreads, 0, stream>>>(ws, cs, step, n,
+                                                                             static_cast<float*>(out));
+  else
+    splitk_reduce_kernel<bf16, true><<<(unsigned)gx, kThreads, 0, stream>>>(ws, cs, step, n, static_cast<bf16*>(out));
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
 

@@ -75,13 +75,13 @@ def wgrad_splits(M: int, co: int, ci: int) -> int:
 
     Splits write fp32 partials with plain stores (a [splits, co, ci] workspace, then one
     reduce pass), so their cost is ~2 x splits x co*ci*4 bytes of streaming traffic: aim
-    at ~1024 workgroups for the 256 CUs, keep >= 256 pixels per split and the partial
+    at ~512 workgroups for the 256 CUs, keep >= 256 pixels per split and the partial
     traffic under half of the operand bytes.
     """
     tiles = max(1, (co + 127) // 128) * max(1, (ci + 127) // 128)
     in_bytes = M * (co + ci) * 2
     out_bytes = co * ci * 4
-    s_occ = -(-1024 // tiles)
+    s_occ = -(-512 // tiles)
     s_bw = max(1, in_bytes // (4 * out_bytes))
     return int(max(1, min(s_occ, s_bw, M // 256)))
 
