@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=int(os.environ.get("BENCH_BATCH", "256")), help="per-GPU batch")
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--image", type=int, default=224)
-    ap.add_argument("--conv", default=os.environ.get("BENCH_CONV", "miopen"), choices=["gemm", "miopen", "fused", "hybrid"])
+    ap.add_argument("--conv", default=os.environ.get("BENCH_CONV", "hybrid"), choices=["gemm", "miopen", "fused", "hybrid"])
     ap.add_argument("--norm", default=os.environ.get("BENCH_NORM", "fused"), choices=["torch", "fused"])
     ap.add_argument("--optimizer", default="adam", choices=["adam", "momentum"])
     ap.add_argument("--no-overlap", action="store_true")
