@@ -62,7 +62,7 @@ void mt_sgd(const std::vector<uintptr_t>& param, const std::vector<uintptr_t>& g
 void bn_fwd_train(const void* x, void* y, const void* residual, const float* weight,
                   const float* bias, float* running_mean, float* running_var, float* save_mean,
                   float* save_invstd, float* workspace, int64_t rows, int64_t C, float momentum,
-                  float eps, int relu, uint8_t* relu_mask, int dtype, hipStream_t stream);
+                  float eps, int relu, uint8_t* relu_mask, int dtype, hipStream_t stream, int64_t* num_batches_tracked = nullptr);
 // Backward: given dy (and y when relu, to mask), computes dx, dweight, dbias and
 // (when residual was fused) d_residual = masked dy.
 // y == nullptr with relu: the ReLU mask is recomputed from x (bit-identical to forward).
@@ -80,7 +80,7 @@ size_t bn_workspace_floats(int64_t rows, int64_t C);
 void bn_stats_finalize(const void* x, const float* w, const float* b, float* running_mean,
                        float* running_var, float* save_mean, float* save_invstd, float* scale,
                        float* shift, float* workspace, int64_t rows, int64_t C, float momentum,
-                       float eps, int stats_ready, int dtype, hipStream_t stream);
+                       float eps, int stats_ready, int dtype, hipStream_t stream, int64_t* num_batches_tracked = nullptr);
 void bn_apply(const void* x, void* y, const void* residual, const float* w, const float* b,
               const float* save_mean, const float* save_invstd, int64_t rows, int64_t C, int relu,
               uint8_t* relu_mask, int dtype, hipStream_t stream);

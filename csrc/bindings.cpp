@@ -66,12 +66,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_fwd_train",
         [](uintptr_t x, uintptr_t y, uintptr_t res, uintptr_t w, uintptr_t b, uintptr_t rm, uintptr_t rv,
            uintptr_t sm, uintptr_t si, uintptr_t ws, int64_t rows, int64_t C, float momentum, float eps, int relu,
-           uintptr_t mask, int dtype, uintptr_t stream) {
+           uintptr_t mask, int dtype, uintptr_t stream, uintptr_t nbt) {
           bn_fwd_train(reinterpret_cast<const void*>(x), reinterpret_cast<void*>(y), reinterpret_cast<const void*>(res),
                        reinterpret_cast<const float*>(w), reinterpret_cast<const float*>(b),
                        reinterpret_cast<float*>(rm), reinterpret_cast<float*>(rv), reinterpret_cast<float*>(sm),
                        reinterpret_cast<float*>(si), reinterpret_cast<float*>(ws), rows, C, momentum, eps, relu,
-                       reinterpret_cast<uint8_t*>(mask), dtype, S(stream));
+                       reinterpret_cast<uint8_t*>(mask), dtype, S(stream), reinterpret_cast<int64_t*>(nbt));
         });
   m.def("bn_fwd_infer",
         [](uintptr_t x, uintptr_t y, uintptr_t res, uintptr_t w, uintptr_t b, uintptr_t rm, uintptr_t rv,
@@ -97,12 +97,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_stats_finalize",
         [](uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t rm, uintptr_t rv, uintptr_t sm, uintptr_t si,
            uintptr_t scale, uintptr_t shift, uintptr_t ws, int64_t rows, int64_t C, float momentum, float eps,
-           int stats_ready, int dtype, uintptr_t stream) {
+           int stats_ready, int dtype, uintptr_t stream, uintptr_t nbt) {
           bn_stats_finalize(reinterpret_cast<const void*>(x), reinterpret_cast<const float*>(w),
                             reinterpret_cast<const float*>(b), reinterpret_cast<float*>(rm),
                             reinterpret_cast<float*>(rv), reinterpret_cast<float*>(sm), reinterpret_cast<float*>(si),
                             reinterpret_cast<float*>(scale), reinterpret_cast<float*>(shift),
-                            reinterpret_cast<float*>(ws), rows, C, momentum, eps, stats_ready, dtype, S(stream));
+                            reinterpret_cast<float*>(ws), rows, C, momentum, eps, stats_ready, dtype, S(stream),
+                            reinterpret_cast<int64_t*>(nbt));
         });
   m.def("bn_apply",
         [](uintptr_t x, uintptr_t y, uintptr_t res, uintptr_t w, uintptr_t b, uintptr_t sm, uintptr_t si,

@@ -128,8 +128,10 @@ __global__ void bn_finalize_fwd_kernel(float* __restrict__ acc, int C, int64_t r
                                        float* __restrict__ smean, float* __restrict__ sinv,
                                        float* __restrict__ rmean, float* __restrict__ rvar,
                                        const float* __restrict__ w, const float* __restrict__ b,
-                                       float* __restrict__ scale, float* __restrict__ shift) {
+                                       float* __restrict__ scale, float* __restrict__ shift,
+                                       int64_t* __restrict__ nbt) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (nbt != nullptr && c == 0) *nbt += 1;  // BatchNorm's num_batches_tracked, without a launch of its own
   if (c >= C) return;
   float s, q;
   take_shards(acc, C, c, s, q);
@@ -519,12 +521,12 @@ void norm_t(const void* x, void* y, const void* res, const float* w, const float
 template <typename T>
 void fwd_train_t(const void* x, void* y, const void* res, const float* w, const float* b, float* rm, float* rv,
                  float* sm, float* si, float* ws, int64_t rows, int64_t C, float momentum, float eps, int relu,
-                 uint8_t* mask, hipStream_t s) {
+                 uint8_t* mask, int64_t* nbt, hipStream_t s) {
   const Geo g = reduce_geometry(reinterpret_cast<const void*>(bn_stats_kernel<T>), rows, C);
   bn_stats_kernel<T><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(static_cast<const T*>(x), rows, (int)C, g, ws);
   FLUXMPI_HIP_CHECK(hipGetLastError());
   bn_finalize_fwd_kernel<<<(int)((C + 255) / 256), 256, 0, s>>>(ws, (int)C, rows, momentum, eps, sm, si, rm, rv,
-                                                                 nullptr, nullptr, nullptr, nullptr);
+                                                                 nullptr, nullptr, nullptr, nullptr, nbt);
   FLUXMPI_HIP_CHECK(hipGetLastError());
   norm_t<T>(x, y, res, w, b, sm, si, rows, C, eps, 1, relu, mask, s);
 }
@@ -588,22 +590,22 @@ size_t bn_workspace_floats(int64_t rows, int64_t C) {
 void bn_fwd_train(const void* x, void* y, const void* residual, const float* weight, const float* bias,
                   float* running_mean, float* running_var, float* save_mean, float* save_invstd, float* workspace,
                   int64_t rows, int64_t C, float momentum, float eps, int relu, uint8_t* relu_mask, int dtype,
-                  hipStream_t stream) {
+                  hipStream_t stream, int64_t* nbt) {
   check(C);
   switch (dtype) {
     case kBF16: fwd_train_t<bf16>(x, y, residual, weight, bias, running_mean, running_var, save_mean, save_invstd,
-                                  workspace, rows, C, momentum, eps, relu, relu_mask, stream); break;
+                                  workspace, rows, C, momentum, eps, relu, relu_mask, nbt, stream); break;
     case kF16: fwd_train_t<f16>(x, y, residual, weight, bias, running_mean, running_var, save_mean, save_invstd,
-                                workspace, rows, C, momentum, eps, relu, relu_mask, stream); break;
+                                workspace, rows, C, momentum, eps, relu, relu_mask, nbt, stream); break;
     case kF32: fwd_train_t<float>(x, y, residual, weight, bias, running_mean, running_var, save_mean, save_invstd,
-                                  workspace, rows, C, momentum, eps, relu, relu_mask, stream); break;
+                                  workspace, rows, C, momentum, eps, relu, relu_mask, nbt, stream); break;
     default: throw std::runtime_error("fused batchnorm: unsupported dtype");
   }
 }
 
 void bn_stats_finalize(const void* x, const float* w, const float* b, float* rm, float* rv, float* sm, float* si,
                        float* scale, float* shift, float* ws, int64_t rows, int64_t C, float momentum, float eps,
-                       int stats_ready, int dtype, hipStream_t s) {
+                       int stats_ready, int dtype, hipStream_t s, int64_t* nbt) {
   check(C);
   if (!stats_ready) {
 #define STATS(T)                                                                                              \
@@ -621,7 +623,7 @@ void bn_stats_finalize(const void* x, const float* w, const float* b, float* rm,
     FLUXMPI_HIP_CHECK(hipGetLastError());
   }
   bn_finalize_fwd_kernel<<<(int)((C + 255) / 256), 256, 0, s>>>(ws, (int)C, rows, momentum, eps, sm, si, rm, rv, w, b,
-                                                                 scale, shift);
+                                                                 scale, shift, nbt);
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
 

@@ -85,9 +85,22 @@ class GradLink:
         return g
 
 
+def bn_counter(bn):
+    """(momentum, counter) for a training-mode BatchNorm module: the ``num_batches_tracked``
+    tensor the finalize kernel increments (no launch of its own), or None when nothing is
+    tracked / the cumulative average (momentum None) needs the host-side count now."""
+    if not (bn.training and bn.track_running_stats):
+        return (0.1 if bn.momentum is None else bn.momentum), None
+    if bn.momentum is None:
+        bn.num_batches_tracked.add_(1)
+        return 1.0 / float(bn.num_batches_tracked), None
+    return bn.momentum, bn.num_batches_tracked
+
+
 class _FusedBN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, running_mean, running_var, momentum, eps, relu, link=None):
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, momentum, eps, relu, link=None,
+                nbt=None):
         C = _ext.get(required=True)
         x = _nhwc(x)
         res = _nhwc(residual) if residual is not None else None
@@ -107,7 +120,8 @@ class _FusedBN(torch.autograd.Function):
                        running_mean.data_ptr() if running_mean is not None else 0,
                        running_var.data_ptr() if running_var is not None else 0,
                        save_mean.data_ptr(), save_inv.data_ptr(), ws.data_ptr(), rows, ch, float(momentum),
-                       float(eps), int(relu), mask.data_ptr() if mask is not None else 0, DTYPE_CODE[x.dtype], stream)
+                       float(eps), int(relu), mask.data_ptr() if mask is not None else 0, DTYPE_CODE[x.dtype], stream,
+                       nbt.data_ptr() if nbt is not None else 0)
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.link = link if residual is not None else None
@@ -147,7 +161,7 @@ class _FusedBN(torch.autograd.Function):
             db = db.to(ctx.wdtype)
         if ctx.link is not None:
             ctx.link.grad, dres = dres, None
-        return dx, dw, db, dres, None, None, None, None, None, None
+        return dx, dw, db, dres, None, None, None, None, None, None, None
 
 
 def batch_norm_reference(x, weight, bias, running_mean, running_var, training, momentum, eps, relu=False,
@@ -163,11 +177,16 @@ def batch_norm_reference(x, weight, bias, running_mean, running_var, training, m
 
 
 def fused_batch_norm(x, weight, bias, running_mean, running_var, training=True, momentum=0.1, eps=1e-5,
-                     relu=False, residual=None, link: GradLink | None = None):
+                     relu=False, residual=None, link: GradLink | None = None,
+                     num_batches_tracked: torch.Tensor | None = None):
     """``link``: deliver the residual's gradient through a :class:`GradLink` instead of
-    returning it to autograd (training with the fused kernels only; otherwise ignored)."""
+    returning it to autograd (training with the fused kernels only; otherwise ignored).
+    ``num_batches_tracked``: counter incremented once (inside the finalize kernel)."""
     if training and kernel_supported(x):
-        return _FusedBN.apply(x, weight, bias, residual, running_mean, running_var, momentum, eps, relu, link)
+        return _FusedBN.apply(x, weight, bias, residual, running_mean, running_var, momentum, eps, relu, link,
+                              num_batches_tracked)
+    if num_batches_tracked is not None and training:
+        num_batches_tracked.add_(1)
     if (not training) and kernel_supported(x) and not torch.is_grad_enabled():
         C = _ext.get(required=True)
         x = _nhwc(x)
@@ -187,11 +206,9 @@ class FusedBatchNorm2d(nn.BatchNorm2d):
     """``nn.BatchNorm2d`` with optional fused ReLU / residual add (NHWC HIP kernels on GPU)."""
 
     def forward(self, x, relu: bool = False, residual: torch.Tensor | None = None, link: GradLink | None = None):
-        if self.training and self.track_running_stats:
-            self.num_batches_tracked.add_(1)
-        mom = 0.1 if self.momentum is None else self.momentum
+        mom, nbt = bn_counter(self)
         use_batch = self.training or not self.track_running_stats
         return fused_batch_norm(x, self.weight, self.bias,
                                 self.running_mean if self.track_running_stats else None,
                                 self.running_var if self.track_running_stats else None,
-                                use_batch, mom, self.eps, relu, residual, link)
+                                use_batch, mom, self.eps, relu, residual, link, nbt)

@@ -29,7 +29,7 @@ from __future__ import annotations
 import torch
 
 from . import _ext
-from .batchnorm import GradLink, _workspace  # noqa: F401 (GradLink re-exported)
+from .batchnorm import GradLink, _workspace, bn_counter  # noqa: F401 (GradLink re-exported)
 from .gemm import conv1x1_dgrad, conv1x1_wgrad, gemm
 from .multi_tensor import DTYPE_CODE
 
@@ -137,7 +137,7 @@ class _BNFromStats(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, momentum, eps, relu, stats_ready,
-                link=None):
+                link=None, nbt=None):
         C = _ext.get(required=True)
         ch = x.shape[1]
         rows = x.numel() // ch
@@ -148,7 +148,7 @@ class _BNFromStats(torch.autograd.Function):
         ws = _workspace(x)
         C.bn_stats_finalize(x.data_ptr(), w32.data_ptr(), b32.data_ptr(), _p(running_mean), _p(running_var),
                             mean.data_ptr(), inv.data_ptr(), 0, 0, ws.data_ptr(), rows, ch, float(momentum),
-                            float(eps), int(stats_ready), DTYPE_CODE[x.dtype], _stream(x))
+                            float(eps), int(stats_ready), DTYPE_CODE[x.dtype], _stream(x), _p(nbt))
         res = None
         if residual is not None:
             res = residual if residual.is_contiguous(memory_format=torch.channels_last) else \
@@ -171,7 +171,7 @@ class _BNFromStats(torch.autograd.Function):
         dx, dres, dw, db = _bn_bwd(dy, x, mask, w32, b32, mean, inv, ctx.relu, ctx.has_res)
         if ctx.link is not None:
             ctx.link.grad, dres = dres, None
-        return dx, dw.to(ctx.wdtype), db.to(ctx.wdtype), dres, None, None, None, None, None, None, None
+        return dx, dw.to(ctx.wdtype), db.to(ctx.wdtype), dres, None, None, None, None, None, None, None, None
 
 
 class _BNReluConv1x1(torch.autograd.Function):
@@ -179,7 +179,7 @@ class _BNReluConv1x1(torch.autograd.Function):
     go to the workspace (consumed by the next ``bn_from_stats``)."""
 
     @staticmethod
-    def forward(ctx, c2, bn_weight, bn_bias, running_mean, running_var, weight, momentum, eps):
+    def forward(ctx, c2, bn_weight, bn_bias, running_mean, running_var, weight, momentum, eps, nbt=None):
         C = _ext.get(required=True)
         if not c2.is_contiguous(memory_format=torch.channels_last):
             c2 = c2.contiguous(memory_format=torch.channels_last)
@@ -193,7 +193,7 @@ class _BNReluConv1x1(torch.autograd.Function):
         ws = _workspace(c2)
         C.bn_stats_finalize(c2.data_ptr(), w32.data_ptr(), b32.data_ptr(), _p(running_mean), _p(running_var),
                             mean.data_ptr(), inv.data_ptr(), scale.data_ptr(), shift.data_ptr(), ws.data_ptr(),
-                            rows, ch, float(momentum), float(eps), 0, DTYPE_CODE[c2.dtype], _stream(c2))
+                            rows, ch, float(momentum), float(eps), 0, DTYPE_CODE[c2.dtype], _stream(c2), _p(nbt))
         co = weight.shape[0]
         c3 = _empty_nhwc(n, co, h, w, c2)
         gemm(_nhwc2d(c2), weight.reshape(co, ch), c3, M=rows, N=co, K=ch, lda=ch, ldb=ch, ldc=co, a_kmajor=True,
@@ -214,7 +214,7 @@ class _BNReluConv1x1(torch.autograd.Function):
         # d(relu(bn(c2))) = dc3 @ W, then the BN backward with the ReLU mask recomputed from c2
         da = conv1x1_dgrad(dc3_2d, weight.reshape(co, ch)).view(n, h, w, ch).permute(0, 3, 1, 2)
         dc2, _, dbw, dbb = _bn_bwd(da, c2, None, w32, b32, mean, inv, True, False)
-        return dc2, dbw.to(ctx.bn_wdtype), dbb.to(ctx.bn_wdtype), None, None, dw, None, None
+        return dc2, dbw.to(ctx.bn_wdtype), dbb.to(ctx.bn_wdtype), None, None, dw, None, None, None
 
 
 def conv1x1_stats(x, weight, link=None):
@@ -226,18 +226,14 @@ def conv1x1_hybrid(x, weight, link=None):
 
 
 def bn_from_stats(x, bn, relu=False, residual=None, stats_ready=True, link=None):
-    if bn.training and bn.track_running_stats:
-        bn.num_batches_tracked.add_(1)
-    mom = 0.1 if bn.momentum is None else bn.momentum
+    mom, nbt = bn_counter(bn)
     return _BNFromStats.apply(x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, mom, bn.eps, relu,
-                              stats_ready, link)
+                              stats_ready, link, nbt)
 
 
 def bn_relu_conv1x1(c2, bn, weight):
-    if bn.training and bn.track_running_stats:
-        bn.num_batches_tracked.add_(1)
-    mom = 0.1 if bn.momentum is None else bn.momentum
-    return _BNReluConv1x1.apply(c2, bn.weight, bn.bias, bn.running_mean, bn.running_var, weight, mom, bn.eps)
+    mom, nbt = bn_counter(bn)
+    return _BNReluConv1x1.apply(c2, bn.weight, bn.bias, bn.running_mean, bn.running_var, weight, mom, bn.eps, nbt)
 
 
 def supported(x: torch.Tensor, *channels: int) -> bool:

@@ -28,7 +28,7 @@ def _out(n, k, s, p):
 
 class _BNReluMaxPool(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, k, s, p):
+    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, k, s, p, nbt=None):
         C = _ext.get(required=True)
         if not x.is_contiguous(memory_format=torch.channels_last):
             x = x.contiguous(memory_format=torch.channels_last)
@@ -41,7 +41,7 @@ class _BNReluMaxPool(torch.autograd.Function):
         ws = _workspace(x)
         C.bn_stats_finalize(x.data_ptr(), w32.data_ptr(), b32.data_ptr(), _p(running_mean), _p(running_var),
                             mean.data_ptr(), inv.data_ptr(), scale.data_ptr(), shift.data_ptr(), ws.data_ptr(), rows,
-                            ch, float(momentum), float(eps), 0, DTYPE_CODE[x.dtype], _stream(x))
+                            ch, float(momentum), float(eps), 0, DTYPE_CODE[x.dtype], _stream(x), _p(nbt))
         oh, ow = _out(h, k, s, p), _out(w, k, s, p)
         y = _empty_nhwc(n, ch, oh, ow, x)
         idx = torch.empty(n * oh * ow * ch, device=x.device, dtype=torch.uint8)
@@ -67,7 +67,7 @@ class _BNReluMaxPool(torch.autograd.Function):
         dx, _, dw, db = _bn_bwd(dz, x, None, w32, b32, mean, inv, False, False)
         has_w, has_b = ctx.has_affine
         return (dx, dw.to(ctx.wdtype) if has_w else None, db.to(ctx.wdtype) if has_b else None,
-                None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None)
 
 
 def supported(x: torch.Tensor) -> bool:
@@ -77,10 +77,11 @@ def supported(x: torch.Tensor) -> bool:
 
 def bn_relu_maxpool(x: torch.Tensor, bn, k: int = 3, s: int = 2, p: int = 1) -> torch.Tensor:
     """``max_pool2d(relu(bn(x)), k, s, p)`` for a training-mode BatchNorm module ``bn``."""
-    if bn.training and bn.track_running_stats:
-        bn.num_batches_tracked.add_(1)
-    mom = 0.1 if bn.momentum is None else bn.momentum
+    from .batchnorm import bn_counter
+    mom, nbt = bn_counter(bn)
     if not (bn.training and supported(x)):
+        if nbt is not None:
+            nbt.add_(1)
         y = F.batch_norm(x.float(), bn.running_mean, bn.running_var,
                          bn.weight.float() if bn.weight is not None else None,
                          bn.bias.float() if bn.bias is not None else None,
@@ -88,7 +89,7 @@ def bn_relu_maxpool(x: torch.Tensor, bn, k: int = 3, s: int = 2, p: int = 1) -> 
         return F.max_pool2d(F.relu(y), k, s, p).to(x.dtype)
     rm = bn.running_mean if bn.track_running_stats else None
     rv = bn.running_var if bn.track_running_stats else None
-    return _BNReluMaxPool.apply(x, bn.weight, bn.bias, rm, rv, mom, bn.eps, k, s, p)
+    return _BNReluMaxPool.apply(x, bn.weight, bn.bias, rm, rv, mom, bn.eps, k, s, p, nbt)
 
 
 __all__ = ["bn_relu_maxpool"]

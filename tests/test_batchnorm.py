@@ -128,6 +128,7 @@ def test_bn_relu_maxpool_vs_reference(gpu_ext, shape, k, s, p):
     torch.testing.assert_close(y.float(), yr, rtol=2e-2, atol=2e-2)
     torch.testing.assert_close(bn.running_mean, ref_bn.running_mean, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(bn.running_var, ref_bn.running_var, rtol=1e-3, atol=1e-4)
+    assert int(bn.num_batches_tracked) == int(ref_bn.num_batches_tracked) == 1
     g = torch.randn_like(yr)
     (y.float() * g).sum().backward()
     (yr * g).sum().backward()
