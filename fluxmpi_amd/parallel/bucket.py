@@ -4,9 +4,10 @@ The reference issues one collective per leaf (``src/optimizer.jl:21,53``,
 ``src/synchronize.jl:16``), each staged through host memory. For ResNet-50
 that is ~161 allreduces of 1 element .. 2.4 M elements per step. Here leaves
 are grouped by (device, dtype), packed by one multi-tensor HIP launch into
-64 B-aligned flat buckets (``FLUXMPI_BUCKET_MB``, default 64 MiB: on xGMI a
-ring allreduce is per-link bandwidth bound, so fewer, larger messages
-amortise the ~10-30 µs per-collective latency), reduced on the comm stream
+64 B-aligned flat buckets (``FLUXMPI_BUCKET_MB``, default 16 MiB: on xGMI a
+ring allreduce is per-link bandwidth bound, so messages of MBs amortise the
+~10-30 µs per-collective latency; the DDP engine's overlap wants them no
+larger, see ``ddp.py``), reduced on the comm stream
 while the next bucket is packed, and unpacked after the stream-side wait.
 
 Leaves larger than half a bucket that are already contiguous skip the

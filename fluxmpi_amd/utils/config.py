@@ -21,8 +21,8 @@ Environment knobs (all optional):
 ``FLUXMPI_BACKEND``        ``auto`` (default) | ``rccl`` (native C++ RCCL
                            communicator) | ``torch`` (torch.distributed
                            ProcessGroup) | ``gloo`` (CPU)
-``FLUXMPI_BUCKET_MB``      gradient bucket size in MiB (default 64)
-``FLUXMPI_FIRST_BUCKET_MB`` size of the first (last-layer) bucket (default 8)
+``FLUXMPI_BUCKET_MB``      gradient bucket size in MiB (default 16)
+``FLUXMPI_FIRST_BUCKET_MB`` size of the first (last-layer) bucket (default 4)
 ``FLUXMPI_COMM_DTYPE``     ``native`` | ``fp32`` | ``bf16`` grad comm dtype
 ``FLUXMPI_OVERLAP``        ``1`` (default) overlap allreduce with backward
 ``FLUXMPI_PROFILE``        ``1`` emit roctx ranges + per-step timers
@@ -129,8 +129,8 @@ def _env_float(name: str, default: float) -> float:
 class Config:
     backend: str = "auto"
     host_staged: bool = False  # reference's CUDA-unaware path (Q1), debug only
-    bucket_mb: float = 64.0
-    first_bucket_mb: float = 8.0
+    bucket_mb: float = 16.0
+    first_bucket_mb: float = 4.0
     comm_dtype: str = "native"
     overlap: bool = True
     profile: bool = False
@@ -150,8 +150,8 @@ class Config:
         return cls(
             backend=os.environ.get("FLUXMPI_BACKEND", prefs.get("backend", "auto")).lower(),
             host_staged=bool(prefs.get(PREF_DISABLE_KEY, False)),
-            bucket_mb=_env_float("FLUXMPI_BUCKET_MB", float(prefs.get("bucket_mb", 64.0))),
-            first_bucket_mb=_env_float("FLUXMPI_FIRST_BUCKET_MB", float(prefs.get("first_bucket_mb", 8.0))),
+            bucket_mb=_env_float("FLUXMPI_BUCKET_MB", float(prefs.get("bucket_mb", 16.0))),
+            first_bucket_mb=_env_float("FLUXMPI_FIRST_BUCKET_MB", float(prefs.get("first_bucket_mb", 4.0))),
             comm_dtype=os.environ.get("FLUXMPI_COMM_DTYPE", prefs.get("comm_dtype", "native")).lower(),
             overlap=_env_bool("FLUXMPI_OVERLAP", bool(prefs.get("overlap", True))),
             profile=_env_bool("FLUXMPI_PROFILE", False),
