@@ -91,7 +91,10 @@ __global__ __launch_bounds__(kThreads) void bn_relu_maxpool_fwd_kernel(const T* 
   }
 }
 
-template <typename T>
+// NW = max windows covering one input position per dimension (ceil(K/S)): the candidate
+// windows are visited in a fixed, fully unrolled NW x NW pattern and all of their index
+// and gradient loads are issued before any is consumed (no load -> compare -> load chains).
+template <typename T, int NW>
 __global__ __launch_bounds__(kThreads) void maxpool_bwd_gather_kernel(const T* __restrict__ dy,
                                                                       const uint8_t* __restrict__ idx,
                                                                       T* __restrict__ dx, PoolGeo g, int64_t nvec) {
@@ -113,29 +116,38 @@ __global__ __launch_bounds__(kThreads) void maxpool_bwd_gather_kernel(const T* _
     ow_lo = ow_lo <= 0 ? 0 : (ow_lo + g.S - 1) / g.S;
     int64_t ow_hi = (w + g.P) / g.S;
     if (ow_hi > g.OW - 1) ow_hi = g.OW - 1;
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int64_t oh = oh_lo; oh <= oh_hi; ++oh) {
-      const int kh = static_cast<int>(h - (oh * g.S - g.P));
-      for (int64_t ow = ow_lo; ow <= ow_hi; ++ow) {
-        const int k = kh * g.K + static_cast<int>(w - (ow * g.S - g.P));
-        const int64_t o = ((n * g.OH + oh) * g.OW + ow) * g.C + c8 * 8;
-        const uint2 packed = *reinterpret_cast<const uint2*>(idx + o);
-        uint8_t a8[8];
-        __builtin_memcpy(a8, &packed, 8);
-        bool any = false;
+    uint2 ix[NW][NW];
+    T d[NW][NW][8];
+    int kk[NW][NW];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) any |= a8[j] == k;
-        if (!any) continue;
-        T d[8];
-        load8(dy + o, d);
+    for (int i = 0; i < NW; ++i)
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (a8[j] == k) acc[j] += static_cast<float>(d[j]);
+      for (int j = 0; j < NW; ++j) {
+        const int64_t oh = oh_lo + i, ow = ow_lo + j;
+        const bool ok = oh <= oh_hi && ow <= ow_hi;
+        kk[i][j] = ok ? static_cast<int>((h - (oh * g.S - g.P)) * g.K + (w - (ow * g.S - g.P))) : -1;
+        if (ok) {
+          const int64_t o = ((n * g.OH + oh) * g.OW + ow) * g.C + c8 * 8;
+          ix[i][j] = *reinterpret_cast<const uint2*>(idx + o);
+          load8(dy + o, d[i][j]);
+        } else {
+          ix[i][j] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+        }
       }
-    }
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < NW; ++i)
+#pragma unroll
+      for (int j = 0; j < NW; ++j) {
+        uint8_t a8[8];
+        __builtin_memcpy(a8, &ix[i][j], 8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (static_cast<int>(a8[e]) == kk[i][j]) acc[e] += static_cast<float>(d[i][j][e]);
+      }
     T out[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) out[j] = static_cast<T>(acc[j]);
+    for (int e = 0; e < 8; ++e) out[e] = static_cast<T>(acc[e]);
     store8(dx + v * 8, out);
   }
 }
@@ -187,22 +199,25 @@ void maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, int64_t N, int64_
   const PoolGeo g = make_geo(N, H, W, C, K, S, P);
   const int64_t nvec = N * H * W * C / 8;
   const int nb = grid_for(nvec);
-  switch (dtype) {
-    case kBF16:
-      maxpool_bwd_gather_kernel<bf16><<<nb, kThreads, 0, s>>>(static_cast<const bf16*>(dy), idx,
-                                                              static_cast<bf16*>(dx), g, nvec);
-      break;
-    case kF16:
-      maxpool_bwd_gather_kernel<f16><<<nb, kThreads, 0, s>>>(static_cast<const f16*>(dy), idx,
-                                                             static_cast<f16*>(dx), g, nvec);
-      break;
-    case kF32:
-      maxpool_bwd_gather_kernel<float><<<nb, kThreads, 0, s>>>(static_cast<const float*>(dy), idx,
-                                                               static_cast<float*>(dx), g, nvec);
-      break;
-    default:
-      throw std::runtime_error("maxpool_bwd: unsupported dtype");
+  const int nw = (K + S - 1) / S;
+#define POOL_BWD(T, NW)                                                                                         \
+  maxpool_bwd_gather_kernel<T, NW><<<nb, kThreads, 0, s>>>(static_cast<const T*>(dy), idx, static_cast<T*>(dx), \
+                                                           g, nvec)
+#define POOL_BWD_NW(T)                              \
+  {                                                 \
+    if (nw == 1) POOL_BWD(T, 1);                    \
+    else if (nw == 2) POOL_BWD(T, 2);               \
+    else if (nw == 3) POOL_BWD(T, 3);               \
+    else throw std::runtime_error("maxpool_bwd: ceil(K/S) > 3 unsupported"); \
   }
+  switch (dtype) {
+    case kBF16: POOL_BWD_NW(bf16) break;
+    case kF16: POOL_BWD_NW(f16) break;
+    case kF32: POOL_BWD_NW(float) break;
+    default: throw std::runtime_error("maxpool_bwd: unsupported dtype");
+  }
+#undef POOL_BWD_NW
+#undef POOL_BWD
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
 
