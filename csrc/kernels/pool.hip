@@ -30,22 +30,25 @@ struct PoolGeo {
   int K, S, P;
 };
 
+// One workgroup per output row (n, oh); lanes walk (ow, channel vector) of the row with
+// 32-bit index math (64-bit division per element made the first version ALU-bound).
 template <typename T>
 __global__ __launch_bounds__(kThreads) void bn_relu_maxpool_fwd_kernel(const T* __restrict__ x,
                                                                        const float* __restrict__ scale,
                                                                        const float* __restrict__ shift,
                                                                        T* __restrict__ y, uint8_t* __restrict__ idx,
-                                                                       PoolGeo g, int64_t nvec) {
+                                                                       PoolGeo g) {
   const int cv = static_cast<int>(g.C / 8);
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
-  for (int64_t v = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; v < nvec; v += stride) {
-    const int c8 = static_cast<int>(v % cv);
-    int64_t pix = v / cv;  // (n, oh, ow)
-    const int64_t ow = pix % g.OW;
-    pix /= g.OW;
-    const int64_t oh = pix % g.OH;
-    const int64_t n = pix / g.OH;
+  const int row = blockIdx.x;  // n * OH + oh
+  const int oh = row % static_cast<int>(g.OH);
+  const int64_t n = row / static_cast<int>(g.OH);
+  const int h0 = oh * g.S - g.P;
+  const int per_row = static_cast<int>(g.OW) * cv;
+  const T* xn = x + n * g.H * g.W * g.C;
+  for (int t = threadIdx.x; t < per_row; t += kThreads) {
+    const int ow = t / cv, c8 = t - ow * cv;
     const int c0 = c8 * 8;
+    const int w0 = ow * g.S - g.P;
     float sc[8], sh[8], best[8];
     int arg[8];
 #pragma unroll
@@ -55,15 +58,14 @@ __global__ __launch_bounds__(kThreads) void bn_relu_maxpool_fwd_kernel(const T* 
       best[j] = -INFINITY;
       arg[j] = 0;
     }
-    const int64_t h0 = oh * g.S - g.P, w0 = ow * g.S - g.P;
     for (int kh = 0; kh < g.K; ++kh) {
-      const int64_t h = h0 + kh;
+      const int h = h0 + kh;
       if (h < 0 || h >= g.H) continue;
       for (int kw = 0; kw < g.K; ++kw) {
-        const int64_t w = w0 + kw;
+        const int w = w0 + kw;
         if (w < 0 || w >= g.W) continue;
         T raw[8];
-        load8(x + ((n * g.H + h) * g.W + w) * g.C + c0, raw);
+        load8(xn + (static_cast<int64_t>(h) * g.W + w) * g.C + c0, raw);
         const int k = kh * g.K + kw;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -84,10 +86,11 @@ __global__ __launch_bounds__(kThreads) void bn_relu_maxpool_fwd_kernel(const T* 
       out[j] = static_cast<T>(pos ? best[j] : 0.f);
       a8[j] = pos ? static_cast<uint8_t>(arg[j]) : static_cast<uint8_t>(0xFF);
     }
-    store8(y + v * 8, out);
+    const int64_t o = static_cast<int64_t>(row) * per_row * 8 + static_cast<int64_t>(t) * 8;
+    store8(y + o, out);
     uint2 packed;
     __builtin_memcpy(&packed, a8, 8);
-    *reinterpret_cast<uint2*>(idx + v * 8) = packed;
+    *reinterpret_cast<uint2*>(idx + o) = packed;
   }
 }
 
@@ -97,25 +100,24 @@ __global__ __launch_bounds__(kThreads) void bn_relu_maxpool_fwd_kernel(const T* 
 template <typename T, int NW>
 __global__ __launch_bounds__(kThreads) void maxpool_bwd_gather_kernel(const T* __restrict__ dy,
                                                                       const uint8_t* __restrict__ idx,
-                                                                      T* __restrict__ dx, PoolGeo g, int64_t nvec) {
+                                                                      T* __restrict__ dx, PoolGeo g) {
   const int cv = static_cast<int>(g.C / 8);
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
-  for (int64_t v = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; v < nvec; v += stride) {
-    const int c8 = static_cast<int>(v % cv);
-    int64_t pix = v / cv;  // (n, h, w) of the input
-    const int64_t w = pix % g.W;
-    pix /= g.W;
-    const int64_t h = pix % g.H;
-    const int64_t n = pix / g.H;
-    // windows oh with oh*S - P <= h <= oh*S - P + K - 1
-    int64_t oh_lo = h + g.P - g.K + 1;
-    oh_lo = oh_lo <= 0 ? 0 : (oh_lo + g.S - 1) / g.S;
-    int64_t oh_hi = (h + g.P) / g.S;
-    if (oh_hi > g.OH - 1) oh_hi = g.OH - 1;
-    int64_t ow_lo = w + g.P - g.K + 1;
+  const int row = blockIdx.x;  // n * H + h of the input
+  const int h = row % static_cast<int>(g.H);
+  const int64_t n = row / static_cast<int>(g.H);
+  // windows oh with oh*S - P <= h <= oh*S - P + K - 1
+  int oh_lo = h + g.P - g.K + 1;
+  oh_lo = oh_lo <= 0 ? 0 : (oh_lo + g.S - 1) / g.S;
+  int oh_hi = (h + g.P) / g.S;
+  if (oh_hi > g.OH - 1) oh_hi = static_cast<int>(g.OH) - 1;
+  const int per_row = static_cast<int>(g.W) * cv;
+  const int64_t obase = n * g.OH * g.OW * g.C;
+  for (int t = threadIdx.x; t < per_row; t += kThreads) {
+    const int w = t / cv, c8 = t - w * cv;
+    int ow_lo = w + g.P - g.K + 1;
     ow_lo = ow_lo <= 0 ? 0 : (ow_lo + g.S - 1) / g.S;
-    int64_t ow_hi = (w + g.P) / g.S;
-    if (ow_hi > g.OW - 1) ow_hi = g.OW - 1;
+    int ow_hi = (w + g.P) / g.S;
+    if (ow_hi > g.OW - 1) ow_hi = static_cast<int>(g.OW) - 1;
     uint2 ix[NW][NW];
     T d[NW][NW][8];
     int kk[NW][NW];
@@ -123,11 +125,11 @@ __global__ __launch_bounds__(kThreads) void maxpool_bwd_gather_kernel(const T* _
     for (int i = 0; i < NW; ++i)
 #pragma unroll
       for (int j = 0; j < NW; ++j) {
-        const int64_t oh = oh_lo + i, ow = ow_lo + j;
+        const int oh = oh_lo + i, ow = ow_lo + j;
         const bool ok = oh <= oh_hi && ow <= ow_hi;
-        kk[i][j] = ok ? static_cast<int>((h - (oh * g.S - g.P)) * g.K + (w - (ow * g.S - g.P))) : -1;
+        kk[i][j] = ok ? (h - (oh * g.S - g.P)) * g.K + (w - (ow * g.S - g.P)) : -1;
         if (ok) {
-          const int64_t o = ((n * g.OH + oh) * g.OW + ow) * g.C + c8 * 8;
+          const int64_t o = obase + (static_cast<int64_t>(oh) * g.OW + ow) * g.C + c8 * 8;
           ix[i][j] = *reinterpret_cast<const uint2*>(idx + o);
           load8(dy + o, d[i][j]);
         } else {
@@ -148,15 +150,8 @@ __global__ __launch_bounds__(kThreads) void maxpool_bwd_gather_kernel(const T* _
     T out[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) out[e] = static_cast<T>(acc[e]);
-    store8(dx + v * 8, out);
+    store8(dx + static_cast<int64_t>(row) * per_row * 8 + static_cast<int64_t>(t) * 8, out);
   }
-}
-
-int grid_for(int64_t nvec) {
-  int64_t b = (nvec + kThreads - 1) / kThreads;
-  if (b > 8192) b = 8192;
-  if (b < 1) b = 1;
-  return static_cast<int>(b);
 }
 
 PoolGeo make_geo(int64_t N, int64_t H, int64_t W, int64_t C, int K, int S, int P) {
@@ -165,6 +160,8 @@ PoolGeo make_geo(int64_t N, int64_t H, int64_t W, int64_t C, int K, int S, int P
     throw std::runtime_error("maxpool: need 1 <= K, K*K <= 255, S >= 1, 0 <= P < K");
   PoolGeo g{N, H, W, C, (H + 2 * P - K) / S + 1, (W + 2 * P - K) / S + 1, K, S, P};
   if (g.OH < 1 || g.OW < 1) throw std::runtime_error("maxpool: empty output");
+  if (N * H >= (int64_t(1) << 31) || W * (C / 8) >= (int64_t(1) << 31))
+    throw std::runtime_error("maxpool: tensor too large for the row-per-workgroup grid");
   return g;
 }
 
@@ -173,20 +170,19 @@ PoolGeo make_geo(int64_t N, int64_t H, int64_t W, int64_t C, int K, int S, int P
 void bn_relu_maxpool_fwd(const void* x, const float* scale, const float* shift, void* y, uint8_t* idx, int64_t N,
                          int64_t H, int64_t W, int64_t C, int K, int S, int P, int dtype, hipStream_t s) {
   const PoolGeo g = make_geo(N, H, W, C, K, S, P);
-  const int64_t nvec = N * g.OH * g.OW * C / 8;
-  const int nb = grid_for(nvec);
+  const int nb = static_cast<int>(N * g.OH);  // one workgroup per output row
   switch (dtype) {
     case kBF16:
       bn_relu_maxpool_fwd_kernel<bf16><<<nb, kThreads, 0, s>>>(static_cast<const bf16*>(x), scale, shift,
-                                                               static_cast<bf16*>(y), idx, g, nvec);
+                                                               static_cast<bf16*>(y), idx, g);
       break;
     case kF16:
       bn_relu_maxpool_fwd_kernel<f16><<<nb, kThreads, 0, s>>>(static_cast<const f16*>(x), scale, shift,
-                                                              static_cast<f16*>(y), idx, g, nvec);
+                                                              static_cast<f16*>(y), idx, g);
       break;
     case kF32:
       bn_relu_maxpool_fwd_kernel<float><<<nb, kThreads, 0, s>>>(static_cast<const float*>(x), scale, shift,
-                                                                static_cast<float*>(y), idx, g, nvec);
+                                                                static_cast<float*>(y), idx, g);
       break;
     default:
       throw std::runtime_error("bn_relu_maxpool_fwd: unsupported dtype");
@@ -197,12 +193,10 @@ void bn_relu_maxpool_fwd(const void* x, const float* scale, const float* shift, 
 void maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, int64_t N, int64_t H, int64_t W, int64_t C, int K,
                  int S, int P, int dtype, hipStream_t s) {
   const PoolGeo g = make_geo(N, H, W, C, K, S, P);
-  const int64_t nvec = N * H * W * C / 8;
-  const int nb = grid_for(nvec);
+  const int nb = static_cast<int>(N * H);  // one workgroup per input row
   const int nw = (K + S - 1) / S;
 #define POOL_BWD(T, NW)                                                                                         \
-  maxpool_bwd_gather_kernel<T, NW><<<nb, kThreads, 0, s>>>(static_cast<const T*>(dy), idx, static_cast<T*>(dx), \
-                                                           g, nvec)
+  maxpool_bwd_gather_kernel<T, NW><<<nb, kThreads, 0, s>>>(static_cast<const T*>(dy), idx, static_cast<T*>(dx), g)
 #define POOL_BWD_NW(T)                              \
   {                                                 \
     if (nw == 1) POOL_BWD(T, 1);                    \

@@ -35,6 +35,11 @@ def launch(nprocs: int, argv: list[str], env: dict | None = None, timeout: float
     base = dict(os.environ)
     # like torchrun: avoid nprocs x all-cores OpenMP oversubscription on CPU ranks
     base.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // max(1, nprocs))))
+    # the ranks import this package even when the script lives elsewhere (mpiexecjl --project)
+    pkg_root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    paths = base.get("PYTHONPATH", "").split(os.pathsep) if base.get("PYTHONPATH") else []
+    if pkg_root not in paths:
+        base["PYTHONPATH"] = os.pathsep.join([pkg_root] + paths)
     if env:
         base.update(env)
     for r in range(nprocs):
