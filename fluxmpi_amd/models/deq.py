@@ -22,30 +22,36 @@ import torch.nn.functional as F
 def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0):
     """Anderson acceleration for ``x = f(x)`` over batch-flattened tensors. Returns (x, iters, rel_residual)."""
     bsz = x0.shape[0]
-    shape = x0.shape
+    shape, dt = x0.shape, x0.dtype
     d = x0[0].numel()
-    X = torch.zeros(bsz, m, d, dtype=x0.dtype, device=x0.device)
+    # the solver history and the small (m+1)^2 systems are kept in fp32 whatever the model
+    # dtype (bf16 has no batched LU, and 8-bit mantissas would stall the extrapolation)
+    X = torch.zeros(bsz, m, d, dtype=torch.float32, device=x0.device)
     Fv = torch.zeros_like(X)
-    X[:, 0], Fv[:, 0] = x0.reshape(bsz, -1), f(x0).reshape(bsz, -1)
-    X[:, 1], Fv[:, 1] = Fv[:, 0], f(Fv[:, 0].reshape(shape)).reshape(bsz, -1)
-    H = torch.zeros(bsz, m + 1, m + 1, dtype=x0.dtype, device=x0.device)
+
+    def fx(v):
+        return f(v.reshape(shape).to(dt)).reshape(bsz, -1).float()
+
+    X[:, 0], Fv[:, 0] = x0.reshape(bsz, -1).float(), fx(x0)
+    X[:, 1], Fv[:, 1] = Fv[:, 0], fx(Fv[:, 0])
+    H = torch.zeros(bsz, m + 1, m + 1, dtype=torch.float32, device=x0.device)
     H[:, 0, 1:] = H[:, 1:, 0] = 1
-    y = torch.zeros(bsz, m + 1, 1, dtype=x0.dtype, device=x0.device)
+    y = torch.zeros(bsz, m + 1, 1, dtype=torch.float32, device=x0.device)
     y[:, 0] = 1
     res = float("inf")
     k = 1
     for k in range(2, max_iter):
         n = min(k, m)
         G = Fv[:, :n] - X[:, :n]
-        H[:, 1:n + 1, 1:n + 1] = torch.bmm(G, G.transpose(1, 2)) + lam * torch.eye(n, dtype=x0.dtype,
+        H[:, 1:n + 1, 1:n + 1] = torch.bmm(G, G.transpose(1, 2)) + lam * torch.eye(n, dtype=torch.float32,
                                                                                    device=x0.device)[None]
         alpha = torch.linalg.solve(H[:, :n + 1, :n + 1], y[:, :n + 1])[:, 1:n + 1, 0]
         X[:, k % m] = beta * (alpha[:, None] @ Fv[:, :n])[:, 0] + (1 - beta) * (alpha[:, None] @ X[:, :n])[:, 0]
-        Fv[:, k % m] = f(X[:, k % m].reshape(shape)).reshape(bsz, -1)
+        Fv[:, k % m] = fx(X[:, k % m])
         res = float((Fv[:, k % m] - X[:, k % m]).norm() / (1e-5 + Fv[:, k % m].norm()))
         if res < tol:
             break
-    return X[:, k % m].reshape(shape), k, res
+    return X[:, k % m].reshape(shape).to(dt), k, res
 
 
 class DEQFixedPoint(nn.Module):
