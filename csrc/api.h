@@ -71,7 +71,7 @@ void bn_bwd(const void* dy, const void* x, const void* y, const uint8_t* relu_ma
             const float* bias,
             const float* save_mean, const float* save_invstd, void* dx, void* dres,
             float* dweight, float* dbias, float* workspace, int64_t rows, int64_t C, int relu,
-            int dtype, hipStream_t stream);
+            int dtype, hipStream_t stream, int stats_ready = 0);
 size_t bn_workspace_floats(int64_t rows, int64_t C);
 // Split forward for producer/consumer fusion with the GEMM:
 // bn_stats_finalize: [stats pass over x unless stats_ready (a GEMM epilogue already
@@ -119,6 +119,15 @@ struct GemmProblem {
   int nbuf;            // LDS buffers: 0 = auto (2), 1, 2
   const void* res;     // optional bf16 residual [M][ldr] added in the epilogue (modes 0/1)
   int64_t ldr;
+  // mode 1 + bnb_x: stats = BatchNorm-backward reductions (sum dy_eff, sum dy_eff*xhat) of a BN
+  // whose input is bnb_x ([M][N] dense) and whose output gradient is C (see gemm.hip)
+  const void* bnb_x;
+  const float* bnb_w;
+  const float* bnb_b;
+  const float* bnb_mean;
+  const float* bnb_inv;
+  const uint8_t* bnb_mask;
+  int bnb_rm;
 };
 void gemm_bf16(const GemmProblem& g, hipStream_t stream);
 // out[e] = sum over s < splits of ws[s*n + e] (mode-3 split-K partials; ws is clobbered); out fp32 or bf16

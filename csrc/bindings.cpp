@@ -85,13 +85,13 @@ PYBIND11_MODULE(_C, m) {
         [](uintptr_t dy, uintptr_t x, uintptr_t y, uintptr_t mask, uintptr_t w, uintptr_t b, uintptr_t sm, uintptr_t si,
            uintptr_t dx,
            uintptr_t dres, uintptr_t dw, uintptr_t db, uintptr_t ws, int64_t rows, int64_t C, int relu, int dtype,
-           uintptr_t stream) {
+           uintptr_t stream, int stats_ready) {
           bn_bwd(reinterpret_cast<const void*>(dy), reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(y),
                  reinterpret_cast<const uint8_t*>(mask),
                  reinterpret_cast<const float*>(w), reinterpret_cast<const float*>(b), reinterpret_cast<const float*>(sm),
                  reinterpret_cast<const float*>(si), reinterpret_cast<void*>(dx), reinterpret_cast<void*>(dres),
                  reinterpret_cast<float*>(dw), reinterpret_cast<float*>(db), reinterpret_cast<float*>(ws), rows, C,
-                 relu, dtype, S(stream));
+                 relu, dtype, S(stream), stats_ready);
         });
 
   m.def("bn_stats_finalize",
@@ -132,20 +132,26 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_bf16",
         [](uintptr_t a, uintptr_t b, uintptr_t c, int64_t lda, int64_t ldb, int64_t ldc, int64_t M, int64_t N,
            int64_t K, bool a_kmajor, bool b_kmajor, int mode, int splits, uintptr_t a_scale, uintptr_t a_shift,
-           uintptr_t b_scale, uintptr_t b_shift, uintptr_t stats, int tile_m, int tile_n, uintptr_t stream, int nbuf, uintptr_t res, int64_t ldr) {
+           uintptr_t b_scale, uintptr_t b_shift, uintptr_t stats, int tile_m, int tile_n, uintptr_t stream, int nbuf, uintptr_t res, int64_t ldr,
+           uintptr_t bnb_x, uintptr_t bnb_w, uintptr_t bnb_b, uintptr_t bnb_mean, uintptr_t bnb_inv,
+           uintptr_t bnb_mask, int bnb_rm) {
           GemmProblem g{reinterpret_cast<const void*>(a), reinterpret_cast<const void*>(b),
                         reinterpret_cast<void*>(c), lda, ldb, ldc, M, N, K, a_kmajor, b_kmajor, mode, splits,
                         reinterpret_cast<const float*>(a_scale), reinterpret_cast<const float*>(a_shift),
                         reinterpret_cast<const float*>(b_scale), reinterpret_cast<const float*>(b_shift),
                         reinterpret_cast<float*>(stats), tile_m, tile_n, nbuf,
-                        reinterpret_cast<const void*>(res), ldr};
+                        reinterpret_cast<const void*>(res), ldr, reinterpret_cast<const void*>(bnb_x),
+                        reinterpret_cast<const float*>(bnb_w), reinterpret_cast<const float*>(bnb_b),
+                        reinterpret_cast<const float*>(bnb_mean), reinterpret_cast<const float*>(bnb_inv),
+                        reinterpret_cast<const uint8_t*>(bnb_mask), bnb_rm};
           gemm_bf16(g, S(stream));
         },
         py::arg("a"), py::arg("b"), py::arg("c"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("M"),
         py::arg("N"), py::arg("K"), py::arg("a_kmajor"), py::arg("b_kmajor"), py::arg("mode"), py::arg("splits"),
         py::arg("a_scale"), py::arg("a_shift"), py::arg("b_scale"), py::arg("b_shift"), py::arg("stats"),
         py::arg("tile_m"), py::arg("tile_n"), py::arg("stream"), py::arg("nbuf") = 0, py::arg("res") = 0,
-        py::arg("ldr") = 0);
+        py::arg("ldr") = 0, py::arg("bnb_x") = 0, py::arg("bnb_w") = 0, py::arg("bnb_b") = 0,
+        py::arg("bnb_mean") = 0, py::arg("bnb_inv") = 0, py::arg("bnb_mask") = 0, py::arg("bnb_rm") = 0);
 
   m.def("gemm_splitk_reduce",
         [](uintptr_t ws, int splits, int64_t n, uintptr_t out, int out_dtype, uintptr_t stream) {

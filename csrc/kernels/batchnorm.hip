@@ -534,7 +534,7 @@ void fwd_train_t(const void* x, void* y, const void* res, const float* w, const 
 template <typename T>
 void bwd_t(const void* dy, const void* x, const void* y, const uint8_t* mask, const float* w, const float* b,
            const float* sm, const float* si, void* dx, void* dres, float* dw, float* db, float* ws, int64_t rows,
-           int64_t C, int relu, hipStream_t s) {
+           int64_t C, int relu, int stats_ready, hipStream_t s) {
   const T* dyr = static_cast<const T*>(dy);
   const T* xr = static_cast<const T*>(x);
   const T* yr = static_cast<const T*>(y);
@@ -546,7 +546,10 @@ void bwd_t(const void* dy, const void* x, const void* y, const uint8_t* mask, co
     bn_bwd_reduce_kernel<T, RM><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(dyr, xr, yr, mask, w, b, sm, si,   \
                                                                               rows, (int)C, g, ws);             \
   }
-  if (rm == 0) RED(0)
+  // stats_ready: the reductions were accumulated into ws by the producer of dy (the GEMM's
+  // BN-backward epilogue), so the reduce pass over (dy, x) is skipped
+  if (stats_ready) {}
+  else if (rm == 0) RED(0)
   else if (rm == 1) RED(1)
   else if (rm == 2) RED(2)
   else RED(3)
@@ -653,15 +656,15 @@ void bn_fwd_infer(const void* x, void* y, const void* residual, const float* wei
 void bn_bwd(const void* dy, const void* x, const void* y, const uint8_t* relu_mask, const float* weight,
             const float* bias, const float* save_mean,
             const float* save_invstd, void* dx, void* dres, float* dweight, float* dbias, float* workspace,
-            int64_t rows, int64_t C, int relu, int dtype, hipStream_t stream) {
+            int64_t rows, int64_t C, int relu, int dtype, hipStream_t stream, int stats_ready) {
   check(C);
   switch (dtype) {
     case kBF16: bwd_t<bf16>(dy, x, y, relu_mask, weight, bias, save_mean, save_invstd, dx, dres, dweight, dbias, workspace, rows, C,
-                            relu, stream); break;
+                            relu, stats_ready, stream); break;
     case kF16: bwd_t<f16>(dy, x, y, relu_mask, weight, bias, save_mean, save_invstd, dx, dres, dweight, dbias, workspace, rows, C,
-                          relu, stream); break;
+                          relu, stats_ready, stream); break;
     case kF32: bwd_t<float>(dy, x, y, relu_mask, weight, bias, save_mean, save_invstd, dx, dres, dweight, dbias, workspace, rows, C,
-                            relu, stream); break;
+                            relu, stats_ready, stream); break;
     default: throw std::runtime_error("fused batchnorm: unsupported dtype");
   }
 }

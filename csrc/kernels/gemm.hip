@@ -58,6 +58,17 @@ struct GemmArgs {
   float* stats;  // [kShards][2][N] sharded per-column sum / sumsq (epilogue mode 1)
   const bf16* res;  // optional residual added in the bf16 epilogue (modes 0/1), row stride ldr
   int64_t ldr;
+  // mode 1 with bnb_x: instead of sum/sumsq of the output, accumulate the BatchNorm-backward
+  // reductions of a BN whose output gradient IS this GEMM's output: sum(dy_eff) and
+  // sum(dy_eff * xhat), xhat = (x - mean) * invstd, dy_eff = dy masked by the BN's ReLU
+  // (bnb_rm 0: none, 2: recomputed as fma(x, w*invstd, b - mean*w*invstd) > 0, 3: bit mask)
+  const bf16* bnb_x;  // BN input, [M][N] dense
+  const float* bnb_w;
+  const float* bnb_b;
+  const float* bnb_mean;
+  const float* bnb_inv;
+  const uint8_t* bnb_mask;
+  int bnb_rm;
   int mode;      // 0: store bf16; 1: store bf16 + stats; 2: fp32 atomic add into c
   int tiles_m, tiles_n;
 };
@@ -282,10 +293,23 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs p) {
   const bool ncol_ok = n + 8 <= p.N;
   bf16* c = static_cast<bf16*>(p.c);
   float cs[8], cq[8];
+  float bmu[8], bis[8], bsc[8], bsh[8];  // BN-backward epilogue: per-column coefficients
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     cs[e] = 0.f;
     cq[e] = 0.f;
+    bmu[e] = bis[e] = bsc[e] = bsh[e] = 0.f;
+  }
+  const bool bnb = p.mode == 1 && p.bnb_x != nullptr;
+  if (bnb) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int64_t col = n + e < p.N ? n + e : p.N - 1;
+      bmu[e] = p.bnb_mean[col];
+      bis[e] = p.bnb_inv[col];
+      bsc[e] = (p.bnb_w ? p.bnb_w[col] : 1.f) * bis[e];                 // == forward scale
+      bsh[e] = fmaf(-bmu[e], bsc[e], p.bnb_b ? p.bnb_b[col] : 0.f);     // == forward shift
+    }
   }
 #pragma unroll
   for (int h = 0; h < NP; ++h) {
@@ -324,7 +348,28 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs p) {
         const bf16* e8 = reinterpret_cast<const bf16*>(&v);
         for (int e = 0; e < 8 && n + e < p.N; ++e) c[m * p.ldc + n + e] = e8[e];
       }
-      if (p.mode == 1) {
+      if (bnb) {
+        bf16 e8[8], x8[8];
+        __builtin_memcpy(e8, &v, 16);
+        const int64_t xo = m * p.N + n;  // x is dense [M][N]
+        if (ncol_ok) {
+          const uint4 xv = *reinterpret_cast<const uint4*>(p.bnb_x + xo);
+          __builtin_memcpy(x8, &xv, 16);
+        } else {
+          for (int e = 0; e < 8; ++e) x8[e] = n + e < p.N ? p.bnb_x[xo + e] : static_cast<bf16>(0.f);
+        }
+        const unsigned mb = p.bnb_rm == 3 ? p.bnb_mask[xo >> 3] : 0xFFu;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float xf = static_cast<float>(x8[e]);
+          bool keep = n + e < p.N;
+          if (p.bnb_rm == 2) keep = keep && fmaf(xf, bsc[e], bsh[e]) > 0.f;
+          if (p.bnb_rm == 3) keep = keep && ((mb >> e) & 1u);
+          const float dd = keep ? static_cast<float>(e8[e]) : 0.f;
+          cs[e] += dd;
+          cq[e] = fmaf(dd, (xf - bmu[e]) * bis[e], cq[e]);
+        }
+      } else if (p.mode == 1) {
         bf16 e8[8];
         __builtin_memcpy(e8, &v, 16);
 #pragma unroll
@@ -457,6 +502,19 @@ void gemm_bf16(const GemmProblem& g, hipStream_t stream) {
   a.mode = g.mode;
   a.res = static_cast<const bf16*>(g.res);
   a.ldr = g.ldr;
+  a.bnb_x = static_cast<const bf16*>(g.bnb_x);
+  a.bnb_w = g.bnb_w;
+  a.bnb_b = g.bnb_b;
+  a.bnb_mean = g.bnb_mean;
+  a.bnb_inv = g.bnb_inv;
+  a.bnb_mask = g.bnb_mask;
+  a.bnb_rm = g.bnb_rm;
+  if (a.bnb_x != nullptr) {
+    if (g.mode != 1 || g.ldc != g.N || g.N % 8 != 0 || g.bnb_mean == nullptr || g.bnb_inv == nullptr ||
+        (g.bnb_rm == 3 && g.bnb_mask == nullptr) || (g.bnb_rm != 0 && g.bnb_rm != 2 && g.bnb_rm != 3))
+      throw std::runtime_error("gemm_bf16: BN-backward epilogue needs mode 1, dense C (ldc == N, N % 8 == 0), "
+                               "mean/invstd and a valid ReLU mode");
+  }
   if (a.res != nullptr && (g.mode > 1 || g.ldr % 8 != 0))
     throw std::runtime_error("gemm_bf16: residual epilogue needs mode 0/1 and ldr % 8 == 0");
   if (splits > 1 && g.mode != 2 && g.mode != 3)

@@ -86,19 +86,28 @@ class Bottleneck(nn.Module):
         if (self.gemm_fused or self.hybrid) and self.training:
             from ..ops import fused_block as fb
             if fb.supported(x, *self.dims):
-                # identity blocks: bn3's residual gradient goes straight into conv1's dgrad epilogue
-                link = fb.GradLink() if (self.downsample is None and x.requires_grad
-                                         and torch.is_grad_enabled()) else None
+                grad = torch.is_grad_enabled()
+                # identity blocks: bn3's residual gradient goes straight into conv1's dgrad epilogue,
+                # and that epilogue (whose output is then the whole gradient of the previous
+                # block's output) also reduces the previous block's bn3 backward statistics
+                link = fb.GradLink() if (self.downsample is None and x.requires_grad and grad) else None
+                prev = getattr(x, "_fluxmpi_bnlink", None) if link is not None else None
+                out_link = fb.BNStatsLink() if grad else None
                 if self.hybrid:
-                    a1 = self.bn1(fb.conv1x1_hybrid(x, self.conv1.weight, link), relu=True)
-                    a2 = self.bn2(self.conv2(a1), relu=True)
-                    return self.bn3(fb.conv1x1_hybrid(a2, self.conv3.weight), relu=True, residual=identity,
-                                    link=link)
-                c1 = fb.conv1x1_stats(x, self.conv1.weight, link)    # + bn1 statistics (GEMM epilogue)
-                a1 = fb.bn_from_stats(c1, self.bn1, relu=True)
-                c2 = self.conv2(a1)
-                c3 = fb.bn_relu_conv1x1(c2, self.bn2, self.conv3.weight)  # bn2+relu fused into the A load
-                return fb.bn_from_stats(c3, self.bn3, relu=True, residual=identity, link=link)
+                    bl2 = fb.BNStatsLink() if grad else None  # bn2 -> conv3 (its only consumer)
+                    a1 = self.bn1(fb.conv1x1_hybrid(x, self.conv1.weight, link, prev), relu=True)
+                    a2 = self.bn2(self.conv2(a1), relu=True, bnlink=bl2)
+                    out = self.bn3(fb.conv1x1_hybrid(a2, self.conv3.weight, None, bl2), relu=True,
+                                   residual=identity, link=link, bnlink=out_link)
+                else:
+                    c1 = fb.conv1x1_stats(x, self.conv1.weight, link, prev)  # + bn1 statistics (GEMM epilogue)
+                    a1 = fb.bn_from_stats(c1, self.bn1, relu=True)
+                    c2 = self.conv2(a1)
+                    c3 = fb.bn_relu_conv1x1(c2, self.bn2, self.conv3.weight)  # bn2+relu fused into the A load
+                    out = fb.bn_from_stats(c3, self.bn3, relu=True, residual=identity, link=link, bnlink=out_link)
+                if out_link is not None:
+                    out._fluxmpi_bnlink = out_link  # for the next block's conv1 (used iff it is an identity block)
+                return out
         if self.fused:
             out = self.bn1(self.conv1(x), relu=True)
             out = self.bn2(self.conv2(out), relu=True)

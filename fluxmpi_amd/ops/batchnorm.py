@@ -85,6 +85,44 @@ class GradLink:
         return g
 
 
+class BNStatsLink:
+    """Lets the kernel that produces a BatchNorm's output gradient (a dgrad GEMM) accumulate
+    that BatchNorm's backward reductions — sum(dy_eff), sum(dy_eff * xhat) — in its epilogue,
+    so the BatchNorm backward skips its reduce pass over (dy, x).
+
+    The BatchNorm's forward ``bind``\ s its saved tensors; the consumer's backward runs the
+    GEMM with the BN-backward epilogue into the shared statistics workspace and sets
+    ``ready``; the BatchNorm's backward then only finalizes and applies. Valid only when the
+    linked consumer's dgrad output IS the whole gradient of the BatchNorm output (a single
+    consumer, or the residual sum handed over through a :class:`GradLink`); otherwise the
+    link stays unused and the BatchNorm reduces as usual.
+    """
+
+    __slots__ = ("x", "mask", "w32", "b32", "mean", "inv", "relu", "ready")
+
+    def __init__(self):
+        self.x = self.mask = self.w32 = self.b32 = self.mean = self.inv = None
+        self.relu = False
+        self.ready = False
+
+    def bind(self, x, mask, w32, b32, mean, inv, relu):
+        self.x, self.mask, self.w32, self.b32, self.mean, self.inv, self.relu = x, mask, w32, b32, mean, inv, relu
+        self.ready = False
+
+    @property
+    def bound(self) -> bool:
+        return self.x is not None
+
+    @property
+    def relu_mode(self) -> int:
+        """0: no ReLU; 2: mask recomputed from x; 3: saved 1-bit mask."""
+        return 0 if not self.relu else (3 if self.mask is not None else 2)
+
+    def release(self):
+        self.x = self.mask = self.w32 = self.b32 = self.mean = self.inv = None
+        self.ready = False
+
+
 def bn_counter(bn):
     """(momentum, counter) for a training-mode BatchNorm module: the ``num_batches_tracked``
     tensor the finalize kernel increments (no launch of its own), or None when nothing is
@@ -100,7 +138,7 @@ def bn_counter(bn):
 class _FusedBN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, momentum, eps, relu, link=None,
-                nbt=None):
+                nbt=None, bnlink=None):
         C = _ext.get(required=True)
         x = _nhwc(x)
         res = _nhwc(residual) if residual is not None else None
@@ -131,6 +169,10 @@ class _FusedBN(torch.autograd.Function):
         # kernels (bit-identical to the forward); with one, the 1-bit mask is used.
         # Either way y is neither saved nor re-read.
         ctx.save_for_backward(x, mask, w32, b32, save_mean, save_inv)
+        ctx.bnlink = bnlink
+        if bnlink is not None:
+            bnlink.bind(x, mask, w32 if w32 is not None else torch.ones(ch, device=x.device),
+                        b32 if b32 is not None else torch.zeros(ch, device=x.device), save_mean, save_inv, relu)
         return y
 
     @staticmethod
@@ -138,6 +180,8 @@ class _FusedBN(torch.autograd.Function):
         C = _ext.get(required=True)
         x, mask, w32, b32, save_mean, save_inv = ctx.saved_tensors
         dy = _nhwc(dy)
+        # the producer of dy already accumulated this BN's reductions into the workspace
+        stats_ready = ctx.bnlink is not None and ctx.bnlink.ready
         rows, ch = _rows_c(x)
         dx = torch.empty_like(x)
         dres = torch.empty_like(x) if ctx.has_res else None
@@ -150,7 +194,9 @@ class _FusedBN(torch.autograd.Function):
                  w32.data_ptr() if w32 is not None else 0, b32.data_ptr() if b32 is not None else 0,
                  save_mean.data_ptr(), save_inv.data_ptr(), dx.data_ptr(),
                  dres.data_ptr() if dres is not None else 0, dw.data_ptr(), db.data_ptr(), ws.data_ptr(), rows, ch,
-                 int(ctx.relu), DTYPE_CODE[x.dtype], stream)
+                 int(ctx.relu), DTYPE_CODE[x.dtype], stream, int(stats_ready))
+        if ctx.bnlink is not None:
+            ctx.bnlink.release()
         if w32 is None:
             dw = None
         elif ctx.wdtype != torch.float32:
@@ -161,7 +207,7 @@ class _FusedBN(torch.autograd.Function):
             db = db.to(ctx.wdtype)
         if ctx.link is not None:
             ctx.link.grad, dres = dres, None
-        return dx, dw, db, dres, None, None, None, None, None, None, None
+        return dx, dw, db, dres, None, None, None, None, None, None, None, None
 
 
 def batch_norm_reference(x, weight, bias, running_mean, running_var, training, momentum, eps, relu=False,
@@ -178,13 +224,13 @@ def batch_norm_reference(x, weight, bias, running_mean, running_var, training, m
 
 def fused_batch_norm(x, weight, bias, running_mean, running_var, training=True, momentum=0.1, eps=1e-5,
                      relu=False, residual=None, link: GradLink | None = None,
-                     num_batches_tracked: torch.Tensor | None = None):
+                     num_batches_tracked: torch.Tensor | None = None, bnlink: BNStatsLink | None = None):
     """``link``: deliver the residual's gradient through a :class:`GradLink` instead of
     returning it to autograd (training with the fused kernels only; otherwise ignored).
     ``num_batches_tracked``: counter incremented once (inside the finalize kernel)."""
     if training and kernel_supported(x):
         return _FusedBN.apply(x, weight, bias, residual, running_mean, running_var, momentum, eps, relu, link,
-                              num_batches_tracked)
+                              num_batches_tracked, bnlink)
     if num_batches_tracked is not None and training:
         num_batches_tracked.add_(1)
     if (not training) and kernel_supported(x) and not torch.is_grad_enabled():
@@ -205,10 +251,11 @@ def fused_batch_norm(x, weight, bias, running_mean, running_var, training=True, 
 class FusedBatchNorm2d(nn.BatchNorm2d):
     """``nn.BatchNorm2d`` with optional fused ReLU / residual add (NHWC HIP kernels on GPU)."""
 
-    def forward(self, x, relu: bool = False, residual: torch.Tensor | None = None, link: GradLink | None = None):
+    def forward(self, x, relu: bool = False, residual: torch.Tensor | None = None, link: GradLink | None = None,
+                bnlink: BNStatsLink | None = None):
         mom, nbt = bn_counter(self)
         use_batch = self.training or not self.track_running_stats
         return fused_batch_norm(x, self.weight, self.bias,
                                 self.running_mean if self.track_running_stats else None,
                                 self.running_var if self.track_running_stats else None,
-                                use_batch, mom, self.eps, relu, residual, link, nbt)
+                                use_batch, mom, self.eps, relu, residual, link, nbt, bnlink)

@@ -29,7 +29,7 @@ from __future__ import annotations
 import torch
 
 from . import _ext
-from .batchnorm import GradLink, _workspace, bn_counter  # noqa: F401 (GradLink re-exported)
+from .batchnorm import BNStatsLink, GradLink, _workspace, bn_counter  # noqa: F401 (links re-exported)
 from .gemm import conv1x1_dgrad, conv1x1_wgrad, gemm
 from .multi_tensor import DTYPE_CODE
 
@@ -54,7 +54,7 @@ def _empty_nhwc(n, c, h, w, like):
     return torch.empty(n, h, w, c, device=like.device, dtype=like.dtype).permute(0, 3, 1, 2)
 
 
-def _bn_bwd(dy, x, mask, w32, b32, mean, inv, relu, has_res):
+def _bn_bwd(dy, x, mask, w32, b32, mean, inv, relu, has_res, stats_ready=False):
     """Shared fused-BN backward; returns (dx, dres, dw, db) (fp32 dw/db)."""
     C = _ext.get(required=True)
     rows, ch = x.numel() // x.shape[1], x.shape[1]
@@ -65,7 +65,7 @@ def _bn_bwd(dy, x, mask, w32, b32, mean, inv, relu, has_res):
     ws = _workspace(x)
     C.bn_bwd(dy.data_ptr(), x.data_ptr(), 0, _p(mask), _p(w32), _p(b32), mean.data_ptr(), inv.data_ptr(),
              dx.data_ptr(), _p(dres), dw.data_ptr(), db.data_ptr(), ws.data_ptr(), rows, ch, int(relu),
-             DTYPE_CODE[x.dtype], _stream(x))
+             DTYPE_CODE[x.dtype], _stream(x), int(stats_ready))
     return dx, dres, dw, db
 
 
@@ -73,9 +73,9 @@ class _Conv1x1Stats(torch.autograd.Function):
     """c = conv1x1(x, W); the output's per-channel sum/sumsq go to the BN workspace."""
 
     @staticmethod
-    def forward(ctx, x, weight, link=None):
+    def forward(ctx, x, weight, link=None, bnlink=None):
         x = x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
-        ctx.link = link
+        ctx.link, ctx.bnlink = link, bnlink
         n, ci, h, w = x.shape
         co = weight.shape[0]
         w2 = weight.reshape(co, ci)
@@ -91,18 +91,27 @@ class _Conv1x1Stats(torch.autograd.Function):
         x, weight = ctx.saved_tensors
         co, ci = weight.shape[0], weight.shape[1]
         dc2 = _nhwc2d(dc)
-        dx = _dgrad_nhwc(dc2, weight, x, ctx.link) if ctx.needs_input_grad[0] else None
+        dx = _dgrad_nhwc(dc2, weight, x, ctx.link, ctx.bnlink) if ctx.needs_input_grad[0] else None
         dw = conv1x1_wgrad(dc2, _nhwc2d(x), out_dtype=weight.dtype).view_as(weight)
-        return dx, dw, None
+        return dx, dw, None, None
 
 
-def _dgrad_nhwc(dc2, weight, x, link):
-    """dX (NHWC, x's shape) = dC @ W [+ the residual gradient delivered through ``link``]."""
+def _dgrad_nhwc(dc2, weight, x, link, bnlink=None):
+    """dX (NHWC, x's shape) = dC @ W [+ the residual gradient delivered through ``link``]; with a
+    bound ``bnlink`` the epilogue also accumulates the backward reductions of the BatchNorm
+    that produced x (whose output gradient dX is), so that BatchNorm skips its reduce pass."""
     co, ci = weight.shape[0], weight.shape[1]
     n, _, h, w = x.shape
     dx = _empty_nhwc(n, ci, h, w, x)
     res = _nhwc2d(link.take()) if link is not None else None
-    conv1x1_dgrad(dc2, weight.reshape(co, ci), residual=res, out=_nhwc2d(dx))
+    bn = stats = None
+    if bnlink is not None and bnlink.bound and bnlink.x.shape == x.shape and \
+            bnlink.x.is_contiguous(memory_format=torch.channels_last):
+        bn = (_nhwc2d(bnlink.x), bnlink.w32, bnlink.b32, bnlink.mean, bnlink.inv, bnlink.mask, bnlink.relu_mode)
+        stats = _workspace(dx)
+    conv1x1_dgrad(dc2, weight.reshape(co, ci), residual=res, out=_nhwc2d(dx), bn_bwd=bn, stats=stats)
+    if bn is not None:
+        bnlink.ready = True
     return dx
 
 
@@ -112,9 +121,9 @@ class _Conv1x1Hybrid(torch.autograd.Function):
     with the block's residual gradient added in its epilogue (``link``)."""
 
     @staticmethod
-    def forward(ctx, x, weight, link=None):
+    def forward(ctx, x, weight, link=None, bnlink=None):
         x = x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
-        ctx.link = link
+        ctx.link, ctx.bnlink = link, bnlink
         ctx.save_for_backward(x, weight)
         return torch.nn.functional.conv2d(x, weight)
 
@@ -123,12 +132,12 @@ class _Conv1x1Hybrid(torch.autograd.Function):
         x, weight = ctx.saved_tensors
         if not dc.is_contiguous(memory_format=torch.channels_last):
             dc = dc.contiguous(memory_format=torch.channels_last)
-        dx = _dgrad_nhwc(_nhwc2d(dc), weight, x, ctx.link) if ctx.needs_input_grad[0] else None
+        dx = _dgrad_nhwc(_nhwc2d(dc), weight, x, ctx.link, ctx.bnlink) if ctx.needs_input_grad[0] else None
         dw = None
         if ctx.needs_input_grad[1]:
             dw = torch.ops.aten.convolution_backward(dc, x, weight, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
                                                      [False, True, False])[1]
-        return dx, dw, None
+        return dx, dw, None, None
 
 
 class _BNFromStats(torch.autograd.Function):
@@ -137,7 +146,7 @@ class _BNFromStats(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, momentum, eps, relu, stats_ready,
-                link=None, nbt=None):
+                link=None, nbt=None, bnlink=None):
         C = _ext.get(required=True)
         ch = x.shape[1]
         rows = x.numel() // ch
@@ -160,6 +169,9 @@ class _BNFromStats(torch.autograd.Function):
                    inv.data_ptr(), rows, ch, int(relu), _p(mask), DTYPE_CODE[x.dtype], _stream(x))
         ctx.relu, ctx.has_res, ctx.wdtype = relu, residual is not None, weight.dtype
         ctx.link = link if residual is not None else None
+        ctx.bnlink = bnlink
+        if bnlink is not None:
+            bnlink.bind(x, mask, w32, b32, mean, inv, relu)
         ctx.save_for_backward(x, mask, w32, b32, mean, inv)
         return y
 
@@ -168,10 +180,13 @@ class _BNFromStats(torch.autograd.Function):
         x, mask, w32, b32, mean, inv = ctx.saved_tensors
         if not dy.is_contiguous(memory_format=torch.channels_last):
             dy = dy.contiguous(memory_format=torch.channels_last)
-        dx, dres, dw, db = _bn_bwd(dy, x, mask, w32, b32, mean, inv, ctx.relu, ctx.has_res)
+        ready = ctx.bnlink is not None and ctx.bnlink.ready
+        dx, dres, dw, db = _bn_bwd(dy, x, mask, w32, b32, mean, inv, ctx.relu, ctx.has_res, ready)
+        if ctx.bnlink is not None:
+            ctx.bnlink.release()
         if ctx.link is not None:
             ctx.link.grad, dres = dres, None
-        return dx, dw.to(ctx.wdtype), db.to(ctx.wdtype), dres, None, None, None, None, None, None, None, None
+        return dx, dw.to(ctx.wdtype), db.to(ctx.wdtype), dres, None, None, None, None, None, None, None, None, None
 
 
 class _BNReluConv1x1(torch.autograd.Function):
@@ -211,24 +226,26 @@ class _BNReluConv1x1(torch.autograd.Function):
         c2_2d = _nhwc2d(c2)
         # dW = dc3^T @ relu(bn(c2))  — the activation is rebuilt on the fly in the B-operand load
         dw = conv1x1_wgrad(dc3_2d, c2_2d, in_affine=(scale, shift), out_dtype=weight.dtype).view_as(weight)
-        # d(relu(bn(c2))) = dc3 @ W, then the BN backward with the ReLU mask recomputed from c2
-        da = conv1x1_dgrad(dc3_2d, weight.reshape(co, ch)).view(n, h, w, ch).permute(0, 3, 1, 2)
-        dc2, _, dbw, dbb = _bn_bwd(da, c2, None, w32, b32, mean, inv, True, False)
+        # d(relu(bn(c2))) = dc3 @ W with the BN-backward reductions (ReLU mask recomputed from c2)
+        # accumulated in the same GEMM's epilogue, then the BN backward without its reduce pass
+        da = conv1x1_dgrad(dc3_2d, weight.reshape(co, ch), bn_bwd=(c2_2d, w32, b32, mean, inv, None, 2),
+                           stats=_workspace(c2)).view(n, h, w, ch).permute(0, 3, 1, 2)
+        dc2, _, dbw, dbb = _bn_bwd(da, c2, None, w32, b32, mean, inv, True, False, stats_ready=True)
         return dc2, dbw.to(ctx.bn_wdtype), dbb.to(ctx.bn_wdtype), None, None, dw, None, None, None
 
 
-def conv1x1_stats(x, weight, link=None):
-    return _Conv1x1Stats.apply(x, weight, link)
+def conv1x1_stats(x, weight, link=None, bnlink=None):
+    return _Conv1x1Stats.apply(x, weight, link, bnlink)
 
 
-def conv1x1_hybrid(x, weight, link=None):
-    return _Conv1x1Hybrid.apply(x, weight, link)
+def conv1x1_hybrid(x, weight, link=None, bnlink=None):
+    return _Conv1x1Hybrid.apply(x, weight, link, bnlink)
 
 
-def bn_from_stats(x, bn, relu=False, residual=None, stats_ready=True, link=None):
+def bn_from_stats(x, bn, relu=False, residual=None, stats_ready=True, link=None, bnlink=None):
     mom, nbt = bn_counter(bn)
     return _BNFromStats.apply(x, bn.weight, bn.bias, residual, bn.running_mean, bn.running_var, mom, bn.eps, relu,
-                              stats_ready, link, nbt)
+                              stats_ready, link, nbt, bnlink)
 
 
 def bn_relu_conv1x1(c2, bn, weight):

@@ -30,13 +30,18 @@ def _ptr(t):
 
 
 def gemm(a, b, c, *, M, N, K, lda, ldb, ldc, a_kmajor=True, b_kmajor=True, mode=0, splits=1, a_affine=None,
-         b_affine=None, stats=None, tile_m=0, tile_n=0, nbuf=0, residual=None):
+         b_affine=None, stats=None, tile_m=0, tile_n=0, nbuf=0, residual=None, bn_bwd=None):
+    """``bn_bwd``: ``(x2d, w32, b32, mean, inv, mask, relu_mode)`` of a BatchNorm whose output
+    gradient is C — with ``mode=1`` the epilogue accumulates that BatchNorm's backward
+    reductions into ``stats`` instead of C's sum / sum of squares."""
     C = _ext.get(required=True)
     asc, ash = a_affine if a_affine is not None else (None, None)
     bsc, bsh = b_affine if b_affine is not None else (None, None)
+    bx, bw, bb, bmean, binv, bmask, brm = bn_bwd if bn_bwd is not None else (None,) * 6 + (0,)
     C.gemm_bf16(a.data_ptr(), b.data_ptr(), c.data_ptr(), lda, ldb, ldc, M, N, K, a_kmajor, b_kmajor, mode, splits,
                 _ptr(asc), _ptr(ash), _ptr(bsc), _ptr(bsh), _ptr(stats), tile_m, tile_n, _stream(c), nbuf or NBUF,
-                _ptr(residual), residual.stride(0) if residual is not None else 0)
+                _ptr(residual), residual.stride(0) if residual is not None else 0, _ptr(bx), _ptr(bw), _ptr(bb),
+                _ptr(bmean), _ptr(binv), _ptr(bmask), int(brm))
     return c
 
 
@@ -54,16 +59,20 @@ def conv1x1_fwd(x2d: torch.Tensor, w2d: torch.Tensor, in_affine=None, stats: tor
 
 
 def conv1x1_dgrad(dy2d: torch.Tensor, w2d: torch.Tensor, residual: torch.Tensor | None = None,
-                  out: torch.Tensor | None = None):
+                  out: torch.Tensor | None = None, bn_bwd=None, stats: torch.Tensor | None = None):
     """``dy2d`` [M, Cout], ``w2d`` [Cout, Cin] -> dX [M, Cin] bf16 (``+ residual`` [M, Cin] bf16 fused
-    into the epilogue: the gradient of a residual block's input in one pass)."""
+    into the epilogue: the gradient of a residual block's input in one pass). ``bn_bwd`` /
+    ``stats``: accumulate the backward reductions of the BatchNorm that produced the conv's
+    input (see :func:`gemm`) into the sharded ``stats`` workspace."""
     M, Co = dy2d.shape
     Ci = w2d.shape[1]
     dx = out if out is not None else torch.empty(M, Ci, device=dy2d.device, dtype=torch.bfloat16)
     if residual is not None:
         assert residual.shape == (M, Ci) and residual.dtype == torch.bfloat16 and residual.stride(1) == 1
+    if bn_bwd is not None:
+        assert stats is not None and dx.stride(0) == Ci and bn_bwd[0].shape == (M, Ci) and bn_bwd[0].stride(0) == Ci
     gemm(dy2d, w2d, dx, M=M, N=Ci, K=Co, lda=dy2d.stride(0), ldb=w2d.stride(0), ldc=dx.stride(0), a_kmajor=True,
-         b_kmajor=False, residual=residual)
+         b_kmajor=False, residual=residual, mode=1 if bn_bwd is not None else 0, stats=stats, bn_bwd=bn_bwd)
     return dx
 
 

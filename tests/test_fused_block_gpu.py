@@ -105,3 +105,33 @@ def test_hybrid_conv_with_link(gpu_ext):
     assert link.grad is None  # consumed
     assert _rel(xb.grad, xa.grad) < 1e-2 and _rel(wb.grad, wa.grad) < 1e-2
     assert _rel(bn_b.weight.grad, bn_a.weight.grad) < 1e-4  # float atomics: order-dependent rounding
+
+
+@pytest.mark.parametrize("with_res", [False, True])
+def test_bn_stats_link(gpu_ext, with_res):
+    """BN -> 1x1 conv (its only consumer): the conv's dgrad epilogue reduces the BN backward
+    statistics (ReLU mask recomputed, or the 1-bit mask after a residual add) and the BN
+    skips its reduce pass — gradients equal the unlinked chain's."""
+    from fluxmpi_amd.ops import fused_block as fb
+    from fluxmpi_amd.ops.batchnorm import FusedBatchNorm2d
+    torch.manual_seed(4)
+    c = torch.randn(4, 128, 14, 14, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    r = torch.randn_like(c) if with_res else None
+    w = (torch.randn(64, 128, 1, 1, device="cuda") * 0.1).bfloat16()
+    grads = []
+    for use_link in (False, True):
+        bn = FusedBatchNorm2d(128).cuda()
+        with torch.no_grad():
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.2, 0.2)
+        ci, wi = c.clone().requires_grad_(), w.clone().requires_grad_()
+        ri = r.clone().requires_grad_() if with_res else None
+        link = fb.BNStatsLink() if use_link else None
+        y = bn(ci, relu=True, residual=ri, bnlink=link)
+        z = fb.conv1x1_hybrid(y, wi, None, link)
+        (z.float() * torch.linspace(-1, 1, z.numel(), device="cuda").view_as(z)).sum().backward()
+        if use_link:
+            assert not link.bound  # consumed and released by the BN backward
+        grads.append([ci.grad, wi.grad, bn.weight.grad, bn.bias.grad] + ([ri.grad] if with_res else []))
+    for a, b in zip(*grads):
+        assert _rel(b, a) < 2e-3, (_rel(b, a))
