@@ -7,7 +7,8 @@ point of this config for the DDP layer (bucketing + backward/comm overlap).
 
 Attention uses ``F.scaled_dot_product_attention`` (the flash-attention
 kernels PyTorch-ROCm ships for gfx950); the patch embedding is a GEMM on the
-unfolded patches.
+unfolded patches; LayerNorms are the fused HIP kernels with the residual adds
+folded in (``fluxmpi_amd.ops.layernorm``).
 """
 from __future__ import annotations
 
@@ -31,23 +32,33 @@ class PatchEmbed(nn.Module):
 
 
 class Block(nn.Module):
+    """Pre-LN transformer block. ``forward(x, m)`` takes the residual stream ``x`` and the
+    previous block's pending MLP output ``m`` and returns ``(x + m + attn, mlp)``: each
+    residual add is fused into the LayerNorm that reads its result (``FusedLayerNorm.
+    add_forward``), so the stream is never re-read by a standalone add kernel."""
+
     def __init__(self, dim, heads, mlp):
         super().__init__()
+        from ..ops.layernorm import FusedLayerNorm
         self.heads = heads
-        self.ln1 = nn.LayerNorm(dim, eps=1e-6)
+        self.ln1 = FusedLayerNorm(dim, eps=1e-6)
         self.qkv = nn.Linear(dim, 3 * dim)
         self.proj = nn.Linear(dim, dim)
-        self.ln2 = nn.LayerNorm(dim, eps=1e-6)
+        self.ln2 = FusedLayerNorm(dim, eps=1e-6)
         self.fc1 = nn.Linear(dim, mlp)
         self.fc2 = nn.Linear(mlp, dim)
 
-    def forward(self, x):
+    def forward(self, x, m=None):
         b, t, d = x.shape
         h = self.heads
-        q, k, v = self.qkv(self.ln1(x)).view(b, t, 3, h, d // h).permute(2, 0, 3, 1, 4)
+        if m is None:
+            y = self.ln1(x)
+        else:
+            x, y = self.ln1.add_forward(x, m)  # x <- x + m (previous block's MLP branch)
+        q, k, v = self.qkv(y).view(b, t, 3, h, d // h).permute(2, 0, 3, 1, 4)
         a = F.scaled_dot_product_attention(q, k, v)
-        x = x + self.proj(a.transpose(1, 2).reshape(b, t, d))
-        return x + self.fc2(F.gelu(self.fc1(self.ln2(x))))
+        x, y = self.ln2.add_forward(x, self.proj(a.transpose(1, 2).reshape(b, t, d)))
+        return x, self.fc2(F.gelu(self.fc1(y)))
 
 
 class ViT(nn.Module):
@@ -57,7 +68,8 @@ class ViT(nn.Module):
         self.cls = nn.Parameter(torch.zeros(1, 1, dim))
         self.pos = nn.Parameter(torch.randn(1, self.embed.n + 1, dim) * 0.02)
         self.blocks = nn.ModuleList([Block(dim, heads, mlp) for _ in range(depth)])
-        self.ln = nn.LayerNorm(dim, eps=1e-6)
+        from ..ops.layernorm import FusedLayerNorm
+        self.ln = FusedLayerNorm(dim, eps=1e-6)
         self.head = nn.Linear(dim, num_classes)
         for m in self.modules():
             if isinstance(m, nn.Linear):
@@ -67,9 +79,12 @@ class ViT(nn.Module):
     def forward(self, x):
         x = self.embed(x)
         x = torch.cat([self.cls.expand(x.shape[0], -1, -1).to(x.dtype), x], 1) + self.pos.to(x.dtype)
+        m = None
         for blk in self.blocks:
-            x = blk(x)
-        return self.head(self.ln(x)[:, 0])
+            x, m = blk(x, m)
+        # only the [CLS] token reaches the head: finish its residual stream and normalise it alone
+        c = x[:, 0] if m is None else x[:, 0] + m[:, 0]
+        return self.head(self.ln(c))
 
 
 def vit_b16(num_classes=1000, img=224, **kw) -> ViT:

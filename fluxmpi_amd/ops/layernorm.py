@@ -1,0 +1,138 @@
+"""Fused LayerNorm (+ residual add) for transformer blocks (``csrc/kernels/layernorm.hip``).
+
+``FusedLayerNorm`` is an ``nn.LayerNorm`` (same parameters / state dict) whose GPU path
+runs one wavefront per row with the row held in registers. Its ``add_forward(x, r)``
+returns ``(h, ln(h))`` with ``h = x + r`` — the residual add of a pre-LN block fused into
+the normalisation pass — and the backward adds the gradient ``h`` receives from the
+rest of the residual stream in the same pass, so a ViT block has no separate residual
+add kernels in either direction. dw/db are reduced from per-workgroup partials (no
+atomics). CPU tensors (and unsupported shapes) use the PyTorch composition.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _ext
+from .multi_tensor import DTYPE_CODE
+
+_MAX_BLOCKS = 4096
+
+
+def _stream(t):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _p(t):
+    return t.data_ptr() if t is not None else 0
+
+
+def supported(x: torch.Tensor) -> bool:
+    d = x.shape[-1]
+    return (x.is_cuda and x.dtype in (torch.bfloat16, torch.float16, torch.float32) and d % 8 == 0
+            and 8 <= d <= 8192 and x.numel() > 0)
+
+
+def _fwd(x, r, w32, b32, eps):
+    C = _ext.get(required=True)
+    d = x.shape[-1]
+    rows = x.numel() // d
+    y = torch.empty_like(x)
+    h = torch.empty_like(x) if r is not None else None
+    mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+    rstd = torch.empty_like(mean)
+    C.layernorm_fwd(x.data_ptr(), _p(r), _p(h), y.data_ptr(), _p(w32), _p(b32), mean.data_ptr(), rstd.data_ptr(),
+                    rows, d, float(eps), DTYPE_CODE[x.dtype], _stream(x))
+    return h, y, mean, rstd
+
+
+def _bwd(dy, x, dh_ext, mean, rstd, w32, need_wb):
+    C = _ext.get(required=True)
+    d = x.shape[-1]
+    rows = x.numel() // d
+    dx = torch.empty_like(x)
+    part = torch.empty(_MAX_BLOCKS, 2 * d, device=x.device, dtype=torch.float32)
+    nb = C.layernorm_bwd(dy.data_ptr(), x.data_ptr(), _p(dh_ext), mean.data_ptr(), rstd.data_ptr(), _p(w32),
+                         dx.data_ptr(), part.data_ptr(), _MAX_BLOCKS, rows, d, DTYPE_CODE[x.dtype], _stream(x))
+    wb = None
+    if need_wb:
+        wb = torch.empty(2 * d, device=x.device, dtype=torch.float32)
+        C.gemm_splitk_reduce(part.data_ptr(), nb, 2 * d, wb.data_ptr(), 7, _stream(x))
+    return dx, wb
+
+
+class _LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        x = x.contiguous()
+        w32 = weight.float() if weight is not None else None
+        b32 = bias.float() if bias is not None else None
+        _, y, mean, rstd = _fwd(x, None, w32, b32, eps)
+        ctx.save_for_backward(x, w32, mean, rstd)
+        ctx.dtypes = (weight.dtype if weight is not None else None, bias.dtype if bias is not None else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w32, mean, rstd = ctx.saved_tensors
+        wd, bd = ctx.dtypes
+        dx, wb = _bwd(dy.contiguous(), x, None, mean, rstd, w32, wd is not None or bd is not None)
+        d = x.shape[-1]
+        dw = wb[:d].to(wd) if wd is not None else None
+        db = wb[d:].to(bd) if bd is not None else None
+        return dx, dw, db, None
+
+
+class _AddLayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, r, weight, bias, eps):
+        x, r = x.contiguous(), r.contiguous()
+        w32 = weight.float() if weight is not None else None
+        b32 = bias.float() if bias is not None else None
+        h, y, mean, rstd = _fwd(x, r, w32, b32, eps)
+        ctx.save_for_backward(h, w32, mean, rstd)
+        ctx.dtypes = (weight.dtype if weight is not None else None, bias.dtype if bias is not None else None)
+        return h, y
+
+    @staticmethod
+    def backward(ctx, dh, dy):
+        h, w32, mean, rstd = ctx.saved_tensors
+        wd, bd = ctx.dtypes
+        if dy is None:
+            dy = torch.zeros_like(h)
+        dh = dh.contiguous() if dh is not None else None
+        dx, wb = _bwd(dy.contiguous(), h, dh, mean, rstd, w32, wd is not None or bd is not None)
+        d = h.shape[-1]
+        dw = wb[:d].to(wd) if wd is not None else None
+        db = wb[d:].to(bd) if bd is not None else None
+        return dx, dx, dw, db, None  # h = x + r: both inputs get the same gradient
+
+
+def layer_norm(x, weight, bias, eps=1e-5):
+    if supported(x) and (weight is None or weight.shape[-1] == x.shape[-1]):
+        return _LayerNormFn.apply(x, weight, bias, eps)
+    return F.layer_norm(x, x.shape[-1:], weight, bias, eps)
+
+
+def add_layer_norm(x, r, weight, bias, eps=1e-5):
+    """``(h, layer_norm(h))`` with ``h = x + r``."""
+    if supported(x) and x.shape == r.shape and x.dtype == r.dtype:
+        return _AddLayerNormFn.apply(x, r, weight, bias, eps)
+    h = x + r
+    return h, F.layer_norm(h, h.shape[-1:], weight, bias, eps)
+
+
+class FusedLayerNorm(nn.LayerNorm):
+    """``nn.LayerNorm`` over the last dimension with the fused HIP kernels on the GPU."""
+
+    def forward(self, x):
+        if len(self.normalized_shape) != 1:
+            return super().forward(x)
+        return layer_norm(x, self.weight, self.bias, self.eps)
+
+    def add_forward(self, x, r):
+        return add_layer_norm(x, r, self.weight, self.bias, self.eps)
+
+
+__all__ = ["FusedLayerNorm", "layer_norm", "add_layer_norm"]

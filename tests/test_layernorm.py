@@ -1,0 +1,54 @@
+"""Fused LayerNorm (+ residual add) vs the PyTorch fp32 composition."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
+
+
+def test_add_layer_norm_cpu_fallback():
+    from fluxmpi_amd.ops.layernorm import FusedLayerNorm
+    ln = FusedLayerNorm(16)
+    x, r = torch.randn(3, 5, 16), torch.randn(3, 5, 16)
+    h, y = ln.add_forward(x, r)
+    torch.testing.assert_close(h, x + r)
+    torch.testing.assert_close(y, F.layer_norm(x + r, (16,), ln.weight, ln.bias, ln.eps))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(4, 197, 768), (3, 5, 64), (2, 7, 1032), (2, 3, 4096)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("add", [False, True])
+def test_layer_norm_vs_reference(gpu_ext, shape, dtype, add):
+    from fluxmpi_amd.ops.layernorm import add_layer_norm, layer_norm
+    torch.manual_seed(0)
+    d = shape[-1]
+    x = torch.randn(shape, device="cuda").to(dtype)
+    r = torch.randn(shape, device="cuda").to(dtype)
+    w = (torch.rand(d, device="cuda") + 0.5).to(dtype)
+    b = (torch.randn(d, device="cuda") * 0.1).to(dtype)
+    xa, ra, wa, ba = (t.clone().requires_grad_() for t in (x, r, w, b))
+    xr, rr, wr, br = (t.float().clone().requires_grad_() for t in (x, r, w, b))
+    if add:
+        h, y = add_layer_norm(xa, ra, wa, ba, 1e-6)
+        hr = (xr + rr).to(dtype).float()  # the kernel normalises the stored (rounded) h
+        yr = F.layer_norm(hr, (d,), wr, br, 1e-6)
+        torch.testing.assert_close(h.float(), (xr + rr).detach(), rtol=1e-2, atol=1e-2)
+        gh = torch.randn_like(yr)
+        gy = torch.randn_like(yr)
+        ((h.float() * gh).sum() + (y.float() * gy).sum()).backward()
+        ((hr * gh).sum() + (yr * gy).sum()).backward()
+    else:
+        y = layer_norm(xa, wa, ba, 1e-6)
+        yr = F.layer_norm(xr, (d,), wr, br, 1e-6)
+        gy = torch.randn_like(yr)
+        (y.float() * gy).sum().backward()
+        (yr * gy).sum().backward()
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    assert _rel(y, yr) < tol
+    assert _rel(xa.grad, xr.grad) < tol
+    assert _rel(wa.grad, wr.grad) < tol and _rel(ba.grad, br.grad) < tol
+    if add:
+        assert _rel(ra.grad, rr.grad) < tol
