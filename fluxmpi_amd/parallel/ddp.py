@@ -195,10 +195,13 @@ class DDP:
                 cur_bytes += nb
             if cur:
                 buckets.append(self._make_bucket(len(buckets), dt, cur, names))
-        # re-index in creation order (backward order within each dtype, dtypes interleaved
-        # by first appearance in backward order)
+        # launch order = expected completion order: a bucket is ready when its LAST parameter
+        # (in backward order) has its gradient. Ordering by the first parameter instead would
+        # put a small bucket of another dtype (ResNet's fp32 BatchNorm parameters, spread over
+        # the whole network) early in the sequence and hold every later bucket's allreduce
+        # until the end of backward. Identical on every rank (built from the parameter list).
         order = {id(p): i for i, p in enumerate(rev)}
-        buckets.sort(key=lambda b: order[id(b.params[0])])
+        buckets.sort(key=lambda b: max(order[id(p)] for p in b.params))
         for i, b in enumerate(buckets):
             b.index = i
         return buckets

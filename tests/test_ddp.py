@@ -150,3 +150,28 @@ def worker_ddp_resnet():
 
 def test_ddp_resnet_gloo(spmd):
     spmd("tests.test_ddp:worker_ddp_resnet", nprocs=2)
+
+
+def test_bucket_launch_order_mixed_dtypes():
+    """Buckets are ordered by when they complete (their last parameter in backward order):
+    a small bucket of another dtype spread over the whole model goes last instead of
+    blocking the in-order launches of every bucket after its first parameter."""
+    from fluxmpi_amd import optimisers as O
+    from fluxmpi_amd.parallel.ddp import DDP
+    torch.manual_seed(0)
+    layers = []
+    for _ in range(6):
+        layers += [torch.nn.Linear(64, 64), torch.nn.LayerNorm(64)]
+    model = torch.nn.Sequential(*layers)
+    for m in model:
+        if isinstance(m, torch.nn.Linear):
+            m.to(torch.float64)  # "bf16 weights": a different dtype from the norm parameters
+    ddp = DDP(model, O.Descent(0.1), bucket_mb=0.05, first_bucket_mb=0.02)
+    pos = {id(p): i for i, p in enumerate(reversed(list(model.parameters())))}
+    last = [max(pos[id(p)] for p in b.params) for b in ddp.buckets]
+    assert last == sorted(last)
+    # the norm parameters' bucket completes with the first LayerNorm: behind every float64
+    # bucket except the ones holding the first Linear (with the old first-parameter order
+    # it came second and blocked all of them)
+    kinds = [b.dtype for b in ddp.buckets]
+    assert len(kinds) > 4 and kinds.index(torch.float32) >= len(kinds) - 3
