@@ -176,7 +176,9 @@ __device__ __forceinline__ bf16x8 read_frag(const bf16* __restrict__ lds, int r0
 // NBUF = 2: double-buffered LDS, the next K-tile's loads overlap this tile's MFMAs
 // (compute-bound shapes). NBUF = 1: half the LDS, so twice the workgroups per CU —
 // for short K (memory-bound 1x1 convs) other workgroups' loads hide the latency.
-template <int BM, int BN, bool AK, bool BKM, int NBUF>
+// EX: epilogue extras (residual add, BN-backward statistics) compiled in; the plain variant
+// keeps the lean epilogue (its register footprint sets the occupancy of the main loop)
+template <int BM, int BN, bool AK, bool BKM, int NBUF, bool EX>
 __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs p) {
   using TA = Tile<BM, AK>;
   using TB = Tile<BN, BKM>;
@@ -293,24 +295,31 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs p) {
   const bool ncol_ok = n + 8 <= p.N;
   bf16* c = static_cast<bf16*>(p.c);
   float cs[8], cq[8];
-  float bmu[8], bis[8], bsc[8], bsh[8];  // BN-backward epilogue: per-column coefficients
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     cs[e] = 0.f;
     cq[e] = 0.f;
-    bmu[e] = bis[e] = bsc[e] = bsh[e] = 0.f;
   }
-  const bool bnb = p.mode == 1 && p.bnb_x != nullptr;
-  if (bnb) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int64_t col = n + e < p.N ? n + e : p.N - 1;
-      bmu[e] = p.bnb_mean[col];
-      bis[e] = p.bnb_inv[col];
-      bsc[e] = (p.bnb_w ? p.bnb_w[col] : 1.f) * bis[e];                 // == forward scale
-      bsh[e] = fmaf(-bmu[e], bsc[e], p.bnb_b ? p.bnb_b[col] : 0.f);     // == forward shift
+  const bool bnb = EX && p.mode == 1 && p.bnb_x != nullptr;
+  // BN-backward epilogue: per-column (mean, invstd, forward scale, forward shift) in LDS
+  // (registers would lower the occupancy of the whole kernel)
+  __shared__ float bcoef[EX ? 4 : 1][EX ? BN : 1];
+  if (EX && bnb) {
+    for (int col = threadIdx.x; col < BN; col += kThreads) {
+      const int64_t c = n0 + col < p.N ? n0 + col : p.N - 1;
+      const float mu = p.bnb_mean[c], iv = p.bnb_inv[c];
+      const float sc = (p.bnb_w ? p.bnb_w[c] : 1.f) * iv;  // == forward scale
+      bcoef[0][col] = mu;
+      bcoef[1][col] = iv;
+      bcoef[2][col] = sc;
+      bcoef[3][col] = fmaf(-mu, sc, p.bnb_b ? p.bnb_b[c] : 0.f);  // == forward shift
     }
   }
+  // rows this thread stores per pass; the residual / BN-input rows they need are fetched
+  // PB rows at a time (one latency per batch instead of one per row)
+  constexpr int NIT = (PR + RPI - 1) / RPI;
+  constexpr int PB = EX ? (NIT < 3 ? NIT : 3) : 1;
+  const bool want_res = EX && p.res != nullptr, want_x = bnb, want_mask = bnb && p.bnb_rm == 3;
 #pragma unroll
   for (int h = 0; h < NP; ++h) {
     if (h > 0) __syncthreads();  // previous pass fully read
@@ -325,58 +334,79 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs p) {
                 static_cast<bf16>(acc[i][j][r]);
     }
     __syncthreads();
-    for (int r = r0; r < PR; r += RPI) {
-      const int64_t m = m0 + h * PR + r;
-      if (m >= p.M) break;
-      uint4 v = *reinterpret_cast<const uint4*>(cl + r * CS + cc * 8);
-      if (p.res != nullptr) {  // fused residual add: C = bf16(bf16(A*B) + R)
-        bf16 e8[8], r8[8];
-        __builtin_memcpy(e8, &v, 16);
-        if (ncol_ok) {
-          const uint4 rv = *reinterpret_cast<const uint4*>(p.res + m * p.ldr + n);
-          __builtin_memcpy(r8, &rv, 16);
-        } else {
-          for (int e = 0; e < 8; ++e) r8[e] = n + e < p.N ? p.res[m * p.ldr + n + e] : static_cast<bf16>(0.f);
-        }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) e8[e] = static_cast<bf16>(static_cast<float>(e8[e]) + static_cast<float>(r8[e]));
-        __builtin_memcpy(&v, e8, 16);
+    for (int it0 = 0; it0 < NIT; it0 += PB) {
+      uint4 rv[PB], xv[PB];
+      unsigned mbv[PB];
+#pragma unroll
+      for (int b = 0; b < PB; ++b) {
+        const int r = r0 + (it0 + b) * RPI;
+        const int64_t m = m0 + h * PR + r;
+        const bool ok = it0 + b < NIT && r < PR && m < p.M && ncol_ok;
+        rv[b] = xv[b] = make_uint4(0, 0, 0, 0);
+        mbv[b] = 0u;
+        if (want_res && ok) rv[b] = *reinterpret_cast<const uint4*>(p.res + m * p.ldr + n);
+        if (want_x && ok) xv[b] = *reinterpret_cast<const uint4*>(p.bnb_x + m * p.N + n);
+        if (want_mask && ok) mbv[b] = p.bnb_mask[(m * p.N + n) >> 3];
       }
-      if (ncol_ok) {
-        *reinterpret_cast<uint4*>(c + m * p.ldc + n) = v;
-      } else {
-        const bf16* e8 = reinterpret_cast<const bf16*>(&v);
-        for (int e = 0; e < 8 && n + e < p.N; ++e) c[m * p.ldc + n + e] = e8[e];
-      }
-      if (bnb) {
-        bf16 e8[8], x8[8];
-        __builtin_memcpy(e8, &v, 16);
-        const int64_t xo = m * p.N + n;  // x is dense [M][N]
+#pragma unroll
+      for (int b = 0; b < PB; ++b) {
+        const int it = it0 + b;
+        const int r = r0 + it * RPI;
+        const int64_t m = m0 + h * PR + r;
+        if (it >= NIT || r >= PR || m >= p.M) continue;
+        uint4 v = *reinterpret_cast<const uint4*>(cl + r * CS + cc * 8);
+        if (want_res) {  // fused residual add: C = bf16(bf16(A*B) + R)
+          bf16 e8[8], r8[8];
+          __builtin_memcpy(e8, &v, 16);
+          if (ncol_ok) {
+            __builtin_memcpy(r8, &rv[b], 16);
+          } else {
+            for (int e = 0; e < 8; ++e) r8[e] = n + e < p.N ? p.res[m * p.ldr + n + e] : static_cast<bf16>(0.f);
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            e8[e] = static_cast<bf16>(static_cast<float>(e8[e]) + static_cast<float>(r8[e]));
+          __builtin_memcpy(&v, e8, 16);
+        }
         if (ncol_ok) {
-          const uint4 xv = *reinterpret_cast<const uint4*>(p.bnb_x + xo);
-          __builtin_memcpy(x8, &xv, 16);
+          *reinterpret_cast<uint4*>(c + m * p.ldc + n) = v;
         } else {
-          for (int e = 0; e < 8; ++e) x8[e] = n + e < p.N ? p.bnb_x[xo + e] : static_cast<bf16>(0.f);
+          const bf16* e8 = reinterpret_cast<const bf16*>(&v);
+          for (int e = 0; e < 8 && n + e < p.N; ++e) c[m * p.ldc + n + e] = e8[e];
         }
-        const unsigned mb = p.bnb_rm == 3 ? p.bnb_mask[xo >> 3] : 0xFFu;
+        if (bnb) {
+          bf16 e8[8], x8[8];
+          __builtin_memcpy(e8, &v, 16);
+          const int64_t xo = m * p.N + n;  // x is dense [M][N]
+          unsigned mb = 0xFFu;
+          if (ncol_ok) {
+            __builtin_memcpy(x8, &xv[b], 16);
+            if (want_mask) mb = mbv[b];
+          } else {
+            for (int e = 0; e < 8; ++e) x8[e] = n + e < p.N ? p.bnb_x[xo + e] : static_cast<bf16>(0.f);
+            if (want_mask) mb = p.bnb_mask[xo >> 3];
+          }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float xf = static_cast<float>(x8[e]);
-          bool keep = n + e < p.N;
-          if (p.bnb_rm == 2) keep = keep && fmaf(xf, bsc[e], bsh[e]) > 0.f;
-          if (p.bnb_rm == 3) keep = keep && ((mb >> e) & 1u);
-          const float dd = keep ? static_cast<float>(e8[e]) : 0.f;
-          cs[e] += dd;
-          cq[e] = fmaf(dd, (xf - bmu[e]) * bis[e], cq[e]);
-        }
-      } else if (p.mode == 1) {
-        bf16 e8[8];
-        __builtin_memcpy(e8, &v, 16);
+          for (int e = 0; e < 8; ++e) {
+            const int col = cc * 8 + e;
+            const float xf = static_cast<float>(x8[e]);
+            bool keep = n + e < p.N;
+            if (p.bnb_rm == 2) keep = keep && fmaf(xf, bcoef[2][col], bcoef[3][col]) > 0.f;
+            if (p.bnb_rm == 3) keep = keep && ((mb >> e) & 1u);
+            const float dd = keep ? static_cast<float>(e8[e]) : 0.f;
+            cs[e] += dd;
+            cq[e] = fmaf(dd, (xf - bcoef[0][col]) * bcoef[1][col], cq[e]);
+          }
+        } else if (p.mode == 1) {
+          bf16 e8[8];
+          __builtin_memcpy(e8, &v, 16);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float f = static_cast<float>(e8[e]);
-          cs[e] += f;
-          cq[e] = fmaf(f, f, cq[e]);
+          for (int e = 0; e < 8; ++e) {
+            const float f = static_cast<float>(e8[e]);
+            cs[e] += f;
+            cq[e] = fmaf(f, f, cq[e]);
+          }
         }
       }
     }
@@ -467,13 +497,13 @@ __global__ __launch_bounds__(kThreads) void splitk_reduce_kernel(float* __restri
   }
 }
 
-template <int BM, int BN, bool AK, bool BKM, int NBUF>
+template <int BM, int BN, bool AK, bool BKM, int NBUF, bool EX = false>
 void launch(const GemmArgs& a0, int splits, hipStream_t s) {
   GemmArgs a = a0;
   a.tiles_m = static_cast<int>((a.M + BM - 1) / BM);
   a.tiles_n = static_cast<int>((a.N + BN - 1) / BN);
   dim3 grid(a.tiles_m * a.tiles_n, 1, splits);
-  gemm_kernel<BM, BN, AK, BKM, NBUF><<<grid, kThreads, 0, s>>>(a);
+  gemm_kernel<BM, BN, AK, BKM, NBUF, EX><<<grid, kThreads, 0, s>>>(a);
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
 
@@ -531,6 +561,16 @@ void gemm_bf16(const GemmProblem& g, hipStream_t stream) {
   // double buffering measured faster for every ResNet-50 1x1 shape (fwd/dgrad/wgrad);
   // the single-buffered variant is kept selectable for experiments
   const bool single = g.nbuf == 1;
+  if (a.res != nullptr || a.bnb_x != nullptr) {
+    // epilogue extras: compiled for the dgrad layout (K-major dY, N-major W) only
+    if (!(g.a_kmajor && !g.b_kmajor) || single || splits != 1)
+      throw std::runtime_error("gemm_bf16: residual / BN-backward epilogues need the dgrad layout, NBUF 2, no split");
+    if (bm128 && bn128) launch<128, 128, true, false, 2, true>(a, 1, stream);
+    else if (bm128) launch<128, 64, true, false, 2, true>(a, 1, stream);
+    else if (bn128) launch<64, 128, true, false, 2, true>(a, 1, stream);
+    else launch<64, 64, true, false, 2, true>(a, 1, stream);
+    return;
+  }
   if (g.a_kmajor && g.b_kmajor) { DISPATCH(true, true) }
   else if (g.a_kmajor && !g.b_kmajor) { DISPATCH(true, false) }
   else if (!g.a_kmajor && !g.b_kmajor) { DISPATCH(false, false) }

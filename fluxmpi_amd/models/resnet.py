@@ -92,9 +92,10 @@ class Bottleneck(nn.Module):
                 # block's output) also reduces the previous block's bn3 backward statistics
                 link = fb.GradLink() if (self.downsample is None and x.requires_grad and grad) else None
                 prev = getattr(x, "_fluxmpi_bnlink", None) if link is not None else None
-                out_link = fb.BNStatsLink() if grad else None
+                bnl = grad and fb.BN_LINK
+                out_link = fb.BNStatsLink() if bnl else None
                 if self.hybrid:
-                    bl2 = fb.BNStatsLink() if grad else None  # bn2 -> conv3 (its only consumer)
+                    bl2 = fb.BNStatsLink() if bnl else None  # bn2 -> conv3 (its only consumer)
                     a1 = self.bn1(fb.conv1x1_hybrid(x, self.conv1.weight, link, prev), relu=True)
                     a2 = self.bn2(self.conv2(a1), relu=True, bnlink=bl2)
                     out = self.bn3(fb.conv1x1_hybrid(a2, self.conv3.weight, None, bl2), relu=True,

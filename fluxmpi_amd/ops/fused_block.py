@@ -26,12 +26,18 @@ recomputed in the backward match the forward bit for bit.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _ext
 from .batchnorm import BNStatsLink, GradLink, _workspace, bn_counter  # noqa: F401 (links re-exported)
 from .gemm import conv1x1_dgrad, conv1x1_wgrad, gemm
 from .multi_tensor import DTYPE_CODE
+
+
+# BNStatsLink on by default; FLUXMPI_BN_LINK=0 keeps every BatchNorm's own reduce pass (A/B)
+BN_LINK = os.environ.get("FLUXMPI_BN_LINK", "1") != "0"
 
 
 def _stream(t):

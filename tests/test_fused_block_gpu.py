@@ -98,7 +98,7 @@ def test_hybrid_conv_with_link(gpu_ext):
     ya = bn_a(torch.nn.functional.conv2d(xa, wa), relu=True, residual=xa)
     link = fb.GradLink()
     yb = bn_b(fb.conv1x1_hybrid(xb, wb, link), relu=True, residual=xb, link=link)
-    assert torch.equal(ya, yb)
+    assert _rel(yb, ya) < 1e-2  # batch statistics: float-atomic order differs between calls
     g = torch.randn_like(ya)
     (ya.float() * g).sum().backward()
     (yb.float() * g).sum().backward()
