@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--graph", action="store_true", help="capture the step in a HIP graph")
     ap.add_argument("--miopen-find", type=int, default=int(os.environ.get("BENCH_MIOPEN_FIND", "1")))
+    ap.add_argument("--tunableop", default=os.environ.get("BENCH_TUNABLEOP", "auto"), choices=["auto", "off"],
+                    help="auto: use the shipped hipBLASLt/rocBLAS GEMM selections (tuning/tunableop/<model>.csv)")
     return ap.parse_args()
 
 
@@ -55,6 +57,17 @@ def main():
     from fluxmpi_amd.models import build_model
     from fluxmpi_amd.parallel.ddp import DDP
 
+    # PyTorch TunableOp: per-shape GEMM solution choices recorded on MI355X (read-only here)
+    tuned = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuning", "tunableop", f"{args.model}.csv")
+    use_tunableop = args.tunableop == "auto" and os.path.exists(tuned) and "PYTORCH_TUNABLEOP_ENABLED" not in os.environ
+    if use_tunableop:
+        torch.cuda.tunable.enable(True)
+        torch.cuda.tunable.tuning_enable(False)
+        torch.cuda.tunable.record_untuned_enable(False) if hasattr(torch.cuda.tunable, "record_untuned_enable") else None
+        torch.cuda.tunable.read_file(tuned)
+        # results are written back at exit: keep that copy out of the repository
+        torch.cuda.tunable.set_filename(os.path.join(os.environ.get("TMPDIR", "/tmp"),
+                                                     f"fluxmpi_tunableop_{os.getuid()}_{args.model}.csv"))
     FluxMPI.Init()
     # MIOpen find mode, seeded with the tuning db recorded on MI355X (tuning/miopen): the
     # per-shape solver choice without the ~3.5 min search. --miopen-find 0: immediate mode.
@@ -137,7 +150,7 @@ def main():
             "config": {"model": mname, "global_batch": world * B, "per_gpu_batch": B, "seq_len": None,
                        "image_size": args.image, "parallelism": f"dp{world}", "optimizer": args.optimizer,
                        "conv": args.conv, "norm": args.norm, "backend": FluxMPI.backend_name(),
-                       "overlap": not args.no_overlap, "miopen_find": bool(args.miopen_find), "hip_graph": bool(args.graph), "loss": round(lval, 4),
+                       "overlap": not args.no_overlap, "miopen_find": bool(args.miopen_find), "hip_graph": bool(args.graph), "tunableop": use_tunableop, "loss": round(lval, 4),
                        "exposed_comm_ms": None if exposed is None else round(exposed, 3)},
         }
         print(json.dumps(rec), flush=True)
