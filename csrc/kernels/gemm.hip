@@ -563,8 +563,9 @@ void gemm_bf16(const GemmProblem& g, hipStream_t stream) {
   const bool single = g.nbuf == 1;
   if (a.res != nullptr || a.bnb_x != nullptr) {
     // epilogue extras: compiled for the dgrad layout (K-major dY, N-major W) only
-    if (!(g.a_kmajor && !g.b_kmajor) || single || splits != 1)
-      throw std::runtime_error("gemm_bf16: residual / BN-backward epilogues need the dgrad layout, NBUF 2, no split");
+    // (always double-buffered: the single-buffered variant is not compiled with extras)
+    if (!(g.a_kmajor && !g.b_kmajor) || splits != 1)
+      throw std::runtime_error("gemm_bf16: residual / BN-backward epilogues need the dgrad layout and no split");
     if (bm128 && bn128) launch<128, 128, true, false, 2, true>(a, 1, stream);
     else if (bm128) launch<128, 64, true, false, 2, true>(a, 1, stream);
     else if (bn128) launch<64, 128, true, false, 2, true>(a, 1, stream);

@@ -36,8 +36,11 @@ from .gemm import conv1x1_dgrad, conv1x1_wgrad, gemm
 from .multi_tensor import DTYPE_CODE
 
 
-# BNStatsLink on by default; FLUXMPI_BN_LINK=0 keeps every BatchNorm's own reduce pass (A/B)
-BN_LINK = os.environ.get("FLUXMPI_BN_LINK", "1") != "0"
+# BNStatsLink: off by default. Measured on MI355X (ResNet-50 bs256, hybrid): the epilogue's
+# extra read of the BN input makes the dgrad GEMMs +1.4 ms/step slower while the removed
+# reduce passes save 1.05 ms — a net loss until the GEMM epilogue streams as well as the
+# BN kernels do. FLUXMPI_BN_LINK=1 enables it (numerics covered by tests either way).
+BN_LINK = os.environ.get("FLUXMPI_BN_LINK", "0") == "1"
 
 
 def _stream(t):

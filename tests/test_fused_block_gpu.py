@@ -23,13 +23,15 @@ def _models(impl="fused"):
     return ref, fus
 
 
-@pytest.mark.parametrize("impl", ["fused", "hybrid"])
-def test_fused_resnet_matches_unfused(gpu_ext, impl):
+@pytest.mark.parametrize("impl", ["fused", "hybrid", "fused+bnlink", "hybrid+bnlink"])
+def test_fused_resnet_matches_unfused(gpu_ext, impl, monkeypatch):
     """Both bf16 pipelines are compared with an fp32 model holding the same (bf16-rounded)
     weights: the fused pipeline must be about as accurate as the unfused one. Layer 1 has an
     identity block, so the GradLink residual-gradient hand-off is exercised."""
     from fluxmpi_amd.models.resnet import ResNet
-    ref, fus = _models(impl)
+    from fluxmpi_amd.ops import fused_block as fb
+    monkeypatch.setattr(fb, "BN_LINK", impl.endswith("+bnlink"))
+    ref, fus = _models(impl.split("+")[0])
     f32 = ResNet((2, 1, 1, 1), 10, conv_impl="miopen", norm="fused").cuda().to(memory_format=torch.channels_last)
     f32.load_state_dict({k: v.float() if v.is_floating_point() else v for k, v in ref.state_dict().items()})
     x = torch.randn(8, 3, 64, 64, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
@@ -118,12 +120,13 @@ def test_bn_stats_link(gpu_ext, with_res):
     c = torch.randn(4, 128, 14, 14, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
     r = torch.randn_like(c) if with_res else None
     w = (torch.randn(64, 128, 1, 1, device="cuda") * 0.1).bfloat16()
+    bn_w, bn_b = torch.rand(128, device="cuda") + 0.5, torch.rand(128, device="cuda") * 0.4 - 0.2
     grads = []
     for use_link in (False, True):
         bn = FusedBatchNorm2d(128).cuda()
         with torch.no_grad():
-            bn.weight.uniform_(0.5, 1.5)
-            bn.bias.uniform_(-0.2, 0.2)
+            bn.weight.copy_(bn_w)
+            bn.bias.copy_(bn_b)
         ci, wi = c.clone().requires_grad_(), w.clone().requires_grad_()
         ri = r.clone().requires_grad_() if with_res else None
         link = fb.BNStatsLink() if use_link else None
