@@ -38,7 +38,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=int(os.environ.get("BENCH_BATCH", "256")), help="per-GPU batch")
     ap.add_argument("--model", default="resnet50")
-    ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--image", type=int, default=None, help="input resolution (default: 224; DEQ: 28, MNIST-shaped)")
     ap.add_argument("--conv", default=os.environ.get("BENCH_CONV", "hybrid"), choices=["gemm", "miopen", "fused", "hybrid"])
     ap.add_argument("--norm", default=os.environ.get("BENCH_NORM", "fused"), choices=["torch", "fused"])
     ap.add_argument("--optimizer", default="adam", choices=["adam", "momentum"])
@@ -52,6 +52,8 @@ def parse():
 
 def main():
     args = parse()
+    if args.image is None:
+        args.image = 28 if args.model == "deq" else 224
     import fluxmpi_amd as FluxMPI
     from fluxmpi_amd import optimisers as O
     from fluxmpi_amd.models import build_model

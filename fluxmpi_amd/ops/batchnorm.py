@@ -90,7 +90,7 @@ class BNStatsLink:
     that BatchNorm's backward reductions — sum(dy_eff), sum(dy_eff * xhat) — in its epilogue,
     so the BatchNorm backward skips its reduce pass over (dy, x).
 
-    The BatchNorm's forward ``bind``\ s its saved tensors; the consumer's backward runs the
+    The BatchNorm's forward binds its saved tensors; the consumer's backward runs the
     GEMM with the BN-backward epilogue into the shared statistics workspace and sets
     ``ready``; the BatchNorm's backward then only finalizes and applies. Valid only when the
     linked consumer's dgrad output IS the whole gradient of the BatchNorm output (a single
