@@ -81,34 +81,65 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
         self.fused = norm == "fused"
 
+    def _fused_downsample(self) -> bool:
+        ds = self.downsample
+        return (ds is not None and len(ds) == 2 and isinstance(ds[0], nn.Conv2d) and ds[0].kernel_size == (1, 1)
+                and ds[0].bias is None and ds[0].padding == (0, 0) and ds[0].stride[0] == ds[0].stride[1]
+                and ds[0].groups == 1 and ds[0].dilation == (1, 1))
+
     def forward(self, x):
-        identity = x if self.downsample is None else self.downsample(x)
         if (self.gemm_fused or self.hybrid) and self.training:
             from ..ops import fused_block as fb
             if fb.supported(x, *self.dims):
                 grad = torch.is_grad_enabled()
+                needs = x.requires_grad and grad
                 # identity blocks: bn3's residual gradient goes straight into conv1's dgrad epilogue,
                 # and that epilogue (whose output is then the whole gradient of the previous
-                # block's output) also reduces the previous block's bn3 backward statistics
-                link = fb.GradLink() if (self.downsample is None and x.requires_grad and grad) else None
-                prev = getattr(x, "_fluxmpi_bnlink", None) if link is not None else None
+                # block's output) also reduces the previous block's bn3 backward statistics.
+                # downsample blocks: the downsample conv's input gradient goes into that epilogue.
+                fused_ds = self.downsample is not None and self._fused_downsample()
+                if self.downsample is None:
+                    link = fb.GradLink() if needs else None
+                else:
+                    link = fb.SideGradLink() if (needs and fused_ds) else None
+                prev = getattr(x, "_fluxmpi_bnlink", None) if (link is not None and self.downsample is None) else None
                 bnl = grad and fb.BN_LINK
                 out_link = fb.BNStatsLink() if bnl else None
                 if self.hybrid:
-                    bl2 = fb.BNStatsLink() if bnl else None  # bn2 -> conv3 (its only consumer)
                     a1 = self.bn1(fb.conv1x1_hybrid(x, self.conv1.weight, link, prev), relu=True)
-                    a2 = self.bn2(self.conv2(a1), relu=True, bnlink=bl2)
-                    out = self.bn3(fb.conv1x1_hybrid(a2, self.conv3.weight, None, bl2), relu=True,
-                                   residual=identity, link=link, bnlink=out_link)
                 else:
                     c1 = fb.conv1x1_stats(x, self.conv1.weight, link, prev)  # + bn1 statistics (GEMM epilogue)
                     a1 = fb.bn_from_stats(c1, self.bn1, relu=True)
+                # the downsample branch is built AFTER conv1: autograd runs ready nodes newest-first
+                # and conv1's backward becomes ready last, so the downsample conv's backward (which
+                # offers its input gradient to conv1's dgrad through the SideGradLink) runs before
+                # it. (And after bn1 consumed conv1's epilogue statistics: the downsample BN uses
+                # the same statistics workspace.)
+                if self.downsample is None:
+                    identity = x
+                elif fused_ds:
+                    ds = self.downsample
+                    identity = ds[1](fb.conv1x1_downsample(x, ds[0].weight, ds[0].stride[0],
+                                                           link if isinstance(link, fb.SideGradLink) else None))
+                else:
+                    identity = self.downsample(x)
+                if self.hybrid:
+                    bl2 = fb.BNStatsLink() if bnl else None  # bn2 -> conv3 (its only consumer)
+                    a2 = self.bn2(self.conv2(a1), relu=True, bnlink=bl2)
+                    c3 = fb.conv1x1_hybrid(a2, self.conv3.weight, None, bl2)
+                else:
                     c2 = self.conv2(a1)
                     c3 = fb.bn_relu_conv1x1(c2, self.bn2, self.conv3.weight)  # bn2+relu fused into the A load
-                    out = fb.bn_from_stats(c3, self.bn3, relu=True, residual=identity, link=link, bnlink=out_link)
+                if self.hybrid:
+                    out = self.bn3(c3, relu=True, residual=identity, link=link if self.downsample is None else None,
+                                   bnlink=out_link)
+                else:
+                    out = fb.bn_from_stats(c3, self.bn3, relu=True, residual=identity,
+                                           link=link if self.downsample is None else None, bnlink=out_link)
                 if out_link is not None:
                     out._fluxmpi_bnlink = out_link  # for the next block's conv1 (used iff it is an identity block)
                 return out
+        identity = x if self.downsample is None else self.downsample(x)
         if self.fused:
             out = self.bn1(self.conv1(x), relu=True)
             out = self.bn2(self.conv2(out), relu=True)

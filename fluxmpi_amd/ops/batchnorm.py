@@ -85,6 +85,34 @@ class GradLink:
         return g
 
 
+class SideGradLink:
+    """Like :class:`GradLink`, for a producer that autograd does NOT order before the
+    consumer by data dependency: the downsample convolution of a ResNet block, whose input
+    gradient is the second summand of the block input's gradient (the first is conv1's
+    dgrad). Autograd runs ready nodes newest-first, so the downsample branch (created after
+    the main path) normally runs first and :meth:`offer` hands its gradient over; if the
+    consumer ran first, it has closed the link and the producer returns its gradient to
+    autograd as usual — correct either way, never dropped or double counted."""
+
+    __slots__ = ("grad", "closed", "delivered")
+
+    def __init__(self):
+        self.grad = None
+        self.closed = False
+        self.delivered = False  # the consumer added the producer's gradient (diagnostics/tests)
+
+    def offer(self, g: torch.Tensor) -> bool:
+        if self.closed:
+            return False
+        self.grad = g
+        return True
+
+    def take(self):
+        g, self.grad, self.closed = self.grad, None, True
+        self.delivered = g is not None
+        return g
+
+
 class BNStatsLink:
     """Lets the kernel that produces a BatchNorm's output gradient (a dgrad GEMM) accumulate
     that BatchNorm's backward reductions — sum(dy_eff), sum(dy_eff * xhat) — in its epilogue,

@@ -31,7 +31,7 @@ import os
 import torch
 
 from . import _ext
-from .batchnorm import BNStatsLink, GradLink, _workspace, bn_counter  # noqa: F401 (links re-exported)
+from .batchnorm import BNStatsLink, GradLink, SideGradLink, _workspace, bn_counter  # noqa: F401 (links re-exported)
 from .gemm import conv1x1_dgrad, conv1x1_wgrad, gemm
 from .multi_tensor import DTYPE_CODE
 
@@ -112,7 +112,10 @@ def _dgrad_nhwc(dc2, weight, x, link, bnlink=None):
     co, ci = weight.shape[0], weight.shape[1]
     n, _, h, w = x.shape
     dx = _empty_nhwc(n, ci, h, w, x)
-    res = _nhwc2d(link.take()) if link is not None else None
+    res = None
+    if link is not None:
+        g = link.take()  # SideGradLink: None if its producer has not run (it then returns its own)
+        res = _nhwc2d(g) if g is not None else None
     bn = stats = None
     if bnlink is not None and bnlink.bound and bnlink.x.shape == x.shape and \
             bnlink.x.is_contiguous(memory_format=torch.channels_last):
@@ -147,6 +150,42 @@ class _Conv1x1Hybrid(torch.autograd.Function):
             dw = torch.ops.aten.convolution_backward(dc, x, weight, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
                                                      [False, True, False])[1]
         return dx, dw, None, None
+
+
+class _Conv1x1Downsample(torch.autograd.Function):
+    """The downsample 1x1 convolution (stride 1 or 2) of a ResNet block, MIOpen forward and
+    weight gradient. Its input gradient (our dgrad GEMM at stride 1, MIOpen's strided dgrad
+    at stride 2) is handed to the block's conv1 through a :class:`SideGradLink`, whose dgrad
+    epilogue adds it: no separate add kernel over the block input's gradient."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride, link):
+        x = x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
+        ctx.stride, ctx.link = stride, link
+        ctx.save_for_backward(x, weight)
+        return torch.nn.functional.conv2d(x, weight, None, stride)
+
+    @staticmethod
+    def backward(ctx, dc):
+        x, weight = ctx.saved_tensors
+        if not dc.is_contiguous(memory_format=torch.channels_last):
+            dc = dc.contiguous(memory_format=torch.channels_last)
+        s = ctx.stride
+        need_x, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        dx = dw = None
+        if s == 1 and need_x:
+            dx = _dgrad_nhwc(_nhwc2d(dc), weight, x, None)
+        if need_w or (need_x and dx is None):
+            dx_m, dw = torch.ops.aten.convolution_backward(dc, x, weight, None, [s, s], [0, 0], [1, 1], False,
+                                                           [0, 0], 1, [need_x and dx is None, need_w, False])[:2]
+            dx = dx if dx is not None else dx_m
+        if dx is not None and ctx.link is not None and ctx.link.offer(dx):
+            dx = None  # delivered to conv1's dgrad epilogue
+        return dx, dw, None, None
+
+
+def conv1x1_downsample(x, weight, stride, link=None):
+    return _Conv1x1Downsample.apply(x, weight, stride, link)
 
 
 class _BNFromStats(torch.autograd.Function):

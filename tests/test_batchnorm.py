@@ -147,3 +147,16 @@ def test_bn_relu_maxpool_cpu_fallback():
     y = bn_relu_maxpool(x, bn)
     torch.testing.assert_close(y, F.max_pool2d(F.relu(ref(x)), 3, 2, 1))
     torch.testing.assert_close(bn.running_mean, ref.running_mean)
+
+
+def test_side_grad_link_never_drops_or_doubles():
+    """SideGradLink: delivered when the producer runs first; handed back to autograd when the
+    consumer already ran (closed link) — the gradient is counted exactly once either way."""
+    from fluxmpi_amd.ops.batchnorm import SideGradLink
+    g = torch.ones(3)
+    lk = SideGradLink()
+    assert lk.offer(g)  # producer first: accepted
+    assert lk.take() is g and lk.delivered and lk.grad is None
+    lk = SideGradLink()
+    assert lk.take() is None and not lk.delivered  # consumer first: closes the link
+    assert not lk.offer(g)  # producer must return its gradient itself

@@ -109,6 +109,37 @@ def test_hybrid_conv_with_link(gpu_ext):
     assert _rel(bn_b.weight.grad, bn_a.weight.grad) < 1e-4  # float atomics: order-dependent rounding
 
 
+@pytest.mark.parametrize("impl", ["hybrid", "fused"])
+def test_downsample_grad_delivered(gpu_ext, impl, monkeypatch):
+    """Every downsample block (stride 1 in layer 1, stride 2 after) hands its input gradient to
+    conv1's dgrad epilogue (autograd's newest-first order runs the downsample branch first), so
+    no add kernel sums the block input's two gradients; the gradients equal the plain model's."""
+    from fluxmpi_amd.ops import fused_block as fb
+    links = []
+
+    class Recording(fb.SideGradLink):
+        __slots__ = ()
+
+        def __init__(self):
+            super().__init__()
+            links.append(self)
+
+    monkeypatch.setattr(fb, "SideGradLink", Recording)
+    from fluxmpi_amd.models.resnet import ResNet
+    ref, fus = _models(impl)
+    f32 = ResNet((2, 1, 1, 1), 10, conv_impl="miopen", norm="fused").cuda().to(memory_format=torch.channels_last)
+    f32.load_state_dict({k: v.float() if v.is_floating_point() else v for k, v in ref.state_dict().items()})
+    x = torch.randn(8, 3, 64, 64, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    ya, yb, yc = ref(x), fus(x), f32(x.float())
+    g = torch.randn_like(yc)
+    for y in (ya, yb, yc):
+        (y.float() * g).sum().backward()
+    assert len(links) == 4 and all(lk.delivered and lk.grad is None for lk in links)
+    for (n, pa), pb, pc in zip(ref.named_parameters(), fus.parameters(), f32.parameters()):
+        ea, eb = _rel(pa.grad, pc.grad), _rel(pb.grad, pc.grad)
+        assert eb < 2 * ea + 2e-2, f"{n}: linked {eb:.3e} vs unlinked {ea:.3e}"
+
+
 @pytest.mark.parametrize("with_res", [False, True])
 def test_bn_stats_link(gpu_ext, with_res):
     """BN -> 1x1 conv (its only consumer): the conv's dgrad epilogue reduces the BN backward
