@@ -140,8 +140,21 @@ struct GemmProblem {
   const float* bnb_inv;
   const uint8_t* bnb_mask;
   int bnb_rm;
+  // conv_h > 0: A is implicit — the 3x3 / stride 1 / pad 1 im2col of an NHWC image batch
+  // [M/(H*W)][H][W][conv_c] (K = 9*conv_c, K-major B = [N][3][3][conv_c] filter)
+  int conv_h = 0, conv_w = 0, conv_c = 0;
+  int engine = 0;  // 0 auto, 1 register-staged kernel (gemm.hip), 2 LDS-DMA pipelined kernel (gemm_glds.hip)
 };
 void gemm_bf16(const GemmProblem& g, hipStream_t stream);
+// the LDS-DMA pipelined kernel: K-major A (or implicit conv) and B, modes 0/1, optional residual,
+// no prologue affine / split-K / BN-backward epilogue
+bool gemm_glds_supported(const GemmProblem& g);
+void gemm_glds(const GemmProblem& g, hipStream_t stream);
+// out_i[ci][t][co] = in_i[co][taps-1-t][ci] (bf16) for every filter i, one launch per 40 filters:
+// the K-major B operand of the input-gradient GEMMs (1x1: W^T; 3x3: transposed + flipped)
+void transpose_filters(const std::vector<uintptr_t>& src, const std::vector<uintptr_t>& dst,
+                       const std::vector<int>& co, const std::vector<int>& ci, const std::vector<int>& taps,
+                       hipStream_t stream);
 // out[e] = sum over s < splits of ws[s*n + e] (mode-3 split-K partials; ws is clobbered); out fp32 or bf16
 void gemm_splitk_reduce(const float* ws, int splits, int64_t n, void* out, int out_dtype, hipStream_t stream);
 

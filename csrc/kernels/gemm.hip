@@ -71,6 +71,10 @@ struct GemmArgs {
   int bnb_rm;
   int mode;      // 0: store bf16; 1: store bf16 + stats; 2: fp32 atomic add into c
   int tiles_m, tiles_n;
+  // implicit 3x3 / stride 1 / pad 1 convolution (CONV kernels): A row m is output pixel m of an
+  // NHWC image batch [M / (H*W)][H][W][C]; K = 9*C ordered (tap r*3+s, channel); K-tile t reads
+  // the C-slice of tap t*BK/C from pixel m + (r-1)*W + (s-1) (zero outside the image)
+  int conv_h, conv_w, conv_c;
 };
 
 template <int ROWS, bool KMAJOR>
@@ -132,6 +136,32 @@ __device__ __forceinline__ void stage_load(uint4 (&reg)[CPT],
   }
 }
 
+// Implicit-convolution A tile (K-major, BK channels of one tap per K-tile): chunk i of this
+// thread is row r_i of the tile, whose output pixel lies at image position (ph[i], pw[i]).
+template <int ROWS, int CPT>
+__device__ __forceinline__ void stage_load_conv(uint4 (&reg)[CPT], const bf16* __restrict__ x, int64_t rows,
+                                                int64_t r0, int64_t k0, const int (&ph)[CPT], const int (&pw)[CPT],
+                                                int H, int W, int C, const float* __restrict__ sc,
+                                                const float* __restrict__ sh) {
+  const int tap = static_cast<int>(k0 / C);
+  const int c0 = static_cast<int>(k0 - static_cast<int64_t>(tap) * C);
+  const int dr = tap / 3 - 1, ds = tap % 3 - 1;
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int idx = threadIdx.x + i * kThreads;
+    const int r = idx / (BK / 8), kc = idx % (BK / 8);
+    const int64_t row = r0 + r;
+    uint4 v = make_uint4(0, 0, 0, 0);  // zero padding of the (activated) input
+    if (row < rows && static_cast<unsigned>(ph[i] + dr) < static_cast<unsigned>(H) &&
+        static_cast<unsigned>(pw[i] + ds) < static_cast<unsigned>(W)) {
+      const int64_t pix = row + dr * W + ds;
+      v = *reinterpret_cast<const uint4*>(x + pix * C + c0 + kc * 8);
+      if (sc != nullptr) affine_relu8(v, sc, sh, c0 + kc * 8);
+    }
+    reg[i] = v;
+  }
+}
+
 template <int ROWS, bool KMAJOR, int CPT>
 __device__ __forceinline__ void stage_store(bf16* __restrict__ lds, const uint4 (&reg)[CPT]) {
   constexpr int S = Tile<ROWS, KMAJOR>::kStride;
@@ -178,7 +208,7 @@ __device__ __forceinline__ bf16x8 read_frag(const bf16* __restrict__ lds, int r0
 // for short K (memory-bound 1x1 convs) other workgroups' loads hide the latency.
 // EX: epilogue extras (residual add, BN-backward statistics) compiled in; the plain variant
 // keeps the lean epilogue (its register footprint sets the occupancy of the main loop)
-template <int BM, int BN, bool AK, bool BKM, int NBUF, bool EX>
+template <int BM, int BN, bool AK, bool BKM, int NBUF, bool EX, bool CONV = false>
 __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs p) {
   using TA = Tile<BM, AK>;
   using TB = Tile<BN, BKM>;
@@ -213,10 +243,26 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  uint4 ra[TA::kChunks / kThreads], rb[TB::kChunks / kThreads];
+  constexpr int CA = TA::kChunks / kThreads;
+  uint4 ra[CA], rb[TB::kChunks / kThreads];
+  // CONV: image position of the output pixel of each A row this thread stages (fixed over K)
+  int ph[CA], pw[CA];
+  if (CONV) {
+#pragma unroll
+    for (int i = 0; i < CA; ++i) {
+      const int64_t row = m0 + (threadIdx.x + i * kThreads) / (BK / 8);
+      const int hw = static_cast<int>(row % (static_cast<int64_t>(p.conv_h) * p.conv_w));
+      ph[i] = hw / p.conv_w;
+      pw[i] = hw - ph[i] * p.conv_w;
+    }
+  }
+  auto load_a = [&](int64_t k0) {
+    if (CONV) stage_load_conv<BM>(ra, p.a, p.M, m0, k0, ph, pw, p.conv_h, p.conv_w, p.conv_c, p.a_scale, p.a_shift);
+    else stage_load<BM, AK>(ra, p.a, p.lda, p.M, m0, k0, p.a_scale, p.a_shift, kend);
+  };
   const int64_t nk = (kend - kbeg + BK - 1) / BK;  // last K-tile may be partial (zero-filled)
   if (nk > 0) {
-    stage_load<BM, AK>(ra, p.a, p.lda, p.M, m0, kbeg, p.a_scale, p.a_shift, kend);
+    load_a(kbeg);
     stage_load<BN, BKM>(rb, p.b, p.ldb, p.N, n0, kbeg, p.b_scale, p.b_shift, kend);
     stage_store<BM, AK>(la(0), ra);
     stage_store<BN, BKM>(lb(0), rb);
@@ -233,7 +279,7 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs p) {
     }
     if (more) {  // issue next tile's global loads before this tile's MFMAs
       const int64_t k1 = kbeg + (t + 1) * BK;
-      stage_load<BM, AK>(ra, p.a, p.lda, p.M, m0, k1, p.a_scale, p.a_shift, kend);
+      load_a(k1);
       stage_load<BN, BKM>(rb, p.b, p.ldb, p.N, n0, k1, p.b_scale, p.b_shift, kend);
     }
     bf16x8 fa[FM], fb[FN];
@@ -497,19 +543,24 @@ __global__ __launch_bounds__(kThreads) void splitk_reduce_kernel(float* __restri
   }
 }
 
-template <int BM, int BN, bool AK, bool BKM, int NBUF, bool EX = false>
+template <int BM, int BN, bool AK, bool BKM, int NBUF, bool EX = false, bool CONV = false>
 void launch(const GemmArgs& a0, int splits, hipStream_t s) {
   GemmArgs a = a0;
   a.tiles_m = static_cast<int>((a.M + BM - 1) / BM);
   a.tiles_n = static_cast<int>((a.N + BN - 1) / BN);
   dim3 grid(a.tiles_m * a.tiles_n, 1, splits);
-  gemm_kernel<BM, BN, AK, BKM, NBUF, EX><<<grid, kThreads, 0, s>>>(a);
+  gemm_kernel<BM, BN, AK, BKM, NBUF, EX, CONV><<<grid, kThreads, 0, s>>>(a);
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
 
 }  // namespace
 
 void gemm_bf16(const GemmProblem& g, hipStream_t stream) {
+  // engine 0 (auto): the LDS-DMA pipelined kernel for every problem it covers
+  if (g.engine >= 2 || (g.engine == 0 && gemm_glds_supported(g))) {
+    gemm_glds(g, stream);
+    return;
+  }
   if ((g.a_kmajor || g.b_kmajor) && g.K % 8 != 0) throw std::runtime_error("gemm_bf16: K-major operands need K % 8 == 0");
   if ((g.a_kmajor ? g.lda : g.lda) % 8 != 0 || g.ldb % 8 != 0)
     throw std::runtime_error("gemm_bf16: leading dimensions must be multiples of 8");
@@ -551,6 +602,22 @@ void gemm_bf16(const GemmProblem& g, hipStream_t stream) {
     throw std::runtime_error("gemm_bf16: split-K needs mode 2 (fp32 atomics) or 3 (fp32 partials)");
   const bool bm128 = g.M >= 128 && g.tile_m != 64;
   const bool bn128 = g.N >= 128 && g.tile_n != 64;
+  if (g.conv_h > 0) {
+    // implicit 3x3/s1/p1 convolution: A = NHWC image (K = 9*C), B = K-major [N][9*C] filter
+    if (!g.a_kmajor || !g.b_kmajor || g.conv_c % BK != 0 || g.K != 9LL * g.conv_c || g.conv_w <= 0 ||
+        g.M % (static_cast<int64_t>(g.conv_h) * g.conv_w) != 0 || splits != 1 || g.mode > 1 ||
+        a.res != nullptr || a.bnb_x != nullptr)
+      throw std::runtime_error("gemm_bf16: implicit conv needs K-major A/B, C % 32 == 0, K == 9*C, M a multiple of "
+                               "H*W, no split and mode 0/1 without residual / BN-backward epilogue");
+    a.conv_h = g.conv_h;
+    a.conv_w = g.conv_w;
+    a.conv_c = g.conv_c;
+    if (bm128 && bn128) launch<128, 128, true, true, 2, false, true>(a, 1, stream);
+    else if (bm128) launch<128, 64, true, true, 2, false, true>(a, 1, stream);
+    else if (bn128) launch<64, 128, true, true, 2, false, true>(a, 1, stream);
+    else launch<64, 64, true, true, 2, false, true>(a, 1, stream);
+    return;
+  }
 #define DISPATCH2(AK, BKM, NB)                                          \
   if (bm128 && bn128) launch<128, 128, AK, BKM, NB>(a, splits, stream);  \
   else if (bm128) launch<128, 64, AK, BKM, NB>(a, splits, stream);       \

@@ -1,0 +1,422 @@
+// Pipelined MFMA bf16 GEMM (C = A * B^T, both operands K-major) with direct global->LDS
+// staging — gfx950.
+//
+// The register-staged kernel in gemm.hip keeps one K-tile in flight: the next tile's global
+// loads are issued before the current tile's MFMAs and must land before the LDS store that
+// follows them, so at a 32-deep K-tile (256 MFMA cycles per wave) an L2 round trip is exposed
+// on every step. Here the operand tiles go straight from global memory into LDS with
+// `global_load_lds_dwordx4` (no staging registers, no ds_write pass) through a ring of
+// kStages LDS stages, kStages-1 tiles in flight: a wave waits with a counted
+// `s_waitcnt vmcnt(N)` for the OLDEST tile only, then a raw `s_barrier` (never
+// __syncthreads(), whose fence would drain the younger DMAs) publishes it to all waves.
+//
+// LDS image of a stage: [rows][32] bf16 (64 B rows, no padding: an LDS-DMA writes
+// lane-linear 1 KiB pieces = 16 rows). The 16-B chunk q of row r sits in slot
+// q ^ ((r >> 2) & 3) — the swizzle is applied on the per-lane GLOBAL source address — so
+// the 16 lanes of a ds_read_b128 fragment read (16 rows, one chunk) hit 16 distinct
+// 16-B bank groups.
+//
+// A is either a plain K-major matrix or (CONV) the implicit im2col of a 3x3 / stride 1 /
+// pad 1 convolution over an NHWC image batch; out-of-image taps read a line of zeros.
+// Epilogue: bf16 C staged through LDS (16-B stores), optional residual add, optional
+// per-column sum / sum of squares into the sharded BatchNorm workspace (mode 1).
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../api.h"
+#include "common.h"
+
+namespace fluxmpi {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+constexpr int kThreads = 256;
+constexpr int kShards = 64;  // must match batchnorm.hip
+
+__device__ __attribute__((aligned(16))) uint4 g_zero_line[4];  // source of zero-filled chunks
+
+struct GldsArgs {
+  const bf16* a;
+  const bf16* b;
+  bf16* c;
+  const bf16* res;
+  float* stats;
+  int64_t lda, ldb, ldc, ldr;
+  int64_t M, N, K;
+  int mode;  // 0: C; 1: C + column statistics
+  int tiles_m, tiles_n;
+  int conv_h, conv_w, conv_c;
+};
+
+// s_waitcnt vmcnt(N) with expcnt / lgkmcnt left alone (gfx9 encoding)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+template <int LPT, int MAXAHEAD>
+__device__ __forceinline__ void wait_tiles_ahead(int ahead) {
+  if (MAXAHEAD >= 2 && ahead >= 2) wait_vmcnt<(MAXAHEAD >= 2 ? 2 : 0) * LPT>();
+  else if (ahead == 1) wait_vmcnt<LPT>();
+  else wait_vmcnt<0>();
+}
+
+// chunk-slot swizzle of a [rows][BK] bf16 stage tile (BK/8 16-B chunks per row): the 16 rows of
+// a ds_read_b128 fragment read land in 16 distinct 16-B bank groups of the 256-B bank row
+template <int BK>
+__device__ __forceinline__ int swz(int row) {
+  return BK == 32 ? ((row >> 2) & 3) : ((row >> 1) & 7);
+}
+
+// Issue this wave's LDS-DMA pieces of one operand tile (ROWS x BK) for K offset k0.
+// A 1 KiB piece holds RPP = 512/BK rows; piece j of wave w covers tile rows
+// (w * PPW + j) * RPP ..; lane l fills row +(l / CPR), slot (l % CPR) with global chunk
+// slot ^ swz(row).
+template <int ROWS, int BK, bool CONV>
+__device__ __forceinline__ void issue_tile(bf16* lds_tile, const bf16* __restrict__ g, int64_t ld,
+                                           int64_t rows, int64_t r0, int64_t k0, int64_t kend,
+                                           const int* ph, const int* pw, int H, int W, int C) {
+  constexpr int CPR = BK / 8, RPP = 64 / CPR;
+  constexpr int PPW = ROWS * BK / 2048;  // 1 KiB pieces per wave
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  int dr = 0, ds = 0, c0 = 0;
+  if (CONV) {
+    const int tap = static_cast<int>(k0 / C);
+    c0 = static_cast<int>(k0 - static_cast<int64_t>(tap) * C);
+    dr = tap / 3 - 1;
+    ds = tap % 3 - 1;
+  }
+#pragma unroll
+  for (int j = 0; j < PPW; ++j) {
+    const int piece = wave * PPW + j;
+    const int row = piece * RPP + lane / CPR;
+    const int q = (lane % CPR) ^ swz<BK>(row);
+    const int64_t grow = r0 + row;
+    const void* src = g_zero_line;
+    if (CONV) {
+      if (grow < rows && static_cast<unsigned>(ph[j] + dr) < static_cast<unsigned>(H) &&
+          static_cast<unsigned>(pw[j] + ds) < static_cast<unsigned>(W))
+        src = g + (grow + dr * W + ds) * C + c0 + q * 8;
+    } else {
+      if (grow < rows && k0 + q * 8 < kend) src = g + grow * ld + k0 + q * 8;
+    }
+    typedef __attribute__((address_space(3))) char lds_char;
+    typedef __attribute__((address_space(1))) void gl_void;
+    __builtin_amdgcn_global_load_lds((gl_void*)(src), (lds_char*)(reinterpret_cast<char*>(lds_tile) + piece * 1024), 16,
+                                     0, 0);
+  }
+}
+
+// MFMA fragment (16 rows from r0, k = 32 * kh + 8 * (lane >> 4) .. +7) of a swizzled stage tile
+template <int BK>
+__device__ __forceinline__ bf16x8 read_frag(const bf16* __restrict__ tile, int r0, int kh) {
+  const int l = threadIdx.x & 63;
+  const int row = r0 + (l & 15);
+  const int q = ((l >> 4) + 4 * kh) ^ swz<BK>(row);
+  return *reinterpret_cast<const bf16x8*>(tile + row * BK + q * 8);
+}
+
+template <int BM, int BN, int kBK, int kStages, bool CONV, bool RES>
+__global__ __launch_bounds__(kThreads, 2) void gemm_glds_kernel(GldsArgs p) {
+  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+  constexpr int A_ELEMS = BM * kBK, B_ELEMS = BN * kBK;
+  constexpr int kRing = kStages * (A_ELEMS + B_ELEMS);
+  constexpr int CS = BN + 8;  // epilogue C staging row (bf16)
+  constexpr int kSmem = kRing > BM * CS ? kRing : BM * CS;
+  constexpr int LPT = (BM + BN) * kBK / 2048;  // LDS-DMA instructions per wave per K-tile
+  // ONE __shared__ array for the ring, the epilogue staging and the statistics scratch
+  __shared__ __attribute__((aligned(16))) bf16 smem[kSmem];
+  auto sa = [&](int s) { return smem + s * A_ELEMS; };
+  auto sb = [&](int s) { return smem + kStages * A_ELEMS + s * B_ELEMS; };
+
+  // XCD-aware tile order (bijective): blocks sharing an XCD get a contiguous tile range
+  const int nt = p.tiles_m * p.tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int q = nt / 8, r = nt % 8, xcd = bid % 8, pos = bid / 8;
+    bid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+  }
+  const int tm = bid / p.tiles_n, tn = bid % p.tiles_n;
+  const int64_t m0 = static_cast<int64_t>(tm) * BM, n0 = static_cast<int64_t>(tn) * BN;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // CONV: image position of each A row this lane stages (fixed over K)
+  constexpr int PPWA = BM * kBK / 2048, RPPA = 512 / kBK;
+  int ph[PPWA], pw[PPWA];
+  if (CONV) {
+#pragma unroll
+    for (int j = 0; j < PPWA; ++j) {
+      const int64_t row = m0 + (wave * PPWA + j) * RPPA + lane / (kBK / 8);
+      const int hw = static_cast<int>(row % (static_cast<int64_t>(p.conv_h) * p.conv_w));
+      ph[j] = hw / p.conv_w;
+      pw[j] = hw - ph[j] * p.conv_w;
+    }
+  }
+  auto issue = [&](int s, int64_t k0) {
+    issue_tile<BM, kBK, CONV>(sa(s), p.a, p.lda, p.M, m0, k0, p.K, ph, pw, p.conv_h, p.conv_w, p.conv_c);
+    issue_tile<BN, kBK, false>(sb(s), p.b, p.ldb, p.N, n0, k0, p.K, nullptr, nullptr, 0, 0, 0);
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = static_cast<int>((p.K + kBK - 1) / kBK);
+#pragma unroll
+  for (int s = 0; s < kStages - 1; ++s)
+    if (s < nk) issue(s, static_cast<int64_t>(s) * kBK);
+  for (int t = 0; t < nk; ++t) {
+    const int ahead = nk - 1 - t < kStages - 2 ? nk - 1 - t : kStages - 2;
+    wait_tiles_ahead<LPT, kStages - 2>(ahead);  // this wave's pieces of tile t have landed
+    __builtin_amdgcn_s_barrier();   // ... and every wave's; every wave is done with tile t-1
+    if (t + kStages - 1 < nk) issue((t + kStages - 1) % kStages, static_cast<int64_t>(t + kStages - 1) * kBK);
+    const bf16* ta = sa(t % kStages);
+    const bf16* tb = sb(t % kStages);
+#pragma unroll
+    for (int kh = 0; kh < kBK / 32; ++kh) {
+      bf16x8 fa[FM], fb[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) fa[i] = read_frag<kBK>(ta, wm * WM + i * 16, kh);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) fb[j] = read_frag<kBK>(tb, wn * WN + j * 16, kh);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();  // ring fully consumed (no DMA in flight: the last wait was vmcnt(0))
+
+  // ---------------------------------------------------------------- epilogue
+  // acc[i][j][r]: row m0 + wm*WM + i*16 + 4*(lane>>4) + r, col n0 + wn*WN + j*16 + (lane&15)
+  const int col_in = lane & 15, rq = 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        smem[(wm * WM + i * 16 + rq + r) * CS + wn * WN + j * 16 + col_in] = static_cast<bf16>(acc[i][j][r]);
+  __syncthreads();
+  constexpr int CPR = BN / 8;          // 16-B chunks per row
+  constexpr int RPI = kThreads / CPR;  // rows per sweep
+  const int cc = threadIdx.x % CPR, r0 = threadIdx.x / CPR;
+  const int64_t n = n0 + cc * 8;
+  const bool ncol_ok = n + 8 <= p.N;
+  float cs[8], cq[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) cs[e] = cq[e] = 0.f;
+#pragma unroll 4
+  for (int r = r0; r < BM; r += RPI) {
+    const int64_t m = m0 + r;
+    if (m >= p.M) break;
+    uint4 v = *reinterpret_cast<const uint4*>(smem + r * CS + cc * 8);
+    bf16 e8[8];
+    __builtin_memcpy(e8, &v, 16);
+    if (RES) {
+      bf16 r8[8];
+      if (ncol_ok) {
+        const uint4 rv = *reinterpret_cast<const uint4*>(p.res + m * p.ldr + n);
+        __builtin_memcpy(r8, &rv, 16);
+      } else {
+        for (int e = 0; e < 8; ++e) r8[e] = n + e < p.N ? p.res[m * p.ldr + n + e] : static_cast<bf16>(0.f);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) e8[e] = static_cast<bf16>(static_cast<float>(e8[e]) + static_cast<float>(r8[e]));
+      __builtin_memcpy(&v, e8, 16);
+    }
+    if (ncol_ok) {
+      *reinterpret_cast<uint4*>(p.c + m * p.ldc + n) = v;
+    } else {
+      for (int e = 0; e < 8 && n + e < p.N; ++e) p.c[m * p.ldc + n + e] = e8[e];
+    }
+    if (p.mode == 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float f = n + e < p.N ? static_cast<float>(e8[e]) : 0.f;
+        cs[e] += f;
+        cq[e] = fmaf(f, f, cq[e]);
+      }
+    }
+  }
+  if (p.mode == 1) {
+    // lanes of a wave with equal cc differ in the bits above log2(CPR): butterfly them, then
+    // combine the 4 waves through LDS and add one atomic per column per block
+#pragma unroll
+    for (int off = CPR; off < 64; off <<= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        cs[e] += __shfl_xor(cs[e], off, 64);
+        cq[e] += __shfl_xor(cq[e], off, 64);
+      }
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [4 waves][2][BN]
+    static_assert(4 * 2 * BN * 4 <= kSmem * 2, "stats scratch");
+    if (lane < CPR) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(wave * 2 + 0) * BN + cc * 8 + e] = cs[e];
+        red[(wave * 2 + 1) * BN + cc * 8 + e] = cq[e];
+      }
+    }
+    __syncthreads();
+    float* shard = p.stats + static_cast<size_t>(blockIdx.x % kShards) * 2 * p.N;
+    for (int col = threadIdx.x; col < BN; col += kThreads) {
+      const float s = red[0 * BN + col] + red[2 * BN + col] + red[4 * BN + col] + red[6 * BN + col];
+      const float q = red[1 * BN + col] + red[3 * BN + col] + red[5 * BN + col] + red[7 * BN + col];
+      if (n0 + col < p.N) {
+        atomicAdd(shard + n0 + col, s);
+        atomicAdd(shard + p.N + n0 + col, q);
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int BK, int ST, bool CONV, bool RES>
+void launch_glds(GldsArgs a, hipStream_t s) {
+  a.tiles_m = static_cast<int>((a.M + BM - 1) / BM);
+  a.tiles_n = static_cast<int>((a.N + BN - 1) / BN);
+  gemm_glds_kernel<BM, BN, BK, ST, CONV, RES><<<a.tiles_m * a.tiles_n, kThreads, 0, s>>>(a);
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Filter transposition for the input-gradient GEMMs: out[ci][t][co] = in[co][T-1-t][ci] for
+// every tensor of a list (T = taps: 1 for a 1x1 filter, 9 for a 3x3 one, whose taps are then
+// also flipped). One launch for up to kMaxXT filters; 64x64 (co x ci) tiles through LDS so
+// both the reads and the writes are 128-B coalesced rows.
+constexpr int kMaxXT = 40;
+struct XposeArgs {
+  uintptr_t src[kMaxXT];
+  uintptr_t dst[kMaxXT];
+  int co[kMaxXT], ci[kMaxXT], taps[kMaxXT];
+  int32_t start[kMaxXT + 1];  // prefix of tiles per tensor
+  int n;
+};
+
+__global__ __launch_bounds__(kThreads) void xpose_taps_kernel(XposeArgs a) {
+  __shared__ bf16 tile[64][66];
+  const int b = blockIdx.x;
+  const int t = find_tensor(a.start, a.n, b);
+  const int co = a.co[t], ci = a.ci[t], T = a.taps[t];
+  const int tci = (ci + 63) / 64, tco = (co + 63) / 64;
+  int rem = b - a.start[t];
+  const int tap = rem / (tco * tci);
+  rem -= tap * tco * tci;
+  const int bco = rem / tci, bci = rem % tci;
+  const bf16* __restrict__ src = reinterpret_cast<const bf16*>(a.src[t]);
+  bf16* __restrict__ dst = reinterpret_cast<bf16*>(a.dst[t]);
+  const int r = threadIdx.x / 4, c0 = (threadIdx.x % 4) * 16;
+  {  // read rows co = bco*64 + r, 16 ci each, of source tap T-1-tap
+    const int oc = bco * 64 + r;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int ic = bci * 64 + c0 + j;
+      tile[r][c0 + j] = (oc < co && ic < ci) ? src[(static_cast<int64_t>(oc) * T + (T - 1 - tap)) * ci + ic]
+                                            : static_cast<bf16>(0.f);
+    }
+  }
+  __syncthreads();
+  {  // write rows ci = bci*64 + r, 16 co each, of destination tap `tap`
+    const int ic = bci * 64 + r;
+    if (ic < ci) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int oc = bco * 64 + c0 + j;
+        if (oc < co) dst[(static_cast<int64_t>(ic) * T + tap) * co + oc] = tile[c0 + j][r];
+      }
+    }
+  }
+}
+}  // namespace
+
+bool gemm_glds_supported(const GemmProblem& g) {
+  return g.a_kmajor && g.b_kmajor && g.mode <= 1 && (g.splits <= 1) && g.a_scale == nullptr &&
+         g.b_scale == nullptr && g.bnb_x == nullptr && g.K % 8 == 0 && g.lda % 8 == 0 && g.ldb % 8 == 0 &&
+         g.ldc % 8 == 0 && (g.res == nullptr || g.ldr % 8 == 0) &&
+         (g.conv_h == 0 || (g.conv_c % 32 == 0 && g.K == 9LL * g.conv_c));
+}
+
+void gemm_glds(const GemmProblem& g, hipStream_t stream) {
+  if (!gemm_glds_supported(g)) throw std::runtime_error("gemm_glds: unsupported problem");
+  GldsArgs a{};
+  a.a = static_cast<const bf16*>(g.a);
+  a.b = static_cast<const bf16*>(g.b);
+  a.c = static_cast<bf16*>(g.c);
+  a.res = static_cast<const bf16*>(g.res);
+  a.stats = g.stats;
+  a.lda = g.lda; a.ldb = g.ldb; a.ldc = g.ldc; a.ldr = g.ldr;
+  a.M = g.M; a.N = g.N; a.K = g.K;
+  a.mode = g.mode;
+  a.conv_h = g.conv_h; a.conv_w = g.conv_w; a.conv_c = g.conv_c;
+  const bool conv = g.conv_h > 0, res = g.res != nullptr;
+  // variant: 1 BK32/3 stages; 2 BK32/4; 3 BK64/2; 4 BK64/3 (engine 3..6 force one, for experiments).
+  // Auto (measured on MI355X, ResNet-50 1x1 and 3x3 shapes): a 64-deep K-step in a 2-stage ring
+  // (64 KiB at 128x128: 2 workgroups/CU) wins for the 3x3 convolutions and once K >= 1024;
+  // shorter K (memory-bound 1x1 convolutions) prefers the 32-deep 3-stage ring (48 KiB:
+  // 3 workgroups/CU).
+  int var = g.engine >= 3 ? g.engine - 2 : 0;
+  const bool k64ok = !conv || g.conv_c % 64 == 0;
+  if (var == 0) var = ((conv || g.K >= 1024) && k64ok) ? 3 : 1;
+  if ((var == 3 || var == 4) && !k64ok) var = 1;
+  // 128x128 tiles whenever both dimensions allow (measured: 128x64 tiles lose more to the lower
+  // operand reuse than they win back from finer wave quantization)
+  const bool bm128 = g.M > 64 && g.tile_m != 64;
+  const bool bn128 = g.N > 64 && g.tile_n != 64;
+#define GV(BM, BN, BK, ST)                                                                                \
+  {                                                                                                      \
+    if (conv) { if (res) launch_glds<BM, BN, BK, ST, true, true>(a, stream); else launch_glds<BM, BN, BK, ST, true, false>(a, stream); } \
+    else { if (res) launch_glds<BM, BN, BK, ST, false, true>(a, stream); else launch_glds<BM, BN, BK, ST, false, false>(a, stream); }    \
+  }
+#define GL(BM, BN)                          \
+  {                                         \
+    if (var == 1) GV(BM, BN, 32, 3)         \
+    else if (var == 3) GV(BM, BN, 64, 2)    \
+    else if (var == 4) GV(BM, BN, 64, 3)    \
+    else GV(BM, BN, 32, 4)                  \
+  }
+  if (bm128 && bn128) GL(128, 128)
+  else if (bm128) GL(128, 64)
+  else if (bn128) GL(64, 128)
+  else GL(64, 64)
+#undef GV
+#undef GL
+}
+
+void transpose_filters(const std::vector<uintptr_t>& src, const std::vector<uintptr_t>& dst,
+                       const std::vector<int>& co, const std::vector<int>& ci, const std::vector<int>& taps,
+                       hipStream_t stream) {
+  const size_t n = src.size();
+  if (dst.size() != n || co.size() != n || ci.size() != n || taps.size() != n)
+    throw std::runtime_error("transpose_filters: length mismatch");
+  for (size_t i0 = 0; i0 < n; i0 += kMaxXT) {
+    XposeArgs a{};
+    a.n = static_cast<int>(n - i0 < static_cast<size_t>(kMaxXT) ? n - i0 : kMaxXT);
+    int32_t tiles = 0;
+    for (int i = 0; i < a.n; ++i) {
+      a.src[i] = src[i0 + i];
+      a.dst[i] = dst[i0 + i];
+      a.co[i] = co[i0 + i];
+      a.ci[i] = ci[i0 + i];
+      a.taps[i] = taps[i0 + i];
+      a.start[i] = tiles;
+      tiles += a.taps[i] * ((a.co[i] + 63) / 64) * ((a.ci[i] + 63) / 64);
+    }
+    a.start[a.n] = tiles;
+    if (tiles == 0) continue;
+    xpose_taps_kernel<<<tiles, kThreads, 0, stream>>>(a);
+    FLUXMPI_HIP_CHECK(hipGetLastError());
+  }
+}
+
+}  // namespace fluxmpi

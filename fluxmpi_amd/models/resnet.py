@@ -125,10 +125,17 @@ class Bottleneck(nn.Module):
                     identity = self.downsample(x)
                 if self.hybrid:
                     bl2 = fb.BNStatsLink() if bnl else None  # bn2 -> conv3 (its only consumer)
-                    a2 = self.bn2(self.conv2(a1), relu=True, bnlink=bl2)
+                    if fb.conv3x3_supported(a1, self.conv2):
+                        # implicit-GEMM conv2 (input gradient always; forward where measured faster,
+                        # then bn2's statistics come from its epilogue)
+                        ours = fb.conv3x3_forward_is_ours(a1, self.conv2.weight)
+                        c2 = fb.conv3x3(a1, self.conv2.weight, with_stats=True)
+                        a2 = fb.bn_from_stats(c2, self.bn2, relu=True, stats_ready=ours, bnlink=bl2)
+                    else:
+                        a2 = self.bn2(self.conv2(a1), relu=True, bnlink=bl2)
                     c3 = fb.conv1x1_hybrid(a2, self.conv3.weight, None, bl2)
                 else:
-                    c2 = self.conv2(a1)
+                    c2 = fb.conv3x3(a1, self.conv2.weight) if fb.conv3x3_supported(a1, self.conv2) else self.conv2(a1)
                     c3 = fb.bn_relu_conv1x1(c2, self.bn2, self.conv3.weight)  # bn2+relu fused into the A load
                 if self.hybrid:
                     out = self.bn3(c3, relu=True, residual=identity, link=link if self.downsample is None else None,

@@ -32,7 +32,7 @@ import torch
 
 from . import _ext
 from .batchnorm import BNStatsLink, GradLink, SideGradLink, _workspace, bn_counter  # noqa: F401 (links re-exported)
-from .gemm import conv1x1_dgrad, conv1x1_wgrad, gemm
+from .gemm import conv1x1_dgrad, conv1x1_wgrad, conv3x3_dgrad, conv3x3_fwd, gemm, note_filter
 from .multi_tensor import DTYPE_CODE
 
 
@@ -41,6 +41,10 @@ from .multi_tensor import DTYPE_CODE
 # reduce passes save 1.05 ms — a net loss until the GEMM epilogue streams as well as the
 # BN kernels do. FLUXMPI_BN_LINK=1 enables it (numerics covered by tests either way).
 BN_LINK = os.environ.get("FLUXMPI_BN_LINK", "0") == "1"
+# 3x3 / stride-1 convolutions of the bottlenecks: "ours" = forward (+ the next BatchNorm's
+# statistics in the epilogue) and input gradient on the implicit-GEMM MFMA kernel, weight
+# gradient on MIOpen; "dgrad" = only the input gradient ours; "miopen" = all MIOpen
+CONV3X3 = os.environ.get("FLUXMPI_CONV3X3", "ours")
 
 
 def _stream(t):
@@ -85,6 +89,7 @@ class _Conv1x1Stats(torch.autograd.Function):
     def forward(ctx, x, weight, link=None, bnlink=None):
         x = x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
         ctx.link, ctx.bnlink = link, bnlink
+        note_filter(weight)
         n, ci, h, w = x.shape
         co = weight.shape[0]
         w2 = weight.reshape(co, ci)
@@ -121,7 +126,7 @@ def _dgrad_nhwc(dc2, weight, x, link, bnlink=None):
             bnlink.x.is_contiguous(memory_format=torch.channels_last):
         bn = (_nhwc2d(bnlink.x), bnlink.w32, bnlink.b32, bnlink.mean, bnlink.inv, bnlink.mask, bnlink.relu_mode)
         stats = _workspace(dx)
-    conv1x1_dgrad(dc2, weight.reshape(co, ci), residual=res, out=_nhwc2d(dx), bn_bwd=bn, stats=stats)
+    conv1x1_dgrad(dc2, weight.reshape(co, ci), residual=res, out=_nhwc2d(dx), bn_bwd=bn, stats=stats, w4d=weight)
     if bn is not None:
         bnlink.ready = True
     return dx
@@ -136,6 +141,7 @@ class _Conv1x1Hybrid(torch.autograd.Function):
     def forward(ctx, x, weight, link=None, bnlink=None):
         x = x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
         ctx.link, ctx.bnlink = link, bnlink
+        note_filter(weight)
         ctx.save_for_backward(x, weight)
         return torch.nn.functional.conv2d(x, weight)
 
@@ -162,6 +168,8 @@ class _Conv1x1Downsample(torch.autograd.Function):
     def forward(ctx, x, weight, stride, link):
         x = x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
         ctx.stride, ctx.link = stride, link
+        if stride == 1:
+            note_filter(weight)
         ctx.save_for_backward(x, weight)
         return torch.nn.functional.conv2d(x, weight, None, stride)
 
@@ -280,6 +288,92 @@ class _BNReluConv1x1(torch.autograd.Function):
                            stats=_workspace(c2)).view(n, h, w, ch).permute(0, 3, 1, 2)
         dc2, _, dbw, dbb = _bn_bwd(da, c2, None, w32, b32, mean, inv, True, False, stats_ready=True)
         return dc2, dbw.to(ctx.bn_wdtype), dbb.to(ctx.bn_wdtype), None, None, dw, None, None, None
+
+
+class _Conv3x3(torch.autograd.Function):
+    """3x3 / stride 1 / pad 1 convolution: implicit-GEMM forward (optionally with the next
+    BatchNorm's statistics accumulated in its epilogue) and input gradient on the LDS-DMA
+    MFMA kernel; weight gradient on MIOpen."""
+
+    @staticmethod
+    def forward(ctx, x, weight, fwd_ours, with_stats):
+        x = x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
+        note_filter(weight)
+        if fwd_ours:
+            y = conv3x3_fwd(x, weight, stats=_workspace(x) if with_stats else None)
+        else:
+            y = torch.nn.functional.conv2d(x, weight, None, 1, 1)
+        ctx.save_for_backward(x, weight)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        if not dy.is_contiguous(memory_format=torch.channels_last):
+            dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = conv3x3_dgrad(dy, weight) if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
+                                                     [False, True, False])[1]
+        return dx, dw, None, None
+
+
+def conv3x3_supported(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
+    return (CONV3X3 in ("ours", "dgrad") and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
+            and conv.kernel_size == (3, 3) and conv.stride == (1, 1) and conv.padding == (1, 1)
+            and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None
+            and conv.in_channels % 32 == 0 and conv.weight.dtype == torch.bfloat16)
+
+
+_FWD_CHOICE: dict = {}  # (N, C, H, W, Co) -> True: our forward (+ statistics epilogue) is faster
+
+
+def _time_us(fn, iters=5):
+    for _ in range(2):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) * 1e3 / iters
+
+
+def conv3x3_forward_is_ours(x, weight) -> bool:
+    """Per-shape choice of the 3x3 forward, measured once (like cudnn.benchmark): our implicit
+    GEMM with the statistics epilogue vs MIOpen plus the separate statistics pass it then needs
+    (priced at one read of the output at 5 TB/s). Wave quantization makes some shapes (e.g.
+    ResNet-50's 14x14x256 at batch 256: 1.5 rounds of 128x128 tiles) slower on our kernel."""
+    if CONV3X3 != "ours":
+        return False
+    key = (tuple(x.shape), weight.shape[0])
+    hit = _FWD_CHOICE.get(key)
+    if hit is not None:
+        return hit
+    if torch.cuda.is_current_stream_capturing():
+        return True
+    with torch.no_grad():
+        xs = x.detach().contiguous(memory_format=torch.channels_last)
+        w = weight.detach()
+        ws = torch.zeros_like(_workspace(xs))
+        ours = _time_us(lambda: conv3x3_fwd(xs, w, stats=ws))
+        theirs = _time_us(lambda: torch.nn.functional.conv2d(xs, w, None, 1, 1))
+    n, _, h, wd = x.shape
+    stats_pass_us = n * h * wd * weight.shape[0] * x.element_size() / 5e12 * 1e6
+    choice = ours <= theirs + stats_pass_us
+    _FWD_CHOICE[key] = choice
+    return choice
+
+
+def conv3x3(x, weight, with_stats=False):
+    """Returns the conv output. If the forward runs on our kernel (:func:`conv3x3_forward_is_ours`)
+    and ``with_stats``, its per-channel sum / sumsq are pending in the BatchNorm workspace
+    (consume them with ``bn_from_stats(..., stats_ready=True)``); check with
+    ``conv3x3_forward_is_ours`` first."""
+    ours = conv3x3_forward_is_ours(x, weight)
+    return _Conv3x3.apply(x, weight, ours, with_stats and ours)
 
 
 def conv1x1_stats(x, weight, link=None, bnlink=None):

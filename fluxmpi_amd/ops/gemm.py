@@ -11,6 +11,7 @@ given: the previous BatchNorm + ReLU applied on the fly (never stored).
 from __future__ import annotations
 
 import os
+import weakref
 
 import torch
 
@@ -19,6 +20,8 @@ from . import _ext
 SHARDS = 64  # == kShards in csrc/kernels/{batchnorm,gemm}.hip
 # LDS buffering of the GEMM main loop: 0 = per-shape choice in the kernel launcher, 1 or 2 forces it
 NBUF = int(os.environ.get("FLUXMPI_GEMM_NBUF", "0"))
+# GEMM kernel: 0 = launcher's choice, 1 = register-staged (gemm.hip), 2 = LDS-DMA pipelined (gemm_glds.hip)
+ENGINE = int(os.environ.get("FLUXMPI_GEMM_ENGINE", "0"))
 
 
 def _stream(t):
@@ -30,10 +33,11 @@ def _ptr(t):
 
 
 def gemm(a, b, c, *, M, N, K, lda, ldb, ldc, a_kmajor=True, b_kmajor=True, mode=0, splits=1, a_affine=None,
-         b_affine=None, stats=None, tile_m=0, tile_n=0, nbuf=0, residual=None, bn_bwd=None):
+         b_affine=None, stats=None, tile_m=0, tile_n=0, nbuf=0, residual=None, bn_bwd=None, conv=None, engine=None):
     """``bn_bwd``: ``(x2d, w32, b32, mean, inv, mask, relu_mode)`` of a BatchNorm whose output
     gradient is C — with ``mode=1`` the epilogue accumulates that BatchNorm's backward
-    reductions into ``stats`` instead of C's sum / sum of squares."""
+    reductions into ``stats`` instead of C's sum / sum of squares. ``conv=(H, W, C)``: A is the
+    implicit 3x3/s1/p1 im2col of the NHWC image batch ``a`` (K = 9*C)."""
     C = _ext.get(required=True)
     asc, ash = a_affine if a_affine is not None else (None, None)
     bsc, bsh = b_affine if b_affine is not None else (None, None)
@@ -41,7 +45,8 @@ def gemm(a, b, c, *, M, N, K, lda, ldb, ldc, a_kmajor=True, b_kmajor=True, mode=
     C.gemm_bf16(a.data_ptr(), b.data_ptr(), c.data_ptr(), lda, ldb, ldc, M, N, K, a_kmajor, b_kmajor, mode, splits,
                 _ptr(asc), _ptr(ash), _ptr(bsc), _ptr(bsh), _ptr(stats), tile_m, tile_n, _stream(c), nbuf or NBUF,
                 _ptr(residual), residual.stride(0) if residual is not None else 0, _ptr(bx), _ptr(bw), _ptr(bb),
-                _ptr(bmean), _ptr(binv), _ptr(bmask), int(brm))
+                _ptr(bmean), _ptr(binv), _ptr(bmask), int(brm), *(conv if conv is not None else (0, 0, 0)),
+                ENGINE if engine is None else engine)
     return c
 
 
@@ -59,11 +64,13 @@ def conv1x1_fwd(x2d: torch.Tensor, w2d: torch.Tensor, in_affine=None, stats: tor
 
 
 def conv1x1_dgrad(dy2d: torch.Tensor, w2d: torch.Tensor, residual: torch.Tensor | None = None,
-                  out: torch.Tensor | None = None, bn_bwd=None, stats: torch.Tensor | None = None):
+                  out: torch.Tensor | None = None, bn_bwd=None, stats: torch.Tensor | None = None,
+                  w4d: torch.Tensor | None = None):
     """``dy2d`` [M, Cout], ``w2d`` [Cout, Cin] -> dX [M, Cin] bf16 (``+ residual`` [M, Cin] bf16 fused
     into the epilogue: the gradient of a residual block's input in one pass). ``bn_bwd`` /
     ``stats``: accumulate the backward reductions of the BatchNorm that produced the conv's
-    input (see :func:`gemm`) into the sharded ``stats`` workspace."""
+    input (see :func:`gemm`) into the sharded ``stats`` workspace. ``w4d``: the filter parameter
+    itself (its forward called :func:`note_filter`): enables the LDS-DMA kernel on the cached W^T."""
     M, Co = dy2d.shape
     Ci = w2d.shape[1]
     dx = out if out is not None else torch.empty(M, Ci, device=dy2d.device, dtype=torch.bfloat16)
@@ -71,8 +78,104 @@ def conv1x1_dgrad(dy2d: torch.Tensor, w2d: torch.Tensor, residual: torch.Tensor 
         assert residual.shape == (M, Ci) and residual.dtype == torch.bfloat16 and residual.stride(1) == 1
     if bn_bwd is not None:
         assert stats is not None and dx.stride(0) == Ci and bn_bwd[0].shape == (M, Ci) and bn_bwd[0].stride(0) == Ci
+    if bn_bwd is None and ENGINE != 1 and w4d is not None and dy2d.stride(0) % 8 == 0:
+        # LDS-DMA kernel on the cached W^T (K-major B)
+        gemm(dy2d, filter_t(w4d), dx, M=M, N=Ci, K=Co, lda=dy2d.stride(0), ldb=Co, ldc=dx.stride(0),
+             residual=residual, engine=ENGINE or 2)
+        return dx
     gemm(dy2d, w2d, dx, M=M, N=Ci, K=Co, lda=dy2d.stride(0), ldb=w2d.stride(0), ldc=dx.stride(0), a_kmajor=True,
-         b_kmajor=False, residual=residual, mode=1 if bn_bwd is not None else 0, stats=stats, bn_bwd=bn_bwd)
+         b_kmajor=False, residual=residual, mode=1 if bn_bwd is not None else 0, stats=stats, bn_bwd=bn_bwd,
+         engine=1)
+    return dx
+
+
+# ---- transposed filters for the input-gradient GEMMs ------------------------------------------
+# The dgrad GEMMs of the LDS-DMA kernel take the filter as a K-major B operand: W^T [ci][co] for
+# a 1x1 convolution, the transposed AND flipped [ci][3][3][co] for a 3x3 one. Every forward of
+# one of our convolutions marks its filter stale; the first input-gradient request of the
+# backward then refreshes ALL stale filters in one launch (csrc transpose_filters), so a
+# ResNet-50 step pays ~2 launches instead of one transpose per convolution. (Weights change
+# only between a forward and the next one — the optimiser step — so the backward always sees
+# the filters its forward used; a captured HIP graph replays the refresh launch too.)
+_FILT: dict = {}  # id(w) -> [weakref(w), wt | None, fresh]
+
+
+def note_filter(w: torch.Tensor) -> None:
+    e = _FILT.get(id(w))
+    if e is None or e[0]() is not w:
+        _FILT[id(w)] = [weakref.ref(w), None, False]
+    else:
+        e[2] = False
+
+
+def filter_t(w: torch.Tensor) -> torch.Tensor:
+    """``w`` [co, ci, kh, kw] -> ``[ci, kh*kw*co]`` (taps flipped), from the batched cache."""
+    e = _FILT.get(id(w))
+    if e is None or e[0]() is not w:
+        note_filter(w)
+        e = _FILT[id(w)]
+    if not e[2]:
+        srcs, dsts, cos, cis, taps, keep, fresh = [], [], [], [], [], [], []
+        for k, ent in list(_FILT.items()):
+            t = ent[0]()
+            if t is None:
+                del _FILT[k]
+                continue
+            if ent[2] or t.device != w.device:
+                continue
+            co, ci = t.shape[0], t.shape[1]
+            T = t.shape[2] * t.shape[3] if t.dim() == 4 else 1
+            src = t.permute(0, 2, 3, 1).contiguous() if t.dim() == 4 else t.contiguous()  # [co][taps][ci]
+            if ent[1] is None or ent[1].numel() != ci * T * co or ent[1].dtype != t.dtype:
+                ent[1] = torch.empty(ci, T * co, device=t.device, dtype=t.dtype)
+            srcs.append(src.data_ptr())
+            dsts.append(ent[1].data_ptr())
+            cos.append(co)
+            cis.append(ci)
+            taps.append(T)
+            keep.append(src)  # alive until the launch is enqueued
+            fresh.append(ent)
+        C = _ext.get(required=True)
+        C.transpose_filters(srcs, dsts, cos, cis, taps, _stream(w))
+        for ent in fresh:
+            ent[2] = True
+    return e[1]
+
+
+def conv3x3_fwd(x: torch.Tensor, w: torch.Tensor, in_affine=None, stats: torch.Tensor | None = None,
+                out: torch.Tensor | None = None) -> torch.Tensor:
+    """3x3 / stride 1 / pad 1 convolution as an implicit GEMM on the MFMA kernel.
+
+    ``x`` [N, C, H, W] bf16 channels_last, ``w`` [Co, C, 3, 3] bf16 -> [N, Co, H, W] channels_last.
+    ``in_affine=(scale, shift)``: relu(x * scale + shift) per input channel applied on load (the
+    previous BatchNorm + ReLU; the zero padding stays zero). ``stats``: per-output-channel
+    sum / sumsq into the sharded BatchNorm workspace.
+    """
+    n, c, h, wd = x.shape
+    co = w.shape[0]
+    xs = x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
+    w2 = w.permute(0, 2, 3, 1).contiguous()  # [Co][3][3][C]: K-major over (tap, channel)
+    note_filter(w)
+    y = out if out is not None else torch.empty(n, h, wd, co, device=x.device, dtype=x.dtype).permute(0, 3, 1, 2)
+    M = n * h * wd
+    gemm(xs, w2, y, M=M, N=co, K=9 * c, lda=c, ldb=9 * c, ldc=co, mode=1 if stats is not None else 0,
+         a_affine=in_affine, stats=stats, conv=(h, wd, c))
+    return y
+
+
+def conv3x3_dgrad(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Input gradient of the 3x3/s1/p1 convolution: the same implicit GEMM over dY with the
+    filter transposed and flipped (``WT[ci][r][s][co] = W[co][ci][2-r][2-s]``)."""
+    n, co, h, wd = dy.shape
+    ci = w.shape[1]
+    dys = dy if dy.is_contiguous(memory_format=torch.channels_last) else dy.contiguous(
+        memory_format=torch.channels_last)
+    if ENGINE == 1:  # register-staged kernel: transpose on the spot
+        wt = w.flip(2, 3).permute(1, 2, 3, 0).contiguous()  # [Ci][3][3][Co]
+    else:
+        wt = filter_t(w)
+    dx = out if out is not None else torch.empty(n, h, wd, ci, device=dy.device, dtype=dy.dtype).permute(0, 3, 1, 2)
+    gemm(dys, wt, dx, M=n * h * wd, N=ci, K=9 * co, lda=co, ldb=9 * co, ldc=ci, conv=(h, wd, co))
     return dx
 
 

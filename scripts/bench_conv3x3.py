@@ -1,0 +1,64 @@
+#!/usr/bin/env python
+"""ResNet-50's 3x3 convolutions (batch 256, stride 1): the implicit-GEMM MFMA kernel vs MIOpen
+(tuned find-db), forward and input gradient. One JSON line per shape and a total."""
+import json
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from fluxmpi_amd.ops import gemm as G  # noqa: E402
+from fluxmpi_amd.ops.gemm import conv3x3_dgrad, conv3x3_fwd  # noqa: E402
+from fluxmpi_amd.utils.miopen import install_tuned_db  # noqa: E402
+
+
+def bench(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return round(s.elapsed_time(e) / iters * 1e3, 1)
+
+
+def main():
+    install_tuned_db()
+    torch.backends.cudnn.benchmark = True
+    B = int(os.environ.get("BENCH_BATCH", "256"))
+    tot = {}
+    for H, C in [(56, 64), (28, 128), (14, 256), (7, 512)]:
+        x = torch.randn(B, C, H, H, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+        w = (torch.randn(C, C, 3, 3, device="cuda") * 0.05).bfloat16().contiguous(memory_format=torch.channels_last)
+        dy = torch.randn_like(x)
+        y = torch.empty_like(x)
+        flop = 2 * B * H * H * C * C * 9
+        rec = {"H": H, "C": C}
+        for eng in (1, 2, 3, 5, 6):
+            G.ENGINE = eng
+            rec[f"e{eng}_fwd"] = bench(lambda: conv3x3_fwd(x, w, out=y))
+            rec[f"e{eng}_dgrad"] = bench(lambda: conv3x3_dgrad(dy, w, out=y))
+        G.ENGINE = 2
+        rec["ours_fwd"] = rec["e2_fwd"]
+        rec["miopen_fwd"] = bench(lambda: F.conv2d(x, w, padding=1))
+        rec["ours_dgrad"] = rec["e2_dgrad"]
+        rec["miopen_dgrad"] = bench(lambda: torch.ops.aten.convolution_backward(
+            dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False]))
+        rec["miopen_wgrad"] = bench(lambda: torch.ops.aten.convolution_backward(
+            dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False]))
+        for k in ("ours_fwd", "miopen_fwd", "ours_dgrad", "miopen_dgrad"):
+            rec[k + "_TF"] = round(flop / rec[k] / 1e6, 1)
+        for k, v in rec.items():
+            if k not in ("H", "C") and not k.endswith("_TF"):
+                tot[k] = round(tot.get(k, 0.0) + v, 1)
+        print(json.dumps(rec), flush=True)
+    print(json.dumps({"total_us": tot}))
+
+
+if __name__ == "__main__":
+    main()

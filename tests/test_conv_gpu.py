@@ -1,0 +1,89 @@
+"""Implicit-GEMM 3x3 convolution (MFMA kernel) vs PyTorch fp32 references (GPU only)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(2, 32, 5, 7, 64), (3, 64, 14, 14, 128), (1, 96, 9, 11, 32), (2, 128, 8, 8, 256), (4, 64, 3, 3, 64)]
+
+
+@pytest.fixture(params=[1, 2, 3, 5, 6], ids=["regstage", "glds", "glds_bk32s3", "glds_bk64s2", "glds_bk64s3"],
+                autouse=True)
+def engine(request, monkeypatch):
+    """Every case runs on both GEMM kernels (register-staged, LDS-DMA pipelined)."""
+    from fluxmpi_amd.ops import gemm
+    monkeypatch.setattr(gemm, "ENGINE", request.param)
+    return request.param
+
+
+def _nhwc(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
+
+
+@pytest.mark.parametrize("N,C,H,W,Co", SHAPES)
+@pytest.mark.parametrize("use_aff", [False, True])
+def test_conv3x3_fwd(gpu_ext, N, C, H, W, Co, use_aff, engine):
+    from fluxmpi_amd.ops.gemm import SHARDS, conv3x3_fwd
+    if use_aff and engine >= 2:
+        pytest.skip("the LDS-DMA kernel has no prologue affine (register staging applies it)")
+    torch.manual_seed(0)
+    x = _nhwc(torch.randn(N, C, H, W, device="cuda").bfloat16())
+    w = _nhwc((torch.randn(Co, C, 3, 3, device="cuda") * 0.1).bfloat16())
+    aff = None
+    xin = x.float()
+    if use_aff:
+        s, t = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.5
+        aff = (s, t)
+        xin = torch.relu((x.double() * s.view(1, -1, 1, 1).double() + t.view(1, -1, 1, 1).double()).float())
+        xin = xin.bfloat16().float()  # the kernel rounds the activated operand to bf16
+    stats = torch.zeros(SHARDS, 2, Co, device="cuda")
+    y = conv3x3_fwd(x, w, in_affine=aff, stats=stats)
+    ref = F.conv2d(xin, w.float(), padding=1)
+    assert y.is_contiguous(memory_format=torch.channels_last) and y.shape == ref.shape
+    assert _rel(y, ref) < 1e-2
+    yb = y.float()
+    torch.testing.assert_close(stats[:, 0].sum(0), yb.sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(stats[:, 1].sum(0), (yb * yb).sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("N,C,H,W,Co", SHAPES)
+def test_conv3x3_dgrad(gpu_ext, N, C, H, W, Co):
+    from fluxmpi_amd.ops.gemm import conv3x3_dgrad
+    torch.manual_seed(1)
+    x = torch.randn(N, C, H, W, device="cuda", requires_grad=True)
+    w = (torch.randn(Co, C, 3, 3, device="cuda") * 0.1).bfloat16()
+    dy = _nhwc(torch.randn(N, Co, H, W, device="cuda").bfloat16())
+    F.conv2d(x, w.float(), padding=1).backward(dy.float())
+    dx = conv3x3_dgrad(dy, _nhwc(w))
+    assert dx.shape == x.shape and dx.is_contiguous(memory_format=torch.channels_last)
+    assert _rel(dx, x.grad) < 1e-2
+
+
+@pytest.mark.parametrize("M,K,N", [(4096, 64, 256), (1000, 96, 160), (512, 256, 64), (2048, 512, 1024),
+                                   (200, 32, 32), (777, 64, 192), (300, 40, 72)])
+@pytest.mark.parametrize("mode,use_res", [(0, False), (1, False), (0, True)])
+def test_gemm_tn(gpu_ext, M, K, N, mode, use_res, engine):
+    """C = A @ B^T (both K-major) [+ residual] [+ column statistics] on the selected kernel."""
+    from fluxmpi_amd.ops.gemm import SHARDS, gemm
+    torch.manual_seed(3)
+    a = torch.randn(M, K, device="cuda").bfloat16()
+    b = torch.randn(N, K, device="cuda").bfloat16()
+    r = torch.randn(M, N, device="cuda").bfloat16() if use_res else None
+    c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    st = torch.zeros(SHARDS, 2, N, device="cuda") if mode == 1 else None
+    if use_res and engine == 1:
+        pytest.skip("residual epilogue of the register-staged kernel is the dgrad layout only")
+    gemm(a, b, c, M=M, N=N, K=K, lda=K, ldb=K, ldc=N, mode=mode, stats=st, residual=r)
+    ref = a.float() @ b.float().t()
+    if use_res:
+        ref = (ref.bfloat16().float() + r.float())
+    assert _rel(c, ref) < 1e-2
+    if mode == 1:
+        cf = c.float()
+        torch.testing.assert_close(st[:, 0].sum(0), cf.sum(0), rtol=1e-3, atol=1e-1)
+        torch.testing.assert_close(st[:, 1].sum(0), (cf * cf).sum(0), rtol=1e-3, atol=1e-1)
