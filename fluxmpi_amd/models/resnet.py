@@ -106,7 +106,9 @@ class Bottleneck(nn.Module):
                 bnl = grad and fb.BN_LINK
                 out_link = fb.BNStatsLink() if bnl else None
                 if self.hybrid:
-                    a1 = self.bn1(fb.conv1x1_hybrid(x, self.conv1.weight, link, prev), relu=True)
+                    o1 = fb.conv1x1_forward_is_ours(x, self.conv1.weight)
+                    c1 = fb.conv1x1_hybrid(x, self.conv1.weight, link, prev, ours_stats=o1)
+                    a1 = fb.bn_from_stats(c1, self.bn1, relu=True, stats_ready=True) if o1 else self.bn1(c1, relu=True)
                 else:
                     c1 = fb.conv1x1_stats(x, self.conv1.weight, link, prev)  # + bn1 statistics (GEMM epilogue)
                     a1 = fb.bn_from_stats(c1, self.bn1, relu=True)
@@ -133,13 +135,17 @@ class Bottleneck(nn.Module):
                         a2 = fb.bn_from_stats(c2, self.bn2, relu=True, stats_ready=ours, bnlink=bl2)
                     else:
                         a2 = self.bn2(self.conv2(a1), relu=True, bnlink=bl2)
-                    c3 = fb.conv1x1_hybrid(a2, self.conv3.weight, None, bl2)
+                    o3 = fb.conv1x1_forward_is_ours(a2, self.conv3.weight)
+                    c3 = fb.conv1x1_hybrid(a2, self.conv3.weight, None, bl2, ours_stats=o3)
                 else:
                     c2 = fb.conv3x3(a1, self.conv2.weight) if fb.conv3x3_supported(a1, self.conv2) else self.conv2(a1)
                     c3 = fb.bn_relu_conv1x1(c2, self.bn2, self.conv3.weight)  # bn2+relu fused into the A load
-                if self.hybrid:
+                if self.hybrid and not o3:
                     out = self.bn3(c3, relu=True, residual=identity, link=link if self.downsample is None else None,
                                    bnlink=out_link)
+                elif self.hybrid:
+                    out = fb.bn_from_stats(c3, self.bn3, relu=True, residual=identity, stats_ready=True,
+                                           link=link if self.downsample is None else None, bnlink=out_link)
                 else:
                     out = fb.bn_from_stats(c3, self.bn3, relu=True, residual=identity,
                                            link=link if self.downsample is None else None, bnlink=out_link)

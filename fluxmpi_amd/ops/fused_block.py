@@ -45,6 +45,9 @@ BN_LINK = os.environ.get("FLUXMPI_BN_LINK", "0") == "1"
 # statistics in the epilogue) and input gradient on the implicit-GEMM MFMA kernel, weight
 # gradient on MIOpen; "dgrad" = only the input gradient ours; "miopen" = all MIOpen
 CONV3X3 = os.environ.get("FLUXMPI_CONV3X3", "ours")
+# 1x1 forward of the bottlenecks: "ours" = our GEMM + statistics epilogue where measured faster
+# than MIOpen + the statistics pass; "miopen" = always MIOpen
+CONV1X1 = os.environ.get("FLUXMPI_CONV1X1", "ours")
 
 
 def _stream(t):
@@ -138,11 +141,19 @@ class _Conv1x1Hybrid(torch.autograd.Function):
     with the block's residual gradient added in its epilogue (``link``)."""
 
     @staticmethod
-    def forward(ctx, x, weight, link=None, bnlink=None):
+    def forward(ctx, x, weight, link=None, bnlink=None, ours_stats=False):
         x = x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
         ctx.link, ctx.bnlink = link, bnlink
         note_filter(weight)
         ctx.save_for_backward(x, weight)
+        if ours_stats:
+            # our GEMM, the next BatchNorm's statistics accumulated in its epilogue
+            n, ci, h, w = x.shape
+            co = weight.shape[0]
+            c = _empty_nhwc(n, co, h, w, x)
+            gemm(_nhwc2d(x), weight.reshape(co, ci), c, M=n * h * w, N=co, K=ci, lda=ci, ldb=ci, ldc=co, mode=1,
+                 stats=_workspace(x))
+            return c
         return torch.nn.functional.conv2d(x, weight)
 
     @staticmethod
@@ -155,7 +166,7 @@ class _Conv1x1Hybrid(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             dw = torch.ops.aten.convolution_backward(dc, x, weight, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
                                                      [False, True, False])[1]
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
 class _Conv1x1Downsample(torch.autograd.Function):
@@ -380,8 +391,41 @@ def conv1x1_stats(x, weight, link=None, bnlink=None):
     return _Conv1x1Stats.apply(x, weight, link, bnlink)
 
 
-def conv1x1_hybrid(x, weight, link=None, bnlink=None):
-    return _Conv1x1Hybrid.apply(x, weight, link, bnlink)
+_FWD1_CHOICE: dict = {}
+
+
+def conv1x1_forward_is_ours(x, weight) -> bool:
+    """Per-shape choice of a 1x1 forward, measured once: our GEMM with the statistics epilogue
+    vs MIOpen plus the statistics pass the next BatchNorm then needs (one read of the output
+    at 5 TB/s)."""
+    if CONV1X1 != "ours":
+        return False
+    key = (tuple(x.shape), weight.shape[0])
+    hit = _FWD1_CHOICE.get(key)
+    if hit is not None:
+        return hit
+    if torch.cuda.is_current_stream_capturing():
+        return True
+    with torch.no_grad():
+        xs = x.detach().contiguous(memory_format=torch.channels_last)
+        w = weight.detach()
+        n, ci, h, wd = xs.shape
+        co = w.shape[0]
+        ws = torch.zeros_like(_workspace(xs))
+        c = _empty_nhwc(n, co, h, wd, xs)
+        ours = _time_us(lambda: gemm(_nhwc2d(xs), w.reshape(co, ci), c, M=n * h * wd, N=co, K=ci, lda=ci, ldb=ci,
+                                     ldc=co, mode=1, stats=ws))
+        theirs = _time_us(lambda: torch.nn.functional.conv2d(xs, w))
+    stats_pass_us = n * h * wd * co * xs.element_size() / 5e12 * 1e6
+    choice = ours <= theirs + stats_pass_us
+    _FWD1_CHOICE[key] = choice
+    return choice
+
+
+def conv1x1_hybrid(x, weight, link=None, bnlink=None, ours_stats=False):
+    """``ours_stats``: forward on our GEMM with the next BatchNorm's statistics left pending in
+    the workspace (``bn_from_stats(..., stats_ready=True)``); else MIOpen's forward."""
+    return _Conv1x1Hybrid.apply(x, weight, link, bnlink, ours_stats)
 
 
 def bn_from_stats(x, bn, relu=False, residual=None, stats_ready=True, link=None, bnlink=None):
