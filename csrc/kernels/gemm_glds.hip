@@ -291,6 +291,206 @@ void launch_glds(GldsArgs a, hipStream_t s) {
 
 
 // ---------------------------------------------------------------------------------------------
+// Weight gradient: C[m][n] (+)= sum_k A[k][m] * B[k][n] with BOTH operands stored k-major-rows
+// ([K][M] / [K][N], the pixel index k slowest: dY [pix][Cout] and X [pix][Cin] of NHWC
+// activations), split over K (blockIdx.z) into fp32 partials. The tiles [32 k][ROWS] go
+// global -> LDS by LDS-DMA through a 3-stage ring and are read as MFMA fragments with
+// ds_read_b64_tr_b16 (the transposed LDS read). Swizzle of a 16-B slot in a k-row,
+// swz_tr(k): the 64 lanes of one tr read touch 16 k-rows x 32 B, and every 32 lanes (8 rows)
+// land on 8 distinct 32-B bank groups. CONVB: B is the implicit im2col of a 3x3 / s1 / p1
+// convolution (n = tap * Cin + ci, out-of-image taps read zeros).
+template <int ROWS>
+__device__ __forceinline__ int swz_tr(int k) {
+  return ROWS == 128 ? (((k & 3) << 1) | (((k >> 3) & 1) << 3)) : (((((k >> 1) & 1) | (((k >> 3) & 1) << 1))) << 1);
+}
+
+struct WgradArgs {
+  const bf16* a;  // [K][lda] (M contiguous)
+  const bf16* b;  // [K][ldb] (N contiguous), or the NHWC image (CONVB)
+  float* c;       // [splits][M][N] fp32 partials
+  int64_t lda, ldb;
+  int64_t M, N, K;
+  int64_t k_per_split;
+  int tiles_m, tiles_n;
+  int conv_h, conv_w, conv_c;
+};
+
+// Per-lane LDS-DMA loader of a [BK k-rows][ROWS] tile sequence (k advancing by BK per step).
+// A lane's tile row and column (hence its swizzled chunk) never change, so every division is
+// done once: the loop only bumps a pointer (plain operand) or a pixel index with its image
+// position (CONVB, where the tap shift and channel of the lane's column are fixed too).
+template <int ROWS, int BK, bool CONVB>
+struct TrLoader {
+  static constexpr int SPR = ROWS / 8;      // 16-B slots per k-row
+  static constexpr int RPP = 64 / SPR;      // k-rows per 1 KiB piece
+  static constexpr int PPW = BK / RPP / 4;  // pieces per wave (BK k-rows, 4 waves)
+  const bf16* ptr[PPW];  // plain: address of (k, col); CONVB: image + ci
+  int k[PPW];            // pixel / row index of the current step
+  int h[PPW], w[PPW];    // CONVB: image position of pixel k
+  int off[PPW];          // CONVB: tap shift in pixels, dr * W + ds
+  int dr[PPW], ds[PPW];
+  bool colok[PPW];
+
+  __device__ __forceinline__ void init(const bf16* __restrict__ g, int64_t ld, int64_t cols, int64_t c0, int64_t kbeg,
+                                       int H, int W, int C) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      const int row = (wave * PPW + j) * RPP + lane / SPR;
+      const int chunk = (lane % SPR) ^ swz_tr<ROWS>(row);
+      const int64_t col = c0 + chunk * 8;
+      colok[j] = col < cols;
+      k[j] = static_cast<int>(kbeg) + row;
+      if (CONVB) {
+        const int tap = static_cast<int>(col) / C;
+        const int ci = static_cast<int>(col) - tap * C;
+        dr[j] = tap / 3 - 1;
+        ds[j] = tap % 3 - 1;
+        off[j] = dr[j] * W + ds[j];
+        ptr[j] = g + ci;
+        const int hw = k[j] % (H * W);
+        h[j] = hw / W;
+        w[j] = hw - h[j] * W;
+      } else {
+        ptr[j] = g + static_cast<int64_t>(k[j]) * ld + col;
+      }
+    }
+  }
+
+  // issue this wave's pieces of the current step into lds_tile, then advance one step
+  __device__ __forceinline__ void issue_next(bf16* lds_tile, int kend, int64_t ld, int H, int W, int C, int dh_step,
+                                             int dw_step) {
+    const int wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      const void* src = g_zero_line;
+      if (colok[j] && k[j] < kend) {
+        if (CONVB) {
+          if (static_cast<unsigned>(h[j] + dr[j]) < static_cast<unsigned>(H) &&
+              static_cast<unsigned>(w[j] + ds[j]) < static_cast<unsigned>(W))
+            src = ptr[j] + static_cast<int64_t>(k[j] + off[j]) * C;
+        } else {
+          src = ptr[j];
+        }
+      }
+      typedef __attribute__((address_space(3))) char lds_char;
+      typedef __attribute__((address_space(1))) void gl_void;
+      __builtin_amdgcn_global_load_lds((gl_void*)(src),
+                                       (lds_char*)(reinterpret_cast<char*>(lds_tile) + (wave * PPW + j) * 1024), 16, 0, 0);
+      k[j] += BK;
+      if (CONVB) {  // pixel k -> k + BK: (h, w) += (BK / W mod H, BK % W) with one carry each
+        w[j] += dw_step;
+        h[j] += dh_step;
+        if (w[j] >= W) {
+          w[j] -= W;
+          ++h[j];
+        }
+        if (h[j] >= H) h[j] -= H;
+      } else {
+        ptr[j] += BK * ld;
+      }
+    }
+  }
+};
+
+// fragment of 16 columns from r0 of a swizzled [BK][ROWS] tile: lane l holds
+// tile[k = 32 * kh + 8 * (l >> 4) + j][r0 + (l & 15)], j = 0..7 (two ds_read_b64_tr_b16)
+template <int ROWS>
+__device__ __forceinline__ bf16x8 read_frag_tr(const bf16* __restrict__ tile, int r0, int kh = 0) {
+  const int l = threadIdx.x & 63;
+  const int g = l >> 4, li = l & 15, q = li >> 2, p = li & 3;
+  const int col = r0 + 4 * p;
+  const int k0 = 32 * kh + 8 * g + q, k1 = k0 + 4;
+  const bf16* a0 = tile + k0 * ROWS + (((col >> 3) ^ swz_tr<ROWS>(k0)) << 3) + (col & 7);
+  const bf16* a1 = tile + k1 * ROWS + (((col >> 3) ^ swz_tr<ROWS>(k1)) << 3) + (col & 7);
+  typedef short short4v __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) short4v lds_short4v;
+  short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(a0));
+  short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(a1));
+  bf16x8 out;
+  __builtin_memcpy(&out, &lo, 8);
+  __builtin_memcpy(reinterpret_cast<char*>(&out) + 8, &hi, 8);
+  return out;
+}
+
+template <int BM, int BN, int kBK, int kStages, bool CONVB>
+__global__ __launch_bounds__(kThreads, 2) void gemm_wgrad_kernel(WgradArgs p) {
+  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+  constexpr int A_ELEMS = BM * kBK, B_ELEMS = BN * kBK;
+  constexpr int LPT = (BM + BN) * kBK / 2048;
+  __shared__ __attribute__((aligned(16))) bf16 smem[kStages * (A_ELEMS + B_ELEMS)];
+  auto sa = [&](int s) { return smem + s * A_ELEMS; };
+  auto sb = [&](int s) { return smem + kStages * A_ELEMS + s * B_ELEMS; };
+  const int nt = p.tiles_m * p.tiles_n;
+  int bid = blockIdx.x;
+  {
+    const int q = nt / 8, r = nt % 8, xcd = bid % 8, pos = bid / 8;
+    bid = nt >= 8 ? (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos : bid;
+  }
+  const int tm = bid / p.tiles_n, tn = bid % p.tiles_n;
+  const int64_t m0 = static_cast<int64_t>(tm) * BM, n0 = static_cast<int64_t>(tn) * BN;
+  const int64_t kbeg = static_cast<int64_t>(blockIdx.z) * p.k_per_split;
+  const int64_t kend = kbeg + p.k_per_split < p.K ? kbeg + p.k_per_split : p.K;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  TrLoader<BM, kBK, false> la;
+  TrLoader<BN, kBK, CONVB> lb;
+  const int H = p.conv_h, W = p.conv_w, C = p.conv_c;
+  const int dw_step = CONVB ? kBK % W : 0, dh_step = CONVB ? (kBK / W) % H : 0;
+  la.init(p.a, p.lda, p.M, m0, kbeg, 0, 1, 1);
+  lb.init(p.b, p.ldb, p.N, n0, kbeg, H, W, C);
+  const int kend32 = static_cast<int>(kend);
+  auto issue = [&](int s) {
+    la.issue_next(sa(s), kend32, p.lda, 0, 1, 1, 0, 0);
+    lb.issue_next(sb(s), kend32, p.ldb, H, W, C, dh_step, dw_step);
+  };
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = kend > kbeg ? static_cast<int>((kend - kbeg + kBK - 1) / kBK) : 0;
+#pragma unroll
+  for (int s = 0; s < kStages - 1; ++s)
+    if (s < nk) issue(s);
+  for (int t = 0; t < nk; ++t) {
+    const int ahead = nk - 1 - t < kStages - 2 ? nk - 1 - t : kStages - 2;
+    wait_tiles_ahead<LPT, kStages - 2>(ahead);
+    __builtin_amdgcn_s_barrier();
+    if (t + kStages - 1 < nk) issue((t + kStages - 1) % kStages);
+    const bf16* ta = sa(t % kStages);
+    const bf16* tb = sb(t % kStages);
+#pragma unroll
+    for (int kh = 0; kh < kBK / 32; ++kh) {
+      bf16x8 fa[FM], fb[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) fa[i] = read_frag_tr<BM>(ta, wm * WM + i * 16, kh);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) fb[j] = read_frag_tr<BN>(tb, wn * WN + j * 16, kh);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  // fp32 partial of this split: acc[i][j][r] is (row wm*WM + i*16 + 4*(lane>>4) + r, col wn*WN + j*16 + lane&15)
+  float* c = p.c + static_cast<int64_t>(blockIdx.z) * p.M * p.N;
+  const int col_in = lane & 15, rq = 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int64_t n = n0 + wn * WN + j * 16 + col_in;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = m0 + wm * WM + i * 16 + rq + r;
+        if (m < p.M && n < p.N) c[m * p.N + n] = acc[i][j][r];
+      }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Filter transposition for the input-gradient GEMMs: out[ci][t][co] = in[co][T-1-t][ci] for
 // every tensor of a list (T = taps: 1 for a 1x1 filter, 9 for a 3x3 one, whose taps are then
 // also flipped). One launch for up to kMaxXT filters; 64x64 (co x ci) tiles through LDS so
@@ -391,6 +591,47 @@ void gemm_glds(const GemmProblem& g, hipStream_t stream) {
   else GL(64, 64)
 #undef GV
 #undef GL
+}
+
+void gemm_wgrad(const void* a, const void* b, float* ws, int64_t lda, int64_t ldb, int64_t M, int64_t N, int64_t K,
+                int splits, int conv_h, int conv_w, int conv_c, hipStream_t stream, int variant) {
+  if (lda % 8 != 0 || ldb % 8 != 0 || M % 8 != 0 || N % 8 != 0 || splits < 1)
+    throw std::runtime_error("gemm_wgrad: M, N, lda, ldb must be multiples of 8");
+  if (conv_h > 0 && (conv_c % 8 != 0 || N != 9LL * conv_c))
+    throw std::runtime_error("gemm_wgrad: implicit 3x3 B needs C % 8 == 0 and N == 9*C");
+  if (K >= (1LL << 31) || (conv_h > 0 && K % (static_cast<int64_t>(conv_h) * conv_w) != 0))
+    throw std::runtime_error("gemm_wgrad: K must fit 31 bits (and be whole images for the implicit conv)");
+  WgradArgs w{};
+  w.a = static_cast<const bf16*>(a);
+  w.b = static_cast<const bf16*>(b);
+  w.c = ws;
+  w.lda = lda; w.ldb = ldb; w.M = M; w.N = N; w.K = K;
+  // variant 0/1: 32-deep K-step, 3-stage ring; 2: 64-deep, 2 stages. Split boundaries are
+  // multiples of 64 for both (the Python side computes the same split count).
+  const int64_t nk = (K + 63) / 64;
+  w.k_per_split = (nk + splits - 1) / splits * 64;
+  const int sp = static_cast<int>((K + w.k_per_split - 1) / w.k_per_split);
+  w.conv_h = conv_h; w.conv_w = conv_w; w.conv_c = conv_c;
+  const bool m128 = M > 64, n128 = N > 64;
+#define WG(BM, BN)                                                                                      \
+  {                                                                                                     \
+    w.tiles_m = static_cast<int>((M + BM - 1) / BM);                                                   \
+    w.tiles_n = static_cast<int>((N + BN - 1) / BN);                                                   \
+    dim3 grid(w.tiles_m * w.tiles_n, 1, sp);                                                            \
+    if (variant == 2) {                                                                                 \
+      if (conv_h > 0) gemm_wgrad_kernel<BM, BN, 64, 2, true><<<grid, kThreads, 0, stream>>>(w);         \
+      else gemm_wgrad_kernel<BM, BN, 64, 2, false><<<grid, kThreads, 0, stream>>>(w);                   \
+    } else {                                                                                            \
+      if (conv_h > 0) gemm_wgrad_kernel<BM, BN, 32, 3, true><<<grid, kThreads, 0, stream>>>(w);         \
+      else gemm_wgrad_kernel<BM, BN, 32, 3, false><<<grid, kThreads, 0, stream>>>(w);                   \
+    }                                                                                                   \
+  }
+  if (m128 && n128) WG(128, 128)
+  else if (m128) WG(128, 64)
+  else if (n128) WG(64, 128)
+  else WG(64, 64)
+#undef WG
+  FLUXMPI_HIP_CHECK(hipGetLastError());
 }
 
 void transpose_filters(const std::vector<uintptr_t>& src, const std::vector<uintptr_t>& dst,

@@ -32,6 +32,7 @@ import torch
 
 from . import _ext
 from .batchnorm import BNStatsLink, GradLink, SideGradLink, _workspace, bn_counter  # noqa: F401 (links re-exported)
+from . import gemm as G
 from .gemm import conv1x1_dgrad, conv1x1_wgrad, conv3x3_dgrad, conv3x3_fwd, gemm, note_filter
 from .multi_tensor import DTYPE_CODE
 
@@ -48,6 +49,9 @@ CONV3X3 = os.environ.get("FLUXMPI_CONV3X3", "ours")
 # 1x1 forward of the bottlenecks: "ours" = our GEMM + statistics epilogue where measured faster
 # than MIOpen + the statistics pass; "miopen" = always MIOpen
 CONV1X1 = os.environ.get("FLUXMPI_CONV1X1", "ours")
+# weight gradients of the bottleneck convolutions: "auto" = the fastest (measured once per
+# shape) of MIOpen and our split-K transposed-operand kernel in a few configurations
+WGRAD = os.environ.get("FLUXMPI_WGRAD", "auto")
 
 
 def _stream(t):
@@ -164,8 +168,11 @@ class _Conv1x1Hybrid(torch.autograd.Function):
         dx = _dgrad_nhwc(_nhwc2d(dc), weight, x, ctx.link, ctx.bnlink) if ctx.needs_input_grad[0] else None
         dw = None
         if ctx.needs_input_grad[1]:
-            dw = torch.ops.aten.convolution_backward(dc, x, weight, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
-                                                     [False, True, False])[1]
+            co, ci = weight.shape[0], weight.shape[1]
+            dw = wgrad_best(("1x1", tuple(x.shape), co), {
+                "miopen": lambda: torch.ops.aten.convolution_backward(dc, x, weight, None, [1, 1], [0, 0], [1, 1], False,
+                                                                      [0, 0], 1, [False, True, False])[1],
+                "ours": lambda: G.conv1x1_wgrad_v2(_nhwc2d(dc), _nhwc2d(x), out_dtype=weight.dtype).view(co, ci, 1, 1)})
         return dx, dw, None, None, None
 
 
@@ -325,8 +332,10 @@ class _Conv3x3(torch.autograd.Function):
         dx = conv3x3_dgrad(dy, weight) if ctx.needs_input_grad[0] else None
         dw = None
         if ctx.needs_input_grad[1]:
-            dw = torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
-                                                     [False, True, False])[1]
+            dw = wgrad_best(("3x3", tuple(x.shape), weight.shape[0]), {
+                "miopen": lambda: torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [1, 1], [1, 1], False,
+                                                                      [0, 0], 1, [False, True, False])[1],
+                "ours": lambda: G.conv3x3_wgrad(dy, x)})
         return dx, dw, None, None
 
 
@@ -350,6 +359,44 @@ def _time_us(fn, iters=5):
     e.record()
     e.synchronize()
     return s.elapsed_time(e) * 1e3 / iters
+
+
+_WG_CHOICE: dict = {}
+# our weight-gradient kernel configurations tried by the autotune: (variant, target workgroups)
+_WG_CONFIGS = ((2, 512), (2, 768), (1, 1536))
+
+
+def wgrad_best(key, impls: dict):
+    """Run the fastest weight-gradient implementation for ``key`` (measured on first use, like
+    cudnn.benchmark: MIOpen vs our kernel in each of ``_WG_CONFIGS``) and return its result."""
+    choice = _WG_CHOICE.get(key)
+    if choice is None:
+        if WGRAD == "miopen" or torch.cuda.is_current_stream_capturing():
+            choice = ("miopen", None)
+        elif WGRAD == "ours":
+            choice = ("ours", _WG_CONFIGS[0])
+        else:
+            best = (_time_us(impls["miopen"]), ("miopen", None))
+            saved = G.WGRAD_VARIANT, G.WGRAD_TARGET_WG
+            try:
+                for cfg in _WG_CONFIGS:
+                    G.WGRAD_VARIANT, G.WGRAD_TARGET_WG = cfg
+                    t = _time_us(impls["ours"])
+                    if t < best[0]:
+                        best = (t, ("ours", cfg))
+            finally:
+                G.WGRAD_VARIANT, G.WGRAD_TARGET_WG = saved
+            choice = best[1]
+        _WG_CHOICE[key] = choice
+    name, cfg = choice
+    if cfg is None:
+        return impls[name]()
+    saved = G.WGRAD_VARIANT, G.WGRAD_TARGET_WG
+    G.WGRAD_VARIANT, G.WGRAD_TARGET_WG = cfg
+    try:
+        return impls[name]()
+    finally:
+        G.WGRAD_VARIANT, G.WGRAD_TARGET_WG = saved
 
 
 def conv3x3_forward_is_ours(x, weight) -> bool:

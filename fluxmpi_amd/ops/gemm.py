@@ -230,3 +230,66 @@ def conv1x1_wgrad(dy2d: torch.Tensor, x2d: torch.Tensor, in_affine=None, out: to
     C.gemm_splitk_reduce(ws.data_ptr(), s, Co * Ci, dw.data_ptr(), 9 if dw.dtype == torch.bfloat16 else 7,
                          _stream(dw))
     return dw
+
+
+# ---- weight gradients on the LDS-DMA transposed-operand kernel --------------------------------
+# workgroups the weight-gradient split-K aims at (one round of the 3-per-CU kernel on 256 CUs)
+WGRAD_TARGET_WG = int(os.environ.get("FLUXMPI_WGRAD_TARGET_WG", "768"))
+
+
+def _wgrad_splits_v2(M: int, N: int, K: int) -> int:
+    """Split-K factor: ~WGRAD_TARGET_WG workgroups, >= 256 pixels per split, and at most 64 MiB
+    of fp32 partials (each is written once and read once by the reduce)."""
+    tiles = max(1, -(-M // 128)) * max(1, -(-N // 128))
+    s_occ = -(-WGRAD_TARGET_WG // tiles)
+    s_bytes = max(1, (64 << 20) // (M * N * 4))
+    return int(max(1, min(s_occ, s_bytes, K // 256)))
+
+
+def _wgrad_reduce(ws, splits, dw):
+    C = _ext.get(required=True)
+    C.gemm_splitk_reduce(ws.data_ptr(), splits, dw.numel(), dw.data_ptr(), 9 if dw.dtype == torch.bfloat16 else 7,
+                         _stream(dw))
+    return dw
+
+
+def _actual_splits_v2(K: int, splits: int) -> int:
+    nk = -(-K // 64)
+    kps = -(-nk // splits) * 64
+    return -(-K // kps)
+
+
+# weight-gradient kernel variant: 1 = 32-deep K-step / 3 stages, 2 = 64-deep / 2 stages
+WGRAD_VARIANT = int(os.environ.get("FLUXMPI_WGRAD_VARIANT", "1"))
+
+
+def conv1x1_wgrad_v2(dy2d: torch.Tensor, x2d: torch.Tensor, out_dtype=torch.bfloat16, splits: int | None = None):
+    """dW [Cout, Cin] = dY^T X over the pixels, split-K fp32 partials + one reduce launch."""
+    K, Co = dy2d.shape
+    Ci = x2d.shape[1]
+    s = _actual_splits_v2(K, splits or _wgrad_splits_v2(Co, Ci, K))
+    ws = torch.empty(s, Co, Ci, device=dy2d.device, dtype=torch.float32)
+    C = _ext.get(required=True)
+    C.gemm_wgrad(dy2d.data_ptr(), x2d.data_ptr(), ws.data_ptr(), dy2d.stride(0), x2d.stride(0), Co, Ci, K, s, 0, 0, 0,
+                 _stream(dy2d), WGRAD_VARIANT)
+    return _wgrad_reduce(ws, s, torch.empty(Co, Ci, device=dy2d.device, dtype=out_dtype))
+
+
+def conv3x3_wgrad(dy: torch.Tensor, x: torch.Tensor, splits: int | None = None) -> torch.Tensor:
+    """Weight gradient of the 3x3/s1/p1 convolution: dW[co][(r, s, ci)] = sum over pixels of
+    dY[pix][co] * X[pix + (r-1)*W + (s-1)][ci] — the implicit im2col is the B operand. Returns
+    [Co, Ci, 3, 3] in channels_last (the filter parameters' layout)."""
+    n, co, h, wd = dy.shape
+    ci = x.shape[1]
+    dys = dy if dy.is_contiguous(memory_format=torch.channels_last) else dy.contiguous(
+        memory_format=torch.channels_last)
+    xs = x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
+    K, N = n * h * wd, 9 * ci
+    s = _actual_splits_v2(K, splits or _wgrad_splits_v2(co, N, K))
+    ws = torch.empty(s, co, N, device=dy.device, dtype=torch.float32)
+    C = _ext.get(required=True)
+    C.gemm_wgrad(dys.data_ptr(), xs.data_ptr(), ws.data_ptr(), co, ci, co, N, K, s, h, wd, ci, _stream(dy),
+                 WGRAD_VARIANT)
+    dw = torch.empty(co, 3, 3, ci, device=dy.device, dtype=dy.dtype)
+    _wgrad_reduce(ws, s, dw)
+    return dw.permute(0, 3, 1, 2)

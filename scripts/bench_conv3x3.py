@@ -10,7 +10,7 @@ import torch.nn.functional as F
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from fluxmpi_amd.ops import gemm as G  # noqa: E402
-from fluxmpi_amd.ops.gemm import conv3x3_dgrad, conv3x3_fwd  # noqa: E402
+from fluxmpi_amd.ops.gemm import conv1x1_wgrad_v2, conv3x3_dgrad, conv3x3_fwd, conv3x3_wgrad  # noqa: E402
 from fluxmpi_amd.utils.miopen import install_tuned_db  # noqa: E402
 
 
@@ -49,6 +49,9 @@ def main():
         rec["ours_dgrad"] = rec["e2_dgrad"]
         rec["miopen_dgrad"] = bench(lambda: torch.ops.aten.convolution_backward(
             dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False]))
+        for v, tw in ((1, 768), (2, 768), (1, 1536), (2, 512)):
+            G.WGRAD_VARIANT, G.WGRAD_TARGET_WG = v, tw
+            rec[f"ours_wgrad_v{v}_{tw}"] = bench(lambda: conv3x3_wgrad(dy, x))
         rec["miopen_wgrad"] = bench(lambda: torch.ops.aten.convolution_backward(
             dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False]))
         for k in ("ours_fwd", "miopen_fwd", "ours_dgrad", "miopen_dgrad"):
@@ -58,6 +61,25 @@ def main():
                 tot[k] = round(tot.get(k, 0.0) + v, 1)
         print(json.dumps(rec), flush=True)
     print(json.dumps({"total_us": tot}))
+    # 1x1 weight gradients (ResNet-50 bottleneck shapes)
+    tot1 = {}
+    for H, ci, co in [(56, 64, 64), (56, 64, 256), (56, 256, 64), (28, 128, 512), (28, 512, 128), (14, 256, 1024),
+                      (14, 1024, 256), (7, 512, 2048), (7, 2048, 512)]:
+        x = torch.randn(B, ci, H, H, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+        dy = torch.randn(B, co, H, H, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+        w = torch.randn(co, ci, 1, 1, device="cuda").bfloat16()
+        x2, dy2 = x.permute(0, 2, 3, 1).reshape(-1, ci), dy.permute(0, 2, 3, 1).reshape(-1, co)
+        rec = {"H": H, "Cin": ci, "Cout": co}
+        for v, tw in ((1, 768), (2, 768), (1, 1536), (2, 512)):
+            G.WGRAD_VARIANT, G.WGRAD_TARGET_WG = v, tw
+            rec[f"ours_wgrad1_v{v}_{tw}"] = bench(lambda: conv1x1_wgrad_v2(dy2, x2))
+        rec["miopen_wgrad1"] = bench(lambda: torch.ops.aten.convolution_backward(
+            dy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1, [False, True, False]))
+        for k, v in rec.items():
+            if "wgrad" in k:
+                tot1[k] = round(tot1.get(k, 0.0) + v, 1)
+        print(json.dumps(rec), flush=True)
+    print(json.dumps({"total_us_wgrad1": tot1}))
 
 
 if __name__ == "__main__":

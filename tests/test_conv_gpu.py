@@ -87,3 +87,37 @@ def test_gemm_tn(gpu_ext, M, K, N, mode, use_res, engine):
         cf = c.float()
         torch.testing.assert_close(st[:, 0].sum(0), cf.sum(0), rtol=1e-3, atol=1e-1)
         torch.testing.assert_close(st[:, 1].sum(0), (cf * cf).sum(0), rtol=1e-3, atol=1e-1)
+
+
+@pytest.mark.parametrize("N,C,H,W,Co", SHAPES)
+def test_conv3x3_wgrad(gpu_ext, N, C, H, W, Co, engine, monkeypatch):
+    from fluxmpi_amd.ops import gemm as G
+    from fluxmpi_amd.ops.gemm import conv3x3_wgrad
+    if engine not in (1, 2):
+        pytest.skip("engine 1/2 select the wgrad variant here")
+    monkeypatch.setattr(G, "WGRAD_VARIANT", engine)
+    torch.manual_seed(5)
+    x = _nhwc(torch.randn(N, C, H, W, device="cuda").bfloat16())
+    dy = _nhwc(torch.randn(N, Co, H, W, device="cuda").bfloat16())
+    w = torch.zeros(Co, C, 3, 3, device="cuda", requires_grad=True)
+    F.conv2d(x.float(), w, padding=1).backward(dy.float())
+    for splits in (None, 1, 3):
+        dw = conv3x3_wgrad(dy, x, splits=splits)
+        assert dw.shape == w.shape and dw.is_contiguous(memory_format=torch.channels_last)
+        assert _rel(dw, w.grad) < 1e-2, splits
+
+
+@pytest.mark.parametrize("M,K,N", [(4096, 64, 256), (1000, 96, 160), (512, 256, 64), (2048, 512, 1024), (777, 64, 192)])
+def test_conv1x1_wgrad_v2(gpu_ext, M, K, N, engine, monkeypatch):
+    from fluxmpi_amd.ops import gemm as G
+    from fluxmpi_amd.ops.gemm import conv1x1_wgrad_v2
+    if engine not in (1, 2):
+        pytest.skip("engine 1/2 select the wgrad variant here")
+    monkeypatch.setattr(G, "WGRAD_VARIANT", engine)
+    torch.manual_seed(6)
+    dy = torch.randn(M, N, device="cuda").bfloat16()
+    x = torch.randn(M, K, device="cuda").bfloat16()
+    ref = dy.float().t() @ x.float()
+    for splits in (None, 1, 5):
+        dw = conv1x1_wgrad_v2(dy, x, out_dtype=torch.float32, splits=splits)
+        assert _rel(dw, ref) < 1e-3, splits

@@ -169,3 +169,25 @@ def test_bn_stats_link(gpu_ext, with_res):
         grads.append([ci.grad, wi.grad, bn.weight.grad, bn.bias.grad] + ([ri.grad] if with_res else []))
     for a, b in zip(*grads):
         assert _rel(b, a) < 2e-3, (_rel(b, a))
+
+
+@pytest.mark.parametrize("wgrad", ["ours", "miopen"])
+def test_hybrid_resnet_weight_gradient_kernels(gpu_ext, wgrad, monkeypatch):
+    """The hybrid ResNet with every bottleneck weight gradient forced onto our split-K kernel
+    (or MIOpen) matches the fp32 model as closely as the unfused bf16 pipeline does."""
+    from fluxmpi_amd.models.resnet import ResNet
+    from fluxmpi_amd.ops import fused_block as fb
+    monkeypatch.setattr(fb, "WGRAD", wgrad)
+    monkeypatch.setattr(fb, "_WG_CHOICE", {})
+    ref, fus = _models("hybrid")
+    f32 = ResNet((2, 1, 1, 1), 10, conv_impl="miopen", norm="fused").cuda().to(memory_format=torch.channels_last)
+    f32.load_state_dict({k: v.float() if v.is_floating_point() else v for k, v in ref.state_dict().items()})
+    x = torch.randn(8, 3, 64, 64, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    ya, yb, yc = ref(x), fus(x), f32(x.float())
+    g = torch.randn_like(yc)
+    for y in (ya, yb, yc):
+        (y.float() * g).sum().backward()
+    assert fb._WG_CHOICE and all(c[0] == wgrad for c in fb._WG_CHOICE.values())
+    for (n, pa), pb, pc in zip(ref.named_parameters(), fus.parameters(), f32.parameters()):
+        ea, eb = _rel(pa.grad, pc.grad), _rel(pb.grad, pc.grad)
+        assert eb < 2 * ea + 2e-2, f"{n}: {wgrad} {eb:.3e} vs unfused {ea:.3e}"
