@@ -47,9 +47,16 @@ struct GldsArgs {
   float* stats;
   int64_t lda, ldb, ldc, ldr;
   int64_t M, N, K;
-  int mode;  // 0: C; 1: C + column statistics
+  int mode;  // 0: C; 1: C + column statistics (or BN-backward reductions, bnb_x != nullptr)
   int tiles_m, tiles_n;
   int conv_h, conv_w, conv_c;
+  const bf16* bnb_x;  // BN-backward epilogue: the BatchNorm input [M][N] dense
+  const float* bnb_w;
+  const float* bnb_b;
+  const float* bnb_mean;
+  const float* bnb_inv;
+  const uint8_t* bnb_mask;
+  int bnb_rm;
 };
 
 // s_waitcnt vmcnt(N) with expcnt / lgkmcnt left alone (gfx9 encoding)
@@ -209,42 +216,82 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_glds_kernel(GldsArgs p) {
   __syncthreads();
   constexpr int CPR = BN / 8;          // 16-B chunks per row
   constexpr int RPI = kThreads / CPR;  // rows per sweep
+  constexpr int UB = 4;                // rows per batch: their residual / BN-input loads issue together
   const int cc = threadIdx.x % CPR, r0 = threadIdx.x / CPR;
   const int64_t n = n0 + cc * 8;
-  const bool ncol_ok = n + 8 <= p.N;
+  const bool ncol_ok = n < p.N;  // N % 8 == 0 (host-checked): a chunk is all in or all out
+  const int rows_valid = p.M - m0 < BM ? static_cast<int>(p.M - m0) : BM;
+  // BN-backward epilogue (mode 1 + bnb_x): C is the output gradient of a BatchNorm whose input is
+  // bnb_x; accumulate sum(dy_eff) and sum(dy_eff * xhat) per column instead of sum / sumsq of C.
+  // dy_eff = C masked by the BN's ReLU: rm 2 recomputes it bit-identically to the forward
+  // (fma(x, w*invstd, b - mean*w*invstd) > 0), rm 3 reads the 1-bit mask.
+  const bool bnb = p.bnb_x != nullptr;
+  float bmu[8], biv[8], bsc[8], bsh[8];
+  if (bnb) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int64_t c = ncol_ok ? n + e : 0;
+      bmu[e] = p.bnb_mean[c];
+      biv[e] = p.bnb_inv[c];
+      bsc[e] = (p.bnb_w ? p.bnb_w[c] : 1.f) * biv[e];
+      bsh[e] = fmaf(-bmu[e], bsc[e], p.bnb_b ? p.bnb_b[c] : 0.f);
+    }
+  }
   float cs[8], cq[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) cs[e] = cq[e] = 0.f;
-#pragma unroll 4
-  for (int r = r0; r < BM; r += RPI) {
-    const int64_t m = m0 + r;
-    if (m >= p.M) break;
-    uint4 v = *reinterpret_cast<const uint4*>(smem + r * CS + cc * 8);
-    bf16 e8[8];
-    __builtin_memcpy(e8, &v, 16);
-    if (RES) {
-      bf16 r8[8];
-      if (ncol_ok) {
-        const uint4 rv = *reinterpret_cast<const uint4*>(p.res + m * p.ldr + n);
-        __builtin_memcpy(r8, &rv, 16);
-      } else {
-        for (int e = 0; e < 8; ++e) r8[e] = n + e < p.N ? p.res[m * p.ldr + n + e] : static_cast<bf16>(0.f);
+  for (int rb = r0; rb < BM; rb += UB * RPI) {
+    uint4 rv[UB], xv[UB];
+    unsigned mk[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int r = rb + u * RPI;
+      const int64_t m = m0 + r;
+      const bool ok = r < BM && r < rows_valid && ncol_ok;
+      rv[u] = xv[u] = make_uint4(0, 0, 0, 0);
+      mk[u] = 0xFFu;
+      if (RES && ok) rv[u] = *reinterpret_cast<const uint4*>(p.res + m * p.ldr + n);
+      if (bnb && ok) {
+        xv[u] = *reinterpret_cast<const uint4*>(p.bnb_x + m * p.N + n);
+        if (p.bnb_rm == 3) mk[u] = p.bnb_mask[(m * p.N + n) >> 3];
       }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) e8[e] = static_cast<bf16>(static_cast<float>(e8[e]) + static_cast<float>(r8[e]));
-      __builtin_memcpy(&v, e8, 16);
     }
-    if (ncol_ok) {
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int r = rb + u * RPI;
+      if (r >= BM || r >= rows_valid || !ncol_ok) continue;
+      const int64_t m = m0 + r;
+      uint4 v = *reinterpret_cast<const uint4*>(smem + r * CS + cc * 8);
+      bf16 e8[8];
+      __builtin_memcpy(e8, &v, 16);
+      if (RES) {
+        bf16 r8[8];
+        __builtin_memcpy(r8, &rv[u], 16);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) e8[e] = static_cast<bf16>(static_cast<float>(e8[e]) + static_cast<float>(r8[e]));
+        __builtin_memcpy(&v, e8, 16);
+      }
       *reinterpret_cast<uint4*>(p.c + m * p.ldc + n) = v;
-    } else {
-      for (int e = 0; e < 8 && n + e < p.N; ++e) p.c[m * p.ldc + n + e] = e8[e];
-    }
-    if (p.mode == 1) {
+      if (bnb) {
+        bf16 x8[8];
+        __builtin_memcpy(x8, &xv[u], 16);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float f = n + e < p.N ? static_cast<float>(e8[e]) : 0.f;
-        cs[e] += f;
-        cq[e] = fmaf(f, f, cq[e]);
+        for (int e = 0; e < 8; ++e) {
+          const float xf = static_cast<float>(x8[e]);
+          bool keep = true;
+          if (p.bnb_rm == 2) keep = fmaf(xf, bsc[e], bsh[e]) > 0.f;
+          if (p.bnb_rm == 3) keep = (mk[u] >> e) & 1u;
+          const float dd = keep ? static_cast<float>(e8[e]) : 0.f;
+          cs[e] += dd;
+          cq[e] = fmaf(dd, (xf - bmu[e]) * biv[e], cq[e]);
+        }
+      } else if (p.mode == 1) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float f = static_cast<float>(e8[e]);
+          cs[e] += f;
+          cq[e] = fmaf(f, f, cq[e]);
+        }
       }
     }
   }
@@ -542,8 +589,10 @@ __global__ __launch_bounds__(kThreads) void xpose_taps_kernel(XposeArgs a) {
 
 bool gemm_glds_supported(const GemmProblem& g) {
   return g.a_kmajor && g.b_kmajor && g.mode <= 1 && (g.splits <= 1) && g.a_scale == nullptr &&
-         g.b_scale == nullptr && g.bnb_x == nullptr && g.K % 8 == 0 && g.lda % 8 == 0 && g.ldb % 8 == 0 &&
+         g.b_scale == nullptr && g.K % 8 == 0 && g.N % 8 == 0 && g.lda % 8 == 0 && g.ldb % 8 == 0 &&
          g.ldc % 8 == 0 && (g.res == nullptr || g.ldr % 8 == 0) &&
+         (g.bnb_x == nullptr || (g.mode == 1 && g.ldc == g.N && g.bnb_mean != nullptr && g.bnb_inv != nullptr &&
+                                 (g.bnb_rm == 0 || g.bnb_rm == 2 || (g.bnb_rm == 3 && g.bnb_mask != nullptr)))) &&
          (g.conv_h == 0 || (g.conv_c % 32 == 0 && g.K == 9LL * g.conv_c));
 }
 
@@ -559,6 +608,9 @@ void gemm_glds(const GemmProblem& g, hipStream_t stream) {
   a.M = g.M; a.N = g.N; a.K = g.K;
   a.mode = g.mode;
   a.conv_h = g.conv_h; a.conv_w = g.conv_w; a.conv_c = g.conv_c;
+  a.bnb_x = static_cast<const bf16*>(g.bnb_x);
+  a.bnb_w = g.bnb_w; a.bnb_b = g.bnb_b; a.bnb_mean = g.bnb_mean; a.bnb_inv = g.bnb_inv;
+  a.bnb_mask = g.bnb_mask; a.bnb_rm = g.bnb_rm;
   const bool conv = g.conv_h > 0, res = g.res != nullptr;
   // variant: 1 BK32/3 stages; 2 BK32/4; 3 BK64/2; 4 BK64/3 (engine 3..6 force one, for experiments).
   // Auto (measured on MI355X, ResNet-50 1x1 and 3x3 shapes): a 64-deep K-step in a 2-stage ring

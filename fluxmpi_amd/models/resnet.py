@@ -105,10 +105,14 @@ class Bottleneck(nn.Module):
                 prev = getattr(x, "_fluxmpi_bnlink", None) if (link is not None and self.downsample is None) else None
                 bnl = grad and fb.BN_LINK
                 out_link = fb.BNStatsLink() if bnl else None
+                bl1 = None
                 if self.hybrid:
+                    # bn1 -> conv2 (its only consumer): conv2's dgrad epilogue reduces bn1's backward
+                    bl1 = fb.BNStatsLink() if (bnl and fb.conv3x3_supported(x, self.conv2)) else None
                     o1 = fb.conv1x1_forward_is_ours(x, self.conv1.weight)
                     c1 = fb.conv1x1_hybrid(x, self.conv1.weight, link, prev, ours_stats=o1)
-                    a1 = fb.bn_from_stats(c1, self.bn1, relu=True, stats_ready=True) if o1 else self.bn1(c1, relu=True)
+                    a1 = fb.bn_from_stats(c1, self.bn1, relu=True, stats_ready=True, bnlink=bl1) if o1 else \
+                        self.bn1(c1, relu=True, bnlink=bl1)
                 else:
                     c1 = fb.conv1x1_stats(x, self.conv1.weight, link, prev)  # + bn1 statistics (GEMM epilogue)
                     a1 = fb.bn_from_stats(c1, self.bn1, relu=True)
@@ -131,7 +135,7 @@ class Bottleneck(nn.Module):
                         # implicit-GEMM conv2 (input gradient always; forward where measured faster,
                         # then bn2's statistics come from its epilogue)
                         ours = fb.conv3x3_forward_is_ours(a1, self.conv2.weight)
-                        c2 = fb.conv3x3(a1, self.conv2.weight, with_stats=True)
+                        c2 = fb.conv3x3(a1, self.conv2.weight, with_stats=True, bnlink=bl1)
                         a2 = fb.bn_from_stats(c2, self.bn2, relu=True, stats_ready=ours, bnlink=bl2)
                     else:
                         a2 = self.bn2(self.conv2(a1), relu=True, bnlink=bl2)

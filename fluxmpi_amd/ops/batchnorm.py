@@ -53,6 +53,24 @@ def _workspace(x: torch.Tensor) -> torch.Tensor:
     return ws
 
 
+_LWS: dict = {}
+
+
+def _link_workspace(x: torch.Tensor) -> torch.Tensor:
+    """A second persistent zeroed accumulator, for BatchNorm-backward reductions that a GEMM
+    epilogue deposits for a LATER BatchNorm backward (:class:`BNStatsLink`). Autograd may run
+    another BatchNorm backward in between (e.g. a ResNet downsample branch between conv2's
+    dgrad and bn1's backward), which reduces into :func:`_workspace`; keeping the linked sums
+    apart makes the two independent."""
+    stream = torch.cuda.current_stream(x.device)
+    key = (x.device.index, stream.cuda_stream)
+    ws = _LWS.get(key)
+    if ws is None:
+        ws = torch.zeros(_SHARDS * 2 * _MAXC, device=x.device, dtype=torch.float32)
+        _LWS[key] = ws
+    return ws
+
+
 def kernel_supported(x: torch.Tensor) -> bool:
     if not x.is_cuda or x.dtype not in (torch.bfloat16, torch.float16, torch.float32):
         return False
@@ -216,7 +234,7 @@ class _FusedBN(torch.autograd.Function):
         # the finalize kernel always produces both reductions (they feed dx)
         dw = torch.empty(ch, device=x.device, dtype=torch.float32)
         db = torch.empty(ch, device=x.device, dtype=torch.float32)
-        ws = _workspace(x)
+        ws = _link_workspace(x) if stats_ready else _workspace(x)
         stream = torch.cuda.current_stream(x.device).cuda_stream
         C.bn_bwd(dy.data_ptr(), x.data_ptr(), 0, mask.data_ptr() if mask is not None else 0,
                  w32.data_ptr() if w32 is not None else 0, b32.data_ptr() if b32 is not None else 0,

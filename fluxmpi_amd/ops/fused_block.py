@@ -31,7 +31,7 @@ import os
 import torch
 
 from . import _ext
-from .batchnorm import BNStatsLink, GradLink, SideGradLink, _workspace, bn_counter  # noqa: F401 (links re-exported)
+from .batchnorm import BNStatsLink, GradLink, SideGradLink, _link_workspace, _workspace, bn_counter  # noqa: F401 (links re-exported)
 from . import gemm as G
 from .gemm import conv1x1_dgrad, conv1x1_wgrad, conv3x3_dgrad, conv3x3_fwd, gemm, note_filter
 from .multi_tensor import DTYPE_CODE
@@ -82,7 +82,7 @@ def _bn_bwd(dy, x, mask, w32, b32, mean, inv, relu, has_res, stats_ready=False):
     dres = torch.empty_like(x) if has_res else None
     dw = torch.empty(ch, device=x.device, dtype=torch.float32)
     db = torch.empty(ch, device=x.device, dtype=torch.float32)
-    ws = _workspace(x)
+    ws = _link_workspace(x) if stats_ready else _workspace(x)
     C.bn_bwd(dy.data_ptr(), x.data_ptr(), 0, _p(mask), _p(w32), _p(b32), mean.data_ptr(), inv.data_ptr(),
              dx.data_ptr(), _p(dres), dw.data_ptr(), db.data_ptr(), ws.data_ptr(), rows, ch, int(relu),
              DTYPE_CODE[x.dtype], _stream(x), int(stats_ready))
@@ -132,7 +132,7 @@ def _dgrad_nhwc(dc2, weight, x, link, bnlink=None):
     if bnlink is not None and bnlink.bound and bnlink.x.shape == x.shape and \
             bnlink.x.is_contiguous(memory_format=torch.channels_last):
         bn = (_nhwc2d(bnlink.x), bnlink.w32, bnlink.b32, bnlink.mean, bnlink.inv, bnlink.mask, bnlink.relu_mode)
-        stats = _workspace(dx)
+        stats = _link_workspace(dx)
     conv1x1_dgrad(dc2, weight.reshape(co, ci), residual=res, out=_nhwc2d(dx), bn_bwd=bn, stats=stats, w4d=weight)
     if bn is not None:
         bnlink.ready = True
@@ -303,7 +303,7 @@ class _BNReluConv1x1(torch.autograd.Function):
         # d(relu(bn(c2))) = dc3 @ W with the BN-backward reductions (ReLU mask recomputed from c2)
         # accumulated in the same GEMM's epilogue, then the BN backward without its reduce pass
         da = conv1x1_dgrad(dc3_2d, weight.reshape(co, ch), bn_bwd=(c2_2d, w32, b32, mean, inv, None, 2),
-                           stats=_workspace(c2)).view(n, h, w, ch).permute(0, 3, 1, 2)
+                           stats=_link_workspace(c2)).view(n, h, w, ch).permute(0, 3, 1, 2)
         dc2, _, dbw, dbb = _bn_bwd(da, c2, None, w32, b32, mean, inv, True, False, stats_ready=True)
         return dc2, dbw.to(ctx.bn_wdtype), dbb.to(ctx.bn_wdtype), None, None, dw, None, None, None
 
@@ -314,8 +314,9 @@ class _Conv3x3(torch.autograd.Function):
     MFMA kernel; weight gradient on MIOpen."""
 
     @staticmethod
-    def forward(ctx, x, weight, fwd_ours, with_stats):
+    def forward(ctx, x, weight, fwd_ours, with_stats, bnlink=None):
         x = x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
+        ctx.bnlink = bnlink
         note_filter(weight)
         if fwd_ours:
             y = conv3x3_fwd(x, weight, stats=_workspace(x) if with_stats else None)
@@ -329,14 +330,25 @@ class _Conv3x3(torch.autograd.Function):
         x, weight = ctx.saved_tensors
         if not dy.is_contiguous(memory_format=torch.channels_last):
             dy = dy.contiguous(memory_format=torch.channels_last)
-        dx = conv3x3_dgrad(dy, weight) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            bl = ctx.bnlink
+            bn = stats = None
+            if bl is not None and bl.bound and bl.x.shape == x.shape and \
+                    bl.x.is_contiguous(memory_format=torch.channels_last) and G.ENGINE != 1:
+                # the epilogue reduces the backward statistics of the BatchNorm that produced x
+                bn = (_nhwc2d(bl.x), bl.w32, bl.b32, bl.mean, bl.inv, bl.mask, bl.relu_mode)
+                stats = _link_workspace(x)
+            dx = conv3x3_dgrad(dy, weight, bn_bwd=bn, stats=stats)
+            if bn is not None:
+                bl.ready = True
         dw = None
         if ctx.needs_input_grad[1]:
             dw = wgrad_best(("3x3", tuple(x.shape), weight.shape[0]), {
                 "miopen": lambda: torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [1, 1], [1, 1], False,
                                                                       [0, 0], 1, [False, True, False])[1],
                 "ours": lambda: G.conv3x3_wgrad(dy, x)})
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
 def conv3x3_supported(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
@@ -425,13 +437,13 @@ def conv3x3_forward_is_ours(x, weight) -> bool:
     return choice
 
 
-def conv3x3(x, weight, with_stats=False):
+def conv3x3(x, weight, with_stats=False, bnlink=None):
     """Returns the conv output. If the forward runs on our kernel (:func:`conv3x3_forward_is_ours`)
     and ``with_stats``, its per-channel sum / sumsq are pending in the BatchNorm workspace
     (consume them with ``bn_from_stats(..., stats_ready=True)``); check with
     ``conv3x3_forward_is_ours`` first."""
     ours = conv3x3_forward_is_ours(x, weight)
-    return _Conv3x3.apply(x, weight, ours, with_stats and ours)
+    return _Conv3x3.apply(x, weight, ours, with_stats and ours, bnlink)
 
 
 def conv1x1_stats(x, weight, link=None, bnlink=None):

@@ -78,10 +78,11 @@ def conv1x1_dgrad(dy2d: torch.Tensor, w2d: torch.Tensor, residual: torch.Tensor 
         assert residual.shape == (M, Ci) and residual.dtype == torch.bfloat16 and residual.stride(1) == 1
     if bn_bwd is not None:
         assert stats is not None and dx.stride(0) == Ci and bn_bwd[0].shape == (M, Ci) and bn_bwd[0].stride(0) == Ci
-    if bn_bwd is None and ENGINE != 1 and w4d is not None and dy2d.stride(0) % 8 == 0:
-        # LDS-DMA kernel on the cached W^T (K-major B)
+    if ENGINE != 1 and w4d is not None and dy2d.stride(0) % 8 == 0 and Ci % 8 == 0:
+        # LDS-DMA kernel on the cached W^T (K-major B); the BN-backward epilogue is supported too
         gemm(dy2d, filter_t(w4d), dx, M=M, N=Ci, K=Co, lda=dy2d.stride(0), ldb=Co, ldc=dx.stride(0),
-             residual=residual, engine=ENGINE or 2)
+             residual=residual, mode=1 if bn_bwd is not None else 0, stats=stats, bn_bwd=bn_bwd,
+             engine=ENGINE or 2)
         return dx
     gemm(dy2d, w2d, dx, M=M, N=Ci, K=Co, lda=dy2d.stride(0), ldb=w2d.stride(0), ldc=dx.stride(0), a_kmajor=True,
          b_kmajor=False, residual=residual, mode=1 if bn_bwd is not None else 0, stats=stats, bn_bwd=bn_bwd,
@@ -163,9 +164,12 @@ def conv3x3_fwd(x: torch.Tensor, w: torch.Tensor, in_affine=None, stats: torch.T
     return y
 
 
-def conv3x3_dgrad(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+def conv3x3_dgrad(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None, bn_bwd=None,
+                  stats: torch.Tensor | None = None) -> torch.Tensor:
     """Input gradient of the 3x3/s1/p1 convolution: the same implicit GEMM over dY with the
-    filter transposed and flipped (``WT[ci][r][s][co] = W[co][ci][2-r][2-s]``)."""
+    filter transposed and flipped (``WT[ci][r][s][co] = W[co][ci][2-r][2-s]``). ``bn_bwd`` /
+    ``stats``: the epilogue accumulates the backward reductions of the BatchNorm that produced
+    the convolution's input (see :func:`gemm`)."""
     n, co, h, wd = dy.shape
     ci = w.shape[1]
     dys = dy if dy.is_contiguous(memory_format=torch.channels_last) else dy.contiguous(
@@ -175,7 +179,10 @@ def conv3x3_dgrad(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = 
     else:
         wt = filter_t(w)
     dx = out if out is not None else torch.empty(n, h, wd, ci, device=dy.device, dtype=dy.dtype).permute(0, 3, 1, 2)
-    gemm(dys, wt, dx, M=n * h * wd, N=ci, K=9 * co, lda=co, ldb=9 * co, ldc=ci, conv=(h, wd, co))
+    if bn_bwd is not None:
+        assert stats is not None and bn_bwd[0].shape == (n * h * wd, ci) and ENGINE != 1
+    gemm(dys, wt, dx, M=n * h * wd, N=ci, K=9 * co, lda=co, ldb=9 * co, ldc=ci, conv=(h, wd, co),
+         mode=1 if bn_bwd is not None else 0, stats=stats, bn_bwd=bn_bwd)
     return dx
 
 

@@ -191,3 +191,35 @@ def test_hybrid_resnet_weight_gradient_kernels(gpu_ext, wgrad, monkeypatch):
     for (n, pa), pb, pc in zip(ref.named_parameters(), fus.parameters(), f32.parameters()):
         ea, eb = _rel(pa.grad, pc.grad), _rel(pb.grad, pc.grad)
         assert eb < 2 * ea + 2e-2, f"{n}: {wgrad} {eb:.3e} vs unfused {ea:.3e}"
+
+
+@pytest.mark.parametrize("with_res", [False, True])
+def test_bn_stats_link_conv3x3(gpu_ext, with_res):
+    """BN -> 3x3 conv (implicit GEMM): the conv's dgrad epilogue reduces the BN backward
+    statistics and the BN skips its reduce pass — gradients equal the unlinked chain's."""
+    from fluxmpi_amd.ops import fused_block as fb
+    from fluxmpi_amd.ops.batchnorm import FusedBatchNorm2d
+    torch.manual_seed(7)
+    c = torch.randn(4, 64, 14, 14, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    r = torch.randn_like(c) if with_res else None
+    w = (torch.randn(64, 64, 3, 3, device="cuda") * 0.05).bfloat16().contiguous(memory_format=torch.channels_last)
+    bn_w, bn_b = torch.rand(64, device="cuda") + 0.5, torch.rand(64, device="cuda") * 0.4 - 0.2
+    grads = []
+    for use_link in (False, True):
+        bn = FusedBatchNorm2d(64).cuda()
+        with torch.no_grad():
+            bn.weight.copy_(bn_w)
+            bn.bias.copy_(bn_b)
+        ci, wi = c.clone().requires_grad_(), w.clone().requires_grad_()
+        ri = r.clone().requires_grad_() if with_res else None
+        link = fb.BNStatsLink() if use_link else None
+        y = bn(ci, relu=True, residual=ri, bnlink=link)
+        z = fb.conv3x3(y, wi, bnlink=link)
+        if fb.conv3x3_forward_is_ours(y, wi):
+            torch.cuda.synchronize()
+        (z.float() * torch.linspace(-1, 1, z.numel(), device="cuda").view_as(z)).sum().backward()
+        if use_link:
+            assert not link.bound  # consumed and released by the BN backward
+        grads.append([ci.grad, wi.grad, bn.weight.grad, bn.bias.grad] + ([ri.grad] if with_res else []))
+    for a, b in zip(*grads):
+        assert _rel(b, a) < 2e-3, (_rel(b, a))
