@@ -557,7 +557,9 @@ void launch(const GemmArgs& a0, int splits, hipStream_t s) {
 
 void gemm_bf16(const GemmProblem& g, hipStream_t stream) {
   // engine 0 (auto): the LDS-DMA pipelined kernel for every problem it covers
-  if (g.engine >= 2 || (g.engine == 0 && gemm_glds_supported(g))) {
+  // (not for a prologue affine: its per-fragment transform costs the LDS-DMA kernel 1.3-2.3x —
+  // measured — while register staging applies it on the way to LDS; engine 2 forces it)
+  if (g.engine >= 2 || (g.engine == 0 && g.a_scale == nullptr && gemm_glds_supported(g))) {
     gemm_glds(g, stream);
     return;
   }

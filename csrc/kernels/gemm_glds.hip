@@ -38,6 +38,14 @@ constexpr int kThreads = 256;
 constexpr int kShards = 64;  // must match batchnorm.hip
 
 __device__ __attribute__((aligned(16))) uint4 g_zero_line[4];  // source of zero-filled chunks
+// Out-of-image / out-of-range chunks of an operand that gets the BatchNorm+ReLU prologue: a
+// bf16 NaN payload (0x7FC1) the fragment transform maps to 0 (the padding of the ACTIVATED
+// tensor), which relu(0 * scale + shift) would not be.
+constexpr unsigned short kPadBits = 0x7FC1;
+__device__ __attribute__((aligned(16))) uint4 g_pad_line[4] = {
+    {0x7FC17FC1u, 0x7FC17FC1u, 0x7FC17FC1u, 0x7FC17FC1u}, {0x7FC17FC1u, 0x7FC17FC1u, 0x7FC17FC1u, 0x7FC17FC1u},
+    {0x7FC17FC1u, 0x7FC17FC1u, 0x7FC17FC1u, 0x7FC17FC1u}, {0x7FC17FC1u, 0x7FC17FC1u, 0x7FC17FC1u, 0x7FC17FC1u}};
+constexpr int kMaxAffC = 512;  // channels of a prologue affine (scale/shift staged in LDS)
 
 struct GldsArgs {
   const bf16* a;
@@ -57,6 +65,9 @@ struct GldsArgs {
   const float* bnb_inv;
   const uint8_t* bnb_mask;
   int bnb_rm;
+  const float* a_scale;  // AFF: A element (m, k) -> relu(A * a_scale[c] + a_shift[c]), c = channel of k
+  const float* a_shift;
+  int aff_c;             // channels of the affine (C for the implicit conv, K for a 1x1)
 };
 
 // s_waitcnt vmcnt(N) with expcnt / lgkmcnt left alone (gfx9 encoding)
@@ -84,7 +95,7 @@ __device__ __forceinline__ int swz(int row) {
 // A 1 KiB piece holds RPP = 512/BK rows; piece j of wave w covers tile rows
 // (w * PPW + j) * RPP ..; lane l fills row +(l / CPR), slot (l % CPR) with global chunk
 // slot ^ swz(row).
-template <int ROWS, int BK, bool CONV>
+template <int ROWS, int BK, bool CONV, bool PAD = false>
 __device__ __forceinline__ void issue_tile(bf16* lds_tile, const bf16* __restrict__ g, int64_t ld,
                                            int64_t rows, int64_t r0, int64_t k0, int64_t kend,
                                            const int* ph, const int* pw, int H, int W, int C) {
@@ -104,7 +115,7 @@ __device__ __forceinline__ void issue_tile(bf16* lds_tile, const bf16* __restric
     const int row = piece * RPP + lane / CPR;
     const int q = (lane % CPR) ^ swz<BK>(row);
     const int64_t grow = r0 + row;
-    const void* src = g_zero_line;
+    const void* src = PAD ? static_cast<const void*>(g_pad_line) : static_cast<const void*>(g_zero_line);
     if (CONV) {
       if (grow < rows && static_cast<unsigned>(ph[j] + dr) < static_cast<unsigned>(H) &&
           static_cast<unsigned>(pw[j] + ds) < static_cast<unsigned>(W))
@@ -128,13 +139,40 @@ __device__ __forceinline__ bf16x8 read_frag(const bf16* __restrict__ tile, int r
   return *reinterpret_cast<const bf16x8*>(tile + row * BK + q * 8);
 }
 
-template <int BM, int BN, int kBK, int kStages, bool CONV, bool RES>
+// relu(x * s + t) of the 8 channels of a fragment, bit-identical to the fused BN kernels'
+// fmaf; padding chunks (kPadBits) become 0
+__device__ __forceinline__ bf16x8 affine_frag(bf16x8 f, const float* __restrict__ st) {
+  const float4 q0 = *reinterpret_cast<const float4*>(st);       // s0 t0 s1 t1
+  const float4 q1 = *reinterpret_cast<const float4*>(st + 4);   // s2 t2 s3 t3
+  const float4 q2 = *reinterpret_cast<const float4*>(st + 8);
+  const float4 q3 = *reinterpret_cast<const float4*>(st + 12);
+  const float s[8] = {q0.x, q0.z, q1.x, q1.z, q2.x, q2.z, q3.x, q3.z};
+  const float t[8] = {q0.y, q0.w, q1.y, q1.w, q2.y, q2.w, q3.y, q3.w};
+  unsigned short u[8];
+  __builtin_memcpy(u, &f, 16);
+  bf16 e[8];
+  __builtin_memcpy(e, &f, 16);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float o = fmaf(static_cast<float>(e[j]), s[j], t[j]);
+    e[j] = u[j] == kPadBits ? static_cast<bf16>(0.f) : static_cast<bf16>(o > 0.f ? o : 0.f);
+  }
+  bf16x8 out;
+  __builtin_memcpy(&out, e, 16);
+  return out;
+}
+
+// BNB: the BN-backward epilogue is compiled in (its registers would otherwise cost the lean
+// variants occupancy: the allocation covers the epilogue's peak too)
+template <int BM, int BN, int kBK, int kStages, bool CONV, bool RES, bool AFF = false, bool BNB = false>
 __global__ __launch_bounds__(kThreads, 2) void gemm_glds_kernel(GldsArgs p) {
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
   constexpr int A_ELEMS = BM * kBK, B_ELEMS = BN * kBK;
   constexpr int kRing = kStages * (A_ELEMS + B_ELEMS);
   constexpr int CS = BN + 8;  // epilogue C staging row (bf16)
-  constexpr int kSmem = kRing > BM * CS ? kRing : BM * CS;
+  constexpr int kRingOrC = kRing > BM * CS ? kRing : BM * CS;
+  // AFF: interleaved (scale, shift) fp32 pairs of the A channels after the ring
+  constexpr int kSmem = kRingOrC + (AFF ? kMaxAffC * 4 : 0);
   constexpr int LPT = (BM + BN) * kBK / 2048;  // LDS-DMA instructions per wave per K-tile
   // ONE __shared__ array for the ring, the epilogue staging and the statistics scratch
   __shared__ __attribute__((aligned(16))) bf16 smem[kSmem];
@@ -166,9 +204,17 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_glds_kernel(GldsArgs p) {
     }
   }
   auto issue = [&](int s, int64_t k0) {
-    issue_tile<BM, kBK, CONV>(sa(s), p.a, p.lda, p.M, m0, k0, p.K, ph, pw, p.conv_h, p.conv_w, p.conv_c);
+    issue_tile<BM, kBK, CONV, AFF>(sa(s), p.a, p.lda, p.M, m0, k0, p.K, ph, pw, p.conv_h, p.conv_w, p.conv_c);
     issue_tile<BN, kBK, false>(sb(s), p.b, p.ldb, p.N, n0, k0, p.K, nullptr, nullptr, 0, 0, 0);
   };
+  float* st_lds = reinterpret_cast<float*>(smem + kRingOrC);
+  if (AFF) {  // stage the affine pairs once (read back with ds_read_b128 per fragment)
+    for (int c = threadIdx.x; c < p.aff_c; c += kThreads) {
+      st_lds[2 * c] = p.a_scale[c];
+      st_lds[2 * c + 1] = p.a_shift[c];
+    }
+    __syncthreads();
+  }
 
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -187,6 +233,9 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_glds_kernel(GldsArgs p) {
     if (t + kStages - 1 < nk) issue((t + kStages - 1) % kStages, static_cast<int64_t>(t + kStages - 1) * kBK);
     const bf16* ta = sa(t % kStages);
     const bf16* tb = sb(t % kStages);
+    // AFF: channel of this lane's fragment chunk = (k0 - tap * C) + 8 * ((lane >> 4) + 4 * kh)
+    const int c_base = AFF ? static_cast<int>(CONV ? (static_cast<int64_t>(t) * kBK) % p.conv_c
+                                                   : static_cast<int64_t>(t) * kBK) + 8 * (lane >> 4) : 0;
 #pragma unroll
     for (int kh = 0; kh < kBK / 32; ++kh) {
       bf16x8 fa[FM], fb[FN];
@@ -194,6 +243,12 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_glds_kernel(GldsArgs p) {
       for (int i = 0; i < FM; ++i) fa[i] = read_frag<kBK>(ta, wm * WM + i * 16, kh);
 #pragma unroll
       for (int j = 0; j < FN; ++j) fb[j] = read_frag<kBK>(tb, wn * WN + j * 16, kh);
+      if (AFF) {
+        const int c = c_base + 32 * kh;
+        const float* st = st_lds + 2 * (c < p.aff_c ? c : 0);  // K tail: padding chunks anyway
+#pragma unroll
+        for (int i = 0; i < FM; ++i) fa[i] = affine_frag(fa[i], st);
+      }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -225,9 +280,9 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_glds_kernel(GldsArgs p) {
   // bnb_x; accumulate sum(dy_eff) and sum(dy_eff * xhat) per column instead of sum / sumsq of C.
   // dy_eff = C masked by the BN's ReLU: rm 2 recomputes it bit-identically to the forward
   // (fma(x, w*invstd, b - mean*w*invstd) > 0), rm 3 reads the 1-bit mask.
-  const bool bnb = p.bnb_x != nullptr;
-  float bmu[8], biv[8], bsc[8], bsh[8];
-  if (bnb) {
+  const bool bnb = BNB && p.bnb_x != nullptr;
+  float bmu[BNB ? 8 : 1], biv[BNB ? 8 : 1], bsc[BNB ? 8 : 1], bsh[BNB ? 8 : 1];
+  if (BNB && bnb) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int64_t c = ncol_ok ? n + e : 0;
@@ -241,17 +296,20 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_glds_kernel(GldsArgs p) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) cs[e] = cq[e] = 0.f;
   for (int rb = r0; rb < BM; rb += UB * RPI) {
-    uint4 rv[UB], xv[UB];
-    unsigned mk[UB];
+    uint4 rv[RES ? UB : 1], xv[BNB ? UB : 1];
+    unsigned mk[BNB ? UB : 1];
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
       const int r = rb + u * RPI;
       const int64_t m = m0 + r;
       const bool ok = r < BM && r < rows_valid && ncol_ok;
-      rv[u] = xv[u] = make_uint4(0, 0, 0, 0);
-      mk[u] = 0xFFu;
+      if (RES) rv[u] = make_uint4(0, 0, 0, 0);
+      if (BNB) {
+        xv[u] = make_uint4(0, 0, 0, 0);
+        mk[u] = 0xFFu;
+      }
       if (RES && ok) rv[u] = *reinterpret_cast<const uint4*>(p.res + m * p.ldr + n);
-      if (bnb && ok) {
+      if (BNB && bnb && ok) {
         xv[u] = *reinterpret_cast<const uint4*>(p.bnb_x + m * p.N + n);
         if (p.bnb_rm == 3) mk[u] = p.bnb_mask[(m * p.N + n) >> 3];
       }
@@ -272,7 +330,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_glds_kernel(GldsArgs p) {
         __builtin_memcpy(&v, e8, 16);
       }
       *reinterpret_cast<uint4*>(p.c + m * p.ldc + n) = v;
-      if (bnb) {
+      if (BNB && bnb) {
         bf16 x8[8];
         __builtin_memcpy(x8, &xv[u], 16);
 #pragma unroll
@@ -328,11 +386,11 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_glds_kernel(GldsArgs p) {
   }
 }
 
-template <int BM, int BN, int BK, int ST, bool CONV, bool RES>
+template <int BM, int BN, int BK, int ST, bool CONV, bool RES, bool AFF = false, bool BNB = false>
 void launch_glds(GldsArgs a, hipStream_t s) {
   a.tiles_m = static_cast<int>((a.M + BM - 1) / BM);
   a.tiles_n = static_cast<int>((a.N + BN - 1) / BN);
-  gemm_glds_kernel<BM, BN, BK, ST, CONV, RES><<<a.tiles_m * a.tiles_n, kThreads, 0, s>>>(a);
+  gemm_glds_kernel<BM, BN, BK, ST, CONV, RES, AFF, BNB><<<a.tiles_m * a.tiles_n, kThreads, 0, s>>>(a);
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
 
@@ -588,7 +646,9 @@ __global__ __launch_bounds__(kThreads) void xpose_taps_kernel(XposeArgs a) {
 }  // namespace
 
 bool gemm_glds_supported(const GemmProblem& g) {
-  return g.a_kmajor && g.b_kmajor && g.mode <= 1 && (g.splits <= 1) && g.a_scale == nullptr &&
+  const int64_t aff_c = g.conv_h > 0 ? g.conv_c : g.K;
+  return g.a_kmajor && g.b_kmajor && g.mode <= 1 && (g.splits <= 1) &&
+         (g.a_scale == nullptr || (aff_c <= kMaxAffC && g.res == nullptr && g.bnb_x == nullptr)) &&
          g.b_scale == nullptr && g.K % 8 == 0 && g.N % 8 == 0 && g.lda % 8 == 0 && g.ldb % 8 == 0 &&
          g.ldc % 8 == 0 && (g.res == nullptr || g.ldr % 8 == 0) &&
          (g.bnb_x == nullptr || (g.mode == 1 && g.ldc == g.N && g.bnb_mean != nullptr && g.bnb_inv != nullptr &&
@@ -611,6 +671,10 @@ void gemm_glds(const GemmProblem& g, hipStream_t stream) {
   a.bnb_x = static_cast<const bf16*>(g.bnb_x);
   a.bnb_w = g.bnb_w; a.bnb_b = g.bnb_b; a.bnb_mean = g.bnb_mean; a.bnb_inv = g.bnb_inv;
   a.bnb_mask = g.bnb_mask; a.bnb_rm = g.bnb_rm;
+  a.a_scale = g.a_scale; a.a_shift = g.a_shift;
+  a.aff_c = static_cast<int>(g.conv_h > 0 ? g.conv_c : g.K);
+  const bool aff = g.a_scale != nullptr;
+  const bool bnb = g.bnb_x != nullptr;
   const bool conv = g.conv_h > 0, res = g.res != nullptr;
   // variant: 1 BK32/3 stages; 2 BK32/4; 3 BK64/2; 4 BK64/3 (engine 3..6 force one, for experiments).
   // Auto (measured on MI355X, ResNet-50 1x1 and 3x3 shapes): a 64-deep K-step in a 2-stage ring
@@ -627,7 +691,11 @@ void gemm_glds(const GemmProblem& g, hipStream_t stream) {
   const bool bn128 = g.N > 64 && g.tile_n != 64;
 #define GV(BM, BN, BK, ST)                                                                                \
   {                                                                                                      \
-    if (conv) { if (res) launch_glds<BM, BN, BK, ST, true, true>(a, stream); else launch_glds<BM, BN, BK, ST, true, false>(a, stream); } \
+    if (aff) { if (conv) launch_glds<BM, BN, BK, ST, true, false, true>(a, stream); else launch_glds<BM, BN, BK, ST, false, false, true>(a, stream); } \
+    else if (bnb) { if (conv) launch_glds<BM, BN, BK, ST, true, false, false, true>(a, stream);                    \
+                    else if (res) launch_glds<BM, BN, BK, ST, false, true, false, true>(a, stream);                \
+                    else launch_glds<BM, BN, BK, ST, false, false, false, true>(a, stream); }                      \
+    else if (conv) { if (res) launch_glds<BM, BN, BK, ST, true, true>(a, stream); else launch_glds<BM, BN, BK, ST, true, false>(a, stream); } \
     else { if (res) launch_glds<BM, BN, BK, ST, false, true>(a, stream); else launch_glds<BM, BN, BK, ST, false, false>(a, stream); }    \
   }
 #define GL(BM, BN)                          \

@@ -45,6 +45,8 @@ def main():
             rec[f"e{eng}_dgrad"] = bench(lambda: conv3x3_dgrad(dy, w, out=y))
         G.ENGINE = 2
         rec["ours_fwd"] = rec["e2_fwd"]
+        sc, sh = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.1
+        rec["ours_fwd_affine"] = bench(lambda: conv3x3_fwd(x, w, in_affine=(sc, sh), out=y))
         rec["miopen_fwd"] = bench(lambda: F.conv2d(x, w, padding=1))
         rec["ours_dgrad"] = rec["e2_dgrad"]
         rec["miopen_dgrad"] = bench(lambda: torch.ops.aten.convolution_backward(
@@ -61,6 +63,18 @@ def main():
                 tot[k] = round(tot.get(k, 0.0) + v, 1)
         print(json.dumps(rec), flush=True)
     print(json.dumps({"total_us": tot}))
+    # 1x1 forward with / without the BN+ReLU prologue (conv3 of each stage: width -> 4 width)
+    for H, ci in [(56, 64), (28, 128), (14, 256), (7, 512)]:
+        x2 = torch.randn(B * H * H, ci, device="cuda").bfloat16()
+        w2 = torch.randn(4 * ci, ci, device="cuda").bfloat16()
+        y2 = torch.empty(B * H * H, 4 * ci, device="cuda", dtype=torch.bfloat16)
+        sc, sh = torch.rand(ci, device="cuda") + 0.5, torch.randn(ci, device="cuda") * 0.1
+        M = B * H * H
+        rec = {"H": H, "Cin": ci, "Cout": 4 * ci,
+               "fwd1": bench(lambda: G.gemm(x2, w2, y2, M=M, N=4 * ci, K=ci, lda=ci, ldb=ci, ldc=4 * ci)),
+               "fwd1_affine": bench(lambda: G.gemm(x2, w2, y2, M=M, N=4 * ci, K=ci, lda=ci, ldb=ci, ldc=4 * ci,
+                                                  a_affine=(sc, sh)))}
+        print(json.dumps(rec), flush=True)
     # 1x1 weight gradients (ResNet-50 bottleneck shapes)
     tot1 = {}
     for H, ci, co in [(56, 64, 64), (56, 64, 256), (56, 256, 64), (28, 128, 512), (28, 512, 128), (14, 256, 1024),

@@ -29,8 +29,8 @@ def _rel(a, b):
 @pytest.mark.parametrize("use_aff", [False, True])
 def test_conv3x3_fwd(gpu_ext, N, C, H, W, Co, use_aff, engine):
     from fluxmpi_amd.ops.gemm import SHARDS, conv3x3_fwd
-    if use_aff and engine >= 2:
-        pytest.skip("the LDS-DMA kernel has no prologue affine (register staging applies it)")
+    if use_aff and engine in (3, 5, 6):
+        pytest.skip("forced variants: the prologue affine is covered by engines 1 and 2")
     torch.manual_seed(0)
     x = _nhwc(torch.randn(N, C, H, W, device="cuda").bfloat16())
     w = _nhwc((torch.randn(Co, C, 3, 3, device="cuda") * 0.1).bfloat16())
