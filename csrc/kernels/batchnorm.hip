@@ -18,6 +18,7 @@
 // needs no memset per call); the consumer kernels derive their per-channel
 // coefficients from those statistics (registers, or LDS when C/8 does not divide
 // the workgroup). Grids are one full round of resident workgroups (occupancy x CUs).
+#include <initializer_list>
 #include <stdexcept>
 #include <string>
 
@@ -49,6 +50,16 @@ __device__ __forceinline__ void st8f(T* __restrict__ p, const float (&f)[8]) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) t[j] = static_cast<T>(f[j]);
   store8(p, t);
+}
+
+// 8 consecutive per-channel floats (c0 % 8 == 0, 16-B aligned array) with two 16-B loads:
+// the lanes of a wave read consecutive 32-B pieces, where 8 scalar loads per lane would each
+// touch a different cache line (a kernel-wide prologue that alone cost ~25 us per launch)
+__device__ __forceinline__ void ld8ch(const float* __restrict__ p, int c0, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p + c0);
+  const float4 b = *reinterpret_cast<const float4*>(p + c0 + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
 struct Geo {
@@ -247,8 +258,17 @@ __global__ __launch_bounds__(kThreads) void bn_norm_kernel(const T* __restrict__
   float rsc[8], rsh[8];
   if (FIXED) {
     const int c0 = (threadIdx.x % (C / 8)) * 8;
+    float mu[8], s2[8], ww[8], bb[8];
+    ld8ch(mean_in, c0, mu);
+    ld8ch(stat2, c0, s2);
+    if (w) ld8ch(w, c0, ww);
+    if (b) ld8ch(b, c0, bb);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) coef(c0 + j, rsc[j], rsh[j]);
+    for (int j = 0; j < 8; ++j) {
+      const float invstd = train ? s2[j] : rsqrtf(s2[j] + eps);  // save_invstd | running_var
+      rsc[j] = (w ? ww[j] : 1.f) * invstd;
+      rsh[j] = fmaf(-mu[j], rsc[j], b ? bb[j] : 0.f);
+    }
   } else {
     for (int c = threadIdx.x; c < C; c += kThreads) coef(c, smem[c], smem[C + c]);
     __syncthreads();
@@ -308,14 +328,15 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const T* __rest
   const int r0 = t / g.cv, c8 = t % g.cv;
   float s[8] = {0}, q[8] = {0};
   if (r0 < g.rpi) {
-    float mu[8], is[8], sc[8], sh[8];
+    float mu[8], is[8], sc[8], sh[8], ww[8], bb[8];
+    ld8ch(smean, c8 * 8, mu);
+    ld8ch(sinv, c8 * 8, is);
+    if (w) ld8ch(w, c8 * 8, ww);
+    if (b) ld8ch(b, c8 * 8, bb);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = c8 * 8 + j;
-      mu[j] = smean[c];
-      is[j] = sinv[c];
-      sc[j] = (w ? w[c] : 1.f) * is[j];
-      sh[j] = fmaf(-mu[j], sc[j], b ? b[c] : 0.f);
+      sc[j] = (w ? ww[j] : 1.f) * is[j];
+      sh[j] = fmaf(-mu[j], sc[j], b ? bb[j] : 0.f);
     }
     const int64_t start = static_cast<int64_t>(blockIdx.x) * g.rows_per_block;
     int64_t end = start + g.rows_per_block;
@@ -421,8 +442,22 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const T* __restrict
   DxCoef rk[8];
   if (FIXED) {
     const int c0 = (threadIdx.x % (C / 8)) * 8;
+    float iv[8], m[8], ww[8], bb[8], kdb[8], kdw[8];
+    ld8ch(sinv, c0, iv);
+    ld8ch(smean, c0, m);
+    ld8ch(db, c0, kdb);
+    ld8ch(dw, c0, kdw);
+    if (w) ld8ch(w, c0, ww);
+    if (bias) ld8ch(bias, c0, bb);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) rk[j] = dx_coef(c0 + j, w, bias, smean, sinv, dw, db, inv_n);
+    for (int j = 0; j < 8; ++j) {  // == dx_coef, from vector loads
+      const float sc = (w ? ww[j] : 1.f) * iv[j];
+      const float k2 = kdb[j] * inv_n, k3 = kdw[j] * inv_n;
+      rk[j].a = sc;
+      rk[j].b = -sc * iv[j] * k3;
+      rk[j].d = sc * (m[j] * iv[j] * k3 - k2);
+      rk[j].sh = fmaf(-m[j], sc, bias ? bb[j] : 0.f);
+    }
   } else {
     for (int c = threadIdx.x; c < C; c += kThreads) ksm[c] = dx_coef(c, w, bias, smean, sinv, dw, db, inv_n);
     __syncthreads();
@@ -464,7 +499,8 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const T* __restrict
 
 // one full round of resident workgroups (or fewer if the tensor is small)
 int elementwise_grid(const void* kernel, size_t smem, int64_t nvec) {
-  int64_t b = (nvec + kThreads - 1) / kThreads;
+  // >= 4 vectors per lane: every workgroup pays its coefficient prologue once
+  int64_t b = (nvec + 4 * kThreads - 1) / (4 * kThreads);
   const int64_t cap = resident_blocks(kernel, kThreads, smem);
   if (b > cap) b = cap;
   if (b < 1) b = 1;
@@ -476,6 +512,13 @@ bool fixed_channels(int64_t C) { return kThreads % (C / 8) == 0; }
 void check(int64_t C) {
   if (C % 8 != 0 || C > kMaxC || C < 8)
     throw std::runtime_error("fused batchnorm: need C % 8 == 0 and 8 <= C <= 2048 (got " + std::to_string(C) + ")");
+}
+
+// the per-channel arrays are read 8 channels at a time with 16-B loads
+void check_aligned(std::initializer_list<const void*> ptrs) {
+  for (const void* p : ptrs)
+    if (p != nullptr && (reinterpret_cast<uintptr_t>(p) & 15u) != 0)
+      throw std::runtime_error("fused batchnorm: per-channel parameter / statistics arrays must be 16-B aligned");
 }
 
 size_t reduce_smem(const Geo& g, int64_t C) { return static_cast<size_t>(2 * g.rpi * C) * sizeof(float); }
@@ -595,6 +638,7 @@ void bn_fwd_train(const void* x, void* y, const void* residual, const float* wei
                   int64_t rows, int64_t C, float momentum, float eps, int relu, uint8_t* relu_mask, int dtype,
                   hipStream_t stream, int64_t* nbt) {
   check(C);
+  check_aligned({weight, bias, save_mean, save_invstd});
   switch (dtype) {
     case kBF16: fwd_train_t<bf16>(x, y, residual, weight, bias, running_mean, running_var, save_mean, save_invstd,
                                   workspace, rows, C, momentum, eps, relu, relu_mask, nbt, stream); break;
@@ -633,6 +677,7 @@ void bn_stats_finalize(const void* x, const float* w, const float* b, float* rm,
 void bn_apply(const void* x, void* y, const void* res, const float* w, const float* b, const float* sm,
               const float* si, int64_t rows, int64_t C, int relu, uint8_t* mask, int dtype, hipStream_t s) {
   check(C);
+  check_aligned({w, b, sm, si});
   switch (dtype) {
     case kBF16: norm_t<bf16>(x, y, res, w, b, sm, si, rows, C, 0.f, 1, relu, mask, s); break;
     case kF16: norm_t<f16>(x, y, res, w, b, sm, si, rows, C, 0.f, 1, relu, mask, s); break;
@@ -645,6 +690,7 @@ void bn_fwd_infer(const void* x, void* y, const void* residual, const float* wei
                   const float* running_mean, const float* running_var, int64_t rows, int64_t C, float eps, int relu,
                   int dtype, hipStream_t stream) {
   check(C);
+  check_aligned({weight, bias, running_mean, running_var});
   switch (dtype) {
     case kBF16: norm_t<bf16>(x, y, residual, weight, bias, running_mean, running_var, rows, C, eps, 0, relu, nullptr, stream); break;
     case kF16: norm_t<f16>(x, y, residual, weight, bias, running_mean, running_var, rows, C, eps, 0, relu, nullptr, stream); break;
@@ -658,6 +704,7 @@ void bn_bwd(const void* dy, const void* x, const void* y, const uint8_t* relu_ma
             const float* save_invstd, void* dx, void* dres, float* dweight, float* dbias, float* workspace,
             int64_t rows, int64_t C, int relu, int dtype, hipStream_t stream, int stats_ready) {
   check(C);
+  check_aligned({weight, bias, save_mean, save_invstd, dweight, dbias});
   switch (dtype) {
     case kBF16: bwd_t<bf16>(dy, x, y, relu_mask, weight, bias, save_mean, save_invstd, dx, dres, dweight, dbias, workspace, rows, C,
                             relu, stats_ready, stream); break;
