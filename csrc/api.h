@@ -144,6 +144,9 @@ struct GemmProblem {
   // [M/(H*W)][H][W][conv_c] (K = 9*conv_c, K-major B = [N][3][3][conv_c] filter)
   int conv_h = 0, conv_w = 0, conv_c = 0;
   int engine = 0;  // 0 auto, 1 register-staged kernel (gemm.hip), 2 LDS-DMA pipelined kernel (gemm_glds.hip)
+  // LDS-DMA kernel: residual element (m, n) counts only if bit n%8 of res_mask[(m*N + n)/8] is set
+  // (the 1-bit ReLU mask of the BatchNorm whose output gradient the residual is)
+  const uint8_t* res_mask = nullptr;
 };
 void gemm_bf16(const GemmProblem& g, hipStream_t stream);
 // the LDS-DMA pipelined kernel: K-major A (or implicit conv) and B, modes 0/1, optional residual,

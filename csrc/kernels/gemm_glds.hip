@@ -65,6 +65,7 @@ struct GldsArgs {
   const float* bnb_inv;
   const uint8_t* bnb_mask;
   int bnb_rm;
+  const uint8_t* res_mask;  // RES: 1-bit mask of the residual ([M][N] bits, n fastest), or nullptr
   const float* a_scale;  // AFF: A element (m, k) -> relu(A * a_scale[c] + a_shift[c]), c = channel of k
   const float* a_shift;
   int aff_c;             // channels of the affine (C for the implicit conv, K for a 1x1)
@@ -297,18 +298,24 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_glds_kernel(GldsArgs p) {
   for (int e = 0; e < 8; ++e) cs[e] = cq[e] = 0.f;
   for (int rb = r0; rb < BM; rb += UB * RPI) {
     uint4 rv[RES ? UB : 1], xv[BNB ? UB : 1];
-    unsigned mk[BNB ? UB : 1];
+    unsigned mk[BNB ? UB : 1], rmk[RES ? UB : 1];
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
       const int r = rb + u * RPI;
       const int64_t m = m0 + r;
       const bool ok = r < BM && r < rows_valid && ncol_ok;
-      if (RES) rv[u] = make_uint4(0, 0, 0, 0);
+      if (RES) {
+        rv[u] = make_uint4(0, 0, 0, 0);
+        rmk[u] = 0xFFu;
+      }
       if (BNB) {
         xv[u] = make_uint4(0, 0, 0, 0);
         mk[u] = 0xFFu;
       }
-      if (RES && ok) rv[u] = *reinterpret_cast<const uint4*>(p.res + m * p.ldr + n);
+      if (RES && ok) {
+        rv[u] = *reinterpret_cast<const uint4*>(p.res + m * p.ldr + n);
+        if (p.res_mask != nullptr) rmk[u] = p.res_mask[(m * p.N + n) >> 3];
+      }
       if (BNB && bnb && ok) {
         xv[u] = *reinterpret_cast<const uint4*>(p.bnb_x + m * p.N + n);
         if (p.bnb_rm == 3) mk[u] = p.bnb_mask[(m * p.N + n) >> 3];
@@ -326,7 +333,10 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_glds_kernel(GldsArgs p) {
         bf16 r8[8];
         __builtin_memcpy(r8, &rv[u], 16);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) e8[e] = static_cast<bf16>(static_cast<float>(e8[e]) + static_cast<float>(r8[e]));
+        for (int e = 0; e < 8; ++e) {
+          const float rf = (rmk[u] >> e) & 1u ? static_cast<float>(r8[e]) : 0.f;
+          e8[e] = static_cast<bf16>(static_cast<float>(e8[e]) + rf);
+        }
         __builtin_memcpy(&v, e8, 16);
       }
       *reinterpret_cast<uint4*>(p.c + m * p.ldc + n) = v;
@@ -672,6 +682,7 @@ void gemm_glds(const GemmProblem& g, hipStream_t stream) {
   a.bnb_w = g.bnb_w; a.bnb_b = g.bnb_b; a.bnb_mean = g.bnb_mean; a.bnb_inv = g.bnb_inv;
   a.bnb_mask = g.bnb_mask; a.bnb_rm = g.bnb_rm;
   a.a_scale = g.a_scale; a.a_shift = g.a_shift;
+  a.res_mask = g.res_mask;
   a.aff_c = static_cast<int>(g.conv_h > 0 ? g.conv_c : g.K);
   const bool aff = g.a_scale != nullptr;
   const bool bnb = g.bnb_x != nullptr;

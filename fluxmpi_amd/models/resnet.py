@@ -99,7 +99,8 @@ class Bottleneck(nn.Module):
                 # downsample blocks: the downsample conv's input gradient goes into that epilogue.
                 fused_ds = self.downsample is not None and self._fused_downsample()
                 if self.downsample is None:
-                    link = fb.GradLink() if needs else None
+                    # masked: bn3 hands over (dy, relu mask); conv1's dgrad epilogue applies the mask
+                    link = fb.GradLink(masked=fb.masked_links_ok()) if needs else None
                 else:
                     link = fb.SideGradLink() if (needs and fused_ds) else None
                 prev = getattr(x, "_fluxmpi_bnlink", None) if (link is not None and self.downsample is None) else None

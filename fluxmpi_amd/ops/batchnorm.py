@@ -91,12 +91,16 @@ class GradLink:
     backward needs gradients that pass through the BatchNorm's backward).
     """
 
-    __slots__ = ("grad",)
+    __slots__ = ("grad", "masked")
 
-    def __init__(self):
+    def __init__(self, masked: bool = False):
         self.grad = None
+        # masked: the consumer can take (dy, relu_mask) and apply the mask itself (the LDS-DMA
+        # dgrad epilogue does), so the BatchNorm backward never writes dres = dy * mask
+        self.masked = masked
 
-    def take(self) -> torch.Tensor:
+    def take(self):
+        """The residual gradient: a tensor, or ``(dy, mask)`` (1 bit per element) when masked."""
         g, self.grad = self.grad, None
         if g is None:
             raise RuntimeError("GradLink: the residual gradient was not produced before its consumer ran")
@@ -230,7 +234,9 @@ class _FusedBN(torch.autograd.Function):
         stats_ready = ctx.bnlink is not None and ctx.bnlink.ready
         rows, ch = _rows_c(x)
         dx = torch.empty_like(x)
-        dres = torch.empty_like(x) if ctx.has_res else None
+        # a masked GradLink takes (dy, mask) instead of dres = dy * mask: one write pass less
+        hand_masked = ctx.link is not None and ctx.link.masked and mask is not None and ctx.relu
+        dres = torch.empty_like(x) if (ctx.has_res and not hand_masked) else None
         # the finalize kernel always produces both reductions (they feed dx)
         dw = torch.empty(ch, device=x.device, dtype=torch.float32)
         db = torch.empty(ch, device=x.device, dtype=torch.float32)
@@ -252,7 +258,7 @@ class _FusedBN(torch.autograd.Function):
         elif ctx.wdtype != torch.float32:
             db = db.to(ctx.wdtype)
         if ctx.link is not None:
-            ctx.link.grad, dres = dres, None
+            ctx.link.grad, dres = ((dy, mask) if hand_masked else dres), None
         return dx, dw, db, dres, None, None, None, None, None, None, None, None
 
 

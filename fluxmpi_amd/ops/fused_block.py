@@ -124,16 +124,20 @@ def _dgrad_nhwc(dc2, weight, x, link, bnlink=None):
     co, ci = weight.shape[0], weight.shape[1]
     n, _, h, w = x.shape
     dx = _empty_nhwc(n, ci, h, w, x)
-    res = None
+    res = res_mask = None
     if link is not None:
         g = link.take()  # SideGradLink: None if its producer has not run (it then returns its own)
-        res = _nhwc2d(g) if g is not None else None
+        if isinstance(g, tuple):  # masked GradLink: (dy, 1-bit ReLU mask), masked in the epilogue
+            res, res_mask = _nhwc2d(g[0]), g[1]
+        elif g is not None:
+            res = _nhwc2d(g)
     bn = stats = None
     if bnlink is not None and bnlink.bound and bnlink.x.shape == x.shape and \
             bnlink.x.is_contiguous(memory_format=torch.channels_last):
         bn = (_nhwc2d(bnlink.x), bnlink.w32, bnlink.b32, bnlink.mean, bnlink.inv, bnlink.mask, bnlink.relu_mode)
         stats = _link_workspace(dx)
-    conv1x1_dgrad(dc2, weight.reshape(co, ci), residual=res, out=_nhwc2d(dx), bn_bwd=bn, stats=stats, w4d=weight)
+    conv1x1_dgrad(dc2, weight.reshape(co, ci), residual=res, out=_nhwc2d(dx), bn_bwd=bn, stats=stats, w4d=weight,
+                  residual_mask=res_mask)
     if bn is not None:
         bnlink.ready = True
     return dx
@@ -255,11 +259,14 @@ class _BNFromStats(torch.autograd.Function):
         if not dy.is_contiguous(memory_format=torch.channels_last):
             dy = dy.contiguous(memory_format=torch.channels_last)
         ready = ctx.bnlink is not None and ctx.bnlink.ready
-        dx, dres, dw, db = _bn_bwd(dy, x, mask, w32, b32, mean, inv, ctx.relu, ctx.has_res, ready)
+        # a masked GradLink takes (dy, mask) instead of dres = dy * mask (one write pass less)
+        hand_masked = ctx.link is not None and ctx.link.masked and mask is not None and ctx.relu
+        dx, dres, dw, db = _bn_bwd(dy, x, mask, w32, b32, mean, inv, ctx.relu, ctx.has_res and not hand_masked,
+                                   ready)
         if ctx.bnlink is not None:
             ctx.bnlink.release()
         if ctx.link is not None:
-            ctx.link.grad, dres = dres, None
+            ctx.link.grad, dres = ((dy, mask) if hand_masked else dres), None
         return dx, dw.to(ctx.wdtype), db.to(ctx.wdtype), dres, None, None, None, None, None, None, None, None, None
 
 
@@ -444,6 +451,11 @@ def conv3x3(x, weight, with_stats=False, bnlink=None):
     ``conv3x3_forward_is_ours`` first."""
     ours = conv3x3_forward_is_ours(x, weight)
     return _Conv3x3.apply(x, weight, ours, with_stats and ours, bnlink)
+
+
+def masked_links_ok() -> bool:
+    """GradLinks may carry (dy, mask) instead of dres: the LDS-DMA dgrad kernel masks in its epilogue."""
+    return G.ENGINE != 1
 
 
 def conv1x1_stats(x, weight, link=None, bnlink=None):

@@ -223,3 +223,24 @@ def test_bn_stats_link_conv3x3(gpu_ext, with_res):
         grads.append([ci.grad, wi.grad, bn.weight.grad, bn.bias.grad] + ([ri.grad] if with_res else []))
     for a, b in zip(*grads):
         assert _rel(b, a) < 2e-3, (_rel(b, a))
+
+
+def test_masked_grad_link(gpu_ext):
+    """A masked GradLink hands (dy, relu mask) to conv1's dgrad epilogue, which applies the mask:
+    the BatchNorm backward writes no dres, and the gradients equal the unmasked hand-off's."""
+    from fluxmpi_amd.ops import fused_block as fb
+    from fluxmpi_amd.ops.batchnorm import FusedBatchNorm2d
+    torch.manual_seed(8)
+    x = torch.randn(4, 128, 14, 14, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(128, 128, 1, 1, device="cuda") * 0.1).bfloat16().contiguous(memory_format=torch.channels_last)
+    grads = []
+    for masked in (False, True):
+        bn = FusedBatchNorm2d(128).cuda()
+        xi, wi = x.clone().requires_grad_(), w.clone().requires_grad_()
+        link = fb.GradLink(masked=masked)
+        y = bn(fb.conv1x1_hybrid(xi, wi, link), relu=True, residual=xi, link=link)
+        (y.float() * torch.linspace(-1, 1, y.numel(), device="cuda").view_as(y)).sum().backward()
+        assert link.grad is None
+        grads.append([xi.grad, wi.grad, bn.weight.grad, bn.bias.grad])
+    for a, b in zip(*grads):  # the two forwards' batch statistics differ in float-atomic order only
+        assert _rel(b, a) < 1e-3
