@@ -84,6 +84,17 @@ void bn_stats_finalize(const void* x, const float* w, const float* b, float* run
 void bn_apply(const void* x, void* y, const void* residual, const float* w, const float* b,
               const float* save_mean, const float* save_invstd, int64_t rows, int64_t C, int relu,
               uint8_t* relu_mask, int dtype, hipStream_t stream);
+// Dual BatchNorm of a downsample block: y = relu(BN(x) + BN2(x2)) (+ 1-bit ReLU mask), and its
+// backward: dx, dx2 and both BatchNorms' dweight/dbias from one reduce + one dx pass over
+// (dy, mask, x, x2). ws/ws2: two zeroed statistics workspaces. C/8 must divide 256.
+void bn_apply_dual(const void* x, const void* x2, void* y, const float* w, const float* b, const float* save_mean,
+                   const float* save_invstd, const float* w2, const float* b2, const float* save_mean2,
+                   const float* save_invstd2, int64_t rows, int64_t C, uint8_t* relu_mask, int dtype,
+                   hipStream_t stream);
+void bn_bwd_dual(const void* dy, const uint8_t* relu_mask, const void* x, const void* x2, const float* w,
+                 const float* save_mean, const float* save_invstd, const float* w2, const float* save_mean2,
+                 const float* save_invstd2, void* dx, void* dx2, float* dweight, float* dbias, float* dweight2,
+                 float* dbias2, float* ws, float* ws2, int64_t rows, int64_t C, int dtype, hipStream_t stream);
 // Inference: y = act(x * scale + shift [+ residual]) from running statistics.
 void bn_fwd_infer(const void* x, void* y, const void* residual, const float* weight,
                   const float* bias, const float* running_mean, const float* running_var,

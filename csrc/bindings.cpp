@@ -114,6 +114,28 @@ PYBIND11_MODULE(_C, m) {
                    reinterpret_cast<uint8_t*>(mask), dtype, S(stream));
         });
 
+  m.def("bn_apply_dual",
+        [](uintptr_t x, uintptr_t x2, uintptr_t y, uintptr_t w, uintptr_t b, uintptr_t sm, uintptr_t si, uintptr_t w2,
+           uintptr_t b2, uintptr_t sm2, uintptr_t si2, int64_t rows, int64_t C, uintptr_t mask, int dtype,
+           uintptr_t stream) {
+          auto F = [](uintptr_t p) { return reinterpret_cast<const float*>(p); };
+          bn_apply_dual(reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(x2), reinterpret_cast<void*>(y),
+                        F(w), F(b), F(sm), F(si), F(w2), F(b2), F(sm2), F(si2), rows, C,
+                        reinterpret_cast<uint8_t*>(mask), dtype, S(stream));
+        });
+  m.def("bn_bwd_dual",
+        [](uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t x2, uintptr_t w, uintptr_t sm, uintptr_t si,
+           uintptr_t w2, uintptr_t sm2, uintptr_t si2, uintptr_t dx, uintptr_t dx2, uintptr_t dw, uintptr_t db,
+           uintptr_t dw2, uintptr_t db2, uintptr_t ws, uintptr_t ws2, int64_t rows, int64_t C, int dtype,
+           uintptr_t stream) {
+          auto F = [](uintptr_t p) { return reinterpret_cast<const float*>(p); };
+          auto W = [](uintptr_t p) { return reinterpret_cast<float*>(p); };
+          bn_bwd_dual(reinterpret_cast<const void*>(dy), reinterpret_cast<const uint8_t*>(mask),
+                      reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(x2), F(w), F(sm), F(si), F(w2),
+                      F(sm2), F(si2), reinterpret_cast<void*>(dx), reinterpret_cast<void*>(dx2), W(dw), W(db), W(dw2),
+                      W(db2), W(ws), W(ws2), rows, C, dtype, S(stream));
+        });
+
   // ---- fused stem pool -------------------------------------------------------
   m.def("bn_relu_maxpool_fwd",
         [](uintptr_t x, uintptr_t scale, uintptr_t shift, uintptr_t y, uintptr_t idx, int64_t N, int64_t H, int64_t W,

@@ -523,6 +523,206 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const T* __restrict
   }
 }
 
+// ---------------------------------------------------------------- dual (downsample block)
+// y = relu(BN_a(x) + BN_b(x2)): a ResNet downsample block's bn3 with the downsample branch's
+// BatchNorm folded into the residual read. The branch output BN_b(x2) is never materialised:
+// forward saves one write + one read per element, backward computes both input gradients in
+// one pass from (dy, relu mask, x, x2) (dy_eff is the same for both BatchNorms) instead of
+// bn3 writing dres and the branch BN reading it twice. FIXED channel mapping only
+// (C/8 divides the workgroup), per-lane coefficients of both BatchNorms in registers.
+__device__ __forceinline__ void coef8(const float* __restrict__ w, const float* __restrict__ b,
+                                      const float* __restrict__ mean, const float* __restrict__ inv, int c0,
+                                      float (&sc)[8], float (&sh)[8]) {
+  float mu[8], iv[8], ww[8], bb[8];
+  ld8ch(mean, c0, mu);
+  ld8ch(inv, c0, iv);
+  if (w) ld8ch(w, c0, ww);
+  if (b) ld8ch(b, c0, bb);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sc[j] = (w ? ww[j] : 1.f) * iv[j];
+    sh[j] = fmaf(-mu[j], sc[j], b ? bb[j] : 0.f);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void bn_norm_dual_kernel(
+    const T* __restrict__ x, const T* __restrict__ x2, T* __restrict__ y, const float* __restrict__ w,
+    const float* __restrict__ b, const float* __restrict__ mean, const float* __restrict__ inv,
+    const float* __restrict__ w2, const float* __restrict__ b2, const float* __restrict__ mean2,
+    const float* __restrict__ inv2, int C, int64_t nvec, uint8_t* __restrict__ mask) {
+  const int c0 = (threadIdx.x % (C / 8)) * 8;
+  float sc[8], sh[8], sc2[8], sh2[8];
+  coef8(w, b, mean, inv, c0, sc, sh);
+  coef8(w2, b2, mean2, inv2, c0, sc2, sh2);
+  auto vec = [&](float (&f)[8], const float (&g)[8]) {
+    unsigned bits = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float o = fmaf(f[j], sc[j], sh[j]) + fmaf(g[j], sc2[j], sh2[j]);
+      bits |= (o > 0.f ? 1u : 0u) << j;
+      f[j] = o > 0.f ? o : 0.f;
+    }
+    return bits;
+  };
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  int64_t v = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  for (; v + stride < nvec; v += 2 * stride) {
+    float f0[8], f1[8], g0[8], g1[8];
+    ld8f(x + v * 8, f0);
+    ld8f(x + (v + stride) * 8, f1);
+    ld8f(x2 + v * 8, g0);
+    ld8f(x2 + (v + stride) * 8, g1);
+    const unsigned b0 = vec(f0, g0), b1 = vec(f1, g1);
+    st8f(y + v * 8, f0);
+    st8f(y + (v + stride) * 8, f1);
+    mask[v] = static_cast<uint8_t>(b0);
+    mask[v + stride] = static_cast<uint8_t>(b1);
+  }
+  if (v < nvec) {
+    float f0[8], g0[8];
+    ld8f(x + v * 8, f0);
+    ld8f(x2 + v * 8, g0);
+    const unsigned b0 = vec(f0, g0);
+    st8f(y + v * 8, f0);
+    mask[v] = static_cast<uint8_t>(b0);
+  }
+}
+
+// acc[0:C] += sum(dy_eff), acc[C:2C] += sum(dy_eff * xhat) and acc2 likewise with xhat2
+template <typename T>
+__global__ __launch_bounds__(kThreads) void bn_bwd_reduce_dual_kernel(
+    const T* __restrict__ dy, const uint8_t* __restrict__ mask, const T* __restrict__ x, const T* __restrict__ x2,
+    const float* __restrict__ mean, const float* __restrict__ inv, const float* __restrict__ mean2,
+    const float* __restrict__ inv2, int64_t rows, int C, Geo g, float* __restrict__ acc, float* __restrict__ acc2) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int t = threadIdx.x;
+  const int r0 = t / g.cv, c8 = t % g.cv;
+  float s[8] = {0}, q[8] = {0}, q2[8] = {0};
+  if (r0 < g.rpi) {
+    float mu[8], is[8], mu2[8], is2[8];
+    ld8ch(mean, c8 * 8, mu);
+    ld8ch(inv, c8 * 8, is);
+    ld8ch(mean2, c8 * 8, mu2);
+    ld8ch(inv2, c8 * 8, is2);
+    const int64_t start = static_cast<int64_t>(blockIdx.x) * g.rows_per_block;
+    int64_t end = start + g.rows_per_block;
+    if (end > rows) end = rows;
+    int64_t r = start + r0;
+    constexpr int U = 4;  // 4 rows x 3 tensors of 16 B loads in flight per lane
+    for (; r + (U - 1) * g.rpi < end; r += U * g.rpi) {
+      T d[U][8], xv[U][8], x2v[U][8];
+      unsigned mb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t off = (r + u * g.rpi) * C + c8 * 8;
+        load8(dy + off, d[u]);
+        load8(x + off, xv[u]);
+        load8(x2 + off, x2v[u]);
+        mb[u] = mask[off >> 3];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float dd = (mb[u] >> j) & 1u ? static_cast<float>(d[u][j]) : 0.f;
+          s[j] += dd;
+          q[j] = fmaf(dd, (static_cast<float>(xv[u][j]) - mu[j]) * is[j], q[j]);
+          q2[j] = fmaf(dd, (static_cast<float>(x2v[u][j]) - mu2[j]) * is2[j], q2[j]);
+        }
+    }
+    for (; r < end; r += g.rpi) {
+      const int64_t off = r * C + c8 * 8;
+      float d[8], xv[8], x2v[8];
+      ld8f(dy + off, d);
+      ld8f(x + off, xv);
+      ld8f(x2 + off, x2v);
+      const unsigned mbs = mask[off >> 3];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float dd = (mbs >> j) & 1u ? d[j] : 0.f;
+        s[j] += dd;
+        q[j] = fmaf(dd, (xv[j] - mu[j]) * is[j], q[j]);
+        q2[j] = fmaf(dd, (x2v[j] - mu2[j]) * is2[j], q2[j]);
+      }
+    }
+  }
+  block_reduce_atomic(s, q, g.cv, g.rpi, C, acc, smem);
+  __syncthreads();  // the LDS staging is reused
+  block_reduce_atomic(s, q2, g.cv, g.rpi, C, acc2, smem);
+}
+
+// dx = A*dy_eff + B*x + D, dx2 = A2*dy_eff + B2*x2 + D2 (coefficients as in bn_bwd_dx_kernel)
+__device__ __forceinline__ void dx_coef8(const float* __restrict__ w, const float* __restrict__ mean,
+                                         const float* __restrict__ inv, const float* __restrict__ dw,
+                                         const float* __restrict__ db, float inv_n, int c0, float (&a)[8],
+                                         float (&bb)[8], float (&d)[8]) {
+  float iv[8], m[8], ww[8], kdb[8], kdw[8];
+  ld8ch(inv, c0, iv);
+  ld8ch(mean, c0, m);
+  ld8ch(db, c0, kdb);
+  ld8ch(dw, c0, kdw);
+  if (w) ld8ch(w, c0, ww);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float sc = (w ? ww[j] : 1.f) * iv[j];
+    const float k2 = kdb[j] * inv_n, k3 = kdw[j] * inv_n;
+    a[j] = sc;
+    bb[j] = -sc * iv[j] * k3;
+    d[j] = sc * (m[j] * iv[j] * k3 - k2);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void bn_bwd_dx_dual_kernel(
+    const T* __restrict__ dy, const uint8_t* __restrict__ mask, const T* __restrict__ x, const T* __restrict__ x2,
+    const float* __restrict__ w, const float* __restrict__ mean, const float* __restrict__ inv,
+    const float* __restrict__ dw, const float* __restrict__ db, const float* __restrict__ w2,
+    const float* __restrict__ mean2, const float* __restrict__ inv2, const float* __restrict__ dw2,
+    const float* __restrict__ db2, T* __restrict__ dx, T* __restrict__ dx2, int64_t rows, int C, int64_t nvec) {
+  const float inv_n = 1.f / static_cast<float>(rows);
+  const int c0 = (threadIdx.x % (C / 8)) * 8;
+  float a[8], bq[8], dq[8], a2[8], bq2[8], dq2[8];
+  dx_coef8(w, mean, inv, dw, db, inv_n, c0, a, bq, dq);
+  dx_coef8(w2, mean2, inv2, dw2, db2, inv_n, c0, a2, bq2, dq2);
+  auto vec = [&](float (&d)[8], float (&xv)[8], float (&x2v)[8], unsigned mbs) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float dd = (mbs >> j) & 1u ? d[j] : 0.f;
+      xv[j] = fmaf(a[j], dd, fmaf(bq[j], xv[j], dq[j]));
+      x2v[j] = fmaf(a2[j], dd, fmaf(bq2[j], x2v[j], dq2[j]));
+    }
+  };
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  int64_t v = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  for (; v + stride < nvec; v += 2 * stride) {
+    const int64_t v1 = v + stride;
+    float d0[8], x0[8], z0[8], d1[8], x1[8], z1[8];
+    ld8f(dy + v * 8, d0);
+    ld8f(x + v * 8, x0);
+    ld8f(x2 + v * 8, z0);
+    ld8f(dy + v1 * 8, d1);
+    ld8f(x + v1 * 8, x1);
+    ld8f(x2 + v1 * 8, z1);
+    const unsigned m0 = mask[v], m1 = mask[v1];
+    vec(d0, x0, z0, m0);
+    vec(d1, x1, z1, m1);
+    st8f(dx + v * 8, x0);
+    st8f(dx2 + v * 8, z0);
+    st8f(dx + v1 * 8, x1);
+    st8f(dx2 + v1 * 8, z1);
+  }
+  if (v < nvec) {
+    float d0[8], x0[8], z0[8];
+    ld8f(dy + v * 8, d0);
+    ld8f(x + v * 8, x0);
+    ld8f(x2 + v * 8, z0);
+    vec(d0, x0, z0, mask[v]);
+    st8f(dx + v * 8, x0);
+    st8f(dx2 + v * 8, z0);
+  }
+}
+
 // one full round of resident workgroups (or fewer if the tensor is small)
 int elementwise_grid(const void* kernel, size_t smem, int64_t nvec) {
   // >= 4 vectors per lane: every workgroup pays its coefficient prologue once
@@ -652,7 +852,76 @@ void bwd_t(const void* dy, const void* x, const void* y, const uint8_t* mask, co
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
 
+template <typename T>
+void apply_dual_t(const void* x, const void* x2, void* y, const float* w, const float* b, const float* sm,
+                  const float* si, const float* w2, const float* b2, const float* sm2, const float* si2, int64_t rows,
+                  int64_t C, uint8_t* mask, hipStream_t s) {
+  const int64_t nvec = rows * C / 8;
+  auto k = bn_norm_dual_kernel<T>;
+  k<<<elementwise_grid(reinterpret_cast<const void*>(k), 0, nvec), kThreads, 0, s>>>(
+      static_cast<const T*>(x), static_cast<const T*>(x2), static_cast<T*>(y), w, b, sm, si, w2, b2, sm2, si2,
+      (int)C, nvec, mask);
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+}
+
+template <typename T>
+void bwd_dual_t(const void* dy, const uint8_t* mask, const void* x, const void* x2, const float* w, const float* sm,
+                const float* si, const float* w2, const float* sm2, const float* si2, void* dx, void* dx2, float* dw,
+                float* db, float* dw2, float* db2, float* ws, float* ws2, int64_t rows, int64_t C, hipStream_t s) {
+  const T* dyr = static_cast<const T*>(dy);
+  const T* xr = static_cast<const T*>(x);
+  const T* x2r = static_cast<const T*>(x2);
+  const Geo g = reduce_geometry(reinterpret_cast<const void*>(bn_bwd_reduce_dual_kernel<T>), rows, C);
+  bn_bwd_reduce_dual_kernel<T><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(dyr, mask, xr, x2r, sm, si, sm2, si2,
+                                                                             rows, (int)C, g, ws, ws2);
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+  bn_finalize_bwd_kernel<<<finalize_blocks(C), kFinCh * kFinGroups, 0, s>>>(ws, (int)C, dw, db);
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+  bn_finalize_bwd_kernel<<<finalize_blocks(C), kFinCh * kFinGroups, 0, s>>>(ws2, (int)C, dw2, db2);
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+  const int64_t nvec = rows * C / 8;
+  auto k = bn_bwd_dx_dual_kernel<T>;
+  k<<<elementwise_grid(reinterpret_cast<const void*>(k), 0, nvec), kThreads, 0, s>>>(
+      dyr, mask, xr, x2r, w, sm, si, dw, db, w2, sm2, si2, dw2, db2, static_cast<T*>(dx), static_cast<T*>(dx2), rows,
+      (int)C, nvec);
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+}
+
+void check_dual(int64_t C, const uint8_t* mask) {
+  check(C);
+  if (!fixed_channels(C))
+    throw std::runtime_error("dual batchnorm: C/8 must divide 256 (got C=" + std::to_string(C) + ")");
+  if (mask == nullptr) throw std::runtime_error("dual batchnorm: the ReLU mask is required");
+}
+
 }  // namespace
+
+void bn_apply_dual(const void* x, const void* x2, void* y, const float* w, const float* b, const float* sm,
+                   const float* si, const float* w2, const float* b2, const float* sm2, const float* si2,
+                   int64_t rows, int64_t C, uint8_t* mask, int dtype, hipStream_t s) {
+  check_dual(C, mask);
+  check_aligned({w, b, sm, si, w2, b2, sm2, si2});
+  switch (dtype) {
+    case kBF16: apply_dual_t<bf16>(x, x2, y, w, b, sm, si, w2, b2, sm2, si2, rows, C, mask, s); break;
+    case kF16: apply_dual_t<f16>(x, x2, y, w, b, sm, si, w2, b2, sm2, si2, rows, C, mask, s); break;
+    case kF32: apply_dual_t<float>(x, x2, y, w, b, sm, si, w2, b2, sm2, si2, rows, C, mask, s); break;
+    default: throw std::runtime_error("dual batchnorm: unsupported dtype");
+  }
+}
+
+void bn_bwd_dual(const void* dy, const uint8_t* mask, const void* x, const void* x2, const float* w, const float* sm,
+                 const float* si, const float* w2, const float* sm2, const float* si2, void* dx, void* dx2, float* dw,
+                 float* db, float* dw2, float* db2, float* ws, float* ws2, int64_t rows, int64_t C, int dtype,
+                 hipStream_t s) {
+  check_dual(C, mask);
+  check_aligned({w, sm, si, w2, sm2, si2, dw, db, dw2, db2});
+  switch (dtype) {
+    case kBF16: bwd_dual_t<bf16>(dy, mask, x, x2, w, sm, si, w2, sm2, si2, dx, dx2, dw, db, dw2, db2, ws, ws2, rows, C, s); break;
+    case kF16: bwd_dual_t<f16>(dy, mask, x, x2, w, sm, si, w2, sm2, si2, dx, dx2, dw, db, dw2, db2, ws, ws2, rows, C, s); break;
+    case kF32: bwd_dual_t<float>(dy, mask, x, x2, w, sm, si, w2, sm2, si2, dx, dx2, dw, db, dw2, db2, ws, ws2, rows, C, s); break;
+    default: throw std::runtime_error("dual batchnorm: unsupported dtype");
+  }
+}
 
 size_t bn_workspace_floats(int64_t rows, int64_t C) {
   (void)rows;

@@ -122,12 +122,17 @@ class Bottleneck(nn.Module):
                 # offers its input gradient to conv1's dgrad through the SideGradLink) runs before
                 # it. (And after bn1 consumed conv1's epilogue statistics: the downsample BN uses
                 # the same statistics workspace.)
+                cds = None  # downsample conv output whose BN is fused into bn3 (dual_bn_relu)
                 if self.downsample is None:
                     identity = x
                 elif fused_ds:
                     ds = self.downsample
-                    identity = ds[1](fb.conv1x1_downsample(x, ds[0].weight, ds[0].stride[0],
-                                                           link if isinstance(link, fb.SideGradLink) else None))
+                    identity = fb.conv1x1_downsample(x, ds[0].weight, ds[0].stride[0],
+                                                     link if isinstance(link, fb.SideGradLink) else None)
+                    if out_link is None and fb.dual_bn_supported(identity, self.bn3, ds[1]):
+                        cds, identity = identity, None
+                    else:
+                        identity = ds[1](identity)
                 else:
                     identity = self.downsample(x)
                 if self.hybrid:
@@ -145,7 +150,10 @@ class Bottleneck(nn.Module):
                 else:
                     c2 = fb.conv3x3(a1, self.conv2.weight) if fb.conv3x3_supported(a1, self.conv2) else self.conv2(a1)
                     c3 = fb.bn_relu_conv1x1(c2, self.bn2, self.conv3.weight)  # bn2+relu fused into the A load
-                if self.hybrid and not o3:
+                if cds is not None:
+                    out = fb.dual_bn_relu(c3, self.bn3, cds, self.downsample[1],
+                                          stats_ready=o3 if self.hybrid else True)
+                elif self.hybrid and not o3:
                     out = self.bn3(c3, relu=True, residual=identity, link=link if self.downsample is None else None,
                                    bnlink=out_link)
                 elif self.hybrid:

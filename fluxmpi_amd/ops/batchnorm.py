@@ -71,6 +71,21 @@ def _link_workspace(x: torch.Tensor) -> torch.Tensor:
     return ws
 
 
+_DWS: dict = {}
+
+
+def _dual_workspace(x: torch.Tensor) -> torch.Tensor:
+    """Third persistent zeroed accumulator: the downsample branch's sums of the dual
+    (bn3 + downsample BN) backward, reduced in the same pass as bn3's into :func:`_workspace`."""
+    stream = torch.cuda.current_stream(x.device)
+    key = (x.device.index, stream.cuda_stream)
+    ws = _DWS.get(key)
+    if ws is None:
+        ws = torch.zeros(_SHARDS * 2 * _MAXC, device=x.device, dtype=torch.float32)
+        _DWS[key] = ws
+    return ws
+
+
 def kernel_supported(x: torch.Tensor) -> bool:
     if not x.is_cuda or x.dtype not in (torch.bfloat16, torch.float16, torch.float32):
         return False

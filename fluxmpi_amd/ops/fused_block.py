@@ -31,7 +31,7 @@ import os
 import torch
 
 from . import _ext
-from .batchnorm import BNStatsLink, GradLink, SideGradLink, _link_workspace, _workspace, bn_counter  # noqa: F401 (links re-exported)
+from .batchnorm import BNStatsLink, GradLink, SideGradLink, _dual_workspace, _link_workspace, _workspace, bn_counter  # noqa: F401 (links re-exported)
 from . import gemm as G
 from .gemm import conv1x1_dgrad, conv1x1_wgrad, conv3x3_dgrad, conv3x3_fwd, gemm, note_filter
 from .multi_tensor import DTYPE_CODE
@@ -52,6 +52,9 @@ CONV1X1 = os.environ.get("FLUXMPI_CONV1X1", "ours")
 # weight gradients of the bottleneck convolutions: "auto" = the fastest (measured once per
 # shape) of MIOpen and our split-K transposed-operand kernel in a few configurations
 WGRAD = os.environ.get("FLUXMPI_WGRAD", "auto")
+# downsample blocks: bn3 and the downsample branch's BatchNorm as one dual kernel pair
+# (relu(bn3(c3) + bn_ds(c_ds)) without materialising bn_ds(c_ds); see dual_bn_relu)
+DUAL_BN = os.environ.get("FLUXMPI_DUAL_BN", "1") == "1"
 
 
 def _stream(t):
@@ -268,6 +271,83 @@ class _BNFromStats(torch.autograd.Function):
         if ctx.link is not None:
             ctx.link.grad, dres = ((dy, mask) if hand_masked else dres), None
         return dx, dw.to(ctx.wdtype), db.to(ctx.wdtype), dres, None, None, None, None, None, None, None, None, None
+
+
+class _DualBN(torch.autograd.Function):
+    """out = relu(bn3(c3) + bn_ds(c_ds)) for a ResNet downsample block, without materialising the
+    downsample branch's output bn_ds(c_ds). Forward: bn3's statistics (pending from the conv3
+    GEMM epilogue when ``stats_ready``, else a stats pass), bn_ds's stats pass, one apply pass
+    reading (c3, c_ds). Backward: dy_eff = dy * relu_mask is the output gradient of BOTH
+    BatchNorms, so one reduce pass over (dy, mask, c3, c_ds) produces both BatchNorms' sums
+    and one pass writes both input gradients: versus two separate BatchNorms, the identity is
+    neither written nor read forward, and dres is neither written nor read twice backward
+    (~10 B/element saved on a block's largest activations)."""
+
+    @staticmethod
+    def forward(ctx, c3, w, b, rm, rv, mom, eps, nbt, stats_ready, cds, w2, b2, rm2, rv2, mom2, eps2, nbt2):
+        C = _ext.get(required=True)
+        cl = torch.channels_last
+        c3 = c3 if c3.is_contiguous(memory_format=cl) else c3.contiguous(memory_format=cl)
+        cds = cds if cds.is_contiguous(memory_format=cl) else cds.contiguous(memory_format=cl)
+        ch = c3.shape[1]
+        rows = c3.numel() // ch
+        f32 = dict(device=c3.device, dtype=torch.float32)
+        w32, b32, w232, b232 = w.float(), b.float(), w2.float(), b2.float()
+        mean, inv, mean2, inv2 = (torch.empty(ch, **f32) for _ in range(4))
+        ws, code, st = _workspace(c3), DTYPE_CODE[c3.dtype], _stream(c3)
+        # bn3 first: its sums may be pending in the workspace (conv3's GEMM epilogue)
+        C.bn_stats_finalize(c3.data_ptr(), w32.data_ptr(), b32.data_ptr(), _p(rm), _p(rv), mean.data_ptr(),
+                            inv.data_ptr(), 0, 0, ws.data_ptr(), rows, ch, float(mom), float(eps), int(stats_ready),
+                            code, st, _p(nbt))
+        C.bn_stats_finalize(cds.data_ptr(), w232.data_ptr(), b232.data_ptr(), _p(rm2), _p(rv2), mean2.data_ptr(),
+                            inv2.data_ptr(), 0, 0, ws.data_ptr(), rows, ch, float(mom2), float(eps2), 0, code, st,
+                            _p(nbt2))
+        y = torch.empty_like(c3)
+        mask = torch.empty(c3.numel() // 8, device=c3.device, dtype=torch.uint8)
+        C.bn_apply_dual(c3.data_ptr(), cds.data_ptr(), y.data_ptr(), w32.data_ptr(), b32.data_ptr(), mean.data_ptr(),
+                        inv.data_ptr(), w232.data_ptr(), b232.data_ptr(), mean2.data_ptr(), inv2.data_ptr(), rows, ch,
+                        mask.data_ptr(), code, st)
+        ctx.wdtypes = (w.dtype, w2.dtype)
+        ctx.save_for_backward(c3, cds, mask, w32, mean, inv, w232, mean2, inv2)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = _ext.get(required=True)
+        c3, cds, mask, w32, mean, inv, w232, mean2, inv2 = ctx.saved_tensors
+        if not dy.is_contiguous(memory_format=torch.channels_last):
+            dy = dy.contiguous(memory_format=torch.channels_last)
+        ch = c3.shape[1]
+        rows = c3.numel() // ch
+        dx, dx2 = torch.empty_like(c3), torch.empty_like(cds)
+        dw, db, dw2, db2 = (torch.empty(ch, device=c3.device, dtype=torch.float32) for _ in range(4))
+        C.bn_bwd_dual(dy.data_ptr(), mask.data_ptr(), c3.data_ptr(), cds.data_ptr(), w32.data_ptr(), mean.data_ptr(),
+                      inv.data_ptr(), w232.data_ptr(), mean2.data_ptr(), inv2.data_ptr(), dx.data_ptr(),
+                      dx2.data_ptr(), dw.data_ptr(), db.data_ptr(), dw2.data_ptr(), db2.data_ptr(),
+                      _workspace(c3).data_ptr(), _dual_workspace(c3).data_ptr(), rows, ch, DTYPE_CODE[c3.dtype],
+                      _stream(c3))
+        t1, t2 = ctx.wdtypes
+        return (dx, dw.to(t1), db.to(t1), None, None, None, None, None, None,
+                dx2, dw2.to(t2), db2.to(t2), None, None, None, None, None)
+
+
+def dual_bn_supported(c, bn, bn_ds) -> bool:
+    """``dual_bn_relu`` applies: fused training-mode affine BatchNorms with running statistics,
+    channels a power of two <= 2048 (C/8 divides the 256-lane workgroup)."""
+    from .batchnorm import FusedBatchNorm2d, kernel_supported
+    ch = c.shape[1]
+    return (DUAL_BN and kernel_supported(c) and c.dim() == 4 and (ch & (ch - 1)) == 0
+            and all(isinstance(m, FusedBatchNorm2d) and m.training and m.affine and m.track_running_stats
+                    for m in (bn, bn_ds)))
+
+
+def dual_bn_relu(c3, bn, cds, bn_ds, stats_ready=False):
+    """relu(bn(c3) + bn_ds(cds)) (training); ``stats_ready``: bn's sums are pending in the
+    workspace from the GEMM that produced c3."""
+    mom, nbt = bn_counter(bn)
+    mom2, nbt2 = bn_counter(bn_ds)
+    return _DualBN.apply(c3, bn.weight, bn.bias, bn.running_mean, bn.running_var, mom, bn.eps, nbt, stats_ready,
+                         cds, bn_ds.weight, bn_ds.bias, bn_ds.running_mean, bn_ds.running_var, mom2, bn_ds.eps, nbt2)
 
 
 class _BNReluConv1x1(torch.autograd.Function):

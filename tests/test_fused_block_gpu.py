@@ -244,3 +244,68 @@ def test_masked_grad_link(gpu_ext):
         grads.append([xi.grad, wi.grad, bn.weight.grad, bn.bias.grad])
     for a, b in zip(*grads):  # the two forwards' batch statistics differ in float-atomic order only
         assert _rel(b, a) < 1e-3
+
+
+@pytest.mark.parametrize("ch,hw", [(256, 14), (512, 7), (2048, 4)])
+def test_dual_bn_relu(gpu_ext, ch, hw):
+    """relu(bn3(c3) + bn_ds(c_ds)) through the dual kernels vs the fp32 composition: output,
+    both inputs' gradients, both BatchNorms' parameter gradients and running statistics."""
+    import torch.nn.functional as F
+    from fluxmpi_amd.ops import fused_block as fb
+    from fluxmpi_amd.ops.batchnorm import FusedBatchNorm2d
+    torch.manual_seed(ch)
+    cl = torch.channels_last
+    c3 = (torch.randn(8, ch, hw, hw, device="cuda") * 2 + 0.5).bfloat16().contiguous(memory_format=cl)
+    cds = (torch.randn(8, ch, hw, hw, device="cuda") * 0.7 - 0.3).bfloat16().contiguous(memory_format=cl)
+    bn, bnd = FusedBatchNorm2d(ch).cuda(), FusedBatchNorm2d(ch).cuda()
+    with torch.no_grad():
+        for m in (bn, bnd):
+            m.weight.uniform_(0.5, 1.5)
+            m.bias.uniform_(-0.2, 0.2)
+    rb = [t.clone() for t in (bn.running_mean, bn.running_var, bnd.running_mean, bnd.running_var)]
+    a, b = c3.clone().requires_grad_(), cds.clone().requires_grad_()
+    y = fb.dual_bn_relu(a, bn, b, bnd, stats_ready=False)
+    g = torch.randn(y.shape, device="cuda")
+    (y.float() * g).sum().backward()
+    a32, b32 = c3.float().requires_grad_(), cds.float().requires_grad_()
+    w1, b1, w2, b2 = (t.detach().clone().requires_grad_() for t in (bn.weight, bn.bias, bnd.weight, bnd.bias))
+    rm1, rv1, rm2, rv2 = rb
+    y32 = F.relu(F.batch_norm(a32, rm1, rv1, w1, b1, True, 0.1, 1e-5)
+                 + F.batch_norm(b32, rm2, rv2, w2, b2, True, 0.1, 1e-5))
+    (y32 * g).sum().backward()
+    assert _rel(y, y32) < 1e-2
+    for got, ref in ((a.grad, a32.grad), (b.grad, b32.grad), (bn.weight.grad, w1.grad), (bn.bias.grad, b1.grad),
+                     (bnd.weight.grad, w2.grad), (bnd.bias.grad, b2.grad)):
+        assert _rel(got, ref) < 2e-2
+    for got, ref in ((bn.running_mean, rm1), (bn.running_var, rv1), (bnd.running_mean, rm2), (bnd.running_var, rv2)):
+        assert _rel(got, ref) < 1e-3
+    assert int(bn.num_batches_tracked) == 1 and int(bnd.num_batches_tracked) == 1
+
+
+@pytest.mark.parametrize("impl", ["hybrid", "fused"])
+def test_resnet_dual_bn_matches_separate(gpu_ext, impl, monkeypatch):
+    """The ResNet downsample blocks with the dual BatchNorm vs the separate bn_ds + bn3 path,
+    both measured against the fp32 model (bf16 gradients of a deep net differ by ~10-30% at
+    the stem between any two bf16 pipelines; the dual one must be as accurate)."""
+    from fluxmpi_amd.models.resnet import ResNet
+    from fluxmpi_amd.ops import fused_block as fb
+    outs = []
+    x = torch.randn(8, 3, 64, 64, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    for dual in (False, True):
+        monkeypatch.setattr(fb, "DUAL_BN", dual)
+        ref, fus = _models(impl)
+        y = fus(x)
+        outs.append((y, fus))
+    f32 = ResNet((2, 1, 1, 1), 10, conv_impl="miopen", norm="fused").cuda().to(memory_format=torch.channels_last)
+    f32.load_state_dict({k: v.float() if v.is_floating_point() else v for k, v in ref.state_dict().items()})
+    yc = f32(x.float())
+    g = torch.randn_like(yc)
+    for y, m in outs + [(yc, f32)]:
+        (y.float() * g).sum().backward()
+    (ya, ma), (yb, mb) = outs
+    assert _rel(yb, yc) < 2 * _rel(ya, yc) + 1e-2
+    for (n, pa), pb, pc in zip(ma.named_parameters(), mb.parameters(), f32.parameters()):
+        ea, eb = _rel(pa.grad, pc.grad), _rel(pb.grad, pc.grad)
+        assert eb < 2 * ea + 2e-2, f"{n}: dual {eb:.3e} vs separate {ea:.3e}"
+    for (n, a), b in zip(ma.named_buffers(), mb.buffers()):
+        assert (torch.equal(a, b) if not a.dtype.is_floating_point else _rel(b, a) < 1e-2), n
