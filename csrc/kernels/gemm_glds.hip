@@ -692,7 +692,21 @@ void gemm_glds(const GemmProblem& g, hipStream_t stream) {
   // (64 KiB at 128x128: 2 workgroups/CU) wins for the 3x3 convolutions and once K >= 1024;
   // shorter K (memory-bound 1x1 convolutions) prefers the 32-deep 3-stage ring (48 KiB:
   // 3 workgroups/CU).
-  int var = g.engine >= 3 ? g.engine - 2 : 0;
+  int var = g.engine >= 3 && g.engine <= 6 ? g.engine - 2 : 0;
+  // engine 7 / 8: 256x128 tiles (waves of 128x64: 25% less LDS fragment traffic per MFMA than
+  // 64x64 waves), 32-deep 3-stage / 64-deep 2-stage ring; plain / residual / implicit-conv only
+  const bool big = (g.engine == 7 || g.engine == 8) && !aff && !bnb && g.M > 128 && g.N > 64;
+  if (big) {
+    const bool k64 = g.engine == 8 && (!conv || g.conv_c % 64 == 0);
+#define GB(BK, ST)                                                                                      \
+  {                                                                                                    \
+    if (conv) { if (res) launch_glds<256, 128, BK, ST, true, true>(a, stream); else launch_glds<256, 128, BK, ST, true, false>(a, stream); } \
+    else { if (res) launch_glds<256, 128, BK, ST, false, true>(a, stream); else launch_glds<256, 128, BK, ST, false, false>(a, stream); } \
+  }
+    if (k64) GB(64, 2) else GB(32, 3)
+#undef GB
+    return;
+  }
   const bool k64ok = !conv || g.conv_c % 64 == 0;
   if (var == 0) var = ((conv || g.K >= 1024) && k64ok) ? 3 : 1;
   if ((var == 3 || var == 4) && !k64ok) var = 1;

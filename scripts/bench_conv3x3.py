@@ -14,6 +14,9 @@ from fluxmpi_amd.ops.gemm import conv1x1_wgrad_v2, conv3x3_dgrad, conv3x3_fwd, c
 from fluxmpi_amd.utils.miopen import install_tuned_db  # noqa: E402
 
 
+ENGINES = tuple(int(e) for e in os.environ.get("BENCH_ENGINES", "1,2,3,5,6").split(","))
+
+
 def bench(fn, iters=20):
     for _ in range(3):
         fn()
@@ -39,7 +42,7 @@ def main():
         y = torch.empty_like(x)
         flop = 2 * B * H * H * C * C * 9
         rec = {"H": H, "C": C}
-        for eng in (1, 2, 3, 5, 6):
+        for eng in ENGINES:
             G.ENGINE = eng
             rec[f"e{eng}_fwd"] = bench(lambda: conv3x3_fwd(x, w, out=y))
             rec[f"e{eng}_dgrad"] = bench(lambda: conv3x3_dgrad(dy, w, out=y))

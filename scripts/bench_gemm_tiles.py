@@ -14,6 +14,9 @@ from fluxmpi_amd.ops import gemm as G  # noqa: E402
 from fluxmpi_amd.utils.miopen import install_tuned_db  # noqa: E402
 
 
+ENGINES = tuple(int(e) for e in os.environ.get("BENCH_ENGINES", "1,2,3,5,6").split(","))
+
+
 def bench(fn, iters=20):
     for _ in range(3):
         fn()
@@ -43,7 +46,7 @@ def main():
         y = torch.empty(M, co, device="cuda", dtype=torch.bfloat16)
         dx = torch.empty(M, ci, device="cuda", dtype=torch.bfloat16)
         rec = {"H": H, "Cin": ci, "Cout": co}
-        for eng in (1, 2, 3, 5, 6):
+        for eng in ENGINES:
             G.ENGINE = eng
             rec[f"fwd_e{eng}"] = bench(lambda: gemm(x, w, y, M=M, N=co, K=ci, lda=ci, ldb=ci, ldc=co))
         G.ENGINE = 0
@@ -67,7 +70,7 @@ def main():
         b = torch.randn(n, n, device="cuda").bfloat16()
         c = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
         rec = {"square": n}
-        for eng in (1, 2, 3, 5, 6):
+        for eng in ENGINES:
             G.ENGINE = eng
             us = bench(lambda: gemm(a, b, c, M=n, N=n, K=n, lda=n, ldb=n, ldc=n), iters=10)
             rec[f"e{eng}_TF"] = round(2 * n ** 3 / us / 1e6, 1)

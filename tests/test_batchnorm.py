@@ -106,7 +106,8 @@ def test_resnet_fused_vs_torch_norm(gpu_ext):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("shape,k,s,p", [((4, 64, 32, 32), 3, 2, 1), ((2, 16, 17, 15), 3, 2, 1),
-                                          ((2, 32, 12, 12), 2, 2, 0), ((3, 8, 9, 11), 3, 1, 1)])
+                                          ((2, 32, 12, 12), 2, 2, 0), ((3, 8, 9, 11), 3, 1, 1),
+                                          ((2, 24, 10, 10), 3, 2, 1)])
 def test_bn_relu_maxpool_vs_reference(gpu_ext, shape, k, s, p):
     """Fused stem tail vs max_pool2d(relu(batch_norm(x))) in fp32 on the same bf16 input."""
     import torch.nn.functional as F

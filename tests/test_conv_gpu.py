@@ -8,7 +8,8 @@ pytestmark = pytest.mark.gpu
 SHAPES = [(2, 32, 5, 7, 64), (3, 64, 14, 14, 128), (1, 96, 9, 11, 32), (2, 128, 8, 8, 256), (4, 64, 3, 3, 64)]
 
 
-@pytest.fixture(params=[1, 2, 3, 5, 6], ids=["regstage", "glds", "glds_bk32s3", "glds_bk64s2", "glds_bk64s3"],
+@pytest.fixture(params=[1, 2, 3, 5, 6, 7, 8],
+                ids=["regstage", "glds", "glds_bk32s3", "glds_bk64s2", "glds_bk64s3", "glds256_bk32", "glds256_bk64"],
                 autouse=True)
 def engine(request, monkeypatch):
     """Every case runs on both GEMM kernels (register-staged, LDS-DMA pipelined)."""
@@ -29,7 +30,7 @@ def _rel(a, b):
 @pytest.mark.parametrize("use_aff", [False, True])
 def test_conv3x3_fwd(gpu_ext, N, C, H, W, Co, use_aff, engine):
     from fluxmpi_amd.ops.gemm import SHARDS, conv3x3_fwd
-    if use_aff and engine in (3, 5, 6):
+    if use_aff and engine in (3, 5, 6, 7, 8):
         pytest.skip("forced variants: the prologue affine is covered by engines 1 and 2")
     torch.manual_seed(0)
     x = _nhwc(torch.randn(N, C, H, W, device="cuda").bfloat16())
@@ -65,7 +66,7 @@ def test_conv3x3_dgrad(gpu_ext, N, C, H, W, Co):
 
 
 @pytest.mark.parametrize("M,K,N", [(4096, 64, 256), (1000, 96, 160), (512, 256, 64), (2048, 512, 1024),
-                                   (200, 32, 32), (777, 64, 192), (300, 40, 72)])
+                                   (200, 32, 32), (777, 64, 192), (300, 40, 72), (1300, 320, 136)])
 @pytest.mark.parametrize("mode,use_res", [(0, False), (1, False), (0, True)])
 def test_gemm_tn(gpu_ext, M, K, N, mode, use_res, engine):
     """C = A @ B^T (both K-major) [+ residual] [+ column statistics] on the selected kernel."""
