@@ -408,7 +408,7 @@ void launch_glds(GldsArgs a, hipStream_t s) {
 // ---------------------------------------------------------------------------------------------
 // Weight gradient: C[m][n] (+)= sum_k A[k][m] * B[k][n] with BOTH operands stored k-major-rows
 // ([K][M] / [K][N], the pixel index k slowest: dY [pix][Cout] and X [pix][Cin] of NHWC
-// activations), split over K (blockIdx.z) into fp32 partials. The tiles [32 k][ROWS] go
+// activations), split over K (one 1-D grid over split x tile) into fp32 partials. The tiles [32 k][ROWS] go
 // global -> LDS by LDS-DMA through a 3-stage ring and are read as MFMA fragments with
 // ds_read_b64_tr_b16 (the transposed LDS read). Swizzle of a 16-B slot in a k-row,
 // swz_tr(k): the 64 lanes of one tr read touch 16 k-rows x 32 B, and every 32 lanes (8 rows)
@@ -428,6 +428,7 @@ struct WgradArgs {
   int64_t k_per_split;
   int tiles_m, tiles_n;
   int conv_h, conv_w, conv_c;
+  int remap;  // 1: XCD-aware (split, tile) order over the whole grid (default); 0: dispatch order
 };
 
 // Per-lane LDS-DMA loader of a [BK k-rows][ROWS] tile sequence (k advancing by BK per step).
@@ -536,15 +537,20 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_wgrad_kernel(WgradArgs p) {
   __shared__ __attribute__((aligned(16))) bf16 smem[kStages * (A_ELEMS + B_ELEMS)];
   auto sa = [&](int s) { return smem + s * A_ELEMS; };
   auto sb = [&](int s) { return smem + kStages * A_ELEMS + s * B_ELEMS; };
+  // 1-D grid over (split, tile), XCD-aware and bijective over the whole grid: each XCD gets a
+  // contiguous range of (split-major) ids, so the tiles of one K-split — which read the same
+  // A / B rows — run on one XCD and share its L2 (blockIdx round-robins the XCDs otherwise)
   const int nt = p.tiles_m * p.tiles_n;
-  int bid = blockIdx.x;
-  {
-    const int q = nt / 8, r = nt % 8, xcd = bid % 8, pos = bid / 8;
-    bid = nt >= 8 ? (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos : bid;
+  const int total = static_cast<int>(gridDim.x);
+  int lid = blockIdx.x;
+  if (p.remap && total >= 8) {
+    const int q = total / 8, r = total % 8, xcd = lid % 8, pos = lid / 8;
+    lid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
   }
+  const int split = lid / nt, bid = lid - split * nt;
   const int tm = bid / p.tiles_n, tn = bid % p.tiles_n;
   const int64_t m0 = static_cast<int64_t>(tm) * BM, n0 = static_cast<int64_t>(tn) * BN;
-  const int64_t kbeg = static_cast<int64_t>(blockIdx.z) * p.k_per_split;
+  const int64_t kbeg = static_cast<int64_t>(split) * p.k_per_split;
   const int64_t kend = kbeg + p.k_per_split < p.K ? kbeg + p.k_per_split : p.K;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wm = wave >> 1, wn = wave & 1;
@@ -590,7 +596,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_wgrad_kernel(WgradArgs p) {
     }
   }
   // fp32 partial of this split: acc[i][j][r] is (row wm*WM + i*16 + 4*(lane>>4) + r, col wn*WN + j*16 + lane&15)
-  float* c = p.c + static_cast<int64_t>(blockIdx.z) * p.M * p.N;
+  float* c = p.c + static_cast<int64_t>(split) * p.M * p.N;
   const int col_in = lane & 15, rq = 4 * (lane >> 4);
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -757,12 +763,14 @@ void gemm_wgrad(const void* a, const void* b, float* ws, int64_t lda, int64_t ld
   w.k_per_split = (nk + splits - 1) / splits * 64;
   const int sp = static_cast<int>((K + w.k_per_split - 1) / w.k_per_split);
   w.conv_h = conv_h; w.conv_w = conv_w; w.conv_c = conv_c;
+  w.remap = (variant & 4) ? 0 : 1;  // bit 2 of variant: plain dispatch order (A/B experiments)
+  variant &= 3;
   const bool m128 = M > 64, n128 = N > 64;
 #define WG(BM, BN)                                                                                      \
   {                                                                                                     \
     w.tiles_m = static_cast<int>((M + BM - 1) / BM);                                                   \
     w.tiles_n = static_cast<int>((N + BN - 1) / BN);                                                   \
-    dim3 grid(w.tiles_m * w.tiles_n, 1, sp);                                                            \
+    dim3 grid(w.tiles_m * w.tiles_n * sp);                                                              \
     if (variant == 2) {                                                                                 \
       if (conv_h > 0) gemm_wgrad_kernel<BM, BN, 64, 2, true><<<grid, kThreads, 0, stream>>>(w);         \
       else gemm_wgrad_kernel<BM, BN, 64, 2, false><<<grid, kThreads, 0, stream>>>(w);                   \

@@ -273,6 +273,8 @@ def _actual_splits_v2(K: int, splits: int) -> int:
 
 # weight-gradient kernel variant: 1 = 32-deep K-step / 3 stages, 2 = 64-deep / 2 stages
 WGRAD_VARIANT = int(os.environ.get("FLUXMPI_WGRAD_VARIANT", "1"))
+# 1 (default): XCD-aware (split, tile) block order in the weight-gradient grid; 0: dispatch order
+WGRAD_REMAP = os.environ.get("FLUXMPI_WGRAD_REMAP", "1") == "1"
 
 
 def conv1x1_wgrad_v2(dy2d: torch.Tensor, x2d: torch.Tensor, out_dtype=torch.bfloat16, splits: int | None = None):
@@ -283,7 +285,7 @@ def conv1x1_wgrad_v2(dy2d: torch.Tensor, x2d: torch.Tensor, out_dtype=torch.bflo
     ws = torch.empty(s, Co, Ci, device=dy2d.device, dtype=torch.float32)
     C = _ext.get(required=True)
     C.gemm_wgrad(dy2d.data_ptr(), x2d.data_ptr(), ws.data_ptr(), dy2d.stride(0), x2d.stride(0), Co, Ci, K, s, 0, 0, 0,
-                 _stream(dy2d), WGRAD_VARIANT)
+                 _stream(dy2d), WGRAD_VARIANT | (0 if WGRAD_REMAP else 4))
     return _wgrad_reduce(ws, s, torch.empty(Co, Ci, device=dy2d.device, dtype=out_dtype))
 
 
@@ -301,7 +303,7 @@ def conv3x3_wgrad(dy: torch.Tensor, x: torch.Tensor, splits: int | None = None) 
     ws = torch.empty(s, co, N, device=dy.device, dtype=torch.float32)
     C = _ext.get(required=True)
     C.gemm_wgrad(dys.data_ptr(), xs.data_ptr(), ws.data_ptr(), co, ci, co, N, K, s, h, wd, ci, _stream(dy),
-                 WGRAD_VARIANT)
+                 WGRAD_VARIANT | (0 if WGRAD_REMAP else 4))
     dw = torch.empty(co, 3, 3, ci, device=dy.device, dtype=dy.dtype)
     _wgrad_reduce(ws, s, dw)
     return dw.permute(0, 3, 1, 2)
