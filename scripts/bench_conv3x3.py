@@ -14,6 +14,8 @@ from fluxmpi_amd.ops.gemm import conv1x1_wgrad_v2, conv3x3_dgrad, conv3x3_fwd, c
 from fluxmpi_amd.utils.miopen import install_tuned_db  # noqa: E402
 
 
+WG_CFGS = tuple(tuple(int(t) for t in c.split(":")) for c in
+                os.environ.get("BENCH_WG_CFGS", "1:768,2:768,1:1536,2:512").split(","))
 ENGINES = tuple(int(e) for e in os.environ.get("BENCH_ENGINES", "1,2,3,5,6").split(","))
 
 
@@ -54,7 +56,7 @@ def main():
         rec["ours_dgrad"] = rec["e2_dgrad"]
         rec["miopen_dgrad"] = bench(lambda: torch.ops.aten.convolution_backward(
             dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [True, False, False]))
-        for v, tw in ((1, 768), (2, 768), (1, 1536), (2, 512)):
+        for v, tw in WG_CFGS:
             G.WGRAD_VARIANT, G.WGRAD_TARGET_WG = v, tw
             rec[f"ours_wgrad_v{v}_{tw}"] = bench(lambda: conv3x3_wgrad(dy, x))
         rec["miopen_wgrad"] = bench(lambda: torch.ops.aten.convolution_backward(
@@ -87,7 +89,7 @@ def main():
         w = torch.randn(co, ci, 1, 1, device="cuda").bfloat16()
         x2, dy2 = x.permute(0, 2, 3, 1).reshape(-1, ci), dy.permute(0, 2, 3, 1).reshape(-1, co)
         rec = {"H": H, "Cin": ci, "Cout": co}
-        for v, tw in ((1, 768), (2, 768), (1, 1536), (2, 512)):
+        for v, tw in WG_CFGS:
             G.WGRAD_VARIANT, G.WGRAD_TARGET_WG = v, tw
             rec[f"ours_wgrad1_v{v}_{tw}"] = bench(lambda: conv1x1_wgrad_v2(dy2, x2))
         rec["miopen_wgrad1"] = bench(lambda: torch.ops.aten.convolution_backward(
