@@ -158,6 +158,11 @@ struct GemmProblem {
   // LDS-DMA kernel: residual element (m, n) counts only if bit n%8 of res_mask[(m*N + n)/8] is set
   // (the 1-bit ReLU mask of the BatchNorm whose output gradient the residual is)
   const uint8_t* res_mask = nullptr;
+  // LDS-DMA kernel: res_sub_h > 0 — the residual is the compact stride-2 subsample of an
+  // [M/(H*W)][H][W] row grid (H = res_sub_h, W = res_sub_w): output row (n, h, w) adds residual row
+  // (n, h/2, w/2) when h and w are even and nothing otherwise (a stride-2 1x1 convolution's input
+  // gradient, without the zero-filled full-resolution tensor). No res_mask with it.
+  int res_sub_h = 0, res_sub_w = 0;
 };
 void gemm_bf16(const GemmProblem& g, hipStream_t stream);
 // the LDS-DMA pipelined kernel: K-major A (or implicit conv) and B, modes 0/1, optional residual,

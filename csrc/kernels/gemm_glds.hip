@@ -66,6 +66,7 @@ struct GldsArgs {
   const uint8_t* bnb_mask;
   int bnb_rm;
   const uint8_t* res_mask;  // RES: 1-bit mask of the residual ([M][N] bits, n fastest), or nullptr
+  int res_sub_h, res_sub_w;  // RES: > 0 — compact stride-2 residual of an [M/(H*W)][H][W] row grid
   const float* a_scale;  // AFF: A element (m, k) -> relu(A * a_scale[c] + a_shift[c]), c = channel of k
   const float* a_shift;
   int aff_c;             // channels of the affine (C for the implicit conv, K for a 1x1)
@@ -313,8 +314,19 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_glds_kernel(GldsArgs p) {
         mk[u] = 0xFFu;
       }
       if (RES && ok) {
-        rv[u] = *reinterpret_cast<const uint4*>(p.res + m * p.ldr + n);
-        if (p.res_mask != nullptr) rmk[u] = p.res_mask[(m * p.N + n) >> 3];
+        if (p.res_sub_h > 0) {  // 32-bit row math (host-checked M < 2^31)
+          const unsigned mm = static_cast<unsigned>(m), W = p.res_sub_w;
+          const unsigned HW = static_cast<unsigned>(p.res_sub_h) * W;
+          const unsigned img = mm / HW, hw = mm - img * HW, h = hw / W, w = hw - h * W;
+          if (((h | w) & 1u) == 0) {
+            const unsigned ho = (p.res_sub_h + 1) >> 1, wo = (W + 1) >> 1;
+            const int64_t rrow = static_cast<int64_t>((img * ho + (h >> 1)) * wo + (w >> 1));
+            rv[u] = *reinterpret_cast<const uint4*>(p.res + rrow * p.ldr + n);
+          }
+        } else {
+          rv[u] = *reinterpret_cast<const uint4*>(p.res + m * p.ldr + n);
+          if (p.res_mask != nullptr) rmk[u] = p.res_mask[(m * p.N + n) >> 3];
+        }
       }
       if (BNB && bnb && ok) {
         xv[u] = *reinterpret_cast<const uint4*>(p.bnb_x + m * p.N + n);
@@ -669,7 +681,9 @@ bool gemm_glds_supported(const GemmProblem& g) {
          g.ldc % 8 == 0 && (g.res == nullptr || g.ldr % 8 == 0) &&
          (g.bnb_x == nullptr || (g.mode == 1 && g.ldc == g.N && g.bnb_mean != nullptr && g.bnb_inv != nullptr &&
                                  (g.bnb_rm == 0 || g.bnb_rm == 2 || (g.bnb_rm == 3 && g.bnb_mask != nullptr)))) &&
-         (g.conv_h == 0 || (g.conv_c % 32 == 0 && g.K == 9LL * g.conv_c));
+         (g.conv_h == 0 || (g.conv_c % 32 == 0 && g.K == 9LL * g.conv_c)) &&
+         (g.res_sub_h == 0 || (g.res != nullptr && g.res_mask == nullptr && g.res_sub_w > 0 && g.M < (1LL << 31) &&
+                               g.M % (static_cast<int64_t>(g.res_sub_h) * g.res_sub_w) == 0));
 }
 
 void gemm_glds(const GemmProblem& g, hipStream_t stream) {
@@ -689,6 +703,7 @@ void gemm_glds(const GemmProblem& g, hipStream_t stream) {
   a.bnb_mask = g.bnb_mask; a.bnb_rm = g.bnb_rm;
   a.a_scale = g.a_scale; a.a_shift = g.a_shift;
   a.res_mask = g.res_mask;
+  a.res_sub_h = g.res_sub_h; a.res_sub_w = g.res_sub_w;
   a.aff_c = static_cast<int>(g.conv_h > 0 ? g.conv_c : g.K);
   const bool aff = g.a_scale != nullptr;
   const bool bnb = g.bnb_x != nullptr;

@@ -120,6 +120,23 @@ class _Conv1x1Stats(torch.autograd.Function):
         return dx, dw, None, None
 
 
+class Stride2Grad:
+    """The input gradient of a stride-2 1x1 convolution in compact form ([N, C, ceil(H/2),
+    ceil(W/2)]: only the even positions of the full-resolution gradient are nonzero), as handed
+    through a :class:`SideGradLink`; the consumer's dgrad epilogue adds it at even (h, w)."""
+
+    __slots__ = ("t",)
+
+    def __init__(self, t):
+        self.t = t
+
+    def expand(self, shape):
+        n, c, h, w = shape
+        full = _empty_nhwc(n, c, h, w, self.t).zero_()
+        full[:, :, ::2, ::2] = self.t
+        return full
+
+
 def _dgrad_nhwc(dc2, weight, x, link, bnlink=None):
     """dX (NHWC, x's shape) = dC @ W [+ the residual gradient delivered through ``link``]; with a
     bound ``bnlink`` the epilogue also accumulates the backward reductions of the BatchNorm
@@ -127,11 +144,13 @@ def _dgrad_nhwc(dc2, weight, x, link, bnlink=None):
     co, ci = weight.shape[0], weight.shape[1]
     n, _, h, w = x.shape
     dx = _empty_nhwc(n, ci, h, w, x)
-    res = res_mask = None
+    res = res_mask = res_sub = None
     if link is not None:
         g = link.take()  # SideGradLink: None if its producer has not run (it then returns its own)
         if isinstance(g, tuple):  # masked GradLink: (dy, 1-bit ReLU mask), masked in the epilogue
             res, res_mask = _nhwc2d(g[0]), g[1]
+        elif isinstance(g, Stride2Grad):  # compact gradient of a stride-2 1x1 conv's input
+            res, res_sub = _nhwc2d(g.t), (h, w)
         elif g is not None:
             res = _nhwc2d(g)
     bn = stats = None
@@ -140,7 +159,7 @@ def _dgrad_nhwc(dc2, weight, x, link, bnlink=None):
         bn = (_nhwc2d(bnlink.x), bnlink.w32, bnlink.b32, bnlink.mean, bnlink.inv, bnlink.mask, bnlink.relu_mode)
         stats = _link_workspace(dx)
     conv1x1_dgrad(dc2, weight.reshape(co, ci), residual=res, out=_nhwc2d(dx), bn_bwd=bn, stats=stats, w4d=weight,
-                  residual_mask=res_mask)
+                  residual_mask=res_mask, residual_sub=res_sub)
     if bn is not None:
         bnlink.ready = True
     return dx
@@ -185,16 +204,16 @@ class _Conv1x1Hybrid(torch.autograd.Function):
 
 class _Conv1x1Downsample(torch.autograd.Function):
     """The downsample 1x1 convolution (stride 1 or 2) of a ResNet block, MIOpen forward and
-    weight gradient. Its input gradient (our dgrad GEMM at stride 1, MIOpen's strided dgrad
-    at stride 2) is handed to the block's conv1 through a :class:`SideGradLink`, whose dgrad
-    epilogue adds it: no separate add kernel over the block input's gradient."""
+    weight gradient. Its input gradient (our dgrad GEMM; at stride 2 over the output pixels
+    only, in the compact :class:`Stride2Grad` form) is handed to the block's conv1 through a
+    :class:`SideGradLink`, whose dgrad epilogue adds it: no separate add kernel over the block
+    input's gradient, and at stride 2 no zero-filled full-resolution gradient either."""
 
     @staticmethod
     def forward(ctx, x, weight, stride, link):
         x = x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
         ctx.stride, ctx.link = stride, link
-        if stride == 1:
-            note_filter(weight)
+        note_filter(weight)
         ctx.save_for_backward(x, weight)
         return torch.nn.functional.conv2d(x, weight, None, stride)
 
@@ -208,6 +227,18 @@ class _Conv1x1Downsample(torch.autograd.Function):
         dx = dw = None
         if s == 1 and need_x:
             dx = _dgrad_nhwc(_nhwc2d(dc), weight, x, None)
+        elif s == 2 and need_x and ctx.link is not None and G.ENGINE != 1 and x.shape[1] % 8 == 0:
+            # compact: the GEMM over the strided output pixels only; conv1's dgrad epilogue adds it
+            # at the even positions (no zero-filled full-resolution gradient is written or read)
+            n, co, ho, wo = dc.shape
+            ci = weight.shape[1]
+            dxc = _empty_nhwc(n, ci, ho, wo, dc)
+            conv1x1_dgrad(_nhwc2d(dc), weight.reshape(co, ci), out=_nhwc2d(dxc), w4d=weight)
+            if ctx.link.offer(Stride2Grad(dxc)):
+                dxc = None
+                need_x = False  # delivered
+            else:
+                dx = Stride2Grad(dxc).expand(x.shape)
         if need_w or (need_x and dx is None):
             dx_m, dw = torch.ops.aten.convolution_backward(dc, x, weight, None, [s, s], [0, 0], [1, 1], False,
                                                            [0, 0], 1, [need_x and dx is None, need_w, False])[:2]

@@ -34,8 +34,9 @@ def _ptr(t):
 
 def gemm(a, b, c, *, M, N, K, lda, ldb, ldc, a_kmajor=True, b_kmajor=True, mode=0, splits=1, a_affine=None,
          b_affine=None, stats=None, tile_m=0, tile_n=0, nbuf=0, residual=None, bn_bwd=None, conv=None, engine=None,
-         res_mask=None):
-    """``bn_bwd``: ``(x2d, w32, b32, mean, inv, mask, relu_mode)`` of a BatchNorm whose output
+         res_mask=None, res_sub=None):
+    """``res_sub=(H, W)``: ``residual`` is the compact stride-2 subsample of the [M/(H*W), H, W]
+    row grid (added at even (h, w) only). ``bn_bwd``: ``(x2d, w32, b32, mean, inv, mask, relu_mode)`` of a BatchNorm whose output
     gradient is C — with ``mode=1`` the epilogue accumulates that BatchNorm's backward
     reductions into ``stats`` instead of C's sum / sum of squares. ``conv=(H, W, C)``: A is the
     implicit 3x3/s1/p1 im2col of the NHWC image batch ``a`` (K = 9*C)."""
@@ -47,7 +48,7 @@ def gemm(a, b, c, *, M, N, K, lda, ldb, ldc, a_kmajor=True, b_kmajor=True, mode=
                 _ptr(asc), _ptr(ash), _ptr(bsc), _ptr(bsh), _ptr(stats), tile_m, tile_n, _stream(c), nbuf or NBUF,
                 _ptr(residual), residual.stride(0) if residual is not None else 0, _ptr(bx), _ptr(bw), _ptr(bb),
                 _ptr(bmean), _ptr(binv), _ptr(bmask), int(brm), *(conv if conv is not None else (0, 0, 0)),
-                ENGINE if engine is None else engine, _ptr(res_mask))
+                ENGINE if engine is None else engine, _ptr(res_mask), *(res_sub if res_sub is not None else (0, 0)))
     return c
 
 
@@ -66,17 +67,20 @@ def conv1x1_fwd(x2d: torch.Tensor, w2d: torch.Tensor, in_affine=None, stats: tor
 
 def conv1x1_dgrad(dy2d: torch.Tensor, w2d: torch.Tensor, residual: torch.Tensor | None = None,
                   out: torch.Tensor | None = None, bn_bwd=None, stats: torch.Tensor | None = None,
-                  w4d: torch.Tensor | None = None, residual_mask: torch.Tensor | None = None):
+                  w4d: torch.Tensor | None = None, residual_mask: torch.Tensor | None = None, residual_sub=None):
     """``dy2d`` [M, Cout], ``w2d`` [Cout, Cin] -> dX [M, Cin] bf16 (``+ residual`` [M, Cin] bf16 fused
     into the epilogue: the gradient of a residual block's input in one pass). ``bn_bwd`` /
     ``stats``: accumulate the backward reductions of the BatchNorm that produced the conv's
     input (see :func:`gemm`) into the sharded ``stats`` workspace. ``w4d``: the filter parameter
-    itself (its forward called :func:`note_filter`): enables the LDS-DMA kernel on the cached W^T."""
+    itself (its forward called :func:`note_filter`): enables the LDS-DMA kernel on the cached W^T.
+    ``residual_sub=(H, W)``: the residual is the compact stride-2 subsample (see :func:`gemm`)."""
     M, Co = dy2d.shape
     Ci = w2d.shape[1]
     dx = out if out is not None else torch.empty(M, Ci, device=dy2d.device, dtype=torch.bfloat16)
     if residual is not None:
-        assert residual.shape == (M, Ci) and residual.dtype == torch.bfloat16 and residual.stride(1) == 1
+        rows = M if residual_sub is None else \
+            M // (residual_sub[0] * residual_sub[1]) * ((residual_sub[0] + 1) // 2) * ((residual_sub[1] + 1) // 2)
+        assert residual.shape == (rows, Ci) and residual.dtype == torch.bfloat16 and residual.stride(1) == 1
     if bn_bwd is not None:
         assert stats is not None and dx.stride(0) == Ci and bn_bwd[0].shape == (M, Ci) and bn_bwd[0].stride(0) == Ci
     if ENGINE != 1 and w4d is not None and dy2d.stride(0) % 8 == 0 and Ci % 8 == 0:
@@ -85,10 +89,11 @@ def conv1x1_dgrad(dy2d: torch.Tensor, w2d: torch.Tensor, residual: torch.Tensor 
             assert residual is not None and residual.stride(0) == Ci and residual_mask.numel() * 8 == M * Ci
         gemm(dy2d, filter_t(w4d), dx, M=M, N=Ci, K=Co, lda=dy2d.stride(0), ldb=Co, ldc=dx.stride(0),
              residual=residual, mode=1 if bn_bwd is not None else 0, stats=stats, bn_bwd=bn_bwd,
-             engine=ENGINE or 2, res_mask=residual_mask)
+             engine=ENGINE or 2, res_mask=residual_mask, res_sub=residual_sub)
         return dx
-    if residual_mask is not None:
-        raise RuntimeError("conv1x1_dgrad: a masked residual needs the LDS-DMA kernel (w4d, FLUXMPI_GEMM_ENGINE != 1)")
+    if residual_mask is not None or residual_sub is not None:
+        raise RuntimeError("conv1x1_dgrad: a masked / stride-2 residual needs the LDS-DMA kernel "
+                           "(w4d, FLUXMPI_GEMM_ENGINE != 1)")
     gemm(dy2d, w2d, dx, M=M, N=Ci, K=Co, lda=dy2d.stride(0), ldb=w2d.stride(0), ldc=dx.stride(0), a_kmajor=True,
          b_kmajor=False, residual=residual, mode=1 if bn_bwd is not None else 0, stats=stats, bn_bwd=bn_bwd,
          engine=1)

@@ -122,3 +122,53 @@ def test_conv1x1_wgrad_v2(gpu_ext, M, K, N, engine, monkeypatch):
     for splits in (None, 1, 5):
         dw = conv1x1_wgrad_v2(dy, x, out_dtype=torch.float32, splits=splits)
         assert _rel(dw, ref) < 1e-3, splits
+
+
+@pytest.mark.parametrize("n,h,w,c,k", [(2, 8, 8, 64, 32), (3, 7, 9, 32, 64), (1, 5, 5, 128, 96)])
+def test_gemm_stride2_residual(gpu_ext, n, h, w, c, k, engine):
+    """dX = dY @ W^T + (compact stride-2 residual added at even (h, w) only) vs the reference with
+    the residual zero-filled to full resolution."""
+    from fluxmpi_amd.ops.gemm import conv1x1_dgrad, note_filter
+    if engine in (1,):
+        pytest.skip("the stride-2 residual is an LDS-DMA epilogue")
+    torch.manual_seed(5)
+    dy = _nhwc(torch.randn(n, k, h, w, device="cuda").bfloat16())
+    wt = _nhwc((torch.randn(k, c, 1, 1, device="cuda") * 0.1).bfloat16())
+    note_filter(wt)
+    ho, wo = (h + 1) // 2, (w + 1) // 2
+    rc = _nhwc(torch.randn(n, c, ho, wo, device="cuda").bfloat16())
+    dy2 = dy.permute(0, 2, 3, 1).reshape(-1, k)
+    rc2 = rc.permute(0, 2, 3, 1).reshape(-1, c)
+    out = conv1x1_dgrad(dy2, wt.reshape(k, c), residual=rc2, w4d=wt, residual_sub=(h, w))
+    full = torch.zeros(n, c, h, w, device="cuda")
+    full[:, :, ::2, ::2] = rc.float()
+    ref = (dy2.float() @ wt.reshape(k, c).float()).bfloat16().float() + full.permute(0, 2, 3, 1).reshape(-1, c)
+    assert _rel(out, ref) < 1e-2
+    odd = out.view(n, h, w, c)[:, 1::2].float()
+    assert _rel(odd, (dy2.float() @ wt.reshape(k, c).float()).view(n, h, w, c)[:, 1::2]) < 1e-2
+
+
+@pytest.mark.parametrize("closed", [False, True])
+def test_downsample_stride2_compact_grad(gpu_ext, closed, engine):
+    """The stride-2 downsample conv's input gradient: compact hand-off to conv1's dgrad epilogue,
+    or (link already closed) expanded to full resolution — equal to the dense gradient."""
+    from fluxmpi_amd.ops import fused_block as fb
+    if engine not in (2,):
+        pytest.skip("one engine is enough")
+    torch.manual_seed(6)
+    x = _nhwc(torch.randn(4, 64, 14, 14, device="cuda").bfloat16()).requires_grad_()
+    w1 = _nhwc((torch.randn(32, 64, 1, 1, device="cuda") * 0.1).bfloat16()).requires_grad_()
+    wd = _nhwc((torch.randn(128, 64, 1, 1, device="cuda") * 0.1).bfloat16()).requires_grad_()
+    link = fb.SideGradLink()
+    if closed:
+        link.take()
+    a = fb.conv1x1_hybrid(x, w1, link if not closed else None)
+    b = fb.conv1x1_downsample(x, wd, 2, link)
+    g1, g2 = torch.randn_like(a), torch.randn_like(b)
+    # one backward: autograd runs the newer node (the downsample conv) first, which offers
+    ((a.float() * g1.float()).sum() + (b.float() * g2.float()).sum()).backward()
+    xr = x.detach().float().requires_grad_()
+    (F.conv2d(xr, w1.float()) * g1.float()).sum().backward()
+    (F.conv2d(xr, wd.float(), stride=2) * g2.float()).sum().backward()
+    assert link.delivered == (not closed)
+    assert _rel(x.grad, xr.grad) < 2e-2
