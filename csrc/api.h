@@ -104,6 +104,8 @@ void bn_fwd_infer(const void* x, void* y, const void* residual, const float* wei
 // y = relu(max over KxK/S window (pad P) of x*scale+shift), idx = window index (0xFF: max <= 0)
 void bn_relu_maxpool_fwd(const void* x, const float* scale, const float* shift, void* y, uint8_t* idx, int64_t N,
                          int64_t H, int64_t W, int64_t C, int K, int S, int P, int dtype, hipStream_t stream);
+// y[p][0..3] = (x[p][0], x[p][1], x[p][2], 0) for npix 16-bit NHWC pixels (stem channel pad)
+void pad_c3_to_c4(const void* x, void* y, int64_t npix, int dtype, hipStream_t stream);
 // dx[n,h,w,c] = sum of dy over the windows whose idx points at (h,w) (gather; dx fully written)
 void maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, int64_t N, int64_t H, int64_t W, int64_t C, int K,
                  int S, int P, int dtype, hipStream_t stream);

@@ -144,6 +144,10 @@ PYBIND11_MODULE(_C, m) {
                               reinterpret_cast<const float*>(shift), reinterpret_cast<void*>(y),
                               reinterpret_cast<uint8_t*>(idx), N, H, W, C, K, S, P, dtype, reinterpret_cast<hipStream_t>(stream));
         });
+  m.def("pad_c3_to_c4", [](uintptr_t x, uintptr_t y, int64_t npix, int dtype, uintptr_t stream) {
+    pad_c3_to_c4(reinterpret_cast<const void*>(x), reinterpret_cast<void*>(y), npix, dtype,
+                 reinterpret_cast<hipStream_t>(stream));
+  });
   m.def("maxpool_bwd", [](uintptr_t dy, uintptr_t idx, uintptr_t dx, int64_t N, int64_t H, int64_t W, int64_t C,
                           int K, int S, int P, int dtype, uintptr_t stream) {
     maxpool_bwd(reinterpret_cast<const void*>(dy), reinterpret_cast<const uint8_t*>(idx), reinterpret_cast<void*>(dx),

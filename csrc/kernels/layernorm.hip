@@ -33,6 +33,25 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// Forward: a persistent grid (one full round of resident workgroups); each wave walks rows
+// row, row + step, ... with the NEXT row's x (and residual) loads issued before the current
+// row's reductions, and the affine w/b held in registers for the whole kernel (16-byte
+// loads, once). The one-row-per-wave version issued 16 scalar w/b loads per vector after
+// the reductions and had only one row's loads in flight: 141-155 us per ViT-B LayerNorm
+// (50432 x 768 bf16) on MI355X, ~2-3x its HBM time (s48 trace).
+template <typename T, int VPL, bool ADD>
+__device__ __forceinline__ void ln_fwd_load(const T* __restrict__ x, const T* __restrict__ r, int64_t row, int D,
+                                            int lane, int nv, T (&rx)[VPL][8], T (&rr)[VPL][8]) {
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int v = lane + i * 64;
+    if (v < nv) {
+      load8(x + row * D + v * 8, rx[i]);
+      if (ADD) load8(r + row * D + v * 8, rr[i]);
+    }
+  }
+}
+
 template <typename T, bool ADD, int VPL>
 __global__ __launch_bounds__(kThreads) void ln_fwd_kernel(const T* __restrict__ x, const T* __restrict__ r,
                                                           T* __restrict__ h, T* __restrict__ y,
@@ -40,65 +59,88 @@ __global__ __launch_bounds__(kThreads) void ln_fwd_kernel(const T* __restrict__ 
                                                           float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                           int64_t rows, int D, float eps) {
   const int lane = threadIdx.x & 63;
-  const int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6);
-  if (row >= rows) return;
   const int nv = D / 8;
-  const T* xr = x + row * D;
-  float f[VPL][8];
-  float s = 0.f;
+  const float inv_d = 1.f / static_cast<float>(D);
+  float wv[VPL][8], bv[VPL][8];
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
     const int v = lane + i * 64;
-    if (v < nv) {
-      T t[8];
-      load8(xr + v * 8, t);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) f[i][j] = static_cast<float>(t[j]);
-      if (ADD) {
-        load8(r + row * D + v * 8, t);
-        T o[8];
+    for (int j = 0; j < 8; ++j) {
+      wv[i][j] = 1.f;
+      bv[i][j] = 0.f;
+    }
+    if (v < nv) {
+      if (w) {
+        const float4 a0 = *reinterpret_cast<const float4*>(w + v * 8);
+        const float4 a1 = *reinterpret_cast<const float4*>(w + v * 8 + 4);
+        wv[i][0] = a0.x; wv[i][1] = a0.y; wv[i][2] = a0.z; wv[i][3] = a0.w;
+        wv[i][4] = a1.x; wv[i][5] = a1.y; wv[i][6] = a1.z; wv[i][7] = a1.w;
+      }
+      if (b) {
+        const float4 a0 = *reinterpret_cast<const float4*>(b + v * 8);
+        const float4 a1 = *reinterpret_cast<const float4*>(b + v * 8 + 4);
+        bv[i][0] = a0.x; bv[i][1] = a0.y; bv[i][2] = a0.z; bv[i][3] = a0.w;
+        bv[i][4] = a1.x; bv[i][5] = a1.y; bv[i][6] = a1.z; bv[i][7] = a1.w;
+      }
+    }
+  }
+  const int64_t step = static_cast<int64_t>(gridDim.x) * kWaves;
+  int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6);
+  T rx[VPL][8], rr[VPL][8];
+  if (row < rows) ln_fwd_load<T, VPL, ADD>(x, r, row, D, lane, nv, rx, rr);
+  for (; row < rows; row += step) {
+    float f[VPL][8];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int v = lane + i * 64;
+      if (v < nv) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[i][j] = static_cast<float>(rx[i][j]);
+        if (ADD) {
+          T o[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            o[j] = static_cast<T>(f[i][j] + static_cast<float>(rr[i][j]));
+            f[i][j] = static_cast<float>(o[j]);  // normalise exactly the stored (rounded) h
+          }
+          store8(h + row * D + v * 8, o);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += f[i][j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[i][j] = 0.f;
+      }
+    }
+    // next row's loads in flight during this row's reductions and stores
+    if (row + step < rows) ln_fwd_load<T, VPL, ADD>(x, r, row + step, D, lane, nv, rx, rr);
+    const float mean = wave_sum(s) * inv_d;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i)
+      if (lane + i * 64 < nv)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          o[j] = static_cast<T>(f[i][j] + static_cast<float>(t[j]));
-          f[i][j] = static_cast<float>(o[j]);  // normalise exactly the stored (rounded) h
+          const float d = f[i][j] - mean;
+          q = fmaf(d, d, q);
         }
-        store8(h + row * D + v * 8, o);
+    const float rstd = rsqrtf(wave_sum(q) * inv_d + eps);
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int v = lane + i * 64;
+      if (v < nv) {
+        T o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = static_cast<T>(fmaf((f[i][j] - mean) * rstd, wv[i][j], bv[i][j]));
+        store8(y + row * D + v * 8, o);
       }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s += f[i][j];
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[i][j] = 0.f;
     }
-  }
-  const float inv_d = 1.f / static_cast<float>(D);
-  const float mean = wave_sum(s) * inv_d;
-  float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < VPL; ++i)
-    if (lane + i * 64 < nv)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float d = f[i][j] - mean;
-        q = fmaf(d, d, q);
-      }
-  const float rstd = rsqrtf(wave_sum(q) * inv_d + eps);
-#pragma unroll
-  for (int i = 0; i < VPL; ++i) {
-    const int v = lane + i * 64;
-    if (v < nv) {
-      T o[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int c = v * 8 + j;
-        o[j] = static_cast<T>(fmaf((f[i][j] - mean) * rstd, w ? w[c] : 1.f, b ? b[c] : 0.f));
-      }
-      store8(y + row * D + v * 8, o);
+    if (lane == 0) {
+      mean_out[row] = mean;
+      rstd_out[row] = rstd;
     }
-  }
-  if (lane == 0) {
-    mean_out[row] = mean;
-    rstd_out[row] = rstd;
   }
 }
 
@@ -202,8 +244,12 @@ int vpl_for(int64_t D) {
 template <typename T, bool ADD, int VPL>
 void fwd_launch(const void* x, const void* r, void* h, void* y, const float* w, const float* b, float* mean,
                 float* rstd, int64_t rows, int64_t D, float eps, hipStream_t s) {
-  const int64_t blocks = (rows + kWaves - 1) / kWaves;
-  ln_fwd_kernel<T, ADD, VPL><<<(unsigned)blocks, kThreads, 0, s>>>(
+  auto k = ln_fwd_kernel<T, ADD, VPL>;
+  int64_t blocks = resident_blocks(reinterpret_cast<const void*>(k), kThreads, 0);
+  const int64_t need = (rows + kWaves - 1) / kWaves;
+  if (blocks > need) blocks = need;
+  if (blocks < 1) blocks = 1;
+  k<<<(unsigned)blocks, kThreads, 0, s>>>(
       static_cast<const T*>(x), static_cast<const T*>(r), static_cast<T*>(h), static_cast<T*>(y), w, b, mean, rstd,
       rows, static_cast<int>(D), eps);
 }
@@ -243,6 +289,8 @@ void layernorm_fwd(const void* x, const void* residual, void* h, void* y, const 
                    float* rstd, int64_t rows, int64_t D, float eps, int dtype, hipStream_t stream) {
   const int vpl = vpl_for(D);
   const bool add = residual != nullptr;
+  if ((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(b)) % 16 != 0)
+    throw std::runtime_error("fused layernorm: w and b must be 16-byte aligned fp32");
 #define CALL_ADD(V) fwd_launch<TT, true, V>(x, residual, h, y, w, b, mean, rstd, rows, D, eps, stream)
 #define CALL_NOADD(V) fwd_launch<TT, false, V>(x, residual, h, y, w, b, mean, rstd, rows, D, eps, stream)
   switch (dtype) {

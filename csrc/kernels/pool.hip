@@ -165,7 +165,63 @@ PoolGeo make_geo(int64_t N, int64_t H, int64_t W, int64_t C, int K, int S, int P
   return g;
 }
 
+// Stem input channel pad: NHWC [P][3] 16-bit pixels -> [P][4] with a zero 4th channel, in one
+// pass (read 6 B, write 8 B per pixel). A lane moves 8 pixels: three 16-byte loads, four
+// 16-byte stores. (PyTorch's version is a strided fill plus a strided copy: ~80 us for a
+// 256x224x224 batch on MI355X, s47 trace.)
+union Vec48 {
+  uint4 v[3];
+  uint16_t h[24];
+};
+union Vec64 {
+  uint4 v[4];
+  uint16_t h[32];
+};
+
+__global__ __launch_bounds__(kThreads) void pad_c3_to_c4_kernel(const uint16_t* __restrict__ x,
+                                                                uint16_t* __restrict__ y, int64_t npix) {
+  const int64_t groups = npix / 8;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  for (int64_t g = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; g < groups; g += stride) {
+    Vec48 in;
+    const uint4* src = reinterpret_cast<const uint4*>(x + g * 24);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) in.v[i] = src[i];
+    Vec64 out;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      out.h[4 * p] = in.h[3 * p];
+      out.h[4 * p + 1] = in.h[3 * p + 1];
+      out.h[4 * p + 2] = in.h[3 * p + 2];
+      out.h[4 * p + 3] = 0;
+    }
+    uint4* dst = reinterpret_cast<uint4*>(y + g * 32);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dst[i] = out.v[i];
+  }
+  // tail pixels (npix % 8), one per lane of the first workgroup
+  if (blockIdx.x == 0 && threadIdx.x < (npix & 7)) {
+    const int64_t p = groups * 8 + threadIdx.x;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) y[p * 4 + c] = x[p * 3 + c];
+    y[p * 4 + 3] = 0;
+  }
+}
+
 }  // namespace
+
+void pad_c3_to_c4(const void* x, void* y, int64_t npix, int dtype, hipStream_t s) {
+  if (dtype != kBF16 && dtype != kF16) throw std::runtime_error("pad_c3_to_c4: bf16/fp16 only");
+  if ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) % 16 != 0)
+    throw std::runtime_error("pad_c3_to_c4: x and y must be 16-byte aligned");
+  if (npix <= 0) return;
+  int64_t nb = (npix / 8 + kThreads - 1) / kThreads;
+  if (nb < 1) nb = 1;
+  if (nb > 65536) nb = 65536;
+  pad_c3_to_c4_kernel<<<static_cast<unsigned>(nb), kThreads, 0, s>>>(static_cast<const uint16_t*>(x),
+                                                                      static_cast<uint16_t*>(y), npix);
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+}
 
 void bn_relu_maxpool_fwd(const void* x, const float* scale, const float* shift, void* y, uint8_t* idx, int64_t N,
                          int64_t H, int64_t W, int64_t C, int K, int S, int P, int dtype, hipStream_t s) {

@@ -44,6 +44,34 @@ class Conv1x1(nn.Module):
         return y.view(n, h, w, -1).permute(0, 3, 1, 2)
 
 
+class _GlobalAvgPool(torch.autograd.Function):
+    """``x.mean((2, 3))`` whose backward writes the broadcast ``dy / (H*W)`` straight into a
+    gradient with x's memory format (one write pass). ``adaptive_avg_pool2d``'s backward on
+    a channels_last input is an NCHW expand + divide + layout copy: ~100 us per ResNet-50
+    step on MI355X (s47 trace) for a 51 MB gradient."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.shape = x.shape
+        ctx.cl = x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous()
+        return x.mean((2, 3))
+
+    @staticmethod
+    def backward(ctx, dy):
+        n, c, h, w = ctx.shape
+        g = (dy / (h * w)).to(dy.dtype)
+        if ctx.cl:
+            out = torch.empty((n, h, w, c), device=dy.device, dtype=dy.dtype)
+            out.copy_(g[:, None, None, :].expand(n, h, w, c))
+            return out.permute(0, 3, 1, 2)
+        return g[:, :, None, None].expand(n, c, h, w).contiguous()
+
+
+def global_avg_pool(x):
+    """``flatten(adaptive_avg_pool2d(x, 1), 1)`` with a single-pass backward."""
+    return _GlobalAvgPool.apply(x)
+
+
 def conv1x1(cin, cout, stride=1, impl="gemm"):
     if impl == "gemm":
         return Conv1x1(cin, cout, stride)
@@ -203,17 +231,23 @@ class ResNet(nn.Module):
         """7x7/2 stem. On the GPU the 3 input channels are zero-padded to 4 (image and
         filter; same math, and the filter's gradient is the slice of the padded one):
         MIOpen's NHWC kernels for C=4 run the forward 1.3x and the weight gradient 1.4x
-        faster than for C=3 on MI355X (scripts/bench_stem.py), for one 50 us pad copy."""
+        faster than for C=3 on MI355X (scripts/bench_stem.py), for one ~30 us pad pass."""
         w = self.conv1.weight
         if not (x.is_cuda and x.dim() == 4 and x.shape[1] == 3 and w.shape[1] == 3
                 and self.conv_impl in ("hybrid", "fused")):
             return self.conv1(x)
-        n, _, h, wd = x.shape
-        x4 = torch.empty(n, h, wd, 4, device=x.device, dtype=x.dtype)
-        x4[..., 3] = 0
-        x4[..., :3] = x.permute(0, 2, 3, 1)
         w4 = F.pad(w, (0, 0, 0, 0, 0, 1)).contiguous(memory_format=torch.channels_last)
-        return F.conv2d(x4.permute(0, 3, 1, 2), w4, None, self.conv1.stride, self.conv1.padding)
+        if (not x.requires_grad and x.dtype in (torch.bfloat16, torch.float16)
+                and x.permute(0, 2, 3, 1).is_contiguous() and x.data_ptr() % 16 == 0):
+            from ..ops.pool import pad_c3_to_c4
+            x4 = pad_c3_to_c4(x)  # one HIP pass (6 B read, 8 B written per pixel)
+        else:
+            n, _, h, wd = x.shape
+            x4 = torch.empty(n, h, wd, 4, device=x.device, dtype=x.dtype)
+            x4[..., 3] = 0
+            x4[..., :3] = x.permute(0, 2, 3, 1)
+            x4 = x4.permute(0, 3, 1, 2)
+        return F.conv2d(x4, w4, None, self.conv1.stride, self.conv1.padding)
 
     def _make(self, width, blocks, stride):
         down = None
@@ -239,8 +273,7 @@ class ResNet(nn.Module):
         else:
             x = self.maxpool(F.relu(self.bn1(self.conv1(x))))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
-        x = torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
-        return self.fc(x)
+        return self.fc(global_avg_pool(x))
 
 
 def resnet50(num_classes=1000, **kw) -> ResNet:

@@ -5,8 +5,9 @@
 head: 86.6 M parameters in 152 tensors — large gradient buckets, which is the
 point of this config for the DDP layer (bucketing + backward/comm overlap).
 
-Attention uses ``F.scaled_dot_product_attention`` (the flash-attention
-kernels PyTorch-ROCm ships for gfx950); the patch embedding is a GEMM on the
+Attention runs the flash-attention kernels PyTorch-ROCm ships for gfx950 (AOTriton)
+on the packed QKV projection, with the three input gradients written straight into one
+packed gradient (``packed_attention``); the patch embedding is a GEMM on the
 unfolded patches; LayerNorms are the fused HIP kernels with the residual adds
 folded in (``fluxmpi_amd.ops.layernorm``).
 """
@@ -31,6 +32,51 @@ class PatchEmbed(nn.Module):
         return self.proj(x)
 
 
+class _PackedAttention(torch.autograd.Function):
+    """Multi-head self-attention on the packed QKV projection ``[B, T, 3*D]`` (AOTriton flash
+    kernels), returning ``[B, T, D]``; the backward writes dQ/dK/dV straight back into one
+    packed ``[B, T, 3, H, Dh]`` gradient with a single interleaving copy. Through autograd,
+    ``view(..).permute(2, 0, 3, 1, 4)`` + SDPA backward stacks the three gradients head-major
+    and then copies them back to the projection layout: 271 + 151 us per ViT-B block per step
+    on MI355X (s48 trace), ~5 ms of a 61 ms step."""
+
+    @staticmethod
+    def forward(ctx, qkv, heads):
+        b, t, d3 = qkv.shape
+        d = d3 // 3
+        q, k, v = qkv.view(b, t, 3, heads, d // heads).unbind(2)
+        q, k, v = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
+        out, lse, cq, ck, mq, mk, seed, off, _ = torch.ops.aten._scaled_dot_product_flash_attention(q, k, v, 0.0, False)
+        ctx.save_for_backward(qkv, out, lse, cq, ck, seed, off)
+        ctx.meta = (heads, mq, mk)
+        return out.transpose(1, 2).reshape(b, t, d)
+
+    @staticmethod
+    def backward(ctx, dy):
+        qkv, out, lse, cq, ck, seed, off = ctx.saved_tensors
+        heads, mq, mk = ctx.meta
+        b, t, d3 = qkv.shape
+        d = d3 // 3
+        dh = d // heads
+        q, k, v = (u.transpose(1, 2) for u in qkv.view(b, t, 3, heads, dh).unbind(2))
+        dout = dy.reshape(b, t, heads, dh).transpose(1, 2)
+        dq, dk, dv = torch.ops.aten._scaled_dot_product_flash_attention_backward(
+            dout, q, k, v, out, lse, cq, ck, mq, mk, 0.0, False, seed, off)
+        dqkv = torch.empty((b, t, 3, heads, dh), device=qkv.device, dtype=qkv.dtype)
+        torch.stack([dq.transpose(1, 2), dk.transpose(1, 2), dv.transpose(1, 2)], dim=2, out=dqkv)
+        return dqkv.view(b, t, d3), None
+
+
+def packed_attention(qkv: torch.Tensor, heads: int) -> torch.Tensor:
+    """``[B, T, 3*D]`` packed q|k|v -> ``[B, T, D]`` softmax attention (no mask, no dropout)."""
+    b, t, d3 = qkv.shape
+    d = d3 // 3
+    if qkv.is_cuda and qkv.dtype in (torch.bfloat16, torch.float16) and (d // heads) % 8 == 0 and (d // heads) <= 256:
+        return _PackedAttention.apply(qkv, heads)
+    q, k, v = qkv.view(b, t, 3, heads, d // heads).permute(2, 0, 3, 1, 4)
+    return F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(b, t, d)
+
+
 class Block(nn.Module):
     """Pre-LN transformer block. ``forward(x, m)`` takes the residual stream ``x`` and the
     previous block's pending MLP output ``m`` and returns ``(x + m + attn, mlp)``: each
@@ -49,15 +95,13 @@ class Block(nn.Module):
         self.fc2 = nn.Linear(mlp, dim)
 
     def forward(self, x, m=None):
-        b, t, d = x.shape
         h = self.heads
         if m is None:
             y = self.ln1(x)
         else:
             x, y = self.ln1.add_forward(x, m)  # x <- x + m (previous block's MLP branch)
-        q, k, v = self.qkv(y).view(b, t, 3, h, d // h).permute(2, 0, 3, 1, 4)
-        a = F.scaled_dot_product_attention(q, k, v)
-        x, y = self.ln2.add_forward(x, self.proj(a.transpose(1, 2).reshape(b, t, d)))
+        a = packed_attention(self.qkv(y), h)
+        x, y = self.ln2.add_forward(x, self.proj(a))
         return x, self.fc2(F.gelu(self.fc1(y)))
 
 

@@ -70,6 +70,19 @@ class _BNReluMaxPool(torch.autograd.Function):
                 None, None, None, None, None, None, None, None)
 
 
+def pad_c3_to_c4(x: torch.Tensor) -> torch.Tensor:
+    """NHWC ``[N, H, W, 3]`` -> ``[N, H, W, 4]`` with a zero 4th channel (16-bit dtypes), one HIP
+    pass (``csrc/kernels/pool.hip``); returned as the NCHW-shaped channels_last view."""
+    C = _ext.get(required=True)
+    n, c, h, w = x.shape
+    xp = x.permute(0, 2, 3, 1)
+    if c != 3 or not xp.is_contiguous() or x.dtype not in (torch.bfloat16, torch.float16):
+        raise ValueError("pad_c3_to_c4: needs a channels_last bf16/fp16 [N, 3, H, W] tensor")
+    y = torch.empty(n, h, w, 4, device=x.device, dtype=x.dtype)
+    C.pad_c3_to_c4(xp.data_ptr(), y.data_ptr(), n * h * w, DTYPE_CODE[x.dtype], _stream(x))
+    return y.permute(0, 3, 1, 2)
+
+
 def supported(x: torch.Tensor) -> bool:
     return (x.is_cuda and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float16, torch.float32)
             and x.shape[1] % 8 == 0 and 8 <= x.shape[1] <= 2048)
@@ -92,4 +105,4 @@ def bn_relu_maxpool(x: torch.Tensor, bn, k: int = 3, s: int = 2, p: int = 1) -> 
     return _BNReluMaxPool.apply(x, bn.weight, bn.bias, rm, rv, mom, bn.eps, k, s, p, nbt)
 
 
-__all__ = ["bn_relu_maxpool"]
+__all__ = ["bn_relu_maxpool", "pad_c3_to_c4"]

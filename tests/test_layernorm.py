@@ -18,7 +18,7 @@ def test_add_layer_norm_cpu_fallback():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape", [(4, 197, 768), (3, 5, 64), (2, 7, 1032), (2, 3, 4096)])
+@pytest.mark.parametrize("shape", [(4, 197, 768), (3, 5, 64), (2, 7, 1032), (2, 3, 4096), (64, 197, 768)])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("add", [False, True])
 def test_layer_norm_vs_reference(gpu_ext, shape, dtype, add):
