@@ -1,0 +1,314 @@
+// Softmax attention backward for short sequences (ViT: T = 197, head dim 64) — gfx950.
+//
+// Why a kernel of our own: PyTorch-ROCm's flash backward (AOTriton bwd_kernel_dk_dv +
+// bwd_kernel_dq + bwd_preprocess) takes ~740 us per ViT-B/16 block at batch 256 on MI355X
+// (s49 trace, profiles/r1_vit_b16_s49.md) — ~4x its forward, far from the ~75 MB x 5 of
+// operand traffic, and its three gradients still have to be interleaved into the packed QKV
+// gradient by a separate copy (another ~170 us per block).
+//
+// Here the whole key (or query) range of one (batch, head) is swept by one workgroup in
+// 32-row chunks staged through LDS, and each gradient is written straight into its slot of
+// the packed [B, T, 3, H, 64] gradient:
+//
+//   attn_bwd_dq  one workgroup = (b, h, 64 queries), 4 waves x 16 queries.  Works in the
+//                transposed orientation S^T[key, q] = K . Q^T so that every product sums
+//                over an accumulator ROW index (the MFMA C/D layout keeps rows in registers):
+//                pass 1: row statistics lse = ln sum exp(S/sqrt(d)) (online, per lane) and
+//                        D = rowsum(dO * O);
+//                pass 2: dS^T = P^T * (dO V^T - D)^T, dQ^T += K^T . dS^T (K^T from LDS).
+//                Writes lse and D to a small fp32 side buffer for the second kernel.
+//   attn_bwd_dkv one workgroup = (b, h, 64 keys), 4 waves x 16 keys, dK^T / dV^T held in
+//                accumulators while the workgroup sweeps all queries:
+//                S = Q K^T, P = exp(S/sqrt(d) - lse), dP = dO V^T, dS = P (dP - D),
+//                dV^T += dO^T P, dK^T += Q^T dS  (dO^T, Q^T from transposed LDS images).
+//
+// MFMA: v_mfma_f32_16x16x32_bf16 (A[row l&15][k = 8(l>>4)+j], B[k = 8(l>>4)+j][col l&15],
+// C[row 4(l>>4)+r][col l&15]). An accumulator pair (rows 0-15, 16-31 of a 32-row chunk) is
+// reused as the next B operand with k-slot j of lane group g <-> row 4g+j (j<4) and
+// 16+4g+j-4 (j>=4); the A operand reads the same rows from a transposed LDS image as two
+// 8-byte pieces.  1-D grid with an XCD-aware order (the blocks of one (b, h) share an L2).
+#include <cmath>
+#include <stdexcept>
+
+#include "../api.h"
+#include "common.h"
+
+namespace fluxmpi {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int DH = 64;      // head dim
+constexpr int CH = 32;      // rows per staged chunk
+constexpr int LN = DH + 8;  // padded row (elements) of a [CH][DH] LDS image (144 B)
+constexpr int LT = CH + 4;  // padded row of a transposed [DH][CH] image (72 B)
+constexpr float kInf = __builtin_huge_valf();
+
+struct AttnBwdArgs {
+  const bf16* q;
+  const bf16* k;
+  const bf16* v;
+  const bf16* o;
+  const bf16* dout;
+  bf16* dq;
+  bf16* dk;
+  bf16* dv;
+  float* stats;              // [B][H][T][2] = (lse, D)
+  int64_t sq_b, sq_t;        // q/k/v/dq/dk/dv strides (head stride DH)
+  int64_t so_b, so_t, so_h;  // o strides
+  int64_t sg_b, sg_t;        // dout strides (head stride DH)
+  int B, T, H, nblk;
+  float scale;
+};
+
+__device__ __forceinline__ bf16x8 ld8(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+
+__device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// A operand from a transposed [DH][CH] image: row m, k-slots {4g..4g+3, 16+4g..16+4g+3}
+__device__ __forceinline__ bf16x8 ld_tr(const bf16* img, int m, int g) {
+  const bf16* p = img + m * LT;
+  const bf16x4 lo = *reinterpret_cast<const bf16x4*>(p + 4 * g);
+  const bf16x4 hi = *reinterpret_cast<const bf16x4*>(p + 16 + 4 * g);
+  return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+// B operand from an accumulator pair (rows 0-15 in a, 16-31 in b)
+__device__ __forceinline__ bf16x8 pack(f32x4 a, f32x4 b) {
+  return bf16x8{(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3], (bf16)b[0], (bf16)b[1], (bf16)b[2], (bf16)b[3]};
+}
+
+// (b, h, row block) of this workgroup; consecutive ids of one XCD take consecutive blocks
+__device__ __forceinline__ void block_coords(const AttnBwdArgs& a, int& b, int& h, int& blk) {
+  const int total = a.B * a.H * a.nblk;
+  int id = blockIdx.x;
+  if ((total & 7) == 0) id = (id & 7) * (total >> 3) + (id >> 3);
+  blk = id % a.nblk;
+  const int bh = id / a.nblk;
+  h = bh % a.H;
+  b = bh / a.H;
+}
+
+// Stage rows [r0, r0+CH) of a [T][DH] operand (row stride st): row-major image (if img) and
+// transposed image (if tr); rows >= T are zero. 256 threads, one 16-byte piece each.
+__device__ __forceinline__ void stage(const bf16* base, int64_t st, int r0, int T, bf16* img, bf16* tr) {
+  const int t = threadIdx.x, r = t >> 3, d0 = (t & 7) * 8;
+  bf16x8 x = {};
+  if (r0 + r < T) x = ld8(base + static_cast<int64_t>(r0 + r) * st + d0);
+  if (img) *reinterpret_cast<bf16x8*>(img + r * LN + d0) = x;
+  if (tr) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) tr[(d0 + j) * LT + r] = x[j];
+  }
+}
+
+__device__ __forceinline__ float merge_factor(float m, float mn) { return m == -kInf ? 0.f : __expf(m - mn); }
+
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16 sK[CH * LN];
+  __shared__ __attribute__((aligned(16))) bf16 sV[CH * LN];
+  __shared__ __attribute__((aligned(16))) bf16 sKt[DH * LT];
+  int b, h, blk;
+  block_coords(a, b, h, blk);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, col = lane & 15, g = lane >> 4;
+  const int qi = blk * 64 + w * 16 + col;
+  const bool qok = qi < a.T;
+  const int64_t qoff = b * a.sq_b + static_cast<int64_t>(qi) * a.sq_t + h * DH;
+  const bf16* kbase = a.k + b * a.sq_b + h * DH;
+  const bf16* vbase = a.v + b * a.sq_b + h * DH;
+  bf16x8 qf[2] = {}, gf[2] = {};
+  float dsum = 0.f;
+  if (qok) {
+    qf[0] = ld8(a.q + qoff + 8 * g);
+    qf[1] = ld8(a.q + qoff + 32 + 8 * g);
+    const bf16* gp = a.dout + b * a.sg_b + static_cast<int64_t>(qi) * a.sg_t + h * DH;
+    gf[0] = ld8(gp + 8 * g);
+    gf[1] = ld8(gp + 32 + 8 * g);
+    const bf16* op = a.o + b * a.so_b + static_cast<int64_t>(qi) * a.so_t + h * a.so_h;
+    const bf16x8 o0 = ld8(op + 8 * g), o1 = ld8(op + 32 + 8 * g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dsum += (float)gf[0][j] * (float)o0[j] + (float)gf[1][j] * (float)o1[j];
+  }
+  dsum += __shfl_xor(dsum, 16);
+  dsum += __shfl_xor(dsum, 32);
+
+  // pass 1: lse of this lane's query column (online over the keys of lane group g)
+  const int nch = (a.T + CH - 1) / CH;
+  float m = -kInf, l = 0.f;
+  for (int c = 0; c < nch; ++c) {
+    __syncthreads();
+    stage(kbase, a.sq_t, c * CH, a.T, sK, nullptr);
+    __syncthreads();
+    float x[8];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      const bf16* kp = sK + (kt * 16 + col) * LN + 8 * g;
+      f32x4 s = {};
+      s = mfma(ld8(kp), qf[0], s);
+      s = mfma(ld8(kp + 32), qf[1], s);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) x[kt * 4 + r] = (c * CH + kt * 16 + 4 * g + r < a.T) ? s[r] * a.scale : -kInf;
+    }
+    float mx = m;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mx = fmaxf(mx, x[j]);
+    if (mx != -kInf) {
+      l *= merge_factor(m, mx);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) l += __expf(x[j] - mx);
+      m = mx;
+    }
+  }
+#pragma unroll
+  for (int off = 16; off <= 32; off <<= 1) {
+    const float m2 = __shfl_xor(m, off), l2 = __shfl_xor(l, off);
+    const float mn = fmaxf(m, m2);
+    if (mn != -kInf) l = l * merge_factor(m, mn) + l2 * merge_factor(m2, mn);
+    m = mn;
+  }
+  const float lse = m + __logf(l);
+  if (qok && g == 0) {
+    float* st = a.stats + ((static_cast<int64_t>(b) * a.H + h) * a.T + qi) * 2;
+    st[0] = lse;
+    st[1] = dsum;
+  }
+
+  // pass 2: dQ^T[d, q] = sum over keys of K^T[d, key] dS^T[key, q]
+  f32x4 acc[4] = {};
+  for (int c = 0; c < nch; ++c) {
+    __syncthreads();
+    stage(kbase, a.sq_t, c * CH, a.T, sK, sKt);
+    stage(vbase, a.sq_t, c * CH, a.T, sV, nullptr);
+    __syncthreads();
+    f32x4 ds[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      const bf16* kp = sK + (kt * 16 + col) * LN + 8 * g;
+      const bf16* vp = sV + (kt * 16 + col) * LN + 8 * g;
+      f32x4 s = {}, dp = {};
+      s = mfma(ld8(kp), qf[0], s);
+      s = mfma(ld8(kp + 32), qf[1], s);
+      dp = mfma(ld8(vp), gf[0], dp);
+      dp = mfma(ld8(vp + 32), gf[1], dp);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = (c * CH + kt * 16 + 4 * g + r < a.T) ? __expf(s[r] * a.scale - lse) : 0.f;
+        ds[kt][r] = p * (dp[r] - dsum);
+      }
+    }
+    const bf16x8 bop = pack(ds[0], ds[1]);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma(ld_tr(sKt, dt * 16 + col, g), bop, acc[dt]);
+  }
+  if (qok) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const bf16x4 o = {(bf16)(acc[dt][0] * a.scale), (bf16)(acc[dt][1] * a.scale), (bf16)(acc[dt][2] * a.scale),
+                        (bf16)(acc[dt][3] * a.scale)};
+      *reinterpret_cast<bf16x4*>(a.dq + qoff + dt * 16 + 4 * g) = o;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16 sQ[CH * LN];
+  __shared__ __attribute__((aligned(16))) bf16 sG[CH * LN];
+  __shared__ __attribute__((aligned(16))) bf16 sQt[DH * LT];
+  __shared__ __attribute__((aligned(16))) bf16 sGt[DH * LT];
+  __shared__ float sL[CH], sD[CH];
+  int b, h, blk;
+  block_coords(a, b, h, blk);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, col = lane & 15, g = lane >> 4;
+  const int ki = blk * 64 + w * 16 + col;
+  const bool kok = ki < a.T;
+  const int64_t koff = b * a.sq_b + static_cast<int64_t>(ki) * a.sq_t + h * DH;
+  bf16x8 kf[2] = {}, vf[2] = {};
+  if (kok) {
+    kf[0] = ld8(a.k + koff + 8 * g);
+    kf[1] = ld8(a.k + koff + 32 + 8 * g);
+    vf[0] = ld8(a.v + koff + 8 * g);
+    vf[1] = ld8(a.v + koff + 32 + 8 * g);
+  }
+  const bf16* qbase = a.q + b * a.sq_b + h * DH;
+  const bf16* gbase = a.dout + b * a.sg_b + h * DH;
+  const float* st = a.stats + (static_cast<int64_t>(b) * a.H + h) * a.T * 2;
+  const int nch = (a.T + CH - 1) / CH;
+  f32x4 accK[4] = {}, accV[4] = {};
+  for (int c = 0; c < nch; ++c) {
+    __syncthreads();
+    stage(qbase, a.sq_t, c * CH, a.T, sQ, sQt);
+    stage(gbase, a.sg_t, c * CH, a.T, sG, sGt);
+    if (threadIdx.x < CH) {
+      const int qq = c * CH + threadIdx.x;
+      sL[threadIdx.x] = qq < a.T ? st[2 * qq] : kInf;
+      sD[threadIdx.x] = qq < a.T ? st[2 * qq + 1] : 0.f;
+    }
+    __syncthreads();
+    f32x4 p[2], ds[2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const bf16* qp = sQ + (qt * 16 + col) * LN + 8 * g;
+      const bf16* gp = sG + (qt * 16 + col) * LN + 8 * g;
+      f32x4 s = {}, dp = {};
+      s = mfma(ld8(qp), kf[0], s);
+      s = mfma(ld8(qp + 32), kf[1], s);
+      dp = mfma(ld8(gp), vf[0], dp);
+      dp = mfma(ld8(gp + 32), vf[1], dp);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qq = qt * 16 + 4 * g + r;
+        const float pv = __expf(s[r] * a.scale - sL[qq]);
+        p[qt][r] = pv;
+        ds[qt][r] = pv * (dp[r] - sD[qq]);
+      }
+    }
+    const bf16x8 pb = pack(p[0], p[1]), db = pack(ds[0], ds[1]);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      accV[dt] = mfma(ld_tr(sGt, dt * 16 + col, g), pb, accV[dt]);
+      accK[dt] = mfma(ld_tr(sQt, dt * 16 + col, g), db, accK[dt]);
+    }
+  }
+  if (kok) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const bf16x4 v = {(bf16)accV[dt][0], (bf16)accV[dt][1], (bf16)accV[dt][2], (bf16)accV[dt][3]};
+      const bf16x4 k = {(bf16)(accK[dt][0] * a.scale), (bf16)(accK[dt][1] * a.scale),
+                        (bf16)(accK[dt][2] * a.scale), (bf16)(accK[dt][3] * a.scale)};
+      *reinterpret_cast<bf16x4*>(a.dv + koff + dt * 16 + 4 * g) = v;
+      *reinterpret_cast<bf16x4*>(a.dk + koff + dt * 16 + 4 * g) = k;
+    }
+  }
+}
+
+bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+}  // namespace
+
+void attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, void* dq, void* dk,
+              void* dv, float* stats, int64_t sq_b, int64_t sq_t, int64_t so_b, int64_t so_t, int64_t so_h,
+              int64_t sg_b, int64_t sg_t, int B, int T, int H, int Dh, float scale, hipStream_t s) {
+  if (Dh != DH) throw std::runtime_error("attn_bwd: head dim must be 64");
+  if (B <= 0 || T <= 0 || H <= 0) throw std::runtime_error("attn_bwd: empty problem");
+  for (const void* p : {q, k, v, o, dout, static_cast<const void*>(dq), static_cast<const void*>(dk),
+                        static_cast<const void*>(dv)})
+    if (!al16(p)) throw std::runtime_error("attn_bwd: operands must be 16-byte aligned");
+  for (int64_t st : {sq_b, sq_t, so_b, so_t, so_h, sg_b, sg_t})
+    if (st % 8 != 0) throw std::runtime_error("attn_bwd: strides must be multiples of 8 elements");
+  AttnBwdArgs a{static_cast<const bf16*>(q), static_cast<const bf16*>(k), static_cast<const bf16*>(v),
+                static_cast<const bf16*>(o), static_cast<const bf16*>(dout), static_cast<bf16*>(dq),
+                static_cast<bf16*>(dk), static_cast<bf16*>(dv), stats, sq_b, sq_t, so_b, so_t, so_h, sg_b, sg_t,
+                B, T, H, (T + 63) / 64, scale};
+  const int64_t total = static_cast<int64_t>(B) * H * a.nblk;
+  if (total > 0x7fffffff) throw std::runtime_error("attn_bwd: grid too large");
+  attn_bwd_dq_kernel<<<static_cast<unsigned>(total), 256, 0, s>>>(a);
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+  attn_bwd_dkv_kernel<<<static_cast<unsigned>(total), 256, 0, s>>>(a);
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace fluxmpi

@@ -32,10 +32,21 @@ class PatchEmbed(nn.Module):
         return self.proj(x)
 
 
+def _attn_native(qkv, heads) -> bool:
+    """Our HIP attention backward (``csrc/kernels/attention.hip``) for bf16, head dim 64;
+    ``FLUXMPI_ATTN_BWD=aten`` selects PyTorch's flash backward instead (A/B runs)."""
+    import os
+    if os.environ.get("FLUXMPI_ATTN_BWD", "native") == "aten":
+        return False
+    from ..ops.attention import supported
+    return supported(qkv, heads)
+
+
 class _PackedAttention(torch.autograd.Function):
     """Multi-head self-attention on the packed QKV projection ``[B, T, 3*D]`` (AOTriton flash
-    kernels), returning ``[B, T, D]``; the backward writes dQ/dK/dV straight back into one
-    packed ``[B, T, 3, H, Dh]`` gradient with a single interleaving copy. Through autograd,
+    kernels), returning ``[B, T, D]``; the backward writes dQ/dK/dV straight into one packed
+    ``[B, T, 3, H, Dh]`` gradient — with our HIP kernels for bf16 / head dim 64
+    (``fluxmpi_amd.ops.attention``), else AOTriton's backward + one interleaving copy. Through autograd,
     ``view(..).permute(2, 0, 3, 1, 4)`` + SDPA backward stacks the three gradients head-major
     and then copies them back to the projection layout: 271 + 151 us per ViT-B block per step
     on MI355X (s48 trace), ~5 ms of a 61 ms step."""
@@ -59,6 +70,9 @@ class _PackedAttention(torch.autograd.Function):
         d = d3 // 3
         dh = d // heads
         q, k, v = (u.transpose(1, 2) for u in qkv.view(b, t, 3, heads, dh).unbind(2))
+        if _attn_native(qkv, heads):
+            from ..ops.attention import attn_bwd_packed
+            return attn_bwd_packed(qkv, out, dy, heads), None
         dout = dy.reshape(b, t, heads, dh).transpose(1, 2)
         dq, dk, dv = torch.ops.aten._scaled_dot_product_flash_attention_backward(
             dout, q, k, v, out, lse, cq, ck, mq, mk, 0.0, False, seed, off)
