@@ -106,9 +106,12 @@ void bn_relu_maxpool_fwd(const void* x, const float* scale, const float* shift, 
                          int64_t H, int64_t W, int64_t C, int K, int S, int P, int dtype, hipStream_t stream);
 // y[p][0..3] = (x[p][0], x[p][1], x[p][2], 0) for npix 16-bit NHWC pixels (stem channel pad)
 void pad_c3_to_c4(const void* x, void* y, int64_t npix, int dtype, hipStream_t stream);
-// Softmax attention backward, head dim 64, bf16 (csrc/kernels/attention.hip). q/k/v and dq/dk/dv
-// share strides (sq_b, sq_t; head stride 64), o has (so_b, so_t, so_h), dout (sg_b, sg_t; head
-// stride 64); stats is fp32 scratch [B][H][T][2] (lse, rowsum(dO*O)) written by the kernel.
+// Softmax attention, head dim 64, bf16 (csrc/kernels/attention.hip). q/k/v and dq/dk/dv share
+// strides (sq_b, sq_t; head stride 64), o has (so_b, so_t, so_h), dout (sg_b, sg_t; head stride
+// 64); stats is fp32 [B][H][T][2]: attn_fwd writes [..][0] = base-2 log-sum-exp of the scaled
+// scores, attn_bwd reads it and writes [..][1] = rowsum(dO*O).
+void attn_fwd(const void* q, const void* k, const void* v, void* o, float* stats, int64_t sq_b, int64_t sq_t,
+              int64_t so_b, int64_t so_t, int64_t so_h, int B, int T, int H, int Dh, float scale, hipStream_t stream);
 void attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, void* dq, void* dk,
               void* dv, float* stats, int64_t sq_b, int64_t sq_t, int64_t so_b, int64_t so_t, int64_t so_h,
               int64_t sg_b, int64_t sg_t, int B, int T, int H, int Dh, float scale, hipStream_t stream);

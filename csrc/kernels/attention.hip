@@ -1,26 +1,32 @@
-// Softmax attention backward for short sequences (ViT: T = 197, head dim 64) — gfx950.
+// Softmax attention (forward + backward) for short sequences (ViT: T = 197, head dim 64) — gfx950.
 //
-// Why a kernel of our own: PyTorch-ROCm's flash backward (AOTriton bwd_kernel_dk_dv +
+// Why kernels of our own: PyTorch-ROCm's flash backward (AOTriton bwd_kernel_dk_dv +
 // bwd_kernel_dq + bwd_preprocess) takes ~740 us per ViT-B/16 block at batch 256 on MI355X
 // (s49 trace, profiles/r1_vit_b16_s49.md) — ~4x its forward, far from the ~75 MB x 5 of
-// operand traffic, and its three gradients still have to be interleaved into the packed QKV
-// gradient by a separate copy (another ~170 us per block).
+// operand traffic — and its forward output / three gradients need layout copies to and from
+// the packed QKV projection (another ~170 us per block).
 //
 // Here the whole key (or query) range of one (batch, head) is swept by one workgroup in
-// 32-row chunks staged through LDS, and each gradient is written straight into its slot of
-// the packed [B, T, 3, H, 64] gradient:
+// 32-row chunks staged through LDS (the next chunk's global loads in flight during the
+// current one), the output is written in the [B, T, H, 64] layout the projection GEMM reads,
+// and each gradient straight into its slot of the packed [B, T, 3, H, 64] gradient:
 //
-//   attn_bwd_dq  one workgroup = (b, h, 64 queries), 4 waves x 16 queries.  Works in the
-//                transposed orientation S^T[key, q] = K . Q^T so that every product sums
-//                over an accumulator ROW index (the MFMA C/D layout keeps rows in registers):
-//                pass 1: row statistics lse = ln sum exp(S/sqrt(d)) (online, per lane) and
-//                        D = rowsum(dO * O);
-//                pass 2: dS^T = P^T * (dO V^T - D)^T, dQ^T += K^T . dS^T (K^T from LDS).
-//                Writes lse and D to a small fp32 side buffer for the second kernel.
+//   attn_fwd     one workgroup = (b, h, 64 queries), 4 waves x 16 queries, transposed
+//                orientation S^T[key, q] = K . Q^T: each lane owns ONE query column, so the
+//                online-softmax rescale of its O^T accumulators is a per-lane scalar;
+//                O^T += V^T . P^T (V^T from a transposed LDS image). Writes O and the row
+//                log-sum-exp (base 2, of the scaled scores) to an fp32 side buffer.
+//   attn_bwd_dq  same decomposition: D = rowsum(dO * O) (written for the next kernel),
+//                dS^T = P^T * (dO V^T - D)^T, dQ^T += K^T . dS^T.
 //   attn_bwd_dkv one workgroup = (b, h, 64 keys), 4 waves x 16 keys, dK^T / dV^T held in
 //                accumulators while the workgroup sweeps all queries:
-//                S = Q K^T, P = exp(S/sqrt(d) - lse), dP = dO V^T, dS = P (dP - D),
+//                S = Q K^T, P = exp2(S c - lse2), dP = dO V^T, dS = P (dP - D),
 //                dV^T += dO^T P, dK^T += Q^T dS  (dO^T, Q^T from transposed LDS images).
+//
+// Masking of rows >= T: staged rows past the end are zero, so a padded key contributes
+// nothing to O, dQ (its K^T / V^T columns are zero) or anything stored; only the softmax
+// denominator of the forward needs an explicit mask, in the last chunk. Padded queries get
+// lse = +inf in the dK/dV sweep (P = 0).
 //
 // MFMA: v_mfma_f32_16x16x32_bf16 (A[row l&15][k = 8(l>>4)+j], B[k = 8(l>>4)+j][col l&15],
 // C[row 4(l>>4)+r][col l&15]). An accumulator pair (rows 0-15, 16-31 of a 32-row chunk) is
@@ -45,6 +51,7 @@ constexpr int CH = 32;      // rows per staged chunk
 constexpr int LN = DH + 8;  // padded row (elements) of a [CH][DH] LDS image (144 B)
 constexpr int LT = CH + 4;  // padded row of a transposed [DH][CH] image (72 B)
 constexpr float kInf = __builtin_huge_valf();
+constexpr float kLog2e = 1.4426950408889634f;
 
 struct AttnBwdArgs {
   const bf16* q;
@@ -52,10 +59,11 @@ struct AttnBwdArgs {
   const bf16* v;
   const bf16* o;
   const bf16* dout;
+  bf16* o_out;  // forward output (same strides as o)
   bf16* dq;
   bf16* dk;
   bf16* dv;
-  float* stats;              // [B][H][T][2] = (lse, D)
+  float* stats;              // [B][H][T][2] = (lse2 from attn_fwd, D)
   int64_t sq_b, sq_t;        // q/k/v/dq/dk/dv strides (head stride DH)
   int64_t so_b, so_t, so_h;  // o strides
   int64_t sg_b, sg_t;        // dout strides (head stride DH)
@@ -93,12 +101,21 @@ __device__ __forceinline__ void block_coords(const AttnBwdArgs& a, int& b, int& 
   b = bh / a.H;
 }
 
-// Stage rows [r0, r0+CH) of a [T][DH] operand (row stride st): row-major image (if img) and
-// transposed image (if tr); rows >= T are zero. 256 threads, one 16-byte piece each.
-__device__ __forceinline__ void stage(const bf16* base, int64_t st, int r0, int T, bf16* img, bf16* tr) {
-  const int t = threadIdx.x, r = t >> 3, d0 = (t & 7) * 8;
+// Staging of rows [r0, r0+CH) of a [T][DH] operand (row stride st), split into a global fetch
+// into registers (issued one chunk ahead, so its latency hides behind the current chunk's
+// MFMAs) and an LDS write: row-major image (if img) and transposed image (if tr); rows >= T
+// are zero. 256 threads, one 16-byte piece each: thread t takes row t & 31, columns
+// 8 (t >> 5) .. +7, so a wave's transposed 2-byte writes for one column cover 16 consecutive
+// dwords per 32-lane half and the two halves land 16 banks apart.
+__device__ __forceinline__ bf16x8 fetch(const bf16* base, int64_t st, int r0, int T) {
+  const int r = threadIdx.x & 31, d0 = (threadIdx.x >> 5) * 8;
   bf16x8 x = {};
   if (r0 + r < T) x = ld8(base + static_cast<int64_t>(r0 + r) * st + d0);
+  return x;
+}
+
+__device__ __forceinline__ void put(bf16x8 x, bf16* img, bf16* tr) {
+  const int r = threadIdx.x & 31, d0 = (threadIdx.x >> 5) * 8;
   if (img) *reinterpret_cast<bf16x8*>(img + r * LN + d0) = x;
   if (tr) {
 #pragma unroll
@@ -106,7 +123,88 @@ __device__ __forceinline__ void stage(const bf16* base, int64_t st, int r0, int 
   }
 }
 
-__device__ __forceinline__ float merge_factor(float m, float mn) { return m == -kInf ? 0.f : __expf(m - mn); }
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnBwdArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16 sK[CH * LN];
+  __shared__ __attribute__((aligned(16))) bf16 sVt[DH * LT];
+  int b, h, blk;
+  block_coords(a, b, h, blk);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, col = lane & 15, g = lane >> 4;
+  const int qi = blk * 64 + w * 16 + col;
+  const bool qok = qi < a.T;
+  const int64_t qoff = b * a.sq_b + static_cast<int64_t>(qi) * a.sq_t + h * DH;
+  const bf16* kbase = a.k + b * a.sq_b + h * DH;
+  const bf16* vbase = a.v + b * a.sq_b + h * DH;
+  bf16x8 qf[2] = {};
+  if (qok) {
+    qf[0] = ld8(a.q + qoff + 8 * g);
+    qf[1] = ld8(a.q + qoff + 32 + 8 * g);
+  }
+  const int nch = (a.T + CH - 1) / CH;
+  const float c2 = a.scale * kLog2e;
+  float m = -kInf, l = 0.f;  // running max (uniform over the 4 lane groups of a column), partial sum
+  f32x4 acc[4] = {};
+  bf16x8 kx = fetch(kbase, a.sq_t, 0, a.T), vx = fetch(vbase, a.sq_t, 0, a.T);
+  for (int c = 0; c < nch; ++c) {
+    __syncthreads();
+    put(kx, sK, nullptr);
+    put(vx, nullptr, sVt);
+    __syncthreads();
+    if (c + 1 < nch) {
+      kx = fetch(kbase, a.sq_t, (c + 1) * CH, a.T);
+      vx = fetch(vbase, a.sq_t, (c + 1) * CH, a.T);
+    }
+    f32x4 x[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      const bf16* kp = sK + (kt * 16 + col) * LN + 8 * g;
+      f32x4 s = {};
+      s = mfma(ld8(kp), qf[0], s);
+      s = mfma(ld8(kp + 32), qf[1], s);
+      x[kt] = s * c2;
+    }
+    if ((c + 1) * CH > a.T) {  // last, partial chunk: padded keys leave the denominator
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (c * CH + kt * 16 + 4 * g + r >= a.T) x[kt][r] = -kInf;
+    }
+    float mx = fmaxf(fmaxf(fmaxf(x[0][0], x[0][1]), fmaxf(x[0][2], x[0][3])),
+                     fmaxf(fmaxf(x[1][0], x[1][1]), fmaxf(x[1][2], x[1][3])));
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float mn = fmaxf(m, mx);  // finite from the first chunk on (key 0 is real)
+    const float f = exp2f(m - mn);
+    m = mn;
+    l *= f;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) acc[dt] *= f;
+    f32x4 p[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        p[kt][r] = exp2f(x[kt][r] - m);
+        l += p[kt][r];
+      }
+    const bf16x8 bop = pack(p[0], p[1]);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma(ld_tr(sVt, dt * 16 + col, g), bop, acc[dt]);
+  }
+  l += __shfl_xor(l, 16);
+  l += __shfl_xor(l, 32);
+  if (qok) {
+    const float inv = 1.f / l;
+    bf16* op = a.o_out + b * a.so_b + static_cast<int64_t>(qi) * a.so_t + h * a.so_h;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const bf16x4 o = {(bf16)(acc[dt][0] * inv), (bf16)(acc[dt][1] * inv), (bf16)(acc[dt][2] * inv),
+                        (bf16)(acc[dt][3] * inv)};
+      *reinterpret_cast<bf16x4*>(op + dt * 16 + 4 * g) = o;
+    }
+    if (g == 0) a.stats[((static_cast<int64_t>(b) * a.H + h) * a.T + qi) * 2] = m + __log2f(l);
+  }
+}
 
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 sK[CH * LN];
@@ -136,54 +234,26 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
   dsum += __shfl_xor(dsum, 16);
   dsum += __shfl_xor(dsum, 32);
 
-  // pass 1: lse of this lane's query column (online over the keys of lane group g)
   const int nch = (a.T + CH - 1) / CH;
-  float m = -kInf, l = 0.f;
-  for (int c = 0; c < nch; ++c) {
-    __syncthreads();
-    stage(kbase, a.sq_t, c * CH, a.T, sK, nullptr);
-    __syncthreads();
-    float x[8];
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      const bf16* kp = sK + (kt * 16 + col) * LN + 8 * g;
-      f32x4 s = {};
-      s = mfma(ld8(kp), qf[0], s);
-      s = mfma(ld8(kp + 32), qf[1], s);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) x[kt * 4 + r] = (c * CH + kt * 16 + 4 * g + r < a.T) ? s[r] * a.scale : -kInf;
-    }
-    float mx = m;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) mx = fmaxf(mx, x[j]);
-    if (mx != -kInf) {
-      l *= merge_factor(m, mx);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) l += __expf(x[j] - mx);
-      m = mx;
-    }
-  }
-#pragma unroll
-  for (int off = 16; off <= 32; off <<= 1) {
-    const float m2 = __shfl_xor(m, off), l2 = __shfl_xor(l, off);
-    const float mn = fmaxf(m, m2);
-    if (mn != -kInf) l = l * merge_factor(m, mn) + l2 * merge_factor(m2, mn);
-    m = mn;
-  }
-  const float lse = m + __logf(l);
-  if (qok && g == 0) {
-    float* st = a.stats + ((static_cast<int64_t>(b) * a.H + h) * a.T + qi) * 2;
-    st[0] = lse;
-    st[1] = dsum;
-  }
+  const float c2 = a.scale * kLog2e;
+  float* st = a.stats + ((static_cast<int64_t>(b) * a.H + h) * a.T + (qok ? qi : 0)) * 2;
+  const float lse = qok ? st[0] : 0.f;
+  if (qok && g == 0) st[1] = dsum;
+  bf16x8 kx;
 
   // pass 2: dQ^T[d, q] = sum over keys of K^T[d, key] dS^T[key, q]
   f32x4 acc[4] = {};
+  kx = fetch(kbase, a.sq_t, 0, a.T);
+  bf16x8 vx = fetch(vbase, a.sq_t, 0, a.T);
   for (int c = 0; c < nch; ++c) {
     __syncthreads();
-    stage(kbase, a.sq_t, c * CH, a.T, sK, sKt);
-    stage(vbase, a.sq_t, c * CH, a.T, sV, nullptr);
+    put(kx, sK, sKt);
+    put(vx, sV, nullptr);
     __syncthreads();
+    if (c + 1 < nch) {
+      kx = fetch(kbase, a.sq_t, (c + 1) * CH, a.T);
+      vx = fetch(vbase, a.sq_t, (c + 1) * CH, a.T);
+    }
     f32x4 ds[2];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
@@ -195,10 +265,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
       dp = mfma(ld8(vp), gf[0], dp);
       dp = mfma(ld8(vp + 32), gf[1], dp);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = (c * CH + kt * 16 + 4 * g + r < a.T) ? __expf(s[r] * a.scale - lse) : 0.f;
-        ds[kt][r] = p * (dp[r] - dsum);
-      }
+      for (int r = 0; r < 4; ++r) ds[kt][r] = exp2f(fmaf(s[r], c2, -lse)) * (dp[r] - dsum);
     }
     const bf16x8 bop = pack(ds[0], ds[1]);
 #pragma unroll
@@ -237,17 +304,34 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
   const bf16* gbase = a.dout + b * a.sg_b + h * DH;
   const float* st = a.stats + (static_cast<int64_t>(b) * a.H + h) * a.T * 2;
   const int nch = (a.T + CH - 1) / CH;
+  const float c2 = a.scale * kLog2e;
   f32x4 accK[4] = {}, accV[4] = {};
+  auto fetch_stats = [&](int c, float& lv, float& dv) {
+    const int qq = c * CH + static_cast<int>(threadIdx.x);
+    lv = kInf;
+    dv = 0.f;
+    if (threadIdx.x < CH && qq < a.T) {
+      lv = st[2 * qq];
+      dv = st[2 * qq + 1];
+    }
+  };
+  bf16x8 qx = fetch(qbase, a.sq_t, 0, a.T), gx = fetch(gbase, a.sg_t, 0, a.T);
+  float lx, dx;
+  fetch_stats(0, lx, dx);
   for (int c = 0; c < nch; ++c) {
     __syncthreads();
-    stage(qbase, a.sq_t, c * CH, a.T, sQ, sQt);
-    stage(gbase, a.sg_t, c * CH, a.T, sG, sGt);
+    put(qx, sQ, sQt);
+    put(gx, sG, sGt);
     if (threadIdx.x < CH) {
-      const int qq = c * CH + threadIdx.x;
-      sL[threadIdx.x] = qq < a.T ? st[2 * qq] : kInf;
-      sD[threadIdx.x] = qq < a.T ? st[2 * qq + 1] : 0.f;
+      sL[threadIdx.x] = lx;
+      sD[threadIdx.x] = dx;
     }
     __syncthreads();
+    if (c + 1 < nch) {
+      qx = fetch(qbase, a.sq_t, (c + 1) * CH, a.T);
+      gx = fetch(gbase, a.sg_t, (c + 1) * CH, a.T);
+      fetch_stats(c + 1, lx, dx);
+    }
     f32x4 p[2], ds[2];
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
@@ -261,7 +345,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int qq = qt * 16 + 4 * g + r;
-        const float pv = __expf(s[r] * a.scale - sL[qq]);
+        const float pv = exp2f(fmaf(s[r], c2, -sL[qq]));
         p[qt][r] = pv;
         ds[qt][r] = pv * (dp[r] - sD[qq]);
       }
@@ -300,7 +384,7 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* o, const 
   for (int64_t st : {sq_b, sq_t, so_b, so_t, so_h, sg_b, sg_t})
     if (st % 8 != 0) throw std::runtime_error("attn_bwd: strides must be multiples of 8 elements");
   AttnBwdArgs a{static_cast<const bf16*>(q), static_cast<const bf16*>(k), static_cast<const bf16*>(v),
-                static_cast<const bf16*>(o), static_cast<const bf16*>(dout), static_cast<bf16*>(dq),
+                static_cast<const bf16*>(o), static_cast<const bf16*>(dout), nullptr, static_cast<bf16*>(dq),
                 static_cast<bf16*>(dk), static_cast<bf16*>(dv), stats, sq_b, sq_t, so_b, so_t, so_h, sg_b, sg_t,
                 B, T, H, (T + 63) / 64, scale};
   const int64_t total = static_cast<int64_t>(B) * H * a.nblk;
@@ -308,6 +392,36 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* o, const 
   attn_bwd_dq_kernel<<<static_cast<unsigned>(total), 256, 0, s>>>(a);
   FLUXMPI_HIP_CHECK(hipGetLastError());
   attn_bwd_dkv_kernel<<<static_cast<unsigned>(total), 256, 0, s>>>(a);
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+}
+
+void attn_fwd(const void* q, const void* k, const void* v, void* o, float* stats, int64_t sq_b, int64_t sq_t,
+              int64_t so_b, int64_t so_t, int64_t so_h, int B, int T, int H, int Dh, float scale, hipStream_t s) {
+  if (Dh != DH) throw std::runtime_error("attn_fwd: head dim must be 64");
+  if (B <= 0 || T <= 0 || H <= 0) throw std::runtime_error("attn_fwd: empty problem");
+  for (const void* p : {q, k, v, static_cast<const void*>(o)})
+    if (!al16(p)) throw std::runtime_error("attn_fwd: operands must be 16-byte aligned");
+  for (int64_t st : {sq_b, sq_t, so_b, so_t, so_h})
+    if (st % 8 != 0) throw std::runtime_error("attn_fwd: strides must be multiples of 8 elements");
+  AttnBwdArgs a{};
+  a.q = static_cast<const bf16*>(q);
+  a.k = static_cast<const bf16*>(k);
+  a.v = static_cast<const bf16*>(v);
+  a.o_out = static_cast<bf16*>(o);
+  a.stats = stats;
+  a.sq_b = sq_b;
+  a.sq_t = sq_t;
+  a.so_b = so_b;
+  a.so_t = so_t;
+  a.so_h = so_h;
+  a.B = B;
+  a.T = T;
+  a.H = H;
+  a.nblk = (T + 63) / 64;
+  a.scale = scale;
+  const int64_t total = static_cast<int64_t>(B) * H * a.nblk;
+  if (total > 0x7fffffff) throw std::runtime_error("attn_fwd: grid too large");
+  attn_fwd_kernel<<<static_cast<unsigned>(total), 256, 0, s>>>(a);
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
 

@@ -5,9 +5,9 @@
 head: 86.6 M parameters in 152 tensors — large gradient buckets, which is the
 point of this config for the DDP layer (bucketing + backward/comm overlap).
 
-Attention runs the flash-attention kernels PyTorch-ROCm ships for gfx950 (AOTriton)
-on the packed QKV projection, with the three input gradients written straight into one
-packed gradient (``packed_attention``); the patch embedding is a GEMM on the
+Attention runs our HIP kernels (``csrc/kernels/attention.hip``: MFMA, whole key range per
+workgroup) on the packed QKV projection, output written in the projection's layout and the
+three input gradients straight into one packed gradient (``packed_attention``); the patch embedding is a GEMM on the
 unfolded patches; LayerNorms are the fused HIP kernels with the residual adds
 folded in (``fluxmpi_amd.ops.layernorm``).
 """
@@ -33,46 +33,53 @@ class PatchEmbed(nn.Module):
 
 
 def _attn_native(qkv, heads) -> bool:
-    """Our HIP attention backward (``csrc/kernels/attention.hip``) for bf16, head dim 64;
-    ``FLUXMPI_ATTN_BWD=aten`` selects PyTorch's flash backward instead (A/B runs)."""
+    """Our HIP attention kernels (``csrc/kernels/attention.hip``) for bf16, head dim 64;
+    ``FLUXMPI_ATTN=aten`` selects PyTorch's flash kernels (AOTriton) instead (A/B runs)."""
     import os
-    if os.environ.get("FLUXMPI_ATTN_BWD", "native") == "aten":
+    if os.environ.get("FLUXMPI_ATTN", "native") == "aten":
         return False
     from ..ops.attention import supported
     return supported(qkv, heads)
 
 
 class _PackedAttention(torch.autograd.Function):
-    """Multi-head self-attention on the packed QKV projection ``[B, T, 3*D]`` (AOTriton flash
-    kernels), returning ``[B, T, D]``; the backward writes dQ/dK/dV straight into one packed
-    ``[B, T, 3, H, Dh]`` gradient — with our HIP kernels for bf16 / head dim 64
-    (``fluxmpi_amd.ops.attention``), else AOTriton's backward + one interleaving copy. Through autograd,
-    ``view(..).permute(2, 0, 3, 1, 4)`` + SDPA backward stacks the three gradients head-major
-    and then copies them back to the projection layout: 271 + 151 us per ViT-B block per step
-    on MI355X (s48 trace), ~5 ms of a 61 ms step."""
+    """Multi-head self-attention on the packed QKV projection ``[B, T, 3*D]``, returning
+    ``[B, T, D]``. bf16 with head dim 64 runs our HIP kernels (``fluxmpi_amd.ops.attention``):
+    the output is written in the projection's layout and the backward writes dQ/dK/dV straight
+    into one packed gradient. Otherwise AOTriton's flash kernels + one interleaving copy.
+    Through plain autograd, ``view(..).permute(2, 0, 3, 1, 4)`` + SDPA backward stacks the three
+    gradients head-major and copies them back to the projection layout: 271 + 151 us per ViT-B
+    block per step on MI355X (s48 trace); AOTriton's backward alone is ~740 us per block (s49)."""
 
     @staticmethod
     def forward(ctx, qkv, heads):
         b, t, d3 = qkv.shape
         d = d3 // 3
+        if _attn_native(qkv, heads):
+            from ..ops.attention import attn_fwd_packed
+            out, stats = attn_fwd_packed(qkv, heads)
+            ctx.save_for_backward(qkv, out, stats)
+            ctx.meta = (heads, True)
+            return out
         q, k, v = qkv.view(b, t, 3, heads, d // heads).unbind(2)
         q, k, v = q.transpose(1, 2), k.transpose(1, 2), v.transpose(1, 2)
         out, lse, cq, ck, mq, mk, seed, off, _ = torch.ops.aten._scaled_dot_product_flash_attention(q, k, v, 0.0, False)
         ctx.save_for_backward(qkv, out, lse, cq, ck, seed, off)
-        ctx.meta = (heads, mq, mk)
+        ctx.meta = (heads, False, mq, mk)
         return out.transpose(1, 2).reshape(b, t, d)
 
     @staticmethod
     def backward(ctx, dy):
+        if ctx.meta[1]:
+            from ..ops.attention import attn_bwd_packed
+            qkv, out, stats = ctx.saved_tensors
+            return attn_bwd_packed(qkv, out, dy, ctx.meta[0], stats), None
         qkv, out, lse, cq, ck, seed, off = ctx.saved_tensors
-        heads, mq, mk = ctx.meta
+        heads, _, mq, mk = ctx.meta
         b, t, d3 = qkv.shape
         d = d3 // 3
         dh = d // heads
         q, k, v = (u.transpose(1, 2) for u in qkv.view(b, t, 3, heads, dh).unbind(2))
-        if _attn_native(qkv, heads):
-            from ..ops.attention import attn_bwd_packed
-            return attn_bwd_packed(qkv, out, dy, heads), None
         dout = dy.reshape(b, t, heads, dh).transpose(1, 2)
         dq, dk, dv = torch.ops.aten._scaled_dot_product_flash_attention_backward(
             dout, q, k, v, out, lse, cq, ck, mq, mk, 0.0, False, seed, off)

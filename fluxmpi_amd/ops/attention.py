@@ -1,15 +1,14 @@
-"""Packed-QKV softmax attention backward on our gfx950 kernels (``csrc/kernels/attention.hip``).
+"""Packed-QKV softmax attention on our gfx950 kernels (``csrc/kernels/attention.hip``).
 
-``attn_bwd_packed(qkv, out, dy, heads)`` returns the gradient of ``[B, T, 3*D]`` packed
-q|k|v for ``out = softmax(q k^T / sqrt(64)) v`` (no mask, no dropout), written straight into
-one ``[B, T, 3, H, 64]`` buffer: no per-gradient tensors, no interleaving copy.
-``out`` is the forward's ``[B, H, T, 64]`` (any strides with a contiguous head dim);
-``dy`` the ``[B, T, D]`` output gradient. The softmax statistics are recomputed from q and
-k, so the forward's log-sum-exp is not needed.
+``attn_fwd_packed(qkv, heads) -> (out, stats)``: ``out = softmax(q k^T / 8) v`` for the
+``[B, T, 3*H*64]`` packed q|k|v projection (no mask, no dropout), written as ``[B, T, H*64]``
+(the layout the output projection reads: no transpose copy), plus fp32 ``stats``
+``[B, H, T, 2]`` holding the row log-sum-exp for the backward.
+
+``attn_bwd_packed(qkv, out, dy, heads, stats)``: the gradient of the packed q|k|v, written
+straight into one ``[B, T, 3, H, 64]`` buffer (no per-gradient tensors, no interleaving copy).
 """
 from __future__ import annotations
-
-import math
 
 import torch
 
@@ -23,29 +22,44 @@ def supported(qkv: torch.Tensor, heads: int) -> bool:
             and qkv.is_contiguous())
 
 
-def attn_bwd_packed(qkv: torch.Tensor, out: torch.Tensor, dy: torch.Tensor, heads: int) -> torch.Tensor:
+def _check(qkv, heads):
+    if not supported(qkv, heads):
+        raise ValueError("attention: needs a contiguous bf16 [B, T, 3*H*64] qkv on the GPU")
+
+
+def attn_fwd_packed(qkv: torch.Tensor, heads: int):
     C = _ext.get(required=True)
+    _check(qkv, heads)
     b, t, d3 = qkv.shape
     d = d3 // 3
-    dh = d // heads
-    if not supported(qkv, heads):
-        raise ValueError("attn_bwd_packed: needs a contiguous bf16 [B, T, 3*H*64] qkv")
-    if out.shape != (b, heads, t, dh) or out.stride(3) != 1 or out.dtype != qkv.dtype:
-        raise ValueError(f"attn_bwd_packed: out must be [B, H, T, {dh}] with a contiguous head dim")
+    out = torch.empty((b, t, d), device=qkv.device, dtype=qkv.dtype)
+    stats = torch.empty((b, heads, t, 2), device=qkv.device, dtype=torch.float32)
+    p, es = qkv.data_ptr(), qkv.element_size()
+    C.attn_fwd(p, p + d * es, p + 2 * d * es, out.data_ptr(), stats.data_ptr(), t * d3, d3, t * d, d, 64,
+               b, t, heads, 64, 0.125, _stream(qkv))
+    return out, stats
+
+
+def attn_bwd_packed(qkv: torch.Tensor, out: torch.Tensor, dy: torch.Tensor, heads: int,
+                    stats: torch.Tensor) -> torch.Tensor:
+    C = _ext.get(required=True)
+    _check(qkv, heads)
+    b, t, d3 = qkv.shape
+    d = d3 // 3
+    if out.shape != (b, t, d) or not out.is_contiguous() or out.dtype != qkv.dtype:
+        raise ValueError("attn_bwd_packed: out must be attn_fwd_packed's contiguous [B, T, H*64]")
+    if stats.shape != (b, heads, t, 2) or stats.dtype != torch.float32 or not stats.is_contiguous():
+        raise ValueError("attn_bwd_packed: stats must be attn_fwd_packed's [B, H, T, 2] fp32")
     dy = dy.reshape(b, t, d)
     if not dy.is_contiguous():
         dy = dy.contiguous()
     if dy.dtype != qkv.dtype:
         dy = dy.to(qkv.dtype)
     dqkv = torch.empty_like(qkv)
-    stats = torch.empty((b, heads, t, 2), device=qkv.device, dtype=torch.float32)
-    p = qkv.data_ptr()
-    g = dqkv.data_ptr()
-    es = qkv.element_size()
+    p, g, es = qkv.data_ptr(), dqkv.data_ptr(), qkv.element_size()
     C.attn_bwd(p, p + d * es, p + 2 * d * es, out.data_ptr(), dy.data_ptr(), g, g + d * es, g + 2 * d * es,
-               stats.data_ptr(), t * d3, d3, out.stride(0), out.stride(2), out.stride(1), t * d, d,
-               b, t, heads, dh, 1.0 / math.sqrt(dh), _stream(qkv))
+               stats.data_ptr(), t * d3, d3, t * d, d, 64, t * d, d, b, t, heads, 64, 0.125, _stream(qkv))
     return dqkv
 
 
-__all__ = ["attn_bwd_packed", "supported"]
+__all__ = ["attn_fwd_packed", "attn_bwd_packed", "supported"]

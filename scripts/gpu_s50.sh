@@ -4,6 +4,6 @@ source "$(dirname "$0")/gpu_lib.sh"
 rm -f "$OUT/steps.log" "$OUT/bench_results.jsonl"
 step pytest_attn 200 0 python -u -m pytest tests/test_attention_gpu.py tests/test_vit_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread
 step bench_vit 300 0 python bench.py --model vit_b16
-FLUXMPI_ATTN_BWD=aten step bench_vit_aten 300 0 python bench.py --model vit_b16
+
 cd /tmp && step prof50 300 0 rocprofv3 --kernel-trace --stats -d "$OUT/prof50" -o run --output-format csv -- python3 "$ROOT/bench.py" --model vit_b16 --steps 5 --warmup 5
 echo done

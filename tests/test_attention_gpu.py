@@ -1,5 +1,7 @@
-"""HIP attention backward (csrc/kernels/attention.hip) vs a plain PyTorch fp32 reference:
-the packed [B, T, 3*D] q|k|v gradient of softmax(q k^T / 8) v, head dim 64."""
+"""HIP attention (csrc/kernels/attention.hip) vs a plain PyTorch fp32 reference: the output of
+softmax(q k^T / 8) v and the packed [B, T, 3*D] q|k|v gradient, head dim 64."""
+import math
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -22,21 +24,37 @@ def test_supported_gate_cpu():
     assert not supported(torch.zeros(1, 4, 3 * 64, dtype=torch.bfloat16), 1)  # CPU tensor
 
 
+SHAPES = [(4, 197, 12), (2, 50, 4), (1, 7, 2), (2, 64, 3), (1, 1, 1), (3, 300, 2), (2, 33, 5)]
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("b,t,heads", [(4, 197, 12), (2, 50, 4), (1, 7, 2), (2, 64, 3), (1, 1, 1), (3, 300, 2),
-                                       (2, 33, 5)])
-def test_attn_bwd_vs_fp32(gpu_ext, b, t, heads):
-    from fluxmpi_amd.ops.attention import attn_bwd_packed
+@pytest.mark.parametrize("b,t,heads", SHAPES)
+def test_attn_fwd_vs_fp32(gpu_ext, b, t, heads):
+    from fluxmpi_amd.ops.attention import attn_fwd_packed
     torch.manual_seed(0)
-    x = torch.randn(b, t, 3 * heads * 64, device="cuda") * 1.5
-    xb = x.to(torch.bfloat16)
+    xb = (torch.randn(b, t, 3 * heads * 64, device="cuda") * 1.5).to(torch.bfloat16)
+    out, stats = attn_fwd_packed(xb, heads)
+    ref = _ref(xb.float(), heads)
+    assert out.shape == ref.shape and out.dtype == torch.bfloat16
+    assert _rel(out, ref) < 1e-2
+    # stats[..., 0]: base-2 log-sum-exp of the scaled scores
+    q, k, _ = xb.float().view(b, t, 3, heads, 64).permute(2, 0, 3, 1, 4)
+    lse2 = torch.logsumexp((q @ k.transpose(-1, -2)) / 8, -1) / math.log(2)
+    torch.testing.assert_close(stats[..., 0], lse2, rtol=1e-3, atol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("b,t,heads", SHAPES)
+def test_attn_bwd_vs_fp32(gpu_ext, b, t, heads):
+    from fluxmpi_amd.ops.attention import attn_bwd_packed, attn_fwd_packed
+    torch.manual_seed(0)
+    xb = (torch.randn(b, t, 3 * heads * 64, device="cuda") * 1.5).to(torch.bfloat16)
     xr = xb.float().requires_grad_()
     yr = _ref(xr, heads)
     g = torch.randn_like(yr)
     yr.backward(g)
-    q, k, v = xb.view(b, t, 3, heads, 64).permute(2, 0, 3, 1, 4)
-    out = F.scaled_dot_product_attention(q, k, v)  # [B, H, T, 64] (forward output, bf16)
-    dqkv = attn_bwd_packed(xb, out, g.to(torch.bfloat16), heads)
+    out, stats = attn_fwd_packed(xb, heads)
+    dqkv = attn_bwd_packed(xb, out, g.to(torch.bfloat16), heads, stats)
     assert dqkv.shape == xb.shape and dqkv.dtype == torch.bfloat16
     assert torch.isfinite(dqkv).all()
     for i in range(3):
@@ -46,33 +64,19 @@ def test_attn_bwd_vs_fp32(gpu_ext, b, t, heads):
 
 
 @pytest.mark.gpu
-def test_attn_bwd_strided_out(gpu_ext):
-    """out in the [B, T, H, 64] memory layout (transposed view), as some forwards return it."""
-    from fluxmpi_amd.ops.attention import attn_bwd_packed
-    torch.manual_seed(1)
-    b, t, heads = 2, 77, 3
-    xb = torch.randn(b, t, 3 * heads * 64, device="cuda").to(torch.bfloat16)
-    xr = xb.float().requires_grad_()
-    yr = _ref(xr, heads)
-    g = torch.randn_like(yr)
-    yr.backward(g)
-    out = yr.detach().to(torch.bfloat16).view(b, t, heads, 64).transpose(1, 2)
-    dqkv = attn_bwd_packed(xb, out, g.to(torch.bfloat16), heads)
-    assert _rel(dqkv, xr.grad) < 2e-2
-
-
-@pytest.mark.gpu
-def test_packed_attention_uses_native_bwd(gpu_ext, monkeypatch):
-    """The ViT attention path runs our backward and agrees with PyTorch's flash backward."""
+def test_packed_attention_native_vs_aten(gpu_ext, monkeypatch):
+    """The ViT attention path runs our kernels and agrees with PyTorch's flash kernels."""
     from fluxmpi_amd.models import vit
     torch.manual_seed(2)
     x = torch.randn(4, 197, 3 * 768, device="cuda").to(torch.bfloat16)
-    grads = {}
+    g = torch.randn(4, 197, 768, device="cuda").to(torch.bfloat16)
+    res = {}
     for mode in ("native", "aten"):
-        monkeypatch.setenv("FLUXMPI_ATTN_BWD", mode)
+        monkeypatch.setenv("FLUXMPI_ATTN", mode)
+        assert vit._attn_native(x, 12) == (mode == "native")
         xa = x.clone().requires_grad_()
         y = vit.packed_attention(xa, 12)
-        y.backward(torch.ones_like(y))
-        grads[mode] = xa.grad
-        assert vit._attn_native(x, 12) == (mode == "native")
-    assert _rel(grads["native"], grads["aten"]) < 2e-2
+        y.backward(g)
+        res[mode] = (y.detach(), xa.grad)
+    assert _rel(res["native"][0], res["aten"][0]) < 1e-2
+    assert _rel(res["native"][1], res["aten"][1]) < 2e-2
