@@ -193,4 +193,17 @@ void transpose_filters(const std::vector<uintptr_t>& src, const std::vector<uint
 // out[e] = sum over s < splits of ws[s*n + e] (mode-3 split-K partials; ws is clobbered); out fp32 or bf16
 void gemm_splitk_reduce(const float* ws, int splits, int64_t n, void* out, int out_dtype, hipStream_t stream);
 
+// ---- Anderson-acceleration solver (DEQ) --------------------------------------------
+// X, F: fp32 histories [bsz][m rows of row_stride][d] (batch_stride between batches).
+// anderson_gram: partials[b][chunk][37]: the upper-triangle pair sums of G G^T (G = F - X over
+// rows < n; pair (i, j>=i) at index i*n - i*(i-1)/2 + (j-i)) and |F[last]|^2 at [36];
+// sum over chunks on the host side. anderson_gram_chunks: the chunk count to allocate for.
+int anderson_gram_chunks(int64_t bsz, int64_t d);
+void anderson_gram(const float* X, const float* F, float* partials, int64_t bsz, int64_t d, int64_t row_stride,
+                   int64_t batch_stride, int n, int last, int chunks, hipStream_t stream);
+// X[b, slot] = beta * sum_i alpha[b][i] F[b, i] + (1 - beta) * sum_i alpha[b][i] X[b, i] (i < n);
+// z (nullable, [bsz][d], dtype z_dtype): the new iterate cast to the model dtype.
+void anderson_mix(float* X, const float* F, const float* alpha, void* z, int z_dtype, int64_t bsz, int64_t d,
+                  int64_t row_stride, int64_t batch_stride, int n, int slot, float beta, hipStream_t stream);
+
 }  // namespace fluxmpi

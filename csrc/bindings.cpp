@@ -170,6 +170,19 @@ PYBIND11_MODULE(_C, m) {
                 N, H, W, C, K, S, P, dtype, reinterpret_cast<hipStream_t>(stream));
   });
 
+  // ---- Anderson solver (DEQ) ---------------------------------------------------
+  m.def("anderson_gram_chunks", &anderson_gram_chunks);
+  m.def("anderson_gram", [](uintptr_t X, uintptr_t F, uintptr_t part, int64_t bsz, int64_t d, int64_t rs, int64_t bs,
+                            int n, int last, int chunks, uintptr_t stream) {
+    anderson_gram(reinterpret_cast<const float*>(X), reinterpret_cast<const float*>(F), reinterpret_cast<float*>(part),
+                  bsz, d, rs, bs, n, last, chunks, S(stream));
+  });
+  m.def("anderson_mix", [](uintptr_t X, uintptr_t F, uintptr_t alpha, uintptr_t z, int zdt, int64_t bsz, int64_t d,
+                           int64_t rs, int64_t bs, int n, int slot, float beta, uintptr_t stream) {
+    anderson_mix(reinterpret_cast<float*>(X), reinterpret_cast<const float*>(F), reinterpret_cast<const float*>(alpha),
+                 reinterpret_cast<void*>(z), zdt, bsz, d, rs, bs, n, slot, beta, S(stream));
+  });
+
   // ---- fused LayerNorm ------------------------------------------------------
   m.def("layernorm_fwd", [](uintptr_t x, uintptr_t res, uintptr_t h, uintptr_t y, uintptr_t w, uintptr_t b,
                             uintptr_t mean, uintptr_t rstd, int64_t rows, int64_t D, float eps, int dtype,

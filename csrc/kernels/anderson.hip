@@ -1,0 +1,213 @@
+// Anderson-acceleration solver kernels for the Deep Equilibrium Model — gfx950.
+//
+// The solver keeps a history of m iterates X[b, i, :] and their images F[b, i, :] (fp32,
+// row length d = C*H*W, e.g. 48*28*28 = 37632) and, every iteration, needs
+//   gram[b]  = G G^T  with G = F[b, :n] - X[b, :n]         (n <= m <= 8 rows)
+//   X[b, s]  = beta * alpha[b] F[b, :n] + (1 - beta) * alpha[b] X[b, :n]
+// PyTorch composes these as a strided subtract (materialising G), a batched fp32 GEMM whose
+// output is n x n (hipBLASLt picks a 256x16 macro tile: ~570 us per call on MI355X for
+// bsz 256, ~0.34 TB/s) and two more batched GEMMs for the mix. Both are HBM-bound
+// streaming reductions, so here:
+//   anderson_gram: one pass over F and X rows (G formed in registers, never stored); each
+//       workgroup owns one (batch, d-chunk), keeps the n(n+1)/2 pair sums plus |F[s]|^2 of
+//       the newest row in registers, reduces them across its 4 waves through LDS and stores
+//       one partial row (no atomics; the host sums the chunk partials).
+//   anderson_mix:  one pass that writes the new iterate and, optionally, its cast copy in
+//       the model dtype (the next f(z) input) — no separate cast kernel.
+// 16-byte (float4) accesses throughout; grids are bsz x chunks >= 2048 workgroups.
+#include <stdexcept>
+#include <string>
+
+#include "../api.h"
+#include "common.h"
+
+namespace fluxmpi {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxRows = 8;
+constexpr int kPairs = kMaxRows * (kMaxRows + 1) / 2;  // 36 upper-triangle pairs
+constexpr int kOut = kPairs + 1;                        // + |F[last]|^2
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__device__ __forceinline__ float dot4(const float4& a, const float4& b) {
+  return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+}
+
+// grid (chunks, bsz). part[b][chunk][kOut]
+template <int N>
+__global__ __launch_bounds__(kThreads) void gram_kernel(const float* __restrict__ X, const float* __restrict__ F,
+                                                        float* __restrict__ part, int64_t d4, int64_t row_stride,
+                                                        int64_t batch_stride, int64_t chunk4, int last) {
+  const int b = blockIdx.y;
+  const int c = blockIdx.x;
+  const float4* xb = reinterpret_cast<const float4*>(X + b * batch_stride);
+  const float4* fb = reinterpret_cast<const float4*>(F + b * batch_stride);
+  const int64_t rs4 = row_stride / 4;
+  float acc[kPairs];
+  float fn = 0.f;
+#pragma unroll
+  for (int p = 0; p < kPairs; ++p) acc[p] = 0.f;
+  const int64_t v0 = static_cast<int64_t>(c) * chunk4;
+  int64_t v1 = v0 + chunk4;
+  if (v1 > d4) v1 = d4;
+  for (int64_t v = v0 + threadIdx.x; v < v1; v += kThreads) {
+    float4 g[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const float4 f = fb[i * rs4 + v];
+      const float4 x = xb[i * rs4 + v];
+      g[i] = make_float4(f.x - x.x, f.y - x.y, f.z - x.z, f.w - x.w);
+      if (i == last) fn += dot4(f, f);
+    }
+    int p = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+      for (int j = i; j < N; ++j) acc[p++] += dot4(g[i], g[j]);
+  }
+  __shared__ float red[kThreads / 64][kOut];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr int kUsed = N * (N + 1) / 2;
+#pragma unroll
+  for (int p = 0; p < kUsed; ++p) {
+    const float s = wave_sum(acc[p]);
+    if (lane == 0) red[wave][p] = s;
+  }
+  {
+    const float s = wave_sum(fn);
+    if (lane == 0) red[wave][kPairs] = s;
+  }
+  __syncthreads();
+  float* out = part + (static_cast<int64_t>(b) * gridDim.x + c) * kOut;
+  for (int p = threadIdx.x; p < kOut; p += kThreads) {
+    if (p < kUsed || p == kPairs) {
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < kThreads / 64; ++w) s += red[w][p];
+      out[p] = s;
+    } else {
+      out[p] = 0.f;
+    }
+  }
+}
+
+// grid (ceil(d4 / kThreads), bsz): X[b, slot] = beta * sum_i a_i F[b,i] + (1-beta) * sum_i a_i X[b,i]
+template <int N, bool MIXX, typename Z>
+__global__ __launch_bounds__(kThreads) void mix_kernel(float* __restrict__ X, const float* __restrict__ F,
+                                                       const float* __restrict__ alpha, Z* __restrict__ z, int64_t d4,
+                                                       int64_t row_stride, int64_t batch_stride, int slot, float beta) {
+  const int b = blockIdx.y;
+  const int64_t v = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  if (v >= d4) return;
+  const int64_t rs4 = row_stride / 4;
+  float4* xb = reinterpret_cast<float4*>(X + b * batch_stride);
+  const float4* fb = reinterpret_cast<const float4*>(F + b * batch_stride);
+  float a[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) a[i] = alpha[b * N + i];
+  float4 sf = make_float4(0.f, 0.f, 0.f, 0.f), sx = sf;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const float4 f = fb[i * rs4 + v];
+    sf.x += a[i] * f.x; sf.y += a[i] * f.y; sf.z += a[i] * f.z; sf.w += a[i] * f.w;
+    if (MIXX) {
+      const float4 x = xb[i * rs4 + v];
+      sx.x += a[i] * x.x; sx.y += a[i] * x.y; sx.z += a[i] * x.z; sx.w += a[i] * x.w;
+    }
+  }
+  float4 o = sf;
+  if (MIXX) {
+    const float c = 1.f - beta;
+    o = make_float4(beta * sf.x + c * sx.x, beta * sf.y + c * sx.y, beta * sf.z + c * sx.z, beta * sf.w + c * sx.w);
+  }
+  xb[slot * rs4 + v] = o;
+  if (z != nullptr) {
+    Z* zp = z + (static_cast<int64_t>(b) * d4 + v) * 4;
+    zp[0] = static_cast<Z>(o.x);
+    zp[1] = static_cast<Z>(o.y);
+    zp[2] = static_cast<Z>(o.z);
+    zp[3] = static_cast<Z>(o.w);
+  }
+}
+
+void check_layout(const void* X, const void* F, int64_t d, int64_t row_stride, int64_t batch_stride, int n) {
+  if (n < 1 || n > kMaxRows) throw std::runtime_error("anderson: need 1 <= n <= 8 (got " + std::to_string(n) + ")");
+  if (d % 4 != 0 || row_stride % 4 != 0 || batch_stride % 4 != 0 || row_stride < d)
+    throw std::runtime_error("anderson: d and strides must be multiples of 4 floats");
+  if (((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(F)) & 15u) != 0)
+    throw std::runtime_error("anderson: X and F must be 16-byte aligned");
+}
+
+}  // namespace
+
+int anderson_gram_chunks(int64_t bsz, int64_t d) {
+  // >= ~2048 workgroups over the batch, >= 4 float4 per lane per chunk
+  const int64_t d4 = d / 4;
+  int64_t chunks = (2048 + bsz - 1) / (bsz > 0 ? bsz : 1);
+  const int64_t max_chunks = (d4 + 4 * kThreads - 1) / (4 * kThreads);
+  if (chunks > max_chunks) chunks = max_chunks;
+  if (chunks < 1) chunks = 1;
+  return static_cast<int>(chunks);
+}
+
+void anderson_gram(const float* X, const float* F, float* partials, int64_t bsz, int64_t d, int64_t row_stride,
+                   int64_t batch_stride, int n, int last, int chunks, hipStream_t stream) {
+  check_layout(X, F, d, row_stride, batch_stride, n);
+  if (last < 0 || last >= n) throw std::runtime_error("anderson_gram: last row out of range");
+  if (bsz > 65535) throw std::runtime_error("anderson_gram: bsz > 65535");
+  const int64_t d4 = d / 4;
+  const int64_t chunk4 = (d4 + chunks - 1) / chunks;
+  dim3 grid(chunks, static_cast<unsigned>(bsz));
+#define GRAM_CASE(NN)                                                                                   \
+  case NN:                                                                                              \
+    gram_kernel<NN><<<grid, kThreads, 0, stream>>>(X, F, partials, d4, row_stride, batch_stride, chunk4, \
+                                                   last);                                               \
+    break;
+  switch (n) {
+    GRAM_CASE(1) GRAM_CASE(2) GRAM_CASE(3) GRAM_CASE(4) GRAM_CASE(5) GRAM_CASE(6) GRAM_CASE(7) GRAM_CASE(8)
+  }
+#undef GRAM_CASE
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+}
+
+template <int N, bool MIXX>
+void mix_launch(float* X, const float* F, const float* alpha, void* z, int zdt, int64_t bsz, int64_t d4,
+                int64_t rs, int64_t bs, int slot, float beta, hipStream_t s) {
+  dim3 grid(static_cast<unsigned>((d4 + kThreads - 1) / kThreads), static_cast<unsigned>(bsz));
+  switch (zdt) {
+    case kBF16: mix_kernel<N, MIXX, bf16><<<grid, kThreads, 0, s>>>(X, F, alpha, static_cast<bf16*>(z), d4, rs, bs, slot, beta); break;
+    case kF16: mix_kernel<N, MIXX, f16><<<grid, kThreads, 0, s>>>(X, F, alpha, static_cast<f16*>(z), d4, rs, bs, slot, beta); break;
+    case kF32: mix_kernel<N, MIXX, float><<<grid, kThreads, 0, s>>>(X, F, alpha, static_cast<float*>(z), d4, rs, bs, slot, beta); break;
+    default: throw std::runtime_error("anderson_mix: unsupported z dtype");
+  }
+}
+
+void anderson_mix(float* X, const float* F, const float* alpha, void* z, int z_dtype, int64_t bsz, int64_t d,
+                  int64_t row_stride, int64_t batch_stride, int n, int slot, float beta, hipStream_t stream) {
+  check_layout(X, F, d, row_stride, batch_stride, n);
+  if (slot < 0 || slot * row_stride + d > batch_stride) throw std::runtime_error("anderson_mix: slot out of range");
+  if (bsz > 65535) throw std::runtime_error("anderson_mix: bsz > 65535");
+  if (z != nullptr && (reinterpret_cast<uintptr_t>(z) & 7u) != 0)
+    throw std::runtime_error("anderson_mix: z must be 8-byte aligned");
+  const int64_t d4 = d / 4;
+  const bool mixx = beta != 1.f;
+  const int zdt = z != nullptr ? z_dtype : kF32;
+#define MIX_CASE(NN)                                                                                 \
+  case NN:                                                                                           \
+    if (mixx) mix_launch<NN, true>(X, F, alpha, z, zdt, bsz, d4, row_stride, batch_stride, slot, beta, stream); \
+    else mix_launch<NN, false>(X, F, alpha, z, zdt, bsz, d4, row_stride, batch_stride, slot, beta, stream);    \
+    break;
+  switch (n) {
+    MIX_CASE(1) MIX_CASE(2) MIX_CASE(3) MIX_CASE(4) MIX_CASE(5) MIX_CASE(6) MIX_CASE(7) MIX_CASE(8)
+  }
+#undef MIX_CASE
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace fluxmpi

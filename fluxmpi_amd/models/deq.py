@@ -20,7 +20,14 @@ import torch.nn.functional as F
 
 
 def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0):
-    """Anderson acceleration for ``x = f(x)`` over batch-flattened tensors. Returns (x, iters, rel_residual)."""
+    """Anderson acceleration for ``x = f(x)`` over batch-flattened tensors. Returns (x, iters, rel_residual).
+
+    The history Gram matrix and the mix run as single-pass HIP kernels on the GPU
+    (``fluxmpi_amd.ops.anderson``). The residual of iterate k is read off the diagonal of
+    the Gram matrix computed at the top of iteration k + 1 (same value, no extra pass).
+    """
+    from ..ops import anderson as AO
+
     bsz = x0.shape[0]
     shape, dt = x0.shape, x0.dtype
     d = x0[0].numel()
@@ -39,18 +46,23 @@ def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0):
     y = torch.zeros(bsz, m + 1, 1, dtype=torch.float32, device=x0.device)
     y[:, 0] = 1
     res = float("inf")
-    k = 1
+    k, converged = 1, False
     for k in range(2, max_iter):
         n = min(k, m)
-        G = Fv[:, :n] - X[:, :n]
-        H[:, 1:n + 1, 1:n + 1] = torch.bmm(G, G.transpose(1, 2)) + lam * torch.eye(n, dtype=torch.float32,
-                                                                                   device=x0.device)[None]
+        last = (k - 1) % m
+        gram, fn2 = AO.gram(X, Fv, n, last)
+        if k > 2:  # residual of the iterate produced by the previous iteration
+            res = float(gram[:, last, last].sum().sqrt() / (1e-5 + fn2.sum().sqrt()))
+            if res < tol:
+                k, converged = k - 1, True
+                break
+        H[:, 1:n + 1, 1:n + 1] = gram + lam * torch.eye(n, dtype=torch.float32, device=x0.device)[None]
         alpha = torch.linalg.solve(H[:, :n + 1, :n + 1], y[:, :n + 1])[:, 1:n + 1, 0]
-        X[:, k % m] = beta * (alpha[:, None] @ Fv[:, :n])[:, 0] + (1 - beta) * (alpha[:, None] @ X[:, :n])[:, 0]
-        Fv[:, k % m] = fx(X[:, k % m])
-        res = float((Fv[:, k % m] - X[:, k % m]).norm() / (1e-5 + Fv[:, k % m].norm()))
-        if res < tol:
-            break
+        z = AO.mix(X, Fv, alpha, k % m, beta, dt)
+        Fv[:, k % m] = fx(z)
+    if not converged:
+        s = k % m
+        res = float((Fv[:, s] - X[:, s]).norm() / (1e-5 + Fv[:, s].norm()))
     return X[:, k % m].reshape(shape).to(dt), k, res
 
 

@@ -1,0 +1,76 @@
+"""Anderson-acceleration solver ops for the DEQ fixed-point solve (``csrc/kernels/anderson.hip``).
+
+The solver history ``X, F`` is ``[bsz, m, d]`` fp32. Every iteration needs the Gram matrix
+``G G^T`` of ``G = F[:, :n] - X[:, :n]`` and the mix ``X[:, s] = beta * alpha F + (1 - beta)
+* alpha X``. On the GPU both are single streaming HIP passes (G formed in registers, the
+new iterate's model-dtype copy written by the mix); CPU tensors use the PyTorch
+composition, which is also the test oracle.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _ext
+from .multi_tensor import DTYPE_CODE
+
+_MAX_ROWS = 8
+
+
+def _stream(t):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _native(X: torch.Tensor, F: torch.Tensor, n: int) -> bool:
+    if not (X.is_cuda and F.is_cuda):
+        return False
+    ok = (X.dtype == F.dtype == torch.float32 and X.dim() == F.dim() == 3 and X.shape == F.shape
+          and X.stride() == F.stride() and X.stride(2) == 1 and X.shape[2] % 4 == 0 and X.stride(1) % 4 == 0
+          and X.stride(0) % 4 == 0 and 1 <= n <= min(_MAX_ROWS, X.shape[1]) and X.shape[0] <= 65535
+          and X.data_ptr() % 16 == 0 and F.data_ptr() % 16 == 0)
+    if not ok:
+        raise ValueError("anderson ops: need fp32 [bsz<=65535, m, d%4==0] histories with matching strides, n<=8")
+    return True
+
+
+def gram(X: torch.Tensor, F: torch.Tensor, n: int, last: int):
+    """``(G G^T [bsz, n, n], |F[:, last]|^2 [bsz])`` with ``G = F[:, :n] - X[:, :n]`` (fp32)."""
+    if not _native(X, F, n):
+        G = F[:, :n] - X[:, :n]
+        return torch.bmm(G, G.transpose(1, 2)), F[:, last].pow(2).sum(1)
+    C = _ext.get(required=True)
+    bsz, _, d = X.shape
+    chunks = C.anderson_gram_chunks(bsz, d)
+    part = torch.empty(bsz, chunks, 37, device=X.device, dtype=torch.float32)
+    C.anderson_gram(X.data_ptr(), F.data_ptr(), part.data_ptr(), bsz, d, X.stride(1), X.stride(0), n, last, chunks,
+                    _stream(X))
+    tot = part.sum(1)
+    iu = torch.triu_indices(n, n, device=X.device)
+    H = X.new_zeros(bsz, n, n)
+    H[:, iu[0], iu[1]] = tot[:, : iu.shape[1]]
+    H[:, iu[1], iu[0]] = tot[:, : iu.shape[1]]
+    return H, tot[:, 36]
+
+
+def mix(X: torch.Tensor, F: torch.Tensor, alpha: torch.Tensor, slot: int, beta: float = 1.0,
+        z_dtype: torch.dtype | None = None):
+    """``X[:, slot] = beta * alpha F[:, :n] + (1 - beta) * alpha X[:, :n]`` in place (n = alpha.shape[1]).
+
+    Returns the new iterate as a ``[bsz, d]`` tensor of ``z_dtype`` (a fresh copy when it is not fp32;
+    the ``X[:, slot]`` view otherwise)."""
+    n = alpha.shape[1]
+    if not _native(X, F, n):
+        new = beta * torch.bmm(alpha[:, None], F[:, :n])[:, 0]
+        if beta != 1.0:
+            new = new + (1 - beta) * torch.bmm(alpha[:, None], X[:, :n])[:, 0]
+        X[:, slot] = new
+        return X[:, slot] if z_dtype in (None, torch.float32) else X[:, slot].to(z_dtype)
+    C = _ext.get(required=True)
+    bsz, _, d = X.shape
+    a = alpha.float().contiguous()
+    z = None
+    if z_dtype not in (None, torch.float32):
+        z = torch.empty(bsz, d, device=X.device, dtype=z_dtype)
+    C.anderson_mix(X.data_ptr(), F.data_ptr(), a.data_ptr(), z.data_ptr() if z is not None else 0,
+                   DTYPE_CODE[z_dtype] if z is not None else 7, bsz, d, X.stride(1), X.stride(0), n, slot, float(beta),
+                   _stream(X))
+    return z if z is not None else X[:, slot]

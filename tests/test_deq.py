@@ -1,0 +1,112 @@
+"""DEQ model + Anderson solver ops (``csrc/kernels/anderson.hip``, ``fluxmpi_amd/ops/anderson.py``).
+
+CPU: the solver converges to the fixed point of a contraction; the implicit-gradient DEQ
+trains end to end. GPU: the HIP Gram / mix kernels against the plain fp32 PyTorch
+composition of the same op.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from fluxmpi_amd.models.deq import anderson, deq_mnist
+from fluxmpi_amd.ops import anderson as AO
+
+
+def _ref_gram(X, Fv, n, last):
+    G = (Fv[:, :n] - X[:, :n]).double()
+    return torch.bmm(G, G.transpose(1, 2)), Fv[:, last].double().pow(2).sum(1)
+
+
+def _ref_mix(X, Fv, alpha, beta):
+    n = alpha.shape[1]
+    a = alpha.double()[:, :, None]
+    return beta * (a * Fv[:, :n].double()).sum(1) + (1 - beta) * (a * X[:, :n].double()).sum(1)
+
+
+def test_anderson_contraction_cpu():
+    torch.manual_seed(0)
+    d = 64
+    A = torch.randn(d, d)
+    A = 0.5 * A / torch.linalg.matrix_norm(A, 2)
+    b = torch.randn(3, d)
+    f = lambda z: z @ A.T + b  # noqa: E731
+    z, k, res = anderson(f, torch.zeros(3, d), max_iter=50, tol=1e-6)
+    exact = torch.linalg.solve(torch.eye(d) - A, b.T).T
+    assert res < 1e-4
+    assert torch.allclose(z, exact, atol=1e-4), (z - exact).abs().max()
+    assert 2 <= k < 50
+
+
+def test_anderson_ops_fallback_cpu():
+    torch.manual_seed(1)
+    X, Fv = torch.randn(4, 5, 32), torch.randn(4, 5, 32)
+    H, fn = AO.gram(X, Fv, 3, 2)
+    Hr, fr = _ref_gram(X, Fv, 3, 2)
+    assert torch.allclose(H.double(), Hr, rtol=1e-5, atol=1e-4) and torch.allclose(fn.double(), fr, rtol=1e-5)
+    alpha = torch.randn(4, 3)
+    want = _ref_mix(X.clone(), Fv, alpha, 0.7)
+    z = AO.mix(X, Fv, alpha, 4, beta=0.7, z_dtype=torch.bfloat16)
+    assert torch.allclose(X[:, 4].double(), want, rtol=1e-5, atol=1e-5)
+    assert z.dtype == torch.bfloat16
+
+
+def test_deq_train_step_cpu():
+    torch.manual_seed(2)
+    model = deq_mnist(max_iter=12, bwd_iter=12)
+    x, y = torch.randn(4, 1, 12, 12), torch.randint(0, 10, (4,))
+    model.head = torch.nn.Linear(48 * 16, 10)
+    loss = F.cross_entropy(model(x), y)
+    loss.backward()
+    assert torch.isfinite(loss)
+    g = model.deq.f.conv1.weight.grad
+    assert g is not None and torch.isfinite(g).all() and g.abs().sum() > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("bsz,d", [(3, 36), (64, 4100), (256, 37632)])
+def test_anderson_gram_gpu(n, bsz, d):
+    torch.manual_seed(n)
+    m = max(n, 5)
+    X = torch.randn(bsz, m, d, device="cuda")
+    Fv = torch.randn(bsz, m, d, device="cuda")
+    last = n - 1
+    H, fn = AO.gram(X, Fv, n, last)
+    Hr, fr = _ref_gram(X, Fv, n, last)
+    torch.testing.assert_close(H.double(), Hr, rtol=1e-4, atol=1e-3 * d ** 0.5)
+    torch.testing.assert_close(fn.double(), fr, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,beta", [(1, 1.0), (3, 1.0), (5, 1.0), (5, 0.8), (8, 0.5)])
+@pytest.mark.parametrize("zdt", [None, torch.bfloat16, torch.float16])
+def test_anderson_mix_gpu(n, beta, zdt):
+    torch.manual_seed(10 + n)
+    bsz, m, d = 37, 8, 4100
+    X = torch.randn(bsz, m, d, device="cuda")
+    Fv = torch.randn(bsz, m, d, device="cuda")
+    alpha = torch.randn(bsz, n, device="cuda")
+    slot = (n + 2) % m
+    keep = X.clone()
+    want = _ref_mix(X, Fv, alpha, beta)
+    z = AO.mix(X, Fv, alpha, slot, beta, zdt)
+    torch.testing.assert_close(X[:, slot].double(), want, rtol=1e-5, atol=1e-4)
+    others = [i for i in range(m) if i != slot]
+    assert torch.equal(X[:, others], keep[:, others])
+    if zdt is not None:
+        assert z.dtype == zdt and z.shape == (bsz, d)
+        torch.testing.assert_close(z.float(), X[:, slot].to(zdt).float())
+
+
+@pytest.mark.gpu
+def test_anderson_solver_gpu_matches_cpu():
+    torch.manual_seed(3)
+    d = 256
+    A = torch.randn(d, d, dtype=torch.float64)
+    A = (0.6 * A / torch.linalg.matrix_norm(A, 2)).float()
+    b = torch.randn(16, d)
+    zc, kc, _ = anderson(lambda z: z @ A.T + b, torch.zeros(16, d), max_iter=40, tol=1e-5)
+    Ag, bg = A.cuda(), b.cuda()
+    zg, kg, rg = anderson(lambda z: z @ Ag.T + bg, torch.zeros(16, d, device="cuda"), max_iter=40, tol=1e-5)
+    assert rg < 1e-5 and abs(kg - kc) <= 2
+    torch.testing.assert_close(zg.cpu(), zc, rtol=1e-4, atol=1e-4)
