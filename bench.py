@@ -42,6 +42,9 @@ def parse():
     ap.add_argument("--conv", default=os.environ.get("BENCH_CONV", "hybrid"), choices=["gemm", "miopen", "fused", "hybrid"])
     ap.add_argument("--norm", default=os.environ.get("BENCH_NORM", "fused"), choices=["torch", "fused"])
     ap.add_argument("--optimizer", default="adam", choices=["adam", "momentum"])
+    ap.add_argument("--memory-format", default=os.environ.get("BENCH_MEMFMT", "auto"),
+                    choices=["auto", "channels_last", "contiguous"],
+                    help="activation layout (auto: the model's `memory_format` attribute, else channels_last)")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--graph", action="store_true", help="capture the step in a HIP graph")
     ap.add_argument("--miopen-find", type=int, default=int(os.environ.get("BENCH_MIOPEN_FIND", "1")))
@@ -88,7 +91,9 @@ def main():
 
     torch.manual_seed(1234 + rank)
     model = build_model(args.model, conv_impl=args.conv, norm=args.norm)
-    model = model.to(dev, memory_format=torch.channels_last)
+    memfmt = {"channels_last": torch.channels_last, "contiguous": torch.contiguous_format}.get(
+        args.memory_format, getattr(model, "memory_format", torch.channels_last))
+    model = model.to(dev, memory_format=memfmt)
     # bf16 compute; BatchNorm affine params + running stats stay fp32
     for m in model.modules():
         is_norm = isinstance(m, torch.nn.modules.batchnorm._BatchNorm) or type(m).__name__ == "FusedBatchNorm2d"
@@ -102,7 +107,7 @@ def main():
     gx = torch.Generator(device=dev).manual_seed(rank)
     cin, ncls = (1, 10) if args.model == "deq" else (3, 1000)  # DEQ: MNIST-shaped (FastDEQ example)
     x = torch.randn(B, cin, args.image, args.image, device=dev, generator=gx).to(torch.bfloat16)
-    x = x.contiguous(memory_format=torch.channels_last)
+    x = x.contiguous(memory_format=memfmt)
     y = torch.randint(0, ncls, (B,), device=dev, generator=gx)
 
     def step():
@@ -151,7 +156,7 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
             "config": {"model": mname, "global_batch": world * B, "per_gpu_batch": B, "seq_len": None,
                        "image_size": args.image, "parallelism": f"dp{world}", "optimizer": args.optimizer,
-                       "conv": args.conv, "norm": args.norm, "backend": FluxMPI.backend_name(),
+                       "conv": args.conv, "norm": args.norm, "memory_format": "contiguous" if memfmt is torch.contiguous_format else "channels_last", "backend": FluxMPI.backend_name(),
                        "overlap": not args.no_overlap, "miopen_find": bool(args.miopen_find), "hip_graph": bool(args.graph), "tunableop": use_tunableop, "loss": round(lval, 4),
                        "exposed_comm_ms": None if exposed is None else round(exposed, 3)},
         }

@@ -206,4 +206,15 @@ void anderson_gram(const float* X, const float* F, float* partials, int64_t bsz,
 void anderson_mix(float* X, const float* F, const float* alpha, void* z, int z_dtype, int64_t bsz, int64_t d,
                   int64_t row_stride, int64_t batch_stride, int n, int slot, float beta, hipStream_t stream);
 
+// ---- fused NHWC GroupNorm (+ add, + ReLU on its input); one workgroup per sample ---------
+// forward: h = [relu](x [+ add]) (stored when h != nullptr); y = GN(h) * w + b (w/b fp32, nullable);
+// mean / rstd [N][G] fp32 saved. backward: dh = d(GN)/dh [* (h > 0) when relu], the gradient of
+// both x and add; partials[N][2][C] = per-sample (dw, db).
+void groupnorm_nhwc_fwd(const void* x, const void* add, void* h, void* y, const float* w, const float* b, float* mean,
+                        float* rstd, int64_t N, int64_t HW, int64_t C, int64_t G, bool relu, float eps, int dtype,
+                        hipStream_t stream);
+void groupnorm_nhwc_bwd(const void* dy, const void* h, const float* mean, const float* rstd, const float* w, void* dh,
+                        float* partials, int64_t N, int64_t HW, int64_t C, int64_t G, bool relu, int dtype,
+                        hipStream_t stream);
+
 }  // namespace fluxmpi

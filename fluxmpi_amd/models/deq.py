@@ -18,6 +18,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.groupnorm import FusedGroupNorm
+
 
 def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0):
     """Anderson acceleration for ``x = f(x)`` over batch-flattened tensors. Returns (x, iters, rel_residual).
@@ -36,10 +38,23 @@ def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0):
     X = torch.zeros(bsz, m, d, dtype=torch.float32, device=x0.device)
     Fv = torch.zeros_like(X)
 
-    def fx(v):
-        return f(v.reshape(shape).to(dt)).reshape(bsz, -1).float()
+    # flatten in MEMORY order: a channels_last iterate stays channels_last through f (views,
+    # no layout copies), which is the layout the fused NHWC GroupNorm kernels take
+    cl = x0.dim() == 4 and x0.is_contiguous(memory_format=torch.channels_last) and not x0.is_contiguous()
 
-    X[:, 0], Fv[:, 0] = x0.reshape(bsz, -1).float(), fx(x0)
+    def flat(t):
+        return (t.permute(0, 2, 3, 1) if cl else t).reshape(bsz, -1)
+
+    def unflat(v):
+        if cl:
+            n_, c_, h_, w_ = shape
+            return v.reshape(n_, h_, w_, c_).permute(0, 3, 1, 2)
+        return v.reshape(shape)
+
+    def fx(v):
+        return flat(f(unflat(v.contiguous()).to(dt))).float()
+
+    X[:, 0], Fv[:, 0] = flat(x0).float(), fx(flat(x0))
     X[:, 1], Fv[:, 1] = Fv[:, 0], fx(Fv[:, 0])
     H = torch.zeros(bsz, m + 1, m + 1, dtype=torch.float32, device=x0.device)
     H[:, 0, 1:] = H[:, 1:, 0] = 1
@@ -63,7 +78,7 @@ def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0):
     if not converged:
         s = k % m
         res = float((Fv[:, s] - X[:, s]).norm() / (1e-5 + Fv[:, s].norm()))
-    return X[:, k % m].reshape(shape).to(dt), k, res
+    return unflat(X[:, k % m].contiguous()).to(dt), k, res
 
 
 class DEQFixedPoint(nn.Module):
@@ -105,13 +120,14 @@ class ResidualCell(nn.Module):
         super().__init__()
         self.conv1 = nn.Conv2d(ch, ch, 3, padding=1, bias=False)
         self.conv2 = nn.Conv2d(ch, ch, 3, padding=1, bias=False)
-        self.n1, self.n2, self.n3 = nn.GroupNorm(groups, ch), nn.GroupNorm(groups, ch), nn.GroupNorm(groups, ch)
+        # FusedGroupNorm: GN(relu(x + add)) in one NHWC pass on the GPU (ops/groupnorm.py)
+        self.n1, self.n2, self.n3 = (FusedGroupNorm(groups, ch) for _ in range(3))
         for c in (self.conv1, self.conv2):
             nn.init.normal_(c.weight, 0, 0.01)
 
     def forward(self, z, x):
-        y = self.n1(F.relu(self.conv1(z)))
-        return self.n3(F.relu(z + self.n2(x + self.conv2(y))))
+        y = self.n1(self.conv1(z), relu=True)
+        return self.n3(z, add=self.n2(self.conv2(y), add=x), relu=True)
 
 
 class DEQClassifier(nn.Module):

@@ -1,0 +1,83 @@
+"""Fused NHWC GroupNorm (+ residual add, + ReLU on its input) (``csrc/kernels/groupnorm.hip``).
+
+``FusedGroupNorm`` is an ``nn.GroupNorm`` (same parameters / state dict) whose
+``forward(x, add=None, relu=False)`` computes ``GN(relu(x + add))``. On channels_last GPU
+tensors one workgroup per sample does statistics and apply (no NCHW layout copies, no
+separate add / ReLU kernels) and the backward writes the gradient of the GroupNorm input
+(times the ReLU mask) once — it is the gradient of both ``x`` and ``add``. Other tensors
+use the PyTorch composition, which is also the test oracle.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _ext
+from .multi_tensor import DTYPE_CODE
+
+
+def _stream(t):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def supported(x: torch.Tensor, groups: int) -> bool:
+    if not (x.is_cuda and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float16, torch.float32)):
+        return False
+    C = x.shape[1]
+    return (C % 8 == 0 and C <= 2048 and C % groups == 0 and groups <= 64 and x.numel() > 0
+            and x.is_contiguous(memory_format=torch.channels_last))
+
+
+class _GroupNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, add, weight, bias, groups, eps, relu):
+        C = _ext.get(required=True)
+        N, Ch, H, W = x.shape
+        if add is not None:
+            add = add.contiguous(memory_format=torch.channels_last)
+        w32 = weight.float().contiguous() if weight is not None else None
+        b32 = bias.float().contiguous() if bias is not None else None
+        y = torch.empty_like(x, memory_format=torch.channels_last)
+        h = torch.empty_like(y) if (add is not None or relu) else None
+        mean = torch.empty(N, groups, device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        C.groupnorm_nhwc_fwd(x.data_ptr(), add.data_ptr() if add is not None else 0, h.data_ptr() if h is not None else 0,
+                             y.data_ptr(), w32.data_ptr() if w32 is not None else 0,
+                             b32.data_ptr() if b32 is not None else 0, mean.data_ptr(), rstd.data_ptr(), N, H * W, Ch,
+                             groups, bool(relu), float(eps), DTYPE_CODE[x.dtype], _stream(x))
+        ctx.save_for_backward(h if h is not None else x, mean, rstd, w32)
+        ctx.cfg = (groups, bool(relu), add is not None,
+                   weight.dtype if weight is not None else None, bias.dtype if bias is not None else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = _ext.get(required=True)
+        h, mean, rstd, w32 = ctx.saved_tensors
+        groups, relu, has_add, wd, bd = ctx.cfg
+        N, Ch, H, W = h.shape
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dh = torch.empty_like(h, memory_format=torch.channels_last)
+        part = torch.empty(N, 2, Ch, device=h.device, dtype=torch.float32)
+        C.groupnorm_nhwc_bwd(dy.data_ptr(), h.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                             w32.data_ptr() if w32 is not None else 0, dh.data_ptr(), part.data_ptr(), N, H * W, Ch,
+                             groups, relu, DTYPE_CODE[h.dtype], _stream(h))
+        dw = part[:, 0].sum(0).to(wd) if wd is not None and ctx.needs_input_grad[2] else None
+        db = part[:, 1].sum(0).to(bd) if bd is not None and ctx.needs_input_grad[3] else None
+        return dh, (dh if has_add else None), dw, db, None, None, None
+
+
+def group_norm(x, groups, weight=None, bias=None, eps=1e-5, add=None, relu=False):
+    """``F.group_norm(relu(x + add), groups, weight, bias, eps)`` with the add / ReLU optional."""
+    if supported(x, groups) and (add is None or (add.shape == x.shape and add.dtype == x.dtype)):
+        return _GroupNormFn.apply(x, add, weight, bias, groups, eps, relu)
+    h = x + add if add is not None else x
+    if relu:
+        h = F.relu(h)
+    return F.group_norm(h, groups, weight, bias, eps)
+
+
+class FusedGroupNorm(nn.GroupNorm):
+    def forward(self, x, add=None, relu=False):  # noqa: D102
+        return group_norm(x, self.num_groups, self.weight, self.bias, self.eps, add, relu)

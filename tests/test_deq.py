@@ -110,3 +110,59 @@ def test_anderson_solver_gpu_matches_cpu():
     zg, kg, rg = anderson(lambda z: z @ Ag.T + bg, torch.zeros(16, d, device="cuda"), max_iter=40, tol=1e-5)
     assert rg < 1e-5 and abs(kg - kc) <= 2
     torch.testing.assert_close(zg.cpu(), zc, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("add,relu", [(False, False), (False, True), (True, False), (True, True)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape,groups", [((4, 48, 28, 28), 8), ((3, 16, 5, 7), 4), ((2, 64, 9, 9), 64)])
+def test_fused_groupnorm_gpu(add, relu, dtype, shape, groups):
+    from fluxmpi_amd.ops.groupnorm import FusedGroupNorm, _GroupNormFn  # noqa: F401
+
+    torch.manual_seed(7)
+    N, C, H, W = shape
+    gn = FusedGroupNorm(groups, C).cuda()
+    with torch.no_grad():
+        gn.weight.normal_(1, 0.3)
+        gn.bias.normal_(0, 0.3)
+    cl = torch.channels_last
+    x = (torch.randn(shape, device="cuda") + 0.3).to(dtype).contiguous(memory_format=cl).requires_grad_()
+    a = torch.randn(shape, device="cuda").to(dtype).contiguous(memory_format=cl).requires_grad_() if add else None
+    y = gn(x, add=a, relu=relu)
+    dy = torch.randn(shape, device="cuda").to(dtype).contiguous(memory_format=cl)
+    y.backward(dy)
+    # fp32 PyTorch reference on the same (rounded) inputs
+    xr = x.detach().float().clone().requires_grad_()
+    ar = a.detach().float().clone().requires_grad_() if add else None
+    wr = gn.weight.detach().clone().requires_grad_()
+    br = gn.bias.detach().clone().requires_grad_()
+    h = xr + ar if add else xr
+    if relu:
+        h = torch.relu(h)
+    h = h.to(dtype).float()  # the kernel normalises the stored (rounded) h
+    yr = torch.nn.functional.group_norm(h, groups, wr, br, gn.eps)
+    yr.backward(dy.float())
+    tol = dict(rtol=2e-2, atol=3e-2) if dtype == torch.bfloat16 else dict(rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(y.float(), yr, **tol)
+    torch.testing.assert_close(x.grad.float(), xr.grad, **tol)
+    if add:
+        torch.testing.assert_close(a.grad.float(), ar.grad, **tol)
+    gtol = dict(rtol=2e-2, atol=2e-2 * N * H * W ** 0.5) if dtype == torch.bfloat16 else dict(rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(gn.weight.grad, wr.grad, **gtol)
+    torch.testing.assert_close(gn.bias.grad, br.grad, **gtol)
+
+
+@pytest.mark.gpu
+def test_deq_cell_fused_path_gpu():
+    """The DEQ cell on channels_last bf16 takes the HIP GroupNorm path and matches the fp32 composition."""
+    from fluxmpi_amd.models.deq import ResidualCell
+
+    torch.manual_seed(8)
+    cell = ResidualCell(48).cuda()
+    z = torch.randn(8, 48, 14, 14, device="cuda").contiguous(memory_format=torch.channels_last)
+    x = torch.randn_like(z)
+    out = cell(z, x)
+    n1, n2, n3 = cell.n1, cell.n2, cell.n3
+    gn = lambda m, t: torch.nn.functional.group_norm(t, m.num_groups, m.weight, m.bias, m.eps)  # noqa: E731
+    ref = gn(n3, torch.relu(z + gn(n2, x + cell.conv2(gn(n1, torch.relu(cell.conv1(z)))))))
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-4)
