@@ -51,10 +51,10 @@ def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0):
             return v.reshape(n_, h_, w_, c_).permute(0, 3, 1, 2)
         return v.reshape(shape)
 
-    def fx(v):
-        return flat(f(unflat(v.contiguous()).to(dt))).float()
+    def fx(v):  # f in the model dtype; the fp32 history slot assignment is the (one) cast
+        return flat(f(unflat(v.contiguous()).to(dt)))
 
-    X[:, 0], Fv[:, 0] = flat(x0).float(), fx(flat(x0))
+    X[:, 0], Fv[:, 0] = flat(x0), fx(flat(x0))
     X[:, 1], Fv[:, 1] = Fv[:, 0], fx(Fv[:, 0])
     H = torch.zeros(bsz, m + 1, m + 1, dtype=torch.float32, device=x0.device)
     H[:, 0, 1:] = H[:, 1:, 0] = 1
