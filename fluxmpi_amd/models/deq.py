@@ -18,7 +18,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.groupnorm import FusedGroupNorm
+from ..ops.groupnorm import FusedGroupNorm, skip_param_grads
 
 
 def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0):
@@ -101,7 +101,8 @@ class DEQFixedPoint(nn.Module):
         def backward_hook(grad):
             u = grad
             for _ in range(self.bwd_iter):  # u = J^T u + grad
-                u_new = torch.autograd.grad(f0, z0, u, retain_graph=True)[0] + grad
+                with skip_param_grads():  # VJPs w.r.t. z only: no GroupNorm dw/db reductions
+                    u_new = torch.autograd.grad(f0, z0, u, retain_graph=True)[0] + grad
                 if (u_new - u).norm() <= self.bwd_tol * (grad.norm() + 1e-9):
                     u = u_new
                     break

@@ -17,6 +17,25 @@ from . import _ext
 from .multi_tensor import DTYPE_CODE
 
 
+_SKIP_PARAM_GRADS = False
+
+
+class skip_param_grads:
+    """Within this context the GroupNorm backward returns no weight / bias gradients.
+
+    For vector-Jacobian products taken w.r.t. activations only (the DEQ adjoint solve:
+    ``autograd.grad(f(z), z, u)``), where ``ctx.needs_input_grad`` still reports the
+    parameters and their (discarded) reductions would run every iteration."""
+
+    def __enter__(self):
+        global _SKIP_PARAM_GRADS
+        self._prev, _SKIP_PARAM_GRADS = _SKIP_PARAM_GRADS, True
+
+    def __exit__(self, *exc):
+        global _SKIP_PARAM_GRADS
+        _SKIP_PARAM_GRADS = self._prev
+
+
 def _stream(t):
     return torch.cuda.current_stream(t.device).cuda_stream
 
@@ -63,8 +82,9 @@ class _GroupNormFn(torch.autograd.Function):
         C.groupnorm_nhwc_bwd(dy.data_ptr(), h.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
                              w32.data_ptr() if w32 is not None else 0, dh.data_ptr(), part.data_ptr(), N, H * W, Ch,
                              groups, relu, DTYPE_CODE[h.dtype], _stream(h))
-        dw = part[:, 0].sum(0).to(wd) if wd is not None and ctx.needs_input_grad[2] else None
-        db = part[:, 1].sum(0).to(bd) if bd is not None and ctx.needs_input_grad[3] else None
+        want = not _SKIP_PARAM_GRADS
+        dw = part[:, 0].sum(0).to(wd) if want and wd is not None and ctx.needs_input_grad[2] else None
+        db = part[:, 1].sum(0).to(bd) if want and bd is not None and ctx.needs_input_grad[3] else None
         return dh, (dh if has_add else None), dw, db, None, None, None
 
 

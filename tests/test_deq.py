@@ -166,3 +166,23 @@ def test_deq_cell_fused_path_gpu():
     gn = lambda m, t: torch.nn.functional.group_norm(t, m.num_groups, m.weight, m.bias, m.eps)  # noqa: E731
     ref = gn(n3, torch.relu(z + gn(n2, x + cell.conv2(gn(n1, torch.relu(cell.conv1(z)))))))
     torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_deq_train_step_gpu_param_grads():
+    """bf16 channels_last DEQ step on the GPU: every parameter (incl. the fused GroupNorms,
+    whose reductions are skipped only inside the adjoint VJPs) gets a finite gradient."""
+    torch.manual_seed(9)
+    model = deq_mnist(max_iter=10, bwd_iter=10).cuda().to(memory_format=torch.channels_last)
+    for m in model.modules():
+        if not isinstance(m, torch.nn.modules.batchnorm._BatchNorm):
+            for p in m.parameters(recurse=False):
+                p.data = p.data.to(torch.bfloat16)
+    x = torch.randn(16, 1, 28, 28, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (16,), device="cuda")
+    loss = F.cross_entropy(model(x).float(), y)
+    loss.backward()
+    assert torch.isfinite(loss)
+    for name, p in model.named_parameters():
+        assert p.grad is not None and torch.isfinite(p.grad.float()).all(), name
+    assert model.deq.f.n3.weight.grad.abs().sum() > 0
