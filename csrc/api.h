@@ -217,4 +217,11 @@ void groupnorm_nhwc_bwd(const void* dy, const void* h, const float* mean, const 
                         float* partials, int64_t N, int64_t HW, int64_t C, int64_t G, bool relu, int dtype,
                         hipStream_t stream);
 
+// ---- GELU backward + bias gradient (transformer MLP fc1) ---------------------------------
+// dh = dy * gelu'(h) (exact erf form); partials[blocks][N] = per-workgroup column sums of dh
+// (sum with gemm_splitk_reduce). N/8 must be a multiple of 64, <= 1024.
+int gelu_bwd_bias_blocks(int64_t rows);
+void gelu_bwd_bias(const void* dy, const void* h, void* dh, float* partials, int blocks, int64_t rows, int64_t N,
+                   int dtype, hipStream_t stream);
+
 }  // namespace fluxmpi

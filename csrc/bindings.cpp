@@ -201,6 +201,14 @@ PYBIND11_MODULE(_C, m) {
                        HW, C, G, relu, dtype, S(stream));
   });
 
+  // ---- GELU backward + bias gradient -------------------------------------------------
+  m.def("gelu_bwd_bias_blocks", &gelu_bwd_bias_blocks);
+  m.def("gelu_bwd_bias", [](uintptr_t dy, uintptr_t h, uintptr_t dh, uintptr_t part, int blocks, int64_t rows,
+                            int64_t N, int dtype, uintptr_t stream) {
+    gelu_bwd_bias(reinterpret_cast<const void*>(dy), reinterpret_cast<const void*>(h), reinterpret_cast<void*>(dh),
+                  reinterpret_cast<float*>(part), blocks, rows, N, dtype, S(stream));
+  });
+
   // ---- fused LayerNorm ------------------------------------------------------
   m.def("layernorm_fwd", [](uintptr_t x, uintptr_t res, uintptr_t h, uintptr_t y, uintptr_t w, uintptr_t b,
                             uintptr_t mean, uintptr_t rstd, int64_t rows, int64_t D, float eps, int dtype,

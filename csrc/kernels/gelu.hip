@@ -1,0 +1,109 @@
+// GELU backward fused with the bias gradient of the Linear that produced its input — gfx950.
+//
+// Transformer MLP: h = x W1^T + b1, y = gelu(h). Autograd runs the GELU backward as one
+// elementwise pass (read dy, h; write dh) and then the bias gradient db1 = sum_rows dh as a
+// separate column reduction that reads dh again (ViT-B/16: 50432 x 3072 bf16 per block).
+// Here one pass writes dh and accumulates db1: every lane owns ONE fixed 8-column vector
+// (blockDim = N/8 lanes, N/8 a multiple of 64), so its column sums stay in registers over
+// the workgroup's row range; each workgroup stores one fp32 partial row (no atomics), summed
+// by gemm_splitk_reduce. Exact (erf) GELU derivative in fp32.
+#include <stdexcept>
+#include <string>
+
+#include "../api.h"
+#include "common.h"
+
+namespace fluxmpi {
+namespace {
+
+template <typename T>
+__global__ __launch_bounds__(1024) void gelu_bwd_bias_kernel(const T* __restrict__ dy, const T* __restrict__ h,
+                                                             T* __restrict__ dh, float* __restrict__ part,
+                                                             int64_t rows, int64_t N, int64_t rows_per_wg) {
+  const int64_t cv = threadIdx.x;  // column vector owned by this lane
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_wg;
+  int64_t r1 = r0 + rows_per_wg;
+  if (r1 > rows) r1 = rows;
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  constexpr float kInvSqrt2 = 0.70710678118654752f, kInvSqrt2Pi = 0.39894228040143268f;
+  // kU rows per iteration with all their loads issued before any math (one row at a time
+  // left the loop latency-bound at ~2.5 TB/s)
+  constexpr int kU = 4;
+  int64_t r = r0;
+  for (; r + kU <= r1; r += kU) {
+    T dv[kU][8], hv[kU][8];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      load8(dy + (r + u) * N + cv * 8, dv[u]);
+      load8(h + (r + u) * N + cv * 8, hv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      T ov[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x = to_f(hv[u][j]);
+        const float cdf = 0.5f * (1.f + erff(x * kInvSqrt2));
+        const float pdf = kInvSqrt2Pi * __expf(-0.5f * x * x);
+        ov[j] = from_f<T>(to_f(dv[u][j]) * (cdf + x * pdf));
+        acc[j] += to_f(ov[j]);  // db of the rounded dh the weight / input gradients use
+      }
+      store8(dh + (r + u) * N + cv * 8, ov);
+    }
+  }
+  for (; r < r1; ++r) {
+    const int64_t off = r * N + cv * 8;
+    T dv[8], hv[8], ov[8];
+    load8(dy + off, dv);
+    load8(h + off, hv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float x = to_f(hv[j]);
+      const float cdf = 0.5f * (1.f + erff(x * kInvSqrt2));
+      const float pdf = kInvSqrt2Pi * __expf(-0.5f * x * x);
+      ov[j] = from_f<T>(to_f(dv[j]) * (cdf + x * pdf));
+      acc[j] += to_f(ov[j]);
+    }
+    store8(dh + off, ov);
+  }
+  float* out = part + static_cast<int64_t>(blockIdx.x) * N + cv * 8;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) out[j] = acc[j];
+}
+
+}  // namespace
+
+int gelu_bwd_bias_blocks(int64_t rows) {
+  int64_t b = rows / 32;  // >= 32 rows per workgroup, at most 1024 workgroups
+  if (b > 1024) b = 1024;
+  if (b < 1) b = 1;
+  return static_cast<int>(b);
+}
+
+void gelu_bwd_bias(const void* dy, const void* h, void* dh, float* partials, int blocks, int64_t rows, int64_t N,
+                   int dtype, hipStream_t stream) {
+  if (N % 8 != 0 || (N / 8) % 64 != 0 || N / 8 > 1024)
+    throw std::runtime_error("gelu_bwd_bias: need N/8 a multiple of 64 and <= 1024 (got N=" + std::to_string(N) + ")");
+  if (blocks < 1 || rows < 1) throw std::runtime_error("gelu_bwd_bias: bad grid");
+  if (((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(h) | reinterpret_cast<uintptr_t>(dh)) & 15u) != 0)
+    throw std::runtime_error("gelu_bwd_bias: tensors must be 16-byte aligned");
+  const int64_t rpw = (rows + blocks - 1) / blocks;
+  const unsigned threads = static_cast<unsigned>(N / 8);
+  switch (dtype) {
+    case kBF16:
+      gelu_bwd_bias_kernel<bf16><<<blocks, threads, 0, stream>>>(static_cast<const bf16*>(dy), static_cast<const bf16*>(h),
+                                                                 static_cast<bf16*>(dh), partials, rows, N, rpw);
+      break;
+    case kF16:
+      gelu_bwd_bias_kernel<f16><<<blocks, threads, 0, stream>>>(static_cast<const f16*>(dy), static_cast<const f16*>(h),
+                                                                static_cast<f16*>(dh), partials, rows, N, rpw);
+      break;
+    default:
+      throw std::runtime_error("gelu_bwd_bias: bf16 / fp16 only");
+  }
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace fluxmpi

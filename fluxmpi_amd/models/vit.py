@@ -13,9 +13,16 @@ folded in (``fluxmpi_amd.ops.layernorm``).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+from ..ops.gelu import linear_gelu
+
+# FLUXMPI_VIT_FUSED_GELU=0: autograd's GELU backward + separate bias reduction (A/B runs)
+_FUSED_GELU = os.environ.get("FLUXMPI_VIT_FUSED_GELU", "1") != "0"
 
 
 class PatchEmbed(nn.Module):
@@ -123,6 +130,9 @@ class Block(nn.Module):
             x, y = self.ln1.add_forward(x, m)  # x <- x + m (previous block's MLP branch)
         a = packed_attention(self.qkv(y), h)
         x, y = self.ln2.add_forward(x, self.proj(a))
+        # fc1 + GELU: GELU backward and fc1's bias gradient in one pass (ops/gelu.py)
+        if _FUSED_GELU:
+            return x, self.fc2(linear_gelu(y, self.fc1.weight, self.fc1.bias))
         return x, self.fc2(F.gelu(self.fc1(y)))
 
 

@@ -1,0 +1,78 @@
+"""``gelu(linear(x, W, b))`` with the GELU backward and the bias gradient in one HIP pass
+(``csrc/kernels/gelu.hip``).
+
+Autograd would run the GELU backward (read dy, h; write dh) and then reduce dh again for
+the Linear's bias gradient. ``linear_gelu`` owns both ops: its backward writes ``dh`` and
+per-workgroup column sums in one pass, then issues the same two GEMMs as ``nn.Linear``'s
+backward (``dh @ W``, ``dh^T @ x``). CPU tensors and unsupported widths use the PyTorch
+composition.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import _ext
+from .multi_tensor import DTYPE_CODE
+
+
+def _native(h: torch.Tensor) -> bool:
+    n = h.shape[-1]
+    return (h.is_cuda and h.dtype in (torch.bfloat16, torch.float16) and n % 8 == 0 and (n // 8) % 64 == 0
+            and n // 8 <= 1024 and h.numel() > 0)
+
+
+def gelu_bwd_bias(dy: torch.Tensor, h: torch.Tensor, bias_dtype=torch.float32):
+    """``(dh, db)``: ``dh = dy * gelu'(h)`` (erf form), ``db = dh.sum(rows)`` in ``bias_dtype``."""
+    if not _native(h):
+        hf = h.float()
+        cdf = 0.5 * (1 + torch.erf(hf * 0.7071067811865476))
+        pdf = torch.exp(-0.5 * hf * hf) * 0.3989422804014327
+        dh = (dy.float() * (cdf + hf * pdf)).to(h.dtype)
+        return dh, dh.float().reshape(-1, h.shape[-1]).sum(0).to(bias_dtype)
+    C = _ext.get(required=True)
+    n = h.shape[-1]
+    rows = h.numel() // n
+    h = h.contiguous()
+    dy = dy.contiguous()
+    dh = torch.empty_like(h)
+    blocks = C.gelu_bwd_bias_blocks(rows)
+    part = torch.empty(blocks, n, device=h.device, dtype=torch.float32)
+    stream = torch.cuda.current_stream(h.device).cuda_stream
+    C.gelu_bwd_bias(dy.data_ptr(), h.data_ptr(), dh.data_ptr(), part.data_ptr(), blocks, rows, n,
+                    DTYPE_CODE[h.dtype], stream)
+    out_dt = bias_dtype if bias_dtype in (torch.float32, torch.bfloat16) else torch.float32
+    db = torch.empty(n, device=h.device, dtype=out_dt)
+    C.gemm_splitk_reduce(part.data_ptr(), blocks, n, db.data_ptr(), DTYPE_CODE[out_dt], stream)
+    return dh, db.to(bias_dtype)
+
+
+class _LinearGeluFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        h = F.linear(x, weight, bias)
+        ctx.save_for_backward(x, weight, h)
+        ctx.has_bias = bias is not None
+        ctx.bias_dtype = bias.dtype if bias is not None else None
+        return F.gelu(h)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, h = ctx.saved_tensors
+        dh, db = gelu_bwd_bias(dy, h, ctx.bias_dtype or torch.float32)
+        n = h.shape[-1]
+        dh2 = dh.reshape(-1, n)
+        dx = (dh2 @ w).reshape(x.shape) if ctx.needs_input_grad[0] else None
+        dw = dh2.t() @ x.reshape(-1, x.shape[-1]) if ctx.needs_input_grad[1] else None
+        return dx, dw, (db if ctx.has_bias and ctx.needs_input_grad[2] else None)
+
+
+def linear_gelu(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
+    """``F.gelu(F.linear(x, weight, bias))`` (exact GELU) with the fused backward on the GPU."""
+    if x.is_cuda and _native_width(weight.shape[0], x.dtype):
+        return _LinearGeluFn.apply(x, weight, bias)
+    return F.gelu(F.linear(x, weight, bias))
+
+
+def _native_width(n: int, dtype) -> bool:
+    return dtype in (torch.bfloat16, torch.float16) and n % 8 == 0 and (n // 8) % 64 == 0 and n // 8 <= 1024

@@ -1,0 +1,62 @@
+"""Fused GELU backward + bias gradient (``csrc/kernels/gelu.hip``, ``ops/gelu.py``)
+against the fp32 PyTorch composition ``gelu(linear(x, W, b))``."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from fluxmpi_amd.ops.gelu import gelu_bwd_bias, linear_gelu
+
+
+def _ref(x, w, b, dy):
+    xr, wr, br = (t.detach().float().clone().requires_grad_() for t in (x, w, b))
+    y = F.gelu(F.linear(xr, wr, br))
+    y.backward(dy.float())
+    return y, xr.grad, wr.grad, br.grad
+
+
+def test_linear_gelu_cpu_fallback():
+    torch.manual_seed(0)
+    x, w, b = torch.randn(3, 5, 16, requires_grad=True), torch.randn(24, 16, requires_grad=True), torch.randn(24, requires_grad=True)
+    y = linear_gelu(x, w, b)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    yr, dxr, dwr, dbr = _ref(x, w, b, dy)
+    torch.testing.assert_close(y, yr)
+    torch.testing.assert_close(x.grad, dxr)
+    torch.testing.assert_close(w.grad, dwr)
+    torch.testing.assert_close(b.grad, dbr)
+    h = torch.randn(7, 24)
+    dh, db = gelu_bwd_bias(dy.reshape(-1, 24)[:7], h)
+    torch.testing.assert_close(db, dh.sum(0))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,k,n", [(197 * 4, 768, 3072), (1000, 64, 512), (37, 128, 8192), (50432, 768, 3072)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_linear_gelu_gpu(rows, k, n, dtype):
+    torch.manual_seed(rows + n)
+    x = (torch.randn(rows, k, device="cuda") * 0.5).to(dtype).requires_grad_()
+    w = (torch.randn(n, k, device="cuda") / k ** 0.5).to(dtype).requires_grad_()
+    b = (torch.randn(n, device="cuda") * 0.1).to(dtype).requires_grad_()
+    y = linear_gelu(x, w, b)
+    dy = torch.randn(rows, n, device="cuda").to(dtype)
+    y.backward(dy)
+    yr, dxr, dwr, dbr = _ref(x, w, b, dy)
+    tol = dict(rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(y.float(), yr, **tol)
+    torch.testing.assert_close(x.grad.float(), dxr, rtol=3e-2, atol=5e-2 * (n / k) ** 0.5)
+    scale = rows ** 0.5
+    torch.testing.assert_close(w.grad.float(), dwr, rtol=3e-2, atol=3e-2 * scale)
+    torch.testing.assert_close(b.grad.float(), dbr, rtol=3e-2, atol=3e-2 * scale)
+
+
+@pytest.mark.gpu
+def test_gelu_bwd_bias_kernel_gpu():
+    torch.manual_seed(5)
+    h = torch.randn(3001, 1024, device="cuda").to(torch.bfloat16)
+    dy = torch.randn_like(h)
+    dh, db = gelu_bwd_bias(dy, h)
+    hf = h.float().requires_grad_()
+    F.gelu(hf).backward(dy.float())
+    torch.testing.assert_close(dh.float(), hf.grad, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(db, dh.float().sum(0), rtol=1e-4, atol=1e-3)
