@@ -199,8 +199,10 @@ void gemm_splitk_reduce(const float* ws, int splits, int64_t n, void* out, int o
 // rows < n; pair (i, j>=i) at index i*n - i*(i-1)/2 + (j-i)) and |F[last]|^2 at [36];
 // sum over chunks on the host side. anderson_gram_chunks: the chunk count to allocate for.
 int anderson_gram_chunks(int64_t bsz, int64_t d);
-void anderson_gram(const float* X, const float* F, float* partials, int64_t bsz, int64_t d, int64_t row_stride,
-                   int64_t batch_stride, int n, int last, int chunks, hipStream_t stream);
+// G (nullable): stored G = F - X rows (same layout); rows with their bit set in `fresh` are
+// recomputed from F - X and written to G, the others are read from G.
+void anderson_gram(const float* X, const float* F, float* G, unsigned fresh, float* partials, int64_t bsz, int64_t d,
+                   int64_t row_stride, int64_t batch_stride, int n, int last, int chunks, hipStream_t stream);
 // X[b, slot] = beta * sum_i alpha[b][i] F[b, i] + (1 - beta) * sum_i alpha[b][i] X[b, i] (i < n);
 // z (nullable, [bsz][d], dtype z_dtype): the new iterate cast to the model dtype.
 void anderson_mix(float* X, const float* F, const float* alpha, void* z, int z_dtype, int64_t bsz, int64_t d,

@@ -172,10 +172,10 @@ PYBIND11_MODULE(_C, m) {
 
   // ---- Anderson solver (DEQ) ---------------------------------------------------
   m.def("anderson_gram_chunks", &anderson_gram_chunks);
-  m.def("anderson_gram", [](uintptr_t X, uintptr_t F, uintptr_t part, int64_t bsz, int64_t d, int64_t rs, int64_t bs,
-                            int n, int last, int chunks, uintptr_t stream) {
-    anderson_gram(reinterpret_cast<const float*>(X), reinterpret_cast<const float*>(F), reinterpret_cast<float*>(part),
-                  bsz, d, rs, bs, n, last, chunks, S(stream));
+  m.def("anderson_gram", [](uintptr_t X, uintptr_t F, uintptr_t G, unsigned fresh, uintptr_t part, int64_t bsz,
+                            int64_t d, int64_t rs, int64_t bs, int n, int last, int chunks, uintptr_t stream) {
+    anderson_gram(reinterpret_cast<const float*>(X), reinterpret_cast<const float*>(F), reinterpret_cast<float*>(G),
+                  fresh, reinterpret_cast<float*>(part), bsz, d, rs, bs, n, last, chunks, S(stream));
   });
   m.def("anderson_mix", [](uintptr_t X, uintptr_t F, uintptr_t alpha, uintptr_t z, int zdt, int64_t bsz, int64_t d,
                            int64_t rs, int64_t bs, int n, int slot, float beta, uintptr_t stream) {

@@ -40,14 +40,19 @@ __device__ __forceinline__ float dot4(const float4& a, const float4& b) {
 }
 
 // grid (chunks, bsz). part[b][chunk][kOut]
+// G (nullable): stored differences, same layout as X / F. With G, rows whose bit is set in
+// `fresh` are formed from F - X and written back to G; the other rows are read from G
+// (k > 2: one fresh row, so 2 + (n-1) rows are read instead of 2n).
 template <int N>
 __global__ __launch_bounds__(kThreads) void gram_kernel(const float* __restrict__ X, const float* __restrict__ F,
-                                                        float* __restrict__ part, int64_t d4, int64_t row_stride,
-                                                        int64_t batch_stride, int64_t chunk4, int last) {
+                                                        float* __restrict__ G, float* __restrict__ part, int64_t d4,
+                                                        int64_t row_stride, int64_t batch_stride, int64_t chunk4,
+                                                        int last, unsigned fresh) {
   const int b = blockIdx.y;
   const int c = blockIdx.x;
   const float4* xb = reinterpret_cast<const float4*>(X + b * batch_stride);
   const float4* fb = reinterpret_cast<const float4*>(F + b * batch_stride);
+  float4* gb = G != nullptr ? reinterpret_cast<float4*>(G + b * batch_stride) : nullptr;
   const int64_t rs4 = row_stride / 4;
   float acc[kPairs];
   float fn = 0.f;
@@ -60,10 +65,19 @@ __global__ __launch_bounds__(kThreads) void gram_kernel(const float* __restrict_
     float4 g[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      const float4 f = fb[i * rs4 + v];
-      const float4 x = xb[i * rs4 + v];
-      g[i] = make_float4(f.x - x.x, f.y - x.y, f.z - x.z, f.w - x.w);
-      if (i == last) fn += dot4(f, f);
+      if (gb == nullptr || ((fresh >> i) & 1u) || i == last) {
+        const float4 f = fb[i * rs4 + v];
+        if (gb == nullptr || ((fresh >> i) & 1u)) {
+          const float4 x = xb[i * rs4 + v];
+          g[i] = make_float4(f.x - x.x, f.y - x.y, f.z - x.z, f.w - x.w);
+          if (gb != nullptr) gb[i * rs4 + v] = g[i];
+        } else {
+          g[i] = gb[i * rs4 + v];
+        }
+        if (i == last) fn += dot4(f, f);
+      } else {
+        g[i] = gb[i * rs4 + v];
+      }
     }
     int p = 0;
 #pragma unroll
@@ -156,9 +170,11 @@ int anderson_gram_chunks(int64_t bsz, int64_t d) {
   return static_cast<int>(chunks);
 }
 
-void anderson_gram(const float* X, const float* F, float* partials, int64_t bsz, int64_t d, int64_t row_stride,
-                   int64_t batch_stride, int n, int last, int chunks, hipStream_t stream) {
+void anderson_gram(const float* X, const float* F, float* G, unsigned fresh, float* partials, int64_t bsz, int64_t d,
+                   int64_t row_stride, int64_t batch_stride, int n, int last, int chunks, hipStream_t stream) {
   check_layout(X, F, d, row_stride, batch_stride, n);
+  if (G != nullptr && (reinterpret_cast<uintptr_t>(G) & 15u) != 0)
+    throw std::runtime_error("anderson_gram: G must be 16-byte aligned");
   if (last < 0 || last >= n) throw std::runtime_error("anderson_gram: last row out of range");
   if (bsz > 65535) throw std::runtime_error("anderson_gram: bsz > 65535");
   const int64_t d4 = d / 4;
@@ -166,8 +182,8 @@ void anderson_gram(const float* X, const float* F, float* partials, int64_t bsz,
   dim3 grid(chunks, static_cast<unsigned>(bsz));
 #define GRAM_CASE(NN)                                                                                   \
   case NN:                                                                                              \
-    gram_kernel<NN><<<grid, kThreads, 0, stream>>>(X, F, partials, d4, row_stride, batch_stride, chunk4, \
-                                                   last);                                               \
+    gram_kernel<NN><<<grid, kThreads, 0, stream>>>(X, F, G, partials, d4, row_stride, batch_stride, chunk4, \
+                                                   last, fresh);                                           \
     break;
   switch (n) {
     GRAM_CASE(1) GRAM_CASE(2) GRAM_CASE(3) GRAM_CASE(4) GRAM_CASE(5) GRAM_CASE(6) GRAM_CASE(7) GRAM_CASE(8)

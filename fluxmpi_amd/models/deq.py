@@ -37,6 +37,7 @@ def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0):
     # dtype (bf16 has no batched LU, and 8-bit mantissas would stall the extrapolation)
     X = torch.zeros(bsz, m, d, dtype=torch.float32, device=x0.device)
     Fv = torch.zeros_like(X)
+    Gs = torch.zeros_like(X)
 
     # flatten in MEMORY order: a channels_last iterate stays channels_last through f (views,
     # no layout copies), which is the layout the fused NHWC GroupNorm kernels take
@@ -65,7 +66,8 @@ def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0):
     for k in range(2, max_iter):
         n = min(k, m)
         last = (k - 1) % m
-        gram, fn2 = AO.gram(X, Fv, n, last)
+        # stored G = F - X: only the row(s) changed since the last Gram are recomputed
+        gram, fn2 = AO.gram(X, Fv, n, last, Gs, (0, 1) if k == 2 else (last,))
         if k > 2:  # residual of the iterate produced by the previous iteration
             res = float(gram[:, last, last].sum().sqrt() / (1e-5 + fn2.sum().sqrt()))
             if res < tol:

@@ -32,17 +32,32 @@ def _native(X: torch.Tensor, F: torch.Tensor, n: int) -> bool:
     return True
 
 
-def gram(X: torch.Tensor, F: torch.Tensor, n: int, last: int):
-    """``(G G^T [bsz, n, n], |F[:, last]|^2 [bsz])`` with ``G = F[:, :n] - X[:, :n]`` (fp32)."""
+def gram(X: torch.Tensor, F: torch.Tensor, n: int, last: int, G: torch.Tensor | None = None, fresh=None):
+    """``(G G^T [bsz, n, n], |F[:, last]|^2 [bsz])`` with ``G = F[:, :n] - X[:, :n]`` (fp32).
+
+    ``G`` (optional, same shape/strides as X): stored differences. Rows listed in ``fresh``
+    are recomputed from ``F - X`` and written to ``G``; the others are read from ``G``
+    (an iteration that changed one row reads 2 + (n - 1) rows instead of 2n)."""
     if not _native(X, F, n):
-        G = F[:, :n] - X[:, :n]
-        return torch.bmm(G, G.transpose(1, 2)), F[:, last].pow(2).sum(1)
+        if G is not None:
+            for i in fresh:
+                G[:, i] = F[:, i] - X[:, i]
+            Gn = G[:, :n]
+        else:
+            Gn = F[:, :n] - X[:, :n]
+        return torch.bmm(Gn, Gn.transpose(1, 2)), F[:, last].pow(2).sum(1)
     C = _ext.get(required=True)
     bsz, _, d = X.shape
     chunks = C.anderson_gram_chunks(bsz, d)
     part = torch.empty(bsz, chunks, 37, device=X.device, dtype=torch.float32)
-    C.anderson_gram(X.data_ptr(), F.data_ptr(), part.data_ptr(), bsz, d, X.stride(1), X.stride(0), n, last, chunks,
-                    _stream(X))
+    mask = 0
+    if G is not None:
+        if G.shape != X.shape or G.stride() != X.stride() or G.dtype != torch.float32 or G.data_ptr() % 16:
+            raise ValueError("anderson gram: G must match X's shape, strides and dtype")
+        for i in fresh:
+            mask |= 1 << int(i)
+    C.anderson_gram(X.data_ptr(), F.data_ptr(), G.data_ptr() if G is not None else 0, mask, part.data_ptr(), bsz, d,
+                    X.stride(1), X.stride(0), n, last, chunks, _stream(X))
     tot = part.sum(1)
     iu = torch.triu_indices(n, n, device=X.device)
     H = X.new_zeros(bsz, n, n)

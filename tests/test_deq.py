@@ -186,3 +186,23 @@ def test_deq_train_step_gpu_param_grads():
     for name, p in model.named_parameters():
         assert p.grad is not None and torch.isfinite(p.grad.float()).all(), name
     assert model.deq.f.n3.weight.grad.abs().sum() > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [2, 5, 8])
+def test_anderson_gram_stored_g_gpu(n):
+    torch.manual_seed(20 + n)
+    bsz, m, d = 64, 8, 4100
+    X = torch.randn(bsz, m, d, device="cuda")
+    Fv = torch.randn(bsz, m, d, device="cuda")
+    G = torch.zeros_like(X)
+    H0, _ = AO.gram(X, Fv, n, n - 1, G, tuple(range(n)))  # all rows fresh: fills G
+    torch.testing.assert_close(G[:, :n], Fv[:, :n] - X[:, :n])
+    s = n // 2  # one row changes: only it is recomputed, the others come from G
+    X[:, s].normal_()
+    Fv[:, s].normal_()
+    H, fn = AO.gram(X, Fv, n, s, G, (s,))
+    Hr, fr = _ref_gram(X, Fv, n, s)
+    torch.testing.assert_close(H.double(), Hr, rtol=1e-4, atol=1e-3 * d ** 0.5)
+    torch.testing.assert_close(fn.double(), fr, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(G[:, s], Fv[:, s] - X[:, s])
