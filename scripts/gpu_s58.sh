@@ -1,5 +1,5 @@
 #!/bin/bash
-# session 58/62: full GPU suite, smoke, all three benchmark configs on the current tree
+# session 58/62/66: full GPU suite, smoke, all three benchmark configs on the current tree
 source "$(dirname "$0")/gpu_lib.sh"
 rm -f "$OUT/steps.log" "$OUT/bench_results.jsonl"
 step pytest_gpu 600 1 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
