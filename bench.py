@@ -46,6 +46,12 @@ def parse():
                     choices=["auto", "channels_last", "contiguous"],
                     help="activation layout (auto: the model's `memory_format` attribute, else channels_last)")
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--force-comm", action="store_true",
+                    help="issue the gradient collectives even at N=1 (hooks, packing, RCCL on the comm "
+                         "stream): measures the data-parallel layer's own cost on one GPU")
+    ap.add_argument("--same-device", action="store_true",
+                    help="all ranks on cuda:0 with gloo collectives on device tensors (RCCL refuses a "
+                         "shared GPU): runs the N>1 code path on a 1-GPU box; no throughput claim")
     ap.add_argument("--graph", action="store_true", help="capture the step in a HIP graph")
     ap.add_argument("--miopen-find", type=int, default=int(os.environ.get("BENCH_MIOPEN_FIND", "1")))
     ap.add_argument("--tunableop", default=os.environ.get("BENCH_TUNABLEOP", "auto"), choices=["auto", "off"],
@@ -73,7 +79,11 @@ def main():
         # results are written back at exit: keep that copy out of the repository
         torch.cuda.tunable.set_filename(os.path.join(os.environ.get("TMPDIR", "/tmp"),
                                                      f"fluxmpi_tunableop_{os.getuid()}_{args.model}.csv"))
-    FluxMPI.Init()
+    if args.same_device:
+        os.environ["FLUXMPI_BACKEND"] = "gloo-device"
+        FluxMPI.Init(gpu_devices=[0] * int(os.environ.get("WORLD_SIZE", "1")))
+    else:
+        FluxMPI.Init()
     # MIOpen find mode, seeded with the tuning db recorded on MI355X (tuning/miopen): the
     # per-shape solver choice without the ~3.5 min search. --miopen-find 0: immediate mode.
     if args.miopen_find:
@@ -101,7 +111,7 @@ def main():
             for p in m.parameters(recurse=False):
                 p.data = p.data.to(torch.bfloat16)
     rule = O.Adam(1e-3) if args.optimizer == "adam" else O.Momentum(0.1, 0.9)
-    ddp = DDP(model, rule, average=True, overlap=not args.no_overlap)
+    ddp = DDP(model, rule, average=True, overlap=not args.no_overlap, force_comm=args.force_comm)
 
     B = args.batch
     gx = torch.Generator(device=dev).manual_seed(rank)
@@ -136,7 +146,7 @@ def main():
     dt_max = FluxMPI.allreduce(torch.tensor([dt], dtype=torch.float64), max).item() if world > 1 else dt
     lval = float(loss.item())
     exposed = None
-    if world > 1 and not args.graph:
+    if ddp.communicate and not args.graph:
         # after the timed region: a few steps with event timing around the gradient-allreduce
         # wait (exposed = not hidden behind backward), max over ranks
         ddp.timing = True
@@ -144,7 +154,10 @@ def main():
             step()
         ddp.timing = False
         e = ddp.exposed_comm_ms()
-        exposed = FluxMPI.allreduce(torch.tensor([e or 0.0], dtype=torch.float64), max).item()
+        exposed = e or 0.0
+        if world > 1:
+            exposed = FluxMPI.allreduce(torch.tensor([exposed], dtype=torch.float64), max).item()
+    cs = ddp.comm_summary()
     if rank == 0:
         ips = world * B * args.steps / dt_max
         names = {"resnet50": "ResNet50", "vit_b16": "ViT-B/16", "deq": "DEQ"}
@@ -157,8 +170,11 @@ def main():
             "config": {"model": mname, "global_batch": world * B, "per_gpu_batch": B, "seq_len": None,
                        "image_size": args.image, "parallelism": f"dp{world}", "optimizer": args.optimizer,
                        "conv": args.conv, "norm": args.norm, "memory_format": "contiguous" if memfmt is torch.contiguous_format else "channels_last", "backend": FluxMPI.backend_name(),
-                       "overlap": not args.no_overlap, "miopen_find": bool(args.miopen_find), "hip_graph": bool(args.graph), "tunableop": use_tunableop, "loss": round(lval, 4),
-                       "exposed_comm_ms": None if exposed is None else round(exposed, 3)},
+                       "miopen_find": bool(args.miopen_find), "hip_graph": bool(args.graph),
+                       "tunableop": use_tunableop, "loss": round(lval, 4),
+                       # what the data-parallel layer actually did: at N=1 nothing is communicated
+                       # (overlap false, comm "none") unless --force-comm
+                       **cs, "exposed_comm_ms": None if exposed is None else round(exposed, 3)},
         }
         print(json.dumps(rec), flush=True)
     FluxMPI.Finalize()

@@ -292,9 +292,11 @@ PYBIND11_MODULE(_C, m) {
       .def("allgather", &RcclComm::allgather, py::call_guard<py::gil_scoped_release>())
       .def("reduce_scatter", &RcclComm::reduce_scatter, py::call_guard<py::gil_scoped_release>())
       .def("alltoall", &RcclComm::alltoall, py::call_guard<py::gil_scoped_release>())
-      .def("async_error", &RcclComm::async_error)
+      .def("async_error", &RcclComm::async_error, py::call_guard<py::gil_scoped_release>())
       .def_static("error_string", &RcclComm::error_string)
-      .def("abort", &RcclComm::abort, py::call_guard<py::gil_scoped_release>())
+      .def("abort", &RcclComm::abort, py::arg("abort_wait_ms") = 2000, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("aborted", &RcclComm::aborted)
+      .def_property_readonly("is_open", &RcclComm::is_open)
       .def("destroy", &RcclComm::destroy, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("rank", &RcclComm::rank)
       .def_property_readonly("size", &RcclComm::size)

@@ -16,6 +16,7 @@
 
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -59,7 +60,7 @@ RcclComm::RcclComm(const std::string& uid, int rank, int size, int device)
 }
 
 RcclComm::~RcclComm() {
-  if (comm_ != nullptr) {
+  if (comm_ != nullptr && !aborted_.load()) {
     // Best effort: never throw from a destructor.
     ncclCommDestroy(C(comm_));
     comm_ = nullptr;
@@ -67,11 +68,15 @@ RcclComm::~RcclComm() {
 }
 
 void RcclComm::check_open() const {
+  if (aborted_.load()) throw std::runtime_error("RcclComm: communicator aborted (watchdog or explicit abort)");
   if (comm_ == nullptr) throw std::runtime_error("RcclComm: communicator destroyed");
 }
 
+using Lock = std::lock_guard<std::timed_mutex>;
+
 void RcclComm::allreduce(uintptr_t send, uintptr_t recv, size_t count, int dtype, int op,
                          uintptr_t stream) {
+  Lock lk(mu_);
   check_open();
   RCCL_CHECK(ncclAllReduce(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), count,
                            static_cast<ncclDataType_t>(dtype), static_cast<ncclRedOp_t>(op), C(comm_),
@@ -80,6 +85,7 @@ void RcclComm::allreduce(uintptr_t send, uintptr_t recv, size_t count, int dtype
 
 void RcclComm::allreduce_many(const std::vector<uintptr_t>& bufs, const std::vector<size_t>& counts,
                               const std::vector<int>& dtypes, int op, uintptr_t stream) {
+  Lock lk(mu_);
   check_open();
   if (bufs.size() != counts.size() || bufs.size() != dtypes.size())
     throw std::runtime_error("allreduce_many: length mismatch");
@@ -98,6 +104,7 @@ void RcclComm::allreduce_many(const std::vector<uintptr_t>& bufs, const std::vec
 
 void RcclComm::broadcast(uintptr_t send, uintptr_t recv, size_t count, int dtype, int root,
                          uintptr_t stream) {
+  Lock lk(mu_);
   check_open();
   RCCL_CHECK(ncclBroadcast(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), count,
                            static_cast<ncclDataType_t>(dtype), root, C(comm_),
@@ -106,6 +113,7 @@ void RcclComm::broadcast(uintptr_t send, uintptr_t recv, size_t count, int dtype
 
 void RcclComm::reduce(uintptr_t send, uintptr_t recv, size_t count, int dtype, int op, int root,
                       uintptr_t stream) {
+  Lock lk(mu_);
   check_open();
   RCCL_CHECK(ncclReduce(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), count,
                         static_cast<ncclDataType_t>(dtype), static_cast<ncclRedOp_t>(op), root, C(comm_),
@@ -113,6 +121,7 @@ void RcclComm::reduce(uintptr_t send, uintptr_t recv, size_t count, int dtype, i
 }
 
 void RcclComm::allgather(uintptr_t send, uintptr_t recv, size_t sendcount, int dtype, uintptr_t stream) {
+  Lock lk(mu_);
   check_open();
   RCCL_CHECK(ncclAllGather(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), sendcount,
                            static_cast<ncclDataType_t>(dtype), C(comm_), reinterpret_cast<hipStream_t>(stream)));
@@ -120,6 +129,7 @@ void RcclComm::allgather(uintptr_t send, uintptr_t recv, size_t sendcount, int d
 
 void RcclComm::reduce_scatter(uintptr_t send, uintptr_t recv, size_t recvcount, int dtype, int op,
                               uintptr_t stream) {
+  Lock lk(mu_);
   check_open();
   RCCL_CHECK(ncclReduceScatter(reinterpret_cast<const void*>(send), reinterpret_cast<void*>(recv), recvcount,
                                static_cast<ncclDataType_t>(dtype), static_cast<ncclRedOp_t>(op), C(comm_),
@@ -127,6 +137,7 @@ void RcclComm::reduce_scatter(uintptr_t send, uintptr_t recv, size_t recvcount, 
 }
 
 void RcclComm::alltoall(uintptr_t send, uintptr_t recv, size_t count_per_peer, int dtype, uintptr_t stream) {
+  Lock lk(mu_);
   check_open();
   // Built from grouped send/recv so it works on every RCCL build.
   const size_t esz = dtype_size(dtype);
@@ -134,16 +145,25 @@ void RcclComm::alltoall(uintptr_t send, uintptr_t recv, size_t count_per_peer, i
   for (int peer = 0; peer < size_; ++peer) {
     const char* s = reinterpret_cast<const char*>(send) + peer * count_per_peer * esz;
     char* r = reinterpret_cast<char*>(recv) + peer * count_per_peer * esz;
-    ncclSend(s, count_per_peer, static_cast<ncclDataType_t>(dtype), peer, C(comm_),
-             reinterpret_cast<hipStream_t>(stream));
-    ncclRecv(r, count_per_peer, static_cast<ncclDataType_t>(dtype), peer, C(comm_),
-             reinterpret_cast<hipStream_t>(stream));
+    ncclResult_t rs = ncclSend(s, count_per_peer, static_cast<ncclDataType_t>(dtype), peer, C(comm_),
+                               reinterpret_cast<hipStream_t>(stream));
+    ncclResult_t rr = (rs == ncclSuccess || rs == ncclInProgress)
+                          ? ncclRecv(r, count_per_peer, static_cast<ncclDataType_t>(dtype), peer, C(comm_),
+                                     reinterpret_cast<hipStream_t>(stream))
+                          : rs;
+    if (rr != ncclSuccess && rr != ncclInProgress) {
+      ncclGroupEnd();  // close the group before reporting, so the communicator stays usable
+      throw std::runtime_error(std::string("RCCL error in alltoall (peer ") + std::to_string(peer) +
+                               "): " + ncclGetErrorString(rr));
+    }
   }
   RCCL_CHECK(ncclGroupEnd());
 }
 
-int RcclComm::async_error() const {
-  if (comm_ == nullptr) return 0;
+int RcclComm::async_error() {
+  // Polled from the watchdog thread: never wait behind an enqueue, just skip this poll.
+  std::unique_lock<std::timed_mutex> lk(mu_, std::try_to_lock);
+  if (!lk.owns_lock() || comm_ == nullptr) return 0;
   ncclResult_t r = ncclSuccess;
   ncclResult_t q = ncclCommGetAsyncError(C(comm_), &r);
   if (q != ncclSuccess) return static_cast<int>(q);
@@ -152,17 +172,21 @@ int RcclComm::async_error() const {
 
 std::string RcclComm::error_string(int code) { return ncclGetErrorString(static_cast<ncclResult_t>(code)); }
 
-void RcclComm::abort() {
-  if (comm_ != nullptr) {
-    ncclCommAbort(C(comm_));
-    comm_ = nullptr;
-  }
+void RcclComm::abort(int abort_wait_ms) {
+  aborted_.store(true);  // new enqueues fail fast from here on
+  std::unique_lock<std::timed_mutex> lk(mu_, std::defer_lock);
+  (void)lk.try_lock_for(std::chrono::milliseconds(abort_wait_ms));
+  void* c = comm_;
+  comm_ = nullptr;
+  if (c != nullptr) ncclCommAbort(C(c));
 }
 
 void RcclComm::destroy() {
+  Lock lk(mu_);
   if (comm_ != nullptr) {
-    RCCL_CHECK(ncclCommDestroy(C(comm_)));
+    ncclComm_t c = C(comm_);
     comm_ = nullptr;
+    RCCL_CHECK(ncclCommDestroy(c));
   }
 }
 

@@ -1,7 +1,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -11,6 +13,15 @@ std::string rccl_unique_id();
 int rccl_version();
 
 // Thin owner of an ncclComm_t; all operations are stream-ordered and async.
+//
+// Thread safety: the training thread enqueues collectives while the watchdog
+// thread polls async_error() and may abort(). Every use of comm_ holds mu_, so
+// abort/destroy can never free the communicator under a running enqueue. An
+// enqueue that does not return (a wedged launch queue) must not make the
+// watchdog hang as well: abort() waits at most `abort_wait_ms` for the lock and
+// then aborts regardless (ncclCommAbort is the documented way to unblock a
+// communicator from another thread). Once aborted, every call throws
+// "communicator aborted" instead of touching a freed handle.
 class RcclComm {
  public:
   RcclComm(const std::string& uid, int rank, int size, int device);
@@ -26,10 +37,12 @@ class RcclComm {
   void allgather(uintptr_t send, uintptr_t recv, size_t sendcount, int dtype, uintptr_t stream);
   void reduce_scatter(uintptr_t send, uintptr_t recv, size_t recvcount, int dtype, int op, uintptr_t stream);
   void alltoall(uintptr_t send, uintptr_t recv, size_t count_per_peer, int dtype, uintptr_t stream);
-  int async_error() const;
+  int async_error();
   static std::string error_string(int code);
-  void abort();
+  void abort(int abort_wait_ms = 2000);
   void destroy();
+  bool aborted() const { return aborted_.load(); }
+  bool is_open() const { return comm_ != nullptr; }
 
   int rank() const { return rank_; }
   int size() const { return size_; }
@@ -38,6 +51,8 @@ class RcclComm {
  private:
   void check_open() const;
   static size_t dtype_size(int dtype);
+  std::timed_mutex mu_;
+  std::atomic<bool> aborted_{false};
   void* comm_ = nullptr;
   int rank_, size_, device_;
 };

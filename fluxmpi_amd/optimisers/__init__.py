@@ -50,6 +50,10 @@ class AbstractRule:
         """Return ``(new_state, dx')``; ``x -= dx'`` is applied by the caller."""
         raise NotImplementedError
 
+    #: True for rules that issue collectives (``DistributedOptimizer``): every rank must then
+    #: hand them the same leaves, so a missing gradient is zero-filled instead of skipped.
+    collective = False
+
     def apply_batch(self, items: list) -> list:
         """``items``: list of ``(leaf, x, dx)``. Returns the ``dx'`` list; updates ``leaf.state``.
 
@@ -278,6 +282,10 @@ class OptimiserChain(AbstractRule):
     def __init__(self, *opts: AbstractRule):
         self.opts = tuple(opts)
 
+    @property
+    def collective(self) -> bool:
+        return any(getattr(o, "collective", False) for o in self.opts)
+
     def init(self, x):
         return tuple(o.init(x) for o in self.opts)
 
@@ -343,8 +351,14 @@ def _collect(tree, model, grads):
 
     def walk(s, x, g):
         if isinstance(s, Leaf):
-            if g is None or s.frozen:
+            if s.frozen:
                 return
+            if g is None:
+                if not getattr(s.rule, "collective", False):
+                    return
+                # a rank without a gradient for this leaf still takes part in the
+                # collective (the plan comes from the state tree), contributing zeros
+                g = torch.zeros_like(_as_tensor(x))
             x_t, g_t = _as_tensor(x), _as_tensor(g)
             if id(s) in items:
                 leaf, xx, gg = items[id(s)]

@@ -12,6 +12,10 @@ while the next bucket is packed, and unpacked after the stream-side wait.
 
 Leaves larger than half a bucket that are already contiguous skip the
 pack/unpack copies and are reduced in place.
+
+In a world of one the collectives are the identity and are skipped, unless
+``force_comm`` (``FLUXMPI_FORCE_COMM=1``) asks for the real path: pack, RCCL
+on the comm stream, event fence, unpack, exactly as with N ranks.
 """
 from __future__ import annotations
 
@@ -95,21 +99,33 @@ def _comm_for(dev: torch.device, comm: Communicator | None) -> Communicator:
     return runtime.comm_for(torch.empty(0, device=dev))
 
 
+def _forced(force_comm: bool | None) -> bool:
+    return get_config().force_comm if force_comm is None else bool(force_comm)
+
+
+def _bump_versions(tensors) -> None:
+    """The multi-tensor kernels write through raw pointers; tell autograd's version
+    counters (and the DDP engine's stale-master check) that the tensors changed."""
+    for t in tensors:
+        torch.autograd.graph.increment_version(t)
+
+
 def allreduce_tensors(tensors: list, op=ReduceOp.SUM, comm: Communicator | None = None,
-                      bucket_bytes: int | None = None) -> list:
+                      bucket_bytes: int | None = None, force_comm: bool | None = None) -> list:
     """In-place allreduce of many tensors with bucketing. Returns ``tensors``."""
     tensors = [t for t in tensors if t is not None]
     if not tensors:
         return tensors
     op = to_op(op)
+    forced = _forced(force_comm)
     work_t, back = _contig(tensors)
     plan = plan_buckets(work_t, bucket_bytes)
     pending = []
     ws_off: dict = {}
     for kind, dev, dt, idx, offs, total in plan:
         c = _comm_for(dev, comm)
-        if c.size == 1 and op in (ReduceOp.SUM, ReduceOp.PROD, ReduceOp.MAX, ReduceOp.MIN, ReduceOp.AVG):
-            continue  # identity for a world of one
+        if c.size == 1 and not forced:
+            continue  # every reduction is the identity for a world of one
         if kind == "direct":
             pending.append((c.allreduce(work_t[idx[0]], op, async_op=True), None, idx, offs))
             continue
@@ -132,21 +148,25 @@ def allreduce_tensors(tensors: list, op=ReduceOp.SUM, comm: Communicator | None 
         mt.pack([work_t[i] for i in idx], flat, offs)
         c = _comm_for(dev, comm)
         launched.append((c.allreduce(flat, op, async_op=True), flat, idx, offs))
+    written = []
     for w, flat, idx, offs in launched:
         w.wait()
         if flat is not None:
             mt.unpack(flat, [work_t[i] for i in idx], offs)
+            written.extend(work_t[i] for i in idx)
     for orig, c in back:
         orig.copy_(c)
+    _bump_versions([t for t in written if t.is_cuda])
     return tensors
 
 
 def broadcast_tensors(tensors: list, root: int = 0, comm: Communicator | None = None,
-                      bucket_bytes: int | None = None) -> list:
+                      bucket_bytes: int | None = None, force_comm: bool | None = None) -> list:
     """In-place broadcast of many tensors from ``root`` with bucketing."""
     tensors = [t for t in tensors if t is not None]
     if not tensors:
         return tensors
+    forced = _forced(force_comm)
     work_t, back = _contig(tensors)
     plan = plan_buckets(work_t, bucket_bytes)
     launched = []
@@ -155,7 +175,8 @@ def broadcast_tensors(tensors: list, root: int = 0, comm: Communicator | None = 
         if c.size == 1:
             if root != 0:
                 raise ValueError(f"root {root} out of range for a world of size 1")
-            continue
+            if not forced:
+                continue
         if kind == "direct":
             launched.append((c.broadcast(work_t[idx[0]], root, async_op=True), None, idx, offs, c))
             continue
@@ -163,10 +184,13 @@ def broadcast_tensors(tensors: list, root: int = 0, comm: Communicator | None = 
         if c.rank == root:
             mt.pack([work_t[i] for i in idx], flat, offs)
         launched.append((c.broadcast(flat, root, async_op=True), flat, idx, offs, c))
+    written = []
     for w, flat, idx, offs, c in launched:
         w.wait()
         if flat is not None and c.rank != root:  # root already holds the data
             mt.unpack(flat, [work_t[i] for i in idx], offs)
+            written.extend(work_t[i] for i in idx)
     for orig, cc in back:
         orig.copy_(cc)
+    _bump_versions([t for t in written if t.is_cuda])
     return tensors

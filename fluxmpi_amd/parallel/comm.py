@@ -81,6 +81,24 @@ _TORCH_OP = {
     ReduceOp.MIN: dist.ReduceOp.MIN,
 }
 
+# Reductions over bool buffers run on a uint8 copy with the logical equivalent of the
+# requested op (SUM/MAX = OR, PROD/MIN = AND), so no rank count can overflow or wrap
+# the byte, and the result is renormalised to {0, 1} when it is copied back.
+_BOOL_OP = {ReduceOp.SUM: ReduceOp.MAX, ReduceOp.MAX: ReduceOp.MAX, ReduceOp.PROD: ReduceOp.MIN,
+            ReduceOp.MIN: ReduceOp.MIN}
+
+
+def bool_op(op: ReduceOp) -> ReduceOp:
+    try:
+        return _BOOL_OP[op]
+    except KeyError:
+        raise ValueError(f"reduction {op.name} is not defined for bool buffers") from None
+
+
+class CommAbortedError(RuntimeError):
+    """The communicator was aborted (by the watchdog or :meth:`RcclComm.abort`)."""
+
+
 # torch dtype -> ncclDataType_t
 NCCL_DTYPE = {
     torch.int8: 0, torch.uint8: 1, torch.int32: 2, torch.int64: 4,
@@ -291,7 +309,7 @@ class TorchComm(Communicator):
         if t.dtype == torch.bool:
             # reductions over bool are not supported by every backend
             tmp = t.to(torch.uint8)
-            w = dist.all_reduce(tmp, op=tdop, group=self.group, async_op=True)
+            w = dist.all_reduce(tmp, op=_TORCH_OP[bool_op(op)], group=self.group, async_op=True)
             work = _TorchWork(w, t, post=lambda: t.copy_(tmp.bool()))
         else:
             w = dist.all_reduce(t, op=tdop, group=self.group, async_op=True)
@@ -354,6 +372,59 @@ class TorchComm(Communicator):
         dist.barrier(group=self.group)
 
 
+class GlooDeviceComm(TorchComm):
+    """gloo collectives on *device* tensors (backend ``gloo-device``).
+
+    RCCL refuses two ranks on one GPU (``ncclCommInitRank`` -> invalid usage,
+    ``profiles/r2_probe_rccl_two_ranks_one_gpu.json``), so this is how several
+    ranks sharing one MI355X run the device-side engine: DDP's hook-driven
+    overlap, packing and stream fencing over CUDA tensors, with gloo's own
+    device<->host staging. allreduce and broadcast go to gloo directly (its CUDA
+    work makes the caller's stream wait on completion); the rarer collectives
+    stage through host memory explicitly. A test/rehearsal backend, not a fast one.
+    """
+
+    name = "gloo-device"
+
+    def __init__(self, group, rank: int, size: int):
+        super().__init__(group, rank, size, "gloo")
+        self.name = "gloo-device"
+
+    def _host(self, fn, out, *inputs):
+        hs = [t.detach().cpu() for t in inputs]
+        ho = out.detach().cpu()
+        fn(ho, *hs)
+        out.copy_(ho)
+        return out
+
+    def reduce(self, t, op=ReduceOp.SUM, root=0, async_op=False):
+        if not t.is_cuda:
+            return super().reduce(t, op, root, async_op)
+        h = t.detach().cpu()
+        TorchComm.reduce(self, h, op, root)
+        if self.rank == root:
+            t.copy_(h)
+        return Work(t) if async_op else t
+
+    def allgather(self, out, inp, async_op=False):
+        if not out.is_cuda:
+            return super().allgather(out, inp, async_op)
+        r = self._host(lambda ho, hi: TorchComm.allgather(self, ho, hi), out, inp)
+        return Work(r) if async_op else r
+
+    def reduce_scatter(self, out, inp, op=ReduceOp.SUM, async_op=False):
+        if not out.is_cuda:
+            return super().reduce_scatter(out, inp, op, async_op)
+        r = self._host(lambda ho, hi: TorchComm.reduce_scatter(self, ho, hi, op), out, inp)
+        return Work(r) if async_op else r
+
+    def alltoall(self, out, inp, async_op=False):
+        if not out.is_cuda:
+            return super().alltoall(out, inp, async_op)
+        r = self._host(lambda ho, hi: TorchComm.alltoall(self, ho, hi), out, inp)
+        return Work(r) if async_op else r
+
+
 class RcclComm(Communicator):
     """Native RCCL communicator (C++ ``fluxmpi::RcclComm``) on a dedicated HIP stream.
 
@@ -372,14 +443,21 @@ class RcclComm(Communicator):
         if C is None or not hasattr(C, "RcclComm"):
             raise RuntimeError("native RCCL communicator not available in fluxmpi_amd._C")
         self.device = torch.device(device)
-        key = f"fluxmpi_amd/rccl_uid/{tag}"
+        self.abort_reason: str | None = None
         if size == 1:
             uid = C.rccl_unique_id()
-        elif rank == 0:
-            uid = C.rccl_unique_id()
-            store.set(key, uid)
         else:
-            uid = store.get(key)
+            # One key per Init generation: every rank bumps the counter once per bootstrap,
+            # and all adds of generation k precede any add of k+1 (ncclCommInitRank is
+            # collective), so Init -> Finalize -> Init on a surviving store can never read
+            # the previous generation's id.
+            gen = (int(store.add(f"fluxmpi_amd/rccl_gen/{tag}", 1)) - 1) // size
+            key = f"fluxmpi_amd/rccl_uid/{tag}/{gen}"
+            if rank == 0:
+                uid = C.rccl_unique_id()
+                store.set(key, uid)
+            else:
+                uid = store.get(key)
         with torch.cuda.device(self.device):
             self._h = C.RcclComm(bytes(uid), rank, size, self.device.index)
             # high priority: comm kernels should win the CU arbitration against
@@ -403,6 +481,27 @@ class RcclComm(Communicator):
             return work
         return work.wait()
 
+    @property
+    def aborted(self) -> bool:
+        return self.abort_reason is not None
+
+    def _handle(self):
+        if self.abort_reason is not None:
+            raise CommAbortedError(f"RCCL communicator was aborted ({self.abort_reason}); "
+                                   "re-run Init in a new process to continue")
+        if self._h is None:
+            raise RuntimeError("RCCL communicator has been destroyed (Finalize)")
+        return self._h
+
+    def abort(self, reason: str = "abort() called") -> None:
+        """``ncclCommAbort``: unblock every pending collective; later calls raise
+        :class:`CommAbortedError`. Safe to call from the watchdog thread."""
+        if self.abort_reason is None:
+            self.abort_reason = reason
+        h = self._h
+        if h is not None:
+            h.abort()
+
     @staticmethod
     def _check(t: torch.Tensor):
         if not t.is_cuda:
@@ -416,9 +515,16 @@ class RcclComm(Communicator):
     def allreduce(self, t, op=ReduceOp.SUM, async_op=False):
         self._check(t)
         op = to_op(op)
+        h = self._handle()
+        if t.dtype == torch.bool:
+            # RCCL has no bool type: reduce a uint8 copy with the logical op, renormalise back
+            tmp = t.to(torch.uint8)
+            self._enter()
+            h.allreduce(tmp.data_ptr(), tmp.data_ptr(), tmp.numel(), NCCL_DTYPE[torch.uint8], int(bool_op(op)),
+                        self.stream.cuda_stream)
+            return self._exit([tmp], t, async_op, post=lambda: t.copy_(tmp.bool()))
         self._enter(t)
-        self._h.allreduce(t.data_ptr(), t.data_ptr(), t.numel(), NCCL_DTYPE[t.dtype], int(op),
-                          self.stream.cuda_stream)
+        h.allreduce(t.data_ptr(), t.data_ptr(), t.numel(), NCCL_DTYPE[t.dtype], int(op), self.stream.cuda_stream)
         return self._exit([t], t, async_op)
 
     def allreduce_out(self, send, recv, op=ReduceOp.SUM, async_op=False):
@@ -426,14 +532,14 @@ class RcclComm(Communicator):
         self._check(recv)
         op = to_op(op)
         self._enter()
-        self._h.allreduce(send.data_ptr(), recv.data_ptr(), send.numel(), NCCL_DTYPE[send.dtype], int(op),
+        self._handle().allreduce(send.data_ptr(), recv.data_ptr(), send.numel(), NCCL_DTYPE[send.dtype], int(op),
                           self.stream.cuda_stream)
         return self._exit([send, recv], recv, async_op)
 
     def broadcast(self, t, root=0, async_op=False):
         self._check(t)
         self._enter()
-        self._h.broadcast(t.data_ptr(), t.data_ptr(), t.numel(), NCCL_DTYPE[t.dtype], int(root),
+        self._handle().broadcast(t.data_ptr(), t.data_ptr(), t.numel(), NCCL_DTYPE[t.dtype], int(root),
                           self.stream.cuda_stream)
         return self._exit([t], t, async_op)
 
@@ -442,12 +548,12 @@ class RcclComm(Communicator):
         op = to_op(op)
         self._enter()
         if self.rank == root:
-            self._h.reduce(t.data_ptr(), t.data_ptr(), t.numel(), NCCL_DTYPE[t.dtype], int(op), int(root),
+            self._handle().reduce(t.data_ptr(), t.data_ptr(), t.numel(), NCCL_DTYPE[t.dtype], int(op), int(root),
                            self.stream.cuda_stream)
             return self._exit([t], t, async_op)
         # non-root keeps its input (reference contract): send from t, receive nowhere useful
         scratch = torch.empty_like(t)
-        self._h.reduce(t.data_ptr(), scratch.data_ptr(), t.numel(), NCCL_DTYPE[t.dtype], int(op), int(root),
+        self._handle().reduce(t.data_ptr(), scratch.data_ptr(), t.numel(), NCCL_DTYPE[t.dtype], int(op), int(root),
                        self.stream.cuda_stream)
         return self._exit([t, scratch], t, async_op)
 
@@ -455,7 +561,7 @@ class RcclComm(Communicator):
         self._check(out)
         self._check(inp)
         self._enter()
-        self._h.allgather(inp.data_ptr(), out.data_ptr(), inp.numel(), NCCL_DTYPE[inp.dtype],
+        self._handle().allgather(inp.data_ptr(), out.data_ptr(), inp.numel(), NCCL_DTYPE[inp.dtype],
                           self.stream.cuda_stream)
         return self._exit([out, inp], out, async_op)
 
@@ -464,7 +570,7 @@ class RcclComm(Communicator):
         self._check(inp)
         op = to_op(op)
         self._enter()
-        self._h.reduce_scatter(inp.data_ptr(), out.data_ptr(), out.numel(), NCCL_DTYPE[inp.dtype], int(op),
+        self._handle().reduce_scatter(inp.data_ptr(), out.data_ptr(), out.numel(), NCCL_DTYPE[inp.dtype], int(op),
                                self.stream.cuda_stream)
         return self._exit([out, inp], out, async_op)
 
@@ -472,7 +578,7 @@ class RcclComm(Communicator):
         self._check(out)
         self._check(inp)
         self._enter()
-        self._h.alltoall(inp.data_ptr(), out.data_ptr(), inp.numel() // self.size, NCCL_DTYPE[inp.dtype],
+        self._handle().alltoall(inp.data_ptr(), out.data_ptr(), inp.numel() // self.size, NCCL_DTYPE[inp.dtype],
                          self.stream.cuda_stream)
         return self._exit([out, inp], out, async_op)
 
@@ -487,22 +593,24 @@ class RcclComm(Communicator):
             self._check(t)
         op = to_op(op)
         self._enter()
-        self._h.allreduce_many([t.data_ptr() for t in tensors], [t.numel() for t in tensors],
+        self._handle().allreduce_many([t.data_ptr() for t in tensors], [t.numel() for t in tensors],
                                [NCCL_DTYPE[t.dtype] for t in tensors], int(op), self.stream.cuda_stream)
         return self._exit(list(tensors), list(tensors), async_op)
 
     def check_async_error(self):
         h = self._h
-        if h is None:  # destroyed (Finalize) — nothing left to watch
+        if h is None or self.abort_reason is not None:  # destroyed (Finalize) or aborted
             return
         code = h.async_error()
         if code != 0:
-            raise RuntimeError(f"RCCL asynchronous error {code}: {self._h.error_string(code)}")
+            raise RuntimeError(f"RCCL asynchronous error {code}: {h.error_string(code)}")
 
     def destroy(self):
-        if getattr(self, "_h", None) is not None:
-            torch.cuda.synchronize(self.device)
-            self._h.destroy()
+        h = getattr(self, "_h", None)
+        if h is not None:
+            if self.abort_reason is None:
+                torch.cuda.synchronize(self.device)
+                h.destroy()
             self._h = None
 
 

@@ -32,6 +32,12 @@ for MI355X + RCCL over xGMI:
    whole step can be captured in a HIP graph.
 5. **Semantics.** Gradients are SUMmed like the reference; ``average=True``
    scales by ``1/world`` inside the optimiser kernel (free).
+6. **World of one.** With nothing to communicate (world 1) the engine neither
+   registers hooks nor packs: the fused optimiser reads autograd's gradient
+   tensors in place (pointer lists, no copy into the flat buffer).
+   ``force_comm=True`` (``FLUXMPI_FORCE_COMM=1``) runs the full N>1 path
+   anyway — hooks, packing, real collectives on the communicator's stream
+   with event fencing — so a single GPU exercises and measures it.
 
 The Optimisers.jl-compatible state tree is available via
 :meth:`DDP.optimiser_state` (``Leaf(rule, (mt, vt, βt))`` with tensor views
@@ -119,7 +125,7 @@ class DDP:
                  master_weights: bool = True, average: bool = False, overlap: bool | None = None,
                  broadcast: bool = True, root_rank: int = 0, comm: Communicator | None = None,
                  comm_dtype: torch.dtype | None = None, watchdog: bool | None = None,
-                 grad_mode: str | None = None):
+                 grad_mode: str | None = None, force_comm: bool | None = None):
         cfg = get_config()
         # "steal": autograd hands over each freshly produced gradient (no in-place accumulate
         # kernel per parameter, no zero fill) and one multi-tensor launch per bucket packs them
@@ -140,6 +146,11 @@ class DDP:
             comm = runtime.comm_for(params[0]) if runtime.Initialized() else None
         self.comm = comm
         self.world = comm.size if comm is not None else 1
+        self.force_comm = cfg.force_comm if force_comm is None else bool(force_comm)
+        if self.force_comm and comm is None:
+            raise RuntimeError("DDP(force_comm=True) needs a communicator: call fluxmpi_amd.Init() first")
+        # collectives are issued whenever there is a peer, or when forced (world-1 rehearsal)
+        self.communicate = comm is not None and (self.world > 1 or self.force_comm)
         if comm_dtype is None:
             comm_dtype = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16,
                           "bfloat16": torch.bfloat16, "fp16": torch.float16}.get(cfg.comm_dtype)
@@ -154,7 +165,7 @@ class DDP:
                 self._param_bucket[id(p)] = b
         self._hooks = []
         self._sync_enabled = True
-        if self.overlap and self.world > 1:
+        if self.overlap and self.communicate:
             for p in params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad_ready))
         self._setup_optimizer()
@@ -164,11 +175,14 @@ class DDP:
             # every rank must build the same bucket plan, or collectives would mismatch
             check_same_structure([(str(b.dtype), b.numel, len(b.params)) for b in self.buckets],
                                  comm=runtime.cpu_comm(), what="DDP bucket plan")
+        if self.communicate and runtime.Initialized():
             if watchdog if watchdog is not None else cfg.extra.get("watchdog", True):
                 self.watchdog = Watchdog(comm, timeout_s=cfg.timeout_s)
         if broadcast and self.world > 1:
             self.broadcast_parameters(root_rank)
         self._next_launch = 0
+        self._direct_cache: dict = {}
+        self._record_versions()
         self.zero_grad()
         self.step_count = 0
         # exposed-communication timing (off by default: event timing costs a little)
@@ -298,7 +312,7 @@ class DDP:
         if b.launched:
             return
         b.launched = True
-        if self.world == 1:
+        if not self.communicate:
             return
         self._pack(b)
         buf = b.flat_grad
@@ -324,16 +338,21 @@ class DDP:
         fill launch per dtype); "steal" mode drops the per-step gradient tensors."""
         if self.grad_mode == "view":
             mt.fill_([b.flat_grad for b in self.buckets], 0.0)
+        self._rearm()
         for b in self.buckets:
-            b.pending = len(b.params)
-            b.ready = b.launched = b.packed = False
-            b.work = None
             for p, o in zip(b.params, b.offsets):
                 if self.grad_mode == "steal":
                     p.grad = None
                 elif p.grad is None or p.grad.data_ptr() != b.flat_grad.data_ptr() + o * b.flat_grad.element_size():
                     # someone replaced .grad (e.g. set_to_none): restore the view
                     p.grad = _strided_view(b.flat_grad, p, o)
+
+    def _rearm(self):
+        """Reset the per-step bucket state (countdowns, launch/pack flags) for the next backward."""
+        for b in self.buckets:
+            b.pending = len(b.params)
+            b.ready = b.launched = b.packed = False
+            b.work = None
         self._next_launch = 0
 
     def _pack(self, b: _Bucket):
@@ -388,8 +407,22 @@ class DDP:
                 mt.unpack(b.comm_buf, [b.flat_grad], [0])
 
     def step(self, zero_grad: bool = True):
-        """Finish the gradient allreduces and apply the fused optimiser to every bucket."""
+        """Finish the gradient allreduces and apply the fused optimiser to every bucket.
+
+        The buckets are re-armed here whatever ``zero_grad`` is, so a following
+        backward + ``step(zero_grad=False)`` (gradient accumulation across steps)
+        launches, packs and waits on every bucket again.
+        """
         gscale = 1.0 / self.world if self.average else 1.0
+        self._sync_masters()
+        if not self.communicate and self.grad_mode == "steal":
+            # nothing to reduce: the optimiser reads autograd's gradients where they are
+            for b in self.buckets:
+                if not self._apply_direct(b, gscale):
+                    self._pack(b)
+                    self._apply(b, gscale)
+            self._finish_step(zero_grad)
+            return
         for b in self.buckets:
             if not b.launched:
                 b.ready = True
@@ -412,6 +445,9 @@ class DDP:
                 self._pack(b)
                 self._finish(b)
                 self._apply(b, gscale)
+        self._finish_step(zero_grad)
+
+    def _finish_step(self, zero_grad: bool):
         if self.kind == "adam":
             fused.adam_advance_(self.hyper, self.adam.beta[0], self.adam.beta[1])
         self.step_count += 1
@@ -419,8 +455,35 @@ class DDP:
             self.watchdog.check()
         if self.debug_checks and self.world > 1:
             check_replicas(self.module, comm=runtime.cpu_comm())
+        self._rearm()
+        self._record_versions()  # the optimiser's own writes are not "outside" changes
         if zero_grad:
             self.zero_grad()
+
+    # ------------------------------------------------------------------ masters
+    def _record_versions(self):
+        self._versions = [[p._version for p in b.params] for b in self.buckets]
+
+    def _sync_masters(self):
+        """Pick up parameter changes made outside the engine (``load_state_dict``,
+        ``checkpoint.load``, ``synchronize``, in-place edits): a changed version counter
+        means the fp32 master of that parameter is stale, so it is re-read from the param."""
+        for b, vs in zip(self.buckets, self._versions):
+            for i, p in enumerate(b.params):
+                if p._version != vs[i]:
+                    if b.master is not None:
+                        o = b.offsets[i]
+                        with torch.no_grad():
+                            _strided_view(b.master, p, o).copy_(p.detach())
+                    vs[i] = p._version
+
+    def refresh_master(self):
+        """Re-read every fp32 master weight from its (low-precision) parameter."""
+        with torch.no_grad():
+            for b in self.buckets:
+                if b.master is not None:
+                    b.master.copy_(b.flat_param)
+        self._record_versions()
 
     def exposed_comm_ms(self, reset: bool = True) -> float | None:
         """Mean exposed (not overlapped with backward) allreduce time per step, in ms,
@@ -446,6 +509,35 @@ class DDP:
                        lr=self.rule.eta, momentum=mom, nesterov=self.kind == "nesterov", weight_decay=self.wd,
                        grad_scale=gscale, masters=masters, dev_lr=self.hyper)
 
+    def _apply_direct(self, b: _Bucket, gscale: float) -> bool:
+        """Fused optimiser on the autograd gradients in place (no pack). False if some gradient
+        cannot be read directly (missing, other dtype/layout/device): the caller packs instead."""
+        grads = []
+        for p in b.params:
+            g = p.grad
+            if g is None or g.dtype != b.dtype or g.device != b.device or not _same_layout(g, p) \
+                    or not _is_dense(g):
+                return False
+            grads.append(g)
+        st = self._direct_cache.get(b.index)
+        if st is None:
+            def sl(flat):
+                return [flat[o:o + p.numel()] for p, o in zip(b.params, b.offsets)] if flat is not None else None
+            st = (sl(b.flat_param), sl(b.exp_avg), sl(b.exp_avg_sq), sl(b.master))
+            self._direct_cache[b.index] = st
+        ps, ms, vs, ws = st
+        # the flat slices are in memory order; a gradient with its parameter's strides is too
+        gs = [g.view(-1) if g.is_contiguous() else g.as_strided((g.numel(),), (1,)) for g in grads]
+        if self.kind == "adam":
+            a = self.adam
+            fused.adam_(ps, gs, ms, vs, lr=a.eta, beta1=a.beta[0], beta2=a.beta[1], eps=a.epsilon, bc1=0.0,
+                        bc2=0.0, weight_decay=self.wd, grad_scale=gscale, masters=ws, dev_hyper=self.hyper)
+        else:
+            mom = {"descent": 0.0}.get(self.kind, getattr(self.rule, "rho", 0.0))
+            fused.sgd_(ps, gs, ms, lr=self.rule.eta, momentum=mom, nesterov=self.kind == "nesterov",
+                       weight_decay=self.wd, grad_scale=gscale, masters=ws, dev_lr=self.hyper)
+        return True
+
     def set_lr(self, lr: float):
         """Change the learning rate (device-side, so captured graphs see it)."""
         self.hyper[0].fill_(lr)
@@ -463,10 +555,11 @@ class DDP:
         for b in self.buckets:
             for name, p, o in zip(b.names, b.params, b.offsets):
                 n = p.numel()
+                # moments follow the parameter's memory order (NHWC for channels_last weights)
                 if self.kind == "adam":
-                    st = (b.exp_avg[o:o + n].view(p.shape), b.exp_avg_sq[o:o + n].view(p.shape), tuple(bt))
+                    st = (_strided_view(b.exp_avg, p, o), _strided_view(b.exp_avg_sq, p, o), tuple(bt))
                 elif b.exp_avg is not None:
-                    st = b.exp_avg[o:o + n].view(p.shape)
+                    st = _strided_view(b.exp_avg, p, o)
                 else:
                     st = None
                 out[name] = O.Leaf(self.rule, st)
@@ -489,15 +582,27 @@ class DDP:
             self.step_count = int(sd["step"])
             self.hyper.copy_(sd["hyper"])
             for b, s in zip(self.buckets, sd["buckets"]):
-                if s["master"] is not None and b.master is not None:
-                    b.master.copy_(s["master"])
+                if b.master is not None:
+                    if s["master"] is not None:
+                        b.master.copy_(s["master"])
+                    else:  # checkpoint without masters: start them from the loaded params
+                        b.master.copy_(b.flat_param)
                 if s["m"] is not None:
                     b.exp_avg.copy_(s["m"])
                 if s["v"] is not None:
                     b.exp_avg_sq.copy_(s["v"])
+        self._record_versions()
 
     def num_parameters(self) -> int:
         return sum(p.numel() for b in self.buckets for p in b.params)
+
+    def comm_summary(self) -> dict:
+        """What the engine communicates per step (for bench records)."""
+        return {"communicate": self.communicate, "force_comm": self.force_comm,
+                "overlap": bool(self.overlap and self.communicate), "grad_mode": self.grad_mode,
+                "buckets": len(self.buckets),
+                "bucket_mb": [round(b.numel * b.flat_grad.element_size() / 2 ** 20, 2) for b in self.buckets],
+                "comm": (self.comm.name if self.communicate else "none")}
 
     def bucket_summary(self) -> list:
         return [{"index": b.index, "dtype": str(b.dtype), "numel": b.numel, "params": len(b.params),

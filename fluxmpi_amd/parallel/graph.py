@@ -41,13 +41,15 @@ class GraphedStep:
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
         wd = ddp.watchdog
-        ddp.watchdog = None  # event queries are illegal while the stream is capturing
+        if wd is not None:
+            wd.pause()  # event queries from the watchdog thread are illegal during capture
         self.graph = torch.cuda.CUDAGraph()
         try:
             with torch.cuda.graph(self.graph):
                 self.static_loss = self._eager()
         finally:
-            ddp.watchdog = wd
+            if wd is not None:
+                wd.resume()
         ddp.step_count -= 1  # capture records the step but executes nothing
         self.replays = 0
 

@@ -10,6 +10,15 @@ Semantics kept from the reference:
 * ``allreduce_gradients`` returns the reduced gradient tree; non-array leaves
   pass through.
 
+Irregular gradient trees: in the reference a rank whose gradient
+for some leaf is ``nothing`` skips that leaf's ``MPI_Allreduce`` while the
+others issue it, and the job hangs. Here the reduction plan comes from the
+*state* tree: ``Optimisers.update_`` zero-fills a missing gradient for a
+``collective`` rule, so every rank reduces the same leaves in the same order.
+Before each bucketed reduction the plan's structure hash is compared across
+ranks (one tiny host allreduce, ``FLUXMPI_CHECK_PLANS``), so a tree that
+really differs raises :class:`CollectiveMismatchError` instead of deadlocking.
+
 What changed (the MI355X design): the reference performs one blocking,
 host-staged ``MPI_Allreduce`` per leaf inside ``apply!``. Here
 :meth:`DistributedOptimizer.apply_batch` receives *all* leaves of an update
@@ -19,20 +28,49 @@ rule's fused kernel (multi-tensor Adam etc.). Gradients are reduced in place.
 """
 from __future__ import annotations
 
+import os
 from typing import Any
 
 import numpy as np
 import torch
 
 from ..optimisers import AbstractRule
-from ..utils.tree import fmap
+from ..utils.config import get_config
+from ..utils.debug import check_same_structure, structure_hash
+from ..utils.tree import fmap, node_def
 from . import runtime
 from .bucket import allreduce_tensors
 from .comm import ReduceOp
 
+_CHECKED: set = set()
+
+
+def check_plan(obj, what: str) -> None:
+    """Cross-rank structure check of a reduction plan (``FLUXMPI_CHECK_PLANS``).
+
+    ``always`` (default): every call, one 16-byte host allreduce — every rank
+    checks, so a rank can never sit in the check while another is already in the
+    gradient collective. ``first``: once per distinct plan on this rank (cheaper;
+    only safe when trees can differ from the first step on). ``never``: off.
+    """
+    mode = str(get_config().extra.get("check_plans", "")) or os.environ.get("FLUXMPI_CHECK_PLANS", "always")
+    mode = mode.lower()
+    if mode == "never" or not runtime.Initialized() or runtime.total_workers() == 1:
+        return
+    if mode == "first":
+        h = structure_hash(obj)
+        if h in _CHECKED:
+            return
+        check_same_structure(obj, what=what)
+        _CHECKED.add(h)
+        return
+    check_same_structure(obj, what=what)
+
 
 class DistributedOptimizer(AbstractRule):
     """Wrap an Optimisers-style rule; gradients are allreduce-SUMmed before it runs."""
+
+    collective = True
 
     def __init__(self, optimizer: AbstractRule, average: bool = False):
         self.optimizer = optimizer
@@ -43,6 +81,7 @@ class DistributedOptimizer(AbstractRule):
 
     def _reduce(self, grads: list) -> None:
         grads = [g for g in grads if g is not None]
+        check_plan(grads, "DistributedOptimizer gradient batch")
         if not grads:
             return
         op = ReduceOp.AVG if self.average else ReduceOp.SUM
@@ -63,14 +102,44 @@ class DistributedOptimizer(AbstractRule):
         return f"DistributedOptimizer({self.optimizer!r})"
 
 
-def allreduce_gradients(gs: Any, on_gpu: bool | None = None, op=ReduceOp.SUM) -> Any:
+def _zero_fill(gs: Any, like: Any) -> Any:
+    """``gs`` with every missing (``None``) gradient replaced by zeros shaped like ``like``."""
+    if gs is None:
+        if isinstance(like, torch.Tensor):
+            return torch.zeros_like(like)
+        if isinstance(like, np.ndarray):
+            return np.zeros_like(like)
+    if isinstance(like, torch.nn.Module):
+        named = dict(like.named_parameters())
+        g = gs if isinstance(gs, dict) else {n: p.grad for n, p in named.items()}
+        return {n: _zero_fill(g.get(n), p) for n, p in named.items()}
+    nd = node_def(like)
+    if nd is None:
+        return gs
+    lc, aux = nd[0](like)
+    gc = [None] * len(lc) if gs is None else nd[0](gs)[0]
+    if len(gc) != len(lc):
+        raise ValueError("allreduce_gradients: gradient tree and `like` tree differ in structure")
+    return nd[1](aux, [_zero_fill(g, c) for g, c in zip(gc, lc)])
+
+
+def allreduce_gradients(gs: Any, on_gpu: bool | None = None, op=ReduceOp.SUM, like: Any = None) -> Any:
     """Allreduce (SUM) every array leaf of the gradient tree ``gs``; returns the tree.
 
     ``on_gpu`` is accepted for API parity with the reference (which staged
     GPU gradients through the host when set). Collectives here are always
     device-direct, so it only serves as an assertion when given explicitly.
+
+    ``like`` (the parameter tree, or the module) makes the reduction plan come from
+    the parameters: a ``None`` gradient is zero-filled, so a rank missing one still
+    joins every collective. Without it, the gradient tree's structure
+    (``None`` positions included) is checked across ranks and a mismatch raises
+    :class:`CollectiveMismatchError` instead of hanging.
     """
     runtime._require()
+    if like is not None:
+        gs = _zero_fill(gs, like)
+    check_plan(gs, "gradient tree")
     leaves: list = []
     seen: set = set()
 

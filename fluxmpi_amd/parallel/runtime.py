@@ -104,7 +104,8 @@ def Init(gpu_devices: list[int] | None = None, verbose: bool = False, backend: s
 
     Idempotent. ``gpu_devices[rank]`` selects the GPU explicitly; otherwise the
     node-local rank round-robins over the visible GPUs. ``backend`` overrides
-    ``FLUXMPI_BACKEND`` (``auto``/``rccl``/``torch``/``gloo``).
+    ``FLUXMPI_BACKEND`` (``auto``/``rccl``/``torch``/``gloo``/``gloo-device``; the last
+    keeps the GPU but runs collectives through gloo, so several ranks can share one device).
     """
     if _S.initialized and not _S.finalized:
         if verbose:
@@ -168,6 +169,11 @@ def _make_device_comm(backend, cfg, rank, size, device, cpu_comm):
     if cfg.host_staged:
         log.info("Device-direct collectives disabled using LocalPreferences.toml (host-staged path).")
         return _comm.HostStagedComm(cpu_comm), "host-staged"
+    if backend in ("gloo-device", "gloo-cuda"):
+        # several ranks may share one GPU (RCCL refuses that): gloo over device tensors
+        if size == 1:
+            return _comm.SelfComm(), "self"
+        return _comm.GlooDeviceComm(cpu_comm.group, rank, size), "gloo-device"
     store = None
     if size > 1:
         store = dist.distributed_c10d._get_default_store()
@@ -193,6 +199,9 @@ def Finalize() -> None:
     """
     if not _S.initialized or _S.finalized:
         return
+    from ..utils.debug import stop_all
+
+    stop_all()  # no watchdog may poll a communicator while (or after) it is destroyed
     if _S.dev_comm is not None:
         try:
             _S.dev_comm.destroy()

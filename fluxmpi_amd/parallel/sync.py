@@ -92,7 +92,9 @@ def _sync_module(m: torch.nn.Module, root: int) -> torch.nn.Module:
     for t in list(m.parameters()) + list(m.buffers()):
         if id(t) not in seen and t.numel() > 0:
             seen.add(id(t))
-            ts.append(t.data)
+            # detach() (not .data) shares the version counter, so the write is visible to
+            # the DDP engine's stale-master check
+            ts.append(t.detach())
     _broadcast_any(ts, root)
     return m
 
@@ -159,7 +161,7 @@ def _sync_tree(x: Any, root: int) -> Any:
             for t in list(leaf.parameters()) + list(leaf.buffers()):
                 if id(t) not in seen:
                     seen.add(id(t))
-                    tensors.append(t.data)
+                    tensors.append(t.detach())
         elif isinstance(leaf, FlatParams):
             if id(leaf.data) not in seen:
                 seen.add(id(leaf.data))

@@ -20,7 +20,9 @@ Environment knobs (all optional):
 =========================  ==================================================
 ``FLUXMPI_BACKEND``        ``auto`` (default) | ``rccl`` (native C++ RCCL
                            communicator) | ``torch`` (torch.distributed
-                           ProcessGroup) | ``gloo`` (CPU)
+                           ProcessGroup) | ``gloo`` (CPU) | ``gloo-device``
+                           (GPU compute, gloo collectives on device tensors:
+                           several ranks on one GPU, which RCCL refuses)
 ``FLUXMPI_BUCKET_MB``      gradient bucket size in MiB (default 16)
 ``FLUXMPI_FIRST_BUCKET_MB`` size of the first (last-layer) bucket (default 4)
 ``FLUXMPI_COMM_DTYPE``     ``native`` | ``fp32`` | ``bf16`` grad comm dtype
@@ -28,6 +30,9 @@ Environment knobs (all optional):
 ``FLUXMPI_PROFILE``        ``1`` emit roctx ranges + per-step timers
 ``FLUXMPI_DEBUG_CHECKS``   ``1`` cross-rank checksum after every collective
 ``FLUXMPI_TIMEOUT_S``      collective watchdog timeout (default 600)
+``FLUXMPI_FORCE_COMM``     ``1``: issue the collectives even in a world of
+                           one (hooks, packing, RCCL on the comm stream), to
+                           exercise and time the N>1 path on a single GPU
 =========================  ==================================================
 """
 from __future__ import annotations
@@ -136,6 +141,7 @@ class Config:
     profile: bool = False
     debug_checks: bool = False
     timeout_s: float = 600.0
+    force_comm: bool = False
     extra: dict = field(default_factory=dict)
 
     @classmethod
@@ -157,6 +163,7 @@ class Config:
             profile=_env_bool("FLUXMPI_PROFILE", False),
             debug_checks=_env_bool("FLUXMPI_DEBUG_CHECKS", False),
             timeout_s=_env_float("FLUXMPI_TIMEOUT_S", 600.0),
+            force_comm=_env_bool("FLUXMPI_FORCE_COMM", bool(prefs.get("force_comm", False))),
             extra=prefs,
         )
 

@@ -23,6 +23,7 @@ from __future__ import annotations
 import hashlib
 import threading
 import time
+import weakref
 
 import torch
 
@@ -82,17 +83,30 @@ def check_same_structure(obj, comm=None, what: str = "tree") -> None:
     c = comm or runtime.cpu_comm()
     if c.size == 1:
         return
-    h = torch.tensor([structure_hash(obj)], dtype=torch.int64)
-    hi, lo = h.clone(), h.clone()
-    c.allreduce(hi, "max")
-    c.allreduce(lo, "min")
-    if int(hi) != int(lo):
+    mine = structure_hash(obj)
+    # one collective: max of (h, -h) gives the max and (minus) the min at once
+    hl = torch.tensor([mine, -mine], dtype=torch.int64)
+    c.allreduce(hl, "max")
+    hi, lo = int(hl[0]), -int(hl[1])
+    h = mine
+    if hi != lo:
         raise CollectiveMismatchError(f"ranks disagree about the structure of the {what} "
                                       f"(rank {c.rank} hash {int(h)}); collectives would mismatch")
 
 
+_WATCHDOGS: "weakref.WeakSet[Watchdog]" = weakref.WeakSet()
+
+
 class Watchdog:
-    """Background failure detector for the device communicator."""
+    """Background failure detector for the device communicator.
+
+    Each poll runs under ``_poll_lock``; :meth:`pause` takes the same lock, so
+    once it returns no poll is running and none starts until :meth:`resume`.
+    HIP-graph capture needs that (an event query from another thread is illegal
+    while a stream captures), and :func:`stop_all` (``Finalize``) stops every
+    watchdog before the communicator is destroyed, so the thread can never poll
+    a freed communicator.
+    """
 
     def __init__(self, comm, timeout_s: float = 600.0, interval_s: float = 1.0):
         self.comm = comm
@@ -101,38 +115,67 @@ class Watchdog:
         self.error: BaseException | None = None
         self._inflight: dict = {}
         self._lock = threading.Lock()
+        self._poll_lock = threading.Lock()
+        self._paused = False
         self._stop = threading.Event()
         self._thread = threading.Thread(target=self._run, name="fluxmpi-watchdog", daemon=True)
+        _WATCHDOGS.add(self)
         self._thread.start()
 
     def track(self, work, what: str = "collective"):
         """Register an in-flight :class:`Work`; returns it."""
+        if self._paused:
+            return work  # captured into a graph: nothing runs now, nothing to watch
         with self._lock:
             self._inflight[id(work)] = (work, time.time(), what)
         return work
 
+    def _poll(self):
+        self.comm.check_async_error()
+        now = time.time()
+        with self._lock:
+            items = list(self._inflight.items())
+        for k, (w, t0, what) in items:
+            if w.is_completed():
+                with self._lock:
+                    self._inflight.pop(k, None)
+            elif now - t0 > self.timeout_s:
+                raise TimeoutError(f"{what} did not complete within {self.timeout_s:.0f}s")
+
     def _run(self):
         while not self._stop.wait(self.interval_s):
-            try:
-                self.comm.check_async_error()
-                now = time.time()
-                with self._lock:
-                    items = list(self._inflight.items())
-                for k, (w, t0, what) in items:
-                    if w.is_completed():
-                        with self._lock:
-                            self._inflight.pop(k, None)
-                    elif now - t0 > self.timeout_s:
-                        raise TimeoutError(f"{what} did not complete within {self.timeout_s:.0f}s")
-            except BaseException as e:  # noqa: BLE001 - recorded and re-raised on the main thread
-                self.error = e
-                abort = getattr(getattr(self.comm, "_h", None), "abort", None)
-                if abort is not None:
-                    try:
-                        abort()
-                    except Exception:
-                        pass
-                return
+            with self._poll_lock:
+                if self._paused or self._stop.is_set():
+                    continue
+                try:
+                    self._poll()
+                except BaseException as e:  # noqa: BLE001 - recorded and re-raised on the main thread
+                    self.error = e
+                    self._abort(repr(e))
+                    return
+
+    def _abort(self, reason: str):
+        abort = getattr(self.comm, "abort", None)
+        try:
+            if abort is not None:
+                abort(f"watchdog: {reason}")
+            else:
+                h = getattr(self.comm, "_h", None)
+                if h is not None and hasattr(h, "abort"):
+                    h.abort()
+        except Exception:
+            pass
+
+    def pause(self):
+        """Stop polling (returns once no poll is running); forget in-flight works."""
+        with self._poll_lock:
+            self._paused = True
+            with self._lock:
+                self._inflight.clear()
+
+    def resume(self):
+        with self._poll_lock:
+            self._paused = False
 
     def check(self):
         if self.error is not None:
@@ -140,8 +183,17 @@ class Watchdog:
 
     def stop(self):
         self._stop.set()
-        self._thread.join(timeout=5)
+        with self._poll_lock:  # wait for a running poll to end
+            pass
+        if self._thread is not threading.current_thread():
+            self._thread.join(timeout=5)
+
+
+def stop_all() -> None:
+    """Stop every live watchdog (``Finalize`` calls this before destroying communicators)."""
+    for w in list(_WATCHDOGS):
+        w.stop()
 
 
 __all__ = ["ReplicaDivergenceError", "CollectiveMismatchError", "checksum", "check_replicas", "structure_hash",
-           "check_same_structure", "Watchdog"]
+           "check_same_structure", "Watchdog", "stop_all"]

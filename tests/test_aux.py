@@ -121,3 +121,70 @@ def test_step_timer_and_ranges():
             torch.randn(100, 100) @ torch.randn(100, 100)
     s = t.summary()
     assert "fwd" in s and s["fwd"] >= 0
+
+
+def test_watchdog_pause_resume_stop():
+    """pause() returns with no poll running and none starting; stop_all() (Finalize) stops it."""
+    import time
+    from fluxmpi_amd.utils import debug
+
+    class FakeComm:
+        polls = 0
+
+        def check_async_error(self):
+            FakeComm.polls += 1
+
+    class FakeWork:
+        def is_completed(self):
+            raise AssertionError("polled while paused")
+
+    wd = debug.Watchdog(FakeComm(), timeout_s=60, interval_s=0.01)
+    time.sleep(0.05)
+    assert FakeComm.polls > 0
+    wd.pause()
+    n = FakeComm.polls
+    wd.track(FakeWork())  # tracked during "capture": ignored
+    time.sleep(0.05)
+    assert FakeComm.polls == n and wd.error is None
+    wd.resume()
+    time.sleep(0.05)
+    assert FakeComm.polls > n
+    debug.stop_all()
+    assert not wd._thread.is_alive()
+    n = FakeComm.polls
+    time.sleep(0.03)
+    assert FakeComm.polls == n
+
+
+def test_watchdog_abort_marks_comm():
+    """On a timeout the watchdog calls comm.abort(reason); later collectives must fail loudly."""
+    import time
+    from fluxmpi_amd.utils import debug
+
+    class FakeComm:
+        reason = None
+
+        def check_async_error(self):
+            pass
+
+        def abort(self, reason):
+            FakeComm.reason = reason
+
+    class Stuck:
+        def is_completed(self):
+            return False
+
+    wd = debug.Watchdog(FakeComm(), timeout_s=0.0, interval_s=0.01)
+    wd.track(Stuck(), "allreduce of bucket 0")
+    for _ in range(200):
+        if wd.error is not None:
+            break
+        time.sleep(0.01)
+    assert isinstance(wd.error, TimeoutError) and "bucket 0" in FakeComm.reason
+    try:
+        wd.check()
+    except RuntimeError as e:
+        assert "watchdog" in str(e)
+    else:
+        raise AssertionError
+    wd.stop()

@@ -175,3 +175,148 @@ def test_bucket_launch_order_mixed_dtypes():
     # it came second and blocked all of them)
     kinds = [b.dtype for b in ddp.buckets]
     assert len(kinds) > 4 and kinds.index(torch.float32) >= len(kinds) - 3
+
+
+def test_ddp_force_comm_world1_matches():
+    """force_comm runs hooks + packing + (identity) collectives at world 1; same result."""
+    import fluxmpi_amd as FluxMPI
+    from fluxmpi_amd import optimisers as O
+    from fluxmpi_amd.parallel.ddp import DDP
+
+    FluxMPI.Init()
+    for grad_mode in ("steal", "view"):
+        m1, m2 = _mlp(0), _mlp(0)
+        d1 = DDP(m1, O.Adam(1e-2), bucket_mb=0.001, first_bucket_mb=0.0005, grad_mode=grad_mode, force_comm=True)
+        d2 = DDP(m2, O.Adam(1e-2), bucket_mb=0.001, first_bucket_mb=0.0005, grad_mode=grad_mode)
+        assert d1.communicate and d1._hooks and not d2.communicate and not d2._hooks
+        x, y = _data(0)
+        for _ in range(3):
+            for d in (d1, d2):
+                ((d(x) - y) ** 2).mean().backward()
+            assert all(b.launched for b in d1.buckets)  # every bucket launched from the hooks
+            d1.step()
+            d2.step()
+        for p, q in zip(m1.parameters(), m2.parameters()):
+            assert torch.equal(p, q)
+        assert d1.comm_summary()["comm"] != "none" and d2.comm_summary()["comm"] == "none"
+
+
+def test_ddp_step_without_zero_grad_rearms():
+    """step(zero_grad=False) must re-arm the buckets: the next step launches again."""
+    import fluxmpi_amd as FluxMPI
+    from fluxmpi_amd import optimisers as O
+    from fluxmpi_amd.parallel.ddp import DDP
+
+    FluxMPI.Init()
+    m = _mlp(0)
+    d = DDP(m, O.Descent(0.1), bucket_mb=0.001, first_bucket_mb=0.0005, force_comm=True)
+    x, y = _data(0)
+    ((d(x) - y) ** 2).mean().backward()
+    d.step(zero_grad=False)
+    assert all(not b.launched and b.pending == len(b.params) for b in d.buckets) and d._next_launch == 0
+    ((d(x) - y) ** 2).mean().backward()
+    assert all(b.launched for b in d.buckets)
+    d.step()
+
+
+def worker_ddp_no_zero_grad():
+    import fluxmpi_amd as FluxMPI
+    from fluxmpi_amd import optimisers as O
+    from fluxmpi_amd.parallel.ddp import DDP
+    from fluxmpi_amd.utils.debug import check_replicas
+
+    FluxMPI.Init()
+    r = FluxMPI.local_rank()
+    for grad_mode in ("steal", "view"):
+        m = _mlp(50 + r)
+        d = DDP(m, O.Adam(1e-2), bucket_mb=0.001, first_bucket_mb=0.0005, grad_mode=grad_mode)
+        x, y = _data(r)
+        for _ in range(3):
+            ((d(x) - y) ** 2).mean().backward()
+            d.step(zero_grad=False)
+            check_replicas(m)  # raises if a step applied local-only gradients
+        d.zero_grad()
+    FluxMPI.Finalize()
+
+
+def test_ddp_no_zero_grad_gloo(spmd):
+    spmd("tests.test_ddp:worker_ddp_no_zero_grad", nprocs=2, timeout=120)
+
+
+def test_ddp_master_follows_outside_param_changes(tmp_path):
+    """bf16 params with fp32 masters: load_state_dict / checkpoint.load / in-place edits made
+    outside the engine are picked up at the next step."""
+    from fluxmpi_amd import optimisers as O
+    from fluxmpi_amd.parallel.ddp import DDP
+    from fluxmpi_amd.utils import checkpoint
+
+    def bf16(seed):
+        return _mlp(seed).to(torch.bfloat16)
+
+    x, y = _data(0)
+    x, y = x.bfloat16(), y.bfloat16()
+    for how in ("load_state_dict", "checkpoint", "inplace"):
+        m = bf16(0)
+        d = DDP(m, O.Descent(0.1), master_weights=True)
+        assert all(b.master is not None for b in d.buckets)
+        src = bf16(1)
+        if how == "load_state_dict":
+            m.load_state_dict(src.state_dict())
+        elif how == "checkpoint":
+            checkpoint.save(str(tmp_path / "m.pt"), src)
+            checkpoint.load(str(tmp_path / "m.pt"), like=m)
+        else:
+            with torch.no_grad():
+                for p, q in zip(m.parameters(), src.parameters()):
+                    p.copy_(q)
+        # reference: a fresh engine built on the loaded weights
+        m_ref = bf16(1)
+        d_ref = DDP(m_ref, O.Descent(0.1), master_weights=True)
+        for dd in (d, d_ref):
+            ((dd(x) - y) ** 2).mean().backward()
+            dd.step()
+        for p, q in zip(m.parameters(), m_ref.parameters()):
+            assert torch.equal(p, q), how
+    # explicit refresh + a checkpoint without masters
+    m = bf16(0)
+    d = DDP(m, O.Adam(1e-2), master_weights=True)
+    sd = d.state_dict()
+    for b in sd["buckets"]:
+        b["master"] = None
+    with torch.no_grad():
+        for p in m.parameters():
+            p.zero_()
+    sd["module"] = bf16(2).state_dict()
+    d.load_state_dict(sd)
+    for b in d.buckets:
+        assert torch.equal(b.master, b.flat_param.float())
+    d.refresh_master()
+
+
+def test_ddp_optimiser_state_channels_last():
+    """optimiser_state() views follow the parameter memory order (NHWC conv weights)."""
+    from fluxmpi_amd import optimisers as O
+    from fluxmpi_amd.parallel.ddp import DDP
+
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Conv2d(3, 4, 3, padding=1), torch.nn.ReLU(), torch.nn.Conv2d(4, 2, 3))
+    ref = torch.nn.Sequential(torch.nn.Conv2d(3, 4, 3, padding=1), torch.nn.ReLU(), torch.nn.Conv2d(4, 2, 3))
+    ref.load_state_dict(net.state_dict())
+    net = net.to(memory_format=torch.channels_last)
+    assert net[0].weight.is_contiguous(memory_format=torch.channels_last)
+    d = DDP(net, O.Adam(1e-2))
+    ps = {n: p.detach().clone() for n, p in ref.named_parameters()}
+    st = O.setup(O.Adam(1e-2), ps)
+    x = torch.randn(2, 3, 6, 6)
+    for _ in range(2):
+        d(x.contiguous(memory_format=torch.channels_last)).square().mean().backward()
+        d.step()
+        for n, p in ref.named_parameters():
+            p.data.copy_(ps[n])
+            p.grad = None
+        ref(x).square().mean().backward()
+        st, ps = O.update(st, ps, {n: p.grad for n, p in ref.named_parameters()})
+    state = d.optimiser_state()
+    for n in ps:
+        torch.testing.assert_close(state[n].state[0], st[n].state[0], rtol=1e-4, atol=1e-7)
+        torch.testing.assert_close(state[n].state[1], st[n].state[1], rtol=1e-4, atol=1e-9)
