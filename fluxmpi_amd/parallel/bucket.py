@@ -62,10 +62,13 @@ def plan_buckets(tensors: list, bucket_bytes: int | None = None):
         esz = torch.empty((), dtype=dt).element_size()
         cur: list = []
         cur_bytes = 0
+        packable = dt in mt.DTYPE_CODE or dev.type != "cuda"  # the HIP pack kernels' dtypes
         for i in idx:
             t = tensors[i]
             nb = t.numel() * esz
-            if nb >= bb // 2 and t.is_contiguous():
+            if (nb >= bb // 2 or not packable) and t.is_contiguous():
+                # big leaves, and leaves the pack kernels cannot move (int64 step counters,
+                # bool masks ...), are reduced in place, one collective each
                 plan.append(("direct", dev, dt, [i], [0], t.numel()))
                 continue
             if cur and cur_bytes + nb > bb:

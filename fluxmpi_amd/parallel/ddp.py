@@ -178,7 +178,7 @@ class DDP:
         if self.communicate and runtime.Initialized():
             if watchdog if watchdog is not None else cfg.extra.get("watchdog", True):
                 self.watchdog = Watchdog(comm, timeout_s=cfg.timeout_s)
-        if broadcast and self.world > 1:
+        if broadcast and self.communicate:
             self.broadcast_parameters(root_rank)
         self._next_launch = 0
         self._direct_cache: dict = {}
@@ -282,7 +282,8 @@ class DDP:
             bufs = [t for t in self.module.buffers() if t.numel() > 0]
             if bufs:
                 from .bucket import broadcast_tensors
-                broadcast_tensors([t.data for t in bufs], root_rank, comm=self.comm)
+                broadcast_tensors([t.detach() for t in bufs], root_rank, comm=self.comm,
+                                  force_comm=self.force_comm)
 
     # ------------------------------------------------------------------ hooks
     @contextmanager

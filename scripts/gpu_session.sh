@@ -39,6 +39,7 @@ for s in $STEPS; do
                    --batch 32 --same-device ;;
     probe2) step probe2 120 0 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
               --master-addr 127.0.0.1 --master-port 29521 scripts/probe_two_ranks_one_gpu.py ;;
+    vit_gemm) step vit_gemm 300 0 python scripts/bench_vit_gemm.py ;;
     prof) prof resnet50 --steps 5 --warmup 5 ;;
     prof_comm) prof resnet50_comm --steps 5 --warmup 5 --force-comm ;;
     prof_vit) prof vit --model vit_b16 --steps 5 --warmup 5 ;;

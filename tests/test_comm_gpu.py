@@ -77,6 +77,37 @@ def test_force_comm_bitwise_equal(gpu_ext, grad_mode, dtype):
         assert torch.equal(p, q)
 
 
+def test_force_comm_bench_construction(gpu_ext):
+    """bench.py's DDP construction at N>1: parameter + buffer broadcast (fp32 BN stats, int64
+    step counters that the pack kernels cannot move) and a step, over real RCCL calls."""
+    _init()
+    from fluxmpi_amd import optimisers as O
+    from fluxmpi_amd.models.resnet import ResNet
+    from fluxmpi_amd.parallel.ddp import DDP
+
+    def build():
+        torch.manual_seed(11)
+        m = ResNet((1, 1, 1, 1), 10, conv_impl="hybrid", norm="fused").to("cuda", memory_format=torch.channels_last)
+        for mod in m.modules():
+            if not (isinstance(mod, torch.nn.modules.batchnorm._BatchNorm) or type(mod).__name__ == "FusedBatchNorm2d"):
+                for p in mod.parameters(recurse=False):
+                    p.data = p.data.to(torch.bfloat16)
+        return m
+
+    m1, m2 = build(), build()
+    assert any(b.dtype == torch.int64 for b in m1.buffers())
+    d1 = DDP(m1, O.Adam(1e-3), average=True, force_comm=True)
+    d2 = DDP(m2, O.Adam(1e-3), average=True)
+    x = torch.randn(8, 3, 32, 32, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (8,), device="cuda")
+    for d in (d1, d2):
+        F.cross_entropy(d(x).float(), y).backward()
+        d.step()
+    torch.cuda.synchronize()
+    for p, q in zip(m1.parameters(), m2.parameters()):
+        torch.testing.assert_close(p, q, rtol=0, atol=2e-3)
+
+
 def test_force_comm_bf16_wire(gpu_ext):
     """fp32 gradients sent as bf16 (K5 cast kernels around a real RCCL call)."""
     _init()
