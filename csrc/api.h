@@ -223,6 +223,10 @@ void groupnorm_nhwc_bwd(const void* dy, const void* h, const float* mean, const 
 // dh = dy * gelu'(h) (exact erf form); partials[blocks][N] = per-workgroup column sums of dh
 // (sum with gemm_splitk_reduce). N/8 must be a multiple of 64, <= 1024.
 int gelu_bwd_bias_blocks(int64_t rows);
+// Column sums of a row-major [rows][N] matrix (N % 8 == 0, N <= 8192) into per-workgroup fp32
+// partial rows [blocks][N] (sum them with gemm_splitk_reduce): the bias gradient of a Linear.
+int colsum_blocks(int64_t rows);
+void colsum(const void* x, float* partials, int blocks, int64_t rows, int64_t N, int dtype, hipStream_t stream);
 void gelu_bwd_bias(const void* dy, const void* h, void* dh, float* partials, int blocks, int64_t rows, int64_t N,
                    int dtype, hipStream_t stream);
 

@@ -203,6 +203,10 @@ PYBIND11_MODULE(_C, m) {
 
   // ---- GELU backward + bias gradient -------------------------------------------------
   m.def("gelu_bwd_bias_blocks", &gelu_bwd_bias_blocks);
+  m.def("colsum_blocks", &colsum_blocks);
+  m.def("colsum", [](uintptr_t x, uintptr_t part, int blocks, int64_t rows, int64_t N, int dtype, uintptr_t stream) {
+    colsum(reinterpret_cast<const void*>(x), reinterpret_cast<float*>(part), blocks, rows, N, dtype, S(stream));
+  });
   m.def("gelu_bwd_bias", [](uintptr_t dy, uintptr_t h, uintptr_t dh, uintptr_t part, int blocks, int64_t rows,
                             int64_t N, int dtype, uintptr_t stream) {
     gelu_bwd_bias(reinterpret_cast<const void*>(dy), reinterpret_cast<const void*>(h), reinterpret_cast<void*>(dh),

@@ -73,7 +73,87 @@ __global__ __launch_bounds__(1024) void gelu_bwd_bias_kernel(const T* __restrict
   for (int j = 0; j < 8; ++j) out[j] = acc[j];
 }
 
+// Column sums of a row-major [rows][N] matrix (the bias gradient of a Linear: db = sum_rows dy),
+// any N % 8 == 0: a workgroup is R row-phases x V = N/8 column vectors (V*R <= 1024); each lane
+// keeps the fp32 sums of its 8 columns over the rows of its phase (kU rows' loads in flight per
+// iteration), the R phases are combined through LDS and each workgroup stores one fp32 partial
+// row (summed by gemm_splitk_reduce, which also casts).
+template <typename T>
+__global__ __launch_bounds__(1024) void colsum_kernel(const T* __restrict__ x, float* __restrict__ part, int64_t rows,
+                                                      int64_t N, int64_t rows_per_wg, int R) {
+  extern __shared__ float red[];  // [R][N]
+  const int V = static_cast<int>(N / 8);
+  const int cv = threadIdx.x % V, ph = threadIdx.x / V;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_wg;
+  int64_t r1 = r0 + rows_per_wg;
+  if (r1 > rows) r1 = rows;
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  constexpr int kU = 4;
+  int64_t r = r0 + ph;
+  for (; r + (kU - 1) * R < r1; r += kU * R) {
+    T v[kU][8];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) load8(x + (r + u * R) * N + cv * 8, v[u]);
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += to_f(v[u][j]);
+  }
+  for (; r < r1; r += R) {
+    T v[8];
+    load8(x + r * N + cv * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += to_f(v[j]);
+  }
+  if (ph < R) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[ph * N + cv * 8 + j] = acc[j];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < N; c += blockDim.x) {
+    float s = 0.f;
+    for (int q = 0; q < R; ++q) s += red[q * N + c];
+    part[static_cast<int64_t>(blockIdx.x) * N + c] = s;
+  }
+}
+
 }  // namespace
+
+int colsum_blocks(int64_t rows) {
+  int64_t b = rows / 64;  // >= 64 rows per workgroup, at most 1024 workgroups
+  if (b > 1024) b = 1024;
+  if (b < 1) b = 1;
+  return static_cast<int>(b);
+}
+
+void colsum(const void* x, float* partials, int blocks, int64_t rows, int64_t N, int dtype, hipStream_t stream) {
+  if (N % 8 != 0 || N / 8 > 1024 || N > 8192)
+    throw std::runtime_error("colsum: need N % 8 == 0 and N <= 8192 (got N=" + std::to_string(N) + ")");
+  if (blocks < 1 || rows < 1) throw std::runtime_error("colsum: bad grid");
+  if ((reinterpret_cast<uintptr_t>(x) & 15u) != 0) throw std::runtime_error("colsum: input must be 16-byte aligned");
+  const int V = static_cast<int>(N / 8);
+  int R = 256 / V;
+  if (R < 1) R = 1;
+  const int64_t rpw = (rows + blocks - 1) / blocks;
+  const unsigned threads = static_cast<unsigned>(V * R);
+  const size_t smem = static_cast<size_t>(R) * N * sizeof(float);
+  switch (dtype) {
+    case kBF16:
+      colsum_kernel<bf16><<<blocks, threads, smem, stream>>>(static_cast<const bf16*>(x), partials, rows, N, rpw, R);
+      break;
+    case kF16:
+      colsum_kernel<f16><<<blocks, threads, smem, stream>>>(static_cast<const f16*>(x), partials, rows, N, rpw, R);
+      break;
+    case kF32:
+      colsum_kernel<float><<<blocks, threads, smem, stream>>>(static_cast<const float*>(x), partials, rows, N, rpw, R);
+      break;
+    default:
+      throw std::runtime_error("colsum: bf16 / fp16 / fp32 only");
+  }
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+}
 
 int gelu_bwd_bias_blocks(int64_t rows) {
   int64_t b = rows / 32;  // >= 32 rows per workgroup, at most 1024 workgroups

@@ -14,19 +14,68 @@ gradient arrival order).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.groupnorm import FusedGroupNorm, skip_param_grads
 
+# Convergence tests read a device value back LAG iterations late (FLUXMPI_DEQ_CHECK_LAG,
+# default 2 on the GPU): the host never drains the queue, so the GPU always has LAG
+# iterations of work in flight while the host waits for an old flag; the price is at most
+# LAG extra (harmless, still-contracting) iterations after convergence. 0 = test every
+# iteration synchronously (the round-1 behaviour: ~11 % of the step idle, profiles/r1_deq_s63).
+CHECK_LAG = int(os.environ.get("FLUXMPI_DEQ_CHECK_LAG", "2"))
 
-def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0):
+
+class LaggedFlags:
+    """Scalars produced on the device, read on the host ``lag`` pushes later without a sync
+    of the whole queue: each value goes to pinned memory by an async copy with an event."""
+
+    def __init__(self, lag: int, n: int):
+        self.lag = lag
+        self.buf = torch.zeros(max(n, 1), dtype=torch.float32, pin_memory=True)
+        self.pending: list = []
+
+    def push(self, i: int, value: torch.Tensor) -> None:
+        self.buf[i:i + 1].copy_(value.reshape(1).float(), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.pending.append((i, ev))
+
+    def pop_ready(self):
+        """``(i, value)`` of the push made ``lag`` pushes ago (blocks on its event only), else None."""
+        if len(self.pending) <= self.lag:
+            return None
+        i, ev = self.pending.pop(0)
+        ev.synchronize()
+        return i, float(self.buf[i])
+
+
+_EYE: dict = {}
+
+
+def _lam_eye(n, lam, device):
+    key = (n, float(lam), str(device))
+    t = _EYE.get(key)
+    if t is None:
+        t = _EYE[key] = lam * torch.eye(n, dtype=torch.float32, device=device)[None]
+    return t
+
+
+def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0, check_lag: int | None = None):
     """Anderson acceleration for ``x = f(x)`` over batch-flattened tensors. Returns (x, iters, rel_residual).
 
     The history Gram matrix and the mix run as single-pass HIP kernels on the GPU
     (``fluxmpi_amd.ops.anderson``). The residual of iterate k is read off the diagonal of
     the Gram matrix computed at the top of iteration k + 1 (same value, no extra pass).
+
+    ``check_lag`` (GPU; default :data:`CHECK_LAG`): the residual test of iterate k is read
+    back ``check_lag`` iterations later (:class:`LaggedFlags`), so the host never waits for
+    the queue to drain; the returned iterate is then the newest one and the residual a 0-d
+    device tensor when the solve ends without convergence. 0: test synchronously (float).
     """
     from ..ops import anderson as AO
 
@@ -61,6 +110,8 @@ def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0):
     H[:, 0, 1:] = H[:, 1:, 0] = 1
     y = torch.zeros(bsz, m + 1, 1, dtype=torch.float32, device=x0.device)
     y[:, 0] = 1
+    lag = (CHECK_LAG if check_lag is None else int(check_lag)) if x0.is_cuda else 0
+    flags = LaggedFlags(lag, max_iter) if lag > 0 else None
     res = float("inf")
     k, converged = 1, False
     for k in range(2, max_iter):
@@ -69,31 +120,44 @@ def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0):
         # stored G = F - X: only the row(s) changed since the last Gram are recomputed
         gram, fn2 = AO.gram(X, Fv, n, last, Gs, (0, 1) if k == 2 else (last,))
         if k > 2:  # residual of the iterate produced by the previous iteration
-            res = float(gram[:, last, last].sum().sqrt() / (1e-5 + fn2.sum().sqrt()))
-            if res < tol:
-                k, converged = k - 1, True
-                break
-        H[:, 1:n + 1, 1:n + 1] = gram + lam * torch.eye(n, dtype=torch.float32, device=x0.device)[None]
-        alpha = torch.linalg.solve(H[:, :n + 1, :n + 1], y[:, :n + 1])[:, 1:n + 1, 0]
+            res_t = gram[:, last, last].sum().sqrt() / (1e-5 + fn2.sum().sqrt())
+            if flags is None:
+                res = float(res_t)
+                if res < tol:
+                    k, converged = k - 1, True
+                    break
+            else:
+                flags.push(k, res_t)
+                hit = flags.pop_ready()
+                if hit is not None and hit[1] < tol:
+                    # iterate hit[0] - 1 converged; the newest one (iteration k - 1) is at least as good
+                    res, k, converged = hit[1], k - 1, True
+                    break
+        H[:, 1:n + 1, 1:n + 1] = gram + _lam_eye(n, lam, x0.device)
+        # solve_ex without error checks: no host sync on the pivots' info
+        alpha = torch.linalg.solve_ex(H[:, :n + 1, :n + 1], y[:, :n + 1], check_errors=False)[0][:, 1:n + 1, 0]
         z = AO.mix(X, Fv, alpha, k % m, beta, dt)
         Fv[:, k % m] = fx(z)
     if not converged:
         s = k % m
-        res = float((Fv[:, s] - X[:, s]).norm() / (1e-5 + Fv[:, s].norm()))
+        res_t = (Fv[:, s] - X[:, s]).norm() / (1e-5 + Fv[:, s].norm())
+        res = res_t if flags is not None else float(res_t)
     return unflat(X[:, k % m].contiguous()).to(dt), k, res
 
 
 class DEQFixedPoint(nn.Module):
-    def __init__(self, f: nn.Module, max_iter=30, tol=1e-4, bwd_iter=30, bwd_tol=1e-4):
+    def __init__(self, f: nn.Module, max_iter=30, tol=1e-4, bwd_iter=30, bwd_tol=1e-4, check_lag: int | None = None):
         super().__init__()
         self.f = f
         self.max_iter, self.tol, self.bwd_iter, self.bwd_tol = max_iter, tol, bwd_iter, bwd_tol
+        self.check_lag = check_lag
         self.last_iters = 0
+        self.last_bwd_iters = 0
 
     def forward(self, x):
         with torch.no_grad():
             z, self.last_iters, _ = anderson(lambda z: self.f(z, x), torch.zeros_like(x), max_iter=self.max_iter,
-                                             tol=self.tol)
+                                             tol=self.tol, check_lag=self.check_lag)
         z = self.f(z, x)  # one differentiable step re-engages autograd at z*
         if not torch.is_grad_enabled():
             return z
@@ -101,14 +165,25 @@ class DEQFixedPoint(nn.Module):
         f0 = self.f(z0, x)
 
         def backward_hook(grad):
+            lag = (CHECK_LAG if self.check_lag is None else int(self.check_lag)) if grad.is_cuda else 0
+            flags = LaggedFlags(lag, self.bwd_iter) if lag > 0 else None
+            thresh = self.bwd_tol * (grad.norm() + 1e-9)  # device scalar, computed once
             u = grad
-            for _ in range(self.bwd_iter):  # u = J^T u + grad
+            it = 0
+            for it in range(self.bwd_iter):  # u = J^T u + grad
                 with skip_param_grads():  # VJPs w.r.t. z only: no GroupNorm dw/db reductions
                     u_new = torch.autograd.grad(f0, z0, u, retain_graph=True)[0] + grad
-                if (u_new - u).norm() <= self.bwd_tol * (grad.norm() + 1e-9):
-                    u = u_new
-                    break
+                done = (u_new - u).norm() <= thresh
                 u = u_new
+                if flags is None:
+                    if bool(done):
+                        break
+                else:  # lagged test: a converged adjoint keeps contracting for <= lag more steps
+                    flags.push(it, done)
+                    hit = flags.pop_ready()
+                    if hit is not None and hit[1] > 0.5:
+                        break
+            self.last_bwd_iters = it + 1
             return u
 
         if z.requires_grad:

@@ -9,7 +9,9 @@ Attention runs our HIP kernels (``csrc/kernels/attention.hip``: MFMA, whole key 
 workgroup) on the packed QKV projection, output written in the projection's layout and the
 three input gradients straight into one packed gradient (``packed_attention``); the patch embedding is a GEMM on the
 unfolded patches; LayerNorms are the fused HIP kernels with the residual adds
-folded in (``fluxmpi_amd.ops.layernorm``).
+folded in (``fluxmpi_amd.ops.layernorm``); every token-major Linear takes its weight
+gradient from the split-K HIP GEMM and its bias gradient from the ``colsum`` kernel
+(``fluxmpi_amd.ops.linear``).
 """
 from __future__ import annotations
 
@@ -20,6 +22,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.gelu import linear_gelu
+from ..ops.linear import Linear
 
 # FLUXMPI_VIT_FUSED_GELU=0: autograd's GELU backward + separate bias reduction (A/B runs)
 _FUSED_GELU = os.environ.get("FLUXMPI_VIT_FUSED_GELU", "1") != "0"
@@ -30,7 +33,7 @@ class PatchEmbed(nn.Module):
         super().__init__()
         self.patch = patch
         self.n = (img // patch) ** 2
-        self.proj = nn.Linear(cin * patch * patch, dim)
+        self.proj = Linear(cin * patch * patch, dim)
 
     def forward(self, x):
         n, c, h, w = x.shape
@@ -116,11 +119,11 @@ class Block(nn.Module):
         from ..ops.layernorm import FusedLayerNorm
         self.heads = heads
         self.ln1 = FusedLayerNorm(dim, eps=1e-6)
-        self.qkv = nn.Linear(dim, 3 * dim)
-        self.proj = nn.Linear(dim, dim)
+        self.qkv = Linear(dim, 3 * dim)
+        self.proj = Linear(dim, dim)
         self.ln2 = FusedLayerNorm(dim, eps=1e-6)
         self.fc1 = nn.Linear(dim, mlp)
-        self.fc2 = nn.Linear(mlp, dim)
+        self.fc2 = Linear(mlp, dim)
 
     def forward(self, x, m=None):
         h = self.heads

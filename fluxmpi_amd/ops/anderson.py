@@ -14,6 +14,20 @@ from . import _ext
 from .multi_tensor import DTYPE_CODE
 
 _MAX_ROWS = 8
+_SYM_IDX: dict = {}
+
+
+def _sym_index(n: int, device) -> torch.Tensor:
+    """[n*n] positions in the packed upper-triangle order of the Gram kernel: H = tot[:, idx]."""
+    key = (n, str(device))
+    t = _SYM_IDX.get(key)
+    if t is None:
+        iu = torch.triu_indices(n, n)
+        pos = torch.empty(n, n, dtype=torch.long)
+        pos[iu[0], iu[1]] = torch.arange(iu.shape[1])
+        pos[iu[1], iu[0]] = torch.arange(iu.shape[1])
+        t = _SYM_IDX[key] = pos.reshape(-1).to(device)
+    return t
 
 
 def _stream(t):
@@ -59,10 +73,8 @@ def gram(X: torch.Tensor, F: torch.Tensor, n: int, last: int, G: torch.Tensor | 
     C.anderson_gram(X.data_ptr(), F.data_ptr(), G.data_ptr() if G is not None else 0, mask, part.data_ptr(), bsz, d,
                     X.stride(1), X.stride(0), n, last, chunks, _stream(X))
     tot = part.sum(1)
-    iu = torch.triu_indices(n, n, device=X.device)
-    H = X.new_zeros(bsz, n, n)
-    H[:, iu[0], iu[1]] = tot[:, : iu.shape[1]]
-    H[:, iu[1], iu[0]] = tot[:, : iu.shape[1]]
+    # one gather (cached symmetric index) instead of building the index and two scatters
+    H = tot.index_select(1, _sym_index(n, X.device)).view(bsz, n, n)
     return H, tot[:, 36]
 
 

@@ -62,8 +62,13 @@ class _LinearGeluFn(torch.autograd.Function):
         dh, db = gelu_bwd_bias(dy, h, ctx.bias_dtype or torch.float32)
         n = h.shape[-1]
         dh2 = dh.reshape(-1, n)
+        x2 = x.reshape(-1, x.shape[-1])
         dx = (dh2 @ w).reshape(x.shape) if ctx.needs_input_grad[0] else None
-        dw = dh2.t() @ x.reshape(-1, x.shape[-1]) if ctx.needs_input_grad[1] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            from .linear import _wgrad_mode, native_ok, weight_grad
+            # long-K weight gradient on the split-K HIP kernel (ops/linear.py)
+            dw = weight_grad(dh2, x2, w.dtype) if _wgrad_mode() == "ours" and native_ok(x2, dh2) else dh2.t() @ x2
         return dx, dw, (db if ctx.has_bias and ctx.needs_input_grad[2] else None)
 
 

@@ -1,0 +1,104 @@
+"""``nn.Linear`` for token-major activations with MI355X-shaped backward GEMMs.
+
+Forward and input gradient stay on hipBLASLt (``F.linear``, ``dy @ W``: M = tokens is
+large, plenty of 256x256 tiles). The weight gradient ``dW = dY^T X`` is the awkward one:
+K = tokens (50432 for ViT-B/16 at batch 256) and a small output (768..3072 squared), so
+hipBLASLt's 256x256 tiles leave most of the 256 CUs idle (36-108 workgroups; 312-431 us
+per call, ``profiles/r1_vit_b16_s61_steady.md``). It runs on our split-K MFMA kernel
+instead (``gemm_wgrad``: LDS-DMA staged, transposed LDS reads, fp32 partials + one reduce;
+split count per shape measured by ``scripts/bench_vit_gemm.py``). The bias gradient is the
+``colsum`` HIP kernel (one read of dy at HBM rate) instead of autograd's generic reduction.
+
+``FLUXMPI_LINEAR_WGRAD=torch`` keeps hipBLASLt for the weight gradient (A/B runs).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.nn.functional as F
+
+from . import _ext
+from .multi_tensor import DTYPE_CODE
+
+# (N_out, N_in) -> split-K factor, from scripts/bench_vit_gemm.py on MI355X (M = 50432 tokens)
+_SPLITS = {(2304, 768): 16, (768, 768): 16, (3072, 768): 8, (768, 3072): 4}
+
+
+def _wgrad_mode() -> str:
+    return os.environ.get("FLUXMPI_LINEAR_WGRAD", "ours")
+
+
+def native_ok(x2: torch.Tensor, dy2: torch.Tensor) -> bool:
+    """Shapes / layouts the HIP weight-gradient and column-sum kernels take."""
+    return (x2.is_cuda and x2.dtype == torch.bfloat16 and dy2.dtype == torch.bfloat16 and x2.is_contiguous()
+            and dy2.is_contiguous() and x2.shape[1] % 8 == 0 and dy2.shape[1] % 8 == 0 and dy2.shape[1] <= 8192
+            and x2.shape[0] >= 1024 and x2.shape[0] < (1 << 31) and x2.data_ptr() % 16 == 0
+            and dy2.data_ptr() % 16 == 0)
+
+
+def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype) -> torch.Tensor:
+    """``dy2^T @ x2`` ([N_out, N_in]) on the split-K HIP kernel (bf16 operands, fp32 accumulation)."""
+    from .gemm import conv1x1_wgrad_v2
+
+    return conv1x1_wgrad_v2(dy2, x2, out_dtype=out_dtype, splits=_SPLITS.get((dy2.shape[1], x2.shape[1])))
+
+
+def bias_grad(dy2: torch.Tensor, out_dtype: torch.dtype) -> torch.Tensor:
+    """Column sums of ``dy2`` [rows, N] -> [N] (fp32 accumulation, cast to ``out_dtype``)."""
+    if not (dy2.is_cuda and dy2.dtype in DTYPE_CODE and dy2.is_contiguous() and dy2.shape[1] % 8 == 0
+            and dy2.shape[1] <= 8192 and dy2.data_ptr() % 16 == 0):
+        return dy2.float().sum(0).to(out_dtype)
+    C = _ext.get(required=True)
+    rows, n = dy2.shape
+    blocks = C.colsum_blocks(rows)
+    part = torch.empty(blocks, n, device=dy2.device, dtype=torch.float32)
+    stream = torch.cuda.current_stream(dy2.device).cuda_stream
+    C.colsum(dy2.data_ptr(), part.data_ptr(), blocks, rows, n, DTYPE_CODE[dy2.dtype], stream)
+    odt = out_dtype if out_dtype in (torch.float32, torch.bfloat16) else torch.float32
+    db = torch.empty(n, device=dy2.device, dtype=odt)
+    C.gemm_splitk_reduce(part.data_ptr(), blocks, n, db.data_ptr(), DTYPE_CODE[odt], stream)
+    return db.to(out_dtype)
+
+
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        ctx.bias_dtype = bias.dtype if bias is not None else None
+        return F.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        n_out, n_in = w.shape
+        dy2 = dy.reshape(-1, n_out)
+        x2 = x.reshape(-1, n_in)
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        dx = (dy2 @ w).reshape(x.shape) if ctx.needs_input_grad[0] else None
+        dw = db = None
+        native = _wgrad_mode() == "ours" and native_ok(x2, dy2)
+        if ctx.needs_input_grad[1]:
+            dw = weight_grad(dy2, x2, w.dtype) if native else dy2.t() @ x2
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = bias_grad(dy2, ctx.bias_dtype) if native else dy2.sum(0).to(ctx.bias_dtype)
+        return dx, dw, db
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
+    """``F.linear`` with the HIP weight/bias-gradient backward for bf16 token-major inputs."""
+    if x.is_cuda and x.dtype == torch.bfloat16 and torch.is_grad_enabled() and weight.requires_grad:
+        return _LinearFn.apply(x, weight, bias)
+    return F.linear(x, weight, bias)
+
+
+class Linear(torch.nn.Linear):
+    """Drop-in ``nn.Linear`` whose backward uses :func:`linear`'s kernels."""
+
+    def forward(self, x):
+        return linear(x, self.weight, self.bias)
+
+
+__all__ = ["linear", "Linear", "weight_grad", "bias_grad", "native_ok"]

@@ -206,3 +206,45 @@ def test_anderson_gram_stored_g_gpu(n):
     torch.testing.assert_close(H.double(), Hr, rtol=1e-4, atol=1e-3 * d ** 0.5)
     torch.testing.assert_close(fn.double(), fr, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(G[:, s], Fv[:, s] - X[:, s])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lag", [1, 2, 3])
+def test_anderson_lagged_check_gpu(lag):
+    """Lagged (no queue drain) convergence tests: at most `lag` extra iterations, same fixed point."""
+    torch.manual_seed(3)
+    d = 256
+    A = torch.randn(d, d, dtype=torch.float64)
+    A = (0.6 * A / torch.linalg.matrix_norm(A, 2)).float()
+    b = torch.randn(16, d)
+    zc, kc, _ = anderson(lambda z: z @ A.T + b, torch.zeros(16, d), max_iter=40, tol=1e-5)
+    Ag, bg = A.cuda(), b.cuda()
+    zg, kg, rg = anderson(lambda z: z @ Ag.T + bg, torch.zeros(16, d, device="cuda"), max_iter=40, tol=1e-5,
+                          check_lag=lag)
+    assert float(rg) < 1e-5 and kc - 2 <= kg <= kc + lag + 2
+    torch.testing.assert_close(zg.cpu(), zc, rtol=1e-4, atol=1e-4)
+    # not converging within max_iter: the residual stays on the device (no sync)
+    z2, k2, r2 = anderson(lambda z: z @ Ag.T + bg, torch.zeros(16, d, device="cuda"), max_iter=4, tol=1e-12,
+                          check_lag=lag)
+    assert isinstance(r2, torch.Tensor) and r2.is_cuda and k2 == 3
+
+
+@pytest.mark.gpu
+def test_deq_lagged_matches_sync():
+    """DEQ forward + implicit backward with lagged checks vs synchronous checks."""
+    from fluxmpi_amd.models.deq import deq_mnist
+    torch.manual_seed(0)
+    m0 = deq_mnist(check_lag=0).cuda()
+    m2 = deq_mnist(check_lag=2).cuda()
+    m2.load_state_dict(m0.state_dict())
+    x = torch.randn(8, 1, 28, 28, device="cuda")
+    y = torch.randint(0, 10, (8,), device="cuda")
+    outs = []
+    for m in (m0, m2):
+        out = m(x)
+        torch.nn.functional.cross_entropy(out, y).backward()
+        outs.append(out.detach())
+    torch.testing.assert_close(outs[0], outs[1], rtol=1e-3, atol=1e-3)
+    for (n, p), q in zip(m0.named_parameters(), m2.parameters()):
+        torch.testing.assert_close(p.grad, q.grad, rtol=2e-2, atol=1e-4, msg=n)
+    assert m2.deq.last_bwd_iters <= m0.deq.last_bwd_iters + 2
