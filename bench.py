@@ -127,6 +127,11 @@ def main():
         ddp.step()
         return loss
 
+    if args.graph and args.model == "deq":
+        # the implicit layer's solver lengths are data dependent (host-side loop exits), which a
+        # captured graph cannot express; the lagged device-side checks remove the queue drains instead
+        print("bench.py: --graph is not supported for the DEQ model (data-dependent solver loops)", file=sys.stderr)
+        return 2
     if args.graph:
         from fluxmpi_amd.parallel.graph import GraphedStep
 

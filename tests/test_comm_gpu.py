@@ -105,7 +105,7 @@ def test_force_comm_bench_construction(gpu_ext):
         d.step()
     torch.cuda.synchronize()
     for p, q in zip(m1.parameters(), m2.parameters()):
-        torch.testing.assert_close(p, q, rtol=0, atol=2e-3)
+        torch.testing.assert_close(p, q, rtol=0, atol=4e-3)  # 2 bf16 ulps at |w| < 0.5
 
 
 def test_force_comm_bf16_wire(gpu_ext):
@@ -260,6 +260,11 @@ def worker_two_ranks_one_gpu():
     FluxMPI.Init(gpu_devices=[0, 0])
     r, W = FluxMPI.local_rank(), FluxMPI.total_workers()
     assert FluxMPI.backend_name() == "gloo-device" and FluxMPI.device().index == 0
+    # MIOpen's default solvers are not run-to-run deterministic (two identical fp32 backward
+    # passes of one module differed by up to 4 % of the gradient's max in a 2-block stage on
+    # MI355X); the comparison below is about the communication, so pin deterministic solvers
+    torch.backends.cudnn.deterministic = True
+    torch.backends.cudnn.benchmark = False
     dev = torch.device("cuda", 0)
     torch.manual_seed(5 + r)  # different init per rank: DDP broadcasts rank 0's
     model = ResNet((1, 1, 1, 1), 10, conv_impl="hybrid", norm="fused").to(dev, memory_format=torch.channels_last)
@@ -283,7 +288,8 @@ def worker_two_ranks_one_gpu():
                 p -= 0.05 * p.grad
     torch.cuda.synchronize()
     for (n, p), q in zip(model.named_parameters(), ref.parameters()):
-        torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-3, atol=1e-4, msg=n)
+        tol = 1e-3 * float(q.detach().abs().max()) + 1e-5
+        torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-3, atol=tol, msg=lambda m: f"{n}: {m}")
     # the device-tensor functional paths too: bucketed allreduce + synchronize
     t = torch.full((1000,), float(r + 1), device=dev)
     FluxMPI.allreduce_gradients({"t": t})

@@ -233,9 +233,12 @@ def test_anderson_lagged_check_gpu(lag):
 def test_deq_lagged_matches_sync():
     """DEQ forward + implicit backward with lagged checks vs synchronous checks."""
     from fluxmpi_amd.models.deq import deq_mnist
+    torch.backends.cudnn.deterministic = True  # MIOpen's default solvers vary run to run
     torch.manual_seed(0)
-    m0 = deq_mnist(check_lag=0).cuda()
-    m2 = deq_mnist(check_lag=2).cuda()
+    # tight tolerances: both solves converge, so the lagged run's extra iterations change little
+    kw = dict(max_iter=80, tol=1e-6, bwd_iter=80, bwd_tol=1e-6)
+    m0 = deq_mnist(check_lag=0, **kw).cuda()
+    m2 = deq_mnist(check_lag=2, **kw).cuda()
     m2.load_state_dict(m0.state_dict())
     x = torch.randn(8, 1, 28, 28, device="cuda")
     y = torch.randint(0, 10, (8,), device="cuda")
@@ -246,5 +249,8 @@ def test_deq_lagged_matches_sync():
         outs.append(out.detach())
     torch.testing.assert_close(outs[0], outs[1], rtol=1e-3, atol=1e-3)
     for (n, p), q in zip(m0.named_parameters(), m2.parameters()):
-        torch.testing.assert_close(p.grad, q.grad, rtol=2e-2, atol=1e-4, msg=n)
-    assert m2.deq.last_bwd_iters <= m0.deq.last_bwd_iters + 2
+        # the lagged solve runs up to 2 more (contracting) iterations: differences at the solver tolerance
+        tol = 1e-3 * float(p.grad.abs().max()) + 1e-6
+        torch.testing.assert_close(p.grad, q.grad, rtol=2e-2, atol=tol, msg=lambda m: f"{n}: {m}")
+    assert m0.deq.last_bwd_iters < 80 and m2.deq.last_bwd_iters <= m0.deq.last_bwd_iters + 2
+    assert m0.deq.last_iters < 79 and m2.deq.last_iters <= m0.deq.last_iters + 2

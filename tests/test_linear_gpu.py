@@ -52,6 +52,14 @@ def test_linear_gelu_wgrad_native(gpu_ext):
     linear_gelu(x, w, b).backward(gy)
     wr, br, xr = (t.detach().float().requires_grad_() for t in (w, b, x))
     torch.nn.functional.gelu(torch.nn.functional.linear(xr, wr, br)).backward(gy.float())
-    M = 4 * 197
-    torch.testing.assert_close(w.grad.float(), wr.grad, rtol=3e-2, atol=3e-2 * M ** 0.5 * 0.1)
-    torch.testing.assert_close(b.grad.float(), br.grad, rtol=3e-2, atol=3e-2 * M ** 0.5 * 0.1)
+    # dh is rounded to bf16 before both GEMMs (as in the torch path): compare against the
+    # fp32 reference at the error the bf16 torch GEMM of the same dh makes, with margin
+    from fluxmpi_amd.ops.gelu import gelu_bwd_bias
+    h = torch.nn.functional.linear(x.detach(), w.detach(), b.detach())
+    dh, _ = gelu_bwd_bias(gy, h, torch.bfloat16)
+    dw_torch = (dh.reshape(-1, 3072).t() @ x.detach().reshape(-1, 768)).float()
+    e_ours = (w.grad.float() - wr.grad).abs().max()
+    e_torch = (dw_torch - wr.grad).abs().max()
+    assert e_ours <= 1.5 * e_torch + 1e-3, (float(e_ours), float(e_torch))
+    # db sums 788 bf16-rounded dh values (like the torch path) and is stored in bf16
+    torch.testing.assert_close(b.grad.float(), br.grad, rtol=1e-2, atol=0.25)
