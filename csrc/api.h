@@ -192,6 +192,12 @@ void transpose_filters(const std::vector<uintptr_t>& src, const std::vector<uint
                        hipStream_t stream);
 // out[e] = sum over s < splits of ws[s*n + e] (mode-3 split-K partials; ws is clobbered); out fp32 or bf16
 void gemm_splitk_reduce(const float* ws, int splits, int64_t n, void* out, int out_dtype, hipStream_t stream);
+// Weight gradient on 256 x 256 tiles (wgrad256.hip): ws[split][M][N] = sum over the split's k of
+// A[k][m] * B[k][n] (bf16 A [K][lda], B [K][ldb], M and N multiples of 256), fp32 partials.
+bool wgrad256_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
+int wgrad256_actual_splits(int64_t K, int splits);
+void gemm_wgrad256(const void* a, const void* b, float* ws, int64_t lda, int64_t ldb, int64_t M, int64_t N, int64_t K,
+                   int splits, hipStream_t stream);
 
 // ---- Anderson-acceleration solver (DEQ) --------------------------------------------
 // X, F: fp32 histories [bsz][m rows of row_stride][d] (batch_stride between batches).

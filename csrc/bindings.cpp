@@ -204,6 +204,13 @@ PYBIND11_MODULE(_C, m) {
   // ---- GELU backward + bias gradient -------------------------------------------------
   m.def("gelu_bwd_bias_blocks", &gelu_bwd_bias_blocks);
   m.def("colsum_blocks", &colsum_blocks);
+  m.def("wgrad256_supported", &wgrad256_supported);
+  m.def("wgrad256_actual_splits", &wgrad256_actual_splits);
+  m.def("gemm_wgrad256", [](uintptr_t a, uintptr_t b, uintptr_t ws, int64_t lda, int64_t ldb, int64_t M, int64_t N,
+                            int64_t K, int splits, uintptr_t stream) {
+    gemm_wgrad256(reinterpret_cast<const void*>(a), reinterpret_cast<const void*>(b), reinterpret_cast<float*>(ws), lda,
+                  ldb, M, N, K, splits, S(stream));
+  });
   m.def("colsum", [](uintptr_t x, uintptr_t part, int blocks, int64_t rows, int64_t N, int dtype, uintptr_t stream) {
     colsum(reinterpret_cast<const void*>(x), reinterpret_cast<float*>(part), blocks, rows, N, dtype, S(stream));
   });

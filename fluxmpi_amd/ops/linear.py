@@ -4,9 +4,11 @@ Forward and input gradient stay on hipBLASLt (``F.linear``, ``dy @ W``: M = toke
 large, plenty of 256x256 tiles). The weight gradient ``dW = dY^T X`` is the awkward one:
 K = tokens (50432 for ViT-B/16 at batch 256) and a small output (768..3072 squared), so
 hipBLASLt's 256x256 tiles leave most of the 256 CUs idle (36-108 workgroups; 312-431 us
-per call, ``profiles/r1_vit_b16_s61_steady.md``). It runs on our split-K MFMA kernel
-instead (``gemm_wgrad``: LDS-DMA staged, transposed LDS reads, fp32 partials + one reduce;
-split count per shape measured by ``scripts/bench_vit_gemm.py``). The bias gradient is the
+per call, ``profiles/r1_vit_b16_s61_steady.md``). It runs on our split-K MFMA kernels
+instead: ``wgrad256.hip`` (256x256 tiles, 8 waves, 4-stage LDS-DMA ring, transposed LDS
+reads; 0.91-0.98 PF/s on the ViT shapes) when both widths are multiples of 256, else
+``gemm_glds.hip``'s 128x128 kernel; fp32 partials + one reduce, split counts measured by
+``scripts/bench_vit_gemm.py``. The bias gradient is the
 ``colsum`` HIP kernel (one read of dy at HBM rate) instead of autograd's generic reduction.
 
 ``FLUXMPI_LINEAR_WGRAD=torch`` keeps hipBLASLt for the weight gradient (A/B runs).
@@ -37,11 +39,35 @@ def native_ok(x2: torch.Tensor, dy2: torch.Tensor) -> bool:
             and dy2.data_ptr() % 16 == 0)
 
 
-def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype) -> torch.Tensor:
-    """``dy2^T @ x2`` ([N_out, N_in]) on the split-K HIP kernel (bf16 operands, fp32 accumulation)."""
+# workgroups the 256x256 kernel's split-K aims at (one per CU: 128 KiB of LDS each)
+WG256_TARGET = int(os.environ.get("FLUXMPI_WGRAD256_WG", "256"))
+
+
+def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype, splits: int | None = None) -> torch.Tensor:
+    """``dy2^T @ x2`` ([N_out, N_in]) on the split-K HIP kernels (bf16 operands, fp32 accumulation):
+    the 256x256-tile kernel (``wgrad256.hip``) when both widths are multiples of 256, else the
+    128x128 one (``gemm_glds.hip``)."""
     from .gemm import conv1x1_wgrad_v2
 
-    return conv1x1_wgrad_v2(dy2, x2, out_dtype=out_dtype, splits=_SPLITS.get((dy2.shape[1], x2.shape[1])))
+    K, n_out = dy2.shape
+    n_in = x2.shape[1]
+    C = _ext.get(required=True)
+    if os.environ.get("FLUXMPI_WGRAD256", "1") != "0" and C.wgrad256_supported(n_out, n_in, K, dy2.stride(0),
+                                                                                  x2.stride(0)):
+        tiles = (n_out // 256) * (n_in // 256)
+        # exactly one round of workgroups (floor, not ceil: a second, partial round costs a whole
+        # round — fc1 7 splits x 36 tiles = 252 workgroups ran in 245 us, 8 x 36 = 288 in 375 us)
+        s = splits or max(1, min(WG256_TARGET // tiles, K // 512))
+        s = C.wgrad256_actual_splits(K, s)
+        ws = torch.empty(s, n_out, n_in, device=dy2.device, dtype=torch.float32)
+        stream = torch.cuda.current_stream(dy2.device).cuda_stream
+        C.gemm_wgrad256(dy2.data_ptr(), x2.data_ptr(), ws.data_ptr(), dy2.stride(0), x2.stride(0), n_out, n_in, K, s,
+                        stream)
+        odt = out_dtype if out_dtype in (torch.float32, torch.bfloat16) else torch.float32
+        dw = torch.empty(n_out, n_in, device=dy2.device, dtype=odt)
+        C.gemm_splitk_reduce(ws.data_ptr(), s, dw.numel(), dw.data_ptr(), DTYPE_CODE[odt], stream)
+        return dw.to(out_dtype)
+    return conv1x1_wgrad_v2(dy2, x2, out_dtype=out_dtype, splits=splits or _SPLITS.get((n_out, n_in)))
 
 
 def bias_grad(dy2: torch.Tensor, out_dtype: torch.dtype) -> torch.Tensor:

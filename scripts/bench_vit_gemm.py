@@ -46,14 +46,11 @@ def main():
             "torch": lambda: dy.t() @ x,
             "torch32": lambda: torch.mm(dy.t(), x, out_dtype=torch.float32),
         }
-        for s in (4, 8):
-            if M % s == 0:
-                cands[f"bmm{s}"] = (lambda s=s: torch.bmm(dy.view(s, M // s, no).transpose(1, 2),
-                                                          x.view(s, M // s, ni), out_dtype=torch.float32).sum(0)) \
-                    if False else (lambda s=s: torch.bmm(dy.view(s, M // s, no).transpose(1, 2).float(),
-                                                         x.view(s, M // s, ni).float()).sum(0))
-        for s in (0, 2, 4, 8, 16):
+        for s in (0, 4, 8, 16):
             cands[f"ours{s}"] = lambda s=s: conv1x1_wgrad_v2(dy, x, torch.bfloat16, splits=s or None)
+        from fluxmpi_amd.ops.linear import weight_grad
+        for s in (0, 4, 7, 9, 14, 28):
+            cands[f"w256_{s}"] = lambda s=s: weight_grad(dy, x, torch.bfloat16, splits=s or None)
         for cname, fn in cands.items():
             try:
                 out = fn()

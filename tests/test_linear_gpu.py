@@ -63,3 +63,35 @@ def test_linear_gelu_wgrad_native(gpu_ext):
     assert e_ours <= 1.5 * e_torch + 1e-3, (float(e_ours), float(e_torch))
     # db sums 788 bf16-rounded dh values (like the torch path) and is stored in bf16
     torch.testing.assert_close(b.grad.float(), br.grad, rtol=1e-2, atol=0.25)
+
+
+@pytest.mark.parametrize("shape", [(256, 256), (768, 768), (3072, 768), (768, 3072), (512, 1024)])
+@pytest.mark.parametrize("K", [64, 1000, 50432])
+@pytest.mark.parametrize("splits", [None, 1, 3, 28])
+def test_wgrad256_matches_fp32(gpu_ext, shape, K, splits):
+    """The 256x256-tile weight-gradient kernel (wgrad256.hip) vs an fp32 GEMM of the same bf16 operands."""
+    from fluxmpi_amd.ops.linear import weight_grad
+    n_out, n_in = shape
+    if K * (n_out + n_in) > 120_000_000:
+        pytest.skip("size")
+    assert gpu_ext.wgrad256_supported(n_out, n_in, K, n_out, n_in)
+    g = torch.Generator(device="cuda").manual_seed(K + n_out)
+    dy = torch.randn(K, n_out, device="cuda", generator=g).to(torch.bfloat16)
+    x = torch.randn(K, n_in, device="cuda", generator=g).to(torch.bfloat16)
+    ref = dy.float().t() @ x.float()
+    out = weight_grad(dy, x, torch.float32, splits=splits)
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-3 * K ** 0.5)
+    outb = weight_grad(dy, x, torch.bfloat16, splits=splits)
+    torch.testing.assert_close(outb.float(), ref, rtol=1e-2, atol=1e-2 * K ** 0.5)
+
+
+def test_wgrad256_strided_rows(gpu_ext):
+    """Row strides wider than the matrix (a column slice of a packed projection)."""
+    from fluxmpi_amd.ops.linear import weight_grad
+    K = 4096
+    big = torch.randn(K, 1024, device="cuda").to(torch.bfloat16)
+    x = torch.randn(K, 512, device="cuda").to(torch.bfloat16)
+    dy = big[:, 256:768]
+    ref = dy.float().t() @ x.float()
+    out = weight_grad(dy, x, torch.float32)
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-3 * K ** 0.5)
