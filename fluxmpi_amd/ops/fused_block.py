@@ -195,10 +195,14 @@ class _Conv1x1Hybrid(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             co, ci = weight.shape[0], weight.shape[1]
-            dw = wgrad_best(("1x1", tuple(x.shape), co), {
+            impls = {
                 "miopen": lambda: torch.ops.aten.convolution_backward(dc, x, weight, None, [1, 1], [0, 0], [1, 1], False,
                                                                       [0, 0], 1, [False, True, False])[1],
-                "ours": lambda: G.conv1x1_wgrad_v2(_nhwc2d(dc), _nhwc2d(x), out_dtype=weight.dtype).view(co, ci, 1, 1)})
+                "ours": lambda: G.conv1x1_wgrad_v2(_nhwc2d(dc), _nhwc2d(x), out_dtype=weight.dtype).view(co, ci, 1, 1)}
+            if _w256_ok(co, ci, dc):
+                from .linear import weight_grad
+                impls["w256"] = lambda: weight_grad(_nhwc2d(dc), _nhwc2d(x), weight.dtype).view(co, ci, 1, 1)
+            dw = wgrad_best(("1x1", tuple(x.shape), co), impls)
         return dx, dw, None, None, None
 
 
@@ -501,6 +505,14 @@ _WG_CHOICE: dict = {}
 _WG_CONFIGS = ((2, 512), (2, 768), (2, 1024), (2, 384))  # (variant, target workgroups); s44 sweep
 
 
+def _w256_ok(co: int, ci: int, dc: torch.Tensor) -> bool:
+    if os.environ.get("FLUXMPI_WGRAD256", "1") == "0" or dc.dtype != torch.bfloat16:
+        return False
+    C = _ext.get(required=True)
+    k = dc.numel() // co
+    return bool(C.wgrad256_supported(co, ci, k, co, ci)) and k >= 4096
+
+
 def wgrad_best(key, impls: dict):
     """Run the fastest weight-gradient implementation for ``key`` (measured on first use, like
     cudnn.benchmark: MIOpen vs our kernel in each of ``_WG_CONFIGS``) and return its result."""
@@ -521,6 +533,10 @@ def wgrad_best(key, impls: dict):
                         best = (t, ("ours", cfg))
             finally:
                 G.WGRAD_VARIANT, G.WGRAD_TARGET_WG = saved
+            if "w256" in impls:  # 256x256-tile kernel (wgrad256.hip) where both widths allow it
+                t = _time_us(impls["w256"])
+                if t < best[0]:
+                    best = (t, ("w256", None))
             choice = best[1]
         _WG_CHOICE[key] = choice
     name, cfg = choice
