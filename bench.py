@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--force-comm", action="store_true",
                     help="issue the gradient collectives even at N=1 (hooks, packing, RCCL on the comm "
                          "stream): measures the data-parallel layer's own cost on one GPU")
+    ap.add_argument("--emulate-comm", default="",
+                    help="WGS:GBPS — with --force-comm at N=1, hold WGS workgroups on the comm stream for the "
+                         "time an 8-rank ring allreduce of each bucket takes at GBPS (RCCL's CU footprint)")
     ap.add_argument("--same-device", action="store_true",
                     help="all ranks on cuda:0 with gloo collectives on device tensors (RCCL refuses a "
                          "shared GPU): runs the N>1 code path on a 1-GPU box; no throughput claim")
@@ -79,6 +82,8 @@ def main():
         # results are written back at exit: keep that copy out of the repository
         torch.cuda.tunable.set_filename(os.path.join(os.environ.get("TMPDIR", "/tmp"),
                                                      f"fluxmpi_tunableop_{os.getuid()}_{args.model}.csv"))
+    if args.emulate_comm:
+        os.environ["FLUXMPI_EMULATE_COMM"] = args.emulate_comm
     if args.same_device:
         os.environ["FLUXMPI_BACKEND"] = "gloo-device"
         FluxMPI.Init(gpu_devices=[0] * int(os.environ.get("WORLD_SIZE", "1")))
@@ -179,7 +184,9 @@ def main():
                        "tunableop": use_tunableop, "loss": round(lval, 4),
                        # what the data-parallel layer actually did: at N=1 nothing is communicated
                        # (overlap false, comm "none") unless --force-comm
-                       **cs, "exposed_comm_ms": None if exposed is None else round(exposed, 3)},
+                       **cs, "exposed_comm_ms": None if exposed is None else round(exposed, 3),
+                       **({"emulate_comm": args.emulate_comm} if args.emulate_comm else {}),
+                       "grid_rounds": int(os.environ.get("FLUXMPI_GRID_ROUNDS", "1"))},
         }
         print(json.dumps(rec), flush=True)
     FluxMPI.Finalize()

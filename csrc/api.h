@@ -232,6 +232,9 @@ int gelu_bwd_bias_blocks(int64_t rows);
 // Column sums of a row-major [rows][N] matrix (N % 8 == 0, N <= 8192) into per-workgroup fp32
 // partial rows [blocks][N] (sum them with gemm_splitk_reduce): the bias gradient of a Linear.
 int colsum_blocks(int64_t rows);
+// Measurement tool: `blocks` workgroups holding their CU slots for `microseconds` of wall time
+// on `stream` (stands in for RCCL's kernels at world size 1, where RCCL launches none).
+void emulate_comm(int blocks, double microseconds, hipStream_t stream, int threads, int lds_bytes);
 void colsum(const void* x, float* partials, int blocks, int64_t rows, int64_t N, int dtype, hipStream_t stream);
 void gelu_bwd_bias(const void* dy, const void* h, void* dh, float* partials, int blocks, int64_t rows, int64_t N,
                    int dtype, hipStream_t stream);

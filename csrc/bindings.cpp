@@ -204,6 +204,9 @@ PYBIND11_MODULE(_C, m) {
   // ---- GELU backward + bias gradient -------------------------------------------------
   m.def("gelu_bwd_bias_blocks", &gelu_bwd_bias_blocks);
   m.def("colsum_blocks", &colsum_blocks);
+  m.def("emulate_comm", [](int blocks, double us, uintptr_t stream, int threads, int lds) {
+    emulate_comm(blocks, us, S(stream), threads, lds);
+  });
   m.def("wgrad256_supported", &wgrad256_supported);
   m.def("wgrad256_actual_splits", &wgrad256_actual_splits);
   m.def("gemm_wgrad256", [](uintptr_t a, uintptr_t b, uintptr_t ws, int64_t lda, int64_t ldb, int64_t M, int64_t N,

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <stdexcept>
@@ -82,6 +83,19 @@ __device__ __forceinline__ int find_tensor(const int32_t (&start)[N], int n, int
 // launched with exactly this many workgroups run as one full round — no partial last
 // round of workgroups (a 2048-block grid on a 7-block/CU kernel is 1.14 rounds: the
 // 0.14 tail costs as much as a whole round).
+// Rounds of resident workgroups a "persistent" grid is sized to (FLUXMPI_GRID_ROUNDS, default 1).
+// With several rounds, a kernel sharing the chip with others (RCCL's workgroups during the
+// backward/allreduce overlap) ends with a partial round instead of waiting a whole extra one
+// for the slots the other kernel holds.
+inline int grid_rounds() {
+  static int r = [] {
+    const char* e = std::getenv("FLUXMPI_GRID_ROUNDS");
+    const int v = e != nullptr ? std::atoi(e) : 1;
+    return v < 1 ? 1 : (v > 16 ? 16 : v);
+  }();
+  return r;
+}
+
 inline int resident_blocks(const void* kernel, int threads, size_t smem) {
   static std::mutex mu;
   static std::map<std::tuple<const void*, int, size_t, int>, int> cache;
@@ -95,7 +109,7 @@ inline int resident_blocks(const void* kernel, int threads, size_t smem) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, smem) != hipSuccess || per_cu < 1)
     per_cu = 1;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
-  const int n = per_cu * cus;
+  const int n = per_cu * cus * grid_rounds();
   cache.emplace(key, n);
   return n;
 }

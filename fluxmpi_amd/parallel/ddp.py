@@ -45,6 +45,7 @@ into the flat moment buffers).
 """
 from __future__ import annotations
 
+import os
 from contextlib import contextmanager
 from dataclasses import dataclass, field
 
@@ -151,6 +152,16 @@ class DDP:
             raise RuntimeError("DDP(force_comm=True) needs a communicator: call fluxmpi_amd.Init() first")
         # collectives are issued whenever there is a peer, or when forced (world-1 rehearsal)
         self.communicate = comm is not None and (self.world > 1 or self.force_comm)
+        # measurement tool (FLUXMPI_EMULATE_COMM="WGS:GBPS[:THREADS[:LDS_KB]]"): with each bucket's
+        # collective, hold WGS workgroups (THREADS threads, LDS_KB of LDS each) on the comm stream
+        # for the time a ring allreduce of the bucket would take at GBPS bus bandwidth on 8
+        # ranks — RCCL's CU footprint, which a world of one lacks
+        self._emulate = None
+        emu = cfg.extra.get("emulate_comm") or os.environ.get("FLUXMPI_EMULATE_COMM", "")
+        if emu and self.communicate and self.device.type == "cuda":
+            f = emu.split(":")
+            self._emulate = (int(f[0]), float(f[1]), int(f[2]) if len(f) > 2 else 256,
+                             int(f[3]) * 1024 if len(f) > 3 else 0)
         if comm_dtype is None:
             comm_dtype = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16,
                           "bfloat16": torch.bfloat16, "fp16": torch.float16}.get(cfg.comm_dtype)
@@ -324,6 +335,12 @@ class DDP:
             mt.pack([b.flat_grad], b.comm_buf, [0])
             buf = b.comm_buf
         with profiling.range(f"fluxmpi.allreduce.bucket{b.index}"):
+            if self._emulate is not None and hasattr(self.comm, "stream"):
+                wgs, gbps, thr, lds = self._emulate
+                nbytes = buf.numel() * buf.element_size()
+                us = 2.0 * 7.0 / 8.0 * nbytes / (gbps * 1e3)  # ring allreduce, 8 ranks
+                self.comm.stream.wait_stream(torch.cuda.current_stream(self.device))
+                _ext.get(required=True).emulate_comm(wgs, max(us, 5.0), self.comm.stream.cuda_stream, thr, lds)
             b.work = self.comm.allreduce(buf, ReduceOp.SUM, async_op=True)
         if self.watchdog is not None:
             self.watchdog.track(b.work, f"allreduce of gradient bucket {b.index} ({b.numel} elements)")
