@@ -34,7 +34,9 @@
 // 16+4g+j-4 (j>=4); the A operand reads the same rows from a transposed LDS image as two
 // 8-byte pieces.  1-D grid with an XCD-aware order (the blocks of one (b, h) share an L2).
 #include <cmath>
+#include <cstdlib>
 #include <stdexcept>
+#include <string>
 
 #include "../api.h"
 #include "common.h"
@@ -369,6 +371,139 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Forward with the whole (b, h) resident: one workgroup per (batch, head), one wave per 16
+// queries (T <= 256: up to 16 waves). K and V of the head are staged ONCE into LDS by
+// LDS-DMA (8-row x 128-B pieces, zero rows past T), so each is read from HBM exactly once
+// (the 64-query-block kernel above re-stages them for every query block, and its last block
+// of a T = 197 head holds 5 real queries of 64). A wave then computes all of its query
+// column's scores S^T = K Q^T (every key tile), the exact softmax in registers (no online
+// rescale: the whole row is there), and O^T = V^T P^T with V^T fragments taken by
+// ds_read_b64_tr_b16 from the row-major V image (no transposed LDS writes).
+// Chunk-slot swizzles: K image slot = chunk ^ ((row >> 1) & 7) (16-row row reads), V image
+// slot = chunk ^ (((row >> 1) & 3) << 1) (the 8 rows of a half-wave's transposed read land
+// on 8 distinct 32-B bank groups).
+constexpr int kResMaxT = 256;
+
+__device__ __forceinline__ int swz_k(int r) { return (r >> 1) & 7; }
+__device__ __forceinline__ int swz_v(int r) { return ((r >> 1) & 3) << 1; }
+
+__device__ __attribute__((aligned(16))) uint4 g_attn_zero[4];
+
+// LDS-DMA of rows [0, rows) of a [T][64] head operand (row stride st) into a swizzled 128-B-row
+// image; rows >= T read a zero line. Pieces are spread over the workgroup's waves.
+template <bool V>
+__device__ __forceinline__ void stage_rows(char* img, const bf16* __restrict__ base, int64_t st, int rows, int T) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  for (int pc = wave; pc < rows / 8; pc += nw) {
+    const int row = 8 * pc + (lane >> 3);
+    const int chunk = (lane & 7) ^ (V ? swz_v(row) : swz_k(row));
+    const void* src = row < T ? static_cast<const void*>(base + static_cast<int64_t>(row) * st + chunk * 8)
+                              : static_cast<const void*>(g_attn_zero);
+    typedef __attribute__((address_space(3))) char lds_char;
+    typedef __attribute__((address_space(1))) void gl_void;
+    __builtin_amdgcn_global_load_lds((gl_void*)(src), (lds_char*)(img + pc * 1024), 16, 0, 0);
+  }
+}
+
+__global__ __launch_bounds__(1024) void attn_fwd_res_kernel(AttnBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int TP = (a.T + 15) & ~15, TV = (a.T + 31) & ~31;
+  char* kimg = smem;
+  char* vimg = smem + TP * 128;
+  int id = blockIdx.x;
+  const int total = a.B * a.H;
+  if ((total & 7) == 0) id = (id & 7) * (total >> 3) + (id >> 3);
+  const int h = id % a.H, b = id / a.H;
+  stage_rows<false>(kimg, a.k + b * a.sq_b + h * DH, a.sq_t, TP, a.T);
+  stage_rows<true>(vimg, a.v + b * a.sq_b + h * DH, a.sq_t, TV, a.T);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, col = lane & 15, g = lane >> 4;
+  const int q0 = 16 * w;
+  const int qi = q0 + col;
+  const bool qok = qi < a.T;
+  const int64_t qoff = b * a.sq_b + static_cast<int64_t>(qi) * a.sq_t + h * DH;
+  bf16x8 qf[2] = {};
+  if (qok) {  // issued before the wait: the Q loads fly with the staging DMA
+    qf[0] = ld8(a.q + qoff + 8 * g);
+    qf[1] = ld8(a.q + qoff + 32 + 8 * g);
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (q0 >= a.T) return;  // wave-uniform: no partial EXEC below (the transposed reads need all lanes)
+  const int nt = TP / 16;
+  const float c2 = a.scale * kLog2e;
+  f32x4 x[kResMaxT / 16];
+  float m = -kInf;
+#pragma unroll
+  for (int kt = 0; kt < kResMaxT / 16; ++kt) {
+    x[kt] = f32x4{-kInf, -kInf, -kInf, -kInf};
+    if (kt < nt) {
+      const int row = 16 * kt + col;
+      const bf16* kr = reinterpret_cast<const bf16*>(kimg + row * 128);
+      const bf16x8 k0 = *reinterpret_cast<const bf16x8*>(kr + ((g ^ swz_k(row)) << 3));
+      const bf16x8 k1 = *reinterpret_cast<const bf16x8*>(kr + (((4 + g) ^ swz_k(row)) << 3));
+      f32x4 s = {};
+      s = mfma(k0, qf[0], s);
+      s = mfma(k1, qf[1], s);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = 16 * kt + 4 * g + r;
+        x[kt][r] = key < a.T ? s[r] * c2 : -kInf;
+        m = fmaxf(m, x[kt][r]);
+      }
+    }
+  }
+  m = fmaxf(m, __shfl_xor(m, 16));
+  m = fmaxf(m, __shfl_xor(m, 32));
+  float l = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < kResMaxT / 16; ++kt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float pv = kt < nt ? exp2f(x[kt][r] - m) : 0.f;  // -inf (padded key) -> 0
+      x[kt][r] = pv;
+      l += pv;
+    }
+  l += __shfl_xor(l, 16);
+  l += __shfl_xor(l, 32);
+  // O^T[d][q] = sum over keys of V^T[d][key] P^T[key][q]; k-step ks covers keys 32ks .. +31 in
+  // the accumulator-pair order (j < 4: 32ks + 4g + j, j >= 4: 32ks + 16 + 4g + j - 4)
+  f32x4 acc[4] = {};
+  const int qv = lane >> 2 & 3, pv4 = lane & 3;  // transposed-read roles: row q of the block, column quad p
+#pragma unroll
+  for (int ks = 0; ks < kResMaxT / 32; ++ks) {
+    if (32 * ks < TV) {
+      const bf16x8 bop = pack(x[2 * ks], x[2 * ks + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int r0 = 32 * ks + 4 * g + qv, r1 = r0 + 16;
+        const int cch = 2 * dt + (pv4 >> 1);
+        const char* a0 = vimg + r0 * 128 + ((cch ^ swz_v(r0)) << 4) + (pv4 & 1) * 8;
+        const char* a1 = vimg + r1 * 128 + ((cch ^ swz_v(r1)) << 4) + (pv4 & 1) * 8;
+        typedef short short4v __attribute__((ext_vector_type(4)));
+        typedef __attribute__((address_space(3))) short4v lds_short4v;
+        short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(a0));
+        short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(a1));
+        bf16x8 vop;
+        __builtin_memcpy(&vop, &lo, 8);
+        __builtin_memcpy(reinterpret_cast<char*>(&vop) + 8, &hi, 8);
+        acc[dt] = mfma(vop, bop, acc[dt]);
+      }
+    }
+  }
+  if (qok) {
+    const float inv = 1.f / l;
+    bf16* op = a.o_out + b * a.so_b + static_cast<int64_t>(qi) * a.so_t + h * a.so_h;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const bf16x4 o = {(bf16)(acc[dt][0] * inv), (bf16)(acc[dt][1] * inv), (bf16)(acc[dt][2] * inv),
+                        (bf16)(acc[dt][3] * inv)};
+      *reinterpret_cast<bf16x4*>(op + dt * 16 + 4 * g) = o;
+    }
+    if (g == 0) a.stats[((static_cast<int64_t>(b) * a.H + h) * a.T + qi) * 2] = m + __log2f(l);
+  }
+}
+
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 }  // namespace
@@ -419,6 +554,20 @@ void attn_fwd(const void* q, const void* k, const void* v, void* o, float* stats
   a.H = H;
   a.nblk = (T + 63) / 64;
   a.scale = scale;
+  static const bool resident = [] {
+    const char* e = std::getenv("FLUXMPI_ATTN_FWD");
+    return e == nullptr || std::string(e) != "blocked";
+  }();
+  if (resident && T <= kResMaxT && (sq_t % 8) == 0) {
+    // whole head resident in LDS: one workgroup per (b, h), one wave per 16 queries
+    const int64_t total = static_cast<int64_t>(B) * H;
+    if (total > 0x7fffffff) throw std::runtime_error("attn_fwd: grid too large");
+    const int waves = (T + 15) / 16;
+    const size_t lds = static_cast<size_t>(((T + 15) & ~15) + ((T + 31) & ~31)) * 128;
+    attn_fwd_res_kernel<<<static_cast<unsigned>(total), waves * 64, lds, s>>>(a);
+    FLUXMPI_HIP_CHECK(hipGetLastError());
+    return;
+  }
   const int64_t total = static_cast<int64_t>(B) * H * a.nblk;
   if (total > 0x7fffffff) throw std::runtime_error("attn_fwd: grid too large");
   attn_fwd_kernel<<<static_cast<unsigned>(total), 256, 0, s>>>(a);

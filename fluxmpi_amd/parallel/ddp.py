@@ -193,6 +193,7 @@ class DDP:
             self.broadcast_parameters(root_rank)
         self._next_launch = 0
         self._direct_cache: dict = {}
+        self._views: dict = {}
         self._record_versions()
         self.zero_grad()
         self.step_count = 0
@@ -383,29 +384,45 @@ class DDP:
         if self.grad_mode != "steal" or b.packed:
             return
         b.packed = True
-        srcs, offs = [], []
-        for p, o in zip(b.params, b.offsets):
+        views = self._grad_views(b)
+        srcs, dptrs, ns = [], [], []
+        for p, dst, dptr in views:
             g = p.grad
-            dst = _strided_view(b.flat_grad, p, o)
             if g is None:
                 dst.zero_()
-            elif g.data_ptr() == dst.data_ptr() and _same_layout(g, dst):
-                continue  # already in place (e.g. user set p.grad to the view)
+            elif g.data_ptr() == dptr:
+                if not _same_layout(g, dst):
+                    dst.copy_(g.clone())
+                # else already in place (e.g. user set p.grad to the view)
+            elif g.dtype is b.dtype and g.is_cuda and g.stride() == dst.stride():
+                # the common case: autograd's layout contract (the parameter's dense strides)
+                srcs.append(g)
+                dptrs.append(dptr)
+                ns.append(dst.numel())
             elif g.is_cuda and g.dtype == b.dtype and _same_layout(g, p) and _is_dense(g):
                 srcs.append(g)
-                offs.append(o)
+                dptrs.append(dptr)
+                ns.append(dst.numel())
             else:
                 dst.copy_(g)
         if srcs:
             C = _ext.get(required=True)
+            code = mt.DTYPE_CODE[b.dtype]
+            C.mt_copy([g.data_ptr() for g in srcs], dptrs, ns, code, code, 1.0,
+                      torch.cuda.current_stream(b.device).cuda_stream)
+        # from here on p.grad aliases the (soon reduced) flat buffer, as in "view" mode
+        for p, dst, _ in views:
+            p.grad = dst
+
+    def _grad_views(self, b: _Bucket) -> list:
+        """``(param, view of its flat-gradient slice, slice address)`` per parameter (cached)."""
+        v = self._views.get(b.index)
+        if v is None:
             es = b.flat_grad.element_size()
             base = b.flat_grad.data_ptr()
-            code = mt.DTYPE_CODE[b.dtype]
-            C.mt_copy([g.data_ptr() for g in srcs], [base + o * es for o in offs], [g.numel() for g in srcs],
-                      code, code, 1.0, torch.cuda.current_stream(b.device).cuda_stream)
-        # from here on p.grad aliases the (soon reduced) flat buffer, as in "view" mode
-        for p, o in zip(b.params, b.offsets):
-            p.grad = _strided_view(b.flat_grad, p, o)
+            v = [(p, _strided_view(b.flat_grad, p, o), base + o * es) for p, o in zip(b.params, b.offsets)]
+            self._views[b.index] = v
+        return v
 
     def reduce_gradients(self):
         """Make sure every bucket has been allreduced (launch the rest, in order) and wait."""
@@ -533,9 +550,11 @@ class DDP:
         grads = []
         for p in b.params:
             g = p.grad
-            if g is None or g.dtype != b.dtype or g.device != b.device or not _same_layout(g, p) \
-                    or not _is_dense(g):
+            if g is None:
                 return False
+            if not (g.dtype is b.dtype and g.stride() == p.stride() and g.device == b.device):
+                if g.dtype != b.dtype or g.device != b.device or not _same_layout(g, p) or not _is_dense(g):
+                    return False
             grads.append(g)
         st = self._direct_cache.get(b.index)
         if st is None:
