@@ -75,6 +75,10 @@ struct AttnBwdArgs {
 
 __device__ __forceinline__ bf16x8 ld8(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
+// 2^x as the bare v_exp_f32 (exp2f adds a denormal range check and rescale around it: five
+// more VALU instructions per element; softmax weights below 2^-126 may flush to zero)
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 __device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -176,7 +180,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnBwdArgs a) {
     mx = fmaxf(mx, __shfl_xor(mx, 16));
     mx = fmaxf(mx, __shfl_xor(mx, 32));
     const float mn = fmaxf(m, mx);  // finite from the first chunk on (key 0 is real)
-    const float f = exp2f(m - mn);
+    const float f = fast_exp2(m - mn);
     m = mn;
     l *= f;
 #pragma unroll
@@ -186,7 +190,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnBwdArgs a) {
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        p[kt][r] = exp2f(x[kt][r] - m);
+        p[kt][r] = fast_exp2(x[kt][r] - m);
         l += p[kt][r];
       }
     const bf16x8 bop = pack(p[0], p[1]);
@@ -267,7 +271,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
       dp = mfma(ld8(vp), gf[0], dp);
       dp = mfma(ld8(vp + 32), gf[1], dp);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) ds[kt][r] = exp2f(fmaf(s[r], c2, -lse)) * (dp[r] - dsum);
+      for (int r = 0; r < 4; ++r) ds[kt][r] = fast_exp2(fmaf(s[r], c2, -lse)) * (dp[r] - dsum);
     }
     const bf16x8 bop = pack(ds[0], ds[1]);
 #pragma unroll
@@ -347,7 +351,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int qq = qt * 16 + 4 * g + r;
-        const float pv = exp2f(fmaf(s[r], c2, -sL[qq]));
+        const float pv = fast_exp2(fmaf(s[r], c2, -sL[qq]));
         p[qt][r] = pv;
         ds[qt][r] = pv * (dp[r] - sD[qq]);
       }
@@ -380,13 +384,38 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnBwdArgs a) {
 // column's scores S^T = K Q^T (every key tile), the exact softmax in registers (no online
 // rescale: the whole row is there), and O^T = V^T P^T with V^T fragments taken by
 // ds_read_b64_tr_b16 from the row-major V image (no transposed LDS writes).
-// Chunk-slot swizzles: K image slot = chunk ^ ((row >> 1) & 7) (16-row row reads), V image
-// slot = chunk ^ (((row >> 1) & 3) << 1) (the 8 rows of a half-wave's transposed read land
-// on 8 distinct 32-B bank groups).
+// Chunk-slot swizzle of the 128-B-row images, slot = chunk ^ ((((row >> 1) & 3) << 1) |
+// ((row >> 3) & 1)): the 16 rows of a row read (ds_read_b128, same chunk) land on 16
+// distinct 16-B bank slots, and the 8 rows of a half-wave's transposed read (two 4-row
+// blocks, one 32-B column pair) on 8 distinct 32-B groups — one image serves both reads.
 constexpr int kResMaxT = 256;
 
-__device__ __forceinline__ int swz_k(int r) { return (r >> 1) & 7; }
-__device__ __forceinline__ int swz_v(int r) { return ((r >> 1) & 3) << 1; }
+__device__ __forceinline__ int swz_b(int r) { return (((r >> 1) & 3) << 1) | ((r >> 3) & 1); }
+__device__ __forceinline__ int swz_k(int r) { return swz_b(r); }
+__device__ __forceinline__ int swz_v(int r) { return swz_b(r); }
+
+// 16-B row-read fragment (8 consecutive columns from logical chunk ch) of a swizzled image
+__device__ __forceinline__ bf16x8 img_row(const char* img, int row, int ch) {
+  return *reinterpret_cast<const bf16x8*>(img + row * 128 + ((ch ^ swz_b(row)) << 4));
+}
+
+// transposed fragment of a swizzled image for the accumulator-pair k order: lane l gets
+// column c0 + (l & 15) of rows r0 + 4 (l >> 4) + j (j < 4) and r0 + 16 + 4 (l >> 4) + j - 4
+__device__ __forceinline__ bf16x8 img_tr(const char* img, int r0, int c0) {
+  const int l = threadIdx.x & 63, g = l >> 4, q = (l >> 2) & 3, p = l & 3;
+  const int ra = r0 + 4 * g + q, rb = ra + 16;
+  const int ch = (c0 >> 3) + (p >> 1);
+  const char* a0 = img + ra * 128 + ((ch ^ swz_b(ra)) << 4) + (p & 1) * 8;
+  const char* a1 = img + rb * 128 + ((ch ^ swz_b(rb)) << 4) + (p & 1) * 8;
+  typedef short short4v __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) short4v lds_short4v;
+  short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(a0));
+  short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(a1));
+  bf16x8 out;
+  __builtin_memcpy(&out, &lo, 8);
+  __builtin_memcpy(reinterpret_cast<char*>(&out) + 8, &hi, 8);
+  return out;
+}
 
 __device__ __attribute__((aligned(16))) uint4 g_attn_zero[4];
 
@@ -406,19 +435,29 @@ __device__ __forceinline__ void stage_rows(char* img, const bf16* __restrict__ b
   }
 }
 
+// (b, h, part) of this workgroup: a.nblk parts (row-tile ranges) per (b, h); the parts of one
+// head get adjacent logical ids, on one XCD (their second staging of the head hits L2)
+__device__ __forceinline__ void res_coords(const AttnBwdArgs& a, int& b, int& h, int& part) {
+  int id = blockIdx.x;
+  const int total = a.B * a.H * a.nblk;
+  if ((total & 7) == 0) id = (id & 7) * (total >> 3) + (id >> 3);
+  part = id % a.nblk;
+  const int bh = id / a.nblk;
+  h = bh % a.H;
+  b = bh / a.H;
+}
+
 __global__ __launch_bounds__(1024) void attn_fwd_res_kernel(AttnBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int TP = (a.T + 15) & ~15, TV = (a.T + 31) & ~31;
   char* kimg = smem;
   char* vimg = smem + TP * 128;
-  int id = blockIdx.x;
-  const int total = a.B * a.H;
-  if ((total & 7) == 0) id = (id & 7) * (total >> 3) + (id >> 3);
-  const int h = id % a.H, b = id / a.H;
+  int part, h, b;
+  res_coords(a, b, h, part);
   stage_rows<false>(kimg, a.k + b * a.sq_b + h * DH, a.sq_t, TP, a.T);
   stage_rows<true>(vimg, a.v + b * a.sq_b + h * DH, a.sq_t, TV, a.T);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, col = lane & 15, g = lane >> 4;
-  const int q0 = 16 * w;
+  const int q0 = 16 * (part * (blockDim.x >> 6) + w);
   const int qi = q0 + col;
   const bool qok = qi < a.T;
   const int64_t qoff = b * a.sq_b + static_cast<int64_t>(qi) * a.sq_t + h * DH;
@@ -439,17 +478,22 @@ __global__ __launch_bounds__(1024) void attn_fwd_res_kernel(AttnBwdArgs a) {
     x[kt] = f32x4{-kInf, -kInf, -kInf, -kInf};
     if (kt < nt) {
       const int row = 16 * kt + col;
-      const bf16* kr = reinterpret_cast<const bf16*>(kimg + row * 128);
-      const bf16x8 k0 = *reinterpret_cast<const bf16x8*>(kr + ((g ^ swz_k(row)) << 3));
-      const bf16x8 k1 = *reinterpret_cast<const bf16x8*>(kr + (((4 + g) ^ swz_k(row)) << 3));
       f32x4 s = {};
-      s = mfma(k0, qf[0], s);
-      s = mfma(k1, qf[1], s);
+      s = mfma(img_row(kimg, row, g), qf[0], s);
+      s = mfma(img_row(kimg, row, 4 + g), qf[1], s);
+      if (16 * kt + 16 <= a.T) {  // wave-uniform: only the last tile has padded keys
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = 16 * kt + 4 * g + r;
-        x[kt][r] = key < a.T ? s[r] * c2 : -kInf;
-        m = fmaxf(m, x[kt][r]);
+        for (int r = 0; r < 4; ++r) {
+          x[kt][r] = s[r] * c2;
+          m = fmaxf(m, x[kt][r]);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = 16 * kt + 4 * g + r;
+          x[kt][r] = key < a.T ? s[r] * c2 : -kInf;
+          m = fmaxf(m, x[kt][r]);
+        }
       }
     }
   }
@@ -457,38 +501,29 @@ __global__ __launch_bounds__(1024) void attn_fwd_res_kernel(AttnBwdArgs a) {
   m = fmaxf(m, __shfl_xor(m, 32));
   float l = 0.f;
 #pragma unroll
-  for (int kt = 0; kt < kResMaxT / 16; ++kt)
+  for (int kt = 0; kt < kResMaxT / 16; ++kt) {
+    if (kt < nt) {  // wave-uniform
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float pv = kt < nt ? exp2f(x[kt][r] - m) : 0.f;  // -inf (padded key) -> 0
-      x[kt][r] = pv;
-      l += pv;
+      for (int r = 0; r < 4; ++r) {
+        const float pv = fast_exp2(x[kt][r] - m);  // -inf (padded key) -> 0
+        x[kt][r] = pv;
+        l += pv;
+      }
+    } else {
+      x[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+  }
   l += __shfl_xor(l, 16);
   l += __shfl_xor(l, 32);
   // O^T[d][q] = sum over keys of V^T[d][key] P^T[key][q]; k-step ks covers keys 32ks .. +31 in
   // the accumulator-pair order (j < 4: 32ks + 4g + j, j >= 4: 32ks + 16 + 4g + j - 4)
   f32x4 acc[4] = {};
-  const int qv = lane >> 2 & 3, pv4 = lane & 3;  // transposed-read roles: row q of the block, column quad p
 #pragma unroll
   for (int ks = 0; ks < kResMaxT / 32; ++ks) {
     if (32 * ks < TV) {
       const bf16x8 bop = pack(x[2 * ks], x[2 * ks + 1]);
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const int r0 = 32 * ks + 4 * g + qv, r1 = r0 + 16;
-        const int cch = 2 * dt + (pv4 >> 1);
-        const char* a0 = vimg + r0 * 128 + ((cch ^ swz_v(r0)) << 4) + (pv4 & 1) * 8;
-        const char* a1 = vimg + r1 * 128 + ((cch ^ swz_v(r1)) << 4) + (pv4 & 1) * 8;
-        typedef short short4v __attribute__((ext_vector_type(4)));
-        typedef __attribute__((address_space(3))) short4v lds_short4v;
-        short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(a0));
-        short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(a1));
-        bf16x8 vop;
-        __builtin_memcpy(&vop, &lo, 8);
-        __builtin_memcpy(reinterpret_cast<char*>(&vop) + 8, &hi, 8);
-        acc[dt] = mfma(vop, bop, acc[dt]);
-      }
+      for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma(img_tr(vimg, 32 * ks, 16 * dt), bop, acc[dt]);
     }
   }
   if (qok) {
@@ -504,7 +539,178 @@ __global__ __launch_bounds__(1024) void attn_fwd_res_kernel(AttnBwdArgs a) {
   }
 }
 
+// Backward with the head resident (T <= 256), two kernels like the blocked pair above:
+//   attn_bwd_dq_res   K, V images; one wave per 16 queries: D = rowsum(dO * O) (written to
+//                     stats[.., 1] for the next kernel), S^T = K Q^T, dP^T = V dO^T,
+//                     dS^T = P^T (dP^T - D), dQ^T = K^T dS^T (K^T by transposed reads).
+//   attn_bwd_dkv_res  Q, dO images + the per-query lse / D rows; one wave per 16 keys:
+//                     S = Q K^T, dP = dO V^T, dS = P (dP - D), dV^T += dO^T P, dK^T += Q^T dS.
+// Each image is read by rows (ds_read_b128) and by columns (ds_read_b64_tr_b16), one
+// swizzle for both (swz_b). Padded rows (>= T) are zero; padded queries get lse = +inf.
+__global__ __launch_bounds__(1024) void attn_bwd_dq_res_kernel(AttnBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int TP = (a.T + 15) & ~15, TV = (a.T + 31) & ~31;
+  char* kimg = smem;              // TV rows (transposed reads in k-steps of 32 keys)
+  char* vimg = smem + TV * 128;   // TP rows
+  int part, h, b;
+  res_coords(a, b, h, part);
+  stage_rows<false>(kimg, a.k + b * a.sq_b + h * DH, a.sq_t, TV, a.T);
+  stage_rows<false>(vimg, a.v + b * a.sq_b + h * DH, a.sq_t, TP, a.T);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, col = lane & 15, g = lane >> 4;
+  const int q0 = 16 * (part * (blockDim.x >> 6) + w);
+  const int qi = q0 + col;
+  const bool qok = qi < a.T;
+  const int64_t qoff = b * a.sq_b + static_cast<int64_t>(qi) * a.sq_t + h * DH;
+  bf16x8 qf[2] = {}, gf[2] = {}, o0 = {}, o1 = {};
+  float lse = 0.f;
+  float* st = a.stats + ((static_cast<int64_t>(b) * a.H + h) * a.T + (qok ? qi : 0)) * 2;
+  if (qok) {
+    qf[0] = ld8(a.q + qoff + 8 * g);
+    qf[1] = ld8(a.q + qoff + 32 + 8 * g);
+    const bf16* gp = a.dout + b * a.sg_b + static_cast<int64_t>(qi) * a.sg_t + h * DH;
+    gf[0] = ld8(gp + 8 * g);
+    gf[1] = ld8(gp + 32 + 8 * g);
+    const bf16* op = a.o + b * a.so_b + static_cast<int64_t>(qi) * a.so_t + h * a.so_h;
+    o0 = ld8(op + 8 * g);
+    o1 = ld8(op + 32 + 8 * g);
+    lse = st[0];
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (q0 >= a.T) return;  // wave-uniform
+  float dsum = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dsum += (float)gf[0][j] * (float)o0[j] + (float)gf[1][j] * (float)o1[j];
+  dsum += __shfl_xor(dsum, 16);
+  dsum += __shfl_xor(dsum, 32);
+  if (qok && g == 0) st[1] = dsum;
+  const int nt = TP / 16;
+  const float c2 = a.scale * kLog2e;
+  f32x4 ds[kResMaxT / 16];
+#pragma unroll
+  for (int kt = 0; kt < kResMaxT / 16; ++kt) {
+    ds[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (kt < nt) {
+      const int row = 16 * kt + col;
+      f32x4 sv = {}, dp = {};
+      sv = mfma(img_row(kimg, row, g), qf[0], sv);
+      sv = mfma(img_row(kimg, row, 4 + g), qf[1], sv);
+      dp = mfma(img_row(vimg, row, g), gf[0], dp);
+      dp = mfma(img_row(vimg, row, 4 + g), gf[1], dp);
+      if (16 * kt + 16 <= a.T) {  // wave-uniform
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ds[kt][r] = fast_exp2(fmaf(sv[r], c2, -lse)) * (dp[r] - dsum);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = 16 * kt + 4 * g + r;
+          ds[kt][r] = key < a.T ? fast_exp2(fmaf(sv[r], c2, -lse)) * (dp[r] - dsum) : 0.f;
+        }
+      }
+    }
+  }
+  f32x4 acc[4] = {};
+#pragma unroll
+  for (int ks = 0; ks < kResMaxT / 32; ++ks) {
+    if (32 * ks < TV) {
+      const bf16x8 bop = pack(ds[2 * ks], ds[2 * ks + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma(img_tr(kimg, 32 * ks, 16 * dt), bop, acc[dt]);
+    }
+  }
+  if (qok) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const bf16x4 o = {(bf16)(acc[dt][0] * a.scale), (bf16)(acc[dt][1] * a.scale), (bf16)(acc[dt][2] * a.scale),
+                        (bf16)(acc[dt][3] * a.scale)};
+      *reinterpret_cast<bf16x4*>(a.dq + qoff + dt * 16 + 4 * g) = o;
+    }
+  }
+}
+
+__global__ __launch_bounds__(1024) void attn_bwd_dkv_res_kernel(AttnBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int TV = (a.T + 31) & ~31;
+  char* qimg = smem;               // TV rows
+  char* gimg = smem + TV * 128;    // TV rows
+  float* sL = reinterpret_cast<float*>(smem + 2 * TV * 128);
+  float* sD = sL + TV;
+  int part, h, b;
+  res_coords(a, b, h, part);
+  stage_rows<false>(qimg, a.q + b * a.sq_b + h * DH, a.sq_t, TV, a.T);
+  stage_rows<false>(gimg, a.dout + b * a.sg_b + h * DH, a.sg_t, TV, a.T);
+  const float* st = a.stats + (static_cast<int64_t>(b) * a.H + h) * a.T * 2;
+  for (int qq = threadIdx.x; qq < TV; qq += blockDim.x) {
+    sL[qq] = qq < a.T ? st[2 * qq] : kInf;
+    sD[qq] = qq < a.T ? st[2 * qq + 1] : 0.f;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, col = lane & 15, g = lane >> 4;
+  const int k0 = 16 * (part * (blockDim.x >> 6) + w);
+  const int ki = k0 + col;
+  const bool kok = ki < a.T;
+  const int64_t koff = b * a.sq_b + static_cast<int64_t>(ki) * a.sq_t + h * DH;
+  bf16x8 kf[2] = {}, vf[2] = {};
+  if (kok) {
+    kf[0] = ld8(a.k + koff + 8 * g);
+    kf[1] = ld8(a.k + koff + 32 + 8 * g);
+    vf[0] = ld8(a.v + koff + 8 * g);
+    vf[1] = ld8(a.v + koff + 32 + 8 * g);
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (k0 >= a.T) return;  // wave-uniform
+  const float c2 = a.scale * kLog2e;
+  f32x4 accK[4] = {}, accV[4] = {};
+  for (int ks = 0; ks < TV / 32; ++ks) {
+    f32x4 p[2], dsv[2];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int row = 32 * ks + 16 * half + col;  // query row of the A fragment
+      f32x4 sv = {}, dp = {};
+      sv = mfma(img_row(qimg, row, g), kf[0], sv);
+      sv = mfma(img_row(qimg, row, 4 + g), kf[1], sv);
+      dp = mfma(img_row(gimg, row, g), vf[0], dp);
+      dp = mfma(img_row(gimg, row, 4 + g), vf[1], dp);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qq = 32 * ks + 16 * half + 4 * g + r;
+        const float pv = fast_exp2(fmaf(sv[r], c2, -sL[qq]));  // padded query: lse = +inf -> 0
+        p[half][r] = pv;
+        dsv[half][r] = pv * (dp[r] - sD[qq]);
+      }
+    }
+    const bf16x8 pb = pack(p[0], p[1]), db = pack(dsv[0], dsv[1]);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      accV[dt] = mfma(img_tr(gimg, 32 * ks, 16 * dt), pb, accV[dt]);
+      accK[dt] = mfma(img_tr(qimg, 32 * ks, 16 * dt), db, accK[dt]);
+    }
+  }
+  if (kok) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const bf16x4 v = {(bf16)accV[dt][0], (bf16)accV[dt][1], (bf16)accV[dt][2], (bf16)accV[dt][3]};
+      const bf16x4 k = {(bf16)(accK[dt][0] * a.scale), (bf16)(accK[dt][1] * a.scale),
+                        (bf16)(accK[dt][2] * a.scale), (bf16)(accK[dt][3] * a.scale)};
+      *reinterpret_cast<bf16x4*>(a.dv + koff + dt * 16 + 4 * g) = v;
+      *reinterpret_cast<bf16x4*>(a.dk + koff + dt * 16 + 4 * g) = k;
+    }
+  }
+}
+
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// workgroups per (b, h) of the resident kernels (FLUXMPI_ATTN_PARTS, default 2): with the head's
+// ~55 KB of LDS and <= 8 waves each, two workgroups share a CU, so one stages its head while
+// the other computes (one workgroup of 13 waves per CU left every staging exposed)
+int res_parts(int tiles) {
+  static const int parts = [] {
+    const char* e = std::getenv("FLUXMPI_ATTN_PARTS");
+    const int v = e != nullptr ? std::atoi(e) : 2;
+    return v < 1 ? 1 : (v > 16 ? 16 : v);
+  }();
+  return parts < tiles ? parts : tiles;
+}
 
 }  // namespace
 
@@ -522,6 +728,24 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* o, const 
                 static_cast<const bf16*>(o), static_cast<const bf16*>(dout), nullptr, static_cast<bf16*>(dq),
                 static_cast<bf16*>(dk), static_cast<bf16*>(dv), stats, sq_b, sq_t, so_b, so_t, so_h, sg_b, sg_t,
                 B, T, H, (T + 63) / 64, scale};
+  static const bool resident = [] {
+    const char* e = std::getenv("FLUXMPI_ATTN_BWD");
+    return e == nullptr || std::string(e) != "blocked";
+  }();
+  if (resident && T <= kResMaxT && (sq_t % 8) == 0 && (sg_t % 8) == 0) {
+    const int tiles = (T + 15) / 16;
+    a.nblk = res_parts(tiles);
+    const int64_t bh = static_cast<int64_t>(B) * H * a.nblk;
+    if (bh > 0x7fffffff) throw std::runtime_error("attn_bwd: grid too large");
+    const int waves = (tiles + a.nblk - 1) / a.nblk;
+    const int TP = (T + 15) & ~15, TV = (T + 31) & ~31;
+    attn_bwd_dq_res_kernel<<<static_cast<unsigned>(bh), waves * 64, static_cast<size_t>(TV + TP) * 128, s>>>(a);
+    FLUXMPI_HIP_CHECK(hipGetLastError());
+    attn_bwd_dkv_res_kernel<<<static_cast<unsigned>(bh), waves * 64, static_cast<size_t>(2 * TV) * 128 + 2 * TV * 4,
+                              s>>>(a);
+    FLUXMPI_HIP_CHECK(hipGetLastError());
+    return;
+  }
   const int64_t total = static_cast<int64_t>(B) * H * a.nblk;
   if (total > 0x7fffffff) throw std::runtime_error("attn_bwd: grid too large");
   attn_bwd_dq_kernel<<<static_cast<unsigned>(total), 256, 0, s>>>(a);
@@ -559,10 +783,12 @@ void attn_fwd(const void* q, const void* k, const void* v, void* o, float* stats
     return e == nullptr || std::string(e) != "blocked";
   }();
   if (resident && T <= kResMaxT && (sq_t % 8) == 0) {
-    // whole head resident in LDS: one workgroup per (b, h), one wave per 16 queries
-    const int64_t total = static_cast<int64_t>(B) * H;
+    // whole head resident in LDS: res_parts() workgroups per (b, h), one wave per 16 queries
+    const int tiles = (T + 15) / 16;
+    a.nblk = res_parts(tiles);
+    const int64_t total = static_cast<int64_t>(B) * H * a.nblk;
     if (total > 0x7fffffff) throw std::runtime_error("attn_fwd: grid too large");
-    const int waves = (T + 15) / 16;
+    const int waves = (tiles + a.nblk - 1) / a.nblk;
     const size_t lds = static_cast<size_t>(((T + 15) & ~15) + ((T + 31) & ~31)) * 128;
     attn_fwd_res_kernel<<<static_cast<unsigned>(total), waves * 64, lds, s>>>(a);
     FLUXMPI_HIP_CHECK(hipGetLastError());
