@@ -661,6 +661,7 @@ __global__ __launch_bounds__(1024) void attn_bwd_dkv_res_kernel(AttnBwdArgs a) {
   if (k0 >= a.T) return;  // wave-uniform
   const float c2 = a.scale * kLog2e;
   f32x4 accK[4] = {}, accV[4] = {};
+#pragma unroll 2
   for (int ks = 0; ks < TV / 32; ++ks) {
     f32x4 p[2], dsv[2];
 #pragma unroll
