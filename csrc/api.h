@@ -106,6 +106,15 @@ void bn_relu_maxpool_fwd(const void* x, const float* scale, const float* shift, 
                          int64_t H, int64_t W, int64_t C, int K, int S, int P, int dtype, hipStream_t stream);
 // y[p][0..3] = (x[p][0], x[p][1], x[p][2], 0) for npix 16-bit NHWC pixels (stem channel pad)
 void pad_c3_to_c4(const void* x, void* y, int64_t npix, int dtype, hipStream_t stream);
+
+// ---- ResNet stem on MFMA (stem.hip): 7x7/2 conv of NHWC4 224x224 images + BN statistics;
+// the fused backward (pool gather + BN backward + filter gradient)
+void stem_fwd(const void* x, const void* wp, void* y, float* stats, int64_t n, hipStream_t stream);
+int stem_bwd_blocks(int64_t n);
+int64_t stem_part_floats();
+void stem_bwd(const void* x, const void* c, const void* dp, const uint8_t* idx, const float* w, const float* mean,
+              const float* inv, float* part, int blocks, float* stats, float* dw_bn, float* db_bn, float* dwp,
+              int64_t n, hipStream_t stream);
 // Softmax attention, head dim 64, bf16 (csrc/kernels/attention.hip). q/k/v and dq/dk/dv share
 // strides (sq_b, sq_t; head stride 64), o has (so_b, so_t, so_h), dout (sg_b, sg_t; head stride
 // 64); stats is fp32 [B][H][T][2]: attn_fwd writes [..][0] = base-2 log-sum-exp of the scaled

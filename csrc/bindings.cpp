@@ -164,6 +164,21 @@ PYBIND11_MODULE(_C, m) {
     pad_c3_to_c4(reinterpret_cast<const void*>(x), reinterpret_cast<void*>(y), npix, dtype,
                  reinterpret_cast<hipStream_t>(stream));
   });
+  m.def("stem_fwd", [](uintptr_t x, uintptr_t wp, uintptr_t y, uintptr_t stats, int64_t n, uintptr_t stream) {
+    stem_fwd(reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(wp), reinterpret_cast<void*>(y),
+             reinterpret_cast<float*>(stats), n, reinterpret_cast<hipStream_t>(stream));
+  });
+  m.def("stem_bwd_blocks", &stem_bwd_blocks);
+  m.def("stem_part_floats", &stem_part_floats);
+  m.def("stem_bwd", [](uintptr_t x, uintptr_t c, uintptr_t dp, uintptr_t idx, uintptr_t w, uintptr_t mean,
+                       uintptr_t inv, uintptr_t part, int blocks, uintptr_t stats, uintptr_t dw_bn, uintptr_t db_bn,
+                       uintptr_t dwp, int64_t n, uintptr_t stream) {
+    auto F = [](uintptr_t q) { return reinterpret_cast<const float*>(q); };
+    auto W = [](uintptr_t q) { return reinterpret_cast<float*>(q); };
+    stem_bwd(reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(c), reinterpret_cast<const void*>(dp),
+             reinterpret_cast<const uint8_t*>(idx), F(w), F(mean), F(inv), W(part), blocks, W(stats), W(dw_bn),
+             W(db_bn), W(dwp), n, reinterpret_cast<hipStream_t>(stream));
+  });
   m.def("maxpool_bwd", [](uintptr_t dy, uintptr_t idx, uintptr_t dx, int64_t N, int64_t H, int64_t W, int64_t C,
                           int K, int S, int P, int dtype, uintptr_t stream) {
     maxpool_bwd(reinterpret_cast<const void*>(dy), reinterpret_cast<const uint8_t*>(idx), reinterpret_cast<void*>(dx),

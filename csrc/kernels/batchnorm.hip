@@ -945,6 +945,12 @@ void bn_fwd_train(const void* x, void* y, const void* residual, const float* wei
   }
 }
 
+void bn_finalize_bwd(float* ws, int64_t C, float* dw, float* db, hipStream_t s) {
+  check(C);
+  bn_finalize_bwd_kernel<<<finalize_blocks(C), kFinCh * kFinGroups, 0, s>>>(ws, (int)C, dw, db);
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+}
+
 void bn_stats_finalize(const void* x, const float* w, const float* b, float* rm, float* rv, float* sm, float* si,
                        float* scale, float* shift, float* ws, int64_t rows, int64_t C, float momentum, float eps,
                        int stats_ready, int dtype, hipStream_t s, int64_t* nbt) {

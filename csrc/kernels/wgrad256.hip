@@ -101,7 +101,7 @@ __device__ __forceinline__ bf16x8 frag(const bf16* __restrict__ img, int r0, int
 
 // BK k-rows per step, ST LDS stages (ST - 1 steps of DMA in flight). Stage images are
 // [BK][256] bf16 for A and for B; ST * BK * 2 KiB of LDS in all.
-template <int BK, int ST>
+template <int BK, int ST, bool PRIO = false>
 __global__ __launch_bounds__(kThreads, 1) void wgrad256_kernel(W256Args p) {
   constexpr int kImgBytes = BK * kTile * 2;
   constexpr int kStageBytes = 2 * kImgBytes;
@@ -151,6 +151,7 @@ __global__ __launch_bounds__(kThreads, 1) void wgrad256_kernel(W256Args p) {
     if (t + ST - 1 < nk) issue(t + ST - 1);
     const bf16* ta = reinterpret_cast<const bf16*>(smem + (t % ST) * kStageBytes);
     const bf16* tb = reinterpret_cast<const bf16*>(smem + (t % ST) * kStageBytes + kImgBytes);
+    if (PRIO) __builtin_amdgcn_s_setprio(1);  // MFMA-issuing waves first (T5)
 #pragma unroll
     for (int kh = 0; kh < BK / 32; ++kh) {
       bf16x8 fb[4];
@@ -163,6 +164,7 @@ __global__ __launch_bounds__(kThreads, 1) void wgrad256_kernel(W256Args p) {
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[j], acc[i][j], 0, 0, 0);
       }
     }
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
   }
   // fp32 partial: acc[i][j][r] is (row wm*128 + i*16 + 4*(lane>>4) + r, col wn*64 + j*16 + lane&15)
   float* c = p.c + static_cast<int64_t>(split) * p.M * p.N;
@@ -180,12 +182,149 @@ __global__ __launch_bounds__(kThreads, 1) void wgrad256_kernel(W256Args p) {
     }
 }
 
-// pipeline variant: 0 = BK 32 x 4 stages (default), 1 = BK 64 x 2 stages
+// Variant 3: the same pipeline with every per-step address computation hoisted out of the
+// k-loop (PMC: 2.2 VALU instructions per MFMA in variant 0, mostly 64-bit DMA source
+// addresses and the swizzled fragment offsets recomputed each step). A lane's DMA pieces
+// keep their (row, chunk) for the whole loop, so their source pointers just advance by BK
+// rows; a fragment's swizzle term depends only on the lane (k rows 32 kh + 8 g + q and
+// + 4 share it), so its LDS offset is one per-lane constant per fragment plus immediates.
+template <int BK, int ST>
+__global__ __launch_bounds__(kThreads, 1) void wgrad256h_kernel(W256Args p) {
+  constexpr int kImgBytes = BK * kTile * 2;
+  constexpr int kStageBytes = 2 * kImgBytes;
+  constexpr int kP = kImgBytes / 1024 / 8;  // DMA pieces per wave per operand
+  constexpr int kG = 2 * kP;                // DMA instructions per wave per step
+  constexpr int kRow = kTile * 2;           // bytes per k-row of an image
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nt = p.tiles_m * p.tiles_n;
+  const int total = static_cast<int>(gridDim.x);
+  int lid = blockIdx.x;
+  if (total >= 8) {
+    const int q = total / 8, r = total % 8, xcd = lid % 8, pos = lid / 8;
+    lid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+  }
+  const int split = lid / nt, bid = lid - split * nt;
+  const int tm = bid / p.tiles_n, tn = bid - tm * p.tiles_n;
+  const int64_t m0 = static_cast<int64_t>(tm) * kTile, n0 = static_cast<int64_t>(tn) * kTile;
+  const int64_t kbeg = static_cast<int64_t>(split) * p.k_per_split;
+  const int64_t kend = kbeg + p.k_per_split < p.K ? kbeg + p.k_per_split : p.K;
+  const int nk = kend > kbeg ? static_cast<int>((kend - kbeg + BK - 1) / BK) : 0;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wm = wave >> 2, wn = wave & 3;
+
+  // DMA: this lane's pieces (row 2 * piece + lane / 32, chunk slot lane % 32)
+  const bf16* pa[kP];
+  const bf16* pb[kP];
+  int krow[kP];  // k row relative to kbeg
+#pragma unroll
+  for (int j = 0; j < kP; ++j) {
+    const int row = 2 * (wave * kP + j) + (lane >> 5);
+    const int chunk = (lane & 31) ^ swz(row);
+    krow[j] = row;
+    pa[j] = p.a + (kbeg + row) * p.lda + m0 + chunk * 8;
+    pb[j] = p.b + (kbeg + row) * p.ldb + n0 + chunk * 8;
+  }
+  const int64_t stepA = static_cast<int64_t>(BK) * p.lda, stepB = static_cast<int64_t>(BK) * p.ldb;
+  const int klim = static_cast<int>(kend - kbeg);
+  auto issue = [&](int t) {
+    char* st = smem + (t % ST) * kStageBytes;
+    typedef __attribute__((address_space(3))) char lds_char;
+    typedef __attribute__((address_space(1))) void gl_void;
+#pragma unroll
+    for (int j = 0; j < kP; ++j) {
+      const bool ok = krow[j] < klim;
+      const void* sa = ok ? static_cast<const void*>(pa[j]) : static_cast<const void*>(g_zero256);
+      const void* sb = ok ? static_cast<const void*>(pb[j]) : static_cast<const void*>(g_zero256);
+      __builtin_amdgcn_global_load_lds((gl_void*)(sa), (lds_char*)(st + (wave * kP + j) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gl_void*)(sb), (lds_char*)(st + kImgBytes + (wave * kP + j) * 1024), 16,
+                                       0, 0);
+      pa[j] += stepA;
+      pb[j] += stepB;
+      krow[j] += BK;
+    }
+  };
+
+  // fragment offsets within an image (kh = 0, first transposed read)
+  const int g = lane >> 4, li = lane & 15, qq = li >> 2, pp = li & 3;
+  const int k0 = 8 * g + qq;
+  const int sw = swz(k0);
+  int offA[8], offB[4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int col = wm * 128 + i * 16 + 4 * pp;
+    offA[i] = k0 * kRow + ((((col >> 3) ^ sw)) << 4) + (col & 7) * 2;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = wn * 64 + j * 16 + 4 * pp;
+    offB[j] = k0 * kRow + ((((col >> 3) ^ sw)) << 4) + (col & 7) * 2;
+  }
+  typedef short short4v __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) short4v lds_short4v;
+  // __restrict__ matters: it gives the reads alias scopes, without which the waitcnt pass
+  // assumes they may read the DMA just issued and drains vmcnt(0) before them
+  auto frag_at = [&](const char* __restrict__ img, int off) {
+    short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(img + off));
+    short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(img + off + 4 * kRow));
+    bf16x8 out;
+    __builtin_memcpy(&out, &lo, 8);
+    __builtin_memcpy(reinterpret_cast<char*>(&out) + 8, &hi, 8);
+    return out;
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < ST - 1; ++t)
+    if (t < nk) issue(t);
+  for (int t = 0; t < nk; ++t) {
+    const int ahead = nk - 1 - t;
+    if (ST >= 4 && ahead >= 2) wait_vm<(ST >= 4 ? 2 : 0) * kG>();
+    else if (ST >= 3 && ahead >= 1) wait_vm<(ST >= 3 ? 1 : 0) * kG>();
+    else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    if (t + ST - 1 < nk) issue(t + ST - 1);
+    const char* ta = smem + (t % ST) * kStageBytes;
+    const char* tb = ta + kImgBytes;
+#pragma unroll
+    for (int kh = 0; kh < BK / 32; ++kh) {
+      bf16x8 fb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = frag_at(tb, offB[j] + kh * 32 * kRow);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const bf16x8 fa = frag_at(ta, offA[i] + kh * 32 * kRow);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  float* c = p.c + static_cast<int64_t>(split) * p.M * p.N;
+  const int col_in = lane & 15, rq = 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t n = n0 + wn * 64 + j * 16 + col_in;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = m0 + wm * 128 + i * 16 + rq + r;
+        c[m * p.N + n] = acc[i][j][r];
+      }
+    }
+}
+
+// pipeline variant: 0 = BK 32 x 4 stages, 1 = BK 64 x 2 stages, 2 = variant 0 with s_setprio(1)
+// around each step's MFMAs, 3 (default) = variant 0 with the addressing hoisted out of the loop
 int g_variant = -1;
 int variant() {
   if (g_variant < 0) {
     const char* e = std::getenv("FLUXMPI_WGRAD256_VARIANT");
-    g_variant = (e != nullptr && e[0] == '1') ? 1 : 0;
+    g_variant = e != nullptr ? std::atoi(e) : 3;
+    if (g_variant < 0 || g_variant > 3) g_variant = 3;
   }
   return g_variant;
 }
@@ -216,14 +355,18 @@ void gemm_wgrad256(const void* a, const void* b, float* ws, int64_t lda, int64_t
   const int64_t grid = static_cast<int64_t>(s) * p.tiles_m * p.tiles_n;
   if (grid > 0x7fffffff) throw std::runtime_error("gemm_wgrad256: grid too large");
   constexpr int kSmem = 128 * 1024;  // both variants: 4 x 32 KiB / 2 x 64 KiB
-  static bool attr[2] = {false, false};
-  const void* fn = v == 1 ? reinterpret_cast<const void*>(&wgrad256_kernel<64, 2>)
-                          : reinterpret_cast<const void*>(&wgrad256_kernel<32, 4>);
+  static bool attr[4] = {false, false, false, false};
+  const void* fn = v == 1   ? reinterpret_cast<const void*>(&wgrad256_kernel<64, 2>)
+                   : v == 2 ? reinterpret_cast<const void*>(&wgrad256_kernel<32, 4, true>)
+                   : v == 3 ? reinterpret_cast<const void*>(&wgrad256h_kernel<32, 4>)
+                            : reinterpret_cast<const void*>(&wgrad256_kernel<32, 4>);
   if (!attr[v]) {
     FLUXMPI_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kSmem));
     attr[v] = true;
   }
   if (v == 1) wgrad256_kernel<64, 2><<<static_cast<unsigned>(grid), kThreads, kSmem, stream>>>(p);
+  else if (v == 2) wgrad256_kernel<32, 4, true><<<static_cast<unsigned>(grid), kThreads, kSmem, stream>>>(p);
+  else if (v == 3) wgrad256h_kernel<32, 4><<<static_cast<unsigned>(grid), kThreads, kSmem, stream>>>(p);
   else wgrad256_kernel<32, 4><<<static_cast<unsigned>(grid), kThreads, kSmem, stream>>>(p);
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }

@@ -20,9 +20,16 @@ MI355X choices:
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
+
+# ResNet stem: "ours" = the MFMA stem kernels (ops/stem.py: conv + BN statistics forward, one fused
+# backward pass) when the input is a 224x224 bf16 NHWC batch; "miopen" = padded MIOpen conv + the
+# fused BN/ReLU/max-pool of ops/pool.py
+STEM = os.environ.get("FLUXMPI_STEM", "ours")
 
 
 class Conv1x1(nn.Module):
@@ -264,6 +271,14 @@ class ResNet(nn.Module):
     def forward(self, x):
         if self.norm_kind == "fused":
             from ..ops import pool
+            from ..ops import stem as stem_ops
+            if (self.training and self.conv_impl in ("hybrid", "fused") and STEM == "ours"
+                    and stem_ops.supported(x, self.conv1.weight, self.conv1, self.bn1)):
+                # conv + BN statistics + BN/ReLU/max-pool on the MFMA stem kernels; the backward
+                # is one fused pass (ops/stem.py)
+                x = stem_ops.stem(x, self.conv1, self.bn1)
+                x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+                return self.fc(global_avg_pool(x))
             c = self._stem_conv(x)
             if self.training and pool.supported(c):
                 # BN + ReLU + 3x3/2 max-pool in one pass over the stem output

@@ -1,7 +1,10 @@
 #!/usr/bin/env python
-"""ResNet-50 stem conv (7x7/2, 64 filters, 224x224, batch 256, bf16 NHWC) on MIOpen with the
-input channels padded 3 -> 4 / 8 (zero channel, zero weights: same math): forward, weight
-gradient, and the pad copy itself."""
+"""ResNet-50 stem (7x7/2, 64 filters, 224x224, batch 256, bf16 NHWC).
+
+1. MIOpen with the input channels padded 3 -> 4 / 8 (zero channel, zero weights: same math):
+   forward, weight gradient, and the pad copy itself.
+2. The whole stem (conv -> BN -> ReLU -> max-pool), forward and forward + backward: the MFMA
+   stem kernels (ops/stem.py) vs the padded MIOpen conv + ops/pool.py's fused BN/ReLU/pool."""
 import json
 import os
 import sys
@@ -44,6 +47,27 @@ def main():
             rec["pad_us"] = bench(lambda: F.pad(x3, (0, 0, 0, 0, 0, cin - 3)).contiguous(
                 memory_format=torch.channels_last))
         print(json.dumps(rec), flush=True)
+
+    from fluxmpi_amd.models import resnet as R
+    from fluxmpi_amd.ops import pool
+    from fluxmpi_amd.ops import stem as S
+    conv = torch.nn.Conv2d(3, 64, 7, 2, 3, bias=False).cuda()
+    bn = R._norm(64, "fused").cuda()
+    w4 = torch.nn.functional.pad(conv.weight.detach(), (0, 0, 0, 0, 0, 1)).bfloat16().contiguous(
+        memory_format=torch.channels_last).requires_grad_(True)
+
+    def old_fwd():
+        return pool.bn_relu_maxpool(F.conv2d(pool.pad_c3_to_c4(x3), w4, None, 2, 3), bn, 3, 2, 1)
+
+    def new_fwd():
+        return S.stem(x3, conv, bn)
+
+    y = new_fwd()
+    gy = torch.randn_like(y)
+    rec = {"stem": "fused", "ours_fwd_us": bench(new_fwd), "miopen_fwd_us": bench(old_fwd),
+           "ours_fwd_bwd_us": bench(lambda: new_fwd().backward(gy)),
+           "miopen_fwd_bwd_us": bench(lambda: old_fwd().backward(gy))}
+    print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":
