@@ -107,6 +107,11 @@ void bn_relu_maxpool_fwd(const void* x, const float* scale, const float* shift, 
 // y[p][0..3] = (x[p][0], x[p][1], x[p][2], 0) for npix 16-bit NHWC pixels (stem channel pad)
 void pad_c3_to_c4(const void* x, void* y, int64_t npix, int dtype, hipStream_t stream);
 
+// ---- 3x3 / stride-1 / pad-1 convolution over LDS image halos (conv3x3.hip)
+bool conv3x3_halo_supported(int64_t N, int H, int W, int C, int Co);
+void conv3x3_halo(const void* x, const void* w, void* y, float* stats, int64_t N, int H, int W, int C, int Co,
+                  hipStream_t stream);
+
 // ---- ResNet stem on MFMA (stem.hip): 7x7/2 conv of NHWC4 224x224 images + BN statistics;
 // the fused backward (pool gather + BN backward + filter gradient)
 void stem_fwd(const void* x, const void* wp, void* y, float* stats, int64_t n, hipStream_t stream);

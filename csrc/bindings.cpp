@@ -164,6 +164,12 @@ PYBIND11_MODULE(_C, m) {
     pad_c3_to_c4(reinterpret_cast<const void*>(x), reinterpret_cast<void*>(y), npix, dtype,
                  reinterpret_cast<hipStream_t>(stream));
   });
+  m.def("conv3x3_halo_supported", &conv3x3_halo_supported);
+  m.def("conv3x3_halo", [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, int64_t N, int H, int W, int C,
+                           int Co, uintptr_t stream) {
+    conv3x3_halo(reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(w), reinterpret_cast<void*>(y),
+                 reinterpret_cast<float*>(stats), N, H, W, C, Co, reinterpret_cast<hipStream_t>(stream));
+  });
   m.def("stem_fwd", [](uintptr_t x, uintptr_t wp, uintptr_t y, uintptr_t stats, int64_t n, uintptr_t stream) {
     stem_fwd(reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(wp), reinterpret_cast<void*>(y),
              reinterpret_cast<float*>(stats), n, reinterpret_cast<hipStream_t>(stream));

@@ -16,7 +16,7 @@ from fluxmpi_amd.utils.miopen import install_tuned_db  # noqa: E402
 
 WG_CFGS = tuple(tuple(int(t) for t in c.split(":")) for c in
                 os.environ.get("BENCH_WG_CFGS", "1:768,2:768,1:1536,2:512").split(","))
-ENGINES = tuple(int(e) for e in os.environ.get("BENCH_ENGINES", "1,2,3,5,6").split(","))
+ENGINES = tuple(int(e) for e in os.environ.get("BENCH_ENGINES", "2").split(","))
 
 
 def bench(fn, iters=20):
@@ -44,6 +44,10 @@ def main():
         y = torch.empty_like(x)
         flop = 2 * B * H * H * C * C * 9
         rec = {"H": H, "C": C}
+        G.HALO = True
+        rec["halo_fwd"] = bench(lambda: conv3x3_fwd(x, w, out=y))
+        rec["halo_dgrad"] = bench(lambda: conv3x3_dgrad(dy, w, out=y))
+        G.HALO = False
         for eng in ENGINES:
             G.ENGINE = eng
             rec[f"e{eng}_fwd"] = bench(lambda: conv3x3_fwd(x, w, out=y))
@@ -61,7 +65,7 @@ def main():
             rec[f"ours_wgrad_v{v}_{tw}"] = bench(lambda: conv3x3_wgrad(dy, x))
         rec["miopen_wgrad"] = bench(lambda: torch.ops.aten.convolution_backward(
             dy, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1, [False, True, False]))
-        for k in ("ours_fwd", "miopen_fwd", "ours_dgrad", "miopen_dgrad"):
+        for k in ("halo_fwd", "halo_dgrad", "ours_fwd", "miopen_fwd", "ours_dgrad", "miopen_dgrad"):
             rec[k + "_TF"] = round(flop / rec[k] / 1e6, 1)
         for k, v in rec.items():
             if k not in ("H", "C") and not k.endswith("_TF"):
