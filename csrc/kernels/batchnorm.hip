@@ -201,6 +201,19 @@ __global__ __launch_bounds__(kFinCh * kFinGroups) void bn_finalize_bwd_kernel(fl
   dw[c] = q;  // sum(dy_eff * xhat)
 }
 
+// the dual (bn3 + downsample) backward's two finalizes in one launch: blockIdx.y picks the workspace
+__global__ __launch_bounds__(kFinCh * kFinGroups) void bn_finalize_bwd2_kernel(float* __restrict__ acc, float* __restrict__ acc2,
+                                                                               int C, float* __restrict__ dw,
+                                                                               float* __restrict__ db, float* __restrict__ dw2,
+                                                                               float* __restrict__ db2) {
+  float s, q;
+  int c;
+  const bool second = blockIdx.y != 0;
+  if (!take_shards(second ? acc2 : acc, C, s, q, c)) return;
+  (second ? db2 : db)[c] = s;
+  (second ? dw2 : dw)[c] = q;
+}
+
 // ---------------------------------------------------------------- forward
 template <typename T>
 __global__ __launch_bounds__(kThreads) void bn_stats_kernel(const T* __restrict__ x, int64_t rows, int C, Geo g,
@@ -875,9 +888,7 @@ void bwd_dual_t(const void* dy, const uint8_t* mask, const void* x, const void* 
   bn_bwd_reduce_dual_kernel<T><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(dyr, mask, xr, x2r, sm, si, sm2, si2,
                                                                              rows, (int)C, g, ws, ws2);
   FLUXMPI_HIP_CHECK(hipGetLastError());
-  bn_finalize_bwd_kernel<<<finalize_blocks(C), kFinCh * kFinGroups, 0, s>>>(ws, (int)C, dw, db);
-  FLUXMPI_HIP_CHECK(hipGetLastError());
-  bn_finalize_bwd_kernel<<<finalize_blocks(C), kFinCh * kFinGroups, 0, s>>>(ws2, (int)C, dw2, db2);
+  bn_finalize_bwd2_kernel<<<dim3(finalize_blocks(C), 2), kFinCh * kFinGroups, 0, s>>>(ws, ws2, (int)C, dw, db, dw2, db2);
   FLUXMPI_HIP_CHECK(hipGetLastError());
   const int64_t nvec = rows * C / 8;
   auto k = bn_bwd_dx_dual_kernel<T>;

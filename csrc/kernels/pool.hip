@@ -33,7 +33,7 @@ struct PoolGeo {
 // One workgroup per output row (n, oh); lanes walk (ow, channel vector) of the row with
 // 32-bit index math (64-bit division per element made the first version ALU-bound).
 template <typename T>
-__global__ __launch_bounds__(kThreads) void bn_relu_maxpool_fwd_kernel(const T* __restrict__ x,
+__global__ __launch_bounds__(1024) void bn_relu_maxpool_fwd_kernel(const T* __restrict__ x,
                                                                        const float* __restrict__ scale,
                                                                        const float* __restrict__ shift,
                                                                        T* __restrict__ y, uint8_t* __restrict__ idx,
@@ -45,7 +45,7 @@ __global__ __launch_bounds__(kThreads) void bn_relu_maxpool_fwd_kernel(const T* 
   const int h0 = oh * g.S - g.P;
   const int per_row = static_cast<int>(g.OW) * cv;
   const T* xn = x + n * g.H * g.W * g.C;
-  for (int t = threadIdx.x; t < per_row; t += kThreads) {
+  for (int t = threadIdx.x; t < per_row; t += blockDim.x) {
     const int ow = t / cv, c8 = t - ow * cv;
     const int c0 = c8 * 8;
     const int w0 = ow * g.S - g.P;
@@ -227,17 +227,21 @@ void bn_relu_maxpool_fwd(const void* x, const float* scale, const float* shift, 
                          int64_t H, int64_t W, int64_t C, int K, int S, int P, int dtype, hipStream_t s) {
   const PoolGeo g = make_geo(N, H, W, C, K, S, P);
   const int nb = static_cast<int>(N * g.OH);  // one workgroup per output row
+  // one lane per (output column, 8 channels) of the row when it fits a workgroup (ResNet stem:
+  // 56 x 8 = 448 lanes; a 256-lane workgroup looping over it left a quarter of its lanes idle)
+  const int64_t per_row = g.OW * (C / 8);
+  const int thr = per_row <= 1024 ? static_cast<int>((per_row + 63) / 64 * 64) : kThreads;
   switch (dtype) {
     case kBF16:
-      bn_relu_maxpool_fwd_kernel<bf16><<<nb, kThreads, 0, s>>>(static_cast<const bf16*>(x), scale, shift,
+      bn_relu_maxpool_fwd_kernel<bf16><<<nb, thr, 0, s>>>(static_cast<const bf16*>(x), scale, shift,
                                                                static_cast<bf16*>(y), idx, g);
       break;
     case kF16:
-      bn_relu_maxpool_fwd_kernel<f16><<<nb, kThreads, 0, s>>>(static_cast<const f16*>(x), scale, shift,
+      bn_relu_maxpool_fwd_kernel<f16><<<nb, thr, 0, s>>>(static_cast<const f16*>(x), scale, shift,
                                                               static_cast<f16*>(y), idx, g);
       break;
     case kF32:
-      bn_relu_maxpool_fwd_kernel<float><<<nb, kThreads, 0, s>>>(static_cast<const float*>(x), scale, shift,
+      bn_relu_maxpool_fwd_kernel<float><<<nb, thr, 0, s>>>(static_cast<const float*>(x), scale, shift,
                                                                 static_cast<float*>(y), idx, g);
       break;
     default:

@@ -232,7 +232,7 @@ constexpr int kPoolBytes = kPoolPer * kBT * 16;            // 24576
 constexpr int kStageBytes = kBHaloBytes + kPoolBytes;      // one iteration's DMA'd inputs
 constexpr int kTileBytes = kBPix * kCo * 2;                // 28672
 constexpr int kBSmemMain = 2 * kTileBytes + 2 * kStageBytes;  // 155648 B: two input stages
-constexpr int kBSmem = kBSmemMain + 2 * kCo * 4;           // + mean / inv
+constexpr int kBSmem = kBSmemMain + 3 * kCo * 4;           // + mean / inv / -mean * inv
 constexpr int kBDma = kBHaloPer + kPoolPer;                // DMA instructions per wave per stage
 constexpr int kPart = 2 * kKk * kCo + kKk;                 // G1 [256][64], G2 [256][64], G3 [256]
 
@@ -249,7 +249,9 @@ struct StemBwdArgs {
   int total_iters;      // N * 56
 };
 
-__device__ __forceinline__ bf16x8 tr_frag(const char* lo, const char* hi) {
+// __restrict__: gives the transposed reads alias scopes; without them the waitcnt pass assumes they
+// may read the LDS-DMA just issued into the other stage and drains vmcnt(0) before them
+__device__ __forceinline__ bf16x8 tr_frag(const char* __restrict__ lo, const char* __restrict__ hi) {
   const short4v a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(lo));
   const short4v b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(hi));
   bf16x8 out;
@@ -291,6 +293,9 @@ __device__ __forceinline__ Item item_of(int r, int wave, int slot) {
 // Pipelined: while the MFMA phase of row pair `it` runs, the DMA of row pair it + 1's image
 // halo and pooled-gradient rows (into the other stage) and this lane's conv-output loads for
 // it + 1 (registers) are in flight. One workgroup per CU (LDS: two stages + the dz / x tiles).
+// MODE (bottleneck experiments, FLUXMPI_STEM_BWD_MODE): 0 = normal, 1 = no MFMA phase,
+// 2 = no element-phase gather (dz = 0), 3 = no next-iteration loads (stale stages)
+template <int MODE>
 __global__ __launch_bounds__(kBT, 2) void stem_bwd_kernel(StemBwdArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* tdz = smem;
@@ -299,10 +304,12 @@ __global__ __launch_bounds__(kBT, 2) void stem_bwd_kernel(StemBwdArgs p) {
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4, li = lane & 15, q4 = li >> 2, pp = li & 3;
   const int cg = lane & 7, slot = lane >> 3;  // element phase: channel group, pixel slot
-  float* smi = reinterpret_cast<float*>(smem + kBSmemMain);  // [64] mean, [64] inverse std
+  float* smi = reinterpret_cast<float*>(smem + kBSmemMain);  // [64] mean, [64] inv std, [64] -mean * inv
   if (threadIdx.x < kCo) {
-    smi[threadIdx.x] = p.mean[threadIdx.x];
-    smi[kCo + threadIdx.x] = p.inv[threadIdx.x];
+    const float m = p.mean[threadIdx.x], v = p.inv[threadIdx.x];
+    smi[threadIdx.x] = m;
+    smi[kCo + threadIdx.x] = v;
+    smi[2 * kCo + threadIdx.x] = -m * v;
   }
   float s1[8], s2[8];
 #pragma unroll
@@ -392,8 +399,10 @@ __global__ __launch_bounds__(kBT, 2) void stem_bwd_kernel(StemBwdArgs p) {
     const bf16* cb = p.c + (static_cast<int64_t>(img) * kOH + h0) * kOW * kCo + cg * 8;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
+      // unconditional load (an idle item re-reads pixel 0): a branch around it made the compiler
+      // wait for every load (and every older LDS-DMA) right after issuing it
       const Item im = item_of(r, wave, slot);
-      xr[r] = im.on ? *reinterpret_cast<const uint4*>(cb + im.pix * kCo) : make_uint4(0, 0, 0, 0);
+      xr[r] = *reinterpret_cast<const uint4*>(cb + (im.on ? im.pix : 0) * kCo);
     }
   };
 
@@ -436,25 +445,26 @@ __global__ __launch_bounds__(kBT, 2) void stem_bwd_kernel(StemBwdArgs p) {
           for (int e = 0; e < 8; ++e)
             if (static_cast<int>(a8[e]) == kk) dz[e] += static_cast<float>(d8[e]);
         };
-        visit(e00, kya * 3 + kxa);
-        if (im.par) {
+        if (MODE != 2) visit(e00, kya * 3 + kxa);
+        if (MODE != 2 && im.par) {
           if (two_w) visit(e00 + kCo, kya * 3);
         }
-        if (two_h) {
+        if (MODE != 2 && two_h) {
           visit(e00 + kPW * kCo, kxa);
           if (im.par && two_w) visit(e00 + kPW * kCo + kCo, 0);
         }
         bf16 x8[8], z8[8];
         __builtin_memcpy(x8, &xr[r], 16);
-        float mu[8], iv[8];
-        __builtin_memcpy(mu, smi + cg * 8, 32);
+        float iv[8], nm[8];  // xhat = x * inv + (-mean * inv)
         __builtin_memcpy(iv, smi + kCo + cg * 8, 32);
+        __builtin_memcpy(nm, smi + 2 * kCo + cg * 8, 32);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           z8[e] = static_cast<bf16>(dz[e]);
-          const float d = static_cast<float>(z8[e]);
-          s1[e] += d;
-          s2[e] = fmaf(d, (static_cast<float>(x8[e]) - mu[e]) * iv[e], s2[e]);
+          // BN sums from the fp32 gather (the tiles get the bf16 dz); the rounding of one pool
+          // gradient per element is below the sums' own fp32 noise
+          s1[e] += dz[e];
+          s2[e] = fmaf(dz[e], fmaf(static_cast<float>(x8[e]), iv[e], nm[e]), s2[e]);
         }
         uint4 zv;
         __builtin_memcpy(&zv, z8, 16);
@@ -464,15 +474,18 @@ __global__ __launch_bounds__(kBT, 2) void stem_bwd_kernel(StemBwdArgs p) {
       }
     }
     // next row pair's inputs: its stage was last read before this iteration's barrier
-    if (it + 1 < it1) {
+    if (MODE != 3 && it + 1 < it1) {
       issue(it + 1, st ^ 1);
       load_x(it + 1, xr);
     }
-    __syncthreads();  // tiles written
+    // tiles written: LDS writes drained (lgkmcnt) and a raw barrier — __syncthreads()' fence would
+    // also drain the next row pair's loads just issued (vmcnt) and serialize them with the MFMAs
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
     // ---- MFMA phase: 7 k-steps of 32 pixels
     const char* sb = smem + sbase;
 #pragma unroll
-    for (int ks = 0; ks < kBPix / 32; ++ks) {
+    for (int ks = 0; ks < (MODE == 1 ? 0 : kBPix / 32); ++ks) {
       bf16x8 fa[4], fb[4];
 #pragma unroll
       for (int t = 0; t < 4; ++t) fa[t] = tr_frag(smem + a_lo[t] + ks * 4096, smem + a_lo[t] + ks * 4096 + 512);
@@ -603,8 +616,9 @@ void set_lds_attrs() {
   if (done) return;
   FLUXMPI_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_fwd_kernel),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, kFSmem));
-  FLUXMPI_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_bwd_kernel),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, kBSmem));
+  for (const void* k : {reinterpret_cast<const void*>(&stem_bwd_kernel<0>), reinterpret_cast<const void*>(&stem_bwd_kernel<1>),
+                        reinterpret_cast<const void*>(&stem_bwd_kernel<2>), reinterpret_cast<const void*>(&stem_bwd_kernel<3>)})
+    FLUXMPI_HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kBSmem));
   done = true;
 }
 }  // namespace
@@ -612,7 +626,7 @@ void set_lds_attrs() {
 int stem_bwd_blocks(int64_t n) {
   static int b = [] {
     set_lds_attrs();
-    const int r = resident_blocks(reinterpret_cast<const void*>(&stem_bwd_kernel), kBT, kBSmem);
+    const int r = resident_blocks(reinterpret_cast<const void*>(&stem_bwd_kernel<0>), kBT, kBSmem);
     return r > 0 ? r : 512;
   }();
   const int64_t iters = n * kPH;
@@ -650,7 +664,14 @@ void stem_bwd(const void* x, const void* c, const void* dp, const uint8_t* idx, 
   const int total = static_cast<int>(n * kPH);
   StemBwdArgs a{static_cast<const bf16*>(x), static_cast<const bf16*>(c), static_cast<const bf16*>(dp), idx, mean, inv,
                 part, stats, (total + blocks - 1) / blocks, total};
-  stem_bwd_kernel<<<static_cast<unsigned>(blocks), kBT, kBSmem, s>>>(a);
+  static const int mode = [] {
+    const char* e = std::getenv("FLUXMPI_STEM_BWD_MODE");
+    return e != nullptr ? std::atoi(e) : 0;
+  }();
+  if (mode == 1) stem_bwd_kernel<1><<<static_cast<unsigned>(blocks), kBT, kBSmem, s>>>(a);
+  else if (mode == 2) stem_bwd_kernel<2><<<static_cast<unsigned>(blocks), kBT, kBSmem, s>>>(a);
+  else if (mode == 3) stem_bwd_kernel<3><<<static_cast<unsigned>(blocks), kBT, kBSmem, s>>>(a);
+  else stem_bwd_kernel<0><<<static_cast<unsigned>(blocks), kBT, kBSmem, s>>>(a);
   FLUXMPI_HIP_CHECK(hipGetLastError());
   bn_finalize_bwd(stats, kCo, dw_bn, db_bn, s);
   stem_wgrad_combine_kernel<<<kKk, kCT, 0, s>>>(part, blocks, w, mean, inv, dw_bn, db_bn,
