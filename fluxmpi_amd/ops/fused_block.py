@@ -31,6 +31,7 @@ import os
 import torch
 
 from . import _ext
+from . import streams
 from .batchnorm import BNStatsLink, GradLink, SideGradLink, _dual_workspace, _link_workspace, _workspace, bn_counter  # noqa: F401 (links re-exported)
 from . import gemm as G
 from .gemm import conv1x1_dgrad, conv1x1_wgrad, conv3x3_dgrad, conv3x3_fwd, gemm, note_filter
@@ -115,8 +116,10 @@ class _Conv1x1Stats(torch.autograd.Function):
         x, weight = ctx.saved_tensors
         co, ci = weight.shape[0], weight.shape[1]
         dc2 = _nhwc2d(dc)
+        # weight gradient first, on the side stream: it overlaps the input-gradient chain
+        dw = streams.run(lambda: conv1x1_wgrad(dc2, _nhwc2d(x), out_dtype=weight.dtype).view_as(weight), dc, x,
+                         param=weight)
         dx = _dgrad_nhwc(dc2, weight, x, ctx.link, ctx.bnlink) if ctx.needs_input_grad[0] else None
-        dw = conv1x1_wgrad(dc2, _nhwc2d(x), out_dtype=weight.dtype).view_as(weight)
         return dx, dw, None, None
 
 
@@ -191,7 +194,6 @@ class _Conv1x1Hybrid(torch.autograd.Function):
         x, weight = ctx.saved_tensors
         if not dc.is_contiguous(memory_format=torch.channels_last):
             dc = dc.contiguous(memory_format=torch.channels_last)
-        dx = _dgrad_nhwc(_nhwc2d(dc), weight, x, ctx.link, ctx.bnlink) if ctx.needs_input_grad[0] else None
         dw = None
         if ctx.needs_input_grad[1]:
             co, ci = weight.shape[0], weight.shape[1]
@@ -202,7 +204,8 @@ class _Conv1x1Hybrid(torch.autograd.Function):
             if _w256_ok(co, ci, dc):
                 from .linear import weight_grad
                 impls["w256"] = lambda: weight_grad(_nhwc2d(dc), _nhwc2d(x), weight.dtype).view(co, ci, 1, 1)
-            dw = wgrad_best(("1x1", tuple(x.shape), co), impls)
+            dw = streams.run(lambda: wgrad_best(("1x1", tuple(x.shape), co), impls), dc, x, param=weight)
+        dx = _dgrad_nhwc(_nhwc2d(dc), weight, x, ctx.link, ctx.bnlink) if ctx.needs_input_grad[0] else None
         return dx, dw, None, None, None
 
 
@@ -243,7 +246,11 @@ class _Conv1x1Downsample(torch.autograd.Function):
                 need_x = False  # delivered
             else:
                 dx = Stride2Grad(dxc).expand(x.shape)
-        if need_w or (need_x and dx is None):
+        if need_w and not (need_x and dx is None):
+            dw = streams.run(lambda: torch.ops.aten.convolution_backward(
+                dc, x, weight, None, [s, s], [0, 0], [1, 1], False, [0, 0], 1, [False, True, False])[1], dc, x,
+                param=weight)
+        elif need_w or (need_x and dx is None):
             dx_m, dw = torch.ops.aten.convolution_backward(dc, x, weight, None, [s, s], [0, 0], [1, 1], False,
                                                            [0, 0], 1, [need_x and dx is None, need_w, False])[:2]
             dx = dx if dx is not None else dx_m
@@ -421,7 +428,10 @@ class _BNReluConv1x1(torch.autograd.Function):
         dc3_2d = _nhwc2d(dc3)
         c2_2d = _nhwc2d(c2)
         # dW = dc3^T @ relu(bn(c2))  — the activation is rebuilt on the fly in the B-operand load
-        dw = conv1x1_wgrad(dc3_2d, c2_2d, in_affine=(scale, shift), out_dtype=weight.dtype).view_as(weight)
+        # (side stream: overlaps the input-gradient chain below)
+        dw = streams.run(lambda: conv1x1_wgrad(dc3_2d, c2_2d, in_affine=(scale, shift),
+                                               out_dtype=weight.dtype).view_as(weight), dc3, c2, scale, shift,
+                         param=weight)
         # d(relu(bn(c2))) = dc3 @ W with the BN-backward reductions (ReLU mask recomputed from c2)
         # accumulated in the same GEMM's epilogue, then the BN backward without its reduce pass
         da = conv1x1_dgrad(dc3_2d, weight.reshape(co, ch), bn_bwd=(c2_2d, w32, b32, mean, inv, None, 2),
@@ -452,6 +462,12 @@ class _Conv3x3(torch.autograd.Function):
         x, weight = ctx.saved_tensors
         if not dy.is_contiguous(memory_format=torch.channels_last):
             dy = dy.contiguous(memory_format=torch.channels_last)
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = streams.run(lambda: wgrad_best(("3x3", tuple(x.shape), weight.shape[0]), {
+                "miopen": lambda: torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [1, 1], [1, 1], False,
+                                                                      [0, 0], 1, [False, True, False])[1],
+                "ours": lambda: G.conv3x3_wgrad(dy, x)}), dy, x, param=weight)
         dx = None
         if ctx.needs_input_grad[0]:
             bl = ctx.bnlink
@@ -464,12 +480,6 @@ class _Conv3x3(torch.autograd.Function):
             dx = conv3x3_dgrad(dy, weight, bn_bwd=bn, stats=stats)
             if bn is not None:
                 bl.ready = True
-        dw = None
-        if ctx.needs_input_grad[1]:
-            dw = wgrad_best(("3x3", tuple(x.shape), weight.shape[0]), {
-                "miopen": lambda: torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [1, 1], [1, 1], False,
-                                                                      [0, 0], 1, [False, True, False])[1],
-                "ours": lambda: G.conv3x3_wgrad(dy, x)})
         return dx, dw, None, None, None
 
 

@@ -21,6 +21,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _ext
+from . import streams
 from .multi_tensor import DTYPE_CODE
 
 # (N_out, N_in) -> split-K factor, from scripts/bench_vit_gemm.py on MI355X (M = 50432 tokens)
@@ -103,13 +104,20 @@ class _LinearFn(torch.autograd.Function):
         x2 = x.reshape(-1, n_in)
         if not dy2.is_contiguous():
             dy2 = dy2.contiguous()
-        dx = (dy2 @ w).reshape(x.shape) if ctx.needs_input_grad[0] else None
         dw = db = None
         native = _wgrad_mode() == "ours" and native_ok(x2, dy2)
-        if ctx.needs_input_grad[1]:
-            dw = weight_grad(dy2, x2, w.dtype) if native else dy2.t() @ x2
-        if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = bias_grad(dy2, ctx.bias_dtype) if native else dy2.sum(0).to(ctx.bias_dtype)
+        need_w = ctx.needs_input_grad[1]
+        need_b = ctx.has_bias and ctx.needs_input_grad[2]
+
+        def grads():
+            gw = (weight_grad(dy2, x2, w.dtype) if native else dy2.t() @ x2) if need_w else None
+            gb = (bias_grad(dy2, ctx.bias_dtype) if native else dy2.sum(0).to(ctx.bias_dtype)) if need_b else None
+            return gw, gb
+
+        if need_w or need_b:
+            # weight / bias gradients on the side stream, overlapping the input-gradient chain
+            dw, db = streams.run(grads, dy2, x2, param=w if need_w else None)
+        dx = (dy2 @ w).reshape(x.shape) if ctx.needs_input_grad[0] else None
         return dx, dw, db
 
 
