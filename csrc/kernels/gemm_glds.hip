@@ -38,6 +38,8 @@ constexpr int kThreads = 256;
 constexpr int kShards = 64;  // must match batchnorm.hip
 
 __device__ __attribute__((aligned(16))) uint4 g_zero_line[4];  // source of zero-filled chunks
+// stand-in for an absent 1-bit mask (all bits set)
+__device__ __attribute__((aligned(16))) uint4 g_ff_line[1] = {{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu}};
 // Out-of-image / out-of-range chunks of an operand that gets the BatchNorm+ReLU prologue: a
 // bf16 NaN payload (0x7FC1) the fragment transform maps to 0 (the padding of the ACTIVATED
 // tensor), which relu(0 * scale + shift) would not be.
@@ -224,15 +226,61 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_glds_kernel(GldsArgs p) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = static_cast<int>((p.K + kBK - 1) / kBK);
+  // ---------------------------------------------------------------- epilogue geometry
+  // each thread owns one 16-B column chunk (cc) of rows r0, r0 + RPI, ...; its residual /
+  // BN-input / mask loads go out in batches of UB rows
+  constexpr int CPR = BN / 8;          // 16-B chunks per row
+  constexpr int RPI = kThreads / CPR;  // rows per sweep
+  constexpr int UB = 4;                // rows per batch
+  constexpr int NB = (BM + UB * RPI - 1) / (UB * RPI);
+  const int cc = threadIdx.x % CPR, r0 = threadIdx.x / CPR;
+  const int64_t n = n0 + cc * 8;
+  const bool ncol_ok = n < p.N;  // N % 8 == 0 (host-checked): a chunk is all in or all out
+  const int rows_valid = p.M - m0 < BM ? static_cast<int>(p.M - m0) : BM;
+  const bool bnb = BNB && p.bnb_x != nullptr;
+  // Epilogue operand loads are UNCONDITIONAL (rows / columns outside the problem read row m0 /
+  // column 0, which exist, and are skipped when used): a load under a branch makes the compiler
+  // wait for it at the join, one exposed memory latency per row. Masks: a 0xFF byte stands in
+  // when there is none, and the even-position test of a compact stride-2 residual zeroes its mask.
+  struct EpiIn {
+    uint4 rv[RES ? UB : 1], xv[BNB ? UB : 1];
+    unsigned rmk[RES ? UB : 1], mk[BNB ? UB : 1];
+  };
+  auto epi_load = [&](int b, EpiIn& e) {
 #pragma unroll
-  for (int s = 0; s < kStages - 1; ++s)
-    if (s < nk) issue(s, static_cast<int64_t>(s) * kBK);
-  for (int t = 0; t < nk; ++t) {
-    const int ahead = nk - 1 - t < kStages - 2 ? nk - 1 - t : kStages - 2;
-    wait_tiles_ahead<LPT, kStages - 2>(ahead);  // this wave's pieces of tile t have landed
-    __builtin_amdgcn_s_barrier();   // ... and every wave's; every wave is done with tile t-1
-    if (t + kStages - 1 < nk) issue((t + kStages - 1) % kStages, static_cast<int64_t>(t + kStages - 1) * kBK);
+    for (int u = 0; u < UB; ++u) {
+      const int r = r0 + (b * UB + u) * RPI;
+      const bool ok = r < BM && r < rows_valid && ncol_ok;
+      const int64_t m = m0 + (ok ? r : 0);
+      const int64_t nn = ncol_ok ? n : 0;
+      if (RES) {
+        int64_t roff;
+        unsigned keep = 0xFFu;
+        if (p.res_sub_h > 0) {  // 32-bit row math (host-checked M < 2^31)
+          const unsigned mm = static_cast<unsigned>(m), W = p.res_sub_w;
+          const unsigned HW = static_cast<unsigned>(p.res_sub_h) * W;
+          const unsigned img = mm / HW, hw = mm - img * HW, h = hw / W, w = hw - h * W;
+          const unsigned ho = (p.res_sub_h + 1) >> 1, wo = (W + 1) >> 1;
+          roff = static_cast<int64_t>((img * ho + (h >> 1)) * wo + (w >> 1)) * p.ldr + nn;
+          keep = ((h | w) & 1u) == 0 ? 0xFFu : 0u;
+        } else {
+          roff = m * p.ldr + nn;
+        }
+        e.rv[u] = *reinterpret_cast<const uint4*>(p.res + roff);
+        const uint8_t* mp = p.res_mask != nullptr ? p.res_mask + ((m * p.N + nn) >> 3)
+                                                  : reinterpret_cast<const uint8_t*>(g_ff_line);
+        e.rmk[u] = *mp & keep;
+      }
+      if (BNB) {
+        const bf16* xp = bnb ? p.bnb_x + m * p.N + nn : reinterpret_cast<const bf16*>(g_zero_line);
+        e.xv[u] = *reinterpret_cast<const uint4*>(xp);
+        const uint8_t* mp = (bnb && p.bnb_rm == 3) ? p.bnb_mask + ((m * p.N + nn) >> 3)
+                                                   : reinterpret_cast<const uint8_t*>(g_ff_line);
+        e.mk[u] = *mp;
+      }
+    }
+  };
+  auto mma_tile = [&](int t) {
     const bf16* ta = sa(t % kStages);
     const bf16* tb = sb(t % kStages);
     // AFF: channel of this lane's fragment chunk = (k0 - tap * C) + 8 * ((lane >> 4) + 4 * kh)
@@ -255,34 +303,55 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_glds_kernel(GldsArgs p) {
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+          // B as the MFMA's first operand: D = C^T, so a lane's 4 accumulators are 4 consecutive
+          // COLUMNS of one row (one 8-B LDS write in the epilogue instead of four 2-B ones)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
     }
+  };
+
+  const int nk = static_cast<int>((p.K + kBK - 1) / kBK);
+#pragma unroll
+  for (int s = 0; s < kStages - 1; ++s)
+    if (s < nk) issue(s, static_cast<int64_t>(s) * kBK);
+  for (int t = 0; t < nk - 1; ++t) {
+    const int ahead = nk - 1 - t < kStages - 2 ? nk - 1 - t : kStages - 2;
+    wait_tiles_ahead<LPT, kStages - 2>(ahead);  // this wave's pieces of tile t have landed
+    __builtin_amdgcn_s_barrier();   // ... and every wave's; every wave is done with tile t-1
+    if (t + kStages - 1 < nk) issue((t + kStages - 1) % kStages, static_cast<int64_t>(t + kStages - 1) * kBK);
+    mma_tile(t);
   }
-  __syncthreads();  // ring fully consumed (no DMA in flight: the last wait was vmcnt(0))
+  // last tile: nothing is left to stage, so the first epilogue batch's loads go out before its
+  // MFMAs and land under them
+  wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
+  EpiIn ecur;
+  if (RES || BNB) epi_load(0, ecur);
+  if (nk > 0) mma_tile(nk - 1);
+  // ring fully consumed; lgkmcnt only (a __syncthreads() would also wait for the epilogue loads)
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_s_barrier();
 
   // ---------------------------------------------------------------- epilogue
-  // acc[i][j][r]: row m0 + wm*WM + i*16 + 4*(lane>>4) + r, col n0 + wn*WN + j*16 + (lane&15)
-  const int col_in = lane & 15, rq = 4 * (lane >> 4);
+  // acc[i][j][r]: row m0 + wm*WM + i*16 + (lane&15), col n0 + wn*WN + j*16 + 4*(lane>>4) + r
+  // (row pitch CS = BN + 8 bf16: the 32 lanes of a half-wave's 8-B writes cover 64 distinct banks)
+  const int row_in = lane & 15, cq4 = 4 * (lane >> 4);
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < FN; ++j)
+    for (int j = 0; j < FN; ++j) {
+      bf16 e4[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        smem[(wm * WM + i * 16 + rq + r) * CS + wn * WN + j * 16 + col_in] = static_cast<bf16>(acc[i][j][r]);
-  __syncthreads();
-  constexpr int CPR = BN / 8;          // 16-B chunks per row
-  constexpr int RPI = kThreads / CPR;  // rows per sweep
-  constexpr int UB = 4;                // rows per batch: their residual / BN-input loads issue together
-  const int cc = threadIdx.x % CPR, r0 = threadIdx.x / CPR;
-  const int64_t n = n0 + cc * 8;
-  const bool ncol_ok = n < p.N;  // N % 8 == 0 (host-checked): a chunk is all in or all out
-  const int rows_valid = p.M - m0 < BM ? static_cast<int>(p.M - m0) : BM;
+      for (int r = 0; r < 4; ++r) e4[r] = static_cast<bf16>(acc[i][j][r]);
+      uint2 pk;
+      __builtin_memcpy(&pk, e4, 8);
+      *reinterpret_cast<uint2*>(smem + (wm * WM + i * 16 + row_in) * CS + wn * WN + j * 16 + cq4) = pk;
+    }
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_s_barrier();
   // BN-backward epilogue (mode 1 + bnb_x): C is the output gradient of a BatchNorm whose input is
   // bnb_x; accumulate sum(dy_eff) and sum(dy_eff * xhat) per column instead of sum / sumsq of C.
   // dy_eff = C masked by the BN's ReLU: rm 2 recomputes it bit-identically to the forward
   // (fma(x, w*invstd, b - mean*w*invstd) > 0), rm 3 reads the 1-bit mask.
-  const bool bnb = BNB && p.bnb_x != nullptr;
   float bmu[BNB ? 8 : 1], biv[BNB ? 8 : 1], bsc[BNB ? 8 : 1], bsh[BNB ? 8 : 1];
   if (BNB && bnb) {
 #pragma unroll
@@ -297,45 +366,13 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_glds_kernel(GldsArgs p) {
   float cs[8], cq[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) cs[e] = cq[e] = 0.f;
-  for (int rb = r0; rb < BM; rb += UB * RPI) {
-    uint4 rv[RES ? UB : 1], xv[BNB ? UB : 1];
-    unsigned mk[BNB ? UB : 1], rmk[RES ? UB : 1];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    EpiIn enext;  // the next batch's loads fly while this one is processed
+    if ((RES || BNB) && b + 1 < NB) epi_load(b + 1, enext);
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
-      const int r = rb + u * RPI;
-      const int64_t m = m0 + r;
-      const bool ok = r < BM && r < rows_valid && ncol_ok;
-      if (RES) {
-        rv[u] = make_uint4(0, 0, 0, 0);
-        rmk[u] = 0xFFu;
-      }
-      if (BNB) {
-        xv[u] = make_uint4(0, 0, 0, 0);
-        mk[u] = 0xFFu;
-      }
-      if (RES && ok) {
-        if (p.res_sub_h > 0) {  // 32-bit row math (host-checked M < 2^31)
-          const unsigned mm = static_cast<unsigned>(m), W = p.res_sub_w;
-          const unsigned HW = static_cast<unsigned>(p.res_sub_h) * W;
-          const unsigned img = mm / HW, hw = mm - img * HW, h = hw / W, w = hw - h * W;
-          if (((h | w) & 1u) == 0) {
-            const unsigned ho = (p.res_sub_h + 1) >> 1, wo = (W + 1) >> 1;
-            const int64_t rrow = static_cast<int64_t>((img * ho + (h >> 1)) * wo + (w >> 1));
-            rv[u] = *reinterpret_cast<const uint4*>(p.res + rrow * p.ldr + n);
-          }
-        } else {
-          rv[u] = *reinterpret_cast<const uint4*>(p.res + m * p.ldr + n);
-          if (p.res_mask != nullptr) rmk[u] = p.res_mask[(m * p.N + n) >> 3];
-        }
-      }
-      if (BNB && bnb && ok) {
-        xv[u] = *reinterpret_cast<const uint4*>(p.bnb_x + m * p.N + n);
-        if (p.bnb_rm == 3) mk[u] = p.bnb_mask[(m * p.N + n) >> 3];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < UB; ++u) {
-      const int r = rb + u * RPI;
+      const int r = r0 + (b * UB + u) * RPI;
       if (r >= BM || r >= rows_valid || !ncol_ok) continue;
       const int64_t m = m0 + r;
       uint4 v = *reinterpret_cast<const uint4*>(smem + r * CS + cc * 8);
@@ -343,10 +380,10 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_glds_kernel(GldsArgs p) {
       __builtin_memcpy(e8, &v, 16);
       if (RES) {
         bf16 r8[8];
-        __builtin_memcpy(r8, &rv[u], 16);
+        __builtin_memcpy(r8, &ecur.rv[u], 16);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const float rf = (rmk[u] >> e) & 1u ? static_cast<float>(r8[e]) : 0.f;
+          const float rf = (ecur.rmk[u] >> e) & 1u ? static_cast<float>(r8[e]) : 0.f;
           e8[e] = static_cast<bf16>(static_cast<float>(e8[e]) + rf);
         }
         __builtin_memcpy(&v, e8, 16);
@@ -354,13 +391,12 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_glds_kernel(GldsArgs p) {
       *reinterpret_cast<uint4*>(p.c + m * p.ldc + n) = v;
       if (BNB && bnb) {
         bf16 x8[8];
-        __builtin_memcpy(x8, &xv[u], 16);
+        __builtin_memcpy(x8, &ecur.xv[u], 16);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float xf = static_cast<float>(x8[e]);
-          bool keep = true;
+          bool keep = (ecur.mk[u] >> e) & 1u;  // rm 3: the saved bit; 0xFF otherwise
           if (p.bnb_rm == 2) keep = fmaf(xf, bsc[e], bsh[e]) > 0.f;
-          if (p.bnb_rm == 3) keep = (mk[u] >> e) & 1u;
           const float dd = keep ? static_cast<float>(e8[e]) : 0.f;
           cs[e] += dd;
           cq[e] = fmaf(dd, (xf - bmu[e]) * biv[e], cq[e]);
@@ -374,6 +410,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_glds_kernel(GldsArgs p) {
         }
       }
     }
+    if ((RES || BNB) && b + 1 < NB) ecur = enext;
   }
   if (p.mode == 1) {
     // lanes of a wave with equal cc differ in the bits above log2(CPR): butterfly them, then
@@ -708,12 +745,12 @@ void gemm_glds(const GemmProblem& g, hipStream_t stream) {
   const bool aff = g.a_scale != nullptr;
   const bool bnb = g.bnb_x != nullptr;
   const bool conv = g.conv_h > 0, res = g.res != nullptr;
-  // variant: 1 BK32/3 stages; 2 BK32/4; 3 BK64/2; 4 BK64/3 (engine 3..6 force one, for experiments).
+  // variant: 1 BK32/3 stages; 2 BK32/4; 3 BK64/2; 4 BK64/3; 5 BK32/2 (engine 3..6 / 9 force one).
   // Auto (measured on MI355X, ResNet-50 1x1 and 3x3 shapes): a 64-deep K-step in a 2-stage ring
   // (64 KiB at 128x128: 2 workgroups/CU) wins for the 3x3 convolutions and once K >= 1024;
   // shorter K (memory-bound 1x1 convolutions) prefers the 32-deep 3-stage ring (48 KiB:
   // 3 workgroups/CU).
-  int var = g.engine >= 3 && g.engine <= 6 ? g.engine - 2 : 0;
+  int var = g.engine >= 3 && g.engine <= 6 ? g.engine - 2 : (g.engine == 9 ? 5 : 0);
   // engine 7 / 8: 256x128 tiles (waves of 128x64: 25% less LDS fragment traffic per MFMA than
   // 64x64 waves), 32-deep 3-stage / 64-deep 2-stage ring; plain / residual / implicit-conv only
   const bool big = (g.engine == 7 || g.engine == 8) && !aff && !bnb && g.M > 128 && g.N > 64;
@@ -729,7 +766,10 @@ void gemm_glds(const GemmProblem& g, hipStream_t stream) {
     return;
   }
   const bool k64ok = !conv || g.conv_c % 64 == 0;
-  if (var == 0) var = ((conv || g.K >= 1024) && k64ok) ? 3 : 1;
+  // K <= 64 (two 32-deep steps: all in flight after one wait anyway): a 2-stage ring, whose
+  // smaller LDS footprint (the C staging tile sets it) fits a 4th workgroup per CU — measured
+  // 153 -> 116 us on ResNet-50's 56x56 64->256 forward (scripts/bench_gemm_bw.py)
+  if (var == 0) var = ((conv || g.K >= 1024) && k64ok) ? 3 : (g.K <= 64 ? 5 : 1);
   if ((var == 3 || var == 4) && !k64ok) var = 1;
   // 128x128 tiles whenever both dimensions allow (measured: 128x64 tiles lose more to the lower
   // operand reuse than they win back from finer wave quantization)
@@ -749,6 +789,7 @@ void gemm_glds(const GemmProblem& g, hipStream_t stream) {
     if (var == 1) GV(BM, BN, 32, 3)         \
     else if (var == 3) GV(BM, BN, 64, 2)    \
     else if (var == 4) GV(BM, BN, 64, 3)    \
+    else if (var == 5) GV(BM, BN, 32, 2)    \
     else GV(BM, BN, 32, 4)                  \
   }
   if (bm128 && bn128) GL(128, 128)
