@@ -188,6 +188,10 @@ struct GemmProblem {
   // (n, h/2, w/2) when h and w are even and nothing otherwise (a stride-2 1x1 convolution's input
   // gradient, without the zero-filled full-resolution tensor). No res_mask with it.
   int res_sub_h = 0, res_sub_w = 0;
+  // LDS-DMA kernel: a_sub_h > 0 — A row (n, ho, wo) of an [M/(Ho*Wo)][Ho][Wo] output grid is row
+  // (n, 2*ho, 2*wo) of the NHWC image [M/(Ho*Wo)][a_sub_h][a_sub_w][lda] (Ho = ceil(H/2)): a
+  // stride-2 1x1 convolution without the strided copy of its input. Plain K-major A only.
+  int a_sub_h = 0, a_sub_w = 0;
 };
 void gemm_bf16(const GemmProblem& g, hipStream_t stream);
 // the LDS-DMA pipelined kernel: K-major A (or implicit conv) and B, modes 0/1, optional residual,

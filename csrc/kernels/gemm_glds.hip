@@ -72,6 +72,7 @@ struct GldsArgs {
   const float* a_scale;  // AFF: A element (m, k) -> relu(A * a_scale[c] + a_shift[c]), c = channel of k
   const float* a_shift;
   int aff_c;             // channels of the affine (C for the implicit conv, K for a 1x1)
+  int a_sub_h, a_sub_w;  // > 0: A row (n, ho, wo) is image row (n, 2ho, 2wo) of [.][a_sub_h][a_sub_w] (see api.h)
 };
 
 // s_waitcnt vmcnt(N) with expcnt / lgkmcnt left alone (gfx9 encoding)
@@ -99,10 +100,12 @@ __device__ __forceinline__ int swz(int row) {
 // A 1 KiB piece holds RPP = 512/BK rows; piece j of wave w covers tile rows
 // (w * PPW + j) * RPP ..; lane l fills row +(l / CPR), slot (l % CPR) with global chunk
 // slot ^ swz(row).
+// srow (plain operand, optional): the source row of piece j's rows, if not grow itself.
 template <int ROWS, int BK, bool CONV, bool PAD = false>
 __device__ __forceinline__ void issue_tile(bf16* lds_tile, const bf16* __restrict__ g, int64_t ld,
                                            int64_t rows, int64_t r0, int64_t k0, int64_t kend,
-                                           const int* ph, const int* pw, int H, int W, int C) {
+                                           const int* ph, const int* pw, int H, int W, int C,
+                                           const int64_t* srow = nullptr) {
   constexpr int CPR = BK / 8, RPP = 64 / CPR;
   constexpr int PPW = ROWS * BK / 2048;  // 1 KiB pieces per wave
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -125,7 +128,7 @@ __device__ __forceinline__ void issue_tile(bf16* lds_tile, const bf16* __restric
           static_cast<unsigned>(pw[j] + ds) < static_cast<unsigned>(W))
         src = g + (grow + dr * W + ds) * C + c0 + q * 8;
     } else {
-      if (grow < rows && k0 + q * 8 < kend) src = g + grow * ld + k0 + q * 8;
+      if (grow < rows && k0 + q * 8 < kend) src = g + (srow != nullptr ? srow[j] : grow) * ld + k0 + q * 8;
     }
     typedef __attribute__((address_space(3))) char lds_char;
     typedef __attribute__((address_space(1))) void gl_void;
@@ -207,8 +210,24 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_glds_kernel(GldsArgs p) {
       pw[j] = hw - ph[j] * p.conv_w;
     }
   }
+  // plain A: the image row each staged A row reads (a_sub: the stride-2 subsample's source pixel)
+  int64_t arow[CONV ? 1 : PPWA];
+  if (!CONV) {
+#pragma unroll
+    for (int j = 0; j < PPWA; ++j) {
+      const int64_t row = m0 + (wave * PPWA + j) * RPPA + lane / (kBK / 8);
+      arow[j] = row;
+      if (p.a_sub_h > 0) {  // 32-bit math (host-checked M < 2^31)
+        const unsigned ho = (p.a_sub_h + 1) >> 1, wo = (p.a_sub_w + 1) >> 1;
+        const unsigned mm = static_cast<unsigned>(row), hw = ho * wo;
+        const unsigned img = mm / hw, r = mm - img * hw, y = r / wo, x = r - y * wo;
+        arow[j] = (static_cast<int64_t>(img) * p.a_sub_h + 2 * y) * p.a_sub_w + 2 * x;
+      }
+    }
+  }
   auto issue = [&](int s, int64_t k0) {
-    issue_tile<BM, kBK, CONV, AFF>(sa(s), p.a, p.lda, p.M, m0, k0, p.K, ph, pw, p.conv_h, p.conv_w, p.conv_c);
+    issue_tile<BM, kBK, CONV, AFF>(sa(s), p.a, p.lda, p.M, m0, k0, p.K, ph, pw, p.conv_h, p.conv_w, p.conv_c,
+                                   CONV ? nullptr : arow);
     issue_tile<BN, kBK, false>(sb(s), p.b, p.ldb, p.N, n0, k0, p.K, nullptr, nullptr, 0, 0, 0);
   };
   float* st_lds = reinterpret_cast<float*>(smem + kRingOrC);
@@ -719,6 +738,8 @@ bool gemm_glds_supported(const GemmProblem& g) {
          (g.bnb_x == nullptr || (g.mode == 1 && g.ldc == g.N && g.bnb_mean != nullptr && g.bnb_inv != nullptr &&
                                  (g.bnb_rm == 0 || g.bnb_rm == 2 || (g.bnb_rm == 3 && g.bnb_mask != nullptr)))) &&
          (g.conv_h == 0 || (g.conv_c % 32 == 0 && g.K == 9LL * g.conv_c)) &&
+         (g.a_sub_h == 0 || (g.conv_h == 0 && g.a_kmajor && g.a_sub_w > 0 && g.M < (1LL << 31) &&
+                             g.M % (static_cast<int64_t>((g.a_sub_h + 1) / 2) * ((g.a_sub_w + 1) / 2)) == 0)) &&
          (g.res_sub_h == 0 || (g.res != nullptr && g.res_mask == nullptr && g.res_sub_w > 0 && g.M < (1LL << 31) &&
                                g.M % (static_cast<int64_t>(g.res_sub_h) * g.res_sub_w) == 0));
 }
@@ -741,6 +762,7 @@ void gemm_glds(const GemmProblem& g, hipStream_t stream) {
   a.a_scale = g.a_scale; a.a_shift = g.a_shift;
   a.res_mask = g.res_mask;
   a.res_sub_h = g.res_sub_h; a.res_sub_w = g.res_sub_w;
+  a.a_sub_h = g.a_sub_h; a.a_sub_w = g.a_sub_w;
   a.aff_c = static_cast<int>(g.conv_h > 0 ? g.conv_c : g.K);
   const bool aff = g.a_scale != nullptr;
   const bool bnb = g.bnb_x != nullptr;
@@ -769,7 +791,9 @@ void gemm_glds(const GemmProblem& g, hipStream_t stream) {
   // K <= 64 (two 32-deep steps: all in flight after one wait anyway): a 2-stage ring, whose
   // smaller LDS footprint (the C staging tile sets it) fits a 4th workgroup per CU — measured
   // 153 -> 116 us on ResNet-50's 56x56 64->256 forward (scripts/bench_gemm_bw.py)
-  if (var == 0) var = ((conv || g.K >= 1024) && k64ok) ? 3 : (g.K <= 64 ? 5 : 1);
+  // The stride-2 row gather (a_sub) likewise: 108 / 73 us vs 119 / 83 us with 3 stages on the
+  // 56x56 256->512 and 28x28 512->1024 downsample convolutions (scripts/bench_ds.py).
+  if (var == 0) var = ((conv || g.K >= 1024) && k64ok) ? 3 : ((g.K <= 64 || g.a_sub_h > 0) ? 5 : 1);
   if ((var == 3 || var == 4) && !k64ok) var = 1;
   // 128x128 tiles whenever both dimensions allow (measured: 128x64 tiles lose more to the lower
   // operand reuse than they win back from finer wave quantization)

@@ -162,9 +162,13 @@ class Bottleneck(nn.Module):
                     identity = x
                 elif fused_ds:
                     ds = self.downsample
+                    dual = out_link is None and fb.dual_bn_ok(x, ds[0].out_channels, self.bn3, ds[1])
+                    # our GEMM (+ the downsample BN's sums in its epilogue) where measured faster
+                    ds_stats = dual and fb.ds_forward_is_ours(x, ds[0].weight, ds[0].stride[0])
                     identity = fb.conv1x1_downsample(x, ds[0].weight, ds[0].stride[0],
-                                                     link if isinstance(link, fb.SideGradLink) else None)
-                    if out_link is None and fb.dual_bn_supported(identity, self.bn3, ds[1]):
+                                                     link if isinstance(link, fb.SideGradLink) else None,
+                                                     ours_stats=ds_stats)
+                    if dual:
                         cds, identity = identity, None
                     else:
                         identity = ds[1](identity)
@@ -187,7 +191,7 @@ class Bottleneck(nn.Module):
                     c3 = fb.bn_relu_conv1x1(c2, self.bn2, self.conv3.weight)  # bn2+relu fused into the A load
                 if cds is not None:
                     out = fb.dual_bn_relu(c3, self.bn3, cds, self.downsample[1],
-                                          stats_ready=o3 if self.hybrid else True)
+                                          stats_ready=o3 if self.hybrid else True, ds_stats_ready=ds_stats)
                 elif self.hybrid and not o3:
                     out = self.bn3(c3, relu=True, residual=identity, link=link if self.downsample is None else None,
                                    bnlink=out_link)

@@ -56,6 +56,10 @@ WGRAD = os.environ.get("FLUXMPI_WGRAD", "auto")
 # downsample blocks: bn3 and the downsample branch's BatchNorm as one dual kernel pair
 # (relu(bn3(c3) + bn_ds(c_ds)) without materialising bn_ds(c_ds); see dual_bn_relu)
 DUAL_BN = os.environ.get("FLUXMPI_DUAL_BN", "1") == "1"
+# downsample 1x1 forward: "ours" = our GEMM (stride 2 gathers the even pixels in the A staging)
+# with the downsample BatchNorm's sums in its epilogue where measured faster than MIOpen + the
+# statistics pass (dual-BN blocks only); "force" = ours wherever supported; "miopen" = always MIOpen
+DS_FWD = os.environ.get("FLUXMPI_DS_FWD", "ours")
 
 
 def _stream(t):
@@ -209,19 +213,72 @@ class _Conv1x1Hybrid(torch.autograd.Function):
         return dx, dw, None, None, None
 
 
+def _ds_fwd_ours(x, weight, stride, stats):
+    """The downsample convolution on our GEMM (stride 2: A rows gathered from the even pixels,
+    no strided copy), its BatchNorm's per-channel sums into ``stats``."""
+    n, ci, h, w = x.shape
+    co = weight.shape[0]
+    ho, wo = (h + stride - 1) // stride, (w + stride - 1) // stride
+    c = _empty_nhwc(n, co, ho, wo, x)
+    gemm(_nhwc2d(x), weight.reshape(co, ci), c, M=n * ho * wo, N=co, K=ci, lda=ci, ldb=ci, ldc=co, mode=1,
+         stats=stats, a_sub=(h, w) if stride == 2 else None)
+    return c
+
+
+def ds_forward_supported(x, weight, stride) -> bool:
+    return (DS_FWD in ("ours", "force") and G.ENGINE != 1 and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
+            and weight.dtype == torch.bfloat16 and stride in (1, 2) and x.shape[1] % 8 == 0
+            and weight.shape[0] % 8 == 0 and x.numel() // x.shape[1] < 2 ** 31)
+
+
+_DS_CHOICE: dict = {}
+
+
+def ds_forward_is_ours(x, weight, stride) -> bool:
+    """Per-shape choice of the downsample forward, measured once: our GEMM with the statistics
+    epilogue vs MIOpen plus the statistics pass its BatchNorm then needs (one read of the output
+    at 5 TB/s)."""
+    if not ds_forward_supported(x, weight, stride):
+        return False
+    if DS_FWD == "force":
+        return True
+    key = (tuple(x.shape), weight.shape[0], stride)
+    hit = _DS_CHOICE.get(key)
+    if hit is not None:
+        return hit
+    if torch.cuda.is_current_stream_capturing():
+        return True
+    with torch.no_grad():
+        xs = x.detach().contiguous(memory_format=torch.channels_last)
+        w = weight.detach()
+        ws = torch.zeros_like(_workspace(xs))
+        ours = _time_us(lambda: _ds_fwd_ours(xs, w, stride, ws))
+        theirs = _time_us(lambda: torch.nn.functional.conv2d(xs, w, None, stride))
+    n, _, h, wd = x.shape
+    stats_pass_us = n * ((h + stride - 1) // stride) * ((wd + stride - 1) // stride) * weight.shape[0] * \
+        x.element_size() / 5e12 * 1e6
+    choice = ours <= theirs + stats_pass_us
+    _DS_CHOICE[key] = choice
+    return choice
+
+
 class _Conv1x1Downsample(torch.autograd.Function):
-    """The downsample 1x1 convolution (stride 1 or 2) of a ResNet block, MIOpen forward and
-    weight gradient. Its input gradient (our dgrad GEMM; at stride 2 over the output pixels
-    only, in the compact :class:`Stride2Grad` form) is handed to the block's conv1 through a
-    :class:`SideGradLink`, whose dgrad epilogue adds it: no separate add kernel over the block
-    input's gradient, and at stride 2 no zero-filled full-resolution gradient either."""
+    """The downsample 1x1 convolution (stride 1 or 2) of a ResNet block: forward on MIOpen, or
+    (``stats``) on our GEMM with its BatchNorm's sums left pending in ``stats`` (the dual BN
+    consumes them); weight gradient on MIOpen. Its input gradient (our dgrad GEMM; at stride 2
+    over the output pixels only, in the compact :class:`Stride2Grad` form) is handed to the
+    block's conv1 through a :class:`SideGradLink`, whose dgrad epilogue adds it: no separate add
+    kernel over the block input's gradient, and at stride 2 no zero-filled full-resolution
+    gradient either."""
 
     @staticmethod
-    def forward(ctx, x, weight, stride, link):
+    def forward(ctx, x, weight, stride, link, stats=None):
         x = x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
         ctx.stride, ctx.link = stride, link
         note_filter(weight)
         ctx.save_for_backward(x, weight)
+        if stats is not None:
+            return _ds_fwd_ours(x, weight, stride, stats)
         return torch.nn.functional.conv2d(x, weight, None, stride)
 
     @staticmethod
@@ -256,11 +313,13 @@ class _Conv1x1Downsample(torch.autograd.Function):
             dx = dx if dx is not None else dx_m
         if dx is not None and ctx.link is not None and ctx.link.offer(dx):
             dx = None  # delivered to conv1's dgrad epilogue
-        return dx, dw, None, None
+        return dx, dw, None, None, None
 
 
-def conv1x1_downsample(x, weight, stride, link=None):
-    return _Conv1x1Downsample.apply(x, weight, stride, link)
+def conv1x1_downsample(x, weight, stride, link=None, ours_stats=False):
+    """``ours_stats`` (see :func:`ds_forward_is_ours`): forward on our GEMM with the output's
+    BatchNorm sums pending in the dual workspace, for ``dual_bn_relu(..., ds_stats_ready=True)``."""
+    return _Conv1x1Downsample.apply(x, weight, stride, link, _dual_workspace(x) if ours_stats else None)
 
 
 class _BNFromStats(torch.autograd.Function):
@@ -326,7 +385,8 @@ class _DualBN(torch.autograd.Function):
     (~10 B/element saved on a block's largest activations)."""
 
     @staticmethod
-    def forward(ctx, c3, w, b, rm, rv, mom, eps, nbt, stats_ready, cds, w2, b2, rm2, rv2, mom2, eps2, nbt2):
+    def forward(ctx, c3, w, b, rm, rv, mom, eps, nbt, stats_ready, cds, w2, b2, rm2, rv2, mom2, eps2, nbt2,
+                ds_ready=False):
         C = _ext.get(required=True)
         cl = torch.channels_last
         c3 = c3 if c3.is_contiguous(memory_format=cl) else c3.contiguous(memory_format=cl)
@@ -341,9 +401,11 @@ class _DualBN(torch.autograd.Function):
         C.bn_stats_finalize(c3.data_ptr(), w32.data_ptr(), b32.data_ptr(), _p(rm), _p(rv), mean.data_ptr(),
                             inv.data_ptr(), 0, 0, ws.data_ptr(), rows, ch, float(mom), float(eps), int(stats_ready),
                             code, st, _p(nbt))
+        # bn_ds: its sums pending in the dual workspace (the downsample GEMM's epilogue), or a stats pass
+        ws2 = _dual_workspace(c3) if ds_ready else ws
         C.bn_stats_finalize(cds.data_ptr(), w232.data_ptr(), b232.data_ptr(), _p(rm2), _p(rv2), mean2.data_ptr(),
-                            inv2.data_ptr(), 0, 0, ws.data_ptr(), rows, ch, float(mom2), float(eps2), 0, code, st,
-                            _p(nbt2))
+                            inv2.data_ptr(), 0, 0, ws2.data_ptr(), rows, ch, float(mom2), float(eps2), int(ds_ready),
+                            code, st, _p(nbt2))
         y = torch.empty_like(c3)
         mask = torch.empty(c3.numel() // 8, device=c3.device, dtype=torch.uint8)
         C.bn_apply_dual(c3.data_ptr(), cds.data_ptr(), y.data_ptr(), w32.data_ptr(), b32.data_ptr(), mean.data_ptr(),
@@ -370,7 +432,7 @@ class _DualBN(torch.autograd.Function):
                       _stream(c3))
         t1, t2 = ctx.wdtypes
         return (dx, dw.to(t1), db.to(t1), None, None, None, None, None, None,
-                dx2, dw2.to(t2), db2.to(t2), None, None, None, None, None)
+                dx2, dw2.to(t2), db2.to(t2), None, None, None, None, None, None)
 
 
 def dual_bn_supported(c, bn, bn_ds) -> bool:
@@ -383,13 +445,25 @@ def dual_bn_supported(c, bn, bn_ds) -> bool:
                     for m in (bn, bn_ds)))
 
 
-def dual_bn_relu(c3, bn, cds, bn_ds, stats_ready=False):
+def dual_bn_relu(c3, bn, cds, bn_ds, stats_ready=False, ds_stats_ready=False):
     """relu(bn(c3) + bn_ds(cds)) (training); ``stats_ready``: bn's sums are pending in the
-    workspace from the GEMM that produced c3."""
+    workspace from the GEMM that produced c3; ``ds_stats_ready``: bn_ds's sums are pending in the
+    dual workspace (``conv1x1_downsample(..., ours_stats=True)``)."""
     mom, nbt = bn_counter(bn)
     mom2, nbt2 = bn_counter(bn_ds)
     return _DualBN.apply(c3, bn.weight, bn.bias, bn.running_mean, bn.running_var, mom, bn.eps, nbt, stats_ready,
-                         cds, bn_ds.weight, bn_ds.bias, bn_ds.running_mean, bn_ds.running_var, mom2, bn_ds.eps, nbt2)
+                         cds, bn_ds.weight, bn_ds.bias, bn_ds.running_mean, bn_ds.running_var, mom2, bn_ds.eps, nbt2,
+                         ds_stats_ready)
+
+
+def dual_bn_ok(x, ch, bn, bn_ds) -> bool:
+    """:func:`dual_bn_supported` for the output (``ch`` channels, x's dtype/device) of a
+    convolution of ``x``, decided before running it."""
+    from .batchnorm import FusedBatchNorm2d
+    return (DUAL_BN and x.is_cuda and x.dtype in (torch.bfloat16, torch.float16, torch.float32) and x.dim() == 4
+            and ch % 8 == 0 and 8 <= ch <= 2048 and (ch & (ch - 1)) == 0
+            and all(isinstance(m, FusedBatchNorm2d) and m.training and m.affine and m.track_running_stats
+                    for m in (bn, bn_ds)))
 
 
 class _BNReluConv1x1(torch.autograd.Function):

@@ -44,9 +44,10 @@ def _ptr(t):
 
 def gemm(a, b, c, *, M, N, K, lda, ldb, ldc, a_kmajor=True, b_kmajor=True, mode=0, splits=1, a_affine=None,
          b_affine=None, stats=None, tile_m=0, tile_n=0, nbuf=0, residual=None, bn_bwd=None, conv=None, engine=None,
-         res_mask=None, res_sub=None):
+         res_mask=None, res_sub=None, a_sub=None):
     """``res_sub=(H, W)``: ``residual`` is the compact stride-2 subsample of the [M/(H*W), H, W]
-    row grid (added at even (h, w) only). ``bn_bwd``: ``(x2d, w32, b32, mean, inv, mask, relu_mode)`` of a BatchNorm whose output
+    row grid (added at even (h, w) only). ``a_sub=(H, W)``: A row (n, ho, wo) is pixel (n, 2ho, 2wo)
+    of the NHWC image ``a`` [M/(Ho*Wo), H, W, lda] (a stride-2 1x1 convolution). ``bn_bwd``: ``(x2d, w32, b32, mean, inv, mask, relu_mode)`` of a BatchNorm whose output
     gradient is C — with ``mode=1`` the epilogue accumulates that BatchNorm's backward
     reductions into ``stats`` instead of C's sum / sum of squares. ``conv=(H, W, C)``: A is the
     implicit 3x3/s1/p1 im2col of the NHWC image batch ``a`` (K = 9*C)."""
@@ -58,7 +59,8 @@ def gemm(a, b, c, *, M, N, K, lda, ldb, ldc, a_kmajor=True, b_kmajor=True, mode=
                 _ptr(asc), _ptr(ash), _ptr(bsc), _ptr(bsh), _ptr(stats), tile_m, tile_n, _stream(c), nbuf or NBUF,
                 _ptr(residual), residual.stride(0) if residual is not None else 0, _ptr(bx), _ptr(bw), _ptr(bb),
                 _ptr(bmean), _ptr(binv), _ptr(bmask), int(brm), *(conv if conv is not None else (0, 0, 0)),
-                ENGINE if engine is None else engine, _ptr(res_mask), *(res_sub if res_sub is not None else (0, 0)))
+                ENGINE if engine is None else engine, _ptr(res_mask), *(res_sub if res_sub is not None else (0, 0)),
+                *(a_sub if a_sub is not None else (0, 0)))
     return c
 
 

@@ -283,12 +283,15 @@ def test_dual_bn_relu(gpu_ext, ch, hw):
 
 
 @pytest.mark.parametrize("impl", ["hybrid", "fused"])
-def test_resnet_dual_bn_matches_separate(gpu_ext, impl, monkeypatch):
+@pytest.mark.parametrize("ds_fwd", ["miopen", "force"])
+def test_resnet_dual_bn_matches_separate(gpu_ext, impl, ds_fwd, monkeypatch):
     """The ResNet downsample blocks with the dual BatchNorm vs the separate bn_ds + bn3 path,
     both measured against the fp32 model (bf16 gradients of a deep net differ by ~10-30% at
-    the stem between any two bf16 pipelines; the dual one must be as accurate)."""
+    the stem between any two bf16 pipelines; the dual one must be as accurate). ``force``: the
+    downsample forward on our GEMM (stride-2 row gather) with bn_ds's sums from its epilogue."""
     from fluxmpi_amd.models.resnet import ResNet
     from fluxmpi_amd.ops import fused_block as fb
+    monkeypatch.setattr(fb, "DS_FWD", ds_fwd)
     outs = []
     x = torch.randn(8, 3, 64, 64, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
     for dual in (False, True):

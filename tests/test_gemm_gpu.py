@@ -87,3 +87,24 @@ def test_asymmetric_identity(gpu_ext):
     b = (torch.arange(n * n, device="cuda").reshape(n, n) % 97).to(torch.bfloat16)
     assert torch.equal(conv1x1_fwd(eye, b).float(), b.float().t())
     assert torch.equal(conv1x1_dgrad(eye, b).float(), b.float())
+
+
+@pytest.mark.parametrize("n,h,w,ci,co", [(2, 8, 8, 64, 128), (3, 7, 5, 32, 64), (1, 14, 14, 256, 512)])
+@pytest.mark.parametrize("engine", [2, 3, 6, 9])
+def test_stride2_rows(gpu_ext, n, h, w, ci, co, engine):
+    """a_sub: the stride-2 1x1 convolution as a GEMM whose A rows are gathered from the even
+    pixels (odd image sizes included), with the BatchNorm statistics epilogue."""
+    from fluxmpi_amd.ops.gemm import SHARDS, gemm
+    x = _rand(n, h, w, ci)
+    wt = _rand(co, ci) * 0.1
+    ho, wo = (h + 1) // 2, (w + 1) // 2
+    c = torch.empty(n * ho * wo, co, device="cuda", dtype=torch.bfloat16)
+    stats = torch.zeros(SHARDS, 2, co, device="cuda")
+    gemm(x.reshape(-1, ci), wt, c, M=n * ho * wo, N=co, K=ci, lda=ci, ldb=ci, ldc=co, mode=1, stats=stats,
+         a_sub=(h, w), engine=engine)
+    ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).float(), wt.float()[:, :, None, None], stride=2)
+    ref = ref.permute(0, 2, 3, 1).reshape(-1, co)
+    torch.testing.assert_close(c.float(), ref.to(torch.bfloat16).float(), rtol=2e-2, atol=2e-2)
+    cf = c.float()
+    torch.testing.assert_close(stats[:, 0].sum(0), cf.sum(0), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(stats[:, 1].sum(0), (cf * cf).sum(0), rtol=1e-3, atol=1e-2)
