@@ -567,7 +567,7 @@ def conv3x3_supported(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
 _FWD_CHOICE: dict = {}  # (N, C, H, W, Co) -> True: our forward (+ statistics epilogue) is faster
 
 
-def _time_us(fn, iters=5, repeats=2):
+def _time_us(fn, iters=10, repeats=3):
     """Best of ``repeats`` timings of ``iters`` back-to-back calls (autotune: choices flip on
     single-sample noise otherwise)."""
     for _ in range(2):
