@@ -18,6 +18,7 @@
 // needs no memset per call); the consumer kernels derive their per-channel
 // coefficients from those statistics (registers, or LDS when C/8 does not divide
 // the workgroup). Grids are one full round of resident workgroups (occupancy x CUs).
+#include <cstdlib>
 #include <initializer_list>
 #include <stdexcept>
 #include <string>
@@ -277,7 +278,7 @@ __device__ __forceinline__ void norm_vec(float (&f)[8], const float (&rr)[8], co
   }
 }
 
-template <typename T, bool RELU, bool RES, bool FIXED>
+template <typename T, bool RELU, bool RES, bool FIXED, int U = 2>
 __global__ __launch_bounds__(kThreads) void bn_norm_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                            const T* __restrict__ res, const float* __restrict__ w,
                                                            const float* __restrict__ b,
@@ -300,8 +301,10 @@ __global__ __launch_bounds__(kThreads) void bn_norm_kernel(const T* __restrict__
     float mu[8], s2[8], ww[8], bb[8];
     ld8ch(mean_in, c0, mu);
     ld8ch(stat2, c0, s2);
-    if (w) ld8ch(w, c0, ww);
-    if (b) ld8ch(b, c0, bb);
+    // unconditional (a stand-in source when absent): a load under `if (w)` is waited for at the
+    // join, one exposed latency each before the streaming starts
+    ld8ch(w ? w : mean_in, c0, ww);
+    ld8ch(b ? b : mean_in, c0, bb);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float invstd = train ? s2[j] : rsqrtf(s2[j] + eps);  // save_invstd | running_var
@@ -312,31 +315,28 @@ __global__ __launch_bounds__(kThreads) void bn_norm_kernel(const T* __restrict__
     for (int c = threadIdx.x; c < C; c += kThreads) coef(c, smem[c], smem[C + c]);
     __syncthreads();
   }
+  // U vectors per lane per iteration, every load issued before any math
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
   int64_t v = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
-  for (; v + stride < nvec; v += 2 * stride) {
-    float f0[8], f1[8], r0[8], r1[8];
-    ld8f(x + v * 8, f0);
-    ld8f(x + (v + stride) * 8, f1);
-    if (RES) {
-      ld8f(res + v * 8, r0);
-      ld8f(res + (v + stride) * 8, r1);
+  for (; v + (U - 1) * stride < nvec; v += U * stride) {
+    float f[U][8], r[U][8];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      ld8f(x + (v + u * stride) * 8, f[u]);
+      if (RES) ld8f(res + (v + u * stride) * 8, r[u]);
     }
-    const float* sc0 = FIXED ? rsc : smem + (v * 8) % C;
-    const float* sh0 = FIXED ? rsh : smem + C + (v * 8) % C;
-    const float* sc1 = FIXED ? rsc : smem + ((v + stride) * 8) % C;
-    const float* sh1 = FIXED ? rsh : smem + C + ((v + stride) * 8) % C;
-    unsigned b0, b1;
-    norm_vec<T, RELU, RES>(f0, r0, sc0, sh0, b0);
-    norm_vec<T, RELU, RES>(f1, r1, sc1, sh1, b1);
-    st8f(y + v * 8, f0);
-    st8f(y + (v + stride) * 8, f1);
-    if (RELU && mask != nullptr) {
-      mask[v] = static_cast<uint8_t>(b0);
-      mask[v + stride] = static_cast<uint8_t>(b1);
+    __builtin_amdgcn_sched_barrier(0);  // keep every load ahead of the first store
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t vu = v + u * stride;
+      unsigned bits;
+      norm_vec<T, RELU, RES>(f[u], r[u], FIXED ? rsc : smem + (vu * 8) % C, FIXED ? rsh : smem + C + (vu * 8) % C,
+                             bits);
+      st8f(y + vu * 8, f[u]);
+      if (RELU && mask != nullptr) mask[vu] = static_cast<uint8_t>(bits);
     }
   }
-  if (v < nvec) {
+  for (; v < nvec; v += stride) {
     float f0[8], r0[8];
     ld8f(x + v * 8, f0);
     if (RES) ld8f(res + v * 8, r0);
@@ -370,8 +370,8 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const T* __rest
     float mu[8], is[8], sc[8], sh[8], ww[8], bb[8];
     ld8ch(smean, c8 * 8, mu);
     ld8ch(sinv, c8 * 8, is);
-    if (w) ld8ch(w, c8 * 8, ww);
-    if (b) ld8ch(b, c8 * 8, bb);
+    ld8ch(w ? w : smean, c8 * 8, ww);  // unconditional: see bn_norm_kernel
+    ld8ch(b ? b : smean, c8 * 8, bb);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       sc[j] = (w ? ww[j] : 1.f) * is[j];
@@ -464,7 +464,7 @@ __device__ __forceinline__ void dx_vec(float (&d)[8], float (&xv)[8], const floa
   }
 }
 
-template <typename T, int RM, bool DRES, bool FIXED>
+template <typename T, int RM, bool DRES, bool FIXED, int U = 2>
 __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                              const T* __restrict__ y,
                                                              const uint8_t* __restrict__ mask,
@@ -486,8 +486,8 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const T* __restrict
     ld8ch(smean, c0, m);
     ld8ch(db, c0, kdb);
     ld8ch(dw, c0, kdw);
-    if (w) ld8ch(w, c0, ww);
-    if (bias) ld8ch(bias, c0, bb);
+    ld8ch(w ? w : smean, c0, ww);  // unconditional: see bn_norm_kernel
+    ld8ch(bias ? bias : smean, c0, bb);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {  // == dx_coef, from vector loads
       const float sc = (w ? ww[j] : 1.f) * iv[j];
@@ -501,30 +501,30 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_kernel(const T* __restrict
     for (int c = threadIdx.x; c < C; c += kThreads) ksm[c] = dx_coef(c, w, bias, smean, sinv, dw, db, inv_n);
     __syncthreads();
   }
+  // U vectors per lane per iteration, every load issued before any math
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
   int64_t v = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
-  for (; v + stride < nvec; v += 2 * stride) {
-    const int64_t v1 = v + stride;
-    float d0[8], x0[8], y0[8], d1[8], x1[8], y1[8];
-    ld8f(dy + v * 8, d0);
-    ld8f(x + v * 8, x0);
-    ld8f(dy + v1 * 8, d1);
-    ld8f(x + v1 * 8, x1);
-    if (RM == 1) {
-      ld8f(y + v * 8, y0);
-      ld8f(y + v1 * 8, y1);
+  for (; v + (U - 1) * stride < nvec; v += U * stride) {
+    float d[U][8], xv[U][8], yv[U][8];
+    unsigned mb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t vu = v + u * stride;
+      ld8f(dy + vu * 8, d[u]);
+      ld8f(x + vu * 8, xv[u]);
+      if (RM == 1) ld8f(y + vu * 8, yv[u]);
+      mb[u] = RM == 3 ? mask[vu] : 0u;
     }
-    const unsigned m0 = RM == 3 ? mask[v] : 0u, m1 = RM == 3 ? mask[v1] : 0u;
-    dx_vec<T, RM, DRES>(d0, x0, y0, m0, FIXED ? rk : ksm + (v * 8) % C);
-    dx_vec<T, RM, DRES>(d1, x1, y1, m1, FIXED ? rk : ksm + (v1 * 8) % C);
-    st8f(dx + v * 8, x0);
-    st8f(dx + v1 * 8, x1);
-    if (DRES) {
-      st8f(dres + v * 8, d0);
-      st8f(dres + v1 * 8, d1);
+    __builtin_amdgcn_sched_barrier(0);  // keep every load ahead of the first store
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t vu = v + u * stride;
+      dx_vec<T, RM, DRES>(d[u], xv[u], yv[u], mb[u], FIXED ? rk : ksm + (vu * 8) % C);
+      st8f(dx + vu * 8, xv[u]);
+      if (DRES) st8f(dres + vu * 8, d[u]);
     }
   }
-  if (v < nvec) {
+  for (; v < nvec; v += stride) {
     float d0[8], x0[8], y0[8];
     ld8f(dy + v * 8, d0);
     ld8f(x + v * 8, x0);
@@ -549,8 +549,8 @@ __device__ __forceinline__ void coef8(const float* __restrict__ w, const float* 
   float mu[8], iv[8], ww[8], bb[8];
   ld8ch(mean, c0, mu);
   ld8ch(inv, c0, iv);
-  if (w) ld8ch(w, c0, ww);
-  if (b) ld8ch(b, c0, bb);
+  ld8ch(w ? w : mean, c0, ww);  // unconditional: see bn_norm_kernel
+  ld8ch(b ? b : mean, c0, bb);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     sc[j] = (w ? ww[j] : 1.f) * iv[j];
@@ -675,7 +675,7 @@ __device__ __forceinline__ void dx_coef8(const float* __restrict__ w, const floa
   ld8ch(mean, c0, m);
   ld8ch(db, c0, kdb);
   ld8ch(dw, c0, kdw);
-  if (w) ld8ch(w, c0, ww);
+  ld8ch(w ? w : mean, c0, ww);  // unconditional: see bn_norm_kernel
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const float sc = (w ? ww[j] : 1.f) * iv[j];
@@ -736,6 +736,15 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_dual_kernel(
   }
 }
 
+// vectors per lane per iteration of the elementwise BN kernels (FLUXMPI_BN_UNROLL: 2 or 4)
+int bn_unroll() {
+  static const int u = [] {
+    const char* e = std::getenv("FLUXMPI_BN_UNROLL");
+    return (e != nullptr && std::atoi(e) == 4) ? 4 : 2;
+  }();
+  return u;
+}
+
 // one full round of resident workgroups (or fewer if the tensor is small)
 int elementwise_grid(const void* kernel, size_t smem, int64_t nvec) {
   // >= 4 vectors per lane: every workgroup pays its coefficient prologue once
@@ -781,7 +790,7 @@ void norm_t(const void* x, void* y, const void* res, const float* w, const float
 #define LAUNCH(RELU, RES, FX)                                                                                   \
   {                                                                                                            \
     const size_t sm = FX ? 0 : 2 * C * sizeof(float);                                                          \
-    auto k = bn_norm_kernel<T, RELU, RES, FX>;                                                                 \
+    auto k = bn_unroll() == 4 ? bn_norm_kernel<T, RELU, RES, FX, 4> : bn_norm_kernel<T, RELU, RES, FX, 2>;   \
     k<<<elementwise_grid(reinterpret_cast<const void*>(k), sm, nvec), kThreads, sm, s>>>(                      \
         xr, yr, rr, w, b, mean, stat2, (int)C, eps, train, nvec, mask);                                        \
   }
@@ -846,7 +855,7 @@ void bwd_t(const void* dy, const void* x, const void* y, const uint8_t* mask, co
 #define LAUNCH(RM, DRES, FX)                                                                                    \
   {                                                                                                            \
     const size_t lds = FX ? 0 : C * sizeof(DxCoef);                                                            \
-    auto k = bn_bwd_dx_kernel<T, RM, DRES, FX>;                                                                \
+    auto k = bn_unroll() == 4 ? bn_bwd_dx_kernel<T, RM, DRES, FX, 4> : bn_bwd_dx_kernel<T, RM, DRES, FX, 2>;   \
     k<<<elementwise_grid(reinterpret_cast<const void*>(k), lds, nvec), kThreads, lds, s>>>(                    \
         dyr, xr, yr, mask, w, b, sm, si, dw, db, dxr, drr, rows, (int)C, nvec);                                \
   }
