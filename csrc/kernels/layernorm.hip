@@ -27,31 +27,55 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
+// DPP row sums (quad_perm xor 1, xor 2, row_ror 4, 8: every lane of a 16-lane row holds the
+// row's sum), then the four row sums read as scalars: no LDS round trips (the ds_bpermute
+// butterfly was 6 dependent LDS ops per reduction, on every row's critical path).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
 }
+
+__device__ __forceinline__ float wave_sum(float v) {
+  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x124>(v);  // row_ror:4
+  v += dpp_f<0x128>(v);  // row_ror:8
+  const int b = __builtin_bit_cast(int, v);
+  return (__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 0)) +
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 16))) +
+         (__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 32)) +
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48)));
+}
+
+__device__ __forceinline__ void ld8w(const float* __restrict__ p, int c0, float (&v)[8]) {
+  const float4 a0 = *reinterpret_cast<const float4*>(p + c0);
+  const float4 a1 = *reinterpret_cast<const float4*>(p + c0 + 4);
+  v[0] = a0.x; v[1] = a0.y; v[2] = a0.z; v[3] = a0.w;
+  v[4] = a1.x; v[5] = a1.y; v[6] = a1.z; v[7] = a1.w;
+}
+
+// A lane's vectors i = lane + 64 * i of a row; lanes past the row (D/8 not a multiple of 64)
+// load vector 0 and are masked in the math: every load is unconditional (a load under
+// `if (v < nv)` is waited for at the branch join, one exposed latency per vector).
+template <int VPL>
+struct LnLanes {
+  int vc[VPL];
+  bool act[VPL];
+  __device__ __forceinline__ LnLanes(int lane, int nv) {
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int v = lane + i * 64;
+      act[i] = v < nv;
+      vc[i] = act[i] ? v : 0;
+    }
+  }
+};
 
 // Forward: a persistent grid (one full round of resident workgroups); each wave walks rows
 // row, row + step, ... with the NEXT row's x (and residual) loads issued before the current
 // row's reductions, and the affine w/b held in registers for the whole kernel (16-byte
-// loads, once). The one-row-per-wave version issued 16 scalar w/b loads per vector after
-// the reductions and had only one row's loads in flight: 141-155 us per ViT-B LayerNorm
-// (50432 x 768 bf16) on MI355X, ~2-3x its HBM time (s48 trace).
-template <typename T, int VPL, bool ADD>
-__device__ __forceinline__ void ln_fwd_load(const T* __restrict__ x, const T* __restrict__ r, int64_t row, int D,
-                                            int lane, int nv, T (&rx)[VPL][8], T (&rr)[VPL][8]) {
-#pragma unroll
-  for (int i = 0; i < VPL; ++i) {
-    const int v = lane + i * 64;
-    if (v < nv) {
-      load8(x + row * D + v * 8, rx[i]);
-      if (ADD) load8(r + row * D + v * 8, rr[i]);
-    }
-  }
-}
-
+// loads, once). (The one-row-per-wave version had only one row's loads in flight: 141-155 us
+// per ViT-B LayerNorm (50432 x 768 bf16) on MI355X, ~2-3x its HBM time, s48 trace.)
 template <typename T, bool ADD, int VPL>
 __global__ __launch_bounds__(kThreads) void ln_fwd_kernel(const T* __restrict__ x, const T* __restrict__ r,
                                                           T* __restrict__ h, T* __restrict__ y,
@@ -59,91 +83,100 @@ __global__ __launch_bounds__(kThreads) void ln_fwd_kernel(const T* __restrict__ 
                                                           float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                           int64_t rows, int D, float eps) {
   const int lane = threadIdx.x & 63;
-  const int nv = D / 8;
+  const LnLanes<VPL> L(lane, D / 8);
   const float inv_d = 1.f / static_cast<float>(D);
   float wv[VPL][8], bv[VPL][8];
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
-    const int v = lane + i * 64;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      wv[i][j] = 1.f;
-      bv[i][j] = 0.f;
-    }
-    if (v < nv) {
-      if (w) {
-        const float4 a0 = *reinterpret_cast<const float4*>(w + v * 8);
-        const float4 a1 = *reinterpret_cast<const float4*>(w + v * 8 + 4);
-        wv[i][0] = a0.x; wv[i][1] = a0.y; wv[i][2] = a0.z; wv[i][3] = a0.w;
-        wv[i][4] = a1.x; wv[i][5] = a1.y; wv[i][6] = a1.z; wv[i][7] = a1.w;
-      }
-      if (b) {
-        const float4 a0 = *reinterpret_cast<const float4*>(b + v * 8);
-        const float4 a1 = *reinterpret_cast<const float4*>(b + v * 8 + 4);
-        bv[i][0] = a0.x; bv[i][1] = a0.y; bv[i][2] = a0.z; bv[i][3] = a0.w;
-        bv[i][4] = a1.x; bv[i][5] = a1.y; bv[i][6] = a1.z; bv[i][7] = a1.w;
-      }
-    }
+    ld8w(w, L.vc[i] * 8, wv[i]);
+    ld8w(b, L.vc[i] * 8, bv[i]);
   }
   const int64_t step = static_cast<int64_t>(gridDim.x) * kWaves;
   int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6);
+  if (row >= rows) return;  // no block-level synchronisation below
   T rx[VPL][8], rr[VPL][8];
-  if (row < rows) ln_fwd_load<T, VPL, ADD>(x, r, row, D, lane, nv, rx, rr);
-  for (; row < rows; row += step) {
+  auto load = [&](int64_t rw, T (&ox)[VPL][8], T (&orr)[VPL][8]) {
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      load8(x + rw * D + L.vc[i] * 8, ox[i]);
+      if (ADD) load8(r + rw * D + L.vc[i] * 8, orr[i]);
+    }
+  };
+  // one row: (h,) the statistics, y
+  auto process = [&](int64_t rw, const T (&cx)[VPL][8], const T (&cr)[VPL][8]) {
     float f[VPL][8];
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
-      const int v = lane + i * 64;
-      if (v < nv) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[i][j] = static_cast<float>(rx[i][j]);
-        if (ADD) {
-          T o[8];
+      for (int j = 0; j < 8; ++j) f[i][j] = static_cast<float>(cx[i][j]);
+      if (ADD) {
+        T o[8];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            o[j] = static_cast<T>(f[i][j] + static_cast<float>(rr[i][j]));
-            f[i][j] = static_cast<float>(o[j]);  // normalise exactly the stored (rounded) h
-          }
-          store8(h + row * D + v * 8, o);
+        for (int j = 0; j < 8; ++j) {
+          o[j] = static_cast<T>(f[i][j] + static_cast<float>(cr[i][j]));
+          f[i][j] = static_cast<float>(o[j]);  // normalise exactly the stored (rounded) h
         }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) s += f[i][j];
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[i][j] = 0.f;
+        if (L.act[i]) store8(h + rw * D + L.vc[i] * 8, o);
       }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += L.act[i] ? f[i][j] : 0.f;
     }
-    // next row's loads in flight during this row's reductions and stores
-    if (row + step < rows) ln_fwd_load<T, VPL, ADD>(x, r, row + step, D, lane, nv, rx, rr);
     const float mean = wave_sum(s) * inv_d;
     float q = 0.f;
 #pragma unroll
     for (int i = 0; i < VPL; ++i)
-      if (lane + i * 64 < nv)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float d = f[i][j] - mean;
-          q = fmaf(d, d, q);
-        }
+      for (int j = 0; j < 8; ++j) {
+        const float d = f[i][j] - mean;
+        q = fmaf(L.act[i] ? d : 0.f, d, q);
+      }
     const float rstd = rsqrtf(wave_sum(q) * inv_d + eps);
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
-      const int v = lane + i * 64;
-      if (v < nv) {
-        T o[8];
+      T o[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = static_cast<T>(fmaf((f[i][j] - mean) * rstd, wv[i][j], bv[i][j]));
-        store8(y + row * D + v * 8, o);
-      }
+      for (int j = 0; j < 8; ++j) o[j] = static_cast<T>(fmaf((f[i][j] - mean) * rstd, wv[i][j], bv[i][j]));
+      if (L.act[i]) store8(y + rw * D + L.vc[i] * 8, o);
     }
     if (lane == 0) {
-      mean_out[row] = mean;
-      rstd_out[row] = rstd;
+      mean_out[rw] = mean;
+      rstd_out[rw] = rstd;
     }
+  };
+  // PF (up to 4 vectors per lane): the next row's loads in flight during this row's
+  // reductions and stores (unconditional: the last row re-reads itself); wider rows would
+  // spill the second buffer
+  constexpr bool PF = VPL <= 4;
+  load(row, rx, rr);
+  while (true) {
+    const int64_t nrow = row + step;
+    const bool more = nrow < rows;
+    if (PF) {
+      T nx[VPL][8], nr[VPL][8];
+      load(more ? nrow : row, nx, nr);
+      process(row, rx, rr);
+      if (!more) break;
+#pragma unroll
+      for (int i = 0; i < VPL; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          rx[i][j] = nx[i][j];
+          if (ADD) rr[i][j] = nr[i][j];
+        }
+    } else {
+      process(row, rx, rr);
+      if (!more) break;
+      load(nrow, rx, rr);
+    }
+    row = nrow;
   }
 }
 
+// Backward: same persistent walk, the next row's (dy, x[, dh_ext], mean, rstd) in flight
+// during the current row's two reductions and its dx stores (PF: up to 4 vectors per lane;
+// wider rows would spill the second buffer). dy and xhat are recomputed from the raw row in
+// the second pass rather than kept as fp32 arrays.
 template <typename T, bool DH, int VPL>
 __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                           const T* __restrict__ dh_ext,
@@ -151,63 +184,81 @@ __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(const T* __restrict__ 
                                                           const float* __restrict__ rstd_in,
                                                           const float* __restrict__ w, T* __restrict__ dx,
                                                           float* __restrict__ part, int64_t rows, int D) {
+  constexpr bool PF = VPL <= 4;
   extern __shared__ __attribute__((aligned(16))) float red[];  // [2][D]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nv = D / 8;
+  const LnLanes<VPL> L(lane, nv);
   const float inv_d = 1.f / static_cast<float>(D);
   float wv[VPL][8], dwp[VPL][8], dbp[VPL][8];
 #pragma unroll
-  for (int i = 0; i < VPL; ++i)
+  for (int i = 0; i < VPL; ++i) {
+    ld8w(w, L.vc[i] * 8, wv[i]);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = (lane + i * 64) * 8 + j;
-      wv[i][j] = (lane + i * 64 < nv && w) ? w[c] : 1.f;
-      dwp[i][j] = dbp[i][j] = 0.f;
-    }
-  const int64_t step = static_cast<int64_t>(gridDim.x) * kWaves;
-  for (int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + wave; row < rows; row += step) {
-    const float mean = mean_in[row], rstd = rstd_in[row];
-    float d[VPL][8], xh[VPL][8], e[VPL][8];
-    float s1 = 0.f, s2 = 0.f;
+    for (int j = 0; j < 8; ++j) dwp[i][j] = dbp[i][j] = 0.f;
+  }
+  struct Buf {
+    T d[VPL][8], x[VPL][8], e[DH ? VPL : 1][8];
+    float mean, rstd;
+  };
+  auto load = [&](int64_t rw, Buf& o) {
+    o.mean = mean_in[rw];
+    o.rstd = rstd_in[rw];
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
-      const int v = lane + i * 64;
-      if (v < nv) {
-        T td[8], tx[8];
-        load8(dy + row * D + v * 8, td);
-        load8(x + row * D + v * 8, tx);
-        if (DH) {
-          T te[8];
-          load8(dh_ext + row * D + v * 8, te);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) e[i][j] = static_cast<float>(te[j]);
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          d[i][j] = static_cast<float>(td[j]);
-          xh[i][j] = (static_cast<float>(tx[j]) - mean) * rstd;
-          const float g = d[i][j] * wv[i][j];
-          s1 += g;
-          s2 = fmaf(g, xh[i][j], s2);
-          dwp[i][j] = fmaf(d[i][j], xh[i][j], dwp[i][j]);
-          dbp[i][j] += d[i][j];
-        }
-      }
+      load8(dy + rw * D + L.vc[i] * 8, o.d[i]);
+      load8(x + rw * D + L.vc[i] * 8, o.x[i]);
+      if (DH) load8(dh_ext + rw * D + L.vc[i] * 8, o.e[i]);
     }
+  };
+  auto process = [&](int64_t rw, const Buf& c) {
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = L.act[i] ? static_cast<float>(c.d[i][j]) : 0.f;
+        const float xh = (static_cast<float>(c.x[i][j]) - c.mean) * c.rstd;
+        const float g = d * wv[i][j];
+        s1 += g;
+        s2 = fmaf(g, xh, s2);
+        dwp[i][j] = fmaf(d, xh, dwp[i][j]);
+        dbp[i][j] += d;
+      }
     const float m1 = wave_sum(s1) * inv_d, m2 = wave_sum(s2) * inv_d;
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
-      const int v = lane + i * 64;
-      if (v < nv) {
-        T o[8];
+      T o[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          float g = rstd * (d[i][j] * wv[i][j] - m1 - xh[i][j] * m2);
-          if (DH) g += e[i][j];
-          o[j] = static_cast<T>(g);
-        }
-        store8(dx + row * D + v * 8, o);
+      for (int j = 0; j < 8; ++j) {
+        const float xh = (static_cast<float>(c.x[i][j]) - c.mean) * c.rstd;
+        float g = c.rstd * (static_cast<float>(c.d[i][j]) * wv[i][j] - m1 - xh * m2);
+        if (DH) g += static_cast<float>(c.e[i][j]);
+        o[j] = static_cast<T>(g);
       }
+      if (L.act[i]) store8(dx + rw * D + L.vc[i] * 8, o);
+    }
+  };
+  const int64_t step = static_cast<int64_t>(gridDim.x) * kWaves;
+  int64_t row = static_cast<int64_t>(blockIdx.x) * kWaves + wave;
+  if (row < rows) {  // (every wave reaches the block reduction below)
+    Buf cur;
+    load(row, cur);
+    while (true) {
+      const int64_t nrow = row + step;
+      const bool more = nrow < rows;
+      if (PF) {
+        Buf nxt;
+        load(more ? nrow : row, nxt);  // unconditional: the last row re-reads itself
+        process(row, cur);
+        if (!more) break;
+        cur = nxt;
+      } else {
+        process(row, cur);
+        if (!more) break;
+        load(nrow, cur);
+      }
+      row = nrow;
     }
   }
   // block partial of dw / db: the waves add their register partials into one [2][D] LDS
@@ -216,11 +267,10 @@ __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(const T* __restrict__ 
     if (wave == k) {
 #pragma unroll
       for (int i = 0; i < VPL; ++i) {
-        const int v = lane + i * 64;
-        if (v < nv)
+        if (L.act[i])
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const int c = v * 8 + j;
+            const int c = L.vc[i] * 8 + j;
             red[c] = k == 0 ? dwp[i][j] : red[c] + dwp[i][j];
             red[D + c] = k == 0 ? dbp[i][j] : red[D + c] + dbp[i][j];
           }
@@ -289,8 +339,8 @@ void layernorm_fwd(const void* x, const void* residual, void* h, void* y, const 
                    float* rstd, int64_t rows, int64_t D, float eps, int dtype, hipStream_t stream) {
   const int vpl = vpl_for(D);
   const bool add = residual != nullptr;
-  if ((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(b)) % 16 != 0)
-    throw std::runtime_error("fused layernorm: w and b must be 16-byte aligned fp32");
+  if (w == nullptr || b == nullptr || (reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(b)) % 16 != 0)
+    throw std::runtime_error("fused layernorm: w and b must be 16-byte aligned fp32 (ones / zeros when absent)");
 #define CALL_ADD(V) fwd_launch<TT, true, V>(x, residual, h, y, w, b, mean, rstd, rows, D, eps, stream)
 #define CALL_NOADD(V) fwd_launch<TT, false, V>(x, residual, h, y, w, b, mean, rstd, rows, D, eps, stream)
   switch (dtype) {
@@ -322,6 +372,8 @@ int layernorm_bwd(const void* dy, const void* x, const void* dh_ext, const float
                   hipStream_t stream) {
   const int vpl = vpl_for(D);
   const bool dh = dh_ext != nullptr;
+  if (w == nullptr || reinterpret_cast<uintptr_t>(w) % 16 != 0)
+    throw std::runtime_error("fused layernorm backward: w must be 16-byte aligned fp32 (ones when absent)");
   int blocks = 0;
 #define CALL_DH(V) blocks = bwd_launch<TT, true, V>(dy, x, dh_ext, mean, rstd, w, dx, partials, max_blocks, rows, D, stream)
 #define CALL_NODH(V) blocks = bwd_launch<TT, false, V>(dy, x, dh_ext, mean, rstd, w, dx, partials, max_blocks, rows, D, stream)

@@ -34,9 +34,25 @@ def supported(x: torch.Tensor) -> bool:
             and 8 <= d <= 8192 and x.numel() > 0)
 
 
+_AFFINE: dict = {}
+
+
+def _const(d: int, device, value: float) -> torch.Tensor:
+    """Cached fp32 ones / zeros standing in for an absent LayerNorm weight / bias (the kernels
+    load the affine unconditionally)."""
+    key = (d, str(device), value)
+    t = _AFFINE.get(key)
+    if t is None:
+        t = torch.full((d,), value, device=device, dtype=torch.float32)
+        _AFFINE[key] = t
+    return t
+
+
 def _fwd(x, r, w32, b32, eps):
     C = _ext.get(required=True)
     d = x.shape[-1]
+    w32 = w32 if w32 is not None else _const(d, x.device, 1.0)
+    b32 = b32 if b32 is not None else _const(d, x.device, 0.0)
     rows = x.numel() // d
     y = torch.empty_like(x)
     h = torch.empty_like(x) if r is not None else None
@@ -50,6 +66,7 @@ def _fwd(x, r, w32, b32, eps):
 def _bwd(dy, x, dh_ext, mean, rstd, w32, need_wb):
     C = _ext.get(required=True)
     d = x.shape[-1]
+    w32 = w32 if w32 is not None else _const(d, x.device, 1.0)
     rows = x.numel() // d
     dx = torch.empty_like(x)
     part = torch.empty(_MAX_BLOCKS, 2 * d, device=x.device, dtype=torch.float32)
