@@ -29,11 +29,7 @@ constexpr int kMaxRows = 8;
 constexpr int kPairs = kMaxRows * (kMaxRows + 1) / 2;  // 36 upper-triangle pairs
 constexpr int kOut = kPairs + 1;                        // + |F[last]|^2
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
+__device__ __forceinline__ float wave_sum(float v) { return wave_sum_dpp(v); }  // common.h
 
 __device__ __forceinline__ float dot4(const float4& a, const float4& b) {
   return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
@@ -61,22 +57,33 @@ __global__ __launch_bounds__(kThreads) void gram_kernel(const float* __restrict_
   const int64_t v0 = static_cast<int64_t>(c) * chunk4;
   int64_t v1 = v0 + chunk4;
   if (v1 > d4) v1 = d4;
+  // Per row, two UNCONDITIONAL loads from wave-uniformly chosen sources (a load under a
+  // branch is waited for at the join: N serial memory latencies per iteration otherwise):
+  //   fresh row (g = f - x):     A = f, B = x
+  //   stored row, the last one:  A = g, B = f   (|f_last|^2)
+  //   stored row:                A = g, B = g   (a cache hit)
+  const float4* gsrc = gb != nullptr ? gb : fb;
   for (int64_t v = v0 + threadIdx.x; v < v1; v += kThreads) {
+    float4 av[N], bv[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const bool fr = gb == nullptr || ((fresh >> i) & 1u);
+      av[i] = (fr ? fb : gsrc)[i * rs4 + v];
+      bv[i] = (fr ? xb : (i == last ? fb : gsrc))[i * rs4 + v];
+    }
     float4 g[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      if (gb == nullptr || ((fresh >> i) & 1u) || i == last) {
-        const float4 f = fb[i * rs4 + v];
-        if (gb == nullptr || ((fresh >> i) & 1u)) {
-          const float4 x = xb[i * rs4 + v];
-          g[i] = make_float4(f.x - x.x, f.y - x.y, f.z - x.z, f.w - x.w);
-          if (gb != nullptr) gb[i * rs4 + v] = g[i];
-        } else {
-          g[i] = gb[i * rs4 + v];
-        }
-        if (i == last) fn += dot4(f, f);
+      const bool fr = gb == nullptr || ((fresh >> i) & 1u);
+      if (fr) {
+        g[i] = make_float4(av[i].x - bv[i].x, av[i].y - bv[i].y, av[i].z - bv[i].z, av[i].w - bv[i].w);
+        if (gb != nullptr) gb[i * rs4 + v] = g[i];
       } else {
-        g[i] = gb[i * rs4 + v];
+        g[i] = av[i];
+      }
+      if (i == last) {
+        const float4 f = fr ? av[i] : bv[i];
+        fn += dot4(f, f);
       }
     }
     int p = 0;

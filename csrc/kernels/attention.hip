@@ -177,8 +177,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnBwdArgs a) {
     }
     float mx = fmaxf(fmaxf(fmaxf(x[0][0], x[0][1]), fmaxf(x[0][2], x[0][3])),
                      fmaxf(fmaxf(x[1][0], x[1][1]), fmaxf(x[1][2], x[1][3])));
-    mx = fmaxf(mx, __shfl_xor(mx, 16));
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    mx = xor_max<32>(xor_max<16>(mx));  // permlane swaps (common.h)
     const float mn = fmaxf(m, mx);  // finite from the first chunk on (key 0 is real)
     const float f = fast_exp2(m - mn);
     m = mn;
@@ -197,8 +196,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnBwdArgs a) {
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma(ld_tr(sVt, dt * 16 + col, g), bop, acc[dt]);
   }
-  l += __shfl_xor(l, 16);
-  l += __shfl_xor(l, 32);
+  l = butterfly_from<16>(l);  // permlane swaps (common.h)
   if (qok) {
     const float inv = 1.f / l;
     bf16* op = a.o_out + b * a.so_b + static_cast<int64_t>(qi) * a.so_t + h * a.so_h;
@@ -237,8 +235,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnBwdArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) dsum += (float)gf[0][j] * (float)o0[j] + (float)gf[1][j] * (float)o1[j];
   }
-  dsum += __shfl_xor(dsum, 16);
-  dsum += __shfl_xor(dsum, 32);
+  dsum = butterfly_from<16>(dsum);  // permlane swaps (common.h)
 
   const int nch = (a.T + CH - 1) / CH;
   const float c2 = a.scale * kLog2e;
@@ -497,8 +494,7 @@ __global__ __launch_bounds__(1024) void attn_fwd_res_kernel(AttnBwdArgs a) {
       }
     }
   }
-  m = fmaxf(m, __shfl_xor(m, 16));
-  m = fmaxf(m, __shfl_xor(m, 32));
+  m = xor_max<32>(xor_max<16>(m));  // permlane swaps (common.h)
   float l = 0.f;
 #pragma unroll
   for (int kt = 0; kt < kResMaxT / 16; ++kt) {
@@ -513,8 +509,7 @@ __global__ __launch_bounds__(1024) void attn_fwd_res_kernel(AttnBwdArgs a) {
       x[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
-  l += __shfl_xor(l, 16);
-  l += __shfl_xor(l, 32);
+  l = butterfly_from<16>(l);  // permlane swaps (common.h)
   // O^T[d][q] = sum over keys of V^T[d][key] P^T[key][q]; k-step ks covers keys 32ks .. +31 in
   // the accumulator-pair order (j < 4: 32ks + 4g + j, j >= 4: 32ks + 16 + 4g + j - 4)
   f32x4 acc[4] = {};
@@ -581,8 +576,7 @@ __global__ __launch_bounds__(1024) void attn_bwd_dq_res_kernel(AttnBwdArgs a) {
   float dsum = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) dsum += (float)gf[0][j] * (float)o0[j] + (float)gf[1][j] * (float)o1[j];
-  dsum += __shfl_xor(dsum, 16);
-  dsum += __shfl_xor(dsum, 32);
+  dsum = butterfly_from<16>(dsum);  // permlane swaps (common.h)
   if (qok && g == 0) st[1] = dsum;
   const int nt = TP / 16;
   const float c2 = a.scale * kLog2e;

@@ -33,6 +33,96 @@ template <> struct Acc<double> { using type = double; };
 template <typename T> __device__ __forceinline__ float to_f(T x) { return static_cast<float>(x); }
 template <typename T> __device__ __forceinline__ T from_f(float x) { return static_cast<T>(x); }
 
+// ---- cross-lane reductions without LDS -------------------------------------------------------
+// __shfl_xor compiles to ds_bpermute_b32: an LDS-crossbar round trip per step, on the critical
+// path of every reduction. gfx950 has VALU cross-lane moves instead: DPP within 16-lane rows
+// (fused into the add as v_add_f32_dpp), v_permlane16_swap / v_permlane32_swap across rows and
+// halves, v_readlane to scalars.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+
+// v[lane ^ 32] and v[lane ^ 16] as the two halves of a permlane swap of v with itself:
+// {r0, r1} hold {v, partner} in some order on every lane (measured on MI355X:
+// scripts/probe_lanes.hip). The elements are copied out before the bit cast:
+// __builtin_bit_cast(float, r[1]) on the returned ext-vector reads element 0 (clang codegen).
+__device__ __forceinline__ void swap_halves(unsigned r0, unsigned r1, float& a, float& b) {
+  a = __builtin_bit_cast(float, r0);
+  b = __builtin_bit_cast(float, r1);
+}
+__device__ __forceinline__ void xor32_pair(float v, float& a, float& b) {
+  const unsigned u = __builtin_bit_cast(unsigned, v);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  const unsigned r0 = r[0], r1 = r[1];
+  swap_halves(r0, r1, a, b);
+}
+__device__ __forceinline__ void xor16_pair(float v, float& a, float& b) {
+  const unsigned u = __builtin_bit_cast(unsigned, v);
+  const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  const unsigned r0 = r[0], r1 = r[1];
+  swap_halves(r0, r1, a, b);
+}
+
+// v + v[lane ^ OFF] (OFF a power of two < 64); EXEC must be full
+template <int OFF>
+__device__ __forceinline__ float xor_sum(float v) {
+  static_assert(OFF > 0 && OFF < 64 && (OFF & (OFF - 1)) == 0, "butterfly offset");
+  if constexpr (OFF == 32) {
+    float a, b;
+    xor32_pair(v, a, b);
+    return a + b;
+  } else if constexpr (OFF == 16) {
+    float a, b;
+    xor16_pair(v, a, b);
+    return a + b;
+  } else if constexpr (OFF == 8) {
+    return v + dpp_f<0x128>(v);  // row_ror:8 == lane ^ 8 within a 16-lane row
+  } else if constexpr (OFF == 2) {
+    return v + dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+  } else if constexpr (OFF == 1) {
+    return v + dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+  } else {
+    return v + __shfl_xor(v, OFF, 64);
+  }
+}
+
+// butterfly over lane offsets OFF, 2*OFF, ..., 32: the sum over the lanes that agree with this
+// one in the lane-index bits below log2(OFF)
+template <int OFF>
+__device__ __forceinline__ float butterfly_from(float v) {
+  if constexpr (OFF >= 64) return v;
+  else return butterfly_from<OFF * 2>(xor_sum<OFF>(v));
+}
+
+template <int OFF>
+__device__ __forceinline__ float xor_max(float v) {
+  static_assert(OFF == 16 || OFF == 32, "butterfly offset");
+  float a, b;
+  if constexpr (OFF == 32) xor32_pair(v, a, b);
+  else xor16_pair(v, a, b);
+  return fmaxf(a, b);
+}
+
+// sum over each 16-lane row, in every lane of the row (DPP only)
+__device__ __forceinline__ float row_sum16(float v) {
+  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x124>(v);  // row_ror:4
+  return v + dpp_f<0x128>(v);  // row_ror:8
+}
+
+// sum over all 64 lanes, wave-uniform result: DPP row sums (every lane of a row holds its
+// row's total), then the four row totals read as scalars
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v = row_sum16(v);
+  const int b = __builtin_bit_cast(int, v);
+  return (__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 0)) +
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 16))) +
+         (__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 32)) +
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48)));
+}
+
 // 8 elements per lane: 16 B for 2-byte types, 2 x 16 B for fp32, 4 x 16 B for fp64.
 template <typename T> struct Vec8 {
   T v[8];

@@ -461,12 +461,10 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs p) {
     // lanes of a wave with equal cc differ in the bits above log2(CPR): butterfly them,
     // then combine the 4 waves through LDS and add one atomic per column per block.
 #pragma unroll
-    for (int off = CPR; off < 64; off <<= 1)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        cs[e] += __shfl_xor(cs[e], off, 64);
-        cq[e] += __shfl_xor(cq[e], off, 64);
-      }
+    for (int e = 0; e < 8; ++e) {  // LDS-free cross-lane butterflies (common.h)
+      cs[e] = butterfly_from<CPR>(cs[e]);
+      cq[e] = butterfly_from<CPR>(cq[e]);
+    }
     __syncthreads();
     float* red = reinterpret_cast<float*>(smem);  // [4 waves][2][BN]
     static_assert(4 * 2 * BN * 4 <= kSmem * 2, "stats scratch");

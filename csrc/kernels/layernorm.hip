@@ -27,25 +27,9 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 
-// DPP row sums (quad_perm xor 1, xor 2, row_ror 4, 8: every lane of a 16-lane row holds the
-// row's sum), then the four row sums read as scalars: no LDS round trips (the ds_bpermute
-// butterfly was 6 dependent LDS ops per reduction, on every row's critical path).
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
-}
-
-__device__ __forceinline__ float wave_sum(float v) {
-  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
-  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
-  v += dpp_f<0x124>(v);  // row_ror:4
-  v += dpp_f<0x128>(v);  // row_ror:8
-  const int b = __builtin_bit_cast(int, v);
-  return (__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 0)) +
-          __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 16))) +
-         (__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 32)) +
-          __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48)));
-}
+// wave sums by DPP + readlane (common.h): no LDS round trips (the ds_bpermute butterfly was 6
+// dependent LDS ops per reduction, on every row's critical path)
+__device__ __forceinline__ float wave_sum(float v) { return wave_sum_dpp(v); }
 
 __device__ __forceinline__ void ld8w(const float* __restrict__ p, int c0, float (&v)[8]) {
   const float4 a0 = *reinterpret_cast<const float4*>(p + c0);

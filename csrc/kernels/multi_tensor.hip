@@ -110,11 +110,7 @@ __global__ __launch_bounds__(kThreads) void mt_fill_kernel(CopyArgs a, float val
   }
 }
 
-__device__ __forceinline__ float wave_sum(float x) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
-  return x;
-}
+__device__ __forceinline__ float wave_sum(float x) { return wave_sum_dpp(x); }  // common.h
 
 template <typename T>
 __global__ __launch_bounds__(kThreads) void mt_sumsq_kernel(CopyArgs a, float* out) {

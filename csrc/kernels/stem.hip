@@ -190,12 +190,10 @@ __global__ __launch_bounds__(kFT, 2) void stem_fwd_kernel(StemFwdArgs p) {
     __builtin_amdgcn_s_barrier();  // this buffer is refilled two groups on
   }
 #pragma unroll
-  for (int off = 1; off < 16; off <<= 1)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      cs[e] += __shfl_xor(cs[e], off, 64);
-      cq[e] += __shfl_xor(cq[e], off, 64);
-    }
+  for (int e = 0; e < 16; ++e) {  // 16-lane row sums by DPP (common.h)
+    cs[e] = row_sum16(cs[e]);
+    cq[e] = row_sum16(cq[e]);
+  }
   wait_vm0();
   __syncthreads();  // every wave is done with the filter / halo: reuse the LDS
   float* red = reinterpret_cast<float*>(smem);  // [8 waves][2][64]
@@ -526,10 +524,7 @@ __global__ __launch_bounds__(kBT, 2) void stem_bwd_kernel(StemBwdArgs p) {
     }
   // G3: both wave groups hold partial column sums of their 4 n tiles (the other half of the k-steps)
 #pragma unroll
-  for (int n = 0; n < 4; ++n) {
-    g3[n] += __shfl_xor(g3[n], 16, 64);
-    g3[n] += __shfl_xor(g3[n], 32, 64);
-  }
+  for (int n = 0; n < 4; ++n) g3[n] = butterfly_from<16>(g3[n]);
   float* red3 = reinterpret_cast<float*>(smem) + 2 * (kBT / 64) * kCo;  // [256]
   if (gx && g == 0) {
 #pragma unroll
@@ -537,12 +532,10 @@ __global__ __launch_bounds__(kBT, 2) void stem_bwd_kernel(StemBwdArgs p) {
   }
   // ---- BatchNorm backward sums: lanes with equal lane & 7 share channels
 #pragma unroll
-  for (int off = 8; off < 64; off <<= 1)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      s1[e] += __shfl_xor(s1[e], off, 64);
-      s2[e] += __shfl_xor(s2[e], off, 64);
-    }
+  for (int e = 0; e < 8; ++e) {  // LDS-free cross-lane butterflies (common.h)
+    s1[e] = butterfly_from<8>(s1[e]);
+    s2[e] = butterfly_from<8>(s2[e]);
+  }
   float* red = reinterpret_cast<float*>(smem);  // [8 waves][2][64]
   if (lane < 8) {
 #pragma unroll
