@@ -200,9 +200,11 @@ bool gemm_glds_supported(const GemmProblem& g);
 void gemm_glds(const GemmProblem& g, hipStream_t stream);
 // weight gradient, fp32 split-K partials ws[s][M][N] = sum over split s of A[k][m] * B[k][n]
 // (A: [K][lda], B: [K][ldb] or, conv_h > 0, the implicit 3x3/s1/p1 im2col of an NHWC image
-// [K/(H*W)][H][W][conv_c] with N = 9*conv_c); returns nothing, reduce with gemm_splitk_reduce
+// [K/(H*W)][H][W][conv_c] with N = 9*conv_c; b_sub: row k of B = pixel (n, 2ho, 2wo) of the NHWC image
+// [.][conv_h][conv_w][ldb] for output pixel k = (n, ho, wo) of a stride-2 1x1 convolution);
+// returns nothing, reduce with gemm_splitk_reduce
 void gemm_wgrad(const void* a, const void* b, float* ws, int64_t lda, int64_t ldb, int64_t M, int64_t N, int64_t K,
-                int splits, int conv_h, int conv_w, int conv_c, hipStream_t stream, int variant = 0);
+                int splits, int conv_h, int conv_w, int conv_c, hipStream_t stream, int variant = 0, int b_sub = 0);
 // out_i[ci][t][co] = in_i[co][taps-1-t][ci] (bf16) for every filter i, one launch per 40 filters:
 // the K-major B operand of the input-gradient GEMMs (1x1: W^T; 3x3: transposed + flipped)
 void transpose_filters(const std::vector<uintptr_t>& src, const std::vector<uintptr_t>& dst,

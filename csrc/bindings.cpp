@@ -294,13 +294,13 @@ PYBIND11_MODULE(_C, m) {
 
   m.def("gemm_wgrad",
         [](uintptr_t a, uintptr_t b, uintptr_t ws, int64_t lda, int64_t ldb, int64_t M, int64_t N, int64_t K,
-           int splits, int conv_h, int conv_w, int conv_c, uintptr_t stream, int variant) {
+           int splits, int conv_h, int conv_w, int conv_c, uintptr_t stream, int variant, int b_sub) {
           gemm_wgrad(reinterpret_cast<const void*>(a), reinterpret_cast<const void*>(b), reinterpret_cast<float*>(ws),
-                     lda, ldb, M, N, K, splits, conv_h, conv_w, conv_c, S(stream), variant);
+                     lda, ldb, M, N, K, splits, conv_h, conv_w, conv_c, S(stream), variant, b_sub);
         },
         py::arg("a"), py::arg("b"), py::arg("ws"), py::arg("lda"), py::arg("ldb"), py::arg("M"), py::arg("N"),
         py::arg("K"), py::arg("splits"), py::arg("conv_h") = 0, py::arg("conv_w") = 0, py::arg("conv_c") = 0,
-        py::arg("stream") = 0, py::arg("variant") = 0);
+        py::arg("stream") = 0, py::arg("variant") = 0, py::arg("b_sub") = 0);
 
   m.def("transpose_filters",
         [](const std::vector<uintptr_t>& src, const std::vector<uintptr_t>& dst, const std::vector<int>& co,

@@ -501,14 +501,19 @@ struct WgradArgs {
 // A lane's tile row and column (hence its swizzled chunk) never change, so every division is
 // done once: the loop only bumps a pointer (plain operand) or a pixel index with its image
 // position (CONVB, where the tap shift and channel of the lane's column are fixed too).
-template <int ROWS, int BK, bool CONVB>
+// MODE 0: plain [K][ld] rows; 1 (CONVB): the implicit 3x3 im2col; 2 (SUB): row k = pixel
+// (img, ho, wo) of the [.][Ho][Wo] grid of a stride-2 1x1 convolution's output reads image row
+// (img, 2ho, 2wo) of the NHWC input [.][H][W][ld] (H, W as the conv_h / conv_w arguments).
+template <int ROWS, int BK, int MODE>
 struct TrLoader {
+  static constexpr bool CONVB = MODE == 1, SUB = MODE == 2;
   static constexpr int SPR = ROWS / 8;      // 16-B slots per k-row
   static constexpr int RPP = 64 / SPR;      // k-rows per 1 KiB piece
   static constexpr int PPW = BK / RPP / 4;  // pieces per wave (BK k-rows, 4 waves)
-  const bf16* ptr[PPW];  // plain: address of (k, col); CONVB: image + ci
+  const bf16* ptr[PPW];  // plain: address of (k, col); CONVB: image + ci; SUB: image + col
   int k[PPW];            // pixel / row index of the current step
-  int h[PPW], w[PPW];    // CONVB: image position of pixel k
+  int h[PPW], w[PPW];    // CONVB: image position of pixel k; SUB: (ho, wo) of output pixel k
+  int img[PPW];          // SUB: image of output pixel k
   int off[PPW];          // CONVB: tap shift in pixels, dr * W + ds
   int dr[PPW], ds[PPW];
   bool colok[PPW];
@@ -533,6 +538,13 @@ struct TrLoader {
         const int hw = k[j] % (H * W);
         h[j] = hw / W;
         w[j] = hw - h[j] * W;
+      } else if (SUB) {
+        const int ho = (H + 1) >> 1, wo = (W + 1) >> 1;
+        ptr[j] = g + col;
+        img[j] = k[j] / (ho * wo);
+        const int r = k[j] - img[j] * (ho * wo);
+        h[j] = r / wo;
+        w[j] = r - h[j] * wo;
       } else {
         ptr[j] = g + static_cast<int64_t>(k[j]) * ld + col;
       }
@@ -541,7 +553,7 @@ struct TrLoader {
 
   // issue this wave's pieces of the current step into lds_tile, then advance one step
   __device__ __forceinline__ void issue_next(bf16* lds_tile, int kend, int64_t ld, int H, int W, int C, int dh_step,
-                                             int dw_step) {
+                                             int dw_step, int dimg_step = 0) {
     const int wave = threadIdx.x >> 6;
 #pragma unroll
     for (int j = 0; j < PPW; ++j) {
@@ -551,6 +563,8 @@ struct TrLoader {
           if (static_cast<unsigned>(h[j] + dr[j]) < static_cast<unsigned>(H) &&
               static_cast<unsigned>(w[j] + ds[j]) < static_cast<unsigned>(W))
             src = ptr[j] + static_cast<int64_t>(k[j] + off[j]) * C;
+        } else if (SUB) {
+          src = ptr[j] + ((static_cast<int64_t>(img[j]) * H + 2 * h[j]) * W + 2 * w[j]) * ld;
         } else {
           src = ptr[j];
         }
@@ -568,6 +582,19 @@ struct TrLoader {
           ++h[j];
         }
         if (h[j] >= H) h[j] -= H;
+      } else if (SUB) {  // output pixel k -> k + BK over the (Ho, Wo) grid, carries into img
+        const int ho = (H + 1) >> 1, wo = (W + 1) >> 1;
+        img[j] += dimg_step;
+        w[j] += dw_step;
+        h[j] += dh_step;
+        if (w[j] >= wo) {
+          w[j] -= wo;
+          ++h[j];
+        }
+        if (h[j] >= ho) {
+          h[j] -= ho;
+          ++img[j];
+        }
       } else {
         ptr[j] += BK * ld;
       }
@@ -595,8 +622,9 @@ __device__ __forceinline__ bf16x8 read_frag_tr(const bf16* __restrict__ tile, in
   return out;
 }
 
-template <int BM, int BN, int kBK, int kStages, bool CONVB>
+template <int BM, int BN, int kBK, int kStages, int BMODE>
 __global__ __launch_bounds__(kThreads, 2) void gemm_wgrad_kernel(WgradArgs p) {
+  constexpr bool CONVB = BMODE == 1;
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
   constexpr int A_ELEMS = BM * kBK, B_ELEMS = BN * kBK;
   constexpr int LPT = (BM + BN) * kBK / 2048;
@@ -620,16 +648,20 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_wgrad_kernel(WgradArgs p) {
   const int64_t kend = kbeg + p.k_per_split < p.K ? kbeg + p.k_per_split : p.K;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wm = wave >> 1, wn = wave & 1;
-  TrLoader<BM, kBK, false> la;
-  TrLoader<BN, kBK, CONVB> lb;
+  TrLoader<BM, kBK, 0> la;
+  TrLoader<BN, kBK, BMODE> lb;
   const int H = p.conv_h, W = p.conv_w, C = p.conv_c;
-  const int dw_step = CONVB ? kBK % W : 0, dh_step = CONVB ? (kBK / W) % H : 0;
+  // per-step advance of a lane's pixel: CONVB over (H, W); SUB over the (Ho, Wo) output grid
+  const int sho = (H + 1) >> 1, swo = (W + 1) >> 1;
+  const int dw_step = CONVB ? kBK % W : (BMODE == 2 ? (kBK % (sho * swo)) % swo : 0);
+  const int dh_step = CONVB ? (kBK / W) % H : (BMODE == 2 ? (kBK % (sho * swo)) / swo : 0);
+  const int dimg_step = BMODE == 2 ? kBK / (sho * swo) : 0;
   la.init(p.a, p.lda, p.M, m0, kbeg, 0, 1, 1);
   lb.init(p.b, p.ldb, p.N, n0, kbeg, H, W, C);
   const int kend32 = static_cast<int>(kend);
   auto issue = [&](int s) {
     la.issue_next(sa(s), kend32, p.lda, 0, 1, 1, 0, 0);
-    lb.issue_next(sb(s), kend32, p.ldb, H, W, C, dh_step, dw_step);
+    lb.issue_next(sb(s), kend32, p.ldb, H, W, C, dh_step, dw_step, dimg_step);
   };
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -823,12 +855,16 @@ void gemm_glds(const GemmProblem& g, hipStream_t stream) {
 }
 
 void gemm_wgrad(const void* a, const void* b, float* ws, int64_t lda, int64_t ldb, int64_t M, int64_t N, int64_t K,
-                int splits, int conv_h, int conv_w, int conv_c, hipStream_t stream, int variant) {
+                int splits, int conv_h, int conv_w, int conv_c, hipStream_t stream, int variant, int b_sub) {
   if (lda % 8 != 0 || ldb % 8 != 0 || M % 8 != 0 || N % 8 != 0 || splits < 1)
     throw std::runtime_error("gemm_wgrad: M, N, lda, ldb must be multiples of 8");
-  if (conv_h > 0 && (conv_c % 8 != 0 || N != 9LL * conv_c))
+  if (!b_sub && conv_h > 0 && (conv_c % 8 != 0 || N != 9LL * conv_c))
     throw std::runtime_error("gemm_wgrad: implicit 3x3 B needs C % 8 == 0 and N == 9*C");
-  if (K >= (1LL << 31) || (conv_h > 0 && K % (static_cast<int64_t>(conv_h) * conv_w) != 0))
+  const int64_t grid_px = b_sub ? static_cast<int64_t>((conv_h + 1) / 2) * ((conv_w + 1) / 2)
+                                : static_cast<int64_t>(conv_h) * conv_w;
+  if (b_sub && (conv_h <= 0 || conv_w <= 0 || N > ldb))
+    throw std::runtime_error("gemm_wgrad: the stride-2 B gather needs the input H, W and N <= ldb");
+  if (K >= (1LL << 31) || (conv_h > 0 && K % grid_px != 0))
     throw std::runtime_error("gemm_wgrad: K must fit 31 bits (and be whole images for the implicit conv)");
   WgradArgs w{};
   w.a = static_cast<const bf16*>(a);
@@ -850,11 +886,13 @@ void gemm_wgrad(const void* a, const void* b, float* ws, int64_t lda, int64_t ld
     w.tiles_n = static_cast<int>((N + BN - 1) / BN);                                                   \
     dim3 grid(w.tiles_m * w.tiles_n * sp);                                                              \
     if (variant == 2) {                                                                                 \
-      if (conv_h > 0) gemm_wgrad_kernel<BM, BN, 64, 2, true><<<grid, kThreads, 0, stream>>>(w);         \
-      else gemm_wgrad_kernel<BM, BN, 64, 2, false><<<grid, kThreads, 0, stream>>>(w);                   \
+      if (b_sub) gemm_wgrad_kernel<BM, BN, 64, 2, 2><<<grid, kThreads, 0, stream>>>(w);                 \
+      else if (conv_h > 0) gemm_wgrad_kernel<BM, BN, 64, 2, 1><<<grid, kThreads, 0, stream>>>(w);       \
+      else gemm_wgrad_kernel<BM, BN, 64, 2, 0><<<grid, kThreads, 0, stream>>>(w);                       \
     } else {                                                                                            \
-      if (conv_h > 0) gemm_wgrad_kernel<BM, BN, 32, 3, true><<<grid, kThreads, 0, stream>>>(w);         \
-      else gemm_wgrad_kernel<BM, BN, 32, 3, false><<<grid, kThreads, 0, stream>>>(w);                   \
+      if (b_sub) gemm_wgrad_kernel<BM, BN, 32, 3, 2><<<grid, kThreads, 0, stream>>>(w);                 \
+      else if (conv_h > 0) gemm_wgrad_kernel<BM, BN, 32, 3, 1><<<grid, kThreads, 0, stream>>>(w);       \
+      else gemm_wgrad_kernel<BM, BN, 32, 3, 0><<<grid, kThreads, 0, stream>>>(w);                       \
     }                                                                                                   \
   }
   if (m128 && n128) WG(128, 128)

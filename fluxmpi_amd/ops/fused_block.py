@@ -60,6 +60,9 @@ DUAL_BN = os.environ.get("FLUXMPI_DUAL_BN", "1") == "1"
 # with the downsample BatchNorm's sums in its epilogue where measured faster than MIOpen + the
 # statistics pass (dual-BN blocks only); "force" = ours wherever supported; "miopen" = always MIOpen
 DS_FWD = os.environ.get("FLUXMPI_DS_FWD", "ours")
+# downsample weight gradient: MIOpen vs our split-K kernel (stride 2 with the B-row gather),
+# measured per shape (FLUXMPI_DS_WGRAD=0: always MIOpen)
+DS_WGRAD = os.environ.get("FLUXMPI_DS_WGRAD", "1") == "1"
 
 
 def _stream(t):
@@ -304,9 +307,7 @@ class _Conv1x1Downsample(torch.autograd.Function):
             else:
                 dx = Stride2Grad(dxc).expand(x.shape)
         if need_w and not (need_x and dx is None):
-            dw = streams.run(lambda: torch.ops.aten.convolution_backward(
-                dc, x, weight, None, [s, s], [0, 0], [1, 1], False, [0, 0], 1, [False, True, False])[1], dc, x,
-                param=weight)
+            dw = streams.run(lambda: _ds_wgrad(dc, x, weight, s), dc, x, param=weight)
         elif need_w or (need_x and dx is None):
             dx_m, dw = torch.ops.aten.convolution_backward(dc, x, weight, None, [s, s], [0, 0], [1, 1], False,
                                                            [0, 0], 1, [need_x and dx is None, need_w, False])[:2]
@@ -314,6 +315,26 @@ class _Conv1x1Downsample(torch.autograd.Function):
         if dx is not None and ctx.link is not None and ctx.link.offer(dx):
             dx = None  # delivered to conv1's dgrad epilogue
         return dx, dw, None, None, None
+
+
+def _ds_wgrad(dc, x, weight, s):
+    """The downsample convolution's weight gradient: the fastest (measured once per shape) of
+    MIOpen and our split-K kernel (stride 2: B rows gathered from the even pixels)."""
+    co, ci = weight.shape[0], weight.shape[1]
+    impls = {"miopen": lambda: torch.ops.aten.convolution_backward(
+        dc, x, weight, None, [s, s], [0, 0], [1, 1], False, [0, 0], 1, [False, True, False])[1]}
+    if DS_WGRAD and dc.dtype == torch.bfloat16 and ci % 8 == 0 and co % 8 == 0 and G.ENGINE != 1:
+        if s == 1:
+            impls["ours"] = lambda: G.conv1x1_wgrad_v2(_nhwc2d(dc), _nhwc2d(x), out_dtype=weight.dtype).view(
+                co, ci, 1, 1)
+            if _w256_ok(co, ci, dc):
+                from .linear import weight_grad
+                impls["w256"] = lambda: weight_grad(_nhwc2d(dc), _nhwc2d(x), weight.dtype).view(co, ci, 1, 1)
+        elif s == 2:
+            impls["ours"] = lambda: G.conv1x1_wgrad_s2(_nhwc2d(dc), x, out_dtype=weight.dtype).view(co, ci, 1, 1)
+    if "ours" not in impls:
+        return impls["miopen"]()
+    return wgrad_best(("ds", tuple(x.shape), co, s), impls)
 
 
 def conv1x1_downsample(x, weight, stride, link=None, ours_stats=False):

@@ -316,6 +316,22 @@ def conv1x1_wgrad_v2(dy2d: torch.Tensor, x2d: torch.Tensor, out_dtype=torch.bflo
     return _wgrad_reduce(ws, s, torch.empty(Co, Ci, device=dy2d.device, dtype=out_dtype))
 
 
+def conv1x1_wgrad_s2(dy2d: torch.Tensor, x: torch.Tensor, out_dtype=torch.bfloat16, splits: int | None = None):
+    """Weight gradient of a stride-2 1x1 convolution: dW [Cout, Cin] = sum over the output pixels
+    (n, ho, wo) of dY[pixel] x X[n, 2ho, 2wo] — the kernel gathers the even input pixels in its
+    B staging (no strided copy of X). ``dy2d`` [N*Ho*Wo, Cout], ``x`` NCHW channels_last."""
+    K, Co = dy2d.shape
+    n, ci, h, w = x.shape
+    xs = x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
+    assert K == n * ((h + 1) // 2) * ((w + 1) // 2)
+    s = _actual_splits_v2(K, splits or _wgrad_splits_v2(Co, ci, K))
+    ws = torch.empty(s, Co, ci, device=dy2d.device, dtype=torch.float32)
+    C = _ext.get(required=True)
+    C.gemm_wgrad(dy2d.data_ptr(), xs.data_ptr(), ws.data_ptr(), dy2d.stride(0), ci, Co, ci, K, s, h, w, 0,
+                 _stream(dy2d), WGRAD_VARIANT | (0 if WGRAD_REMAP else 4), 1)
+    return _wgrad_reduce(ws, s, torch.empty(Co, ci, device=dy2d.device, dtype=out_dtype))
+
+
 def conv3x3_wgrad(dy: torch.Tensor, x: torch.Tensor, splits: int | None = None) -> torch.Tensor:
     """Weight gradient of the 3x3/s1/p1 convolution: dW[co][(r, s, ci)] = sum over pixels of
     dY[pix][co] * X[pix + (r-1)*W + (s-1)][ci] — the implicit im2col is the B operand. Returns

@@ -108,3 +108,20 @@ def test_stride2_rows(gpu_ext, n, h, w, ci, co, engine):
     cf = c.float()
     torch.testing.assert_close(stats[:, 0].sum(0), cf.sum(0), rtol=1e-3, atol=1e-2)
     torch.testing.assert_close(stats[:, 1].sum(0), (cf * cf).sum(0), rtol=1e-3, atol=1e-2)
+
+
+@pytest.mark.parametrize("n,h,w,ci,co", [(2, 8, 8, 64, 128), (3, 7, 5, 32, 64), (2, 14, 14, 256, 512)])
+@pytest.mark.parametrize("variant", [1, 2])
+def test_wgrad_stride2_rows(gpu_ext, n, h, w, ci, co, variant, monkeypatch):
+    """b_sub: the stride-2 1x1 convolution's weight gradient with the B rows gathered from the even
+    pixels (odd image sizes, several splits) vs the fp32 reference."""
+    from fluxmpi_amd.ops import gemm as G
+    monkeypatch.setattr(G, "WGRAD_VARIANT", variant)
+    x = _rand(n, ci, h, w).contiguous(memory_format=torch.channels_last)
+    ho, wo = (h + 1) // 2, (w + 1) // 2
+    dy = _rand(n * ho * wo, co)
+    for splits in (1, 3):
+        dw = G.conv1x1_wgrad_s2(dy, x, out_dtype=torch.float32, splits=splits)
+        xs = x[:, :, ::2, ::2].permute(0, 2, 3, 1).reshape(-1, ci).float()
+        ref = dy.float().t() @ xs
+        torch.testing.assert_close(dw, ref, rtol=1e-2, atol=1e-2)
