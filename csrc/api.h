@@ -201,7 +201,8 @@ void gemm_glds(const GemmProblem& g, hipStream_t stream);
 // weight gradient, fp32 split-K partials ws[s][M][N] = sum over split s of A[k][m] * B[k][n]
 // (A: [K][lda], B: [K][ldb] or, conv_h > 0, the implicit 3x3/s1/p1 im2col of an NHWC image
 // [K/(H*W)][H][W][conv_c] with N = 9*conv_c; b_sub: row k of B = pixel (n, 2ho, 2wo) of the NHWC image
-// [.][conv_h][conv_w][ldb] for output pixel k = (n, ho, wo) of a stride-2 1x1 convolution);
+// [.][conv_h][conv_w][ldb] for output pixel k = (n, ho, wo) of a stride-2 1x1 convolution, or with
+// conv_c > 0 the implicit im2col of a 3x3 / stride 2 / pad 1 convolution over that grid);
 // returns nothing, reduce with gemm_splitk_reduce
 void gemm_wgrad(const void* a, const void* b, float* ws, int64_t lda, int64_t ldb, int64_t M, int64_t N, int64_t K,
                 int splits, int conv_h, int conv_w, int conv_c, hipStream_t stream, int variant = 0, int b_sub = 0);

@@ -503,10 +503,12 @@ struct WgradArgs {
 // position (CONVB, where the tap shift and channel of the lane's column are fixed too).
 // MODE 0: plain [K][ld] rows; 1 (CONVB): the implicit 3x3 im2col; 2 (SUB): row k = pixel
 // (img, ho, wo) of the [.][Ho][Wo] grid of a stride-2 1x1 convolution's output reads image row
-// (img, 2ho, 2wo) of the NHWC input [.][H][W][ld] (H, W as the conv_h / conv_w arguments).
+// (img, 2ho, 2wo) of the NHWC input [.][H][W][ld] (H, W as the conv_h / conv_w arguments);
+// 3: the implicit im2col of a 3x3 / stride 2 / pad 1 convolution (tap (dr, ds) of output pixel
+// (img, ho, wo) reads input pixel (img, 2ho + dr, 2wo + ds), zeros outside the image).
 template <int ROWS, int BK, int MODE>
 struct TrLoader {
-  static constexpr bool CONVB = MODE == 1, SUB = MODE == 2;
+  static constexpr bool CONVB = MODE == 1 || MODE == 3, SUB = MODE == 2 || MODE == 3, S2 = MODE == 3;
   static constexpr int SPR = ROWS / 8;      // 16-B slots per k-row
   static constexpr int RPP = 64 / SPR;      // k-rows per 1 KiB piece
   static constexpr int PPW = BK / RPP / 4;  // pieces per wave (BK k-rows, 4 waves)
@@ -535,12 +537,14 @@ struct TrLoader {
         ds[j] = tap % 3 - 1;
         off[j] = dr[j] * W + ds[j];
         ptr[j] = g + ci;
+      }
+      if (CONVB && !S2) {
         const int hw = k[j] % (H * W);
         h[j] = hw / W;
         w[j] = hw - h[j] * W;
       } else if (SUB) {
         const int ho = (H + 1) >> 1, wo = (W + 1) >> 1;
-        ptr[j] = g + col;
+        if (!S2) ptr[j] = g + col;
         img[j] = k[j] / (ho * wo);
         const int r = k[j] - img[j] * (ho * wo);
         h[j] = r / wo;
@@ -559,7 +563,11 @@ struct TrLoader {
     for (int j = 0; j < PPW; ++j) {
       const void* src = g_zero_line;
       if (colok[j] && k[j] < kend) {
-        if (CONVB) {
+        if (S2) {
+          const int hi = 2 * h[j] + dr[j], wi = 2 * w[j] + ds[j];
+          if (static_cast<unsigned>(hi) < static_cast<unsigned>(H) && static_cast<unsigned>(wi) < static_cast<unsigned>(W))
+            src = ptr[j] + ((static_cast<int64_t>(img[j]) * H + hi) * W + wi) * C;
+        } else if (CONVB) {
           if (static_cast<unsigned>(h[j] + dr[j]) < static_cast<unsigned>(H) &&
               static_cast<unsigned>(w[j] + ds[j]) < static_cast<unsigned>(W))
             src = ptr[j] + static_cast<int64_t>(k[j] + off[j]) * C;
@@ -574,7 +582,7 @@ struct TrLoader {
       __builtin_amdgcn_global_load_lds((gl_void*)(src),
                                        (lds_char*)(reinterpret_cast<char*>(lds_tile) + (wave * PPW + j) * 1024), 16, 0, 0);
       k[j] += BK;
-      if (CONVB) {  // pixel k -> k + BK: (h, w) += (BK / W mod H, BK % W) with one carry each
+      if (CONVB && !S2) {  // pixel k -> k + BK: (h, w) += (BK / W mod H, BK % W) with one carry each
         w[j] += dw_step;
         h[j] += dh_step;
         if (w[j] >= W) {
@@ -624,7 +632,7 @@ __device__ __forceinline__ bf16x8 read_frag_tr(const bf16* __restrict__ tile, in
 
 template <int BM, int BN, int kBK, int kStages, int BMODE>
 __global__ __launch_bounds__(kThreads, 2) void gemm_wgrad_kernel(WgradArgs p) {
-  constexpr bool CONVB = BMODE == 1;
+  constexpr bool CONVB = BMODE == 1;  // (BMODE 2 / 3: stride-2 gathers over the output grid)
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
   constexpr int A_ELEMS = BM * kBK, B_ELEMS = BN * kBK;
   constexpr int LPT = (BM + BN) * kBK / 2048;
@@ -653,9 +661,9 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_wgrad_kernel(WgradArgs p) {
   const int H = p.conv_h, W = p.conv_w, C = p.conv_c;
   // per-step advance of a lane's pixel: CONVB over (H, W); SUB over the (Ho, Wo) output grid
   const int sho = (H + 1) >> 1, swo = (W + 1) >> 1;
-  const int dw_step = CONVB ? kBK % W : (BMODE == 2 ? (kBK % (sho * swo)) % swo : 0);
-  const int dh_step = CONVB ? (kBK / W) % H : (BMODE == 2 ? (kBK % (sho * swo)) / swo : 0);
-  const int dimg_step = BMODE == 2 ? kBK / (sho * swo) : 0;
+  const int dw_step = CONVB ? kBK % W : (BMODE >= 2 ? (kBK % (sho * swo)) % swo : 0);
+  const int dh_step = CONVB ? (kBK / W) % H : (BMODE >= 2 ? (kBK % (sho * swo)) / swo : 0);
+  const int dimg_step = BMODE >= 2 ? kBK / (sho * swo) : 0;
   la.init(p.a, p.lda, p.M, m0, kbeg, 0, 1, 1);
   lb.init(p.b, p.ldb, p.N, n0, kbeg, H, W, C);
   const int kend32 = static_cast<int>(kend);
@@ -858,11 +866,11 @@ void gemm_wgrad(const void* a, const void* b, float* ws, int64_t lda, int64_t ld
                 int splits, int conv_h, int conv_w, int conv_c, hipStream_t stream, int variant, int b_sub) {
   if (lda % 8 != 0 || ldb % 8 != 0 || M % 8 != 0 || N % 8 != 0 || splits < 1)
     throw std::runtime_error("gemm_wgrad: M, N, lda, ldb must be multiples of 8");
-  if (!b_sub && conv_h > 0 && (conv_c % 8 != 0 || N != 9LL * conv_c))
+  if (conv_c > 0 && (conv_c % 8 != 0 || N != 9LL * conv_c))
     throw std::runtime_error("gemm_wgrad: implicit 3x3 B needs C % 8 == 0 and N == 9*C");
   const int64_t grid_px = b_sub ? static_cast<int64_t>((conv_h + 1) / 2) * ((conv_w + 1) / 2)
                                 : static_cast<int64_t>(conv_h) * conv_w;
-  if (b_sub && (conv_h <= 0 || conv_w <= 0 || N > ldb))
+  if (b_sub && (conv_h <= 0 || conv_w <= 0 || (conv_c == 0 && N > ldb)))
     throw std::runtime_error("gemm_wgrad: the stride-2 B gather needs the input H, W and N <= ldb");
   if (K >= (1LL << 31) || (conv_h > 0 && K % grid_px != 0))
     throw std::runtime_error("gemm_wgrad: K must fit 31 bits (and be whole images for the implicit conv)");
@@ -886,11 +894,13 @@ void gemm_wgrad(const void* a, const void* b, float* ws, int64_t lda, int64_t ld
     w.tiles_n = static_cast<int>((N + BN - 1) / BN);                                                   \
     dim3 grid(w.tiles_m * w.tiles_n * sp);                                                              \
     if (variant == 2) {                                                                                 \
-      if (b_sub) gemm_wgrad_kernel<BM, BN, 64, 2, 2><<<grid, kThreads, 0, stream>>>(w);                 \
+      if (b_sub && conv_c > 0) gemm_wgrad_kernel<BM, BN, 64, 2, 3><<<grid, kThreads, 0, stream>>>(w);   \
+      else if (b_sub) gemm_wgrad_kernel<BM, BN, 64, 2, 2><<<grid, kThreads, 0, stream>>>(w);            \
       else if (conv_h > 0) gemm_wgrad_kernel<BM, BN, 64, 2, 1><<<grid, kThreads, 0, stream>>>(w);       \
       else gemm_wgrad_kernel<BM, BN, 64, 2, 0><<<grid, kThreads, 0, stream>>>(w);                       \
     } else {                                                                                            \
-      if (b_sub) gemm_wgrad_kernel<BM, BN, 32, 3, 2><<<grid, kThreads, 0, stream>>>(w);                 \
+      if (b_sub && conv_c > 0) gemm_wgrad_kernel<BM, BN, 32, 3, 3><<<grid, kThreads, 0, stream>>>(w);   \
+      else if (b_sub) gemm_wgrad_kernel<BM, BN, 32, 3, 2><<<grid, kThreads, 0, stream>>>(w);            \
       else if (conv_h > 0) gemm_wgrad_kernel<BM, BN, 32, 3, 1><<<grid, kThreads, 0, stream>>>(w);       \
       else gemm_wgrad_kernel<BM, BN, 32, 3, 0><<<grid, kThreads, 0, stream>>>(w);                       \
     }                                                                                                   \

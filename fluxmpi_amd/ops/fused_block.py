@@ -60,8 +60,9 @@ DUAL_BN = os.environ.get("FLUXMPI_DUAL_BN", "1") == "1"
 # with the downsample BatchNorm's sums in its epilogue where measured faster than MIOpen + the
 # statistics pass (dual-BN blocks only); "force" = ours wherever supported; "miopen" = always MIOpen
 DS_FWD = os.environ.get("FLUXMPI_DS_FWD", "ours")
-# downsample weight gradient: MIOpen vs our split-K kernel (stride 2 with the B-row gather),
-# measured per shape (FLUXMPI_DS_WGRAD=0: always MIOpen)
+# weight gradients of the downsample 1x1 and the stride-2 3x3 convolutions: MIOpen vs our split-K
+# kernel (stride-2 B-row gather / implicit stride-2 im2col), measured per shape
+# (FLUXMPI_DS_WGRAD=0: always MIOpen)
 DS_WGRAD = os.environ.get("FLUXMPI_DS_WGRAD", "1") == "1"
 
 
@@ -576,6 +577,46 @@ class _Conv3x3(torch.autograd.Function):
             if bn is not None:
                 bl.ready = True
         return dx, dw, None, None, None
+
+
+class _Conv3x3S2(torch.autograd.Function):
+    """3x3 / stride 2 / pad 1 convolution (the first conv2 of ResNet stages 2-4): forward and input
+    gradient on MIOpen, weight gradient measured per shape between MIOpen and our split-K kernel
+    over the stride-2 implicit im2col (``gemm.conv3x3_wgrad_s2``)."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        x = x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
+        ctx.save_for_backward(x, weight)
+        return torch.nn.functional.conv2d(x, weight, None, 2, 1)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        if not dy.is_contiguous(memory_format=torch.channels_last):
+            dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = dw = None
+        if ctx.needs_input_grad[1]:
+            dw = streams.run(lambda: wgrad_best(("3x3s2", tuple(x.shape), weight.shape[0]), {
+                "miopen": lambda: torch.ops.aten.convolution_backward(dy, x, weight, None, [2, 2], [1, 1], [1, 1], False,
+                                                                      [0, 0], 1, [False, True, False])[1],
+                "ours": lambda: G.conv3x3_wgrad_s2(dy, x)}), dy, x, param=weight)
+        if ctx.needs_input_grad[0]:
+            dx = torch.ops.aten.convolution_backward(dy, x, weight, None, [2, 2], [1, 1], [1, 1], False, [0, 0], 1,
+                                                     [True, False, False])[0]
+        return dx, dw
+
+
+def conv3x3_s2_supported(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
+    return (DS_WGRAD and G.ENGINE != 1 and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
+            and conv.kernel_size == (3, 3) and conv.stride == (2, 2) and conv.padding == (1, 1)
+            and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None
+            and conv.in_channels % 8 == 0 and conv.out_channels % 8 == 0 and conv.weight.dtype == torch.bfloat16
+            and x.numel() // x.shape[1] < 2 ** 31)
+
+
+def conv3x3_s2(x, weight):
+    return _Conv3x3S2.apply(x, weight)
 
 
 def conv3x3_supported(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:

@@ -332,6 +332,27 @@ def conv1x1_wgrad_s2(dy2d: torch.Tensor, x: torch.Tensor, out_dtype=torch.bfloat
     return _wgrad_reduce(ws, s, torch.empty(Co, ci, device=dy2d.device, dtype=out_dtype))
 
 
+def conv3x3_wgrad_s2(dy: torch.Tensor, x: torch.Tensor, splits: int | None = None) -> torch.Tensor:
+    """Weight gradient of the 3x3 / stride 2 / pad 1 convolution: the B operand is the implicit
+    im2col over the output grid (tap (r, s) of output pixel (n, ho, wo) reads input pixel
+    (n, 2ho + r - 1, 2wo + s - 1)). Returns [Co, Ci, 3, 3] in channels_last."""
+    n, co, ho, wo = dy.shape
+    ci, h, wd = x.shape[1], x.shape[2], x.shape[3]
+    assert ho == (h + 1) // 2 and wo == (wd + 1) // 2
+    dys = dy if dy.is_contiguous(memory_format=torch.channels_last) else dy.contiguous(
+        memory_format=torch.channels_last)
+    xs = x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
+    K, N = n * ho * wo, 9 * ci
+    s = _actual_splits_v2(K, splits or _wgrad_splits_v2(co, N, K))
+    ws = torch.empty(s, co, N, device=dy.device, dtype=torch.float32)
+    C = _ext.get(required=True)
+    C.gemm_wgrad(dys.data_ptr(), xs.data_ptr(), ws.data_ptr(), co, ci, co, N, K, s, h, wd, ci, _stream(dy),
+                 WGRAD_VARIANT | (0 if WGRAD_REMAP else 4), 1)
+    dw = torch.empty(co, 3, 3, ci, device=dy.device, dtype=dy.dtype)
+    _wgrad_reduce(ws, s, dw)
+    return dw.permute(0, 3, 1, 2)
+
+
 def conv3x3_wgrad(dy: torch.Tensor, x: torch.Tensor, splits: int | None = None) -> torch.Tensor:
     """Weight gradient of the 3x3/s1/p1 convolution: dW[co][(r, s, ci)] = sum over pixels of
     dY[pix][co] * X[pix + (r-1)*W + (s-1)][ci] — the implicit im2col is the B operand. Returns

@@ -125,3 +125,21 @@ def test_wgrad_stride2_rows(gpu_ext, n, h, w, ci, co, variant, monkeypatch):
         xs = x[:, :, ::2, ::2].permute(0, 2, 3, 1).reshape(-1, ci).float()
         ref = dy.float().t() @ xs
         torch.testing.assert_close(dw, ref, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("n,h,w,ci,co", [(2, 8, 8, 32, 64), (3, 7, 5, 32, 32), (2, 14, 14, 64, 128)])
+@pytest.mark.parametrize("variant", [1, 2])
+def test_wgrad_conv3x3_stride2(gpu_ext, n, h, w, ci, co, variant, monkeypatch):
+    """The 3x3 / stride 2 / pad 1 weight gradient over the implicit stride-2 im2col (odd sizes
+    included) vs torch's fp32 convolution backward."""
+    from fluxmpi_amd.ops import gemm as G
+    monkeypatch.setattr(G, "WGRAD_VARIANT", variant)
+    x = _rand(n, ci, h, w).contiguous(memory_format=torch.channels_last)
+    ho, wo = (h + 1) // 2, (w + 1) // 2
+    dy = _rand(n, co, ho, wo).contiguous(memory_format=torch.channels_last)
+    for splits in (1, 3):
+        dw = G.conv3x3_wgrad_s2(dy, x, splits=splits)
+        ref = torch.ops.aten.convolution_backward(dy.float(), x.float(), torch.zeros(co, ci, 3, 3, device="cuda"),
+                                                  None, [2, 2], [1, 1], [1, 1], False, [0, 0], 1,
+                                                  [False, True, False])[1]
+        torch.testing.assert_close(dw.float(), ref, rtol=2e-2, atol=5e-2)
