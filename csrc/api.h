@@ -192,6 +192,9 @@ struct GemmProblem {
   // (n, 2*ho, 2*wo) of the NHWC image [M/(Ho*Wo)][a_sub_h][a_sub_w][lda] (Ho = ceil(H/2)): a
   // stride-2 1x1 convolution without the strided copy of its input. Plain K-major A only.
   int a_sub_h = 0, a_sub_w = 0;
+  // LDS-DMA kernel, implicit conv: conv_s == 2 — a 3x3 / stride 2 / pad 1 convolution over the
+  // NHWC image [M/(Ho*Wo)][conv_h][conv_w][conv_c] (conv_h / conv_w the INPUT size, Ho = ceil(H/2))
+  int conv_s = 1;
 };
 void gemm_bf16(const GemmProblem& g, hipStream_t stream);
 // the LDS-DMA pipelined kernel: K-major A (or implicit conv) and B, modes 0/1, optional residual,

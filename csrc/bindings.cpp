@@ -269,7 +269,7 @@ PYBIND11_MODULE(_C, m) {
            uintptr_t b_scale, uintptr_t b_shift, uintptr_t stats, int tile_m, int tile_n, uintptr_t stream, int nbuf, uintptr_t res, int64_t ldr,
            uintptr_t bnb_x, uintptr_t bnb_w, uintptr_t bnb_b, uintptr_t bnb_mean, uintptr_t bnb_inv,
            uintptr_t bnb_mask, int bnb_rm, int conv_h, int conv_w, int conv_c, int engine, uintptr_t res_mask,
-           int res_sub_h, int res_sub_w, int a_sub_h, int a_sub_w) {
+           int res_sub_h, int res_sub_w, int a_sub_h, int a_sub_w, int conv_s) {
           GemmProblem g{reinterpret_cast<const void*>(a), reinterpret_cast<const void*>(b),
                         reinterpret_cast<void*>(c), lda, ldb, ldc, M, N, K, a_kmajor, b_kmajor, mode, splits,
                         reinterpret_cast<const float*>(a_scale), reinterpret_cast<const float*>(a_shift),
@@ -279,7 +279,7 @@ PYBIND11_MODULE(_C, m) {
                         reinterpret_cast<const float*>(bnb_w), reinterpret_cast<const float*>(bnb_b),
                         reinterpret_cast<const float*>(bnb_mean), reinterpret_cast<const float*>(bnb_inv),
                         reinterpret_cast<const uint8_t*>(bnb_mask), bnb_rm, conv_h, conv_w, conv_c, engine,
-                        reinterpret_cast<const uint8_t*>(res_mask), res_sub_h, res_sub_w, a_sub_h, a_sub_w};
+                        reinterpret_cast<const uint8_t*>(res_mask), res_sub_h, res_sub_w, a_sub_h, a_sub_w, conv_s};
           gemm_bf16(g, S(stream));
         },
         py::arg("a"), py::arg("b"), py::arg("c"), py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("M"),
@@ -290,7 +290,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bnb_mean") = 0, py::arg("bnb_inv") = 0, py::arg("bnb_mask") = 0, py::arg("bnb_rm") = 0,
         py::arg("conv_h") = 0, py::arg("conv_w") = 0, py::arg("conv_c") = 0, py::arg("engine") = 0,
         py::arg("res_mask") = 0, py::arg("res_sub_h") = 0, py::arg("res_sub_w") = 0, py::arg("a_sub_h") = 0,
-        py::arg("a_sub_w") = 0);
+        py::arg("a_sub_w") = 0, py::arg("conv_s") = 1);
 
   m.def("gemm_wgrad",
         [](uintptr_t a, uintptr_t b, uintptr_t ws, int64_t lda, int64_t ldb, int64_t M, int64_t N, int64_t K,

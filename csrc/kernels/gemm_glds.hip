@@ -73,6 +73,7 @@ struct GldsArgs {
   const float* a_shift;
   int aff_c;             // channels of the affine (C for the implicit conv, K for a 1x1)
   int a_sub_h, a_sub_w;  // > 0: A row (n, ho, wo) is image row (n, 2ho, 2wo) of [.][a_sub_h][a_sub_w] (see api.h)
+  int conv_s;            // CONV: 1, or 2 (stride-2 3x3 over the [.][conv_h][conv_w] input; rows = output pixels)
 };
 
 // s_waitcnt vmcnt(N) with expcnt / lgkmcnt left alone (gfx9 encoding)
@@ -101,11 +102,12 @@ __device__ __forceinline__ int swz(int row) {
 // (w * PPW + j) * RPP ..; lane l fills row +(l / CPR), slot (l % CPR) with global chunk
 // slot ^ swz(row).
 // srow (plain operand, optional): the source row of piece j's rows, if not grow itself.
+// CONV: ph / pw / pbase = input row, column and pixel index of the tap-centre of piece j's row.
 template <int ROWS, int BK, bool CONV, bool PAD = false>
 __device__ __forceinline__ void issue_tile(bf16* lds_tile, const bf16* __restrict__ g, int64_t ld,
                                            int64_t rows, int64_t r0, int64_t k0, int64_t kend,
                                            const int* ph, const int* pw, int H, int W, int C,
-                                           const int64_t* srow = nullptr) {
+                                           const int64_t* srow = nullptr, const int* pbase = nullptr) {
   constexpr int CPR = BK / 8, RPP = 64 / CPR;
   constexpr int PPW = ROWS * BK / 2048;  // 1 KiB pieces per wave
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -126,7 +128,7 @@ __device__ __forceinline__ void issue_tile(bf16* lds_tile, const bf16* __restric
     if (CONV) {
       if (grow < rows && static_cast<unsigned>(ph[j] + dr) < static_cast<unsigned>(H) &&
           static_cast<unsigned>(pw[j] + ds) < static_cast<unsigned>(W))
-        src = g + (grow + dr * W + ds) * C + c0 + q * 8;
+        src = g + (static_cast<int64_t>(pbase[j]) + dr * W + ds) * C + c0 + q * 8;
     } else {
       if (grow < rows && k0 + q * 8 < kend) src = g + (srow != nullptr ? srow[j] : grow) * ld + k0 + q * 8;
     }
@@ -200,14 +202,23 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_glds_kernel(GldsArgs p) {
 
   // CONV: image position of each A row this lane stages (fixed over K)
   constexpr int PPWA = BM * kBK / 2048, RPPA = 512 / kBK;
-  int ph[PPWA], pw[PPWA];
+  int ph[PPWA], pw[PPWA], pbase[CONV ? PPWA : 1];
   if (CONV) {
 #pragma unroll
     for (int j = 0; j < PPWA; ++j) {
       const int64_t row = m0 + (wave * PPWA + j) * RPPA + lane / (kBK / 8);
-      const int hw = static_cast<int>(row % (static_cast<int64_t>(p.conv_h) * p.conv_w));
-      ph[j] = hw / p.conv_w;
-      pw[j] = hw - ph[j] * p.conv_w;
+      if (p.conv_s == 2) {  // output pixel (img, oh, ow) -> input tap-centre (2oh, 2ow); M < 2^31 host-checked
+        const int ho = (p.conv_h + 1) >> 1, wo = (p.conv_w + 1) >> 1;
+        const int r = static_cast<int>(row), img = r / (ho * wo), rr = r - img * (ho * wo), oh = rr / wo;
+        ph[j] = 2 * oh;
+        pw[j] = 2 * (rr - oh * wo);
+        pbase[j] = (img * p.conv_h + ph[j]) * p.conv_w + pw[j];
+      } else {
+        const int hw = static_cast<int>(row % (static_cast<int64_t>(p.conv_h) * p.conv_w));
+        ph[j] = hw / p.conv_w;
+        pw[j] = hw - ph[j] * p.conv_w;
+        pbase[j] = static_cast<int>(row);
+      }
     }
   }
   // plain A: the image row each staged A row reads (a_sub: the stride-2 subsample's source pixel)
@@ -227,7 +238,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_glds_kernel(GldsArgs p) {
   }
   auto issue = [&](int s, int64_t k0) {
     issue_tile<BM, kBK, CONV, AFF>(sa(s), p.a, p.lda, p.M, m0, k0, p.K, ph, pw, p.conv_h, p.conv_w, p.conv_c,
-                                   CONV ? nullptr : arow);
+                                   CONV ? nullptr : arow, CONV ? pbase : nullptr);
     issue_tile<BN, kBK, false>(sb(s), p.b, p.ldb, p.N, n0, k0, p.K, nullptr, nullptr, 0, 0, 0);
   };
   float* st_lds = reinterpret_cast<float*>(smem + kRingOrC);
@@ -775,7 +786,8 @@ bool gemm_glds_supported(const GemmProblem& g) {
          g.ldc % 8 == 0 && (g.res == nullptr || g.ldr % 8 == 0) &&
          (g.bnb_x == nullptr || (g.mode == 1 && g.ldc == g.N && g.bnb_mean != nullptr && g.bnb_inv != nullptr &&
                                  (g.bnb_rm == 0 || g.bnb_rm == 2 || (g.bnb_rm == 3 && g.bnb_mask != nullptr)))) &&
-         (g.conv_h == 0 || (g.conv_c % 32 == 0 && g.K == 9LL * g.conv_c)) &&
+         (g.conv_h == 0 || (g.conv_c % 32 == 0 && g.K == 9LL * g.conv_c && g.M < (1LL << 31))) &&
+         (g.conv_s != 2 || (g.conv_h > 0 && g.M % (static_cast<int64_t>((g.conv_h + 1) / 2) * ((g.conv_w + 1) / 2)) == 0)) &&
          (g.a_sub_h == 0 || (g.conv_h == 0 && g.a_kmajor && g.a_sub_w > 0 && g.M < (1LL << 31) &&
                              g.M % (static_cast<int64_t>((g.a_sub_h + 1) / 2) * ((g.a_sub_w + 1) / 2)) == 0)) &&
          (g.res_sub_h == 0 || (g.res != nullptr && g.res_mask == nullptr && g.res_sub_w > 0 && g.M < (1LL << 31) &&
@@ -801,6 +813,7 @@ void gemm_glds(const GemmProblem& g, hipStream_t stream) {
   a.res_mask = g.res_mask;
   a.res_sub_h = g.res_sub_h; a.res_sub_w = g.res_sub_w;
   a.a_sub_h = g.a_sub_h; a.a_sub_w = g.a_sub_w;
+  a.conv_s = g.conv_s == 2 ? 2 : 1;
   a.aff_c = static_cast<int>(g.conv_h > 0 ? g.conv_c : g.K);
   const bool aff = g.a_scale != nullptr;
   const bool bnb = g.bnb_x != nullptr;

@@ -182,10 +182,14 @@ class Bottleneck(nn.Module):
                         ours = fb.conv3x3_forward_is_ours(a1, self.conv2.weight)
                         c2 = fb.conv3x3(a1, self.conv2.weight, with_stats=True, bnlink=bl1)
                         a2 = fb.bn_from_stats(c2, self.bn2, relu=True, stats_ready=ours, bnlink=bl2)
+                    elif fb.conv3x3_s2_supported(a1, self.conv2):
+                        # stride-2 conv2: forward where measured faster on our implicit GEMM (+ bn2's
+                        # sums from its epilogue), weight gradient autotuned (fused_block._Conv3x3S2)
+                        ours = fb.conv3x3_s2_forward_is_ours(a1, self.conv2.weight)
+                        c2 = fb.conv3x3_s2(a1, self.conv2.weight, with_stats=ours)
+                        a2 = fb.bn_from_stats(c2, self.bn2, relu=True, stats_ready=ours, bnlink=bl2)
                     else:
-                        c2 = fb.conv3x3_s2(a1, self.conv2.weight) if fb.conv3x3_s2_supported(a1, self.conv2) \
-                            else self.conv2(a1)
-                        a2 = self.bn2(c2, relu=True, bnlink=bl2)
+                        a2 = self.bn2(self.conv2(a1), relu=True, bnlink=bl2)
                     o3 = fb.conv1x1_forward_is_ours(a2, self.conv3.weight)
                     c3 = fb.conv1x1_hybrid(a2, self.conv3.weight, None, bl2, ours_stats=o3)
                 else:

@@ -64,6 +64,8 @@ DS_FWD = os.environ.get("FLUXMPI_DS_FWD", "ours")
 # kernel (stride-2 B-row gather / implicit stride-2 im2col), measured per shape
 # (FLUXMPI_DS_WGRAD=0: always MIOpen)
 DS_WGRAD = os.environ.get("FLUXMPI_DS_WGRAD", "1") == "1"
+# stride-2 3x3 forward: our implicit GEMM (+ statistics epilogue) where measured faster (0: MIOpen)
+S2_FWD = os.environ.get("FLUXMPI_S2_FWD", "1") == "1"
 
 
 def _stream(t):
@@ -580,14 +582,17 @@ class _Conv3x3(torch.autograd.Function):
 
 
 class _Conv3x3S2(torch.autograd.Function):
-    """3x3 / stride 2 / pad 1 convolution (the first conv2 of ResNet stages 2-4): forward and input
-    gradient on MIOpen, weight gradient measured per shape between MIOpen and our split-K kernel
-    over the stride-2 implicit im2col (``gemm.conv3x3_wgrad_s2``)."""
+    """3x3 / stride 2 / pad 1 convolution (the first conv2 of ResNet stages 2-4). Forward: MIOpen,
+    or (``with_stats``) our implicit GEMM over the output pixels with the next BatchNorm's sums in
+    its epilogue; input gradient on MIOpen; weight gradient measured per shape between MIOpen and
+    our split-K kernel over the stride-2 implicit im2col (``gemm.conv3x3_wgrad_s2``)."""
 
     @staticmethod
-    def forward(ctx, x, weight):
+    def forward(ctx, x, weight, with_stats=False):
         x = x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
         ctx.save_for_backward(x, weight)
+        if with_stats:
+            return G.conv3x3_s2_fwd(x, weight, stats=_workspace(x))
         return torch.nn.functional.conv2d(x, weight, None, 2, 1)
 
     @staticmethod
@@ -604,7 +609,7 @@ class _Conv3x3S2(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.ops.aten.convolution_backward(dy, x, weight, None, [2, 2], [1, 1], [1, 1], False, [0, 0], 1,
                                                      [True, False, False])[0]
-        return dx, dw
+        return dx, dw, None
 
 
 def conv3x3_s2_supported(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
@@ -615,8 +620,37 @@ def conv3x3_s2_supported(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
             and x.numel() // x.shape[1] < 2 ** 31)
 
 
-def conv3x3_s2(x, weight):
-    return _Conv3x3S2.apply(x, weight)
+_S2_CHOICE: dict = {}
+
+
+def conv3x3_s2_forward_is_ours(x, weight) -> bool:
+    """Per-shape choice of the stride-2 3x3 forward, measured once: our implicit GEMM with the
+    statistics epilogue vs MIOpen plus the statistics pass (one read of the output at 5 TB/s)."""
+    if CONV3X3 != "ours" or not S2_FWD or x.shape[1] % 32 != 0:
+        return False
+    key = (tuple(x.shape), weight.shape[0])
+    hit = _S2_CHOICE.get(key)
+    if hit is not None:
+        return hit
+    if torch.cuda.is_current_stream_capturing():
+        return True
+    with torch.no_grad():
+        xs = x.detach().contiguous(memory_format=torch.channels_last)
+        w = weight.detach()
+        ws = torch.zeros_like(_workspace(xs))
+        ours = _time_us(lambda: G.conv3x3_s2_fwd(xs, w, stats=ws))
+        theirs = _time_us(lambda: torch.nn.functional.conv2d(xs, w, None, 2, 1))
+    n, _, h, wd = x.shape
+    stats_pass_us = n * ((h + 1) // 2) * ((wd + 1) // 2) * weight.shape[0] * x.element_size() / 5e12 * 1e6
+    choice = ours <= theirs + stats_pass_us
+    _S2_CHOICE[key] = choice
+    return choice
+
+
+def conv3x3_s2(x, weight, with_stats=False):
+    """``with_stats``: our forward, the output's BatchNorm sums pending in the workspace (consume
+    with ``bn_from_stats(..., stats_ready=True)``); decide with :func:`conv3x3_s2_forward_is_ours`."""
+    return _Conv3x3S2.apply(x, weight, with_stats)
 
 
 def conv3x3_supported(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:

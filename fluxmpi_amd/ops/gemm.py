@@ -44,7 +44,7 @@ def _ptr(t):
 
 def gemm(a, b, c, *, M, N, K, lda, ldb, ldc, a_kmajor=True, b_kmajor=True, mode=0, splits=1, a_affine=None,
          b_affine=None, stats=None, tile_m=0, tile_n=0, nbuf=0, residual=None, bn_bwd=None, conv=None, engine=None,
-         res_mask=None, res_sub=None, a_sub=None):
+         res_mask=None, res_sub=None, a_sub=None, conv_stride=1):
     """``res_sub=(H, W)``: ``residual`` is the compact stride-2 subsample of the [M/(H*W), H, W]
     row grid (added at even (h, w) only). ``a_sub=(H, W)``: A row (n, ho, wo) is pixel (n, 2ho, 2wo)
     of the NHWC image ``a`` [M/(Ho*Wo), H, W, lda] (a stride-2 1x1 convolution). ``bn_bwd``: ``(x2d, w32, b32, mean, inv, mask, relu_mode)`` of a BatchNorm whose output
@@ -60,7 +60,7 @@ def gemm(a, b, c, *, M, N, K, lda, ldb, ldc, a_kmajor=True, b_kmajor=True, mode=
                 _ptr(residual), residual.stride(0) if residual is not None else 0, _ptr(bx), _ptr(bw), _ptr(bb),
                 _ptr(bmean), _ptr(binv), _ptr(bmask), int(brm), *(conv if conv is not None else (0, 0, 0)),
                 ENGINE if engine is None else engine, _ptr(res_mask), *(res_sub if res_sub is not None else (0, 0)),
-                *(a_sub if a_sub is not None else (0, 0)))
+                *(a_sub if a_sub is not None else (0, 0)), int(conv_stride))
     return c
 
 
@@ -188,6 +188,20 @@ def conv3x3_fwd(x: torch.Tensor, w: torch.Tensor, in_affine=None, stats: torch.T
         return y
     gemm(xs, w2, y, M=M, N=co, K=9 * c, lda=c, ldb=9 * c, ldc=co, mode=1 if stats is not None else 0,
          a_affine=in_affine, stats=stats, conv=(h, wd, c))
+    return y
+
+
+def conv3x3_s2_fwd(x: torch.Tensor, w: torch.Tensor, stats: torch.Tensor | None = None) -> torch.Tensor:
+    """3x3 / stride 2 / pad 1 convolution as an implicit GEMM over the output pixels (each A row
+    stages the taps around input pixel (2ho, 2wo)); ``stats`` as in :func:`conv3x3_fwd`."""
+    n, c, h, wd = x.shape
+    co = w.shape[0]
+    ho, wo = (h + 1) // 2, (wd + 1) // 2
+    xs = x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
+    w2 = w.permute(0, 2, 3, 1).contiguous()  # [Co][3][3][C]
+    y = torch.empty(n, ho, wo, co, device=x.device, dtype=x.dtype).permute(0, 3, 1, 2)
+    gemm(xs, w2, y, M=n * ho * wo, N=co, K=9 * c, lda=c, ldb=9 * c, ldc=co, mode=1 if stats is not None else 0,
+         stats=stats, conv=(h, wd, c), conv_stride=2)
     return y
 
 

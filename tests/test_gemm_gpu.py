@@ -143,3 +143,20 @@ def test_wgrad_conv3x3_stride2(gpu_ext, n, h, w, ci, co, variant, monkeypatch):
                                                   None, [2, 2], [1, 1], [1, 1], False, [0, 0], 1,
                                                   [False, True, False])[1]
         torch.testing.assert_close(dw.float(), ref, rtol=2e-2, atol=5e-2)
+
+
+@pytest.mark.parametrize("n,h,w,ci,co", [(2, 8, 8, 32, 64), (3, 7, 5, 64, 32), (2, 14, 14, 128, 128)])
+def test_conv3x3_stride2_fwd(gpu_ext, n, h, w, ci, co):
+    """The 3x3 / stride 2 / pad 1 forward on the implicit GEMM (odd sizes included) with the
+    BatchNorm statistics epilogue vs torch's fp32 convolution."""
+    from fluxmpi_amd.ops.gemm import SHARDS, conv3x3_s2_fwd
+    x = _rand(n, ci, h, w).contiguous(memory_format=torch.channels_last)
+    wt = _rand(co, ci, 3, 3) * 0.1
+    stats = torch.zeros(SHARDS, 2, co, device="cuda")
+    y = conv3x3_s2_fwd(x, wt, stats=stats)
+    ref = torch.nn.functional.conv2d(x.float(), wt.float(), None, 2, 1)
+    assert y.shape == ref.shape
+    torch.testing.assert_close(y.float(), ref.to(torch.bfloat16).float(), rtol=2e-2, atol=2e-2)
+    yf = y.float().permute(0, 2, 3, 1).reshape(-1, co)
+    torch.testing.assert_close(stats[:, 0].sum(0), yf.sum(0), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(stats[:, 1].sum(0), (yf * yf).sum(0), rtol=1e-3, atol=1e-2)
