@@ -166,13 +166,14 @@ def filter_t(w: torch.Tensor) -> torch.Tensor:
 
 
 def conv3x3_fwd(x: torch.Tensor, w: torch.Tensor, in_affine=None, stats: torch.Tensor | None = None,
-                out: torch.Tensor | None = None) -> torch.Tensor:
+                out: torch.Tensor | None = None, engine: int | None = None) -> torch.Tensor:
     """3x3 / stride 1 / pad 1 convolution as an implicit GEMM on the MFMA kernel.
 
     ``x`` [N, C, H, W] bf16 channels_last, ``w`` [Co, C, 3, 3] bf16 -> [N, Co, H, W] channels_last.
     ``in_affine=(scale, shift)``: relu(x * scale + shift) per input channel applied on load (the
     previous BatchNorm + ReLU; the zero padding stays zero). ``stats``: per-output-channel
-    sum / sumsq into the sharded BatchNorm workspace.
+    sum / sumsq into the sharded BatchNorm workspace. ``engine``: force a tile configuration of the
+    LDS-DMA kernel (7 / 8: 256x128 tiles; see gemm_glds.hip), e.g. the one an autotune picked.
     """
     n, c, h, wd = x.shape
     co = w.shape[0]
@@ -181,13 +182,13 @@ def conv3x3_fwd(x: torch.Tensor, w: torch.Tensor, in_affine=None, stats: torch.T
     note_filter(w)
     y = out if out is not None else torch.empty(n, h, wd, co, device=x.device, dtype=x.dtype).permute(0, 3, 1, 2)
     M = n * h * wd
-    if in_affine is None and x.dtype == torch.bfloat16 and halo_ok(n, h, wd, c, co) and \
+    if not engine and in_affine is None and x.dtype == torch.bfloat16 and halo_ok(n, h, wd, c, co) and \
             y.is_contiguous(memory_format=torch.channels_last):
         _ext.get(required=True).conv3x3_halo(xs.data_ptr(), w2.data_ptr(), y.data_ptr(), _ptr(stats), n, h, wd, c,
                                              co, _stream(x))
         return y
     gemm(xs, w2, y, M=M, N=co, K=9 * c, lda=c, ldb=9 * c, ldc=co, mode=1 if stats is not None else 0,
-         a_affine=in_affine, stats=stats, conv=(h, wd, c))
+         a_affine=in_affine, stats=stats, conv=(h, wd, c), engine=engine or None)
     return y
 
 

@@ -29,7 +29,8 @@ def main():
         F.cross_entropy(model(x).float(), y).backward()
     torch.cuda.synchronize()
     for name, d in (("fwd1x1_ours", fb._FWD1_CHOICE), ("fwd3x3_ours", fb._FWD_CHOICE), ("wgrad", fb._WG_CHOICE),
-                    ("fwd_ds_ours", fb._DS_CHOICE), ("fwd3x3s2_ours", fb._S2_CHOICE)):
+                    ("fwd_ds_ours", fb._DS_CHOICE), ("fwd3x3s2_ours", fb._S2_CHOICE),
+                    ("fwd3x3_engine", fb._FWD_ENGINE)):
         for k, v in d.items():
             print(json.dumps({"kind": name, "key": str(k), "choice": str(v)}))
 
