@@ -135,15 +135,15 @@ void maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, int64_t N, int64_
 
 // ---- fused LayerNorm (+ residual add), rows of D (D % 8 == 0, D <= 8192) ----------------
 // forward: [h = x + residual] (h written when residual != nullptr); y = LN(h) * w + b;
-// mean / rstd per row (fp32) saved. w/b fp32 (nullable).
-void layernorm_fwd(const void* x, const void* residual, void* h, void* y, const float* w, const float* b, float* mean,
-                   float* rstd, int64_t rows, int64_t D, float eps, int dtype, hipStream_t stream);
+// mean / rstd per row (fp32) saved. w/b: fp32 or the activation dtype (wdtype), 16-byte aligned.
+void layernorm_fwd(const void* x, const void* residual, void* h, void* y, const void* w, const void* b, float* mean,
+                   float* rstd, int64_t rows, int64_t D, float eps, int dtype, int wdtype, hipStream_t stream);
 // backward: dx = LN backward of dy [+ dh_ext]; per-workgroup [2][D] fp32 partials of (dw, db)
 // stored into `partials` (capacity max_blocks x 2D); returns the number of partial rows written
 // (sum them with gemm_splitk_reduce).
 int layernorm_bwd(const void* dy, const void* x, const void* dh_ext, const float* mean, const float* rstd,
-                  const float* w, void* dx, float* partials, int max_blocks, int64_t rows, int64_t D, int dtype,
-                  hipStream_t stream);
+                  const void* w, void* dx, float* partials, int max_blocks, int64_t rows, int64_t D, int dtype,
+                  int wdtype, hipStream_t stream);
 
 // ---- MFMA bf16 GEMM with BatchNorm fusions (1x1 convolutions) --------------------
 // C[M,N] = A[M,K] * B[N,K]^T. a_kmajor: A stored [M][lda] (K contiguous), else [K][lda]

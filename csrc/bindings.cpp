@@ -247,19 +247,20 @@ PYBIND11_MODULE(_C, m) {
   // ---- fused LayerNorm ------------------------------------------------------
   m.def("layernorm_fwd", [](uintptr_t x, uintptr_t res, uintptr_t h, uintptr_t y, uintptr_t w, uintptr_t b,
                             uintptr_t mean, uintptr_t rstd, int64_t rows, int64_t D, float eps, int dtype,
-                            uintptr_t stream) {
+                            int wdtype, uintptr_t stream) {
     layernorm_fwd(reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(res), reinterpret_cast<void*>(h),
-                  reinterpret_cast<void*>(y), reinterpret_cast<const float*>(w), reinterpret_cast<const float*>(b),
-                  reinterpret_cast<float*>(mean), reinterpret_cast<float*>(rstd), rows, D, eps, dtype, S(stream));
+                  reinterpret_cast<void*>(y), reinterpret_cast<const void*>(w), reinterpret_cast<const void*>(b),
+                  reinterpret_cast<float*>(mean), reinterpret_cast<float*>(rstd), rows, D, eps, dtype, wdtype,
+                  S(stream));
   });
   m.def("layernorm_bwd", [](uintptr_t dy, uintptr_t x, uintptr_t dh, uintptr_t mean, uintptr_t rstd, uintptr_t w,
                             uintptr_t dx, uintptr_t part, int max_blocks, int64_t rows, int64_t D, int dtype,
-                            uintptr_t stream) {
+                            int wdtype, uintptr_t stream) {
     return layernorm_bwd(reinterpret_cast<const void*>(dy), reinterpret_cast<const void*>(x),
                          reinterpret_cast<const void*>(dh), reinterpret_cast<const float*>(mean),
-                         reinterpret_cast<const float*>(rstd), reinterpret_cast<const float*>(w),
+                         reinterpret_cast<const float*>(rstd), reinterpret_cast<const void*>(w),
                          reinterpret_cast<void*>(dx), reinterpret_cast<float*>(part), max_blocks, rows, D, dtype,
-                         S(stream));
+                         wdtype, S(stream));
   });
 
   // ---- MFMA GEMM (1x1 conv) -------------------------------------------------

@@ -38,6 +38,16 @@ __device__ __forceinline__ void ld8w(const float* __restrict__ p, int c0, float 
   v[4] = a1.x; v[5] = a1.y; v[6] = a1.z; v[7] = a1.w;
 }
 
+// the affine in the activation dtype (a bf16 model's LayerNorm parameters as they are: no
+// per-call fp32 copies of w and b, two tiny cast kernels per LayerNorm per step)
+template <typename A>
+__device__ __forceinline__ void ld8w(const A* __restrict__ p, int c0, float (&v)[8]) {
+  A t[8];
+  load8(p + c0, t);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = static_cast<float>(t[j]);
+}
+
 // A lane's vectors i = lane + 64 * i of a row; lanes past the row (D/8 not a multiple of 64)
 // load vector 0 and are masked in the math: every load is unconditional (a load under
 // `if (v < nv)` is waited for at the branch join, one exposed latency per vector).
@@ -60,10 +70,10 @@ struct LnLanes {
 // row's reductions, and the affine w/b held in registers for the whole kernel (16-byte
 // loads, once). (The one-row-per-wave version had only one row's loads in flight: 141-155 us
 // per ViT-B LayerNorm (50432 x 768 bf16) on MI355X, ~2-3x its HBM time, s48 trace.)
-template <typename T, bool ADD, int VPL>
+template <typename T, bool ADD, int VPL, typename A>
 __global__ __launch_bounds__(kThreads) void ln_fwd_kernel(const T* __restrict__ x, const T* __restrict__ r,
                                                           T* __restrict__ h, T* __restrict__ y,
-                                                          const float* __restrict__ w, const float* __restrict__ b,
+                                                          const A* __restrict__ w, const A* __restrict__ b,
                                                           float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                           int64_t rows, int D, float eps) {
   const int lane = threadIdx.x & 63;
@@ -161,12 +171,12 @@ __global__ __launch_bounds__(kThreads) void ln_fwd_kernel(const T* __restrict__ 
 // during the current row's two reductions and its dx stores (PF: up to 4 vectors per lane;
 // wider rows would spill the second buffer). dy and xhat are recomputed from the raw row in
 // the second pass rather than kept as fp32 arrays.
-template <typename T, bool DH, int VPL>
+template <typename T, bool DH, int VPL, typename A>
 __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                           const T* __restrict__ dh_ext,
                                                           const float* __restrict__ mean_in,
                                                           const float* __restrict__ rstd_in,
-                                                          const float* __restrict__ w, T* __restrict__ dx,
+                                                          const A* __restrict__ w, T* __restrict__ dx,
                                                           float* __restrict__ part, int64_t rows, int D) {
   constexpr bool PF = VPL <= 4;
   extern __shared__ __attribute__((aligned(16))) float red[];  // [2][D]
@@ -275,23 +285,24 @@ int vpl_for(int64_t D) {
   return 16;
 }
 
-template <typename T, bool ADD, int VPL>
-void fwd_launch(const void* x, const void* r, void* h, void* y, const float* w, const float* b, float* mean,
+template <typename T, bool ADD, int VPL, typename A>
+void fwd_launch(const void* x, const void* r, void* h, void* y, const void* w, const void* b, float* mean,
                 float* rstd, int64_t rows, int64_t D, float eps, hipStream_t s) {
-  auto k = ln_fwd_kernel<T, ADD, VPL>;
+  auto k = ln_fwd_kernel<T, ADD, VPL, A>;
   int64_t blocks = resident_blocks(reinterpret_cast<const void*>(k), kThreads, 0);
   const int64_t need = (rows + kWaves - 1) / kWaves;
   if (blocks > need) blocks = need;
   if (blocks < 1) blocks = 1;
   k<<<(unsigned)blocks, kThreads, 0, s>>>(
-      static_cast<const T*>(x), static_cast<const T*>(r), static_cast<T*>(h), static_cast<T*>(y), w, b, mean, rstd,
+      static_cast<const T*>(x), static_cast<const T*>(r), static_cast<T*>(h), static_cast<T*>(y),
+      static_cast<const A*>(w), static_cast<const A*>(b), mean, rstd,
       rows, static_cast<int>(D), eps);
 }
 
-template <typename T, bool DH, int VPL>
-int bwd_launch(const void* dy, const void* x, const void* dh, const float* mean, const float* rstd, const float* w,
+template <typename T, bool DH, int VPL, typename A>
+int bwd_launch(const void* dy, const void* x, const void* dh, const float* mean, const float* rstd, const void* w,
                void* dx, float* part, int max_blocks, int64_t rows, int64_t D, hipStream_t s) {
-  auto k = ln_bwd_kernel<T, DH, VPL>;
+  auto k = ln_bwd_kernel<T, DH, VPL, A>;
   const size_t lds = static_cast<size_t>(2) * D * sizeof(float);
   int64_t blocks = resident_blocks(reinterpret_cast<const void*>(k), kThreads, lds);
   const int64_t need = (rows + kWaves - 1) / kWaves;
@@ -299,7 +310,8 @@ int bwd_launch(const void* dy, const void* x, const void* dh, const float* mean,
   if (blocks > max_blocks) blocks = max_blocks;
   if (blocks < 1) blocks = 1;
   k<<<(unsigned)blocks, kThreads, lds, s>>>(static_cast<const T*>(dy), static_cast<const T*>(x),
-                                            static_cast<const T*>(dh), mean, rstd, w, static_cast<T*>(dx), part, rows,
+                                            static_cast<const T*>(dh), mean, rstd, static_cast<const A*>(w),
+                                            static_cast<T*>(dx), part, rows,
                                             static_cast<int>(D));
   return static_cast<int>(blocks);
 }
@@ -319,67 +331,85 @@ int bwd_launch(const void* dy, const void* x, const void* dh, const float* mean,
 
 }  // namespace
 
-void layernorm_fwd(const void* x, const void* residual, void* h, void* y, const float* w, const float* b, float* mean,
-                   float* rstd, int64_t rows, int64_t D, float eps, int dtype, hipStream_t stream) {
+// the affine is fp32 or in the activation dtype (wdtype == dtype)
+static void check_affine(int dtype, int wdtype, const char* who) {
+  if (wdtype != static_cast<int>(kF32) && wdtype != dtype)
+    throw std::runtime_error(std::string(who) + ": w / b must be fp32 or in the activation dtype");
+}
+
+void layernorm_fwd(const void* x, const void* residual, void* h, void* y, const void* w, const void* b, float* mean,
+                   float* rstd, int64_t rows, int64_t D, float eps, int dtype, int wdtype, hipStream_t stream) {
   const int vpl = vpl_for(D);
   const bool add = residual != nullptr;
   if (w == nullptr || b == nullptr || (reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(b)) % 16 != 0)
-    throw std::runtime_error("fused layernorm: w and b must be 16-byte aligned fp32 (ones / zeros when absent)");
-#define CALL_ADD(V) fwd_launch<TT, true, V>(x, residual, h, y, w, b, mean, rstd, rows, D, eps, stream)
-#define CALL_NOADD(V) fwd_launch<TT, false, V>(x, residual, h, y, w, b, mean, rstd, rows, D, eps, stream)
+    throw std::runtime_error("fused layernorm: w and b must be 16-byte aligned (ones / zeros when absent)");
+  check_affine(dtype, wdtype, "fused layernorm");
+  const bool wt = wdtype != static_cast<int>(kF32);
+#define CALL_ADD(V) fwd_launch<TT, true, V, AT>(x, residual, h, y, w, b, mean, rstd, rows, D, eps, stream)
+#define CALL_NOADD(V) fwd_launch<TT, false, V, AT>(x, residual, h, y, w, b, mean, rstd, rows, D, eps, stream)
+#define CALL_ALL                                                                \
+  if (add) { LN_VPL_SWITCH(vpl, CALL_ADD) } else { LN_VPL_SWITCH(vpl, CALL_NOADD) }
   switch (dtype) {
     case kBF16: {
       using TT = bf16;
-      if (add) { LN_VPL_SWITCH(vpl, CALL_ADD) } else { LN_VPL_SWITCH(vpl, CALL_NOADD) }
+      if (wt) { using AT = bf16; CALL_ALL } else { using AT = float; CALL_ALL }
       break;
     }
     case kF16: {
       using TT = f16;
-      if (add) { LN_VPL_SWITCH(vpl, CALL_ADD) } else { LN_VPL_SWITCH(vpl, CALL_NOADD) }
+      if (wt) { using AT = f16; CALL_ALL } else { using AT = float; CALL_ALL }
       break;
     }
     case kF32: {
       using TT = float;
-      if (add) { LN_VPL_SWITCH(vpl, CALL_ADD) } else { LN_VPL_SWITCH(vpl, CALL_NOADD) }
+      using AT = float;
+      CALL_ALL
       break;
     }
     default:
       throw std::runtime_error("fused layernorm: unsupported dtype");
   }
+#undef CALL_ALL
 #undef CALL_ADD
 #undef CALL_NOADD
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
 
 int layernorm_bwd(const void* dy, const void* x, const void* dh_ext, const float* mean, const float* rstd,
-                  const float* w, void* dx, float* partials, int max_blocks, int64_t rows, int64_t D, int dtype,
-                  hipStream_t stream) {
+                  const void* w, void* dx, float* partials, int max_blocks, int64_t rows, int64_t D, int dtype,
+                  int wdtype, hipStream_t stream) {
   const int vpl = vpl_for(D);
   const bool dh = dh_ext != nullptr;
   if (w == nullptr || reinterpret_cast<uintptr_t>(w) % 16 != 0)
-    throw std::runtime_error("fused layernorm backward: w must be 16-byte aligned fp32 (ones when absent)");
+    throw std::runtime_error("fused layernorm backward: w must be 16-byte aligned (ones when absent)");
+  check_affine(dtype, wdtype, "fused layernorm backward");
+  const bool wt = wdtype != static_cast<int>(kF32);
   int blocks = 0;
-#define CALL_DH(V) blocks = bwd_launch<TT, true, V>(dy, x, dh_ext, mean, rstd, w, dx, partials, max_blocks, rows, D, stream)
-#define CALL_NODH(V) blocks = bwd_launch<TT, false, V>(dy, x, dh_ext, mean, rstd, w, dx, partials, max_blocks, rows, D, stream)
+#define CALL_DH(V) blocks = bwd_launch<TT, true, V, AT>(dy, x, dh_ext, mean, rstd, w, dx, partials, max_blocks, rows, D, stream)
+#define CALL_NODH(V) blocks = bwd_launch<TT, false, V, AT>(dy, x, dh_ext, mean, rstd, w, dx, partials, max_blocks, rows, D, stream)
+#define CALL_ALL                                                                \
+  if (dh) { LN_VPL_SWITCH(vpl, CALL_DH) } else { LN_VPL_SWITCH(vpl, CALL_NODH) }
   switch (dtype) {
     case kBF16: {
       using TT = bf16;
-      if (dh) { LN_VPL_SWITCH(vpl, CALL_DH) } else { LN_VPL_SWITCH(vpl, CALL_NODH) }
+      if (wt) { using AT = bf16; CALL_ALL } else { using AT = float; CALL_ALL }
       break;
     }
     case kF16: {
       using TT = f16;
-      if (dh) { LN_VPL_SWITCH(vpl, CALL_DH) } else { LN_VPL_SWITCH(vpl, CALL_NODH) }
+      if (wt) { using AT = f16; CALL_ALL } else { using AT = float; CALL_ALL }
       break;
     }
     case kF32: {
       using TT = float;
-      if (dh) { LN_VPL_SWITCH(vpl, CALL_DH) } else { LN_VPL_SWITCH(vpl, CALL_NODH) }
+      using AT = float;
+      CALL_ALL
       break;
     }
     default:
       throw std::runtime_error("fused layernorm: unsupported dtype");
   }
+#undef CALL_ALL
 #undef CALL_DH
 #undef CALL_NODH
   FLUXMPI_HIP_CHECK(hipGetLastError());

@@ -48,56 +48,71 @@ def _const(d: int, device, value: float) -> torch.Tensor:
     return t
 
 
-def _fwd(x, r, w32, b32, eps):
+def _affine(x, weight, bias):
+    """The (w, b) the kernels read: the parameters themselves when both are present in the
+    activation dtype (the kernels convert on load), else fp32 copies / cached ones-zeros."""
+    if (weight is not None and bias is not None and weight.dtype == x.dtype == bias.dtype
+            and weight.is_contiguous() and bias.is_contiguous()
+            and (weight.data_ptr() | bias.data_ptr()) % 16 == 0):
+        return weight, bias
+    d = x.shape[-1]
+    w32 = weight.float().contiguous() if weight is not None else _const(d, x.device, 1.0)
+    b32 = bias.float().contiguous() if bias is not None else _const(d, x.device, 0.0)
+    return w32, b32
+
+
+def _fwd(x, r, w, b, eps):
     C = _ext.get(required=True)
     d = x.shape[-1]
-    w32 = w32 if w32 is not None else _const(d, x.device, 1.0)
-    b32 = b32 if b32 is not None else _const(d, x.device, 0.0)
     rows = x.numel() // d
     y = torch.empty_like(x)
     h = torch.empty_like(x) if r is not None else None
     mean = torch.empty(rows, device=x.device, dtype=torch.float32)
     rstd = torch.empty_like(mean)
-    C.layernorm_fwd(x.data_ptr(), _p(r), _p(h), y.data_ptr(), _p(w32), _p(b32), mean.data_ptr(), rstd.data_ptr(),
-                    rows, d, float(eps), DTYPE_CODE[x.dtype], _stream(x))
+    C.layernorm_fwd(x.data_ptr(), _p(r), _p(h), y.data_ptr(), w.data_ptr(), b.data_ptr(), mean.data_ptr(),
+                    rstd.data_ptr(), rows, d, float(eps), DTYPE_CODE[x.dtype], DTYPE_CODE[w.dtype], _stream(x))
     return h, y, mean, rstd
 
 
-def _bwd(dy, x, dh_ext, mean, rstd, w32, need_wb):
+def _bwd(dy, x, dh_ext, mean, rstd, w, dtypes):
+    """``(dx, dw, db)``; dw / db reduced straight into the parameter dtype when it is fp32 or bf16
+    and both share it (no cast kernels), else reduced in fp32 and cast."""
     C = _ext.get(required=True)
     d = x.shape[-1]
-    w32 = w32 if w32 is not None else _const(d, x.device, 1.0)
     rows = x.numel() // d
     dx = torch.empty_like(x)
     part = torch.empty(_MAX_BLOCKS, 2 * d, device=x.device, dtype=torch.float32)
-    nb = C.layernorm_bwd(dy.data_ptr(), x.data_ptr(), _p(dh_ext), mean.data_ptr(), rstd.data_ptr(), _p(w32),
-                         dx.data_ptr(), part.data_ptr(), _MAX_BLOCKS, rows, d, DTYPE_CODE[x.dtype], _stream(x))
-    wb = None
-    if need_wb:
-        wb = torch.empty(2 * d, device=x.device, dtype=torch.float32)
-        C.gemm_splitk_reduce(part.data_ptr(), nb, 2 * d, wb.data_ptr(), 7, _stream(x))
-    return dx, wb
+    nb = C.layernorm_bwd(dy.data_ptr(), x.data_ptr(), _p(dh_ext), mean.data_ptr(), rstd.data_ptr(), w.data_ptr(),
+                         dx.data_ptr(), part.data_ptr(), _MAX_BLOCKS, rows, d, DTYPE_CODE[x.dtype],
+                         DTYPE_CODE[w.dtype], _stream(x))
+    wd, bd = dtypes
+    if wd is None and bd is None:
+        return dx, None, None
+    present = {t for t in dtypes if t is not None}
+    odt = present.pop() if len(present) == 1 else torch.float32
+    if odt not in (torch.float32, torch.bfloat16):
+        odt = torch.float32
+    wb = torch.empty(2 * d, device=x.device, dtype=odt)
+    C.gemm_splitk_reduce(part.data_ptr(), nb, 2 * d, wb.data_ptr(), DTYPE_CODE[odt], _stream(x))
+    dw = wb[:d].to(wd) if wd is not None else None
+    db = wb[d:].to(bd) if bd is not None else None
+    return dx, dw, db
 
 
 class _LayerNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, eps):
         x = x.contiguous()
-        w32 = weight.float() if weight is not None else None
-        b32 = bias.float() if bias is not None else None
-        _, y, mean, rstd = _fwd(x, None, w32, b32, eps)
-        ctx.save_for_backward(x, w32, mean, rstd)
+        w, b = _affine(x, weight, bias)
+        _, y, mean, rstd = _fwd(x, None, w, b, eps)
+        ctx.save_for_backward(x, w, mean, rstd)
         ctx.dtypes = (weight.dtype if weight is not None else None, bias.dtype if bias is not None else None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, w32, mean, rstd = ctx.saved_tensors
-        wd, bd = ctx.dtypes
-        dx, wb = _bwd(dy.contiguous(), x, None, mean, rstd, w32, wd is not None or bd is not None)
-        d = x.shape[-1]
-        dw = wb[:d].to(wd) if wd is not None else None
-        db = wb[d:].to(bd) if bd is not None else None
+        x, w, mean, rstd = ctx.saved_tensors
+        dx, dw, db = _bwd(dy.contiguous(), x, None, mean, rstd, w, ctx.dtypes)
         return dx, dw, db, None
 
 
@@ -105,24 +120,19 @@ class _AddLayerNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, r, weight, bias, eps):
         x, r = x.contiguous(), r.contiguous()
-        w32 = weight.float() if weight is not None else None
-        b32 = bias.float() if bias is not None else None
-        h, y, mean, rstd = _fwd(x, r, w32, b32, eps)
-        ctx.save_for_backward(h, w32, mean, rstd)
+        w, b = _affine(x, weight, bias)
+        h, y, mean, rstd = _fwd(x, r, w, b, eps)
+        ctx.save_for_backward(h, w, mean, rstd)
         ctx.dtypes = (weight.dtype if weight is not None else None, bias.dtype if bias is not None else None)
         return h, y
 
     @staticmethod
     def backward(ctx, dh, dy):
-        h, w32, mean, rstd = ctx.saved_tensors
-        wd, bd = ctx.dtypes
+        h, w, mean, rstd = ctx.saved_tensors
         if dy is None:
             dy = torch.zeros_like(h)
         dh = dh.contiguous() if dh is not None else None
-        dx, wb = _bwd(dy.contiguous(), h, dh, mean, rstd, w32, wd is not None or bd is not None)
-        d = h.shape[-1]
-        dw = wb[:d].to(wd) if wd is not None else None
-        db = wb[d:].to(bd) if bd is not None else None
+        dx, dw, db = _bwd(dy.contiguous(), h, dh, mean, rstd, w, ctx.dtypes)
         return dx, dx, dw, db, None  # h = x + r: both inputs get the same gradient
 
 

@@ -21,14 +21,18 @@ def test_add_layer_norm_cpu_fallback():
 @pytest.mark.parametrize("shape", [(4, 197, 768), (3, 5, 64), (2, 7, 1032), (2, 3, 4096), (64, 197, 768)])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("add", [False, True])
-def test_layer_norm_vs_reference(gpu_ext, shape, dtype, add):
+@pytest.mark.parametrize("affine", ["act", "fp32"])
+def test_layer_norm_vs_reference(gpu_ext, shape, dtype, add, affine):
+    """``affine="act"``: w / b in the activation dtype, read by the kernels as they are (dw / db
+    reduced straight into that dtype); ``"fp32"``: fp32 parameters with bf16 activations."""
     from fluxmpi_amd.ops.layernorm import add_layer_norm, layer_norm
     torch.manual_seed(0)
     d = shape[-1]
     x = torch.randn(shape, device="cuda").to(dtype)
     r = torch.randn(shape, device="cuda").to(dtype)
-    w = (torch.rand(d, device="cuda") + 0.5).to(dtype)
-    b = (torch.randn(d, device="cuda") * 0.1).to(dtype)
+    wdt = dtype if affine == "act" else torch.float32
+    w = (torch.rand(d, device="cuda") + 0.5).to(wdt)
+    b = (torch.randn(d, device="cuda") * 0.1).to(wdt)
     xa, ra, wa, ba = (t.clone().requires_grad_() for t in (x, r, w, b))
     xr, rr, wr, br = (t.float().clone().requires_grad_() for t in (x, r, w, b))
     if add:
@@ -49,6 +53,21 @@ def test_layer_norm_vs_reference(gpu_ext, shape, dtype, add):
     tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
     assert _rel(y, yr) < tol
     assert _rel(xa.grad, xr.grad) < tol
+    assert wa.grad.dtype == wdt and ba.grad.dtype == wdt
     assert _rel(wa.grad, wr.grad) < tol and _rel(ba.grad, br.grad) < tol
     if add:
         assert _rel(ra.grad, rr.grad) < tol
+
+
+@pytest.mark.gpu
+def test_layer_norm_no_affine(gpu_ext):
+    from fluxmpi_amd.ops.layernorm import layer_norm
+    torch.manual_seed(0)
+    x = torch.randn(8, 33, 768, device="cuda").to(torch.bfloat16)
+    xa, xr = x.clone().requires_grad_(), x.float().clone().requires_grad_()
+    y = layer_norm(xa, None, None, 1e-6)
+    yr = F.layer_norm(xr, (768,), None, None, 1e-6)
+    gy = torch.randn_like(yr)
+    (y.float() * gy).sum().backward()
+    (yr * gy).sum().backward()
+    assert _rel(y, yr) < 2e-2 and _rel(xa.grad, xr.grad) < 2e-2
