@@ -237,6 +237,16 @@ void anderson_gram(const float* X, const float* F, float* G, unsigned fresh, flo
 // z (nullable, [bsz][d], dtype z_dtype): the new iterate cast to the model dtype.
 void anderson_mix(float* X, const float* F, const float* alpha, void* z, int z_dtype, int64_t bsz, int64_t d,
                   int64_t row_stride, int64_t batch_stride, int n, int slot, float beta, hipStream_t stream);
+// anderson_solve: from anderson_gram's partials, alpha[b][0..n) of the regularised Anderson system
+// [[0, 1^T], [1, G G^T + lam I]] a = e_0 (a[1..n]) per batch element (bsz <= 1024, one launch),
+// and (res nullable) the relative residual of row `last` into res[0].
+void anderson_solve(const float* partials, int chunks, int64_t bsz, int n, int last, float lam, float* alpha,
+                    float* res, hipStream_t stream);
+// adjoint_step: u_new = vjp + grad (dtype), partials[blocks] = per-workgroup sums of (u_new - u)^2
+// (fp32; n % 8 == 0, 16-byte aligned, same memory layout); adjoint_step_blocks: the grid size.
+int adjoint_step_blocks(int64_t n);
+void adjoint_step(const void* vjp, const void* grad, const void* u, void* u_new, float* partials, int blocks,
+                  int64_t n, int dtype, hipStream_t stream);
 
 // ---- fused NHWC GroupNorm (+ add, + ReLU on its input); one workgroup per sample ---------
 // forward: h = [relu](x [+ add]) (stored when h != nullptr); y = GN(h) * w + b (w/b fp32, nullable);

@@ -198,6 +198,18 @@ PYBIND11_MODULE(_C, m) {
     anderson_gram(reinterpret_cast<const float*>(X), reinterpret_cast<const float*>(F), reinterpret_cast<float*>(G),
                   fresh, reinterpret_cast<float*>(part), bsz, d, rs, bs, n, last, chunks, S(stream));
   });
+  m.def("adjoint_step_blocks", &adjoint_step_blocks);
+  m.def("adjoint_step", [](uintptr_t vjp, uintptr_t grad, uintptr_t u, uintptr_t u_new, uintptr_t part, int blocks,
+                           int64_t n, int dtype, uintptr_t stream) {
+    adjoint_step(reinterpret_cast<const void*>(vjp), reinterpret_cast<const void*>(grad),
+                 reinterpret_cast<const void*>(u), reinterpret_cast<void*>(u_new), reinterpret_cast<float*>(part),
+                 blocks, n, dtype, S(stream));
+  });
+  m.def("anderson_solve", [](uintptr_t part, int chunks, int64_t bsz, int n, int last, float lam, uintptr_t alpha,
+                             uintptr_t res, uintptr_t stream) {
+    anderson_solve(reinterpret_cast<const float*>(part), chunks, bsz, n, last, lam, reinterpret_cast<float*>(alpha),
+                   reinterpret_cast<float*>(res), S(stream));
+  });
   m.def("anderson_mix", [](uintptr_t X, uintptr_t F, uintptr_t alpha, uintptr_t z, int zdt, int64_t bsz, int64_t d,
                            int64_t rs, int64_t bs, int n, int slot, float beta, uintptr_t stream) {
     anderson_mix(reinterpret_cast<float*>(X), reinterpret_cast<const float*>(F), reinterpret_cast<const float*>(alpha),

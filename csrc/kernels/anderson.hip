@@ -157,6 +157,152 @@ __global__ __launch_bounds__(kThreads) void mix_kernel(float* __restrict__ X, co
   }
 }
 
+// One launch for everything between the Gram pass and the mix (was ~15 tiny PyTorch / rocSOLVER
+// launches per solver iteration: chunk sum, symmetric gather, residual sums / sqrt / divide, H
+// assembly, getrf + two triangular solves, the alpha slice copy). One workgroup, thread b owns
+// batch element b: it sums its Gram chunk partials, builds
+//     H = [[0, 1^T], [1, G G^T + lam I]]   ((n+1) x (n+1)),  y = e_0
+// in registers and solves H a = y by Gaussian elimination with partial pivoting (LAPACK getrf's
+// pivot choice: the first largest |H[r][k]|; row swaps as compile-time-indexed selects, so
+// nothing is dynamically indexed / spilled); alpha[b] = a[1..n]. `res` (nullable): the relative
+// residual of the previous iterate, sqrt(sum_b G G^T[last][last]) / (1e-5 + sqrt(sum_b |F_last|^2)),
+// reduced over the workgroup.
+template <int N>
+__global__ __launch_bounds__(1024) void solve_kernel(const float* __restrict__ part, int chunks, int bsz, int last,
+                                                     float lam, float* __restrict__ alpha, float* __restrict__ res) {
+  constexpr int P = N * (N + 1) / 2, M = N + 1;
+  const int b = threadIdx.x;
+  float g[P];
+  float fn = 0.f;
+#pragma unroll
+  for (int p = 0; p < P; ++p) g[p] = 0.f;
+  if (b < bsz) {
+    const float* pp = part + static_cast<int64_t>(b) * chunks * kOut;
+    for (int c = 0; c < chunks; ++c) {
+#pragma unroll
+      for (int p = 0; p < P; ++p) g[p] += pp[c * kOut + p];
+      fn += pp[c * kOut + kPairs];
+    }
+  }
+  auto pidx = [](int i, int j) { return i * N - i * (i - 1) / 2 + (j - i); };  // i <= j, row-major triangle
+  if (res != nullptr) {
+    float dl = 0.f;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      if (i == last) dl = g[pidx(i, i)];
+    __shared__ float red[2][16];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const float s1 = wave_sum(dl), s2 = wave_sum(fn);
+    if (lane == 0) {
+      red[0][wave] = s1;
+      red[1][wave] = s2;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float a1 = 0.f, a2 = 0.f;
+      for (int w = 0; w < static_cast<int>(blockDim.x >> 6); ++w) {
+        a1 += red[0][w];
+        a2 += red[1][w];
+      }
+      res[0] = sqrtf(a1) / (1e-5f + sqrtf(a2));
+    }
+  }
+  if (b >= bsz) return;
+  float H[M][M], y[M];
+#pragma unroll
+  for (int r = 0; r < M; ++r) {
+    y[r] = r == 0 ? 1.f : 0.f;
+#pragma unroll
+    for (int c = 0; c < M; ++c) {
+      float v;
+      if (r == 0 && c == 0) v = 0.f;
+      else if (r == 0 || c == 0) v = 1.f;
+      else v = g[r <= c ? pidx(r - 1, c - 1) : pidx(c - 1, r - 1)] + (r == c ? lam : 0.f);
+      H[r][c] = v;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < M; ++k) {
+    int piv = k;
+    float best = fabsf(H[k][k]);
+#pragma unroll
+    for (int r = k + 1; r < M; ++r) {
+      const float a = fabsf(H[r][k]);
+      if (a > best) {
+        best = a;
+        piv = r;
+      }
+    }
+#pragma unroll
+    for (int r = k + 1; r < M; ++r) {
+      if (r == piv) {
+#pragma unroll
+        for (int c = 0; c < M; ++c) {
+          const float t = H[k][c];
+          H[k][c] = H[r][c];
+          H[r][c] = t;
+        }
+        const float t = y[k];
+        y[k] = y[r];
+        y[r] = t;
+      }
+    }
+    const float inv = 1.f / H[k][k];
+#pragma unroll
+    for (int r = k + 1; r < M; ++r) {
+      const float f = H[r][k] * inv;
+#pragma unroll
+      for (int c = k + 1; c < M; ++c) H[r][c] = fmaf(-f, H[k][c], H[r][c]);
+      y[r] = fmaf(-f, y[k], y[r]);
+    }
+  }
+  float x[M];
+#pragma unroll
+  for (int k = M - 1; k >= 0; --k) {
+    float sacc = y[k];
+#pragma unroll
+    for (int c = k + 1; c < M; ++c) sacc = fmaf(-H[k][c], x[c], sacc);
+    x[k] = sacc / H[k][k];
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) alpha[static_cast<int64_t>(b) * N + i] = x[i + 1];
+}
+
+// DEQ adjoint fixed-point step, one pass: u_new = vjp + grad (model dtype, rounded like the
+// PyTorch add) and per-workgroup partial sums of (u_new - u)^2 in fp32 (the convergence test;
+// summed by gemm_splitk_reduce) — instead of an add, a subtract and a norm pass (7 tensor
+// passes -> 4).
+template <typename T>
+__global__ __launch_bounds__(kThreads) void adjoint_step_kernel(const T* __restrict__ vjp, const T* __restrict__ grad,
+                                                                const T* __restrict__ u, T* __restrict__ u_new,
+                                                                float* __restrict__ part, int64_t n8) {
+  float acc = 0.f;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kThreads;
+  for (int64_t v = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x; v < n8; v += stride) {
+    T a[8], g[8], o[8], r[8];
+    load8(vjp + v * 8, a);
+    load8(grad + v * 8, g);
+    load8(u + v * 8, o);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      r[j] = static_cast<T>(static_cast<float>(a[j]) + static_cast<float>(g[j]));
+      const float dlt = static_cast<float>(r[j]) - static_cast<float>(o[j]);
+      acc = fmaf(dlt, dlt, acc);
+    }
+    store8(u_new + v * 8, r);
+  }
+  __shared__ float red[kThreads / 64];
+  const float s = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < kThreads / 64; ++w) t += red[w];
+    part[blockIdx.x] = t;
+  }
+}
+
 void check_layout(const void* X, const void* F, int64_t d, int64_t row_stride, int64_t batch_stride, int n) {
   if (n < 1 || n > kMaxRows) throw std::runtime_error("anderson: need 1 <= n <= 8 (got " + std::to_string(n) + ")");
   if (d % 4 != 0 || row_stride % 4 != 0 || batch_stride % 4 != 0 || row_stride < d)
@@ -230,6 +376,56 @@ void anderson_mix(float* X, const float* F, const float* alpha, void* z, int z_d
     MIX_CASE(1) MIX_CASE(2) MIX_CASE(3) MIX_CASE(4) MIX_CASE(5) MIX_CASE(6) MIX_CASE(7) MIX_CASE(8)
   }
 #undef MIX_CASE
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+}
+
+void anderson_solve(const float* partials, int chunks, int64_t bsz, int n, int last, float lam, float* alpha,
+                    float* res, hipStream_t stream) {
+  if (n < 1 || n > kMaxRows) throw std::runtime_error("anderson_solve: need 1 <= n <= 8");
+  if (bsz < 1 || bsz > 1024) throw std::runtime_error("anderson_solve: need 1 <= bsz <= 1024 (one workgroup)");
+  if (chunks < 1 || last < 0 || last >= n) throw std::runtime_error("anderson_solve: bad chunks / last row");
+  const unsigned threads = static_cast<unsigned>((bsz + 63) / 64 * 64);
+#define SOLVE_CASE(NN) \
+  case NN: solve_kernel<NN><<<1, threads, 0, stream>>>(partials, chunks, static_cast<int>(bsz), last, lam, alpha, res); break;
+  switch (n) {
+    SOLVE_CASE(1) SOLVE_CASE(2) SOLVE_CASE(3) SOLVE_CASE(4) SOLVE_CASE(5) SOLVE_CASE(6) SOLVE_CASE(7) SOLVE_CASE(8)
+  }
+#undef SOLVE_CASE
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+}
+
+int adjoint_step_blocks(int64_t n) {
+  int64_t b = (n / 8 + kThreads * 4 - 1) / (kThreads * 4);  // >= 4 vectors per lane
+  if (b > 1024) b = 1024;
+  if (b < 1) b = 1;
+  return static_cast<int>(b);
+}
+
+void adjoint_step(const void* vjp, const void* grad, const void* u, void* u_new, float* partials, int blocks,
+                  int64_t n, int dtype, hipStream_t stream) {
+  if (n % 8 != 0 || blocks < 1) throw std::runtime_error("adjoint_step: need n % 8 == 0 and blocks >= 1");
+  if (((reinterpret_cast<uintptr_t>(vjp) | reinterpret_cast<uintptr_t>(grad) | reinterpret_cast<uintptr_t>(u) |
+        reinterpret_cast<uintptr_t>(u_new)) & 15u) != 0)
+    throw std::runtime_error("adjoint_step: tensors must be 16-byte aligned");
+  switch (dtype) {
+    case kBF16:
+      adjoint_step_kernel<bf16><<<blocks, kThreads, 0, stream>>>(static_cast<const bf16*>(vjp), static_cast<const bf16*>(grad),
+                                                                  static_cast<const bf16*>(u), static_cast<bf16*>(u_new),
+                                                                  partials, n / 8);
+      break;
+    case kF16:
+      adjoint_step_kernel<f16><<<blocks, kThreads, 0, stream>>>(static_cast<const f16*>(vjp), static_cast<const f16*>(grad),
+                                                                 static_cast<const f16*>(u), static_cast<f16*>(u_new),
+                                                                 partials, n / 8);
+      break;
+    case kF32:
+      adjoint_step_kernel<float><<<blocks, kThreads, 0, stream>>>(static_cast<const float*>(vjp), static_cast<const float*>(grad),
+                                                                   static_cast<const float*>(u), static_cast<float*>(u_new),
+                                                                   partials, n / 8);
+      break;
+    default:
+      throw std::runtime_error("adjoint_step: bf16 / fp16 / fp32 only");
+  }
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
 

@@ -103,6 +103,9 @@ __device__ __forceinline__ int swz(int row) {
 // slot ^ swz(row).
 // srow (plain operand, optional): the source row of piece j's rows, if not grow itself.
 // CONV: ph / pw / pbase = input row, column and pixel index of the tap-centre of piece j's row.
+// When C is a multiple of BK a K tile lies inside one tap (one division per tile); otherwise
+// (C % 8 == 0, e.g. the 48-channel DEQ cell) a tile straddles taps and every 16-B chunk finds its
+// own tap (a chunk never straddles: C % 8 == 0), with K = 9C's partial last tile reading zeros.
 template <int ROWS, int BK, bool CONV, bool PAD = false>
 __device__ __forceinline__ void issue_tile(bf16* lds_tile, const bf16* __restrict__ g, int64_t ld,
                                            int64_t rows, int64_t r0, int64_t k0, int64_t kend,
@@ -112,7 +115,8 @@ __device__ __forceinline__ void issue_tile(bf16* lds_tile, const bf16* __restric
   constexpr int PPW = ROWS * BK / 2048;  // 1 KiB pieces per wave
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int dr = 0, ds = 0, c0 = 0;
-  if (CONV) {
+  const bool tile_tap = !CONV || C % BK == 0;  // kernel-uniform
+  if (CONV && tile_tap) {
     const int tap = static_cast<int>(k0 / C);
     c0 = static_cast<int>(k0 - static_cast<int64_t>(tap) * C);
     dr = tap / 3 - 1;
@@ -126,9 +130,19 @@ __device__ __forceinline__ void issue_tile(bf16* lds_tile, const bf16* __restric
     const int64_t grow = r0 + row;
     const void* src = PAD ? static_cast<const void*>(g_pad_line) : static_cast<const void*>(g_zero_line);
     if (CONV) {
-      if (grow < rows && static_cast<unsigned>(ph[j] + dr) < static_cast<unsigned>(H) &&
-          static_cast<unsigned>(pw[j] + ds) < static_cast<unsigned>(W))
-        src = g + (static_cast<int64_t>(pbase[j]) + dr * W + ds) * C + c0 + q * 8;
+      int cdr = dr, cds = ds, cc = c0 + q * 8;
+      bool kin = true;
+      if (!tile_tap) {  // K = 9C < 2^31 (host-checked M < 2^31, C <= 8192)
+        const unsigned kq = static_cast<unsigned>(k0) + static_cast<unsigned>(q * 8);
+        const unsigned tap = kq / static_cast<unsigned>(C);
+        cc = static_cast<int>(kq - tap * static_cast<unsigned>(C));
+        cdr = static_cast<int>(tap / 3u) - 1;
+        cds = static_cast<int>(tap % 3u) - 1;
+        kin = static_cast<int64_t>(kq) < kend;
+      }
+      if (kin && grow < rows && static_cast<unsigned>(ph[j] + cdr) < static_cast<unsigned>(H) &&
+          static_cast<unsigned>(pw[j] + cds) < static_cast<unsigned>(W))
+        src = g + (static_cast<int64_t>(pbase[j]) + cdr * W + cds) * C + cc;
     } else {
       if (grow < rows && k0 + q * 8 < kend) src = g + (srow != nullptr ? srow[j] : grow) * ld + k0 + q * 8;
     }
@@ -786,7 +800,10 @@ bool gemm_glds_supported(const GemmProblem& g) {
          g.ldc % 8 == 0 && (g.res == nullptr || g.ldr % 8 == 0) &&
          (g.bnb_x == nullptr || (g.mode == 1 && g.ldc == g.N && g.bnb_mean != nullptr && g.bnb_inv != nullptr &&
                                  (g.bnb_rm == 0 || g.bnb_rm == 2 || (g.bnb_rm == 3 && g.bnb_mask != nullptr)))) &&
-         (g.conv_h == 0 || (g.conv_c % 32 == 0 && g.K == 9LL * g.conv_c && g.M < (1LL << 31))) &&
+         // implicit 3x3 conv: C % 32 == 0 (a K tile inside one tap), or C % 8 == 0 with per-chunk taps
+         // (no A affine then: its per-tile channel base assumes one tap per tile)
+         (g.conv_h == 0 || ((g.conv_c % 32 == 0 || (g.conv_c % 8 == 0 && g.a_scale == nullptr && g.conv_c <= 8192)) &&
+                            g.K == 9LL * g.conv_c && g.M < (1LL << 31))) &&
          (g.conv_s != 2 || (g.conv_h > 0 && g.M % (static_cast<int64_t>((g.conv_h + 1) / 2) * ((g.conv_w + 1) / 2)) == 0)) &&
          (g.a_sub_h == 0 || (g.conv_h == 0 && g.a_kmajor && g.a_sub_w > 0 && g.M < (1LL << 31) &&
                              g.M % (static_cast<int64_t>((g.a_sub_h + 1) / 2) * ((g.a_sub_w + 1) / 2)) == 0)) &&

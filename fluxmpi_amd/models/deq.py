@@ -20,6 +20,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops import anderson as AO
+from ..ops.fused_block import conv3x3, conv3x3_supported
 from ..ops.groupnorm import FusedGroupNorm, skip_param_grads
 
 # Convergence tests read a device value back LAG iterations late (FLUXMPI_DEQ_CHECK_LAG,
@@ -52,17 +54,6 @@ class LaggedFlags:
         i, ev = self.pending.pop(0)
         ev.synchronize()
         return i, float(self.buf[i])
-
-
-_EYE: dict = {}
-
-
-def _lam_eye(n, lam, device):
-    key = (n, float(lam), str(device))
-    t = _EYE.get(key)
-    if t is None:
-        t = _EYE[key] = lam * torch.eye(n, dtype=torch.float32, device=device)[None]
-    return t
 
 
 def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0, check_lag: int | None = None):
@@ -106,10 +97,6 @@ def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0, check_lag: i
 
     X[:, 0], Fv[:, 0] = flat(x0), fx(flat(x0))
     X[:, 1], Fv[:, 1] = Fv[:, 0], fx(Fv[:, 0])
-    H = torch.zeros(bsz, m + 1, m + 1, dtype=torch.float32, device=x0.device)
-    H[:, 0, 1:] = H[:, 1:, 0] = 1
-    y = torch.zeros(bsz, m + 1, 1, dtype=torch.float32, device=x0.device)
-    y[:, 0] = 1
     lag = (CHECK_LAG if check_lag is None else int(check_lag)) if x0.is_cuda else 0
     flags = LaggedFlags(lag, max_iter) if lag > 0 else None
     res = float("inf")
@@ -117,10 +104,10 @@ def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0, check_lag: i
     for k in range(2, max_iter):
         n = min(k, m)
         last = (k - 1) % m
-        # stored G = F - X: only the row(s) changed since the last Gram are recomputed
-        gram, fn2 = AO.gram(X, Fv, n, last, Gs, (0, 1) if k == 2 else (last,))
+        # stored G = F - X: only the row(s) changed since the last Gram are recomputed; on the GPU
+        # the residual and the (n+1)^2 solve are ONE launch after the Gram pass (AO.gram_solve)
+        alpha, res_t = AO.gram_solve(X, Fv, n, last, Gs, (0, 1) if k == 2 else (last,), lam, k > 2)
         if k > 2:  # residual of the iterate produced by the previous iteration
-            res_t = gram[:, last, last].sum().sqrt() / (1e-5 + fn2.sum().sqrt())
             if flags is None:
                 res = float(res_t)
                 if res < tol:
@@ -133,9 +120,6 @@ def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0, check_lag: i
                     # iterate hit[0] - 1 converged; the newest one (iteration k - 1) is at least as good
                     res, k, converged = hit[1], k - 1, True
                     break
-        H[:, 1:n + 1, 1:n + 1] = gram + _lam_eye(n, lam, x0.device)
-        # solve_ex without error checks: no host sync on the pivots' info
-        alpha = torch.linalg.solve_ex(H[:, :n + 1, :n + 1], y[:, :n + 1], check_errors=False)[0][:, 1:n + 1, 0]
         z = AO.mix(X, Fv, alpha, k % m, beta, dt)
         Fv[:, k % m] = fx(z)
     if not converged:
@@ -168,12 +152,15 @@ class DEQFixedPoint(nn.Module):
             lag = (CHECK_LAG if self.check_lag is None else int(self.check_lag)) if grad.is_cuda else 0
             flags = LaggedFlags(lag, self.bwd_iter) if lag > 0 else None
             thresh = self.bwd_tol * (grad.norm() + 1e-9)  # device scalar, computed once
+            thresh2 = thresh * thresh
             u = grad
             it = 0
             for it in range(self.bwd_iter):  # u = J^T u + grad
                 with skip_param_grads():  # VJPs w.r.t. z only: no GroupNorm dw/db reductions
-                    u_new = torch.autograd.grad(f0, z0, u, retain_graph=True)[0] + grad
-                done = (u_new - u).norm() <= thresh
+                    v = torch.autograd.grad(f0, z0, u, retain_graph=True)[0]
+                # u_new = v + grad and |u_new - u|^2 in one pass (ops/anderson.adjoint_step)
+                u_new, ss = AO.adjoint_step(v, grad, u)
+                done = ss <= thresh2
                 u = u_new
                 if flags is None:
                     if bool(done):
@@ -203,9 +190,16 @@ class ResidualCell(nn.Module):
         for c in (self.conv1, self.conv2):
             nn.init.normal_(c.weight, 0, 0.01)
 
+    def _conv(self, conv, t):
+        # bf16 channels_last on the GPU: the implicit-GEMM MFMA kernels (ops/fused_block.conv3x3,
+        # per-shape choice against MIOpen for the forward, input and weight gradients)
+        if conv3x3_supported(t, conv):
+            return conv3x3(t, conv.weight)
+        return conv(t)
+
     def forward(self, z, x):
-        y = self.n1(self.conv1(z), relu=True)
-        return self.n3(z, add=self.n2(self.conv2(y), add=x), relu=True)
+        y = self.n1(self._conv(self.conv1, z), relu=True)
+        return self.n3(z, add=self.n2(self._conv(self.conv2, y), add=x), relu=True)
 
 
 class DEQClassifier(nn.Module):

@@ -78,6 +78,42 @@ def gram(X: torch.Tensor, F: torch.Tensor, n: int, last: int, G: torch.Tensor | 
     return H, tot[:, 36]
 
 
+def gram_solve(X: torch.Tensor, F: torch.Tensor, n: int, last: int, G: torch.Tensor, fresh, lam: float,
+               want_res: bool):
+    """``(alpha [bsz, n], res)`` of one Anderson step: the Gram pass (:func:`gram`, stored ``G``)
+    then ONE launch (``anderson_solve``) for the chunk sums, the relative residual of row ``last``
+    (a 0-d device tensor, or None without ``want_res``) and the batched pivoted solve of
+    ``[[0, 1^T], [1, G G^T + lam I]] a = e_0``, ``alpha = a[1:]``. CPU tensors (and batches over
+    1024) use the PyTorch composition: :func:`gram`, ``torch.linalg.solve_ex``."""
+    bsz = X.shape[0]
+    if not (_native(X, F, n) and bsz <= 1024):
+        H, fn2 = gram(X, F, n, last, G, fresh)
+        res = (H[:, last, last].sum().sqrt() / (1e-5 + fn2.sum().sqrt())) if want_res else None
+        A = torch.zeros(bsz, n + 1, n + 1, dtype=torch.float32, device=X.device)
+        A[:, 0, 1:] = A[:, 1:, 0] = 1
+        A[:, 1:, 1:] = H + lam * torch.eye(n, dtype=torch.float32, device=X.device)
+        y = torch.zeros(bsz, n + 1, 1, dtype=torch.float32, device=X.device)
+        y[:, 0] = 1
+        return torch.linalg.solve_ex(A, y, check_errors=False)[0][:, 1:, 0], res
+    C = _ext.get(required=True)
+    d = X.shape[2]
+    chunks = C.anderson_gram_chunks(bsz, d)
+    part = torch.empty(bsz, chunks, 37, device=X.device, dtype=torch.float32)
+    if G.shape != X.shape or G.stride() != X.stride() or G.dtype != torch.float32 or G.data_ptr() % 16:
+        raise ValueError("anderson gram: G must match X's shape, strides and dtype")
+    mask = 0
+    for i in fresh:
+        mask |= 1 << int(i)
+    stream = _stream(X)
+    C.anderson_gram(X.data_ptr(), F.data_ptr(), G.data_ptr(), mask, part.data_ptr(), bsz, d, X.stride(1),
+                    X.stride(0), n, last, chunks, stream)
+    alpha = torch.empty(bsz, n, device=X.device, dtype=torch.float32)
+    res = torch.empty((), device=X.device, dtype=torch.float32) if want_res else None
+    C.anderson_solve(part.data_ptr(), chunks, bsz, n, last, float(lam), alpha.data_ptr(),
+                     res.data_ptr() if res is not None else 0, stream)
+    return alpha, res
+
+
 def mix(X: torch.Tensor, F: torch.Tensor, alpha: torch.Tensor, slot: int, beta: float = 1.0,
         z_dtype: torch.dtype | None = None):
     """``X[:, slot] = beta * alpha F[:, :n] + (1 - beta) * alpha X[:, :n]`` in place (n = alpha.shape[1]).
@@ -101,3 +137,28 @@ def mix(X: torch.Tensor, F: torch.Tensor, alpha: torch.Tensor, slot: int, beta: 
                    DTYPE_CODE[z_dtype] if z is not None else 7, bsz, d, X.stride(1), X.stride(0), n, slot, float(beta),
                    _stream(X))
     return z if z is not None else X[:, slot]
+
+
+def adjoint_step(vjp: torch.Tensor, grad: torch.Tensor, u: torch.Tensor):
+    """``(u_new, ss)``: ``u_new = vjp + grad`` and ``ss = |u_new - u|^2`` (0-d fp32 device tensor)
+    in one pass on the GPU (``adjoint_step`` + one partial-sum reduce); the DEQ adjoint solve's
+    update and convergence test. Other layouts / CPU: the PyTorch composition."""
+    same = (vjp.shape == grad.shape == u.shape and vjp.dtype == grad.dtype == u.dtype
+            and vjp.stride() == grad.stride() == u.stride())
+    dense = same and vjp.numel() % 8 == 0 and (vjp.is_contiguous() or (vjp.dim() == 4 and vjp.is_contiguous(
+        memory_format=torch.channels_last)))
+    if not (vjp.is_cuda and dense and vjp.dtype in DTYPE_CODE and vjp.numel() > 0
+            and (vjp.data_ptr() | grad.data_ptr() | u.data_ptr()) % 16 == 0):
+        u_new = vjp + grad
+        return u_new, (u_new - u).float().pow(2).sum()
+    C = _ext.get(required=True)
+    n = vjp.numel()
+    blocks = C.adjoint_step_blocks(n)
+    u_new = torch.empty_like(vjp)  # same strides (dense), so the flat element order matches
+    part = torch.empty(blocks, device=vjp.device, dtype=torch.float32)
+    ss = torch.empty((), device=vjp.device, dtype=torch.float32)
+    stream = _stream(vjp)
+    C.adjoint_step(vjp.data_ptr(), grad.data_ptr(), u.data_ptr(), u_new.data_ptr(), part.data_ptr(), blocks, n,
+                   DTYPE_CODE[vjp.dtype], stream)
+    C.gemm_splitk_reduce(part.data_ptr(), blocks, 1, ss.data_ptr(), DTYPE_CODE[torch.float32], stream)
+    return u_new, ss

@@ -34,6 +34,7 @@ from . import _ext
 from . import streams
 from .batchnorm import BNStatsLink, GradLink, SideGradLink, _dual_workspace, _link_workspace, _workspace, bn_counter  # noqa: F401 (links re-exported)
 from . import gemm as G
+from . import groupnorm as _GN
 from .gemm import conv1x1_dgrad, conv1x1_wgrad, conv3x3_dgrad, conv3x3_fwd, gemm, note_filter
 from .multi_tensor import DTYPE_CODE
 
@@ -562,7 +563,9 @@ class _Conv3x3(torch.autograd.Function):
         if not dy.is_contiguous(memory_format=torch.channels_last):
             dy = dy.contiguous(memory_format=torch.channels_last)
         dw = None
-        if ctx.needs_input_grad[1]:
+        # (inside groupnorm.skip_param_grads — the DEQ adjoint's VJPs w.r.t. activations only — the
+        # filter gradient is not wanted although needs_input_grad, fixed at forward time, says so)
+        if ctx.needs_input_grad[1] and not _GN._SKIP_PARAM_GRADS:
             dw = streams.run(lambda: wgrad_best(("3x3", tuple(x.shape), weight.shape[0]), {
                 "miopen": lambda: torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [1, 1], [1, 1], False,
                                                                       [0, 0], 1, [False, True, False])[1],
@@ -576,10 +579,40 @@ class _Conv3x3(torch.autograd.Function):
                 # the epilogue reduces the backward statistics of the BatchNorm that produced x
                 bn = (_nhwc2d(bl.x), bl.w32, bl.b32, bl.mean, bl.inv, bl.mask, bl.relu_mode)
                 stats = _link_workspace(x)
-            dx = conv3x3_dgrad(dy, weight, bn_bwd=bn, stats=stats)
+            if bn is None and not _dgrad_is_ours(dy, weight, x.shape):
+                dx = torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [1, 1], [1, 1], False, [0, 0],
+                                                         1, [True, False, False])[0]
+            else:
+                dx = conv3x3_dgrad(dy, weight, bn_bwd=bn, stats=stats)
             if bn is not None:
                 bl.ready = True
         return dx, dw, None, None, None
+
+
+_DGRAD_CHOICE: dict = {}
+
+
+def _dgrad_is_ours(dy, weight, x_shape) -> bool:
+    """Input gradient on our implicit GEMM, or MIOpen. Channel counts that are multiples of 32
+    (ResNet-50) always take ours; narrower ones (e.g. the 48-channel DEQ cell, whose K tiles
+    straddle filter taps) are measured once per shape, like the forward."""
+    if weight.shape[0] % 32 == 0:
+        return True
+    key = (tuple(x_shape), weight.shape[0])
+    hit = _DGRAD_CHOICE.get(key)
+    if hit is not None:
+        return hit
+    if torch.cuda.is_current_stream_capturing():
+        return True
+    with torch.no_grad():
+        d = dy.detach()
+        w = weight.detach()
+        xe = torch.empty(x_shape, device=dy.device, dtype=dy.dtype).contiguous(memory_format=torch.channels_last)
+        ours = _time_us(lambda: conv3x3_dgrad(d, w))
+        theirs = _time_us(lambda: torch.ops.aten.convolution_backward(d, xe, w, None, [1, 1], [1, 1], [1, 1], False,
+                                                                      [0, 0], 1, [True, False, False]))
+    _DGRAD_CHOICE[key] = ours <= theirs
+    return _DGRAD_CHOICE[key]
 
 
 class _Conv3x3S2(torch.autograd.Function):
@@ -658,7 +691,8 @@ def conv3x3_supported(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
     return (CONV3X3 in ("ours", "dgrad") and x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
             and conv.kernel_size == (3, 3) and conv.stride == (1, 1) and conv.padding == (1, 1)
             and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None
-            and conv.in_channels % 32 == 0 and conv.weight.dtype == torch.bfloat16)
+            and conv.in_channels % 8 == 0 and conv.out_channels % 8 == 0 and conv.weight.dtype == torch.bfloat16
+            and x.numel() // x.shape[1] < 2 ** 31)
 
 
 _FWD_CHOICE: dict = {}  # (N, C, H, W, Co) -> True: our forward (+ statistics epilogue) is faster

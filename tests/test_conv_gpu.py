@@ -172,3 +172,78 @@ def test_downsample_stride2_compact_grad(gpu_ext, closed, engine):
     (F.conv2d(xr, wd.float(), stride=2) * g2.float()).sum().backward()
     assert link.delivered == (not closed)
     assert _rel(x.grad, xr.grad) < 2e-2
+
+
+# channel counts that are not multiples of 32 (the 48-channel DEQ cell): K tiles straddle the
+# filter taps, every 16-B chunk of the implicit im2col finds its own tap, K = 9C has a partial
+# last tile (gemm_glds.hip issue_tile); LDS-DMA engines only
+NARROW = [(2, 48, 28, 28, 48), (3, 24, 7, 9, 40), (2, 8, 5, 5, 16), (1, 48, 6, 6, 96), (2, 40, 9, 7, 24)]
+
+
+@pytest.mark.parametrize("N,C,H,W,Co", NARROW)
+def test_conv3x3_narrow_channels(gpu_ext, N, C, H, W, Co, engine, monkeypatch):
+    from fluxmpi_amd.ops import gemm as G
+    from fluxmpi_amd.ops.gemm import SHARDS, conv3x3_dgrad, conv3x3_fwd, conv3x3_wgrad
+    if engine == 1:
+        pytest.skip("the register-staged kernel takes C % 32 == 0 only")
+    torch.manual_seed(7)
+    x = _nhwc(torch.randn(N, C, H, W, device="cuda").bfloat16())
+    w = _nhwc((torch.randn(Co, C, 3, 3, device="cuda") * 0.1).bfloat16())
+    stats = torch.zeros(SHARDS, 2, Co, device="cuda")
+    y = conv3x3_fwd(x, w, stats=stats)
+    ref = F.conv2d(x.float(), w.float(), padding=1)
+    assert y.shape == ref.shape and _rel(y, ref) < 1e-2
+    torch.testing.assert_close(stats[:, 0].sum(0), y.float().sum((0, 2, 3)), rtol=1e-3, atol=1e-2)
+    # input gradient: K = 9 * Co, the transposed filter [C][3][3][Co]
+    xr = x.float().requires_grad_()
+    dy = _nhwc(torch.randn(N, Co, H, W, device="cuda").bfloat16())
+    F.conv2d(xr, w.float(), padding=1).backward(dy.float())
+    dx = conv3x3_dgrad(dy, w)
+    assert dx.shape == x.shape and _rel(dx, xr.grad) < 1e-2
+    if engine in (2, 3):
+        monkeypatch.setattr(G, "WGRAD_VARIANT", engine - 1)
+        wr = torch.zeros(Co, C, 3, 3, device="cuda", requires_grad=True)
+        F.conv2d(x.float(), wr, padding=1).backward(dy.float())
+        for splits in (None, 1, 3):
+            dw = conv3x3_wgrad(dy, x, splits=splits)
+            assert _rel(dw, wr.grad) < 1e-2, splits
+
+
+def test_deq_cell_conv_autograd(gpu_ext, engine, monkeypatch):
+    """The DEQ cell's convolutions through ops.fused_block.conv3x3 (forward / input / filter
+    gradients, per-shape kernel choice) vs the same bf16 cell on MIOpen convolutions, and both
+    vs the fp32 PyTorch cell (bf16 rounding through three GroupNorms: a looser bound)."""
+    from fluxmpi_amd.models import deq as D
+    if engine != 2:
+        pytest.skip("one engine: the default dispatch")
+    torch.manual_seed(11)
+    cell = D.ResidualCell(48).cuda().to(memory_format=torch.channels_last)
+    ref = D.ResidualCell(48).cuda()
+    ref.load_state_dict(cell.state_dict())
+    for m in cell.modules():
+        if isinstance(m, torch.nn.Conv2d):
+            m.weight.data = m.weight.data.bfloat16().contiguous(memory_format=torch.channels_last)
+    ref.conv1.weight.data = cell.conv1.weight.data.float().contiguous()
+    ref.conv2.weight.data = cell.conv2.weight.data.float().contiguous()
+    z0 = _nhwc(torch.randn(4, 48, 28, 28, device="cuda").bfloat16())
+    x = _nhwc(torch.randn(4, 48, 28, 28, device="cuda").bfloat16())
+    g = torch.randn(4, 48, 28, 28, device="cuda")
+
+    def run(use_ours):
+        monkeypatch.setattr(D, "conv3x3_supported", D.conv3x3_supported if use_ours else (lambda *a: False))
+        cell.zero_grad()
+        z = z0.clone().requires_grad_()
+        y = cell(z, x)
+        (y.float() * g).sum().backward()
+        return y.detach(), z.grad, cell.conv1.weight.grad.clone(), cell.conv2.weight.grad.clone()
+
+    ours, miopen = run(True), run(False)
+    zr = z0.float().requires_grad_()
+    yr = ref(zr, x.float())
+    (yr * g).sum().backward()
+    # the cell amplifies bf16 rounding (GroupNorm over tiny conv outputs: ~2-4 % vs fp32 on either
+    # path): ours must be as close to the fp32 cell as the MIOpen path is
+    for name, a, b, r in zip(("y", "dz", "dw1", "dw2"), ours, miopen,
+                             (yr, zr.grad, ref.conv1.weight.grad, ref.conv2.weight.grad)):
+        e_ours, e_miopen = _rel(a, r), _rel(b, r)
+        assert e_ours < 6e-2 and e_ours <= 1.25 * e_miopen + 5e-3, (name, e_ours, e_miopen)

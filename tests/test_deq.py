@@ -99,6 +99,54 @@ def test_anderson_mix_gpu(n, beta, zdt):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("bsz", [3, 256, 1000])
+def test_anderson_gram_solve_gpu(n, bsz):
+    """One-launch residual + pivoted (n+1)^2 solve (anderson_solve) vs the fp64 composition."""
+    torch.manual_seed(20 + n)
+    m, d = max(n, 5), 4100
+    X = torch.randn(bsz, m, d, device="cuda")
+    Fv = X + 0.1 * torch.randn(bsz, m, d, device="cuda")
+    G = torch.zeros_like(X)
+    last = n - 1
+    lam = 1e-4
+    alpha, res = AO.gram_solve(X, Fv, n, last, G, tuple(range(n)), lam, True)
+    Hr, fr = _ref_gram(X, Fv, n, last)
+    A = torch.zeros(bsz, n + 1, n + 1, dtype=torch.float64, device="cuda")
+    A[:, 0, 1:] = A[:, 1:, 0] = 1
+    A[:, 1:, 1:] = Hr + lam * torch.eye(n, dtype=torch.float64, device="cuda")
+    y = torch.zeros(bsz, n + 1, 1, dtype=torch.float64, device="cuda")
+    y[:, 0] = 1
+    want = torch.linalg.solve(A, y)[:, 1:, 0]
+    assert alpha.shape == (bsz, n) and alpha.dtype == torch.float32
+    torch.testing.assert_close(alpha.double(), want, rtol=2e-3, atol=2e-3)
+    torch.testing.assert_close(alpha.double().sum(1), torch.ones(bsz, dtype=torch.float64, device="cuda"),
+                               rtol=1e-4, atol=1e-4)
+    res_ref = Hr[:, last, last].sum().sqrt() / (1e-5 + fr.sum().sqrt())
+    torch.testing.assert_close(res.double(), res_ref, rtol=1e-4, atol=1e-6)
+    # no residual requested: same alpha, res None
+    alpha2, res2 = AO.gram_solve(X, Fv, n, last, G, (last,), lam, False)
+    assert res2 is None
+    torch.testing.assert_close(alpha2, alpha, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("cl", [False, True])
+def test_adjoint_step_gpu(dtype, cl):
+    """u_new = vjp + grad and |u_new - u|^2 in one pass vs the PyTorch composition."""
+    torch.manual_seed(4)
+    mf = torch.channels_last if cl else torch.contiguous_format
+    v, g, u = (torch.randn(6, 48, 28, 28, device="cuda").to(dtype).contiguous(memory_format=mf) for _ in range(3))
+    u_new, ss = AO.adjoint_step(v, g, u)
+    want = v + g
+    assert u_new.stride() == want.stride()
+    torch.testing.assert_close(u_new, want, rtol=0, atol=0)
+    ref = (want.float() - u.float()).pow(2).sum()
+    torch.testing.assert_close(ss, ref, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.gpu
 def test_anderson_solver_gpu_matches_cpu():
     torch.manual_seed(3)
     d = 256
