@@ -27,6 +27,7 @@
 // LDS double buffer, next tile's global loads issued before the MFMAs of the
 // current one. Blocks are mapped XCD-aware (consecutive tiles of one XCD share
 // the A panel in its L2).
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -541,6 +542,76 @@ __global__ __launch_bounds__(kThreads) void splitk_reduce_kernel(float* __restri
   }
 }
 
+// One-launch column reduction of S (16 < S <= kColMaxS) partial rows (n % 4 == 0): a workgroup owns
+// kColV float4 columns (128 contiguous bytes of a row) x kColPh row phases; each lane sums rows
+// ph, ph + kColPh, ... (4 loads in flight), the phases meet in an LDS tree (fixed order:
+// deterministic). The G-ary tree below needs 2-3 launches for the few hundred to few thousand
+// partial rows of the colsum / LayerNorm / GELU-bias producers and the long-K weight gradients,
+// each mostly launch + memory latency (~5 us).
+constexpr int kColV = 8, kColPh = 32, kColMaxS = 2048;
+
+template <typename TO>
+__global__ __launch_bounds__(kColV * kColPh) void colreduce_kernel(const float* __restrict__ ws, int S, int64_t n,
+                                                                   TO* __restrict__ out) {
+  const int q = threadIdx.x % kColV, ph = threadIdx.x / kColV;
+  const int64_t c4 = static_cast<int64_t>(blockIdx.x) * kColV + q;
+  const int64_t n4 = n / 4;
+  const int64_t cc = c4 < n4 ? c4 : n4 - 1;  // clamped: loads unconditional, the store is masked
+  const float4* w4 = reinterpret_cast<const float4*>(ws);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  int s = ph;
+  for (; s + 3 * kColPh < S; s += 4 * kColPh) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = w4[static_cast<int64_t>(s + u * kColPh) * n4 + cc];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+    }
+  }
+  for (; s < S; s += kColPh) {
+    const float4 v = w4[static_cast<int64_t>(s) * n4 + cc];
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  __shared__ float4 red[kColPh][kColV];
+  red[ph][q] = acc;
+  __syncthreads();
+#pragma unroll
+  for (int w = kColPh / 2; w > 0; w >>= 1) {
+    if (ph < w) {
+      const float4 o = red[ph + w][q];
+      float4& m = red[ph][q];
+      m.x += o.x; m.y += o.y; m.z += o.z; m.w += o.w;
+    }
+    __syncthreads();
+  }
+  if (ph == 0 && c4 < n4) {
+    const float4 r = red[0][q];
+    TO* o = out + c4 * 4;
+    o[0] = static_cast<TO>(r.x);
+    o[1] = static_cast<TO>(r.y);
+    o[2] = static_cast<TO>(r.z);
+    o[3] = static_cast<TO>(r.w);
+  }
+}
+
+// n == 1 (a scalar's partials, e.g. the DEQ adjoint's |u_new - u|^2): one workgroup, fixed order
+template <typename TO>
+__global__ __launch_bounds__(kThreads) void sumall_kernel(const float* __restrict__ ws, int S, TO* __restrict__ out) {
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < S; i += kThreads) acc += ws[i];
+  __shared__ float red[kThreads / 64];
+  const float w = wave_sum_dpp(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = w;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < kThreads / 64; ++i) t += red[i];
+    out[0] = static_cast<TO>(t);
+  }
+}
+
 template <int BM, int BN, bool AK, bool BKM, int NBUF, bool EX = false, bool CONV = false>
 void launch(const GemmArgs& a0, int splits, hipStream_t s) {
   GemmArgs a = a0;
@@ -650,12 +721,38 @@ void gemm_bf16(const GemmProblem& g, hipStream_t stream) {
 #undef DISPATCH
 }
 
+// FLUXMPI_COLREDUCE=0: always the multi-launch tree (A/B)
+static bool colreduce_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("FLUXMPI_COLREDUCE");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+
 void gemm_splitk_reduce(const float* ws_c, int splits, int64_t n, void* out, int out_dtype, hipStream_t stream) {
   if (out_dtype != static_cast<int>(kF32) && out_dtype != static_cast<int>(kBF16))
     throw std::runtime_error("gemm_splitk_reduce: out dtype must be fp32 or bf16");
   float* ws = const_cast<float*>(ws_c);  // intermediate tree levels are written in place
   int64_t bx = (n / 4 + kThreads - 1) / kThreads;
   int cs = splits < 1 ? 1 : splits;
+  if (cs > kReduceGroup && n == 1 && colreduce_on()) {
+    if (out_dtype == static_cast<int>(kF32))
+      sumall_kernel<float><<<1, kThreads, 0, stream>>>(ws, cs, static_cast<float*>(out));
+    else
+      sumall_kernel<bf16><<<1, kThreads, 0, stream>>>(ws, cs, static_cast<bf16*>(out));
+    FLUXMPI_HIP_CHECK(hipGetLastError());
+    return;
+  }
+  if (cs > kReduceGroup && cs <= kColMaxS && n % 4 == 0 && n > 0 && colreduce_on()) {
+    const unsigned gx = static_cast<unsigned>((n / 4 + kColV - 1) / kColV);
+    if (out_dtype == static_cast<int>(kF32))
+      colreduce_kernel<float><<<gx, kColV * kColPh, 0, stream>>>(ws, cs, n, static_cast<float*>(out));
+    else
+      colreduce_kernel<bf16><<<gx, kColV * kColPh, 0, stream>>>(ws, cs, n, static_cast<bf16*>(out));
+    FLUXMPI_HIP_CHECK(hipGetLastError());
+    return;
+  }
   int64_t step = 1;
   while (cs > kReduceGroup) {
     const int groups = (cs + kReduceGroup - 1) / kReduceGroup;

@@ -22,7 +22,7 @@ import torch.nn.functional as F
 
 from ..ops import anderson as AO
 from ..ops.fused_block import conv3x3, conv3x3_supported
-from ..ops.groupnorm import FusedGroupNorm, skip_param_grads
+from ..ops.groupnorm import FusedGroupNorm, fp32_affine_cache, skip_param_grads
 
 # Convergence tests read a device value back LAG iterations late (FLUXMPI_DEQ_CHECK_LAG,
 # default 2 on the GPU): the host never drains the queue, so the GPU always has LAG
@@ -139,6 +139,11 @@ class DEQFixedPoint(nn.Module):
         self.last_bwd_iters = 0
 
     def forward(self, x):
+        # the cell's GroupNorm parameters cast to fp32 once for the ~30 calls below
+        with fp32_affine_cache(self.f):
+            return self._forward(x)
+
+    def _forward(self, x):
         with torch.no_grad():
             z, self.last_iters, _ = anderson(lambda z: self.f(z, x), torch.zeros_like(x), max_iter=self.max_iter,
                                              tol=self.tol, check_lag=self.check_lag)

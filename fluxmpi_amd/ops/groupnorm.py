@@ -36,6 +36,45 @@ class skip_param_grads:
         _SKIP_PARAM_GRADS = self._prev
 
 
+_AFFINE32: dict = {}
+
+
+class fp32_affine_cache:
+    """Within this context the fused GroupNorms of ``module`` read fp32 copies of their
+    low-precision (bf16) weight / bias made ONCE at entry, instead of casting them on every call.
+
+    The DEQ solver calls its cell ~30 times per forward with unchanged parameters: two cast
+    kernels per GroupNorm per call were ~190 launches per step. The copies are only valid while
+    the parameters do not change, i.e. within one forward pass."""
+
+    def __init__(self, module: nn.Module):
+        self.module = module
+
+    def __enter__(self):
+        global _AFFINE32
+        cache = dict(_AFFINE32)
+        for mod in self.module.modules():
+            if isinstance(mod, FusedGroupNorm):
+                for p in (mod.weight, mod.bias):
+                    if p is not None and p.dtype != torch.float32:
+                        cache[id(p)] = (p, p.detach().float().contiguous())
+        self._prev, _AFFINE32 = _AFFINE32, cache
+        return self
+
+    def __exit__(self, *exc):
+        global _AFFINE32
+        _AFFINE32 = self._prev
+
+
+def _f32(p):
+    if p is None:
+        return None
+    hit = _AFFINE32.get(id(p))
+    if hit is not None and hit[0] is p:
+        return hit[1]
+    return p.float().contiguous()
+
+
 def _stream(t):
     return torch.cuda.current_stream(t.device).cuda_stream
 
@@ -55,8 +94,7 @@ class _GroupNormFn(torch.autograd.Function):
         N, Ch, H, W = x.shape
         if add is not None:
             add = add.contiguous(memory_format=torch.channels_last)
-        w32 = weight.float().contiguous() if weight is not None else None
-        b32 = bias.float().contiguous() if bias is not None else None
+        w32, b32 = _f32(weight), _f32(bias)
         y = torch.empty_like(x, memory_format=torch.channels_last)
         h = torch.empty_like(y) if (add is not None or relu) else None
         mean = torch.empty(N, groups, device=x.device, dtype=torch.float32)

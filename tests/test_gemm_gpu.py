@@ -160,3 +160,4 @@ def test_conv3x3_stride2_fwd(gpu_ext, n, h, w, ci, co):
     yf = y.float().permute(0, 2, 3, 1).reshape(-1, co)
     torch.testing.assert_close(stats[:, 0].sum(0), yf.sum(0), rtol=1e-3, atol=1e-2)
     torch.testing.assert_close(stats[:, 1].sum(0), (yf * yf).sum(0), rtol=1e-3, atol=1e-2)
+

@@ -182,3 +182,25 @@ def test_optimisers_update_gpu_matches_cpu(gpu_ext):
     for k in ps:
         torch.testing.assert_close(psg[k].cpu(), ps[k], rtol=1e-5, atol=1e-6)
     assert stg["w"].state[2] == st["w"].state[2]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S", [1, 7, 16, 17, 100, 788, 2048, 2049, 5000])
+@pytest.mark.parametrize("n", [1, 4, 768, 1000, 3072, 6])
+@pytest.mark.parametrize("odt", [torch.float32, torch.bfloat16])
+def test_splitk_reduce(gpu_ext, S, n, odt):
+    """gemm_splitk_reduce over S partial rows (one launch, the column-reduction kernel for
+    16 < S <= 2048 and n % 4 == 0; the G-ary tree otherwise) vs torch.sum in fp64."""
+    from fluxmpi_amd.ops import _ext
+    from fluxmpi_amd.ops.multi_tensor import DTYPE_CODE
+    torch.manual_seed(S + n)
+    ws = torch.randn(S, n, device="cuda")
+    want = ws.double().sum(0)
+    out = torch.empty(n, device="cuda", dtype=odt)
+    scratch = ws.clone()  # the tree path reduces in place
+    _ext.get(required=True).gemm_splitk_reduce(scratch.data_ptr(), S, n, out.data_ptr(), DTYPE_CODE[odt],
+                                               torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    tol = 1e-4 * S ** 0.5 if odt == torch.float32 else 1e-2 * max(1.0, float(want.abs().max()))
+    torch.testing.assert_close(out.double(), want.to(odt).double() if odt != torch.float32 else want,
+                               rtol=1e-3 if odt == torch.float32 else 1e-2, atol=tol)
