@@ -158,6 +158,10 @@ class DEQFixedPoint(nn.Module):
             flags = LaggedFlags(lag, self.bwd_iter) if lag > 0 else None
             thresh = self.bwd_tol * (grad.norm() + 1e-9)  # device scalar, computed once
             thresh2 = thresh * thresh
+            if z0.dim() == 4 and z0.is_contiguous(memory_format=torch.channels_last):
+                # the incoming gradient (from the BatchNorm after the DEQ) may be NCHW: one layout
+                # copy here instead of one per iteration in the cell's NHWC GroupNorm backward
+                grad = grad.contiguous(memory_format=torch.channels_last)
             u = grad
             it = 0
             for it in range(self.bwd_iter):  # u = J^T u + grad
