@@ -57,6 +57,12 @@ def parse():
                          "shared GPU): runs the N>1 code path on a 1-GPU box; no throughput claim")
     ap.add_argument("--graph", action="store_true", help="capture the step in a HIP graph")
     ap.add_argument("--miopen-find", type=int, default=int(os.environ.get("BENCH_MIOPEN_FIND", "1")))
+    ap.add_argument("--choices", default=os.environ.get("BENCH_CHOICES", "measure"), choices=["measure", "shipped"],
+                    help="measure (default): per-shape kernel choices (ours vs MIOpen, tile configs) timed at the "
+                         "first step; shipped: read tuning/kernel_choices/<model>_bs<batch>.jsonl (no first-step "
+                         "timing, no run-to-run flips; measured 0.8%% slower than a fresh measurement on one box, "
+                         "profiles/r4i_bench_choices_ab.jsonl)")
+    ap.add_argument("--dump-choices", default="", help="write the per-shape kernel choices in use to this file")
     ap.add_argument("--tunableop", default=os.environ.get("BENCH_TUNABLEOP", "auto"), choices=["auto", "off"],
                     help="auto: use the shipped hipBLASLt/rocBLAS GEMM selections (tuning/tunableop/<model>.csv)")
     return ap.parse_args()
@@ -96,6 +102,15 @@ def main():
 
         install_tuned_db(rank=int(os.environ.get("LOCAL_RANK", "0")))
     torch.backends.cudnn.benchmark = bool(args.miopen_find)
+    # shipped per-shape kernel choices (recorded on MI355X; the analogue of the MIOpen find-db):
+    # no first-step measurement, no run-to-run flips of shapes where both kernels are within noise
+    choices = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuning", "kernel_choices",
+                           f"{args.model}_bs{args.batch}.jsonl")
+    use_choices = args.choices == "shipped" and os.path.exists(choices) and "FLUXMPI_KERNEL_CHOICES" not in os.environ
+    if use_choices:
+        from fluxmpi_amd.ops import fused_block
+
+        fused_block.load_choices(choices)
     rank, world = FluxMPI.local_rank(), FluxMPI.total_workers()
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but world size {world}", file=sys.stderr)
@@ -167,6 +182,11 @@ def main():
         exposed = e or 0.0
         if world > 1:
             exposed = FluxMPI.allreduce(torch.tensor([exposed], dtype=torch.float64), max).item()
+    if args.dump_choices and rank == 0:
+        from fluxmpi_amd.ops import fused_block
+
+        with open(args.dump_choices, "w") as f:
+            f.write("\n".join(fused_block.dump_choices()) + "\n")
     cs = ddp.comm_summary()
     if rank == 0:
         ips = world * B * args.steps / dt_max
@@ -181,7 +201,8 @@ def main():
                        "image_size": args.image, "parallelism": f"dp{world}", "optimizer": args.optimizer,
                        "conv": args.conv, "norm": args.norm, "memory_format": "contiguous" if memfmt is torch.contiguous_format else "channels_last", "backend": FluxMPI.backend_name(),
                        "miopen_find": bool(args.miopen_find), "hip_graph": bool(args.graph),
-                       "tunableop": use_tunableop, "loss": round(lval, 4),
+                       "tunableop": use_tunableop, "kernel_choices": "shipped" if use_choices else "measured",
+                       "loss": round(lval, 4),
                        # what the data-parallel layer actually did: at N=1 nothing is communicated
                        # (overlap false, comm "none") unless --force-comm
                        **cs, "exposed_comm_ms": None if exposed is None else round(exposed, 3),

@@ -870,3 +870,46 @@ def supported(x: torch.Tensor, *channels: int) -> bool:
     """Shapes the fused path handles (bf16 NHWC on GPU, channels % 32 == 0, <= 2048)."""
     return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
             and all(c % 32 == 0 and 32 <= c <= 2048 for c in channels))
+
+
+# ---- shipped per-shape kernel choices (the analogue of MIOpen's find-db) -----------------------
+_CHOICE_TABLES = {"fwd1x1_ours": "_FWD1_CHOICE", "fwd3x3_ours": "_FWD_CHOICE", "wgrad": "_WG_CHOICE",
+                  "fwd_ds_ours": "_DS_CHOICE", "fwd3x3s2_ours": "_S2_CHOICE", "fwd3x3_engine": "_FWD_ENGINE",
+                  "dgrad3x3_ours": "_DGRAD_CHOICE"}
+
+
+def dump_choices():
+    """The per-shape choices measured so far, as JSON-lines records (``scripts/show_choices.py``)."""
+    import json
+    g = globals()
+    out = []
+    for kind, name in _CHOICE_TABLES.items():
+        for k, v in g[name].items():
+            out.append(json.dumps({"kind": kind, "key": str(k), "choice": str(v)}))
+    return out
+
+
+def load_choices(path: str) -> int:
+    """Pre-populate the per-shape kernel choices from a JSON-lines record (``dump_choices``):
+    those shapes skip the first-step measurement (no autotune time, no run-to-run flips of
+    marginal shapes); others are still measured. Returns the number of entries loaded."""
+    import ast
+    import json
+    g = globals()
+    n = 0
+    with open(path) as f:
+        for line in f:
+            line = line.strip()
+            if not line:
+                continue
+            rec = json.loads(line)
+            name = _CHOICE_TABLES.get(rec["kind"])
+            if name is None:
+                continue
+            g[name][ast.literal_eval(rec["key"])] = ast.literal_eval(rec["choice"])
+            n += 1
+    return n
+
+
+if os.environ.get("FLUXMPI_KERNEL_CHOICES"):
+    load_choices(os.environ["FLUXMPI_KERNEL_CHOICES"])

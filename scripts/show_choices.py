@@ -1,7 +1,6 @@
 #!/usr/bin/env python
 """Print the per-shape kernel choices the hybrid ResNet-50 makes at its first step (our kernels
 vs MIOpen: 1x1 forwards, 3x3 forwards, weight gradients), after two bench-config steps."""
-import json
 import os
 import sys
 
@@ -28,11 +27,8 @@ def main():
     for _ in range(2):
         F.cross_entropy(model(x).float(), y).backward()
     torch.cuda.synchronize()
-    for name, d in (("fwd1x1_ours", fb._FWD1_CHOICE), ("fwd3x3_ours", fb._FWD_CHOICE), ("wgrad", fb._WG_CHOICE),
-                    ("fwd_ds_ours", fb._DS_CHOICE), ("fwd3x3s2_ours", fb._S2_CHOICE),
-                    ("fwd3x3_engine", fb._FWD_ENGINE)):
-        for k, v in d.items():
-            print(json.dumps({"kind": name, "key": str(k), "choice": str(v)}))
+    for line in fb.dump_choices():  # the format fb.load_choices / bench.py --choices read
+        print(line)
 
 
 if __name__ == "__main__":

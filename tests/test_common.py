@@ -41,3 +41,30 @@ def test_single_process_world(capsys):
     assert FluxMPI.total_workers() == 1 and FluxMPI.local_rank() == 0
     FluxMPI.fluxmpi_println("hello ", 1)
     assert capsys.readouterr().out.endswith("hello 1\n")
+
+
+def test_kernel_choice_table_roundtrip(tmp_path):
+    """The shipped per-shape kernel-choice table (tuning/kernel_choices) loads into the autotune
+    dictionaries and dumps back to the same records."""
+    import json
+    import os
+    from fluxmpi_amd.ops import fused_block as fb
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    path = os.path.join(root, "tuning", "kernel_choices", "resnet50_bs256.jsonl")
+    saved = {name: dict(getattr(fb, name)) for name in fb._CHOICE_TABLES.values()}
+    try:
+        for name in fb._CHOICE_TABLES.values():
+            getattr(fb, name).clear()
+        n = fb.load_choices(path)
+        assert n == sum(1 for line in open(path) if line.strip())
+        assert fb._WG_CHOICE[("1x1", (256, 512, 28, 28), 256)] == ("w256", None)
+        assert fb._FWD_ENGINE[((256, 64, 56, 56), 64)] == 7
+        out = tmp_path / "c.jsonl"
+        out.write_text("\n".join(fb.dump_choices()) + "\n")
+        want = sorted(json.dumps(json.loads(line), sort_keys=True) for line in open(path) if line.strip())
+        got = sorted(json.dumps(json.loads(line), sort_keys=True) for line in open(out) if line.strip())
+        assert got == want
+    finally:
+        for name, d in saved.items():
+            getattr(fb, name).clear()
+            getattr(fb, name).update(d)
