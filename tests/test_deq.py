@@ -50,6 +50,29 @@ def test_anderson_ops_fallback_cpu():
     assert z.dtype == torch.bfloat16
 
 
+def test_gram_solve_and_adjoint_step_fallback_cpu():
+    """The CPU compositions behind AO.gram_solve / AO.adjoint_step (the GPU kernels' oracles)."""
+    torch.manual_seed(2)
+    bsz, m, d, n = 4, 5, 24, 3
+    X = torch.randn(bsz, m, d)
+    Fv = X + 0.1 * torch.randn(bsz, m, d)
+    G = torch.zeros_like(X)
+    alpha, res = AO.gram_solve(X, Fv, n, n - 1, G, tuple(range(n)), 1e-4, True)
+    Hr, fr = _ref_gram(X, Fv, n, n - 1)
+    A = torch.zeros(bsz, n + 1, n + 1, dtype=torch.float64)
+    A[:, 0, 1:] = A[:, 1:, 0] = 1
+    A[:, 1:, 1:] = Hr + 1e-4 * torch.eye(n, dtype=torch.float64)
+    y = torch.zeros(bsz, n + 1, 1, dtype=torch.float64)
+    y[:, 0] = 1
+    torch.testing.assert_close(alpha.double(), torch.linalg.solve(A, y)[:, 1:, 0], rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(res.double(), Hr[:, n - 1, n - 1].sum().sqrt() / (1e-5 + fr.sum().sqrt()),
+                               rtol=1e-4, atol=1e-6)
+    v, g, u = torch.randn(3, 2, 8, 4, 4).unbind(0)
+    u_new, ss = AO.adjoint_step(v, g, u)
+    torch.testing.assert_close(u_new, v + g)
+    torch.testing.assert_close(ss, (v + g - u).pow(2).sum())
+
+
 def test_deq_train_step_cpu():
     torch.manual_seed(2)
     model = deq_mnist(max_iter=12, bwd_iter=12)
