@@ -22,7 +22,9 @@ import torch.nn.functional as F
 
 from ..ops import anderson as AO
 from ..ops.fused_block import conv3x3, conv3x3_supported
+from ..ops.batchnorm import GradLink
 from ..ops.groupnorm import FusedGroupNorm, fp32_affine_cache, skip_param_grads
+from ..ops.groupnorm import native_ok as gn_native_ok
 
 # Convergence tests read a device value back LAG iterations late (FLUXMPI_DEQ_CHECK_LAG,
 # default 2 on the GPU): the host never drains the queue, so the GPU always has LAG
@@ -199,16 +201,22 @@ class ResidualCell(nn.Module):
         for c in (self.conv1, self.conv2):
             nn.init.normal_(c.weight, 0, 0.01)
 
-    def _conv(self, conv, t):
+    def _conv(self, conv, t, link=None):
         # bf16 channels_last on the GPU: the implicit-GEMM MFMA kernels (ops/fused_block.conv3x3,
         # per-shape choice against MIOpen for the forward, input and weight gradients)
         if conv3x3_supported(t, conv):
-            return conv3x3(t, conv.weight)
+            return conv3x3(t, conv.weight, gradlink=link)
         return conv(t)
 
     def forward(self, z, x):
-        y = self.n1(self._conv(self.conv1, z), relu=True)
-        return self.n3(z, add=self.n2(self._conv(self.conv2, y), add=x), relu=True)
+        # z feeds conv1 and n3's add: n3's backward hands its gradient of z to conv1's dgrad
+        # epilogue (GradLink) instead of autograd summing the two with an add kernel
+        link = None
+        if torch.is_grad_enabled() and z.requires_grad and conv3x3_supported(z, self.conv1) and \
+                gn_native_ok(z, self.n3.num_groups):
+            link = GradLink()
+        y = self.n1(self._conv(self.conv1, z, link), relu=True)
+        return self.n3(z, add=self.n2(self._conv(self.conv2, y), add=x), relu=True, link=link)
 
 
 class DEQClassifier(nn.Module):

@@ -545,9 +545,10 @@ class _Conv3x3(torch.autograd.Function):
     MFMA kernel; weight gradient on MIOpen."""
 
     @staticmethod
-    def forward(ctx, x, weight, fwd_ours, with_stats, bnlink=None):
+    def forward(ctx, x, weight, fwd_ours, with_stats, bnlink=None, gradlink=None):
         x = x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
         ctx.bnlink = bnlink
+        ctx.gradlink = gradlink
         note_filter(weight)
         if fwd_ours:
             y = conv3x3_fwd(x, weight, stats=_workspace(x) if with_stats else None,
@@ -579,14 +580,23 @@ class _Conv3x3(torch.autograd.Function):
                 # the epilogue reduces the backward statistics of the BatchNorm that produced x
                 bn = (_nhwc2d(bl.x), bl.w32, bl.b32, bl.mean, bl.inv, bl.mask, bl.relu_mode)
                 stats = _link_workspace(x)
+            # gradlink: x's other consumer deposited its gradient of x (GroupNorm / BatchNorm backward
+            # ran first: autograd orders it by data dependency); added in the dgrad epilogue
+            res = ctx.gradlink.take() if ctx.gradlink is not None else None
             if bn is None and not _dgrad_is_ours(dy, weight, x.shape):
                 dx = torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [1, 1], [1, 1], False, [0, 0],
                                                          1, [True, False, False])[0]
+                if res is not None:
+                    dx = dx + res
+            elif res is not None and bn is not None:
+                dx = conv3x3_dgrad(dy, weight, bn_bwd=bn, stats=stats) + res
             else:
-                dx = conv3x3_dgrad(dy, weight, bn_bwd=bn, stats=stats)
+                dx = conv3x3_dgrad(dy, weight, bn_bwd=bn, stats=stats, residual=res)
             if bn is not None:
                 bl.ready = True
-        return dx, dw, None, None, None
+        elif ctx.gradlink is not None:
+            ctx.gradlink.grad = None
+        return dx, dw, None, None, None, None
 
 
 _DGRAD_CHOICE: dict = {}
@@ -800,13 +810,14 @@ def conv3x3_forward_is_ours(x, weight) -> bool:
     return choice
 
 
-def conv3x3(x, weight, with_stats=False, bnlink=None):
+def conv3x3(x, weight, with_stats=False, bnlink=None, gradlink=None):
     """Returns the conv output. If the forward runs on our kernel (:func:`conv3x3_forward_is_ours`)
     and ``with_stats``, its per-channel sum / sumsq are pending in the BatchNorm workspace
     (consume them with ``bn_from_stats(..., stats_ready=True)``); check with
-    ``conv3x3_forward_is_ours`` first."""
+    ``conv3x3_forward_is_ours`` first. ``gradlink`` (:class:`GradLink`): x's other consumer
+    deposits its gradient of x there; the input gradient adds it in the dgrad epilogue."""
     ours = conv3x3_forward_is_ours(x, weight)
-    return _Conv3x3.apply(x, weight, ours, with_stats and ours, bnlink)
+    return _Conv3x3.apply(x, weight, ours, with_stats and ours, bnlink, gradlink)
 
 
 def masked_links_ok() -> bool:

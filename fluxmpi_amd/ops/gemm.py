@@ -207,11 +207,12 @@ def conv3x3_s2_fwd(x: torch.Tensor, w: torch.Tensor, stats: torch.Tensor | None 
 
 
 def conv3x3_dgrad(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None, bn_bwd=None,
-                  stats: torch.Tensor | None = None) -> torch.Tensor:
+                  stats: torch.Tensor | None = None, residual: torch.Tensor | None = None) -> torch.Tensor:
     """Input gradient of the 3x3/s1/p1 convolution: the same implicit GEMM over dY with the
     filter transposed and flipped (``WT[ci][r][s][co] = W[co][ci][2-r][2-s]``). ``bn_bwd`` /
     ``stats``: the epilogue accumulates the backward reductions of the BatchNorm that produced
-    the convolution's input (see :func:`gemm`)."""
+    the convolution's input (see :func:`gemm`). ``residual`` (NHWC, the input's shape): added in the
+    epilogue — the other summand of the input's gradient when the input has a second consumer."""
     n, co, h, wd = dy.shape
     ci = w.shape[1]
     dys = dy if dy.is_contiguous(memory_format=torch.channels_last) else dy.contiguous(
@@ -223,13 +224,17 @@ def conv3x3_dgrad(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = 
     dx = out if out is not None else torch.empty(n, h, wd, ci, device=dy.device, dtype=dy.dtype).permute(0, 3, 1, 2)
     if bn_bwd is not None:
         assert stats is not None and bn_bwd[0].shape == (n * h * wd, ci) and ENGINE != 1
-    elif ENGINE != 1 and dy.dtype == torch.bfloat16 and halo_ok(n, h, wd, co, ci) and \
+    elif residual is None and ENGINE != 1 and dy.dtype == torch.bfloat16 and halo_ok(n, h, wd, co, ci) and \
             dx.is_contiguous(memory_format=torch.channels_last):
         _ext.get(required=True).conv3x3_halo(dys.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, n, h, wd, co, ci,
                                              _stream(dy))
         return dx
+    r2 = None
+    if residual is not None:
+        assert residual.shape == dx.shape and residual.dtype == dy.dtype and bn_bwd is None
+        r2 = residual.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(-1, ci)
     gemm(dys, wt, dx, M=n * h * wd, N=ci, K=9 * co, lda=co, ldb=9 * co, ldc=ci, conv=(h, wd, co),
-         mode=1 if bn_bwd is not None else 0, stats=stats, bn_bwd=bn_bwd)
+         mode=1 if bn_bwd is not None else 0, stats=stats, bn_bwd=bn_bwd, residual=r2)
     return dx
 
 

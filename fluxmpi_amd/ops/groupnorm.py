@@ -89,7 +89,7 @@ def supported(x: torch.Tensor, groups: int) -> bool:
 
 class _GroupNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, add, weight, bias, groups, eps, relu):
+    def forward(ctx, x, add, weight, bias, groups, eps, relu, link=None):
         C = _ext.get(required=True)
         N, Ch, H, W = x.shape
         if add is not None:
@@ -106,6 +106,7 @@ class _GroupNormFn(torch.autograd.Function):
         ctx.save_for_backward(h if h is not None else x, mean, rstd, w32)
         ctx.cfg = (groups, bool(relu), add is not None,
                    weight.dtype if weight is not None else None, bias.dtype if bias is not None else None)
+        ctx.link = link
         return y
 
     @staticmethod
@@ -123,13 +124,28 @@ class _GroupNormFn(torch.autograd.Function):
         want = not _SKIP_PARAM_GRADS
         dw = part[:, 0].sum(0).to(wd) if want and wd is not None and ctx.needs_input_grad[2] else None
         db = part[:, 1].sum(0).to(bd) if want and bd is not None and ctx.needs_input_grad[3] else None
-        return dh, (dh if has_add else None), dw, db, None, None, None
+        dx = dh
+        if ctx.link is not None and ctx.needs_input_grad[0]:
+            # x's other consumer (a convolution holding the same link) adds dh in its dgrad epilogue
+            ctx.link.grad = dh
+            dx = None
+        return dx, (dh if has_add else None), dw, db, None, None, None, None
 
 
-def group_norm(x, groups, weight=None, bias=None, eps=1e-5, add=None, relu=False):
-    """``F.group_norm(relu(x + add), groups, weight, bias, eps)`` with the add / ReLU optional."""
-    if supported(x, groups) and (add is None or (add.shape == x.shape and add.dtype == x.dtype)):
-        return _GroupNormFn.apply(x, add, weight, bias, groups, eps, relu)
+def native_ok(x, groups, add=None) -> bool:
+    """This call takes the fused kernels (and so honours a ``link``)."""
+    return supported(x, groups) and (add is None or (add.shape == x.shape and add.dtype == x.dtype))
+
+
+def group_norm(x, groups, weight=None, bias=None, eps=1e-5, add=None, relu=False, link=None):
+    """``F.group_norm(relu(x + add), groups, weight, bias, eps)`` with the add / ReLU optional.
+
+    ``link`` (:class:`~fluxmpi_amd.ops.batchnorm.GradLink`, fused path only — check
+    :func:`native_ok`): x's gradient is deposited there for x's other consumer instead of being
+    returned to autograd (which would add the two gradients with a separate kernel)."""
+    if native_ok(x, groups, add):
+        return _GroupNormFn.apply(x, add, weight, bias, groups, eps, relu, link)
+    assert link is None, "group_norm: a GradLink needs the fused path (native_ok)"
     h = x + add if add is not None else x
     if relu:
         h = F.relu(h)
@@ -137,5 +153,5 @@ def group_norm(x, groups, weight=None, bias=None, eps=1e-5, add=None, relu=False
 
 
 class FusedGroupNorm(nn.GroupNorm):
-    def forward(self, x, add=None, relu=False):  # noqa: D102
-        return group_norm(x, self.num_groups, self.weight, self.bias, self.eps, add, relu)
+    def forward(self, x, add=None, relu=False, link=None):  # noqa: D102
+        return group_norm(x, self.num_groups, self.weight, self.bias, self.eps, add, relu, link)

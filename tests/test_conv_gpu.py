@@ -200,6 +200,10 @@ def test_conv3x3_narrow_channels(gpu_ext, N, C, H, W, Co, engine, monkeypatch):
     F.conv2d(xr, w.float(), padding=1).backward(dy.float())
     dx = conv3x3_dgrad(dy, w)
     assert dx.shape == x.shape and _rel(dx, xr.grad) < 1e-2
+    # residual epilogue (the GradLink hand-off: x's other consumer's gradient added in place)
+    r = _nhwc(torch.randn(N, C, H, W, device="cuda").bfloat16())
+    dxr = conv3x3_dgrad(dy, w, residual=r)
+    assert _rel(dxr, xr.grad + r.float()) < 1e-2
     if engine in (2, 3):
         monkeypatch.setattr(G, "WGRAD_VARIANT", engine - 1)
         wr = torch.zeros(Co, C, 3, 3, device="cuda", requires_grad=True)
