@@ -770,23 +770,47 @@ __global__ __launch_bounds__(kThreads) void xpose_taps_kernel(XposeArgs a) {
   const bf16* __restrict__ src = reinterpret_cast<const bf16*>(a.src[t]);
   bf16* __restrict__ dst = reinterpret_cast<bf16*>(a.dst[t]);
   const int r = threadIdx.x / 4, c0 = (threadIdx.x % 4) * 16;
+  // full 16-element runs in range with 16-B aligned rows (ci, co % 8 == 0): two 16-B loads /
+  // stores per lane instead of 16 predicated 2-byte ones (the scalar form ran ~47 us per
+  // ResNet-50 step's batch of 3x3 filters)
   {  // read rows co = bco*64 + r, 16 ci each, of source tap T-1-tap
     const int oc = bco * 64 + r;
+    const int ic0 = bci * 64 + c0;
+    const bf16* sp = src + (static_cast<int64_t>(oc) * T + (T - 1 - tap)) * ci + ic0;
+    if (oc < co && ic0 + 16 <= ci && ci % 8 == 0) {
+      bf16 v0[8], v1[8];
+      load8(sp, v0);
+      load8(sp + 8, v1);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int ic = bci * 64 + c0 + j;
-      tile[r][c0 + j] = (oc < co && ic < ci) ? src[(static_cast<int64_t>(oc) * T + (T - 1 - tap)) * ci + ic]
-                                            : static_cast<bf16>(0.f);
+      for (int j = 0; j < 8; ++j) {
+        tile[r][c0 + j] = v0[j];
+        tile[r][c0 + 8 + j] = v1[j];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        tile[r][c0 + j] = (oc < co && ic0 + j < ci) ? sp[j] : static_cast<bf16>(0.f);
     }
   }
   __syncthreads();
   {  // write rows ci = bci*64 + r, 16 co each, of destination tap `tap`
     const int ic = bci * 64 + r;
+    const int oc0 = bco * 64 + c0;
     if (ic < ci) {
+      bf16* dp = dst + (static_cast<int64_t>(ic) * T + tap) * co + oc0;
+      if (oc0 + 16 <= co && co % 8 == 0) {
+        bf16 v0[8], v1[8];
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int oc = bco * 64 + c0 + j;
-        if (oc < co) dst[(static_cast<int64_t>(ic) * T + tap) * co + oc] = tile[c0 + j][r];
+        for (int j = 0; j < 8; ++j) {
+          v0[j] = tile[c0 + j][r];
+          v1[j] = tile[c0 + 8 + j][r];
+        }
+        store8(dp, v0);
+        store8(dp + 8, v1);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (oc0 + j < co) dp[j] = tile[c0 + j][r];
       }
     }
   }
