@@ -140,10 +140,11 @@ void layernorm_fwd(const void* x, const void* residual, void* h, void* y, const 
                    float* rstd, int64_t rows, int64_t D, float eps, int dtype, int wdtype, hipStream_t stream);
 // backward: dx = LN backward of dy [+ dh_ext]; per-workgroup [2][D] fp32 partials of (dw, db)
 // stored into `partials` (capacity max_blocks x 2D); returns the number of partial rows written
-// (sum them with gemm_splitk_reduce).
+// (sum them with gemm_splitk_reduce). colsum (dh_ext required): [3][D] rows, the third the
+// column sums of dx.
 int layernorm_bwd(const void* dy, const void* x, const void* dh_ext, const float* mean, const float* rstd,
                   const void* w, void* dx, float* partials, int max_blocks, int64_t rows, int64_t D, int dtype,
-                  int wdtype, hipStream_t stream);
+                  int wdtype, bool colsum, hipStream_t stream);
 
 // ---- MFMA bf16 GEMM with BatchNorm fusions (1x1 convolutions) --------------------
 // C[M,N] = A[M,K] * B[N,K]^T. a_kmajor: A stored [M][lda] (K contiguous), else [K][lda]

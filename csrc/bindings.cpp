@@ -267,12 +267,12 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("layernorm_bwd", [](uintptr_t dy, uintptr_t x, uintptr_t dh, uintptr_t mean, uintptr_t rstd, uintptr_t w,
                             uintptr_t dx, uintptr_t part, int max_blocks, int64_t rows, int64_t D, int dtype,
-                            int wdtype, uintptr_t stream) {
+                            int wdtype, uintptr_t stream, bool colsum) {
     return layernorm_bwd(reinterpret_cast<const void*>(dy), reinterpret_cast<const void*>(x),
                          reinterpret_cast<const void*>(dh), reinterpret_cast<const float*>(mean),
                          reinterpret_cast<const float*>(rstd), reinterpret_cast<const void*>(w),
                          reinterpret_cast<void*>(dx), reinterpret_cast<float*>(part), max_blocks, rows, D, dtype,
-                         wdtype, S(stream));
+                         wdtype, colsum, S(stream));
   });
 
   // ---- MFMA GEMM (1x1 conv) -------------------------------------------------

@@ -171,7 +171,10 @@ __global__ __launch_bounds__(kThreads) void ln_fwd_kernel(const T* __restrict__ 
 // during the current row's two reductions and its dx stores (PF: up to 4 vectors per lane;
 // wider rows would spill the second buffer). dy and xhat are recomputed from the raw row in
 // the second pass rather than kept as fp32 arrays.
-template <typename T, bool DH, int VPL, typename A>
+// CS (with DH): also the column sums of dx — in a pre-LN block dx is the gradient of h = x + p
+// where p is the previous Linear's output, so these are that Linear's bias gradient (no colsum
+// pass over dx afterwards); the partial row is then [3][D].
+template <typename T, bool DH, int VPL, typename A, bool CS = false>
 __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                           const T* __restrict__ dh_ext,
                                                           const float* __restrict__ mean_in,
@@ -179,18 +182,22 @@ __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(const T* __restrict__ 
                                                           const A* __restrict__ w, T* __restrict__ dx,
                                                           float* __restrict__ part, int64_t rows, int D) {
   constexpr bool PF = VPL <= 4;
-  extern __shared__ __attribute__((aligned(16))) float red[];  // [2][D]
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [2 or 3][D]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nv = D / 8;
   const LnLanes<VPL> L(lane, nv);
   const float inv_d = 1.f / static_cast<float>(D);
-  float wv[VPL][8], dwp[VPL][8], dbp[VPL][8];
+  float wv[VPL][8], dwp[VPL][8], dbp[VPL][8], csp[CS ? VPL : 1][8];
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
     ld8w(w, L.vc[i] * 8, wv[i]);
 #pragma unroll
     for (int j = 0; j < 8; ++j) dwp[i][j] = dbp[i][j] = 0.f;
   }
+#pragma unroll
+  for (int i = 0; i < (CS ? VPL : 1); ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) csp[i][j] = 0.f;
   struct Buf {
     T d[VPL][8], x[VPL][8], e[DH ? VPL : 1][8];
     float mean, rstd;
@@ -229,6 +236,7 @@ __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(const T* __restrict__ 
         float g = c.rstd * (static_cast<float>(c.d[i][j]) * wv[i][j] - m1 - xh * m2);
         if (DH) g += static_cast<float>(c.e[i][j]);
         o[j] = static_cast<T>(g);
+        if (CS) csp[CS ? i : 0][j] += L.act[i] ? static_cast<float>(o[j]) : 0.f;  // of the stored (rounded) dx
       }
       if (L.act[i]) store8(dx + rw * D + L.vc[i] * 8, o);
     }
@@ -267,13 +275,15 @@ __global__ __launch_bounds__(kThreads) void ln_bwd_kernel(const T* __restrict__ 
             const int c = L.vc[i] * 8 + j;
             red[c] = k == 0 ? dwp[i][j] : red[c] + dwp[i][j];
             red[D + c] = k == 0 ? dbp[i][j] : red[D + c] + dbp[i][j];
+            if (CS) red[2 * D + c] = k == 0 ? csp[CS ? i : 0][j] : red[2 * D + c] + csp[CS ? i : 0][j];
           }
       }
     }
     __syncthreads();
   }
-  float* out = part + static_cast<int64_t>(blockIdx.x) * 2 * D;
-  for (int c = threadIdx.x; c < 2 * D; c += kThreads) out[c] = red[c];
+  constexpr int NP = CS ? 3 : 2;
+  float* out = part + static_cast<int64_t>(blockIdx.x) * NP * D;
+  for (int c = threadIdx.x; c < NP * D; c += kThreads) out[c] = red[c];
 }
 
 int vpl_for(int64_t D) {
@@ -299,11 +309,11 @@ void fwd_launch(const void* x, const void* r, void* h, void* y, const void* w, c
       rows, static_cast<int>(D), eps);
 }
 
-template <typename T, bool DH, int VPL, typename A>
+template <typename T, bool DH, int VPL, typename A, bool CS = false>
 int bwd_launch(const void* dy, const void* x, const void* dh, const float* mean, const float* rstd, const void* w,
                void* dx, float* part, int max_blocks, int64_t rows, int64_t D, hipStream_t s) {
-  auto k = ln_bwd_kernel<T, DH, VPL, A>;
-  const size_t lds = static_cast<size_t>(2) * D * sizeof(float);
+  auto k = ln_bwd_kernel<T, DH, VPL, A, CS>;
+  const size_t lds = static_cast<size_t>(CS ? 3 : 2) * D * sizeof(float);
   int64_t blocks = resident_blocks(reinterpret_cast<const void*>(k), kThreads, lds);
   const int64_t need = (rows + kWaves - 1) / kWaves;
   if (blocks > need) blocks = need;
@@ -377,9 +387,10 @@ void layernorm_fwd(const void* x, const void* residual, void* h, void* y, const 
 
 int layernorm_bwd(const void* dy, const void* x, const void* dh_ext, const float* mean, const float* rstd,
                   const void* w, void* dx, float* partials, int max_blocks, int64_t rows, int64_t D, int dtype,
-                  int wdtype, hipStream_t stream) {
+                  int wdtype, bool colsum, hipStream_t stream) {
   const int vpl = vpl_for(D);
   const bool dh = dh_ext != nullptr;
+  if (colsum && !dh) throw std::runtime_error("fused layernorm backward: colsum needs the residual-stream input");
   if (w == nullptr || reinterpret_cast<uintptr_t>(w) % 16 != 0)
     throw std::runtime_error("fused layernorm backward: w must be 16-byte aligned (ones when absent)");
   check_affine(dtype, wdtype, "fused layernorm backward");
@@ -387,8 +398,10 @@ int layernorm_bwd(const void* dy, const void* x, const void* dh_ext, const float
   int blocks = 0;
 #define CALL_DH(V) blocks = bwd_launch<TT, true, V, AT>(dy, x, dh_ext, mean, rstd, w, dx, partials, max_blocks, rows, D, stream)
 #define CALL_NODH(V) blocks = bwd_launch<TT, false, V, AT>(dy, x, dh_ext, mean, rstd, w, dx, partials, max_blocks, rows, D, stream)
+#define CALL_DHCS(V) blocks = bwd_launch<TT, true, V, AT, true>(dy, x, dh_ext, mean, rstd, w, dx, partials, max_blocks, rows, D, stream)
 #define CALL_ALL                                                                \
-  if (dh) { LN_VPL_SWITCH(vpl, CALL_DH) } else { LN_VPL_SWITCH(vpl, CALL_NODH) }
+  if (dh && colsum) { LN_VPL_SWITCH(vpl, CALL_DHCS) } else if (dh) { LN_VPL_SWITCH(vpl, CALL_DH) }      \
+  else { LN_VPL_SWITCH(vpl, CALL_NODH) }
   switch (dtype) {
     case kBF16: {
       using TT = bf16;
@@ -411,6 +424,7 @@ int layernorm_bwd(const void* dy, const void* x, const void* dh_ext, const float
   }
 #undef CALL_ALL
 #undef CALL_DH
+#undef CALL_DHCS
 #undef CALL_NODH
   FLUXMPI_HIP_CHECK(hipGetLastError());
   return blocks;

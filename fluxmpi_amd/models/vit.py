@@ -22,10 +22,12 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.gelu import linear_gelu
+from ..ops.layernorm import linear_add_layer_norm
 from ..ops.linear import Linear
 
 # FLUXMPI_VIT_FUSED_GELU=0: autograd's GELU backward + separate bias reduction (A/B runs)
 _FUSED_GELU = os.environ.get("FLUXMPI_VIT_FUSED_GELU", "1") != "0"
+_FUSED_PROJ_LN = os.environ.get("FLUXMPI_VIT_FUSED_PROJ_LN", "1") != "0"
 
 
 class PatchEmbed(nn.Module):
@@ -132,7 +134,13 @@ class Block(nn.Module):
         else:
             x, y = self.ln1.add_forward(x, m)  # x <- x + m (previous block's MLP branch)
         a = packed_attention(self.qkv(y), h)
-        x, y = self.ln2.add_forward(x, self.proj(a))
+        # proj + residual add + ln2 in one autograd node: proj's bias gradient comes out of the
+        # LayerNorm backward pass (ops/layernorm.linear_add_layer_norm)
+        if _FUSED_PROJ_LN:
+            x, y = linear_add_layer_norm(a, self.proj.weight, self.proj.bias, x, self.ln2.weight, self.ln2.bias,
+                                         self.ln2.eps)
+        else:
+            x, y = self.ln2.add_forward(x, self.proj(a))
         # fc1 + GELU: GELU backward and fc1's bias gradient in one pass (ops/gelu.py)
         if _FUSED_GELU:
             return x, self.fc2(linear_gelu(y, self.fc1.weight, self.fc1.bias))

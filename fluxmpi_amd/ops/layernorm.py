@@ -74,18 +74,31 @@ def _fwd(x, r, w, b, eps):
     return h, y, mean, rstd
 
 
-def _bwd(dy, x, dh_ext, mean, rstd, w, dtypes):
+def _bwd(dy, x, dh_ext, mean, rstd, w, dtypes, colsum_dtype=None):
     """``(dx, dw, db)``; dw / db reduced straight into the parameter dtype when it is fp32 or bf16
-    and both share it (no cast kernels), else reduced in fp32 and cast."""
+    and both share it (no cast kernels), else reduced in fp32 and cast. ``colsum_dtype`` (needs
+    ``dh_ext``): also the column sums of dx, returned fourth in that dtype."""
     C = _ext.get(required=True)
     d = x.shape[-1]
     rows = x.numel() // d
     dx = torch.empty_like(x)
-    part = torch.empty(_MAX_BLOCKS, 2 * d, device=x.device, dtype=torch.float32)
+    cs = colsum_dtype is not None
+    npart = 3 if cs else 2
+    part = torch.empty(_MAX_BLOCKS, npart * d, device=x.device, dtype=torch.float32)
     nb = C.layernorm_bwd(dy.data_ptr(), x.data_ptr(), _p(dh_ext), mean.data_ptr(), rstd.data_ptr(), w.data_ptr(),
                          dx.data_ptr(), part.data_ptr(), _MAX_BLOCKS, rows, d, DTYPE_CODE[x.dtype],
-                         DTYPE_CODE[w.dtype], _stream(x))
+                         DTYPE_CODE[w.dtype], _stream(x), cs)
     wd, bd = dtypes
+    if cs:  # one reduce launch over all 3D columns (straight into the shared dtype when there is one)
+        present = {t for t in (wd, bd, colsum_dtype) if t is not None}
+        rdt = present.pop() if len(present) == 1 else torch.float32
+        if rdt not in (torch.float32, torch.bfloat16):
+            rdt = torch.float32
+        red = torch.empty(3 * d, device=x.device, dtype=rdt)
+        C.gemm_splitk_reduce(part.data_ptr(), nb, 3 * d, red.data_ptr(), DTYPE_CODE[rdt], _stream(x))
+        dw = red[:d].to(wd) if wd is not None else None
+        db = red[d:2 * d].to(bd) if bd is not None else None
+        return dx, dw, db, red[2 * d:].to(colsum_dtype)
     if wd is None and bd is None:
         return dx, None, None
     present = {t for t in dtypes if t is not None}
@@ -136,6 +149,53 @@ class _AddLayerNormFn(torch.autograd.Function):
         return dx, dx, dw, db, None  # h = x + r: both inputs get the same gradient
 
 
+class _LinearAddLayerNormFn(torch.autograd.Function):
+    """``(h, LN(h))`` with ``h = x + a W^T + b``: a pre-LN block's output projection and the next
+    LayerNorm's residual add. The LayerNorm backward's dx IS the projection output's gradient,
+    so its column sums (the projection's bias gradient) come out of the same pass — no colsum
+    kernel over dx; the weight gradient runs on the split-K HIP kernel (ops/linear.py)."""
+
+    @staticmethod
+    def forward(ctx, a, weight, bias, x, ln_w, ln_b, eps):
+        p = F.linear(a, weight, bias)
+        x = x.contiguous()
+        w, b = _affine(x, ln_w, ln_b)
+        h, y, mean, rstd = _fwd(x, p.contiguous(), w, b, eps)
+        ctx.save_for_backward(a, weight, h, w, mean, rstd)
+        ctx.dtypes = (ln_w.dtype if ln_w is not None else None, ln_b.dtype if ln_b is not None else None)
+        ctx.bias_dtype = bias.dtype
+        return h, y
+
+    @staticmethod
+    def backward(ctx, dh, dy):
+        from .linear import native_ok, weight_grad
+        a, weight, h, w, mean, rstd = ctx.saved_tensors
+        if dy is None:
+            dy = torch.zeros_like(h)
+        if dh is None:
+            dh = torch.zeros_like(h)
+        dx, dlw, dlb, dbias = _bwd(dy.contiguous(), h, dh.contiguous(), mean, rstd, w, ctx.dtypes, ctx.bias_dtype)
+        n_out, n_in = weight.shape
+        g2 = dx.reshape(-1, n_out)
+        a2 = a.reshape(-1, n_in)
+        da = (g2 @ weight).reshape(a.shape) if ctx.needs_input_grad[0] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw = weight_grad(g2, a2, weight.dtype) if native_ok(a2, g2) else g2.t() @ a2
+        return da, dw, (dbias if ctx.needs_input_grad[2] else None), dx, dlw, dlb, None
+
+
+def linear_add_layer_norm(a, weight, bias, x, ln_w, ln_b, eps=1e-5):
+    """``(h, layer_norm(h))`` with ``h = x + F.linear(a, weight, bias)`` (see
+    :class:`_LinearAddLayerNormFn`); the PyTorch composition off the fused path."""
+    if (supported(x) and bias is not None and a.is_contiguous() and a.shape[:-1] == x.shape[:-1]
+            and weight.shape[0] == x.shape[-1] and a.dtype == x.dtype == weight.dtype and torch.is_grad_enabled()
+            and (ln_w is None or ln_w.shape[-1] == x.shape[-1])):
+        return _LinearAddLayerNormFn.apply(a, weight, bias, x, ln_w, ln_b, eps)
+    from .linear import linear
+    return add_layer_norm(x, linear(a, weight, bias), ln_w, ln_b, eps)
+
+
 def layer_norm(x, weight, bias, eps=1e-5):
     if supported(x) and (weight is None or weight.shape[-1] == x.shape[-1]):
         return _LayerNormFn.apply(x, weight, bias, eps)
@@ -162,4 +222,4 @@ class FusedLayerNorm(nn.LayerNorm):
         return add_layer_norm(x, r, self.weight, self.bias, self.eps)
 
 
-__all__ = ["FusedLayerNorm", "layer_norm", "add_layer_norm"]
+__all__ = ["FusedLayerNorm", "layer_norm", "add_layer_norm", "linear_add_layer_norm"]

@@ -71,3 +71,33 @@ def test_layer_norm_no_affine(gpu_ext):
     (y.float() * gy).sum().backward()
     (yr * gy).sum().backward()
     assert _rel(y, yr) < 2e-2 and _rel(xa.grad, xr.grad) < 2e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16])
+@pytest.mark.parametrize("shape", [(4, 197, 768), (2, 7, 1032)])
+def test_linear_add_layer_norm(gpu_ext, dtype, shape):
+    """proj + residual add + LayerNorm as one node (the LayerNorm backward's dx column sums are the
+    projection's bias gradient) vs the fp32 PyTorch composition."""
+    from fluxmpi_amd.ops.layernorm import linear_add_layer_norm
+    torch.manual_seed(3)
+    d = shape[-1]
+    k = 256
+    a = (torch.randn(*shape[:-1], k, device="cuda") * 0.5).to(dtype)
+    W = (torch.randn(d, k, device="cuda") * 0.05).to(dtype)
+    b = (torch.randn(d, device="cuda") * 0.1).to(dtype)
+    x = torch.randn(shape, device="cuda").to(dtype)
+    lw = (torch.rand(d, device="cuda") + 0.5).to(dtype)
+    lb = (torch.randn(d, device="cuda") * 0.1).to(dtype)
+    ins = [t.clone().requires_grad_() for t in (a, W, b, x, lw, lb)]
+    ref = [t.float().clone().requires_grad_() for t in (a, W, b, x, lw, lb)]
+    h, y = linear_add_layer_norm(*ins, 1e-6)
+    hr = ref[3] + F.linear(ref[0], ref[1], ref[2])
+    yr = F.layer_norm(hr, (d,), ref[4], ref[5], 1e-6)
+    gh, gy = torch.randn_like(hr), torch.randn_like(yr)
+    ((h.float() * gh).sum() + (y.float() * gy).sum()).backward()
+    ((hr * gh).sum() + (yr * gy).sum()).backward()
+    assert _rel(h, hr) < 2e-2 and _rel(y, yr) < 2e-2
+    for t, r in zip(ins, ref):
+        assert t.grad is not None and t.grad.dtype == t.dtype
+        assert _rel(t.grad, r.grad) < 3e-2
