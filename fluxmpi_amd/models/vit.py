@@ -111,10 +111,13 @@ def packed_attention(qkv: torch.Tensor, heads: int) -> torch.Tensor:
 
 
 class Block(nn.Module):
-    """Pre-LN transformer block. ``forward(x, m)`` takes the residual stream ``x`` and the
-    previous block's pending MLP output ``m`` and returns ``(x + m + attn, mlp)``: each
-    residual add is fused into the LayerNorm that reads its result (``FusedLayerNorm.
-    add_forward``), so the stream is never re-read by a standalone add kernel."""
+    """Pre-LN transformer block. ``forward(x, pend)`` takes the residual stream ``x`` and the
+    previous block's pending MLP branch ``pend = (g, fc2)`` (its GELU activations and its fc2)
+    and returns ``(x + fc2(g) + attn, (g', self.fc2))``: each residual add is fused into the
+    LayerNorm that reads its result, and the Linear producing the added branch (proj here, the
+    previous block's fc2 at ln1) joins that LayerNorm in one autograd node
+    (``ops/layernorm.linear_add_layer_norm``) whose backward also yields the Linear's bias
+    gradient — no standalone add or bias-gradient kernels in either direction."""
 
     def __init__(self, dim, heads, mlp):
         super().__init__()
@@ -127,24 +130,24 @@ class Block(nn.Module):
         self.fc1 = nn.Linear(dim, mlp)
         self.fc2 = Linear(mlp, dim)
 
-    def forward(self, x, m=None):
+    @staticmethod
+    def _add_ln(ln, x, a, lin):
+        """``(x + lin(a), ln(x + lin(a)))``."""
+        if _FUSED_PROJ_LN:
+            return linear_add_layer_norm(a, lin.weight, lin.bias, x, ln.weight, ln.bias, ln.eps)
+        return ln.add_forward(x, lin(a))
+
+    def forward(self, x, pend=None):
         h = self.heads
-        if m is None:
+        if pend is None:
             y = self.ln1(x)
         else:
-            x, y = self.ln1.add_forward(x, m)  # x <- x + m (previous block's MLP branch)
+            x, y = self._add_ln(self.ln1, x, *pend)  # x <- x + fc2(g) (previous block's MLP branch)
         a = packed_attention(self.qkv(y), h)
-        # proj + residual add + ln2 in one autograd node: proj's bias gradient comes out of the
-        # LayerNorm backward pass (ops/layernorm.linear_add_layer_norm)
-        if _FUSED_PROJ_LN:
-            x, y = linear_add_layer_norm(a, self.proj.weight, self.proj.bias, x, self.ln2.weight, self.ln2.bias,
-                                         self.ln2.eps)
-        else:
-            x, y = self.ln2.add_forward(x, self.proj(a))
+        x, y = self._add_ln(self.ln2, x, a, self.proj)
         # fc1 + GELU: GELU backward and fc1's bias gradient in one pass (ops/gelu.py)
-        if _FUSED_GELU:
-            return x, self.fc2(linear_gelu(y, self.fc1.weight, self.fc1.bias))
-        return x, self.fc2(F.gelu(self.fc1(y)))
+        g = linear_gelu(y, self.fc1.weight, self.fc1.bias) if _FUSED_GELU else F.gelu(self.fc1(y))
+        return x, (g, self.fc2)
 
 
 class ViT(nn.Module):
@@ -165,11 +168,15 @@ class ViT(nn.Module):
     def forward(self, x):
         x = self.embed(x)
         x = torch.cat([self.cls.expand(x.shape[0], -1, -1).to(x.dtype), x], 1) + self.pos.to(x.dtype)
-        m = None
+        pend = None
         for blk in self.blocks:
-            x, m = blk(x, m)
+            x, pend = blk(x, pend)
         # only the [CLS] token reaches the head: finish its residual stream and normalise it alone
-        c = x[:, 0] if m is None else x[:, 0] + m[:, 0]
+        if pend is None:
+            c = x[:, 0]
+        else:
+            g, fc2 = pend
+            c = x[:, 0] + fc2(g)[:, 0]
         return self.head(self.ln(c))
 
 
