@@ -22,6 +22,9 @@ namespace {
 
 constexpr int kMaxThreads = 256;
 constexpr int kMaxG = 64;
+// pixels per lane whose loads are issued together (one workgroup per sample: at one pixel per
+// iteration every pass was a chain of dependent memory round trips, ~2.6 TB/s on the DEQ cell)
+constexpr int kU = 4;
 
 struct GnShape {
   int HW, C, G, CV, PL, T;  // CV = C/8 channel vectors per pixel, PL pixel lanes, T = PL*CV lanes
@@ -80,10 +83,7 @@ __global__ __launch_bounds__(kMaxThreads) void gn_fwd_kernel(const T* __restrict
 #pragma unroll
   for (int j = 0; j < 8; ++j) sum[j] = sq[j] = 0.f;
   if (active) {
-    for (int p = pl; p < s.HW; p += s.PL) {
-      T xv[8], av[8];
-      load8(x + base + static_cast<int64_t>(p) * s.C, xv);
-      if (ADD) load8(a + base + static_cast<int64_t>(p) * s.C, av);
+    auto acc = [&](const T (&xv)[8], const T (&av)[8]) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float v = to_f(xv[j]);
@@ -93,6 +93,23 @@ __global__ __launch_bounds__(kMaxThreads) void gn_fwd_kernel(const T* __restrict
         sum[j] += v;
         sq[j] += v * v;
       }
+    };
+    int p = pl;
+    for (; p + (kU - 1) * s.PL < s.HW; p += kU * s.PL) {  // kU pixels' loads in flight
+      T xv[kU][8], av[kU][8];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        load8(x + base + static_cast<int64_t>(p + u * s.PL) * s.C, xv[u]);
+        if (ADD) load8(a + base + static_cast<int64_t>(p + u * s.PL) * s.C, av[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) acc(xv[u], av[u]);
+    }
+    for (; p < s.HW; p += s.PL) {
+      T xv[8], av[8];
+      load8(x + base + static_cast<int64_t>(p) * s.C, xv);
+      if (ADD) load8(a + base + static_cast<int64_t>(p) * s.C, av);
+      acc(xv, av);
     }
   }
   reduce_channels(red, sum, sq, pl, cv, s.PL, s.C, chan, active);
@@ -122,11 +139,8 @@ __global__ __launch_bounds__(kMaxThreads) void gn_fwd_kernel(const T* __restrict
     sc[j] = grp[s.G + g] * wc;
     sh[j] = bc - grp[g] * sc[j];
   }
-  for (int p = pl; p < s.HW; p += s.PL) {
-    const int64_t off = base + static_cast<int64_t>(p) * s.C;
-    T xv[8], av[8], hv[8], yv[8];
-    load8(x + off, xv);
-    if (ADD) load8(a + off, av);
+  auto apply = [&](int64_t off, const T (&xv)[8], const T (&av)[8]) {
+    T hv[8], yv[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float v = to_f(xv[j]);
@@ -137,6 +151,25 @@ __global__ __launch_bounds__(kMaxThreads) void gn_fwd_kernel(const T* __restrict
     }
     if (SAVEH) store8(h + off, hv);
     store8(y + off, yv);
+  };
+  int p = pl;
+  for (; p + (kU - 1) * s.PL < s.HW; p += kU * s.PL) {
+    T xv[kU][8], av[kU][8];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t off = base + static_cast<int64_t>(p + u * s.PL) * s.C;
+      load8(x + off, xv[u]);
+      if (ADD) load8(a + off, av[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) apply(base + static_cast<int64_t>(p + u * s.PL) * s.C, xv[u], av[u]);
+  }
+  for (; p < s.HW; p += s.PL) {
+    const int64_t off = base + static_cast<int64_t>(p) * s.C;
+    T xv[8], av[8];
+    load8(x + off, xv);
+    if (ADD) load8(a + off, av);
+    apply(off, xv, av);
   }
 }
 
@@ -158,16 +191,30 @@ __global__ __launch_bounds__(kMaxThreads) void gn_bwd_kernel(const T* __restrict
 #pragma unroll
   for (int j = 0; j < 8; ++j) sdy[j] = sdyh[j] = 0.f;
   if (active) {
-    for (int p = pl; p < s.HW; p += s.PL) {
-      T dv[8], hv[8];
-      load8(dy + base + static_cast<int64_t>(p) * s.C, dv);
-      load8(h + base + static_cast<int64_t>(p) * s.C, hv);
+    auto acc = [&](const T (&dv)[8], const T (&hv)[8]) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float d = to_f(dv[j]);
         sdy[j] += d;
         sdyh[j] += d * to_f(hv[j]);
       }
+    };
+    int p = pl;
+    for (; p + (kU - 1) * s.PL < s.HW; p += kU * s.PL) {  // kU pixels' loads in flight
+      T dv[kU][8], hv[kU][8];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        load8(dy + base + static_cast<int64_t>(p + u * s.PL) * s.C, dv[u]);
+        load8(h + base + static_cast<int64_t>(p + u * s.PL) * s.C, hv[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) acc(dv[u], hv[u]);
+    }
+    for (; p < s.HW; p += s.PL) {
+      T dv[8], hv[8];
+      load8(dy + base + static_cast<int64_t>(p) * s.C, dv);
+      load8(h + base + static_cast<int64_t>(p) * s.C, hv);
+      acc(dv, hv);
     }
   }
   reduce_channels(red, sdy, sdyh, pl, cv, s.PL, s.C, chan, active);
@@ -205,11 +252,8 @@ __global__ __launch_bounds__(kMaxThreads) void gn_bwd_kernel(const T* __restrict
     m1[j] = grp[g];
     m2[j] = grp[s.G + g];
   }
-  for (int p = pl; p < s.HW; p += s.PL) {
-    const int64_t off = base + static_cast<int64_t>(p) * s.C;
-    T dv[8], hv[8], ov[8];
-    load8(dy + off, dv);
-    load8(h + off, hv);
+  auto apply = [&](int64_t off, const T (&dv)[8], const T (&hv)[8]) {
+    T ov[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const float hf = to_f(hv[j]);
@@ -219,6 +263,25 @@ __global__ __launch_bounds__(kMaxThreads) void gn_bwd_kernel(const T* __restrict
       ov[j] = from_f<T>(g);
     }
     store8(dh + off, ov);
+  };
+  int p = pl;
+  for (; p + (kU - 1) * s.PL < s.HW; p += kU * s.PL) {
+    T dv[kU][8], hv[kU][8];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int64_t off = base + static_cast<int64_t>(p + u * s.PL) * s.C;
+      load8(dy + off, dv[u]);
+      load8(h + off, hv[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) apply(base + static_cast<int64_t>(p + u * s.PL) * s.C, dv[u], hv[u]);
+  }
+  for (; p < s.HW; p += s.PL) {
+    const int64_t off = base + static_cast<int64_t>(p) * s.C;
+    T dv[8], hv[8];
+    load8(dy + off, dv);
+    load8(h + off, hv);
+    apply(off, dv, hv);
   }
 }
 
