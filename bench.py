@@ -130,6 +130,12 @@ def main():
         if not is_norm:
             for p in m.parameters(recurse=False):
                 p.data = p.data.to(torch.bfloat16)
+    if world > 1 and not args.same_device and FluxMPI.backend_name() != "rccl":
+        # no silent fallback: an N>1 number must come from the native RCCL communicator
+        print(f"bench.py: device backend is {FluxMPI.backend_name()!r}, not the native 'rccl' "
+              "communicator; refusing to report an N>1 number (use --same-device for a rehearsal)",
+              file=sys.stderr)
+        return 3
     rule = O.Adam(1e-3) if args.optimizer == "adam" else O.Momentum(0.1, 0.9)
     ddp = DDP(model, rule, average=True, overlap=not args.no_overlap, force_comm=args.force_comm)
 
@@ -146,6 +152,15 @@ def main():
         loss.backward()
         ddp.step()
         return loss
+
+    calibrated = False
+    if world > 1:
+        # per-shape kernel choices measured once on rank 0 with no collective in flight, shared
+        # with every rank and frozen (parallel/autotune.py): all ranks run the same kernels
+        from fluxmpi_amd.parallel.autotune import calibrate
+
+        calibrate(ddp, lambda: F.cross_entropy(ddp(x).float(), y).backward())
+        calibrated = True
 
     if args.graph and args.model == "deq":
         # the implicit layer's solver lengths are data dependent (host-side loop exits), which a
@@ -165,6 +180,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
+    t_host = time.perf_counter() - t0  # the host's enqueue time: ~wall when launch-bound
     torch.cuda.synchronize()
     FluxMPI.barrier()
     dt = time.perf_counter() - t0
@@ -201,7 +217,10 @@ def main():
                        "image_size": args.image, "parallelism": f"dp{world}", "optimizer": args.optimizer,
                        "conv": args.conv, "norm": args.norm, "memory_format": "contiguous" if memfmt is torch.contiguous_format else "channels_last", "backend": FluxMPI.backend_name(),
                        "miopen_find": bool(args.miopen_find), "hip_graph": bool(args.graph),
-                       "tunableop": use_tunableop, "kernel_choices": "shipped" if use_choices else "measured",
+                       "tunableop": use_tunableop,
+                       "kernel_choices": ("shipped" if use_choices else "measured")
+                       + ("+rank0-calibrated" if calibrated else ""),
+                       "host_ms_per_step": round(1000 * t_host / args.steps, 3),
                        "loss": round(lval, 4),
                        # what the data-parallel layer actually did: at N=1 nothing is communicated
                        # (overlap false, comm "none") unless --force-comm

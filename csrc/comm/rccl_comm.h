@@ -7,6 +7,8 @@
 #include <string>
 #include <vector>
 
+struct ncclComm;  // rccl.h's opaque communicator (ncclComm_t), kept out of this header
+
 namespace fluxmpi {
 
 std::string rccl_unique_id();
@@ -42,18 +44,20 @@ class RcclComm {
   void abort(int abort_wait_ms = 2000);
   void destroy();
   bool aborted() const { return aborted_.load(); }
-  bool is_open() const { return comm_ != nullptr; }
+  bool is_open() const { return comm_.load() != nullptr; }
 
   int rank() const { return rank_; }
   int size() const { return size_; }
   int device() const { return device_; }
 
  private:
-  void check_open() const;
+  // the handle, read once per call under mu_ (abort() may clear it without the lock)
+  ::ncclComm* open_comm() const;
+  void check_not_aborted() const;
   static size_t dtype_size(int dtype);
   std::timed_mutex mu_;
   std::atomic<bool> aborted_{false};
-  void* comm_ = nullptr;
+  std::atomic<void*> comm_{nullptr};
   int rank_, size_, device_;
 };
 

@@ -253,7 +253,7 @@ def ds_forward_is_ours(x, weight, stride) -> bool:
     hit = _DS_CHOICE.get(key)
     if hit is not None:
         return hit
-    if torch.cuda.is_current_stream_capturing():
+    if _no_measure():
         return True
     with torch.no_grad():
         xs = x.detach().contiguous(memory_format=torch.channels_last)
@@ -612,7 +612,7 @@ def _dgrad_is_ours(dy, weight, x_shape) -> bool:
     hit = _DGRAD_CHOICE.get(key)
     if hit is not None:
         return hit
-    if torch.cuda.is_current_stream_capturing():
+    if _no_measure():
         return True
     with torch.no_grad():
         d = dy.detach()
@@ -676,7 +676,7 @@ def conv3x3_s2_forward_is_ours(x, weight) -> bool:
     hit = _S2_CHOICE.get(key)
     if hit is not None:
         return hit
-    if torch.cuda.is_current_stream_capturing():
+    if _no_measure():
         return True
     with torch.no_grad():
         xs = x.detach().contiguous(memory_format=torch.channels_last)
@@ -708,6 +708,14 @@ def conv3x3_supported(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
 _FWD_CHOICE: dict = {}  # (N, C, H, W, Co) -> True: our forward (+ statistics epilogue) is faster
 _FWD_ENGINE: dict = {}  # (N, C, H, W, Co) -> the fastest of _FWD_ENGINES for our forward
 _FWD_ENGINES = (0, 8, 7)  # 0: auto (128x128 tiles); 8 / 7: 256x128 tiles, 64- / 32-deep K-steps
+
+
+_FROZEN = False  # freeze_choices(): no more measurements (rank-consistent tables at N > 1)
+
+
+def _no_measure() -> bool:
+    """Take the default instead of timing: inside a HIP-graph capture, or once frozen."""
+    return _FROZEN or torch.cuda.is_current_stream_capturing()
 
 
 def _time_us(fn, iters=10, repeats=3):
@@ -745,7 +753,7 @@ def wgrad_best(key, impls: dict):
     cudnn.benchmark: MIOpen vs our kernel in each of ``_WG_CONFIGS``) and return its result."""
     choice = _WG_CHOICE.get(key)
     if choice is None:
-        if WGRAD == "miopen" or torch.cuda.is_current_stream_capturing():
+        if WGRAD == "miopen" or _no_measure():
             choice = ("miopen", None)
         elif WGRAD == "ours":
             choice = ("ours", _WG_CONFIGS[0])
@@ -788,7 +796,7 @@ def conv3x3_forward_is_ours(x, weight) -> bool:
     hit = _FWD_CHOICE.get(key)
     if hit is not None:
         return hit
-    if torch.cuda.is_current_stream_capturing():
+    if _no_measure():
         return True
     with torch.no_grad():
         xs = x.detach().contiguous(memory_format=torch.channels_last)
@@ -842,7 +850,7 @@ def conv1x1_forward_is_ours(x, weight) -> bool:
     hit = _FWD1_CHOICE.get(key)
     if hit is not None:
         return hit
-    if torch.cuda.is_current_stream_capturing():
+    if _no_measure():
         return True
     with torch.no_grad():
         xs = x.detach().contiguous(memory_format=torch.channels_last)
@@ -900,26 +908,43 @@ def dump_choices():
     return out
 
 
-def load_choices(path: str) -> int:
-    """Pre-populate the per-shape kernel choices from a JSON-lines record (``dump_choices``):
+def load_choice_lines(lines) -> int:
+    """Pre-populate the per-shape kernel choices from JSON-lines records (``dump_choices``):
     those shapes skip the first-step measurement (no autotune time, no run-to-run flips of
-    marginal shapes); others are still measured. Returns the number of entries loaded."""
+    marginal shapes); others are still measured (unless frozen). Returns the entries loaded."""
     import ast
     import json
     g = globals()
     n = 0
-    with open(path) as f:
-        for line in f:
-            line = line.strip()
-            if not line:
-                continue
-            rec = json.loads(line)
-            name = _CHOICE_TABLES.get(rec["kind"])
-            if name is None:
-                continue
-            g[name][ast.literal_eval(rec["key"])] = ast.literal_eval(rec["choice"])
-            n += 1
+    for line in lines:
+        line = line.strip()
+        if not line:
+            continue
+        rec = json.loads(line)
+        name = _CHOICE_TABLES.get(rec["kind"])
+        if name is None:
+            continue
+        g[name][ast.literal_eval(rec["key"])] = ast.literal_eval(rec["choice"])
+        n += 1
     return n
+
+
+def load_choices(path: str) -> int:
+    """:func:`load_choice_lines` from a file."""
+    with open(path) as f:
+        return load_choice_lines(f.readlines())
+
+
+def freeze_choices(frozen: bool = True) -> None:
+    """Stop measuring: a shape missing from the tables takes the deterministic default (what a
+    HIP-graph capture takes) instead of a timing that could differ between ranks
+    (``parallel/autotune.calibrate``)."""
+    global _FROZEN
+    _FROZEN = frozen
+
+
+def choices_frozen() -> bool:
+    return _FROZEN
 
 
 if os.environ.get("FLUXMPI_KERNEL_CHOICES"):

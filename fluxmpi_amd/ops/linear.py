@@ -94,6 +94,7 @@ class _LinearFn(torch.autograd.Function):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
         ctx.bias_dtype = bias.dtype if bias is not None else None
+        ctx.bias = bias  # the leaf itself (not saved data): streams.run checks its .grad
         return F.linear(x, weight, bias)
 
     @staticmethod
@@ -116,7 +117,9 @@ class _LinearFn(torch.autograd.Function):
 
         if need_w or need_b:
             # weight / bias gradients on the side stream, overlapping the input-gradient chain
-            dw, db = streams.run(grads, dy2, x2, param=w if need_w else None)
+            # both parameters: if either already holds a .grad, autograd accumulates into it on
+            # the main stream, which must not race a side-stream producer
+            dw, db = streams.run(grads, dy2, x2, param=[w if need_w else None, ctx.bias if need_b else None])
         dx = (dy2 @ w).reshape(x.shape) if ctx.needs_input_grad[0] else None
         return dx, dw, db
 

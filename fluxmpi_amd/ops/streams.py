@@ -64,9 +64,12 @@ def run(fn, *inputs, param=None):
     returns its result. Falls back to a plain call when the side stream is off or capturing, and
     when ``param`` (the weight whose gradient ``fn`` computes) already holds a gradient: autograd
     would then accumulate into it with a kernel on the current stream, which must not race the
-    side stream ("steal"-mode DDP and ``zero_grad(set_to_none=True)`` leave it None)."""
+    side stream ("steal"-mode DDP and ``zero_grad(set_to_none=True)`` leave it None). ``param``
+    may be a list when ``fn`` produces several parameters' gradients (weight and bias): every
+    one of them must be gradient-free."""
     dev = inputs[0].device
-    if not active(dev) or (param is not None and param.grad is not None):
+    params = param if isinstance(param, (list, tuple)) else (param,)
+    if not active(dev) or any(p is not None and p.grad is not None for p in params):
         return fn()
     main = torch.cuda.current_stream(dev)
     side = side_stream(dev)

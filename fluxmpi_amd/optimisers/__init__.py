@@ -101,11 +101,24 @@ def _as_tensor(x):
     return x
 
 
+_T_CACHE: dict = {}
+
+
 def _T(x: torch.Tensor, v: float) -> float:
-    """Julia's ``T(η)`` cast: round a hyperparameter to the array's precision."""
-    if x.dtype in (torch.float32, torch.bfloat16, torch.float16):
-        return float(np.float32(v)) if x.dtype == torch.float32 else float(v)
-    return float(v)
+    """Julia's ``T(η)`` cast (Optimisers.jl rules convert η, β, ϵ to ``eltype(x)``): round a
+    hyperparameter to the array's precision — fp32, and for bf16 / fp16 arrays bf16 / fp16
+    (``BFloat16(0.9) == 0.8984375``; ``Float16(1e-8) == 0``), exactly as the Julia rule does.
+    fp64 (and non-float) arrays keep the double."""
+    dt = x.dtype
+    if dt not in (torch.float32, torch.bfloat16, torch.float16):
+        return float(v)
+    key = (dt, v)
+    r = _T_CACHE.get(key)
+    if r is None:
+        r = float(np.float32(v)) if dt == torch.float32 else float(torch.tensor(float(v), dtype=dt))
+        if len(_T_CACHE) < 4096:
+            _T_CACHE[key] = r
+    return r
 
 
 # ------------------------------------------------------------------ rules
@@ -164,10 +177,17 @@ def _sgd_batch(rule, items, rho, nesterov):
         if i not in gset:
             leaf.state, out[i] = rule.apply(leaf.state, x, dx)
     if gpu:
-        xs = [items[i][1] for i in gpu]
-        gs = [items[i][2] for i in gpu]
-        bufs = [items[i][0].state for i in gpu] if rho != 0.0 else None
-        _fused.sgd_(xs, gs, bufs, lr=rule.eta, momentum=rho, nesterov=nesterov)
+        by_dtype: dict = {}
+        for i in gpu:
+            by_dtype.setdefault(items[i][1].dtype, []).append(i)
+        for idx in by_dtype.values():
+            x0 = items[idx[0]][1]
+            xs = [items[i][1] for i in idx]
+            gs = [items[i][2] for i in idx]
+            bufs = [items[i][0].state for i in idx] if rho != 0.0 else None
+            # hyperparameters rounded to the leaves' precision, as in Julia (``_T``)
+            _fused.sgd_(xs, gs, bufs, lr=_T(x0, rule.eta), momentum=_T(x0, rho) if rho else 0.0,
+                        nesterov=nesterov)
     return out
 
 
@@ -228,7 +248,7 @@ def _adam_batch(rule: Adam, items, weight_decay: float):
               and isinstance(leaf.state, tuple) and len(leaf.state) == 3
               and _fused.supported(x.dtype, dx.dtype, leaf.state[0].dtype, False))
         if ok:
-            key = (x.device, tuple(leaf.state[2]))  # same beta^t -> one launch
+            key = (x.device, x.dtype, tuple(leaf.state[2]))  # same precision and beta^t -> one launch
             fused.setdefault(key, []).append(i)
         elif (not x.is_cuda and dx is not None and x.dtype in (torch.float32, torch.float64)
               and dx.dtype == x.dtype and isinstance(leaf.state, tuple) and len(leaf.state) == 3
@@ -265,13 +285,16 @@ def _adam_batch(rule: Adam, items, weight_decay: float):
             m, v, b = leaf.state
             leaf.state = (m, v, (_T(x0, b[0] * b1), _T(x0, b[1] * b2)))
             out[i] = num[k]
-    for (_, bt), idx in fused.items():
+    for (_, _, bt), idx in fused.items():
+        x0 = items[idx[0]][1]
         xs = [items[i][1] for i in idx]
         gs = [items[i][2] for i in idx]
         ms = [items[i][0].state[0] for i in idx]
         vs = [items[i][0].state[1] for i in idx]
-        _fused.adam_(xs, gs, ms, vs, lr=rule.eta, beta1=rule.beta[0], beta2=rule.beta[1], eps=rule.epsilon,
-                     bc1=1.0 - bt[0], bc2=1.0 - bt[1], weight_decay=weight_decay)
+        # hyperparameters rounded to the leaves' precision, as in Julia (``_T``)
+        _fused.adam_(xs, gs, ms, vs, lr=_T(x0, rule.eta), beta1=_T(x0, rule.beta[0]), beta2=_T(x0, rule.beta[1]),
+                     eps=_T(x0, rule.epsilon), bc1=1.0 - bt[0], bc2=1.0 - bt[1],
+                     weight_decay=_T(x0, weight_decay) if weight_decay else 0.0)
         for i in idx:
             leaf, x = items[i][0], items[i][1]
             m, v, b = leaf.state

@@ -156,10 +156,12 @@ def allreduce_tensors(tensors: list, op=ReduceOp.SUM, comm: Communicator | None 
         w.wait()
         if flat is not None:
             mt.unpack(flat, [work_t[i] for i in idx], offs)
-            written.extend(work_t[i] for i in idx)
+        # packed leaves are written by the unpack kernel, "direct" ones by the collective
+        # itself through their raw pointer: both bypass autograd's version counters
+        written.extend(work_t[i] for i in idx)
     for orig, c in back:
         orig.copy_(c)
-    _bump_versions([t for t in written if t.is_cuda])
+    _bump_versions(written)
     return tensors
 
 
@@ -192,8 +194,11 @@ def broadcast_tensors(tensors: list, root: int = 0, comm: Communicator | None = 
         w.wait()
         if flat is not None and c.rank != root:  # root already holds the data
             mt.unpack(flat, [work_t[i] for i in idx], offs)
-            written.extend(work_t[i] for i in idx)
+        # every rank, root included, bumps every leaf the broadcast covered (packed or direct):
+        # a DDP engine's fp32 master of a synchronised parameter is then re-read from the
+        # parameter on ALL ranks, so the masters stay identical across ranks
+        written.extend(work_t[i] for i in idx)
     for orig, cc in back:
         orig.copy_(cc)
-    _bump_versions([t for t in written if t.is_cuda])
+    _bump_versions(written)
     return tensors

@@ -425,6 +425,27 @@ class GlooDeviceComm(TorchComm):
         return Work(r) if async_op else r
 
 
+def bootstrap_unique_id(make_uid, store, rank: int, size: int, tag: str = "world") -> bytes:
+    """The RCCL unique id of this communicator generation, shared through the host store.
+
+    Rank 0 creates it (``make_uid()`` = ``ncclGetUniqueId``) and publishes it; the others
+    block in ``store.get`` until it is there. One key per Init generation: every rank bumps the
+    counter once per bootstrap, and all adds of generation k precede any add of k+1
+    (``ncclCommInitRank`` is collective), so Init -> Finalize -> Init on a surviving store can
+    never read the previous generation's id. (The reference's analogue is ``MPI.Init``'s PMI
+    wire-up, ``/root/reference/src/common.jl:22``.)
+    """
+    if size == 1:
+        return bytes(make_uid())
+    gen = (int(store.add(f"fluxmpi_amd/rccl_gen/{tag}", 1)) - 1) // size
+    key = f"fluxmpi_amd/rccl_uid/{tag}/{gen}"
+    if rank == 0:
+        uid = bytes(make_uid())
+        store.set(key, uid)
+        return uid
+    return bytes(store.get(key))
+
+
 class RcclComm(Communicator):
     """Native RCCL communicator (C++ ``fluxmpi::RcclComm``) on a dedicated HIP stream.
 
@@ -444,20 +465,7 @@ class RcclComm(Communicator):
             raise RuntimeError("native RCCL communicator not available in fluxmpi_amd._C")
         self.device = torch.device(device)
         self.abort_reason: str | None = None
-        if size == 1:
-            uid = C.rccl_unique_id()
-        else:
-            # One key per Init generation: every rank bumps the counter once per bootstrap,
-            # and all adds of generation k precede any add of k+1 (ncclCommInitRank is
-            # collective), so Init -> Finalize -> Init on a surviving store can never read
-            # the previous generation's id.
-            gen = (int(store.add(f"fluxmpi_amd/rccl_gen/{tag}", 1)) - 1) // size
-            key = f"fluxmpi_amd/rccl_uid/{tag}/{gen}"
-            if rank == 0:
-                uid = C.rccl_unique_id()
-                store.set(key, uid)
-            else:
-                uid = store.get(key)
+        uid = bootstrap_unique_id(C.rccl_unique_id, store, rank, size, tag)
         with torch.cuda.device(self.device):
             self._h = C.RcclComm(bytes(uid), rank, size, self.device.index)
             # high priority: comm kernels should win the CU arbitration against

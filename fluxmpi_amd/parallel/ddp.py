@@ -46,6 +46,7 @@ into the flat moment buffers).
 from __future__ import annotations
 
 import os
+import weakref
 from contextlib import contextmanager
 from dataclasses import dataclass, field
 
@@ -61,6 +62,14 @@ from ..utils import profiling
 from ..utils.debug import Watchdog, check_replicas, check_same_structure
 from . import runtime
 from .comm import Communicator, ReduceOp
+
+
+_ENGINES: "weakref.WeakKeyDictionary[torch.nn.Module, DDP]" = weakref.WeakKeyDictionary()
+
+
+def engine_for(module: torch.nn.Module) -> "DDP | None":
+    """The DDP engine managing ``module`` (None if there is none)."""
+    return _ENGINES.get(module)
 
 
 @dataclass
@@ -83,6 +92,7 @@ class _Bucket:
     work: object = None
     names: list = field(default_factory=list)
     comm_buf: torch.Tensor | None = None
+    carry: torch.Tensor | None = None
 
 
 def _strided_view(flat: torch.Tensor, like: torch.Tensor, offset: int) -> torch.Tensor:
@@ -196,6 +206,10 @@ class DDP:
         self._direct_cache: dict = {}
         self._views: dict = {}
         self._record_versions()
+        self._carry_live = False
+        self._carry_hook = None
+        self.collectives_launched = 0  # gradient-bucket allreduces issued so far
+        _ENGINES[module] = self
         self.zero_grad()
         self.step_count = 0
         # exposed-communication timing (off by default: event timing costs a little)
@@ -286,17 +300,22 @@ class DDP:
             self.hyper = torch.tensor([self.rule.eta], dtype=torch.float32, device=dev)
 
     def broadcast_parameters(self, root_rank: int = 0):
-        """One broadcast per flat bucket + module buffers (``synchronize`` of the model)."""
+        """One broadcast per flat bucket (+ its fp32 master) + module buffers (``synchronize``
+        of the model). Broadcasting the masters keeps them bit-identical on every rank."""
+        if hasattr(self, "_versions"):
+            self._sync_masters()  # the root's outside edits reach its master before it is sent
         with torch.no_grad():
             for b in self.buckets:
                 self.comm.broadcast(b.flat_param, root_rank)
                 if b.master is not None:
-                    b.master.copy_(b.flat_param)
+                    self.comm.broadcast(b.master, root_rank)
             bufs = [t for t in self.module.buffers() if t.numel() > 0]
             if bufs:
                 from .bucket import broadcast_tensors
                 broadcast_tensors([t.detach() for t in bufs], root_rank, comm=self.comm,
                                   force_comm=self.force_comm)
+        if hasattr(self, "_versions"):
+            self._record_versions()  # params and masters were written together: nothing stale
 
     # ------------------------------------------------------------------ hooks
     @contextmanager
@@ -355,6 +374,7 @@ class DDP:
                 self.comm.stream.wait_stream(torch.cuda.current_stream(self.device))
                 _ext.get(required=True).emulate_comm(wgs, max(us, 5.0), self.comm.stream.cuda_stream, thr, lds)
             b.work = self.comm.allreduce(buf, ReduceOp.SUM, async_op=True)
+        self.collectives_launched += 1
         if self.watchdog is not None:
             self.watchdog.track(b.work, f"allreduce of gradient bucket {b.index} ({b.numel} elements)")
 
@@ -369,6 +389,7 @@ class DDP:
         fill launch per dtype); "steal" mode drops the per-step gradient tensors."""
         if self.grad_mode == "view":
             mt.fill_([b.flat_grad for b in self.buckets], 0.0)
+        self._drop_carry()
         self._rearm()
         for b in self.buckets:
             for p, o in zip(b.params, b.offsets):
@@ -453,15 +474,56 @@ class DDP:
             if b.comm_buf is not None and self.comm_dtype != b.dtype:
                 mt.unpack(b.comm_buf, [b.flat_grad], [0])
 
+    def _arm_carry(self):
+        """``step(zero_grad=False)`` with communication: the flat buffers hold the REDUCED sum
+        S1. Accumulating the next backward into them and reducing again would apply
+        ``W*S1 + S2``; the reference semantics (gradients summed over ranks, then applied:
+        ``/root/reference/src/optimizer.jl:20-23``) ask for ``S1 + S2``. So S1 moves to a carry
+        buffer that is added back after the next reduction, and the next forward (a one-shot
+        pre-hook) clears the local gradients so only the new local part is reduced. Until that
+        forward ``p.grad`` still shows S1."""
+        for b in self.buckets:
+            if b.carry is None:
+                b.carry = torch.empty_like(b.flat_grad)
+            b.carry.copy_(b.flat_grad)
+        self._carry_live = True
+        if self._carry_hook is None:
+            self._carry_hook = self.module.register_forward_pre_hook(lambda m, a: self._start_carry())
+
+    def _start_carry(self):
+        """First forward after ``step(zero_grad=False)``: drop the (reduced) gradients."""
+        if self._carry_hook is not None:
+            self._carry_hook.remove()
+            self._carry_hook = None
+        if self.grad_mode == "view":
+            mt.fill_([b.flat_grad for b in self.buckets], 0.0)
+        else:
+            for b in self.buckets:
+                for p in b.params:
+                    p.grad = None
+
+    def _drop_carry(self):
+        self._carry_live = False
+        if self._carry_hook is not None:
+            self._carry_hook.remove()
+            self._carry_hook = None
+
+    def _add_carry(self, b: _Bucket):
+        if self._carry_live and b.carry is not None:
+            b.flat_grad.add_(b.carry)
+
     def step(self, zero_grad: bool = True):
         """Finish the gradient allreduces and apply the fused optimiser to every bucket.
 
         The buckets are re-armed here whatever ``zero_grad`` is, so a following
         backward + ``step(zero_grad=False)`` (gradient accumulation across steps)
-        launches, packs and waits on every bucket again.
+        launches, packs and waits on every bucket again; the applied gradient of that
+        step is the sum over ranks of both backwards' gradients (see ``_arm_carry``).
         """
         gscale = 1.0 / self.world if self.average else 1.0
         self._sync_masters()
+        if self._carry_hook is not None:
+            self._start_carry()  # no forward since step(zero_grad=False): no new local gradient
         if not self.communicate and self.grad_mode == "steal":
             # nothing to reduce: the optimiser reads autograd's gradients where they are
             for b in self.buckets:
@@ -486,11 +548,13 @@ class DDP:
             e1.record()
             self._comm_events.append((e0, e1))
             for b in self.buckets:
+                self._add_carry(b)
                 self._apply(b, gscale)
         else:
             for b in self.buckets:
                 self._pack(b)
                 self._finish(b)
+                self._add_carry(b)
                 self._apply(b, gscale)
         self._finish_step(zero_grad)
 
@@ -506,6 +570,8 @@ class DDP:
         self._record_versions()  # the optimiser's own writes are not "outside" changes
         if zero_grad:
             self.zero_grad()
+        elif self.communicate:
+            self._arm_carry()
 
     # ------------------------------------------------------------------ masters
     def _record_versions(self):

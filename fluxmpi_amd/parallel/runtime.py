@@ -184,7 +184,11 @@ def _make_device_comm(backend, cfg, rank, size, device, cpu_comm):
         except Exception as e:  # extension missing / RCCL init failure
             if backend == "rccl":
                 raise
-            log.warning("native RCCL communicator unavailable (%r); using torch.distributed nccl", e)
+            # loud, not silent: the fallback is a different (slower, untuned) code path, and
+            # bench.py refuses to report an N>1 number from it; backend_name() says which ran
+            msg = f"native RCCL communicator unavailable ({e!r}); falling back to torch.distributed nccl"
+            log.warning(msg)
+            warnings.warn(msg, RuntimeWarning, stacklevel=3)
     if size == 1:
         return _comm.SelfComm(), "self"
     grp = dist.new_group(backend="nccl")

@@ -88,6 +88,15 @@ def _sync_scalars(values: list, root: int) -> list:
 
 
 def _sync_module(m: torch.nn.Module, root: int) -> torch.nn.Module:
+    from .ddp import engine_for
+
+    eng = engine_for(m)
+    if eng is not None and eng.communicate:
+        # a module under a DDP engine: its flat buckets AND fp32 masters are broadcast, so
+        # masters stay bit-identical across ranks (a parameter-only broadcast would leave the
+        # root with m_root and the others with bf16(m_root))
+        eng.broadcast_parameters(root)
+        return m
     ts, seen = [], set()
     for t in list(m.parameters()) + list(m.buffers()):
         if id(t) not in seen and t.numel() > 0:

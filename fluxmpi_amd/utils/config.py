@@ -142,6 +142,8 @@ class Config:
     debug_checks: bool = False
     timeout_s: float = 600.0
     force_comm: bool = False
+    # cross-rank structure check of functional reduction plans: always / first / never
+    check_plans: str = "always"
     extra: dict = field(default_factory=dict)
 
     @classmethod
@@ -164,6 +166,7 @@ class Config:
             debug_checks=_env_bool("FLUXMPI_DEBUG_CHECKS", False),
             timeout_s=_env_float("FLUXMPI_TIMEOUT_S", 600.0),
             force_comm=_env_bool("FLUXMPI_FORCE_COMM", bool(prefs.get("force_comm", False))),
+            check_plans=os.environ.get("FLUXMPI_CHECK_PLANS", str(prefs.get("check_plans", "always"))).lower(),
             extra=prefs,
         )
 

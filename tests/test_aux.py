@@ -188,3 +188,36 @@ def test_watchdog_abort_marks_comm():
     else:
         raise AssertionError
     wd.stop()
+
+
+def worker_calibrate_cpu():
+    """autotune.calibrate on 2 CPU ranks: the root's choice table (injected here, CPU ops measure
+    nothing) reaches every rank, the tables freeze, and no gradient collective was launched."""
+    import torch
+    import fluxmpi_amd as FluxMPI
+    from fluxmpi_amd import optimisers as O
+    from fluxmpi_amd.ops import fused_block
+    from fluxmpi_amd.parallel.autotune import calibrate
+    from fluxmpi_amd.parallel.ddp import DDP
+
+    FluxMPI.Init()
+    r = FluxMPI.local_rank()
+    m = torch.nn.Linear(4, 2)
+    ddp = DDP(m, O.Descent(0.1))
+
+    def fwd_bwd():
+        fused_block._FWD1_CHOICE[(256, 64, 56, 56, 256)] = r == 0  # "measured" on the root only
+        fused_block._WG_CHOICE[("3x3", (256, 64, 56, 56), 64)] = ("ours", (2, 512))
+        ddp(torch.ones(3, 4)).sum().backward()
+
+    calibrate(ddp, fwd_bwd)
+    assert ddp.collectives_launched == 0 and fused_block.choices_frozen()
+    assert fused_block._FWD1_CHOICE[(256, 64, 56, 56, 256)] is True
+    assert fused_block._WG_CHOICE[("3x3", (256, 64, 56, 56), 64)] == ("ours", (2, 512))
+    assert all(p.grad is None for p in m.parameters())  # calibration gradients discarded
+    fused_block.freeze_choices(False)
+    FluxMPI.Finalize()
+
+
+def test_calibrate_cpu(spmd):
+    spmd("tests.test_aux:worker_calibrate_cpu", nprocs=2, timeout=120)

@@ -304,3 +304,50 @@ def test_two_ranks_one_gpu_gloo_device(gpu_ext):
 
     run_spmd("tests.test_comm_gpu:worker_two_ranks_one_gpu", nprocs=2,
              env={"FLUXMPI_BACKEND": "gloo-device"}, timeout=240)
+
+
+def worker_calibrate_two_ranks():
+    """Rank-consistent kernel choices at N>1 (parallel/autotune.py): rank 0 measures during a
+    no_sync forward+backward with no gradient collective in flight, every rank ends with the
+    identical frozen table, and later steps add nothing rank-local to it."""
+    import torch.distributed as dist
+
+    import fluxmpi_amd as FluxMPI
+    from fluxmpi_amd import optimisers as O
+    from fluxmpi_amd.models.resnet import ResNet
+    from fluxmpi_amd.ops import fused_block
+    from fluxmpi_amd.parallel.autotune import calibrate
+    from fluxmpi_amd.parallel.ddp import DDP
+    from fluxmpi_amd.parallel.runtime import cpu_comm
+
+    FluxMPI.Init(gpu_devices=[0, 0])
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(5)
+    model = ResNet((1, 1, 1, 1), 10, conv_impl="hybrid", norm="fused").to(dev, memory_format=torch.channels_last)
+    for m in model.modules():
+        if not isinstance(m, torch.nn.modules.batchnorm._BatchNorm) and type(m).__name__ != "FusedBatchNorm2d":
+            for p in m.parameters(recurse=False):
+                p.data = p.data.to(torch.bfloat16)
+    ddp = DDP(model, O.Adam(1e-3), bucket_mb=0.5, first_bucket_mb=0.1, overlap=True)
+    x = torch.randn(8, 3, 64, 64, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (8,), device=dev)
+    assert not fused_block.dump_choices()  # nothing measured yet
+    recs = calibrate(ddp, lambda: F.cross_entropy(ddp(x).float(), y).backward())
+    assert ddp.collectives_launched == 0  # the table was fixed before any gradient collective
+    assert recs and fused_block.choices_frozen()
+    mine = sorted(fused_block.dump_choices())
+    everyone = [None, None]
+    dist.all_gather_object(everyone, mine, group=cpu_comm().group)
+    assert everyone[0] == everyone[1] == sorted(recs)
+    for _ in range(2):
+        F.cross_entropy(ddp(x).float(), y).backward()
+        ddp.step()
+    assert ddp.collectives_launched > 0 and sorted(fused_block.dump_choices()) == mine
+    FluxMPI.Finalize()
+
+
+def test_calibrate_two_ranks_one_gpu(gpu_ext):
+    from tests.conftest import run_spmd
+
+    run_spmd("tests.test_comm_gpu:worker_calibrate_two_ranks", nprocs=2,
+             env={"FLUXMPI_BACKEND": "gloo-device"}, timeout=240)

@@ -220,22 +220,42 @@ def test_ddp_step_without_zero_grad_rearms():
 
 
 def worker_ddp_no_zero_grad():
+    """``step(zero_grad=False)``: the next step applies the rank-sum of BOTH backwards'
+    gradients, S1 + S2 (SUM) or (S1 + S2) / W (average) — not W*S1 + S2 (VERDICT r2 repro:
+    Linear(4->1), x = rank+1, Descent(1.0) applied 9 instead of 6 at step 2)."""
     import fluxmpi_amd as FluxMPI
     from fluxmpi_amd import optimisers as O
     from fluxmpi_amd.parallel.ddp import DDP
     from fluxmpi_amd.utils.debug import check_replicas
 
     FluxMPI.Init()
-    r = FluxMPI.local_rank()
+    r, W = FluxMPI.local_rank(), FluxMPI.total_workers()
+    S = float(sum(k + 1 for k in range(W)))  # the per-step rank-sum of d(sum(w.x))/dw
     for grad_mode in ("steal", "view"):
-        m = _mlp(50 + r)
-        d = DDP(m, O.Adam(1e-2), bucket_mb=0.001, first_bucket_mb=0.0005, grad_mode=grad_mode)
-        x, y = _data(r)
-        for _ in range(3):
-            ((d(x) - y) ** 2).mean().backward()
-            d.step(zero_grad=False)
-            check_replicas(m)  # raises if a step applied local-only gradients
-        d.zero_grad()
+        for average in (False, True):
+            for overlap in (True, False):
+                m = torch.nn.Linear(4, 1, bias=False)
+                with torch.no_grad():
+                    m.weight.fill_(10.0)
+                d = DDP(m, O.Descent(1.0), grad_mode=grad_mode, average=average, overlap=overlap)
+                x = torch.full((1, 4), float(r + 1))
+                scale = 1.0 / W if average else 1.0
+                expect = 10.0
+                # zero_grad pattern: F F T T -> applied S, 2S, 3S, S
+                for k, zg in enumerate((False, False, True, True)):
+                    d(x).sum().backward()
+                    d.step(zero_grad=zg)
+                    expect -= scale * S * (k + 1 if k < 3 else 1)
+                    torch.testing.assert_close(m.weight.detach(), torch.full((1, 4), expect),
+                                               msg=f"{grad_mode} avg={average} ov={overlap} step {k}")
+                    check_replicas(m)
+                # a step with no backward after step(zero_grad=False) applies the carried sum again
+                d(x).sum().backward()
+                d.step(zero_grad=False)
+                expect -= scale * S
+                d.step()
+                expect -= scale * S
+                torch.testing.assert_close(m.weight.detach(), torch.full((1, 4), expect))
     FluxMPI.Finalize()
 
 
@@ -320,3 +340,50 @@ def test_ddp_optimiser_state_channels_last():
     for n in ps:
         torch.testing.assert_close(state[n].state[0], st[n].state[0], rtol=1e-4, atol=1e-7)
         torch.testing.assert_close(state[n].state[1], st[n].state[1], rtol=1e-4, atol=1e-9)
+
+
+def worker_ddp_master_sync():
+    """``synchronize`` of DDP-managed bf16 params must leave the fp32 masters
+    identical on every rank — through the engine (``synchronize(model)``) and through a plain
+    tensor tree (``synchronize(params)``), with small buckets so some leaves are "direct"
+    (reduced/broadcast in place, no pack kernel)."""
+    import fluxmpi_amd as FluxMPI
+    from fluxmpi_amd import optimisers as O
+    from fluxmpi_amd.parallel.ddp import DDP
+    from fluxmpi_amd.utils.debug import check_replicas
+
+    FluxMPI.Init()
+    r = FluxMPI.local_rank()
+    for how in ("module", "tree", "flux_model"):
+        m = _mlp(3).to(torch.bfloat16)
+        d = DDP(m, O.Adam(1e-2), master_weights=True, bucket_mb=0.0005, first_bucket_mb=0.0002)
+        assert all(b.master is not None for b in d.buckets)
+        # ranks drift apart (e.g. a rank-local edit): rank r's params move by r * 1e-2 + tiny
+        with torch.no_grad():
+            for p in m.parameters():
+                p.add_(r * 1e-2 + 1e-4 * torch.randn_like(p))
+        d.refresh_master()  # the edits are "known": only the synchronize below changes params
+        with torch.no_grad():
+            for b in d.buckets:  # and the masters hold bits the bf16 params cannot show
+                for p, o in zip(b.params, b.offsets):
+                    b.master[o:o + p.numel()] += 1e-5 * (r + 1)
+        if how == "module":
+            FluxMPI.synchronize(m)
+        elif how == "flux_model":
+            FluxMPI.synchronize(FluxMPI.FluxMPIFluxModel(m))
+        else:
+            FluxMPI.synchronize({n: p for n, p in m.named_parameters()})
+        x, y = _data(r)
+        for _ in range(3):
+            ((d(x.bfloat16()) - y.bfloat16()) ** 2).mean().backward()
+            d.step()
+        check_replicas(m)
+        for b in d.buckets:
+            for p, o in zip(b.params, b.offsets):  # the slices (alignment padding is never used)
+                g = FluxMPI.allgather(b.master[o:o + p.numel()].clone())
+                assert torch.equal(g[0], g[1]), how
+    FluxMPI.Finalize()
+
+
+def test_ddp_master_sync_gloo(spmd):
+    spmd("tests.test_ddp:worker_ddp_master_sync", nprocs=2, timeout=120)

@@ -93,3 +93,51 @@ def test_op_coercion():
     import pytest
     with pytest.raises(ValueError):
         to_op("xor")
+
+
+def worker_rccl_bootstrap():
+    """The N>1 RCCL bootstrap logic on CPU (no GPU, no RCCL): rank 0's unique id reaches every
+    rank through the host store, and each Init generation (Init -> Finalize -> Init on a
+    surviving store) gets a fresh id — a late rank can never pick up the previous one."""
+    import os
+    import time
+
+    import torch.distributed as dist
+
+    import fluxmpi_amd as FluxMPI
+    from fluxmpi_amd.parallel.comm import bootstrap_unique_id
+
+    FluxMPI.Init()
+    r, W = FluxMPI.local_rank(), FluxMPI.total_workers()
+    store = dist.distributed_c10d._get_default_store()
+    made = []
+
+    def make_uid():  # the ncclGetUniqueId stand-in: only rank 0 may call it
+        assert r == 0
+        made.append(os.urandom(128))
+        return made[-1]
+
+    seen = []
+    for gen in range(3):
+        if r == W - 1:
+            time.sleep(0.2 * gen)  # a straggler: the others already wait on the next generation
+        uid = bootstrap_unique_id(make_uid, store, r, W, tag="test")
+        assert isinstance(uid, bytes) and len(uid) == 128
+        seen.append(uid)
+        store.set(f"check/{gen}/{r}", uid)
+        FluxMPI.barrier()  # ncclCommInitRank is collective: generation k ends on every rank first
+    assert len(set(seen)) == 3  # a new id per generation
+    for gen in range(3):
+        ids = {bytes(store.get(f"check/{gen}/{k}")) for k in range(W)}
+        assert ids == {seen[gen]}  # every rank got rank 0's id of that generation
+    if r == 0:
+        assert made == seen
+    # another tag is an independent sequence
+    other = bootstrap_unique_id(make_uid, store, r, W, tag="other")
+    assert other not in seen
+    FluxMPI.barrier()
+    FluxMPI.Finalize()
+
+
+def test_rccl_bootstrap_cpu(spmd):
+    spmd("tests.test_mpi_extensions:worker_rccl_bootstrap", nprocs=3, timeout=120)

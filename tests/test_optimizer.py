@@ -84,3 +84,32 @@ def worker_buckets():
 
 def test_bucketed_collectives(spmd):
     spmd("tests.test_optimizer:worker_buckets", nprocs=3)
+
+
+def test_hyperparameters_cast_to_leaf_precision():
+    """Optimisers.jl converts η, β, ϵ to ``eltype(x)`` (``T(η)``): bf16 / fp16 leaves see the
+    rounded values. Parity unpinned against Julia itself (not installed);
+    the expected numbers are the IEEE / bfloat16 roundings."""
+    import torch
+    from fluxmpi_amd import optimisers as O
+    from fluxmpi_amd.optimisers import _T
+
+    bf, hf, f32, f64 = (torch.zeros(2, dtype=d) for d in (torch.bfloat16, torch.float16, torch.float32,
+                                                           torch.float64))
+    assert _T(bf, 0.9) == 0.8984375 and _T(bf, 0.999) == 1.0
+    assert _T(hf, 0.9) == 0.89990234375 and _T(hf, 0.999) == 0.9990234375
+    assert _T(hf, 1e-8) == 0.0  # below fp16's smallest subnormal, as Float16(1e-8) in Julia
+    assert _T(f32, 0.1) == float(torch.tensor(0.1, dtype=torch.float32)) and _T(f64, 0.1) == 0.1
+    st = O.setup(O.Adam(1e-3), {"a": hf, "b": f64})
+    assert st["a"].state[2] == (0.89990234375, 0.9990234375)
+    assert st["b"].state[2] == (0.9, 0.999)
+    # one fp16 Adam step: the bias corrections use the rounded beta^t
+    x = torch.ones(4, dtype=torch.float16)
+    st = O.setup(O.Adam(0.5), x)
+    g = torch.full((4,), 0.25, dtype=torch.float16)
+    st, x2 = O.update(st, x, g)
+    b1, b2 = 0.89990234375, 0.9990234375
+    m, v = (1 - b1) * 0.25, (1 - b2) * 0.0625
+    step = m / (1 - b1) / ((v / (1 - b2)) ** 0.5 + 0.0) * 0.5
+    torch.testing.assert_close(x2.float(), torch.full((4,), 1.0 - step), rtol=2e-3, atol=2e-3)
+    assert st.state[2] == (_T(x, b1 * b1), _T(x, b2 * b2))
