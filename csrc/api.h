@@ -223,6 +223,15 @@ bool wgrad256_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ld
 int wgrad256_actual_splits(int64_t K, int splits);
 void gemm_wgrad256(const void* a, const void* b, float* ws, int64_t lda, int64_t ldb, int64_t M, int64_t N, int64_t K,
                    int splits, hipStream_t stream);
+// Token-major Linear GEMM on 256 x 256 tiles (gemm256.hip): C[M][N] = A[M][K] (b_t ? B[K][N] : B[N][K]^T)
+// with epilogue epi 0 (+ bias), 1 (+ bias, C = h, C2 = gelu(h)), 2 (C = bf16(acc) * gelu'(h),
+// colpart[2 * M / 256][N] = per-half-tile column sums of C; needs b_t).
+bool gemm256_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, bool b_t);
+int gemm256_colpart_rows(int64_t M);
+void gemm256_set_bk(int bk);  // pipeline depth variant (32: 4 x 32-deep stages, 64: 2 x 64-deep); A/B runs
+void gemm256(const void* a, const void* b, void* c, void* c2, const void* bias, int bias_f32, const void* h,
+             float* colpart, int64_t lda, int64_t ldb, int64_t ldc, int64_t M, int64_t N, int64_t K, bool b_t,
+             int epi, hipStream_t stream);
 
 // ---- Anderson-acceleration solver (DEQ) --------------------------------------------
 // X, F: fp32 histories [bsz][m rows of row_stride][d] (batch_stride between batches).

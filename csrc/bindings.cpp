@@ -247,6 +247,16 @@ PYBIND11_MODULE(_C, m) {
     gemm_wgrad256(reinterpret_cast<const void*>(a), reinterpret_cast<const void*>(b), reinterpret_cast<float*>(ws), lda,
                   ldb, M, N, K, splits, S(stream));
   });
+  m.def("gemm256_supported", &gemm256_supported);
+  m.def("gemm256_colpart_rows", &gemm256_colpart_rows);
+  m.def("gemm256_set_bk", &gemm256_set_bk);
+  m.def("gemm256", [](uintptr_t a, uintptr_t b, uintptr_t c, uintptr_t c2, uintptr_t bias, int bias_f32, uintptr_t h,
+                      uintptr_t colpart, int64_t lda, int64_t ldb, int64_t ldc, int64_t M, int64_t N, int64_t K,
+                      bool b_t, int epi, uintptr_t stream) {
+    gemm256(reinterpret_cast<const void*>(a), reinterpret_cast<const void*>(b), reinterpret_cast<void*>(c),
+            reinterpret_cast<void*>(c2), reinterpret_cast<const void*>(bias), bias_f32, reinterpret_cast<const void*>(h),
+            reinterpret_cast<float*>(colpart), lda, ldb, ldc, M, N, K, b_t, epi, S(stream));
+  });
   m.def("colsum", [](uintptr_t x, uintptr_t part, int blocks, int64_t rows, int64_t N, int dtype, uintptr_t stream) {
     colsum(reinterpret_cast<const void*>(x), reinterpret_cast<float*>(part), blocks, rows, N, dtype, S(stream));
   });

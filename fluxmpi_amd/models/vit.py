@@ -21,13 +21,15 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.gelu import linear_gelu
+from ..ops.gelu import GeluLink, linear_gelu
 from ..ops.layernorm import linear_add_layer_norm
 from ..ops.linear import Linear
 
 # FLUXMPI_VIT_FUSED_GELU=0: autograd's GELU backward + separate bias reduction (A/B runs)
 _FUSED_GELU = os.environ.get("FLUXMPI_VIT_FUSED_GELU", "1") != "0"
 _FUSED_PROJ_LN = os.environ.get("FLUXMPI_VIT_FUSED_PROJ_LN", "1") != "0"
+# FLUXMPI_VIT_CLS_ONLY=0: the last block's MLP over every token (A/B runs; same result)
+_CLS_ONLY = os.environ.get("FLUXMPI_VIT_CLS_ONLY", "1") != "0"
 
 
 class PatchEmbed(nn.Module):
@@ -131,23 +133,30 @@ class Block(nn.Module):
         self.fc2 = Linear(mlp, dim)
 
     @staticmethod
-    def _add_ln(ln, x, a, lin):
+    def _add_ln(ln, x, a, lin, link=None):
         """``(x + lin(a), ln(x + lin(a)))``."""
         if _FUSED_PROJ_LN:
-            return linear_add_layer_norm(a, lin.weight, lin.bias, x, ln.weight, ln.bias, ln.eps)
+            return linear_add_layer_norm(a, lin.weight, lin.bias, x, ln.weight, ln.bias, ln.eps, gelu_link=link)
         return ln.add_forward(x, lin(a))
 
-    def forward(self, x, pend=None):
+    def forward(self, x, pend=None, cls_only=False):
+        """``cls_only`` (the last block): only the [CLS] token's residual stream reaches the head,
+        so after attention (which needs every token's keys / values) proj, ln2, fc1, GELU and fc2
+        run on that token alone — exact, and ~1/13 of the step's GEMM FLOPs saved."""
         h = self.heads
         if pend is None:
             y = self.ln1(x)
         else:
             x, y = self._add_ln(self.ln1, x, *pend)  # x <- x + fc2(g) (previous block's MLP branch)
         a = packed_attention(self.qkv(y), h)
+        if cls_only:
+            x, a = x[:, 0], a[:, 0].contiguous()
         x, y = self._add_ln(self.ln2, x, a, self.proj)
-        # fc1 + GELU: GELU backward and fc1's bias gradient in one pass (ops/gelu.py)
-        g = linear_gelu(y, self.fc1.weight, self.fc1.bias) if _FUSED_GELU else F.gelu(self.fc1(y))
-        return x, (g, self.fc2)
+        # fc1 + GELU: the GELU derivative and fc1's bias gradient come out of the consumer's
+        # (the next ln1 node's fc2) input-gradient GEMM through the link (ops/gelu.py)
+        link = GeluLink() if (_FUSED_GELU and not cls_only) else None
+        g = linear_gelu(y, self.fc1.weight, self.fc1.bias, link=link) if _FUSED_GELU else F.gelu(self.fc1(y))
+        return x, (g, self.fc2, link)
 
 
 class ViT(nn.Module):
@@ -169,14 +178,15 @@ class ViT(nn.Module):
         x = self.embed(x)
         x = torch.cat([self.cls.expand(x.shape[0], -1, -1).to(x.dtype), x], 1) + self.pos.to(x.dtype)
         pend = None
-        for blk in self.blocks:
-            x, pend = blk(x, pend)
+        last = len(self.blocks) - 1
+        for i, blk in enumerate(self.blocks):
+            x, pend = blk(x, pend, cls_only=_CLS_ONLY and i == last)
         # only the [CLS] token reaches the head: finish its residual stream and normalise it alone
         if pend is None:
             c = x[:, 0]
         else:
-            g, fc2 = pend
-            c = x[:, 0] + fc2(g)[:, 0]
+            g, fc2, _ = pend
+            c = x + fc2(g) if x.dim() == 2 else x[:, 0] + fc2(g)[:, 0]
         return self.head(self.ln(c))
 
 

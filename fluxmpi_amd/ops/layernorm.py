@@ -156,8 +156,10 @@ class _LinearAddLayerNormFn(torch.autograd.Function):
     kernel over dx; the weight gradient runs on the split-K HIP kernel (ops/linear.py)."""
 
     @staticmethod
-    def forward(ctx, a, weight, bias, x, ln_w, ln_b, eps):
-        p = F.linear(a, weight, bias)
+    def forward(ctx, a, weight, bias, x, ln_w, ln_b, eps, gelu_link=None):
+        from .linear import fwd
+        p = fwd(a, weight, bias)
+        ctx.gelu_link = gelu_link
         x = x.contiguous()
         w, b = _affine(x, ln_w, ln_b)
         h, y, mean, rstd = _fwd(x, p.contiguous(), w, b, eps)
@@ -178,20 +180,34 @@ class _LinearAddLayerNormFn(torch.autograd.Function):
         n_out, n_in = weight.shape
         g2 = dx.reshape(-1, n_out)
         a2 = a.reshape(-1, n_in)
-        da = (g2 @ weight).reshape(a.shape) if ctx.needs_input_grad[0] else None
+        da = None
+        if ctx.needs_input_grad[0]:
+            from . import gemm256
+            from .linear import dgrad
+            link = ctx.gelu_link
+            if (link is not None and link.h is not None and link.h.shape == a.shape
+                    and gemm256.supported(g2.shape[0], n_in, n_out, g2, weight, link.h, b_t=True, fused=True)):
+                # `a` = gelu(h) of the linear_gelu node upstream: its GELU derivative and its bias
+                # gradient come out of this input-gradient GEMM's epilogue (gemm256.hip EPI 2)
+                link.dh, link.db = gemm256.linear_dgrad(g2, weight, gelu_h=link.h, bias_dtype=link.bias_dtype)
+                da = torch.zeros((), device=a.device, dtype=a.dtype).expand(a.shape)  # placeholder, never read
+            else:
+                da = dgrad(g2, weight).reshape(a.shape)
         dw = None
         if ctx.needs_input_grad[1]:
             dw = weight_grad(g2, a2, weight.dtype) if native_ok(a2, g2) else g2.t() @ a2
-        return da, dw, (dbias if ctx.needs_input_grad[2] else None), dx, dlw, dlb, None
+        return da, dw, (dbias if ctx.needs_input_grad[2] else None), dx, dlw, dlb, None, None
 
 
-def linear_add_layer_norm(a, weight, bias, x, ln_w, ln_b, eps=1e-5):
+def linear_add_layer_norm(a, weight, bias, x, ln_w, ln_b, eps=1e-5, gelu_link=None):
     """``(h, layer_norm(h))`` with ``h = x + F.linear(a, weight, bias)`` (see
-    :class:`_LinearAddLayerNormFn`); the PyTorch composition off the fused path."""
+    :class:`_LinearAddLayerNormFn`); the PyTorch composition off the fused path. ``gelu_link``
+    (:class:`ops.gelu.GeluLink`): ``a`` is ``linear_gelu(..., link=gelu_link)``'s output, whose
+    GELU backward this node's input-gradient GEMM then performs."""
     if (supported(x) and bias is not None and a.is_contiguous() and a.shape[:-1] == x.shape[:-1]
             and weight.shape[0] == x.shape[-1] and a.dtype == x.dtype == weight.dtype and torch.is_grad_enabled()
             and (ln_w is None or ln_w.shape[-1] == x.shape[-1])):
-        return _LinearAddLayerNormFn.apply(a, weight, bias, x, ln_w, ln_b, eps)
+        return _LinearAddLayerNormFn.apply(a, weight, bias, x, ln_w, ln_b, eps, gelu_link)
     from .linear import linear
     return add_layer_norm(x, linear(a, weight, bias), ln_w, ln_b, eps)
 

@@ -1,7 +1,8 @@
-"""``nn.Linear`` for token-major activations with MI355X-shaped backward GEMMs.
+"""``nn.Linear`` for token-major activations with MI355X-shaped GEMMs.
 
-Forward and input gradient stay on hipBLASLt (``F.linear``, ``dy @ W``: M = tokens is
-large, plenty of 256x256 tiles). The weight gradient ``dW = dY^T X`` is the awkward one:
+Forward and input gradient run on ``gemm256.hip`` (256x256 tiles, LDS-DMA ring, bias in the
+epilogue; ``ops/gemm256.py``) when the token count and widths tile exactly (ViT-B/16: 50432 =
+197 x 256 tokens), else hipBLASLt (``F.linear``, ``dy @ W``). The weight gradient ``dW = dY^T X`` is the awkward one:
 K = tokens (50432 for ViT-B/16 at batch 256) and a small output (768..3072 squared), so
 hipBLASLt's 256x256 tiles leave most of the 256 CUs idle (36-108 workgroups; 312-431 us
 per call, ``profiles/r1_vit_b16_s61_steady.md``). It runs on our split-K MFMA kernels
@@ -95,7 +96,7 @@ class _LinearFn(torch.autograd.Function):
         ctx.has_bias = bias is not None
         ctx.bias_dtype = bias.dtype if bias is not None else None
         ctx.bias = bias  # the leaf itself (not saved data): streams.run checks its .grad
-        return F.linear(x, weight, bias)
+        return fwd(x, weight, bias)
 
     @staticmethod
     def backward(ctx, dy):
@@ -120,8 +121,27 @@ class _LinearFn(torch.autograd.Function):
             # both parameters: if either already holds a .grad, autograd accumulates into it on
             # the main stream, which must not race a side-stream producer
             dw, db = streams.run(grads, dy2, x2, param=[w if need_w else None, ctx.bias if need_b else None])
-        dx = (dy2 @ w).reshape(x.shape) if ctx.needs_input_grad[0] else None
+        dx = dgrad(dy2, w).reshape(x.shape) if ctx.needs_input_grad[0] else None
         return dx, dw, db
+
+
+def fwd(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None) -> torch.Tensor:
+    """``F.linear`` — on gemm256.hip (bias in the epilogue) when the shape tiles exactly."""
+    from . import gemm256
+    n_out, n_in = weight.shape
+    rows = x.numel() // n_in if n_in else 0
+    if x.is_contiguous() and gemm256.supported(rows, n_out, n_in, x, weight):
+        return gemm256.linear_fwd(x.view(rows, n_in), weight, bias).view(*x.shape[:-1], n_out)
+    return F.linear(x, weight, bias)
+
+
+def dgrad(dy2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """``dy2 [rows, N_out] @ weight [N_out, N_in]`` — on gemm256.hip when the shape tiles exactly."""
+    from . import gemm256
+    n_out, n_in = weight.shape
+    if dy2.is_contiguous() and gemm256.supported(dy2.shape[0], n_in, n_out, dy2, weight, b_t=True):
+        return gemm256.linear_dgrad(dy2, weight)
+    return dy2 @ weight
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
@@ -138,4 +158,4 @@ class Linear(torch.nn.Linear):
         return linear(x, self.weight, self.bias)
 
 
-__all__ = ["linear", "Linear", "weight_grad", "bias_grad", "native_ok"]
+__all__ = ["linear", "Linear", "weight_grad", "bias_grad", "native_ok", "fwd", "dgrad"]

@@ -169,6 +169,15 @@ class _StreamWork(Work):
     def is_completed(self) -> bool:
         return self.event.query()
 
+    def covered(self):
+        """The caller's stream already waits on a LATER collective of the same (in-order) comm
+        stream: this one is complete by then, so skip its own fence (post-processing still runs)."""
+        if not self._waited:
+            if self._post is not None:
+                self._post()
+            self._waited = True
+        return self.result
+
     def synchronize(self):
         self.wait()
         self.event.synchronize()
@@ -457,6 +466,8 @@ class RcclComm(Communicator):
     """
 
     name = "rccl"
+    # every collective runs on ONE stream, in issue order: a wait on the newest covers the rest
+    in_order = True
 
     def __init__(self, rank: int, size: int, device: torch.device, store=None, tag: str = "world"):
         super().__init__(rank, size)

@@ -136,6 +136,7 @@ class Config:
     host_staged: bool = False  # reference's CUDA-unaware path (Q1), debug only
     bucket_mb: float = 16.0
     first_bucket_mb: float = 4.0
+    tail_bucket_mb: float = 2.0  # the last-closing bucket is tapered to this (0: off), ddp._taper
     comm_dtype: str = "native"
     overlap: bool = True
     profile: bool = False
@@ -160,6 +161,7 @@ class Config:
             host_staged=bool(prefs.get(PREF_DISABLE_KEY, False)),
             bucket_mb=_env_float("FLUXMPI_BUCKET_MB", float(prefs.get("bucket_mb", 16.0))),
             first_bucket_mb=_env_float("FLUXMPI_FIRST_BUCKET_MB", float(prefs.get("first_bucket_mb", 4.0))),
+            tail_bucket_mb=_env_float("FLUXMPI_TAIL_BUCKET_MB", float(prefs.get("tail_bucket_mb", 2.0))),
             comm_dtype=os.environ.get("FLUXMPI_COMM_DTYPE", prefs.get("comm_dtype", "native")).lower(),
             overlap=_env_bool("FLUXMPI_OVERLAP", bool(prefs.get("overlap", True))),
             profile=_env_bool("FLUXMPI_PROFILE", False),
