@@ -228,7 +228,8 @@ void gemm_wgrad256(const void* a, const void* b, float* ws, int64_t lda, int64_t
 // colpart[2 * M / 256][N] = per-half-tile column sums of C; needs b_t).
 bool gemm256_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, bool b_t);
 int gemm256_colpart_rows(int64_t M);
-void gemm256_set_bk(int bk);  // pipeline depth variant (32: 4 x 32-deep stages, 64: 2 x 64-deep); A/B runs
+void gemm256_set_bk(int bk);
+void gemm256_set_var(int v);  // main-loop schedule variant (gemm256.hip VAR bits); A/B runs  // pipeline depth variant (32: 4 x 32-deep stages, 64: 2 x 64-deep); A/B runs
 void gemm256(const void* a, const void* b, void* c, void* c2, const void* bias, int bias_f32, const void* h,
              float* colpart, int64_t lda, int64_t ldb, int64_t ldc, int64_t M, int64_t N, int64_t K, bool b_t,
              int epi, hipStream_t stream);

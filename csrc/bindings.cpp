@@ -250,6 +250,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm256_supported", &gemm256_supported);
   m.def("gemm256_colpart_rows", &gemm256_colpart_rows);
   m.def("gemm256_set_bk", &gemm256_set_bk);
+  m.def("gemm256_set_var", &gemm256_set_var);
   m.def("gemm256", [](uintptr_t a, uintptr_t b, uintptr_t c, uintptr_t c2, uintptr_t bias, int bias_f32, uintptr_t h,
                       uintptr_t colpart, int64_t lda, int64_t ldb, int64_t ldc, int64_t M, int64_t N, int64_t K,
                       bool b_t, int epi, uintptr_t stream) {

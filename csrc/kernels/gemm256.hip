@@ -96,7 +96,12 @@ struct G256Args {
   int bias_f32;
 };
 
-template <bool B_T, int EPI, int kBK, int kST>
+// VAR bit 0: the next step's LDS-DMA is issued spread through this step's MFMAs (one piece per
+// four MFMAs) instead of in one burst after the barrier, so its issue cost (~60 cycles a piece)
+// overlaps the partner wave's matrix work; bit 1: waves 4-7 at s_setprio 1 for the whole loop
+// (the static form of cdna_hip_programming.md T5: the younger half stops losing arbitration);
+// bit 2: s_setprio 1 around each MFMA cluster.
+template <bool B_T, int EPI, int kBK, int kST, int VAR = 0>
 __global__ __launch_bounds__(kThreads, 2) void gemm256_kernel(G256Args p) {
   constexpr int kImg = kTile * kBK * 2;   // bytes per operand image (16 / 32 KiB)
   constexpr int kStage = 2 * kImg;
@@ -141,20 +146,26 @@ __global__ __launch_bounds__(kThreads, 2) void gemm256_kernel(G256Args p) {
     }
   }
   const int64_t stepB = B_T ? static_cast<int64_t>(kBK) * p.ldb : kBK;
-  auto issue = [&](int t) {
+  // DMA instruction q (0 .. kG-1) of step t: even q = A piece q/2, odd q = B piece q/2
+  auto issue_piece = [&](int t, int q) {
     char* st = smem + (t % kST) * kStage;
-#pragma unroll
-    for (int j = 0; j < kP; ++j) {
-      // K tail (K % 32 != 0): chunks past K read zeros (both operands, so the products vanish)
+    const int j = q >> 1;
+    // K tail (K % 32 != 0): chunks past K read zeros (both operands, so the products vanish)
+    if ((q & 1) == 0) {
       const bool oka = t * kBK + kq[j] < p.K;
-      const bool okb = B_T ? t * kBK + kr[j] < p.K : oka;
       const void* sa = oka ? static_cast<const void*>(pa[j]) : static_cast<const void*>(g_zero_g256);
-      const void* sb = okb ? static_cast<const void*>(pb[j]) : static_cast<const void*>(g_zero_g256);
       __builtin_amdgcn_global_load_lds((gl_void*)(sa), (lds_char*)(st + (wave * kP + j) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((gl_void*)(sb), (lds_char*)(st + kImg + (wave * kP + j) * 1024), 16, 0, 0);
       pa[j] += kBK;
+    } else {
+      const bool okb = B_T ? t * kBK + kr[j] < p.K : t * kBK + kq[j] < p.K;
+      const void* sb = okb ? static_cast<const void*>(pb[j]) : static_cast<const void*>(g_zero_g256);
+      __builtin_amdgcn_global_load_lds((gl_void*)(sb), (lds_char*)(st + kImg + (wave * kP + j) * 1024), 16, 0, 0);
       pb[j] += stepB;
     }
+  };
+  auto issue = [&](int t) {
+#pragma unroll
+    for (int q = 0; q < kG; ++q) issue_piece(t, q);
   };
 
   // ---- fragment offsets (bytes within an image)
@@ -197,13 +208,17 @@ __global__ __launch_bounds__(kThreads, 2) void gemm256_kernel(G256Args p) {
 #pragma unroll
   for (int t = 0; t < kST - 1; ++t)
     if (t < nk) issue(t);
+  if ((VAR & 2) && __builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+  // VAR & 1: piece g (0 .. kG-1) of the next step's DMA goes out before i-group g of the MFMAs
+  constexpr int kGroups = (kBK / 32) * 8;  // (kh, i) fragment groups of 4 MFMAs per step
   for (int t = 0; t < nk; ++t) {
     const int ahead = nk - 1 - t;
     if (kST >= 4 && ahead >= 2) wait_vm<(kST >= 4 ? 2 : 0) * kG>();
     else if (kST >= 3 && ahead >= 1) wait_vm<(kST >= 3 ? 1 : 0) * kG>();
     else wait_vm<0>();
     __builtin_amdgcn_s_barrier();
-    if (t + kST - 1 < nk) issue(t + kST - 1);
+    const bool pre = t + kST - 1 < nk;
+    if (!(VAR & 1) && pre) issue(t + kST - 1);
     const char* ta = smem + (t % kST) * kStage;
     const char* tb = ta + kImg;
 #pragma unroll
@@ -215,8 +230,14 @@ __global__ __launch_bounds__(kThreads, 2) void gemm256_kernel(G256Args p) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const bf16x8 fa = frag_k(ta, offA0 + i * 16 * (kBK * 2) + slot[kh]);
+        if (VAR & 1) {
+          const int g = kh * 8 + i;  // spread the kG pieces evenly over the kGroups groups
+          if (pre && (g * kG) % kGroups < kG) issue_piece(t + kST - 1, (g * kG) / kGroups);
+        }
+        if (VAR & 4) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa, acc[i][j], 0, 0, 0);
+        if (VAR & 4) __builtin_amdgcn_s_setprio(0);
       }
     }
   }
@@ -307,17 +328,37 @@ __global__ __launch_bounds__(kThreads, 2) void gemm256_kernel(G256Args p) {
   }
 }
 
-template <bool B_T, int EPI, int BK>
-void launch_bk(const G256Args& p, hipStream_t stream) {
+template <bool B_T, int EPI, int BK, int VAR>
+void launch_v(const G256Args& p, hipStream_t stream) {
   constexpr int ST = BK == 32 ? 4 : 2;
   static bool attr = false;
   if (!attr) {
-    FLUXMPI_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm256_kernel<B_T, EPI, BK, ST>),
+    FLUXMPI_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm256_kernel<B_T, EPI, BK, ST, VAR>),
                                           hipFuncAttributeMaxDynamicSharedMemorySize, kSmem));
     attr = true;
   }
-  gemm256_kernel<B_T, EPI, BK, ST><<<p.tiles_m * p.tiles_n, kThreads, kSmem, stream>>>(p);
+  gemm256_kernel<B_T, EPI, BK, ST, VAR><<<p.tiles_m * p.tiles_n, kThreads, kSmem, stream>>>(p);
   FLUXMPI_HIP_CHECK(hipGetLastError());
+}
+
+int g_var = -1;
+int var() {
+  if (g_var < 0) {
+    const char* e = std::getenv("FLUXMPI_GEMM256_VAR");
+    g_var = e != nullptr ? (std::atoi(e) & 7) : 0;
+  }
+  return g_var;
+}
+
+template <bool B_T, int EPI, int BK>
+void launch_bk(const G256Args& p, hipStream_t stream) {
+  switch (var()) {
+    case 1: launch_v<B_T, EPI, BK, 1>(p, stream); break;
+    case 2: launch_v<B_T, EPI, BK, 2>(p, stream); break;
+    case 3: launch_v<B_T, EPI, BK, 3>(p, stream); break;
+    case 5: launch_v<B_T, EPI, BK, 5>(p, stream); break;
+    default: launch_v<B_T, EPI, BK, 0>(p, stream); break;
+  }
 }
 
 // pipeline: FLUXMPI_GEMM256_BK = 32 (four 32-deep stages, three in flight) or 64 (default: two
@@ -349,6 +390,7 @@ bool gemm256_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb
 int gemm256_colpart_rows(int64_t M) { return static_cast<int>(2 * (M / kTile)); }
 
 void gemm256_set_bk(int bk_) { g_bk = bk_ == 32 ? 32 : 64; }
+void gemm256_set_var(int v) { g_var = v & 7; }
 
 void gemm256(const void* a, const void* b, void* c, void* c2, const void* bias, int bias_f32, const void* h,
              float* colpart, int64_t lda, int64_t ldb, int64_t ldc, int64_t M, int64_t N, int64_t K, bool b_t,
