@@ -146,11 +146,16 @@ def main():
     x = x.contiguous(memory_format=memfmt)
     y = torch.randint(0, ncls, (B,), device=dev, generator=gx)
 
+    deq = getattr(model, "deq", None)  # DEQ: solver iterations per step are reported with the rate
+    iters: list = []
+
     def step():
         out = ddp(x)
         loss = F.cross_entropy(out.float(), y)
         loss.backward()
         ddp.step()
+        if deq is not None:
+            iters.append((deq.last_iters, deq.last_bwd_iters))
         return loss
 
     calibrated = False
@@ -175,12 +180,14 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    iters.clear()
     FluxMPI.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
     t_host = time.perf_counter() - t0  # the host's enqueue time: ~wall when launch-bound
+    timed_iters = list(iters[:args.steps])
     torch.cuda.synchronize()
     FluxMPI.barrier()
     dt = time.perf_counter() - t0
@@ -226,7 +233,10 @@ def main():
                        # (overlap false, comm "none") unless --force-comm
                        **cs, "exposed_comm_ms": None if exposed is None else round(exposed, 3),
                        **({"emulate_comm": args.emulate_comm} if args.emulate_comm else {}),
-                       "grid_rounds": int(os.environ.get("FLUXMPI_GRID_ROUNDS", "1"))},
+                       "grid_rounds": int(os.environ.get("FLUXMPI_GRID_ROUNDS", "1")),
+                       **({"deq_fwd_iters_per_step": round(sum(i[0] for i in timed_iters) / len(timed_iters), 2),
+                           "deq_bwd_iters_per_step": round(sum(i[1] for i in timed_iters) / len(timed_iters), 2)}
+                          if timed_iters else {})},
         }
         print(json.dumps(rec), flush=True)
     FluxMPI.Finalize()

@@ -100,7 +100,11 @@ struct G256Args {
 // four MFMAs) instead of in one burst after the barrier, so its issue cost (~60 cycles a piece)
 // overlaps the partner wave's matrix work; bit 1: waves 4-7 at s_setprio 1 for the whole loop
 // (the static form of cdna_hip_programming.md T5: the younger half stops losing arbitration);
-// bit 2: s_setprio 1 around each MFMA cluster.
+// bit 2: s_setprio 1 around each MFMA cluster; bit 3 (kST == 2 only): the A operand of the next
+// step goes global -> VGPRs (4 x 16 B per lane, issued after the barrier) and is written to LDS
+// with ds_write_b128 after this step's MFMAs — half the bytes leave the LDS-DMA path, whose
+// chip-wide rate (~6.4 TB/s measured for streams, MI355X_MICROARCH.md ldsdma-fill) caps the
+// all-DMA loop near 0.8 PF/s at 128 FLOP per staged byte.
 template <bool B_T, int EPI, int kBK, int kST, int VAR = 0>
 __global__ __launch_bounds__(kThreads, 2) void gemm256_kernel(G256Args p) {
   constexpr int kImg = kTile * kBK * 2;   // bytes per operand image (16 / 32 KiB)
@@ -167,6 +171,28 @@ __global__ __launch_bounds__(kThreads, 2) void gemm256_kernel(G256Args p) {
 #pragma unroll
     for (int q = 0; q < kG; ++q) issue_piece(t, q);
   };
+  // AREG: A of a step as 4 x 16 B per lane (chunk c = tid + 512 i: row c / kCPR, k chunk c % kCPR;
+  // 8 lanes per 128-B row, coalesced), written to the same swizzled image the DMA would fill
+  constexpr bool AREG = (VAR & 8) && kST == 2;
+  constexpr int kAR = AREG ? kImg / 16 / kThreads : 1;
+  uint4 areg[kAR];
+  auto load_a_regs = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < kAR; ++i) {
+      const int c = threadIdx.x + kThreads * i, row = c / kCPR, kc = c % kCPR;
+      const int64_t k = static_cast<int64_t>(t) * kBK + kc * 8;
+      const bf16* src = k < p.K ? p.a + (m0 + row) * p.lda + k : reinterpret_cast<const bf16*>(g_zero_g256);
+      areg[i] = *reinterpret_cast<const uint4*>(src);
+    }
+  };
+  auto store_a_regs = [&](int t) {
+    char* img = smem + (t % kST) * kStage;
+#pragma unroll
+    for (int i = 0; i < kAR; ++i) {
+      const int c = threadIdx.x + kThreads * i, row = c / kCPR, kc = c % kCPR;
+      *reinterpret_cast<uint4*>(img + row * (kBK * 2) + ((kc ^ swz_k<kBK>(row)) << 4)) = areg[i];
+    }
+  };
 
   // ---- fragment offsets (bytes within an image)
   // k-contiguous: lane reads row r0 + (lane & 15), k chunk (lane >> 4) + 4 kh at slot chunk ^ swz_k(row);
@@ -218,7 +244,15 @@ __global__ __launch_bounds__(kThreads, 2) void gemm256_kernel(G256Args p) {
     else wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     const bool pre = t + kST - 1 < nk;
-    if (!(VAR & 1) && pre) issue(t + kST - 1);
+    if (AREG) {
+      if (pre) {
+#pragma unroll
+        for (int q = 0; q < kP; ++q) issue_piece(t + 1, 2 * q + 1);  // B by LDS-DMA
+        load_a_regs(t + 1);
+      }
+    } else if (!(VAR & 1) && pre) {
+      issue(t + kST - 1);
+    }
     const char* ta = smem + (t % kST) * kStage;
     const char* tb = ta + kImg;
 #pragma unroll
@@ -239,6 +273,11 @@ __global__ __launch_bounds__(kThreads, 2) void gemm256_kernel(G256Args p) {
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa, acc[i][j], 0, 0, 0);
         if (VAR & 4) __builtin_amdgcn_s_setprio(0);
       }
+    }
+    if (AREG && pre) {
+      __builtin_amdgcn_s_waitcnt(0);  // the A registers (and B's DMA) of step t + 1 have landed
+      store_a_regs(t + 1);
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the writes are in LDS before the barrier
     }
   }
 
@@ -345,7 +384,7 @@ int g_var = -1;
 int var() {
   if (g_var < 0) {
     const char* e = std::getenv("FLUXMPI_GEMM256_VAR");
-    g_var = e != nullptr ? (std::atoi(e) & 7) : 0;
+    g_var = e != nullptr ? (std::atoi(e) & 15) : 2;  // 2: measured best (+0.5-3 %, rd3f/rd3g)
   }
   return g_var;
 }
@@ -357,6 +396,8 @@ void launch_bk(const G256Args& p, hipStream_t stream) {
     case 2: launch_v<B_T, EPI, BK, 2>(p, stream); break;
     case 3: launch_v<B_T, EPI, BK, 3>(p, stream); break;
     case 5: launch_v<B_T, EPI, BK, 5>(p, stream); break;
+    case 8: launch_v<B_T, EPI, BK, 8>(p, stream); break;
+    case 10: launch_v<B_T, EPI, BK, 10>(p, stream); break;
     default: launch_v<B_T, EPI, BK, 0>(p, stream); break;
   }
 }
@@ -390,7 +431,7 @@ bool gemm256_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb
 int gemm256_colpart_rows(int64_t M) { return static_cast<int>(2 * (M / kTile)); }
 
 void gemm256_set_bk(int bk_) { g_bk = bk_ == 32 ? 32 : 64; }
-void gemm256_set_var(int v) { g_var = v & 7; }
+void gemm256_set_var(int v) { g_var = v & 15; }
 
 void gemm256(const void* a, const void* b, void* c, void* c2, const void* bias, int bias_f32, const void* h,
              float* colpart, int64_t lda, int64_t ldb, int64_t ldc, int64_t M, int64_t N, int64_t K, bool b_t,
