@@ -22,7 +22,7 @@ import torch.nn.functional as F
 
 from ..ops import anderson as AO
 from ..ops.fused_block import conv3x3, conv3x3_supported
-from ..ops.batchnorm import GradLink
+from ..ops.batchnorm import FusedBatchNorm2d, GradLink
 from ..ops.groupnorm import FusedGroupNorm, fp32_affine_cache, skip_param_grads
 from ..ops.groupnorm import native_ok as gn_native_ok
 
@@ -223,9 +223,11 @@ class DEQClassifier(nn.Module):
     def __init__(self, cin=1, ch=48, num_classes=10, **solver):
         super().__init__()
         self.inj = nn.Conv2d(cin, ch, 3, padding=1, bias=False)
-        self.inj_norm = nn.BatchNorm2d(ch)
+        # our NHWC BatchNorm kernels (ops/batchnorm.py) instead of MIOpen's (nn.BatchNorm2d API,
+        # same parameters / state dict)
+        self.inj_norm = FusedBatchNorm2d(ch)
         self.deq = DEQFixedPoint(ResidualCell(ch), **solver)
-        self.out_norm = nn.BatchNorm2d(ch)
+        self.out_norm = FusedBatchNorm2d(ch)
         self.head = nn.Linear(ch * 4 * 4, num_classes)
 
     def forward(self, x):

@@ -61,6 +61,13 @@ def calibrate(ddp, fwd_bwd: Callable[[], object], root: int = 0) -> list[str]:
         fused_block.load_choice_lines(recs)
     fused_block.freeze_choices()
     ddp.zero_grad()
+    if comm.size > 1:
+        # the root's extra forward moved its BatchNorm running statistics / batch counters: put
+        # every rank's buffers back in step (parameters are untouched: no optimiser step ran)
+        bufs = [t.detach() for t in ddp.module.buffers() if t.numel() > 0]
+        if bufs:
+            from .bucket import broadcast_tensors
+            broadcast_tensors(bufs, root, comm=ddp.comm if ddp.comm is not None else None)
     return recs
 
 
