@@ -32,6 +32,8 @@ from ..ops.groupnorm import native_ok as gn_native_ok
 # LAG extra (harmless, still-contracting) iterations after convergence. 0 = test every
 # iteration synchronously (the round-1 behaviour: ~11 % of the step idle, profiles/r1_deq_s63).
 CHECK_LAG = int(os.environ.get("FLUXMPI_DEQ_CHECK_LAG", "2"))
+# FLUXMPI_DEQ_MANUAL_VJP=0: the adjoint's VJPs through autograd.grad (A/B runs)
+MANUAL_VJP = os.environ.get("FLUXMPI_DEQ_MANUAL_VJP", "1") != "0"
 
 
 class LaggedFlags:
@@ -153,7 +155,18 @@ class DEQFixedPoint(nn.Module):
         if not torch.is_grad_enabled():
             return z
         z0 = z.clone().detach().requires_grad_()
-        f0 = self.f(z0, x)
+        manual = MANUAL_VJP and hasattr(self.f, "manual_ok") and self.f.manual_ok(z0)
+        if manual:
+            # the adjoint's VJPs by direct kernel calls on the saved forward state (no autograd
+            # graph for f0, no engine overhead per iteration)
+            _, state = self.f.forward_state(z0.detach(), x.detach())
+            vjp = lambda u: self.f.vjp(state, u)  # noqa: E731
+        else:
+            f0 = self.f(z0, x)
+
+            def vjp(u):
+                with skip_param_grads():  # VJPs w.r.t. z only: no GroupNorm dw/db reductions
+                    return torch.autograd.grad(f0, z0, u, retain_graph=True)[0]
 
         def backward_hook(grad):
             lag = (CHECK_LAG if self.check_lag is None else int(self.check_lag)) if grad.is_cuda else 0
@@ -167,8 +180,7 @@ class DEQFixedPoint(nn.Module):
             u = grad
             it = 0
             for it in range(self.bwd_iter):  # u = J^T u + grad
-                with skip_param_grads():  # VJPs w.r.t. z only: no GroupNorm dw/db reductions
-                    v = torch.autograd.grad(f0, z0, u, retain_graph=True)[0]
+                v = vjp(u)
                 # u_new = v + grad and |u_new - u|^2 in one pass (ops/anderson.adjoint_step)
                 u_new, ss = AO.adjoint_step(v, grad, u)
                 done = ss <= thresh2
@@ -207,6 +219,37 @@ class ResidualCell(nn.Module):
         if conv3x3_supported(t, conv):
             return conv3x3(t, conv.weight, gradlink=link)
         return conv(t)
+
+    def manual_ok(self, z) -> bool:
+        """The fused GPU path that :meth:`forward_state` / :meth:`vjp` drive directly."""
+        return (conv3x3_supported(z, self.conv1) and conv3x3_supported(z, self.conv2)
+                and gn_native_ok(z, self.n1.num_groups) and gn_native_ok(z, self.n3.num_groups)
+                and gn_native_ok(z, self.n2.num_groups))
+
+    @torch.no_grad()
+    def forward_state(self, z, x):
+        """``f(z, x)`` without autograd, keeping what :meth:`vjp` needs (GPU fused path)."""
+        from ..ops.fused_block import conv3x3_fwd_raw
+        from ..ops.groupnorm import gn_fwd_raw
+        c1 = conv3x3_fwd_raw(z, self.conv1.weight)
+        a1, h1, m1, r1, w1 = gn_fwd_raw(c1, None, self.n1.weight, self.n1.bias, self.n1.num_groups, self.n1.eps, True)
+        c2 = conv3x3_fwd_raw(a1, self.conv2.weight)
+        a2, h2, m2, r2, w2 = gn_fwd_raw(c2, x, self.n2.weight, self.n2.bias, self.n2.num_groups, self.n2.eps, False)
+        out, h3, m3, r3, w3 = gn_fwd_raw(z, a2, self.n3.weight, self.n3.bias, self.n3.num_groups, self.n3.eps, True)
+        return out, (tuple(z.shape), (h1, m1, r1, w1), (h2, m2, r2, w2), (h3, m3, r3, w3))
+
+    @torch.no_grad()
+    def vjp(self, state, u):
+        """``J_f(z)^T u`` from :meth:`forward_state`'s state by direct kernel calls — the adjoint
+        solve's per-iteration VJP without the autograd engine (~6 launches per iteration)."""
+        from ..ops.fused_block import conv3x3_dgrad_raw
+        from ..ops.groupnorm import gn_bwd_raw
+        zs, (h1, m1, r1, w1), (h2, m2, r2, w2), (h3, m3, r3, w3) = state
+        d3, _ = gn_bwd_raw(u, h3, m3, r3, w3, self.n3.num_groups, True)    # d(z + a2), ReLU-masked
+        d2, _ = gn_bwd_raw(d3, h2, m2, r2, w2, self.n2.num_groups, False)  # d conv2 output (x is constant)
+        da1 = conv3x3_dgrad_raw(d2, self.conv2.weight, h1.shape)
+        d1, _ = gn_bwd_raw(da1, h1, m1, r1, w1, self.n1.num_groups, True)  # d conv1 output
+        return conv3x3_dgrad_raw(d1, self.conv1.weight, zs, residual=d3)   # + n3's direct path to z
 
     def forward(self, z, x):
         # z feeds conv1 and n3's add: n3's backward hands its gradient of z to conv1's dgrad

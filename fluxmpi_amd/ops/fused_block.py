@@ -828,6 +828,29 @@ def conv3x3(x, weight, with_stats=False, bnlink=None, gradlink=None):
     return _Conv3x3.apply(x, weight, ours, with_stats and ours, bnlink, gradlink)
 
 
+def conv3x3_fwd_raw(x, weight):
+    """The 3x3 / s1 forward the autograd path would run (per-shape choice), without autograd."""
+    x = x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
+    if conv3x3_forward_is_ours(x, weight):
+        note_filter(weight)
+        return conv3x3_fwd(x, weight, engine=_FWD_ENGINE.get((tuple(x.shape), weight.shape[0])))
+    return torch.nn.functional.conv2d(x, weight, None, 1, 1)
+
+
+def conv3x3_dgrad_raw(dy, weight, x_shape, residual=None):
+    """The 3x3 / s1 input gradient (+ ``residual`` in the epilogue) per the per-shape choice,
+    without autograd."""
+    if not dy.is_contiguous(memory_format=torch.channels_last):
+        dy = dy.contiguous(memory_format=torch.channels_last)
+    if _dgrad_is_ours(dy, weight, x_shape):
+        note_filter(weight)
+        return conv3x3_dgrad(dy, weight, residual=residual)
+    xe = torch.empty(x_shape, device=dy.device, dtype=dy.dtype).contiguous(memory_format=torch.channels_last)
+    dx = torch.ops.aten.convolution_backward(dy, xe, weight, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
+                                             [True, False, False])[0]
+    return dx + residual if residual is not None else dx
+
+
 def masked_links_ok() -> bool:
     """GradLinks may carry (dy, mask) instead of dres: the LDS-DMA dgrad kernel masks in its epilogue."""
     return G.ENGINE != 1

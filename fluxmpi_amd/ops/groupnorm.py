@@ -87,23 +87,45 @@ def supported(x: torch.Tensor, groups: int) -> bool:
             and x.is_contiguous(memory_format=torch.channels_last))
 
 
+def gn_fwd_raw(x, add, weight, bias, groups, eps, relu):
+    """``GN(relu(x + add))`` on the fused kernel, no autograd: returns ``(y, saved, mean, rstd, w32)``
+    where ``saved`` is what the backward reads (the GroupNorm input ``relu(x + add)``, or ``x``)."""
+    C = _ext.get(required=True)
+    N, Ch, H, W = x.shape
+    if add is not None:
+        add = add.contiguous(memory_format=torch.channels_last)
+    w32, b32 = _f32(weight), _f32(bias)
+    y = torch.empty_like(x, memory_format=torch.channels_last)
+    h = torch.empty_like(y) if (add is not None or relu) else None
+    mean = torch.empty(N, groups, device=x.device, dtype=torch.float32)
+    rstd = torch.empty_like(mean)
+    C.groupnorm_nhwc_fwd(x.data_ptr(), add.data_ptr() if add is not None else 0, h.data_ptr() if h is not None else 0,
+                         y.data_ptr(), w32.data_ptr() if w32 is not None else 0,
+                         b32.data_ptr() if b32 is not None else 0, mean.data_ptr(), rstd.data_ptr(), N, H * W, Ch,
+                         groups, bool(relu), float(eps), DTYPE_CODE[x.dtype], _stream(x))
+    return y, (h if h is not None else x), mean, rstd, w32
+
+
+def gn_bwd_raw(dy, h, mean, rstd, w32, groups, relu, part=None):
+    """Gradient of the GroupNorm input (times the ReLU mask) from the saved state of
+    :func:`gn_fwd_raw`; ``part`` ([N, 2, C] fp32) receives the per-sample weight / bias sums."""
+    C = _ext.get(required=True)
+    N, Ch, H, W = h.shape
+    dy = dy.contiguous(memory_format=torch.channels_last)
+    dh = torch.empty_like(h, memory_format=torch.channels_last)
+    if part is None:
+        part = torch.empty(N, 2, Ch, device=h.device, dtype=torch.float32)
+    C.groupnorm_nhwc_bwd(dy.data_ptr(), h.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                         w32.data_ptr() if w32 is not None else 0, dh.data_ptr(), part.data_ptr(), N, H * W, Ch,
+                         groups, relu, DTYPE_CODE[h.dtype], _stream(h))
+    return dh, part
+
+
 class _GroupNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, add, weight, bias, groups, eps, relu, link=None):
-        C = _ext.get(required=True)
-        N, Ch, H, W = x.shape
-        if add is not None:
-            add = add.contiguous(memory_format=torch.channels_last)
-        w32, b32 = _f32(weight), _f32(bias)
-        y = torch.empty_like(x, memory_format=torch.channels_last)
-        h = torch.empty_like(y) if (add is not None or relu) else None
-        mean = torch.empty(N, groups, device=x.device, dtype=torch.float32)
-        rstd = torch.empty_like(mean)
-        C.groupnorm_nhwc_fwd(x.data_ptr(), add.data_ptr() if add is not None else 0, h.data_ptr() if h is not None else 0,
-                             y.data_ptr(), w32.data_ptr() if w32 is not None else 0,
-                             b32.data_ptr() if b32 is not None else 0, mean.data_ptr(), rstd.data_ptr(), N, H * W, Ch,
-                             groups, bool(relu), float(eps), DTYPE_CODE[x.dtype], _stream(x))
-        ctx.save_for_backward(h if h is not None else x, mean, rstd, w32)
+        y, saved, mean, rstd, w32 = gn_fwd_raw(x, add, weight, bias, groups, eps, relu)
+        ctx.save_for_backward(saved, mean, rstd, w32)
         ctx.cfg = (groups, bool(relu), add is not None,
                    weight.dtype if weight is not None else None, bias.dtype if bias is not None else None)
         ctx.link = link
@@ -111,16 +133,9 @@ class _GroupNormFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        C = _ext.get(required=True)
         h, mean, rstd, w32 = ctx.saved_tensors
         groups, relu, has_add, wd, bd = ctx.cfg
-        N, Ch, H, W = h.shape
-        dy = dy.contiguous(memory_format=torch.channels_last)
-        dh = torch.empty_like(h, memory_format=torch.channels_last)
-        part = torch.empty(N, 2, Ch, device=h.device, dtype=torch.float32)
-        C.groupnorm_nhwc_bwd(dy.data_ptr(), h.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
-                             w32.data_ptr() if w32 is not None else 0, dh.data_ptr(), part.data_ptr(), N, H * W, Ch,
-                             groups, relu, DTYPE_CODE[h.dtype], _stream(h))
+        dh, part = gn_bwd_raw(dy, h, mean, rstd, w32, groups, relu)
         want = not _SKIP_PARAM_GRADS
         dw = part[:, 0].sum(0).to(wd) if want and wd is not None and ctx.needs_input_grad[2] else None
         db = part[:, 1].sum(0).to(bd) if want and bd is not None and ctx.needs_input_grad[3] else None
