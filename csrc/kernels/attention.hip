@@ -693,6 +693,164 @@ __global__ __launch_bounds__(1024) void attn_bwd_dkv_res_kernel(AttnBwdArgs a) {
   }
 }
 
+// Fused backward, head resident (T <= 256): ONE kernel per (batch, head) instead of the dq / dkv
+// pair, which both staged the head and both recomputed S = Q K^T and dP = dO V^T. One wave per 16
+// keys holds its dK^T / dV^T accumulators (as attn_bwd_dkv_res) while sweeping the queries in
+// 32-row blocks; the same block's dS also feeds dQ = dS K: the wave transposes its 16 x 32 dS
+// tile through a 1-KiB private LDS scratch (one 8-B write per lane and half, read back by
+// ds_read_b64_tr_b16 as the A operand of v_mfma_f32_16x16x16_bf16, K by transposed reads of the
+// staged K image as B) and adds its partial into an fp32 dQ accumulator in LDS (ds_add_f32; the
+// waves sweep the query blocks in rotated order, so they seldom add into the same rows at once).
+// D = rowsum(dO * O) is computed in the prologue (no separate pass). LDS: Q, dO, K images +
+// dQ [TV][64] fp32 + lse / D + scratch = 156 KiB at T = 197: one workgroup (13 waves) per CU.
+typedef short short4v_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) short4v_t lds_short4v_t;
+
+__device__ __forceinline__ short4v_t tr_read4(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v_t*)(p));
+}
+
+__global__ __launch_bounds__(1024) void attn_bwd_fused_kernel(AttnBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int TV = (a.T + 31) & ~31;
+  const int nw = blockDim.x >> 6;
+  char* qimg = smem;
+  char* gimg = qimg + TV * 128;
+  char* kimg = gimg + TV * 128;
+  float* dqacc = reinterpret_cast<float*>(kimg + TV * 128);  // [TV][64]
+  float* sL = dqacc + TV * 64;
+  float* sD = sL + TV;
+  char* scratch = reinterpret_cast<char*>(sD + TV);          // per wave: 2 halves x [16 k][16 q] bf16
+  const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
+  stage_rows<false>(qimg, a.q + b * a.sq_b + h * DH, a.sq_t, TV, a.T);
+  stage_rows<false>(gimg, a.dout + b * a.sg_b + h * DH, a.sg_t, TV, a.T);
+  stage_rows<false>(kimg, a.k + b * a.sq_b + h * DH, a.sq_t, TV, a.T);
+  for (int i = threadIdx.x; i < TV * 16; i += blockDim.x)
+    reinterpret_cast<float4*>(dqacc)[i] = float4{0.f, 0.f, 0.f, 0.f};
+  const float* st = a.stats + (static_cast<int64_t>(b) * a.H + h) * a.T * 2;
+  for (int qq = threadIdx.x; qq < TV; qq += blockDim.x) {
+    sL[qq] = qq < a.T ? st[2 * qq] : kInf;  // padded query: P = 0
+    if (qq >= a.T) sD[qq] = 0.f;
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, col = lane & 15, g = lane >> 4;
+  // D for this wave's 16 queries (= its key range: one wave per 16 rows either way)
+  {
+    const int qi = 16 * w + col;
+    bf16x8 gf[2] = {}, o0 = {}, o1 = {};
+    if (qi < a.T) {
+      const bf16* gp = a.dout + b * a.sg_b + static_cast<int64_t>(qi) * a.sg_t + h * DH;
+      gf[0] = ld8(gp + 8 * g);
+      gf[1] = ld8(gp + 32 + 8 * g);
+      const bf16* op = a.o + b * a.so_b + static_cast<int64_t>(qi) * a.so_t + h * a.so_h;
+      o0 = ld8(op + 8 * g);
+      o1 = ld8(op + 32 + 8 * g);
+    }
+    float dsum = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dsum += (float)gf[0][j] * (float)o0[j] + (float)gf[1][j] * (float)o1[j];
+    dsum = butterfly_from<16>(dsum);
+    if (g == 0 && qi < a.T) sD[qi] = dsum;
+  }
+  const int k0 = 16 * w;
+  const int ki = k0 + col;
+  const bool kok = ki < a.T;
+  const int64_t koff = b * a.sq_b + static_cast<int64_t>(ki) * a.sq_t + h * DH;
+  bf16x8 kf[2] = {}, vf[2] = {};
+  if (kok) {
+    kf[0] = ld8(a.k + koff + 8 * g);
+    kf[1] = ld8(a.k + koff + 32 + 8 * g);
+    vf[0] = ld8(a.v + koff + 8 * g);
+    vf[1] = ld8(a.v + koff + 32 + 8 * g);
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  const float c2 = a.scale * kLog2e;
+  // transposed-read lane roles (per 16-lane group g: lane 4q'+p addresses row 4g+q', columns 4p..4p+3)
+  const int trq = (lane & 15) >> 2, trp = lane & 3;
+  char* scr = scratch + w * 1024;
+  // B operand of the dQ MFMA: K[k0 + 4g + j][16 dt + (lane & 15)] from the staged K image
+  short4v_t kb[4];
+  {
+    const int kr = k0 + 4 * g + trq;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int c = 16 * dt + 4 * trp;
+      kb[dt] = tr_read4(kimg + kr * 128 + (((c >> 3) ^ swz_b(kr)) << 4) + (c & 7) * 2);
+    }
+  }
+  f32x4 accK[4] = {}, accV[4] = {};
+  const int nks = TV / 32;
+  for (int it = 0; it < nks; ++it) {
+    const int ks = (it + w) % nks;  // rotated: waves add into different dQ rows at a time
+    f32x4 p[2], dsv[2];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int row = 32 * ks + 16 * half + col;
+      f32x4 sv = {}, dp = {};
+      sv = mfma(img_row(qimg, row, g), kf[0], sv);
+      sv = mfma(img_row(qimg, row, 4 + g), kf[1], sv);
+      dp = mfma(img_row(gimg, row, g), vf[0], dp);
+      dp = mfma(img_row(gimg, row, 4 + g), vf[1], dp);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qq = 32 * ks + 16 * half + 4 * g + r;
+        const float pv = fast_exp2(fmaf(sv[r], c2, -sL[qq]));
+        p[half][r] = pv;
+        dsv[half][r] = pv * (dp[r] - sD[qq]);
+      }
+      // dS^T tile of this half: row k = col, queries 4g .. 4g+3 (one 8-B write per lane)
+      const bf16x4 d4 = {(bf16)dsv[half][0], (bf16)dsv[half][1], (bf16)dsv[half][2], (bf16)dsv[half][3]};
+      *reinterpret_cast<bf16x4*>(scr + half * 512 + col * 32 + 8 * g) = d4;
+    }
+    const bf16x8 pb = pack(p[0], p[1]), db = pack(dsv[0], dsv[1]);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      accV[dt] = mfma(img_tr(gimg, 32 * ks, 16 * dt), pb, accV[dt]);
+      accK[dt] = mfma(img_tr(qimg, 32 * ks, 16 * dt), db, accK[dt]);
+    }
+    // dQ[q][d] += sum over this wave's 16 keys of dS[q][k] K[k][d]
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      // A operand: dS[q = lane & 15][k = 4g + j] = column (lane & 15) of scratch rows 4g .. 4g+3
+      const short4v_t da = tr_read4(scr + half * 512 + (4 * g + trq) * 32 + 8 * trp);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        f32x4 c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(da, kb[dt], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          atomicAdd(dqacc + (32 * ks + 16 * half + 4 * g + r) * 64 + 16 * dt + col, c[r]);
+      }
+    }
+  }
+  if (kok) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const bf16x4 v = {(bf16)accV[dt][0], (bf16)accV[dt][1], (bf16)accV[dt][2], (bf16)accV[dt][3]};
+      const bf16x4 k = {(bf16)(accK[dt][0] * a.scale), (bf16)(accK[dt][1] * a.scale),
+                        (bf16)(accK[dt][2] * a.scale), (bf16)(accK[dt][3] * a.scale)};
+      *reinterpret_cast<bf16x4*>(a.dv + koff + dt * 16 + 4 * g) = v;
+      *reinterpret_cast<bf16x4*>(a.dk + koff + dt * 16 + 4 * g) = k;
+    }
+  }
+  __syncthreads();  // every wave's dQ partials are in LDS
+  for (int i = threadIdx.x; i < a.T * 8; i += blockDim.x) {
+    const int qq = i >> 3, c8 = (i & 7) * 8;
+    const float* src = dqacc + qq * 64 + c8;
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)(src[j] * a.scale);
+    *reinterpret_cast<bf16x8*>(a.dq + b * a.sq_b + static_cast<int64_t>(qq) * a.sq_t + h * DH + c8) = o;
+  }
+}
+
+int g_attn_bwd_fused = -1;  // -1: FLUXMPI_ATTN_BWD decides (fused / resident / blocked)
+
+size_t fused_bwd_lds(int T) {
+  const size_t TV = static_cast<size_t>((T + 31) & ~31);
+  const size_t waves = static_cast<size_t>((T + 15) / 16);
+  return 3 * TV * 128 + TV * 64 * 4 + 2 * TV * 4 + waves * 1024;
+}
+
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 // workgroups per (b, h) of the resident kernels (FLUXMPI_ATTN_PARTS, default 2): with the head's
@@ -727,6 +885,24 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* o, const 
     const char* e = std::getenv("FLUXMPI_ATTN_BWD");
     return e == nullptr || std::string(e) != "blocked";
   }();
+  if (g_attn_bwd_fused < 0) {
+    const char* e = std::getenv("FLUXMPI_ATTN_BWD");
+    g_attn_bwd_fused = (e != nullptr && std::string(e) == "fused") ? 1 : 0;
+  }
+  if (g_attn_bwd_fused == 1 && T <= kResMaxT && (sq_t % 8) == 0 && (sg_t % 8) == 0 && fused_bwd_lds(T) <= 160 * 1024) {
+    const int waves = (T + 15) / 16;
+    const int64_t bh = static_cast<int64_t>(B) * H;
+    if (bh > 0x7fffffff) throw std::runtime_error("attn_bwd: grid too large");
+    static bool attr = false;
+    if (!attr) {
+      FLUXMPI_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_fused_kernel),
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      attr = true;
+    }
+    attn_bwd_fused_kernel<<<static_cast<unsigned>(bh), waves * 64, fused_bwd_lds(T), s>>>(a);
+    FLUXMPI_HIP_CHECK(hipGetLastError());
+    return;
+  }
   if (resident && T <= kResMaxT && (sq_t % 8) == 0 && (sg_t % 8) == 0) {
     const int tiles = (T + 15) / 16;
     a.nblk = res_parts(tiles);
@@ -748,6 +924,8 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* o, const 
   attn_bwd_dkv_kernel<<<static_cast<unsigned>(total), 256, 0, s>>>(a);
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
+
+void attn_set_bwd_fused(int on) { g_attn_bwd_fused = on ? 1 : 0; }
 
 void attn_fwd(const void* q, const void* k, const void* v, void* o, float* stats, int64_t sq_b, int64_t sq_t,
               int64_t so_b, int64_t so_t, int64_t so_h, int B, int T, int H, int Dh, float scale, hipStream_t s) {

@@ -148,8 +148,12 @@ class DEQFixedPoint(nn.Module):
             return self._forward(x)
 
     def _forward(self, x):
+        # the solver's ~30 evaluations by direct kernel calls when the cell allows (no autograd
+        # Function objects per call: the DEQ step is host-bound, profiles/rd3h_ab_deq.jsonl)
+        raw = MANUAL_VJP and hasattr(self.f, "manual_ok") and self.f.manual_ok(x)
+        fz = (lambda z: self.f.forward_raw(z, x)) if raw else (lambda z: self.f(z, x))
         with torch.no_grad():
-            z, self.last_iters, _ = anderson(lambda z: self.f(z, x), torch.zeros_like(x), max_iter=self.max_iter,
+            z, self.last_iters, _ = anderson(fz, torch.zeros_like(x), max_iter=self.max_iter,
                                              tol=self.tol, check_lag=self.check_lag)
         z = self.f(z, x)  # one differentiable step re-engages autograd at z*
         if not torch.is_grad_enabled():
@@ -227,7 +231,12 @@ class ResidualCell(nn.Module):
                 and gn_native_ok(z, self.n2.num_groups))
 
     @torch.no_grad()
-    def forward_state(self, z, x):
+    def forward_raw(self, z, x):
+        """``f(z, x)`` by direct kernel calls (no autograd Functions): the solver iterations."""
+        return self.forward_state(z, x, keep=False)
+
+    @torch.no_grad()
+    def forward_state(self, z, x, keep: bool = True):
         """``f(z, x)`` without autograd, keeping what :meth:`vjp` needs (GPU fused path)."""
         from ..ops.fused_block import conv3x3_fwd_raw
         from ..ops.groupnorm import gn_fwd_raw
@@ -236,6 +245,8 @@ class ResidualCell(nn.Module):
         c2 = conv3x3_fwd_raw(a1, self.conv2.weight)
         a2, h2, m2, r2, w2 = gn_fwd_raw(c2, x, self.n2.weight, self.n2.bias, self.n2.num_groups, self.n2.eps, False)
         out, h3, m3, r3, w3 = gn_fwd_raw(z, a2, self.n3.weight, self.n3.bias, self.n3.num_groups, self.n3.eps, True)
+        if not keep:
+            return out
         return out, (tuple(z.shape), (h1, m1, r1, w1), (h2, m2, r2, w2), (h3, m3, r3, w3))
 
     @torch.no_grad()

@@ -831,8 +831,10 @@ def conv3x3(x, weight, with_stats=False, bnlink=None, gradlink=None):
 def conv3x3_fwd_raw(x, weight):
     """The 3x3 / s1 forward the autograd path would run (per-shape choice), without autograd."""
     x = x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
+    # a forward marks the cached transposed filter stale whichever kernel runs (as _Conv3x3 does):
+    # the next input gradient re-derives it from the current weights
+    note_filter(weight)
     if conv3x3_forward_is_ours(x, weight):
-        note_filter(weight)
         return conv3x3_fwd(x, weight, engine=_FWD_ENGINE.get((tuple(x.shape), weight.shape[0])))
     return torch.nn.functional.conv2d(x, weight, None, 1, 1)
 
@@ -843,7 +845,6 @@ def conv3x3_dgrad_raw(dy, weight, x_shape, residual=None):
     if not dy.is_contiguous(memory_format=torch.channels_last):
         dy = dy.contiguous(memory_format=torch.channels_last)
     if _dgrad_is_ours(dy, weight, x_shape):
-        note_filter(weight)
         return conv3x3_dgrad(dy, weight, residual=residual)
     xe = torch.empty(x_shape, device=dy.device, dtype=dy.dtype).contiguous(memory_format=torch.channels_last)
     dx = torch.ops.aten.convolution_backward(dy, xe, weight, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,

@@ -41,6 +41,30 @@ def test_packed_attention_vs_fp32(gpu_ext, b, t, heads, dh):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("b,t,heads", [(4, 197, 12), (2, 50, 4), (3, 7, 2), (2, 256, 2)])
+def test_packed_attention_fused_bwd_vs_fp32(gpu_ext, b, t, heads):
+    """The one-kernel backward (attn_bwd_fused_kernel: dQ through LDS atomics) vs fp32."""
+    from fluxmpi_amd.models.vit import packed_attention
+    gpu_ext.attn_set_bwd_fused(1)
+    try:
+        torch.manual_seed(1)
+        x = torch.randn(b, t, 3 * heads * 64, device="cuda")
+        xa = x.to(torch.bfloat16).requires_grad_()
+        xr = x.to(torch.bfloat16).float().requires_grad_()
+        y = packed_attention(xa, heads)
+        yr = _ref_attention(xr, heads)
+        g = torch.randn_like(yr)
+        y.backward(g.to(torch.bfloat16))
+        yr.backward(g)
+        d = heads * 64
+        for part in range(3):  # dQ, dK, dV slots of the packed gradient
+            sl = slice(part * d, (part + 1) * d)
+            assert _rel(xa.grad[..., sl], xr.grad[..., sl]) < 3e-2, part
+    finally:
+        gpu_ext.attn_set_bwd_fused(0)
+
+
+@pytest.mark.gpu
 def test_vit_tiny_step(gpu_ext):
     from fluxmpi_amd.models.vit import vit_tiny
     torch.manual_seed(0)
