@@ -703,6 +703,10 @@ __global__ __launch_bounds__(1024) void attn_bwd_dkv_res_kernel(AttnBwdArgs a) {
 // waves sweep the query blocks in rotated order, so they seldom add into the same rows at once).
 // D = rowsum(dO * O) is computed in the prologue (no separate pass). LDS: Q, dO, K images +
 // dQ [TV][64] fp32 + lse / D + scratch = 156 KiB at T = 197: one workgroup (13 waves) per CU.
+// MEASURED A LOSS (profiles/rd3i_vit_attnfused_steady.md): 3.1 ms per call vs 0.28 ms for the
+// dq + dkv pair at ViT-B/16 bs256 — the 32 ds_add_f32 per lane per query block (4-way bank
+// conflicted rows) serialise on the LDS atomic path and dominate everything else. Kept opt-in
+// (FLUXMPI_ATTN_BWD=fused) as the record of that experiment; the default stays the pair.
 typedef short short4v_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) short4v_t lds_short4v_t;
 
