@@ -271,6 +271,21 @@ void groupnorm_nhwc_bwd(const void* dy, const void* h, const float* mean, const 
                         float* partials, int64_t N, int64_t HW, int64_t C, int64_t G, bool relu, int dtype,
                         hipStream_t stream);
 
+// ---- the DEQ cell in one kernel per evaluation (kernels/deq_cell.hip) ----------------------
+// f(z, x) = GN3(relu(z + GN2(x + conv2(GN1(relu(conv1 z)))))) on NHWC bf16 [N][H*W][48]; one
+// workgroup per sample, everything LDS-resident. w1 / w2: [C][9C] bf16 with k = tap * C + ci.
+// gn_w / gn_b: 3 fp32 vectors each (nullable). out (bf16) and/or out32 (fp32, sample stride
+// out32_stride elements); h[3] (the GroupNorm inputs) and mean / rstd[3] ([N][G]) nullable.
+// vjp: J_f(z)^T u from that state; w2t / w1t are the transposed tap-flipped filters (k = tap * C + co).
+bool deq_cell_supported(int64_t H, int64_t W, int64_t C, int64_t G);
+void deq_cell_fwd(const void* z, const void* x, const void* w1, const void* w2, const float* const* gn_w,
+                  const float* const* gn_b, void* out, float* out32, int64_t out32_stride, void* const* h,
+                  float* const* mean, float* const* rstd, int64_t N, int64_t H, int64_t W, int64_t C, int64_t G,
+                  float eps, hipStream_t stream);
+void deq_cell_vjp(const void* u, const void* const* h, const void* w2t, const void* w1t, const float* const* gn_w,
+                  const float* const* mean, const float* const* rstd, void* out, int64_t N, int64_t H, int64_t W,
+                  int64_t C, int64_t G, hipStream_t stream);
+
 // ---- GELU backward + bias gradient (transformer MLP fc1) ---------------------------------
 // dh = dy * gelu'(h) (exact erf form); partials[blocks][N] = per-workgroup column sums of dh
 // (sum with gemm_splitk_reduce). N/8 must be a multiple of 64, <= 1024.

@@ -4,6 +4,7 @@
 // torch.cuda.Stream.cuda_stream), which keeps this module independent of the
 // ATen C++ ABI and lets it launch on any stream, including during HIP-graph
 // capture.
+#include <array>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -233,6 +234,46 @@ PYBIND11_MODULE(_C, m) {
                        reinterpret_cast<const float*>(mean), reinterpret_cast<const float*>(rstd),
                        reinterpret_cast<const float*>(w), reinterpret_cast<void*>(dh), reinterpret_cast<float*>(part), N,
                        HW, C, G, relu, dtype, S(stream));
+  });
+
+  // ---- the DEQ cell in one kernel ------------------------------------------------------
+  m.def("deq_cell_supported", &deq_cell_supported);
+  m.def("deq_cell_fwd", [](uintptr_t z, uintptr_t x, uintptr_t w1, uintptr_t w2, std::array<uintptr_t, 3> gw,
+                           std::array<uintptr_t, 3> gb, uintptr_t out, uintptr_t out32, int64_t out32_stride,
+                           std::array<uintptr_t, 3> h, std::array<uintptr_t, 3> mean, std::array<uintptr_t, 3> rstd,
+                           int64_t N, int64_t H, int64_t W, int64_t C, int64_t G, float eps, uintptr_t stream) {
+    const float* gwp[3];
+    const float* gbp[3];
+    void* hp[3];
+    float* mp[3];
+    float* rp[3];
+    for (int i = 0; i < 3; ++i) {
+      gwp[i] = reinterpret_cast<const float*>(gw[i]);
+      gbp[i] = reinterpret_cast<const float*>(gb[i]);
+      hp[i] = reinterpret_cast<void*>(h[i]);
+      mp[i] = reinterpret_cast<float*>(mean[i]);
+      rp[i] = reinterpret_cast<float*>(rstd[i]);
+    }
+    deq_cell_fwd(reinterpret_cast<const void*>(z), reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(w1),
+                 reinterpret_cast<const void*>(w2), gwp, gbp, reinterpret_cast<void*>(out),
+                 reinterpret_cast<float*>(out32), out32_stride, hp, mp, rp, N, H, W, C, G, eps, S(stream));
+  });
+  m.def("deq_cell_vjp", [](uintptr_t u, std::array<uintptr_t, 3> h, uintptr_t w2t, uintptr_t w1t,
+                           std::array<uintptr_t, 3> gw, std::array<uintptr_t, 3> mean, std::array<uintptr_t, 3> rstd,
+                           uintptr_t out, int64_t N, int64_t H, int64_t W, int64_t C, int64_t G, uintptr_t stream) {
+    const void* hp[3];
+    const float* gwp[3];
+    const float* mp[3];
+    const float* rp[3];
+    for (int i = 0; i < 3; ++i) {
+      hp[i] = reinterpret_cast<const void*>(h[i]);
+      gwp[i] = reinterpret_cast<const float*>(gw[i]);
+      mp[i] = reinterpret_cast<const float*>(mean[i]);
+      rp[i] = reinterpret_cast<const float*>(rstd[i]);
+    }
+    deq_cell_vjp(reinterpret_cast<const void*>(u), hp, reinterpret_cast<const void*>(w2t),
+                 reinterpret_cast<const void*>(w1t), gwp, mp, rp, reinterpret_cast<void*>(out), N, H, W, C, G,
+                 S(stream));
   });
 
   // ---- GELU backward + bias gradient -------------------------------------------------

@@ -34,6 +34,10 @@ from ..ops.groupnorm import native_ok as gn_native_ok
 CHECK_LAG = int(os.environ.get("FLUXMPI_DEQ_CHECK_LAG", "2"))
 # FLUXMPI_DEQ_MANUAL_VJP=0: the adjoint's VJPs through autograd.grad (A/B runs)
 MANUAL_VJP = os.environ.get("FLUXMPI_DEQ_MANUAL_VJP", "1") != "0"
+# FLUXMPI_DEQ_GRAPH=1: solver loops replay HIP graphs (SolverGraphs; opt-in, see tests);
+# FLUXMPI_DEQ_GRAPH_CHUNK: adjoint iterations per graph replay
+GRAPHS = os.environ.get("FLUXMPI_DEQ_GRAPH", "0") == "1"  # opt-in until the replay-after-update check passes
+GRAPH_CHUNK = int(os.environ.get("FLUXMPI_DEQ_GRAPH_CHUNK", "5"))
 
 
 class LaggedFlags:
@@ -51,16 +55,17 @@ class LaggedFlags:
         ev.record()
         self.pending.append((i, ev))
 
-    def pop_ready(self):
+    def pop_ready(self, lag: int | None = None):
         """``(i, value)`` of the push made ``lag`` pushes ago (blocks on its event only), else None."""
-        if len(self.pending) <= self.lag:
+        if len(self.pending) <= (self.lag if lag is None else lag):
             return None
         i, ev = self.pending.pop(0)
         ev.synchronize()
         return i, float(self.buf[i])
 
 
-def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0, check_lag: int | None = None):
+def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0, check_lag: int | None = None,
+             graphs: "SolverGraphs | None" = None):
     """Anderson acceleration for ``x = f(x)`` over batch-flattened tensors. Returns (x, iters, rel_residual).
 
     The history Gram matrix and the mix run as single-pass HIP kernels on the GPU
@@ -71,6 +76,11 @@ def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0, check_lag: i
     back ``check_lag`` iterations later (:class:`LaggedFlags`), so the host never waits for
     the queue to drain; the returned iterate is then the newest one and the residual a 0-d
     device tensor when the solve ends without convergence. 0: test synchronously (float).
+
+    ``graphs`` (:class:`SolverGraphs`, GPU): the history lives in its static buffers and, once
+    the iteration is periodic (k >= m: slot k % m, all m rows in the Gram), whole periods of m
+    iterations replay one captured HIP graph; the test then runs per period on the period's
+    smallest residual (read back one period late).
     """
     from ..ops import anderson as AO
 
@@ -79,9 +89,12 @@ def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0, check_lag: i
     d = x0[0].numel()
     # the solver history and the small (m+1)^2 systems are kept in fp32 whatever the model
     # dtype (bf16 has no batched LU, and 8-bit mantissas would stall the extrapolation)
-    X = torch.zeros(bsz, m, d, dtype=torch.float32, device=x0.device)
-    Fv = torch.zeros_like(X)
-    Gs = torch.zeros_like(X)
+    if graphs is not None:
+        X, Fv, Gs = graphs.history(m)
+    else:
+        X = torch.zeros(bsz, m, d, dtype=torch.float32, device=x0.device)
+        Fv = torch.zeros_like(X)
+        Gs = torch.zeros_like(X)
 
     # flatten in MEMORY order: a channels_last iterate stays channels_last through f (views,
     # no layout copies), which is the layout the fused NHWC GroupNorm kernels take
@@ -96,21 +109,50 @@ def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0, check_lag: i
             return v.reshape(n_, h_, w_, c_).permute(0, 3, 1, 2)
         return v.reshape(shape)
 
-    def fx(v):  # f in the model dtype; the fp32 history slot assignment is the (one) cast
-        return flat(f(unflat(v.contiguous()).to(dt)))
+    write_into = getattr(f, "write_into", None)
 
-    X[:, 0], Fv[:, 0] = flat(x0), fx(flat(x0))
-    X[:, 1], Fv[:, 1] = Fv[:, 0], fx(Fv[:, 0])
+    def fx_into(v, slot):
+        # f in the model dtype; the fp32 history slot assignment is the (one) cast — or, when f
+        # can, its kernel writes the fp32 slot itself (no separate cast pass)
+        z = unflat(v.contiguous()).to(dt)
+        if write_into is None or not write_into(z, Fv[:, slot]):
+            Fv[:, slot] = flat(f(z))
+
+    X[:, 0] = flat(x0)
+    fx_into(X[:, 0], 0)
+    X[:, 1] = Fv[:, 0]
+    fx_into(Fv[:, 0], 1)
     lag = (CHECK_LAG if check_lag is None else int(check_lag)) if x0.is_cuda else 0
     flags = LaggedFlags(lag, max_iter) if lag > 0 else None
-    res = float("inf")
-    k, converged = 1, False
-    for k in range(2, max_iter):
-        n = min(k, m)
-        last = (k - 1) % m
+
+    def solve_step(k):
         # stored G = F - X: only the row(s) changed since the last Gram are recomputed; on the GPU
         # the residual and the (n+1)^2 solve are ONE launch after the Gram pass (AO.gram_solve)
-        alpha, res_t = AO.gram_solve(X, Fv, n, last, Gs, (0, 1) if k == 2 else (last,), lam, k > 2)
+        last = (k - 1) % m
+        return AO.gram_solve(X, Fv, min(k, m), last, Gs, (0, 1) if k == 2 else (last,), lam, k > 2)
+
+    def mix_step(k, alpha):
+        fx_into(AO.mix(X, Fv, alpha, k % m, beta, dt), k % m)
+
+    res = float("inf")
+    k, converged = 2, False
+    while k < max_iter:
+        if graphs is not None and k >= max(m, 3) and k % m == 0 and k + m <= max_iter:
+            # iterations k .. k + m - 1 in one replay; iterate k - 1 + m is then complete
+            rmin = graphs.anderson_period(k, m, solve_step, mix_step)
+            k += m
+            if flags is None:
+                res = float(rmin)
+                converged = res < tol
+            else:
+                flags.push(k - 1, rmin)
+                while not converged and (hit := flags.pop_ready(lag=1)) is not None:
+                    res, converged = hit[1], hit[1] < tol
+            if converged:
+                k -= 1
+                break
+            continue
+        alpha, res_t = solve_step(k)
         if k > 2:  # residual of the iterate produced by the previous iteration
             if flags is None:
                 res = float(res_t)
@@ -124,13 +166,155 @@ def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0, check_lag: i
                     # iterate hit[0] - 1 converged; the newest one (iteration k - 1) is at least as good
                     res, k, converged = hit[1], k - 1, True
                     break
-        z = AO.mix(X, Fv, alpha, k % m, beta, dt)
-        Fv[:, k % m] = fx(z)
+        mix_step(k, alpha)
+        k += 1
     if not converged:
+        k = max(k - 1, 1)  # the last completed iteration
         s = k % m
         res_t = (Fv[:, s] - X[:, s]).norm() / (1e-5 + Fv[:, s].norm())
         res = res_t if flags is not None else float(res_t)
     return unflat(X[:, k % m].contiguous()).to(dt), k, res
+
+
+class _CellEval:
+    """``z -> f(z, x)`` for the solver: direct kernel calls when ``raw`` (else the autograd-free
+    module call under no_grad); ``write_into`` lets the fused cell kernel write an fp32 history
+    slot itself (ops/deq_cell.py)."""
+
+    def __init__(self, cell, x, raw: bool):
+        self.cell, self.x, self.raw = cell, x, raw
+
+    def __call__(self, z):
+        return self.cell.forward_raw(z, self.x) if self.raw else self.cell(z, self.x)
+
+    def write_into(self, z, dst) -> bool:
+        if not self.raw or dst.stride(-1) != 1:
+            return False
+        from ..ops import deq_cell
+        if not (hasattr(self.cell, "conv1") and deq_cell.supported(self.cell, z)):
+            return False
+        deq_cell.cell_forward(self.cell, z, self.x, out32=dst, want_out=False)
+        return True
+
+
+def _capture(graph: "torch.cuda.CUDAGraph"):
+    # thread-local capture mode: a DDP watchdog thread polling events must not invalidate it
+    return torch.cuda.graph(graph, capture_error_mode="thread_local")
+
+
+class SolverGraphs:
+    """HIP graphs of one :class:`DEQFixedPoint`'s two solver loops at one input shape.
+
+    Both loops are periodic: Anderson iteration k (k >= m) reads and writes history slots
+    by ``k % m`` only, and every adjoint iteration ``u <- J^T u + g`` is the same launch
+    sequence. One period of each (m forward iterations, :data:`GRAPH_CHUNK` adjoint ones) is
+    captured once and replayed: the host issues one graph launch per period instead of ~10
+    kernel launches (and their Python dispatch) per iteration, which is what bounds the eager
+    DEQ step (wall ~1.25x the GPU's busy time, profiles/rd3h_deq_steady.md). Convergence is
+    tested per replay on the period's best residual, read back one period late, so a solve
+    stops at most two periods after the iterate that met the tolerance (the extra iterations
+    keep contracting) and the reported iteration counts are the ones executed.
+
+    Everything a graph reads lives at a fixed address and is refreshed before a replay: the
+    injection ``x`` (copied in), the fp32 history, the GroupNorm fp32 affine copies
+    (``fp32_affine_cache(buffers=...)``), the adjoint's right-hand side / iterate / threshold,
+    the cached transposed conv filters (re-derived eagerly before the adjoint replays:
+    :meth:`ResidualCell.refresh_filters`). The VJPs' forward state comes from a third graph
+    (``forward_state`` at ``z = f(z*)``), so its tensors are static too. Parameters are read in
+    place (the optimiser updates them in place). Built from the SECOND call at a shape: the
+    first runs eagerly and measures the per-shape kernel choices the capture then bakes in.
+    """
+
+    def __init__(self, x: torch.Tensor):
+        self.x = torch.empty_like(x)  # the solve's injection, same strides (channels_last stays)
+        self.x.copy_(x)
+        self.aff: dict = {}
+        self._hist = None
+        self.rbuf = self.rmin = None
+        self.g_fwd = self.g_state = self.g_adj = None
+        self.state = self.z0 = self.grad = self.u = self.thresh2 = self.dmax = None
+        self.chunk = 0
+
+    def history(self, m: int):
+        bsz, d = self.x.shape[0], self.x[0].numel()
+        if self._hist is None or self._hist[0].shape[1] != m:
+            X = torch.zeros(bsz, m, d, dtype=torch.float32, device=self.x.device)
+            self._hist = (X, torch.zeros_like(X), torch.zeros_like(X))
+            self.g_fwd = None
+        return self._hist
+
+    def anderson_period(self, k0: int, m: int, solve_step, mix_step) -> torch.Tensor:
+        """Replay iterations ``k0 .. k0 + m - 1`` (capturing them on first use); returns the
+        smallest residual of the period (0-d device tensor, static)."""
+        if self.g_fwd is None:
+            self.rbuf = torch.zeros(m, dtype=torch.float32, device=self.x.device)
+            self.rmin = torch.zeros((), dtype=torch.float32, device=self.x.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.no_grad(), _capture(g):
+                for i in range(m):
+                    alpha, res_t = solve_step(k0 + i)
+                    self.rbuf[i].copy_(res_t)
+                    mix_step(k0 + i, alpha)
+                self.rmin.copy_(self.rbuf.min())
+            self.g_fwd = g
+        self.g_fwd.replay()
+        return self.rmin
+
+    def capture_adjoint(self, cell, z: torch.Tensor, chunk: int) -> None:
+        """Capture ``forward_state`` at a static ``z0`` and ``chunk`` adjoint iterations."""
+        with torch.no_grad():
+            self.z0 = torch.empty_like(z)
+            self.z0.copy_(z)
+            g = torch.cuda.CUDAGraph()
+            with _capture(g):
+                _, self.state = cell.forward_state(self.z0, self.x)
+            self.g_state = g
+            self.grad = torch.empty_like(self.z0)
+            self.u = torch.empty_like(self.z0)
+            self.thresh2 = torch.zeros((), dtype=torch.float32, device=z.device)
+            done = torch.zeros(chunk, dtype=torch.float32, device=z.device)
+            self.dmax = torch.zeros((), dtype=torch.float32, device=z.device)
+            cell.refresh_filters()  # fresh now: the capture below records no refresh launch
+            g = torch.cuda.CUDAGraph()
+            with _capture(g):
+                u = self.u
+                for i in range(chunk):
+                    u, ss = AO.adjoint_step(cell.vjp(self.state, u), self.grad, u)
+                    done[i].copy_((ss <= self.thresh2).float())
+                self.u.copy_(u)
+                self.dmax.copy_(done.max())
+            self.g_adj = g
+            self.chunk = chunk
+
+    def forward_state(self, z: torch.Tensor) -> None:
+        self.z0.copy_(z)
+        self.g_state.replay()
+
+    def adjoint(self, cell, grad: torch.Tensor, tol: float, max_iter: int, lag: int):
+        """Solve ``u = J^T u + grad`` by replays of the adjoint graph; returns ``(u, iterations)``."""
+        self.grad.copy_(grad)
+        self.u.copy_(grad)
+        thresh = tol * (grad.norm() + 1e-9)
+        self.thresh2.copy_(thresh * thresh)
+        cell.refresh_filters()  # the optimiser may have changed the weights since the capture
+        flags = LaggedFlags(min(lag, 1), max_iter) if lag > 0 else None
+        it, P = 0, self.chunk
+        while it + P <= max_iter:
+            self.g_adj.replay()
+            it += P
+            if flags is None:
+                if float(self.dmax) > 0.5:
+                    return self.u.clone(), it
+            else:
+                flags.push(it - 1, self.dmax)
+                hit = flags.pop_ready()
+                if hit is not None and hit[1] > 0.5:
+                    return self.u.clone(), it
+        u = self.u.clone()
+        while it < max_iter:  # a partial period: eager iterations
+            u, _ = AO.adjoint_step(cell.vjp(self.state, u), self.grad, u)
+            it += 1
+        return u, it
 
 
 class DEQFixedPoint(nn.Module):
@@ -141,22 +325,55 @@ class DEQFixedPoint(nn.Module):
         self.check_lag = check_lag
         self.last_iters = 0
         self.last_bwd_iters = 0
+        self.use_graphs = GRAPHS  # HIP graphs of the solver loops (SolverGraphs), GPU fused path
+        self._graphs: dict = {}   # input signature -> SolverGraphs (None after the first, eager call)
+
+    def _graphs_for(self, x) -> SolverGraphs | None:
+        if not (self.use_graphs and x.is_cuda and MANUAL_VJP and hasattr(self.f, "manual_ok")
+                and self.f.manual_ok(x)) or torch.cuda.is_current_stream_capturing():
+            return None
+        key = (tuple(x.shape), x.stride(), x.dtype, x.device)
+        if key not in self._graphs:  # first call at this shape: eager (measures the kernel choices)
+            self._graphs[key] = None
+            return None
+        gs = self._graphs[key]
+        if gs is None:
+            gs = self._graphs[key] = SolverGraphs(x)
+        else:
+            gs.x.copy_(x)
+        return gs
 
     def forward(self, x):
-        # the cell's GroupNorm parameters cast to fp32 once for the ~30 calls below
-        with fp32_affine_cache(self.f):
-            return self._forward(x)
+        gs = self._graphs_for(x)
+        # the cell's GroupNorm parameters cast to fp32 once for the ~30 calls below (into the
+        # graphs' static buffers when the solver loops replay graphs)
+        with fp32_affine_cache(self.f, buffers=gs.aff if gs is not None else None):
+            return self._forward(x, gs)
 
-    def _forward(self, x):
+    def _forward(self, x, gs: SolverGraphs | None = None):
         # the solver's ~30 evaluations by direct kernel calls when the cell allows (no autograd
         # Function objects per call: the DEQ step is host-bound, profiles/rd3h_ab_deq.jsonl)
         raw = MANUAL_VJP and hasattr(self.f, "manual_ok") and self.f.manual_ok(x)
-        fz = (lambda z: self.f.forward_raw(z, x)) if raw else (lambda z: self.f(z, x))
+        xs = gs.x if gs is not None else x  # the solve reads the graphs' static copy
+        fz = _CellEval(self.f, xs, raw)
         with torch.no_grad():
             z, self.last_iters, _ = anderson(fz, torch.zeros_like(x), max_iter=self.max_iter,
-                                             tol=self.tol, check_lag=self.check_lag)
+                                             tol=self.tol, check_lag=self.check_lag, graphs=gs)
         z = self.f(z, x)  # one differentiable step re-engages autograd at z*
         if not torch.is_grad_enabled():
+            return z
+        if gs is not None:
+            if gs.g_adj is None:
+                gs.capture_adjoint(self.f, z.detach(), max(1, min(GRAPH_CHUNK, self.bwd_iter)))
+            gs.forward_state(z.detach())
+
+            def graphed_hook(grad):
+                lag = CHECK_LAG if self.check_lag is None else int(self.check_lag)
+                u, self.last_bwd_iters = gs.adjoint(self.f, grad, self.bwd_tol, self.bwd_iter, lag)
+                return u
+
+            if z.requires_grad:
+                z.register_hook(graphed_hook)
             return z
         z0 = z.clone().detach().requires_grad_()
         manual = MANUAL_VJP and hasattr(self.f, "manual_ok") and self.f.manual_ok(z0)
@@ -230,6 +447,15 @@ class ResidualCell(nn.Module):
                 and gn_native_ok(z, self.n1.num_groups) and gn_native_ok(z, self.n3.num_groups)
                 and gn_native_ok(z, self.n2.num_groups))
 
+    def refresh_filters(self) -> None:
+        """Re-derive the cached transposed filters of both convolutions from the current weights
+        now (one batched launch), as the first input gradient of a backward would: the solver
+        graphs replay input-gradient GEMMs that read that cache."""
+        from ..ops.gemm import filter_t, note_filter
+        note_filter(self.conv1.weight)
+        note_filter(self.conv2.weight)
+        filter_t(self.conv1.weight)
+
     @torch.no_grad()
     def forward_raw(self, z, x):
         """``f(z, x)`` by direct kernel calls (no autograd Functions): the solver iterations."""
@@ -237,9 +463,13 @@ class ResidualCell(nn.Module):
 
     @torch.no_grad()
     def forward_state(self, z, x, keep: bool = True):
-        """``f(z, x)`` without autograd, keeping what :meth:`vjp` needs (GPU fused path)."""
+        """``f(z, x)`` without autograd, keeping what :meth:`vjp` needs (GPU fused path): one
+        LDS-resident kernel per evaluation where it applies (ops/deq_cell.py), else 5 launches."""
+        from ..ops import deq_cell
         from ..ops.fused_block import conv3x3_fwd_raw
         from ..ops.groupnorm import gn_fwd_raw
+        if deq_cell.supported(self, z):
+            return deq_cell.cell_forward(self, z, x, keep=keep)
         c1 = conv3x3_fwd_raw(z, self.conv1.weight)
         a1, h1, m1, r1, w1 = gn_fwd_raw(c1, None, self.n1.weight, self.n1.bias, self.n1.num_groups, self.n1.eps, True)
         c2 = conv3x3_fwd_raw(a1, self.conv2.weight)
@@ -253,8 +483,11 @@ class ResidualCell(nn.Module):
     def vjp(self, state, u):
         """``J_f(z)^T u`` from :meth:`forward_state`'s state by direct kernel calls — the adjoint
         solve's per-iteration VJP without the autograd engine (~6 launches per iteration)."""
+        from ..ops import deq_cell
         from ..ops.fused_block import conv3x3_dgrad_raw
         from ..ops.groupnorm import gn_bwd_raw
+        if deq_cell.supported(self, u):
+            return deq_cell.cell_vjp(self, state, u)
         zs, (h1, m1, r1, w1), (h2, m2, r2, w2), (h3, m3, r3, w3) = state
         d3, _ = gn_bwd_raw(u, h3, m3, r3, w3, self.n3.num_groups, True)    # d(z + a2), ReLU-masked
         d2, _ = gn_bwd_raw(d3, h2, m2, r2, w2, self.n2.num_groups, False)  # d conv2 output (x is constant)

@@ -45,10 +45,15 @@ class fp32_affine_cache:
 
     The DEQ solver calls its cell ~30 times per forward with unchanged parameters: two cast
     kernels per GroupNorm per call were ~190 launches per step. The copies are only valid while
-    the parameters do not change, i.e. within one forward pass."""
+    the parameters do not change, i.e. within one forward pass.
 
-    def __init__(self, module: nn.Module):
+    ``buffers`` (a dict the caller keeps): the copies are written into the same fp32 tensors on
+    every entry instead of fresh ones, so a HIP graph captured inside the context keeps reading
+    the current values (models/deq.py's solver graphs)."""
+
+    def __init__(self, module: nn.Module, buffers: dict | None = None):
         self.module = module
+        self.buffers = buffers
 
     def __enter__(self):
         global _AFFINE32
@@ -57,7 +62,15 @@ class fp32_affine_cache:
             if isinstance(mod, FusedGroupNorm):
                 for p in (mod.weight, mod.bias):
                     if p is not None and p.dtype != torch.float32:
-                        cache[id(p)] = (p, p.detach().float().contiguous())
+                        if self.buffers is None:
+                            cache[id(p)] = (p, p.detach().float().contiguous())
+                            continue
+                        buf = self.buffers.get(id(p))
+                        if buf is None or buf[0] is not p:
+                            buf = self.buffers[id(p)] = (p, torch.empty(p.shape, device=p.device,
+                                                                         dtype=torch.float32))
+                        buf[1].copy_(p.detach())
+                        cache[id(p)] = buf
         self._prev, _AFFINE32 = _AFFINE32, cache
         return self
 

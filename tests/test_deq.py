@@ -376,3 +376,149 @@ def test_deq_train_step_manual_vjp_gpu(gpu_ext, monkeypatch):
     for a, b in zip(*grads):
         rel = float((a - b).norm() / b.norm().clamp_min(1e-12))
         assert rel < 5e-2, rel
+
+
+def _deq_bf16(**kw):
+    m = deq_mnist(**kw).cuda().to(memory_format=torch.channels_last)
+    for mod in m.modules():
+        if type(mod).__name__ not in ("FusedBatchNorm2d",):
+            for p in mod.parameters(recurse=False):
+                p.data = p.data.to(torch.bfloat16)
+    return m
+
+
+def _graphed_vs_eager(steps, **kw):
+    """``steps`` SGD training steps of the same bf16 DEQ, solver graphs off / on; per step the
+    output, the parameter gradients and the iteration counts."""
+    torch.manual_seed(7)
+    x = torch.randn(32, 1, 28, 28, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (32,), device="cuda")
+    runs = []
+    for graphs in (False, True):
+        torch.manual_seed(3)
+        m = _deq_bf16(**kw)
+        m.deq.use_graphs = graphs
+        rec = []
+        for step in range(steps):
+            out = m(x)
+            F.cross_entropy(out.float(), y).backward()
+            rec.append((out.detach().float().clone(), [p.grad.float().clone() for p in m.parameters()],
+                        m.deq.last_iters, m.deq.last_bwd_iters))
+            # parameters change in place between steps (the same change in both runs, independent of
+            # the gradients): the graphs must read the current weights / affine copies / filters
+            with torch.no_grad():
+                for i, p in enumerate(m.parameters()):
+                    p.grad = None
+                    p.mul_(1.0 + 0.03 * ((i + step) % 3 - 1))
+        runs.append(rec)
+        if graphs:
+            gs = [g for g in m.deq._graphs.values() if g is not None]
+            assert len(gs) == 1 and gs[0].g_fwd is not None and gs[0].g_adj is not None
+    return runs
+
+
+@pytest.mark.gpu
+def test_deq_solver_graphs_match_eager(gpu_ext):
+    """The solver graphs (deq.SolverGraphs) replay exactly the eager loops' launches: with no
+    early exit (tol 0) four training steps — eager, capture, replay, replay — give the eager
+    run's outputs, gradients and iteration counts (max_iter 13 / bwd_iter 12 also exercise the
+    eager head and tail around the replayed periods)."""
+    eager, graphed = _graphed_vs_eager(4, max_iter=13, tol=0.0, bwd_iter=12, bwd_tol=0.0)
+    for s, ((oa, ga, ia, ba), (ob, gb, ib, bb)) in enumerate(zip(eager, graphed)):
+        assert (ia, ba) == (ib, bb) == (12, 12), (s, ia, ba, ib, bb)
+        torch.testing.assert_close(ob, oa, rtol=2e-2, atol=2e-2)
+        for a, b in zip(ga, gb):
+            rel = float((b - a).norm() / a.norm().clamp_min(1e-12))
+            assert rel < 2e-2, (s, rel)
+
+
+@pytest.mark.gpu
+def test_deq_solver_graphs_early_exit(gpu_ext):
+    """With a reachable tolerance the graphed solves stop within two periods of the eager ones
+    (per-period, one-period-late tests) and land on the same fixed point."""
+    eager, graphed = _graphed_vs_eager(3, max_iter=60, tol=1e-2, bwd_iter=60, bwd_tol=1e-2)
+    for (oa, ga, ia, ba), (ob, gb, ib, bb) in zip(eager, graphed):
+        assert ia < 59 and ba < 60, (ia, ba)  # the eager solves converge
+        assert ia <= ib <= ia + 10 and ba <= bb <= ba + 10, (ia, ib, ba, bb)
+        torch.testing.assert_close(ob, oa, rtol=5e-2, atol=5e-2)
+        for a, b in zip(ga, gb):
+            rel = float((b - a).norm() / a.norm().clamp_min(1e-12))
+            assert rel < 2.5e-1, rel  # more (still contracting) iterations: a different point
+
+
+def _cell_inputs(n=6, seed=0):
+    from fluxmpi_amd.models.deq import ResidualCell
+    torch.manual_seed(seed)
+    cell = ResidualCell(48).cuda()
+    with torch.no_grad():
+        for p in cell.parameters():
+            p.add_(0.05 * torch.randn_like(p))
+        for c in (cell.conv1, cell.conv2):
+            c.weight.mul_(20.0)  # O(1) activations through the convolutions
+    cell = cell.to(torch.bfloat16).to(memory_format=torch.channels_last)
+    z = torch.randn(n, 48, 28, 28, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    x = torch.randn_like(z)
+    return cell, z, x
+
+
+def _ref_cell_fp32(cell, z, x):
+    """f(z, x) in plain fp32 PyTorch ops from the cell's (bf16) parameters."""
+    P = {k: v.float() for k, v in cell.state_dict().items()}
+
+    def gn(t, i):
+        m = getattr(cell, f"n{i}")
+        return F.group_norm(t, m.num_groups, P[f"n{i}.weight"], P[f"n{i}.bias"], m.eps)
+
+    zf, xf = z.float(), x.float()
+    a1 = gn(torch.relu(F.conv2d(zf, P["conv1.weight"], padding=1)), 1)
+    a2 = gn(F.conv2d(a1, P["conv2.weight"], padding=1) + xf, 2)
+    return gn(torch.relu(zf + a2), 3)
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
+
+
+@pytest.mark.gpu
+def test_deq_fused_cell_forward(gpu_ext, monkeypatch):
+    """The one-kernel cell (ops/deq_cell.py) against the 5-launch raw path and an fp32 reference:
+    output, saved GroupNorm inputs and statistics; the fp32 history-slot output."""
+    from fluxmpi_amd.ops import deq_cell
+    cell, z, x = _cell_inputs()
+    assert deq_cell.supported(cell, z)
+    out_f, st_f = cell.forward_state(z, x)
+    monkeypatch.setattr(deq_cell, "ENABLED", False)
+    out_u, st_u = cell.forward_state(z, x)
+    ref = _ref_cell_fp32(cell, z, x)
+    e_f, e_u = _rel(out_f, ref), _rel(out_u, ref)
+    assert e_f < 2 * e_u + 5e-3, (e_f, e_u)
+    assert _rel(out_f, out_u) < 2e-2
+    for (hf, mf, rf, _), (hu, mu, ru, _) in zip(st_f[1:], st_u[1:]):
+        assert _rel(hf, hu) < 2e-2 and _rel(mf, mu) < 2e-2 and _rel(rf, ru) < 2e-2
+    # fp32 output into strided history rows (an Anderson slot): exactly the bf16 output's values
+    monkeypatch.setattr(deq_cell, "ENABLED", True)
+    n = z.shape[0]
+    hist = torch.full((n, 3, z[0].numel()), float("nan"), device="cuda")
+    deq_cell.cell_forward(cell, z, x, out32=hist[:, 1], want_out=False)
+    torch.testing.assert_close(hist[:, 1], out_f.permute(0, 2, 3, 1).reshape(n, -1).float(), rtol=0, atol=0)
+    assert torch.isnan(hist[:, 0]).all() and torch.isnan(hist[:, 2]).all()
+
+
+@pytest.mark.gpu
+def test_deq_fused_cell_vjp(gpu_ext, monkeypatch):
+    """The one-kernel adjoint VJP against the 5-launch raw VJP (same state) and fp32 autograd."""
+    from fluxmpi_amd.ops import deq_cell
+    cell, z, x = _cell_inputs(seed=1)
+    _, state = cell.forward_state(z, x)
+    zf = z.float().requires_grad_()
+    ref_out = _ref_cell_fp32(cell, zf, x)
+    for k in range(2):
+        u = torch.randn_like(z)
+        got = cell.vjp(state, u)
+        monkeypatch.setattr(deq_cell, "ENABLED", False)
+        base = cell.vjp(state, u)
+        monkeypatch.setattr(deq_cell, "ENABLED", True)
+        ref = torch.autograd.grad(ref_out, zf, u.float(), retain_graph=True)[0]
+        e_f, e_u = _rel(got, ref), _rel(base, ref)
+        assert e_f < 2 * e_u + 5e-3, (k, e_f, e_u)
+        assert _rel(got, base) < 3e-2, (k, _rel(got, base))
