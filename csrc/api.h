@@ -282,9 +282,14 @@ void deq_cell_fwd(const void* z, const void* x, const void* w1, const void* w2, 
                   const float* const* gn_b, void* out, float* out32, int64_t out32_stride, void* const* h,
                   float* const* mean, float* const* rstd, int64_t N, int64_t H, int64_t W, int64_t C, int64_t G,
                   float eps, hipStream_t stream);
+// grad / ss_part (nullable together): the adjoint update fused in, out = bf16(J^T u + grad) and
+// ss_part[N] the per-sample sum of (out - u)^2; deq_adjoint_check sums them (ss_out) and tests
+// flag = (sum <= *thresh2) in one tiny launch.
 void deq_cell_vjp(const void* u, const void* const* h, const void* w2t, const void* w1t, const float* const* gn_w,
-                  const float* const* mean, const float* const* rstd, void* out, int64_t N, int64_t H, int64_t W,
-                  int64_t C, int64_t G, hipStream_t stream);
+                  const float* const* mean, const float* const* rstd, void* out, const void* grad, float* ss_part,
+                  int64_t N, int64_t H, int64_t W, int64_t C, int64_t G, hipStream_t stream);
+void deq_adjoint_check(const float* part, int64_t n, const float* thresh2, float* ss_out, float* flag,
+                       hipStream_t stream);
 
 // ---- GELU backward + bias gradient (transformer MLP fc1) ---------------------------------
 // dh = dy * gelu'(h) (exact erf form); partials[blocks][N] = per-workgroup column sums of dh

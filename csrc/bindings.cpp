@@ -260,7 +260,8 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("deq_cell_vjp", [](uintptr_t u, std::array<uintptr_t, 3> h, uintptr_t w2t, uintptr_t w1t,
                            std::array<uintptr_t, 3> gw, std::array<uintptr_t, 3> mean, std::array<uintptr_t, 3> rstd,
-                           uintptr_t out, int64_t N, int64_t H, int64_t W, int64_t C, int64_t G, uintptr_t stream) {
+                           uintptr_t out, uintptr_t grad, uintptr_t ss_part, int64_t N, int64_t H, int64_t W,
+                           int64_t C, int64_t G, uintptr_t stream) {
     const void* hp[3];
     const float* gwp[3];
     const float* mp[3];
@@ -272,8 +273,13 @@ PYBIND11_MODULE(_C, m) {
       rp[i] = reinterpret_cast<const float*>(rstd[i]);
     }
     deq_cell_vjp(reinterpret_cast<const void*>(u), hp, reinterpret_cast<const void*>(w2t),
-                 reinterpret_cast<const void*>(w1t), gwp, mp, rp, reinterpret_cast<void*>(out), N, H, W, C, G,
-                 S(stream));
+                 reinterpret_cast<const void*>(w1t), gwp, mp, rp, reinterpret_cast<void*>(out),
+                 reinterpret_cast<const void*>(grad), reinterpret_cast<float*>(ss_part), N, H, W, C, G, S(stream));
+  });
+  m.def("deq_adjoint_check", [](uintptr_t part, int64_t n, uintptr_t thresh2, uintptr_t ss_out, uintptr_t flag,
+                                uintptr_t stream) {
+    deq_adjoint_check(reinterpret_cast<const float*>(part), n, reinterpret_cast<const float*>(thresh2),
+                      reinterpret_cast<float*>(ss_out), reinterpret_cast<float*>(flag), S(stream));
   });
 
   // ---- GELU backward + bias gradient -------------------------------------------------

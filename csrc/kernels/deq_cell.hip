@@ -485,6 +485,8 @@ struct VjpArgs {
   const float* mean[3];
   const float* rstd[3];
   bf16* out;
+  const bf16* grad;  // nullable: fuse the adjoint update, out = bf16(J^T u + grad), and
+  float* ss_part;    //   ss_part[n] = sum over the sample of (out - u)^2 (adjoint_step_kernel's numerics)
 };
 
 __global__ __launch_bounds__(kThreads) void deq_cell_vjp_kernel(VjpArgs a, CellShape s) {
@@ -530,7 +532,50 @@ __global__ __launch_bounds__(kThreads) void deq_cell_vjp_kernel(VjpArgs a, CellS
     for (int i = 0; i < kNBW; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[mb][i][j] = static_cast<bf16>(acc[mb][i][j] + fv(hv, mb, i, j));
+  if (a.grad != nullptr) {  // the adjoint iteration's update u <- J^T u + grad and its step size
+    load_lane(hv, a.grad + so, L);
+    Pk uv;
+    load_lane(uv, a.u + so, L);
+    float ss = 0.f;
+#pragma unroll
+    for (int mb = 0; mb < kMB; ++mb)
+#pragma unroll
+      for (int i = 0; i < kNBW; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bf16 r = static_cast<bf16>(fv(v, mb, i, j) + fv(hv, mb, i, j));
+          const float dlt = static_cast<float>(r) - fv(uv, mb, i, j);  // zero on absent blocks
+          ss = fmaf(dlt, dlt, ss);
+          v[mb][i][j] = r;
+        }
+    ss = wave_sum_dpp(ss);
+    if (L.l == 0) part[L.w] = ss;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) t += part[w];
+      a.ss_part[n] = t;
+    }
+  }
   store_lane(a.out + so, v, L);
+}
+
+// sum of the per-sample step sizes; flag = (sum <= *thresh2) — the adjoint's convergence test
+__global__ __launch_bounds__(256) void deq_adjoint_check_kernel(const float* __restrict__ part, int n,
+                                                                const float* __restrict__ thresh2,
+                                                                float* __restrict__ ss_out, float* __restrict__ flag) {
+  __shared__ float red[4];
+  float t = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) t += part[i];
+  t = wave_sum_dpp(t);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float tot = (red[0] + red[1]) + (red[2] + red[3]);
+    if (ss_out != nullptr) ss_out[0] = tot;
+    if (flag != nullptr) flag[0] = tot <= thresh2[0] ? 1.f : 0.f;
+  }
 }
 
 CellShape cell_shape(int64_t N, int64_t H, int64_t W, int64_t C, int64_t G, float eps) {
@@ -602,15 +647,17 @@ void deq_cell_fwd(const void* z, const void* x, const void* w1, const void* w2, 
 }
 
 void deq_cell_vjp(const void* u, const void* const* h, const void* w2t, const void* w1t, const float* const* gn_w,
-                  const float* const* mean, const float* const* rstd, void* out, int64_t N, int64_t H, int64_t W,
-                  int64_t C, int64_t G, hipStream_t stream) {
+                  const float* const* mean, const float* const* rstd, void* out, const void* grad, float* ss_part,
+                  int64_t N, int64_t H, int64_t W, int64_t C, int64_t G, hipStream_t stream) {
   const CellShape s = cell_shape(N, H, W, C, G, 0.f);
-  check16({u, h[0], h[1], h[2], w2t, w1t, out});
+  check16({u, h[0], h[1], h[2], w2t, w1t, out, grad});
+  if ((grad == nullptr) != (ss_part == nullptr)) throw std::runtime_error("deq_cell_vjp: grad and ss_part go together");
+  if (out == u) throw std::runtime_error("deq_cell_vjp: out must not alias u");
   for (int i = 0; i < 3; ++i)
     if (mean[i] == nullptr || rstd[i] == nullptr || h[i] == nullptr)
       throw std::runtime_error("deq_cell_vjp: missing state");
   VjpArgs a{static_cast<const bf16*>(u), {}, static_cast<const bf16*>(w2t), static_cast<const bf16*>(w1t), {}, {}, {},
-            static_cast<bf16*>(out)};
+            static_cast<bf16*>(out), static_cast<const bf16*>(grad), ss_part};
   for (int i = 0; i < 3; ++i) {
     a.h[i] = static_cast<const bf16*>(h[i]);
     a.gw[i] = gn_w[i];
@@ -624,6 +671,14 @@ void deq_cell_vjp(const void* u, const void* const* h, const void* w2t, const vo
     attr = true;
   }
   deq_cell_vjp_kernel<<<s.N, kThreads, lds, stream>>>(a, s);
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+}
+
+void deq_adjoint_check(const float* part, int64_t n, const float* thresh2, float* ss_out, float* flag,
+                       hipStream_t stream) {
+  if (n < 1 || n > 2147483647LL) throw std::runtime_error("deq_adjoint_check: bad n");
+  if (flag != nullptr && thresh2 == nullptr) throw std::runtime_error("deq_adjoint_check: flag needs thresh2");
+  deq_adjoint_check_kernel<<<1, 256, 0, stream>>>(part, static_cast<int>(n), thresh2, ss_out, flag);
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
 

@@ -34,9 +34,9 @@ from ..ops.groupnorm import native_ok as gn_native_ok
 CHECK_LAG = int(os.environ.get("FLUXMPI_DEQ_CHECK_LAG", "2"))
 # FLUXMPI_DEQ_MANUAL_VJP=0: the adjoint's VJPs through autograd.grad (A/B runs)
 MANUAL_VJP = os.environ.get("FLUXMPI_DEQ_MANUAL_VJP", "1") != "0"
-# FLUXMPI_DEQ_GRAPH=1: solver loops replay HIP graphs (SolverGraphs; opt-in, see tests);
+# FLUXMPI_DEQ_GRAPH=0: no solver graphs (every iteration launched from the host; A/B runs);
 # FLUXMPI_DEQ_GRAPH_CHUNK: adjoint iterations per graph replay
-GRAPHS = os.environ.get("FLUXMPI_DEQ_GRAPH", "0") == "1"  # opt-in until the replay-after-update check passes
+GRAPHS = os.environ.get("FLUXMPI_DEQ_GRAPH", "1") != "0"
 GRAPH_CHUNK = int(os.environ.get("FLUXMPI_DEQ_GRAPH_CHUNK", "5"))
 
 
@@ -232,7 +232,7 @@ class SolverGraphs:
         self._hist = None
         self.rbuf = self.rmin = None
         self.g_fwd = self.g_state = self.g_adj = None
-        self.state = self.z0 = self.grad = self.u = self.thresh2 = self.dmax = None
+        self.state = self.z0 = self.grad = self.u = self.thresh2 = self.dmax = self.done = None
         self.chunk = 0
 
     def history(self, m: int):
@@ -272,17 +272,18 @@ class SolverGraphs:
             self.grad = torch.empty_like(self.z0)
             self.u = torch.empty_like(self.z0)
             self.thresh2 = torch.zeros((), dtype=torch.float32, device=z.device)
-            done = torch.zeros(chunk, dtype=torch.float32, device=z.device)
+            # every tensor a graph reads or writes outside its own pool must stay referenced: a
+            # freed buffer would be handed to other tensors while the replays keep writing into it
+            self.done = torch.zeros(chunk, dtype=torch.float32, device=z.device)
             self.dmax = torch.zeros((), dtype=torch.float32, device=z.device)
             cell.refresh_filters()  # fresh now: the capture below records no refresh launch
             g = torch.cuda.CUDAGraph()
             with _capture(g):
                 u = self.u
                 for i in range(chunk):
-                    u, ss = AO.adjoint_step(cell.vjp(self.state, u), self.grad, u)
-                    done[i].copy_((ss <= self.thresh2).float())
+                    u, _ = cell.adjoint_step(self.state, u, self.grad, self.thresh2, self.done[i:i + 1])
                 self.u.copy_(u)
-                self.dmax.copy_(done.max())
+                self.dmax.copy_(self.done.max())
             self.g_adj = g
             self.chunk = chunk
 
@@ -312,7 +313,7 @@ class SolverGraphs:
                     return self.u.clone(), it
         u = self.u.clone()
         while it < max_iter:  # a partial period: eager iterations
-            u, _ = AO.adjoint_step(cell.vjp(self.state, u), self.grad, u)
+            u, _ = cell.adjoint_step(self.state, u, self.grad)
             it += 1
         return u, it
 
@@ -382,12 +383,17 @@ class DEQFixedPoint(nn.Module):
             # graph for f0, no engine overhead per iteration)
             _, state = self.f.forward_state(z0.detach(), x.detach())
             vjp = lambda u: self.f.vjp(state, u)  # noqa: E731
+            step = lambda u, g: self.f.adjoint_step(state, u, g)  # noqa: E731
         else:
             f0 = self.f(z0, x)
 
             def vjp(u):
                 with skip_param_grads():  # VJPs w.r.t. z only: no GroupNorm dw/db reductions
                     return torch.autograd.grad(f0, z0, u, retain_graph=True)[0]
+
+            def step(u, g):
+                # u_new = v + grad and |u_new - u|^2 in one pass (ops/anderson.adjoint_step)
+                return AO.adjoint_step(vjp(u), g, u)
 
         def backward_hook(grad):
             lag = (CHECK_LAG if self.check_lag is None else int(self.check_lag)) if grad.is_cuda else 0
@@ -401,9 +407,7 @@ class DEQFixedPoint(nn.Module):
             u = grad
             it = 0
             for it in range(self.bwd_iter):  # u = J^T u + grad
-                v = vjp(u)
-                # u_new = v + grad and |u_new - u|^2 in one pass (ops/anderson.adjoint_step)
-                u_new, ss = AO.adjoint_step(v, grad, u)
+                u_new, ss = step(u, grad)
                 done = ss <= thresh2
                 u = u_new
                 if flags is None:
@@ -494,6 +498,21 @@ class ResidualCell(nn.Module):
         da1 = conv3x3_dgrad_raw(d2, self.conv2.weight, h1.shape)
         d1, _ = gn_bwd_raw(da1, h1, m1, r1, w1, self.n1.num_groups, True)  # d conv1 output
         return conv3x3_dgrad_raw(d1, self.conv1.weight, zs, residual=d3)   # + n3's direct path to z
+
+    @torch.no_grad()
+    def adjoint_step(self, state, u, grad, thresh2=None, flag=None):
+        """One adjoint iteration ``u_new = J_f(z)^T u + grad`` with ``ss = |u_new - u|^2`` (0-d fp32
+        device tensor); with ``thresh2`` / ``flag`` also ``flag = ss <= thresh2`` on the device.
+        One-kernel cell: the update is fused into the VJP kernel (2 launches per iteration)."""
+        from ..ops import deq_cell
+        if deq_cell.supported(self, u):
+            u_new, part = deq_cell.cell_vjp(self, state, u, grad=grad)
+            t2 = None if thresh2 is None else thresh2.float()
+            return u_new, deq_cell.adjoint_check(part, t2, flag)
+        u_new, ss = AO.adjoint_step(self.vjp(state, u), grad, u)
+        if flag is not None:
+            flag.copy_((ss <= thresh2).float().reshape(flag.shape))
+        return u_new, ss
 
     def forward(self, z, x):
         # z feeds conv1 and n3's add: n3's backward hands its gradient of z to conv1's dgrad

@@ -92,8 +92,12 @@ def cell_forward(cell, z: torch.Tensor, x: torch.Tensor, keep: bool = False, out
     return out, state
 
 
-def cell_vjp(cell, state, u: torch.Tensor) -> torch.Tensor:
-    """``J_f(z)^T u`` in one launch from a ``forward_state`` state (fused or unfused producer)."""
+def cell_vjp(cell, state, u: torch.Tensor, grad: torch.Tensor | None = None):
+    """``J_f(z)^T u`` in one launch from a ``forward_state`` state (fused or unfused producer).
+
+    ``grad``: the adjoint iteration's update is fused in — returns ``(u_new, part)`` with
+    ``u_new = bf16(J^T u + grad)`` and ``part[n]`` the per-sample ``sum (u_new - u)^2`` (sum them
+    with :func:`adjoint_check`): one launch instead of the VJP + ``adjoint_step`` pair."""
     from .gemm import filter_t
     C = _ext.get(required=True)
     zs, (h1, m1, r1, w1), (h2, m2, r2, w2), (h3, m3, r3, w3) = state
@@ -107,11 +111,29 @@ def cell_vjp(cell, state, u: torch.Tensor) -> torch.Tensor:
         raise ValueError("deq_cell.cell_vjp: state does not match the gradient's shape")
     w2t, w1t = filter_t(cell.conv2.weight), filter_t(cell.conv1.weight)  # [ci][tap * co], taps flipped
     out = torch.empty_like(u, memory_format=torch.channels_last)
+    part = None
+    if grad is not None:
+        if not _cl(grad) or grad.dtype != torch.bfloat16:
+            grad = grad.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        if grad.shape != u.shape:
+            raise ValueError("deq_cell.cell_vjp: grad does not match u")
+        part = torch.empty(n, device=u.device, dtype=torch.float32)
     C.deq_cell_vjp(u.data_ptr(), [t.data_ptr() for t in hs], w2t.data_ptr(), w1t.data_ptr(),
                    [_ptr(w1), _ptr(w2), _ptr(w3)], [m1.data_ptr(), m2.data_ptr(), m3.data_ptr()],
-                   [r1.data_ptr(), r2.data_ptr(), r3.data_ptr()], out.data_ptr(), n, h, wd, ch, G,
-                   _stream(u))
-    return out
+                   [r1.data_ptr(), r2.data_ptr(), r3.data_ptr()], out.data_ptr(), _ptr(grad), _ptr(part),
+                   n, h, wd, ch, G, _stream(u))
+    return out if grad is None else (out, part)
 
 
-__all__ = ["ENABLED", "supported", "cell_forward", "cell_vjp"]
+def adjoint_check(part: torch.Tensor, thresh2: torch.Tensor | None = None, flag: torch.Tensor | None = None):
+    """``ss = part.sum()`` (0-d fp32, returned) and, with ``flag`` (1 fp32 element) and ``thresh2``
+    (fp32 device scalar), ``flag = ss <= thresh2`` — one launch."""
+    C = _ext.get(required=True)
+    ss = torch.empty((), device=part.device, dtype=torch.float32)
+    if flag is not None:
+        assert thresh2 is not None and thresh2.dtype == torch.float32 and flag.dtype == torch.float32
+    C.deq_adjoint_check(part.data_ptr(), part.numel(), _ptr(thresh2), ss.data_ptr(), _ptr(flag), _stream(part))
+    return ss
+
+
+__all__ = ["ENABLED", "supported", "cell_forward", "cell_vjp", "adjoint_check"]

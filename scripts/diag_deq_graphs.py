@@ -70,5 +70,7 @@ for fused in (False, True):
         worst_e = max(rel(a, b) for a, b in zip(e2[s][2], e1[s][2]))
         gr = [(rel(a, b), n) for a, b, n in zip(g[s][2], e1[s][2], e1[s][3])]
         worst_g = max(gr)
-        print(f"fused={fused} step={s} z* eager2 {zs[0]:.2e} graphed {zs[1]:.2e} | grads eager2 worst "
-              f"{worst_e:.2e} graphed worst {worst_g[0]:.2e} ({worst_g[1]})", flush=True)
+        ue = rel(g[s][1], e1[s][1]) if g[s][1] is not None else -1
+        print(f"fused={fused} step={s} z* eager2 {zs[0]:.2e} graphed {zs[1]:.2e} | u graphed {ue:.2e} | grads "
+              f"eager2 worst {worst_e:.2e} graphed worst {worst_g[0]:.2e} ({worst_g[1]})", flush=True)
+        print("   per-param graphed:", " ".join(f"{n}={e:.1e}" for e, n in gr), flush=True)

@@ -522,3 +522,26 @@ def test_deq_fused_cell_vjp(gpu_ext, monkeypatch):
         e_f, e_u = _rel(got, ref), _rel(base, ref)
         assert e_f < 2 * e_u + 5e-3, (k, e_f, e_u)
         assert _rel(got, base) < 3e-2, (k, _rel(got, base))
+
+
+@pytest.mark.gpu
+def test_deq_fused_adjoint_step(gpu_ext, monkeypatch):
+    """The adjoint update fused into the VJP kernel (u_new = J^T u + grad, |u_new - u|^2, the
+    device-side convergence flag) against the VJP + adjoint_step pair."""
+    from fluxmpi_amd.ops import deq_cell
+    cell, z, x = _cell_inputs(seed=2)
+    _, state = cell.forward_state(z, x)
+    u = torch.randn_like(z)
+    g = torch.randn_like(z)
+    flag = torch.full((1,), -1.0, device="cuda")
+    big = torch.tensor(1e30, device="cuda")
+    un_f, ss_f = cell.adjoint_step(state, u, g, big, flag)
+    assert float(flag) == 1.0
+    monkeypatch.setattr(deq_cell, "ENABLED", False)
+    un_u, ss_u = cell.adjoint_step(state, u, g)
+    assert _rel(un_f, un_u) < 3e-2
+    assert abs(float(ss_f) - float(ss_u)) <= 5e-2 * float(ss_u)
+    # the flag is exactly ss <= thresh2
+    monkeypatch.setattr(deq_cell, "ENABLED", True)
+    _, ss2 = cell.adjoint_step(state, u, g, torch.tensor(float(ss_f) * 0.5, device="cuda"), flag)
+    assert float(flag) == 0.0 and float(ss2) == float(ss_f)
