@@ -847,7 +847,178 @@ __global__ __launch_bounds__(1024) void attn_bwd_fused_kernel(AttnBwdArgs a) {
   }
 }
 
-int g_attn_bwd_fused = -1;  // -1: FLUXMPI_ATTN_BWD decides (fused / resident / blocked)
+// Two-phase backward, head resident (T <= 256): attn_bwd_dq_res and attn_bwd_dkv_res as the two
+// phases of ONE kernel, sharing one 2 x [TV][64] LDS image pair (57 KiB: two workgroups per CU,
+// as the pair's). Phase 1 (dQ) stages K, V and reads each wave's query rows of Q, dO, O from
+// global; phase 2 (dK, dV) first takes its key rows' K / V fragments out of those images, then
+// restages the pair with Q and dO. What the pair paid and this does not: the dkv kernel's
+// re-reads of Q, dO, K, V from HBM (the dq kernel had swept every head in between, so nothing
+// was left in L2; here phase 2's staging re-reads rows phase 1 of this and the sibling
+// workgroup just loaded, and K / V come from LDS), D = rowsum(dO * O) written and read back
+// through global memory (each part computes it for all queries in LDS), one launch.
+// a.nblk parts per (b, h): part p owns query rows [16 p nw, ..) in phase 1 and the same key rows
+// in phase 2 (nw waves).
+__global__ __launch_bounds__(1024) void attn_bwd_two_kernel(AttnBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int TP = (a.T + 15) & ~15, TV = (a.T + 31) & ~31;
+  char* img0 = smem;               // K (phase 1) | Q (phase 2), TV rows
+  char* img1 = smem + TV * 128;    // V (phase 1) | dO (phase 2), TV rows
+  float* sL = reinterpret_cast<float*>(smem + 2 * TV * 128);
+  float* sD = sL + TV;
+  int part, h, b;
+  res_coords(a, b, h, part);
+  const bf16* kb = a.k + b * a.sq_b + h * DH;
+  const bf16* vb = a.v + b * a.sq_b + h * DH;
+  const bf16* qb = a.q + b * a.sq_b + h * DH;
+  const bf16* gb = a.dout + b * a.sg_b + h * DH;
+  const bf16* ob = a.o + b * a.so_b + h * a.so_h;
+  stage_rows<false>(img0, kb, a.sq_t, TV, a.T);
+  stage_rows<false>(img1, vb, a.sq_t, TP, a.T);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, col = lane & 15, g = lane >> 4;
+  const int r0 = 16 * (part * (blockDim.x >> 6) + w);  // this wave's 16 queries, then 16 keys
+  const float c2 = a.scale * kLog2e;
+  float* st = a.stats + (static_cast<int64_t>(b) * a.H + h) * a.T * 2;
+  // ---------------- phase 1: dQ for queries r0 .. r0 + 15 (attn_bwd_dq_res)
+  {
+    const int qi = r0 + col;
+    const bool qok = qi < a.T;
+    const int64_t qoff = static_cast<int64_t>(qi) * a.sq_t;
+    bf16x8 qf[2] = {}, gf[2] = {}, o0 = {}, o1 = {};
+    float lse = 0.f;
+    if (qok) {
+      qf[0] = ld8(qb + qoff + 8 * g);
+      qf[1] = ld8(qb + qoff + 32 + 8 * g);
+      const bf16* gp = gb + static_cast<int64_t>(qi) * a.sg_t;
+      gf[0] = ld8(gp + 8 * g);
+      gf[1] = ld8(gp + 32 + 8 * g);
+      const bf16* op = ob + static_cast<int64_t>(qi) * a.so_t;
+      o0 = ld8(op + 8 * g);
+      o1 = ld8(op + 32 + 8 * g);
+      lse = st[2 * qi];
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (r0 < a.T) {  // wave-uniform
+      float dsum = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dsum += (float)gf[0][j] * (float)o0[j] + (float)gf[1][j] * (float)o1[j];
+      dsum = butterfly_from<16>(dsum);
+      const int nt = TP / 16;
+      f32x4 ds[kResMaxT / 16];
+#pragma unroll
+      for (int kt = 0; kt < kResMaxT / 16; ++kt) {
+        ds[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (kt < nt) {
+          const int row = 16 * kt + col;
+          f32x4 sv = {}, dp = {};
+          sv = mfma(img_row(img0, row, g), qf[0], sv);
+          sv = mfma(img_row(img0, row, 4 + g), qf[1], sv);
+          dp = mfma(img_row(img1, row, g), gf[0], dp);
+          dp = mfma(img_row(img1, row, 4 + g), gf[1], dp);
+          if (16 * kt + 16 <= a.T) {  // wave-uniform
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ds[kt][r] = fast_exp2(fmaf(sv[r], c2, -lse)) * (dp[r] - dsum);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int key = 16 * kt + 4 * g + r;
+              ds[kt][r] = key < a.T ? fast_exp2(fmaf(sv[r], c2, -lse)) * (dp[r] - dsum) : 0.f;
+            }
+          }
+        }
+      }
+      f32x4 acc[4] = {};
+#pragma unroll
+      for (int ks = 0; ks < kResMaxT / 32; ++ks) {
+        if (32 * ks < TV) {
+          const bf16x8 bop = pack(ds[2 * ks], ds[2 * ks + 1]);
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma(img_tr(img0, 32 * ks, 16 * dt), bop, acc[dt]);
+        }
+      }
+      if (qok) {
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const bf16x4 o = {(bf16)(acc[dt][0] * a.scale), (bf16)(acc[dt][1] * a.scale),
+                            (bf16)(acc[dt][2] * a.scale), (bf16)(acc[dt][3] * a.scale)};
+          *reinterpret_cast<bf16x4*>(a.dq + b * a.sq_b + qoff + h * DH + dt * 16 + 4 * g) = o;
+        }
+      }
+    }
+  }
+  // ---------------- phase 2: dK, dV for keys r0 .. r0 + 15 (attn_bwd_dkv_res)
+  const int ki = r0 + col;
+  const bool kok = ki < a.T;
+  bf16x8 kf[2], vf[2];
+  // this wave's K / V rows out of the phase-1 images (rows >= T are zero there; r0 < TP <= TV)
+  const int kr = ki < TV ? ki : TV - 1;  // waves past the last tile (r0 >= T) read a valid row
+  kf[0] = img_row(img0, kr, g);
+  kf[1] = img_row(img0, kr, 4 + g);
+  vf[0] = img_row(img1, kr, g);
+  vf[1] = img_row(img1, kr, 4 + g);
+  __syncthreads();  // every wave is done with the K / V images
+  stage_rows<false>(img0, qb, a.sq_t, TV, a.T);
+  stage_rows<false>(img1, gb, a.sg_t, TV, a.T);
+  // lse and D = rowsum(dO * O) of every query (8 lanes per row, 8 columns each)
+  for (int i = threadIdx.x; i < TV * 8; i += blockDim.x) {  // wave-uniform trip count (TV * 8 % 256 == 0)
+    const int qq = i >> 3, c8 = (i & 7) * 8;
+    float d = 0.f;
+    if (qq < a.T) {
+      const bf16x8 gv = ld8(gb + static_cast<int64_t>(qq) * a.sg_t + c8);
+      const bf16x8 ov = ld8(ob + static_cast<int64_t>(qq) * a.so_t + c8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d += (float)gv[j] * (float)ov[j];
+    }
+    d = xor_sum<4>(xor_sum<2>(xor_sum<1>(d)));
+    if ((i & 7) == 0) {
+      sD[qq] = d;
+      sL[qq] = qq < a.T ? st[2 * qq] : kInf;  // padded query: P = 0
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (r0 >= a.T) return;  // wave-uniform
+  f32x4 accK[4] = {}, accV[4] = {};
+#pragma unroll 2
+  for (int ks = 0; ks < TV / 32; ++ks) {
+    f32x4 p[2], dsv[2];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int row = 32 * ks + 16 * half + col;  // query row of the A fragment
+      f32x4 sv = {}, dp = {};
+      sv = mfma(img_row(img0, row, g), kf[0], sv);
+      sv = mfma(img_row(img0, row, 4 + g), kf[1], sv);
+      dp = mfma(img_row(img1, row, g), vf[0], dp);
+      dp = mfma(img_row(img1, row, 4 + g), vf[1], dp);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qq = 32 * ks + 16 * half + 4 * g + r;
+        const float pv = fast_exp2(fmaf(sv[r], c2, -sL[qq]));
+        p[half][r] = pv;
+        dsv[half][r] = pv * (dp[r] - sD[qq]);
+      }
+    }
+    const bf16x8 pb = pack(p[0], p[1]), db = pack(dsv[0], dsv[1]);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      accV[dt] = mfma(img_tr(img1, 32 * ks, 16 * dt), pb, accV[dt]);
+      accK[dt] = mfma(img_tr(img0, 32 * ks, 16 * dt), db, accK[dt]);
+    }
+  }
+  if (kok) {
+    const int64_t koff = b * a.sq_b + static_cast<int64_t>(ki) * a.sq_t + h * DH;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const bf16x4 v = {(bf16)accV[dt][0], (bf16)accV[dt][1], (bf16)accV[dt][2], (bf16)accV[dt][3]};
+      const bf16x4 k = {(bf16)(accK[dt][0] * a.scale), (bf16)(accK[dt][1] * a.scale),
+                        (bf16)(accK[dt][2] * a.scale), (bf16)(accK[dt][3] * a.scale)};
+      *reinterpret_cast<bf16x4*>(a.dv + koff + dt * 16 + 4 * g) = v;
+      *reinterpret_cast<bf16x4*>(a.dk + koff + dt * 16 + 4 * g) = k;
+    }
+  }
+}
+
+int g_attn_bwd_fused = -1;  // backward variant (attn_set_bwd_fused); -1: FLUXMPI_ATTN_BWD decides
 
 size_t fused_bwd_lds(int T) {
   const size_t TV = static_cast<size_t>((T + 31) & ~31);
@@ -889,11 +1060,13 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* o, const 
     const char* e = std::getenv("FLUXMPI_ATTN_BWD");
     return e == nullptr || std::string(e) != "blocked";
   }();
-  if (g_attn_bwd_fused < 0) {
+  static const int env_mode = [] {
     const char* e = std::getenv("FLUXMPI_ATTN_BWD");
-    g_attn_bwd_fused = (e != nullptr && std::string(e) == "fused") ? 1 : 0;
-  }
-  if (g_attn_bwd_fused == 1 && T <= kResMaxT && (sq_t % 8) == 0 && (sg_t % 8) == 0 && fused_bwd_lds(T) <= 160 * 1024) {
+    const std::string v = e != nullptr ? std::string(e) : std::string();
+    return v == "fused" ? 1 : (v == "two" ? 2 : 0);
+  }();
+  const int mode = g_attn_bwd_fused < 0 ? env_mode : g_attn_bwd_fused;
+  if (mode == 1 && T <= kResMaxT && (sq_t % 8) == 0 && (sg_t % 8) == 0 && fused_bwd_lds(T) <= 160 * 1024) {
     const int waves = (T + 15) / 16;
     const int64_t bh = static_cast<int64_t>(B) * H;
     if (bh > 0x7fffffff) throw std::runtime_error("attn_bwd: grid too large");
@@ -904,6 +1077,18 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* o, const 
       attr = true;
     }
     attn_bwd_fused_kernel<<<static_cast<unsigned>(bh), waves * 64, fused_bwd_lds(T), s>>>(a);
+    FLUXMPI_HIP_CHECK(hipGetLastError());
+    return;
+  }
+  if (mode == 2 && T <= kResMaxT && (sq_t % 8) == 0 && (sg_t % 8) == 0) {
+    const int tiles = (T + 15) / 16;
+    a.nblk = res_parts(tiles);
+    const int64_t bh = static_cast<int64_t>(B) * H * a.nblk;
+    if (bh > 0x7fffffff) throw std::runtime_error("attn_bwd: grid too large");
+    const int waves = (tiles + a.nblk - 1) / a.nblk;
+    const int TV = (T + 31) & ~31;
+    attn_bwd_two_kernel<<<static_cast<unsigned>(bh), waves * 64, static_cast<size_t>(2 * TV) * 128 + 2 * TV * 4,
+                          s>>>(a);
     FLUXMPI_HIP_CHECK(hipGetLastError());
     return;
   }
@@ -929,7 +1114,9 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* o, const 
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
 
-void attn_set_bwd_fused(int on) { g_attn_bwd_fused = on ? 1 : 0; }
+// backward variant for A/B runs and tests: -1 FLUXMPI_ATTN_BWD decides, 0 the dq / dkv pair,
+// 1 the one-kernel LDS-atomic backward, 2 the two-phase kernel
+void attn_set_bwd_fused(int mode) { g_attn_bwd_fused = mode < -1 || mode > 2 ? -1 : mode; }
 
 void attn_fwd(const void* q, const void* k, const void* v, void* o, float* stats, int64_t sq_b, int64_t sq_t,
               int64_t so_b, int64_t so_t, int64_t so_h, int B, int T, int H, int Dh, float scale, hipStream_t s) {

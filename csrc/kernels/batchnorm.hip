@@ -93,6 +93,11 @@ Geo geometry(int64_t rows, int64_t C, int64_t max_blocks = 2048) {
 // same-address atomics per line ~blocks/kShards: float atomics execute at the
 // memory side, and thousands of workgroups adding into ONE line serialise.
 constexpr int kShards = 64;  // <= ~200 same-address atomics even for 12k-block GEMM grids
+// The row-reduction kernels here run at most one round of resident workgroups (<= 2048): 16
+// shards keep <= 128 same-address atomics and make the in-kernel finalize's read 4x smaller.
+constexpr int kRedShards = 16;
+// a 32-bit arrival counter per workspace, behind the [kShards][2][kMaxC] shards (kept zero)
+constexpr size_t kCntOff = static_cast<size_t>(kShards) * 2 * kMaxC;
 
 __device__ __forceinline__ void block_reduce_atomic(float (&a)[8], float (&b)[8], int cv, int rpi, int C,
                                                     float* __restrict__ acc, float* smem) {
@@ -109,7 +114,7 @@ __device__ __forceinline__ void block_reduce_atomic(float (&a)[8], float (&b)[8]
     }
   }
   __syncthreads();
-  float* shard = acc + static_cast<size_t>(blockIdx.x % kShards) * 2 * C;
+  float* shard = acc + static_cast<size_t>(blockIdx.x % kRedShards) * 2 * C;
   for (int c = t; c < C; c += kThreads) {
     float x = 0.f, y = 0.f;
     for (int r = 0; r < rpi; ++r) {
@@ -215,10 +220,152 @@ __global__ __launch_bounds__(kFinCh * kFinGroups) void bn_finalize_bwd2_kernel(f
   (second ? dw2 : dw)[c] = q;
 }
 
+// ---------------------------------------------------------------- in-kernel finalize
+// The finalize as the tail of the reduction kernel itself: every workgroup, after its shard
+// atomics, releases them (agent-scope fence) and counts itself in on the workspace's arrival
+// counter; the LAST one to arrive sums the kRedShards shards (all other contributions are
+// visible to it after its acquire), writes the per-channel results, re-zeroes the shards and the
+// counter. One launch (and one dependent launch gap) less per BatchNorm pass: a separate
+// finalize is a ~5 us kernel on the critical path, 98 of them per ResNet-50 step.
+struct Fin {
+  int mode;  // 0: none (a finalize kernel follows); 1: forward statistics; 2: backward reductions
+  int64_t rows;
+  float momentum, eps;
+  float* smean;  // mode 1 outputs
+  float* sinv;
+  float* rmean;
+  float* rvar;
+  int64_t* nbt;
+  float* dw;  // mode 2 outputs (dw = sum(dy_eff * xhat), db = sum(dy_eff)); dw2/db2/acc2: dual
+  float* db;
+  float* dw2;
+  float* db2;
+};
+
+// fp32 sums of 4 consecutive channels over the kRedShards shards (16-B loads), shards re-zeroed
+__device__ __forceinline__ void take4(float* __restrict__ acc, int C, int c, float4& s, float4& q) {
+  float4 vs[kRedShards], vq[kRedShards];
+#pragma unroll
+  for (int k = 0; k < kRedShards; ++k) {
+    const float* sh = acc + static_cast<size_t>(k) * 2 * C;
+    vs[k] = *reinterpret_cast<const float4*>(sh + c);
+    vq[k] = *reinterpret_cast<const float4*>(sh + C + c);
+  }
+  s = make_float4(0.f, 0.f, 0.f, 0.f);
+  q = s;
+#pragma unroll
+  for (int k = 0; k < kRedShards; ++k) {
+    s.x += vs[k].x; s.y += vs[k].y; s.z += vs[k].z; s.w += vs[k].w;
+    q.x += vq[k].x; q.y += vq[k].y; q.z += vq[k].z; q.w += vq[k].w;
+  }
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int k = 0; k < kRedShards; ++k) {
+    float* sh = acc + static_cast<size_t>(k) * 2 * C;
+    *reinterpret_cast<float4*>(sh + c) = z;
+    *reinterpret_cast<float4*>(sh + C + c) = z;
+  }
+}
+
+__device__ __forceinline__ void fin_fwd_channel(const Fin& f, int c, float s, float q) {
+  const float inv_n = 1.f / static_cast<float>(f.rows);
+  const float mean = s * inv_n;
+  float var = q * inv_n - mean * mean;
+  var = var > 0.f ? var : 0.f;
+  f.smean[c] = mean;
+  f.sinv[c] = rsqrtf(var + f.eps);
+  if (f.rmean != nullptr) {
+    const float unbiased = f.rows > 1 ? var * static_cast<float>(f.rows) / static_cast<float>(f.rows - 1) : var;
+    f.rmean[c] = (1.f - f.momentum) * f.rmean[c] + f.momentum * mean;
+    f.rvar[c] = (1.f - f.momentum) * f.rvar[c] + f.momentum * unbiased;
+  }
+}
+
+// Call from EVERY thread of the workgroup after its block_reduce_atomic(s). acc2: the second
+// workspace of the dual backward (its counter is unused: acc's counts both).
+__device__ __forceinline__ void finalize_last(const Fin& f, float* __restrict__ acc, float* __restrict__ acc2, int C) {
+  if (f.mode == 0) return;
+  __shared__ unsigned s_last;
+  // This thread's shard atomics are complete (acknowledged) before the workgroup counts itself
+  // in. NOT __threadfence(): on gfx950 an agent-scope release is buffer_wbl2 (a write-back of the
+  // XCD's L2) — executed by every workgroup it made the reduction kernels ~50 us slower each
+  // (rd3o: 11.0k vs 12.5k img/s). The shard updates are atomics, so only their completion has to
+  // be ordered before the counter's; the "memory" clobber keeps the compiler from moving them.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  unsigned* cnt = reinterpret_cast<unsigned*>(acc + kCntOff);
+  if (threadIdx.x == 0) s_last = atomicAdd(cnt, 1u) == gridDim.x - 1 ? 1u : 0u;
+  __syncthreads();
+  if (s_last == 0u) return;
+  __threadfence();  // acquire, last workgroup only: no stale shard line left in this XCD's caches
+  for (int c = threadIdx.x * 4; c < C; c += kThreads * 4) {
+    float4 s, q;
+    take4(acc, C, c, s, q);
+    const float sv[4] = {s.x, s.y, s.z, s.w}, qv[4] = {q.x, q.y, q.z, q.w};
+    if (f.mode == 1) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fin_fwd_channel(f, c + j, sv[j], qv[j]);
+    } else {
+      *reinterpret_cast<float4*>(f.db + c) = s;
+      *reinterpret_cast<float4*>(f.dw + c) = q;
+      if (acc2 != nullptr) {
+        take4(acc2, C, c, s, q);
+        *reinterpret_cast<float4*>(f.db2 + c) = s;
+        *reinterpret_cast<float4*>(f.dw2 + c) = q;
+      }
+    }
+  }
+  if (threadIdx.x == 0) {
+    *cnt = 0u;
+    if (f.mode == 1 && f.nbt != nullptr) *f.nbt += 1;  // num_batches_tracked, no launch of its own
+  }
+}
+
+// FLUXMPI_BN_FIN=0: separate finalize kernels (the pre-round-3 path, for A/B)
+bool fin_in_kernel() {
+  static const bool on = [] {
+    const char* e = std::getenv("FLUXMPI_BN_FIN");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return on;
+}
+
+Fin no_fin() {
+  Fin f{};
+  f.mode = 0;
+  return f;
+}
+
+Fin fwd_fin(int64_t rows, float momentum, float eps, float* sm, float* si, float* rm, float* rv, int64_t* nbt) {
+  if (!fin_in_kernel()) return no_fin();
+  Fin f{};
+  f.mode = 1;
+  f.rows = rows;
+  f.momentum = momentum;
+  f.eps = eps;
+  f.smean = sm;
+  f.sinv = si;
+  f.rmean = rm;
+  f.rvar = rv;
+  f.nbt = nbt;
+  return f;
+}
+
+Fin bwd_fin(float* dw, float* db, float* dw2, float* db2) {
+  if (!fin_in_kernel()) return no_fin();
+  Fin f{};
+  f.mode = 2;
+  f.dw = dw;
+  f.db = db;
+  f.dw2 = dw2;
+  f.db2 = db2;
+  return f;
+}
+
 // ---------------------------------------------------------------- forward
 template <typename T>
 __global__ __launch_bounds__(kThreads) void bn_stats_kernel(const T* __restrict__ x, int64_t rows, int C, Geo g,
-                                                            float* __restrict__ acc) {
+                                                            float* __restrict__ acc, Fin fin) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int t = threadIdx.x;
   const int r0 = t / g.cv, c8 = t % g.cv;
@@ -254,6 +401,7 @@ __global__ __launch_bounds__(kThreads) void bn_stats_kernel(const T* __restrict_
     }
   }
   block_reduce_atomic(s, q, g.cv, g.rpi, C, acc, smem);
+  finalize_last(fin, acc, nullptr, C);
 }
 
 // y = act(x*scale + shift [+ res]); scale/shift derived from (mean, invstd) = batch
@@ -361,7 +509,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const T* __rest
                                                                  const float* __restrict__ b,
                                                                  const float* __restrict__ smean,
                                                                  const float* __restrict__ sinv, int64_t rows, int C,
-                                                                 Geo g, float* __restrict__ acc) {
+                                                                 Geo g, float* __restrict__ acc, Fin fin) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int t = threadIdx.x;
   const int r0 = t / g.cv, c8 = t % g.cv;
@@ -425,6 +573,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const T* __rest
     }
   }
   block_reduce_atomic(s, q, g.cv, g.rpi, C, acc, smem);
+  finalize_last(fin, acc, nullptr, C);
 }
 
 // dx = w*invstd * (dy_eff - sum_dy/R - xhat * sum_dy_xhat/R); dres = dy_eff
@@ -607,7 +756,8 @@ template <typename T>
 __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_dual_kernel(
     const T* __restrict__ dy, const uint8_t* __restrict__ mask, const T* __restrict__ x, const T* __restrict__ x2,
     const float* __restrict__ mean, const float* __restrict__ inv, const float* __restrict__ mean2,
-    const float* __restrict__ inv2, int64_t rows, int C, Geo g, float* __restrict__ acc, float* __restrict__ acc2) {
+    const float* __restrict__ inv2, int64_t rows, int C, Geo g, float* __restrict__ acc, float* __restrict__ acc2,
+    Fin fin) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int t = threadIdx.x;
   const int r0 = t / g.cv, c8 = t % g.cv;
@@ -663,6 +813,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_dual_kernel(
   block_reduce_atomic(s, q, g.cv, g.rpi, C, acc, smem);
   __syncthreads();  // the LDS staging is reused
   block_reduce_atomic(s, q2, g.cv, g.rpi, C, acc2, smem);
+  finalize_last(fin, acc, acc2, C);
 }
 
 // dx = A*dy_eff + B*x + D, dx2 = A2*dy_eff + B2*x2 + D2 (coefficients as in bn_bwd_dx_kernel)
@@ -814,11 +965,14 @@ void fwd_train_t(const void* x, void* y, const void* res, const float* w, const 
                  float* sm, float* si, float* ws, int64_t rows, int64_t C, float momentum, float eps, int relu,
                  uint8_t* mask, int64_t* nbt, hipStream_t s) {
   const Geo g = reduce_geometry(reinterpret_cast<const void*>(bn_stats_kernel<T>), rows, C);
-  bn_stats_kernel<T><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(static_cast<const T*>(x), rows, (int)C, g, ws);
+  const Fin fin = fwd_fin(rows, momentum, eps, sm, si, rm, rv, nbt);
+  bn_stats_kernel<T><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(static_cast<const T*>(x), rows, (int)C, g, ws, fin);
   FLUXMPI_HIP_CHECK(hipGetLastError());
-  bn_finalize_fwd_kernel<<<finalize_blocks(C), kFinCh * kFinGroups, 0, s>>>(ws, (int)C, rows, momentum, eps, sm, si, rm, rv,
-                                                                 nullptr, nullptr, nullptr, nullptr, nbt);
-  FLUXMPI_HIP_CHECK(hipGetLastError());
+  if (fin.mode == 0) {
+    bn_finalize_fwd_kernel<<<finalize_blocks(C), kFinCh * kFinGroups, 0, s>>>(ws, (int)C, rows, momentum, eps, sm, si, rm,
+                                                                              rv, nullptr, nullptr, nullptr, nullptr, nbt);
+    FLUXMPI_HIP_CHECK(hipGetLastError());
+  }
   norm_t<T>(x, y, res, w, b, sm, si, rows, C, eps, 1, relu, mask, s);
 }
 
@@ -835,8 +989,9 @@ void bwd_t(const void* dy, const void* x, const void* y, const uint8_t* mask, co
   {                                                                                                             \
     const Geo g = reduce_geometry(reinterpret_cast<const void*>(bn_bwd_reduce_kernel<T, RM>), rows, C);          \
     bn_bwd_reduce_kernel<T, RM><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(dyr, xr, yr, mask, w, b, sm, si,   \
-                                                                              rows, (int)C, g, ws);             \
+                                                                              rows, (int)C, g, ws, fin);        \
   }
+  const Fin fin = stats_ready ? no_fin() : bwd_fin(dw, db, nullptr, nullptr);
   // stats_ready: the reductions were accumulated into ws by the producer of dy (the GEMM's
   // BN-backward epilogue), so the reduce pass over (dy, x) is skipped
   if (stats_ready) {}
@@ -846,8 +1001,10 @@ void bwd_t(const void* dy, const void* x, const void* y, const uint8_t* mask, co
   else RED(3)
 #undef RED
   FLUXMPI_HIP_CHECK(hipGetLastError());
-  bn_finalize_bwd_kernel<<<finalize_blocks(C), kFinCh * kFinGroups, 0, s>>>(ws, (int)C, dw, db);
-  FLUXMPI_HIP_CHECK(hipGetLastError());
+  if (fin.mode == 0) {
+    bn_finalize_bwd_kernel<<<finalize_blocks(C), kFinCh * kFinGroups, 0, s>>>(ws, (int)C, dw, db);
+    FLUXMPI_HIP_CHECK(hipGetLastError());
+  }
   const int64_t nvec = rows * C / 8;
   T* dxr = static_cast<T*>(dx);
   T* drr = static_cast<T*>(dres);
@@ -894,11 +1051,15 @@ void bwd_dual_t(const void* dy, const uint8_t* mask, const void* x, const void* 
   const T* xr = static_cast<const T*>(x);
   const T* x2r = static_cast<const T*>(x2);
   const Geo g = reduce_geometry(reinterpret_cast<const void*>(bn_bwd_reduce_dual_kernel<T>), rows, C);
+  const Fin fin = bwd_fin(dw, db, dw2, db2);
   bn_bwd_reduce_dual_kernel<T><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(dyr, mask, xr, x2r, sm, si, sm2, si2,
-                                                                             rows, (int)C, g, ws, ws2);
+                                                                             rows, (int)C, g, ws, ws2, fin);
   FLUXMPI_HIP_CHECK(hipGetLastError());
-  bn_finalize_bwd2_kernel<<<dim3(finalize_blocks(C), 2), kFinCh * kFinGroups, 0, s>>>(ws, ws2, (int)C, dw, db, dw2, db2);
-  FLUXMPI_HIP_CHECK(hipGetLastError());
+  if (fin.mode == 0) {
+    bn_finalize_bwd2_kernel<<<dim3(finalize_blocks(C), 2), kFinCh * kFinGroups, 0, s>>>(ws, ws2, (int)C, dw, db, dw2,
+                                                                                        db2);
+    FLUXMPI_HIP_CHECK(hipGetLastError());
+  }
   const int64_t nvec = rows * C / 8;
   auto k = bn_bwd_dx_dual_kernel<T>;
   k<<<elementwise_grid(reinterpret_cast<const void*>(k), 0, nvec), kThreads, 0, s>>>(
@@ -975,11 +1136,15 @@ void bn_stats_finalize(const void* x, const float* w, const float* b, float* rm,
                        float* scale, float* shift, float* ws, int64_t rows, int64_t C, float momentum, float eps,
                        int stats_ready, int dtype, hipStream_t s, int64_t* nbt) {
   check(C);
+  // the stats pass finalizes in its last workgroup unless the consumer wants the GEMM affine
+  // (scale / shift: only the finalize kernel writes it)
+  const Fin fin = (stats_ready || scale != nullptr) ? no_fin() : fwd_fin(rows, momentum, eps, sm, si, rm, rv, nbt);
   if (!stats_ready) {
 #define STATS(T)                                                                                              \
   {                                                                                                          \
     const Geo g = reduce_geometry(reinterpret_cast<const void*>(bn_stats_kernel<T>), rows, C);               \
-    bn_stats_kernel<T><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(static_cast<const T*>(x), rows, (int)C, g, ws); \
+    bn_stats_kernel<T><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(static_cast<const T*>(x), rows, (int)C, g, ws, \
+                                                                     fin);                                     \
   }
     switch (dtype) {
       case kBF16: STATS(bf16) break;
@@ -990,9 +1155,11 @@ void bn_stats_finalize(const void* x, const float* w, const float* b, float* rm,
 #undef STATS
     FLUXMPI_HIP_CHECK(hipGetLastError());
   }
-  bn_finalize_fwd_kernel<<<finalize_blocks(C), kFinCh * kFinGroups, 0, s>>>(ws, (int)C, rows, momentum, eps, sm, si, rm, rv, w, b,
-                                                                 scale, shift, nbt);
-  FLUXMPI_HIP_CHECK(hipGetLastError());
+  if (fin.mode == 0) {
+    bn_finalize_fwd_kernel<<<finalize_blocks(C), kFinCh * kFinGroups, 0, s>>>(ws, (int)C, rows, momentum, eps, sm, si, rm,
+                                                                              rv, w, b, scale, shift, nbt);
+    FLUXMPI_HIP_CHECK(hipGetLastError());
+  }
 }
 
 void bn_apply(const void* x, void* y, const void* res, const float* w, const float* b, const float* sm,

@@ -14,6 +14,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _ext
+from . import graddst
 from .multi_tensor import DTYPE_CODE
 
 
@@ -36,19 +37,22 @@ def _nhwc(x: torch.Tensor) -> torch.Tensor:
 _WS: dict = {}
 _SHARDS = 64  # == kShards in csrc/kernels/{batchnorm,gemm}.hip
 _MAXC = 2048
+# [_SHARDS][2][_MAXC] shards + the arrival counter of the in-kernel finalize (kCntOff in batchnorm.hip)
+_WS_FLOATS = _SHARDS * 2 * _MAXC + 64
 
 
 def _workspace(x: torch.Tensor) -> torch.Tensor:
-    """Persistent zeroed [16][2][2048] fp32 accumulator per (device, stream).
+    """Persistent zeroed [64][2][2048] fp32 accumulator (+ an arrival counter) per (device, stream).
 
-    The kernels leave it zeroed after every call (the finalize kernel re-zeroes
-    the shards it consumes), so there is no memset per BatchNorm launch.
+    The kernels leave it zeroed after every call (the finalize — a kernel of its own, or the
+    last workgroup of the reduction kernel — re-zeroes the shards it consumes), so there is no
+    memset per BatchNorm launch.
     """
     stream = torch.cuda.current_stream(x.device)
     key = (x.device.index, stream.cuda_stream)
     ws = _WS.get(key)
     if ws is None:
-        ws = torch.zeros(_SHARDS * 2 * _MAXC, device=x.device, dtype=torch.float32)
+        ws = torch.zeros(_WS_FLOATS, device=x.device, dtype=torch.float32)
         _WS[key] = ws
     return ws
 
@@ -66,7 +70,7 @@ def _link_workspace(x: torch.Tensor) -> torch.Tensor:
     key = (x.device.index, stream.cuda_stream)
     ws = _LWS.get(key)
     if ws is None:
-        ws = torch.zeros(_SHARDS * 2 * _MAXC, device=x.device, dtype=torch.float32)
+        ws = torch.zeros(_WS_FLOATS, device=x.device, dtype=torch.float32)
         _LWS[key] = ws
     return ws
 
@@ -81,7 +85,7 @@ def _dual_workspace(x: torch.Tensor) -> torch.Tensor:
     key = (x.device.index, stream.cuda_stream)
     ws = _DWS.get(key)
     if ws is None:
-        ws = torch.zeros(_SHARDS * 2 * _MAXC, device=x.device, dtype=torch.float32)
+        ws = torch.zeros(_WS_FLOATS, device=x.device, dtype=torch.float32)
         _DWS[key] = ws
     return ws
 
@@ -93,6 +97,11 @@ def kernel_supported(x: torch.Tensor) -> bool:
         return False
     c = x.shape[1]
     return c % 8 == 0 and 8 <= c <= 2048 and x.numel() > 0
+
+
+def _grad_out(p, ch, like):
+    t = graddst.take(p, (ch,), torch.float32)
+    return t if t is not None else torch.empty(ch, device=like.device, dtype=torch.float32)
 
 
 class GradLink:
@@ -230,6 +239,7 @@ class _FusedBN(torch.autograd.Function):
         ctx.link = link if residual is not None else None
         ctx.wdtype = weight.dtype if weight is not None else None
         ctx.has_bias = bias is not None
+        ctx.params = (weight, bias)
         # Without a residual the ReLU mask is recomputed from x in the backward
         # kernels (bit-identical to the forward); with one, the 1-bit mask is used.
         # Either way y is neither saved nor re-read.
@@ -253,8 +263,8 @@ class _FusedBN(torch.autograd.Function):
         hand_masked = ctx.link is not None and ctx.link.masked and mask is not None and ctx.relu
         dres = torch.empty_like(x) if (ctx.has_res and not hand_masked) else None
         # the finalize kernel always produces both reductions (they feed dx)
-        dw = torch.empty(ch, device=x.device, dtype=torch.float32)
-        db = torch.empty(ch, device=x.device, dtype=torch.float32)
+        # fp32 parameters: straight into their DDP bucket slices when attached (graddst)
+        dw, db = (_grad_out(p, ch, x) for p in ctx.params)
         ws = _link_workspace(x) if stats_ready else _workspace(x)
         stream = torch.cuda.current_stream(x.device).cuda_stream
         C.bn_bwd(dy.data_ptr(), x.data_ptr(), 0, mask.data_ptr() if mask is not None else 0,

@@ -31,6 +31,7 @@ import os
 import torch
 
 from . import _ext
+from . import graddst
 from . import streams
 from .batchnorm import BNStatsLink, GradLink, SideGradLink, _dual_workspace, _link_workspace, _workspace, bn_counter  # noqa: F401 (links re-exported)
 from . import gemm as G
@@ -89,14 +90,22 @@ def _empty_nhwc(n, c, h, w, like):
     return torch.empty(n, h, w, c, device=like.device, dtype=like.dtype).permute(0, 3, 1, 2)
 
 
-def _bn_bwd(dy, x, mask, w32, b32, mean, inv, relu, has_res, stats_ready=False):
-    """Shared fused-BN backward; returns (dx, dres, dw, db) (fp32 dw/db)."""
+def _grad_out(p, ch, like):
+    """fp32 [ch] output for the gradient of BatchNorm parameter ``p``: its DDP bucket slice when
+    one is attached (``graddst``, fp32 parameters), else a fresh tensor."""
+    t = graddst.take(p, (ch,), torch.float32)
+    return t if t is not None else torch.empty(ch, device=like.device, dtype=torch.float32)
+
+
+def _bn_bwd(dy, x, mask, w32, b32, mean, inv, relu, has_res, stats_ready=False, params=(None, None)):
+    """Shared fused-BN backward; returns (dx, dres, dw, db) (fp32 dw/db; ``params`` = the
+    (weight, bias) leaves whose bucket slices may receive them)."""
     C = _ext.get(required=True)
     rows, ch = x.numel() // x.shape[1], x.shape[1]
     dx = torch.empty_like(x)
     dres = torch.empty_like(x) if has_res else None
-    dw = torch.empty(ch, device=x.device, dtype=torch.float32)
-    db = torch.empty(ch, device=x.device, dtype=torch.float32)
+    dw = _grad_out(params[0], ch, x)
+    db = _grad_out(params[1], ch, x)
     ws = _link_workspace(x) if stats_ready else _workspace(x)
     C.bn_bwd(dy.data_ptr(), x.data_ptr(), 0, _p(mask), _p(w32), _p(b32), mean.data_ptr(), inv.data_ptr(),
              dx.data_ptr(), _p(dres), dw.data_ptr(), db.data_ptr(), ws.data_ptr(), rows, ch, int(relu),
@@ -128,8 +137,9 @@ class _Conv1x1Stats(torch.autograd.Function):
         co, ci = weight.shape[0], weight.shape[1]
         dc2 = _nhwc2d(dc)
         # weight gradient first, on the side stream: it overlaps the input-gradient chain
-        dw = streams.run(lambda: conv1x1_wgrad(dc2, _nhwc2d(x), out_dtype=weight.dtype).view_as(weight), dc, x,
-                         param=weight)
+        with graddst.into(weight):  # into the DDP bucket slice when one is attached
+            dw = streams.run(lambda: conv1x1_wgrad(dc2, _nhwc2d(x), out_dtype=weight.dtype).view_as(weight), dc, x,
+                             param=weight)
         dx = _dgrad_nhwc(dc2, weight, x, ctx.link, ctx.bnlink) if ctx.needs_input_grad[0] else None
         return dx, dw, None, None
 
@@ -215,7 +225,7 @@ class _Conv1x1Hybrid(torch.autograd.Function):
             if _w256_ok(co, ci, dc):
                 from .linear import weight_grad
                 impls["w256"] = lambda: weight_grad(_nhwc2d(dc), _nhwc2d(x), weight.dtype).view(co, ci, 1, 1)
-            dw = streams.run(lambda: wgrad_best(("1x1", tuple(x.shape), co), impls), dc, x, param=weight)
+            dw = streams.run(lambda: wgrad_best(("1x1", tuple(x.shape), co), impls, param=weight), dc, x, param=weight)
         dx = _dgrad_nhwc(_nhwc2d(dc), weight, x, ctx.link, ctx.bnlink) if ctx.needs_input_grad[0] else None
         return dx, dw, None, None, None
 
@@ -338,7 +348,7 @@ def _ds_wgrad(dc, x, weight, s):
             impls["ours"] = lambda: G.conv1x1_wgrad_s2(_nhwc2d(dc), x, out_dtype=weight.dtype).view(co, ci, 1, 1)
     if "ours" not in impls:
         return impls["miopen"]()
-    return wgrad_best(("ds", tuple(x.shape), co, s), impls)
+    return wgrad_best(("ds", tuple(x.shape), co, s), impls, param=weight)
 
 
 def conv1x1_downsample(x, weight, stride, link=None, ours_stats=False):
@@ -375,6 +385,7 @@ class _BNFromStats(torch.autograd.Function):
         C.bn_apply(x.data_ptr(), y.data_ptr(), _p(res), w32.data_ptr(), b32.data_ptr(), mean.data_ptr(),
                    inv.data_ptr(), rows, ch, int(relu), _p(mask), DTYPE_CODE[x.dtype], _stream(x))
         ctx.relu, ctx.has_res, ctx.wdtype = relu, residual is not None, weight.dtype
+        ctx.params = (weight, bias)
         ctx.link = link if residual is not None else None
         ctx.bnlink = bnlink
         if bnlink is not None:
@@ -391,7 +402,7 @@ class _BNFromStats(torch.autograd.Function):
         # a masked GradLink takes (dy, mask) instead of dres = dy * mask (one write pass less)
         hand_masked = ctx.link is not None and ctx.link.masked and mask is not None and ctx.relu
         dx, dres, dw, db = _bn_bwd(dy, x, mask, w32, b32, mean, inv, ctx.relu, ctx.has_res and not hand_masked,
-                                   ready)
+                                   ready, ctx.params)
         if ctx.bnlink is not None:
             ctx.bnlink.release()
         if ctx.link is not None:
@@ -437,6 +448,7 @@ class _DualBN(torch.autograd.Function):
                         inv.data_ptr(), w232.data_ptr(), b232.data_ptr(), mean2.data_ptr(), inv2.data_ptr(), rows, ch,
                         mask.data_ptr(), code, st)
         ctx.wdtypes = (w.dtype, w2.dtype)
+        ctx.params = (w, b, w2, b2)
         ctx.save_for_backward(c3, cds, mask, w32, mean, inv, w232, mean2, inv2)
         return y
 
@@ -449,7 +461,7 @@ class _DualBN(torch.autograd.Function):
         ch = c3.shape[1]
         rows = c3.numel() // ch
         dx, dx2 = torch.empty_like(c3), torch.empty_like(cds)
-        dw, db, dw2, db2 = (torch.empty(ch, device=c3.device, dtype=torch.float32) for _ in range(4))
+        dw, db, dw2, db2 = (_grad_out(p, ch, c3) for p in ctx.params)
         C.bn_bwd_dual(dy.data_ptr(), mask.data_ptr(), c3.data_ptr(), cds.data_ptr(), w32.data_ptr(), mean.data_ptr(),
                       inv.data_ptr(), w232.data_ptr(), mean2.data_ptr(), inv2.data_ptr(), dx.data_ptr(),
                       dx2.data_ptr(), dw.data_ptr(), db.data_ptr(), dw2.data_ptr(), db2.data_ptr(),
@@ -528,9 +540,10 @@ class _BNReluConv1x1(torch.autograd.Function):
         c2_2d = _nhwc2d(c2)
         # dW = dc3^T @ relu(bn(c2))  — the activation is rebuilt on the fly in the B-operand load
         # (side stream: overlaps the input-gradient chain below)
-        dw = streams.run(lambda: conv1x1_wgrad(dc3_2d, c2_2d, in_affine=(scale, shift),
-                                               out_dtype=weight.dtype).view_as(weight), dc3, c2, scale, shift,
-                         param=weight)
+        with graddst.into(weight):
+            dw = streams.run(lambda: conv1x1_wgrad(dc3_2d, c2_2d, in_affine=(scale, shift),
+                                                   out_dtype=weight.dtype).view_as(weight), dc3, c2, scale, shift,
+                             param=weight)
         # d(relu(bn(c2))) = dc3 @ W with the BN-backward reductions (ReLU mask recomputed from c2)
         # accumulated in the same GEMM's epilogue, then the BN backward without its reduce pass
         da = conv1x1_dgrad(dc3_2d, weight.reshape(co, ch), bn_bwd=(c2_2d, w32, b32, mean, inv, None, 2),
@@ -570,7 +583,7 @@ class _Conv3x3(torch.autograd.Function):
             dw = streams.run(lambda: wgrad_best(("3x3", tuple(x.shape), weight.shape[0]), {
                 "miopen": lambda: torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [1, 1], [1, 1], False,
                                                                       [0, 0], 1, [False, True, False])[1],
-                "ours": lambda: G.conv3x3_wgrad(dy, x)}), dy, x, param=weight)
+                "ours": lambda: G.conv3x3_wgrad(dy, x)}, param=weight), dy, x, param=weight)
         dx = None
         if ctx.needs_input_grad[0]:
             bl = ctx.bnlink
@@ -649,7 +662,7 @@ class _Conv3x3S2(torch.autograd.Function):
             dw = streams.run(lambda: wgrad_best(("3x3s2", tuple(x.shape), weight.shape[0]), {
                 "miopen": lambda: torch.ops.aten.convolution_backward(dy, x, weight, None, [2, 2], [1, 1], [1, 1], False,
                                                                       [0, 0], 1, [False, True, False])[1],
-                "ours": lambda: G.conv3x3_wgrad_s2(dy, x)}), dy, x, param=weight)
+                "ours": lambda: G.conv3x3_wgrad_s2(dy, x)}, param=weight), dy, x, param=weight)
         if ctx.needs_input_grad[0]:
             dx = torch.ops.aten.convolution_backward(dy, x, weight, None, [2, 2], [1, 1], [1, 1], False, [0, 0], 1,
                                                      [True, False, False])[0]
@@ -748,9 +761,11 @@ def _w256_ok(co: int, ci: int, dc: torch.Tensor) -> bool:
     return bool(C.wgrad256_supported(co, ci, k, co, ci)) and k >= 4096
 
 
-def wgrad_best(key, impls: dict):
+def wgrad_best(key, impls: dict, param=None):
     """Run the fastest weight-gradient implementation for ``key`` (measured on first use, like
-    cudnn.benchmark: MIOpen vs our kernel in each of ``_WG_CONFIGS``) and return its result."""
+    cudnn.benchmark: MIOpen vs our kernel in each of ``_WG_CONFIGS``) and return its result.
+    ``param``: the weight, whose DDP bucket slice (if any) receives the returned gradient
+    (``graddst``; never during the measurements)."""
     choice = _WG_CHOICE.get(key)
     if choice is None:
         if WGRAD == "miopen" or _no_measure():
@@ -776,11 +791,13 @@ def wgrad_best(key, impls: dict):
         _WG_CHOICE[key] = choice
     name, cfg = choice
     if cfg is None:
-        return impls[name]()
+        with graddst.into(param):
+            return impls[name]()
     saved = G.WGRAD_VARIANT, G.WGRAD_TARGET_WG
     G.WGRAD_VARIANT, G.WGRAD_TARGET_WG = cfg
     try:
-        return impls[name]()
+        with graddst.into(param):
+            return impls[name]()
     finally:
         G.WGRAD_VARIANT, G.WGRAD_TARGET_WG = saved
 

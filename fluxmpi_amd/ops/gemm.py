@@ -16,6 +16,7 @@ import weakref
 import torch
 
 from . import _ext
+from . import graddst
 
 SHARDS = 64  # == kShards in csrc/kernels/{batchnorm,gemm}.hip
 # LDS buffering of the GEMM main loop: 0 = per-shape choice in the kernel launcher, 1 or 2 forces it
@@ -276,7 +277,7 @@ def conv1x1_wgrad(dy2d: torch.Tensor, x2d: torch.Tensor, in_affine=None, out: to
     Ci = x2d.shape[1]
     if out is not None:
         out_dtype = out.dtype
-    dw = out if out is not None else torch.empty(Co, Ci, device=dy2d.device, dtype=out_dtype)
+    dw = out if out is not None else graddst.empty((Co, Ci), out_dtype, dy2d.device)
     s = _actual_splits(M, splits or wgrad_splits(M, Co, Ci))
     common = dict(M=Co, N=Ci, K=M, lda=dy2d.stride(0), ldb=x2d.stride(0), ldc=Ci, a_kmajor=False, b_kmajor=False,
                   b_affine=in_affine)
@@ -333,7 +334,7 @@ def conv1x1_wgrad_v2(dy2d: torch.Tensor, x2d: torch.Tensor, out_dtype=torch.bflo
     C = _ext.get(required=True)
     C.gemm_wgrad(dy2d.data_ptr(), x2d.data_ptr(), ws.data_ptr(), dy2d.stride(0), x2d.stride(0), Co, Ci, K, s, 0, 0, 0,
                  _stream(dy2d), WGRAD_VARIANT | (0 if WGRAD_REMAP else 4))
-    return _wgrad_reduce(ws, s, torch.empty(Co, Ci, device=dy2d.device, dtype=out_dtype))
+    return _wgrad_reduce(ws, s, graddst.empty((Co, Ci), out_dtype, dy2d.device))
 
 
 def conv1x1_wgrad_s2(dy2d: torch.Tensor, x: torch.Tensor, out_dtype=torch.bfloat16, splits: int | None = None):
@@ -349,7 +350,7 @@ def conv1x1_wgrad_s2(dy2d: torch.Tensor, x: torch.Tensor, out_dtype=torch.bfloat
     C = _ext.get(required=True)
     C.gemm_wgrad(dy2d.data_ptr(), xs.data_ptr(), ws.data_ptr(), dy2d.stride(0), ci, Co, ci, K, s, h, w, 0,
                  _stream(dy2d), WGRAD_VARIANT | (0 if WGRAD_REMAP else 4), 1)
-    return _wgrad_reduce(ws, s, torch.empty(Co, ci, device=dy2d.device, dtype=out_dtype))
+    return _wgrad_reduce(ws, s, graddst.empty((Co, ci), out_dtype, dy2d.device))
 
 
 def conv3x3_wgrad_s2(dy: torch.Tensor, x: torch.Tensor, splits: int | None = None) -> torch.Tensor:
@@ -368,7 +369,7 @@ def conv3x3_wgrad_s2(dy: torch.Tensor, x: torch.Tensor, splits: int | None = Non
     C = _ext.get(required=True)
     C.gemm_wgrad(dys.data_ptr(), xs.data_ptr(), ws.data_ptr(), co, ci, co, N, K, s, h, wd, ci, _stream(dy),
                  WGRAD_VARIANT | (0 if WGRAD_REMAP else 4), 1)
-    dw = torch.empty(co, 3, 3, ci, device=dy.device, dtype=dy.dtype)
+    dw = graddst.empty((co, 3, 3, ci), dy.dtype, dy.device)
     _wgrad_reduce(ws, s, dw)
     return dw.permute(0, 3, 1, 2)
 
@@ -388,6 +389,6 @@ def conv3x3_wgrad(dy: torch.Tensor, x: torch.Tensor, splits: int | None = None) 
     C = _ext.get(required=True)
     C.gemm_wgrad(dys.data_ptr(), xs.data_ptr(), ws.data_ptr(), co, ci, co, N, K, s, h, wd, ci, _stream(dy),
                  WGRAD_VARIANT | (0 if WGRAD_REMAP else 4))
-    dw = torch.empty(co, 3, 3, ci, device=dy.device, dtype=dy.dtype)
+    dw = graddst.empty((co, 3, 3, ci), dy.dtype, dy.device)
     _wgrad_reduce(ws, s, dw)
     return dw.permute(0, 3, 1, 2)

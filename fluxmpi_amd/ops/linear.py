@@ -22,6 +22,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _ext
+from . import graddst
 from . import streams
 from .multi_tensor import DTYPE_CODE
 
@@ -66,7 +67,7 @@ def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype, spl
         C.gemm_wgrad256(dy2.data_ptr(), x2.data_ptr(), ws.data_ptr(), dy2.stride(0), x2.stride(0), n_out, n_in, K, s,
                         stream)
         odt = out_dtype if out_dtype in (torch.float32, torch.bfloat16) else torch.float32
-        dw = torch.empty(n_out, n_in, device=dy2.device, dtype=odt)
+        dw = graddst.empty((n_out, n_in), odt, dy2.device)
         C.gemm_splitk_reduce(ws.data_ptr(), s, dw.numel(), dw.data_ptr(), DTYPE_CODE[odt], stream)
         return dw.to(out_dtype)
     return conv1x1_wgrad_v2(dy2, x2, out_dtype=out_dtype, splits=splits or _SPLITS.get((n_out, n_in)))
@@ -84,7 +85,7 @@ def bias_grad(dy2: torch.Tensor, out_dtype: torch.dtype) -> torch.Tensor:
     stream = torch.cuda.current_stream(dy2.device).cuda_stream
     C.colsum(dy2.data_ptr(), part.data_ptr(), blocks, rows, n, DTYPE_CODE[dy2.dtype], stream)
     odt = out_dtype if out_dtype in (torch.float32, torch.bfloat16) else torch.float32
-    db = torch.empty(n, device=dy2.device, dtype=odt)
+    db = graddst.empty((n,), odt, dy2.device)
     C.gemm_splitk_reduce(part.data_ptr(), blocks, n, db.data_ptr(), DTYPE_CODE[odt], stream)
     return db.to(out_dtype)
 
@@ -112,8 +113,11 @@ class _LinearFn(torch.autograd.Function):
         need_b = ctx.has_bias and ctx.needs_input_grad[2]
 
         def grads():
-            gw = (weight_grad(dy2, x2, w.dtype) if native else dy2.t() @ x2) if need_w else None
-            gb = (bias_grad(dy2, ctx.bias_dtype) if native else dy2.sum(0).to(ctx.bias_dtype)) if need_b else None
+            # written straight into the DDP bucket slices when a communicating engine is attached
+            with graddst.into(w):
+                gw = (weight_grad(dy2, x2, w.dtype) if native else dy2.t() @ x2) if need_w else None
+            with graddst.into(ctx.bias):
+                gb = (bias_grad(dy2, ctx.bias_dtype) if native else dy2.sum(0).to(ctx.bias_dtype)) if need_b else None
             return gw, gb
 
         if need_w or need_b:

@@ -55,6 +55,7 @@ import torch
 from .. import optimisers as O
 from ..ops import multi_tensor as mt
 from ..ops import _ext
+from ..ops import graddst
 from ..ops import optim as fused
 from ..ops import streams
 from ..utils.config import get_config
@@ -187,6 +188,16 @@ class DDP:
         for b in self.buckets:
             for p in b.params:
                 self._param_bucket[id(p)] = b
+        # direct delivery ("steal" mode with collectives): the package's weight-gradient kernels
+        # allocate each parameter's gradient in its bucket slice (ops/graddst.py), so the
+        # per-bucket pack finds it in place (the pack was one copy kernel per bucket)
+        self.direct_grads = bool(cfg.direct_grads) and self.communicate and self.grad_mode == "steal"
+        for b in self.buckets:
+            for p, o in zip(b.params, b.offsets):
+                if self.direct_grads:
+                    graddst.attach(p, b.flat_grad, o)
+                else:
+                    graddst.detach(p)  # a previous engine's buckets are not this one's
         self._hooks = []
         self._sync_enabled = True
         if self.overlap and self.communicate:
@@ -211,6 +222,7 @@ class DDP:
         self._carry_live = False
         self._carry_hook = None
         self.collectives_launched = 0  # gradient-bucket allreduces issued so far
+        self.pack_copies = 0  # gradients the bucket packs had to copy (not delivered in place)
         _ENGINES[module] = self
         self.zero_grad()
         self.step_count = 0
@@ -435,6 +447,9 @@ class DDP:
             b.pending = len(b.params)
             b.ready = b.launched = b.packed = False
             b.work = None
+            if getattr(self, "direct_grads", False):
+                for p in b.params:
+                    graddst.rearm(p)
         self._next_launch = 0
 
     def _pack(self, b: _Bucket):
@@ -456,7 +471,8 @@ class DDP:
             elif g.data_ptr() == dptr:
                 if not _same_layout(g, dst):
                     dst.copy_(g.clone())
-                # else already in place (e.g. user set p.grad to the view)
+                    self.pack_copies += 1
+                # else already in place (delivered by the producing op, or p.grad set to the view)
             elif g.dtype is b.dtype and g.is_cuda and g.stride() == dst.stride():
                 # the common case: autograd's layout contract (the parameter's dense strides)
                 srcs.append(g)
@@ -468,6 +484,8 @@ class DDP:
                 ns.append(dst.numel())
             else:
                 dst.copy_(g)
+                self.pack_copies += 1
+        self.pack_copies += len(srcs)
         if srcs:
             C = _ext.get(required=True)
             code = mt.DTYPE_CODE[b.dtype]
@@ -763,7 +781,10 @@ class DDP:
                 "overlap": bool(self.overlap and self.communicate), "grad_mode": self.grad_mode,
                 "buckets": len(self.buckets),
                 "bucket_mb": [round(b.numel * b.flat_grad.element_size() / 2 ** 20, 2) for b in self.buckets],
-                "comm": (self.comm.name if self.communicate else "none")}
+                "comm": (self.comm.name if self.communicate else "none"),
+                "direct_grads": self.direct_grads,
+                # gradients the packs copied per step so far (0: every one delivered in place)
+                "pack_copies_per_step": round(self.pack_copies / max(1, self.step_count), 2)}
 
     def bucket_summary(self) -> list:
         return [{"index": b.index, "dtype": str(b.dtype), "numel": b.numel, "params": len(b.params),

@@ -33,6 +33,8 @@ Environment knobs (all optional):
 ``FLUXMPI_FORCE_COMM``     ``1``: issue the collectives even in a world of
                            one (hooks, packing, RCCL on the comm stream), to
                            exercise and time the N>1 path on a single GPU
+``FLUXMPI_DIRECT_GRADS``   ``1`` (default): the package's weight-gradient kernels
+                           write straight into the DDP buckets (``ops/graddst``)
 =========================  ==================================================
 """
 from __future__ import annotations
@@ -143,6 +145,7 @@ class Config:
     debug_checks: bool = False
     timeout_s: float = 600.0
     force_comm: bool = False
+    direct_grads: bool = True  # ops write parameter gradients into their DDP bucket slices
     # cross-rank structure check of functional reduction plans: always / first / never
     check_plans: str = "always"
     extra: dict = field(default_factory=dict)
@@ -168,6 +171,7 @@ class Config:
             debug_checks=_env_bool("FLUXMPI_DEBUG_CHECKS", False),
             timeout_s=_env_float("FLUXMPI_TIMEOUT_S", 600.0),
             force_comm=_env_bool("FLUXMPI_FORCE_COMM", bool(prefs.get("force_comm", False))),
+            direct_grads=_env_bool("FLUXMPI_DIRECT_GRADS", bool(prefs.get("direct_grads", True))),
             check_plans=os.environ.get("FLUXMPI_CHECK_PLANS", str(prefs.get("check_plans", "always"))).lower(),
             extra=prefs,
         )
