@@ -858,6 +858,9 @@ __global__ __launch_bounds__(1024) void attn_bwd_fused_kernel(AttnBwdArgs a) {
 // through global memory (each part computes it for all queries in LDS), one launch.
 // a.nblk parts per (b, h): part p owns query rows [16 p nw, ..) in phase 1 and the same key rows
 // in phase 2 (nw waves).
+// MEASURED NO GAIN (rd3p, ViT-B/16 bs256): 293.9 us per call vs 127.5 + 150.8 us for the pair,
+// 7.11k / 7.09k vs 7.11k / 7.11k img/s — the pair is not bound by the traffic this removes (both
+// kernels run at ~2 of 8 possible waves per SIMD, latency-bound). Opt-in: FLUXMPI_ATTN_BWD=two.
 __global__ __launch_bounds__(1024) void attn_bwd_two_kernel(AttnBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int TP = (a.T + 15) & ~15, TV = (a.T + 31) & ~31;

@@ -25,6 +25,7 @@
 
 #include "../api.h"
 #include "common.h"
+#include "bn_fin.h"
 
 namespace fluxmpi {
 namespace {
@@ -221,26 +222,11 @@ __global__ __launch_bounds__(kFinCh * kFinGroups) void bn_finalize_bwd2_kernel(f
 }
 
 // ---------------------------------------------------------------- in-kernel finalize
-// The finalize as the tail of the reduction kernel itself: every workgroup, after its shard
-// atomics, releases them (agent-scope fence) and counts itself in on the workspace's arrival
-// counter; the LAST one to arrive sums the kRedShards shards (all other contributions are
-// visible to it after its acquire), writes the per-channel results, re-zeroes the shards and the
-// counter. One launch (and one dependent launch gap) less per BatchNorm pass: a separate
-// finalize is a ~5 us kernel on the critical path, 98 of them per ResNet-50 step.
-struct Fin {
-  int mode;  // 0: none (a finalize kernel follows); 1: forward statistics; 2: backward reductions
-  int64_t rows;
-  float momentum, eps;
-  float* smean;  // mode 1 outputs
-  float* sinv;
-  float* rmean;
-  float* rvar;
-  int64_t* nbt;
-  float* dw;  // mode 2 outputs (dw = sum(dy_eff * xhat), db = sum(dy_eff)); dw2/db2/acc2: dual
-  float* db;
-  float* dw2;
-  float* db2;
-};
+// The finalize as the tail of the reduction kernel itself (bn_fin.h): the LAST workgroup to
+// arrive sums the kRedShards shards, writes the per-channel results, re-zeroes the shards and
+// the counter. One launch (and one dependent launch gap) less per BatchNorm pass.
+using bnfin::Fin;
+static_assert(bnfin::kShards == kShards && bnfin::kMaxC == kMaxC && bnfin::kCntOff == kCntOff, "bn_fin.h layout");
 
 // fp32 sums of 4 consecutive channels over the kRedShards shards (16-B loads), shards re-zeroed
 __device__ __forceinline__ void take4(float* __restrict__ acc, int C, int c, float4& s, float4& q) {
@@ -267,44 +253,19 @@ __device__ __forceinline__ void take4(float* __restrict__ acc, int C, int c, flo
   }
 }
 
-__device__ __forceinline__ void fin_fwd_channel(const Fin& f, int c, float s, float q) {
-  const float inv_n = 1.f / static_cast<float>(f.rows);
-  const float mean = s * inv_n;
-  float var = q * inv_n - mean * mean;
-  var = var > 0.f ? var : 0.f;
-  f.smean[c] = mean;
-  f.sinv[c] = rsqrtf(var + f.eps);
-  if (f.rmean != nullptr) {
-    const float unbiased = f.rows > 1 ? var * static_cast<float>(f.rows) / static_cast<float>(f.rows - 1) : var;
-    f.rmean[c] = (1.f - f.momentum) * f.rmean[c] + f.momentum * mean;
-    f.rvar[c] = (1.f - f.momentum) * f.rvar[c] + f.momentum * unbiased;
-  }
-}
-
 // Call from EVERY thread of the workgroup after its block_reduce_atomic(s). acc2: the second
 // workspace of the dual backward (its counter is unused: acc's counts both).
 __device__ __forceinline__ void finalize_last(const Fin& f, float* __restrict__ acc, float* __restrict__ acc2, int C) {
   if (f.mode == 0) return;
-  __shared__ unsigned s_last;
-  // This thread's shard atomics are complete (acknowledged) before the workgroup counts itself
-  // in. NOT __threadfence(): on gfx950 an agent-scope release is buffer_wbl2 (a write-back of the
-  // XCD's L2) — executed by every workgroup it made the reduction kernels ~50 us slower each
-  // (rd3o: 11.0k vs 12.5k img/s). The shard updates are atomics, so only their completion has to
-  // be ordered before the counter's; the "memory" clobber keeps the compiler from moving them.
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
   unsigned* cnt = reinterpret_cast<unsigned*>(acc + kCntOff);
-  if (threadIdx.x == 0) s_last = atomicAdd(cnt, 1u) == gridDim.x - 1 ? 1u : 0u;
-  __syncthreads();
-  if (s_last == 0u) return;
-  __threadfence();  // acquire, last workgroup only: no stale shard line left in this XCD's caches
+  if (!bnfin::arrive_last(cnt, gridDim.x)) return;
   for (int c = threadIdx.x * 4; c < C; c += kThreads * 4) {
     float4 s, q;
     take4(acc, C, c, s, q);
     const float sv[4] = {s.x, s.y, s.z, s.w}, qv[4] = {q.x, q.y, q.z, q.w};
     if (f.mode == 1) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fin_fwd_channel(f, c + j, sv[j], qv[j]);
+      for (int j = 0; j < 4; ++j) bnfin::fwd_channel(f, c + j, sv[j], qv[j]);
     } else {
       *reinterpret_cast<float4*>(f.db + c) = s;
       *reinterpret_cast<float4*>(f.dw + c) = q;
@@ -321,11 +282,15 @@ __device__ __forceinline__ void finalize_last(const Fin& f, float* __restrict__ 
   }
 }
 
-// FLUXMPI_BN_FIN=0: separate finalize kernels (the pre-round-3 path, for A/B)
+// FLUXMPI_BN_FIN=1: the in-kernel finalize. Off by default — MEASURED SLOWER (rd3p, same box:
+// 12.36k / 12.36k vs 12.43k / 12.44k img/s with the finalize kernels): the last workgroup's chain
+// (its atomics' completion, the returning counter atomic, the acquire, the shard loads) adds more
+// to the small reduction kernels' tails (bn_stats 8.2 -> 16.6 us, bn_bwd_reduce on 14x14 / 7x7
+// 22.1 -> 25.6 us) than the ~5 us finalize kernel it replaces.
 bool fin_in_kernel() {
   static const bool on = [] {
     const char* e = std::getenv("FLUXMPI_BN_FIN");
-    return e == nullptr || std::atoi(e) != 0;
+    return e != nullptr && std::atoi(e) != 0;
   }();
   return on;
 }
