@@ -129,7 +129,12 @@ void attn_fwd(const void* q, const void* k, const void* v, void* o, float* stats
               int64_t so_b, int64_t so_t, int64_t so_h, int B, int T, int H, int Dh, float scale, hipStream_t stream);
 void attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, void* dq, void* dk,
               void* dv, float* stats, int64_t sq_b, int64_t sq_t, int64_t so_b, int64_t so_t, int64_t so_h,
-              int64_t sg_b, int64_t sg_t, int B, int T, int H, int Dh, float scale, hipStream_t stream);
+              int64_t sg_b, int64_t sg_t, int B, int T, int H, int Dh, float scale, hipStream_t stream,
+              float* colpart = nullptr);
+// rows of attn_bwd's optional column-sum partials ([rows][3*H*64] fp32: per-wave sums of the dQ /
+// dK / dV rows it writes; their reduce is the packed QKV bias gradient), 0 if this call's variant
+// does not write them
+int attn_bwd_colpart_rows(int B, int T, int H, int64_t sq_t, int64_t sg_t);
 // dx[n,h,w,c] = sum of dy over the windows whose idx points at (h,w) (gather; dx fully written)
 void maxpool_bwd(const void* dy, const uint8_t* idx, void* dx, int64_t N, int64_t H, int64_t W, int64_t C, int K,
                  int S, int P, int dtype, hipStream_t stream);

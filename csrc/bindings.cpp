@@ -156,12 +156,17 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_bwd", [](uintptr_t q, uintptr_t k, uintptr_t v, uintptr_t o, uintptr_t dout, uintptr_t dq,
                        uintptr_t dk, uintptr_t dv, uintptr_t stats, int64_t sq_b, int64_t sq_t, int64_t so_b,
                        int64_t so_t, int64_t so_h, int64_t sg_b, int64_t sg_t, int B, int T, int H, int Dh,
-                       float scale, uintptr_t stream) {
+                       float scale, uintptr_t stream, uintptr_t colpart) {
     attn_bwd(reinterpret_cast<const void*>(q), reinterpret_cast<const void*>(k), reinterpret_cast<const void*>(v),
              reinterpret_cast<const void*>(o), reinterpret_cast<const void*>(dout), reinterpret_cast<void*>(dq),
              reinterpret_cast<void*>(dk), reinterpret_cast<void*>(dv), reinterpret_cast<float*>(stats), sq_b, sq_t,
-             so_b, so_t, so_h, sg_b, sg_t, B, T, H, Dh, scale, reinterpret_cast<hipStream_t>(stream));
-  });
+             so_b, so_t, so_h, sg_b, sg_t, B, T, H, Dh, scale, reinterpret_cast<hipStream_t>(stream),
+             reinterpret_cast<float*>(colpart));
+  }, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"), py::arg("dout"), py::arg("dq"), py::arg("dk"),
+     py::arg("dv"), py::arg("stats"), py::arg("sq_b"), py::arg("sq_t"), py::arg("so_b"), py::arg("so_t"),
+     py::arg("so_h"), py::arg("sg_b"), py::arg("sg_t"), py::arg("B"), py::arg("T"), py::arg("H"), py::arg("Dh"),
+     py::arg("scale"), py::arg("stream"), py::arg("colpart") = 0);
+  m.def("attn_bwd_colpart_rows", &attn_bwd_colpart_rows);
   m.def("pad_c3_to_c4", [](uintptr_t x, uintptr_t y, int64_t npix, int dtype, uintptr_t stream) {
     pad_c3_to_c4(reinterpret_cast<const void*>(x), reinterpret_cast<void*>(y), npix, dtype,
                  reinterpret_cast<hipStream_t>(stream));

@@ -71,6 +71,10 @@ struct AttnBwdArgs {
   int64_t sg_b, sg_t;        // dout strides (head stride DH)
   int B, T, H, nblk;
   float scale;
+  // resident backward pair (optional): per (b, part, wave) row, the column sums of the gradient
+  // rows the wave wrote ([rows][3][H][64] fp32, rows = B * nblk * waves): the packed QKV bias
+  // gradient is then one small reduce instead of a column-sum pass over dQKV (ops/linear.py)
+  float* colpart;
 };
 
 __device__ __forceinline__ bf16x8 ld8(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
@@ -444,6 +448,33 @@ __device__ __forceinline__ void res_coords(const AttnBwdArgs& a, int& b, int& h,
   b = bh / a.H;
 }
 
+// this wave's row of a.colpart, slot (0 q, 1 k, 2 v) and head h
+__device__ __forceinline__ float* colpart_row(const AttnBwdArgs& a, int b, int h, int part, int w, int slot) {
+  const int nw = blockDim.x >> 6;
+  return a.colpart + (static_cast<int64_t>(b * a.nblk + part) * nw + w) * (3 * a.H * DH) + slot * a.H * DH + h * DH;
+}
+
+// sums over the wave's 16 rows (lane & 15) of acc[dt][r] = gradient[row][16 dt + 4 (lane >> 4) + r],
+// rows with ok == false excluded; one float4 store per (dt, lane group)
+__device__ __forceinline__ void colpart_store(float* row, const f32x4 (&acc)[4], float scale, bool ok) {
+  const int lane = threadIdx.x & 63, g = lane >> 4;
+  const float keep = ok ? scale : 0.f;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    float4 v;
+    v.x = row_sum16(acc[dt][0] * keep);
+    v.y = row_sum16(acc[dt][1] * keep);
+    v.z = row_sum16(acc[dt][2] * keep);
+    v.w = row_sum16(acc[dt][3] * keep);
+    if ((lane & 15) == 0) *reinterpret_cast<float4*>(row + 16 * dt + 4 * g) = v;
+  }
+}
+
+__device__ __forceinline__ void colpart_zero(float* row) {
+  const int lane = threadIdx.x & 63;
+  row[lane] = 0.f;
+}
+
 __global__ __launch_bounds__(1024) void attn_fwd_res_kernel(AttnBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int TP = (a.T + 15) & ~15, TV = (a.T + 31) & ~31;
@@ -572,7 +603,10 @@ __global__ __launch_bounds__(1024) void attn_bwd_dq_res_kernel(AttnBwdArgs a) {
   }
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-  if (q0 >= a.T) return;  // wave-uniform
+  if (q0 >= a.T) {  // wave-uniform
+    if (a.colpart != nullptr) colpart_zero(colpart_row(a, b, h, part, w, 0));
+    return;
+  }
   float dsum = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) dsum += (float)gf[0][j] * (float)o0[j] + (float)gf[1][j] * (float)o1[j];
@@ -620,6 +654,7 @@ __global__ __launch_bounds__(1024) void attn_bwd_dq_res_kernel(AttnBwdArgs a) {
       *reinterpret_cast<bf16x4*>(a.dq + qoff + dt * 16 + 4 * g) = o;
     }
   }
+  if (a.colpart != nullptr) colpart_store(colpart_row(a, b, h, part, w, 0), acc, a.scale, qok);
 }
 
 __global__ __launch_bounds__(1024) void attn_bwd_dkv_res_kernel(AttnBwdArgs a) {
@@ -652,7 +687,13 @@ __global__ __launch_bounds__(1024) void attn_bwd_dkv_res_kernel(AttnBwdArgs a) {
   }
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-  if (k0 >= a.T) return;  // wave-uniform
+  if (k0 >= a.T) {  // wave-uniform
+    if (a.colpart != nullptr) {
+      colpart_zero(colpart_row(a, b, h, part, w, 1));
+      colpart_zero(colpart_row(a, b, h, part, w, 2));
+    }
+    return;
+  }
   const float c2 = a.scale * kLog2e;
   f32x4 accK[4] = {}, accV[4] = {};
 #pragma unroll 2
@@ -690,6 +731,10 @@ __global__ __launch_bounds__(1024) void attn_bwd_dkv_res_kernel(AttnBwdArgs a) {
       *reinterpret_cast<bf16x4*>(a.dv + koff + dt * 16 + 4 * g) = v;
       *reinterpret_cast<bf16x4*>(a.dk + koff + dt * 16 + 4 * g) = k;
     }
+  }
+  if (a.colpart != nullptr) {
+    colpart_store(colpart_row(a, b, h, part, w, 1), accK, a.scale, kok);
+    colpart_store(colpart_row(a, b, h, part, w, 2), accV, 1.f, kok);
   }
 }
 
@@ -1045,9 +1090,31 @@ int res_parts(int tiles) {
 
 }  // namespace
 
+namespace {
+int bwd_env_mode() {
+  static const int m = [] {
+    const char* e = std::getenv("FLUXMPI_ATTN_BWD");
+    const std::string v = e != nullptr ? std::string(e) : std::string();
+    return v == "fused" ? 1 : (v == "two" ? 2 : (v == "blocked" ? 3 : 0));
+  }();
+  return m;
+}
+int bwd_mode() { return g_attn_bwd_fused < 0 ? bwd_env_mode() : g_attn_bwd_fused; }
+}  // namespace
+
+int attn_bwd_colpart_rows(int B, int T, int H, int64_t sq_t, int64_t sg_t) {
+  // the resident dq / dkv pair writes the column-sum partials; every other variant does not
+  if (bwd_mode() != 0 || T > kResMaxT || T <= 0 || (sq_t % 8) != 0 || (sg_t % 8) != 0) return 0;
+  const int tiles = (T + 15) / 16;
+  const int nblk = res_parts(tiles);
+  const int waves = (tiles + nblk - 1) / nblk;
+  (void)H;
+  return B * nblk * waves;
+}
+
 void attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, void* dq, void* dk,
               void* dv, float* stats, int64_t sq_b, int64_t sq_t, int64_t so_b, int64_t so_t, int64_t so_h,
-              int64_t sg_b, int64_t sg_t, int B, int T, int H, int Dh, float scale, hipStream_t s) {
+              int64_t sg_b, int64_t sg_t, int B, int T, int H, int Dh, float scale, hipStream_t s, float* colpart) {
   if (Dh != DH) throw std::runtime_error("attn_bwd: head dim must be 64");
   if (B <= 0 || T <= 0 || H <= 0) throw std::runtime_error("attn_bwd: empty problem");
   for (const void* p : {q, k, v, o, dout, static_cast<const void*>(dq), static_cast<const void*>(dk),
@@ -1059,16 +1126,8 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* o, const 
                 static_cast<const bf16*>(o), static_cast<const bf16*>(dout), nullptr, static_cast<bf16*>(dq),
                 static_cast<bf16*>(dk), static_cast<bf16*>(dv), stats, sq_b, sq_t, so_b, so_t, so_h, sg_b, sg_t,
                 B, T, H, (T + 63) / 64, scale};
-  static const bool resident = [] {
-    const char* e = std::getenv("FLUXMPI_ATTN_BWD");
-    return e == nullptr || std::string(e) != "blocked";
-  }();
-  static const int env_mode = [] {
-    const char* e = std::getenv("FLUXMPI_ATTN_BWD");
-    const std::string v = e != nullptr ? std::string(e) : std::string();
-    return v == "fused" ? 1 : (v == "two" ? 2 : 0);
-  }();
-  const int mode = g_attn_bwd_fused < 0 ? env_mode : g_attn_bwd_fused;
+  const int mode = bwd_mode();
+  const bool resident = mode != 3;
   if (mode == 1 && T <= kResMaxT && (sq_t % 8) == 0 && (sg_t % 8) == 0 && fused_bwd_lds(T) <= 160 * 1024) {
     const int waves = (T + 15) / 16;
     const int64_t bh = static_cast<int64_t>(B) * H;
@@ -1102,6 +1161,7 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* o, const 
     if (bh > 0x7fffffff) throw std::runtime_error("attn_bwd: grid too large");
     const int waves = (tiles + a.nblk - 1) / a.nblk;
     const int TP = (T + 15) & ~15, TV = (T + 31) & ~31;
+    a.colpart = colpart;  // [B * nblk * waves][3 * H * 64] (attn_bwd_colpart_rows), or nullptr
     attn_bwd_dq_res_kernel<<<static_cast<unsigned>(bh), waves * 64, static_cast<size_t>(TV + TP) * 128, s>>>(a);
     FLUXMPI_HIP_CHECK(hipGetLastError());
     attn_bwd_dkv_res_kernel<<<static_cast<unsigned>(bh), waves * 64, static_cast<size_t>(2 * TV) * 128 + 2 * TV * 4,

@@ -10,6 +10,9 @@ straight into one ``[B, T, 3, H, 64]`` buffer (no per-gradient tensors, no inter
 """
 from __future__ import annotations
 
+import os
+import weakref
+
 import torch
 
 from . import _ext
@@ -40,8 +43,13 @@ def attn_fwd_packed(qkv: torch.Tensor, heads: int):
     return out, stats
 
 
+# FLUXMPI_ATTN_COLSUM=0: no column-sum partials from the backward (the bias gradient of the packed
+# projection then runs its own column-sum pass over dQKV; A/B runs)
+COLSUM = os.environ.get("FLUXMPI_ATTN_COLSUM", "1") != "0"
+
+
 def attn_bwd_packed(qkv: torch.Tensor, out: torch.Tensor, dy: torch.Tensor, heads: int,
-                    stats: torch.Tensor) -> torch.Tensor:
+                    stats: torch.Tensor, colsum: bool | None = None) -> torch.Tensor:
     C = _ext.get(required=True)
     _check(qkv, heads)
     b, t, d3 = qkv.shape
@@ -57,9 +65,34 @@ def attn_bwd_packed(qkv: torch.Tensor, out: torch.Tensor, dy: torch.Tensor, head
         dy = dy.to(qkv.dtype)
     dqkv = torch.empty_like(qkv)
     p, g, es = qkv.data_ptr(), dqkv.data_ptr(), qkv.element_size()
+    # column-sum partials of dQKV from the kernels themselves: the packed projection's bias
+    # gradient becomes a reduce over them (ops/linear.bias_grad takes them by data pointer)
+    rows = C.attn_bwd_colpart_rows(b, t, heads, d3, d) if (COLSUM if colsum is None else colsum) else 0
+    part = torch.empty(rows, d3, device=qkv.device, dtype=torch.float32) if rows > 0 else None
     C.attn_bwd(p, p + d * es, p + 2 * d * es, out.data_ptr(), dy.data_ptr(), g, g + d * es, g + 2 * d * es,
-               stats.data_ptr(), t * d3, d3, t * d, d, 64, t * d, d, b, t, heads, 64, 0.125, _stream(qkv))
+               stats.data_ptr(), t * d3, d3, t * d, d, 64, t * d, d, b, t, heads, 64, 0.125, _stream(qkv),
+               part.data_ptr() if part is not None else 0)
+    _COLPART[0] = (weakref.ref(dqkv), part) if part is not None else None
     return dqkv
 
 
-__all__ = ["attn_fwd_packed", "attn_bwd_packed", "supported"]
+# the latest backward's (weak reference to dQKV, column-sum partials): the next consumer of that gradient
+# (the packed projection's Linear backward, the very next autograd node) takes it
+_COLPART: list = [None]
+
+
+def take_colpart(grad: torch.Tensor):
+    """The [rows, N] fp32 column-sum partials of ``grad`` if it is the last attention backward's
+    dQKV (then ``grad.sum(0) == partials.sum(0)`` up to rounding), else None; consumed once."""
+    hit = _COLPART[0]
+    if hit is None:
+        return None
+    src = hit[0]()  # the dQKV tensor itself, still alive (no reuse of a freed address)
+    if src is None or src.data_ptr() != grad.data_ptr() or src.numel() != grad.numel() \
+            or hit[1].shape[1] != grad.shape[-1]:
+        return None
+    _COLPART[0] = None
+    return hit[1]
+
+
+__all__ = ["attn_fwd_packed", "attn_bwd_packed", "supported", "take_colpart"]

@@ -80,10 +80,15 @@ def bias_grad(dy2: torch.Tensor, out_dtype: torch.dtype) -> torch.Tensor:
         return dy2.float().sum(0).to(out_dtype)
     C = _ext.get(required=True)
     rows, n = dy2.shape
-    blocks = C.colsum_blocks(rows)
-    part = torch.empty(blocks, n, device=dy2.device, dtype=torch.float32)
     stream = torch.cuda.current_stream(dy2.device).cuda_stream
-    C.colsum(dy2.data_ptr(), part.data_ptr(), blocks, rows, n, DTYPE_CODE[dy2.dtype], stream)
+    from .attention import take_colpart
+    part = take_colpart(dy2)  # dQKV of the packed attention: its kernels left the partial sums
+    if part is not None:
+        blocks = part.shape[0]
+    else:
+        blocks = C.colsum_blocks(rows)
+        part = torch.empty(blocks, n, device=dy2.device, dtype=torch.float32)
+        C.colsum(dy2.data_ptr(), part.data_ptr(), blocks, rows, n, DTYPE_CODE[dy2.dtype], stream)
     odt = out_dtype if out_dtype in (torch.float32, torch.bfloat16) else torch.float32
     db = graddst.empty((n,), odt, dy2.device)
     C.gemm_splitk_reduce(part.data_ptr(), blocks, n, db.data_ptr(), DTYPE_CODE[odt], stream)

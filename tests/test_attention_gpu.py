@@ -80,3 +80,23 @@ def test_packed_attention_native_vs_aten(gpu_ext, monkeypatch):
         res[mode] = (y.detach(), xa.grad)
     assert _rel(res["native"][0], res["aten"][0]) < 1e-2
     assert _rel(res["native"][1], res["aten"][1]) < 2e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("b,t,heads", [(3, 197, 4), (2, 50, 2), (2, 7, 1), (1, 256, 2)])
+def test_attn_bwd_colsum_partials(gpu_ext, b, t, heads):
+    """The resident backward pair's per-wave column sums of dQ / dK / dV (the packed QKV bias
+    gradient) vs the column sums of the dQKV it wrote; the hand-off is taken once."""
+    from fluxmpi_amd.ops.attention import attn_bwd_packed, attn_fwd_packed, take_colpart
+    torch.manual_seed(3)
+    xb = (torch.randn(b, t, 3 * heads * 64, device="cuda") * 1.5).to(torch.bfloat16)
+    out, stats = attn_fwd_packed(xb, heads)
+    g = torch.randn(b, t, heads * 64, device="cuda").to(torch.bfloat16)
+    dqkv = attn_bwd_packed(xb, out, g, heads, stats)
+    part = take_colpart(dqkv.view(b * t, -1))
+    assert part is not None and part.shape[1] == 3 * heads * 64
+    assert take_colpart(dqkv.view(b * t, -1)) is None  # consumed
+    ref = dqkv.float().sum((0, 1))
+    got = part.sum(0)
+    # the partials sum the fp32 values before their bf16 rounding
+    torch.testing.assert_close(got, ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item() / 10 + 1e-3)
