@@ -50,3 +50,18 @@ def test_launch_propagates_failure(tmp_path):
     p.write_text("import os, sys\nsys.exit(3 if os.environ['RANK'] == '1' else 0)\n")
     r = subprocess.run([sys.executable, "-m", "fluxmpi_amd.launch", "-n", "2", str(p)], env=_env(), timeout=120)
     assert r.returncode == 3
+
+
+def test_bench_collectives_cpu():
+    """scripts/bench_collectives.py (the nccl-tests analogue) on 2 CPU ranks: one JSON line per
+    (collective, size) with bus bandwidth = algorithm bandwidth x the ring factor."""
+    import json
+    r = subprocess.run([sys.executable, "-m", "fluxmpi_amd.launch", "-n", "2",
+                        os.path.join(ROOT, "scripts", "bench_collectives.py"), "--device", "cpu", "--sizes", "4K,64K",
+                        "--iters", "2", "--warmup", "1"], env=_env(), capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert {ln["op"] for ln in lines} == {"allreduce", "allgather", "reduce_scatter", "broadcast", "alltoall"}
+    assert len(lines) == 10 and all(ln["world"] == 2 and ln["us"] > 0 for ln in lines)
+    ar = [ln for ln in lines if ln["op"] == "allreduce"][0]
+    assert abs(ar["busbw_GBps"] - ar["algbw_GBps"]) < 1e-2  # 2(N-1)/N == 1 at N=2
