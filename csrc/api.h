@@ -124,6 +124,7 @@ void stem_bwd(const void* x, const void* c, const void* dp, const uint8_t* idx, 
 // strides (sq_b, sq_t; head stride 64), o has (so_b, so_t, so_h), dout (sg_b, sg_t; head stride
 // 64); stats is fp32 [B][H][T][2]: attn_fwd writes [..][0] = base-2 log-sum-exp of the scaled
 // scores, attn_bwd reads it and writes [..][1] = rowsum(dO*O).
+void attn_set_fwd_mode(int mode);   // -1 env, 0 two workgroups per head, 1 persistent (next head staged)
 void attn_set_bwd_fused(int mode);  // -1 env, 0 dq/dkv pair, 1 one-kernel (LDS atomics), 2 two-phase
 void attn_fwd(const void* q, const void* k, const void* v, void* o, float* stats, int64_t sq_b, int64_t sq_t,
               int64_t so_b, int64_t so_t, int64_t so_h, int B, int T, int H, int Dh, float scale, hipStream_t stream);

@@ -153,6 +153,7 @@ PYBIND11_MODULE(_C, m) {
              scale, reinterpret_cast<hipStream_t>(stream));
   });
   m.def("attn_set_bwd_fused", &attn_set_bwd_fused);
+  m.def("attn_set_fwd_mode", &attn_set_fwd_mode);
   m.def("attn_bwd", [](uintptr_t q, uintptr_t k, uintptr_t v, uintptr_t o, uintptr_t dout, uintptr_t dq,
                        uintptr_t dk, uintptr_t dv, uintptr_t stats, int64_t sq_b, int64_t sq_t, int64_t so_b,
                        int64_t so_t, int64_t so_h, int64_t sg_b, int64_t sg_t, int B, int T, int H, int Dh,

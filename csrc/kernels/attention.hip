@@ -565,6 +565,189 @@ __global__ __launch_bounds__(1024) void attn_fwd_res_kernel(AttnBwdArgs a) {
   }
 }
 
+// MEASURED NO GAIN (rd3s, ViT-B/16 bs256, same box): 110.3 us per call vs 107.4 us for
+// attn_fwd_res_kernel, 6.96k / 6.96k img/s either way — the forward is not bound by its staging
+// (~9 us of CU time per head against ~1 us of MFMA and ~3 us of HBM traffic: the per-wave
+// LDS-read -> MFMA -> softmax chain at 3-4 waves per SIMD). Opt-in: FLUXMPI_ATTN_FWD=persist.
+// Persistent forward with the next head's staging in flight. attn_fwd_res_kernel's workgroup
+// stages its head, waits, computes, exits: with two workgroups per CU the staging of one only
+// partly hides behind the other's compute (the kernel ran at ~3 of its 104 KB per head per
+// 8.6 us per CU, latency-bound). Here one workgroup per CU (13 waves, the whole head) loops over
+// heads with two LDS image pairs: the LDS-DMA of head i+1's K and V is issued before head i is
+// computed, so HBM streams while the MFMAs run. Every thread issues exactly `per` DMA pieces per
+// head (duplicates of the last piece pad the count), so one counted vmcnt wait leaves exactly
+// the next head's pieces in flight; the LDS reads go through __restrict__ pointers (alias
+// scopes: the waitcnt pass would otherwise drain the prefetch before them).
+template <int PER>
+__device__ __forceinline__ void wait_pieces() {
+  __builtin_amdgcn_s_waitcnt((PER & 15) | ((PER >> 4) << 14) | (7 << 4) | (15 << 8));  // vmcnt(PER)
+}
+
+// The PER staging pieces of this thread, fixed for every head: the element offset of its 16-B
+// chunk inside a head's K or V ([T][64] rows at stride sq_t; -1: a padding row, read from the
+// zero line) and, wave-uniform, the piece index (LDS slot pc * 1024, V when pc >= TP / 8).
+// Computed once: recomputing them per head (or hoisting 64-bit addresses) spilled registers.
+template <int PER>
+struct KvPieces {
+  int32_t off[PER];
+  int pc[PER];
+};
+
+template <int PER>
+__device__ __forceinline__ KvPieces<PER> kv_pieces(const AttnBwdArgs& a, int TP, int TV) {
+  KvPieces<PER> p;
+  // wave-uniform in scalar registers (the piece index only selects the LDS slot and K / V)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  const int kp = TP / 8, np = kp + TV / 8;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    int pc = wave + j * nw;
+    pc = pc < np ? pc : np - 1;  // padding: the last piece again (same bytes, same place)
+    const int row = 8 * (pc >= kp ? pc - kp : pc) + (lane >> 3);
+    const int chunk = (lane & 7) ^ swz_b(row);
+    p.pc[j] = __builtin_amdgcn_readfirstlane(pc);
+    p.off[j] = row < a.T ? static_cast<int32_t>(row * a.sq_t + chunk * 8) : -1;
+  }
+  return p;
+}
+
+// K (TP rows) then V (TV rows) of one head into an image pair: PER pieces per thread (a
+// compile-time count: the waitcnt pass then knows exactly how many are younger than a load)
+template <int PER>
+__device__ __forceinline__ void stage_kv(char* __restrict__ img, const KvPieces<PER>& p, const bf16* kb,
+                                         const bf16* vb, int kp) {
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const bf16* base = p.pc[j] >= kp ? vb : kb;
+    const void* src = p.off[j] >= 0 ? static_cast<const void*>(base + p.off[j])
+                                    : static_cast<const void*>(g_attn_zero);
+    typedef __attribute__((address_space(3))) char lds_char;
+    typedef __attribute__((address_space(1))) void gl_void;
+    __builtin_amdgcn_global_load_lds((gl_void*)(src), (lds_char*)(img + p.pc[j] * 1024), 16, 0, 0);
+  }
+}
+
+template <int PER>
+__global__ __launch_bounds__(1024) void attn_fwd_pers_kernel(AttnBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int TP = (a.T + 15) & ~15, TV = (a.T + 31) & ~31;
+  const int pair = (TP + TV) * 128;
+  const int total = a.B * a.H;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, col = lane & 15, g = lane >> 4;
+  const int q0 = 16 * w, qi = q0 + col;
+  const bool qok = qi < a.T;
+  const int qrow = qok ? qi : 0;  // loads stay unconditional (a valid row), zeroed below
+  const float c2 = a.scale * kLog2e;
+  const int nt = TP / 16;
+  auto row_frag = [&](const char* __restrict__ img, int row, int ch) {
+    return *reinterpret_cast<const bf16x8*>(img + row * 128 + ((ch ^ swz_b(row)) << 4));
+  };
+  auto tr_frag = [&](const char* __restrict__ img, int r0, int c0) {
+    const int q = (lane >> 2) & 3, p = lane & 3;
+    const int ra = r0 + 4 * g + q, rb = ra + 16;
+    const int ch = (c0 >> 3) + (p >> 1);
+    typedef short short4v __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) short4v lds_short4v;
+    short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_short4v*)(img + ra * 128 + ((ch ^ swz_b(ra)) << 4) + (p & 1) * 8));
+    short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_short4v*)(img + rb * 128 + ((ch ^ swz_b(rb)) << 4) + (p & 1) * 8));
+    bf16x8 out;
+    __builtin_memcpy(&out, &lo, 8);
+    __builtin_memcpy(reinterpret_cast<char*>(&out) + 8, &hi, 8);
+    return out;
+  };
+  const KvPieces<PER> pcs = kv_pieces<PER>(a, TP, TV);
+  const int kp = TP / 8;
+  auto kbase = [&](int head) { return a.k + (head / a.H) * a.sq_b + (head % a.H) * DH; };
+  auto vbase = [&](int head) { return a.v + (head / a.H) * a.sq_b + (head % a.H) * DH; };
+  int cur = blockIdx.x;
+  stage_kv<PER>(smem, pcs, kbase(cur), vbase(cur), kp);
+  for (int it = 0; cur < total; ++it, cur += gridDim.x) {  // grid <= total: every workgroup has a head
+    const int b = cur / a.H, h = cur % a.H;
+    const char* kimg = smem + (it & 1) * pair;
+    const char* vimg = kimg + TP * 128;
+    const int64_t qoff = b * a.sq_b + static_cast<int64_t>(qrow) * a.sq_t + h * DH;
+    bf16x8 qf[2];
+    qf[0] = ld8(a.q + qoff + 8 * g);
+    qf[1] = ld8(a.q + qoff + 32 + 8 * g);
+    // every wave is done with the other image pair (the previous head): refill it
+    __builtin_amdgcn_s_barrier();
+    // unconditional (past the last head: a dummy refill of the idle pair, never read), so every
+    // path has the same PER younger loads and the waitcnt pass keeps this wait counted
+    const int nxt = cur + gridDim.x < total ? cur + gridDim.x : cur;
+    stage_kv<PER>(smem + ((it + 1) & 1) * pair, pcs, kbase(nxt), vbase(nxt), kp);
+    wait_pieces<PER>();  // all but the next head's pieces: this head's images, Q
+    __builtin_amdgcn_s_barrier();  // every thread's pieces of this head have landed
+    // (a padded query lane computes on row 0's Q: its column of S, P and O is never stored)
+    if (q0 < a.T) {  // wave-uniform
+      f32x4 x[kResMaxT / 16];
+      float m = -kInf;
+#pragma unroll
+      for (int kt = 0; kt < kResMaxT / 16; ++kt) {
+        x[kt] = f32x4{-kInf, -kInf, -kInf, -kInf};
+        if (kt < nt) {
+          const int row = 16 * kt + col;
+          f32x4 sacc = {};
+          sacc = mfma(row_frag(kimg, row, g), qf[0], sacc);
+          sacc = mfma(row_frag(kimg, row, 4 + g), qf[1], sacc);
+          if (16 * kt + 16 <= a.T) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              x[kt][r] = sacc[r] * c2;
+              m = fmaxf(m, x[kt][r]);
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int key = 16 * kt + 4 * g + r;
+              x[kt][r] = key < a.T ? sacc[r] * c2 : -kInf;
+              m = fmaxf(m, x[kt][r]);
+            }
+          }
+        }
+      }
+      m = xor_max<32>(xor_max<16>(m));
+      float l = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < kResMaxT / 16; ++kt) {
+        if (kt < nt) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float pv = fast_exp2(x[kt][r] - m);
+            x[kt][r] = pv;
+            l += pv;
+          }
+        } else {
+          x[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+      l = butterfly_from<16>(l);
+      f32x4 acc[4] = {};
+#pragma unroll
+      for (int ks = 0; ks < kResMaxT / 32; ++ks) {
+        if (32 * ks < TV) {
+          const bf16x8 bop = pack(x[2 * ks], x[2 * ks + 1]);
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma(tr_frag(vimg, 32 * ks, 16 * dt), bop, acc[dt]);
+        }
+      }
+      if (qok) {
+        const float inv = 1.f / l;
+        bf16* op = a.o_out + b * a.so_b + static_cast<int64_t>(qi) * a.so_t + h * a.so_h;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const bf16x4 o = {(bf16)(acc[dt][0] * inv), (bf16)(acc[dt][1] * inv), (bf16)(acc[dt][2] * inv),
+                            (bf16)(acc[dt][3] * inv)};
+          *reinterpret_cast<bf16x4*>(op + dt * 16 + 4 * g) = o;
+        }
+        if (g == 0) a.stats[((static_cast<int64_t>(b) * a.H + h) * a.T + qi) * 2] = m + __log2f(l);
+      }
+    }
+  }
+  wait_pieces<0>();  // the last (dummy) refill has landed before the workgroup's LDS is released
+}
+
 // Backward with the head resident (T <= 256), two kernels like the blocked pair above:
 //   attn_bwd_dq_res   K, V images; one wave per 16 queries: D = rowsum(dO * O) (written to
 //                     stats[.., 1] for the next kernel), S^T = K Q^T, dP^T = V dO^T,
@@ -1066,7 +1249,20 @@ __global__ __launch_bounds__(1024) void attn_bwd_two_kernel(AttnBwdArgs a) {
   }
 }
 
+void attn_fwd_pers_kernel_attr(const void* k) {
+  static const void* done[4] = {};
+  for (const void*& d : done) {
+    if (d == k) return;
+    if (d == nullptr) {
+      FLUXMPI_HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      d = k;
+      return;
+    }
+  }
+}
+
 int g_attn_bwd_fused = -1;  // backward variant (attn_set_bwd_fused); -1: FLUXMPI_ATTN_BWD decides
+int g_attn_fwd_mode = -1;   // forward variant (attn_set_fwd_mode); -1: FLUXMPI_ATTN_FWD decides
 
 size_t fused_bwd_lds(int T) {
   const size_t TV = static_cast<size_t>((T + 31) & ~31);
@@ -1179,6 +1375,10 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* o, const 
 
 // backward variant for A/B runs and tests: -1 FLUXMPI_ATTN_BWD decides, 0 the dq / dkv pair,
 // 1 the one-kernel LDS-atomic backward, 2 the two-phase kernel
+// forward variant for A/B runs and tests: -1 FLUXMPI_ATTN_FWD decides, 0 two workgroups per head
+// (attn_fwd_res_kernel), 1 the persistent double-buffered kernel (attn_fwd_pers_kernel)
+void attn_set_fwd_mode(int mode) { g_attn_fwd_mode = mode < -1 || mode > 1 ? -1 : mode; }
+
 void attn_set_bwd_fused(int mode) { g_attn_bwd_fused = mode < -1 || mode > 2 ? -1 : mode; }
 
 void attn_fwd(const void* q, const void* k, const void* v, void* o, float* stats, int64_t sq_b, int64_t sq_t,
@@ -1209,6 +1409,29 @@ void attn_fwd(const void* q, const void* k, const void* v, void* o, float* stats
     const char* e = std::getenv("FLUXMPI_ATTN_FWD");
     return e == nullptr || std::string(e) != "blocked";
   }();
+  static const bool persist_env = [] {
+    const char* e = std::getenv("FLUXMPI_ATTN_FWD");
+    return e != nullptr && std::string(e) == "persist";
+  }();
+  const bool persist = g_attn_fwd_mode < 0 ? persist_env : g_attn_fwd_mode == 1;
+  if (persist && T <= kResMaxT && (sq_t % 8) == 0 && (static_cast<int64_t>(T) * sq_t) < (1LL << 31)) {
+    // one workgroup per CU looping over heads, the next head's K / V staged during this one's math
+    a.nblk = 1;
+    const int TP = (T + 15) & ~15, TV = (T + 31) & ~31;
+    const size_t lds = static_cast<size_t>(2 * (TP + TV)) * 128;
+    int cus = 256, dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int64_t heads = static_cast<int64_t>(B) * H;
+    const int grid = static_cast<int>(heads < cus ? heads : cus);
+    const int nw = (T + 15) / 16, per = ((TP + TV) / 8 + nw - 1) / nw;  // 4..6 for T <= 256
+    auto k = per <= 4 ? attn_fwd_pers_kernel<4> : (per == 5 ? attn_fwd_pers_kernel<5> : attn_fwd_pers_kernel<6>);
+    if (per > 6) throw std::runtime_error("attn_fwd: persistent staging count out of range");
+    attn_fwd_pers_kernel_attr(reinterpret_cast<const void*>(k));
+    k<<<grid, nw * 64, lds, s>>>(a);
+    FLUXMPI_HIP_CHECK(hipGetLastError());
+    return;
+  }
   if (resident && T <= kResMaxT && (sq_t % 8) == 0) {
     // whole head resident in LDS: res_parts() workgroups per (b, h), one wave per 16 queries
     const int tiles = (T + 15) / 16;
