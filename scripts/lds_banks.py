@@ -27,7 +27,43 @@ def frag_cycles(bk, swz):
     return worst
 
 
+def _cycles_b64(addr):
+    """ds_read_b64 / ds_read_b64_tr_b16: two 32-lane groups, 2 cycles when conflict-free."""
+    tot = 0
+    for grp in (range(0, 32), range(32, 64)):
+        banks: dict = {}
+        for lane in grp:
+            for d in range(2):
+                banks.setdefault((addr[lane] // 4 + d) % 64, set()).add(addr[lane] // 8)
+        tot += max(len(v) for v in banks.values())
+    return tot
+
+
+def attention_swizzles(swz):
+    """Worst cycles of attention.hip's two reads of a swizzled 128-B-row [T][64] image:
+    the row read (img_row: rows 16 kt + (l & 15), chunk (l >> 4) [+ 4]; ds_read_b128, 4 when
+    conflict-free) and the transposed read (img_tr: rows r0 + 4 (l >> 4) + ((l >> 2) & 3) [+ 16],
+    32-B column pair; ds_read_b64_tr_b16, 2 when conflict-free)."""
+    row = tr = 0
+    for kt in range(16):
+        for half in (0, 4):
+            addr = [(16 * kt + (ln & 15)) * 128 + (((ln >> 4) + half) ^ swz(16 * kt + (ln & 15))) * 16 for ln in range(64)]
+            row = max(row, cycles(addr))
+    for r0 in range(0, 256, 32):
+        for c0 in range(0, 64, 16):
+            for off in (0, 16):
+                addr = []
+                for ln in range(64):
+                    ra = r0 + 4 * (ln >> 4) + ((ln >> 2) & 3) + off
+                    ch = (c0 >> 3) + ((ln & 3) >> 1)
+                    addr.append(ra * 128 + ((ch ^ swz(ra)) << 4) + (ln & 1) * 8)
+                tr = max(tr, _cycles_b64(addr))
+    return row, tr
+
+
 if __name__ == "__main__":
+    print("attention old swz (row, tr):", attention_swizzles(lambda r: (((r >> 1) & 3) << 1) | ((r >> 3) & 1)))
+    print("attention r & 6  (row, tr):", attention_swizzles(lambda r: r & 6))
     print("BK=32 (r>>2)&3      :", frag_cycles(32, lambda r: (r >> 2) & 3))
     print("BK=32 (-(r>>2))&3   :", frag_cycles(32, lambda r: (-(r >> 2)) & 3))
     print("BK=64 (r>>1)&7      :", frag_cycles(64, lambda r: (r >> 1) & 7))
