@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -228,7 +229,7 @@ def main():
                        "kernel_choices": ("shipped" if use_choices else "measured")
                        + ("+rank0-calibrated" if calibrated else ""),
                        "host_ms_per_step": round(1000 * t_host / args.steps, 3),
-                       "loss": round(lval, 4),
+                       "loss": round(lval, 4), "loss_finite": math.isfinite(lval),
                        # what the data-parallel layer actually did: at N=1 nothing is communicated
                        # (overlap false, comm "none") unless --force-comm
                        **cs, "exposed_comm_ms": None if exposed is None else round(exposed, 3),
@@ -240,6 +241,11 @@ def main():
         }
         print(json.dumps(rec), flush=True)
     FluxMPI.Finalize()
+    if not math.isfinite(lval):
+        # a non-finite loss means a kernel produced garbage: NaN/Inf data also changes the timing
+        # (lower power draw, higher clocks), so the number above is not a valid measurement
+        print(f"bench.py: non-finite loss {lval} - the measurement is invalid", file=sys.stderr, flush=True)
+        return 1
     return 0
 
 

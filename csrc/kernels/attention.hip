@@ -479,6 +479,9 @@ __device__ __forceinline__ void colpart_zero(float* row) {
   row[lane] = 0.f;
 }
 
+// NT > 0: the head's key-tile count (TP / 16) at compile time — loops without runtime guards are
+// straight-line code the scheduler can pipeline (LDS reads ahead of the MFMAs); 0: any T <= 256
+template <int NT>
 __global__ __launch_bounds__(1024) void attn_fwd_res_kernel(AttnBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int TP = (a.T + 15) & ~15, TV = (a.T + 31) & ~31;
@@ -501,59 +504,121 @@ __global__ __launch_bounds__(1024) void attn_fwd_res_kernel(AttnBwdArgs a) {
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   if (q0 >= a.T) return;  // wave-uniform: no partial EXEC below (the transposed reads need all lanes)
-  const int nt = TP / 16;
+  const int nt = NT > 0 ? NT : TP / 16;
   const float c2 = a.scale * kLog2e;
   f32x4 x[kResMaxT / 16];
   float m = -kInf;
-#pragma unroll
-  for (int kt = 0; kt < kResMaxT / 16; ++kt) {
-    x[kt] = f32x4{-kInf, -kInf, -kInf, -kInf};
-    if (kt < nt) {
-      const int row = 16 * kt + col;
-      f32x4 s = {};
-      s = mfma(img_row(kimg, row, g), qf[0], s);
-      s = mfma(img_row(kimg, row, 4 + g), qf[1], s);
-      if (16 * kt + 16 <= a.T) {  // wave-uniform: only the last tile has padded keys
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          x[kt][r] = s[r] * c2;
-          m = fmaxf(m, x[kt][r]);
-        }
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = 16 * kt + 4 * g + r;
-          x[kt][r] = key < a.T ? s[r] * c2 : -kInf;
-          m = fmaxf(m, x[kt][r]);
-        }
-      }
-    }
-  }
-  m = xor_max<32>(xor_max<16>(m));  // permlane swaps (common.h)
   float l = 0.f;
+  f32x4 acc[4] = {};
+  if constexpr (NT > 0) {
+    // software-pipelined: the K fragments of tile kt + 2 are read while tile kt's MFMAs run, the
+    // scale / mask / max pass comes after all S tiles (no VALU between the reads and the MFMAs),
+    // and the V^T fragments of k-step ks + 1 are read during k-step ks (PMC rd3t: ~45 % of the
+    // wave cycles waited on a one-tile-at-a-time read -> wait -> MFMA chain)
+    constexpr int KS = (NT + 1) / 2;
+    bf16x8 fk[2][2];
 #pragma unroll
-  for (int kt = 0; kt < kResMaxT / 16; ++kt) {
-    if (kt < nt) {  // wave-uniform
+    for (int t = 0; t < (NT < 2 ? NT : 2); ++t) {
+      fk[t][0] = img_row(kimg, 16 * t + col, g);
+      fk[t][1] = img_row(kimg, 16 * t + col, 4 + g);
+    }
+#pragma unroll
+    for (int kt = 0; kt < NT; ++kt) {
+      f32x4 sacc = {};
+      sacc = mfma(fk[kt & 1][0], qf[0], sacc);
+      sacc = mfma(fk[kt & 1][1], qf[1], sacc);
+      if (kt + 2 < NT) {
+        fk[kt & 1][0] = img_row(kimg, 16 * (kt + 2) + col, g);
+        fk[kt & 1][1] = img_row(kimg, 16 * (kt + 2) + col, 4 + g);
+      }
+      x[kt] = sacc;
+    }
+#pragma unroll
+    for (int kt = 0; kt < NT; ++kt) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float pv = fast_exp2(x[kt][r] - m);  // -inf (padded key) -> 0
-        x[kt][r] = pv;
-        l += pv;
+        const int key = 16 * kt + 4 * g + r;
+        x[kt][r] = (kt < NT - 1 || key < a.T) ? x[kt][r] * c2 : -kInf;  // only the last tile pads
+        m = fmaxf(m, x[kt][r]);
       }
-    } else {
-      x[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-  }
-  l = butterfly_from<16>(l);  // permlane swaps (common.h)
-  // O^T[d][q] = sum over keys of V^T[d][key] P^T[key][q]; k-step ks covers keys 32ks .. +31 in
-  // the accumulator-pair order (j < 4: 32ks + 4g + j, j >= 4: 32ks + 16 + 4g + j - 4)
-  f32x4 acc[4] = {};
+    m = xor_max<32>(xor_max<16>(m));  // permlane swaps (common.h)
 #pragma unroll
-  for (int ks = 0; ks < kResMaxT / 32; ++ks) {
-    if (32 * ks < TV) {
+    for (int kt = 0; kt < 2 * KS; ++kt) {
+      if (kt < NT) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = fast_exp2(x[kt][r] - m);  // -inf (padded key) -> 0
+          x[kt][r] = pv;
+          l += pv;
+        }
+      } else {
+        x[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    l = butterfly_from<16>(l);  // permlane swaps (common.h)
+    bf16x8 fv[2][4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) fv[0][dt] = img_tr(vimg, 0, 16 * dt);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + 1 < KS) {
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) fv[(ks + 1) & 1][dt] = img_tr(vimg, 32 * (ks + 1), 16 * dt);
+      }
       const bf16x8 bop = pack(x[2 * ks], x[2 * ks + 1]);
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma(img_tr(vimg, 32 * ks, 16 * dt), bop, acc[dt]);
+      for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma(fv[ks & 1][dt], bop, acc[dt]);
+    }
+  } else {
+#pragma unroll
+    for (int kt = 0; kt < (NT > 0 ? NT : kResMaxT / 16); ++kt) {
+      x[kt] = f32x4{-kInf, -kInf, -kInf, -kInf};
+      if (NT > 0 || kt < nt) {
+        const int row = 16 * kt + col;
+        f32x4 s = {};
+        s = mfma(img_row(kimg, row, g), qf[0], s);
+        s = mfma(img_row(kimg, row, 4 + g), qf[1], s);
+        if (16 * kt + 16 <= a.T) {  // wave-uniform: only the last tile has padded keys
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            x[kt][r] = s[r] * c2;
+            m = fmaxf(m, x[kt][r]);
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = 16 * kt + 4 * g + r;
+            x[kt][r] = key < a.T ? s[r] * c2 : -kInf;
+            m = fmaxf(m, x[kt][r]);
+          }
+        }
+      }
+    }
+    m = xor_max<32>(xor_max<16>(m));  // permlane swaps (common.h)
+#pragma unroll
+    for (int kt = 0; kt < (NT > 0 ? NT : kResMaxT / 16); ++kt) {
+      if (NT > 0 || kt < nt) {  // wave-uniform
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = fast_exp2(x[kt][r] - m);  // -inf (padded key) -> 0
+          x[kt][r] = pv;
+          l += pv;
+        }
+      } else {
+        x[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    l = butterfly_from<16>(l);  // permlane swaps (common.h)
+    // O^T[d][q] = sum over keys of V^T[d][key] P^T[key][q]; k-step ks covers keys 32ks .. +31 in
+    // the accumulator-pair order (j < 4: 32ks + 4g + j, j >= 4: 32ks + 16 + 4g + j - 4)
+#pragma unroll
+    for (int ks = 0; ks < (NT > 0 ? (NT + 1) / 2 : kResMaxT / 32); ++ks) {
+      if (NT > 0 || 32 * ks < TV) {
+        const bf16x8 bop = pack(x[2 * ks], x[2 * ks + 1]);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma(img_tr(vimg, 32 * ks, 16 * dt), bop, acc[dt]);
+      }
     }
   }
   if (qok) {
@@ -760,6 +825,7 @@ __global__ __launch_bounds__(1024) void attn_fwd_pers_kernel(AttnBwdArgs a) {
 //                     S = Q K^T, dP = dO V^T, dS = P (dP - D), dV^T += dO^T P, dK^T += Q^T dS.
 // Each image is read by rows (ds_read_b128) and by columns (ds_read_b64_tr_b16), one
 // swizzle for both (swz_b). Padded rows (>= T) are zero; padded queries get lse = +inf.
+template <int NT>
 __global__ __launch_bounds__(1024) void attn_bwd_dq_res_kernel(AttnBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int TP = (a.T + 15) & ~15, TV = (a.T + 31) & ~31;
@@ -799,13 +865,60 @@ __global__ __launch_bounds__(1024) void attn_bwd_dq_res_kernel(AttnBwdArgs a) {
   for (int j = 0; j < 8; ++j) dsum += (float)gf[0][j] * (float)o0[j] + (float)gf[1][j] * (float)o1[j];
   dsum = butterfly_from<16>(dsum);  // permlane swaps (common.h)
   if (qok && g == 0) st[1] = dsum;
-  const int nt = TP / 16;
+  const int nt = NT > 0 ? NT : TP / 16;
   const float c2 = a.scale * kLog2e;
   f32x4 ds[kResMaxT / 16];
+  f32x4 acc[4] = {};
+  if constexpr (NT > 0) {
+    // software-pipelined like the forward: the K / V fragments of tile kt + 2 are read while tile
+    // kt's MFMAs run; the K^T fragments of k-step ks + 1 during k-step ks
+    constexpr int KS = (NT + 1) / 2;
+    if constexpr (NT & 1) ds[NT] = f32x4{0.f, 0.f, 0.f, 0.f};  // odd NT: the last k-step's pad half
+    bf16x8 fk[2][2], fw[2][2];
+#pragma unroll
+    for (int t = 0; t < (NT < 2 ? NT : 2); ++t) {
+      fk[t][0] = img_row(kimg, 16 * t + col, g);
+      fk[t][1] = img_row(kimg, 16 * t + col, 4 + g);
+      fw[t][0] = img_row(vimg, 16 * t + col, g);
+      fw[t][1] = img_row(vimg, 16 * t + col, 4 + g);
+    }
+#pragma unroll
+    for (int kt = 0; kt < NT; ++kt) {
+      f32x4 sv = {}, dp = {};
+      sv = mfma(fk[kt & 1][0], qf[0], sv);
+      sv = mfma(fk[kt & 1][1], qf[1], sv);
+      dp = mfma(fw[kt & 1][0], gf[0], dp);
+      dp = mfma(fw[kt & 1][1], gf[1], dp);
+      if (kt + 2 < NT) {
+        fk[kt & 1][0] = img_row(kimg, 16 * (kt + 2) + col, g);
+        fk[kt & 1][1] = img_row(kimg, 16 * (kt + 2) + col, 4 + g);
+        fw[kt & 1][0] = img_row(vimg, 16 * (kt + 2) + col, g);
+        fw[kt & 1][1] = img_row(vimg, 16 * (kt + 2) + col, 4 + g);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = 16 * kt + 4 * g + r;
+        ds[kt][r] = (kt < NT - 1 || key < a.T) ? fast_exp2(fmaf(sv[r], c2, -lse)) * (dp[r] - dsum) : 0.f;
+      }
+    }
+    bf16x8 ft[2][4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) ft[0][dt] = img_tr(kimg, 0, 16 * dt);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + 1 < KS) {
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) ft[(ks + 1) & 1][dt] = img_tr(kimg, 32 * (ks + 1), 16 * dt);
+      }
+      const bf16x8 bop = pack(ds[2 * ks], ds[2 * ks + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma(ft[ks & 1][dt], bop, acc[dt]);
+    }
+  } else {
 #pragma unroll
   for (int kt = 0; kt < kResMaxT / 16; ++kt) {
     ds[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (kt < nt) {
+    if (NT > 0 || kt < nt) {
       const int row = 16 * kt + col;
       f32x4 sv = {}, dp = {};
       sv = mfma(img_row(kimg, row, g), qf[0], sv);
@@ -824,7 +937,6 @@ __global__ __launch_bounds__(1024) void attn_bwd_dq_res_kernel(AttnBwdArgs a) {
       }
     }
   }
-  f32x4 acc[4] = {};
 #pragma unroll
   for (int ks = 0; ks < kResMaxT / 32; ++ks) {
     if (32 * ks < TV) {
@@ -832,6 +944,7 @@ __global__ __launch_bounds__(1024) void attn_bwd_dq_res_kernel(AttnBwdArgs a) {
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma(img_tr(kimg, 32 * ks, 16 * dt), bop, acc[dt]);
     }
+  }
   }
   if (qok) {
 #pragma unroll
@@ -844,6 +957,7 @@ __global__ __launch_bounds__(1024) void attn_bwd_dq_res_kernel(AttnBwdArgs a) {
   if (a.colpart != nullptr) colpart_store(colpart_row(a, b, h, part, w, 0), acc, a.scale, qok);
 }
 
+template <int NT>
 __global__ __launch_bounds__(1024) void attn_bwd_dkv_res_kernel(AttnBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int TV = (a.T + 31) & ~31;
@@ -883,8 +997,7 @@ __global__ __launch_bounds__(1024) void attn_bwd_dkv_res_kernel(AttnBwdArgs a) {
   }
   const float c2 = a.scale * kLog2e;
   f32x4 accK[4] = {}, accV[4] = {};
-#pragma unroll 2
-  for (int ks = 0; ks < TV / 32; ++ks) {
+  auto kstep = [&](int ks) __attribute__((always_inline)) {
     f32x4 p[2], dsv[2];
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
@@ -908,6 +1021,13 @@ __global__ __launch_bounds__(1024) void attn_bwd_dkv_res_kernel(AttnBwdArgs a) {
       accV[dt] = mfma(img_tr(gimg, 32 * ks, 16 * dt), pb, accV[dt]);
       accK[dt] = mfma(img_tr(qimg, 32 * ks, 16 * dt), db, accK[dt]);
     }
+  };
+  if constexpr (NT > 0) {  // compile-time trip count: fully unrolled, next k-step's reads hoisted
+#pragma unroll
+    for (int ks = 0; ks < (NT + 1) / 2; ++ks) kstep(ks);
+  } else {
+#pragma unroll 2
+    for (int ks = 0; ks < TV / 32; ++ks) kstep(ks);
   }
   if (kok) {
 #pragma unroll
@@ -1265,6 +1385,15 @@ void attn_fwd_pers_kernel_attr(const void* k) {
   }
 }
 
+// FLUXMPI_ATTN_GENERIC=1: the runtime-tile-count kernels for every T (A/B of the NT = 13 instances)
+bool attn_generic() {
+  static const bool on = [] {
+    const char* e = std::getenv("FLUXMPI_ATTN_GENERIC");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
+}
+
 int g_attn_bwd_fused = -1;  // backward variant (attn_set_bwd_fused); -1: FLUXMPI_ATTN_BWD decides
 int g_attn_fwd_mode = -1;   // forward variant (attn_set_fwd_mode); -1: FLUXMPI_ATTN_FWD decides
 
@@ -1362,9 +1491,12 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* o, const 
     const int waves = (tiles + a.nblk - 1) / a.nblk;
     const int TP = (T + 15) & ~15, TV = (T + 31) & ~31;
     a.colpart = colpart;  // [B * nblk * waves][3 * H * 64] (attn_bwd_colpart_rows), or nullptr
-    attn_bwd_dq_res_kernel<<<static_cast<unsigned>(bh), waves * 64, static_cast<size_t>(TV + TP) * 128, s>>>(a);
+    const bool vit = tiles == 13 && !attn_generic();  // T 193..208 (ViT: 197): compile-time tile count
+    auto kdq = vit ? attn_bwd_dq_res_kernel<13> : attn_bwd_dq_res_kernel<0>;
+    auto kdkv = vit ? attn_bwd_dkv_res_kernel<13> : attn_bwd_dkv_res_kernel<0>;
+    kdq<<<static_cast<unsigned>(bh), waves * 64, static_cast<size_t>(TV + TP) * 128, s>>>(a);
     FLUXMPI_HIP_CHECK(hipGetLastError());
-    attn_bwd_dkv_res_kernel<<<static_cast<unsigned>(bh), waves * 64, static_cast<size_t>(2 * TV) * 128 + 2 * TV * 4,
+    kdkv<<<static_cast<unsigned>(bh), waves * 64, static_cast<size_t>(2 * TV) * 128 + 2 * TV * 4,
                               s>>>(a);
     FLUXMPI_HIP_CHECK(hipGetLastError());
     return;
@@ -1444,7 +1576,8 @@ void attn_fwd(const void* q, const void* k, const void* v, void* o, float* stats
     if (total > 0x7fffffff) throw std::runtime_error("attn_fwd: grid too large");
     const int waves = (tiles + a.nblk - 1) / a.nblk;
     const size_t lds = static_cast<size_t>(((T + 15) & ~15) + ((T + 31) & ~31)) * 128;
-    attn_fwd_res_kernel<<<static_cast<unsigned>(total), waves * 64, lds, s>>>(a);
+    auto kf = (tiles == 13 && !attn_generic()) ? attn_fwd_res_kernel<13> : attn_fwd_res_kernel<0>;
+    kf<<<static_cast<unsigned>(total), waves * 64, lds, s>>>(a);
     FLUXMPI_HIP_CHECK(hipGetLastError());
     return;
   }
