@@ -69,6 +69,12 @@ def parse():
     return ap.parse_args()
 
 
+def _gelu_form() -> str:
+    from fluxmpi_amd.ops import gelu as GL
+
+    return GL.FORM
+
+
 def main():
     args = parse()
     if args.image is None:
@@ -235,6 +241,7 @@ def main():
                        **cs, "exposed_comm_ms": None if exposed is None else round(exposed, 3),
                        **({"emulate_comm": args.emulate_comm} if args.emulate_comm else {}),
                        "grid_rounds": int(os.environ.get("FLUXMPI_GRID_ROUNDS", "1")),
+                       **({"gelu": _gelu_form()} if args.model == "vit_b16" else {}),
                        **({"deq_fwd_iters_per_step": round(sum(i[0] for i in timed_iters) / len(timed_iters), 2),
                            "deq_bwd_iters_per_step": round(sum(i[1] for i in timed_iters) / len(timed_iters), 2)}
                           if timed_iters else {})},

@@ -310,5 +310,9 @@ void emulate_comm(int blocks, double microseconds, hipStream_t stream, int threa
 void colsum(const void* x, float* partials, int blocks, int64_t rows, int64_t N, int dtype, hipStream_t stream);
 void gelu_bwd_bias(const void* dy, const void* h, void* dh, float* partials, int blocks, int64_t rows, int64_t N,
                    int dtype, hipStream_t stream);
+// GELU form of the fused GELU kernels (gelu_bwd_bias, gemm256 EPI 1 / 2): 1 tanh (NNlib's `gelu`,
+// the default), 0 exact erf. Host-side switch read at launch.
+void gelu_set_form(int tanh_form);
+int gelu_form();
 
 }  // namespace fluxmpi

@@ -321,6 +321,9 @@ PYBIND11_MODULE(_C, m) {
                   reinterpret_cast<float*>(part), blocks, rows, N, dtype, S(stream));
   });
 
+  m.def("gelu_set_form", &gelu_set_form);
+  m.def("gelu_form", &gelu_form);
+
   // ---- fused LayerNorm ------------------------------------------------------
   m.def("layernorm_fwd", [](uintptr_t x, uintptr_t res, uintptr_t h, uintptr_t y, uintptr_t w, uintptr_t b,
                             uintptr_t mean, uintptr_t rstd, int64_t rows, int64_t D, float eps, int dtype,

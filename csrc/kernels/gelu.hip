@@ -6,12 +6,14 @@
 // Here one pass writes dh and accumulates db1: every lane owns ONE fixed 8-column vector
 // (blockDim = N/8 lanes, N/8 a multiple of 64), so its column sums stay in registers over
 // the workgroup's row range; each workgroup stores one fp32 partial row (no atomics), summed
-// by gemm_splitk_reduce. Erf-form GELU derivative in fp32 (polynomial erf, |error| <= 1.5e-7).
+// by gemm_splitk_reduce. GELU derivative in fp32: tanh form (gelu_tanh.h; the default, gelu_set_form)
+// or the exact erf form (polynomial erf, |error| <= 1.5e-7).
 #include <stdexcept>
 #include <string>
 
 #include "../api.h"
 #include "common.h"
+#include "gelu_tanh.h"
 
 namespace fluxmpi {
 namespace {
@@ -34,7 +36,15 @@ __device__ __forceinline__ float gelu_grad(float x) {
   return fmaf(x * kInvSqrt2Pi, e, cdf);
 }
 
-template <typename T>
+int g_gelu_tanh = 1;  // gelu_set_form
+
+template <bool TANH>
+__device__ __forceinline__ float gelu_d(float x) {
+  if constexpr (TANH) return gelu_tanh_grad(x);
+  else return gelu_grad(x);
+}
+
+template <typename T, bool TANH>
 __global__ __launch_bounds__(1024) void gelu_bwd_bias_kernel(const T* __restrict__ dy, const T* __restrict__ h,
                                                              T* __restrict__ dh, float* __restrict__ part,
                                                              int64_t rows, int64_t N, int64_t rows_per_wg) {
@@ -61,7 +71,7 @@ __global__ __launch_bounds__(1024) void gelu_bwd_bias_kernel(const T* __restrict
       T ov[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        ov[j] = from_f<T>(to_f(dv[u][j]) * gelu_grad(to_f(hv[u][j])));
+        ov[j] = from_f<T>(to_f(dv[u][j]) * gelu_d<TANH>(to_f(hv[u][j])));
         acc[j] += to_f(ov[j]);  // db of the rounded dh the weight / input gradients use
       }
       store8(dh + (r + u) * N + cv * 8, ov);
@@ -74,7 +84,7 @@ __global__ __launch_bounds__(1024) void gelu_bwd_bias_kernel(const T* __restrict
     load8(h + off, hv);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      ov[j] = from_f<T>(to_f(dv[j]) * gelu_grad(to_f(hv[j])));
+      ov[j] = from_f<T>(to_f(dv[j]) * gelu_d<TANH>(to_f(hv[j])));
       acc[j] += to_f(ov[j]);
     }
     store8(dh + off, ov);
@@ -173,6 +183,9 @@ int gelu_bwd_bias_blocks(int64_t rows) {
   return static_cast<int>(b);
 }
 
+void gelu_set_form(int tanh_form) { g_gelu_tanh = tanh_form != 0 ? 1 : 0; }
+int gelu_form() { return g_gelu_tanh; }
+
 void gelu_bwd_bias(const void* dy, const void* h, void* dh, float* partials, int blocks, int64_t rows, int64_t N,
                    int dtype, hipStream_t stream) {
   if (N % 8 != 0 || (N / 8) % 64 != 0 || N / 8 > 1024)
@@ -182,15 +195,20 @@ void gelu_bwd_bias(const void* dy, const void* h, void* dh, float* partials, int
     throw std::runtime_error("gelu_bwd_bias: tensors must be 16-byte aligned");
   const int64_t rpw = (rows + blocks - 1) / blocks;
   const unsigned threads = static_cast<unsigned>(N / 8);
+  const bool tanh_form = g_gelu_tanh != 0;
   switch (dtype) {
-    case kBF16:
-      gelu_bwd_bias_kernel<bf16><<<blocks, threads, 0, stream>>>(static_cast<const bf16*>(dy), static_cast<const bf16*>(h),
-                                                                 static_cast<bf16*>(dh), partials, rows, N, rpw);
+    case kBF16: {
+      auto k = tanh_form ? gelu_bwd_bias_kernel<bf16, true> : gelu_bwd_bias_kernel<bf16, false>;
+      k<<<blocks, threads, 0, stream>>>(static_cast<const bf16*>(dy), static_cast<const bf16*>(h), static_cast<bf16*>(dh),
+                                        partials, rows, N, rpw);
       break;
-    case kF16:
-      gelu_bwd_bias_kernel<f16><<<blocks, threads, 0, stream>>>(static_cast<const f16*>(dy), static_cast<const f16*>(h),
-                                                                static_cast<f16*>(dh), partials, rows, N, rpw);
+    }
+    case kF16: {
+      auto k = tanh_form ? gelu_bwd_bias_kernel<f16, true> : gelu_bwd_bias_kernel<f16, false>;
+      k<<<blocks, threads, 0, stream>>>(static_cast<const f16*>(dy), static_cast<const f16*>(h), static_cast<f16*>(dh),
+                                        partials, rows, N, rpw);
       break;
+    }
     default:
       throw std::runtime_error("gelu_bwd_bias: bf16 / fp16 only");
   }

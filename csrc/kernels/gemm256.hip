@@ -10,7 +10,7 @@
 // derivative + fc1's bias gradient (gelu_bwd_bias, 197 us per block). Here those live in
 // the epilogue:
 //   EPI 0: C = acc (+ bias)                                  -> bf16
-//   EPI 1: h = acc + bias -> C (bf16), g = gelu(h) -> C2      (fc1 forward, exact erf GELU)
+//   EPI 1: h = acc + bias -> C (bf16), g = gelu(h) -> C2      (fc1 forward; tanh or erf GELU, gelu_set_form)
 //   EPI 2: dh = bf16(acc) * gelu'(H[m][n]) -> C (bf16), and the column sums of dh over the
 //          tile's rows -> colpart[2 * tile_m + wave_m][n] (fp32, no atomics; fc1's bias
 //          gradient after gemm_splitk_reduce)                (fc2's input gradient)
@@ -34,6 +34,7 @@
 
 #include "../api.h"
 #include "common.h"
+#include "gelu_tanh.h"
 
 namespace fluxmpi {
 namespace {
@@ -94,6 +95,7 @@ struct G256Args {
   int64_t M, N, K;
   int tiles_m, tiles_n;
   int bias_f32;
+  int gelu_tanh;  // EPI 1 / 2: tanh-form GELU (gelu_set_form), else exact erf
 };
 
 // VAR bit 0: the next step's LDS-DMA is issued spread through this step's MFMAs (one piece per
@@ -327,9 +329,13 @@ __global__ __launch_bounds__(kThreads, 2) void gemm256_kernel(G256Args p) {
         for (int r = 0; r < 4; ++r) {
           o[r] = static_cast<bf16>(acc[i][j][r] + bias[j][r]);
           const float x = static_cast<float>(o[r]);  // GELU of the bf16 pre-activation, as F.gelu(h)
-          float cdf, e;
-          gelu_parts(x, cdf, e);
-          g[r] = static_cast<bf16>(x * cdf);
+          if (p.gelu_tanh) {
+            g[r] = static_cast<bf16>(gelu_tanh(x));
+          } else {
+            float cdf, e;
+            gelu_parts(x, cdf, e);
+            g[r] = static_cast<bf16>(x * cdf);
+          }
         }
         uint2 gv;
         __builtin_memcpy(&gv, g, 8);
@@ -341,9 +347,15 @@ __global__ __launch_bounds__(kThreads, 2) void gemm256_kernel(G256Args p) {
         for (int r = 0; r < 4; ++r) {
           const float dg = static_cast<float>(static_cast<bf16>(acc[i][j][r]));  // the bf16 dg, as autograd sees it
           const float x = static_cast<float>(hh[r]);
-          float cdf, e;
-          gelu_parts(x, cdf, e);
-          o[r] = static_cast<bf16>(dg * fmaf(x * 0.39894228040143268f, e, cdf));
+          float d;
+          if (p.gelu_tanh) {
+            d = gelu_tanh_grad(x);
+          } else {
+            float cdf, e;
+            gelu_parts(x, cdf, e);
+            d = fmaf(x * 0.39894228040143268f, e, cdf);
+          }
+          o[r] = static_cast<bf16>(dg * d);
           cs[j][r] += static_cast<float>(o[r]);  // the bias gradient of the rounded dh
         }
       }
@@ -448,7 +460,7 @@ void gemm256(const void* a, const void* b, void* c, void* c2, const void* bias, 
     throw std::runtime_error("gemm256: bias must be 16-byte (fp32) / 8-byte (bf16) aligned");
   G256Args p{static_cast<const bf16*>(a), static_cast<const bf16*>(b), static_cast<bf16*>(c), static_cast<bf16*>(c2),
              bias, static_cast<const bf16*>(h), colpart, lda, ldb, ldc, M, N, K,
-             static_cast<int>(M / kTile), static_cast<int>(N / kTile), bias_f32};
+             static_cast<int>(M / kTile), static_cast<int>(N / kTile), bias_f32, gelu_form()};
   if (b_t) {
     if (epi == 2) launch<true, 2>(p, stream);
     else if (epi == 1) launch<true, 1>(p, stream);

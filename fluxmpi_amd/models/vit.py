@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.gelu import GeluLink, linear_gelu
+from ..ops.gelu import GeluLink, gelu, linear_gelu
 from ..ops.layernorm import linear_add_layer_norm
 from ..ops.linear import Linear
 
@@ -155,7 +155,7 @@ class Block(nn.Module):
         # fc1 + GELU: the GELU derivative and fc1's bias gradient come out of the consumer's
         # (the next ln1 node's fc2) input-gradient GEMM through the link (ops/gelu.py)
         link = GeluLink() if (_FUSED_GELU and not cls_only) else None
-        g = linear_gelu(y, self.fc1.weight, self.fc1.bias, link=link) if _FUSED_GELU else F.gelu(self.fc1(y))
+        g = linear_gelu(y, self.fc1.weight, self.fc1.bias, link=link) if _FUSED_GELU else gelu(self.fc1(y))
         return x, (g, self.fc2, link)
 
 

@@ -1,19 +1,61 @@
 """``gelu(linear(x, W, b))`` with the GELU backward and the bias gradient in one HIP pass
 (``csrc/kernels/gelu.hip``).
 
-Autograd would run the GELU backward (read dy, h; write dh) and then reduce dh again for
-the Linear's bias gradient. ``linear_gelu`` owns both ops: its backward writes ``dh`` and
-per-workgroup column sums in one pass, then issues the same two GEMMs as ``nn.Linear``'s
-backward (``dh @ W``, ``dh^T @ x``). CPU tensors and unsupported widths use the PyTorch
-composition.
+GELU form (``FLUXMPI_GELU`` / :func:`set_form`): ``tanh`` (default) — NNlib's ``gelu``, the
+activation of the reference's Lux / Metalhead ViT (``x/2 (1 + tanh(sqrt(2/pi)(x + 0.044715
+x^3)))``) — or ``erf`` (exact). Both run the same kernels (``gelu.hip``, gemm256's epilogues)
+at the same speed (ViT-B/16 7.04k / 7.06k tanh vs 7.04k / 7.05k erf, same box). A hipBLASLt
+bias + GELU epilogue that also writes the pre-activation (``GELU_AUX_BIAS``, which would drop
+the forward's elementwise GELU pass) has no gfx950 solution in either hipBLASLt of the image
+(``scripts/probe/blaslt_epi_probe.cpp``, ``profiles/rd3y_blaslt_epilogue_probe.txt``).
 """
 from __future__ import annotations
+
+import os
 
 import torch
 import torch.nn.functional as F
 
 from . import _ext
 from .multi_tensor import DTYPE_CODE
+
+FORM = os.environ.get("FLUXMPI_GELU", "tanh").lower()
+if FORM not in ("tanh", "erf"):
+    raise ValueError(f"FLUXMPI_GELU must be 'tanh' or 'erf' (got {FORM!r})")
+_synced = [None]  # form last pushed to the extension
+
+
+def set_form(form: str) -> None:
+    """Select the GELU form of every fused GELU path (``"tanh"`` or ``"erf"``)."""
+    global FORM
+    if form not in ("tanh", "erf"):
+        raise ValueError(f"GELU form must be 'tanh' or 'erf' (got {form!r})")
+    FORM = form
+
+
+def _approx() -> str:
+    return "tanh" if FORM == "tanh" else "none"
+
+
+def gelu(h: torch.Tensor) -> torch.Tensor:
+    """GELU of the selected form (PyTorch composition)."""
+    return F.gelu(h, approximate=_approx())
+
+
+def _sync(C) -> None:
+    if _synced[0] != FORM:
+        C.gelu_set_form(1 if FORM == "tanh" else 0)
+        _synced[0] = FORM
+
+
+def _gelu_grad_ref(hf: torch.Tensor) -> torch.Tensor:
+    if FORM == "tanh":
+        k0 = 0.7978845608028654
+        t = torch.tanh(k0 * (hf + 0.044715 * hf ** 3))
+        return 0.5 * (1 + t) + 0.5 * hf * (1 - t * t) * k0 * (1 + 3 * 0.044715 * hf * hf)
+    cdf = 0.5 * (1 + torch.erf(hf * 0.7071067811865476))
+    pdf = torch.exp(-0.5 * hf * hf) * 0.3989422804014327
+    return cdf + hf * pdf
 
 
 def _native(h: torch.Tensor) -> bool:
@@ -23,14 +65,12 @@ def _native(h: torch.Tensor) -> bool:
 
 
 def gelu_bwd_bias(dy: torch.Tensor, h: torch.Tensor, bias_dtype=torch.float32):
-    """``(dh, db)``: ``dh = dy * gelu'(h)`` (erf form), ``db = dh.sum(rows)`` in ``bias_dtype``."""
+    """``(dh, db)``: ``dh = dy * gelu'(h)`` (the selected form), ``db = dh.sum(rows)`` in ``bias_dtype``."""
     if not _native(h):
-        hf = h.float()
-        cdf = 0.5 * (1 + torch.erf(hf * 0.7071067811865476))
-        pdf = torch.exp(-0.5 * hf * hf) * 0.3989422804014327
-        dh = (dy.float() * (cdf + hf * pdf)).to(h.dtype)
+        dh = (dy.float() * _gelu_grad_ref(h.float())).to(h.dtype)
         return dh, dh.float().reshape(-1, h.shape[-1]).sum(0).to(bias_dtype)
     C = _ext.get(required=True)
+    _sync(C)
     n = h.shape[-1]
     rows = h.numel() // n
     h = h.contiguous()
@@ -69,6 +109,7 @@ class _LinearGeluFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, link=None):
         from . import gemm256
+        _sync(_ext.get(required=True))  # the backward kernels (gelu.hip, gemm256 EPI 2) read the form
         n_out, n_in = weight.shape
         rows = x.numel() // n_in
         if x.is_contiguous() and gemm256.supported(rows, n_out, n_in, x, weight):
@@ -77,7 +118,7 @@ class _LinearGeluFn(torch.autograd.Function):
             h, g = h2.view(*x.shape[:-1], n_out), g2.view(*x.shape[:-1], n_out)
         else:
             h = F.linear(x, weight, bias)
-            g = F.gelu(h)
+            g = gelu(h)
         ctx.save_for_backward(x, weight, h)
         ctx.has_bias = bias is not None
         ctx.bias_dtype = bias.dtype if bias is not None else None
@@ -108,11 +149,11 @@ class _LinearGeluFn(torch.autograd.Function):
 
 def linear_gelu(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None,
                 link: GeluLink | None = None) -> torch.Tensor:
-    """``F.gelu(F.linear(x, weight, bias))`` (exact GELU) with the fused backward on the GPU.
-    ``link``: pass the same :class:`GeluLink` to the consuming ``linear_add_layer_norm``."""
+    """``gelu(F.linear(x, weight, bias))`` (the selected GELU form) with the fused backward on
+    the GPU. ``link``: pass the same :class:`GeluLink` to the consuming ``linear_add_layer_norm``."""
     if x.is_cuda and _native_width(weight.shape[0], x.dtype):
         return _LinearGeluFn.apply(x, weight, bias, link)
-    return F.gelu(F.linear(x, weight, bias))
+    return gelu(F.linear(x, weight, bias))
 
 
 def _native_width(n: int, dtype) -> bool:

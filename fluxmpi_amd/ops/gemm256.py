@@ -1,6 +1,6 @@
 """Token-major Linear GEMMs on 256 x 256 tiles with fused epilogues (``csrc/kernels/gemm256.hip``).
 
-* :func:`linear_fwd` — ``y = x W^T + b`` (``gelu=True``: also ``g = gelu(y)``, exact erf form,
+* :func:`linear_fwd` — ``y = x W^T + b`` (``gelu=True``: also ``g = gelu(y)``, the ops.gelu form,
   from the same registers: fc1 of a transformer MLP writes its pre-activation and its
   activation in one pass, no elementwise GELU kernel);
 * :func:`linear_dgrad` — ``dx = dy W`` (``gelu_h=h``: ``dh = dx * gelu'(h)`` and the column
@@ -60,6 +60,9 @@ def linear_fwd(x2: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None
     w = weight.contiguous()
     y = torch.empty(m, n, device=x2.device, dtype=x2.dtype)
     g = torch.empty_like(y) if gelu else None
+    if gelu:
+        from .gelu import _sync
+        _sync(C)  # EPI 1 computes the selected GELU form
     b = bias.contiguous() if bias is not None else None
     C.gemm256(x2.data_ptr(), w.data_ptr(), y.data_ptr(), g.data_ptr() if gelu else 0,
               b.data_ptr() if b is not None else 0, int(b is not None and b.dtype == torch.float32), 0, 0,
@@ -82,6 +85,8 @@ def linear_dgrad(dy2: torch.Tensor, weight: torch.Tensor, gelu_h: torch.Tensor |
     if gelu_h is None:
         C.gemm256(dy2.data_ptr(), w.data_ptr(), dx.data_ptr(), 0, 0, 0, 0, 0, n, k, k, m, k, n, True, 0, s)
         return dx
+    from .gelu import _sync
+    _sync(C)  # EPI 2 differentiates the selected GELU form
     h = gelu_h.reshape(m, k).contiguous()
     rows = C.gemm256_colpart_rows(m)
     part = torch.empty(rows, k, device=dy2.device, dtype=torch.float32)

@@ -1,20 +1,48 @@
-"""Fused GELU backward + bias gradient (``csrc/kernels/gelu.hip``, ``ops/gelu.py``)
-against the fp32 PyTorch composition ``gelu(linear(x, W, b))``."""
+"""Fused GELU backward + bias gradient (``csrc/kernels/gelu.hip``, ``ops/gelu.py``) against the
+fp32 PyTorch composition ``gelu(linear(x, W, b))``, for both GELU forms (tanh: NNlib's ``gelu``,
+the default; erf)."""
 import pytest
 import torch
 import torch.nn.functional as F
 
+from fluxmpi_amd.ops import gelu as GL
 from fluxmpi_amd.ops.gelu import gelu_bwd_bias, linear_gelu
+
+
+@pytest.fixture(params=["tanh", "erf"])
+def form(request):
+    old = GL.FORM
+    GL.set_form(request.param)
+    yield request.param
+    GL.set_form(old)
 
 
 def _ref(x, w, b, dy):
     xr, wr, br = (t.detach().float().clone().requires_grad_() for t in (x, w, b))
-    y = F.gelu(F.linear(xr, wr, br))
+    y = GL.gelu(F.linear(xr, wr, br))
     y.backward(dy.float())
     return y, xr.grad, wr.grad, br.grad
 
 
-def test_linear_gelu_cpu_fallback():
+def test_default_form_is_nnlib_tanh():
+    assert GL.FORM == "tanh"  # FLUXMPI_GELU unset in the test environment
+    x = torch.linspace(-6, 6, 101, dtype=torch.float64)
+    nnlib = 0.5 * x * (1 + torch.tanh((2 / torch.pi) ** 0.5 * (x + 0.044715 * x ** 3)))
+    torch.testing.assert_close(GL.gelu(x), nnlib)
+
+
+def test_gelu_grad_ref_matches_autograd(form):
+    x = torch.linspace(-8, 8, 1001, dtype=torch.float64, requires_grad=True)
+    GL.gelu(x).sum().backward()
+    torch.testing.assert_close(GL._gelu_grad_ref(x.detach()), x.grad)
+
+
+def test_set_form_rejects_unknown():
+    with pytest.raises(ValueError):
+        GL.set_form("sigmoid")
+
+
+def test_linear_gelu_cpu_fallback(form):
     torch.manual_seed(0)
     x, w, b = torch.randn(3, 5, 16, requires_grad=True), torch.randn(24, 16, requires_grad=True), torch.randn(24, requires_grad=True)
     y = linear_gelu(x, w, b)
@@ -33,7 +61,7 @@ def test_linear_gelu_cpu_fallback():
 @pytest.mark.gpu
 @pytest.mark.parametrize("rows,k,n", [(197 * 4, 768, 3072), (1000, 64, 512), (37, 128, 8192), (50432, 768, 3072)])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
-def test_linear_gelu_gpu(rows, k, n, dtype):
+def test_linear_gelu_gpu(form, rows, k, n, dtype):
     torch.manual_seed(rows + n)
     x = (torch.randn(rows, k, device="cuda") * 0.5).to(dtype).requires_grad_()
     w = (torch.randn(n, k, device="cuda") / k ** 0.5).to(dtype).requires_grad_()
@@ -51,12 +79,12 @@ def test_linear_gelu_gpu(rows, k, n, dtype):
 
 
 @pytest.mark.gpu
-def test_gelu_bwd_bias_kernel_gpu():
+def test_gelu_bwd_bias_kernel_gpu(form):
     torch.manual_seed(5)
     h = torch.randn(3001, 1024, device="cuda").to(torch.bfloat16)
     dy = torch.randn_like(h)
     dh, db = gelu_bwd_bias(dy, h)
     hf = h.float().requires_grad_()
-    F.gelu(hf).backward(dy.float())
+    GL.gelu(hf).backward(dy.float())
     torch.testing.assert_close(dh.float(), hf.grad, rtol=1e-2, atol=1e-2)
     torch.testing.assert_close(db, dh.float().sum(0), rtol=1e-4, atol=1e-3)

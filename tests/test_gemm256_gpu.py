@@ -9,14 +9,23 @@ def _rel(a, b):
     return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
 
 
+@pytest.fixture(params=["tanh", "erf"], autouse=True)
+def gelu_form(request):
+    from fluxmpi_amd.ops import gelu as GL
+    old = GL.FORM
+    GL.set_form(request.param)
+    yield request.param
+    GL.set_form(old)
+
+
 def _gelu_ref(h):
-    return torch.nn.functional.gelu(h.float())
+    from fluxmpi_amd.ops import gelu as GL
+    return GL.gelu(h.float())
 
 
 def _gelu_grad_ref(h):
-    hf = h.float()
-    cdf = 0.5 * (1 + torch.erf(hf * 0.7071067811865476))
-    return cdf + hf * torch.exp(-0.5 * hf * hf) * 0.3989422804014327
+    from fluxmpi_amd.ops import gelu as GL
+    return GL._gelu_grad_ref(h.float())
 
 
 @pytest.mark.parametrize("m,n,k", [(512, 768, 768), (768, 256, 3072), (256, 512, 520), (1024, 2304, 768)])

@@ -11,6 +11,8 @@ import pytest
 import torch
 import torch.nn.functional as F
 
+from fluxmpi_amd.ops.gelu import gelu
+
 pytestmark = pytest.mark.gpu
 
 
@@ -35,7 +37,7 @@ def _plain_forward(P, x, depth, heads, patch=16):
         a = att.transpose(1, 2).reshape(n, -1, d)
         z = z + F.linear(a, P[p + "proj.weight"], P[p + "proj.bias"])
         y = F.layer_norm(z, (d,), P[p + "ln2.weight"], P[p + "ln2.bias"], 1e-6)
-        g = F.gelu(F.linear(y, P[p + "fc1.weight"], P[p + "fc1.bias"]))
+        g = gelu(F.linear(y, P[p + "fc1.weight"], P[p + "fc1.bias"]))  # the model's GELU form
         z = z + F.linear(g, P[p + "fc2.weight"], P[p + "fc2.bias"])
     cl = F.layer_norm(z[:, 0], (d,), P["ln.weight"], P["ln.bias"], 1e-6)
     return F.linear(cl, P["head.weight"], P["head.bias"])
