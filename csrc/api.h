@@ -313,6 +313,8 @@ void gelu_bwd_bias(const void* dy, const void* h, void* dh, float* partials, int
 // GELU form of the fused GELU kernels (gelu_bwd_bias, gemm256 EPI 1 / 2): 1 tanh (NNlib's `gelu`,
 // the default), 0 exact erf. Host-side switch read at launch.
 void gelu_set_form(int tanh_form);
+// g = gelu(h) (the selected form) over n bf16 / fp16 elements, n % 8 == 0, 16-B aligned
+void gelu_fwd(const void* h, void* g, int64_t n, int dtype, hipStream_t stream);
 int gelu_form();
 
 }  // namespace fluxmpi

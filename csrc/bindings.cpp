@@ -322,6 +322,9 @@ PYBIND11_MODULE(_C, m) {
   });
 
   m.def("gelu_set_form", &gelu_set_form);
+  m.def("gelu_fwd", [](uintptr_t h, uintptr_t g, int64_t n, int dtype, uintptr_t stream) {
+    gelu_fwd(reinterpret_cast<const void*>(h), reinterpret_cast<void*>(g), n, dtype, S(stream));
+  });
   m.def("gelu_form", &gelu_form);
 
   // ---- fused LayerNorm ------------------------------------------------------

@@ -23,6 +23,7 @@ FORM = os.environ.get("FLUXMPI_GELU", "tanh").lower()
 if FORM not in ("tanh", "erf"):
     raise ValueError(f"FLUXMPI_GELU must be 'tanh' or 'erf' (got {FORM!r})")
 _synced = [None]  # form last pushed to the extension
+_FWD_NATIVE = os.environ.get("FLUXMPI_GELU_FWD", "hip") != "torch"  # A/B: "torch" = F.gelu
 
 
 def set_form(form: str) -> None:
@@ -40,6 +41,20 @@ def _approx() -> str:
 def gelu(h: torch.Tensor) -> torch.Tensor:
     """GELU of the selected form (PyTorch composition)."""
     return F.gelu(h, approximate=_approx())
+
+
+def _gelu_fwd(h: torch.Tensor) -> torch.Tensor:
+    """``gelu(h)`` without autograd: the HIP kernel (``gelu.hip`` gelu_fwd) for contiguous bf16 /
+    fp16 CUDA tensors, else PyTorch."""
+    if (_FWD_NATIVE and h.is_cuda and h.dtype in (torch.bfloat16, torch.float16) and h.is_contiguous()
+            and h.numel() % 8 == 0):
+        C = _ext.get(required=True)
+        _sync(C)
+        g = torch.empty_like(h)
+        C.gelu_fwd(h.data_ptr(), g.data_ptr(), h.numel(), DTYPE_CODE[h.dtype],
+                   torch.cuda.current_stream(h.device).cuda_stream)
+        return g
+    return gelu(h)
 
 
 def _sync(C) -> None:
@@ -118,7 +133,7 @@ class _LinearGeluFn(torch.autograd.Function):
             h, g = h2.view(*x.shape[:-1], n_out), g2.view(*x.shape[:-1], n_out)
         else:
             h = F.linear(x, weight, bias)
-            g = gelu(h)
+            g = _gelu_fwd(h)
         ctx.save_for_backward(x, weight, h)
         ctx.has_bias = bias is not None
         ctx.bias_dtype = bias.dtype if bias is not None else None

@@ -88,3 +88,15 @@ def test_gelu_bwd_bias_kernel_gpu(form):
     GL.gelu(hf).backward(dy.float())
     torch.testing.assert_close(dh.float(), hf.grad, rtol=1e-2, atol=1e-2)
     torch.testing.assert_close(db, dh.float().sum(0), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [8, 4096 * 8 + 8, 50432 * 3072])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_gelu_fwd_kernel_gpu(gpu_ext, form, n, dtype):
+    torch.manual_seed(n % 97)
+    h = (torch.randn(n, device="cuda") * 3).to(dtype)
+    g = GL._gelu_fwd(h)
+    ref = GL.gelu(h.float())
+    torch.testing.assert_close(g.float(), ref, rtol=1e-2, atol=1e-2)
+    assert float((g.float() - ref).abs().max()) < 2e-2
