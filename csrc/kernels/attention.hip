@@ -957,7 +957,8 @@ __global__ __launch_bounds__(1024) void attn_bwd_dq_res_kernel(AttnBwdArgs a) {
   if (a.colpart != nullptr) colpart_store(colpart_row(a, b, h, part, w, 0), acc, a.scale, qok);
 }
 
-template <int NT>
+// PIPE (NT > 0 only): explicit software pipeline of the k-steps (FLUXMPI_ATTN_DKV_PIPE)
+template <int NT, int PIPE = 0>
 __global__ __launch_bounds__(1024) void attn_bwd_dkv_res_kernel(AttnBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int TV = (a.T + 31) & ~31;
@@ -1022,7 +1023,64 @@ __global__ __launch_bounds__(1024) void attn_bwd_dkv_res_kernel(AttnBwdArgs a) {
       accK[dt] = mfma(img_tr(qimg, 32 * ks, 16 * dt), db, accK[dt]);
     }
   };
-  if constexpr (NT > 0) {  // compile-time trip count: fully unrolled, next k-step's reads hoisted
+  if constexpr (NT > 0 && PIPE) {
+    // explicit pipeline: a k-step's row fragments are reloaded for the next k-step as soon as its
+    // S / dP MFMAs have read them, its transposed fragments are issued before the softmax VALU,
+    // so the LDS latency hides behind the VALU and the other half's MFMAs
+    constexpr int KS = (NT + 1) / 2;
+    bf16x8 fr[2][4];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int row = 16 * half + col;
+      fr[half][0] = img_row(qimg, row, g);
+      fr[half][1] = img_row(qimg, row, 4 + g);
+      fr[half][2] = img_row(gimg, row, g);
+      fr[half][3] = img_row(gimg, row, 4 + g);
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      f32x4 sv[2], dp[2];
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        sv[half] = mfma(fr[half][0], kf[0], f32x4{0.f, 0.f, 0.f, 0.f});
+        sv[half] = mfma(fr[half][1], kf[1], sv[half]);
+        dp[half] = mfma(fr[half][2], vf[0], f32x4{0.f, 0.f, 0.f, 0.f});
+        dp[half] = mfma(fr[half][3], vf[1], dp[half]);
+        if (ks + 1 < KS) {
+          const int row = 32 * (ks + 1) + 16 * half + col;
+          fr[half][0] = img_row(qimg, row, g);
+          fr[half][1] = img_row(qimg, row, 4 + g);
+          fr[half][2] = img_row(gimg, row, g);
+          fr[half][3] = img_row(gimg, row, 4 + g);
+        }
+      }
+      bf16x8 tg[4], tq[4];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        tg[dt] = img_tr(gimg, 32 * ks, 16 * dt);
+        tq[dt] = img_tr(qimg, 32 * ks, 16 * dt);
+      }
+      f32x4 p[2], dsv[2];
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const float4 lv = *reinterpret_cast<const float4*>(sL + 32 * ks + 16 * half + 4 * g);
+        const float4 dv = *reinterpret_cast<const float4*>(sD + 32 * ks + 16 * half + 4 * g);
+        const float lq[4] = {lv.x, lv.y, lv.z, lv.w}, dq[4] = {dv.x, dv.y, dv.z, dv.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = fast_exp2(fmaf(sv[half][r], c2, -lq[r]));  // padded query: lse = +inf -> 0
+          p[half][r] = pv;
+          dsv[half][r] = pv * (dp[half][r] - dq[r]);
+        }
+      }
+      const bf16x8 pb = pack(p[0], p[1]), db = pack(dsv[0], dsv[1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        accV[dt] = mfma(tg[dt], pb, accV[dt]);
+        accK[dt] = mfma(tq[dt], db, accK[dt]);
+      }
+    }
+  } else if constexpr (NT > 0) {  // compile-time trip count: fully unrolled, next k-step's reads hoisted
 #pragma unroll
     for (int ks = 0; ks < (NT + 1) / 2; ++ks) kstep(ks);
   } else {
@@ -1386,6 +1444,15 @@ void attn_fwd_pers_kernel_attr(const void* k) {
 }
 
 // FLUXMPI_ATTN_GENERIC=1: the runtime-tile-count kernels for every T (A/B of the NT = 13 instances)
+// explicitly pipelined dkv k-steps for the compile-time-tile-count kernel (FLUXMPI_ATTN_DKV_PIPE=0: off)
+bool dkv_pipe() {
+  static const bool on = [] {
+    const char* e = std::getenv("FLUXMPI_ATTN_DKV_PIPE");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+
 bool attn_generic() {
   static const bool on = [] {
     const char* e = std::getenv("FLUXMPI_ATTN_GENERIC");
@@ -1493,7 +1560,7 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* o, const 
     a.colpart = colpart;  // [B * nblk * waves][3 * H * 64] (attn_bwd_colpart_rows), or nullptr
     const bool vit = tiles == 13 && !attn_generic();  // T 193..208 (ViT: 197): compile-time tile count
     auto kdq = vit ? attn_bwd_dq_res_kernel<13> : attn_bwd_dq_res_kernel<0>;
-    auto kdkv = vit ? attn_bwd_dkv_res_kernel<13> : attn_bwd_dkv_res_kernel<0>;
+    auto kdkv = !vit ? attn_bwd_dkv_res_kernel<0> : (dkv_pipe() ? attn_bwd_dkv_res_kernel<13, 1> : attn_bwd_dkv_res_kernel<13, 0>);
     kdq<<<static_cast<unsigned>(bh), waves * 64, static_cast<size_t>(TV + TP) * 128, s>>>(a);
     FLUXMPI_HIP_CHECK(hipGetLastError());
     kdkv<<<static_cast<unsigned>(bh), waves * 64, static_cast<size_t>(2 * TV) * 128 + 2 * TV * 4,
