@@ -312,6 +312,9 @@ void gelu_bwd_bias(const void* dy, const void* h, void* dh, float* partials, int
                    int dtype, hipStream_t stream);
 // GELU form of the fused GELU kernels (gelu_bwd_bias, gemm256 EPI 1 / 2): 1 tanh (NNlib's `gelu`,
 // the default), 0 exact erf. Host-side switch read at launch.
+// The comm stream waits for the work enqueued on src so far, through a pooled event without the
+// system-scope fence (comm/fence.cpp)
+void stream_fence(hipStream_t src, hipStream_t dst);
 void gelu_set_form(int tanh_form);
 // g = gelu(h) (the selected form) over n bf16 / fp16 elements, n % 8 == 0, 16-B aligned
 void gelu_fwd(const void* h, void* g, int64_t n, int dtype, hipStream_t stream);

@@ -321,6 +321,7 @@ PYBIND11_MODULE(_C, m) {
                   reinterpret_cast<float*>(part), blocks, rows, N, dtype, S(stream));
   });
 
+  m.def("stream_fence", [](uintptr_t src, uintptr_t dst) { stream_fence(S(src), S(dst)); });
   m.def("gelu_set_form", &gelu_set_form);
   m.def("gelu_fwd", [](uintptr_t h, uintptr_t g, int64_t n, int dtype, uintptr_t stream) {
     gelu_fwd(reinterpret_cast<const void*>(h), reinterpret_cast<void*>(g), n, dtype, S(stream));
