@@ -1,0 +1,8 @@
+#!/bin/bash
+# rd3ze: full GPU suite + smoke on the final round-3 tree (native-fence test added)
+source "$(dirname "$0")/gpu_lib.sh"
+rm -f "$OUT/steps.log" "$OUT/bench_results.jsonl"
+step pytest_gpu 600 1 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+step smoke 240 0 python -c "import __graft_entry__ as g; g.smoke()"
+step r50 300 0 python bench.py
+echo done

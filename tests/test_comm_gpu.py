@@ -77,6 +77,31 @@ def test_force_comm_bitwise_equal(gpu_ext, grad_mode, dtype):
         assert torch.equal(p, q)
 
 
+def test_force_comm_native_fence(gpu_ext, monkeypatch):
+    """The opt-in bucket fence (csrc/comm/fence.cpp, FLUXMPI_NATIVE_FENCE=1) orders the
+    comm stream after the backward kernels exactly like wait_stream: bitwise-equal training."""
+    _init()
+    from fluxmpi_amd import optimisers as O
+    from fluxmpi_amd.parallel import comm as CM
+    from fluxmpi_amd.parallel.ddp import DDP
+
+    monkeypatch.setattr(CM, "_NATIVE_FENCE", True)
+    m1, m2 = _mlp(1, torch.bfloat16), _mlp(1, torch.bfloat16)
+    kw = dict(bucket_mb=0.1, first_bucket_mb=0.05)
+    d1 = DDP(m1, O.Adam(1e-3), force_comm=True, **kw)
+    d2 = DDP(m2, O.Adam(1e-3), **kw)
+    assert isinstance(d1.comm, CM.RcclComm) and len(d1.buckets) >= 3
+    x, y = _data(torch.bfloat16)
+    for _ in range(4):
+        for d in (d1, d2):
+            F.mse_loss(d(x).float(), y.float()).backward()
+        d1.step()
+        d2.step()
+    torch.cuda.synchronize()
+    for p, q in zip(m1.parameters(), m2.parameters()):
+        assert torch.equal(p, q)
+
+
 def test_force_comm_bench_construction(gpu_ext):
     """bench.py's DDP construction at N>1: parameter + buffer broadcast (fp32 BN stats, int64
     step counters that the pack kernels cannot move) and a step, over real RCCL calls."""
