@@ -9,7 +9,7 @@ Here every collective is *device-direct* and *stream-ordered*:
 * :class:`RcclComm` — the native MI355X path. A C++ communicator
   (``csrc/comm/rccl_comm.cpp``) owns an ``ncclComm_t`` (RCCL over xGMI) that
   is bootstrapped from a unique id exchanged through the process-group store.
-  Collectives run on a dedicated high-priority HIP stream; the caller's
+  Collectives run on a dedicated HIP stream (normal priority: measured); the caller's
   stream is fenced with HIP events on both sides, so a blocking call never
   blocks the host and an ``async_op`` call returns a :class:`Work` that can
   be waited on later (the ``MPI_Request`` analogue).
@@ -38,6 +38,11 @@ from ..ops import _ext
 # ResNet-50 --force-comm, same box: 12.09k / 12.15k native vs 12.16k torch): the N=1 comm tax is
 # not the per-bucket event's release
 _NATIVE_FENCE = os.environ.get("FLUXMPI_NATIVE_FENCE", "0") == "1"
+# RcclComm's stream priority: 0 normal (default), -1 high (FLUXMPI_COMM_PRIORITY=-1). Measured
+# (rd3zh / rd3zi, ResNet-50 --force-comm, same boxes): the high-priority queue cost 1.0-2.9 % of
+# the step at N=1 against 0.25-0.5 % at normal priority, and with an emulated RCCL CU footprint
+# (--emulate-comm 64:300) normal priority exposed LESS comm time (0.010 vs 0.037 ms per step)
+_COMM_PRIORITY = int(os.environ.get("FLUXMPI_COMM_PRIORITY", "0"))
 
 
 class ReduceOp(enum.IntEnum):
@@ -486,9 +491,9 @@ class RcclComm(Communicator):
         uid = bootstrap_unique_id(C.rccl_unique_id, store, rank, size, tag)
         with torch.cuda.device(self.device):
             self._h = C.RcclComm(bytes(uid), rank, size, self.device.index)
-            # high priority: comm kernels should win the CU arbitration against
-            # the backward kernels they overlap with
-            self.stream = torch.cuda.Stream(self.device, priority=-1)
+            # normal priority by default: a high-priority queue slowed the overlapped
+            # backward more than it sped up the comm (see _COMM_PRIORITY)
+            self.stream = torch.cuda.Stream(self.device, priority=_COMM_PRIORITY)
         self.version = C.rccl_version()
 
     # --- helpers ---------------------------------------------------------------

@@ -22,7 +22,7 @@ for MI355X + RCCL over xGMI:
    all but ~3 MB of them overlapped with the rest of backward.
 3. **Backward/comm overlap.** A post-accumulate-grad hook per parameter counts
    down its bucket; a full bucket is allreduced immediately on the
-   communicator's high-priority HIP stream (fenced by an event recorded on
+   communicator's own HIP stream (fenced by an event recorded on
    the compute stream). Buckets are launched strictly in index order on every
    rank, so collectives can never be mismatched across ranks.
 4. **Fused optimiser.** ``step()`` waits per bucket and runs one fused
