@@ -75,6 +75,24 @@ def _gelu_form() -> str:
     return GL.FORM
 
 
+def selfcheck_or_code(FluxMPI, world: int, rank: int, dev):
+    """The device communicator's own report (RCCL: ncclCommCount / UserRank / CuDevice, stream
+    priority) checked against WORLD_SIZE / RANK / the pinned device: the dict on success, exit
+    code 4 on a mismatch (no number is reported from a communicator that is not what it claims)."""
+    from fluxmpi_amd.parallel import runtime
+    from fluxmpi_amd.parallel.selfcheck import CommSelfCheckError, comm_selfcheck
+
+    rep, ok = {}, 1
+    try:
+        rep = comm_selfcheck(runtime.device_comm(), world, rank, getattr(dev, "index", None))
+    except CommSelfCheckError as e:
+        print(f"bench.py: rank {rank}: communicator self-check failed: {e}", file=sys.stderr, flush=True)
+        ok = 0
+    if world > 1:  # every rank leaves together (a lone failing rank would hang the others' collectives)
+        ok = int(FluxMPI.allreduce(torch.tensor([ok], dtype=torch.int64), min).item())
+    return rep if ok else 4
+
+
 def main():
     args = parse()
     if args.image is None:
@@ -143,6 +161,9 @@ def main():
               "communicator; refusing to report an N>1 number (use --same-device for a rehearsal)",
               file=sys.stderr)
         return 3
+    comm_report = selfcheck_or_code(FluxMPI, world, rank, dev)
+    if isinstance(comm_report, int):
+        return comm_report
     rule = O.Adam(1e-3) if args.optimizer == "adam" else O.Momentum(0.1, 0.9)
     ddp = DDP(model, rule, average=True, overlap=not args.no_overlap, force_comm=args.force_comm)
 
@@ -198,7 +219,11 @@ def main():
     torch.cuda.synchronize()
     FluxMPI.barrier()
     dt = time.perf_counter() - t0
-    dt_max = FluxMPI.allreduce(torch.tensor([dt], dtype=torch.float64), max).item() if world > 1 else dt
+    if world > 1:
+        per_rank = [float(v) for v in FluxMPI.allgather(torch.tensor([dt], dtype=torch.float64)).flatten()]
+    else:
+        per_rank = [dt]
+    dt_max = max(per_rank)
     lval = float(loss.item())
     exposed = None
     if ddp.communicate and not args.graph:
@@ -241,6 +266,11 @@ def main():
                        **cs, "exposed_comm_ms": None if exposed is None else round(exposed, 3),
                        **({"emulate_comm": args.emulate_comm} if args.emulate_comm else {}),
                        "grid_rounds": int(os.environ.get("FLUXMPI_GRID_ROUNDS", "1")),
+                       # the communicator's own report (checked against the launch before timing)
+                       # and the per-rank spread of the timed region
+                       **comm_report,
+                       "rank_ms_per_step_min": round(1000 * min(per_rank) / args.steps, 3),
+                       "rank_ms_per_step_max": round(1000 * max(per_rank) / args.steps, 3),
                        **({"gelu": _gelu_form()} if args.model == "vit_b16" else {}),
                        **({"deq_fwd_iters_per_step": round(sum(i[0] for i in timed_iters) / len(timed_iters), 2),
                            "deq_bwd_iters_per_step": round(sum(i[1] for i in timed_iters) / len(timed_iters), 2)}

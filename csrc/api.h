@@ -240,6 +240,17 @@ void gemm256_set_var(int v);  // main-loop schedule variant (gemm256.hip VAR bit
 void gemm256(const void* a, const void* b, void* c, void* c2, const void* bias, int bias_f32, const void* h,
              float* colpart, int64_t lda, int64_t ldb, int64_t ldc, int64_t M, int64_t N, int64_t K, bool b_t,
              int epi, hipStream_t stream);
+// Token-major Linear GEMM, both operands k-contiguous (gemm_nt.hip): C[M][N] = A[M][K] B[N][K]^T,
+// 256 x 256 tiles, ping-pong 8-wave schedule; epi 0 (+ bias), 1 (+ bias, C = h, C2 = gelu(h)),
+// 2 (C = bf16(acc) * gelu'(h), colpart[2 * M / 256][N] = per-half-tile column sums of C).
+bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc);
+int gemm_nt_colpart_rows(int64_t M);
+void gemm_nt(const void* a, const void* b, void* c, void* c2, const void* bias, int bias_f32, const void* h,
+             float* colpart, int64_t lda, int64_t ldb, int64_t ldc, int64_t M, int64_t N, int64_t K, int epi,
+             hipStream_t stream);
+// dst[c][r] = src[r][c], bf16 (rows, cols, leading dims multiples of 8)
+void transpose_bf16(const void* src, void* dst, int64_t rows, int64_t cols, int64_t lds, int64_t ldd,
+                    hipStream_t stream);
 
 // ---- Anderson-acceleration solver (DEQ) --------------------------------------------
 // X, F: fp32 histories [bsz][m rows of row_stride][d] (batch_stride between batches).

@@ -312,6 +312,19 @@ PYBIND11_MODULE(_C, m) {
             reinterpret_cast<void*>(c2), reinterpret_cast<const void*>(bias), bias_f32, reinterpret_cast<const void*>(h),
             reinterpret_cast<float*>(colpart), lda, ldb, ldc, M, N, K, b_t, epi, S(stream));
   });
+  m.def("gemm_nt_supported", &gemm_nt_supported);
+  m.def("gemm_nt_colpart_rows", &gemm_nt_colpart_rows);
+  m.def("gemm_nt", [](uintptr_t a, uintptr_t b, uintptr_t c, uintptr_t c2, uintptr_t bias, int bias_f32, uintptr_t h,
+                      uintptr_t colpart, int64_t lda, int64_t ldb, int64_t ldc, int64_t M, int64_t N, int64_t K,
+                      int epi, uintptr_t stream) {
+    gemm_nt(reinterpret_cast<const void*>(a), reinterpret_cast<const void*>(b), reinterpret_cast<void*>(c),
+            reinterpret_cast<void*>(c2), reinterpret_cast<const void*>(bias), bias_f32, reinterpret_cast<const void*>(h),
+            reinterpret_cast<float*>(colpart), lda, ldb, ldc, M, N, K, epi, S(stream));
+  });
+  m.def("transpose_bf16", [](uintptr_t src, uintptr_t dst, int64_t rows, int64_t cols, int64_t lds, int64_t ldd,
+                             uintptr_t stream) {
+    transpose_bf16(reinterpret_cast<const void*>(src), reinterpret_cast<void*>(dst), rows, cols, lds, ldd, S(stream));
+  });
   m.def("colsum", [](uintptr_t x, uintptr_t part, int blocks, int64_t rows, int64_t N, int dtype, uintptr_t stream) {
     colsum(reinterpret_cast<const void*>(x), reinterpret_cast<float*>(part), blocks, rows, N, dtype, S(stream));
   });
@@ -413,6 +426,9 @@ PYBIND11_MODULE(_C, m) {
       .def("allgather", &RcclComm::allgather, py::call_guard<py::gil_scoped_release>())
       .def("reduce_scatter", &RcclComm::reduce_scatter, py::call_guard<py::gil_scoped_release>())
       .def("alltoall", &RcclComm::alltoall, py::call_guard<py::gil_scoped_release>())
+      .def("comm_count", &RcclComm::comm_count, py::call_guard<py::gil_scoped_release>())
+      .def("comm_user_rank", &RcclComm::comm_user_rank, py::call_guard<py::gil_scoped_release>())
+      .def("comm_device", &RcclComm::comm_device, py::call_guard<py::gil_scoped_release>())
       .def("async_error", &RcclComm::async_error, py::call_guard<py::gil_scoped_release>())
       .def_static("error_string", &RcclComm::error_string)
       .def("abort", &RcclComm::abort, py::arg("abort_wait_ms") = 2000, py::call_guard<py::gil_scoped_release>())

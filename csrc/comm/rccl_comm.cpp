@@ -132,6 +132,27 @@ void RcclComm::reduce(uintptr_t send, uintptr_t recv, size_t count, int dtype, i
   check_not_aborted();
 }
 
+int RcclComm::comm_count() {
+  Lock lk(mu_);
+  int n = -1;
+  RCCL_CHECK(ncclCommCount(open_comm(), &n));
+  return n;
+}
+
+int RcclComm::comm_user_rank() {
+  Lock lk(mu_);
+  int r = -1;
+  RCCL_CHECK(ncclCommUserRank(open_comm(), &r));
+  return r;
+}
+
+int RcclComm::comm_device() {
+  Lock lk(mu_);
+  int d = -1;
+  RCCL_CHECK(ncclCommCuDevice(open_comm(), &d));
+  return d;
+}
+
 void RcclComm::allgather(uintptr_t send, uintptr_t recv, size_t sendcount, int dtype, uintptr_t stream) {
   Lock lk(mu_);
   ncclComm_t c = open_comm();

@@ -39,6 +39,11 @@ class RcclComm {
   void allgather(uintptr_t send, uintptr_t recv, size_t sendcount, int dtype, uintptr_t stream);
   void reduce_scatter(uintptr_t send, uintptr_t recv, size_t recvcount, int dtype, int op, uintptr_t stream);
   void alltoall(uintptr_t send, uintptr_t recv, size_t count_per_peer, int dtype, uintptr_t stream);
+  // what the communicator itself reports (ncclCommCount / ncclCommUserRank / ncclCommCuDevice):
+  // bench.py checks them against WORLD_SIZE / RANK / the pinned device before timing
+  int comm_count();
+  int comm_user_rank();
+  int comm_device();
   int async_error();
   static std::string error_string(int code);
   void abort(int abort_wait_ms = 2000);

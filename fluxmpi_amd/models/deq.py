@@ -233,6 +233,7 @@ class SolverGraphs:
         self.rbuf = self.rmin = None
         self.g_fwd = self.g_state = self.g_adj = None
         self.state = self.z0 = self.grad = self.u = self.thresh2 = self.dmax = self.done = None
+        self.gen = 0  # forward_state calls so far (a hook whose generation is stale goes eager)
         self.chunk = 0
 
     def history(self, m: int):
@@ -287,9 +288,14 @@ class SolverGraphs:
             self.g_adj = g
             self.chunk = chunk
 
-    def forward_state(self, z: torch.Tensor) -> None:
+    def forward_state(self, z: torch.Tensor) -> int:
+        """Record the adjoint's forward state at ``z`` (and the static ``x``); returns the
+        generation a later :meth:`adjoint` call must match (another forward at this shape before
+        that backward overwrites the static buffers)."""
         self.z0.copy_(z)
         self.g_state.replay()
+        self.gen += 1
+        return self.gen
 
     def adjoint(self, cell, grad: torch.Tensor, tol: float, max_iter: int, lag: int):
         """Solve ``u = J^T u + grad`` by replays of the adjoint graph; returns ``(u, iterations)``."""
@@ -366,9 +372,16 @@ class DEQFixedPoint(nn.Module):
         if gs is not None:
             if gs.g_adj is None:
                 gs.capture_adjoint(self.f, z.detach(), max(1, min(GRAPH_CHUNK, self.bwd_iter)))
-            gs.forward_state(z.detach())
+            gen = gs.forward_state(z.detach())
+            z_star, x_in = z.detach(), x.detach()
 
             def graphed_hook(grad):
+                if gs.gen != gen:
+                    # another forward at this shape ran before this backward (two micro-batches in
+                    # one loss, a weight-shared DEQ applied twice): the graphs' static state is
+                    # the later call's, so this adjoint runs eagerly on its own state
+                    _, state = self.f.forward_state(z_star, x_in)
+                    return self._adjoint_loop(grad, lambda u, g: self.f.adjoint_step(state, u, g), z_star)
                 lag = CHECK_LAG if self.check_lag is None else int(self.check_lag)
                 u, self.last_bwd_iters = gs.adjoint(self.f, grad, self.bwd_tol, self.bwd_iter, lag)
                 return u
@@ -396,34 +409,38 @@ class DEQFixedPoint(nn.Module):
                 return AO.adjoint_step(vjp(u), g, u)
 
         def backward_hook(grad):
-            lag = (CHECK_LAG if self.check_lag is None else int(self.check_lag)) if grad.is_cuda else 0
-            flags = LaggedFlags(lag, self.bwd_iter) if lag > 0 else None
-            thresh = self.bwd_tol * (grad.norm() + 1e-9)  # device scalar, computed once
-            thresh2 = thresh * thresh
-            if z0.dim() == 4 and z0.is_contiguous(memory_format=torch.channels_last):
-                # the incoming gradient (from the BatchNorm after the DEQ) may be NCHW: one layout
-                # copy here instead of one per iteration in the cell's NHWC GroupNorm backward
-                grad = grad.contiguous(memory_format=torch.channels_last)
-            u = grad
-            it = 0
-            for it in range(self.bwd_iter):  # u = J^T u + grad
-                u_new, ss = step(u, grad)
-                done = ss <= thresh2
-                u = u_new
-                if flags is None:
-                    if bool(done):
-                        break
-                else:  # lagged test: a converged adjoint keeps contracting for <= lag more steps
-                    flags.push(it, done)
-                    hit = flags.pop_ready()
-                    if hit is not None and hit[1] > 0.5:
-                        break
-            self.last_bwd_iters = it + 1
-            return u
+            return self._adjoint_loop(grad, step, z0)
 
         if z.requires_grad:
             z.register_hook(backward_hook)
         return z
+
+    def _adjoint_loop(self, grad, step, z0):
+        """Eager adjoint fixed point ``u = J^T u + grad`` (``step(u, grad) -> (u_new, |u_new - u|^2)``)."""
+        lag = (CHECK_LAG if self.check_lag is None else int(self.check_lag)) if grad.is_cuda else 0
+        flags = LaggedFlags(lag, self.bwd_iter) if lag > 0 else None
+        thresh = self.bwd_tol * (grad.norm() + 1e-9)  # device scalar, computed once
+        thresh2 = thresh * thresh
+        if z0.dim() == 4 and z0.is_contiguous(memory_format=torch.channels_last):
+            # the incoming gradient (from the BatchNorm after the DEQ) may be NCHW: one layout
+            # copy here instead of one per iteration in the cell's NHWC GroupNorm backward
+            grad = grad.contiguous(memory_format=torch.channels_last)
+        u = grad
+        it = 0
+        for it in range(self.bwd_iter):  # u = J^T u + grad
+            u_new, ss = step(u, grad)
+            done = ss <= thresh2
+            u = u_new
+            if flags is None:
+                if bool(done):
+                    break
+            else:  # lagged test: a converged adjoint keeps contracting for <= lag more steps
+                flags.push(it, done)
+                hit = flags.pop_ready()
+                if hit is not None and hit[1] > 0.5:
+                    break
+        self.last_bwd_iters = it + 1
+        return u
 
 
 class ResidualCell(nn.Module):

@@ -72,7 +72,9 @@ def attn_bwd_packed(qkv: torch.Tensor, out: torch.Tensor, dy: torch.Tensor, head
     C.attn_bwd(p, p + d * es, p + 2 * d * es, out.data_ptr(), dy.data_ptr(), g, g + d * es, g + 2 * d * es,
                stats.data_ptr(), t * d3, d3, t * d, d, 64, t * d, d, b, t, heads, 64, 0.125, _stream(qkv),
                part.data_ptr() if part is not None else 0)
-    _COLPART[0] = (weakref.ref(dqkv), part) if part is not None else None
+    # the version pins the values: autograd may accumulate a second gradient into dQKV in place
+    # (same pointer and size) before the projection's backward reads it
+    _COLPART[0] = (weakref.ref(dqkv), part, dqkv._version) if part is not None else None
     return dqkv
 
 
@@ -89,7 +91,7 @@ def take_colpart(grad: torch.Tensor):
         return None
     src = hit[0]()  # the dQKV tensor itself, still alive (no reuse of a freed address)
     if src is None or src.data_ptr() != grad.data_ptr() or src.numel() != grad.numel() \
-            or hit[1].shape[1] != grad.shape[-1]:
+            or hit[1].shape[1] != grad.shape[-1] or src._version != hit[2]:
         return None
     _COLPART[0] = None
     return hit[1]

@@ -121,6 +121,15 @@ def _T(x: torch.Tensor, v: float) -> float:
     return r
 
 
+def _eps(x: torch.Tensor, e: float) -> float:
+    """Optimisers.jl's ``_eps(T, ϵ)``: ``T(ϵ)``, except that a Float16 ϵ is floored at
+    ``Float16(1e-7)`` (a nonzero ϵ must not round to 0: ``Float16(1e-8) == 0`` would give
+    ``0 / (sqrt(0) + 0) = NaN`` on every element whose gradient has been zero so far)."""
+    if x.dtype == torch.float16:
+        return 0.0 if e == 0 else max(_T(x, 1e-7), _T(x, e))
+    return _T(x, e)
+
+
 # ------------------------------------------------------------------ rules
 class Descent(AbstractRule):
     def __init__(self, eta: float = 0.1):
@@ -199,7 +208,7 @@ class RMSProp(AbstractRule):
         return torch.zeros_like(x)
 
     def apply(self, acc, x, dx):
-        eta, rho, eps = _T(x, self.eta), _T(x, self.rho), _T(x, self.epsilon)
+        eta, rho, eps = _T(x, self.eta), _T(x, self.rho), _eps(x, self.epsilon)
         acc.mul_(rho).addcmul_(dx, dx, value=1 - rho)
         return acc, dx * eta / (torch.sqrt(acc) + eps)
 
@@ -213,7 +222,7 @@ class AdaGrad(AbstractRule):
 
     def apply(self, acc, x, dx):
         acc.addcmul_(dx, dx)
-        return acc, dx * _T(x, self.eta) / (torch.sqrt(acc) + _T(x, self.epsilon))
+        return acc, dx * _T(x, self.eta) / (torch.sqrt(acc) + _eps(x, self.epsilon))
 
 
 class Adam(AbstractRule):
@@ -227,7 +236,7 @@ class Adam(AbstractRule):
         return (torch.zeros_like(x), torch.zeros_like(x), (_T(x, self.beta[0]), _T(x, self.beta[1])))
 
     def apply(self, state, x, dx):
-        eta, b1, b2, eps = _T(x, self.eta), _T(x, self.beta[0]), _T(x, self.beta[1]), _T(x, self.epsilon)
+        eta, b1, b2, eps = _T(x, self.eta), _T(x, self.beta[0]), _T(x, self.beta[1]), _eps(x, self.epsilon)
         mt, vt, bt = state
         mt.mul_(b1).add_(dx, alpha=1 - b1)
         vt.mul_(b2).addcmul_(dx, dx, value=1 - b2)
@@ -263,7 +272,7 @@ def _adam_batch(rule: Adam, items, weight_decay: float):
         # CPU leaves: the same formulas as Adam.apply, term by term, as multi-tensor (foreach)
         # ops — one dispatch per term for the whole batch instead of ~10 per leaf
         x0 = items[idx[0]][1]
-        eta, b1, b2, eps = _T(x0, rule.eta), _T(x0, rule.beta[0]), _T(x0, rule.beta[1]), _T(x0, rule.epsilon)
+        eta, b1, b2, eps = _T(x0, rule.eta), _T(x0, rule.beta[0]), _T(x0, rule.beta[1]), _eps(x0, rule.epsilon)
         xs = [items[i][1] for i in idx]
         gs = [items[i][2] for i in idx]
         ms = [items[i][0].state[0] for i in idx]
@@ -293,7 +302,7 @@ def _adam_batch(rule: Adam, items, weight_decay: float):
         vs = [items[i][0].state[1] for i in idx]
         # hyperparameters rounded to the leaves' precision, as in Julia (``_T``)
         _fused.adam_(xs, gs, ms, vs, lr=_T(x0, rule.eta), beta1=_T(x0, rule.beta[0]), beta2=_T(x0, rule.beta[1]),
-                     eps=_T(x0, rule.epsilon), bc1=1.0 - bt[0], bc2=1.0 - bt[1],
+                     eps=_eps(x0, rule.epsilon), bc1=1.0 - bt[0], bc2=1.0 - bt[1],
                      weight_decay=_T(x0, weight_decay) if weight_decay else 0.0)
         for i in idx:
             leaf, x = items[i][0], items[i][1]

@@ -245,6 +245,11 @@ class Communicator:
     def alltoall(self, out: torch.Tensor, inp: torch.Tensor, async_op: bool = False):
         raise NotImplementedError
 
+    def self_report(self) -> dict:
+        """What the backend itself reports about the group (RCCL: rank count, rank, device);
+        empty for backends without such a query."""
+        return {}
+
     def barrier(self) -> None:
         raise NotImplementedError
 
@@ -495,6 +500,15 @@ class RcclComm(Communicator):
             # backward more than it sped up the comm (see _COMM_PRIORITY)
             self.stream = torch.cuda.Stream(self.device, priority=_COMM_PRIORITY)
         self.version = C.rccl_version()
+        self.priority = _COMM_PRIORITY
+
+    def self_report(self) -> dict:
+        """``ncclCommCount`` / ``ncclCommUserRank`` / ``ncclCommCuDevice`` of the live
+        communicator, the stream priority and the RCCL version (bench.py records and checks them)."""
+        h = self._handle()
+        return {"rccl_nranks": int(h.comm_count()), "rccl_rank": int(h.comm_user_rank()),
+                "rccl_device": int(h.comm_device()), "comm_priority": getattr(self, "priority", _COMM_PRIORITY),
+                "rccl_version": getattr(self, "version", None)}
 
     # --- helpers ---------------------------------------------------------------
     def _enter(self, *tensors):

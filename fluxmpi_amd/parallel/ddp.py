@@ -65,12 +65,15 @@ from . import runtime
 from .comm import Communicator, ReduceOp
 
 
-_ENGINES: "weakref.WeakKeyDictionary[torch.nn.Module, DDP]" = weakref.WeakKeyDictionary()
+# module -> weakref to its engine: the engine holds the module strongly, so a strong value here
+# would keep every engine ever built (model, flat buffers, masters, moments) alive for good
+_ENGINES: "weakref.WeakKeyDictionary[torch.nn.Module, weakref.ref]" = weakref.WeakKeyDictionary()
 
 
 def engine_for(module: torch.nn.Module) -> "DDP | None":
-    """The DDP engine managing ``module`` (None if there is none)."""
-    return _ENGINES.get(module)
+    """The DDP engine managing ``module`` (None if there is none, or it was discarded)."""
+    ref = _ENGINES.get(module)
+    return ref() if ref is not None else None
 
 
 @dataclass
@@ -223,7 +226,7 @@ class DDP:
         self._carry_hook = None
         self.collectives_launched = 0  # gradient-bucket allreduces issued so far
         self.pack_copies = 0  # gradients the bucket packs had to copy (not delivered in place)
-        _ENGINES[module] = self
+        _ENGINES[module] = weakref.ref(self)
         self.zero_grad()
         self.step_count = 0
         # exposed-communication timing (off by default: event timing costs a little)
@@ -351,11 +354,17 @@ class DDP:
                 self.comm.broadcast(b.flat_param, root_rank)
                 if b.master is not None:
                     self.comm.broadcast(b.master, root_rank)
-            bufs = [t for t in self.module.buffers() if t.numel() > 0]
-            if bufs:
+            # buffers and the parameters outside every bucket (requires_grad=False: a frozen
+            # backbone or embedding) — the reference's synchronize! reaches every leaf
+            bucketed = {id(p) for b in self.buckets for p in b.params}
+            rest, seen = [], set()
+            for t in list(self.module.parameters()) + list(self.module.buffers()):
+                if id(t) not in bucketed and id(t) not in seen and t.numel() > 0:
+                    seen.add(id(t))
+                    rest.append(t.detach())
+            if rest:
                 from .bucket import broadcast_tensors
-                broadcast_tensors([t.detach() for t in bufs], root_rank, comm=self.comm,
-                                  force_comm=self.force_comm)
+                broadcast_tensors(rest, root_rank, comm=self.comm, force_comm=self.force_comm)
         if hasattr(self, "_versions"):
             self._record_versions()  # params and masters were written together: nothing stale
 

@@ -107,3 +107,7 @@ def test_attn_bwd_colsum_partials(gpu_ext, b, t, heads):
     got = part.sum(0)
     # the partials sum the fp32 values before their bf16 rounding
     torch.testing.assert_close(got, ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item() / 10 + 1e-3)
+    # a gradient accumulated into dQKV in place (same pointer, same size) invalidates the hand-off
+    dqkv2 = attn_bwd_packed(xb, out, g, heads, stats)
+    dqkv2.add_(1.0)
+    assert take_colpart(dqkv2.view(b * t, -1)) is None

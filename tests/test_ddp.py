@@ -387,3 +387,48 @@ def worker_ddp_master_sync():
 
 def test_ddp_master_sync_gloo(spmd):
     spmd("tests.test_ddp:worker_ddp_master_sync", nprocs=2, timeout=120)
+
+
+def worker_ddp_frozen_param_sync():
+    """synchronize(model) of a DDP-managed model reaches the parameters outside every bucket
+    (requires_grad=False: a frozen layer) as the reference's synchronize! reaches every leaf."""
+    import fluxmpi_amd as FluxMPI
+    from fluxmpi_amd import optimisers as O
+    from fluxmpi_amd.parallel.ddp import DDP
+
+    FluxMPI.Init()
+    r = FluxMPI.local_rank()
+    model = _mlp(100 + r)  # different values per rank
+    frozen = next(iter(model.parameters()))
+    frozen.requires_grad_(False)
+    d = DDP(model, O.Descent(0.1), force_comm=True)
+    assert all(id(frozen) != id(p) for b in d.buckets for p in b.params)
+    with torch.no_grad():
+        frozen.fill_(float(r + 1))
+    FluxMPI.synchronize(model, root_rank=0)
+    g = FluxMPI.allgather(frozen.detach().clone())
+    assert torch.equal(g[0], g[1]) and float(g[1].flatten()[0]) == 1.0
+    FluxMPI.Finalize()
+
+
+def test_ddp_frozen_param_sync_gloo(spmd):
+    spmd("tests.test_ddp:worker_ddp_frozen_param_sync", nprocs=2, timeout=120)
+
+
+def test_engine_registry_does_not_keep_engines_alive():
+    """The module -> engine registry holds the engine weakly: a discarded DDP is collected."""
+    import gc
+    import weakref
+
+    import fluxmpi_amd as FluxMPI
+    from fluxmpi_amd import optimisers as O
+    from fluxmpi_amd.parallel.ddp import DDP, engine_for
+
+    FluxMPI.Init()
+    model = _mlp(3)
+    d = DDP(model, O.Descent(0.1))
+    assert engine_for(model) is d
+    ref = weakref.ref(d)
+    del d
+    gc.collect()
+    assert ref() is None and engine_for(model) is None

@@ -433,6 +433,32 @@ def test_deq_solver_graphs_match_eager(gpu_ext):
 
 
 @pytest.mark.gpu
+def test_deq_solver_graphs_two_forwards_one_backward(gpu_ext):
+    """loss = f(x1) + f(x2) at one shape: the second graphed forward overwrites the solver graphs'
+    static state before the first call's adjoint runs, so that adjoint must run on its own state
+    (generation check, deq.SolverGraphs.forward_state): graphed gradients == eager gradients."""
+    torch.manual_seed(11)
+    x1 = torch.randn(16, 1, 28, 28, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    x2 = torch.randn(16, 1, 28, 28, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (16,), device="cuda")
+    grads = []
+    for graphs in (False, True):
+        torch.manual_seed(3)
+        m = _deq_bf16(max_iter=13, tol=0.0, bwd_iter=12, bwd_tol=0.0)
+        m.deq.use_graphs = graphs
+        for _ in range(2):  # eager first call, then capture: the third call replays
+            F.cross_entropy(m(x1).float(), y).backward()
+            for p in m.parameters():
+                p.grad = None
+        loss = F.cross_entropy(m(x1).float(), y) + F.cross_entropy(m(x2).float(), y)
+        loss.backward()
+        grads.append([p.grad.float().clone() for p in m.parameters()])
+    for a, b in zip(*grads):
+        rel = float((b - a).norm() / a.norm().clamp_min(1e-12))
+        assert rel < 2e-2, rel
+
+
+@pytest.mark.gpu
 def test_deq_solver_graphs_early_exit(gpu_ext):
     """With a reachable tolerance the graphed solves stop within two periods of the eager ones
     (per-period, one-period-late tests) and land on the same fixed point."""

@@ -141,3 +141,60 @@ def worker_rccl_bootstrap():
 
 def test_rccl_bootstrap_cpu(spmd):
     spmd("tests.test_mpi_extensions:worker_rccl_bootstrap", nprocs=3, timeout=120)
+
+
+class _FakeRcclHandle:
+    """Stand-in for ``fluxmpi_amd._C.RcclComm``: reports a configurable rank count."""
+
+    def __init__(self, count, rank, device=0):
+        self._c, self._r, self._d = count, rank, device
+
+    def comm_count(self):
+        return self._c
+
+    def comm_user_rank(self):
+        return self._r
+
+    def comm_device(self):
+        return self._d
+
+
+def _stub_rccl(rank, size, count):
+    from fluxmpi_amd.parallel.comm import RcclComm
+
+    c = object.__new__(RcclComm)  # no HIP stream / RCCL init on the CPU: only the report path
+    c.rank, c.size, c.abort_reason = rank, size, None
+    c._h = _FakeRcclHandle(count, rank)
+    c.priority, c.version = 0, 22706
+    return c
+
+
+def worker_bench_selfcheck():
+    """bench.py's communicator self-check on 2 gloo ranks with a stubbed native communicator:
+    a rank count that is not WORLD_SIZE on ONE rank makes every rank return exit code 4 (no
+    number, no hang); the matching report passes and is what the JSON line records."""
+    import importlib.util
+    import os
+
+    import fluxmpi_amd as FluxMPI
+    from fluxmpi_amd.parallel import runtime
+
+    FluxMPI.Init()
+    r, W = FluxMPI.local_rank(), FluxMPI.total_workers()
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(os.path.dirname(__file__), "..", "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    real = runtime.device_comm
+    try:
+        runtime.device_comm = lambda: _stub_rccl(r, W, W if r == 0 else W - 1)  # rank 1 disagrees
+        assert bench.selfcheck_or_code(FluxMPI, W, r, None) == 4
+        runtime.device_comm = lambda: _stub_rccl(r, W, W)
+        rep = bench.selfcheck_or_code(FluxMPI, W, r, None)
+        assert rep["rccl_nranks"] == W and rep["rccl_rank"] == r and rep["comm_priority"] == 0
+    finally:
+        runtime.device_comm = real
+    FluxMPI.Finalize()
+
+
+def test_bench_comm_selfcheck_cpu(spmd):
+    spmd("tests.test_mpi_extensions:worker_bench_selfcheck", nprocs=2, timeout=120)

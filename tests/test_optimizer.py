@@ -110,6 +110,30 @@ def test_hyperparameters_cast_to_leaf_precision():
     st, x2 = O.update(st, x, g)
     b1, b2 = 0.89990234375, 0.9990234375
     m, v = (1 - b1) * 0.25, (1 - b2) * 0.0625
-    step = m / (1 - b1) / ((v / (1 - b2)) ** 0.5 + 0.0) * 0.5
+    eps16 = float(torch.tensor(1e-7, dtype=torch.float16))  # Optimisers.jl _eps(Float16, 1e-8)
+    step = m / (1 - b1) / ((v / (1 - b2)) ** 0.5 + eps16) * 0.5
     torch.testing.assert_close(x2.float(), torch.full((4,), 1.0 - step), rtol=2e-3, atol=2e-3)
     assert st.state[2] == (_T(x, b1 * b1), _T(x, b2 * b2))
+
+
+def test_fp16_adam_zero_gradient_is_finite():
+    """ϵ on fp16 leaves follows Optimisers.jl's ``_eps``: floored at Float16(1e-7), never 0, so
+    an element whose gradient has always been zero stays put instead of becoming NaN
+    (0 / (sqrt(0) + 0)); AdaGrad and RMSProp likewise. Eager and fused paths."""
+    import torch
+    from fluxmpi_amd import optimisers as O
+    from fluxmpi_amd.optimisers import _eps
+
+    hf = torch.zeros(2, dtype=torch.float16)
+    assert _eps(hf, 1e-8) == float(torch.tensor(1e-7, dtype=torch.float16)) > 0
+    assert _eps(hf, 0.0) == 0.0 and _eps(hf, 1e-3) == float(torch.tensor(1e-3, dtype=torch.float16))
+    assert _eps(torch.zeros(1, dtype=torch.bfloat16), 1e-8) == float(torch.tensor(1e-8, dtype=torch.bfloat16))
+    for rule in (O.Adam(1e-3), O.AdaGrad(0.1), O.RMSProp(1e-3)):
+        x = torch.ones(4, dtype=torch.float16)
+        g = torch.tensor([0.5, 0.0, -0.25, 0.0], dtype=torch.float16)
+        st = O.setup(rule, {"w": x})
+        for _ in range(3):
+            st, out = O.update(st, {"w": x}, {"w": g})
+            x = out["w"]
+        assert torch.isfinite(x).all(), (type(rule).__name__, x)
+        assert x[1] == 1.0 and x[3] == 1.0, (type(rule).__name__, x)
