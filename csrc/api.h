@@ -107,11 +107,6 @@ void bn_relu_maxpool_fwd(const void* x, const float* scale, const float* shift, 
 // y[p][0..3] = (x[p][0], x[p][1], x[p][2], 0) for npix 16-bit NHWC pixels (stem channel pad)
 void pad_c3_to_c4(const void* x, void* y, int64_t npix, int dtype, hipStream_t stream);
 
-// ---- 3x3 / stride-1 / pad-1 convolution over LDS image halos (conv3x3.hip)
-bool conv3x3_halo_supported(int64_t N, int H, int W, int C, int Co);
-void conv3x3_halo(const void* x, const void* w, void* y, float* stats, int64_t N, int H, int W, int C, int Co,
-                  hipStream_t stream);
-
 // ---- ResNet stem on MFMA (stem.hip): 7x7/2 conv of NHWC4 224x224 images + BN statistics;
 // the fused backward (pool gather + BN backward + filter gradient)
 void stem_fwd(const void* x, const void* wp, void* y, float* stats, int64_t n, hipStream_t stream);
@@ -124,8 +119,6 @@ void stem_bwd(const void* x, const void* c, const void* dp, const uint8_t* idx, 
 // strides (sq_b, sq_t; head stride 64), o has (so_b, so_t, so_h), dout (sg_b, sg_t; head stride
 // 64); stats is fp32 [B][H][T][2]: attn_fwd writes [..][0] = base-2 log-sum-exp of the scaled
 // scores, attn_bwd reads it and writes [..][1] = rowsum(dO*O).
-void attn_set_fwd_mode(int mode);   // -1 env, 0 two workgroups per head, 1 persistent (next head staged)
-void attn_set_bwd_fused(int mode);  // -1 env, 0 dq/dkv pair, 1 one-kernel (LDS atomics), 2 two-phase
 void attn_fwd(const void* q, const void* k, const void* v, void* o, float* stats, int64_t sq_b, int64_t sq_t,
               int64_t so_b, int64_t so_t, int64_t so_h, int B, int T, int H, int Dh, float scale, hipStream_t stream);
 void attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, void* dq, void* dk,
@@ -230,16 +223,6 @@ bool wgrad256_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ld
 int wgrad256_actual_splits(int64_t K, int splits);
 void gemm_wgrad256(const void* a, const void* b, float* ws, int64_t lda, int64_t ldb, int64_t M, int64_t N, int64_t K,
                    int splits, hipStream_t stream);
-// Token-major Linear GEMM on 256 x 256 tiles (gemm256.hip): C[M][N] = A[M][K] (b_t ? B[K][N] : B[N][K]^T)
-// with epilogue epi 0 (+ bias), 1 (+ bias, C = h, C2 = gelu(h)), 2 (C = bf16(acc) * gelu'(h),
-// colpart[2 * M / 256][N] = per-half-tile column sums of C; needs b_t).
-bool gemm256_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc, bool b_t);
-int gemm256_colpart_rows(int64_t M);
-void gemm256_set_bk(int bk);
-void gemm256_set_var(int v);  // main-loop schedule variant (gemm256.hip VAR bits); A/B runs  // pipeline depth variant (32: 4 x 32-deep stages, 64: 2 x 64-deep); A/B runs
-void gemm256(const void* a, const void* b, void* c, void* c2, const void* bias, int bias_f32, const void* h,
-             float* colpart, int64_t lda, int64_t ldb, int64_t ldc, int64_t M, int64_t N, int64_t K, bool b_t,
-             int epi, hipStream_t stream);
 // Token-major Linear GEMM, both operands k-contiguous (gemm_nt.hip): C[M][N] = A[M][K] B[N][K]^T,
 // 256 x 256 tiles, ping-pong 8-wave schedule; epi 0 (+ bias), 1 (+ bias, C = h, C2 = gelu(h)),
 // 2 (C = bf16(acc) * gelu'(h), colpart[2 * M / 256][N] = per-half-tile column sums of C).
@@ -321,11 +304,8 @@ void emulate_comm(int blocks, double microseconds, hipStream_t stream, int threa
 void colsum(const void* x, float* partials, int blocks, int64_t rows, int64_t N, int dtype, hipStream_t stream);
 void gelu_bwd_bias(const void* dy, const void* h, void* dh, float* partials, int blocks, int64_t rows, int64_t N,
                    int dtype, hipStream_t stream);
-// GELU form of the fused GELU kernels (gelu_bwd_bias, gemm256 EPI 1 / 2): 1 tanh (NNlib's `gelu`,
+// GELU form of the fused GELU kernels (gelu_bwd_bias, gemm_nt EPI 1 / 2): 1 tanh (NNlib's `gelu`,
 // the default), 0 exact erf. Host-side switch read at launch.
-// The comm stream waits for the work enqueued on src so far, through a pooled event without the
-// system-scope fence (comm/fence.cpp)
-void stream_fence(hipStream_t src, hipStream_t dst);
 void gelu_set_form(int tanh_form);
 // g = gelu(h) (the selected form) over n bf16 / fp16 elements, n % 8 == 0, 16-B aligned
 void gelu_fwd(const void* h, void* g, int64_t n, int dtype, hipStream_t stream);

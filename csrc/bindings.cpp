@@ -152,8 +152,6 @@ PYBIND11_MODULE(_C, m) {
              reinterpret_cast<void*>(o), reinterpret_cast<float*>(stats), sq_b, sq_t, so_b, so_t, so_h, B, T, H, Dh,
              scale, reinterpret_cast<hipStream_t>(stream));
   });
-  m.def("attn_set_bwd_fused", &attn_set_bwd_fused);
-  m.def("attn_set_fwd_mode", &attn_set_fwd_mode);
   m.def("attn_bwd", [](uintptr_t q, uintptr_t k, uintptr_t v, uintptr_t o, uintptr_t dout, uintptr_t dq,
                        uintptr_t dk, uintptr_t dv, uintptr_t stats, int64_t sq_b, int64_t sq_t, int64_t so_b,
                        int64_t so_t, int64_t so_h, int64_t sg_b, int64_t sg_t, int B, int T, int H, int Dh,
@@ -171,12 +169,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("pad_c3_to_c4", [](uintptr_t x, uintptr_t y, int64_t npix, int dtype, uintptr_t stream) {
     pad_c3_to_c4(reinterpret_cast<const void*>(x), reinterpret_cast<void*>(y), npix, dtype,
                  reinterpret_cast<hipStream_t>(stream));
-  });
-  m.def("conv3x3_halo_supported", &conv3x3_halo_supported);
-  m.def("conv3x3_halo", [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, int64_t N, int H, int W, int C,
-                           int Co, uintptr_t stream) {
-    conv3x3_halo(reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(w), reinterpret_cast<void*>(y),
-                 reinterpret_cast<float*>(stats), N, H, W, C, Co, reinterpret_cast<hipStream_t>(stream));
   });
   m.def("stem_fwd", [](uintptr_t x, uintptr_t wp, uintptr_t y, uintptr_t stats, int64_t n, uintptr_t stream) {
     stem_fwd(reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(wp), reinterpret_cast<void*>(y),
@@ -301,17 +293,6 @@ PYBIND11_MODULE(_C, m) {
     gemm_wgrad256(reinterpret_cast<const void*>(a), reinterpret_cast<const void*>(b), reinterpret_cast<float*>(ws), lda,
                   ldb, M, N, K, splits, S(stream));
   });
-  m.def("gemm256_supported", &gemm256_supported);
-  m.def("gemm256_colpart_rows", &gemm256_colpart_rows);
-  m.def("gemm256_set_bk", &gemm256_set_bk);
-  m.def("gemm256_set_var", &gemm256_set_var);
-  m.def("gemm256", [](uintptr_t a, uintptr_t b, uintptr_t c, uintptr_t c2, uintptr_t bias, int bias_f32, uintptr_t h,
-                      uintptr_t colpart, int64_t lda, int64_t ldb, int64_t ldc, int64_t M, int64_t N, int64_t K,
-                      bool b_t, int epi, uintptr_t stream) {
-    gemm256(reinterpret_cast<const void*>(a), reinterpret_cast<const void*>(b), reinterpret_cast<void*>(c),
-            reinterpret_cast<void*>(c2), reinterpret_cast<const void*>(bias), bias_f32, reinterpret_cast<const void*>(h),
-            reinterpret_cast<float*>(colpart), lda, ldb, ldc, M, N, K, b_t, epi, S(stream));
-  });
   m.def("gemm_nt_supported", &gemm_nt_supported);
   m.def("gemm_nt_colpart_rows", &gemm_nt_colpart_rows);
   m.def("gemm_nt", [](uintptr_t a, uintptr_t b, uintptr_t c, uintptr_t c2, uintptr_t bias, int bias_f32, uintptr_t h,
@@ -334,7 +315,6 @@ PYBIND11_MODULE(_C, m) {
                   reinterpret_cast<float*>(part), blocks, rows, N, dtype, S(stream));
   });
 
-  m.def("stream_fence", [](uintptr_t src, uintptr_t dst) { stream_fence(S(src), S(dst)); });
   m.def("gelu_set_form", &gelu_set_form);
   m.def("gelu_fwd", [](uintptr_t h, uintptr_t g, int64_t n, int dtype, uintptr_t stream) {
     gelu_fwd(reinterpret_cast<const void*>(h), reinterpret_cast<void*>(g), n, dtype, S(stream));

@@ -634,189 +634,6 @@ __global__ __launch_bounds__(1024) void attn_fwd_res_kernel(AttnBwdArgs a) {
   }
 }
 
-// MEASURED NO GAIN (rd3s, ViT-B/16 bs256, same box): 110.3 us per call vs 107.4 us for
-// attn_fwd_res_kernel, 6.96k / 6.96k img/s either way — the forward is not bound by its staging
-// (~9 us of CU time per head against ~1 us of MFMA and ~3 us of HBM traffic: the per-wave
-// LDS-read -> MFMA -> softmax chain at 3-4 waves per SIMD). Opt-in: FLUXMPI_ATTN_FWD=persist.
-// Persistent forward with the next head's staging in flight. attn_fwd_res_kernel's workgroup
-// stages its head, waits, computes, exits: with two workgroups per CU the staging of one only
-// partly hides behind the other's compute (the kernel ran at ~3 of its 104 KB per head per
-// 8.6 us per CU, latency-bound). Here one workgroup per CU (13 waves, the whole head) loops over
-// heads with two LDS image pairs: the LDS-DMA of head i+1's K and V is issued before head i is
-// computed, so HBM streams while the MFMAs run. Every thread issues exactly `per` DMA pieces per
-// head (duplicates of the last piece pad the count), so one counted vmcnt wait leaves exactly
-// the next head's pieces in flight; the LDS reads go through __restrict__ pointers (alias
-// scopes: the waitcnt pass would otherwise drain the prefetch before them).
-template <int PER>
-__device__ __forceinline__ void wait_pieces() {
-  __builtin_amdgcn_s_waitcnt((PER & 15) | ((PER >> 4) << 14) | (7 << 4) | (15 << 8));  // vmcnt(PER)
-}
-
-// The PER staging pieces of this thread, fixed for every head: the element offset of its 16-B
-// chunk inside a head's K or V ([T][64] rows at stride sq_t; -1: a padding row, read from the
-// zero line) and, wave-uniform, the piece index (LDS slot pc * 1024, V when pc >= TP / 8).
-// Computed once: recomputing them per head (or hoisting 64-bit addresses) spilled registers.
-template <int PER>
-struct KvPieces {
-  int32_t off[PER];
-  int pc[PER];
-};
-
-template <int PER>
-__device__ __forceinline__ KvPieces<PER> kv_pieces(const AttnBwdArgs& a, int TP, int TV) {
-  KvPieces<PER> p;
-  // wave-uniform in scalar registers (the piece index only selects the LDS slot and K / V)
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, nw = blockDim.x >> 6;
-  const int kp = TP / 8, np = kp + TV / 8;
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    int pc = wave + j * nw;
-    pc = pc < np ? pc : np - 1;  // padding: the last piece again (same bytes, same place)
-    const int row = 8 * (pc >= kp ? pc - kp : pc) + (lane >> 3);
-    const int chunk = (lane & 7) ^ swz_b(row);
-    p.pc[j] = __builtin_amdgcn_readfirstlane(pc);
-    p.off[j] = row < a.T ? static_cast<int32_t>(row * a.sq_t + chunk * 8) : -1;
-  }
-  return p;
-}
-
-// K (TP rows) then V (TV rows) of one head into an image pair: PER pieces per thread (a
-// compile-time count: the waitcnt pass then knows exactly how many are younger than a load)
-template <int PER>
-__device__ __forceinline__ void stage_kv(char* __restrict__ img, const KvPieces<PER>& p, const bf16* kb,
-                                         const bf16* vb, int kp) {
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const bf16* base = p.pc[j] >= kp ? vb : kb;
-    const void* src = p.off[j] >= 0 ? static_cast<const void*>(base + p.off[j])
-                                    : static_cast<const void*>(g_attn_zero);
-    typedef __attribute__((address_space(3))) char lds_char;
-    typedef __attribute__((address_space(1))) void gl_void;
-    __builtin_amdgcn_global_load_lds((gl_void*)(src), (lds_char*)(img + p.pc[j] * 1024), 16, 0, 0);
-  }
-}
-
-template <int PER>
-__global__ __launch_bounds__(1024) void attn_fwd_pers_kernel(AttnBwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int TP = (a.T + 15) & ~15, TV = (a.T + 31) & ~31;
-  const int pair = (TP + TV) * 128;
-  const int total = a.B * a.H;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, col = lane & 15, g = lane >> 4;
-  const int q0 = 16 * w, qi = q0 + col;
-  const bool qok = qi < a.T;
-  const int qrow = qok ? qi : 0;  // loads stay unconditional (a valid row), zeroed below
-  const float c2 = a.scale * kLog2e;
-  const int nt = TP / 16;
-  auto row_frag = [&](const char* __restrict__ img, int row, int ch) {
-    return *reinterpret_cast<const bf16x8*>(img + row * 128 + ((ch ^ swz_b(row)) << 4));
-  };
-  auto tr_frag = [&](const char* __restrict__ img, int r0, int c0) {
-    const int q = (lane >> 2) & 3, p = lane & 3;
-    const int ra = r0 + 4 * g + q, rb = ra + 16;
-    const int ch = (c0 >> 3) + (p >> 1);
-    typedef short short4v __attribute__((ext_vector_type(4)));
-    typedef __attribute__((address_space(3))) short4v lds_short4v;
-    short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lds_short4v*)(img + ra * 128 + ((ch ^ swz_b(ra)) << 4) + (p & 1) * 8));
-    short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lds_short4v*)(img + rb * 128 + ((ch ^ swz_b(rb)) << 4) + (p & 1) * 8));
-    bf16x8 out;
-    __builtin_memcpy(&out, &lo, 8);
-    __builtin_memcpy(reinterpret_cast<char*>(&out) + 8, &hi, 8);
-    return out;
-  };
-  const KvPieces<PER> pcs = kv_pieces<PER>(a, TP, TV);
-  const int kp = TP / 8;
-  auto kbase = [&](int head) { return a.k + (head / a.H) * a.sq_b + (head % a.H) * DH; };
-  auto vbase = [&](int head) { return a.v + (head / a.H) * a.sq_b + (head % a.H) * DH; };
-  int cur = blockIdx.x;
-  stage_kv<PER>(smem, pcs, kbase(cur), vbase(cur), kp);
-  for (int it = 0; cur < total; ++it, cur += gridDim.x) {  // grid <= total: every workgroup has a head
-    const int b = cur / a.H, h = cur % a.H;
-    const char* kimg = smem + (it & 1) * pair;
-    const char* vimg = kimg + TP * 128;
-    const int64_t qoff = b * a.sq_b + static_cast<int64_t>(qrow) * a.sq_t + h * DH;
-    bf16x8 qf[2];
-    qf[0] = ld8(a.q + qoff + 8 * g);
-    qf[1] = ld8(a.q + qoff + 32 + 8 * g);
-    // every wave is done with the other image pair (the previous head): refill it
-    __builtin_amdgcn_s_barrier();
-    // unconditional (past the last head: a dummy refill of the idle pair, never read), so every
-    // path has the same PER younger loads and the waitcnt pass keeps this wait counted
-    const int nxt = cur + gridDim.x < total ? cur + gridDim.x : cur;
-    stage_kv<PER>(smem + ((it + 1) & 1) * pair, pcs, kbase(nxt), vbase(nxt), kp);
-    wait_pieces<PER>();  // all but the next head's pieces: this head's images, Q
-    __builtin_amdgcn_s_barrier();  // every thread's pieces of this head have landed
-    // (a padded query lane computes on row 0's Q: its column of S, P and O is never stored)
-    if (q0 < a.T) {  // wave-uniform
-      f32x4 x[kResMaxT / 16];
-      float m = -kInf;
-#pragma unroll
-      for (int kt = 0; kt < kResMaxT / 16; ++kt) {
-        x[kt] = f32x4{-kInf, -kInf, -kInf, -kInf};
-        if (kt < nt) {
-          const int row = 16 * kt + col;
-          f32x4 sacc = {};
-          sacc = mfma(row_frag(kimg, row, g), qf[0], sacc);
-          sacc = mfma(row_frag(kimg, row, 4 + g), qf[1], sacc);
-          if (16 * kt + 16 <= a.T) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              x[kt][r] = sacc[r] * c2;
-              m = fmaxf(m, x[kt][r]);
-            }
-          } else {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int key = 16 * kt + 4 * g + r;
-              x[kt][r] = key < a.T ? sacc[r] * c2 : -kInf;
-              m = fmaxf(m, x[kt][r]);
-            }
-          }
-        }
-      }
-      m = xor_max<32>(xor_max<16>(m));
-      float l = 0.f;
-#pragma unroll
-      for (int kt = 0; kt < kResMaxT / 16; ++kt) {
-        if (kt < nt) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float pv = fast_exp2(x[kt][r] - m);
-            x[kt][r] = pv;
-            l += pv;
-          }
-        } else {
-          x[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-      }
-      l = butterfly_from<16>(l);
-      f32x4 acc[4] = {};
-#pragma unroll
-      for (int ks = 0; ks < kResMaxT / 32; ++ks) {
-        if (32 * ks < TV) {
-          const bf16x8 bop = pack(x[2 * ks], x[2 * ks + 1]);
-#pragma unroll
-          for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma(tr_frag(vimg, 32 * ks, 16 * dt), bop, acc[dt]);
-        }
-      }
-      if (qok) {
-        const float inv = 1.f / l;
-        bf16* op = a.o_out + b * a.so_b + static_cast<int64_t>(qi) * a.so_t + h * a.so_h;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-          const bf16x4 o = {(bf16)(acc[dt][0] * inv), (bf16)(acc[dt][1] * inv), (bf16)(acc[dt][2] * inv),
-                            (bf16)(acc[dt][3] * inv)};
-          *reinterpret_cast<bf16x4*>(op + dt * 16 + 4 * g) = o;
-        }
-        if (g == 0) a.stats[((static_cast<int64_t>(b) * a.H + h) * a.T + qi) * 2] = m + __log2f(l);
-      }
-    }
-  }
-  wait_pieces<0>();  // the last (dummy) refill has landed before the workgroup's LDS is released
-}
-
 // Backward with the head resident (T <= 256), two kernels like the blocked pair above:
 //   attn_bwd_dq_res   K, V images; one wave per 16 queries: D = rowsum(dO * O) (written to
 //                     stats[.., 1] for the next kernel), S^T = K Q^T, dP^T = V dO^T,
@@ -1103,346 +920,6 @@ __global__ __launch_bounds__(1024) void attn_bwd_dkv_res_kernel(AttnBwdArgs a) {
   }
 }
 
-// Fused backward, head resident (T <= 256): ONE kernel per (batch, head) instead of the dq / dkv
-// pair, which both staged the head and both recomputed S = Q K^T and dP = dO V^T. One wave per 16
-// keys holds its dK^T / dV^T accumulators (as attn_bwd_dkv_res) while sweeping the queries in
-// 32-row blocks; the same block's dS also feeds dQ = dS K: the wave transposes its 16 x 32 dS
-// tile through a 1-KiB private LDS scratch (one 8-B write per lane and half, read back by
-// ds_read_b64_tr_b16 as the A operand of v_mfma_f32_16x16x16_bf16, K by transposed reads of the
-// staged K image as B) and adds its partial into an fp32 dQ accumulator in LDS (ds_add_f32; the
-// waves sweep the query blocks in rotated order, so they seldom add into the same rows at once).
-// D = rowsum(dO * O) is computed in the prologue (no separate pass). LDS: Q, dO, K images +
-// dQ [TV][64] fp32 + lse / D + scratch = 156 KiB at T = 197: one workgroup (13 waves) per CU.
-// MEASURED A LOSS (profiles/rd3i_vit_attnfused_steady.md): 3.1 ms per call vs 0.28 ms for the
-// dq + dkv pair at ViT-B/16 bs256 — the 32 ds_add_f32 per lane per query block (4-way bank
-// conflicted rows) serialise on the LDS atomic path and dominate everything else. Kept opt-in
-// (FLUXMPI_ATTN_BWD=fused) as the record of that experiment; the default stays the pair.
-typedef short short4v_t __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) short4v_t lds_short4v_t;
-
-__device__ __forceinline__ short4v_t tr_read4(const char* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v_t*)(p));
-}
-
-__global__ __launch_bounds__(1024) void attn_bwd_fused_kernel(AttnBwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int TV = (a.T + 31) & ~31;
-  const int nw = blockDim.x >> 6;
-  char* qimg = smem;
-  char* gimg = qimg + TV * 128;
-  char* kimg = gimg + TV * 128;
-  float* dqacc = reinterpret_cast<float*>(kimg + TV * 128);  // [TV][64]
-  float* sL = dqacc + TV * 64;
-  float* sD = sL + TV;
-  char* scratch = reinterpret_cast<char*>(sD + TV);          // per wave: 2 halves x [16 k][16 q] bf16
-  const int b = blockIdx.x / a.H, h = blockIdx.x % a.H;
-  stage_rows<false>(qimg, a.q + b * a.sq_b + h * DH, a.sq_t, TV, a.T);
-  stage_rows<false>(gimg, a.dout + b * a.sg_b + h * DH, a.sg_t, TV, a.T);
-  stage_rows<false>(kimg, a.k + b * a.sq_b + h * DH, a.sq_t, TV, a.T);
-  for (int i = threadIdx.x; i < TV * 16; i += blockDim.x)
-    reinterpret_cast<float4*>(dqacc)[i] = float4{0.f, 0.f, 0.f, 0.f};
-  const float* st = a.stats + (static_cast<int64_t>(b) * a.H + h) * a.T * 2;
-  for (int qq = threadIdx.x; qq < TV; qq += blockDim.x) {
-    sL[qq] = qq < a.T ? st[2 * qq] : kInf;  // padded query: P = 0
-    if (qq >= a.T) sD[qq] = 0.f;
-  }
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, col = lane & 15, g = lane >> 4;
-  // D for this wave's 16 queries (= its key range: one wave per 16 rows either way)
-  {
-    const int qi = 16 * w + col;
-    bf16x8 gf[2] = {}, o0 = {}, o1 = {};
-    if (qi < a.T) {
-      const bf16* gp = a.dout + b * a.sg_b + static_cast<int64_t>(qi) * a.sg_t + h * DH;
-      gf[0] = ld8(gp + 8 * g);
-      gf[1] = ld8(gp + 32 + 8 * g);
-      const bf16* op = a.o + b * a.so_b + static_cast<int64_t>(qi) * a.so_t + h * a.so_h;
-      o0 = ld8(op + 8 * g);
-      o1 = ld8(op + 32 + 8 * g);
-    }
-    float dsum = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) dsum += (float)gf[0][j] * (float)o0[j] + (float)gf[1][j] * (float)o1[j];
-    dsum = butterfly_from<16>(dsum);
-    if (g == 0 && qi < a.T) sD[qi] = dsum;
-  }
-  const int k0 = 16 * w;
-  const int ki = k0 + col;
-  const bool kok = ki < a.T;
-  const int64_t koff = b * a.sq_b + static_cast<int64_t>(ki) * a.sq_t + h * DH;
-  bf16x8 kf[2] = {}, vf[2] = {};
-  if (kok) {
-    kf[0] = ld8(a.k + koff + 8 * g);
-    kf[1] = ld8(a.k + koff + 32 + 8 * g);
-    vf[0] = ld8(a.v + koff + 8 * g);
-    vf[1] = ld8(a.v + koff + 32 + 8 * g);
-  }
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  const float c2 = a.scale * kLog2e;
-  // transposed-read lane roles (per 16-lane group g: lane 4q'+p addresses row 4g+q', columns 4p..4p+3)
-  const int trq = (lane & 15) >> 2, trp = lane & 3;
-  char* scr = scratch + w * 1024;
-  // B operand of the dQ MFMA: K[k0 + 4g + j][16 dt + (lane & 15)] from the staged K image
-  short4v_t kb[4];
-  {
-    const int kr = k0 + 4 * g + trq;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const int c = 16 * dt + 4 * trp;
-      kb[dt] = tr_read4(kimg + kr * 128 + (((c >> 3) ^ swz_b(kr)) << 4) + (c & 7) * 2);
-    }
-  }
-  f32x4 accK[4] = {}, accV[4] = {};
-  const int nks = TV / 32;
-  for (int it = 0; it < nks; ++it) {
-    const int ks = (it + w) % nks;  // rotated: waves add into different dQ rows at a time
-    f32x4 p[2], dsv[2];
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      const int row = 32 * ks + 16 * half + col;
-      f32x4 sv = {}, dp = {};
-      sv = mfma(img_row(qimg, row, g), kf[0], sv);
-      sv = mfma(img_row(qimg, row, 4 + g), kf[1], sv);
-      dp = mfma(img_row(gimg, row, g), vf[0], dp);
-      dp = mfma(img_row(gimg, row, 4 + g), vf[1], dp);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int qq = 32 * ks + 16 * half + 4 * g + r;
-        const float pv = fast_exp2(fmaf(sv[r], c2, -sL[qq]));
-        p[half][r] = pv;
-        dsv[half][r] = pv * (dp[r] - sD[qq]);
-      }
-      // dS^T tile of this half: row k = col, queries 4g .. 4g+3 (one 8-B write per lane)
-      const bf16x4 d4 = {(bf16)dsv[half][0], (bf16)dsv[half][1], (bf16)dsv[half][2], (bf16)dsv[half][3]};
-      *reinterpret_cast<bf16x4*>(scr + half * 512 + col * 32 + 8 * g) = d4;
-    }
-    const bf16x8 pb = pack(p[0], p[1]), db = pack(dsv[0], dsv[1]);
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      accV[dt] = mfma(img_tr(gimg, 32 * ks, 16 * dt), pb, accV[dt]);
-      accK[dt] = mfma(img_tr(qimg, 32 * ks, 16 * dt), db, accK[dt]);
-    }
-    // dQ[q][d] += sum over this wave's 16 keys of dS[q][k] K[k][d]
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      // A operand: dS[q = lane & 15][k = 4g + j] = column (lane & 15) of scratch rows 4g .. 4g+3
-      const short4v_t da = tr_read4(scr + half * 512 + (4 * g + trq) * 32 + 8 * trp);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        f32x4 c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(da, kb[dt], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          atomicAdd(dqacc + (32 * ks + 16 * half + 4 * g + r) * 64 + 16 * dt + col, c[r]);
-      }
-    }
-  }
-  if (kok) {
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const bf16x4 v = {(bf16)accV[dt][0], (bf16)accV[dt][1], (bf16)accV[dt][2], (bf16)accV[dt][3]};
-      const bf16x4 k = {(bf16)(accK[dt][0] * a.scale), (bf16)(accK[dt][1] * a.scale),
-                        (bf16)(accK[dt][2] * a.scale), (bf16)(accK[dt][3] * a.scale)};
-      *reinterpret_cast<bf16x4*>(a.dv + koff + dt * 16 + 4 * g) = v;
-      *reinterpret_cast<bf16x4*>(a.dk + koff + dt * 16 + 4 * g) = k;
-    }
-  }
-  __syncthreads();  // every wave's dQ partials are in LDS
-  for (int i = threadIdx.x; i < a.T * 8; i += blockDim.x) {
-    const int qq = i >> 3, c8 = (i & 7) * 8;
-    const float* src = dqacc + qq * 64 + c8;
-    bf16x8 o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = (bf16)(src[j] * a.scale);
-    *reinterpret_cast<bf16x8*>(a.dq + b * a.sq_b + static_cast<int64_t>(qq) * a.sq_t + h * DH + c8) = o;
-  }
-}
-
-// Two-phase backward, head resident (T <= 256): attn_bwd_dq_res and attn_bwd_dkv_res as the two
-// phases of ONE kernel, sharing one 2 x [TV][64] LDS image pair (57 KiB: two workgroups per CU,
-// as the pair's). Phase 1 (dQ) stages K, V and reads each wave's query rows of Q, dO, O from
-// global; phase 2 (dK, dV) first takes its key rows' K / V fragments out of those images, then
-// restages the pair with Q and dO. What the pair paid and this does not: the dkv kernel's
-// re-reads of Q, dO, K, V from HBM (the dq kernel had swept every head in between, so nothing
-// was left in L2; here phase 2's staging re-reads rows phase 1 of this and the sibling
-// workgroup just loaded, and K / V come from LDS), D = rowsum(dO * O) written and read back
-// through global memory (each part computes it for all queries in LDS), one launch.
-// a.nblk parts per (b, h): part p owns query rows [16 p nw, ..) in phase 1 and the same key rows
-// in phase 2 (nw waves).
-// MEASURED NO GAIN (rd3p, ViT-B/16 bs256): 293.9 us per call vs 127.5 + 150.8 us for the pair,
-// 7.11k / 7.09k vs 7.11k / 7.11k img/s — the pair is not bound by the traffic this removes (both
-// kernels run at ~2 of 8 possible waves per SIMD, latency-bound). Opt-in: FLUXMPI_ATTN_BWD=two.
-__global__ __launch_bounds__(1024) void attn_bwd_two_kernel(AttnBwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int TP = (a.T + 15) & ~15, TV = (a.T + 31) & ~31;
-  char* img0 = smem;               // K (phase 1) | Q (phase 2), TV rows
-  char* img1 = smem + TV * 128;    // V (phase 1) | dO (phase 2), TV rows
-  float* sL = reinterpret_cast<float*>(smem + 2 * TV * 128);
-  float* sD = sL + TV;
-  int part, h, b;
-  res_coords(a, b, h, part);
-  const bf16* kb = a.k + b * a.sq_b + h * DH;
-  const bf16* vb = a.v + b * a.sq_b + h * DH;
-  const bf16* qb = a.q + b * a.sq_b + h * DH;
-  const bf16* gb = a.dout + b * a.sg_b + h * DH;
-  const bf16* ob = a.o + b * a.so_b + h * a.so_h;
-  stage_rows<false>(img0, kb, a.sq_t, TV, a.T);
-  stage_rows<false>(img1, vb, a.sq_t, TP, a.T);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, col = lane & 15, g = lane >> 4;
-  const int r0 = 16 * (part * (blockDim.x >> 6) + w);  // this wave's 16 queries, then 16 keys
-  const float c2 = a.scale * kLog2e;
-  float* st = a.stats + (static_cast<int64_t>(b) * a.H + h) * a.T * 2;
-  // ---------------- phase 1: dQ for queries r0 .. r0 + 15 (attn_bwd_dq_res)
-  {
-    const int qi = r0 + col;
-    const bool qok = qi < a.T;
-    const int64_t qoff = static_cast<int64_t>(qi) * a.sq_t;
-    bf16x8 qf[2] = {}, gf[2] = {}, o0 = {}, o1 = {};
-    float lse = 0.f;
-    if (qok) {
-      qf[0] = ld8(qb + qoff + 8 * g);
-      qf[1] = ld8(qb + qoff + 32 + 8 * g);
-      const bf16* gp = gb + static_cast<int64_t>(qi) * a.sg_t;
-      gf[0] = ld8(gp + 8 * g);
-      gf[1] = ld8(gp + 32 + 8 * g);
-      const bf16* op = ob + static_cast<int64_t>(qi) * a.so_t;
-      o0 = ld8(op + 8 * g);
-      o1 = ld8(op + 32 + 8 * g);
-      lse = st[2 * qi];
-    }
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    if (r0 < a.T) {  // wave-uniform
-      float dsum = 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dsum += (float)gf[0][j] * (float)o0[j] + (float)gf[1][j] * (float)o1[j];
-      dsum = butterfly_from<16>(dsum);
-      const int nt = TP / 16;
-      f32x4 ds[kResMaxT / 16];
-#pragma unroll
-      for (int kt = 0; kt < kResMaxT / 16; ++kt) {
-        ds[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (kt < nt) {
-          const int row = 16 * kt + col;
-          f32x4 sv = {}, dp = {};
-          sv = mfma(img_row(img0, row, g), qf[0], sv);
-          sv = mfma(img_row(img0, row, 4 + g), qf[1], sv);
-          dp = mfma(img_row(img1, row, g), gf[0], dp);
-          dp = mfma(img_row(img1, row, 4 + g), gf[1], dp);
-          if (16 * kt + 16 <= a.T) {  // wave-uniform
-#pragma unroll
-            for (int r = 0; r < 4; ++r) ds[kt][r] = fast_exp2(fmaf(sv[r], c2, -lse)) * (dp[r] - dsum);
-          } else {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int key = 16 * kt + 4 * g + r;
-              ds[kt][r] = key < a.T ? fast_exp2(fmaf(sv[r], c2, -lse)) * (dp[r] - dsum) : 0.f;
-            }
-          }
-        }
-      }
-      f32x4 acc[4] = {};
-#pragma unroll
-      for (int ks = 0; ks < kResMaxT / 32; ++ks) {
-        if (32 * ks < TV) {
-          const bf16x8 bop = pack(ds[2 * ks], ds[2 * ks + 1]);
-#pragma unroll
-          for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma(img_tr(img0, 32 * ks, 16 * dt), bop, acc[dt]);
-        }
-      }
-      if (qok) {
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-          const bf16x4 o = {(bf16)(acc[dt][0] * a.scale), (bf16)(acc[dt][1] * a.scale),
-                            (bf16)(acc[dt][2] * a.scale), (bf16)(acc[dt][3] * a.scale)};
-          *reinterpret_cast<bf16x4*>(a.dq + b * a.sq_b + qoff + h * DH + dt * 16 + 4 * g) = o;
-        }
-      }
-    }
-  }
-  // ---------------- phase 2: dK, dV for keys r0 .. r0 + 15 (attn_bwd_dkv_res)
-  const int ki = r0 + col;
-  const bool kok = ki < a.T;
-  bf16x8 kf[2], vf[2];
-  // this wave's K / V rows out of the phase-1 images (rows >= T are zero there; r0 < TP <= TV)
-  const int kr = ki < TV ? ki : TV - 1;  // waves past the last tile (r0 >= T) read a valid row
-  kf[0] = img_row(img0, kr, g);
-  kf[1] = img_row(img0, kr, 4 + g);
-  vf[0] = img_row(img1, kr, g);
-  vf[1] = img_row(img1, kr, 4 + g);
-  __syncthreads();  // every wave is done with the K / V images
-  stage_rows<false>(img0, qb, a.sq_t, TV, a.T);
-  stage_rows<false>(img1, gb, a.sg_t, TV, a.T);
-  // lse and D = rowsum(dO * O) of every query (8 lanes per row, 8 columns each)
-  for (int i = threadIdx.x; i < TV * 8; i += blockDim.x) {  // wave-uniform trip count (TV * 8 % 256 == 0)
-    const int qq = i >> 3, c8 = (i & 7) * 8;
-    float d = 0.f;
-    if (qq < a.T) {
-      const bf16x8 gv = ld8(gb + static_cast<int64_t>(qq) * a.sg_t + c8);
-      const bf16x8 ov = ld8(ob + static_cast<int64_t>(qq) * a.so_t + c8);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) d += (float)gv[j] * (float)ov[j];
-    }
-    d = xor_sum<4>(xor_sum<2>(xor_sum<1>(d)));
-    if ((i & 7) == 0) {
-      sD[qq] = d;
-      sL[qq] = qq < a.T ? st[2 * qq] : kInf;  // padded query: P = 0
-    }
-  }
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  if (r0 >= a.T) return;  // wave-uniform
-  f32x4 accK[4] = {}, accV[4] = {};
-#pragma unroll 2
-  for (int ks = 0; ks < TV / 32; ++ks) {
-    f32x4 p[2], dsv[2];
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      const int row = 32 * ks + 16 * half + col;  // query row of the A fragment
-      f32x4 sv = {}, dp = {};
-      sv = mfma(img_row(img0, row, g), kf[0], sv);
-      sv = mfma(img_row(img0, row, 4 + g), kf[1], sv);
-      dp = mfma(img_row(img1, row, g), vf[0], dp);
-      dp = mfma(img_row(img1, row, 4 + g), vf[1], dp);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int qq = 32 * ks + 16 * half + 4 * g + r;
-        const float pv = fast_exp2(fmaf(sv[r], c2, -sL[qq]));
-        p[half][r] = pv;
-        dsv[half][r] = pv * (dp[r] - sD[qq]);
-      }
-    }
-    const bf16x8 pb = pack(p[0], p[1]), db = pack(dsv[0], dsv[1]);
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      accV[dt] = mfma(img_tr(img1, 32 * ks, 16 * dt), pb, accV[dt]);
-      accK[dt] = mfma(img_tr(img0, 32 * ks, 16 * dt), db, accK[dt]);
-    }
-  }
-  if (kok) {
-    const int64_t koff = b * a.sq_b + static_cast<int64_t>(ki) * a.sq_t + h * DH;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const bf16x4 v = {(bf16)accV[dt][0], (bf16)accV[dt][1], (bf16)accV[dt][2], (bf16)accV[dt][3]};
-      const bf16x4 k = {(bf16)(accK[dt][0] * a.scale), (bf16)(accK[dt][1] * a.scale),
-                        (bf16)(accK[dt][2] * a.scale), (bf16)(accK[dt][3] * a.scale)};
-      *reinterpret_cast<bf16x4*>(a.dv + koff + dt * 16 + 4 * g) = v;
-      *reinterpret_cast<bf16x4*>(a.dk + koff + dt * 16 + 4 * g) = k;
-    }
-  }
-}
-
-void attn_fwd_pers_kernel_attr(const void* k) {
-  static const void* done[4] = {};
-  for (const void*& d : done) {
-    if (d == k) return;
-    if (d == nullptr) {
-      FLUXMPI_HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-      d = k;
-      return;
-    }
-  }
-}
-
 // FLUXMPI_ATTN_GENERIC=1: the runtime-tile-count kernels for every T (A/B of the NT = 13 instances)
 // explicitly pipelined dkv k-steps for the compile-time-tile-count kernel (FLUXMPI_ATTN_DKV_PIPE=0: off)
 bool dkv_pipe() {
@@ -1459,15 +936,6 @@ bool attn_generic() {
     return e != nullptr && e[0] == '1';
   }();
   return on;
-}
-
-int g_attn_bwd_fused = -1;  // backward variant (attn_set_bwd_fused); -1: FLUXMPI_ATTN_BWD decides
-int g_attn_fwd_mode = -1;   // forward variant (attn_set_fwd_mode); -1: FLUXMPI_ATTN_FWD decides
-
-size_t fused_bwd_lds(int T) {
-  const size_t TV = static_cast<size_t>((T + 31) & ~31);
-  const size_t waves = static_cast<size_t>((T + 15) / 16);
-  return 3 * TV * 128 + TV * 64 * 4 + 2 * TV * 4 + waves * 1024;
 }
 
 bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
@@ -1487,20 +955,16 @@ int res_parts(int tiles) {
 }  // namespace
 
 namespace {
-int bwd_env_mode() {
-  static const int m = [] {
-    const char* e = std::getenv("FLUXMPI_ATTN_BWD");
-    const std::string v = e != nullptr ? std::string(e) : std::string();
-    return v == "fused" ? 1 : (v == "two" ? 2 : (v == "blocked" ? 3 : 0));
-  }();
-  return m;
+// FLUXMPI_ATTN_BWD=blocked / FLUXMPI_ATTN_FWD=blocked: the non-resident kernels for every T (A/B)
+bool blocked_env(const char* name) {
+  const char* e = std::getenv(name);
+  return e != nullptr && std::string(e) == "blocked";
 }
-int bwd_mode() { return g_attn_bwd_fused < 0 ? bwd_env_mode() : g_attn_bwd_fused; }
 }  // namespace
 
 int attn_bwd_colpart_rows(int B, int T, int H, int64_t sq_t, int64_t sg_t) {
   // the resident dq / dkv pair writes the column-sum partials; every other variant does not
-  if (bwd_mode() != 0 || T > kResMaxT || T <= 0 || (sq_t % 8) != 0 || (sg_t % 8) != 0) return 0;
+  if (blocked_env("FLUXMPI_ATTN_BWD") || T > kResMaxT || T <= 0 || (sq_t % 8) != 0 || (sg_t % 8) != 0) return 0;
   const int tiles = (T + 15) / 16;
   const int nblk = res_parts(tiles);
   const int waves = (tiles + nblk - 1) / nblk;
@@ -1522,34 +986,7 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* o, const 
                 static_cast<const bf16*>(o), static_cast<const bf16*>(dout), nullptr, static_cast<bf16*>(dq),
                 static_cast<bf16*>(dk), static_cast<bf16*>(dv), stats, sq_b, sq_t, so_b, so_t, so_h, sg_b, sg_t,
                 B, T, H, (T + 63) / 64, scale};
-  const int mode = bwd_mode();
-  const bool resident = mode != 3;
-  if (mode == 1 && T <= kResMaxT && (sq_t % 8) == 0 && (sg_t % 8) == 0 && fused_bwd_lds(T) <= 160 * 1024) {
-    const int waves = (T + 15) / 16;
-    const int64_t bh = static_cast<int64_t>(B) * H;
-    if (bh > 0x7fffffff) throw std::runtime_error("attn_bwd: grid too large");
-    static bool attr = false;
-    if (!attr) {
-      FLUXMPI_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_fused_kernel),
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-      attr = true;
-    }
-    attn_bwd_fused_kernel<<<static_cast<unsigned>(bh), waves * 64, fused_bwd_lds(T), s>>>(a);
-    FLUXMPI_HIP_CHECK(hipGetLastError());
-    return;
-  }
-  if (mode == 2 && T <= kResMaxT && (sq_t % 8) == 0 && (sg_t % 8) == 0) {
-    const int tiles = (T + 15) / 16;
-    a.nblk = res_parts(tiles);
-    const int64_t bh = static_cast<int64_t>(B) * H * a.nblk;
-    if (bh > 0x7fffffff) throw std::runtime_error("attn_bwd: grid too large");
-    const int waves = (tiles + a.nblk - 1) / a.nblk;
-    const int TV = (T + 31) & ~31;
-    attn_bwd_two_kernel<<<static_cast<unsigned>(bh), waves * 64, static_cast<size_t>(2 * TV) * 128 + 2 * TV * 4,
-                          s>>>(a);
-    FLUXMPI_HIP_CHECK(hipGetLastError());
-    return;
-  }
+  static const bool resident = !blocked_env("FLUXMPI_ATTN_BWD");
   if (resident && T <= kResMaxT && (sq_t % 8) == 0 && (sg_t % 8) == 0) {
     const int tiles = (T + 15) / 16;
     a.nblk = res_parts(tiles);
@@ -1576,14 +1013,6 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* o, const 
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
 
-// backward variant for A/B runs and tests: -1 FLUXMPI_ATTN_BWD decides, 0 the dq / dkv pair,
-// 1 the one-kernel LDS-atomic backward, 2 the two-phase kernel
-// forward variant for A/B runs and tests: -1 FLUXMPI_ATTN_FWD decides, 0 two workgroups per head
-// (attn_fwd_res_kernel), 1 the persistent double-buffered kernel (attn_fwd_pers_kernel)
-void attn_set_fwd_mode(int mode) { g_attn_fwd_mode = mode < -1 || mode > 1 ? -1 : mode; }
-
-void attn_set_bwd_fused(int mode) { g_attn_bwd_fused = mode < -1 || mode > 2 ? -1 : mode; }
-
 void attn_fwd(const void* q, const void* k, const void* v, void* o, float* stats, int64_t sq_b, int64_t sq_t,
               int64_t so_b, int64_t so_t, int64_t so_h, int B, int T, int H, int Dh, float scale, hipStream_t s) {
   if (Dh != DH) throw std::runtime_error("attn_fwd: head dim must be 64");
@@ -1608,33 +1037,7 @@ void attn_fwd(const void* q, const void* k, const void* v, void* o, float* stats
   a.H = H;
   a.nblk = (T + 63) / 64;
   a.scale = scale;
-  static const bool resident = [] {
-    const char* e = std::getenv("FLUXMPI_ATTN_FWD");
-    return e == nullptr || std::string(e) != "blocked";
-  }();
-  static const bool persist_env = [] {
-    const char* e = std::getenv("FLUXMPI_ATTN_FWD");
-    return e != nullptr && std::string(e) == "persist";
-  }();
-  const bool persist = g_attn_fwd_mode < 0 ? persist_env : g_attn_fwd_mode == 1;
-  if (persist && T <= kResMaxT && (sq_t % 8) == 0 && (static_cast<int64_t>(T) * sq_t) < (1LL << 31)) {
-    // one workgroup per CU looping over heads, the next head's K / V staged during this one's math
-    a.nblk = 1;
-    const int TP = (T + 15) & ~15, TV = (T + 31) & ~31;
-    const size_t lds = static_cast<size_t>(2 * (TP + TV)) * 128;
-    int cus = 256, dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const int64_t heads = static_cast<int64_t>(B) * H;
-    const int grid = static_cast<int>(heads < cus ? heads : cus);
-    const int nw = (T + 15) / 16, per = ((TP + TV) / 8 + nw - 1) / nw;  // 4..6 for T <= 256
-    auto k = per <= 4 ? attn_fwd_pers_kernel<4> : (per == 5 ? attn_fwd_pers_kernel<5> : attn_fwd_pers_kernel<6>);
-    if (per > 6) throw std::runtime_error("attn_fwd: persistent staging count out of range");
-    attn_fwd_pers_kernel_attr(reinterpret_cast<const void*>(k));
-    k<<<grid, nw * 64, lds, s>>>(a);
-    FLUXMPI_HIP_CHECK(hipGetLastError());
-    return;
-  }
+  static const bool resident = !blocked_env("FLUXMPI_ATTN_FWD");
   if (resident && T <= kResMaxT && (sq_t % 8) == 0) {
     // whole head resident in LDS: res_parts() workgroups per (b, h), one wave per 16 queries
     const int tiles = (T + 15) / 16;

@@ -25,7 +25,6 @@
 
 #include "../api.h"
 #include "common.h"
-#include "bn_fin.h"
 
 namespace fluxmpi {
 namespace {
@@ -95,10 +94,8 @@ Geo geometry(int64_t rows, int64_t C, int64_t max_blocks = 2048) {
 // memory side, and thousands of workgroups adding into ONE line serialise.
 constexpr int kShards = 64;  // <= ~200 same-address atomics even for 12k-block GEMM grids
 // The row-reduction kernels here run at most one round of resident workgroups (<= 2048): 16
-// shards keep <= 128 same-address atomics and make the in-kernel finalize's read 4x smaller.
+// shards keep <= 128 same-address atomics and make the finalize kernel's read 4x smaller.
 constexpr int kRedShards = 16;
-// a 32-bit arrival counter per workspace, behind the [kShards][2][kMaxC] shards (kept zero)
-constexpr size_t kCntOff = static_cast<size_t>(kShards) * 2 * kMaxC;
 
 __device__ __forceinline__ void block_reduce_atomic(float (&a)[8], float (&b)[8], int cv, int rpi, int C,
                                                     float* __restrict__ acc, float* smem) {
@@ -221,116 +218,10 @@ __global__ __launch_bounds__(kFinCh * kFinGroups) void bn_finalize_bwd2_kernel(f
   (second ? dw2 : dw)[c] = q;
 }
 
-// ---------------------------------------------------------------- in-kernel finalize
-// The finalize as the tail of the reduction kernel itself (bn_fin.h): the LAST workgroup to
-// arrive sums the kRedShards shards, writes the per-channel results, re-zeroes the shards and
-// the counter. One launch (and one dependent launch gap) less per BatchNorm pass.
-using bnfin::Fin;
-static_assert(bnfin::kShards == kShards && bnfin::kMaxC == kMaxC && bnfin::kCntOff == kCntOff, "bn_fin.h layout");
-
-// fp32 sums of 4 consecutive channels over the kRedShards shards (16-B loads), shards re-zeroed
-__device__ __forceinline__ void take4(float* __restrict__ acc, int C, int c, float4& s, float4& q) {
-  float4 vs[kRedShards], vq[kRedShards];
-#pragma unroll
-  for (int k = 0; k < kRedShards; ++k) {
-    const float* sh = acc + static_cast<size_t>(k) * 2 * C;
-    vs[k] = *reinterpret_cast<const float4*>(sh + c);
-    vq[k] = *reinterpret_cast<const float4*>(sh + C + c);
-  }
-  s = make_float4(0.f, 0.f, 0.f, 0.f);
-  q = s;
-#pragma unroll
-  for (int k = 0; k < kRedShards; ++k) {
-    s.x += vs[k].x; s.y += vs[k].y; s.z += vs[k].z; s.w += vs[k].w;
-    q.x += vq[k].x; q.y += vq[k].y; q.z += vq[k].z; q.w += vq[k].w;
-  }
-  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-  for (int k = 0; k < kRedShards; ++k) {
-    float* sh = acc + static_cast<size_t>(k) * 2 * C;
-    *reinterpret_cast<float4*>(sh + c) = z;
-    *reinterpret_cast<float4*>(sh + C + c) = z;
-  }
-}
-
-// Call from EVERY thread of the workgroup after its block_reduce_atomic(s). acc2: the second
-// workspace of the dual backward (its counter is unused: acc's counts both).
-__device__ __forceinline__ void finalize_last(const Fin& f, float* __restrict__ acc, float* __restrict__ acc2, int C) {
-  if (f.mode == 0) return;
-  unsigned* cnt = reinterpret_cast<unsigned*>(acc + kCntOff);
-  if (!bnfin::arrive_last(cnt, gridDim.x)) return;
-  for (int c = threadIdx.x * 4; c < C; c += kThreads * 4) {
-    float4 s, q;
-    take4(acc, C, c, s, q);
-    const float sv[4] = {s.x, s.y, s.z, s.w}, qv[4] = {q.x, q.y, q.z, q.w};
-    if (f.mode == 1) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bnfin::fwd_channel(f, c + j, sv[j], qv[j]);
-    } else {
-      *reinterpret_cast<float4*>(f.db + c) = s;
-      *reinterpret_cast<float4*>(f.dw + c) = q;
-      if (acc2 != nullptr) {
-        take4(acc2, C, c, s, q);
-        *reinterpret_cast<float4*>(f.db2 + c) = s;
-        *reinterpret_cast<float4*>(f.dw2 + c) = q;
-      }
-    }
-  }
-  if (threadIdx.x == 0) {
-    *cnt = 0u;
-    if (f.mode == 1 && f.nbt != nullptr) *f.nbt += 1;  // num_batches_tracked, no launch of its own
-  }
-}
-
-// FLUXMPI_BN_FIN=1: the in-kernel finalize. Off by default — MEASURED SLOWER (rd3p, same box:
-// 12.36k / 12.36k vs 12.43k / 12.44k img/s with the finalize kernels): the last workgroup's chain
-// (its atomics' completion, the returning counter atomic, the acquire, the shard loads) adds more
-// to the small reduction kernels' tails (bn_stats 8.2 -> 16.6 us, bn_bwd_reduce on 14x14 / 7x7
-// 22.1 -> 25.6 us) than the ~5 us finalize kernel it replaces.
-bool fin_in_kernel() {
-  static const bool on = [] {
-    const char* e = std::getenv("FLUXMPI_BN_FIN");
-    return e != nullptr && std::atoi(e) != 0;
-  }();
-  return on;
-}
-
-Fin no_fin() {
-  Fin f{};
-  f.mode = 0;
-  return f;
-}
-
-Fin fwd_fin(int64_t rows, float momentum, float eps, float* sm, float* si, float* rm, float* rv, int64_t* nbt) {
-  if (!fin_in_kernel()) return no_fin();
-  Fin f{};
-  f.mode = 1;
-  f.rows = rows;
-  f.momentum = momentum;
-  f.eps = eps;
-  f.smean = sm;
-  f.sinv = si;
-  f.rmean = rm;
-  f.rvar = rv;
-  f.nbt = nbt;
-  return f;
-}
-
-Fin bwd_fin(float* dw, float* db, float* dw2, float* db2) {
-  if (!fin_in_kernel()) return no_fin();
-  Fin f{};
-  f.mode = 2;
-  f.dw = dw;
-  f.db = db;
-  f.dw2 = dw2;
-  f.db2 = db2;
-  return f;
-}
-
 // ---------------------------------------------------------------- forward
 template <typename T>
 __global__ __launch_bounds__(kThreads) void bn_stats_kernel(const T* __restrict__ x, int64_t rows, int C, Geo g,
-                                                            float* __restrict__ acc, Fin fin) {
+                                                            float* __restrict__ acc) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int t = threadIdx.x;
   const int r0 = t / g.cv, c8 = t % g.cv;
@@ -366,7 +257,6 @@ __global__ __launch_bounds__(kThreads) void bn_stats_kernel(const T* __restrict_
     }
   }
   block_reduce_atomic(s, q, g.cv, g.rpi, C, acc, smem);
-  finalize_last(fin, acc, nullptr, C);
 }
 
 // y = act(x*scale + shift [+ res]); scale/shift derived from (mean, invstd) = batch
@@ -474,7 +364,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const T* __rest
                                                                  const float* __restrict__ b,
                                                                  const float* __restrict__ smean,
                                                                  const float* __restrict__ sinv, int64_t rows, int C,
-                                                                 Geo g, float* __restrict__ acc, Fin fin) {
+                                                                 Geo g, float* __restrict__ acc) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int t = threadIdx.x;
   const int r0 = t / g.cv, c8 = t % g.cv;
@@ -538,7 +428,6 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const T* __rest
     }
   }
   block_reduce_atomic(s, q, g.cv, g.rpi, C, acc, smem);
-  finalize_last(fin, acc, nullptr, C);
 }
 
 // dx = w*invstd * (dy_eff - sum_dy/R - xhat * sum_dy_xhat/R); dres = dy_eff
@@ -721,8 +610,7 @@ template <typename T>
 __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_dual_kernel(
     const T* __restrict__ dy, const uint8_t* __restrict__ mask, const T* __restrict__ x, const T* __restrict__ x2,
     const float* __restrict__ mean, const float* __restrict__ inv, const float* __restrict__ mean2,
-    const float* __restrict__ inv2, int64_t rows, int C, Geo g, float* __restrict__ acc, float* __restrict__ acc2,
-    Fin fin) {
+    const float* __restrict__ inv2, int64_t rows, int C, Geo g, float* __restrict__ acc, float* __restrict__ acc2) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int t = threadIdx.x;
   const int r0 = t / g.cv, c8 = t % g.cv;
@@ -778,7 +666,6 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_dual_kernel(
   block_reduce_atomic(s, q, g.cv, g.rpi, C, acc, smem);
   __syncthreads();  // the LDS staging is reused
   block_reduce_atomic(s, q2, g.cv, g.rpi, C, acc2, smem);
-  finalize_last(fin, acc, acc2, C);
 }
 
 // dx = A*dy_eff + B*x + D, dx2 = A2*dy_eff + B2*x2 + D2 (coefficients as in bn_bwd_dx_kernel)
@@ -930,14 +817,11 @@ void fwd_train_t(const void* x, void* y, const void* res, const float* w, const 
                  float* sm, float* si, float* ws, int64_t rows, int64_t C, float momentum, float eps, int relu,
                  uint8_t* mask, int64_t* nbt, hipStream_t s) {
   const Geo g = reduce_geometry(reinterpret_cast<const void*>(bn_stats_kernel<T>), rows, C);
-  const Fin fin = fwd_fin(rows, momentum, eps, sm, si, rm, rv, nbt);
-  bn_stats_kernel<T><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(static_cast<const T*>(x), rows, (int)C, g, ws, fin);
+  bn_stats_kernel<T><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(static_cast<const T*>(x), rows, (int)C, g, ws);
   FLUXMPI_HIP_CHECK(hipGetLastError());
-  if (fin.mode == 0) {
-    bn_finalize_fwd_kernel<<<finalize_blocks(C), kFinCh * kFinGroups, 0, s>>>(ws, (int)C, rows, momentum, eps, sm, si, rm,
-                                                                              rv, nullptr, nullptr, nullptr, nullptr, nbt);
-    FLUXMPI_HIP_CHECK(hipGetLastError());
-  }
+  bn_finalize_fwd_kernel<<<finalize_blocks(C), kFinCh * kFinGroups, 0, s>>>(ws, (int)C, rows, momentum, eps, sm, si, rm,
+                                                                            rv, nullptr, nullptr, nullptr, nullptr, nbt);
+  FLUXMPI_HIP_CHECK(hipGetLastError());
   norm_t<T>(x, y, res, w, b, sm, si, rows, C, eps, 1, relu, mask, s);
 }
 
@@ -954,9 +838,8 @@ void bwd_t(const void* dy, const void* x, const void* y, const uint8_t* mask, co
   {                                                                                                             \
     const Geo g = reduce_geometry(reinterpret_cast<const void*>(bn_bwd_reduce_kernel<T, RM>), rows, C);          \
     bn_bwd_reduce_kernel<T, RM><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(dyr, xr, yr, mask, w, b, sm, si,   \
-                                                                              rows, (int)C, g, ws, fin);        \
+                                                                              rows, (int)C, g, ws);             \
   }
-  const Fin fin = stats_ready ? no_fin() : bwd_fin(dw, db, nullptr, nullptr);
   // stats_ready: the reductions were accumulated into ws by the producer of dy (the GEMM's
   // BN-backward epilogue), so the reduce pass over (dy, x) is skipped
   if (stats_ready) {}
@@ -966,10 +849,8 @@ void bwd_t(const void* dy, const void* x, const void* y, const uint8_t* mask, co
   else RED(3)
 #undef RED
   FLUXMPI_HIP_CHECK(hipGetLastError());
-  if (fin.mode == 0) {
-    bn_finalize_bwd_kernel<<<finalize_blocks(C), kFinCh * kFinGroups, 0, s>>>(ws, (int)C, dw, db);
-    FLUXMPI_HIP_CHECK(hipGetLastError());
-  }
+  bn_finalize_bwd_kernel<<<finalize_blocks(C), kFinCh * kFinGroups, 0, s>>>(ws, (int)C, dw, db);
+  FLUXMPI_HIP_CHECK(hipGetLastError());
   const int64_t nvec = rows * C / 8;
   T* dxr = static_cast<T*>(dx);
   T* drr = static_cast<T*>(dres);
@@ -1016,15 +897,12 @@ void bwd_dual_t(const void* dy, const uint8_t* mask, const void* x, const void* 
   const T* xr = static_cast<const T*>(x);
   const T* x2r = static_cast<const T*>(x2);
   const Geo g = reduce_geometry(reinterpret_cast<const void*>(bn_bwd_reduce_dual_kernel<T>), rows, C);
-  const Fin fin = bwd_fin(dw, db, dw2, db2);
   bn_bwd_reduce_dual_kernel<T><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(dyr, mask, xr, x2r, sm, si, sm2, si2,
-                                                                             rows, (int)C, g, ws, ws2, fin);
+                                                                             rows, (int)C, g, ws, ws2);
   FLUXMPI_HIP_CHECK(hipGetLastError());
-  if (fin.mode == 0) {
-    bn_finalize_bwd2_kernel<<<dim3(finalize_blocks(C), 2), kFinCh * kFinGroups, 0, s>>>(ws, ws2, (int)C, dw, db, dw2,
-                                                                                        db2);
-    FLUXMPI_HIP_CHECK(hipGetLastError());
-  }
+  bn_finalize_bwd2_kernel<<<dim3(finalize_blocks(C), 2), kFinCh * kFinGroups, 0, s>>>(ws, ws2, (int)C, dw, db, dw2,
+                                                                                      db2);
+  FLUXMPI_HIP_CHECK(hipGetLastError());
   const int64_t nvec = rows * C / 8;
   auto k = bn_bwd_dx_dual_kernel<T>;
   k<<<elementwise_grid(reinterpret_cast<const void*>(k), 0, nvec), kThreads, 0, s>>>(
@@ -1101,15 +979,12 @@ void bn_stats_finalize(const void* x, const float* w, const float* b, float* rm,
                        float* scale, float* shift, float* ws, int64_t rows, int64_t C, float momentum, float eps,
                        int stats_ready, int dtype, hipStream_t s, int64_t* nbt) {
   check(C);
-  // the stats pass finalizes in its last workgroup unless the consumer wants the GEMM affine
-  // (scale / shift: only the finalize kernel writes it)
-  const Fin fin = (stats_ready || scale != nullptr) ? no_fin() : fwd_fin(rows, momentum, eps, sm, si, rm, rv, nbt);
   if (!stats_ready) {
 #define STATS(T)                                                                                              \
   {                                                                                                          \
     const Geo g = reduce_geometry(reinterpret_cast<const void*>(bn_stats_kernel<T>), rows, C);               \
-    bn_stats_kernel<T><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(static_cast<const T*>(x), rows, (int)C, g, ws, \
-                                                                     fin);                                     \
+    bn_stats_kernel<T><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(static_cast<const T*>(x), rows, (int)C, g, \
+                                                                     ws);                                      \
   }
     switch (dtype) {
       case kBF16: STATS(bf16) break;
@@ -1120,11 +995,9 @@ void bn_stats_finalize(const void* x, const float* w, const float* b, float* rm,
 #undef STATS
     FLUXMPI_HIP_CHECK(hipGetLastError());
   }
-  if (fin.mode == 0) {
-    bn_finalize_fwd_kernel<<<finalize_blocks(C), kFinCh * kFinGroups, 0, s>>>(ws, (int)C, rows, momentum, eps, sm, si, rm,
-                                                                              rv, w, b, scale, shift, nbt);
-    FLUXMPI_HIP_CHECK(hipGetLastError());
-  }
+  bn_finalize_fwd_kernel<<<finalize_blocks(C), kFinCh * kFinGroups, 0, s>>>(ws, (int)C, rows, momentum, eps, sm, si, rm,
+                                                                            rv, w, b, scale, shift, nbt);
+  FLUXMPI_HIP_CHECK(hipGetLastError());
 }
 
 void bn_apply(const void* x, void* y, const void* res, const float* w, const float* b, const float* sm,

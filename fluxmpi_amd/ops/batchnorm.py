@@ -37,12 +37,12 @@ def _nhwc(x: torch.Tensor) -> torch.Tensor:
 _WS: dict = {}
 _SHARDS = 64  # == kShards in csrc/kernels/{batchnorm,gemm}.hip
 _MAXC = 2048
-# [_SHARDS][2][_MAXC] shards + the arrival counter of the in-kernel finalize (kCntOff in batchnorm.hip)
+# [_SHARDS][2][_MAXC] shards (+ 64 floats of slack)
 _WS_FLOATS = _SHARDS * 2 * _MAXC + 64
 
 
 def _workspace(x: torch.Tensor) -> torch.Tensor:
-    """Persistent zeroed [64][2][2048] fp32 accumulator (+ an arrival counter) per (device, stream).
+    """Persistent zeroed [64][2][2048] fp32 accumulator per (device, stream).
 
     The kernels leave it zeroed after every call (the finalize — a kernel of its own, or the
     last workgroup of the reduction kernel — re-zeroes the shards it consumes), so there is no

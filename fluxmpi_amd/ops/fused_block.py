@@ -32,7 +32,6 @@ import torch
 
 from . import _ext
 from . import graddst
-from . import streams
 from .batchnorm import BNStatsLink, GradLink, SideGradLink, _dual_workspace, _link_workspace, _workspace, bn_counter  # noqa: F401 (links re-exported)
 from . import gemm as G
 from . import groupnorm as _GN
@@ -138,8 +137,7 @@ class _Conv1x1Stats(torch.autograd.Function):
         dc2 = _nhwc2d(dc)
         # weight gradient first, on the side stream: it overlaps the input-gradient chain
         with graddst.into(weight):  # into the DDP bucket slice when one is attached
-            dw = streams.run(lambda: conv1x1_wgrad(dc2, _nhwc2d(x), out_dtype=weight.dtype).view_as(weight), dc, x,
-                             param=weight)
+            dw = conv1x1_wgrad(dc2, _nhwc2d(x), out_dtype=weight.dtype).view_as(weight)
         dx = _dgrad_nhwc(dc2, weight, x, ctx.link, ctx.bnlink) if ctx.needs_input_grad[0] else None
         return dx, dw, None, None
 
@@ -225,7 +223,7 @@ class _Conv1x1Hybrid(torch.autograd.Function):
             if _w256_ok(co, ci, dc):
                 from .linear import weight_grad
                 impls["w256"] = lambda: weight_grad(_nhwc2d(dc), _nhwc2d(x), weight.dtype).view(co, ci, 1, 1)
-            dw = streams.run(lambda: wgrad_best(("1x1", tuple(x.shape), co), impls, param=weight), dc, x, param=weight)
+            dw = wgrad_best(("1x1", tuple(x.shape), co), impls, param=weight)
         dx = _dgrad_nhwc(_nhwc2d(dc), weight, x, ctx.link, ctx.bnlink) if ctx.needs_input_grad[0] else None
         return dx, dw, None, None, None
 
@@ -321,7 +319,7 @@ class _Conv1x1Downsample(torch.autograd.Function):
             else:
                 dx = Stride2Grad(dxc).expand(x.shape)
         if need_w and not (need_x and dx is None):
-            dw = streams.run(lambda: _ds_wgrad(dc, x, weight, s), dc, x, param=weight)
+            dw = _ds_wgrad(dc, x, weight, s)
         elif need_w or (need_x and dx is None):
             dx_m, dw = torch.ops.aten.convolution_backward(dc, x, weight, None, [s, s], [0, 0], [1, 1], False,
                                                            [0, 0], 1, [need_x and dx is None, need_w, False])[:2]
@@ -541,9 +539,7 @@ class _BNReluConv1x1(torch.autograd.Function):
         # dW = dc3^T @ relu(bn(c2))  — the activation is rebuilt on the fly in the B-operand load
         # (side stream: overlaps the input-gradient chain below)
         with graddst.into(weight):
-            dw = streams.run(lambda: conv1x1_wgrad(dc3_2d, c2_2d, in_affine=(scale, shift),
-                                                   out_dtype=weight.dtype).view_as(weight), dc3, c2, scale, shift,
-                             param=weight)
+            dw = conv1x1_wgrad(dc3_2d, c2_2d, in_affine=(scale, shift), out_dtype=weight.dtype).view_as(weight)
         # d(relu(bn(c2))) = dc3 @ W with the BN-backward reductions (ReLU mask recomputed from c2)
         # accumulated in the same GEMM's epilogue, then the BN backward without its reduce pass
         da = conv1x1_dgrad(dc3_2d, weight.reshape(co, ch), bn_bwd=(c2_2d, w32, b32, mean, inv, None, 2),
@@ -580,10 +576,10 @@ class _Conv3x3(torch.autograd.Function):
         # (inside groupnorm.skip_param_grads — the DEQ adjoint's VJPs w.r.t. activations only — the
         # filter gradient is not wanted although needs_input_grad, fixed at forward time, says so)
         if ctx.needs_input_grad[1] and not _GN._SKIP_PARAM_GRADS:
-            dw = streams.run(lambda: wgrad_best(("3x3", tuple(x.shape), weight.shape[0]), {
+            dw = wgrad_best(("3x3", tuple(x.shape), weight.shape[0]), {
                 "miopen": lambda: torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [1, 1], [1, 1], False,
                                                                       [0, 0], 1, [False, True, False])[1],
-                "ours": lambda: G.conv3x3_wgrad(dy, x)}, param=weight), dy, x, param=weight)
+                "ours": lambda: G.conv3x3_wgrad(dy, x)}, param=weight)
         dx = None
         if ctx.needs_input_grad[0]:
             bl = ctx.bnlink
@@ -659,10 +655,10 @@ class _Conv3x3S2(torch.autograd.Function):
             dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = None
         if ctx.needs_input_grad[1]:
-            dw = streams.run(lambda: wgrad_best(("3x3s2", tuple(x.shape), weight.shape[0]), {
+            dw = wgrad_best(("3x3s2", tuple(x.shape), weight.shape[0]), {
                 "miopen": lambda: torch.ops.aten.convolution_backward(dy, x, weight, None, [2, 2], [1, 1], [1, 1], False,
                                                                       [0, 0], 1, [False, True, False])[1],
-                "ours": lambda: G.conv3x3_wgrad_s2(dy, x)}, param=weight), dy, x, param=weight)
+                "ours": lambda: G.conv3x3_wgrad_s2(dy, x)}, param=weight)
         if ctx.needs_input_grad[0]:
             dx = torch.ops.aten.convolution_backward(dy, x, weight, None, [2, 2], [1, 1], [1, 1], False, [0, 0], 1,
                                                      [True, False, False])[0]

@@ -3,7 +3,7 @@
 
 GELU form (``FLUXMPI_GELU`` / :func:`set_form`): ``tanh`` (default) — NNlib's ``gelu``, the
 activation of the reference's Lux / Metalhead ViT (``x/2 (1 + tanh(sqrt(2/pi)(x + 0.044715
-x^3)))``) — or ``erf`` (exact). Both run the same kernels (``gelu.hip``, gemm256's epilogues)
+x^3)))``) — or ``erf`` (exact). Both run the same kernels (``gelu.hip``, gemm_nt's epilogues)
 at the same speed (ViT-B/16 7.04k / 7.06k tanh vs 7.04k / 7.05k erf, same box). A hipBLASLt
 bias + GELU epilogue that also writes the pre-activation (``GELU_AUX_BIAS``, which would drop
 the forward's elementwise GELU pass) has no gfx950 solution in either hipBLASLt of the image
@@ -105,31 +105,32 @@ def gelu_bwd_bias(dy: torch.Tensor, h: torch.Tensor, bias_dtype=torch.float32):
 class GeluLink:
     """Hand-off between ``linear_gelu`` (fc1 + GELU) and the Linear that consumes its output
     (fc2, inside ``linear_add_layer_norm``): the consumer's input-gradient GEMM applies the
-    GELU derivative and reduces fc1's bias gradient in its epilogue (gemm256.hip EPI 2) and
+    GELU derivative and reduces fc1's bias gradient in its epilogue (gemm_nt.hip EPI 2) and
     deposits ``(dh, db)`` here; fc1's backward then skips its own GELU pass. The gradient
-    autograd passes between the two nodes is a zero-stride placeholder (never read)."""
+    autograd passes between the two nodes is a zero-stride placeholder (never read). ``bias``:
+    fc1's bias parameter (its gradient's DDP bucket slice, ``ops/graddst.py``)."""
 
-    __slots__ = ("h", "bias_dtype", "dh", "db")
+    __slots__ = ("h", "bias_dtype", "bias", "dh", "db")
 
     def __init__(self):
-        self.h = self.bias_dtype = self.dh = self.db = None
+        self.h = self.bias_dtype = self.bias = self.dh = self.db = None
 
     def take(self):
         out = (self.dh, self.db)
-        self.h = self.dh = self.db = None
+        self.h = self.bias = self.dh = self.db = None
         return out
 
 
 class _LinearGeluFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, link=None):
-        from . import gemm256
-        _sync(_ext.get(required=True))  # the backward kernels (gelu.hip, gemm256 EPI 2) read the form
+        from . import gemm_nt
+        _sync(_ext.get(required=True))  # the backward kernels (gelu.hip, gemm_nt EPI 2) read the form
         n_out, n_in = weight.shape
         rows = x.numel() // n_in
-        if x.is_contiguous() and gemm256.supported(rows, n_out, n_in, x, weight):
+        if x.is_contiguous() and gemm_nt.supported(rows, n_out, n_in, x, weight, fused=True):
             # bias + GELU in the GEMM epilogue: h and gelu(h) from the same registers
-            h2, g2 = gemm256.linear_fwd(x.view(rows, n_in), weight, bias, gelu=True)
+            h2, g2 = gemm_nt.linear_fwd(x.view(rows, n_in), weight, bias, gelu=True)
             h, g = h2.view(*x.shape[:-1], n_out), g2.view(*x.shape[:-1], n_out)
         else:
             h = F.linear(x, weight, bias)
@@ -139,7 +140,7 @@ class _LinearGeluFn(torch.autograd.Function):
         ctx.bias_dtype = bias.dtype if bias is not None else None
         ctx.link = link
         if link is not None:
-            link.h, link.bias_dtype = h, ctx.bias_dtype or torch.float32
+            link.h, link.bias_dtype, link.bias = h, ctx.bias_dtype or torch.float32, bias
         return g
 
     @staticmethod

@@ -23,18 +23,6 @@ SHARDS = 64  # == kShards in csrc/kernels/{batchnorm,gemm}.hip
 NBUF = int(os.environ.get("FLUXMPI_GEMM_NBUF", "0"))
 # GEMM kernel: 0 = launcher's choice, 1 = register-staged (gemm.hip), 2 = LDS-DMA pipelined (gemm_glds.hip)
 ENGINE = int(os.environ.get("FLUXMPI_GEMM_ENGINE", "0"))
-# 3x3 convolutions on the LDS-halo kernel (conv3x3.hip) — opt-in: at ResNet-50's batch-256 shapes
-# it runs 100-115 us per forward vs 89-111 us for gemm_glds.hip's implicit GEMM (r3 sweep,
-# profiles/r3_conv3x3_halo.md: one workgroup per CU leaves both its LDS-DMA and its MFMA phase
-# latency-bound), so the implicit GEMM stays the default
-HALO = os.environ.get("FLUXMPI_CONV3X3_HALO", "0") == "1"
-
-
-def halo_ok(n: int, h: int, w: int, c: int, co: int) -> bool:
-    """The LDS-halo 3x3 kernel takes this shape (C % 32 == 0, Co % 64 == 0, the halo fits LDS)."""
-    return HALO and _ext.available() and bool(_ext.get(required=True).conv3x3_halo_supported(n, h, w, c, co))
-
-
 def _stream(t):
     return torch.cuda.current_stream(t.device).cuda_stream
 
@@ -183,11 +171,6 @@ def conv3x3_fwd(x: torch.Tensor, w: torch.Tensor, in_affine=None, stats: torch.T
     note_filter(w)
     y = out if out is not None else torch.empty(n, h, wd, co, device=x.device, dtype=x.dtype).permute(0, 3, 1, 2)
     M = n * h * wd
-    if not engine and in_affine is None and x.dtype == torch.bfloat16 and halo_ok(n, h, wd, c, co) and \
-            y.is_contiguous(memory_format=torch.channels_last):
-        _ext.get(required=True).conv3x3_halo(xs.data_ptr(), w2.data_ptr(), y.data_ptr(), _ptr(stats), n, h, wd, c,
-                                             co, _stream(x))
-        return y
     gemm(xs, w2, y, M=M, N=co, K=9 * c, lda=c, ldb=9 * c, ldc=co, mode=1 if stats is not None else 0,
          a_affine=in_affine, stats=stats, conv=(h, wd, c), engine=engine or None)
     return y
@@ -225,11 +208,6 @@ def conv3x3_dgrad(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = 
     dx = out if out is not None else torch.empty(n, h, wd, ci, device=dy.device, dtype=dy.dtype).permute(0, 3, 1, 2)
     if bn_bwd is not None:
         assert stats is not None and bn_bwd[0].shape == (n * h * wd, ci) and ENGINE != 1
-    elif residual is None and ENGINE != 1 and dy.dtype == torch.bfloat16 and halo_ok(n, h, wd, co, ci) and \
-            dx.is_contiguous(memory_format=torch.channels_last):
-        _ext.get(required=True).conv3x3_halo(dys.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, n, h, wd, co, ci,
-                                             _stream(dy))
-        return dx
     r2 = None
     if residual is not None:
         assert residual.shape == dx.shape and residual.dtype == dy.dtype and bn_bwd is None

@@ -1,0 +1,108 @@
+"""Token-major Linear GEMMs on the ping-pong 256x256 NT kernel (``csrc/kernels/gemm_nt.hip``).
+
+* :func:`linear_fwd` — ``y = x W^T + b`` (``gelu=True``: also ``g = gelu(y)`` from the same
+  registers: fc1 of a transformer MLP writes its pre-activation and its activation in one pass,
+  no elementwise GELU kernel);
+* :func:`linear_dgrad` — ``dx = dy W`` on ``W^T`` (one ``transpose_bf16`` of the 0.6-4.7 MB
+  weight per call, so both operands of the GEMM stay k-contiguous); ``gelu_h=h``: ``dh = dx *
+  gelu'(h)`` and the column sums of ``dh`` — the previous Linear's bias gradient, written into
+  its DDP bucket slice when one is attached (``ops/graddst.py``) — in the epilogue.
+
+The ViT-B/16 Linears at batch 256 (M = 50432 = 197 x 256 tokens, N and K in {768, 2304, 3072})
+tile exactly; :func:`supported` says whether a call qualifies, callers keep the PyTorch path
+otherwise. Numerics: bf16 operands, fp32 accumulation, one bf16 rounding of each output (the
+GELU of the ROUNDED pre-activation, like ``F.gelu(F.linear(...))``).
+
+``FLUXMPI_GEMM_NT``: ``all`` (default) every qualifying forward / input gradient; ``fused`` only
+the calls that carry an epilogue fusion (GELU forward / backward); ``0`` never (hipBLASLt).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from . import _ext
+from . import graddst
+from .multi_tensor import DTYPE_CODE
+
+MODE = os.environ.get("FLUXMPI_GEMM_NT", "all").lower()
+ENABLED = MODE != "0"
+
+
+def _stream(t):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def supported(rows: int, n_out: int, k: int, *tensors: torch.Tensor, fused: bool = False) -> bool:
+    """Whether gemm_nt takes ``[rows, k] x [n_out, k]^T`` (both operands k-contiguous after the
+    weight transpose of an input gradient) under the current mode."""
+    if not ENABLED or not tensors or not tensors[0].is_cuda:
+        return False
+    if MODE not in ("all", "1") and not (fused and MODE == "fused"):
+        return False
+    if any(t.dtype != torch.bfloat16 for t in tensors):
+        return False
+    C = _ext.get(required=False)
+    return C is not None and hasattr(C, "gemm_nt") and bool(C.gemm_nt_supported(rows, n_out, k, k, k, n_out))
+
+
+def weight_t(weight: torch.Tensor) -> torch.Tensor:
+    """``weight.t().contiguous()`` by the 16-B-vector transpose kernel."""
+    C = _ext.get(required=True)
+    w = weight.contiguous()
+    r, c = w.shape
+    wt = torch.empty(c, r, device=w.device, dtype=w.dtype)
+    C.transpose_bf16(w.data_ptr(), wt.data_ptr(), r, c, c, r, _stream(w))
+    return wt
+
+
+def linear_fwd(x2: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None, gelu: bool = False):
+    """``x2 [M, K] @ weight[N, K]^T + bias`` -> ``y [M, N]`` (bf16); ``gelu``: ``(y, gelu(y))``."""
+    C = _ext.get(required=True)
+    m, k = x2.shape
+    n = weight.shape[0]
+    x2 = x2.contiguous()
+    w = weight.contiguous()
+    y = torch.empty(m, n, device=x2.device, dtype=x2.dtype)
+    g = torch.empty_like(y) if gelu else None
+    if gelu:
+        from .gelu import _sync
+        _sync(C)  # EPI 1 computes the selected GELU form
+    b = bias.contiguous() if bias is not None else None
+    C.gemm_nt(x2.data_ptr(), w.data_ptr(), y.data_ptr(), g.data_ptr() if gelu else 0,
+              b.data_ptr() if b is not None else 0, int(b is not None and b.dtype == torch.float32), 0, 0,
+              k, k, n, m, n, k, 1 if gelu else 0, _stream(x2))
+    return (y, g) if gelu else y
+
+
+def linear_dgrad(dy2: torch.Tensor, weight: torch.Tensor, gelu_h: torch.Tensor | None = None,
+                 bias_dtype=torch.float32, bias_param: torch.Tensor | None = None):
+    """``dy2 [M, N] @ weight [N, K]`` -> ``dx [M, K]``. With ``gelu_h`` (the GELU input that
+    produced this Linear's input, ``[M, K]``): returns ``(dh, db)`` with ``dh = dx * gelu'(h)``
+    and ``db = dh.sum(0)`` in ``bias_dtype`` (delivered into ``bias_param``'s bucket slice)."""
+    C = _ext.get(required=True)
+    m, n = dy2.shape
+    k = weight.shape[1]
+    dy2 = dy2.contiguous()
+    wt = weight_t(weight)  # [K][N]: the B operand, k(= N)-contiguous
+    dx = torch.empty(m, k, device=dy2.device, dtype=dy2.dtype)
+    s = _stream(dy2)
+    if gelu_h is None:
+        C.gemm_nt(dy2.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, 0, 0, 0, 0, n, n, k, m, k, n, 0, s)
+        return dx
+    from .gelu import _sync
+    _sync(C)  # EPI 2 differentiates the selected GELU form
+    h = gelu_h.reshape(m, k).contiguous()
+    rows = C.gemm_nt_colpart_rows(m)
+    part = torch.empty(rows, k, device=dy2.device, dtype=torch.float32)
+    C.gemm_nt(dy2.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, 0, 0, h.data_ptr(), part.data_ptr(), n, n, k, m, k, n,
+              2, s)
+    odt = bias_dtype if bias_dtype in (torch.float32, torch.bfloat16) else torch.float32
+    with graddst.into(bias_param):
+        db = graddst.empty((k,), odt, dy2.device)
+    C.gemm_splitk_reduce(part.data_ptr(), rows, k, db.data_ptr(), DTYPE_CODE[odt], s)
+    return dx, db.to(bias_dtype)
+
+
+__all__ = ["supported", "weight_t", "linear_fwd", "linear_dgrad", "ENABLED", "MODE"]

@@ -1,8 +1,8 @@
 """``nn.Linear`` for token-major activations with MI355X-shaped GEMMs.
 
-Forward and input gradient run on ``gemm256.hip`` (256x256 tiles, LDS-DMA ring, bias in the
-epilogue; ``ops/gemm256.py``) when the token count and widths tile exactly (ViT-B/16: 50432 =
-197 x 256 tokens), else hipBLASLt (``F.linear``, ``dy @ W``). The weight gradient ``dW = dY^T X`` is the awkward one:
+Forward and input gradient run on ``gemm_nt.hip`` (persistent ping-pong 256x256 MFMA tiles,
+bias in the epilogue; ``ops/gemm_nt.py``) when the token count and widths tile exactly
+(ViT-B/16: 50432 = 197 x 256 tokens), else hipBLASLt (``F.linear``, ``dy @ W``). The weight gradient ``dW = dY^T X`` is the awkward one:
 K = tokens (50432 for ViT-B/16 at batch 256) and a small output (768..3072 squared), so
 hipBLASLt's 256x256 tiles leave most of the 256 CUs idle (36-108 workgroups; 312-431 us
 per call, ``profiles/r1_vit_b16_s61_steady.md``). It runs on our split-K MFMA kernels
@@ -23,7 +23,6 @@ import torch.nn.functional as F
 
 from . import _ext
 from . import graddst
-from . import streams
 from .multi_tensor import DTYPE_CODE
 
 # (N_out, N_in) -> split-K factor, from scripts/bench_vit_gemm.py on MI355X (M = 50432 tokens)
@@ -101,7 +100,7 @@ class _LinearFn(torch.autograd.Function):
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
         ctx.bias_dtype = bias.dtype if bias is not None else None
-        ctx.bias = bias  # the leaf itself (not saved data): streams.run checks its .grad
+        ctx.bias = bias  # the leaf itself (not saved data): the bias gradient's bucket slice
         return fwd(x, weight, bias)
 
     @staticmethod
@@ -117,39 +116,33 @@ class _LinearFn(torch.autograd.Function):
         need_w = ctx.needs_input_grad[1]
         need_b = ctx.has_bias and ctx.needs_input_grad[2]
 
-        def grads():
-            # written straight into the DDP bucket slices when a communicating engine is attached
+        # written straight into the DDP bucket slices when a communicating engine is attached
+        if need_w:
             with graddst.into(w):
-                gw = (weight_grad(dy2, x2, w.dtype) if native else dy2.t() @ x2) if need_w else None
+                dw = weight_grad(dy2, x2, w.dtype) if native else dy2.t() @ x2
+        if need_b:
             with graddst.into(ctx.bias):
-                gb = (bias_grad(dy2, ctx.bias_dtype) if native else dy2.sum(0).to(ctx.bias_dtype)) if need_b else None
-            return gw, gb
-
-        if need_w or need_b:
-            # weight / bias gradients on the side stream, overlapping the input-gradient chain
-            # both parameters: if either already holds a .grad, autograd accumulates into it on
-            # the main stream, which must not race a side-stream producer
-            dw, db = streams.run(grads, dy2, x2, param=[w if need_w else None, ctx.bias if need_b else None])
+                db = bias_grad(dy2, ctx.bias_dtype) if native else dy2.sum(0).to(ctx.bias_dtype)
         dx = dgrad(dy2, w).reshape(x.shape) if ctx.needs_input_grad[0] else None
         return dx, dw, db
 
 
 def fwd(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None) -> torch.Tensor:
-    """``F.linear`` — on gemm256.hip (bias in the epilogue) when the shape tiles exactly."""
-    from . import gemm256
+    """``F.linear`` — on gemm_nt.hip (bias in the epilogue) when the shape tiles exactly."""
+    from . import gemm_nt
     n_out, n_in = weight.shape
     rows = x.numel() // n_in if n_in else 0
-    if x.is_contiguous() and gemm256.supported(rows, n_out, n_in, x, weight):
-        return gemm256.linear_fwd(x.view(rows, n_in), weight, bias).view(*x.shape[:-1], n_out)
+    if x.is_contiguous() and gemm_nt.supported(rows, n_out, n_in, x, weight):
+        return gemm_nt.linear_fwd(x.view(rows, n_in), weight, bias).view(*x.shape[:-1], n_out)
     return F.linear(x, weight, bias)
 
 
 def dgrad(dy2: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
-    """``dy2 [rows, N_out] @ weight [N_out, N_in]`` — on gemm256.hip when the shape tiles exactly."""
-    from . import gemm256
+    """``dy2 [rows, N_out] @ weight [N_out, N_in]`` — on gemm_nt.hip (over W^T) when the shape tiles."""
+    from . import gemm_nt
     n_out, n_in = weight.shape
-    if dy2.is_contiguous() and gemm256.supported(dy2.shape[0], n_in, n_out, dy2, weight, b_t=True):
-        return gemm256.linear_dgrad(dy2, weight)
+    if dy2.is_contiguous() and gemm_nt.supported(dy2.shape[0], n_in, n_out, dy2, weight):
+        return gemm_nt.linear_dgrad(dy2, weight)
     return dy2 @ weight
 
 

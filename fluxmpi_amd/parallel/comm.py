@@ -33,11 +33,6 @@ import torch.distributed as dist
 
 from ..ops import _ext
 
-# RcclComm's bucket fence: torch's Stream.wait_stream (default) or, FLUXMPI_NATIVE_FENCE=1, a
-# pooled event without the system-scope release (csrc/comm/fence.cpp). MEASURED NO GAIN (rd3zd,
-# ResNet-50 --force-comm, same box: 12.09k / 12.15k native vs 12.16k torch): the N=1 comm tax is
-# not the per-bucket event's release
-_NATIVE_FENCE = os.environ.get("FLUXMPI_NATIVE_FENCE", "0") == "1"
 # RcclComm's stream priority: 0 normal (default), -1 high (FLUXMPI_COMM_PRIORITY=-1). Measured
 # (rd3zh / rd3zi, ResNet-50 --force-comm, same boxes): the high-priority queue cost 1.0-2.9 % of
 # the step at N=1 against 0.25-0.5 % at normal priority, and with an emulated RCCL CU footprint
@@ -513,12 +508,7 @@ class RcclComm(Communicator):
     # --- helpers ---------------------------------------------------------------
     def _enter(self, *tensors):
         cur = torch.cuda.current_stream(self.device)
-        if _NATIVE_FENCE:
-            # pooled event without the system-scope release (csrc/comm/fence.cpp): recorded on
-            # the compute stream once per gradient bucket
-            _ext.get(required=True).stream_fence(cur.cuda_stream, self.stream.cuda_stream)
-        else:
-            self.stream.wait_stream(cur)
+        self.stream.wait_stream(cur)
         return cur
 
     def _exit(self, tensors, result, async_op, post=None):

@@ -57,7 +57,6 @@ from ..ops import multi_tensor as mt
 from ..ops import _ext
 from ..ops import graddst
 from ..ops import optim as fused
-from ..ops import streams
 from ..utils.config import get_config
 from ..utils import profiling
 from ..utils.debug import Watchdog, check_replicas, check_same_structure
@@ -398,15 +397,7 @@ class DDP:
         b.launched = True
         if not self.communicate:
             return
-        side = streams.pending(self.device)
-        if side is not None:
-            # weight gradients of this backward run on the side stream (ops/streams.py): pack and
-            # launch the collective from it, after the main stream's gradients (BatchNorm, bias)
-            side.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(side):
-                self._launch_comm(b)
-        else:
-            self._launch_comm(b)
+        self._launch_comm(b)
 
     def _launch_comm(self, b: _Bucket):
         self._pack(b)

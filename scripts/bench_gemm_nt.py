@@ -1,5 +1,5 @@
 #!/usr/bin/env python
-"""gemm_nt.hip (ping-pong 8-wave 256x256 NT GEMM) vs hipBLASLt (torch) vs gemm256.hip, TFLOP/s on
+"""gemm_nt.hip (ping-pong 8-wave 256x256 NT GEMM) vs hipBLASLt (torch), TFLOP/s on
 uniform [-1, 1) bf16 operands (cdna_hip_programming.md rule 25), interleaved rounds in one process.
 
 Shapes: 4096^3 and the ViT-B/16 Linears at batch 256 (M = 50432 tokens), forward (x W^T),
@@ -119,9 +119,6 @@ def main():
             best.setdefault("nt_bias", []).append(t_us(lambda: ours(0, bias_=bias)))
             best.setdefault("nt_gelu", []).append(t_us(lambda: ours(1, bias_=bias)))
             best.setdefault("nt_epi2", []).append(t_us(lambda: ours(2, h=h, part=part)))
-            if hasattr(C, "gemm256") and m % 256 == 0 and n % 256 == 0:
-                best.setdefault("g256", []).append(t_us(lambda: C.gemm256(
-                    a.data_ptr(), w.data_ptr(), c.data_ptr(), 0, 0, 0, 0, 0, k, k, n, m, n, k, False, 0, st)))
         rec = {"shape": name, "M": m, "N": n, "K": k}
         for key, v in best.items():
             us = min(v)

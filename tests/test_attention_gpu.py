@@ -28,19 +28,13 @@ SHAPES = [(4, 197, 12), (2, 50, 4), (1, 7, 2), (2, 64, 3), (1, 1, 1), (3, 300, 2
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("fwd_mode", [0, 1])
 @pytest.mark.parametrize("b,t,heads", SHAPES + [(64, 197, 12)])
-def test_attn_fwd_vs_fp32(gpu_ext, b, t, heads, fwd_mode):
-    """fwd_mode 0: two workgroups per head; 1: persistent workgroups looping over heads with the
-    next head's K / V staged during this one's math (64 x 12 heads: 3 heads per workgroup)."""
+def test_attn_fwd_vs_fp32(gpu_ext, b, t, heads):
+    """The resident forward (two workgroups per head) vs fp32."""
     from fluxmpi_amd.ops.attention import attn_fwd_packed
     torch.manual_seed(0)
     xb = (torch.randn(b, t, 3 * heads * 64, device="cuda") * 1.5).to(torch.bfloat16)
-    gpu_ext.attn_set_fwd_mode(fwd_mode)
-    try:
-        out, stats = attn_fwd_packed(xb, heads)
-    finally:
-        gpu_ext.attn_set_fwd_mode(-1)
+    out, stats = attn_fwd_packed(xb, heads)
     ref = _ref(xb.float(), heads)
     assert out.shape == ref.shape and out.dtype == torch.bfloat16
     assert _rel(out, ref) < 1e-2

@@ -77,29 +77,24 @@ def test_force_comm_bitwise_equal(gpu_ext, grad_mode, dtype):
         assert torch.equal(p, q)
 
 
-def test_force_comm_native_fence(gpu_ext, monkeypatch):
-    """The opt-in bucket fence (csrc/comm/fence.cpp, FLUXMPI_NATIVE_FENCE=1) orders the
-    comm stream after the backward kernels exactly like wait_stream: bitwise-equal training."""
+def test_rccl_self_report(gpu_ext):
+    """The native communicator reports itself (ncclCommCount / ncclCommUserRank / ncclCommCuDevice):
+    what bench.py checks against WORLD_SIZE / RANK / the pinned device before timing."""
     _init()
-    from fluxmpi_amd import optimisers as O
-    from fluxmpi_amd.parallel import comm as CM
-    from fluxmpi_amd.parallel.ddp import DDP
+    import fluxmpi_amd as FluxMPI
+    from fluxmpi_amd.parallel import runtime
+    from fluxmpi_amd.parallel.comm import RcclComm
+    from fluxmpi_amd.parallel.selfcheck import CommSelfCheckError, comm_selfcheck
 
-    monkeypatch.setattr(CM, "_NATIVE_FENCE", True)
-    m1, m2 = _mlp(1, torch.bfloat16), _mlp(1, torch.bfloat16)
-    kw = dict(bucket_mb=0.1, first_bucket_mb=0.05)
-    d1 = DDP(m1, O.Adam(1e-3), force_comm=True, **kw)
-    d2 = DDP(m2, O.Adam(1e-3), **kw)
-    assert isinstance(d1.comm, CM.RcclComm) and len(d1.buckets) >= 3
-    x, y = _data(torch.bfloat16)
-    for _ in range(4):
-        for d in (d1, d2):
-            F.mse_loss(d(x).float(), y.float()).backward()
-        d1.step()
-        d2.step()
-    torch.cuda.synchronize()
-    for p, q in zip(m1.parameters(), m2.parameters()):
-        assert torch.equal(p, q)
+    c = runtime.device_comm()
+    assert isinstance(c, RcclComm)
+    rep = c.self_report()
+    assert rep["rccl_nranks"] == FluxMPI.total_workers() == 1
+    assert rep["rccl_rank"] == 0 and rep["rccl_device"] == FluxMPI.device().index
+    assert rep["comm_priority"] == c.priority and rep["rccl_version"] > 0
+    assert comm_selfcheck(c, 1, 0, FluxMPI.device().index) == rep
+    with pytest.raises(CommSelfCheckError):
+        comm_selfcheck(c, 2, 0, FluxMPI.device().index)
 
 
 def test_force_comm_bench_construction(gpu_ext):

@@ -1,0 +1,109 @@
+"""gemm_nt.hip (ViT forward / input-gradient GEMMs with fused epilogues) vs PyTorch fp32: every
+ViT-B/16 Linear shape at batch 256 (M = 50432 tokens), plus odd k-tile counts, the minimum K and
+tile counts that are not a multiple of the CU count (the persistent kernel's tile stream and its
+LDS buffer parity cross tile boundaries)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+M_VIT = 50432
+# (name, rows, N, K): forward x W^T and input gradient dy W of qkv / proj / fc1 / fc2
+VIT_FWD = [("qkv", M_VIT, 2304, 768), ("proj", M_VIT, 768, 768), ("fc1", M_VIT, 3072, 768),
+           ("fc2", M_VIT, 768, 3072)]
+VIT_DGRAD = [("qkv", M_VIT, 2304, 768), ("proj", M_VIT, 768, 768), ("fc1", M_VIT, 3072, 768),
+             ("fc2", M_VIT, 768, 3072)]  # (rows, N_out, N_in): dx [rows, N_in] = dy [rows, N_out] W
+SMALL = [(512, 768, 768), (768, 256, 3072), (256 * 41, 768, 832), (256 * 37, 512, 128), (256 * 300, 256, 192)]
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
+
+
+@pytest.fixture(params=["tanh", "erf"])
+def gelu_form(request):
+    from fluxmpi_amd.ops import gelu as GL
+    old = GL.FORM
+    GL.set_form(request.param)
+    yield request.param
+    GL.set_form(old)
+
+
+def _uni(*shape, scale=1.0):
+    return ((torch.rand(*shape, device="cuda") * 2 - 1) * scale).bfloat16()
+
+
+def _check_fwd(m, n, k, bias, gelu_form=None):
+    from fluxmpi_amd.ops import gelu as GL
+    from fluxmpi_amd.ops import gemm_nt as G
+    torch.manual_seed(0)
+    x = _uni(m, k)
+    w = _uni(n, k, scale=k ** -0.5)
+    b = None if bias is None else (torch.randn(n, device="cuda") * 0.5).to(torch.float32 if bias == "f32" else torch.bfloat16)
+    assert G.supported(m, n, k, x, w, fused=True)
+    y = G.linear_fwd(x, w, b)
+    ref = x.float() @ w.float().t() + (b.float() if b is not None else 0)
+    assert _rel(y, ref) < 5e-3
+    if gelu_form is not None:
+        yy, g = G.linear_fwd(x, w, b, gelu=True)
+        assert torch.equal(yy, y)
+        assert _rel(g, GL.gelu(y.float())) < 5e-3  # GELU of the rounded pre-activation
+
+
+def _check_dgrad(m, n_out, n_in, gelu_form=None):
+    from fluxmpi_amd.ops import gelu as GL
+    from fluxmpi_amd.ops import gemm_nt as G
+    torch.manual_seed(1)
+    dy = _uni(m, n_out)
+    w = _uni(n_out, n_in, scale=n_out ** -0.5)
+    assert G.supported(m, n_in, n_out, dy, w, fused=True)
+    dx = G.linear_dgrad(dy, w)
+    ref = dy.float() @ w.float()
+    assert _rel(dx, ref) < 5e-3
+    if gelu_form is not None:
+        h = _uni(m, n_in, scale=3.0)
+        dh, db = G.linear_dgrad(dy, w, gelu_h=h)
+        dh_ref = ref.bfloat16().float() * GL._gelu_grad_ref(h.float())
+        assert _rel(dh, dh_ref) < 5e-3
+        torch.testing.assert_close(db, dh.float().sum(0), rtol=1e-3, atol=2e-2)
+        _, db16 = G.linear_dgrad(dy, w, gelu_h=h, bias_dtype=torch.bfloat16)
+        assert db16.dtype == torch.bfloat16 and _rel(db16, db) < 1e-2
+
+
+@pytest.mark.parametrize("name,m,n,k", VIT_FWD)
+@pytest.mark.parametrize("bias", [None, "f32", "bf16"])
+def test_vit_fwd(gpu_ext, name, m, n, k, bias):
+    _check_fwd(m, n, k, bias)
+
+
+@pytest.mark.parametrize("name,m,n,k", VIT_FWD)
+def test_vit_fwd_gelu(gpu_ext, gelu_form, name, m, n, k):
+    _check_fwd(m, n, k, "f32", gelu_form)
+
+
+@pytest.mark.parametrize("name,m,n_out,n_in", VIT_DGRAD)
+def test_vit_dgrad(gpu_ext, gelu_form, name, m, n_out, n_in):
+    _check_dgrad(m, n_out, n_in, gelu_form)
+
+
+@pytest.mark.parametrize("m,n,k", SMALL)
+def test_small_and_odd_shapes(gpu_ext, gelu_form, m, n, k):
+    _check_fwd(m, n, k, "bf16", gelu_form)
+    _check_dgrad(m, n, k, gelu_form)
+
+
+def test_transpose_bf16(gpu_ext):
+    from fluxmpi_amd.ops import gemm_nt as G
+    for r, c in ((768, 3072), (3072, 768), (40, 72), (2304, 768)):
+        w = torch.randn(r, c, device="cuda").bfloat16()
+        assert torch.equal(G.weight_t(w), w.t())
+
+
+def test_unsupported_shapes(gpu_ext):
+    from fluxmpi_amd.ops import gemm_nt as G
+    x = torch.zeros(200, 768, device="cuda", dtype=torch.bfloat16)
+    w = torch.zeros(768, 768, device="cuda", dtype=torch.bfloat16)
+    assert not G.supported(200, 768, 768, x, w, fused=True)  # rows not a multiple of 256
+    assert not G.supported(256, 768, 768, x.float(), w, fused=True)
+    assert not G.supported(256, 768, 64, x, w, fused=True)  # K < 128
+    assert not G.supported(256, 768, 96, x, w, fused=True)  # K not a multiple of 64

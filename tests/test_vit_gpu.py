@@ -41,32 +41,6 @@ def test_packed_attention_vs_fp32(gpu_ext, b, t, heads, dh):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", [1, 2])
-@pytest.mark.parametrize("b,t,heads", [(4, 197, 12), (2, 50, 4), (3, 7, 2), (2, 256, 2), (2, 100, 3)])
-def test_packed_attention_fused_bwd_vs_fp32(gpu_ext, b, t, heads, mode):
-    """The one-kernel backwards vs fp32: mode 1 attn_bwd_fused_kernel (dQ through LDS atomics),
-    mode 2 attn_bwd_two_kernel (dq and dkv phases of one kernel over one LDS image pair)."""
-    from fluxmpi_amd.models.vit import packed_attention
-    gpu_ext.attn_set_bwd_fused(mode)
-    try:
-        torch.manual_seed(1)
-        x = torch.randn(b, t, 3 * heads * 64, device="cuda")
-        xa = x.to(torch.bfloat16).requires_grad_()
-        xr = x.to(torch.bfloat16).float().requires_grad_()
-        y = packed_attention(xa, heads)
-        yr = _ref_attention(xr, heads)
-        g = torch.randn_like(yr)
-        y.backward(g.to(torch.bfloat16))
-        yr.backward(g)
-        d = heads * 64
-        for part in range(3):  # dQ, dK, dV slots of the packed gradient
-            sl = slice(part * d, (part + 1) * d)
-            assert _rel(xa.grad[..., sl], xr.grad[..., sl]) < 3e-2, part
-    finally:
-        gpu_ext.attn_set_bwd_fused(-1)
-
-
-@pytest.mark.gpu
 def test_vit_tiny_step(gpu_ext):
     from fluxmpi_amd.models.vit import vit_tiny
     torch.manual_seed(0)

@@ -1,8 +1,8 @@
-"""Whole-model ViT numerics (VERDICT r2 next #8a): the fused bf16 ViT — gemm256 forward /
+"""Whole-model ViT numerics (VERDICT r2 next #8a): the fused bf16 ViT — gemm_nt forward /
 input-gradient GEMMs with bias / GELU / GELU-backward epilogues, the GELU link into fc2's
 input gradient, proj / fc2 + residual + LayerNorm nodes, packed attention, the CLS-only last
 block — against a plain PyTorch model with the same (bf16-rounded) weights, in fp32 and in
-bf16. Width 768, 197 tokens, depth 2, batch 256 (50432 rows: every gemm256 path is taken).
+bf16. Width 768, 197 tokens, depth 2, batch 256 (50432 rows: every gemm_nt path is taken).
 Criterion (the ResNet pattern of test_fused_block_gpu.py): the fused model's error against
 fp32 stays within a small multiple of plain bf16 PyTorch's error against fp32."""
 import math
