@@ -217,6 +217,10 @@ void transpose_filters(const std::vector<uintptr_t>& src, const std::vector<uint
                        hipStream_t stream);
 // out[e] = sum over s < splits of ws[s*n + e] (mode-3 split-K partials; ws is clobbered); out fp32 or bf16
 void gemm_splitk_reduce(const float* ws, int splits, int64_t n, void* out, int out_dtype, hipStream_t stream);
+// the same with the reduced row split into <= 3 segments of `seg` columns, each to its own output
+// (e.g. a LayerNorm's dw / db straight into two DDP bucket slices)
+void gemm_splitk_reduce_seg(const float* ws, int splits, int64_t n, int64_t seg, void* out0, void* out1, void* out2,
+                            int out_dtype, hipStream_t stream);
 // Weight gradient on 256 x 256 tiles (wgrad256.hip): ws[split][M][N] = sum over the split's k of
 // A[k][m] * B[k][n] (bf16 A [K][lda], B [K][ldb], M and N multiples of 256), fp32 partials.
 bool wgrad256_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);

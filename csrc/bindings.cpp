@@ -387,6 +387,11 @@ PYBIND11_MODULE(_C, m) {
         },
         py::arg("src"), py::arg("dst"), py::arg("co"), py::arg("ci"), py::arg("taps"), py::arg("stream"));
 
+  m.def("gemm_splitk_reduce_seg", [](uintptr_t ws, int splits, int64_t n, int64_t seg, uintptr_t o0, uintptr_t o1,
+                                     uintptr_t o2, int out_dtype, uintptr_t stream) {
+    gemm_splitk_reduce_seg(reinterpret_cast<const float*>(ws), splits, n, seg, reinterpret_cast<void*>(o0),
+                           reinterpret_cast<void*>(o1), reinterpret_cast<void*>(o2), out_dtype, S(stream));
+  });
   m.def("gemm_splitk_reduce",
         [](uintptr_t ws, int splits, int64_t n, uintptr_t out, int out_dtype, uintptr_t stream) {
           gemm_splitk_reduce(reinterpret_cast<const float*>(ws), splits, n, reinterpret_cast<void*>(out), out_dtype,

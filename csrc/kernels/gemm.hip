@@ -497,9 +497,22 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(GemmArgs p) {
 // (small dW, huge K) reduce in a few microseconds.
 constexpr int kReduceGroup = 16;
 
+// The reduced row's destination: columns [k seg, (k + 1) seg) go to p[k] (k < 3) — one launch
+// writes e.g. a LayerNorm's dw and db straight into their two DDP bucket slices. seg % 4 == 0,
+// so a float4 group never straddles two segments.
+template <typename TO>
+struct OutSeg {
+  TO* p[3];
+  int64_t seg;
+  __device__ __forceinline__ TO* at(int64_t e) const {
+    const int64_t k = e / seg;
+    return p[k] + (e - k * seg);
+  }
+};
+
 template <typename TO, bool FINAL>
 __global__ __launch_bounds__(kThreads) void splitk_reduce_kernel(float* __restrict__ ws, int cs, int64_t step,
-                                                                 int64_t n, TO* __restrict__ out) {
+                                                                 int64_t n, OutSeg<TO> out) {
   const int g = blockIdx.y;
   const int i0 = g * kReduceGroup;
   int cnt = cs - i0;
@@ -524,10 +537,11 @@ __global__ __launch_bounds__(kThreads) void splitk_reduce_kernel(float* __restri
         acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
       }
       if (FINAL) {
-        out[e] = static_cast<TO>(acc.x);
-        out[e + 1] = static_cast<TO>(acc.y);
-        out[e + 2] = static_cast<TO>(acc.z);
-        out[e + 3] = static_cast<TO>(acc.w);
+        TO* o = out.at(e);
+        o[0] = static_cast<TO>(acc.x);
+        o[1] = static_cast<TO>(acc.y);
+        o[2] = static_cast<TO>(acc.z);
+        o[3] = static_cast<TO>(acc.w);
       } else {
         *reinterpret_cast<float4*>(base + e) = acc;
       }
@@ -535,7 +549,7 @@ __global__ __launch_bounds__(kThreads) void splitk_reduce_kernel(float* __restri
       for (int64_t k = e; k < e + 4 && k < n; ++k) {
         float a = 0.f;
         for (int i = 0; i < cnt; ++i) a += base[i * step * n + k];
-        if (FINAL) out[k] = static_cast<TO>(a);
+        if (FINAL) *out.at(k) = static_cast<TO>(a);
         else base[k] = a;
       }
     }
@@ -552,7 +566,7 @@ constexpr int kColV = 8, kColPh = 32, kColMaxS = 2048;
 
 template <typename TO>
 __global__ __launch_bounds__(kColV * kColPh) void colreduce_kernel(const float* __restrict__ ws, int S, int64_t n,
-                                                                   TO* __restrict__ out) {
+                                                                   OutSeg<TO> out) {
   const int q = threadIdx.x % kColV, ph = threadIdx.x / kColV;
   const int64_t c4 = static_cast<int64_t>(blockIdx.x) * kColV + q;
   const int64_t n4 = n / 4;
@@ -587,7 +601,7 @@ __global__ __launch_bounds__(kColV * kColPh) void colreduce_kernel(const float* 
   }
   if (ph == 0 && c4 < n4) {
     const float4 r = red[0][q];
-    TO* o = out + c4 * 4;
+    TO* o = out.at(c4 * 4);
     o[0] = static_cast<TO>(r.x);
     o[1] = static_cast<TO>(r.y);
     o[2] = static_cast<TO>(r.z);
@@ -730,26 +744,34 @@ static bool colreduce_on() {
   return on;
 }
 
-void gemm_splitk_reduce(const float* ws_c, int splits, int64_t n, void* out, int out_dtype, hipStream_t stream) {
+namespace {
+template <typename TO>
+OutSeg<TO> out_seg(void* o0, void* o1, void* o2, int64_t seg) {
+  return OutSeg<TO>{{static_cast<TO*>(o0), static_cast<TO*>(o1), static_cast<TO*>(o2)}, seg};
+}
+}  // namespace
+
+void gemm_splitk_reduce_seg(const float* ws_c, int splits, int64_t n, int64_t seg, void* out0, void* out1, void* out2,
+                            int out_dtype, hipStream_t stream) {
   if (out_dtype != static_cast<int>(kF32) && out_dtype != static_cast<int>(kBF16))
     throw std::runtime_error("gemm_splitk_reduce: out dtype must be fp32 or bf16");
+  if (seg <= 0 || seg % 4 != 0 || (n + seg - 1) / seg > 3 || (n > seg && out1 == nullptr) ||
+      (n > 2 * seg && out2 == nullptr))
+    throw std::runtime_error("gemm_splitk_reduce_seg: segments must be multiples of 4, at most 3, all present");
+  const bool f32 = out_dtype == static_cast<int>(kF32);
   float* ws = const_cast<float*>(ws_c);  // intermediate tree levels are written in place
   int64_t bx = (n / 4 + kThreads - 1) / kThreads;
   int cs = splits < 1 ? 1 : splits;
   if (cs > kReduceGroup && n == 1 && colreduce_on()) {
-    if (out_dtype == static_cast<int>(kF32))
-      sumall_kernel<float><<<1, kThreads, 0, stream>>>(ws, cs, static_cast<float*>(out));
-    else
-      sumall_kernel<bf16><<<1, kThreads, 0, stream>>>(ws, cs, static_cast<bf16*>(out));
+    if (f32) sumall_kernel<float><<<1, kThreads, 0, stream>>>(ws, cs, static_cast<float*>(out0));
+    else sumall_kernel<bf16><<<1, kThreads, 0, stream>>>(ws, cs, static_cast<bf16*>(out0));
     FLUXMPI_HIP_CHECK(hipGetLastError());
     return;
   }
   if (cs > kReduceGroup && cs <= kColMaxS && n % 4 == 0 && n > 0 && colreduce_on()) {
     const unsigned gx = static_cast<unsigned>((n / 4 + kColV - 1) / kColV);
-    if (out_dtype == static_cast<int>(kF32))
-      colreduce_kernel<float><<<gx, kColV * kColPh, 0, stream>>>(ws, cs, n, static_cast<float*>(out));
-    else
-      colreduce_kernel<bf16><<<gx, kColV * kColPh, 0, stream>>>(ws, cs, n, static_cast<bf16*>(out));
+    if (f32) colreduce_kernel<float><<<gx, kColV * kColPh, 0, stream>>>(ws, cs, n, out_seg<float>(out0, out1, out2, seg));
+    else colreduce_kernel<bf16><<<gx, kColV * kColPh, 0, stream>>>(ws, cs, n, out_seg<bf16>(out0, out1, out2, seg));
     FLUXMPI_HIP_CHECK(hipGetLastError());
     return;
   }
@@ -762,18 +784,25 @@ void gemm_splitk_reduce(const float* ws_c, int splits, int64_t n, void* out, int
     if (gx > cap) gx = cap;
     if (gx < 1) gx = 1;
     splitk_reduce_kernel<float, false><<<dim3((unsigned)gx, (unsigned)groups), kThreads, 0, stream>>>(
-        ws, cs, step, n, nullptr);
+        ws, cs, step, n, OutSeg<float>{{nullptr, nullptr, nullptr}, n});
     FLUXMPI_HIP_CHECK(hipGetLastError());
     cs = groups;
     step *= kReduceGroup;
   }
   int64_t gx = bx > 4096 ? 4096 : (bx < 1 ? 1 : bx);
-  if (out_dtype == static_cast<int>(kF32))
+  if (f32)
     splitk_reduce_kernel<float, true><<<(unsigned)gx, kThreads, 0, stream>>>(ws, cs, step, n,
-                                                                             static_cast<float*>(out));
+                                                                             out_seg<float>(out0, out1, out2, seg));
   else
-    splitk_reduce_kernel<bf16, true><<<(unsigned)gx, kThreads, 0, stream>>>(ws, cs, step, n, static_cast<bf16*>(out));
+    splitk_reduce_kernel<bf16, true><<<(unsigned)gx, kThreads, 0, stream>>>(ws, cs, step, n,
+                                                                            out_seg<bf16>(out0, out1, out2, seg));
   FLUXMPI_HIP_CHECK(hipGetLastError());
+}
+
+void gemm_splitk_reduce(const float* ws_c, int splits, int64_t n, void* out, int out_dtype, hipStream_t stream) {
+  // one segment covering the row (n % 4 != 0 rows only take the tree path, which masks per element)
+  const int64_t seg = n > 0 ? ((n + 3) / 4) * 4 : 4;
+  gemm_splitk_reduce_seg(ws_c, splits, n, seg, out, nullptr, nullptr, out_dtype, stream);
 }
 
 }  // namespace fluxmpi

@@ -26,6 +26,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.linear import Linear
+
 # ResNet stem: "ours" = the MFMA stem kernels (ops/stem.py: conv + BN statistics forward, one fused
 # backward pass) when the input is a 224x224 bf16 NHWC batch; "miopen" = padded MIOpen conv + the
 # fused BN/ReLU/max-pool of ops/pool.py
@@ -235,7 +237,8 @@ class ResNet(nn.Module):
         self.layer2 = self._make(128, layers[1], 2)
         self.layer3 = self._make(256, layers[2], 2)
         self.layer4 = self._make(512, layers[3], 2)
-        self.fc = nn.Linear(512 * Bottleneck.expansion, num_classes)
+        # ops.linear.Linear: its backward writes dW / db into their DDP bucket slices (graddst)
+        self.fc = Linear(512 * Bottleneck.expansion, num_classes)
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")

@@ -159,6 +159,33 @@ class Block(nn.Module):
         return x, (g, self.fc2, link)
 
 
+class _ClsPos(torch.autograd.Function):
+    """``cat([cls, x], 1) + pos``; the backward writes d(cls) and d(pos) — sums over the batch —
+    into their DDP bucket slices when a communicating engine is attached (``ops/graddst.py``)."""
+
+    @staticmethod
+    def forward(ctx, x, cls, pos):
+        ctx.params = (cls, pos)
+        return torch.cat([cls.expand(x.shape[0], -1, -1).to(x.dtype), x], 1) + pos.to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ..ops import graddst
+        cls, pos = ctx.params
+        need = ctx.needs_input_grad
+        dcls = dpos = None
+        if need[2]:
+            with graddst.into(pos):
+                out = graddst.empty(tuple(pos.shape[1:]), pos.dtype, dy.device) if dy.dtype == pos.dtype else None
+            dpos = (torch.sum(dy, 0, out=out) if out is not None else dy.sum(0).to(pos.dtype)).view(pos.shape)
+        if need[1]:
+            with graddst.into(cls):
+                out = graddst.empty((cls.shape[-1],), cls.dtype, dy.device) if dy.dtype == cls.dtype else None
+            d0 = dy[:, 0]
+            dcls = (torch.sum(d0, 0, out=out) if out is not None else d0.sum(0).to(cls.dtype)).view(cls.shape)
+        return (dy[:, 1:] if need[0] else None), dcls, dpos
+
+
 class ViT(nn.Module):
     def __init__(self, img=224, patch=16, dim=768, depth=12, heads=12, mlp=3072, num_classes=1000):
         super().__init__()
@@ -168,7 +195,7 @@ class ViT(nn.Module):
         self.blocks = nn.ModuleList([Block(dim, heads, mlp) for _ in range(depth)])
         from ..ops.layernorm import FusedLayerNorm
         self.ln = FusedLayerNorm(dim, eps=1e-6)
-        self.head = nn.Linear(dim, num_classes)
+        self.head = Linear(dim, num_classes)  # ops.linear.Linear: dW / db into their bucket slices
         for m in self.modules():
             if isinstance(m, nn.Linear):
                 nn.init.trunc_normal_(m.weight, std=0.02)
@@ -176,7 +203,10 @@ class ViT(nn.Module):
 
     def forward(self, x):
         x = self.embed(x)
-        x = torch.cat([self.cls.expand(x.shape[0], -1, -1).to(x.dtype), x], 1) + self.pos.to(x.dtype)
+        if x.is_cuda and torch.is_grad_enabled():
+            x = _ClsPos.apply(x, self.cls, self.pos)
+        else:
+            x = torch.cat([self.cls.expand(x.shape[0], -1, -1).to(x.dtype), x], 1) + self.pos.to(x.dtype)
         pend = None
         last = len(self.blocks) - 1
         for i, blk in enumerate(self.blocks):

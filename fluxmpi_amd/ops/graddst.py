@@ -101,6 +101,17 @@ def empty(shape, dtype: torch.dtype, device) -> torch.Tensor:
     return torch.empty(*shape, dtype=dtype, device=device)
 
 
+def empty_like(p: torch.Tensor, dtype: torch.dtype | None = None) -> torch.Tensor:
+    """A gradient buffer for ``p`` with ``p``'s strides (``p.shape``, ``p.stride()``, e.g. a
+    channels_last filter) over its bucket slice when one is available (see :func:`take`), else
+    ``torch.empty_like(p)`` (``memory_format`` preserved)."""
+    dt = dtype or p.dtype
+    t = take(p, (p.numel(),), dt) if p.is_contiguous() or p.is_non_overlapping_and_dense() else None
+    if t is not None:
+        return t.as_strided(p.shape, p.stride())
+    return torch.empty_like(p, dtype=dt)
+
+
 def delivered(p: torch.Tensor) -> bool:
     """True if ``p.grad`` lies in ``p``'s destination slice (diagnostics / tests)."""
     d = getattr(p, _ATTR, None)

@@ -15,6 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _ext
+from . import graddst
 from .multi_tensor import DTYPE_CODE
 
 _MAX_BLOCKS = 4096
@@ -74,10 +75,12 @@ def _fwd(x, r, w, b, eps):
     return h, y, mean, rstd
 
 
-def _bwd(dy, x, dh_ext, mean, rstd, w, dtypes, colsum_dtype=None):
+def _bwd(dy, x, dh_ext, mean, rstd, w, dtypes, colsum_dtype=None, params=(None, None, None)):
     """``(dx, dw, db)``; dw / db reduced straight into the parameter dtype when it is fp32 or bf16
     and both share it (no cast kernels), else reduced in fp32 and cast. ``colsum_dtype`` (needs
-    ``dh_ext``): also the column sums of dx, returned fourth in that dtype."""
+    ``dh_ext``): also the column sums of dx, returned fourth in that dtype. ``params``: the leaves
+    (LN weight, LN bias, the producer's bias for the column sums) whose DDP bucket slices the
+    one reduce launch writes when a communicating engine is attached (``ops/graddst.py``)."""
     C = _ext.get(required=True)
     d = x.shape[-1]
     rows = x.numel() // d
@@ -89,26 +92,25 @@ def _bwd(dy, x, dh_ext, mean, rstd, w, dtypes, colsum_dtype=None):
                          dx.data_ptr(), part.data_ptr(), _MAX_BLOCKS, rows, d, DTYPE_CODE[x.dtype],
                          DTYPE_CODE[w.dtype], _stream(x), cs)
     wd, bd = dtypes
-    if cs:  # one reduce launch over all 3D columns (straight into the shared dtype when there is one)
-        present = {t for t in (wd, bd, colsum_dtype) if t is not None}
-        rdt = present.pop() if len(present) == 1 else torch.float32
-        if rdt not in (torch.float32, torch.bfloat16):
-            rdt = torch.float32
-        red = torch.empty(3 * d, device=x.device, dtype=rdt)
-        C.gemm_splitk_reduce(part.data_ptr(), nb, 3 * d, red.data_ptr(), DTYPE_CODE[rdt], _stream(x))
-        dw = red[:d].to(wd) if wd is not None else None
-        db = red[d:2 * d].to(bd) if bd is not None else None
-        return dx, dw, db, red[2 * d:].to(colsum_dtype)
-    if wd is None and bd is None:
+    want = [wd, bd] + ([colsum_dtype] if cs else [])
+    if not cs and wd is None and bd is None:
         return dx, None, None
-    present = {t for t in dtypes if t is not None}
-    odt = present.pop() if len(present) == 1 else torch.float32
-    if odt not in (torch.float32, torch.bfloat16):
-        odt = torch.float32
-    wb = torch.empty(2 * d, device=x.device, dtype=odt)
-    C.gemm_splitk_reduce(part.data_ptr(), nb, 2 * d, wb.data_ptr(), DTYPE_CODE[odt], _stream(x))
-    dw = wb[:d].to(wd) if wd is not None else None
-    db = wb[d:].to(bd) if bd is not None else None
+    present = {t for t in want if t is not None}
+    rdt = present.pop() if len(present) == 1 else torch.float32
+    if rdt not in (torch.float32, torch.bfloat16):
+        rdt = torch.float32
+    # one reduce launch; each d-column segment lands in its own tensor (a bucket slice when the
+    # dtype matches the parameter's, else a piece cast afterwards)
+    outs = []
+    for dt, p in zip(want, params):
+        t = graddst.take(p, (d,), rdt) if (dt == rdt and p is not None) else None
+        outs.append(t if t is not None else torch.empty(d, device=x.device, dtype=rdt))
+    ptrs = [o.data_ptr() for o in outs] + [0] * (3 - len(outs))
+    C.gemm_splitk_reduce_seg(part.data_ptr(), nb, npart * d, d, ptrs[0], ptrs[1], ptrs[2], DTYPE_CODE[rdt], _stream(x))
+    dw = outs[0].to(wd) if wd is not None else None
+    db = outs[1].to(bd) if bd is not None else None
+    if cs:
+        return dx, dw, db, outs[2].to(colsum_dtype)
     return dx, dw, db
 
 
@@ -120,12 +122,13 @@ class _LayerNormFn(torch.autograd.Function):
         _, y, mean, rstd = _fwd(x, None, w, b, eps)
         ctx.save_for_backward(x, w, mean, rstd)
         ctx.dtypes = (weight.dtype if weight is not None else None, bias.dtype if bias is not None else None)
+        ctx.params = (weight if ctx.needs_input_grad[1] else None, bias if ctx.needs_input_grad[2] else None, None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, w, mean, rstd = ctx.saved_tensors
-        dx, dw, db = _bwd(dy.contiguous(), x, None, mean, rstd, w, ctx.dtypes)
+        dx, dw, db = _bwd(dy.contiguous(), x, None, mean, rstd, w, ctx.dtypes, params=ctx.params)
         return dx, dw, db, None
 
 
@@ -137,6 +140,7 @@ class _AddLayerNormFn(torch.autograd.Function):
         h, y, mean, rstd = _fwd(x, r, w, b, eps)
         ctx.save_for_backward(h, w, mean, rstd)
         ctx.dtypes = (weight.dtype if weight is not None else None, bias.dtype if bias is not None else None)
+        ctx.params = (weight if ctx.needs_input_grad[2] else None, bias if ctx.needs_input_grad[3] else None, None)
         return h, y
 
     @staticmethod
@@ -145,7 +149,7 @@ class _AddLayerNormFn(torch.autograd.Function):
         if dy is None:
             dy = torch.zeros_like(h)
         dh = dh.contiguous() if dh is not None else None
-        dx, dw, db = _bwd(dy.contiguous(), h, dh, mean, rstd, w, ctx.dtypes)
+        dx, dw, db = _bwd(dy.contiguous(), h, dh, mean, rstd, w, ctx.dtypes, params=ctx.params)
         return dx, dx, dw, db, None  # h = x + r: both inputs get the same gradient
 
 
@@ -166,6 +170,8 @@ class _LinearAddLayerNormFn(torch.autograd.Function):
         ctx.save_for_backward(a, weight, h, w, mean, rstd)
         ctx.dtypes = (ln_w.dtype if ln_w is not None else None, ln_b.dtype if ln_b is not None else None)
         ctx.bias_dtype = bias.dtype
+        need = ctx.needs_input_grad
+        ctx.params = (ln_w if need[4] else None, ln_b if need[5] else None, bias if need[2] else None)
         return h, y
 
     @staticmethod
@@ -176,7 +182,8 @@ class _LinearAddLayerNormFn(torch.autograd.Function):
             dy = torch.zeros_like(h)
         if dh is None:
             dh = torch.zeros_like(h)
-        dx, dlw, dlb, dbias = _bwd(dy.contiguous(), h, dh.contiguous(), mean, rstd, w, ctx.dtypes, ctx.bias_dtype)
+        dx, dlw, dlb, dbias = _bwd(dy.contiguous(), h, dh.contiguous(), mean, rstd, w, ctx.dtypes, ctx.bias_dtype,
+                                   params=ctx.params)
         n_out, n_in = weight.shape
         g2 = dx.reshape(-1, n_out)
         a2 = a.reshape(-1, n_in)

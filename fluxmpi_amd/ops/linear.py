@@ -117,12 +117,23 @@ class _LinearFn(torch.autograd.Function):
         need_b = ctx.has_bias and ctx.needs_input_grad[2]
 
         # written straight into the DDP bucket slices when a communicating engine is attached
+        same = dy2.dtype == x2.dtype == w.dtype
         if need_w:
             with graddst.into(w):
-                dw = weight_grad(dy2, x2, w.dtype) if native else dy2.t() @ x2
+                if native:
+                    dw = weight_grad(dy2, x2, w.dtype)
+                elif same:  # short K (e.g. a classifier head): hipBLASLt, output in the slice
+                    dw = torch.mm(dy2.t(), x2, out=graddst.empty(tuple(w.shape), w.dtype, dy2.device))
+                else:
+                    dw = (dy2.t() @ x2).to(w.dtype)
         if need_b:
             with graddst.into(ctx.bias):
-                db = bias_grad(dy2, ctx.bias_dtype) if native else dy2.sum(0).to(ctx.bias_dtype)
+                if native:
+                    db = bias_grad(dy2, ctx.bias_dtype)
+                elif dy2.dtype == ctx.bias_dtype:
+                    db = torch.sum(dy2, 0, out=graddst.empty((n_out,), ctx.bias_dtype, dy2.device))
+                else:
+                    db = dy2.sum(0).to(ctx.bias_dtype)
         dx = dgrad(dy2, w).reshape(x.shape) if ctx.needs_input_grad[0] else None
         return dx, dw, db
 

@@ -25,6 +25,7 @@ import functools
 import torch
 
 from . import _ext
+from . import graddst
 from .batchnorm import _workspace
 from .multi_tensor import DTYPE_CODE
 
@@ -156,6 +157,7 @@ class _StemFn(torch.autograd.Function):
                               112, CO, 3, 2, 1, DTYPE_CODE[torch.bfloat16], stream)
         ctx.save_for_backward(x4, c, idx, w32, mean, inv)
         ctx.dtypes = (weight.dtype, bn_w.dtype if bn_w is not None else None, bn_b is not None)
+        ctx.params = (weight, bn_w, bn_b)  # the leaves: their gradients' DDP bucket slices (graddst)
         return y.permute(0, 3, 1, 2)
 
     @staticmethod
@@ -172,14 +174,23 @@ class _StemFn(torch.autograd.Function):
             dy = dy.to(torch.bfloat16)
         blocks = C.stem_bwd_blocks(n)
         part = torch.empty(blocks * C.stem_part_floats(), device=dev, dtype=torch.float32)
-        dw_bn = torch.empty(CO, device=dev, dtype=torch.float32)
-        db_bn = torch.empty_like(dw_bn)
+        weight, bn_w, bn_b = ctx.params
+        need = ctx.needs_input_grad
+
+        def bn_out(p, i):  # fp32 BN parameter gradients straight into their bucket slices
+            t = graddst.take(p, (CO,), torch.float32) if need[i] else None
+            return t if t is not None else torch.empty(CO, device=dev, dtype=torch.float32)
+
+        dw_bn, db_bn = bn_out(bn_w, 2), bn_out(bn_b, 3)
         dwp = torch.empty(CO, KK, device=dev, dtype=torch.float32)
         C.stem_bwd(x4.data_ptr(), c.data_ptr(), dy.data_ptr(), idx.data_ptr(), w32.data_ptr(), mean.data_ptr(),
                    inv.data_ptr(), part.data_ptr(), blocks, _workspace(x4).data_ptr(), dw_bn.data_ptr(),
                    db_bn.data_ptr(), dwp.data_ptr(), n, stream)
         wdt, bdt, has_b = ctx.dtypes
-        dw = unpack_grad(dwp, 3).to(wdt)
+        dw = None
+        if need[1]:  # the unpack's cast writes the filter's bucket slice (in the filter's strides)
+            dw = graddst.empty_like(weight, wdt)
+            dw.copy_(unpack_grad(dwp, 3))
         return (None, dw, dw_bn.to(bdt) if bdt is not None else None, db_bn.to(bdt) if has_b else None,
                 None, None, None, None, None)
 

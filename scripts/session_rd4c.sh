@@ -1,11 +1,13 @@
 #!/bin/bash
-# rd4c: persistent gemm_nt numbers + its GPU tests + the touched GPU tests + ViT/ResNet bench
+# rd4c: persistent gemm_nt numbers + its GPU tests + the touched GPU tests + ViT/ResNet bench (+force-comm)
 source "$(dirname "$0")/gpu_lib.sh"
 rm -f "$OUT/steps.log" "$OUT/bench_results.jsonl"
 T="python -u -m pytest -x -q --timeout 120 --timeout-method thread"
 step bench_gemm_nt 400 0 python -u scripts/bench_gemm_nt.py
 step test_gemm_nt 400 0 $T tests/test_gemm_nt_gpu.py
-step test_touched 500 0 $T tests/test_attention_gpu.py tests/test_vit_gpu.py tests/test_vit_model_gpu.py tests/test_comm_gpu.py tests/test_linear_gpu.py -m gpu
+step test_touched 600 0 $T tests/test_attention_gpu.py tests/test_vit_gpu.py tests/test_vit_model_gpu.py tests/test_comm_gpu.py tests/test_linear_gpu.py tests/test_stem_gpu.py tests/test_layernorm.py tests/test_deq.py -m gpu
 step bench_vit 300 0 python -u bench.py --model vit_b16 --steps 10 --warmup 5
+step bench_vit_fc 300 0 python -u bench.py --model vit_b16 --steps 10 --warmup 5 --force-comm
 step bench_r50 300 0 python -u bench.py --steps 20 --warmup 10
+step bench_r50_fc 300 0 python -u bench.py --steps 20 --warmup 10 --force-comm
 echo done
