@@ -57,6 +57,11 @@ def parse():
                     help="all ranks on cuda:0 with gloo collectives on device tensors (RCCL refuses a "
                          "shared GPU): runs the N>1 code path on a 1-GPU box; no throughput claim")
     ap.add_argument("--graph", action="store_true", help="capture the step in a HIP graph")
+    ap.add_argument("--api", default="ddp", choices=["ddp", "functional"],
+                    help="ddp: the DDP engine (hooks, buckets born in the comm buffers, fused optimiser); "
+                         "functional: the reference's API shape (src/optimizer.jl:45-65) — the nested "
+                         "parameter tree's gradients through allreduce_gradients(like=ps), then "
+                         "Optimisers.update! (fused multi-tensor kernels)")
     ap.add_argument("--miopen-find", type=int, default=int(os.environ.get("BENCH_MIOPEN_FIND", "1")))
     ap.add_argument("--choices", default=os.environ.get("BENCH_CHOICES", "measure"), choices=["measure", "shipped"],
                     help="measure (default): per-shape kernel choices (ours vs MIOpen, tile configs) timed at the "
@@ -73,6 +78,57 @@ def _gelu_form() -> str:
     from fluxmpi_amd.ops import gelu as GL
 
     return GL.FORM
+
+
+class Functional:
+    """The reference's functional training step as a DDP stand-in for the bench loop: the model's
+    parameters as a nested tree (module path -> leaf), broadcast from rank 0 (``synchronize``), the
+    gradient tree reduced by ``allreduce_gradients(gs, like=ps)`` (averaged, as the DDP engine's
+    ``average=True``; ``like``: a rank without some gradient still joins every bucket) and applied
+    by ``Optimisers.update!`` (one fused multi-tensor launch per dtype group)."""
+
+    def __init__(self, FluxMPI, O, model, rule):
+        from fluxmpi_amd.parallel.bucket import plan_buckets
+        from fluxmpi_amd.parallel.comm import ReduceOp
+
+        self.F, self.O, self.module = FluxMPI, O, model
+        self.op = ReduceOp.AVG
+        self.ps: dict = {}
+        for name, p in model.named_parameters():
+            d = self.ps
+            *path, leaf = name.split(".")
+            for k in path:
+                d = d.setdefault(k, {})
+            d[leaf] = p
+        FluxMPI.synchronize(model, root_rank=0)  # parameters and buffers (BatchNorm statistics)
+        self.st = O.setup(rule, self.ps)
+        self.params = [p for p in model.parameters()]
+        self.plan = plan_buckets([p.detach() for p in self.params if p.requires_grad], None)
+        self.communicate = FluxMPI.total_workers() > 1 or os.environ.get("FLUXMPI_FORCE_COMM") == "1"
+        self.timing = False
+        self.step_count = 0
+
+    def __call__(self, x):
+        return self.module(x)
+
+    def _grads(self, t):
+        return {k: self._grads(v) for k, v in t.items()} if isinstance(t, dict) else t.grad
+
+    def step(self):
+        gs = self.F.allreduce_gradients(self._grads(self.ps), op=self.op, like=self.ps)
+        self.O.update_(self.st, self.ps, gs)
+        for p in self.params:
+            p.grad = None
+        self.step_count += 1
+
+    def exposed_comm_ms(self):
+        return None
+
+    def comm_summary(self) -> dict:
+        mb = [round(t[5] * t[2].itemsize / 2 ** 20, 2) for t in self.plan]  # packed buckets and direct leaves
+        return {"api": "functional", "communicate": self.communicate, "overlap": False,
+                "buckets": len(self.plan), "bucket_mb": mb,
+                "comm": self.F.backend_name() if self.communicate else "none"}
 
 
 def selfcheck_or_code(FluxMPI, world: int, rank: int, dev):
@@ -96,7 +152,9 @@ def selfcheck_or_code(FluxMPI, world: int, rank: int, dev):
 def main():
     args = parse()
     if args.image is None:
-        args.image = 28 if args.model == "deq" else 224
+        args.image = {"deq": 28, "deq_cifar": 32}.get(args.model, 224)
+    if args.api == "functional" and args.force_comm:
+        os.environ["FLUXMPI_FORCE_COMM"] = "1"  # allreduce_gradients communicates even at N=1
     import fluxmpi_amd as FluxMPI
     from fluxmpi_amd import optimisers as O
     from fluxmpi_amd.models import build_model
@@ -165,11 +223,18 @@ def main():
     if isinstance(comm_report, int):
         return comm_report
     rule = O.Adam(1e-3) if args.optimizer == "adam" else O.Momentum(0.1, 0.9)
-    ddp = DDP(model, rule, average=True, overlap=not args.no_overlap, force_comm=args.force_comm)
+    if args.api == "functional":
+        if args.graph:
+            print("bench.py: --graph needs --api ddp", file=sys.stderr)
+            return 2
+        ddp = Functional(FluxMPI, O, model, rule)
+    else:
+        ddp = DDP(model, rule, average=True, overlap=not args.no_overlap, force_comm=args.force_comm)
 
     B = args.batch
     gx = torch.Generator(device=dev).manual_seed(rank)
-    cin, ncls = (1, 10) if args.model == "deq" else (3, 1000)  # DEQ: MNIST-shaped (FastDEQ example)
+    # DEQs: MNIST-shaped (deq) and CIFAR-shaped (deq_cifar), the FastDEQ examples' data
+    cin, ncls = {"deq": (1, 10), "deq_cifar": (3, 10)}.get(args.model, (3, 1000))
     x = torch.randn(B, cin, args.image, args.image, device=dev, generator=gx).to(torch.bfloat16)
     x = x.contiguous(memory_format=memfmt)
     y = torch.randint(0, ncls, (B,), device=dev, generator=gx)
@@ -187,7 +252,7 @@ def main():
         return loss
 
     calibrated = False
-    if world > 1:
+    if world > 1 and args.api == "ddp":
         # per-shape kernel choices measured once on rank 0 with no collective in flight, shared
         # with every rank and frozen (parallel/autotune.py): all ranks run the same kernels
         from fluxmpi_amd.parallel.autotune import calibrate
@@ -226,7 +291,7 @@ def main():
     dt_max = max(per_rank)
     lval = float(loss.item())
     exposed = None
-    if ddp.communicate and not args.graph:
+    if ddp.communicate and not args.graph and args.api == "ddp":
         # after the timed region: a few steps with event timing around the gradient-allreduce
         # wait (exposed = not hidden behind backward), max over ranks
         ddp.timing = True
@@ -245,7 +310,7 @@ def main():
     cs = ddp.comm_summary()
     if rank == 0:
         ips = world * B * args.steps / dt_max
-        names = {"resnet50": "ResNet50", "vit_b16": "ViT-B/16", "deq": "DEQ"}
+        names = {"resnet50": "ResNet50", "vit_b16": "ViT-B/16", "deq": "DEQ", "deq_cifar": "DEQ-CIFAR (FastDEQ width)"}
         mname = names.get(args.model, args.model)
         metric = METRIC if args.model == "resnet50" else METRIC.replace("ResNet50 Lux.jl", f"{mname}")
         rec = {

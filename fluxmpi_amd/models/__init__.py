@@ -3,7 +3,8 @@
 * ``mlp``       — the README 4-layer Dense MLP (reference ``README.md:37-38``)
 * ``resnet50``  — ResNet-50 (Lux ImageNet example; the headline benchmark)
 * ``vit_b16``   — ViT-Base/16
-* ``deq``       — a Deep Equilibrium Model (FastDEQ-style implicit layer)
+* ``deq``       — a Deep Equilibrium Model (FastDEQ-style implicit layer, MNIST-shaped, 48 channels)
+* ``deq_cifar`` — the FastDEQ-width DEQ (CIFAR-shaped, 512 channels, 10.6 MB of bf16 gradients)
 """
 from __future__ import annotations
 
@@ -29,4 +30,9 @@ def build_model(name: str, **kw):
         kw.pop("conv_impl", None)
         kw.pop("norm", None)
         return deq_mnist(**kw)
+    if name == "deq_cifar":
+        from .deq import deq_cifar
+        kw.pop("conv_impl", None)
+        kw.pop("norm", None)
+        return deq_cifar(**kw)
     raise ValueError(f"unknown model {name!r}")

@@ -562,3 +562,35 @@ class DEQClassifier(nn.Module):
 
 def deq_mnist(num_classes=10, **kw) -> DEQClassifier:
     return DEQClassifier(1, 48, num_classes, **kw)
+
+
+class DEQCifar(nn.Module):
+    """A FastDEQ-width implicit classifier for 3 x 32 x 32 images (the reference's DEQ example,
+    /root/reference/README.md:76-77, links FastDEQ.jl's CIFAR-10 models): a two-convolution
+    stem (32 x 32, then stride 2 to 16 x 16 and ``ch`` channels), the MDEQ-style residual cell
+    solved to its fixed point at 16 x 16 x ``ch`` (Anderson forward, adjoint fixed-point
+    backward), BatchNorm, global pooling and a linear head. ``ch`` = 512: 5.3 M parameters,
+    10.6 MB of bf16 gradients per step — a DDP workload whose allreduce moves real data, on
+    the nested (irregular) parameter tree the functional API reduces with
+    ``allreduce_gradients(like=...)`` (bench.py ``--api functional``)."""
+
+    def __init__(self, ch=512, num_classes=10, groups=16, **solver):
+        super().__init__()
+        c0 = ch // 4
+        self.stem1 = nn.Conv2d(3, c0, 3, padding=1, bias=False)
+        self.stem1_norm = FusedBatchNorm2d(c0)
+        self.stem2 = nn.Conv2d(c0, ch, 3, stride=2, padding=1, bias=False)
+        self.inj_norm = FusedBatchNorm2d(ch)
+        self.deq = DEQFixedPoint(ResidualCell(ch, groups), **solver)
+        self.out_norm = FusedBatchNorm2d(ch)
+        self.head = nn.Linear(ch, num_classes)
+
+    def forward(self, x):
+        x = F.relu(self.stem1_norm(self.stem1(x)))
+        x = self.inj_norm(self.stem2(x))
+        z = self.out_norm(self.deq(x))
+        return self.head(F.adaptive_avg_pool2d(z, 1).flatten(1))
+
+
+def deq_cifar(num_classes=10, ch=512, **kw) -> DEQCifar:
+    return DEQCifar(ch, num_classes, **kw)

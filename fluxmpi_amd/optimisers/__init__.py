@@ -178,7 +178,8 @@ class Nesterov(AbstractRule):
 def _sgd_batch(rule, items, rho, nesterov):
     """Fused GPU path for Descent / Momentum / Nesterov; per-leaf math elsewhere."""
     gpu = [i for i, (l, x, dx) in enumerate(items)
-           if x.is_cuda and dx is not None and x.is_contiguous() and dx.is_contiguous()
+           if x.is_cuda and dx is not None
+           and _same_dense(x, dx, *([l.state] if rho != 0.0 and isinstance(l.state, torch.Tensor) else []))
            and _fused.supported(x.dtype, dx.dtype, x.dtype, False)]
     out: list = [None] * len(items)
     gset = set(gpu)
@@ -247,14 +248,24 @@ class Adam(AbstractRule):
         return _adam_batch(self, items, 0.0)
 
 
+def _same_dense(*ts) -> bool:
+    """All tensors dense (no gaps or overlaps) with identical shape and strides: the flat
+    multi-tensor kernels then see matching elements at matching offsets (contiguous, or e.g.
+    a channels_last filter with its channels_last gradient and zeros_like moments)."""
+    t0 = ts[0]
+    if not (t0.is_contiguous() or t0.is_non_overlapping_and_dense()):
+        return False
+    return all(t.shape == t0.shape and t.stride() == t0.stride() for t in ts[1:])
+
+
 def _adam_batch(rule: Adam, items, weight_decay: float):
     """Fused multi-tensor Adam on GPU leaves (x updated in place, dx' = None)."""
     out: list = [None] * len(items)
     fused: dict = {}
     host: dict = {}
     for i, (leaf, x, dx) in enumerate(items):
-        ok = (x.is_cuda and dx is not None and x.is_contiguous() and dx.is_contiguous()
-              and isinstance(leaf.state, tuple) and len(leaf.state) == 3
+        ok = (x.is_cuda and dx is not None and isinstance(leaf.state, tuple) and len(leaf.state) == 3
+              and _same_dense(x, dx, leaf.state[0], leaf.state[1])
               and _fused.supported(x.dtype, dx.dtype, leaf.state[0].dtype, False))
         if ok:
             key = (x.device, x.dtype, tuple(leaf.state[2]))  # same precision and beta^t -> one launch

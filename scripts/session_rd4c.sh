@@ -10,4 +10,6 @@ step bench_vit 300 0 python -u bench.py --model vit_b16 --steps 10 --warmup 5
 step bench_vit_fc 300 0 python -u bench.py --model vit_b16 --steps 10 --warmup 5 --force-comm
 step bench_r50 300 0 python -u bench.py --steps 20 --warmup 10
 step bench_r50_fc 300 0 python -u bench.py --steps 20 --warmup 10 --force-comm
+step bench_deqc 400 0 python -u bench.py --model deq_cifar --batch 128 --steps 10 --warmup 5
+step bench_deqc_func 400 0 python -u bench.py --model deq_cifar --batch 128 --steps 10 --warmup 5 --api functional --force-comm
 echo done

@@ -571,3 +571,57 @@ def test_deq_fused_adjoint_step(gpu_ext, monkeypatch):
     monkeypatch.setattr(deq_cell, "ENABLED", True)
     _, ss2 = cell.adjoint_step(state, u, g, torch.tensor(float(ss_f) * 0.5, device="cuda"), flag)
     assert float(flag) == 0.0 and float(ss2) == float(ss_f)
+
+
+def worker_deq_cifar_functional():
+    """The FastDEQ-width DEQ's nested (irregular) parameter tree through bench.py's functional
+    step — allreduce_gradients(gs, op=AVG, like=ps) then Optimisers.update! — on 2 gloo ranks with
+    different data: the ranks end with identical parameters, equal to one process applying the
+    mean of both ranks' gradients."""
+    import importlib.util
+    import os
+
+    import fluxmpi_amd as FluxMPI
+    from fluxmpi_amd import optimisers as O
+    from fluxmpi_amd.models import build_model
+
+    FluxMPI.Init()
+    r, W = FluxMPI.local_rank(), FluxMPI.total_workers()
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(os.path.dirname(__file__), "..", "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+
+    def data(k):
+        g = torch.Generator().manual_seed(50 + k)
+        return torch.randn(2, 3, 32, 32, generator=g), torch.randint(0, 10, (2,), generator=g)
+
+    def model():
+        torch.manual_seed(9)
+        return build_model("deq_cifar", ch=32, groups=8, max_iter=6, tol=0.0, bwd_iter=6, bwd_tol=0.0)
+
+    m = model()
+    f = bench.Functional(FluxMPI, O, m, O.Descent(0.1))
+    assert f.comm_summary()["communicate"] and sum(f.comm_summary()["bucket_mb"]) > 0
+    x, y = data(r)
+    F.cross_entropy(f(x), y).backward()
+    f.step()
+    # reference: one process, mean of both ranks' gradients
+    ref = model()
+    grads = []
+    for k in range(W):
+        ref.zero_grad()
+        xk, yk = data(k)
+        F.cross_entropy(ref(xk), yk).backward()
+        grads.append([p.grad.clone() for p in ref.parameters()])
+    with torch.no_grad():
+        for i, p in enumerate(ref.parameters()):
+            p -= 0.1 * sum(g[i] for g in grads) / W
+    for (n, p), q in zip(m.named_parameters(), ref.parameters()):
+        torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-4, atol=1e-5, msg=n)
+        g = FluxMPI.allgather(p.detach().clone())
+        assert torch.equal(g[0], g[1]), n
+    FluxMPI.Finalize()
+
+
+def test_deq_cifar_functional_gloo(spmd):
+    spmd("tests.test_deq:worker_deq_cifar_functional", nprocs=2, timeout=300)
