@@ -42,9 +42,10 @@ from .bucket import allreduce_tensors
 from .comm import ReduceOp
 
 _CHECKED: set = set()
+_LIKE_CHECKED: set = set()  # id() of `like` trees whose zero-filled plan was checked across ranks
 
 
-def check_plan(obj, what: str) -> None:
+def check_plan(obj, what: str, derived: bool = False) -> None:
     """Cross-rank structure check of a reduction plan (``FLUXMPI_CHECK_PLANS``).
 
     ``always`` (default): every call, one 16-byte host allreduce — every rank
@@ -52,12 +53,18 @@ def check_plan(obj, what: str) -> None:
     gradient collective. ``first``: once per distinct plan on this rank (cheaper;
     only safe when trees can differ from the first step on). ``never``: off. Set with
     ``FLUXMPI_CHECK_PLANS`` or the ``check_plans`` preference (the environment wins, as for
-    every other knob); measured cost of ``always``: one gloo allreduce of 16 bytes per call.
+    every other knob); measured cost of ``always``: one gloo allreduce of 16 bytes per call
+    (``scripts/bench_check_plan.py``).
+
+    ``derived``: the plan is a function of an argument that is identical on every rank (the
+    parameter tree of ``allreduce_gradients(like=...)``: missing gradients are zero-filled, so
+    the structure cannot vary between steps on one rank and not another) — ``always`` then
+    checks once per distinct plan, as ``first`` does.
     """
     mode = get_config().check_plans
     if mode == "never" or not runtime.Initialized() or runtime.total_workers() == 1:
         return
-    if mode == "first":
+    if mode == "first" or derived:
         h = structure_hash(obj)
         if h in _CHECKED:
             return
@@ -139,7 +146,12 @@ def allreduce_gradients(gs: Any, on_gpu: bool | None = None, op=ReduceOp.SUM, li
     runtime._require()
     if like is not None:
         gs = _zero_fill(gs, like)
-    check_plan(gs, "gradient tree")
+        # the plan follows `like` (zero-filled): checked once per parameter-tree object
+        if id(like) not in _LIKE_CHECKED:
+            check_plan(gs, "gradient tree", derived=True)
+            _LIKE_CHECKED.add(id(like))
+    else:
+        check_plan(gs, "gradient tree")
     leaves: list = []
     seen: set = set()
 
