@@ -225,6 +225,7 @@ void gemm_splitk_reduce_seg(const float* ws, int splits, int64_t n, int64_t seg,
 // A[k][m] * B[k][n] (bf16 A [K][lda], B [K][ldb], M and N multiples of 256), fp32 partials.
 bool wgrad256_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
 int wgrad256_actual_splits(int64_t K, int splits);
+void wgrad256_set_variant(int v);  // main-loop variant (A/B runs; 3 hoisted addressing, 4 ping-pong)
 void gemm_wgrad256(const void* a, const void* b, float* ws, int64_t lda, int64_t ldb, int64_t M, int64_t N, int64_t K,
                    int splits, hipStream_t stream);
 // Token-major Linear GEMM, both operands k-contiguous (gemm_nt.hip): C[M][N] = A[M][K] B[N][K]^T,

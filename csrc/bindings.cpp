@@ -288,6 +288,7 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("wgrad256_supported", &wgrad256_supported);
   m.def("wgrad256_actual_splits", &wgrad256_actual_splits);
+  m.def("wgrad256_set_variant", &wgrad256_set_variant);
   m.def("gemm_wgrad256", [](uintptr_t a, uintptr_t b, uintptr_t ws, int64_t lda, int64_t ldb, int64_t M, int64_t N,
                             int64_t K, int splits, uintptr_t stream) {
     gemm_wgrad256(reinterpret_cast<const void*>(a), reinterpret_cast<const void*>(b), reinterpret_cast<float*>(ws), lda,

@@ -317,20 +317,172 @@ __global__ __launch_bounds__(kThreads, 1) void wgrad256h_kernel(W256Args p) {
     }
 }
 
+// Variant 4: wgrad256h's operands, addressing and 4-stage ring in gemm_nt.hip's ping-pong
+// schedule. A 32-deep step is two PHASES (the wave's rows 0..63, then 64..127 of its 128: 16
+// MFMAs each); a phase is a LOAD segment (phase 0: the step's 4 B fragments + the first 4 A
+// fragments, phase 1: the other 4 A fragments, all by ds_read_b64_tr_b16; phase 0 issues the
+// LDS-DMA of A three steps ahead, phase 1 that of B; lgkmcnt(0), and in phase 1 the counted
+// vmcnt(8) that retires step t + 1) then a COMPUTE segment (16 MFMAs between s_setprio 1 / 0),
+// separated by raw s_barriers. Waves 4-7 run one barrier behind waves 0-3, so the two waves of a
+// SIMD alternate compute and load (MI355X_MICROARCH.md "Two waves per SIMD"). The stage a DMA
+// refills was last read one step earlier, before a barrier that follows its readers' lgkmcnt(0).
+__global__ __launch_bounds__(kThreads, 2) void wgrad256pp_kernel(W256Args p) {
+  constexpr int BK = 32, ST = 4;
+  constexpr int kImgBytes = BK * kTile * 2;  // 16 KiB
+  constexpr int kStageBytes = 2 * kImgBytes;
+  constexpr int kP = kImgBytes / 1024 / 8;    // 2 DMA pieces per wave per operand per step
+  constexpr int kRow = kTile * 2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nt = p.tiles_m * p.tiles_n;
+  const int total = static_cast<int>(gridDim.x);
+  int lid = blockIdx.x;
+  if (total >= 8) {
+    const int q = total / 8, r = total % 8, xcd = lid % 8, pos = lid / 8;
+    lid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+  }
+  const int split = lid / nt, bid = lid - split * nt;
+  const int tm = bid / p.tiles_n, tn = bid - tm * p.tiles_n;
+  const int64_t m0 = static_cast<int64_t>(tm) * kTile, n0 = static_cast<int64_t>(tn) * kTile;
+  const int64_t kbeg = static_cast<int64_t>(split) * p.k_per_split;
+  const int64_t kend = kbeg + p.k_per_split < p.K ? kbeg + p.k_per_split : p.K;
+  const int nk = kend > kbeg ? static_cast<int>((kend - kbeg + BK - 1) / BK) : 0;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wm = wave >> 2, wn = wave & 3;
+
+  const bf16* pa[kP];
+  const bf16* pb[kP];
+  int krow[kP];
+#pragma unroll
+  for (int j = 0; j < kP; ++j) {
+    const int row = 2 * (wave * kP + j) + (lane >> 5);
+    const int chunk = (lane & 31) ^ swz(row);
+    krow[j] = row;
+    pa[j] = p.a + (kbeg + row) * p.lda + m0 + chunk * 8;
+    pb[j] = p.b + (kbeg + row) * p.ldb + n0 + chunk * 8;
+  }
+  const int64_t stepA = static_cast<int64_t>(BK) * p.lda, stepB = static_cast<int64_t>(BK) * p.ldb;
+  const int klim = static_cast<int>(kend - kbeg);
+  typedef __attribute__((address_space(3))) char lds_char;
+  typedef __attribute__((address_space(1))) void gl_void;
+  // the DMA of one operand of step t (rows past the split's end read a zero line: same count)
+  auto issue = [&](int t, bool b_op) {
+    char* img = smem + (t % ST) * kStageBytes + (b_op ? kImgBytes : 0);
+#pragma unroll
+    for (int j = 0; j < kP; ++j) {
+      const int kr = krow[j] + t * BK;
+      const void* src = kr < klim ? static_cast<const void*>((b_op ? pb[j] + t * stepB : pa[j] + t * stepA))
+                                  : static_cast<const void*>(g_zero256);
+      __builtin_amdgcn_global_load_lds((gl_void*)(src), (lds_char*)(img + (wave * kP + j) * 1024), 16, 0, 0);
+    }
+  };
+
+  const int g = lane >> 4, li = lane & 15, qq = li >> 2, pp = li & 3;
+  const int k0 = 8 * g + qq;
+  const int sw = swz(k0);
+  int offA[8], offB[4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int col = wm * 128 + i * 16 + 4 * pp;
+    offA[i] = k0 * kRow + ((((col >> 3) ^ sw)) << 4) + (col & 7) * 2;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = wn * 64 + j * 16 + 4 * pp;
+    offB[j] = k0 * kRow + ((((col >> 3) ^ sw)) << 4) + (col & 7) * 2;
+  }
+  typedef short short4v __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) short4v lds_short4v;
+  auto frag_at = [&](const char* __restrict__ img, int off) {
+    short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(img + off));
+    short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(img + off + 4 * kRow));
+    bf16x8 out;
+    __builtin_memcpy(&out, &lo, 8);
+    __builtin_memcpy(reinterpret_cast<char*>(&out) + 8, &hi, 8);
+    return out;
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // prologue: steps 0, 1, 2 (A then B each); step 0 retired with the 8 younger in flight
+#pragma unroll
+  for (int t = 0; t < ST - 1; ++t) {
+    issue(t, false);
+    issue(t, true);
+  }
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) __builtin_amdgcn_s_barrier();  // the stagger
+
+  bf16x8 fb[4];
+  for (int t = 0; t < nk; ++t) {
+    const char* ta = smem + (t % ST) * kStageBytes;
+    const char* tb = ta + kImgBytes;
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph) {
+      // ---------- load segment
+      if (ph == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb[j] = frag_at(tb, offB[j]);
+      }
+      bf16x8 fa[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = frag_at(ta, offA[4 * ph + i]);
+      issue(t + ST - 1, ph == 1);
+      if (ph == 1) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      // ---------- compute segment
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[4 * ph + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[4 * ph + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float* c = p.c + static_cast<int64_t>(split) * p.M * p.N;
+  const int col_in = lane & 15, rq = 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t n = n0 + wn * 64 + j * 16 + col_in;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = m0 + wm * 128 + i * 16 + rq + r;
+        c[m * p.N + n] = acc[i][j][r];
+      }
+    }
+}
+
 // pipeline variant: 0 = BK 32 x 4 stages, 1 = BK 64 x 2 stages, 2 = variant 0 with s_setprio(1)
-// around each step's MFMAs, 3 (default) = variant 0 with the addressing hoisted out of the loop
+// around each step's MFMAs, 3 (default) = variant 0 with the addressing hoisted out of the loop,
+// 4 = the ping-pong schedule (wgrad256pp_kernel)
 int g_variant = -1;
 int variant() {
   if (g_variant < 0) {
     const char* e = std::getenv("FLUXMPI_WGRAD256_VARIANT");
     g_variant = e != nullptr ? std::atoi(e) : 3;
-    if (g_variant < 0 || g_variant > 3) g_variant = 3;
+    if (g_variant < 0 || g_variant > 4) g_variant = 3;
   }
   return g_variant;
 }
 int bk_of(int v) { return v == 1 ? 64 : 32; }
 
 }  // namespace
+
+void wgrad256_set_variant(int v) { g_variant = v >= 0 && v <= 4 ? v : 3; }
 
 bool wgrad256_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) {
   return M % kTile == 0 && N % kTile == 0 && M > 0 && N > 0 && K > 0 && K < (int64_t(1) << 31) && lda % 8 == 0 &&
@@ -355,10 +507,11 @@ void gemm_wgrad256(const void* a, const void* b, float* ws, int64_t lda, int64_t
   const int64_t grid = static_cast<int64_t>(s) * p.tiles_m * p.tiles_n;
   if (grid > 0x7fffffff) throw std::runtime_error("gemm_wgrad256: grid too large");
   constexpr int kSmem = 128 * 1024;  // both variants: 4 x 32 KiB / 2 x 64 KiB
-  static bool attr[4] = {false, false, false, false};
+  static bool attr[5] = {false, false, false, false, false};
   const void* fn = v == 1   ? reinterpret_cast<const void*>(&wgrad256_kernel<64, 2>)
                    : v == 2 ? reinterpret_cast<const void*>(&wgrad256_kernel<32, 4, true>)
                    : v == 3 ? reinterpret_cast<const void*>(&wgrad256h_kernel<32, 4>)
+                   : v == 4 ? reinterpret_cast<const void*>(&wgrad256pp_kernel)
                             : reinterpret_cast<const void*>(&wgrad256_kernel<32, 4>);
   if (!attr[v]) {
     FLUXMPI_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, kSmem));
@@ -367,6 +520,7 @@ void gemm_wgrad256(const void* a, const void* b, float* ws, int64_t lda, int64_t
   if (v == 1) wgrad256_kernel<64, 2><<<static_cast<unsigned>(grid), kThreads, kSmem, stream>>>(p);
   else if (v == 2) wgrad256_kernel<32, 4, true><<<static_cast<unsigned>(grid), kThreads, kSmem, stream>>>(p);
   else if (v == 3) wgrad256h_kernel<32, 4><<<static_cast<unsigned>(grid), kThreads, kSmem, stream>>>(p);
+  else if (v == 4) wgrad256pp_kernel<<<static_cast<unsigned>(grid), kThreads, kSmem, stream>>>(p);
   else wgrad256_kernel<32, 4><<<static_cast<unsigned>(grid), kThreads, kSmem, stream>>>(p);
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }

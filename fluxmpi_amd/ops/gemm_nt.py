@@ -13,8 +13,11 @@ tile exactly; :func:`supported` says whether a call qualifies, callers keep the 
 otherwise. Numerics: bf16 operands, fp32 accumulation, one bf16 rounding of each output (the
 GELU of the ROUNDED pre-activation, like ``F.gelu(F.linear(...))``).
 
-``FLUXMPI_GEMM_NT``: ``all`` (default) every qualifying forward / input gradient; ``fused`` only
-the calls that carry an epilogue fusion (GELU forward / backward); ``0`` never (hipBLASLt).
+``FLUXMPI_GEMM_NT``: ``fused`` (default) only the calls that carry an epilogue fusion (fc1's bias +
+GELU forward, fc2's input gradient with fc1's GELU backward + bias gradient); ``all`` every
+qualifying forward / input gradient; ``0`` never (hipBLASLt). Measured (profiles/rd4c_gemm_nt.md):
+the plain K = 768 GEMMs are 5-10 % behind hipBLASLt's stream-K kernels, whose epilogues do not
+all land in one bandwidth burst.
 """
 from __future__ import annotations
 
@@ -26,7 +29,7 @@ from . import _ext
 from . import graddst
 from .multi_tensor import DTYPE_CODE
 
-MODE = os.environ.get("FLUXMPI_GEMM_NT", "all").lower()
+MODE = os.environ.get("FLUXMPI_GEMM_NT", "fused").lower()
 ENABLED = MODE != "0"
 
 

@@ -3,7 +3,7 @@
 source "$(dirname "$0")/gpu_lib.sh"
 rm -f "$OUT/steps.log" "$OUT/bench_results.jsonl"
 T="python -u -m pytest -x -q --timeout 120 --timeout-method thread"
-step bench_gemm_nt 400 0 python -u scripts/bench_gemm_nt.py
+step bench_wgrad 300 0 python -u scripts/bench_wgrad.py
 step test_gemm_nt 400 0 $T tests/test_gemm_nt_gpu.py
 step test_touched 600 0 $T tests/test_attention_gpu.py tests/test_vit_gpu.py tests/test_vit_model_gpu.py tests/test_comm_gpu.py tests/test_linear_gpu.py tests/test_stem_gpu.py tests/test_layernorm.py tests/test_deq.py -m gpu
 step bench_vit 300 0 python -u bench.py --model vit_b16 --steps 10 --warmup 5
