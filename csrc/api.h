@@ -233,9 +233,11 @@ void gemm_wgrad256(const void* a, const void* b, float* ws, int64_t lda, int64_t
 // 2 (C = bf16(acc) * gelu'(h), colpart[2 * M / 256][N] = per-half-tile column sums of C).
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc);
 int gemm_nt_colpart_rows(int64_t M);
+int64_t gemm_nt_ws_floats();  // per-stream stream-K partial slots (fp32)
+int64_t gemm_nt_flag_ints();  // per-stream publish flags (int32, zero-initialised once)
 void gemm_nt(const void* a, const void* b, void* c, void* c2, const void* bias, int bias_f32, const void* h,
-             float* colpart, int64_t lda, int64_t ldb, int64_t ldc, int64_t M, int64_t N, int64_t K, int epi,
-             hipStream_t stream);
+             float* colpart, float* ws, int* flags, int64_t lda, int64_t ldb, int64_t ldc, int64_t M, int64_t N,
+             int64_t K, int epi, hipStream_t stream);
 // dst[c][r] = src[r][c], bf16 (rows, cols, leading dims multiples of 8)
 void transpose_bf16(const void* src, void* dst, int64_t rows, int64_t cols, int64_t lds, int64_t ldd,
                     hipStream_t stream);

@@ -51,6 +51,8 @@ namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) char lds_char;
 typedef __attribute__((address_space(1))) void gl_void;
 
@@ -73,6 +75,8 @@ struct NTArgs {
   const void* bias;    // [N] fp32 / bf16 (bias_f32), or nullptr
   const bf16* h;       // EPI 2: GELU input [M][ldc]
   float* colpart;      // EPI 2: [2 * tiles_m][N]
+  float* ws;           // stream-K partials: [grid][32][512] float4 (gemm_nt_workspace_bytes)
+  int* flags;          // [grid][8] per-wave publish flags, zero between launches
   int64_t lda, ldb, ldc;
   int64_t N;
   int nk;              // K / 64
@@ -102,48 +106,70 @@ __device__ __forceinline__ void glds16(const void* src, char* dst) {
 
 __device__ __forceinline__ bf16x8 frag(const char* __restrict__ p) { return *reinterpret_cast<const bf16x8*>(p); }
 
-// Tile list of workgroup g (grid G, persistent): rounds i = 0, 1, ... with g + i G < nt; round i
-// covers tile ids [i G, i G + cnt), cnt = min(G, nt - i G), and g takes id i G + xcd_order(g, cnt)
-// (bijective: the workgroups of one XCD take a contiguous range of ids, N fastest).
+// Stream-K over the whole problem: the U = tiles x nk (tile, k-tile) units are dealt to the G
+// persistent workgroups as equal contiguous ranges (workgroups of one XCD take neighbouring
+// ranges: the tiles of one XCD share their A row panels in its L2). Tiles are N-fastest, a
+// tile's k-tiles consecutive. A workgroup's range is ONE stream of k-tiles (stream slot s uses
+// LDS buffer s & 1): the DMA of a tile's first k-tiles is in flight while the previous tile's
+// epilogue stores, and because the ranges start at different points of their tiles the
+// workgroups' epilogues (bandwidth bursts) do not all land at once, and no round is partial.
+// A range that starts inside a tile writes that segment's fp32 partial to its slot of the
+// workspace (each wave its own 32 x 16 B per lane, then an agent-scope release and a per-wave
+// flag); the workgroup whose range covers the tile's FIRST k-tile finishes it: at the end of
+// its range it polls the flags of the following workgroups whose ranges start inside the tile
+// (relaxed agent-scope loads), acquires, adds their partials and runs the epilogue (flags reset
+// to 0 for the next launch). Contributors publish at the START of their ranges and never wait,
+// so the wait is deadlock-free whatever the residency (MI355X_MICROARCH.md "Workgroup dispatch
+// ... inter-workgroup visibility", cdna_hip_programming.md Guideline 16).
+// After an epilogue the first k-tile's waits count its vector-memory instructions (kEpiVm):
+// they are younger than the DMA groups those waits retire.
+// BIAS: 0 none, 1 fp32, 2 bf16 (EPI 0 / 1), staged into LDS by one LDS-DMA of wave 0 at the
+// first k-tile of the finishing segment.
 struct TileInfo {
   int64_t aoff, boff;  // m0 * lda, n0 * ldb
   int64_t m0, n0;
   int tm;
 };
 
-__device__ __forceinline__ TileInfo tile_info(const NTArgs& p, int g, int G, int i) {
-  const int nt = p.tiles_m * p.tiles_n;
-  const int base = i * G;
-  const int cnt = min(G, nt - base);
-  const int q = cnt / 8, r = cnt % 8, xcd = g % 8, pos = g / 8;
-  const int lid = base + (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+__device__ __forceinline__ int64_t uni64(int64_t v) {  // provably wave-uniform (SGPRs)
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32));
+  return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
+}
+
+__device__ __forceinline__ TileInfo tile_of(const NTArgs& p, int T) {
   TileInfo t;
-  t.tm = lid / p.tiles_n;
-  const int tn = lid - t.tm * p.tiles_n;
-  t.m0 = static_cast<int64_t>(t.tm) * kT;
-  t.n0 = static_cast<int64_t>(tn) * kT;
-  t.aoff = t.m0 * p.lda;
-  t.boff = t.n0 * p.ldb;
+  T = __builtin_amdgcn_readfirstlane(T);
+  t.tm = __builtin_amdgcn_readfirstlane(T / p.tiles_n);
+  const int tn = T - t.tm * p.tiles_n;
+  t.m0 = uni64(static_cast<int64_t>(t.tm) * kT);
+  t.n0 = uni64(static_cast<int64_t>(tn) * kT);
+  t.aoff = uni64(t.m0 * p.lda);
+  t.boff = uni64(t.n0 * p.ldb);
   return t;
 }
 
-// Persistent: the k-tiles of all of this workgroup's output tiles form ONE stream (stream slot
-// s uses LDS buffer s & 1); the DMA of the next tile's first k-tiles is in flight while a tile's
-// epilogue stores, so a tile costs its main loop plus its epilogue's issue time, no prologue.
-// After an epilogue the first k-tile's waits count its vector-memory instructions (kEpiVm):
-// they are younger than the DMA groups those waits retire.
-// BIAS: 0 none, 1 fp32, 2 bf16 (EPI 0 / 1). The bias of a tile is loaded at the start of its
-// last k-tile: loaded in the epilogue, its wait would also retire the next tile's DMA.
+// first unit of workgroup (range) r
+__device__ __forceinline__ int range_start(int U, int G, int r) {
+  return static_cast<int>(static_cast<int64_t>(U) * r / G);
+}
+
 template <int EPI, int BIAS>
 __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[kSmem];
   constexpr int kEpiVm = EPI == 0 ? 32 : 56;  // vector-memory instructions per wave in an epilogue (lower bound)
-  const int G = gridDim.x, g = blockIdx.x;
-  const int nt = p.tiles_m * p.tiles_n;
-  const int nmine = (nt - g + G - 1) / G;
+  const int G = gridDim.x;
+  int gi = blockIdx.x;
+  {  // bijective XCD-aware range order: the workgroups of one XCD take neighbouring ranges
+    const int q = G / 8, r = G % 8, xcd = gi % 8, pos = gi / 8;
+    gi = __builtin_amdgcn_readfirstlane((xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos);
+  }
+  const int nk = p.nk;  // >= 2
+  const int U = p.tiles_m * p.tiles_n * nk;  // < 2^31 (gemm_nt_supported)
+  const int u0 = __builtin_amdgcn_readfirstlane(range_start(U, G, gi));
+  const int u1 = __builtin_amdgcn_readfirstlane(range_start(U, G, gi + 1));
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // wave-uniform
   const int wr = wave >> 2, wc = wave & 3;
-  const int nk = p.nk;  // >= 2
 
   // ---- LDS-DMA lanes: a wave-instruction fills 8 rows x 8 chunks; lane -> row lane >> 3, slot lane & 7
   const int lrow = lane >> 3, lslot = lane & 7;
@@ -163,20 +189,25 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
   const int dstB = kImg + 32 * wave * kRow;
   const void* zero = g_zero_nt;
 
-  // DMA of stream slot s (LDS buffer s & 1): k-tile tk of the current tile (nxt = false) or of
-  // the next one (nxt = true; a zero line into the dead slot when there is none)
-  TileInfo cur = tile_info(p, g, G, 0);
-  TileInfo nxt = tile_info(p, g, G, nmine > 1 ? 1 : 0);
-  bool has_nxt = nmine > 1;
-  auto issueA = [&](int s, bool n, int tk, int ph) {
-    const int64_t base = n ? nxt.aoff : cur.aoff;
-    const void* src = (!n || has_nxt) ? static_cast<const void*>(p.a + base + laneA + ph * aPhase + tk * kBK) : zero;
-    glds16(src, smem + (s & 1) * kBuf + dstA + ph * 32 * kRow);
+  // DMA into stream slot s (LDS buffer s & 1) of k-tile tk of tile `ti`. Source = a wave-uniform
+  // base (SGPRs: readfirstlane) + the lane's 32-bit byte offset, so no 64-bit per-lane address is
+  // kept live across the loop. Past the range's end (`ok` false) the slot is dead and the DMA just
+  // re-reads valid bytes (the caller passes the current unit), keeping the vmcnt count fixed.
+  const uint32_t laneAb = static_cast<uint32_t>(laneA) * 2u;
+  uint32_t laneBb[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) laneBb[j] = static_cast<uint32_t>(laneB[j]) * 2u;
+  auto sbase = [](const bf16* base, int64_t elems) {
+    const uint64_t a = reinterpret_cast<uint64_t>(base + elems);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
+    return reinterpret_cast<const char*>((static_cast<uint64_t>(hi) << 32) | lo);
   };
-  auto issueB = [&](int s, bool n, int tk, int j) {
-    const int64_t base = n ? nxt.boff : cur.boff;
-    const void* src = (!n || has_nxt) ? static_cast<const void*>(p.b + base + laneB[j] + tk * kBK) : zero;
-    glds16(src, smem + (s & 1) * kBuf + dstB + j * 8 * kRow);
+  auto issueA = [&](int s, const TileInfo& ti, int tk, int ph) {
+    glds16(sbase(p.a, ti.aoff + ph * aPhase + tk * kBK) + laneAb, smem + (s & 1) * kBuf + dstA + ph * 32 * kRow);
+  };
+  auto issueB = [&](int s, const TileInfo& ti, int tk, int j) {
+    glds16(sbase(p.b, ti.boff + tk * kBK) + laneBb[j], smem + (s & 1) * kBuf + dstB + j * 8 * kRow);
   };
 
   // ---- fragment reads: lane row (lane & 15), chunk (lane >> 4) + 4 kh at slot chunk ^ swz(row)
@@ -191,43 +222,50 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
 
   f32x4 acc[4][2][4];
   bf16x8 fb[4][2];
-  int s = 0;  // stream slot of the current k-tile
+  const int cq = 4 * (lane >> 4);
+  int seg = 0;  // segments (tile pieces) started so far: parity of the bias slot
 
-  // ---- prologue: B(0), A(0) phases 0..3, B(1)
+  // ---- prologue: B(u0), A(u0) phases 0..3, B(u0 + 1)
+  {
+    const int T0 = u0 / nk, t0 = u0 - T0 * nk;
+    const TileInfo a0 = tile_of(p, T0);
+    const TileInfo a1 = t0 + 1 < nk ? a0 : tile_of(p, T0 + 1);
+    const int t1 = t0 + 1 < nk ? t0 + 1 : 0;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) issueB(0, false, 0, j);
+    for (int j = 0; j < 4; ++j) issueB(0, a0, t0, j);
 #pragma unroll
-  for (int ph = 0; ph < 4; ++ph) issueA(0, false, 0, ph);
+    for (int ph = 0; ph < 4; ++ph) issueA(0, a0, t0, ph);
+    const bool ok1 = u0 + 1 < u1;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) issueB(1, false, 1, j);
+    for (int j = 0; j < 4; ++j) issueB(1, ok1 ? a1 : a0, ok1 ? t1 : t0, j);
+  }
   asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if (wr == 1) __builtin_amdgcn_s_barrier();  // the stagger: waves 4-7 one barrier behind
 
-  const int cq = 4 * (lane >> 4);
-  int tile_i = 0;
-
-  // one k-tile (4 phases) of the current tile; FIRST: the accumulators start from zero (and wave 0
-  // stages the tile's bias); XV: vector-memory instructions issued since the DMA groups this
-  // k-tile's first three waits retire
-  auto ktile = [&](int t, auto first_c, auto last_c, auto xv_c) {
+  // one k-tile (4 phases) of unit u; FIRST: the accumulators start from zero (and wave 0 stages
+  // the tile's bias when the segment will finish the tile); XV: vector-memory instructions
+  // issued since the DMA groups this k-tile's first three waits retire
+  auto ktile = [&](int u, int t, const TileInfo& cur, const TileInfo& nxt, bool stage_bias, auto first_c,
+                   auto xv_c) {
     constexpr bool FIRST = decltype(first_c)::value;
-    constexpr bool LAST = decltype(last_c)::value;
     constexpr int XV = decltype(xv_c)::value;
-    if (FIRST && BIAS != 0 && wave == 0) {
-      // the tile's 256 bias values (fp32 1 KiB / bf16 512 B) into its parity's LDS slot by one
-      // LDS-DMA of wave 0; read in the epilogue, after many barriers and wave 0's vmcnt waits
+    if (FIRST && BIAS != 0 && wave == 0 && stage_bias) {
+      // the tile's 256 bias values (fp32 1 KiB / bf16 512 B) into the segment's parity LDS slot
       const char* src = BIAS == 1 ? reinterpret_cast<const char*>(static_cast<const float*>(p.bias) + cur.n0) + 16 * lane
                                   : (lane < 32 ? reinterpret_cast<const char*>(static_cast<const bf16*>(p.bias) + cur.n0) + 16 * lane
                                                : reinterpret_cast<const char*>(zero));
-      glds16(src, smem + kBiasOff + (tile_i & 1) * 1024);
+      glds16(src, smem + kBiasOff + (seg & 1) * 1024);
     }
-    const char* buf = smem + (s & 1) * kBuf;
-    // DMA targets: A of stream slot s + 1, B of slot s + 2
-    const bool an = t + 1 >= nk;
-    const int at = an ? t + 1 - nk : t + 1;
-    const bool bn = t + 2 >= nk;
-    const int bt = bn ? t + 2 - nk : t + 2;
+    const int sl = u - u0;  // stream slot
+    const char* buf = smem + (sl & 1) * kBuf;
+    // DMA targets: A of unit u + 1, B of unit u + 2 (the next tile's first k-tiles at the end;
+    // the current unit again past the range's end)
+    const bool an = t + 1 >= nk, bn = t + 2 >= nk;
+    const bool aok = u + 1 < u1, bok = u + 2 < u1;
+    const int at = !aok ? t : (an ? t + 1 - nk : t + 1), bt = !bok ? t : (bn ? t + 2 - nk : t + 2);
+    const TileInfo& ta = aok && an ? nxt : cur;
+    const TileInfo& tb = bok && bn ? nxt : cur;
 #pragma unroll
     for (int ph = 0; ph < 4; ++ph) {
       // ---------- load segment
@@ -242,12 +280,12 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int kh = 0; kh < 2; ++kh) fa[i][kh] = frag(buf + offA[kh] + (32 * ph + 16 * i) * kRow);
-      issueA(s + 1, an, at, ph);
+      issueA(sl + 1, ta, at, ph);
       if (ph == 1) {
-        issueB(s + 2, bn, bt, 0);
-        issueB(s + 2, bn, bt, 1);
+        issueB(sl + 2, tb, bt, 0);
+        issueB(sl + 2, tb, bt, 1);
       } else if (ph >= 2) {
-        issueB(s + 2, bn, bt, ph);
+        issueB(sl + 2, tb, bt, ph);
       }
       if (ph < 3 && XV > 0) {
         if constexpr (7 + XV >= 63) asm volatile("s_waitcnt vmcnt(63) lgkmcnt(0)" ::: "memory");
@@ -273,21 +311,79 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
     }
-    ++s;
   };
 
+  // partial slots through a buffer resource: the lane offset is one VGPR (threadIdx.x * 16), the
+  // slot + element offset a wave-uniform SGPR (soffset), so the 32 stores / loads of a slot keep
+  // no per-instruction 64-bit address live next to the 128 accumulator VGPRs
+  const __amdgpu_buffer_rsrc_t wsr = __builtin_amdgcn_make_buffer_rsrc(p.ws, 0, 0x7fffffff, 0x00020000);
+  const int wlane = threadIdx.x * 16;
+  auto slot_off = [&](int r, int idx) { return __builtin_amdgcn_readfirstlane((r * 32 + idx) * (kThreads * 16)); };
   using Z = std::integral_constant<int, 0>;
-  for (int i = 0;;) {
-    if (i == 0) ktile(0, std::true_type{}, std::false_type{}, Z{});
-    else ktile(0, std::true_type{}, std::false_type{}, std::integral_constant<int, kEpiVm>{});
-    for (int t = 1; t < nk; ++t) ktile(t, std::false_type{}, std::false_type{}, Z{});
+  bool after_epi = false;
+  int T = u0 / nk;
+  TileInfo cur = tile_of(p, T);
+  for (int u = u0; u < u1;) {
+    const int ts = u - T * nk;
+    const int tile_end = (T + 1) * nk;
+    const int te = (u1 < tile_end ? u1 : tile_end) - T * nk;
+    const TileInfo nxt = tile_of(p, T + 1 < p.tiles_m * p.tiles_n ? T + 1 : T);
+    const bool finish = ts == 0;  // this segment owns the tile's first k-tile: it runs the epilogue
+    if (after_epi) ktile(u, ts, cur, nxt, finish, std::true_type{}, std::integral_constant<int, kEpiVm>{});
+    else ktile(u, ts, cur, nxt, finish, std::true_type{}, Z{});
+    for (int t = ts + 1; t < te; ++t) ktile(u + (t - ts), t, cur, nxt, finish, std::false_type{}, Z{});
+    u += te - ts;
+    after_epi = false;
+    if (!finish) {
+      // ---- contributor: publish this segment's partial for the workgroup that finishes the tile
+#pragma unroll
+      for (int ph = 0; ph < 4; ++ph)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, acc[ph][i][j]), wsr, wlane,
+                                                   slot_off(gi, (ph * 2 + i) * 4 + j), 0);
+          }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep the fence's wait (ROCm 7.2 may drop it)
+      if (lane == 0) __hip_atomic_store(p.flags + gi * 8 + wave, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ++seg;
+      ++T;
+      cur = nxt;
+      continue;  // its waits drained every older transfer: no epilogue count for the next k-tile
+    }
+    if (te < nk) {
+      // ---- finisher of a tile the following ranges complete: add their partials (in order)
+      for (int r = gi + 1; r < G && range_start(U, G, r) < (T + 1) * nk; ++r) {
+        int* flag = p.flags + r * 8 + wave;
+        if (lane == 0) {
+          while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) __builtin_amdgcn_s_sleep(2);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int ph = 0; ph < 4; ++ph) {  // 8 loads in flight at a time (the accumulators hold 128 VGPRs)
+          i32x4 v[2][4];
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[i][j] = __builtin_amdgcn_raw_buffer_load_b128(wsr, wlane, slot_off(r, (ph * 2 + i) * 4 + j), 0);
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[ph][i][j] += __builtin_bit_cast(f32x4, v[i][j]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (lane == 0) __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
 
     // ---- epilogue: acc[ph][i][j][r] = C[m0 + wr*128 + 32ph + 16i + (lane & 15)][n0 + wc*64 + 16j + 4(lane >> 4) + r]
-    const int64_t ncol = cur.n0 + wc * 64 + cq;
     float bias[4][4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const char* bl = smem + kBiasOff + (tile_i & 1) * 1024;
+      const char* bl = smem + kBiasOff + (seg & 1) * 1024;
       const int col = wc * 64 + 16 * j + cq;
       if (BIAS == 1) {
         const float4 v = *reinterpret_cast<const float4*>(bl + 4 * col);
@@ -306,25 +402,36 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
-    uint2 hv[4][2][4];  // EPI 2: every GELU input of the tile's lane issued before the first use (one round trip)
+    // outputs through buffer resources based at the tile's first element (wave-uniform SGPRs):
+    // voffset = the lane's (row, column) byte offset in the tile (one VGPR), soffset = the
+    // (ph, ii) row block, the j column block an immediate
+    auto tile_rsrc = [&](const void* base) {
+      const uint64_t a = reinterpret_cast<uint64_t>(static_cast<const bf16*>(base) + cur.m0 * p.ldc + cur.n0);
+      const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
+      const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
+      return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo), 0,
+                                               0x7fffffff, 0x00020000);
+    };
+    const int ldcb = static_cast<int>(p.ldc) * 2;  // < 2^23 (gemm_nt_supported)
+    const int vo = (wr * 128 + fr) * ldcb + (wc * 64 + cq) * 2;
+    auto rowblk = [&](int ph, int ii) { return __builtin_amdgcn_readfirstlane((32 * ph + 16 * ii) * ldcb); };
+    const __amdgpu_buffer_rsrc_t crs = tile_rsrc(p.c);
+    i32x2 hv[4][2][4];  // EPI 2: every GELU input of the tile's lane issued before the first use (one round trip)
     if (EPI == 2) {
+      const __amdgpu_buffer_rsrc_t hrs = tile_rsrc(p.h);
 #pragma unroll
       for (int ph = 0; ph < 4; ++ph)
 #pragma unroll
         for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            hv[ph][ii][j] = *reinterpret_cast<const uint2*>(
-                p.h + (cur.m0 + wr * 128 + 32 * ph + 16 * ii + fr) * p.ldc + ncol + 16 * j);
+          for (int j = 0; j < 4; ++j) hv[ph][ii][j] = __builtin_amdgcn_raw_buffer_load_b64(hrs, vo + 32 * j, rowblk(ph, ii), 0);
     }
 #pragma unroll
     for (int ph = 0; ph < 4; ++ph) {
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii) {
-        const int64_t m = cur.m0 + wr * 128 + 32 * ph + 16 * ii + fr;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int64_t off = m * p.ldc + ncol + 16 * j;
           bf16 o[4];
           if (EPI == 0) {
 #pragma unroll
@@ -343,9 +450,9 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
                 gg[r] = static_cast<bf16>(x * cdf);
               }
             }
-            uint2 gv;
+            i32x2 gv;
             __builtin_memcpy(&gv, gg, 8);
-            *reinterpret_cast<uint2*>(p.c2 + off) = gv;
+            __builtin_amdgcn_raw_buffer_store_b64(gv, tile_rsrc(p.c2), vo + 32 * j, rowblk(ph, ii), 0);
           } else {
             bf16 hh[4];
             __builtin_memcpy(hh, &hv[ph][ii][j], 8);
@@ -365,9 +472,9 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
               cs[j][r] += static_cast<float>(o[r]);  // the bias gradient of the rounded dh
             }
           }
-          uint2 ov;
+          i32x2 ov;
           __builtin_memcpy(&ov, o, 8);
-          *reinterpret_cast<uint2*>(p.c + off) = ov;
+          __builtin_amdgcn_raw_buffer_store_b64(ov, crs, vo + 32 * j, rowblk(ph, ii), 0);
         }
       }
     }
@@ -377,16 +484,15 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) cs[j][r] = row_sum16(cs[j][r]);
       if (fr == 0) {
-        float* dst = p.colpart + static_cast<int64_t>(2 * cur.tm + wr) * p.N + ncol;
+        float* dst = p.colpart + static_cast<int64_t>(2 * cur.tm + wr) * p.N + cur.n0 + wc * 64 + cq;
 #pragma unroll
         for (int j = 0; j < 4; ++j) *reinterpret_cast<float4*>(dst + 16 * j) = float4{cs[j][0], cs[j][1], cs[j][2], cs[j][3]};
       }
     }
-    if (++i >= nmine) break;
-    tile_i = i;
+    ++seg;
+    after_epi = true;
+    ++T;
     cur = nxt;
-    has_nxt = i + 1 < nmine;
-    nxt = tile_info(p, g, G, has_nxt ? i + 1 : i);
   }
   if (wr == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dead-slot DMAs
@@ -424,17 +530,25 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restr
   }
 }
 
-int g_cus = 0;
+int cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    FLUXMPI_HIP_CHECK(hipGetDevice(&dev));
+    FLUXMPI_HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  return n;
+}
+
+// one persistent workgroup per CU (fewer when there are fewer units than CUs)
+int grid_of(const NTArgs& p) {
+  const int64_t U = static_cast<int64_t>(p.tiles_m) * p.tiles_n * p.nk;
+  return static_cast<int>(U < cus() ? U : cus());
+}
 
 template <int EPI, int BIAS>
 void launch(const NTArgs& p, hipStream_t stream) {
-  if (g_cus == 0) {
-    int dev = 0;
-    FLUXMPI_HIP_CHECK(hipGetDevice(&dev));
-    FLUXMPI_HIP_CHECK(hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev));
-  }
-  const int nt = p.tiles_m * p.tiles_n;
-  gemm_nt_kernel<EPI, BIAS><<<nt < g_cus ? nt : g_cus, kThreads, 0, stream>>>(p);
+  gemm_nt_kernel<EPI, BIAS><<<grid_of(p), kThreads, 0, stream>>>(p);
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
 
@@ -443,15 +557,23 @@ void launch(const NTArgs& p, hipStream_t stream) {
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc) {
   // the tile grid covers M, N and K exactly (no guards in the loaders or the epilogue)
   return M > 0 && N > 0 && K >= 2 * kBK && M % kT == 0 && N % kT == 0 && K % kBK == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
-         ldc % 8 == 0 && lda >= K && ldb >= K && ldc >= N && lda < (int64_t(1) << 23) && ldb < (int64_t(1) << 23) && M / kT * (N / kT) < (int64_t(1) << 31) &&
-         K / kBK < (int64_t(1) << 30);
+         ldc % 8 == 0 && lda >= K && ldb >= K && ldc >= N && lda < (int64_t(1) << 23) && ldb < (int64_t(1) << 23) &&
+         ldc < (int64_t(1) << 22) &&  // the epilogue's 32-bit byte offsets within a tile
+         M / kT * (N / kT) * (K / kBK) < (int64_t(1) << 31);
 }
 
 int gemm_nt_colpart_rows(int64_t M) { return static_cast<int>(2 * (M / kT)); }
 
+// stream-K workspace for one stream: fp32 partial slots [CUs][32][512] float4 and [CUs][8] int flags
+// (zero-initialised once; every launch leaves them zero)
+int64_t gemm_nt_ws_floats() { return static_cast<int64_t>(cus()) * 32 * kThreads * 4; }
+int64_t gemm_nt_flag_ints() { return static_cast<int64_t>(cus()) * 8; }
+
 void gemm_nt(const void* a, const void* b, void* c, void* c2, const void* bias, int bias_f32, const void* h,
-             float* colpart, int64_t lda, int64_t ldb, int64_t ldc, int64_t M, int64_t N, int64_t K, int epi,
-             hipStream_t stream) {
+             float* colpart, float* ws, int* flags, int64_t lda, int64_t ldb, int64_t ldc, int64_t M, int64_t N,
+             int64_t K, int epi, hipStream_t stream) {
+  if (ws == nullptr || flags == nullptr || (reinterpret_cast<uintptr_t>(ws) & 15u) != 0)
+    throw std::runtime_error("gemm_nt: needs its stream-K workspace (gemm_nt_ws_floats / gemm_nt_flag_ints)");
   if (!gemm_nt_supported(M, N, K, lda, ldb, ldc))
     throw std::runtime_error("gemm_nt: unsupported shape (M, N multiples of 256, K of 64, leading dims of 8; M=" +
                              std::to_string(M) + " N=" + std::to_string(N) + " K=" + std::to_string(K) + ")");
@@ -463,7 +585,7 @@ void gemm_nt(const void* a, const void* b, void* c, void* c2, const void* bias, 
   if (bias != nullptr && (reinterpret_cast<uintptr_t>(bias) & (bias_f32 ? 15u : 7u)) != 0)
     throw std::runtime_error("gemm_nt: bias must be 16-byte (fp32) / 8-byte (bf16) aligned");
   NTArgs p{static_cast<const bf16*>(a), static_cast<const bf16*>(b), static_cast<bf16*>(c), static_cast<bf16*>(c2),
-           bias, static_cast<const bf16*>(h), colpart, lda, ldb, ldc, N, static_cast<int>(K / kBK),
+           bias, static_cast<const bf16*>(h), colpart, ws, flags, lda, ldb, ldc, N, static_cast<int>(K / kBK),
            static_cast<int>(M / kT), static_cast<int>(N / kT), bias_f32, gelu_form()};
   const int bk = bias == nullptr ? 0 : bias_f32 ? 1 : 2;
   if (epi == 2) {

@@ -14,6 +14,7 @@ gradient arrival order).
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -366,7 +367,11 @@ class DEQFixedPoint(nn.Module):
         with torch.no_grad():
             z, self.last_iters, _ = anderson(fz, torch.zeros_like(x), max_iter=self.max_iter,
                                              tol=self.tol, check_lag=self.check_lag, graphs=gs)
-        z = self.f(z, x)  # one differentiable step re-engages autograd at z*
+        # one differentiable step re-engages autograd at z*; its GroupNorms save fresh fp32 affine
+        # copies, not the graphs' static buffers (a later forward at this shape rewrites those in
+        # place before this one's backward)
+        with fp32_affine_cache(self.f) if gs is not None else contextlib.nullcontext():
+            z = self.f(z, x)
         if not torch.is_grad_enabled():
             return z
         if gs is not None:

@@ -37,6 +37,21 @@ def _stream(t):
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
+_WS: dict = {}
+
+
+def _workspace(C, device: torch.device, stream: int):
+    """The stream-K partial slots and publish flags of one (device, stream): flags are zeroed once
+    and every launch leaves them zero; launches on one stream are ordered, so they share it."""
+    key = (device.index, stream)
+    ws = _WS.get(key)
+    if ws is None:
+        ws = (torch.empty(int(C.gemm_nt_ws_floats()), device=device, dtype=torch.float32),
+              torch.zeros(int(C.gemm_nt_flag_ints()), device=device, dtype=torch.int32))
+        _WS[key] = ws
+    return ws[0].data_ptr(), ws[1].data_ptr()
+
+
 def supported(rows: int, n_out: int, k: int, *tensors: torch.Tensor, fused: bool = False) -> bool:
     """Whether gemm_nt takes ``[rows, k] x [n_out, k]^T`` (both operands k-contiguous after the
     weight transpose of an input gradient) under the current mode."""
@@ -73,9 +88,10 @@ def linear_fwd(x2: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None
         from .gelu import _sync
         _sync(C)  # EPI 1 computes the selected GELU form
     b = bias.contiguous() if bias is not None else None
+    s = _stream(x2)
     C.gemm_nt(x2.data_ptr(), w.data_ptr(), y.data_ptr(), g.data_ptr() if gelu else 0,
               b.data_ptr() if b is not None else 0, int(b is not None and b.dtype == torch.float32), 0, 0,
-              k, k, n, m, n, k, 1 if gelu else 0, _stream(x2))
+              *_workspace(C, x2.device, s), k, k, n, m, n, k, 1 if gelu else 0, s)
     return (y, g) if gelu else y
 
 
@@ -92,15 +108,16 @@ def linear_dgrad(dy2: torch.Tensor, weight: torch.Tensor, gelu_h: torch.Tensor |
     dx = torch.empty(m, k, device=dy2.device, dtype=dy2.dtype)
     s = _stream(dy2)
     if gelu_h is None:
-        C.gemm_nt(dy2.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, 0, 0, 0, 0, n, n, k, m, k, n, 0, s)
+        C.gemm_nt(dy2.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, 0, 0, 0, 0, *_workspace(C, dy2.device, s),
+                  n, n, k, m, k, n, 0, s)
         return dx
     from .gelu import _sync
     _sync(C)  # EPI 2 differentiates the selected GELU form
     h = gelu_h.reshape(m, k).contiguous()
     rows = C.gemm_nt_colpart_rows(m)
     part = torch.empty(rows, k, device=dy2.device, dtype=torch.float32)
-    C.gemm_nt(dy2.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, 0, 0, h.data_ptr(), part.data_ptr(), n, n, k, m, k, n,
-              2, s)
+    C.gemm_nt(dy2.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, 0, 0, h.data_ptr(), part.data_ptr(),
+              *_workspace(C, dy2.device, s), n, n, k, m, k, n, 2, s)
     odt = bias_dtype if bias_dtype in (torch.float32, torch.bfloat16) else torch.float32
     with graddst.into(bias_param):
         db = graddst.empty((k,), odt, dy2.device)

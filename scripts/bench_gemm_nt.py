@@ -16,6 +16,7 @@ import torch
 
 sys.path.insert(0, __file__.rsplit("/scripts/", 1)[0])
 from fluxmpi_amd.ops import _ext  # noqa: E402
+from fluxmpi_amd.ops.gemm_nt import _workspace  # noqa: E402
 
 
 def t_us(fn, iters=20):
@@ -51,12 +52,13 @@ def checks_only(C, st, name, m, n, k):
     ref = a.float() @ w.float().t()
     for bdt in (torch.float32, torch.bfloat16):
         b = bias.to(bdt)
-        C.gemm_nt(a.data_ptr(), w.data_ptr(), c.data_ptr(), 0, b.data_ptr(), int(bdt == torch.float32), 0, 0,
-                  k, k, n, m, n, k, 0, st)
-        torch.cuda.synchronize()
-        check(f"{name}_epi0_bias_{str(bdt)[6:]}", c, ref + b.float())
+        for _ in range(2):  # twice: the first launch must leave the publish flags zero
+            C.gemm_nt(a.data_ptr(), w.data_ptr(), c.data_ptr(), 0, b.data_ptr(), int(bdt == torch.float32), 0, 0,
+                      *_workspace(C, a.device, st), k, k, n, m, n, k, 0, st)
+            torch.cuda.synchronize()
+            check(f"{name}_epi0_bias_{str(bdt)[6:]}", c, ref + b.float())
     C.gemm_nt(a.data_ptr(), w.data_ptr(), c.data_ptr(), c2.data_ptr(), bias.data_ptr(), 1, 0, 0,
-              k, k, n, m, n, k, 1, st)
+              *_workspace(C, a.device, st), k, k, n, m, n, k, 1, st)
     torch.cuda.synchronize()
     check(f"{name}_epi1_g", c2, torch.nn.functional.gelu((ref + bias).bfloat16().float(), approximate="tanh"))
 
@@ -72,8 +74,9 @@ def main():
     if quick:
         shapes = shapes[:3]
     # correctness-only shapes: odd k-tile counts (LDS buffer parity flips between tiles), the
-    # minimum K, more tiles than CUs with a partial last round
-    for name, m, n, k in (("odd_nk13", 256 * 41, 768, 832), ("nk2", 256 * 37, 512, 128), ("nk3", 256 * 300, 256, 192)):
+    # minimum K, ranges of a few units, one tile split over 128 workgroups (127 contributors)
+    for name, m, n, k in (("odd_nk13", 256 * 41, 768, 832), ("nk2", 256 * 37, 512, 128), ("nk3", 256 * 300, 256, 192),
+                          ("one_tile", 256, 256, 8192), ("few_tiles", 512, 768, 4096), ("u_lt_g", 256, 512, 1344)):
         checks_only(C, st, name, m, n, k)
     for name, m, n, k in shapes:
         a = uni(m, k)
@@ -87,7 +90,8 @@ def main():
         def ours(epi=0, h=None, part=None, bias_=None):
             C.gemm_nt(a.data_ptr(), w.data_ptr(), c.data_ptr(), c2.data_ptr() if epi == 1 else 0,
                       bias_.data_ptr() if bias_ is not None else 0, 1, h.data_ptr() if h is not None else 0,
-                      part.data_ptr() if part is not None else 0, k, k, n, m, n, k, epi, st)
+                      part.data_ptr() if part is not None else 0, *_workspace(C, a.device, st), k, k, n, m, n, k,
+                      epi, st)
 
         ref = a.float() @ w.float().t()
         ours()

@@ -1,7 +1,7 @@
 """gemm_nt.hip (ViT forward / input-gradient GEMMs with fused epilogues) vs PyTorch fp32: every
 ViT-B/16 Linear shape at batch 256 (M = 50432 tokens), plus odd k-tile counts, the minimum K and
 tile counts that are not a multiple of the CU count (the persistent kernel's tile stream and its
-LDS buffer parity cross tile boundaries)."""
+LDS buffer parity cross tile boundaries), and stream-K splits of one tile over many workgroups."""
 import pytest
 import torch
 
@@ -14,6 +14,9 @@ VIT_FWD = [("qkv", M_VIT, 2304, 768), ("proj", M_VIT, 768, 768), ("fc1", M_VIT, 
 VIT_DGRAD = [("qkv", M_VIT, 2304, 768), ("proj", M_VIT, 768, 768), ("fc1", M_VIT, 3072, 768),
              ("fc2", M_VIT, 768, 3072)]  # (rows, N_out, N_in): dx [rows, N_in] = dy [rows, N_out] W
 SMALL = [(512, 768, 768), (768, 256, 3072), (256 * 41, 768, 832), (256 * 37, 512, 128), (256 * 300, 256, 192)]
+# stream-K: one tile split over 128 workgroups (127 contributors add into one finisher), ranges of
+# a few k-tiles crossing tile boundaries, fewer units than CUs
+STREAMK = [(256, 256, 8192), (512, 768, 4096), (256, 512, 1344), (1024, 1024, 2048)]
 
 
 def _rel(a, b):
@@ -91,6 +94,14 @@ def test_small_and_odd_shapes(gpu_ext, gelu_form, m, n, k):
     _check_fwd(m, n, k, "bf16", gelu_form)
     if k % 256 == 0:  # dgrad: dx [m, k] = dy [m, n] W [n, k]: k is the output width
         _check_dgrad(m, n, k, gelu_form)
+
+
+@pytest.mark.parametrize("m,n,k", STREAMK)
+def test_stream_k_splits(gpu_ext, m, n, k):
+    for _ in range(2):  # a launch must leave the publish flags zero for the next
+        _check_fwd(m, n, k, "f32", "tanh")
+    if k % 256 == 0:
+        _check_dgrad(m, n, k, "tanh")
 
 
 def test_transpose_bf16(gpu_ext):
