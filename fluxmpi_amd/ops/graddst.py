@@ -101,12 +101,25 @@ def empty(shape, dtype: torch.dtype, device) -> torch.Tensor:
     return torch.empty(*shape, dtype=dtype, device=device)
 
 
+def _dense(p: torch.Tensor) -> bool:
+    """``p``'s elements fill ``p.numel()`` consecutive slots in some dimension order (contiguous,
+    channels_last, ...): its strides are a permutation of a contiguous layout's."""
+    expect = 1
+    for size, stride in sorted(zip(p.shape, p.stride()), key=lambda t: (t[1], t[0])):
+        if size == 1:
+            continue
+        if stride != expect:
+            return False
+        expect *= size
+    return True
+
+
 def empty_like(p: torch.Tensor, dtype: torch.dtype | None = None) -> torch.Tensor:
     """A gradient buffer for ``p`` with ``p``'s strides (``p.shape``, ``p.stride()``, e.g. a
     channels_last filter) over its bucket slice when one is available (see :func:`take`), else
     ``torch.empty_like(p)`` (``memory_format`` preserved)."""
     dt = dtype or p.dtype
-    t = take(p, (p.numel(),), dt) if p.is_contiguous() or p.is_non_overlapping_and_dense() else None
+    t = take(p, (p.numel(),), dt) if p.is_contiguous() or _dense(p) else None
     if t is not None:
         return t.as_strided(p.shape, p.stride())
     return torch.empty_like(p, dtype=dt)

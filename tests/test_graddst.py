@@ -72,6 +72,20 @@ def test_take_semantics():
     assert graddst.take(p, (12,), p.dtype) is None
 
 
+def test_empty_like_channels_last_filter():
+    """A channels_last filter's gradient lands in its bucket slice with the filter's strides (the
+    stem / 3x3 weight-gradient kernels write it in that layout)."""
+    p = torch.nn.Parameter(torch.zeros(8, 3, 7, 7).contiguous(memory_format=torch.channels_last))
+    flat = torch.zeros(p.numel() + 10)
+    graddst.attach(p, flat, 10)
+    g = graddst.empty_like(p)
+    assert g.shape == p.shape and g.stride() == p.stride() and g.data_ptr() == flat.data_ptr() + 40
+    graddst.detach(p)
+    graddst.rearm(p)
+    assert graddst.empty_like(p).stride() == p.stride()  # not attached: a fresh tensor, same layout
+    assert not graddst._dense(torch.zeros(4, 6)[:, :3])
+
+
 def _reference(shared, W, steps, lr):
     ref = _Net(1000, shared)
     for _ in range(steps):
