@@ -230,14 +230,18 @@ void gemm_wgrad256(const void* a, const void* b, float* ws, int64_t lda, int64_t
                    int splits, hipStream_t stream);
 // Token-major Linear GEMM, both operands k-contiguous (gemm_nt.hip): C[M][N] = A[M][K] B[N][K]^T,
 // 256 x 256 tiles, ping-pong 8-wave schedule; epi 0 (+ bias), 1 (+ bias, C = h, C2 = gelu(h)),
-// 2 (C = bf16(acc) * gelu'(h), colpart[2 * M / 256][N] = per-half-tile column sums of C).
+// 2 (C = bf16(acc) * gelu'(h), colpart[2 * M / 256][N] = per-half-tile column sums of C),
+// 3 (C, and its per-column sum / sum of squares added into the BatchNorm shards stats[64][2][N]).
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc);
+bool gemm_nt_conv_supported(int64_t pixels, int64_t C, int64_t Cout);
 int gemm_nt_colpart_rows(int64_t M);
-int64_t gemm_nt_ws_floats();  // per-stream stream-K partial slots (fp32)
-int64_t gemm_nt_flag_ints();  // per-stream publish flags (int32, zero-initialised once)
 void gemm_nt(const void* a, const void* b, void* c, void* c2, const void* bias, int bias_f32, const void* h,
-             float* colpart, float* ws, int* flags, int64_t lda, int64_t ldb, int64_t ldc, int64_t M, int64_t N,
-             int64_t K, int epi, hipStream_t stream);
+             float* colpart, float* stats, int64_t lda, int64_t ldb, int64_t ldc, int64_t M, int64_t N, int64_t K,
+             int epi, hipStream_t stream);
+// 3x3 / stride 1 / pad 1 convolution on the same kernel: A = the implicit im2col of the NHWC image
+// x [nimg][H][W][C] (C % 64 == 0), B = w [Cout][3][3][C]; y [nimg*H*W][Cout]; epi 0 or 3 (statistics)
+void gemm_nt_conv(const void* x, const void* w, void* y, float* stats, int64_t nimg, int H, int W, int C,
+                  int64_t Cout, int epi, hipStream_t stream);
 // dst[c][r] = src[r][c], bf16 (rows, cols, leading dims multiples of 8)
 void transpose_bf16(const void* src, void* dst, int64_t rows, int64_t cols, int64_t lds, int64_t ldd,
                     hipStream_t stream);

@@ -296,15 +296,23 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("gemm_nt_supported", &gemm_nt_supported);
   m.def("gemm_nt_colpart_rows", &gemm_nt_colpart_rows);
-  m.def("gemm_nt_ws_floats", &gemm_nt_ws_floats);
-  m.def("gemm_nt_flag_ints", &gemm_nt_flag_ints);
   m.def("gemm_nt", [](uintptr_t a, uintptr_t b, uintptr_t c, uintptr_t c2, uintptr_t bias, int bias_f32, uintptr_t h,
-                      uintptr_t colpart, uintptr_t ws, uintptr_t flags, int64_t lda, int64_t ldb, int64_t ldc,
+                      uintptr_t colpart, int64_t lda, int64_t ldb, int64_t ldc,
                       int64_t M, int64_t N, int64_t K, int epi, uintptr_t stream) {
     gemm_nt(reinterpret_cast<const void*>(a), reinterpret_cast<const void*>(b), reinterpret_cast<void*>(c),
             reinterpret_cast<void*>(c2), reinterpret_cast<const void*>(bias), bias_f32, reinterpret_cast<const void*>(h),
-            reinterpret_cast<float*>(colpart), reinterpret_cast<float*>(ws), reinterpret_cast<int*>(flags), lda, ldb,
-            ldc, M, N, K, epi, S(stream));
+            reinterpret_cast<float*>(colpart), nullptr, lda, ldb, ldc, M, N, K, epi, S(stream));
+  });
+  m.def("gemm_nt_stats", [](uintptr_t a, uintptr_t b, uintptr_t c, uintptr_t stats, int64_t lda, int64_t ldb,
+                            int64_t ldc, int64_t M, int64_t N, int64_t K, uintptr_t stream) {
+    gemm_nt(reinterpret_cast<const void*>(a), reinterpret_cast<const void*>(b), reinterpret_cast<void*>(c), nullptr,
+            nullptr, 0, nullptr, nullptr, reinterpret_cast<float*>(stats), lda, ldb, ldc, M, N, K, 3, S(stream));
+  });
+  m.def("gemm_nt_conv_supported", &gemm_nt_conv_supported);
+  m.def("gemm_nt_conv", [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, int64_t nimg, int H, int W, int C,
+                           int64_t Cout, int epi, uintptr_t stream) {
+    gemm_nt_conv(reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(w), reinterpret_cast<void*>(y),
+                 reinterpret_cast<float*>(stats), nimg, H, W, C, Cout, epi, S(stream));
   });
   m.def("transpose_bf16", [](uintptr_t src, uintptr_t dst, int64_t rows, int64_t cols, int64_t lds, int64_t ldd,
                              uintptr_t stream) {

@@ -75,15 +75,22 @@ struct NTArgs {
   const void* bias;    // [N] fp32 / bf16 (bias_f32), or nullptr
   const bf16* h;       // EPI 2: GELU input [M][ldc]
   float* colpart;      // EPI 2: [2 * tiles_m][N]
-  float* ws;           // stream-K partials: [grid][32][512] float4 (gemm_nt_workspace_bytes)
-  int* flags;          // [grid][8] per-wave publish flags, zero between launches
+  float* stats;        // EPI 3: BatchNorm statistics shards [kShards][2][N] (sum, sum of squares)
   int64_t lda, ldb, ldc;
   int64_t N;
   int nk;              // K / 64
   int tiles_m, tiles_n;
   int bias_f32;
   int gelu_tanh;
+  // CONV: A is the implicit im2col of a 3x3 / stride 1 / pad 1 convolution over the NHWC image
+  // batch p.a [pixels][conv_c] (K = 9 conv_c, k = tap * conv_c + channel, conv_c % 64 == 0)
+  int conv_h, conv_w, conv_c;
+  int conv_cpt;        // k-tiles per tap (conv_c / 64)
+  float conv_inv_cpt;  // 1 / conv_cpt
+  uint32_t a_bytes;    // bytes of the image (the buffer resource's range: taps outside read zeros)
 };
+
+constexpr int kShards = 64;  // BatchNorm statistics shards (== batchnorm.hip)
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
@@ -106,58 +113,49 @@ __device__ __forceinline__ void glds16(const void* src, char* dst) {
 
 __device__ __forceinline__ bf16x8 frag(const char* __restrict__ p) { return *reinterpret_cast<const bf16x8*>(p); }
 
-// Stream-K over the whole problem: the U = tiles x nk (tile, k-tile) units are dealt to the G
-// persistent workgroups as equal contiguous ranges (workgroups of one XCD take neighbouring
-// ranges: the tiles of one XCD share their A row panels in its L2). Tiles are N-fastest, a
-// tile's k-tiles consecutive. A workgroup's range is ONE stream of k-tiles (stream slot s uses
-// LDS buffer s & 1): the DMA of a tile's first k-tiles is in flight while the previous tile's
-// epilogue stores, and because the ranges start at different points of their tiles the
-// workgroups' epilogues (bandwidth bursts) do not all land at once, and no round is partial.
-// A range that starts inside a tile writes that segment's fp32 partial to its slot of the
-// workspace (each wave its own 32 x 16 B per lane, then an agent-scope release and a per-wave
-// flag); the workgroup whose range covers the tile's FIRST k-tile finishes it: at the end of
-// its range it polls the flags of the following workgroups whose ranges start inside the tile
-// (relaxed agent-scope loads), acquires, adds their partials and runs the epilogue (flags reset
-// to 0 for the next launch). Contributors publish at the START of their ranges and never wait,
-// so the wait is deadlock-free whatever the residency (MI355X_MICROARCH.md "Workgroup dispatch
-// ... inter-workgroup visibility", cdna_hip_programming.md Guideline 16).
+// Persistent, tile-granular: the tiles (N-fastest) are dealt to the G = min(tiles, CUs)
+// workgroups as equal contiguous ranges (the workgroups of one XCD take neighbouring ranges, so
+// they share A row panels in its L2). A workgroup's tiles are ONE stream of k-tile units (slot s
+// uses LDS buffer s & 1): the DMA of the next tile's first k-tiles is in flight while this tile's
+// epilogue stores. (A stream-K split with fp32 partials handed between workgroups measured
+// 1.5x slower on the ViT shapes: a hand-off across the XCDs' non-coherent L2s costs an L2
+// write-back + invalidate or write-through traffic per tile — MI355X_MICROARCH.md price list,
+// "publish-large" / "splitk-seam"; profiles/rd4d_bench_gemm_nt_streamk_first.jsonl.)
 // After an epilogue the first k-tile's waits count its vector-memory instructions (kEpiVm):
 // they are younger than the DMA groups those waits retire.
 // BIAS: 0 none, 1 fp32, 2 bf16 (EPI 0 / 1), staged into LDS by one LDS-DMA of wave 0 at the
-// first k-tile of the finishing segment.
-struct TileInfo {
-  int64_t aoff, boff;  // m0 * lda, n0 * ldb
-  int64_t m0, n0;
-  int tm;
+// tile's first k-tile (slot = tile parity).
+struct TileInfo {  // wave-uniform (SGPRs); every offset below fits 32 bits (gemm_nt_supported)
+  int tm, tn;
+  __device__ __forceinline__ int m0() const { return tm * kT; }
+  __device__ __forceinline__ int n0() const { return tn * kT; }
 };
-
-__device__ __forceinline__ int64_t uni64(int64_t v) {  // provably wave-uniform (SGPRs)
-  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
-  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(static_cast<uint64_t>(v) >> 32));
-  return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
-}
 
 __device__ __forceinline__ TileInfo tile_of(const NTArgs& p, int T) {
   TileInfo t;
   T = __builtin_amdgcn_readfirstlane(T);
   t.tm = __builtin_amdgcn_readfirstlane(T / p.tiles_n);
-  const int tn = T - t.tm * p.tiles_n;
-  t.m0 = uni64(static_cast<int64_t>(t.tm) * kT);
-  t.n0 = uni64(static_cast<int64_t>(tn) * kT);
-  t.aoff = uni64(t.m0 * p.lda);
-  t.boff = uni64(t.n0 * p.ldb);
+  t.tn = T - t.tm * p.tiles_n;
   return t;
 }
 
-// first unit of workgroup (range) r
-__device__ __forceinline__ int range_start(int U, int G, int r) {
-  return static_cast<int>(static_cast<int64_t>(U) * r / G);
+// an opaque copy: values derived from it are recomputed where they are used instead of being
+// hoisted out of the tile loop by LICM and kept live (spilled) across the whole k-tile stream
+__device__ __forceinline__ int opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
 }
 
-template <int EPI, int BIAS>
+// first tile of workgroup (range) r
+__device__ __forceinline__ int range_start(int tiles, int G, int r) {
+  return static_cast<int>(static_cast<int64_t>(tiles) * r / G);
+}
+
+template <int EPI, int BIAS, bool CONV, int GF = 1>  // GF (EPI 1 / 2): 1 tanh GELU, 0 erf GELU
 __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[kSmem];
-  constexpr int kEpiVm = EPI == 0 ? 32 : 56;  // vector-memory instructions per wave in an epilogue (lower bound)
+  // vector-memory instructions per wave in an epilogue (lower bound: unconditional ones)
+  constexpr int kEpiVm = EPI == 1 || EPI == 2 ? 56 : 32;
   const int G = gridDim.x;
   int gi = blockIdx.x;
   {  // bijective XCD-aware range order: the workgroups of one XCD take neighbouring ranges
@@ -165,9 +163,11 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
     gi = __builtin_amdgcn_readfirstlane((xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos);
   }
   const int nk = p.nk;  // >= 2
-  const int U = p.tiles_m * p.tiles_n * nk;  // < 2^31 (gemm_nt_supported)
-  const int u0 = __builtin_amdgcn_readfirstlane(range_start(U, G, gi));
-  const int u1 = __builtin_amdgcn_readfirstlane(range_start(U, G, gi + 1));
+  const int tiles = p.tiles_m * p.tiles_n;
+  // the workgroup's tiles [T0, T1) as one stream of units (tile, k-tile), u = T * nk + t
+  const int T0 = __builtin_amdgcn_readfirstlane(range_start(tiles, G, gi));
+  const int T1 = __builtin_amdgcn_readfirstlane(range_start(tiles, G, gi + 1));
+  const int u0 = T0 * nk, u1 = T1 * nk;  // < 2^31 (gemm_nt_supported)
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // wave-uniform
   const int wr = wave >> 2, wc = wave & 3;
 
@@ -177,15 +177,18 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
   // the swizzle of row + 32p equals that of row
   const int arow = (wave & 4) * 32 + (wave & 3) * 8 + lrow;
   const int laneA = arow * static_cast<int>(p.lda) + ((lslot ^ swz(arow)) << 3);  // < 2^31: lda < 2^23
-  const int64_t aPhase = 32 * p.lda;
+  const int lda2 = static_cast<int>(p.lda) * 2, ldb2 = static_cast<int>(p.ldb) * 2;  // bytes per row
   const int dstA = (arow - lrow) * kRow;
   // B rows of piece j: 32w + 8j + lrow
-  int laneB[4];
+  // B rows of piece j: 32w + 8j + lrow; the swizzle of row + 8j is that of row ^ 4 (j odd), so
+  // two lane offsets (j even / odd) + a wave-uniform 8j rows
+  uint32_t laneBb[2];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < 2; ++j) {
     const int row = 32 * wave + 8 * j + lrow;
-    laneB[j] = row * static_cast<int>(p.ldb) + ((lslot ^ swz(row)) << 3);
+    laneBb[j] = static_cast<uint32_t>(lrow * static_cast<int>(p.ldb) + ((lslot ^ swz(row)) << 3)) * 2u;
   }
+  const int bwave = 32 * wave * static_cast<int>(p.ldb) * 2;
   const int dstB = kImg + 32 * wave * kRow;
   const void* zero = g_zero_nt;
 
@@ -194,20 +197,59 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
   // kept live across the loop. Past the range's end (`ok` false) the slot is dead and the DMA just
   // re-reads valid bytes (the caller passes the current unit), keeping the vmcnt count fixed.
   const uint32_t laneAb = static_cast<uint32_t>(laneA) * 2u;
-  uint32_t laneBb[4];
+  // CONV: the A rows a lane stages are output pixels m = m0 + arow + 32 ph of the tile whose
+  // info is loaded (conv_info: at the prologue and when the issues move on to the next tile);
+  // pixb = phase 0's pixel byte offset + the lane's chunk, vmask = its in-image taps (9 bits per
+  // phase, phases 2k / 2k+1 in halves of word k). A k-tile lies inside one tap (conv_c % 64 == 0):
+  // the tap's pixel shift and the channel offset are wave-uniform, and an out-of-image tap's
+  // offset is past the buffer's range, which the LDS-DMA reads as zeros (the padding).
+  struct ConvRows {
+    uint32_t pixb = 0;      // phase 0's pixel byte offset + the lane's chunk (phase ph adds 32 ph pixels)
+    uint32_t vmask[2] = {};  // in-image taps: 9 bits per phase, phases 2k / 2k+1 in halves of word k
+  };
+  ConvRows crow, crow_n;  // the current tile's rows, the next tile's (computed once per segment)
+  const __amdgpu_buffer_rsrc_t arsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(p.a), 0, CONV ? p.a_bytes : 0x7fffffffu, 0x00020000);
+  auto conv_info = [&](const TileInfo& ti, ConvRows& cr) {
+    const uint32_t chunkb = static_cast<uint32_t>((lslot ^ swz(arow)) << 4);
+    const int H = p.conv_h, W = p.conv_w, HW = H * W;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) laneBb[j] = static_cast<uint32_t>(laneB[j]) * 2u;
-  auto sbase = [](const bf16* base, int64_t elems) {
-    const uint64_t a = reinterpret_cast<uint64_t>(base + elems);
-    const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
-    const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
-    return reinterpret_cast<const char*>((static_cast<uint64_t>(hi) << 32) | lo);
+    for (int ph = 0; ph < 4; ++ph) {
+      const int m = ti.m0() + arow + 32 * ph;  // < 2^31 (gemm_nt_conv_supported)
+      const int hw = m % HW, h = hw / W, w = hw - h * W;
+      if (ph == 0) cr.pixb = static_cast<uint32_t>(m) * static_cast<uint32_t>(p.conv_c) * 2u + chunkb;
+      const uint32_t rm = (h > 0 ? 1u : 0u) | 2u | (h < H - 1 ? 4u : 0u);
+      const uint32_t cm = (w > 0 ? 1u : 0u) | 2u | (w < W - 1 ? 4u : 0u);
+      const uint32_t m9 = ((rm & 1u) ? cm : 0u) | ((rm & 2u) ? cm << 3 : 0u) | ((rm & 4u) ? cm << 6 : 0u);
+      if (ph & 1) cr.vmask[ph >> 1] |= m9 << 16;
+      else cr.vmask[ph >> 1] = m9;
+    }
   };
-  auto issueA = [&](int s, const TileInfo& ti, int tk, int ph) {
-    glds16(sbase(p.a, ti.aoff + ph * aPhase + tk * kBK) + laneAb, smem + (s & 1) * kBuf + dstA + ph * 32 * kRow);
+  auto issueA = [&](int s, const TileInfo& ti, int tk, int ph, bool next_tile) {
+    if constexpr (CONV) {
+      const int tap = __builtin_amdgcn_readfirstlane(static_cast<int>((static_cast<float>(tk) + 0.5f) * p.conv_inv_cpt));
+      const int r3 = (tap * 11) >> 5;  // tap / 3 for tap < 9
+      const int c0 = (tk - tap * p.conv_cpt) * kBK;
+      const int sh =
+          __builtin_amdgcn_readfirstlane((((r3 - 1) * p.conv_w + (tap - 3 * r3 - 1) + 32 * ph) * p.conv_c + c0) * 2);
+      const uint32_t vm = next_tile ? crow_n.vmask[ph >> 1] : crow.vmask[ph >> 1];
+      const uint32_t pb = next_tile ? crow_n.pixb : crow.pixb;
+      const uint32_t vo = (vm >> (tap + 16 * (ph & 1))) & 1u ? pb + static_cast<uint32_t>(sh) : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc, (lds_char*)(smem + (s & 1) * kBuf + dstA + ph * 32 * kRow), 16,
+                                               vo, 0, 0, 0);
+    } else {
+      const int so = __builtin_amdgcn_readfirstlane((ti.m0() + 32 * ph) * lda2 + tk * kRow);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(arsrc, (lds_char*)(smem + (s & 1) * kBuf + dstA + ph * 32 * kRow), 16,
+                                               laneAb, so, 0, 0);
+    }
   };
+  // B through a buffer resource: the lane's 32-bit byte offset (voffset) + the tile / k-tile
+  // offset (soffset, wave-uniform) — no 64-bit per-lane address is formed or kept
+  const __amdgpu_buffer_rsrc_t brsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(p.b), 0, 0x7fffffff, 0x00020000);
   auto issueB = [&](int s, const TileInfo& ti, int tk, int j) {
-    glds16(sbase(p.b, ti.boff + tk * kBK) + laneBb[j], smem + (s & 1) * kBuf + dstB + j * 8 * kRow);
+    const int so = __builtin_amdgcn_readfirstlane((ti.n0() + 8 * j) * ldb2 + tk * kRow + bwave);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(brsrc, (lds_char*)(smem + (s & 1) * kBuf + dstB + j * 8 * kRow), 16,
+                                             laneBb[j & 1], so, 0, 0);
   };
 
   // ---- fragment reads: lane row (lane & 15), chunk (lane >> 4) + 4 kh at slot chunk ^ swz(row)
@@ -223,7 +265,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
   f32x4 acc[4][2][4];
   bf16x8 fb[4][2];
   const int cq = 4 * (lane >> 4);
-  int seg = 0;  // segments (tile pieces) started so far: parity of the bias slot
+  int seg = 0;  // tiles started so far: parity of the bias slot
 
   // ---- prologue: B(u0), A(u0) phases 0..3, B(u0 + 1)
   {
@@ -231,10 +273,11 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
     const TileInfo a0 = tile_of(p, T0);
     const TileInfo a1 = t0 + 1 < nk ? a0 : tile_of(p, T0 + 1);
     const int t1 = t0 + 1 < nk ? t0 + 1 : 0;
+    if constexpr (CONV) conv_info(a0, crow);
 #pragma unroll
     for (int j = 0; j < 4; ++j) issueB(0, a0, t0, j);
 #pragma unroll
-    for (int ph = 0; ph < 4; ++ph) issueA(0, a0, t0, ph);
+    for (int ph = 0; ph < 4; ++ph) issueA(0, a0, t0, ph, false);
     const bool ok1 = u0 + 1 < u1;
 #pragma unroll
     for (int j = 0; j < 4; ++j) issueB(1, ok1 ? a1 : a0, ok1 ? t1 : t0, j);
@@ -246,14 +289,13 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
   // one k-tile (4 phases) of unit u; FIRST: the accumulators start from zero (and wave 0 stages
   // the tile's bias when the segment will finish the tile); XV: vector-memory instructions
   // issued since the DMA groups this k-tile's first three waits retire
-  auto ktile = [&](int u, int t, const TileInfo& cur, const TileInfo& nxt, bool stage_bias, auto first_c,
-                   auto xv_c) {
+  auto ktile = [&](int u, int t, const TileInfo& cur, const TileInfo& nxt, auto first_c, auto xv_c) {
     constexpr bool FIRST = decltype(first_c)::value;
     constexpr int XV = decltype(xv_c)::value;
-    if (FIRST && BIAS != 0 && wave == 0 && stage_bias) {
+    if (FIRST && BIAS != 0 && wave == 0) {
       // the tile's 256 bias values (fp32 1 KiB / bf16 512 B) into the segment's parity LDS slot
-      const char* src = BIAS == 1 ? reinterpret_cast<const char*>(static_cast<const float*>(p.bias) + cur.n0) + 16 * lane
-                                  : (lane < 32 ? reinterpret_cast<const char*>(static_cast<const bf16*>(p.bias) + cur.n0) + 16 * lane
+      const char* src = BIAS == 1 ? reinterpret_cast<const char*>(static_cast<const float*>(p.bias) + cur.n0()) + 16 * lane
+                                  : (lane < 32 ? reinterpret_cast<const char*>(static_cast<const bf16*>(p.bias) + cur.n0()) + 16 * lane
                                                : reinterpret_cast<const char*>(zero));
       glds16(src, smem + kBiasOff + (seg & 1) * 1024);
     }
@@ -280,7 +322,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int kh = 0; kh < 2; ++kh) fa[i][kh] = frag(buf + offA[kh] + (32 * ph + 16 * i) * kRow);
-      issueA(sl + 1, ta, at, ph);
+      issueA(sl + 1, ta, at, ph, aok && an);
       if (ph == 1) {
         issueB(sl + 2, tb, bt, 0);
         issueB(sl + 2, tb, bt, 1);
@@ -313,78 +355,24 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
     }
   };
 
-  // partial slots through a buffer resource: the lane offset is one VGPR (threadIdx.x * 16), the
-  // slot + element offset a wave-uniform SGPR (soffset), so the 32 stores / loads of a slot keep
-  // no per-instruction 64-bit address live next to the 128 accumulator VGPRs
-  const __amdgpu_buffer_rsrc_t wsr = __builtin_amdgcn_make_buffer_rsrc(p.ws, 0, 0x7fffffff, 0x00020000);
-  const int wlane = threadIdx.x * 16;
-  auto slot_off = [&](int r, int idx) { return __builtin_amdgcn_readfirstlane((r * 32 + idx) * (kThreads * 16)); };
   using Z = std::integral_constant<int, 0>;
   bool after_epi = false;
-  int T = u0 / nk;
+  int T = T0;
   TileInfo cur = tile_of(p, T);
-  for (int u = u0; u < u1;) {
-    const int ts = u - T * nk;
-    const int tile_end = (T + 1) * nk;
-    const int te = (u1 < tile_end ? u1 : tile_end) - T * nk;
-    const TileInfo nxt = tile_of(p, T + 1 < p.tiles_m * p.tiles_n ? T + 1 : T);
-    const bool finish = ts == 0;  // this segment owns the tile's first k-tile: it runs the epilogue
-    if (after_epi) ktile(u, ts, cur, nxt, finish, std::true_type{}, std::integral_constant<int, kEpiVm>{});
-    else ktile(u, ts, cur, nxt, finish, std::true_type{}, Z{});
-    for (int t = ts + 1; t < te; ++t) ktile(u + (t - ts), t, cur, nxt, finish, std::false_type{}, Z{});
-    u += te - ts;
-    after_epi = false;
-    if (!finish) {
-      // ---- contributor: publish this segment's partial for the workgroup that finishes the tile
-#pragma unroll
-      for (int ph = 0; ph < 4; ++ph)
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, acc[ph][i][j]), wsr, wlane,
-                                                   slot_off(gi, (ph * 2 + i) * 4 + j), 0);
-          }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // keep the fence's wait (ROCm 7.2 may drop it)
-      if (lane == 0) __hip_atomic_store(p.flags + gi * 8 + wave, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      ++seg;
-      ++T;
-      cur = nxt;
-      continue;  // its waits drained every older transfer: no epilogue count for the next k-tile
-    }
-    if (te < nk) {
-      // ---- finisher of a tile the following ranges complete: add their partials (in order)
-      for (int r = gi + 1; r < G && range_start(U, G, r) < (T + 1) * nk; ++r) {
-        int* flag = p.flags + r * 8 + wave;
-        if (lane == 0) {
-          while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) __builtin_amdgcn_s_sleep(2);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int ph = 0; ph < 4; ++ph) {  // 8 loads in flight at a time (the accumulators hold 128 VGPRs)
-          i32x4 v[2][4];
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) v[i][j] = __builtin_amdgcn_raw_buffer_load_b128(wsr, wlane, slot_off(r, (ph * 2 + i) * 4 + j), 0);
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[ph][i][j] += __builtin_bit_cast(f32x4, v[i][j]);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        if (lane == 0) __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
+  for (int u = u0; u < u1; u += nk) {
+    const TileInfo nxt = tile_of(p, T + 1 < tiles ? T + 1 : T);
+    if constexpr (CONV) conv_info(nxt, crow_n);  // for the A issues of this tile's last k-tile
+    if (after_epi) ktile(u, 0, cur, nxt, std::true_type{}, std::integral_constant<int, kEpiVm>{});
+    else ktile(u, 0, cur, nxt, std::true_type{}, Z{});
+    for (int t = 1; t < nk; ++t) ktile(u + t, t, cur, nxt, std::false_type{}, Z{});
 
     // ---- epilogue: acc[ph][i][j][r] = C[m0 + wr*128 + 32ph + 16i + (lane & 15)][n0 + wc*64 + 16j + 4(lane >> 4) + r]
+    const int lane_e = opaque(lane), fr_e = lane_e & 15, cq_e = 4 * (lane_e >> 4);
     float bias[4][4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const char* bl = smem + kBiasOff + (seg & 1) * 1024;
-      const int col = wc * 64 + 16 * j + cq;
+      const int col = wc * 64 + 16 * j + cq_e;
       if (BIAS == 1) {
         const float4 v = *reinterpret_cast<const float4*>(bl + 4 * col);
         bias[j][0] = v.x, bias[j][1] = v.y, bias[j][2] = v.z, bias[j][3] = v.w;
@@ -397,23 +385,29 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
         for (int r = 0; r < 4; ++r) bias[j][r] = 0.f;
       }
     }
-    float cs[4][4];
+    float cs[4][4], cq2[EPI == 3 ? 4 : 1][4];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
+    if (EPI == 3) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cq2[j][r] = 0.f;
+    }
     // outputs through buffer resources based at the tile's first element (wave-uniform SGPRs):
     // voffset = the lane's (row, column) byte offset in the tile (one VGPR), soffset = the
     // (ph, ii) row block, the j column block an immediate
     auto tile_rsrc = [&](const void* base) {
-      const uint64_t a = reinterpret_cast<uint64_t>(static_cast<const bf16*>(base) + cur.m0 * p.ldc + cur.n0);
+      const uint64_t a = reinterpret_cast<uint64_t>(static_cast<const bf16*>(base) + static_cast<int64_t>(cur.m0()) * p.ldc + cur.n0());
       const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
       const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
       return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo), 0,
                                                0x7fffffff, 0x00020000);
     };
     const int ldcb = static_cast<int>(p.ldc) * 2;  // < 2^23 (gemm_nt_supported)
-    const int vo = (wr * 128 + fr) * ldcb + (wc * 64 + cq) * 2;
+    const int vo = (wr * 128 + fr_e) * ldcb + (wc * 64 + cq_e) * 2;
     auto rowblk = [&](int ph, int ii) { return __builtin_amdgcn_readfirstlane((32 * ph + 16 * ii) * ldcb); };
     const __amdgpu_buffer_rsrc_t crs = tile_rsrc(p.c);
     i32x2 hv[4][2][4];  // EPI 2: every GELU input of the tile's lane issued before the first use (one round trip)
@@ -436,13 +430,21 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
           if (EPI == 0) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) o[r] = static_cast<bf16>(acc[ph][ii][j][r] + bias[j][r]);
+          } else if (EPI == 3) {  // the BatchNorm statistics of the rounded output
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              o[r] = static_cast<bf16>(acc[ph][ii][j][r]);
+              const float f = static_cast<float>(o[r]);
+              cs[j][r] += f;
+              cq2[j][r] = fmaf(f, f, cq2[j][r]);
+            }
           } else if (EPI == 1) {
             bf16 gg[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               o[r] = static_cast<bf16>(acc[ph][ii][j][r] + bias[j][r]);
               const float x = static_cast<float>(o[r]);  // GELU of the bf16 pre-activation, as F.gelu(h)
-              if (p.gelu_tanh) {
+              if constexpr (GF == 1) {
                 gg[r] = static_cast<bf16>(gelu_tanh(x));
               } else {
                 float cdf, e;
@@ -461,7 +463,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
               const float dg = static_cast<float>(static_cast<bf16>(acc[ph][ii][j][r]));  // the bf16 dg autograd sees
               const float x = static_cast<float>(hh[r]);
               float d;
-              if (p.gelu_tanh) {
+              if constexpr (GF == 1) {
                 d = gelu_tanh_grad(x);
               } else {
                 float cdf, e;
@@ -483,16 +485,38 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) cs[j][r] = row_sum16(cs[j][r]);
-      if (fr == 0) {
-        float* dst = p.colpart + static_cast<int64_t>(2 * cur.tm + wr) * p.N + cur.n0 + wc * 64 + cq;
+      if (fr_e == 0) {
+        float* dst = p.colpart + static_cast<int64_t>(2 * cur.tm + wr) * p.N + cur.n0() + wc * 64 + cq_e;
 #pragma unroll
         for (int j = 0; j < 4; ++j) *reinterpret_cast<float4*>(dst + 16 * j) = float4{cs[j][0], cs[j][1], cs[j][2], cs[j][3]};
+      }
+    }
+    if (EPI == 3) {
+      // the wave's 128 rows summed per column (butterflies over the 16 row lanes), then one
+      // atomic per column per wave row into the tile's statistics shard
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          cs[j][r] = row_sum16(cs[j][r]);
+          cq2[j][r] = row_sum16(cq2[j][r]);
+        }
+      if (fr_e == 0) {
+        float* shard = p.stats + static_cast<int64_t>(T % kShards) * 2 * p.N + cur.n0() + wc * 64 + cq_e;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            atomicAdd(shard + 16 * j + r, cs[j][r]);
+            atomicAdd(shard + p.N + 16 * j + r, cq2[j][r]);
+          }
       }
     }
     ++seg;
     after_epi = true;
     ++T;
     cur = nxt;
+    if constexpr (CONV) crow = crow_n;
   }
   if (wr == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dead-slot DMAs
@@ -540,15 +564,20 @@ int cus() {
   return n;
 }
 
-// one persistent workgroup per CU (fewer when there are fewer units than CUs)
+// one persistent workgroup per CU (fewer when there are fewer tiles than CUs)
 int grid_of(const NTArgs& p) {
-  const int64_t U = static_cast<int64_t>(p.tiles_m) * p.tiles_n * p.nk;
-  return static_cast<int>(U < cus() ? U : cus());
+  const int64_t tiles = static_cast<int64_t>(p.tiles_m) * p.tiles_n;
+  return static_cast<int>(tiles < cus() ? tiles : cus());
 }
 
-template <int EPI, int BIAS>
+template <int EPI, int BIAS, bool CONV = false>
 void launch(const NTArgs& p, hipStream_t stream) {
-  gemm_nt_kernel<EPI, BIAS><<<grid_of(p), kThreads, 0, stream>>>(p);
+  if constexpr (EPI == 1 || EPI == 2) {  // the GELU form is compiled in (its constants would stay live otherwise)
+    if (p.gelu_tanh) gemm_nt_kernel<EPI, BIAS, CONV, 1><<<grid_of(p), kThreads, 0, stream>>>(p);
+    else gemm_nt_kernel<EPI, BIAS, CONV, 0><<<grid_of(p), kThreads, 0, stream>>>(p);
+  } else {
+    gemm_nt_kernel<EPI, BIAS, CONV><<<grid_of(p), kThreads, 0, stream>>>(p);
+  }
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
 
@@ -559,21 +588,21 @@ bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb
   return M > 0 && N > 0 && K >= 2 * kBK && M % kT == 0 && N % kT == 0 && K % kBK == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
          ldc % 8 == 0 && lda >= K && ldb >= K && ldc >= N && lda < (int64_t(1) << 23) && ldb < (int64_t(1) << 23) &&
          ldc < (int64_t(1) << 22) &&  // the epilogue's 32-bit byte offsets within a tile
+         M * lda * 2 < (int64_t(1) << 31) && N * ldb * 2 < (int64_t(1) << 31) &&  // 32-bit DMA offsets
          M / kT * (N / kT) * (K / kBK) < (int64_t(1) << 31);
+}
+
+bool gemm_nt_conv_supported(int64_t pixels, int64_t C, int64_t Cout) {
+  // output pixels tile exactly, a k-tile inside one tap, 32-bit byte offsets into the image
+  return C > 0 && C % kBK == 0 && pixels * C * 2 < (int64_t(1) << 31) &&
+         gemm_nt_supported(pixels, Cout, 9 * C, 9 * C, 9 * C, Cout);
 }
 
 int gemm_nt_colpart_rows(int64_t M) { return static_cast<int>(2 * (M / kT)); }
 
-// stream-K workspace for one stream: fp32 partial slots [CUs][32][512] float4 and [CUs][8] int flags
-// (zero-initialised once; every launch leaves them zero)
-int64_t gemm_nt_ws_floats() { return static_cast<int64_t>(cus()) * 32 * kThreads * 4; }
-int64_t gemm_nt_flag_ints() { return static_cast<int64_t>(cus()) * 8; }
-
 void gemm_nt(const void* a, const void* b, void* c, void* c2, const void* bias, int bias_f32, const void* h,
-             float* colpart, float* ws, int* flags, int64_t lda, int64_t ldb, int64_t ldc, int64_t M, int64_t N,
-             int64_t K, int epi, hipStream_t stream) {
-  if (ws == nullptr || flags == nullptr || (reinterpret_cast<uintptr_t>(ws) & 15u) != 0)
-    throw std::runtime_error("gemm_nt: needs its stream-K workspace (gemm_nt_ws_floats / gemm_nt_flag_ints)");
+             float* colpart, float* stats, int64_t lda, int64_t ldb, int64_t ldc, int64_t M, int64_t N, int64_t K,
+             int epi, hipStream_t stream) {
   if (!gemm_nt_supported(M, N, K, lda, ldb, ldc))
     throw std::runtime_error("gemm_nt: unsupported shape (M, N multiples of 256, K of 64, leading dims of 8; M=" +
                              std::to_string(M) + " N=" + std::to_string(N) + " K=" + std::to_string(K) + ")");
@@ -582,13 +611,20 @@ void gemm_nt(const void* a, const void* b, void* c, void* c2, const void* bias, 
   if (epi == 1 && c2 == nullptr) throw std::runtime_error("gemm_nt: the GELU epilogue needs the second output");
   if (epi == 2 && (h == nullptr || colpart == nullptr))
     throw std::runtime_error("gemm_nt: the GELU-backward epilogue needs h and colpart");
+  if (epi == 3 && (stats == nullptr || bias != nullptr))
+    throw std::runtime_error("gemm_nt: the statistics epilogue needs the shard workspace (and takes no bias)");
   if (bias != nullptr && (reinterpret_cast<uintptr_t>(bias) & (bias_f32 ? 15u : 7u)) != 0)
     throw std::runtime_error("gemm_nt: bias must be 16-byte (fp32) / 8-byte (bf16) aligned");
-  NTArgs p{static_cast<const bf16*>(a), static_cast<const bf16*>(b), static_cast<bf16*>(c), static_cast<bf16*>(c2),
-           bias, static_cast<const bf16*>(h), colpart, ws, flags, lda, ldb, ldc, N, static_cast<int>(K / kBK),
-           static_cast<int>(M / kT), static_cast<int>(N / kT), bias_f32, gelu_form()};
+  NTArgs p{};
+  p.a = static_cast<const bf16*>(a), p.b = static_cast<const bf16*>(b), p.c = static_cast<bf16*>(c);
+  p.c2 = static_cast<bf16*>(c2), p.bias = bias, p.h = static_cast<const bf16*>(h), p.colpart = colpart;
+  p.stats = stats, p.lda = lda, p.ldb = ldb, p.ldc = ldc, p.N = N;
+  p.nk = static_cast<int>(K / kBK), p.tiles_m = static_cast<int>(M / kT), p.tiles_n = static_cast<int>(N / kT);
+  p.bias_f32 = bias_f32, p.gelu_tanh = gelu_form();
   const int bk = bias == nullptr ? 0 : bias_f32 ? 1 : 2;
-  if (epi == 2) {
+  if (epi == 3) {
+    launch<3, 0>(p, stream);
+  } else if (epi == 2) {
     launch<2, 0>(p, stream);
   } else if (epi == 1) {
     if (bk == 1) launch<1, 1>(p, stream);
@@ -599,6 +635,28 @@ void gemm_nt(const void* a, const void* b, void* c, void* c2, const void* bias, 
     else if (bk == 2) launch<0, 2>(p, stream);
     else launch<0, 0>(p, stream);
   }
+}
+
+void gemm_nt_conv(const void* x, const void* w, void* y, float* stats, int64_t nimg, int H, int W, int C,
+                  int64_t Cout, int epi, hipStream_t stream) {
+  const int64_t pixels = nimg * H * W;
+  if (!gemm_nt_conv_supported(pixels, C, Cout))
+    throw std::runtime_error("gemm_nt_conv: unsupported shape (pixels, Cout multiples of 256, C of 64; pixels=" +
+                             std::to_string(pixels) + " C=" + std::to_string(C) + " Cout=" + std::to_string(Cout) + ")");
+  if (((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(y)) & 15u) != 0)
+    throw std::runtime_error("gemm_nt_conv: operands must be 16-byte aligned");
+  if (epi != 0 && epi != 3) throw std::runtime_error("gemm_nt_conv: epilogue 0 (plain) or 3 (statistics)");
+  if (epi == 3 && stats == nullptr) throw std::runtime_error("gemm_nt_conv: the statistics epilogue needs the shards");
+  NTArgs p{};
+  p.a = static_cast<const bf16*>(x), p.b = static_cast<const bf16*>(w), p.c = static_cast<bf16*>(y);
+  p.stats = stats, p.lda = 9 * C, p.ldb = 9 * C, p.ldc = Cout, p.N = Cout;
+  p.nk = 9 * C / kBK, p.tiles_m = static_cast<int>(pixels / kT), p.tiles_n = static_cast<int>(Cout / kT);
+  p.gelu_tanh = 0;
+  p.conv_h = H, p.conv_w = W, p.conv_c = C, p.conv_cpt = C / kBK;
+  p.conv_inv_cpt = 1.f / static_cast<float>(C / kBK);
+  p.a_bytes = static_cast<uint32_t>(pixels * C * 2);
+  if (epi == 3) launch<3, 0, true>(p, stream);
+  else launch<0, 0, true>(p, stream);
 }
 
 void transpose_bf16(const void* src, void* dst, int64_t rows, int64_t cols, int64_t lds, int64_t ldd,

@@ -136,6 +136,7 @@ class _LinearGeluFn(torch.autograd.Function):
             h = F.linear(x, weight, bias)
             g = _gelu_fwd(h)
         ctx.save_for_backward(x, weight, h)
+        ctx.weight = weight  # the leaf itself: its gradient's bucket slice (ops/graddst.py)
         ctx.has_bias = bias is not None
         ctx.bias_dtype = bias.dtype if bias is not None else None
         ctx.link = link
@@ -159,7 +160,9 @@ class _LinearGeluFn(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             # long-K weight gradient on the split-K HIP kernel (ops/linear.py)
-            dw = weight_grad(dh2, x2, w.dtype) if _wgrad_mode() == "ours" and native_ok(x2, dh2) else dh2.t() @ x2
+            from . import graddst
+            with graddst.into(ctx.weight):  # the DDP bucket slice when one is attached
+                dw = weight_grad(dh2, x2, w.dtype) if _wgrad_mode() == "ours" and native_ok(x2, dh2) else dh2.t() @ x2
         return dx, dw, (db if ctx.has_bias and ctx.needs_input_grad[2] else None), None
 
 

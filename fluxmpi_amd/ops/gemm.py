@@ -16,6 +16,7 @@ import weakref
 import torch
 
 from . import _ext
+from . import gemm_nt as _NT
 from . import graddst
 
 SHARDS = 64  # == kShards in csrc/kernels/{batchnorm,gemm}.hip
@@ -61,6 +62,9 @@ def conv1x1_fwd(x2d: torch.Tensor, w2d: torch.Tensor, in_affine=None, stats: tor
     M, K = x2d.shape
     N = w2d.shape[0]
     y = torch.empty(M, N, device=x2d.device, dtype=torch.bfloat16)
+    if (in_affine is None and x2d.stride(0) == K and w2d.stride(0) == K and x2d.stride(1) == 1 and w2d.stride(1) == 1
+            and _NT.gemm_ok(M, N, K, x2d, w2d)):
+        return _NT.gemm_plain(x2d, w2d, y, stats)  # 256x256 persistent kernel (+ statistics epilogue)
     gemm(x2d, w2d, y, M=M, N=N, K=K, lda=x2d.stride(0), ldb=w2d.stride(0), ldc=N, a_kmajor=True, b_kmajor=True,
          mode=1 if stats is not None else 0, a_affine=in_affine, stats=stats)
     return y
@@ -88,6 +92,9 @@ def conv1x1_dgrad(dy2d: torch.Tensor, w2d: torch.Tensor, residual: torch.Tensor 
         # LDS-DMA kernel on the cached W^T (K-major B); the BN-backward epilogue is supported too
         if residual_mask is not None:
             assert residual is not None and residual.stride(0) == Ci and residual_mask.numel() * 8 == M * Ci
+        if (residual is None and bn_bwd is None and dy2d.stride(0) == Co and dx.stride(0) == Ci
+                and _NT.gemm_ok(M, Ci, Co, dy2d, w4d)):
+            return _NT.gemm_plain(dy2d, filter_t(w4d), dx)  # W^T [Ci][Co]: both operands k-contiguous
         gemm(dy2d, filter_t(w4d), dx, M=M, N=Ci, K=Co, lda=dy2d.stride(0), ldb=Co, ldc=dx.stride(0),
              residual=residual, mode=1 if bn_bwd is not None else 0, stats=stats, bn_bwd=bn_bwd,
              engine=ENGINE or 2, res_mask=residual_mask, res_sub=residual_sub)
@@ -171,6 +178,9 @@ def conv3x3_fwd(x: torch.Tensor, w: torch.Tensor, in_affine=None, stats: torch.T
     note_filter(w)
     y = out if out is not None else torch.empty(n, h, wd, co, device=x.device, dtype=x.dtype).permute(0, 3, 1, 2)
     M = n * h * wd
+    if (in_affine is None and engine is None and y.is_contiguous(memory_format=torch.channels_last)
+            and _NT.conv_ok(M, c, co, xs, w2)):
+        return _NT.conv3x3(xs, w2.view(co, 9 * c), y, stats)  # 256x256 persistent implicit GEMM
     gemm(xs, w2, y, M=M, N=co, K=9 * c, lda=c, ldb=9 * c, ldc=co, mode=1 if stats is not None else 0,
          a_affine=in_affine, stats=stats, conv=(h, wd, c), engine=engine or None)
     return y
@@ -208,6 +218,9 @@ def conv3x3_dgrad(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = 
     dx = out if out is not None else torch.empty(n, h, wd, ci, device=dy.device, dtype=dy.dtype).permute(0, 3, 1, 2)
     if bn_bwd is not None:
         assert stats is not None and bn_bwd[0].shape == (n * h * wd, ci) and ENGINE != 1
+    if (bn_bwd is None and residual is None and ENGINE != 1 and dx.is_contiguous(memory_format=torch.channels_last)
+            and _NT.conv_ok(n * h * wd, co, ci, dys, wt)):
+        return _NT.conv3x3(dys, wt, dx)  # the flipped transpose [ci][3][3][co] as B
     r2 = None
     if residual is not None:
         assert residual.shape == dx.shape and residual.dtype == dy.dtype and bn_bwd is None

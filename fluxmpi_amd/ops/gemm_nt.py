@@ -37,21 +37,6 @@ def _stream(t):
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
-_WS: dict = {}
-
-
-def _workspace(C, device: torch.device, stream: int):
-    """The stream-K partial slots and publish flags of one (device, stream): flags are zeroed once
-    and every launch leaves them zero; launches on one stream are ordered, so they share it."""
-    key = (device.index, stream)
-    ws = _WS.get(key)
-    if ws is None:
-        ws = (torch.empty(int(C.gemm_nt_ws_floats()), device=device, dtype=torch.float32),
-              torch.zeros(int(C.gemm_nt_flag_ints()), device=device, dtype=torch.int32))
-        _WS[key] = ws
-    return ws[0].data_ptr(), ws[1].data_ptr()
-
-
 def supported(rows: int, n_out: int, k: int, *tensors: torch.Tensor, fused: bool = False) -> bool:
     """Whether gemm_nt takes ``[rows, k] x [n_out, k]^T`` (both operands k-contiguous after the
     weight transpose of an input gradient) under the current mode."""
@@ -91,7 +76,7 @@ def linear_fwd(x2: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None
     s = _stream(x2)
     C.gemm_nt(x2.data_ptr(), w.data_ptr(), y.data_ptr(), g.data_ptr() if gelu else 0,
               b.data_ptr() if b is not None else 0, int(b is not None and b.dtype == torch.float32), 0, 0,
-              *_workspace(C, x2.device, s), k, k, n, m, n, k, 1 if gelu else 0, s)
+              k, k, n, m, n, k, 1 if gelu else 0, s)
     return (y, g) if gelu else y
 
 
@@ -108,8 +93,7 @@ def linear_dgrad(dy2: torch.Tensor, weight: torch.Tensor, gelu_h: torch.Tensor |
     dx = torch.empty(m, k, device=dy2.device, dtype=dy2.dtype)
     s = _stream(dy2)
     if gelu_h is None:
-        C.gemm_nt(dy2.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, 0, 0, 0, 0, *_workspace(C, dy2.device, s),
-                  n, n, k, m, k, n, 0, s)
+        C.gemm_nt(dy2.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, 0, 0, 0, 0, n, n, k, m, k, n, 0, s)
         return dx
     from .gelu import _sync
     _sync(C)  # EPI 2 differentiates the selected GELU form
@@ -117,7 +101,7 @@ def linear_dgrad(dy2: torch.Tensor, weight: torch.Tensor, gelu_h: torch.Tensor |
     rows = C.gemm_nt_colpart_rows(m)
     part = torch.empty(rows, k, device=dy2.device, dtype=torch.float32)
     C.gemm_nt(dy2.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, 0, 0, h.data_ptr(), part.data_ptr(),
-              *_workspace(C, dy2.device, s), n, n, k, m, k, n, 2, s)
+              n, n, k, m, k, n, 2, s)
     odt = bias_dtype if bias_dtype in (torch.float32, torch.bfloat16) else torch.float32
     with graddst.into(bias_param):
         db = graddst.empty((k,), odt, dy2.device)
@@ -125,4 +109,56 @@ def linear_dgrad(dy2: torch.Tensor, weight: torch.Tensor, gelu_h: torch.Tensor |
     return dx, db.to(bias_dtype)
 
 
-__all__ = ["supported", "weight_t", "linear_fwd", "linear_dgrad", "ENABLED", "MODE"]
+# convolutions on the same kernel (ops/gemm.py routes to these): "1" (default) wherever a shape
+# qualifies, "0" never
+CONV = os.environ.get("FLUXMPI_GEMM_NT_CONV", "1") != "0"
+
+
+def conv_ok(pixels: int, c: int, cout: int, *tensors: torch.Tensor) -> bool:
+    """Whether a 3x3 / stride 1 / pad 1 convolution over ``pixels`` output pixels (C -> Cout)
+    runs on :func:`conv3x3`."""
+    if not CONV or not tensors or not tensors[0].is_cuda or any(t.dtype != torch.bfloat16 for t in tensors):
+        return False
+    C = _ext.get(required=False)
+    return C is not None and hasattr(C, "gemm_nt_conv") and bool(C.gemm_nt_conv_supported(pixels, c, cout))
+
+
+def gemm_ok(rows: int, n_out: int, k: int, *tensors: torch.Tensor) -> bool:
+    """Whether a 1x1 convolution / plain NT GEMM of this shape runs on :func:`gemm_plain`."""
+    if not CONV or not tensors or not tensors[0].is_cuda or any(t.dtype != torch.bfloat16 for t in tensors):
+        return False
+    C = _ext.get(required=False)
+    return C is not None and hasattr(C, "gemm_nt_stats") and bool(C.gemm_nt_supported(rows, n_out, k, k, k, n_out))
+
+
+def conv3x3(x: torch.Tensor, w_taps: torch.Tensor, y: torch.Tensor, stats: torch.Tensor | None = None) -> torch.Tensor:
+    """``y [N*H*W, Cout] = conv3x3(x)``: ``x`` NHWC [N, H, W, C] memory (a channels_last tensor),
+    ``w_taps`` [Cout, 9*C] (tap-major, channel-fastest: a channels_last filter, or the flipped
+    transpose of the input-gradient), ``stats``: the BatchNorm shards [64, 2, Cout] receive the
+    output's per-channel sum / sum of squares (EPI 3)."""
+    C = _ext.get(required=True)
+    n, c, h, wd = x.shape
+    cout = w_taps.shape[0]
+    s = _stream(x)
+    C.gemm_nt_conv(x.data_ptr(), w_taps.data_ptr(), y.data_ptr(), stats.data_ptr() if stats is not None else 0,
+                   n, h, wd, c, cout, 3 if stats is not None else 0, s)
+    return y
+
+
+def gemm_plain(a2: torch.Tensor, b2: torch.Tensor, c2: torch.Tensor, stats: torch.Tensor | None = None) -> torch.Tensor:
+    """``c2 [M, N] = a2 [M, K] @ b2 [N, K]^T`` (both k-contiguous rows); ``stats`` as in :func:`conv3x3`."""
+    C = _ext.get(required=True)
+    m, k = a2.shape
+    n = b2.shape[0]
+    s = _stream(a2)
+    if stats is not None:
+        C.gemm_nt_stats(a2.data_ptr(), b2.data_ptr(), c2.data_ptr(), stats.data_ptr(), a2.stride(0), b2.stride(0),
+                        c2.stride(0), m, n, k, s)
+    else:
+        C.gemm_nt(a2.data_ptr(), b2.data_ptr(), c2.data_ptr(), 0, 0, 0, 0, 0, a2.stride(0), b2.stride(0),
+                  c2.stride(0), m, n, k, 0, s)
+    return c2
+
+
+__all__ = ["supported", "weight_t", "linear_fwd", "linear_dgrad", "conv_ok", "gemm_ok", "conv3x3", "gemm_plain",
+           "ENABLED", "MODE", "CONV"]

@@ -168,6 +168,7 @@ class _LinearAddLayerNormFn(torch.autograd.Function):
         w, b = _affine(x, ln_w, ln_b)
         h, y, mean, rstd = _fwd(x, p.contiguous(), w, b, eps)
         ctx.save_for_backward(a, weight, h, w, mean, rstd)
+        ctx.weight = weight  # the leaf itself: its gradient's bucket slice (ops/graddst.py)
         ctx.dtypes = (ln_w.dtype if ln_w is not None else None, ln_b.dtype if ln_b is not None else None)
         ctx.bias_dtype = bias.dtype
         need = ctx.needs_input_grad
@@ -203,7 +204,8 @@ class _LinearAddLayerNormFn(torch.autograd.Function):
                 da = dgrad(g2, weight).reshape(a.shape)
         dw = None
         if ctx.needs_input_grad[1]:
-            dw = weight_grad(g2, a2, weight.dtype) if native_ok(a2, g2) else g2.t() @ a2
+            with graddst.into(ctx.weight):  # the DDP bucket slice when one is attached
+                dw = weight_grad(g2, a2, weight.dtype) if native_ok(a2, g2) else g2.t() @ a2
         return da, dw, (dbias if ctx.needs_input_grad[2] else None), dx, dlw, dlb, None, None
 
 

@@ -225,6 +225,7 @@ class DDP:
         self._carry_hook = None
         self.collectives_launched = 0  # gradient-bucket allreduces issued so far
         self.pack_copies = 0  # gradients the bucket packs had to copy (not delivered in place)
+        self.pack_copied: dict = {}  # shape -> copies (which producers still miss their slices)
         _ENGINES[module] = weakref.ref(self)
         self.zero_grad()
         self.step_count = 0
@@ -452,6 +453,11 @@ class DDP:
                     graddst.rearm(p)
         self._next_launch = 0
 
+    def _note_copy(self, p) -> None:
+        self.pack_copies += 1
+        key = "x".join(str(d) for d in p.shape)
+        self.pack_copied[key] = self.pack_copied.get(key, 0) + 1
+
     def _pack(self, b: _Bucket):
         """"steal" mode: copy the bucket's gradients into its flat buffer, one multi-tensor launch.
 
@@ -471,21 +477,22 @@ class DDP:
             elif g.data_ptr() == dptr:
                 if not _same_layout(g, dst):
                     dst.copy_(g.clone())
-                    self.pack_copies += 1
+                    self._note_copy(p)
                 # else already in place (delivered by the producing op, or p.grad set to the view)
             elif g.dtype is b.dtype and g.is_cuda and g.stride() == dst.stride():
                 # the common case: autograd's layout contract (the parameter's dense strides)
                 srcs.append(g)
                 dptrs.append(dptr)
                 ns.append(dst.numel())
+                self._note_copy(p)
             elif g.is_cuda and g.dtype == b.dtype and _same_layout(g, p) and _is_dense(g):
                 srcs.append(g)
                 dptrs.append(dptr)
                 ns.append(dst.numel())
+                self._note_copy(p)
             else:
                 dst.copy_(g)
-                self.pack_copies += 1
-        self.pack_copies += len(srcs)
+                self._note_copy(p)
         if srcs:
             C = _ext.get(required=True)
             code = mt.DTYPE_CODE[b.dtype]
@@ -784,7 +791,9 @@ class DDP:
                 "comm": (self.comm.name if self.communicate else "none"),
                 "direct_grads": self.direct_grads,
                 # gradients the packs copied per step so far (0: every one delivered in place)
-                "pack_copies_per_step": round(self.pack_copies / max(1, self.step_count), 2)}
+                "pack_copies_per_step": round(self.pack_copies / max(1, self.step_count), 2),
+                # the parameter shapes the packs copied (total over the steps so far), most first
+                "pack_copied_shapes": dict(sorted(self.pack_copied.items(), key=lambda kv: -kv[1])[:8])}
 
     def bucket_summary(self) -> list:
         return [{"index": b.index, "dtype": str(b.dtype), "numel": b.numel, "params": len(b.params),

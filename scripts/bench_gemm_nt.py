@@ -16,7 +16,6 @@ import torch
 
 sys.path.insert(0, __file__.rsplit("/scripts/", 1)[0])
 from fluxmpi_amd.ops import _ext  # noqa: E402
-from fluxmpi_amd.ops.gemm_nt import _workspace  # noqa: E402
 
 
 def t_us(fn, iters=20):
@@ -52,13 +51,13 @@ def checks_only(C, st, name, m, n, k):
     ref = a.float() @ w.float().t()
     for bdt in (torch.float32, torch.bfloat16):
         b = bias.to(bdt)
-        for _ in range(2):  # twice: the first launch must leave the publish flags zero
+        for _ in range(2):
             C.gemm_nt(a.data_ptr(), w.data_ptr(), c.data_ptr(), 0, b.data_ptr(), int(bdt == torch.float32), 0, 0,
-                      *_workspace(C, a.device, st), k, k, n, m, n, k, 0, st)
+                      k, k, n, m, n, k, 0, st)
             torch.cuda.synchronize()
             check(f"{name}_epi0_bias_{str(bdt)[6:]}", c, ref + b.float())
     C.gemm_nt(a.data_ptr(), w.data_ptr(), c.data_ptr(), c2.data_ptr(), bias.data_ptr(), 1, 0, 0,
-              *_workspace(C, a.device, st), k, k, n, m, n, k, 1, st)
+              k, k, n, m, n, k, 1, st)
     torch.cuda.synchronize()
     check(f"{name}_epi1_g", c2, torch.nn.functional.gelu((ref + bias).bfloat16().float(), approximate="tanh"))
 
@@ -90,7 +89,7 @@ def main():
         def ours(epi=0, h=None, part=None, bias_=None):
             C.gemm_nt(a.data_ptr(), w.data_ptr(), c.data_ptr(), c2.data_ptr() if epi == 1 else 0,
                       bias_.data_ptr() if bias_ is not None else 0, 1, h.data_ptr() if h is not None else 0,
-                      part.data_ptr() if part is not None else 0, *_workspace(C, a.device, st), k, k, n, m, n, k,
+                      part.data_ptr() if part is not None else 0, k, k, n, m, n, k,
                       epi, st)
 
         ref = a.float() @ w.float().t()

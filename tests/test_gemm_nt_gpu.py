@@ -1,7 +1,8 @@
 """gemm_nt.hip (ViT forward / input-gradient GEMMs with fused epilogues) vs PyTorch fp32: every
 ViT-B/16 Linear shape at batch 256 (M = 50432 tokens), plus odd k-tile counts, the minimum K and
 tile counts that are not a multiple of the CU count (the persistent kernel's tile stream and its
-LDS buffer parity cross tile boundaries), and stream-K splits of one tile over many workgroups."""
+LDS buffer parity cross tile boundaries), fewer tiles than CUs, and the implicit-GEMM 3x3
+convolution / BatchNorm-statistics epilogues."""
 import pytest
 import torch
 
@@ -14,9 +15,8 @@ VIT_FWD = [("qkv", M_VIT, 2304, 768), ("proj", M_VIT, 768, 768), ("fc1", M_VIT, 
 VIT_DGRAD = [("qkv", M_VIT, 2304, 768), ("proj", M_VIT, 768, 768), ("fc1", M_VIT, 3072, 768),
              ("fc2", M_VIT, 768, 3072)]  # (rows, N_out, N_in): dx [rows, N_in] = dy [rows, N_out] W
 SMALL = [(512, 768, 768), (768, 256, 3072), (256 * 41, 768, 832), (256 * 37, 512, 128), (256 * 300, 256, 192)]
-# stream-K: one tile split over 128 workgroups (127 contributors add into one finisher), ranges of
-# a few k-tiles crossing tile boundaries, fewer units than CUs
-STREAMK = [(256, 256, 8192), (512, 768, 4096), (256, 512, 1344), (1024, 1024, 2048)]
+# one tile with a long K, a few tiles (fewer than CUs), one tile per workgroup
+FEW_TILES = [(256, 256, 8192), (512, 768, 4096), (256, 512, 1344), (1024, 1024, 2048)]
 
 
 def _rel(a, b):
@@ -96,9 +96,9 @@ def test_small_and_odd_shapes(gpu_ext, gelu_form, m, n, k):
         _check_dgrad(m, n, k, gelu_form)
 
 
-@pytest.mark.parametrize("m,n,k", STREAMK)
-def test_stream_k_splits(gpu_ext, m, n, k):
-    for _ in range(2):  # a launch must leave the publish flags zero for the next
+@pytest.mark.parametrize("m,n,k", FEW_TILES)
+def test_few_tiles_long_k(gpu_ext, m, n, k):
+    for _ in range(2):
         _check_fwd(m, n, k, "f32", "tanh")
     if k % 256 == 0:
         _check_dgrad(m, n, k, "tanh")
@@ -119,3 +119,52 @@ def test_unsupported_shapes(gpu_ext):
     assert not G.supported(256, 768, 768, x.float(), w, fused=True)
     assert not G.supported(256, 768, 64, x, w, fused=True)  # K < 128
     assert not G.supported(256, 768, 96, x, w, fused=True)  # K not a multiple of 64
+
+
+# (nimg, H, W, C, Cout): output pixels tile by 256; odd image sizes (rows of a tile span images,
+# every padding case), the ResNet-50 stage-3/4 widths
+CONV = [(4, 8, 8, 64, 256), (256, 5, 7, 128, 256), (64, 14, 14, 256, 256), (256, 7, 7, 512, 512)]
+
+
+@pytest.mark.parametrize("nimg,h,w,c,co", CONV)
+def test_conv3x3_fwd_stats_and_dgrad(gpu_ext, nimg, h, w, c, co):
+    import torch.nn.functional as F
+    from fluxmpi_amd.ops import gemm as GM
+    from fluxmpi_amd.ops import gemm_nt as G
+    torch.manual_seed(2)
+    x = _uni(nimg, c, h, w).contiguous(memory_format=torch.channels_last)
+    wt = _uni(co, c, 3, 3, scale=(9 * c) ** -0.5).contiguous(memory_format=torch.channels_last)
+    M = nimg * h * w
+    assert G.conv_ok(M, c, co, x)
+    stats = torch.zeros(GM.SHARDS, 2, co, device="cuda")
+    for _ in range(2):
+        stats.zero_()
+        y = GM.conv3x3_fwd(x, wt, stats=stats)
+        ref = F.conv2d(x.float(), wt.float(), padding=1)
+        assert _rel(y, ref) < 5e-3
+    yf = y.float().permute(0, 2, 3, 1).reshape(M, co)
+    torch.testing.assert_close(stats[:, 0].sum(0), yf.sum(0), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(stats[:, 1].sum(0), (yf * yf).sum(0), rtol=1e-3, atol=1e-2)
+    if G.conv_ok(M, co, c, x):  # input gradient: the same kernel on the flipped transpose
+        dy = _uni(nimg, co, h, w).contiguous(memory_format=torch.channels_last)
+        GM.note_filter(wt)
+        dx = GM.conv3x3_dgrad(dy, wt)
+        dref = torch.nn.grad.conv2d_input(x.shape, wt.float(), dy.float(), padding=1)
+        assert _rel(dx, dref) < 5e-3
+
+
+@pytest.mark.parametrize("m,n,k", [(50176, 1024, 256), (12544, 512, 2048), (802816 // 4, 256, 64 * 2)])
+def test_conv1x1_stats(gpu_ext, m, n, k):
+    from fluxmpi_amd.ops import gemm as GM
+    from fluxmpi_amd.ops import gemm_nt as G
+    torch.manual_seed(3)
+    x = _uni(m, k)
+    w = _uni(n, k, scale=k ** -0.5)
+    assert G.gemm_ok(m, n, k, x, w)
+    stats = torch.zeros(GM.SHARDS, 2, n, device="cuda")
+    y = GM.conv1x1_fwd(x, w, stats=stats)
+    ref = x.float() @ w.float().t()
+    assert _rel(y, ref) < 5e-3
+    yf = y.float()
+    torch.testing.assert_close(stats[:, 0].sum(0), yf.sum(0), rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(stats[:, 1].sum(0), (yf * yf).sum(0), rtol=1e-3, atol=1e-2)
