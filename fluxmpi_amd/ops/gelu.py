@@ -79,8 +79,9 @@ def _native(h: torch.Tensor) -> bool:
             and n // 8 <= 1024 and h.numel() > 0)
 
 
-def gelu_bwd_bias(dy: torch.Tensor, h: torch.Tensor, bias_dtype=torch.float32):
-    """``(dh, db)``: ``dh = dy * gelu'(h)`` (the selected form), ``db = dh.sum(rows)`` in ``bias_dtype``."""
+def gelu_bwd_bias(dy: torch.Tensor, h: torch.Tensor, bias_dtype=torch.float32, bias_param=None):
+    """``(dh, db)``: ``dh = dy * gelu'(h)`` (the selected form), ``db = dh.sum(rows)`` in ``bias_dtype``
+    (written into ``bias_param``'s DDP bucket slice when one is attached, ``ops/graddst.py``)."""
     if not _native(h):
         dh = (dy.float() * _gelu_grad_ref(h.float())).to(h.dtype)
         return dh, dh.float().reshape(-1, h.shape[-1]).sum(0).to(bias_dtype)
@@ -97,7 +98,9 @@ def gelu_bwd_bias(dy: torch.Tensor, h: torch.Tensor, bias_dtype=torch.float32):
     C.gelu_bwd_bias(dy.data_ptr(), h.data_ptr(), dh.data_ptr(), part.data_ptr(), blocks, rows, n,
                     DTYPE_CODE[h.dtype], stream)
     out_dt = bias_dtype if bias_dtype in (torch.float32, torch.bfloat16) else torch.float32
-    db = torch.empty(n, device=h.device, dtype=out_dt)
+    from . import graddst
+    with graddst.into(bias_param):
+        db = graddst.empty((n,), out_dt, h.device)
     C.gemm_splitk_reduce(part.data_ptr(), blocks, n, db.data_ptr(), DTYPE_CODE[out_dt], stream)
     return dh, db.to(bias_dtype)
 
@@ -128,7 +131,7 @@ class _LinearGeluFn(torch.autograd.Function):
         _sync(_ext.get(required=True))  # the backward kernels (gelu.hip, gemm_nt EPI 2) read the form
         n_out, n_in = weight.shape
         rows = x.numel() // n_in
-        if x.is_contiguous() and gemm_nt.supported(rows, n_out, n_in, x, weight, fused=True):
+        if x.is_contiguous() and gemm_nt.supported(rows, n_out, n_in, x, weight, fused="fwd"):
             # bias + GELU in the GEMM epilogue: h and gelu(h) from the same registers
             h2, g2 = gemm_nt.linear_fwd(x.view(rows, n_in), weight, bias, gelu=True)
             h, g = h2.view(*x.shape[:-1], n_out), g2.view(*x.shape[:-1], n_out)
@@ -139,6 +142,7 @@ class _LinearGeluFn(torch.autograd.Function):
         ctx.weight = weight  # the leaf itself: its gradient's bucket slice (ops/graddst.py)
         ctx.has_bias = bias is not None
         ctx.bias_dtype = bias.dtype if bias is not None else None
+        ctx.bias = bias  # the leaf: its gradient's bucket slice
         ctx.link = link
         if link is not None:
             link.h, link.bias_dtype, link.bias = h, ctx.bias_dtype or torch.float32, bias
@@ -149,7 +153,7 @@ class _LinearGeluFn(torch.autograd.Function):
         x, w, h = ctx.saved_tensors
         dh, db = ctx.link.take() if ctx.link is not None else (None, None)
         if dh is None:  # the consumer did not fuse the GELU derivative: own pass
-            dh, db = gelu_bwd_bias(dy, h, ctx.bias_dtype or torch.float32)
+            dh, db = gelu_bwd_bias(dy, h, ctx.bias_dtype or torch.float32, bias_param=ctx.bias)
         else:
             dh = dh.view(h.shape)
         n = h.shape[-1]
@@ -162,7 +166,12 @@ class _LinearGeluFn(torch.autograd.Function):
             # long-K weight gradient on the split-K HIP kernel (ops/linear.py)
             from . import graddst
             with graddst.into(ctx.weight):  # the DDP bucket slice when one is attached
-                dw = weight_grad(dh2, x2, w.dtype) if _wgrad_mode() == "ours" and native_ok(x2, dh2) else dh2.t() @ x2
+                if _wgrad_mode() == "ours" and native_ok(x2, dh2):
+                    dw = weight_grad(dh2, x2, w.dtype)
+                elif dh2.dtype == x2.dtype == w.dtype:  # short K ([CLS]-only last block): hipBLASLt, into the slice
+                    dw = torch.mm(dh2.t(), x2, out=graddst.empty(tuple(w.shape), w.dtype, dh2.device))
+                else:
+                    dw = (dh2.t() @ x2).to(w.dtype)
         return dx, dw, (db if ctx.has_bias and ctx.needs_input_grad[2] else None), None
 
 

@@ -13,11 +13,18 @@ tile exactly; :func:`supported` says whether a call qualifies, callers keep the 
 otherwise. Numerics: bf16 operands, fp32 accumulation, one bf16 rounding of each output (the
 GELU of the ROUNDED pre-activation, like ``F.gelu(F.linear(...))``).
 
-``FLUXMPI_GEMM_NT``: ``fused`` (default) only the calls that carry an epilogue fusion (fc1's bias +
-GELU forward, fc2's input gradient with fc1's GELU backward + bias gradient); ``all`` every
-qualifying forward / input gradient; ``0`` never (hipBLASLt). Measured (profiles/rd4c_gemm_nt.md):
-the plain K = 768 GEMMs are 5-10 % behind hipBLASLt's stream-K kernels, whose epilogues do not
-all land in one bandwidth burst.
+``FLUXMPI_GEMM_NT``: ``dgrad`` (default) only fc2's input gradient with fc1's GELU backward + bias
+gradient in the epilogue (EPI 2: 410 vs 435 us for hipBLASLt + the GELU-backward kernel);
+``fused`` also fc1's bias + GELU forward (EPI 1: 368 us vs 340 for hipBLASLt + the GELU kernel —
+its doubled output makes the epilogue the bottleneck); ``all`` every qualifying forward / input
+gradient (plain K = 768 GEMMs 7-12 % behind hipBLASLt); ``0`` never. Measured:
+profiles/rd4f_bench_gemm_nt.jsonl (the hipBLASLt columns are the roofline baseline per shape).
+
+Convolutions (ops/gemm.py routes here, ``FLUXMPI_GEMM_NT_CONV``, default on): the stride-1 3x3
+forward / input gradient and the 1x1 forward / input gradient when the output has >= 160 tiles
+(a persistent workgroup per CU needs them) and K >= 1024 — where the 256x256 tiles beat the
+128-tile kernel: 3x3 at 14x14x256 70 vs 101 us; short K or few tiles lose
+(profiles/rd4f_bench_conv_nt.jsonl).
 """
 from __future__ import annotations
 
@@ -29,7 +36,7 @@ from . import _ext
 from . import graddst
 from .multi_tensor import DTYPE_CODE
 
-MODE = os.environ.get("FLUXMPI_GEMM_NT", "fused").lower()
+MODE = os.environ.get("FLUXMPI_GEMM_NT", "dgrad").lower()
 ENABLED = MODE != "0"
 
 
@@ -37,13 +44,18 @@ def _stream(t):
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
-def supported(rows: int, n_out: int, k: int, *tensors: torch.Tensor, fused: bool = False) -> bool:
+def supported(rows: int, n_out: int, k: int, *tensors: torch.Tensor, fused: bool | str = False) -> bool:
     """Whether gemm_nt takes ``[rows, k] x [n_out, k]^T`` (both operands k-contiguous after the
-    weight transpose of an input gradient) under the current mode."""
+    weight transpose of an input gradient) under the current mode. ``fused``: the call carries an
+    epilogue fusion — ``"fwd"`` (fc1 bias + GELU: modes fused / all), ``"dgrad"`` (GELU backward:
+    modes dgrad / fused / all), ``True`` (either: shape checks of the kernel itself)."""
     if not ENABLED or not tensors or not tensors[0].is_cuda:
         return False
-    if MODE not in ("all", "1") and not (fused and MODE == "fused"):
-        return False
+    if MODE not in ("all", "1"):
+        ok = (fused is True or (fused == "fwd" and MODE == "fused")
+              or (fused == "dgrad" and MODE in ("fused", "dgrad")))
+        if not ok:
+            return False
     if any(t.dtype != torch.bfloat16 for t in tensors):
         return False
     C = _ext.get(required=False)
@@ -114,10 +126,20 @@ def linear_dgrad(dy2: torch.Tensor, weight: torch.Tensor, gelu_h: torch.Tensor |
 CONV = os.environ.get("FLUXMPI_GEMM_NT_CONV", "1") != "0"
 
 
+MIN_TILES = int(os.environ.get("FLUXMPI_GEMM_NT_MIN_TILES", "160"))
+MIN_K = int(os.environ.get("FLUXMPI_GEMM_NT_MIN_K", "1024"))
+
+
+def _worth(rows: int, n_out: int, k: int) -> bool:
+    return (rows // 256) * (n_out // 256) >= MIN_TILES and k >= MIN_K
+
+
 def conv_ok(pixels: int, c: int, cout: int, *tensors: torch.Tensor) -> bool:
     """Whether a 3x3 / stride 1 / pad 1 convolution over ``pixels`` output pixels (C -> Cout)
     runs on :func:`conv3x3`."""
     if not CONV or not tensors or not tensors[0].is_cuda or any(t.dtype != torch.bfloat16 for t in tensors):
+        return False
+    if not _worth(pixels, cout, 9 * c):
         return False
     C = _ext.get(required=False)
     return C is not None and hasattr(C, "gemm_nt_conv") and bool(C.gemm_nt_conv_supported(pixels, c, cout))
@@ -126,6 +148,8 @@ def conv_ok(pixels: int, c: int, cout: int, *tensors: torch.Tensor) -> bool:
 def gemm_ok(rows: int, n_out: int, k: int, *tensors: torch.Tensor) -> bool:
     """Whether a 1x1 convolution / plain NT GEMM of this shape runs on :func:`gemm_plain`."""
     if not CONV or not tensors or not tensors[0].is_cuda or any(t.dtype != torch.bfloat16 for t in tensors):
+        return False
+    if not _worth(rows, n_out, k):
         return False
     C = _ext.get(required=False)
     return C is not None and hasattr(C, "gemm_nt_stats") and bool(C.gemm_nt_supported(rows, n_out, k, k, k, n_out))

@@ -194,7 +194,7 @@ class _LinearAddLayerNormFn(torch.autograd.Function):
             from .linear import dgrad
             link = ctx.gelu_link
             if (link is not None and link.h is not None and link.h.shape == a.shape
-                    and gemm_nt.supported(g2.shape[0], n_in, n_out, g2, weight, link.h, fused=True)):
+                    and gemm_nt.supported(g2.shape[0], n_in, n_out, g2, weight, link.h, fused="dgrad")):
                 # `a` = gelu(h) of the linear_gelu node upstream: its GELU derivative and its bias
                 # gradient come out of this input-gradient GEMM's epilogue (gemm_nt.hip EPI 2)
                 link.dh, link.db = gemm_nt.linear_dgrad(g2, weight, gelu_h=link.h, bias_dtype=link.bias_dtype,
@@ -205,7 +205,12 @@ class _LinearAddLayerNormFn(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[1]:
             with graddst.into(ctx.weight):  # the DDP bucket slice when one is attached
-                dw = weight_grad(g2, a2, weight.dtype) if native_ok(a2, g2) else g2.t() @ a2
+                if native_ok(a2, g2):
+                    dw = weight_grad(g2, a2, weight.dtype)
+                elif g2.dtype == a2.dtype == weight.dtype:  # short K ([CLS]-only last block): into the slice
+                    dw = torch.mm(g2.t(), a2, out=graddst.empty(tuple(weight.shape), weight.dtype, g2.device))
+                else:
+                    dw = (g2.t() @ a2).to(weight.dtype)
         return da, dw, (dbias if ctx.needs_input_grad[2] else None), dx, dlw, dlb, None, None
 
 
