@@ -123,11 +123,20 @@ def test_unsupported_shapes(gpu_ext):
 
 # (nimg, H, W, C, Cout): output pixels tile by 256; odd image sizes (rows of a tile span images,
 # every padding case), the ResNet-50 stage-3/4 widths
-CONV = [(4, 8, 8, 64, 256), (256, 5, 7, 128, 256), (64, 14, 14, 256, 256), (256, 7, 7, 512, 512)]
+CONV_SHAPES = [(4, 8, 8, 64, 256), (256, 5, 7, 128, 256), (64, 14, 14, 256, 256), (256, 7, 7, 512, 512)]
 
 
-@pytest.mark.parametrize("nimg,h,w,c,co", CONV)
-def test_conv3x3_fwd_stats_and_dgrad(gpu_ext, nimg, h, w, c, co):
+@pytest.fixture
+def any_shape(monkeypatch):
+    """The kernel on every shape it supports (the routing's tile-count / K thresholds off)."""
+    from fluxmpi_amd.ops import gemm_nt as G
+    monkeypatch.setattr(G, "MIN_TILES", 0)
+    monkeypatch.setattr(G, "MIN_K", 0)
+    monkeypatch.setattr(G, "CONV", True)
+
+
+@pytest.mark.parametrize("nimg,h,w,c,co", CONV_SHAPES)
+def test_conv3x3_fwd_stats_and_dgrad(gpu_ext, any_shape, nimg, h, w, c, co):
     import torch.nn.functional as F
     from fluxmpi_amd.ops import gemm as GM
     from fluxmpi_amd.ops import gemm_nt as G
@@ -154,7 +163,7 @@ def test_conv3x3_fwd_stats_and_dgrad(gpu_ext, nimg, h, w, c, co):
 
 
 @pytest.mark.parametrize("m,n,k", [(50176, 1024, 256), (12544, 512, 2048), (802816 // 4, 256, 64 * 2)])
-def test_conv1x1_stats(gpu_ext, m, n, k):
+def test_conv1x1_stats(gpu_ext, any_shape, m, n, k):
     from fluxmpi_amd.ops import gemm as GM
     from fluxmpi_amd.ops import gemm_nt as G
     torch.manual_seed(3)
@@ -168,3 +177,14 @@ def test_conv1x1_stats(gpu_ext, m, n, k):
     yf = y.float()
     torch.testing.assert_close(stats[:, 0].sum(0), yf.sum(0), rtol=1e-3, atol=1e-2)
     torch.testing.assert_close(stats[:, 1].sum(0), (yf * yf).sum(0), rtol=1e-3, atol=1e-2)
+
+
+def test_conv_routing_thresholds(gpu_ext):
+    """The default routing takes the 256x256 kernel only where it measured faster: >= 160 output
+    tiles and K >= 1024 (ResNet-50 stage 3's 3x3 yes; stage 4's 98 tiles and K = 256 1x1s no)."""
+    from fluxmpi_amd.ops import gemm_nt as G
+    x = torch.zeros(8, device="cuda", dtype=torch.bfloat16)
+    assert G.conv_ok(50176, 256, 256, x)          # 14x14x256 3x3: 196 tiles, K = 2304
+    assert not G.conv_ok(12544, 512, 512, x)      # 7x7x512: 98 tiles
+    assert G.gemm_ok(50176, 256, 1024, x)         # 1x1 1024 -> 256
+    assert not G.gemm_ok(50176, 1024, 256, x)     # K = 256
