@@ -155,7 +155,7 @@ template <int EPI, int BIAS, bool CONV, int GF = 1>  // GF (EPI 1 / 2): 1 tanh G
 __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[kSmem];
   // vector-memory instructions per wave in an epilogue (lower bound: unconditional ones)
-  constexpr int kEpiVm = EPI == 1 || EPI == 2 ? 56 : 32;
+  constexpr int kEpiVm = EPI == 1 || EPI == 2 ? 32 : 16;
   const int G = gridDim.x;
   int gi = blockIdx.x;
   {  // bijective XCD-aware range order: the workgroups of one XCD take neighbouring ranges
@@ -366,8 +366,13 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
     else ktile(u, 0, cur, nxt, std::true_type{}, Z{});
     for (int t = 1; t < nk; ++t) ktile(u + t, t, cur, nxt, std::false_type{}, Z{});
 
-    // ---- epilogue: acc[ph][i][j][r] = C[m0 + wr*128 + 32ph + 16i + (lane & 15)][n0 + wc*64 + 16j + 4(lane >> 4) + r]
-    const int lane_e = opaque(lane), fr_e = lane_e & 15, cq_e = 4 * (lane_e >> 4);
+    // ---- epilogue. acc[ph][i][j][r] = C[m0 + wr*128 + 32ph + 16i + (lane & 15)][n0 + wc*64 + 16j + 4(lane >> 4) + r].
+    // The rounded values are exchanged between lane rows g and g ^ 1 (v_permlane16_swap: row 2k
+    // keeps its own 4 columns of block 2p and receives row 2k+1's, row 2k+1 likewise for block
+    // 2p + 1), so each lane holds 8 consecutive columns: 16-B stores / GELU-input loads instead
+    // of 8-B ones (half the instructions, whole 64-B segments). Lane row g holds, for pair p,
+    // columns 32p + 16 (g & 1) + 8 (g >> 1) .. + 7 of the wave's 64.
+    const int lane_e = opaque(lane), fr_e = lane_e & 15, g_e = lane_e >> 4, cq_e = 4 * g_e;
     float bias[4][4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -385,32 +390,31 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
         for (int r = 0; r < 4; ++r) bias[j][r] = 0.f;
       }
     }
-    float cs[4][4], cq2[EPI == 3 ? 4 : 1][4];
+    const int colx = wc * 64 + 16 * (g_e & 1) + 8 * (g_e >> 1);  // the lane's first column (pair 0)
+    float cs[2][8], cq2[EPI == 3 ? 2 : 1][8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int q = 0; q < 2; ++q)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) cs[j][r] = 0.f;
-    if (EPI == 3) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) cq2[j][r] = 0.f;
-    }
+      for (int e = 0; e < 8; ++e) {
+        cs[q][e] = 0.f;
+        if (EPI == 3) cq2[q][e] = 0.f;
+      }
     // outputs through buffer resources based at the tile's first element (wave-uniform SGPRs):
     // voffset = the lane's (row, column) byte offset in the tile (one VGPR), soffset = the
-    // (ph, ii) row block, the j column block an immediate
+    // (ph, ii) row block, the column pair an immediate
     auto tile_rsrc = [&](const void* base) {
-      const uint64_t a = reinterpret_cast<uint64_t>(static_cast<const bf16*>(base) + static_cast<int64_t>(cur.m0()) * p.ldc + cur.n0());
+      const uint64_t a = reinterpret_cast<uint64_t>(static_cast<const bf16*>(base) +
+                                                    static_cast<int64_t>(cur.m0()) * p.ldc + cur.n0());
       const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
       const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
       return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo), 0,
                                                0x7fffffff, 0x00020000);
     };
     const int ldcb = static_cast<int>(p.ldc) * 2;  // < 2^23 (gemm_nt_supported)
-    const int vo = (wr * 128 + fr_e) * ldcb + (wc * 64 + cq_e) * 2;
+    const int vo = (wr * 128 + fr_e) * ldcb + colx * 2;
     auto rowblk = [&](int ph, int ii) { return __builtin_amdgcn_readfirstlane((32 * ph + 16 * ii) * ldcb); };
     const __amdgpu_buffer_rsrc_t crs = tile_rsrc(p.c);
-    i32x2 hv[4][2][4];  // EPI 2: every GELU input of the tile's lane issued before the first use (one round trip)
+    i32x4 hv[4][2][2];  // EPI 2: every GELU input of the tile's lane issued before the first use (one round trip)
     if (EPI == 2) {
       const __amdgpu_buffer_rsrc_t hrs = tile_rsrc(p.h);
 #pragma unroll
@@ -418,99 +422,104 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
 #pragma unroll
         for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) hv[ph][ii][j] = __builtin_amdgcn_raw_buffer_load_b64(hrs, vo + 32 * j, rowblk(ph, ii), 0);
+          for (int q = 0; q < 2; ++q) hv[ph][ii][q] = __builtin_amdgcn_raw_buffer_load_b128(hrs, vo + 64 * q, rowblk(ph, ii), 0);
     }
 #pragma unroll
     for (int ph = 0; ph < 4; ++ph) {
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii) {
+        uint32_t lo[4], hi[4];  // bf16 pairs (columns r 0-1 / 2-3) of each block j, this lane's columns
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           bf16 o[4];
-          if (EPI == 0) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = static_cast<bf16>(acc[ph][ii][j][r] + bias[j][r]);
-          } else if (EPI == 3) {  // the BatchNorm statistics of the rounded output
+          for (int r = 0; r < 4; ++r) o[r] = static_cast<bf16>(acc[ph][ii][j][r] + bias[j][r]);  // EPI 2/3: bias 0
+          __builtin_memcpy(&lo[j], o, 4);
+          __builtin_memcpy(&hi[j], o + 2, 4);
+        }
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              o[r] = static_cast<bf16>(acc[ph][ii][j][r]);
-              const float f = static_cast<float>(o[r]);
-              cs[j][r] += f;
-              cq2[j][r] = fmaf(f, f, cq2[j][r]);
+        for (int q = 0; q < 2; ++q) {
+          const auto xl = __builtin_amdgcn_permlane16_swap(lo[2 * q], lo[2 * q + 1], false, false);
+          const auto xh = __builtin_amdgcn_permlane16_swap(hi[2 * q], hi[2 * q + 1], false, false);
+          const uint32_t w0 = xl[0], w1 = xh[0], w2 = xl[1], w3 = xh[1];
+          const i32x4 w = {static_cast<int>(w0), static_cast<int>(w1), static_cast<int>(w2), static_cast<int>(w3)};
+          bf16 v8[8];
+          __builtin_memcpy(v8, &w, 16);
+          i32x4 out = w;
+          if (EPI == 3) {  // the BatchNorm statistics of the rounded output
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float f = static_cast<float>(v8[e]);
+              cs[q][e] += f;
+              cq2[q][e] = fmaf(f, f, cq2[q][e]);
             }
           } else if (EPI == 1) {
-            bf16 gg[4];
+            bf16 gg[8];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              o[r] = static_cast<bf16>(acc[ph][ii][j][r] + bias[j][r]);
-              const float x = static_cast<float>(o[r]);  // GELU of the bf16 pre-activation, as F.gelu(h)
+            for (int e = 0; e < 8; ++e) {
+              const float x = static_cast<float>(v8[e]);  // GELU of the bf16 pre-activation, as F.gelu(h)
               if constexpr (GF == 1) {
-                gg[r] = static_cast<bf16>(gelu_tanh(x));
+                gg[e] = static_cast<bf16>(gelu_tanh(x));
               } else {
-                float cdf, e;
-                gelu_parts(x, cdf, e);
-                gg[r] = static_cast<bf16>(x * cdf);
+                float cdf, ee;
+                gelu_parts(x, cdf, ee);
+                gg[e] = static_cast<bf16>(x * cdf);
               }
             }
-            i32x2 gv;
-            __builtin_memcpy(&gv, gg, 8);
-            __builtin_amdgcn_raw_buffer_store_b64(gv, tile_rsrc(p.c2), vo + 32 * j, rowblk(ph, ii), 0);
-          } else {
-            bf16 hh[4];
-            __builtin_memcpy(hh, &hv[ph][ii][j], 8);
+            i32x4 gv;
+            __builtin_memcpy(&gv, gg, 16);
+            __builtin_amdgcn_raw_buffer_store_b128(gv, tile_rsrc(p.c2), vo + 64 * q, rowblk(ph, ii), 0);
+          } else if (EPI == 2) {
+            bf16 hh[8], oo[8];
+            __builtin_memcpy(hh, &hv[ph][ii][q], 16);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float dg = static_cast<float>(static_cast<bf16>(acc[ph][ii][j][r]));  // the bf16 dg autograd sees
-              const float x = static_cast<float>(hh[r]);
+            for (int e = 0; e < 8; ++e) {
+              const float dg = static_cast<float>(v8[e]);  // the bf16 dg autograd sees
+              const float x = static_cast<float>(hh[e]);
               float d;
               if constexpr (GF == 1) {
                 d = gelu_tanh_grad(x);
               } else {
-                float cdf, e;
-                gelu_parts(x, cdf, e);
-                d = fmaf(x * 0.39894228040143268f, e, cdf);
+                float cdf, ee;
+                gelu_parts(x, cdf, ee);
+                d = fmaf(x * 0.39894228040143268f, ee, cdf);
               }
-              o[r] = static_cast<bf16>(dg * d);
-              cs[j][r] += static_cast<float>(o[r]);  // the bias gradient of the rounded dh
+              oo[e] = static_cast<bf16>(dg * d);
+              cs[q][e] += static_cast<float>(oo[e]);  // the bias gradient of the rounded dh
             }
+            __builtin_memcpy(&out, oo, 16);
           }
-          i32x2 ov;
-          __builtin_memcpy(&ov, o, 8);
-          __builtin_amdgcn_raw_buffer_store_b64(ov, crs, vo + 32 * j, rowblk(ph, ii), 0);
+          __builtin_amdgcn_raw_buffer_store_b128(out, crs, vo + 64 * q, rowblk(ph, ii), 0);
         }
       }
     }
-    if (EPI == 2) {
+    if (EPI == 2 || EPI == 3) {
+      // the wave's 128 rows summed per column (butterflies over the 16 row lanes)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int q = 0; q < 2; ++q)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) cs[j][r] = row_sum16(cs[j][r]);
-      if (fr_e == 0) {
-        float* dst = p.colpart + static_cast<int64_t>(2 * cur.tm + wr) * p.N + cur.n0() + wc * 64 + cq_e;
+        for (int e = 0; e < 8; ++e) {
+          cs[q][e] = row_sum16(cs[q][e]);
+          if (EPI == 3) cq2[q][e] = row_sum16(cq2[q][e]);
+        }
+    }
+    if (EPI == 2 && fr_e == 0) {  // fc1's bias-gradient partials: row 2 tm + wr of colpart
+      float* dst = p.colpart + static_cast<int64_t>(2 * cur.tm + wr) * p.N + cur.n0() + colx;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) *reinterpret_cast<float4*>(dst + 16 * j) = float4{cs[j][0], cs[j][1], cs[j][2], cs[j][3]};
+      for (int q = 0; q < 2; ++q) {
+        *reinterpret_cast<float4*>(dst + 32 * q) = float4{cs[q][0], cs[q][1], cs[q][2], cs[q][3]};
+        *reinterpret_cast<float4*>(dst + 32 * q + 4) = float4{cs[q][4], cs[q][5], cs[q][6], cs[q][7]};
       }
     }
-    if (EPI == 3) {
-      // the wave's 128 rows summed per column (butterflies over the 16 row lanes), then one
-      // atomic per column per wave row into the tile's statistics shard
+    if (EPI == 3 && fr_e == 0) {  // one atomic per column per wave row into the tile's statistics shard
+      float* shard = p.stats + static_cast<int64_t>(T % kShards) * 2 * p.N + cur.n0() + colx;
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int q = 0; q < 2; ++q)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          cs[j][r] = row_sum16(cs[j][r]);
-          cq2[j][r] = row_sum16(cq2[j][r]);
+        for (int e = 0; e < 8; ++e) {
+          atomicAdd(shard + 32 * q + e, cs[q][e]);
+          atomicAdd(shard + p.N + 32 * q + e, cq2[q][e]);
         }
-      if (fr_e == 0) {
-        float* shard = p.stats + static_cast<int64_t>(T % kShards) * 2 * p.N + cur.n0() + wc * 64 + cq_e;
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            atomicAdd(shard + 16 * j + r, cs[j][r]);
-            atomicAdd(shard + p.N + 16 * j + r, cq2[j][r]);
-          }
-      }
     }
     ++seg;
     after_epi = true;

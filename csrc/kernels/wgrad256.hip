@@ -467,14 +467,15 @@ __global__ __launch_bounds__(kThreads, 2) void wgrad256pp_kernel(W256Args p) {
 }
 
 // pipeline variant: 0 = BK 32 x 4 stages, 1 = BK 64 x 2 stages, 2 = variant 0 with s_setprio(1)
-// around each step's MFMAs, 3 (default) = variant 0 with the addressing hoisted out of the loop,
-// 4 = the ping-pong schedule (wgrad256pp_kernel)
+// around each step's MFMAs, 3 = variant 0 with the addressing hoisted out of the loop,
+// 4 (default) = the ping-pong schedule (wgrad256pp_kernel): +1-3 % on three of the four ViT-B/16
+// shapes, equal on the fourth (profiles/rd4c_bench_wgrad_v3_v4.jsonl)
 int g_variant = -1;
 int variant() {
   if (g_variant < 0) {
     const char* e = std::getenv("FLUXMPI_WGRAD256_VARIANT");
-    g_variant = e != nullptr ? std::atoi(e) : 3;
-    if (g_variant < 0 || g_variant > 4) g_variant = 3;
+    g_variant = e != nullptr ? std::atoi(e) : 4;
+    if (g_variant < 0 || g_variant > 4) g_variant = 4;
   }
   return g_variant;
 }
@@ -482,7 +483,7 @@ int bk_of(int v) { return v == 1 ? 64 : 32; }
 
 }  // namespace
 
-void wgrad256_set_variant(int v) { g_variant = v >= 0 && v <= 4 ? v : 3; }
+void wgrad256_set_variant(int v) { g_variant = v >= 0 && v <= 4 ? v : 4; }
 
 bool wgrad256_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb) {
   return M % kTile == 0 && N % kTile == 0 && M > 0 && N > 0 && K > 0 && K < (int64_t(1) << 31) && lda % 8 == 0 &&

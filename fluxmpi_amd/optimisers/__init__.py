@@ -252,8 +252,9 @@ def _same_dense(*ts) -> bool:
     """All tensors dense (no gaps or overlaps) with identical shape and strides: the flat
     multi-tensor kernels then see matching elements at matching offsets (contiguous, or e.g.
     a channels_last filter with its channels_last gradient and zeros_like moments)."""
+    from ..ops.graddst import _dense
     t0 = ts[0]
-    if not (t0.is_contiguous() or t0.is_non_overlapping_and_dense()):
+    if not (t0.is_contiguous() or _dense(t0)):
         return False
     return all(t.shape == t0.shape and t.stride() == t0.stride() for t in ts[1:])
 

@@ -137,3 +137,15 @@ def test_fp16_adam_zero_gradient_is_finite():
             x = out["w"]
         assert torch.isfinite(x).all(), (type(rule).__name__, x)
         assert x[1] == 1.0 and x[3] == 1.0, (type(rule).__name__, x)
+
+
+def test_same_dense_layouts():
+    """The fused-optimiser eligibility check on layouts (CPU tensors: the check itself)."""
+    import torch
+    from fluxmpi_amd.optimisers import _same_dense
+    w = torch.zeros(8, 3, 7, 7).contiguous(memory_format=torch.channels_last)
+    g = torch.zeros_like(w)
+    assert _same_dense(w, g, torch.zeros_like(w), torch.zeros_like(w))
+    assert not _same_dense(w, torch.zeros(8, 3, 7, 7))          # strides differ
+    assert not _same_dense(torch.zeros(4, 6)[:, :3], torch.zeros(4, 3))  # gaps
+    assert _same_dense(torch.nn.Parameter(torch.zeros(5, 5)), torch.zeros(5, 5))
