@@ -101,12 +101,26 @@ class Functional:
                 d = d.setdefault(k, {})
             d[leaf] = p
         FluxMPI.synchronize(model, root_rank=0)  # parameters and buffers (BatchNorm statistics)
-        self.st = O.setup(rule, self.ps)
+        # the optimiser updates fp32 parameters (as a Lux / Optimisers.jl user keeps Float32
+        # parameters: Optimisers.jl casts beta to eltype(x), and BFloat16(0.999) == 1 would make
+        # Adam's bias correction 0/0); the bf16 compute copies are refreshed from them by one
+        # multi-tensor cast launch per step
         self.params = [p for p in model.parameters()]
+        self.ps32 = self._map(self.ps, lambda p: p.detach().float() if p.dtype != torch.float32 else p)
+        self.low = [(p, q) for p, q in zip(self._leaves(self.ps), self._leaves(self.ps32)) if q is not p]
+        self.st = O.setup(rule, self.ps32)
         self.plan = plan_buckets([p.detach() for p in self.params if p.requires_grad], None)
         self.communicate = FluxMPI.total_workers() > 1 or os.environ.get("FLUXMPI_FORCE_COMM") == "1"
         self.timing = False
         self.step_count = 0
+
+    @classmethod
+    def _map(cls, t, fn):
+        return {k: cls._map(v, fn) for k, v in t.items()} if isinstance(t, dict) else fn(t)
+
+    @classmethod
+    def _leaves(cls, t):
+        return [x for v in t.values() for x in cls._leaves(v)] if isinstance(t, dict) else [t]
 
     def __call__(self, x):
         return self.module(x)
@@ -116,7 +130,22 @@ class Functional:
 
     def step(self):
         gs = self.F.allreduce_gradients(self._grads(self.ps), op=self.op, like=self.ps)
-        self.O.update_(self.st, self.ps, gs)
+        self.O.update_(self.st, self.ps32, gs)
+        if self.low:  # the compute copies from the updated fp32 parameters, one launch per dtype
+            from fluxmpi_amd.ops import _ext
+            from fluxmpi_amd.ops.multi_tensor import DTYPE_CODE
+            groups: dict = {}
+            for p, q in self.low:
+                groups.setdefault(p.dtype, []).append((p, q))
+            for dt, pq in groups.items():
+                if not pq[0][0].is_cuda:
+                    for p, q in pq:
+                        p.data.copy_(q)
+                    continue
+                C = _ext.get(required=True)
+                C.mt_copy([q.data_ptr() for _, q in pq], [p.data_ptr() for p, _ in pq], [p.numel() for p, _ in pq],
+                          DTYPE_CODE[torch.float32], DTYPE_CODE[dt], 1.0,
+                          torch.cuda.current_stream(pq[0][0].device).cuda_stream)
         for p in self.params:
             p.grad = None
         self.step_count += 1

@@ -250,6 +250,7 @@ void for_each_group(const std::vector<uintptr_t>& p, const std::vector<uintptr_t
 
 #define FLUXMPI_OPT_COMBOS(X)            \
   X(float, float, float, false)          \
+  X(float, bf16, float, false)           \
   X(bf16, bf16, bf16, false)             \
   X(bf16, bf16, float, false)            \
   X(bf16, bf16, float, true)             \

@@ -13,12 +13,13 @@ tile exactly; :func:`supported` says whether a call qualifies, callers keep the 
 otherwise. Numerics: bf16 operands, fp32 accumulation, one bf16 rounding of each output (the
 GELU of the ROUNDED pre-activation, like ``F.gelu(F.linear(...))``).
 
-``FLUXMPI_GEMM_NT``: ``dgrad`` (default) only fc2's input gradient with fc1's GELU backward + bias
-gradient in the epilogue (EPI 2: 410 vs 435 us for hipBLASLt + the GELU-backward kernel);
-``fused`` also fc1's bias + GELU forward (EPI 1: 368 us vs 340 for hipBLASLt + the GELU kernel —
-its doubled output makes the epilogue the bottleneck); ``all`` every qualifying forward / input
-gradient (plain K = 768 GEMMs 7-12 % behind hipBLASLt); ``0`` never. Measured:
-profiles/rd4f_bench_gemm_nt.jsonl (the hipBLASLt columns are the roofline baseline per shape).
+``FLUXMPI_GEMM_NT``: ``fused`` (default) the calls that carry an epilogue fusion — fc1's bias +
+GELU forward (EPI 1: 318 us vs 336 for hipBLASLt + the GELU kernel) and fc2's input gradient
+with fc1's GELU backward + bias-gradient partials (EPI 2: 364 vs 435 us for hipBLASLt + the
+GELU-backward kernel); ``dgrad`` only the latter; ``all`` also every plain forward / input
+gradient (at parity with hipBLASLt on qkv / proj, 1-5 % behind on the K = 3072 / N = 3072
+ones); ``0`` never. Measured: profiles/rd4i_bench_gemm_nt.jsonl (the hipBLASLt columns are the
+roofline baseline per shape); whole ViT-B/16 step 7.30k (fused) / 7.32k (dgrad) img/s.
 
 Convolutions (ops/gemm.py routes here, ``FLUXMPI_GEMM_NT_CONV``, default on): the stride-1 3x3
 forward / input gradient and the 1x1 forward / input gradient when the output has >= 160 tiles
@@ -36,7 +37,7 @@ from . import _ext
 from . import graddst
 from .multi_tensor import DTYPE_CODE
 
-MODE = os.environ.get("FLUXMPI_GEMM_NT", "dgrad").lower()
+MODE = os.environ.get("FLUXMPI_GEMM_NT", "fused").lower()
 ENABLED = MODE != "0"
 
 

@@ -13,6 +13,7 @@ from .multi_tensor import DTYPE_CODE
 
 _SUPPORTED = {
     (torch.float32, torch.float32, torch.float32, False),
+    (torch.float32, torch.bfloat16, torch.float32, False),  # fp32 parameters, bf16 gradients (mixed precision)
     (torch.bfloat16, torch.bfloat16, torch.bfloat16, False),
     (torch.bfloat16, torch.bfloat16, torch.float32, False),
     (torch.bfloat16, torch.bfloat16, torch.float32, True),

@@ -75,6 +75,7 @@ def main():
             return G.conv1x1_fwd(x2, w2, stats=st)
 
         NT.CONV = True
+        NT.MIN_TILES, NT.MIN_K = 0, 0  # measure every shape the kernel supports (routing thresholds off)
         ok_nt = NT.conv_ok(M, ci, co, x) if k == 3 else NT.gemm_ok(M, co, ci, x2)
         rec["nt_supported"] = bool(ok_nt)
         paths = [("glds", False)] + ([("nt", True)] if ok_nt else [])
@@ -100,6 +101,7 @@ def main():
         del x, wt, ref, y, x2
         torch.cuda.empty_cache()
     NT.CONV = True
+    NT.MIN_TILES, NT.MIN_K = 0, 0
     # input gradients of the 3x3 shapes (the flipped-transpose filter, same kernel)
     for name, h, w, ci, co in (("s3_3x3_dgrad", 14, 14, 256, 256), ("s4_3x3_dgrad", 7, 7, 512, 512)):
         dy = nhwc(B, co, h, w)

@@ -69,6 +69,7 @@ def test_scale_fill_sumsq(gpu_ext):
 
 COMBOS = [
     (torch.float32, torch.float32, torch.float32, False),
+    (torch.float32, torch.bfloat16, torch.float32, False),  # fp32 parameters, bf16 gradients
     (torch.bfloat16, torch.bfloat16, torch.bfloat16, False),
     (torch.bfloat16, torch.bfloat16, torch.float32, True),
     (torch.bfloat16, torch.float32, torch.float32, True),
