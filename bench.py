@@ -305,10 +305,13 @@ def main():
     iters.clear()
     FluxMPI.barrier()
     torch.cuda.synchronize()
+    from fluxmpi_amd.models import deq as _deq_mod
+    wait0 = _deq_mod.HOST_WAIT_S
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
     t_host = time.perf_counter() - t0  # the host's enqueue time: ~wall when launch-bound
+    t_wait = _deq_mod.HOST_WAIT_S - wait0  # DEQ: blocked on the solvers' convergence flags
     timed_iters = list(iters[:args.steps])
     torch.cuda.synchronize()
     FluxMPI.barrier()
@@ -354,6 +357,11 @@ def main():
                        "kernel_choices": ("shipped" if use_choices else "measured")
                        + ("+rank0-calibrated" if calibrated else ""),
                        "host_ms_per_step": round(1000 * t_host / args.steps, 3),
+                       # DEQ: the host's time net of its waits on the solvers' convergence flags
+                       # (those waits are the data-dependent control flow, not host work)
+                       **({"host_flag_wait_ms_per_step": round(1000 * t_wait / args.steps, 3),
+                           "host_busy_ms_per_step": round(1000 * (t_host - t_wait) / args.steps, 3)}
+                          if t_wait > 0 else {}),
                        "loss": round(lval, 4), "loss_finite": math.isfinite(lval),
                        # what the data-parallel layer actually did: at N=1 nothing is communicated
                        # (overlap false, comm "none") unless --force-comm

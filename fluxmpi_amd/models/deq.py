@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import contextlib
 import os
+import time
 
 import torch
 import torch.nn as nn
@@ -41,6 +42,12 @@ GRAPHS = os.environ.get("FLUXMPI_DEQ_GRAPH", "1") != "0"
 GRAPH_CHUNK = int(os.environ.get("FLUXMPI_DEQ_GRAPH_CHUNK", "5"))
 
 
+# host seconds spent blocked on convergence flags (LaggedFlags.pop_ready), cumulative: bench.py
+# reports the solver's host time net of these waits (a data-dependent solve must wait for its
+# flags; what matters is whether the host's own work keeps up with the GPU)
+HOST_WAIT_S = 0.0
+
+
 class LaggedFlags:
     """Scalars produced on the device, read on the host ``lag`` pushes later without a sync
     of the whole queue: each value goes to pinned memory by an async copy with an event."""
@@ -60,8 +67,11 @@ class LaggedFlags:
         """``(i, value)`` of the push made ``lag`` pushes ago (blocks on its event only), else None."""
         if len(self.pending) <= (self.lag if lag is None else lag):
             return None
+        global HOST_WAIT_S
         i, ev = self.pending.pop(0)
+        t0 = time.perf_counter()
         ev.synchronize()
+        HOST_WAIT_S += time.perf_counter() - t0
         return i, float(self.buf[i])
 
 
