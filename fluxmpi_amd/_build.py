@@ -64,6 +64,12 @@ def _obj_for(src: str) -> str:
     return os.path.join(BUILD, rel + ".o")
 
 
+# per-file extra flags. gemm_nt.hip: no SLP vectorisation — plain -O3 packs adjacent f32 epilogue
+# math into v_pk_*_f32 (4028 of them), an anti-lever beside MFMAs (MI355X_MICROARCH.md price
+# list), and without it every variant compiles spill-free
+EXTRA_FLAGS = {"gemm_nt.hip": ["-fno-slp-vectorize"]}
+
+
 def _compile_cmd(src: str, obj: str) -> list[str]:
     import pybind11
 
@@ -71,7 +77,7 @@ def _compile_cmd(src: str, obj: str) -> list[str]:
               "-Wno-unused-variable", "-Wno-unused-but-set-variable"]
     if src.endswith(".hip"):
         return [_tool("hipcc"), f"--offload-arch={ARCH}", "-c", src, "-o", obj, *common,
-                "-munsafe-fp-atomics"]
+                "-munsafe-fp-atomics", *EXTRA_FLAGS.get(os.path.basename(src), [])]
     inc = [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}", f"-I{ROCM}/include"]
     return [_tool("amdclang++"), "-D__HIP_PLATFORM_AMD__=1", "-c", src, "-o", obj, *common, *inc,
             "-fvisibility=hidden"]

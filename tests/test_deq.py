@@ -625,3 +625,61 @@ def worker_deq_cifar_functional():
 
 def test_deq_cifar_functional_gloo(spmd):
     spmd("tests.test_deq:worker_deq_cifar_functional", nprocs=2, timeout=300)
+
+
+def worker_functional_bf16_masters():
+    """bench.py's functional step on bf16 parameters: Optimisers.update! runs on fp32 copies (a
+    BFloat16 beta2 rounds to 1 and would make Adam 0/0) and the bf16 parameters are refreshed
+    from them; both ranks end identical and equal to fp32 Adam on the averaged bf16 gradients."""
+    import importlib.util
+    import os
+
+    import fluxmpi_amd as FluxMPI
+    from fluxmpi_amd import optimisers as O
+
+    FluxMPI.Init()
+    r, W = FluxMPI.local_rank(), FluxMPI.total_workers()
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(os.path.dirname(__file__), "..", "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+
+    def model():
+        torch.manual_seed(4)
+        return torch.nn.Sequential(torch.nn.Linear(6, 5), torch.nn.Tanh(), torch.nn.Linear(5, 3)).bfloat16()
+
+    def data(k):
+        g = torch.Generator().manual_seed(70 + k)
+        return torch.randn(4, 6, generator=g).bfloat16()
+
+    m = model()
+    f = bench.Functional(FluxMPI, O, m, O.Adam(1e-2))
+    assert len(f.low) == 4  # every bf16 leaf has an fp32 copy
+    for _ in range(2):
+        m(data(r)).float().pow(2).mean().backward()
+        f.step()
+    # reference: fp32 masters, Adam on the mean of both ranks' bf16 gradients
+    ref = model()
+    ps = {n: p.detach().float().clone() for n, p in ref.named_parameters()}
+    st = O.setup(O.Adam(1e-2), ps)
+    for _ in range(2):
+        gs = {}
+        for k in range(W):
+            ref.zero_grad()
+            ref(data(k)).float().pow(2).mean().backward()
+            for n, p in ref.named_parameters():
+                gs[n] = gs.get(n, 0) + p.grad.float() / W
+        gs = {n: g.bfloat16() for n, g in gs.items()}  # the bf16 gradient the allreduce delivers
+        st, ps = O.update(st, ps, gs)
+        with torch.no_grad():
+            for n, p in ref.named_parameters():
+                p.copy_(ps[n])
+    for (n, p), q in zip(m.named_parameters(), ref.parameters()):
+        assert p.dtype == torch.bfloat16 and torch.isfinite(p.float()).all(), n
+        torch.testing.assert_close(p.float(), q.float(), rtol=2e-2, atol=2e-2, msg=n)
+        g = FluxMPI.allgather(p.detach().float().clone())
+        assert torch.equal(g[0], g[1]), n
+    FluxMPI.Finalize()
+
+
+def test_functional_bf16_masters_gloo(spmd):
+    spmd("tests.test_deq:worker_functional_bf16_masters", nprocs=2, timeout=300)
