@@ -229,8 +229,8 @@ void wgrad256_set_variant(int v);  // main-loop variant (A/B runs; 3 hoisted add
 void gemm_wgrad256(const void* a, const void* b, float* ws, int64_t lda, int64_t ldb, int64_t M, int64_t N, int64_t K,
                    int splits, hipStream_t stream);
 // Token-major Linear GEMM, both operands k-contiguous (gemm_nt.hip): C[M][N] = A[M][K] B[N][K]^T,
-// 256 x 256 tiles, ping-pong 8-wave schedule; epi 0 (+ bias), 1 (+ bias, C = h, C2 = gelu(h)),
-// 2 (C = bf16(acc) * gelu'(h), colpart[2 * M / 256][N] = per-half-tile column sums of C),
+// 256 x 256 tiles, ping-pong 8-wave schedule; epi 0 (+ bias), 1 (+ bias: C = gelu'(h), C2 = gelu(h)),
+// 2 (C = bf16(acc) * D, D = gelu'(h) as epi 1 stored it; colpart[2 * M / 256][N] = per-half-tile column sums of C),
 // 3 (C, and its per-column sum / sum of squares added into the BatchNorm shards stats[64][2][N]).
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc);
 bool gemm_nt_conv_supported(int64_t pixels, int64_t C, int64_t Cout);

@@ -8,8 +8,9 @@
 //
 // Epilogues (the registers of the accumulator, no extra pass):
 //   EPI 0: C = acc (+ bias)                                 -> bf16
-//   EPI 1: h = bf16(acc + bias) -> C, g = gelu(h) -> C2     (fc1 forward, tanh or erf GELU)
-//   EPI 2: dh = bf16(acc) * gelu'(H[m][n]) -> C, and the column sums of dh over the wave's 128
+//   EPI 1: h = bf16(acc + bias): gelu'(h) -> C, gelu(h) -> C2 (fc1 forward, tanh or erf GELU;
+//          the derivative is what the backward needs, so no GELU math is left for it)
+//   EPI 2: dh = bf16(acc) * D[m][n] (D = EPI 1's gelu'(h)) -> C, and the column sums of dh over the wave's 128
 //          rows -> colpart[2 * tile_m + wave_m][n] (fp32; fc1's bias gradient after one reduce)
 //
 // Main loop (reference: /root/reference has no kernels — this is the compute under
@@ -73,7 +74,7 @@ struct NTArgs {
   bf16* c;             // [M][ldc]
   bf16* c2;            // EPI 1: GELU output [M][ldc]
   const void* bias;    // [N] fp32 / bf16 (bias_f32), or nullptr
-  const bf16* h;       // EPI 2: GELU input [M][ldc]
+  const bf16* h;       // EPI 2: the GELU derivative gelu'(h) [M][ldc] (EPI 1's C)
   float* colpart;      // EPI 2: [2 * tiles_m][N]
   float* stats;        // EPI 3: BatchNorm statistics shards [kShards][2][N] (sum, sum of squares)
   int64_t lda, ldb, ldc;
@@ -414,7 +415,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
     const int vo = (wr * 128 + fr_e) * ldcb + colx * 2;
     auto rowblk = [&](int ph, int ii) { return __builtin_amdgcn_readfirstlane((32 * ph + 16 * ii) * ldcb); };
     const __amdgpu_buffer_rsrc_t crs = tile_rsrc(p.c);
-    i32x4 hv[4][2][2];  // EPI 2: every GELU input of the tile's lane issued before the first use (one round trip)
+    i32x4 hv[4][2][2];  // EPI 2: every GELU derivative of the tile's lane issued before the first use (one round trip)
     if (EPI == 2) {
       const __amdgpu_buffer_rsrc_t hrs = tile_rsrc(p.h);
 #pragma unroll
@@ -454,37 +455,36 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
               cq2[q][e] = fmaf(f, f, cq2[q][e]);
             }
           } else if (EPI == 1) {
-            bf16 gg[8];
+            // h = the bf16 pre-activation (as F.gelu(F.linear(...)) sees it): g = gelu(h) -> C2 and
+            // its derivative gelu'(h) -> C (what the backward multiplies by; the pre-activation
+            // itself is not needed again), both from one tanh / erf evaluation
+            bf16 gg[8], dd[8];
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-              const float x = static_cast<float>(v8[e]);  // GELU of the bf16 pre-activation, as F.gelu(h)
+              const float x = static_cast<float>(v8[e]);
               if constexpr (GF == 1) {
-                gg[e] = static_cast<bf16>(gelu_tanh(x));
+                constexpr float kK0 = 0.79788456080286536f, kK3 = 3.f * 0.044715f;
+                const float t = gelu_tanh_t(x), hx = 0.5f * x;
+                gg[e] = static_cast<bf16>(fmaf(hx, t, hx));
+                dd[e] = static_cast<bf16>(fmaf(hx * fmaf(-t, t, 1.f), kK0 * fmaf(kK3 * x, x, 1.f), fmaf(0.5f, t, 0.5f)));
               } else {
                 float cdf, ee;
                 gelu_parts(x, cdf, ee);
                 gg[e] = static_cast<bf16>(x * cdf);
+                dd[e] = static_cast<bf16>(fmaf(x * 0.39894228040143268f, ee, cdf));
               }
             }
             i32x4 gv;
             __builtin_memcpy(&gv, gg, 16);
             __builtin_amdgcn_raw_buffer_store_b128(gv, tile_rsrc(p.c2), vo + 64 * q, rowblk(ph, ii), 0);
+            __builtin_memcpy(&out, dd, 16);
           } else if (EPI == 2) {
-            bf16 hh[8], oo[8];
-            __builtin_memcpy(hh, &hv[ph][ii][q], 16);
+            // dh = bf16(dg) * gelu'(h), the derivative read as the forward epilogue (EPI 1) stored it
+            bf16 dd[8], oo[8];
+            __builtin_memcpy(dd, &hv[ph][ii][q], 16);
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-              const float dg = static_cast<float>(v8[e]);  // the bf16 dg autograd sees
-              const float x = static_cast<float>(hh[e]);
-              float d;
-              if constexpr (GF == 1) {
-                d = gelu_tanh_grad(x);
-              } else {
-                float cdf, ee;
-                gelu_parts(x, cdf, ee);
-                d = fmaf(x * 0.39894228040143268f, ee, cdf);
-              }
-              oo[e] = static_cast<bf16>(dg * d);
+              oo[e] = static_cast<bf16>(static_cast<float>(v8[e]) * static_cast<float>(dd[e]));
               cs[q][e] += static_cast<float>(oo[e]);  // the bias gradient of the rounded dh
             }
             __builtin_memcpy(&out, oo, 16);
@@ -581,7 +581,7 @@ int grid_of(const NTArgs& p) {
 
 template <int EPI, int BIAS, bool CONV = false>
 void launch(const NTArgs& p, hipStream_t stream) {
-  if constexpr (EPI == 1 || EPI == 2) {  // the GELU form is compiled in (its constants would stay live otherwise)
+  if constexpr (EPI == 1) {  // the GELU form is compiled in (its constants would stay live otherwise)
     if (p.gelu_tanh) gemm_nt_kernel<EPI, BIAS, CONV, 1><<<grid_of(p), kThreads, 0, stream>>>(p);
     else gemm_nt_kernel<EPI, BIAS, CONV, 0><<<grid_of(p), kThreads, 0, stream>>>(p);
   } else {

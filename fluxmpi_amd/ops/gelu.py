@@ -110,13 +110,17 @@ class GeluLink:
     (fc2, inside ``linear_add_layer_norm``): the consumer's input-gradient GEMM applies the
     GELU derivative and reduces fc1's bias gradient in its epilogue (gemm_nt.hip EPI 2) and
     deposits ``(dh, db)`` here; fc1's backward then skips its own GELU pass. The gradient
-    autograd passes between the two nodes is a zero-stride placeholder (never read). ``bias``:
-    fc1's bias parameter (its gradient's DDP bucket slice, ``ops/graddst.py``)."""
+    autograd passes between the two nodes is a zero-stride placeholder (never read). ``h``: what
+    fc1's forward saved — ``gelu'(pre-activation)`` when its GEMM epilogue produced it
+    (``deriv`` True, gemm_nt.hip EPI 1; the only form the consumer's EPI 2 takes), else the
+    pre-activation. ``bias``: fc1's bias parameter (its gradient's DDP bucket slice,
+    ``ops/graddst.py``)."""
 
-    __slots__ = ("h", "bias_dtype", "bias", "dh", "db")
+    __slots__ = ("h", "deriv", "bias_dtype", "bias", "dh", "db")
 
     def __init__(self):
         self.h = self.bias_dtype = self.bias = self.dh = self.db = None
+        self.deriv = False
 
     def take(self):
         out = (self.dh, self.db)
@@ -131,28 +135,39 @@ class _LinearGeluFn(torch.autograd.Function):
         _sync(_ext.get(required=True))  # the backward kernels (gelu.hip, gemm_nt EPI 2) read the form
         n_out, n_in = weight.shape
         rows = x.numel() // n_in
-        if x.is_contiguous() and gemm_nt.supported(rows, n_out, n_in, x, weight, fused="fwd"):
-            # bias + GELU in the GEMM epilogue: h and gelu(h) from the same registers
-            h2, g2 = gemm_nt.linear_fwd(x.view(rows, n_in), weight, bias, gelu=True)
-            h, g = h2.view(*x.shape[:-1], n_out), g2.view(*x.shape[:-1], n_out)
+        deriv = x.is_contiguous() and gemm_nt.supported(rows, n_out, n_in, x, weight, fused="fwd")
+        if deriv:
+            # bias + GELU in the GEMM epilogue: gelu(h) and gelu'(h) from the same registers; the
+            # derivative (not h) is what the backward needs, so it is what is saved
+            d2, g2 = gemm_nt.linear_fwd(x.view(rows, n_in), weight, bias, gelu=True)
+            h, g = d2.view(*x.shape[:-1], n_out), g2.view(*x.shape[:-1], n_out)
         else:
             h = F.linear(x, weight, bias)
             g = _gelu_fwd(h)
         ctx.save_for_backward(x, weight, h)
+        ctx.deriv = deriv
         ctx.weight = weight  # the leaf itself: its gradient's bucket slice (ops/graddst.py)
         ctx.has_bias = bias is not None
         ctx.bias_dtype = bias.dtype if bias is not None else None
         ctx.bias = bias  # the leaf: its gradient's bucket slice
         ctx.link = link
         if link is not None:
-            link.h, link.bias_dtype, link.bias = h, ctx.bias_dtype or torch.float32, bias
+            link.h, link.deriv, link.bias_dtype, link.bias = h, deriv, ctx.bias_dtype or torch.float32, bias
         return g
 
     @staticmethod
     def backward(ctx, dy):
         x, w, h = ctx.saved_tensors
         dh, db = ctx.link.take() if ctx.link is not None else (None, None)
-        if dh is None:  # the consumer did not fuse the GELU derivative: own pass
+        if dh is None and ctx.deriv:  # unfused consumer, saved derivative: dh = dy * gelu'(h)
+            dh = (dy.float() * h.float()).to(h.dtype)
+            db = None
+            if ctx.has_bias and ctx.needs_input_grad[2]:
+                from . import graddst
+                from .linear import bias_grad
+                with graddst.into(ctx.bias):
+                    db = bias_grad(dh.reshape(-1, h.shape[-1]), ctx.bias_dtype)
+        elif dh is None:  # the consumer did not fuse the GELU derivative: own pass
             dh, db = gelu_bwd_bias(dy, h, ctx.bias_dtype or torch.float32, bias_param=ctx.bias)
         else:
             dh = dh.view(h.shape)

@@ -1,25 +1,27 @@
 """Token-major Linear GEMMs on the ping-pong 256x256 NT kernel (``csrc/kernels/gemm_nt.hip``).
 
-* :func:`linear_fwd` — ``y = x W^T + b`` (``gelu=True``: also ``g = gelu(y)`` from the same
-  registers: fc1 of a transformer MLP writes its pre-activation and its activation in one pass,
-  no elementwise GELU kernel);
+* :func:`linear_fwd` — ``y = x W^T + b`` (``gelu=True``: ``gelu(y)`` and ``gelu'(y)`` instead,
+  from the same registers: fc1 of a transformer MLP writes its activation and the derivative
+  its backward needs in one pass, no elementwise GELU kernel);
 * :func:`linear_dgrad` — ``dx = dy W`` on ``W^T`` (one ``transpose_bf16`` of the 0.6-4.7 MB
-  weight per call, so both operands of the GEMM stay k-contiguous); ``gelu_h=h``: ``dh = dx *
-  gelu'(h)`` and the column sums of ``dh`` — the previous Linear's bias gradient, written into
-  its DDP bucket slice when one is attached (``ops/graddst.py``) — in the epilogue.
+  weight per call, so both operands of the GEMM stay k-contiguous); ``gelu_d=gelu'(h)``:
+  ``dh = dx * gelu'(h)`` and the column sums of ``dh`` — the previous Linear's bias gradient,
+  written into its DDP bucket slice when one is attached (``ops/graddst.py``) — in the epilogue.
 
 The ViT-B/16 Linears at batch 256 (M = 50432 = 197 x 256 tokens, N and K in {768, 2304, 3072})
 tile exactly; :func:`supported` says whether a call qualifies, callers keep the PyTorch path
 otherwise. Numerics: bf16 operands, fp32 accumulation, one bf16 rounding of each output (the
-GELU of the ROUNDED pre-activation, like ``F.gelu(F.linear(...))``).
+GELU of the ROUNDED pre-activation, like ``F.gelu(F.linear(...))``); the saved derivative is
+bf16 too, so ``dh`` carries one extra bf16 rounding of ``gelu'(h)`` compared with autograd's
+fp32 derivative (relative error <= 2^-9 per element, below the output's own rounding).
 
 ``FLUXMPI_GEMM_NT``: ``fused`` (default) the calls that carry an epilogue fusion — fc1's bias +
-GELU forward (EPI 1: 318 us vs 336 for hipBLASLt + the GELU kernel) and fc2's input gradient
-with fc1's GELU backward + bias-gradient partials (EPI 2: 364 vs 435 us for hipBLASLt + the
-GELU-backward kernel); ``dgrad`` only the latter; ``all`` also every plain forward / input
-gradient (at parity with hipBLASLt on qkv / proj, 1-5 % behind on the K = 3072 / N = 3072
-ones); ``0`` never. Measured: profiles/rd4i_bench_gemm_nt.jsonl (the hipBLASLt columns are the
-roofline baseline per shape); whole ViT-B/16 step 7.30k (fused) / 7.32k (dgrad) img/s.
+GELU forward (EPI 1: gelu(h) and gelu'(h) from one tanh evaluation; the derivative replaces the
+pre-activation as what the backward saves) and fc2's input gradient times that derivative +
+fc1's bias-gradient partials (EPI 2: no GELU math left in the backward); ``all`` also every
+plain forward / input gradient (at parity with hipBLASLt on qkv / proj, 1-5 % behind on the
+K = 3072 / N = 3072 ones); ``0`` never. Measured: profiles/rd4i_bench_gemm_nt.jsonl (the hipBLASLt
+columns are the roofline baseline per shape).
 
 Convolutions (ops/gemm.py routes here, ``FLUXMPI_GEMM_NT_CONV``, default on): the stride-1 3x3
 forward / input gradient and the 1x1 forward / input gradient when the output has >= 160 tiles
@@ -48,13 +50,13 @@ def _stream(t):
 def supported(rows: int, n_out: int, k: int, *tensors: torch.Tensor, fused: bool | str = False) -> bool:
     """Whether gemm_nt takes ``[rows, k] x [n_out, k]^T`` (both operands k-contiguous after the
     weight transpose of an input gradient) under the current mode. ``fused``: the call carries an
-    epilogue fusion — ``"fwd"`` (fc1 bias + GELU: modes fused / all), ``"dgrad"`` (GELU backward:
-    modes dgrad / fused / all), ``True`` (either: shape checks of the kernel itself)."""
+    epilogue fusion — ``"fwd"`` (fc1 bias + GELU) or ``"dgrad"`` (GELU backward), taken in modes
+    fused / all (the pair works together: the backward multiplies by the derivative the forward
+    stored), ``True`` (either: shape checks of the kernel itself)."""
     if not ENABLED or not tensors or not tensors[0].is_cuda:
         return False
     if MODE not in ("all", "1"):
-        ok = (fused is True or (fused == "fwd" and MODE == "fused")
-              or (fused == "dgrad" and MODE in ("fused", "dgrad")))
+        ok = fused is True or (fused in ("fwd", "dgrad") and MODE in ("fused", "dgrad"))
         if not ok:
             return False
     if any(t.dtype != torch.bfloat16 for t in tensors):
@@ -74,7 +76,9 @@ def weight_t(weight: torch.Tensor) -> torch.Tensor:
 
 
 def linear_fwd(x2: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None, gelu: bool = False):
-    """``x2 [M, K] @ weight[N, K]^T + bias`` -> ``y [M, N]`` (bf16); ``gelu``: ``(y, gelu(y))``."""
+    """``x2 [M, K] @ weight[N, K]^T + bias`` -> ``y [M, N]`` (bf16); ``gelu``: ``(gelu'(y), gelu(y))``
+    — the derivative is what the backward multiplies by (:func:`linear_dgrad`'s ``gelu_d``), so
+    the pre-activation ``y`` itself is never written."""
     C = _ext.get(required=True)
     m, k = x2.shape
     n = weight.shape[0]
@@ -93,11 +97,12 @@ def linear_fwd(x2: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None
     return (y, g) if gelu else y
 
 
-def linear_dgrad(dy2: torch.Tensor, weight: torch.Tensor, gelu_h: torch.Tensor | None = None,
+def linear_dgrad(dy2: torch.Tensor, weight: torch.Tensor, gelu_d: torch.Tensor | None = None,
                  bias_dtype=torch.float32, bias_param: torch.Tensor | None = None):
-    """``dy2 [M, N] @ weight [N, K]`` -> ``dx [M, K]``. With ``gelu_h`` (the GELU input that
-    produced this Linear's input, ``[M, K]``): returns ``(dh, db)`` with ``dh = dx * gelu'(h)``
-    and ``db = dh.sum(0)`` in ``bias_dtype`` (delivered into ``bias_param``'s bucket slice)."""
+    """``dy2 [M, N] @ weight [N, K]`` -> ``dx [M, K]``. With ``gelu_d`` (``gelu'(h)`` of the GELU
+    that produced this Linear's input, ``[M, K]``, as :func:`linear_fwd` stored it): returns
+    ``(dh, db)`` with ``dh = bf16(dx) * gelu'(h)`` and ``db = dh.sum(0)`` in ``bias_dtype``
+    (delivered into ``bias_param``'s bucket slice)."""
     C = _ext.get(required=True)
     m, n = dy2.shape
     k = weight.shape[1]
@@ -105,12 +110,10 @@ def linear_dgrad(dy2: torch.Tensor, weight: torch.Tensor, gelu_h: torch.Tensor |
     wt = weight_t(weight)  # [K][N]: the B operand, k(= N)-contiguous
     dx = torch.empty(m, k, device=dy2.device, dtype=dy2.dtype)
     s = _stream(dy2)
-    if gelu_h is None:
+    if gelu_d is None:
         C.gemm_nt(dy2.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, 0, 0, 0, 0, n, n, k, m, k, n, 0, s)
         return dx
-    from .gelu import _sync
-    _sync(C)  # EPI 2 differentiates the selected GELU form
-    h = gelu_h.reshape(m, k).contiguous()
+    h = gelu_d.reshape(m, k).contiguous()
     rows = C.gemm_nt_colpart_rows(m)
     part = torch.empty(rows, k, device=dy2.device, dtype=torch.float32)
     C.gemm_nt(dy2.data_ptr(), wt.data_ptr(), dx.data_ptr(), 0, 0, 0, h.data_ptr(), part.data_ptr(),

@@ -193,11 +193,11 @@ class _LinearAddLayerNormFn(torch.autograd.Function):
             from . import gemm_nt
             from .linear import dgrad
             link = ctx.gelu_link
-            if (link is not None and link.h is not None and link.h.shape == a.shape
+            if (link is not None and link.h is not None and link.deriv and link.h.shape == a.shape
                     and gemm_nt.supported(g2.shape[0], n_in, n_out, g2, weight, link.h, fused="dgrad")):
                 # `a` = gelu(h) of the linear_gelu node upstream: its GELU derivative and its bias
                 # gradient come out of this input-gradient GEMM's epilogue (gemm_nt.hip EPI 2)
-                link.dh, link.db = gemm_nt.linear_dgrad(g2, weight, gelu_h=link.h, bias_dtype=link.bias_dtype,
+                link.dh, link.db = gemm_nt.linear_dgrad(g2, weight, gelu_d=link.h, bias_dtype=link.bias_dtype,
                                                         bias_param=link.bias)
                 da = torch.zeros((), device=a.device, dtype=a.dtype).expand(a.shape)  # placeholder, never read
             else:

@@ -98,20 +98,23 @@ def main():
         check(f"{name}_epi0", c, ref)
         ours(0, bias_=bias)
         check(f"{name}_epi0_bias", c, ref + bias)
+        def dgelu(hf):
+            t = torch.tanh(0.7978845608 * (hf + 0.044715 * hf ** 3))
+            return 0.5 * (1 + t) + 0.5 * hf * (1 - t * t) * 0.7978845608 * (1 + 3 * 0.044715 * hf * hf)
+
         ours(1, bias_=bias)
         hb = (ref + bias).bfloat16()
-        check(f"{name}_epi1_h", c, ref + bias)
+        check(f"{name}_epi1_dgelu", c, dgelu(hb.float()))  # EPI 1 stores gelu'(h), not h
         check(f"{name}_epi1_g", c2, torch.nn.functional.gelu(hb.float(), approximate="tanh"))
         h = uni(m, n)
+        dgel = dgelu(h.float())
+        h = dgel.bfloat16()  # EPI 2 reads the derivative as EPI 1 stored it
         part = torch.empty(C.gemm_nt_colpart_rows(m), n, device="cuda", dtype=torch.float32)
         ours(2, h=h, part=part)
-        hf = h.float()
-        t = torch.tanh(0.7978845608 * (hf + 0.044715 * hf ** 3))
-        dgel = 0.5 * (1 + t) + 0.5 * hf * (1 - t * t) * 0.7978845608 * (1 + 3 * 0.044715 * hf * hf)
         dh_ref = ref.bfloat16().float() * dgel
         check(f"{name}_epi2_dh", c, dh_ref)
         check(f"{name}_epi2_db", part.sum(0), dh_ref.sum(0), tol=5e-2)
-        del ref, dh_ref, hf, t, dgel
+        del ref, dh_ref, dgel
 
         best: dict = {}
         wt = w.t().contiguous()  # the [K][N] layout hipBLASLt's dgrad form reads (dy @ W)

@@ -48,9 +48,9 @@ def _check_fwd(m, n, k, bias, gelu_form=None):
     ref = x.float() @ w.float().t() + (b.float() if b is not None else 0)
     assert _rel(y, ref) < 5e-3
     if gelu_form is not None:
-        yy, g = G.linear_fwd(x, w, b, gelu=True)
-        assert torch.equal(yy, y)
+        d, g = G.linear_fwd(x, w, b, gelu=True)
         assert _rel(g, GL.gelu(y.float())) < 5e-3  # GELU of the rounded pre-activation
+        assert _rel(d, GL._gelu_grad_ref(y.float())) < 5e-3  # and its derivative
 
 
 def _check_dgrad(m, n_out, n_in, gelu_form=None):
@@ -65,11 +65,12 @@ def _check_dgrad(m, n_out, n_in, gelu_form=None):
     assert _rel(dx, ref) < 5e-3
     if gelu_form is not None:
         h = _uni(m, n_in, scale=3.0)
-        dh, db = G.linear_dgrad(dy, w, gelu_h=h)
+        d = GL._gelu_grad_ref(h.float()).bfloat16()  # the derivative as EPI 1 stores it
+        dh, db = G.linear_dgrad(dy, w, gelu_d=d)
         dh_ref = ref.bfloat16().float() * GL._gelu_grad_ref(h.float())
         assert _rel(dh, dh_ref) < 5e-3
         torch.testing.assert_close(db, dh.float().sum(0), rtol=1e-3, atol=2e-2)
-        _, db16 = G.linear_dgrad(dy, w, gelu_h=h, bias_dtype=torch.bfloat16)
+        _, db16 = G.linear_dgrad(dy, w, gelu_d=d, bias_dtype=torch.bfloat16)
         assert db16.dtype == torch.bfloat16 and _rel(db16, db) < 1e-2
 
 
