@@ -64,10 +64,12 @@ def _obj_for(src: str) -> str:
     return os.path.join(BUILD, rel + ".o")
 
 
-# per-file extra flags. gemm_nt.hip: no SLP vectorisation — plain -O3 packs adjacent f32 epilogue
-# math into v_pk_*_f32 (4028 of them), an anti-lever beside MFMAs (MI355X_MICROARCH.md price
-# list), and without it every variant compiles spill-free
-EXTRA_FLAGS = {"gemm_nt.hip": ["-fno-slp-vectorize"]}
+# per-file extra flags: no SLP vectorisation in the MFMA kernels — plain -O3 packs adjacent f32
+# math (epilogues, softmax, operand prologues) into v_pk_*_f32, an anti-lever beside MFMAs
+# (MI355X_MICROARCH.md price list); in gemm_nt.hip that build also produced NaNs in the GELU
+# derivative epilogue. The memory-bound elementwise kernels keep it (fewer instructions).
+_NO_SLP = ["-fno-slp-vectorize"]
+EXTRA_FLAGS = {f: _NO_SLP for f in ("gemm_nt.hip", "attention.hip", "gemm_glds.hip", "gemm.hip")}
 
 
 def _compile_cmd(src: str, obj: str) -> list[str]:
