@@ -169,7 +169,8 @@ def conv3x3_fwd(x: torch.Tensor, w: torch.Tensor, in_affine=None, stats: torch.T
     ``in_affine=(scale, shift)``: relu(x * scale + shift) per input channel applied on load (the
     previous BatchNorm + ReLU; the zero padding stays zero). ``stats``: per-output-channel
     sum / sumsq into the sharded BatchNorm workspace. ``engine``: force a tile configuration of the
-    LDS-DMA kernel (7 / 8: 256x128 tiles; see gemm_glds.hip), e.g. the one an autotune picked.
+    LDS-DMA kernel (7 / 8: 256x128 tiles; see gemm_glds.hip), e.g. the one an autotune picked;
+    ``None`` / 0: automatic — the 256x256 persistent kernel (``gemm_nt``) where the shape qualifies.
     """
     n, c, h, wd = x.shape
     co = w.shape[0]
@@ -178,7 +179,7 @@ def conv3x3_fwd(x: torch.Tensor, w: torch.Tensor, in_affine=None, stats: torch.T
     note_filter(w)
     y = out if out is not None else torch.empty(n, h, wd, co, device=x.device, dtype=x.dtype).permute(0, 3, 1, 2)
     M = n * h * wd
-    if (in_affine is None and engine is None and y.is_contiguous(memory_format=torch.channels_last)
+    if (in_affine is None and not engine and y.is_contiguous(memory_format=torch.channels_last)
             and _NT.conv_ok(M, c, co, xs, w2)):
         return _NT.conv3x3(xs, w2.view(co, 9 * c), y, stats)  # 256x256 persistent implicit GEMM
     gemm(xs, w2, y, M=M, N=co, K=9 * c, lda=c, ldb=9 * c, ldc=co, mode=1 if stats is not None else 0,
