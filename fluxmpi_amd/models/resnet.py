@@ -176,6 +176,7 @@ class Bottleneck(nn.Module):
                         identity = ds[1](identity)
                 else:
                     identity = self.downsample(x)
+                fold = False
                 if self.hybrid:
                     bl2 = fb.BNStatsLink() if bnl else None  # bn2 -> conv3 (its only consumer)
                     if fb.conv3x3_supported(a1, self.conv2):
@@ -183,7 +184,11 @@ class Bottleneck(nn.Module):
                         # then bn2's statistics come from its epilogue)
                         ours = fb.conv3x3_forward_is_ours(a1, self.conv2.weight)
                         c2 = fb.conv3x3(a1, self.conv2.weight, with_stats=True, bnlink=bl1)
-                        a2 = fb.bn_from_stats(c2, self.bn2, relu=True, stats_ready=ours, bnlink=bl2)
+                        fold = bl2 is None and fb.bn2_fold_ok(c2, self.bn2, self.conv3.weight)
+                        if fold:  # bn2 + ReLU in conv3's A load; c3's sums pending from its epilogue
+                            c3, o3 = fb.bn_relu_conv1x1(c2, self.bn2, self.conv3.weight, stats_ready=ours), True
+                        else:
+                            a2 = fb.bn_from_stats(c2, self.bn2, relu=True, stats_ready=ours, bnlink=bl2)
                     elif fb.conv3x3_s2_supported(a1, self.conv2):
                         # stride-2 conv2: forward where measured faster on our implicit GEMM (+ bn2's
                         # sums from its epilogue), weight gradient autotuned (fused_block._Conv3x3S2)
@@ -192,8 +197,9 @@ class Bottleneck(nn.Module):
                         a2 = fb.bn_from_stats(c2, self.bn2, relu=True, stats_ready=ours, bnlink=bl2)
                     else:
                         a2 = self.bn2(self.conv2(a1), relu=True, bnlink=bl2)
-                    o3 = fb.conv1x1_forward_is_ours(a2, self.conv3.weight)
-                    c3 = fb.conv1x1_hybrid(a2, self.conv3.weight, None, bl2, ours_stats=o3)
+                    if not fold:
+                        o3 = fb.conv1x1_forward_is_ours(a2, self.conv3.weight)
+                        c3 = fb.conv1x1_hybrid(a2, self.conv3.weight, None, bl2, ours_stats=o3)
                 else:
                     c2 = fb.conv3x3(a1, self.conv2.weight) if fb.conv3x3_supported(a1, self.conv2) else self.conv2(a1)
                     c3 = fb.bn_relu_conv1x1(c2, self.bn2, self.conv3.weight)  # bn2+relu fused into the A load

@@ -66,6 +66,9 @@ DS_FWD = os.environ.get("FLUXMPI_DS_FWD", "ours")
 # kernel (stride-2 B-row gather / implicit stride-2 im2col), measured per shape
 # (FLUXMPI_DS_WGRAD=0: always MIOpen)
 DS_WGRAD = os.environ.get("FLUXMPI_DS_WGRAD", "1") == "1"
+# bottleneck bn2 -> conv3: BatchNorm + ReLU applied in conv3's A-operand load (bn_relu_conv1x1: no bn2
+# output pass, bn2's backward reductions in conv3's dgrad epilogue) instead of a bn2 pass + conv3
+BN2_FOLD = os.environ.get("FLUXMPI_BN2_FOLD", "0") == "1"
 # stride-2 3x3 forward: our implicit GEMM (+ statistics epilogue) where measured faster (0: MIOpen)
 S2_FWD = os.environ.get("FLUXMPI_S2_FWD", "1") == "1"
 
@@ -512,7 +515,8 @@ class _BNReluConv1x1(torch.autograd.Function):
     go to the workspace (consumed by the next ``bn_from_stats``)."""
 
     @staticmethod
-    def forward(ctx, c2, bn_weight, bn_bias, running_mean, running_var, weight, momentum, eps, nbt=None):
+    def forward(ctx, c2, bn_weight, bn_bias, running_mean, running_var, weight, momentum, eps, nbt=None,
+                stats_ready=False):
         C = _ext.get(required=True)
         if not c2.is_contiguous(memory_format=torch.channels_last):
             c2 = c2.contiguous(memory_format=torch.channels_last)
@@ -526,12 +530,14 @@ class _BNReluConv1x1(torch.autograd.Function):
         ws = _workspace(c2)
         C.bn_stats_finalize(c2.data_ptr(), w32.data_ptr(), b32.data_ptr(), _p(running_mean), _p(running_var),
                             mean.data_ptr(), inv.data_ptr(), scale.data_ptr(), shift.data_ptr(), ws.data_ptr(),
-                            rows, ch, float(momentum), float(eps), 0, DTYPE_CODE[c2.dtype], _stream(c2), _p(nbt))
+                            rows, ch, float(momentum), float(eps), int(stats_ready), DTYPE_CODE[c2.dtype], _stream(c2),
+                            _p(nbt))
         co = weight.shape[0]
         c3 = _empty_nhwc(n, co, h, w, c2)
         gemm(_nhwc2d(c2), weight.reshape(co, ch), c3, M=rows, N=co, K=ch, lda=ch, ldb=ch, ldc=co, a_kmajor=True,
              b_kmajor=True, mode=1, stats=ws, a_affine=(scale, shift))
         ctx.bn_wdtype = bn_weight.dtype
+        ctx.params = (bn_weight, bn_bias)  # the leaves: their gradients' bucket slices (graddst)
         ctx.save_for_backward(c2, w32, b32, mean, inv, scale, shift, weight)
         return c3
 
@@ -548,10 +554,12 @@ class _BNReluConv1x1(torch.autograd.Function):
             dw = conv1x1_wgrad(dc3_2d, c2_2d, in_affine=(scale, shift), out_dtype=weight.dtype).view_as(weight)
         # d(relu(bn(c2))) = dc3 @ W with the BN-backward reductions (ReLU mask recomputed from c2)
         # accumulated in the same GEMM's epilogue, then the BN backward without its reduce pass
+        # (w4d: the LDS-DMA kernel on the cached W^T, whose epilogue has the BN-backward reductions)
         da = conv1x1_dgrad(dc3_2d, weight.reshape(co, ch), bn_bwd=(c2_2d, w32, b32, mean, inv, None, 2),
-                           stats=_link_workspace(c2)).view(n, h, w, ch).permute(0, 3, 1, 2)
-        dc2, _, dbw, dbb = _bn_bwd(da, c2, None, w32, b32, mean, inv, True, False, stats_ready=True)
-        return dc2, dbw.to(ctx.bn_wdtype), dbb.to(ctx.bn_wdtype), None, None, dw, None, None, None
+                           stats=_link_workspace(c2), w4d=weight).view(n, h, w, ch).permute(0, 3, 1, 2)
+        dc2, _, dbw, dbb = _bn_bwd(da, c2, None, w32, b32, mean, inv, True, False, stats_ready=True,
+                                   params=ctx.params)
+        return dc2, dbw.to(ctx.bn_wdtype), dbb.to(ctx.bn_wdtype), None, None, dw, None, None, None, None
 
 
 class _Conv3x3(torch.autograd.Function):
@@ -921,9 +929,22 @@ def bn_from_stats(x, bn, relu=False, residual=None, stats_ready=True, link=None,
                               stats_ready, link, nbt, bnlink)
 
 
-def bn_relu_conv1x1(c2, bn, weight):
+def bn_relu_conv1x1(c2, bn, weight, stats_ready=False):
+    """conv1x1(relu(bn(c2)), W) with the BatchNorm + ReLU applied in the GEMM's A load (``stats_ready``:
+    c2's sums are pending in the workspace from the GEMM that produced it)."""
     mom, nbt = bn_counter(bn)
-    return _BNReluConv1x1.apply(c2, bn.weight, bn.bias, bn.running_mean, bn.running_var, weight, mom, bn.eps, nbt)
+    return _BNReluConv1x1.apply(c2, bn.weight, bn.bias, bn.running_mean, bn.running_var, weight, mom, bn.eps, nbt,
+                                stats_ready)
+
+
+def bn2_fold_ok(c2, bn, weight) -> bool:
+    """:func:`bn_relu_conv1x1` takes this BatchNorm -> 1x1 pair (``FLUXMPI_BN2_FOLD``): the A-prologue
+    affine holds <= 512 channels, the kernel wants bf16 NHWC with channel counts % 32."""
+    from .batchnorm import FusedBatchNorm2d
+    ch = c2.shape[1]
+    return (BN2_FOLD and G.ENGINE != 1 and c2.is_cuda and c2.dtype == torch.bfloat16 and ch % 32 == 0 and ch <= 512
+            and weight.shape[0] % 32 == 0 and isinstance(bn, FusedBatchNorm2d) and bn.training and bn.affine
+            and bn.track_running_stats)
 
 
 def supported(x: torch.Tensor, *channels: int) -> bool:

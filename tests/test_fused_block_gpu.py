@@ -23,14 +23,16 @@ def _models(impl="fused"):
     return ref, fus
 
 
-@pytest.mark.parametrize("impl", ["fused", "hybrid", "fused+bnlink", "hybrid+bnlink"])
+@pytest.mark.parametrize("impl", ["fused", "hybrid", "fused+bnlink", "hybrid+bnlink", "hybrid+bn2fold"])
 def test_fused_resnet_matches_unfused(gpu_ext, impl, monkeypatch):
     """Both bf16 pipelines are compared with an fp32 model holding the same (bf16-rounded)
     weights: the fused pipeline must be about as accurate as the unfused one. Layer 1 has an
-    identity block, so the GradLink residual-gradient hand-off is exercised."""
+    identity block, so the GradLink residual-gradient hand-off is exercised. ``+bn2fold``: bn2 +
+    ReLU applied in conv3's A load (``FLUXMPI_BN2_FOLD``)."""
     from fluxmpi_amd.models.resnet import ResNet
     from fluxmpi_amd.ops import fused_block as fb
     monkeypatch.setattr(fb, "BN_LINK", impl.endswith("+bnlink"))
+    monkeypatch.setattr(fb, "BN2_FOLD", impl.endswith("+bn2fold"))
     ref, fus = _models(impl.split("+")[0])
     f32 = ResNet((2, 1, 1, 1), 10, conv_impl="miopen", norm="fused").cuda().to(memory_format=torch.channels_last)
     f32.load_state_dict({k: v.float() if v.is_floating_point() else v for k, v in ref.state_dict().items()})
