@@ -1,0 +1,14 @@
+#!/bin/bash
+# rd4v: validation of the current tree as the driver runs it — full GPU suite, smoke(), default bench —
+# plus the DDP-path lines (--force-comm) for ResNet-50 / ViT-B/16 and the DEQ lines
+source "$(dirname "$0")/gpu_lib.sh"
+rm -f "$OUT/steps.log" "$OUT/bench_results.jsonl"
+step gpu_suite 900 0 python -u -m pytest tests/ -x -q -m gpu --timeout 120 --timeout-method thread
+step smoke 300 0 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+step bench_default 600 0 python -u bench.py
+step r50_force_comm 300 0 python -u bench.py --steps 20 --warmup 10 --force-comm
+step vit 300 0 python -u bench.py --model vit_b16 --steps 10 --warmup 5
+step vit_force_comm 300 0 python -u bench.py --model vit_b16 --steps 10 --warmup 5 --force-comm
+step deq 400 0 python -u bench.py --model deq --steps 10 --warmup 5
+step deqc 400 0 python -u bench.py --model deq_cifar --batch 128 --steps 10 --warmup 5 --force-comm
+echo done
