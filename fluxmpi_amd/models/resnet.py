@@ -143,6 +143,7 @@ class Bottleneck(nn.Module):
                 prev = getattr(x, "_fluxmpi_bnlink", None) if (link is not None and self.downsample is None) else None
                 bnl = grad and fb.BN_LINK
                 out_link = fb.BNStatsLink() if bnl else None
+                bnl = bnl and not fb.BN_LINK_BN3_ONLY  # the in-block links (bn1 -> conv2, bn2 -> conv3)
                 bl1 = None
                 if self.hybrid:
                     # bn1 -> conv2 (its only consumer): conv2's dgrad epilogue reduces bn1's backward

@@ -43,8 +43,12 @@ from .multi_tensor import DTYPE_CODE
 # BNStatsLink: off by default. Measured on MI355X (ResNet-50 bs256, hybrid): the epilogue's
 # extra read of the BN input makes the dgrad GEMMs +1.4 ms/step slower while the removed
 # reduce passes save 1.05 ms — a net loss until the GEMM epilogue streams as well as the
-# BN kernels do. FLUXMPI_BN_LINK=1 enables it (numerics covered by tests either way).
-BN_LINK = os.environ.get("FLUXMPI_BN_LINK", "0") == "1"
+# BN kernels do. FLUXMPI_BN_LINK=1 enables it for every link (numerics covered by tests either way);
+# "bn3" only for the previous block's bn3 -> an identity block's conv1 (whose dgrad runs on the
+# LDS-DMA kernel with the residual epilogue anyway: the 3x3 input gradients stay on gemm_nt)
+_BN_LINK_ENV = os.environ.get("FLUXMPI_BN_LINK", "0")
+BN_LINK = _BN_LINK_ENV in ("1", "bn3")
+BN_LINK_BN3_ONLY = _BN_LINK_ENV == "bn3"
 # 3x3 / stride-1 convolutions of the bottlenecks: "ours" = forward (+ the next BatchNorm's
 # statistics in the epilogue) and input gradient on the implicit-GEMM MFMA kernel, weight
 # gradient on MIOpen; "dgrad" = only the input gradient ours; "miopen" = all MIOpen

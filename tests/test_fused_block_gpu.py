@@ -23,7 +23,7 @@ def _models(impl="fused"):
     return ref, fus
 
 
-@pytest.mark.parametrize("impl", ["fused", "hybrid", "fused+bnlink", "hybrid+bnlink", "hybrid+bn2fold"])
+@pytest.mark.parametrize("impl", ["fused", "hybrid", "fused+bnlink", "hybrid+bnlink", "hybrid+bn2fold", "hybrid+bnlink3"])
 def test_fused_resnet_matches_unfused(gpu_ext, impl, monkeypatch):
     """Both bf16 pipelines are compared with an fp32 model holding the same (bf16-rounded)
     weights: the fused pipeline must be about as accurate as the unfused one. Layer 1 has an
@@ -31,7 +31,8 @@ def test_fused_resnet_matches_unfused(gpu_ext, impl, monkeypatch):
     ReLU applied in conv3's A load (``FLUXMPI_BN2_FOLD``)."""
     from fluxmpi_amd.models.resnet import ResNet
     from fluxmpi_amd.ops import fused_block as fb
-    monkeypatch.setattr(fb, "BN_LINK", impl.endswith("+bnlink"))
+    monkeypatch.setattr(fb, "BN_LINK", impl.endswith("+bnlink") or impl.endswith("+bnlink3"))
+    monkeypatch.setattr(fb, "BN_LINK_BN3_ONLY", impl.endswith("+bnlink3"))
     monkeypatch.setattr(fb, "BN2_FOLD", impl.endswith("+bn2fold"))
     ref, fus = _models(impl.split("+")[0])
     f32 = ResNet((2, 1, 1, 1), 10, conv_impl="miopen", norm="fused").cuda().to(memory_format=torch.channels_last)
