@@ -279,7 +279,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_glds_kernel(GldsArgs p) {
   // BN-input / mask loads go out in batches of UB rows
   constexpr int CPR = BN / 8;          // 16-B chunks per row
   constexpr int RPI = kThreads / CPR;  // rows per sweep
-  constexpr int UB = 4;                // rows per batch
+  constexpr int UB = BNB ? 1 : 4;      // rows per batch (BNB: 2 — its x / mask loads would otherwise push the variant to 185 VGPRs, two workgroups per CU instead of three)
   constexpr int NB = (BM + UB * RPI - 1) / (UB * RPI);
   const int cc = threadIdx.x % CPR, r0 = threadIdx.x / CPR;
   const int64_t n = n0 + cc * 8;

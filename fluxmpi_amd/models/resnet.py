@@ -142,7 +142,9 @@ class Bottleneck(nn.Module):
                     link = fb.SideGradLink() if (needs and fused_ds) else None
                 prev = getattr(x, "_fluxmpi_bnlink", None) if (link is not None and self.downsample is None) else None
                 bnl = grad and fb.BN_LINK
-                out_link = fb.BNStatsLink() if bnl else None
+                # bn3-only mode: downsample blocks keep their dual BatchNorm (which hands no link)
+                out_link = fb.BNStatsLink() if (bnl and not (fb.BN_LINK_BN3_ONLY and self.downsample is not None)) \
+                    else None
                 bnl = bnl and not fb.BN_LINK_BN3_ONLY  # the in-block links (bn1 -> conv2, bn2 -> conv3)
                 bl1 = None
                 if self.hybrid:
