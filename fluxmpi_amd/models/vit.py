@@ -159,6 +159,17 @@ class Block(nn.Module):
         return x, (g, self.fc2, link)
 
 
+def cls_pos(x, cls, pos):
+    """``cat([cls, x], 1) + pos`` in one elementwise pass: the patch tokens' sum is written straight
+    into rows 1.. of the token buffer (no concatenated copy followed by a second add pass), the
+    [CLS] row is the broadcast ``cls + pos[0]``; bit-identical to the composition (same bf16 adds)."""
+    b, n, d = x.shape
+    out = torch.empty(b, n + 1, d, device=x.device, dtype=x.dtype)
+    torch.add(x, pos[:, 1:].to(x.dtype), out=out[:, 1:])
+    out[:, 0] = cls[:, 0].to(x.dtype) + pos[:, 0].to(x.dtype)
+    return out
+
+
 class _ClsPos(torch.autograd.Function):
     """``cat([cls, x], 1) + pos``; the backward writes d(cls) and d(pos) — sums over the batch —
     into their DDP bucket slices when a communicating engine is attached (``ops/graddst.py``)."""
@@ -166,7 +177,7 @@ class _ClsPos(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, cls, pos):
         ctx.params = (cls, pos)
-        return torch.cat([cls.expand(x.shape[0], -1, -1).to(x.dtype), x], 1) + pos.to(x.dtype)
+        return cls_pos(x, cls, pos)
 
     @staticmethod
     def backward(ctx, dy):
@@ -206,7 +217,7 @@ class ViT(nn.Module):
         if x.is_cuda and torch.is_grad_enabled():
             x = _ClsPos.apply(x, self.cls, self.pos)
         else:
-            x = torch.cat([self.cls.expand(x.shape[0], -1, -1).to(x.dtype), x], 1) + self.pos.to(x.dtype)
+            x = cls_pos(x, self.cls, self.pos)
         pend = None
         last = len(self.blocks) - 1
         for i, blk in enumerate(self.blocks):
