@@ -162,7 +162,8 @@ class Block(nn.Module):
 def cls_pos(x, cls, pos):
     """``cat([cls, x], 1) + pos`` in one elementwise pass: the patch tokens' sum is written straight
     into rows 1.. of the token buffer (no concatenated copy followed by a second add pass), the
-    [CLS] row is the broadcast ``cls + pos[0]``; bit-identical to the composition (same bf16 adds)."""
+    [CLS] row is the broadcast ``cls + pos[0]``; bit-identical to the composition (same bf16 adds).
+    Not differentiable (``out=``): the forward of :class:`_ClsPos`, whose backward is explicit."""
     b, n, d = x.shape
     out = torch.empty(b, n + 1, d, device=x.device, dtype=x.dtype)
     torch.add(x, pos[:, 1:].to(x.dtype), out=out[:, 1:])
@@ -217,7 +218,8 @@ class ViT(nn.Module):
         if x.is_cuda and torch.is_grad_enabled():
             x = _ClsPos.apply(x, self.cls, self.pos)
         else:
-            x = cls_pos(x, self.cls, self.pos)
+            # the differentiable composition (cls_pos writes through out=, which autograd does not trace)
+            x = torch.cat([self.cls.expand(x.shape[0], -1, -1).to(x.dtype), x], 1) + self.pos.to(x.dtype)
         pend = None
         last = len(self.blocks) - 1
         for i, blk in enumerate(self.blocks):
