@@ -39,6 +39,7 @@
 // Tile order: 1-D grid, XCD-aware (bijective): the workgroups of one XCD take a contiguous
 // range of tile ids in N-fastest order, so they share A row panels in that XCD's L2.
 #include <cstdint>
+#include <cstdlib>
 #include <stdexcept>
 #include <type_traits>
 #include <string>
@@ -89,6 +90,7 @@ struct NTArgs {
   int conv_cpt;        // k-tiles per tap (conv_c / 64)
   float conv_inv_cpt;  // 1 / conv_cpt
   uint32_t a_bytes;    // bytes of the image (the buffer resource's range: taps outside read zeros)
+  int order;           // tile order within an XCD's block: 0 contiguous ranges, 1 interleaved (FLUXMPI_GEMM_NT_ORDER)
 };
 
 constexpr int kShards = 64;  // BatchNorm statistics shards (== batchnorm.hip)
@@ -158,17 +160,37 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
   // vector-memory instructions per wave in an epilogue (lower bound: unconditional ones)
   constexpr int kEpiVm = EPI == 1 || EPI == 2 ? 32 : 16;
   const int G = gridDim.x;
-  int gi = blockIdx.x;
-  {  // bijective XCD-aware range order: the workgroups of one XCD take neighbouring ranges
-    const int q = G / 8, r = G % 8, xcd = gi % 8, pos = gi / 8;
-    gi = __builtin_amdgcn_readfirstlane((xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos);
-  }
   const int nk = p.nk;  // >= 2
   const int tiles = p.tiles_m * p.tiles_n;
-  // the workgroup's tiles [T0, T1) as one stream of units (tile, k-tile), u = T * nk + t
-  const int T0 = __builtin_amdgcn_readfirstlane(range_start(tiles, G, gi));
-  const int T1 = __builtin_amdgcn_readfirstlane(range_start(tiles, G, gi + 1));
-  const int u0 = T0 * nk, u1 = T1 * nk;  // < 2^31 (gemm_nt_supported)
+  // The XCD of workgroup b is b % 8 (round-robin dispatch); its workgroups own one contiguous block
+  // of tiles [tb, te) (bijective over the XCDs, balanced as G contiguous ranges would be). Within
+  // the block, order 0: each workgroup a contiguous range; order 1 (default): workgroup `pos` takes
+  // tiles tb + pos, tb + pos + nx, ... — at any moment the XCD's workgroups work on neighbouring
+  // tiles (N-fastest), which share A row panels and B column panels in its L2 (order 0 re-read a
+  // panel from beyond L2 for each of a workgroup's tiles: L2 hit rate 48 % on qkv,
+  // profiles/rd4ab_gemm_nt_pmc.md).
+  int base, stride, nT;
+  {
+    const int q = G / 8, r = G % 8, xcd = blockIdx.x % 8, pos = blockIdx.x / 8;
+    const int gx0 = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q, nx = q + (xcd < r ? 1 : 0);
+    if (p.order == 0) {
+      base = range_start(tiles, G, gx0 + pos);
+      stride = 1;
+      nT = range_start(tiles, G, gx0 + pos + 1) - base;
+    } else {
+      const int tb = range_start(tiles, G, gx0), te = range_start(tiles, G, gx0 + nx);
+      base = tb + pos;
+      stride = nx;
+      nT = pos < te - tb ? (te - tb - pos + nx - 1) / nx : 0;
+    }
+    base = __builtin_amdgcn_readfirstlane(base);
+    stride = __builtin_amdgcn_readfirstlane(stride);
+    nT = __builtin_amdgcn_readfirstlane(nT);
+  }
+  if (nT <= 0) return;  // workgroup-uniform, before any DMA or barrier
+  auto tmap = [&](int j) { return base + j * stride; };  // the workgroup's j-th tile
+  // the workgroup's tiles as one stream of units (local tile j, k-tile t), u = j * nk + t
+  const int u0 = 0, u1 = nT * nk;  // < 2^31 (gemm_nt_supported)
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // wave-uniform
   const int wr = wave >> 2, wc = wave & 3;
 
@@ -270,9 +292,9 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
 
   // ---- prologue: B(u0), A(u0) phases 0..3, B(u0 + 1)
   {
-    const int T0 = u0 / nk, t0 = u0 - T0 * nk;
-    const TileInfo a0 = tile_of(p, T0);
-    const TileInfo a1 = t0 + 1 < nk ? a0 : tile_of(p, T0 + 1);
+    const int j0 = u0 / nk, t0 = u0 - j0 * nk;
+    const TileInfo a0 = tile_of(p, tmap(j0));
+    const TileInfo a1 = t0 + 1 < nk ? a0 : tile_of(p, tmap(j0 + 1 < nT ? j0 + 1 : j0));
     const int t1 = t0 + 1 < nk ? t0 + 1 : 0;
     if constexpr (CONV) conv_info(a0, crow);
 #pragma unroll
@@ -358,10 +380,10 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
 
   using Z = std::integral_constant<int, 0>;
   bool after_epi = false;
-  int T = T0;
-  TileInfo cur = tile_of(p, T);
+  int j = 0;
+  TileInfo cur = tile_of(p, tmap(0));
   for (int u = u0; u < u1; u += nk) {
-    const TileInfo nxt = tile_of(p, T + 1 < tiles ? T + 1 : T);
+    const TileInfo nxt = tile_of(p, tmap(j + 1 < nT ? j + 1 : j));
     if constexpr (CONV) conv_info(nxt, crow_n);  // for the A issues of this tile's last k-tile
     if (after_epi) ktile(u, 0, cur, nxt, std::true_type{}, std::integral_constant<int, kEpiVm>{});
     else ktile(u, 0, cur, nxt, std::true_type{}, Z{});
@@ -512,7 +534,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
       }
     }
     if (EPI == 3 && fr_e == 0) {  // one atomic per column per wave row into the tile's statistics shard
-      float* shard = p.stats + static_cast<int64_t>(T % kShards) * 2 * p.N + cur.n0() + colx;
+      float* shard = p.stats + static_cast<int64_t>(tmap(j) % kShards) * 2 * p.N + cur.n0() + colx;
 #pragma unroll
       for (int q = 0; q < 2; ++q)
 #pragma unroll
@@ -523,7 +545,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
     }
     ++seg;
     after_epi = true;
-    ++T;
+    ++j;
     cur = nxt;
     if constexpr (CONV) crow = crow_n;
   }
@@ -561,6 +583,15 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restr
       *reinterpret_cast<uint4*>(dst + (c0 + c) * ldd + r0 + ch * 8) = v;
     }
   }
+}
+
+// FLUXMPI_GEMM_NT_ORDER: 1 (default) XCD-interleaved tile order, 0 contiguous ranges (A/B)
+int tile_order() {
+  static const int v = [] {
+    const char* e = std::getenv("FLUXMPI_GEMM_NT_ORDER");
+    return e != nullptr && e[0] == '0' ? 0 : 1;
+  }();
+  return v;
 }
 
 int cus() {
@@ -630,6 +661,7 @@ void gemm_nt(const void* a, const void* b, void* c, void* c2, const void* bias, 
   p.stats = stats, p.lda = lda, p.ldb = ldb, p.ldc = ldc, p.N = N;
   p.nk = static_cast<int>(K / kBK), p.tiles_m = static_cast<int>(M / kT), p.tiles_n = static_cast<int>(N / kT);
   p.bias_f32 = bias_f32, p.gelu_tanh = gelu_form();
+  p.order = tile_order();
   const int bk = bias == nullptr ? 0 : bias_f32 ? 1 : 2;
   if (epi == 3) {
     launch<3, 0>(p, stream);
@@ -661,6 +693,7 @@ void gemm_nt_conv(const void* x, const void* w, void* y, float* stats, int64_t n
   p.stats = stats, p.lda = 9 * C, p.ldb = 9 * C, p.ldc = Cout, p.N = Cout;
   p.nk = 9 * C / kBK, p.tiles_m = static_cast<int>(pixels / kT), p.tiles_n = static_cast<int>(Cout / kT);
   p.gelu_tanh = 0;
+  p.order = tile_order();
   p.conv_h = H, p.conv_w = W, p.conv_c = C, p.conv_cpt = C / kBK;
   p.conv_inv_cpt = 1.f / static_cast<float>(C / kBK);
   p.a_bytes = static_cast<uint32_t>(pixels * C * 2);
