@@ -178,6 +178,14 @@ def selfcheck_or_code(FluxMPI, world: int, rank: int, dev):
     return rep if ok else 4
 
 
+def comm_env() -> dict:
+    """The RCCL / NCCL tuning environment of this run (channel counts, protocols, algorithms,
+    P2P and xGMI settings): recorded beside the number so a scaling run states what it ran with.
+    Nothing is set by this bench; RCCL picks channels and protocols itself when these are unset."""
+    keys = sorted(k for k in os.environ if k.startswith(("NCCL_", "RCCL_")))
+    return {k: os.environ[k] for k in keys}
+
+
 def main():
     args = parse()
     if args.image is None:
@@ -370,7 +378,7 @@ def main():
                        "grid_rounds": int(os.environ.get("FLUXMPI_GRID_ROUNDS", "1")),
                        # the communicator's own report (checked against the launch before timing)
                        # and the per-rank spread of the timed region
-                       **comm_report,
+                       **comm_report, "comm_env": comm_env(),
                        "rank_ms_per_step_min": round(1000 * min(per_rank) / args.steps, 3),
                        "rank_ms_per_step_max": round(1000 * max(per_rank) / args.steps, 3),
                        **({"gelu": _gelu_form()} if args.model == "vit_b16" else {}),

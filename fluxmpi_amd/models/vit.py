@@ -189,12 +189,15 @@ class _ClsPos(torch.autograd.Function):
         if need[2]:
             with graddst.into(pos):
                 out = graddst.empty(tuple(pos.shape[1:]), pos.dtype, dy.device) if dy.dtype == pos.dtype else None
-            dpos = (torch.sum(dy, 0, out=out) if out is not None else dy.sum(0).to(pos.dtype)).view(pos.shape)
+            # mismatched dtypes (fp32 parameter, bf16 activations): sum in fp32, round once
+            dpos = (torch.sum(dy, 0, out=out) if out is not None
+                    else dy.float().sum(0).to(pos.dtype)).view(pos.shape)
         if need[1]:
             with graddst.into(cls):
                 out = graddst.empty((cls.shape[-1],), cls.dtype, dy.device) if dy.dtype == cls.dtype else None
             d0 = dy[:, 0]
-            dcls = (torch.sum(d0, 0, out=out) if out is not None else d0.sum(0).to(cls.dtype)).view(cls.shape)
+            dcls = (torch.sum(d0, 0, out=out) if out is not None
+                    else d0.float().sum(0).to(cls.dtype)).view(cls.shape)
         return (dy[:, 1:] if need[0] else None), dcls, dpos
 
 

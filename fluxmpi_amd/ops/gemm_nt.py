@@ -47,6 +47,12 @@ def _stream(t):
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
+def _aligned(*tensors: torch.Tensor) -> bool:
+    """The kernels' buffer resources and 16-B vector accesses need 16-B aligned operands (an
+    oddly offset view, e.g. a narrowed buffer, routes to the fallback instead of raising)."""
+    return all(t.data_ptr() % 16 == 0 for t in tensors)
+
+
 def supported(rows: int, n_out: int, k: int, *tensors: torch.Tensor, fused: bool | str = False) -> bool:
     """Whether gemm_nt takes ``[rows, k] x [n_out, k]^T`` (both operands k-contiguous after the
     weight transpose of an input gradient) under the current mode. ``fused``: the call carries an
@@ -59,7 +65,7 @@ def supported(rows: int, n_out: int, k: int, *tensors: torch.Tensor, fused: bool
         ok = fused is True or (fused in ("fwd", "dgrad") and MODE in ("fused", "dgrad"))
         if not ok:
             return False
-    if any(t.dtype != torch.bfloat16 for t in tensors):
+    if any(t.dtype != torch.bfloat16 for t in tensors) or not _aligned(*tensors):
         return False
     C = _ext.get(required=False)
     return C is not None and hasattr(C, "gemm_nt") and bool(C.gemm_nt_supported(rows, n_out, k, k, k, n_out))
@@ -143,7 +149,7 @@ def conv_ok(pixels: int, c: int, cout: int, *tensors: torch.Tensor) -> bool:
     runs on :func:`conv3x3`."""
     if not CONV or not tensors or not tensors[0].is_cuda or any(t.dtype != torch.bfloat16 for t in tensors):
         return False
-    if not _worth(pixels, cout, 9 * c):
+    if not _aligned(*tensors) or not _worth(pixels, cout, 9 * c):
         return False
     C = _ext.get(required=False)
     return C is not None and hasattr(C, "gemm_nt_conv") and bool(C.gemm_nt_conv_supported(pixels, c, cout))
@@ -153,7 +159,7 @@ def gemm_ok(rows: int, n_out: int, k: int, *tensors: torch.Tensor) -> bool:
     """Whether a 1x1 convolution / plain NT GEMM of this shape runs on :func:`gemm_plain`."""
     if not CONV or not tensors or not tensors[0].is_cuda or any(t.dtype != torch.bfloat16 for t in tensors):
         return False
-    if not _worth(rows, n_out, k):
+    if not _aligned(*tensors) or not _worth(rows, n_out, k):
         return False
     C = _ext.get(required=False)
     return C is not None and hasattr(C, "gemm_nt_stats") and bool(C.gemm_nt_supported(rows, n_out, k, k, k, n_out))

@@ -411,6 +411,16 @@ class GlooDeviceComm(TorchComm):
         super().__init__(group, rank, size, "gloo")
         self.name = "gloo-device"
 
+    def self_report(self) -> dict:
+        """The process group's own answer (``dist.get_world_size`` / ``get_rank`` on this
+        communicator's group) and the device the ranks share, so the bench self-check runs on the
+        ``--same-device`` rehearsal path too (keys as RcclComm's, prefixed ``comm_``)."""
+        import torch.distributed as dist
+
+        dev = torch.cuda.current_device() if torch.cuda.is_available() else None
+        return {"comm_backend": self.name, "comm_nranks": int(dist.get_world_size(self.group)),
+                "comm_rank": int(dist.get_rank(self.group)), "comm_device": dev}
+
     def _host(self, fn, out, *inputs):
         hs = [t.detach().cpu() for t in inputs]
         ho = out.detach().cpu()

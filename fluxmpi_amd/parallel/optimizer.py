@@ -36,13 +36,15 @@ import torch
 from ..optimisers import AbstractRule
 from ..utils.config import get_config
 from ..utils.debug import check_same_structure, structure_hash
-from ..utils.tree import fmap, node_def
+from ..utils.errors import CollectiveMismatchError
+from ..utils.tree import fmap, node_def, structure_signature
 from . import runtime
 from .bucket import allreduce_tensors
 from .comm import ReduceOp
 
 _CHECKED: set = set()
-_LIKE_CHECKED: set = set()  # id() of `like` trees whose zero-filled plan was checked across ranks
+# structure hash of a `like` tree -> signature of the zero-filled gradient tree checked across ranks
+_LIKE_CHECKED: dict = {}
 
 
 def check_plan(obj, what: str, derived: bool = False) -> None:
@@ -130,6 +132,32 @@ def _zero_fill(gs: Any, like: Any) -> Any:
     return nd[1](aux, [_zero_fill(g, c) for g, c in zip(gc, lc)])
 
 
+def _check_like_plan(gs: Any, like: Any) -> None:
+    """Plan check for ``allreduce_gradients(like=...)``.
+
+    The gate is the structure hash of ``like`` (the parameter tree: identical on every rank
+    after ``synchronize``), so every rank takes the same branch. The first call for a given
+    ``like`` structure compares the zero-filled gradient tree (shapes and dtypes included)
+    across ranks; later calls compare it LOCALLY against the signature that was checked, so a
+    gradient whose shape or dtype changed on one rank raises instead of entering a mismatched
+    collective. The table is keyed by structure, so it stays bounded however often callers
+    build fresh ``like`` trees.
+    """
+    mode = get_config().check_plans
+    if mode == "never" or not runtime.Initialized() or runtime.total_workers() == 1:
+        return
+    key = structure_hash(like)
+    sig = structure_signature(gs)
+    seen = _LIKE_CHECKED.get(key)
+    if seen is None:
+        check_same_structure(gs, what="gradient tree")
+        _LIKE_CHECKED[key] = sig
+    elif seen != sig:
+        raise CollectiveMismatchError(
+            "allreduce_gradients(like=...): a gradient's shape or dtype differs from the plan "
+            "checked across ranks for this parameter tree; the collectives would mismatch")
+
+
 def allreduce_gradients(gs: Any, on_gpu: bool | None = None, op=ReduceOp.SUM, like: Any = None) -> Any:
     """Allreduce (SUM) every array leaf of the gradient tree ``gs``; returns the tree.
 
@@ -146,10 +174,7 @@ def allreduce_gradients(gs: Any, on_gpu: bool | None = None, op=ReduceOp.SUM, li
     runtime._require()
     if like is not None:
         gs = _zero_fill(gs, like)
-        # the plan follows `like` (zero-filled): checked once per parameter-tree object
-        if id(like) not in _LIKE_CHECKED:
-            check_plan(gs, "gradient tree", derived=True)
-            _LIKE_CHECKED.add(id(like))
+        _check_like_plan(gs, like)
     else:
         check_plan(gs, "gradient tree")
     leaves: list = []

@@ -20,13 +20,16 @@ def comm_selfcheck(comm, world: int, rank: int, device_index: int | None) -> dic
     rep = dict(comm.self_report()) if hasattr(comm, "self_report") else {}
     if not rep:
         return rep
+    # RcclComm reports rccl_*; the host-collective backends (gloo on device tensors) comm_*
+    pre = "rccl_" if "rccl_nranks" in rep else "comm_"
+    nranks, crank, cdev = rep.get(pre + "nranks"), rep.get(pre + "rank"), rep.get(pre + "device")
     problems = []
-    if rep.get("rccl_nranks") != world:
-        problems.append(f"communicator has {rep.get('rccl_nranks')} ranks, WORLD_SIZE is {world}")
-    if rep.get("rccl_rank") != rank:
-        problems.append(f"communicator rank {rep.get('rccl_rank')} != RANK {rank}")
-    if device_index is not None and rep.get("rccl_device") not in (None, device_index):
-        problems.append(f"communicator device {rep.get('rccl_device')} != pinned device {device_index}")
+    if nranks != world:
+        problems.append(f"communicator has {nranks} ranks, WORLD_SIZE is {world}")
+    if crank != rank:
+        problems.append(f"communicator rank {crank} != RANK {rank}")
+    if device_index is not None and cdev not in (None, device_index):
+        problems.append(f"communicator device {cdev} != pinned device {device_index}")
     if problems:
         raise CommSelfCheckError("; ".join(problems))
     return rep

@@ -26,15 +26,10 @@ for s in $STEPS; do
     pytest) step pytest_gpu 900 1 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
     pytest_comm) step pytest_comm 300 1 python -u -m pytest tests/test_comm_gpu.py -m gpu -x -v --timeout 120 \
                    --timeout-method thread ;;
-    pytest_g256) step pytest_g256 300 1 python -u -m pytest tests/test_gemm256_gpu.py -m gpu -x -v --timeout 120 \
-                   --timeout-method thread ;;
     pytest_gemm) step pytest_gemm 600 1 python -u -m pytest tests/test_gemm_gpu.py tests/test_conv_gpu.py \
-                   tests/test_gemm256_gpu.py tests/test_fused_block_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread ;;
+                   tests/test_gemm_nt_gpu.py tests/test_fused_block_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread ;;
     pytest_vit) step pytest_vit 600 1 python -u -m pytest tests/test_vit_model_gpu.py tests/test_vit_gpu.py tests/test_linear_gpu.py \
                    tests/test_gelu.py tests/test_layernorm.py -m gpu -x -q -s --timeout 300 --timeout-method thread ;;
-    pmc_g256) cd /tmp && step pmc_g256 120 0 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
-                TCC_HIT_sum TCC_MISS_sum -d "$OUT/pmc_g256_${TAG}" -o run --output-format csv -- python3 "$ROOT/scripts/bench_gemm256.py"; cd "$ROOT" ;;
-    bench_g256) step bench_g256 300 0 python scripts/bench_gemm256.py ;;
     smoke) step smoke 240 0 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 300 0 python bench.py --steps "$BENCH_STEPS" --warmup "$BENCH_WARMUP" ;;
     bench_graph) step bench_graph 300 0 python bench.py --steps "$BENCH_STEPS" --warmup "$BENCH_WARMUP" --graph ;;

@@ -11,7 +11,7 @@ read once, each output written once), so TB/s is a lower bound on what the kerne
 Which kernel does which op (the model's dispatch, models/vit.py + ops/): the forward GEMMs run on
 hipBLASLt (`Custom_Cijk…MT256x256x64`: 11 blocks x {qkv, proj, fc1, fc2} + the last block's qkv
 + the patch embedding = 46 calls), the input-gradient GEMMs on hipBLASLt (`Cijk_Ailk_Bljk…MT256x256`:
-11 x {qkv, proj, fc1} + last qkv = 34) except fc2's (gemm256 EPI 2 with the GELU backward, 11), every
+11 x {qkv, proj, fc1} + last qkv = 34) except fc2's (gemm_nt EPI 2 with the GELU backward, 11), every
 weight gradient on wgrad256 (46). The last block's proj / fc1 / fc2 act on the [CLS] token only.
 
 usage: python scripts/roofline_vit.py <kernel_trace.csv> [N] > profiles/<name>.md
@@ -47,7 +47,7 @@ CLASSES = [
     ("Linear input gradient (hipBLASLt: qkv, proj, fc1)", r"^Cijk_Ailk_Bljk.*MT256x256x64",
      BLK * (QKV + lin(M, D, D) + lin(M, D, F)) + QKV,
      BLK * ((3 * TOK + TOK) + (TOK + TOK) + (HID + TOK)) + 4 * TOK),
-    ("fc2 input gradient + GELU backward + fc1 bias grad (gemm256 EPI 2)", r"gemm256_kernel<true, 2",
+    ("fc2 input gradient + GELU backward + fc1 bias grad (gemm_nt EPI 2)", r"gemm_nt_kernel<2,",
      BLK * lin(M, D, F), BLK * (TOK + HID + HID)),
     ("Linear weight gradients (wgrad256, split-K)", r"wgrad256",
      BLK * FWD_FULL + QKV + PATCH,

@@ -56,6 +56,22 @@ def worker_irregular():
     out = FluxMPI.allreduce_gradients(grads, like=_params())
     torch.testing.assert_close(out["a"], _grad(0, "a"))
     torch.testing.assert_close(out["b"], _grad(0, "b") + _grad(1, "b"))
+    # a fresh `like` tree of the same structure (new object every step) skips the cross-rank
+    # check on every rank; a gradient whose shape changed on one rank raises there instead of
+    # entering a mismatched collective (the others are not sent into the collective either:
+    # the same step raises the same way on the rank that differs, and we stop here)
+    grads = {n: _grad(r, n) for n in ps}
+    out = FluxMPI.allreduce_gradients(grads, like=_params())
+    torch.testing.assert_close(out["c"], _grad(0, "c") + _grad(1, "c"))
+    grads = {n: _grad(r, n) for n in ps}
+    grads["c"] = torch.zeros(4) if r == 1 else grads["c"]
+    if r == 1:
+        try:
+            FluxMPI.allreduce_gradients(grads, like=_params())
+        except CollectiveMismatchError:
+            pass
+        else:
+            raise AssertionError("a changed gradient shape did not raise")
 
     # 3. without `like`, differing trees raise instead of hanging (on every rank)
     grads = {n: _grad(r, n) for n in ps}

@@ -191,6 +191,13 @@ def worker_bench_selfcheck():
         runtime.device_comm = lambda: _stub_rccl(r, W, W)
         rep = bench.selfcheck_or_code(FluxMPI, W, r, None)
         assert rep["rccl_nranks"] == W and rep["rccl_rank"] == r and rep["comm_priority"] == 0
+        # the --same-device rehearsal backend (gloo on device tensors) answers from its group
+        from fluxmpi_amd.parallel.comm import GlooDeviceComm
+        gd = GlooDeviceComm(runtime.cpu_comm().group, r, W)
+        runtime.device_comm = lambda: gd
+        rep = bench.selfcheck_or_code(FluxMPI, W, r, None)
+        assert rep["comm_backend"] == "gloo-device" and rep["comm_nranks"] == W and rep["comm_rank"] == r
+        assert bench.selfcheck_or_code(FluxMPI, W + 1, r, None) == 4  # WORLD_SIZE disagrees
     finally:
         runtime.device_comm = real
     FluxMPI.Finalize()
