@@ -57,6 +57,11 @@ def parse():
                     help="all ranks on cuda:0 with gloo collectives on device tensors (RCCL refuses a "
                          "shared GPU): runs the N>1 code path on a 1-GPU box; no throughput claim")
     ap.add_argument("--graph", action="store_true", help="capture the step in a HIP graph")
+    ap.add_argument("--deq-solver", default="",
+                    help="DEQ models: solver settings as k=v pairs, e.g. 'tol=1e-2,bwd_tol=1e-2,max_iter=30'")
+    ap.add_argument("--overlap-opt", type=int, default=None, choices=[0, 1],
+                    help="per-bucket optimiser overlap (default: FLUXMPI_OVERLAP_OPT): each bucket's fused "
+                         "update is enqueued during backward as soon as its gradient is reduced")
     ap.add_argument("--api", default="ddp", choices=["ddp", "functional"],
                     help="ddp: the DDP engine (hooks, buckets born in the comm buffers, fused optimiser); "
                          "functional: the reference's API shape (src/optimizer.jl:45-65) — the nested "
@@ -240,7 +245,11 @@ def main():
         return 2
 
     torch.manual_seed(1234 + rank)
-    model = build_model(args.model, conv_impl=args.conv, norm=args.norm)
+    solver = {}
+    for kv in filter(None, args.deq_solver.split(",")):
+        k, v = kv.split("=")
+        solver[k.strip()] = int(v) if k.strip() in ("max_iter", "bwd_iter", "check_lag") else float(v)
+    model = build_model(args.model, conv_impl=args.conv, norm=args.norm, **solver)
     memfmt = {"channels_last": torch.channels_last, "contiguous": torch.contiguous_format}.get(
         args.memory_format, getattr(model, "memory_format", torch.channels_last))
     model = model.to(dev, memory_format=memfmt)
@@ -266,7 +275,8 @@ def main():
             return 2
         ddp = Functional(FluxMPI, O, model, rule)
     else:
-        ddp = DDP(model, rule, average=True, overlap=not args.no_overlap, force_comm=args.force_comm)
+        ddp = DDP(model, rule, average=True, overlap=not args.no_overlap, force_comm=args.force_comm,
+                  overlap_opt=None if args.overlap_opt is None else bool(args.overlap_opt))
 
     B = args.batch
     gx = torch.Generator(device=dev).manual_seed(rank)
@@ -382,6 +392,8 @@ def main():
                        "rank_ms_per_step_min": round(1000 * min(per_rank) / args.steps, 3),
                        "rank_ms_per_step_max": round(1000 * max(per_rank) / args.steps, 3),
                        **({"gelu": _gelu_form()} if args.model == "vit_b16" else {}),
+                       **({"deq_solver": {k: getattr(deq, k) for k in ("max_iter", "tol", "bwd_iter", "bwd_tol")}}
+                          if deq is not None else {}),
                        **({"deq_fwd_iters_per_step": round(sum(i[0] for i in timed_iters) / len(timed_iters), 2),
                            "deq_bwd_iters_per_step": round(sum(i[1] for i in timed_iters) / len(timed_iters), 2)}
                           if timed_iters else {})},

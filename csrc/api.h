@@ -235,6 +235,9 @@ void gemm_wgrad256(const void* a, const void* b, float* ws, int64_t lda, int64_t
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc);
 bool gemm_nt_conv_supported(int64_t pixels, int64_t C, int64_t Cout);
 int gemm_nt_colpart_rows(int64_t M);
+// split-K tail: the fewest k-tiles of a workgroup's share of the last round (0: off; default 8 or
+// FLUXMPI_GEMM_NT_SPLIT)
+void gemm_nt_set_split(int min_ktiles);
 void gemm_nt(const void* a, const void* b, void* c, void* c2, const void* bias, int bias_f32, const void* h,
              float* colpart, float* stats, int64_t lda, int64_t ldb, int64_t ldc, int64_t M, int64_t N, int64_t K,
              int epi, hipStream_t stream);

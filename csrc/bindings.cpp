@@ -296,6 +296,7 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("gemm_nt_supported", &gemm_nt_supported);
   m.def("gemm_nt_colpart_rows", &gemm_nt_colpart_rows);
+  m.def("gemm_nt_set_split", &gemm_nt_set_split);
   m.def("gemm_nt", [](uintptr_t a, uintptr_t b, uintptr_t c, uintptr_t c2, uintptr_t bias, int bias_f32, uintptr_t h,
                       uintptr_t colpart, int64_t lda, int64_t ldb, int64_t ldc,
                       int64_t M, int64_t N, int64_t K, int epi, uintptr_t stream) {

@@ -36,8 +36,12 @@
 // tile load a 16-B zero line into a dead slot, so the count never changes. A slot is restaged
 // only after a barrier that follows its readers' lgkmcnt(0).
 //
-// Tile order: 1-D grid, XCD-aware (bijective): the workgroups of one XCD take a contiguous
-// range of tile ids in N-fastest order, so they share A row panels in that XCD's L2.
+// Tile order: 1-D grid, XCD-aware (bijective): the workgroups of one XCD take a contiguous block
+// of tile ids round-robin in N-fastest order, so they share A row / B column panels in its L2.
+// Split-K tail: the last, partial round of each XCD's block is cut into even k-tile ranges over
+// all its workgroups (stream-K on the tail only: the K = 3072 ViT shapes have 591 tiles = 2.3
+// rounds of 256 CUs, a third of the last round's CUs were idle); the pieces of a tile meet in a
+// write-through fp32 workspace and the last arriving workgroup runs the epilogue (TailPlan).
 #include <cstdint>
 #include <cstdlib>
 #include <stdexcept>
@@ -65,7 +69,8 @@ constexpr int kRow = kBK * 2;          // 128-B image rows
 constexpr int kImg = kT * kRow;        // 32 KiB per operand image
 constexpr int kBuf = 2 * kImg;         // [A | B]
 constexpr int kBiasOff = 2 * kBuf;     // 2 x 1 KiB bias slots (tile parity)
-constexpr int kSmem = kBiasOff + 2048;  // 130 KiB
+constexpr int kFlagOff = kBiasOff + 2048;  // split tiles: the arrival ticket's verdict
+constexpr int kSmem = kFlagOff + 16;      // 130 KiB
 
 __device__ __attribute__((aligned(64))) uint4 g_zero_nt[4];
 
@@ -90,10 +95,63 @@ struct NTArgs {
   int conv_cpt;        // k-tiles per tap (conv_c / 64)
   float conv_inv_cpt;  // 1 / conv_cpt
   uint32_t a_bytes;    // bytes of the image (the buffer resource's range: taps outside read zeros)
-  int order;           // tile order within an XCD's block: 0 contiguous ranges, 1 interleaved (FLUXMPI_GEMM_NT_ORDER)
+  // split-K tail (stream-K on the last, partial round of each XCD's block of tiles): 0 off
+  int split;
+  int split_min;       // fewest k-tiles of a WG's share of the tail (even; fewer WGs take part below it)
+  int max_q;           // partial-tile jobs per workgroup (workspace slots per workgroup)
+  float* ws;           // fp32 partial accumulators: [G * max_q] slots of kSlotBytes
+  int* counters;       // [tiles] arrival tickets of split tiles (zero between launches: the last arriver resets)
 };
 
 constexpr int kShards = 64;  // BatchNorm statistics shards (== batchnorm.hip)
+constexpr int kSlotBytes = 8 * 32 * 64 * 16;  // one partial tile: 8 waves x 32 f32x4 accumulators x 64 lanes
+
+// The tile schedule, identical on host and device (host: workspace size, max_q). The tiles
+// (N-fastest) are dealt to the XCDs as G contiguous ranges (workgroup b runs on XCD b % 8, a
+// speed assumption only); inside an XCD's block [tb, te) its nx workgroups take the tiles
+// round-robin (workgroup pos: tb + pos, tb + pos + nx, ...) for the F = (te - tb) / nx full rounds.
+// The R = (te - tb) % nx tiles of the last round: without split, one each for workgroups 0..R-1;
+// with split (stream-K tail), their R * nk k-tiles are cut into nw equal, even-length ranges, one
+// per workgroup (nw = min(nx, units / split_min)), so the tail takes ~R / nx of a round instead
+// of a whole one. A range may cover parts of several tiles: a partial-tile job; the pieces of a
+// tile are summed by whichever workgroup arrives last (below).
+struct TailPlan {
+  int tb, nx, pos;
+  int nfull;     // full-tile jobs of this workgroup
+  int tt0;       // first tail tile (split)
+  int u2, nw;    // tail units in k-tile PAIRS, workgroups sharing it (0 if no split tail)
+  int s, e;      // this workgroup's tail k-tile range [s, e) (split and pos < nw), else s = e = 0
+  __host__ __device__ int bnd(int w) const { return 2 * static_cast<int>(static_cast<int64_t>(u2) * w / nw); }
+  // workgroup (position) whose range holds tail k-tile x
+  __host__ __device__ int wg_of(int x) const {
+    return static_cast<int>((static_cast<int64_t>(x / 2 + 1) * nw - 1) / u2);
+  }
+};
+
+__host__ __device__ inline int range_start_hd(int tiles, int G, int r) {
+  return static_cast<int>(static_cast<int64_t>(tiles) * r / G);
+}
+
+__host__ __device__ inline TailPlan tail_plan(int tiles, int G, int nk, int split, int split_min, int b) {
+  TailPlan t{};
+  const int q = G / 8, r = G % 8, xcd = b % 8, pos = b / 8;
+  const int gx0 = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q, nx = q + (xcd < r ? 1 : 0);
+  const int tb = range_start_hd(tiles, G, gx0), te = range_start_hd(tiles, G, gx0 + nx);
+  t.tb = tb, t.nx = nx, t.pos = pos;
+  const int T = te - tb, F = nx > 0 ? T / nx : 0, R = T - F * nx;
+  t.tt0 = tb + F * nx;
+  if (split && R > 0) {
+    t.u2 = R * nk / 2;
+    const int want = (2 * t.u2) / (split_min > 2 ? split_min : 2);
+    t.nw = want < 1 ? 1 : (want > nx ? nx : want);
+    t.nfull = F;
+    if (pos < t.nw) t.s = t.bnd(pos), t.e = t.bnd(pos + 1);
+  } else {
+    t.u2 = 0, t.nw = 0;
+    t.nfull = F + (pos < R ? 1 : 0);
+  }
+  return t;
+}
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
@@ -114,6 +172,23 @@ __device__ __forceinline__ void glds16(const void* src, char* dst) {
   __builtin_amdgcn_global_load_lds((gl_void*)(src), (lds_char*)(dst), 16, 0, 0);
 }
 
+// After an epilogue's 16-B store: a scheduling fence and STORE_GUARD_NOPS + 1 wait states before
+// any later instruction may overwrite the store's data registers. hipcc (ROCm 7.2) lets a VALU
+// rewrite them 1-2 states after a buffer_store_dwordx4, which gfx950 does not tolerate under a full
+// store queue: the fc2 input-gradient epilogue (EPI 2) wrote ~20 wrong elements per launch, always
+// the lanes of two rows of one 16-row block, on the split tiles (whose epilogue runs while other
+// workgroups store), and the same build with a wait after each store, or with its loads reordered,
+// was clean over 40 launches (profiles/rd5c_gemm_nt_store_hazard.md). The earlier "SLP build gives
+// NaNs in EPI 1" (round 4) is the same hazard: packed VALU moved closer to the stores.
+#ifndef STORE_GUARD_NOPS
+#define STORE_GUARD_NOPS 3
+#endif
+__device__ __forceinline__ void store_guard() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop %0" ::"n"(STORE_GUARD_NOPS));
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 __device__ __forceinline__ bf16x8 frag(const char* __restrict__ p) { return *reinterpret_cast<const bf16x8*>(p); }
 
 // Persistent, tile-granular: the tiles (N-fastest) are dealt to the G = min(tiles, CUs)
@@ -128,8 +203,11 @@ __device__ __forceinline__ bf16x8 frag(const char* __restrict__ p) { return *rei
 // they are younger than the DMA groups those waits retire.
 // BIAS: 0 none, 1 fp32, 2 bf16 (EPI 0 / 1), staged into LDS by one LDS-DMA of wave 0 at the
 // tile's first k-tile (slot = tile parity).
-struct TileInfo {  // wave-uniform (SGPRs); every offset below fits 32 bits (gemm_nt_supported)
+struct TileInfo {  // one job, wave-uniform (SGPRs); every offset below fits 32 bits (gemm_nt_supported)
   int tm, tn;
+  int id;       // tile id (N-fastest)
+  int k0, k1;   // the job's k-tiles [k0, k1) (a full tile: [0, nk)); always >= 2 of them
+  int r;        // split tail: the tile's index in the tail (-1: a full-tile job)
   __device__ __forceinline__ int m0() const { return tm * kT; }
   __device__ __forceinline__ int n0() const { return tn * kT; }
 };
@@ -137,8 +215,10 @@ struct TileInfo {  // wave-uniform (SGPRs); every offset below fits 32 bits (gem
 __device__ __forceinline__ TileInfo tile_of(const NTArgs& p, int T) {
   TileInfo t;
   T = __builtin_amdgcn_readfirstlane(T);
+  t.id = T;
   t.tm = __builtin_amdgcn_readfirstlane(T / p.tiles_n);
   t.tn = T - t.tm * p.tiles_n;
+  t.k0 = 0, t.k1 = p.nk, t.r = -1;
   return t;
 }
 
@@ -149,11 +229,6 @@ __device__ __forceinline__ int opaque(int v) {
   return v;
 }
 
-// first tile of workgroup (range) r
-__device__ __forceinline__ int range_start(int tiles, int G, int r) {
-  return static_cast<int>(static_cast<int64_t>(tiles) * r / G);
-}
-
 template <int EPI, int BIAS, bool CONV, int GF = 1>  // GF (EPI 1 / 2): 1 tanh GELU, 0 erf GELU
 __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[kSmem];
@@ -162,35 +237,25 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
   const int G = gridDim.x;
   const int nk = p.nk;  // >= 2
   const int tiles = p.tiles_m * p.tiles_n;
-  // The XCD of workgroup b is b % 8 (round-robin dispatch); its workgroups own one contiguous block
-  // of tiles [tb, te) (bijective over the XCDs, balanced as G contiguous ranges would be). Within
-  // the block, order 0: each workgroup a contiguous range; order 1 (default): workgroup `pos` takes
-  // tiles tb + pos, tb + pos + nx, ... — at any moment the XCD's workgroups work on neighbouring
-  // tiles (N-fastest), which share A row panels and B column panels in its L2 (order 0 re-read a
-  // panel from beyond L2 for each of a workgroup's tiles: L2 hit rate 48 % on qkv,
-  // profiles/rd4ab_gemm_nt_pmc.md).
-  int base, stride, nT;
-  {
-    const int q = G / 8, r = G % 8, xcd = blockIdx.x % 8, pos = blockIdx.x / 8;
-    const int gx0 = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q, nx = q + (xcd < r ? 1 : 0);
-    if (p.order == 0) {
-      base = range_start(tiles, G, gx0 + pos);
-      stride = 1;
-      nT = range_start(tiles, G, gx0 + pos + 1) - base;
-    } else {
-      const int tb = range_start(tiles, G, gx0), te = range_start(tiles, G, gx0 + nx);
-      base = tb + pos;
-      stride = nx;
-      nT = pos < te - tb ? (te - tb - pos + nx - 1) / nx : 0;
-    }
-    base = __builtin_amdgcn_readfirstlane(base);
-    stride = __builtin_amdgcn_readfirstlane(stride);
-    nT = __builtin_amdgcn_readfirstlane(nT);
-  }
-  if (nT <= 0) return;  // workgroup-uniform, before any DMA or barrier
-  auto tmap = [&](int j) { return base + j * stride; };  // the workgroup's j-th tile
-  // the workgroup's tiles as one stream of units (local tile j, k-tile t), u = j * nk + t
-  const int u0 = 0, u1 = nT * nk;  // < 2^31 (gemm_nt_supported)
+  // The schedule (TailPlan): workgroup `pos` of an XCD takes tiles tb + pos, tb + pos + nx, ... — at
+  // any moment the XCD's workgroups work on neighbouring tiles (N-fastest), which share A row
+  // panels and B column panels in its L2 (contiguous per-workgroup ranges re-read a panel from
+  // beyond L2 for each tile: L2 hit rate 48 % on qkv, profiles/rd4ab_gemm_nt_pmc.md) — then, with
+  // the split tail, its share of the last round's k-tiles as partial-tile jobs.
+  const TailPlan tp = tail_plan(tiles, G, nk, p.split, p.split_min, blockIdx.x);
+  const int ntail = tp.e > tp.s ? (tp.e - 1) / nk - tp.s / nk + 1 : 0;
+  const int nJ = __builtin_amdgcn_readfirstlane(tp.nfull + ntail);
+  if (nJ <= 0) return;  // workgroup-uniform, before any DMA or barrier
+  auto job_of = [&](int jj) -> TileInfo {
+    if (jj < tp.nfull) return tile_of(p, tp.tb + tp.pos + jj * tp.nx);
+    const int r = tp.s / nk + (jj - tp.nfull);
+    TileInfo t = tile_of(p, tp.tt0 + r);
+    const int a = tp.s - r * nk, b = tp.e - r * nk;
+    t.k0 = __builtin_amdgcn_readfirstlane(a > 0 ? a : 0);
+    t.k1 = __builtin_amdgcn_readfirstlane(b < nk ? b : nk);
+    t.r = __builtin_amdgcn_readfirstlane(r);
+    return t;
+  };
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // wave-uniform
   const int wr = wave >> 2, wc = wave & 3;
 
@@ -291,28 +356,24 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
   int seg = 0;  // tiles started so far: parity of the bias slot
 
   // ---- prologue: B(u0), A(u0) phases 0..3, B(u0 + 1)
-  {
-    const int j0 = u0 / nk, t0 = u0 - j0 * nk;
-    const TileInfo a0 = tile_of(p, tmap(j0));
-    const TileInfo a1 = t0 + 1 < nk ? a0 : tile_of(p, tmap(j0 + 1 < nT ? j0 + 1 : j0));
-    const int t1 = t0 + 1 < nk ? t0 + 1 : 0;
-    if constexpr (CONV) conv_info(a0, crow);
+  TileInfo cur = job_of(0);
+  {  // a job has >= 2 k-tiles, so unit 1 is the first job's second k-tile
+    if constexpr (CONV) conv_info(cur, crow);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) issueB(0, a0, t0, j);
+    for (int j = 0; j < 4; ++j) issueB(0, cur, cur.k0, j);
 #pragma unroll
-    for (int ph = 0; ph < 4; ++ph) issueA(0, a0, t0, ph, false);
-    const bool ok1 = u0 + 1 < u1;
+    for (int ph = 0; ph < 4; ++ph) issueA(0, cur, cur.k0, ph, false);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) issueB(1, ok1 ? a1 : a0, ok1 ? t1 : t0, j);
+    for (int j = 0; j < 4; ++j) issueB(1, cur, cur.k0 + 1, j);
   }
   asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if (wr == 1) __builtin_amdgcn_s_barrier();  // the stagger: waves 4-7 one barrier behind
 
-  // one k-tile (4 phases) of unit u; FIRST: the accumulators start from zero (and wave 0 stages
-  // the tile's bias when the segment will finish the tile); XV: vector-memory instructions
-  // issued since the DMA groups this k-tile's first three waits retire
-  auto ktile = [&](int u, int t, const TileInfo& cur, const TileInfo& nxt, auto first_c, auto xv_c) {
+  // one k-tile (4 phases) of stream unit u (k-tile t of job `cur`; `nxt` the next job, if
+  // has_next); FIRST: the accumulators start from zero (and wave 0 stages the tile's bias);
+  // XV: vector-memory instructions issued since the DMA groups this k-tile's first three waits retire
+  auto ktile = [&](int u, int t, const TileInfo& cur, const TileInfo& nxt, bool has_next, auto first_c, auto xv_c) {
     constexpr bool FIRST = decltype(first_c)::value;
     constexpr int XV = decltype(xv_c)::value;
     if (FIRST && BIAS != 0 && wave == 0) {
@@ -322,13 +383,13 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
                                                : reinterpret_cast<const char*>(zero));
       glds16(src, smem + kBiasOff + (seg & 1) * 1024);
     }
-    const int sl = u - u0;  // stream slot
+    const int sl = u;  // stream slot
     const char* buf = smem + (sl & 1) * kBuf;
-    // DMA targets: A of unit u + 1, B of unit u + 2 (the next tile's first k-tiles at the end;
-    // the current unit again past the range's end)
-    const bool an = t + 1 >= nk, bn = t + 2 >= nk;
-    const bool aok = u + 1 < u1, bok = u + 2 < u1;
-    const int at = !aok ? t : (an ? t + 1 - nk : t + 1), bt = !bok ? t : (bn ? t + 2 - nk : t + 2);
+    // DMA targets: A of unit u + 1, B of unit u + 2 (the next job's first k-tiles at the end — it
+    // has >= 2; the current unit again past the last job's end)
+    const bool an = t + 1 >= cur.k1, bn = t + 2 >= cur.k1;
+    const bool aok = !an || has_next, bok = !bn || has_next;
+    const int at = !aok ? t : (an ? nxt.k0 : t + 1), bt = !bok ? t : (bn ? nxt.k0 + (t + 2 - cur.k1) : t + 2);
     const TileInfo& ta = aok && an ? nxt : cur;
     const TileInfo& tb = bok && bn ? nxt : cur;
 #pragma unroll
@@ -380,14 +441,104 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
 
   using Z = std::integral_constant<int, 0>;
   bool after_epi = false;
-  int j = 0;
-  TileInfo cur = tile_of(p, tmap(0));
-  for (int u = u0; u < u1; u += nk) {
-    const TileInfo nxt = tile_of(p, tmap(j + 1 < nT ? j + 1 : j));
-    if constexpr (CONV) conv_info(nxt, crow_n);  // for the A issues of this tile's last k-tile
-    if (after_epi) ktile(u, 0, cur, nxt, std::true_type{}, std::integral_constant<int, kEpiVm>{});
-    else ktile(u, 0, cur, nxt, std::true_type{}, Z{});
-    for (int t = 1; t < nk; ++t) ktile(u + t, t, cur, nxt, std::false_type{}, Z{});
+  bool staggered = true;  // waves 4-7 one barrier behind (undone around a split tile's fix-up)
+  int* const lds_flag = reinterpret_cast<int*>(smem + kFlagOff);
+  int u = 0;
+  for (int jb = 0; jb < nJ; ++jb) {
+    const bool has_next = jb + 1 < nJ;
+    const TileInfo nxt = job_of(has_next ? jb + 1 : jb);
+    if constexpr (CONV) conv_info(nxt, crow_n);  // for the A issues of this job's last k-tile
+    if (!staggered) {  // re-stagger after a fix-up: waves 4-7 fall one barrier behind again
+      if (wr == 1) __builtin_amdgcn_s_barrier();
+      staggered = true;
+    }
+    if (after_epi) ktile(u, cur.k0, cur, nxt, has_next, std::true_type{}, std::integral_constant<int, kEpiVm>{});
+    else ktile(u, cur.k0, cur, nxt, has_next, std::true_type{}, Z{});
+    ++u;
+    for (int t = cur.k0 + 1; t < cur.k1; ++t, ++u) ktile(u, t, cur, nxt, has_next, std::false_type{}, Z{});
+
+    // ---- split tile: every piece stores its fp32 accumulators write-through (sc1) into its
+    // workspace slot; after every wave's stores have completed (vmcnt(0) + barrier) one lane takes
+    // an arrival ticket (agent-scope atomic); the workgroup that arrives last sums ALL pieces'
+    // slots in piece order (deterministic: the same sum whichever arrives last; its own piece
+    // re-read too) with sc1 loads and runs the epilogue; the others move on. No workgroup ever
+    // waits for another (no residency assumption). Hand-off form: MI355X_MICROARCH.md
+    // "Valid forms" table, row 1 (sc1 stores + drained waits + last-add ticket + sc1 loads).
+    bool do_epi = true;
+    if (cur.r >= 0) {
+      const int x0 = cur.r * nk;
+      const int wlo = __builtin_amdgcn_readfirstlane(tp.wg_of(x0)), whi = __builtin_amdgcn_readfirstlane(tp.wg_of(x0 + nk - 1));
+      const int P = whi - wlo + 1;
+      if (P > 1) {
+        if (wr == 0) __builtin_amdgcn_s_barrier();  // unstagger: all 8 waves at the same barrier count
+        staggered = false;
+        const int xcd = blockIdx.x % 8;
+        auto slot_rsrc = [&](int w) {
+          const int qw = cur.r - tp.bnd(w) / nk;
+          const int64_t slot = static_cast<int64_t>(w * 8 + xcd) * p.max_q + qw;
+          const uint64_t a = reinterpret_cast<uint64_t>(reinterpret_cast<char*>(p.ws) + slot * kSlotBytes);
+          const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
+          const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
+          return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo), 0,
+                                                   kSlotBytes, 0x00020000);
+        };
+        // + 1 KiB per accumulator register (opaque: not hoisted out of the job loop, no VGPR kept live)
+        const int pvo = (wave * 32 * 64 + opaque(lane)) * 16;
+        {
+          const __amdgpu_buffer_rsrc_t ms = slot_rsrc(tp.pos);
+#pragma unroll
+          for (int ph = 0; ph < 4; ++ph)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+              for (int jj = 0; jj < 4; ++jj)
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, acc[ph][i][jj]), ms,
+                                                       pvo + 1024 * (8 * ph + 4 * i + jj), 0, 16 /* sc1 */);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (threadIdx.x == 0) {
+          const int tk = __hip_atomic_fetch_add(p.counters + cur.id, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const int last = tk == P - 1 ? 1 : 0;
+          if (last) __hip_atomic_store(p.counters + cur.id, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(lds_flag, last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        do_epi = __builtin_amdgcn_readfirstlane(__hip_atomic_load(lds_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != 0;
+        if (do_epi) {
+          for (int pc = 0; pc < P; ++pc) {  // piece order
+            const __amdgpu_buffer_rsrc_t rs = slot_rsrc(wlo + pc);
+            if (pc == 0) {
+#pragma unroll
+              for (int ph = 0; ph < 4; ++ph)
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                  for (int jj = 0; jj < 4; ++jj)
+                    acc[ph][i][jj] = __builtin_bit_cast(
+                        f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, pvo + 1024 * (8 * ph + 4 * i + jj), 0, 16));
+            } else {
+#pragma unroll
+              for (int ph = 0; ph < 4; ++ph) {  // 8 loads in flight per batch (32 VGPRs)
+                f32x4 tmp[2][4];
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                  for (int jj = 0; jj < 4; ++jj)
+                    tmp[i][jj] = __builtin_bit_cast(
+                        f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, pvo + 1024 * (8 * ph + 4 * i + jj), 0, 16));
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                  for (int jj = 0; jj < 4; ++jj) acc[ph][i][jj] += tmp[i][jj];
+              }
+            }
+          }
+        }
+      }
+    }
+    if (do_epi) {
 
     // ---- epilogue. acc[ph][i][j][r] = C[m0 + wr*128 + 32ph + 16i + (lane & 15)][n0 + wc*64 + 16j + 4(lane >> 4) + r].
     // The rounded values are exchanged between lane rows g and g ^ 1 (v_permlane16_swap: row 2k
@@ -438,6 +589,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
     auto rowblk = [&](int ph, int ii) { return __builtin_amdgcn_readfirstlane((32 * ph + 16 * ii) * ldcb); };
     const __amdgpu_buffer_rsrc_t crs = tile_rsrc(p.c);
     i32x4 hv[4][2][2];  // EPI 2: every GELU derivative of the tile's lane issued before the first use (one round trip)
+#ifndef GNT_DBG_HVLATE
     if (EPI == 2) {
       const __amdgpu_buffer_rsrc_t hrs = tile_rsrc(p.h);
 #pragma unroll
@@ -447,8 +599,18 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
 #pragma unroll
           for (int q = 0; q < 2; ++q) hv[ph][ii][q] = __builtin_amdgcn_raw_buffer_load_b128(hrs, vo + 64 * q, rowblk(ph, ii), 0);
     }
+#endif
 #pragma unroll
     for (int ph = 0; ph < 4; ++ph) {
+#ifdef GNT_DBG_HVLATE
+      if (EPI == 2) {
+        const __amdgpu_buffer_rsrc_t hrs = tile_rsrc(p.h);
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+          for (int q = 0; q < 2; ++q) hv[ph][ii][q] = __builtin_amdgcn_raw_buffer_load_b128(hrs, vo + 64 * q, rowblk(ph, ii), 0);
+      }
+#endif
 #pragma unroll
       for (int ii = 0; ii < 2; ++ii) {
         uint32_t lo[4], hi[4];  // bf16 pairs (columns r 0-1 / 2-3) of each block j, this lane's columns
@@ -499,6 +661,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
             i32x4 gv;
             __builtin_memcpy(&gv, gg, 16);
             __builtin_amdgcn_raw_buffer_store_b128(gv, tile_rsrc(p.c2), vo + 64 * q, rowblk(ph, ii), 0);
+            store_guard();
             __builtin_memcpy(&out, dd, 16);
           } else if (EPI == 2) {
             // dh = bf16(dg) * gelu'(h), the derivative read as the forward epilogue (EPI 1) stored it
@@ -512,6 +675,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
             __builtin_memcpy(&out, oo, 16);
           }
           __builtin_amdgcn_raw_buffer_store_b128(out, crs, vo + 64 * q, rowblk(ph, ii), 0);
+          store_guard();
         }
       }
     }
@@ -534,7 +698,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
       }
     }
     if (EPI == 3 && fr_e == 0) {  // one atomic per column per wave row into the tile's statistics shard
-      float* shard = p.stats + static_cast<int64_t>(tmap(j) % kShards) * 2 * p.N + cur.n0() + colx;
+      float* shard = p.stats + static_cast<int64_t>(cur.id % kShards) * 2 * p.N + cur.n0() + colx;
 #pragma unroll
       for (int q = 0; q < 2; ++q)
 #pragma unroll
@@ -543,13 +707,13 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
           atomicAdd(shard + p.N + 32 * q + e, cq2[q][e]);
         }
     }
+    }  // do_epi
     ++seg;
     after_epi = true;
-    ++j;
     cur = nxt;
     if constexpr (CONV) crow = crow_n;
   }
-  if (wr == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
+  if (staggered && wr == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the dead-slot DMAs
 }
 
@@ -585,15 +749,6 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restr
   }
 }
 
-// FLUXMPI_GEMM_NT_ORDER: 1 (default) XCD-interleaved tile order, 0 contiguous ranges (A/B)
-int tile_order() {
-  static const int v = [] {
-    const char* e = std::getenv("FLUXMPI_GEMM_NT_ORDER");
-    return e != nullptr && e[0] == '0' ? 0 : 1;
-  }();
-  return v;
-}
-
 int cus() {
   static int n = 0;
   if (n == 0) {
@@ -604,19 +759,97 @@ int cus() {
   return n;
 }
 
-// one persistent workgroup per CU (fewer when there are fewer tiles than CUs)
-int grid_of(const NTArgs& p) {
+// FLUXMPI_GEMM_NT_SPLIT: the fewest k-tiles of a workgroup's share of the split tail (default 8;
+// 0: no split). Shapes with an odd k-tile count or fewer than 16 k-tiles are never split.
+int g_split_min = -1;  // < 0: not yet read from the environment
+
+int split_norm(int x) { return x <= 0 ? 0 : (x < 2 ? 2 : x + (x & 1)); }
+
+int split_min() {
+  if (g_split_min < 0) {
+    const char* e = std::getenv("FLUXMPI_GEMM_NT_SPLIT");
+    g_split_min = split_norm(e != nullptr ? std::atoi(e) : 8);
+  }
+  return g_split_min;
+}
+
+// The split-tail workspace of the current device: fp32 partial slots and per-tile arrival
+// counters (zeroed once; each split tile's last arriver resets its counter). One per device:
+// gemm_nt launches are ordered on the compute stream (the DDP comm stream runs no GEMM), so no
+// two launches use it at once. Grown outside stream capture only (warm-up calls size it).
+struct SplitWs {
+  float* ws = nullptr;
+  size_t ws_bytes = 0;
+  int* counters = nullptr;
+  size_t n_counters = 0;
+};
+
+bool split_workspace(size_t ws_bytes, size_t n_counters, hipStream_t stream, float** ws, int** counters) {
+  static SplitWs per_dev[64];
+  int dev = 0;
+  FLUXMPI_HIP_CHECK(hipGetDevice(&dev));
+  SplitWs& w = per_dev[dev & 63];
+  if (w.ws_bytes < ws_bytes || w.n_counters < n_counters) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    FLUXMPI_HIP_CHECK(hipStreamIsCapturing(stream, &cs));
+    if (cs != hipStreamCaptureStatusNone) return false;  // no allocation inside a capture: run unsplit
+    if (w.ws_bytes < ws_bytes) {
+      if (w.ws != nullptr) FLUXMPI_HIP_CHECK(hipFree(w.ws));  // implicit device sync: no launch still reads it
+      FLUXMPI_HIP_CHECK(hipMalloc(&w.ws, ws_bytes));
+      w.ws_bytes = ws_bytes;
+    }
+    if (w.n_counters < n_counters) {
+      if (w.counters != nullptr) FLUXMPI_HIP_CHECK(hipFree(w.counters));
+      FLUXMPI_HIP_CHECK(hipMalloc(&w.counters, n_counters * sizeof(int)));
+      FLUXMPI_HIP_CHECK(hipMemsetAsync(w.counters, 0, n_counters * sizeof(int), stream));
+      w.n_counters = n_counters;
+    }
+  }
+  *ws = w.ws, *counters = w.counters;
+  return true;
+}
+
+// grid and split-tail setup: one persistent workgroup per CU (fewer when there are fewer tiles
+// than CUs and no split); with a split tail every CU takes part and p.max_q / ws / counters are set
+int setup_grid(NTArgs& p, hipStream_t stream) {
   const int64_t tiles = static_cast<int64_t>(p.tiles_m) * p.tiles_n;
-  return static_cast<int>(tiles < cus() ? tiles : cus());
+  const int n = cus();
+  p.split = 0, p.split_min = 2, p.max_q = 0, p.ws = nullptr, p.counters = nullptr;
+  const int sm = split_min();
+  if (sm > 0 && p.nk % 2 == 0 && p.nk >= 16 && tiles % n != 0) {
+    const int G = n;
+    int max_q = 0;
+    for (int b = 0; b < G && b < 8; ++b) {  // every XCD's plan (positions 0..nw-1)
+      for (int pos = 0;; ++pos) {
+        const int bb = pos * 8 + b;
+        if (bb >= G) break;
+        const TailPlan t = tail_plan(static_cast<int>(tiles), G, p.nk, 1, sm, bb);
+        if (t.e > t.s) {
+          const int q = (t.e - 1) / p.nk - t.s / p.nk + 1;
+          max_q = q > max_q ? q : max_q;
+        }
+      }
+    }
+    if (max_q > 0) {
+      float* ws = nullptr;
+      int* cnt = nullptr;
+      if (split_workspace(static_cast<size_t>(G) * max_q * kSlotBytes, static_cast<size_t>(tiles), stream, &ws, &cnt)) {
+        p.split = 1, p.split_min = sm, p.max_q = max_q, p.ws = ws, p.counters = cnt;
+        return G;
+      }
+    }
+  }
+  return static_cast<int>(tiles < n ? tiles : n);
 }
 
 template <int EPI, int BIAS, bool CONV = false>
-void launch(const NTArgs& p, hipStream_t stream) {
+void launch(NTArgs& p, hipStream_t stream) {
+  const int grid = setup_grid(p, stream);
   if constexpr (EPI == 1) {  // the GELU form is compiled in (its constants would stay live otherwise)
-    if (p.gelu_tanh) gemm_nt_kernel<EPI, BIAS, CONV, 1><<<grid_of(p), kThreads, 0, stream>>>(p);
-    else gemm_nt_kernel<EPI, BIAS, CONV, 0><<<grid_of(p), kThreads, 0, stream>>>(p);
+    if (p.gelu_tanh) gemm_nt_kernel<EPI, BIAS, CONV, 1><<<grid, kThreads, 0, stream>>>(p);
+    else gemm_nt_kernel<EPI, BIAS, CONV, 0><<<grid, kThreads, 0, stream>>>(p);
   } else {
-    gemm_nt_kernel<EPI, BIAS, CONV><<<grid_of(p), kThreads, 0, stream>>>(p);
+    gemm_nt_kernel<EPI, BIAS, CONV><<<grid, kThreads, 0, stream>>>(p);
   }
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
@@ -637,6 +870,8 @@ bool gemm_nt_conv_supported(int64_t pixels, int64_t C, int64_t Cout) {
   return C > 0 && C % kBK == 0 && pixels * C * 2 < (int64_t(1) << 31) &&
          gemm_nt_supported(pixels, Cout, 9 * C, 9 * C, 9 * C, Cout);
 }
+
+void gemm_nt_set_split(int min_ktiles) { g_split_min = split_norm(min_ktiles); }
 
 int gemm_nt_colpart_rows(int64_t M) { return static_cast<int>(2 * (M / kT)); }
 
@@ -661,7 +896,6 @@ void gemm_nt(const void* a, const void* b, void* c, void* c2, const void* bias, 
   p.stats = stats, p.lda = lda, p.ldb = ldb, p.ldc = ldc, p.N = N;
   p.nk = static_cast<int>(K / kBK), p.tiles_m = static_cast<int>(M / kT), p.tiles_n = static_cast<int>(N / kT);
   p.bias_f32 = bias_f32, p.gelu_tanh = gelu_form();
-  p.order = tile_order();
   const int bk = bias == nullptr ? 0 : bias_f32 ? 1 : 2;
   if (epi == 3) {
     launch<3, 0>(p, stream);
@@ -693,7 +927,6 @@ void gemm_nt_conv(const void* x, const void* w, void* y, float* stats, int64_t n
   p.stats = stats, p.lda = 9 * C, p.ldb = 9 * C, p.ldc = Cout, p.N = Cout;
   p.nk = 9 * C / kBK, p.tiles_m = static_cast<int>(pixels / kT), p.tiles_n = static_cast<int>(Cout / kT);
   p.gelu_tanh = 0;
-  p.order = tile_order();
   p.conv_h = H, p.conv_w = W, p.conv_c = C, p.conv_cpt = C / kBK;
   p.conv_inv_cpt = 1.f / static_cast<float>(C / kBK);
   p.a_bytes = static_cast<uint32_t>(pixels * C * 2);

@@ -66,8 +66,9 @@ def _obj_for(src: str) -> str:
 
 # per-file extra flags: no SLP vectorisation in the MFMA kernels — plain -O3 packs adjacent f32
 # math (epilogues, softmax, operand prologues) into v_pk_*_f32, an anti-lever beside MFMAs
-# (MI355X_MICROARCH.md price list); in gemm_nt.hip that build also produced NaNs in the GELU
-# derivative epilogue. The memory-bound elementwise kernels keep it (fewer instructions).
+# (MI355X_MICROARCH.md price list). For speed only: the round-4 NaNs of the SLP gemm_nt build were
+# an epilogue store-data hazard, fixed in the source (gemm_nt.hip store_guard; the SLP build is
+# clean: profiles/rd5c_gemm_nt_store_hazard.md). The memory-bound elementwise kernels keep it.
 _NO_SLP = ["-fno-slp-vectorize"]
 EXTRA_FLAGS = {f: _NO_SLP for f in ("gemm_nt.hip", "attention.hip", "gemm_glds.hip", "gemm.hip")}
 

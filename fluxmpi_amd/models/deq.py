@@ -23,7 +23,9 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import anderson as AO
-from ..ops.fused_block import conv3x3, conv3x3_supported
+from ..ops.conv_small import conv3x3_small
+from ..ops.fused_block import conv3x3, conv3x3_s2, conv3x3_s2_supported, conv3x3_supported
+from ..ops.linear import Linear
 from ..ops.batchnorm import FusedBatchNorm2d, GradLink
 from ..ops.groupnorm import FusedGroupNorm, fp32_affine_cache, skip_param_grads
 from ..ops.groupnorm import native_ok as gn_native_ok
@@ -40,6 +42,9 @@ MANUAL_VJP = os.environ.get("FLUXMPI_DEQ_MANUAL_VJP", "1") != "0"
 # FLUXMPI_DEQ_GRAPH_CHUNK: adjoint iterations per graph replay
 GRAPHS = os.environ.get("FLUXMPI_DEQ_GRAPH", "1") != "0"
 GRAPH_CHUNK = int(os.environ.get("FLUXMPI_DEQ_GRAPH_CHUNK", "5"))
+# DEQ-CIFAR solver settings (bench.py --deq-solver overrides): relative-residual tolerances the
+# Anderson forward and the adjoint fixed point reach before their iteration caps
+DEQ_CIFAR_SOLVER = {"max_iter": 30, "tol": 1e-4, "bwd_iter": 30, "bwd_tol": 1e-4}
 
 
 # host seconds spent blocked on convergence flags (LaggedFlags.pop_ready), cumulative: bench.py
@@ -596,14 +601,23 @@ class DEQCifar(nn.Module):
         self.stem1_norm = FusedBatchNorm2d(c0)
         self.stem2 = nn.Conv2d(c0, ch, 3, stride=2, padding=1, bias=False)
         self.inj_norm = FusedBatchNorm2d(ch)
+        for k, v in DEQ_CIFAR_SOLVER.items():
+            solver.setdefault(k, v)
         self.deq = DEQFixedPoint(ResidualCell(ch, groups), **solver)
         self.out_norm = FusedBatchNorm2d(ch)
-        self.head = nn.Linear(ch, num_classes)
+        self.head = Linear(ch, num_classes)  # ops.linear.Linear: dW / db born in their bucket slices
 
     def forward(self, x):
-        x = F.relu(self.stem1_norm(self.stem1(x)))
-        x = self.inj_norm(self.stem2(x))
-        z = self.out_norm(self.deq(x))
+        # every parameter gradient is produced in its DDP bucket slice (ops/graddst.py): the
+        # 3-channel stem's filter gradient by one GEMM (ops/conv_small.py), the stride-2 stem on
+        # the implicit-GEMM path (fused_block.conv3x3_s2), BatchNorm / GroupNorm dw, db and the
+        # head's dW, db by their own backward kernels
+        x = self.stem1_norm(conv3x3_small(x, self.stem1), relu=True)
+        if conv3x3_s2_supported(x, self.stem2):
+            x = conv3x3_s2(x, self.stem2.weight)
+        else:
+            x = self.stem2(x)
+        z = self.out_norm(self.deq(self.inj_norm(x)))
         return self.head(F.adaptive_avg_pool2d(z, 1).flatten(1))
 
 

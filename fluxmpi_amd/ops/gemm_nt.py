@@ -71,6 +71,14 @@ def supported(rows: int, n_out: int, k: int, *tensors: torch.Tensor, fused: bool
     return C is not None and hasattr(C, "gemm_nt") and bool(C.gemm_nt_supported(rows, n_out, k, k, k, n_out))
 
 
+def set_split(min_ktiles: int) -> None:
+    """The split-K tail of the persistent kernel (``FLUXMPI_GEMM_NT_SPLIT``, default 8): the last,
+    partial round of each XCD's tiles is cut into even k-tile ranges of at least ``min_ktiles``
+    spread over all its workgroups (pieces summed by the last arriving workgroup, in piece order:
+    deterministic); ``0`` runs the last round tile-granular."""
+    _ext.get(required=True).gemm_nt_set_split(int(min_ktiles))
+
+
 def weight_t(weight: torch.Tensor) -> torch.Tensor:
     """``weight.t().contiguous()`` by the 16-B-vector transpose kernel."""
     C = _ext.get(required=True)
@@ -194,5 +202,5 @@ def gemm_plain(a2: torch.Tensor, b2: torch.Tensor, c2: torch.Tensor, stats: torc
     return c2
 
 
-__all__ = ["supported", "weight_t", "linear_fwd", "linear_dgrad", "conv_ok", "gemm_ok", "conv3x3", "gemm_plain",
+__all__ = ["supported", "set_split", "weight_t", "linear_fwd", "linear_dgrad", "conv_ok", "gemm_ok", "conv3x3", "gemm_plain",
            "ENABLED", "MODE", "CONV"]

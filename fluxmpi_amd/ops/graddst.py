@@ -125,6 +125,18 @@ def empty_like(p: torch.Tensor, dtype: torch.dtype | None = None) -> torch.Tenso
     return torch.empty_like(p, dtype=dt)
 
 
+def deliver(p: torch.Tensor | None, value: torch.Tensor, dtype: torch.dtype | None = None) -> torch.Tensor:
+    """``value.to(dtype or p.dtype)`` written straight into ``p``'s bucket slice when one is
+    available (the cast a reduction result needs anyway becomes the delivery: no separate pack
+    copy later), else the plain cast."""
+    dt = dtype or (p.dtype if p is not None else value.dtype)
+    t = take(p, tuple(value.shape), dt) if p is not None else None
+    if t is None:
+        return value.to(dt)
+    t.copy_(value)
+    return t
+
+
 def delivered(p: torch.Tensor) -> bool:
     """True if ``p.grad`` lies in ``p``'s destination slice (diagnostics / tests)."""
     d = getattr(p, _ATTR, None)

@@ -14,6 +14,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _ext
+from . import graddst
 from .multi_tensor import DTYPE_CODE
 
 
@@ -141,6 +142,7 @@ class _GroupNormFn(torch.autograd.Function):
         ctx.save_for_backward(saved, mean, rstd, w32)
         ctx.cfg = (groups, bool(relu), add is not None,
                    weight.dtype if weight is not None else None, bias.dtype if bias is not None else None)
+        ctx.params = (weight, bias)  # the leaves: their gradients' DDP bucket slices (graddst)
         ctx.link = link
         return y
 
@@ -150,8 +152,10 @@ class _GroupNormFn(torch.autograd.Function):
         groups, relu, has_add, wd, bd = ctx.cfg
         dh, part = gn_bwd_raw(dy, h, mean, rstd, w32, groups, relu)
         want = not _SKIP_PARAM_GRADS
-        dw = part[:, 0].sum(0).to(wd) if want and wd is not None and ctx.needs_input_grad[2] else None
-        db = part[:, 1].sum(0).to(bd) if want and bd is not None and ctx.needs_input_grad[3] else None
+        # the per-sample sums reduced and cast straight into the parameters' DDP bucket slices
+        wp, bp = ctx.params
+        dw = graddst.deliver(wp, part[:, 0].sum(0), wd) if want and wd is not None and ctx.needs_input_grad[2] else None
+        db = graddst.deliver(bp, part[:, 1].sum(0), bd) if want and bd is not None and ctx.needs_input_grad[3] else None
         dx = dh
         if ctx.link is not None and ctx.needs_input_grad[0]:
             # x's other consumer (a convolution holding the same link) adds dh in its dgrad epilogue

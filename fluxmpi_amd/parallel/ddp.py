@@ -96,6 +96,7 @@ class _Bucket:
     names: list = field(default_factory=list)
     comm_buf: torch.Tensor | None = None
     carry: torch.Tensor | None = None
+    applied: bool = False  # overlap_opt: this step's update already enqueued (during backward)
 
 
 def _strided_view(flat: torch.Tensor, like: torch.Tensor, offset: int) -> torch.Tensor:
@@ -133,6 +134,14 @@ class DDP:
     average: divide the summed gradient by the world size (default False = reference SUM).
     overlap: launch bucket allreduces from backward hooks (default: ``FLUXMPI_OVERLAP``).
     broadcast: synchronise parameters and buffers from ``root_rank`` at construction.
+    overlap_opt: per-bucket optimiser overlap (default ``FLUXMPI_OVERLAP_OPT``): as soon as a
+            bucket's gradients are complete (and, when communicating, its allreduce is enqueued)
+            its fused update is enqueued behind it — on the communicator's in-order stream, or on
+            a side stream at world 1 — instead of after the whole backward in ``step()``. Safe
+            because a bucket is complete only after every backward node that reads its
+            parameters has run (a parameter's post-accumulate hook fires once, after all its
+            uses); ``step()`` then only fences. Contract: every backward that completes buckets
+            is followed by ``step()`` (no inspection of reduced-but-unapplied gradients).
     """
 
     def __init__(self, module: torch.nn.Module, rule: O.AbstractRule | None = None, *,
@@ -141,7 +150,7 @@ class DDP:
                  broadcast: bool = True, root_rank: int = 0, comm: Communicator | None = None,
                  comm_dtype: torch.dtype | None = None, watchdog: bool | None = None,
                  grad_mode: str | None = None, force_comm: bool | None = None,
-                 tail_bucket_mb: float | None = None):
+                 tail_bucket_mb: float | None = None, overlap_opt: bool | None = None):
         cfg = get_config()
         # "steal": autograd hands over each freshly produced gradient (no in-place accumulate
         # kernel per parameter, no zero fill) and one multi-tensor launch per bucket packs them
@@ -202,7 +211,18 @@ class DDP:
                     graddst.detach(p)  # a previous engine's buckets are not this one's
         self._hooks = []
         self._sync_enabled = True
-        if self.overlap and self.communicate:
+        # per-bucket optimiser overlap: on the communicator's in-order stream (behind the bucket's
+        # allreduce) when it has one, on a side stream when nothing is communicated, else in
+        # step() (host-synchronous collectives: nothing to overlap with)
+        want_opt = cfg.overlap_opt if overlap_opt is None else bool(overlap_opt)
+        self.overlap_opt = want_opt and self.overlap and self.grad_mode == "steal"
+        self._opt_stream = None  # None: the update runs right after the (host-waited) reduction
+        if self.overlap_opt and self.device.type == "cuda":
+            if not self.communicate:
+                self._opt_stream = torch.cuda.Stream(self.device)
+            elif getattr(comm, "in_order", False) and getattr(comm, "stream", None) is not None:
+                self._opt_stream = comm.stream
+        if self.overlap and (self.communicate or self.overlap_opt):
             for p in params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad_ready))
         self._setup_optimizer()
@@ -396,9 +416,45 @@ class DDP:
         if b.launched:
             return
         b.launched = True
-        if not self.communicate:
+        if self.overlap_opt and not self._masters_synced:
+            self._sync_masters()  # outside edits reach the masters before the step's first update
+            self._masters_synced = True
+        if self.communicate:
+            self._launch_comm(b)
+        if self.overlap_opt:
+            self._apply_overlapped(b)
+
+    def _apply_overlapped(self, b: _Bucket):
+        """Enqueue bucket ``b``'s update now. Communicating: behind its allreduce on the in-order
+        comm stream (stream order is the dependency: no fence, no host wait). World 1: on the
+        side stream, after an event on the compute stream (the bucket's gradients are produced
+        there) — the compute stream goes on with backward."""
+        gscale = 1.0 / self.world if self.average else 1.0
+        st = self._opt_stream
+        if st is None:
+            # no in-order device stream (CPU tensors, gloo on device tensors): wait for the
+            # reduction here, then update on the current stream — the same order, no overlap
+            if self.communicate:
+                self._finish(b)
+                self._add_carry(b)
+                self._apply(b, gscale)
+            elif not self._apply_direct(b, gscale):
+                self._pack(b)
+                self._apply(b, gscale)
+            b.applied = True
             return
-        self._launch_comm(b)
+        if not self.communicate:
+            st.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(st):
+            if self.communicate:
+                if b.comm_buf is not None and self.comm_dtype != b.dtype:
+                    mt.unpack(b.comm_buf, [b.flat_grad], [0])
+                self._add_carry(b)
+                self._apply(b, gscale)
+            elif not self._apply_direct(b, gscale):
+                self._pack(b)
+                self._apply(b, gscale)
+        b.applied = True
 
     def _launch_comm(self, b: _Bucket):
         self._pack(b)
@@ -446,12 +502,13 @@ class DDP:
         """Reset the per-step bucket state (countdowns, launch/pack flags) for the next backward."""
         for b in self.buckets:
             b.pending = len(b.params)
-            b.ready = b.launched = b.packed = False
+            b.ready = b.launched = b.packed = b.applied = False
             b.work = None
             if getattr(self, "direct_grads", False):
                 for p in b.params:
                     graddst.rearm(p)
         self._next_launch = 0
+        self._masters_synced = False
 
     def _note_copy(self, p) -> None:
         self.pack_copies += 1
@@ -514,6 +571,9 @@ class DDP:
 
     def reduce_gradients(self):
         """Make sure every bucket has been allreduced (launch the rest, in order) and wait."""
+        if self.overlap_opt:
+            raise RuntimeError("DDP.reduce_gradients: with overlap_opt the updates run with the "
+                               "reductions; call step() (or build the engine with overlap_opt=False)")
         for b in self.buckets:
             b.ready = True
         self._launch_ready()
@@ -590,9 +650,14 @@ class DDP:
         step is the sum over ranks of both backwards' gradients (see ``_arm_carry``).
         """
         gscale = 1.0 / self.world if self.average else 1.0
-        self._sync_masters()
+        if not (self.overlap_opt and self._masters_synced):
+            self._sync_masters()
         if self._carry_hook is not None:
             self._start_carry()  # no forward since step(zero_grad=False): no new local gradient
+        if self.overlap_opt:
+            self._step_overlapped()
+            self._finish_step(zero_grad)
+            return
         if not self.communicate and self.grad_mode == "steal":
             # nothing to reduce: the optimiser reads autograd's gradients where they are
             for b in self.buckets:
@@ -628,6 +693,29 @@ class DDP:
                 self._add_carry(b)
                 self._apply(b, gscale)
         self._finish_step(zero_grad)
+
+    def _step_overlapped(self):
+        """step() with the per-bucket updates already enqueued during backward: enqueue the
+        rest (buckets whose hooks did not complete them: unused parameters, no_sync), then ONE
+        compute-stream fence on the optimiser stream (in order: it covers every bucket's
+        allreduce and update)."""
+        for b in self.buckets:
+            if not b.launched:
+                b.ready = True
+        if self.timing and self.communicate:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+        self._launch_ready()
+        if self._opt_stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._opt_stream)
+        for b in self.buckets:
+            if b.work is not None:
+                b.work.covered() if hasattr(b.work, "covered") else b.work.wait()
+                b.work = None
+        if self.timing and self.communicate:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self._comm_events.append((e0, e1))
 
     def _finish_step(self, zero_grad: bool):
         if self.kind == "adam":
@@ -789,7 +877,7 @@ class DDP:
                 "buckets": len(self.buckets),
                 "bucket_mb": [round(b.numel * b.flat_grad.element_size() / 2 ** 20, 2) for b in self.buckets],
                 "comm": (self.comm.name if self.communicate else "none"),
-                "direct_grads": self.direct_grads,
+                "direct_grads": self.direct_grads, "overlap_opt": self.overlap_opt,
                 # gradients the packs copied per step so far (0: every one delivered in place)
                 "pack_copies_per_step": round(self.pack_copies / max(1, self.step_count), 2),
                 # the parameter shapes the packs copied (total over the steps so far), most first

@@ -35,6 +35,10 @@ Environment knobs (all optional):
                            exercise and time the N>1 path on a single GPU
 ``FLUXMPI_DIRECT_GRADS``   ``1`` (default): the package's weight-gradient kernels
                            write straight into the DDP buckets (``ops/graddst``)
+``FLUXMPI_OVERLAP_OPT``    ``1``: the DDP engine updates each bucket as soon as its
+                           reduced gradient exists (comm stream / side stream),
+                           during the rest of backward; ``0`` (default): in
+                           ``step()``
 =========================  ==================================================
 """
 from __future__ import annotations
@@ -146,6 +150,7 @@ class Config:
     timeout_s: float = 600.0
     force_comm: bool = False
     direct_grads: bool = True  # ops write parameter gradients into their DDP bucket slices
+    overlap_opt: bool = False  # per-bucket optimiser update during backward (DDP)
     # cross-rank structure check of functional reduction plans: always / first / never
     check_plans: str = "always"
     extra: dict = field(default_factory=dict)
@@ -172,6 +177,7 @@ class Config:
             timeout_s=_env_float("FLUXMPI_TIMEOUT_S", 600.0),
             force_comm=_env_bool("FLUXMPI_FORCE_COMM", bool(prefs.get("force_comm", False))),
             direct_grads=_env_bool("FLUXMPI_DIRECT_GRADS", bool(prefs.get("direct_grads", True))),
+            overlap_opt=_env_bool("FLUXMPI_OVERLAP_OPT", bool(prefs.get("overlap_opt", False))),
             check_plans=os.environ.get("FLUXMPI_CHECK_PLANS", str(prefs.get("check_plans", "always"))).lower(),
             extra=prefs,
         )

@@ -2,6 +2,8 @@
 """gemm_nt.hip (ping-pong 8-wave 256x256 NT GEMM) vs hipBLASLt (torch), TFLOP/s on
 uniform [-1, 1) bf16 operands (cdna_hip_programming.md rule 25), interleaved rounds in one process.
 
+Split-K tail arms: nt_s<k> = the default kernel with FLUXMPI_GEMM_NT_SPLIT = k (0: off; nt = 8).
+
 Shapes: 4096^3 and the ViT-B/16 Linears at batch 256 (M = 50432 tokens), forward (x W^T),
 input gradient (dy W, ours on W^T), fc1 forward + bias + GELU (EPI 1), fc2 input gradient +
 GELU backward + bias-gradient partials (EPI 2). Every kernel is checked against an fp32 torch
@@ -121,6 +123,11 @@ def main():
         for rnd in range(3):
             best.setdefault("blas", []).append(t_us(lambda: torch.matmul(a, wt)))
             best.setdefault("blas_bias", []).append(t_us(lambda: torch.nn.functional.linear(a, w, bias.bfloat16())))
+            for sm in (0, 4, 16):  # the split-K tail's minimum share (0: the last round tile-granular)
+                C.gemm_nt_set_split(sm)
+                best.setdefault(f"nt_s{sm}", []).append(t_us(lambda: ours()))
+                best.setdefault(f"nt_epi2_s{sm}", []).append(t_us(lambda: ours(2, h=h, part=part)))
+            C.gemm_nt_set_split(8)
             best.setdefault("nt", []).append(t_us(lambda: ours()))
             best.setdefault("nt_bias", []).append(t_us(lambda: ours(0, bias_=bias)))
             best.setdefault("nt_gelu", []).append(t_us(lambda: ours(1, bias_=bias)))

@@ -30,6 +30,15 @@ for s in $STEPS; do
                    tests/test_gemm_nt_gpu.py tests/test_fused_block_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread ;;
     pytest_vit) step pytest_vit 600 1 python -u -m pytest tests/test_vit_model_gpu.py tests/test_vit_gpu.py tests/test_linear_gpu.py \
                    tests/test_gelu.py tests/test_layernorm.py -m gpu -x -q -s --timeout 300 --timeout-method thread ;;
+    pytest_nt) step pytest_nt 600 1 python -u -m pytest tests/test_gemm_nt_gpu.py -m gpu -x -v --timeout 120 \
+                 --timeout-method thread ;;
+    bench_nt) step bench_nt 600 0 python scripts/bench_gemm_nt.py ;;
+    bench_vit_all) step bench_vit_all 300 0 env FLUXMPI_GEMM_NT=all python bench.py --model vit_b16 --steps "$BENCH_STEPS" \
+                     --warmup "$BENCH_WARMUP" ;;
+    bench_vit_nosplit) step bench_vit_nosplit 300 0 env FLUXMPI_GEMM_NT_SPLIT=0 python bench.py --model vit_b16 \
+                         --steps "$BENCH_STEPS" --warmup "$BENCH_WARMUP" ;;
+    bench_nosplit) step bench_nosplit 300 0 env FLUXMPI_GEMM_NT_SPLIT=0 python bench.py --steps "$BENCH_STEPS" \
+                     --warmup "$BENCH_WARMUP" ;;
     smoke) step smoke 240 0 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 300 0 python bench.py --steps "$BENCH_STEPS" --warmup "$BENCH_WARMUP" ;;
     bench_graph) step bench_graph 300 0 python bench.py --steps "$BENCH_STEPS" --warmup "$BENCH_WARMUP" --graph ;;

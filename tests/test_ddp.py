@@ -432,3 +432,44 @@ def test_engine_registry_does_not_keep_engines_alive():
     del d
     gc.collect()
     assert ref() is None and engine_for(model) is None
+
+
+def _opt_overlap_run(overlap_opt, rule_name, steps=3, rank=0, zero_grad_every=1):
+    from fluxmpi_amd import optimisers as O
+    from fluxmpi_amd.parallel.ddp import DDP
+    rule = {"adam": O.Adam(1e-2), "momentum": O.Momentum(0.05, 0.9)}[rule_name]
+    model = _mlp(7)
+    ddp = DDP(model, rule, bucket_mb=0.001, first_bucket_mb=0.0005, overlap=True, overlap_opt=overlap_opt,
+              average=True)
+    assert ddp.overlap_opt == overlap_opt
+    x, y = _data(rank)
+    for s in range(steps):
+        ((ddp(x) - y) ** 2).mean().backward()
+        ddp.step(zero_grad=(s % zero_grad_every == 0))
+    return [p.detach().clone() for p in model.parameters()]
+
+
+@pytest.mark.parametrize("rule_name", ["adam", "momentum"])
+def test_overlap_opt_world1_bitwise(rule_name):
+    """Per-bucket updates enqueued from the backward hooks == updates in step(), bit for bit."""
+    a = _opt_overlap_run(False, rule_name)
+    b = _opt_overlap_run(True, rule_name)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+
+
+def worker_overlap_opt():
+    import fluxmpi_amd as FluxMPI
+    FluxMPI.Init()
+    r = FluxMPI.local_rank()
+    for rule_name in ("adam", "momentum"):
+        for zge in (1, 2):  # 2: step(zero_grad=False) every other step (the carried reduced sum)
+            a = _opt_overlap_run(False, rule_name, steps=4, rank=r, zero_grad_every=zge)
+            b = _opt_overlap_run(True, rule_name, steps=4, rank=r, zero_grad_every=zge)
+            for x, y in zip(a, b):
+                assert torch.equal(x, y), (rule_name, zge)
+    FluxMPI.Finalize()
+
+
+def test_overlap_opt_two_ranks_gloo(spmd):
+    spmd("tests.test_ddp:worker_overlap_opt", nprocs=2, timeout=180)

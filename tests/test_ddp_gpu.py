@@ -81,3 +81,29 @@ def test_bf16_master_weights(gpu_ext):
     assert torch.isfinite(master).all()
     for n, p in m.named_parameters():
         torch.testing.assert_close(p.float(), ps[n], rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("force_comm", [False, True])
+def test_overlap_opt_bitwise_gpu(gpu_ext, force_comm):
+    """Per-bucket optimiser overlap (updates enqueued from the backward hooks: on the RCCL stream
+    behind each bucket's allreduce with force_comm, on a side stream at world 1) gives bit-identical
+    parameters to the updates in step(), with bf16 parameters + fp32 masters, several buckets."""
+    import fluxmpi_amd as FluxMPI
+    from fluxmpi_amd import optimisers as O
+    from fluxmpi_amd.parallel.ddp import DDP
+    FluxMPI.Init()
+    x = torch.randn(64, 32, device="cuda").bfloat16()
+    y = x.float().sum(1, keepdim=True).sin()
+    outs = []
+    for ov in (False, True):
+        m = _mlp(3).bfloat16()
+        d = DDP(m, O.Adam(1e-2), bucket_mb=0.004, first_bucket_mb=0.002, force_comm=force_comm, overlap_opt=ov,
+                average=True)
+        assert d.overlap_opt == ov and len(d.buckets) > 1
+        for _ in range(4):
+            ((d(x).float() - y) ** 2).mean().backward()
+            d.step()
+        torch.cuda.synchronize()
+        outs.append([p.detach().clone() for p in m.parameters()] + [b.master.clone() for b in d.buckets])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)

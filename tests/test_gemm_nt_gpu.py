@@ -189,3 +189,74 @@ def test_conv_routing_thresholds(gpu_ext):
     assert not G.conv_ok(12544, 512, 512, x)      # 7x7x512: 98 tiles
     assert G.gemm_ok(50176, 256, 1024, x)         # 1x1 1024 -> 256
     assert not G.gemm_ok(50176, 1024, 256, x)     # K = 256
+
+
+# ---- split-K tail (the last, partial round cut into k-ranges; pieces summed by the last arriver)
+SPLIT_SHAPES = [(M_VIT, 768, 3072), (M_VIT, 768, 2304), (256 * 300, 512, 1024), (256 * 37, 256, 4096),
+                (256 * 3, 256, 8192)]
+
+
+@pytest.fixture
+def split_mode():
+    from fluxmpi_amd.ops import gemm_nt as G
+    yield G.set_split
+    G.set_split(8)
+
+
+@pytest.mark.parametrize("m,n,k", SPLIT_SHAPES)
+def test_split_tail_matches_unsplit_and_is_deterministic(gpu_ext, split_mode, m, n, k):
+    from fluxmpi_amd.ops import gemm_nt as G
+    torch.manual_seed(3)
+    x = _uni(m, k)
+    w = _uni(n, k, scale=k ** -0.5)
+    b = (torch.randn(n, device="cuda") * 0.5).bfloat16()
+    ref = x.float() @ w.float().t() + b.float()
+    outs = {}
+    for sm in (0, 2, 8, 16):
+        split_mode(sm)
+        y1 = G.linear_fwd(x, w, b)
+        y2 = G.linear_fwd(x, w, b)
+        assert torch.equal(y1, y2), f"split {sm}: two launches differ (non-deterministic fix-up)"
+        assert _rel(y1, ref) < 5e-3, sm
+        outs[sm] = y1
+    # only the fp32 summation order differs: a few bf16 roundings flip by one ulp
+    for sm in (2, 8, 16):
+        d = (outs[sm].float() - outs[0].float()).abs()
+        assert float(d.max()) <= 2.0 ** -6 * float(outs[0].float().abs().max()), sm
+
+
+def test_split_tail_epilogues(gpu_ext, split_mode, gelu_form):
+    """EPI 1 (bias + GELU and its derivative), EPI 2 (GELU backward + bias-gradient partials) and
+    EPI 3 (BatchNorm statistics of a 3x3 convolution) through split tiles, against the unsplit run."""
+    from fluxmpi_amd.ops import gemm_nt as G
+    torch.manual_seed(4)
+    res = {}
+    for sm in (0, 2):
+        split_mode(sm)
+        _check_fwd(M_VIT, 768, 3072, "f32", gelu_form)
+        _check_dgrad(M_VIT, 3072, 768, gelu_form)
+        _check_dgrad(256 * 41, 768, 3072, gelu_form)
+        x = _uni(M_VIT, 3072)
+        w = _uni(768, 3072, scale=3072 ** -0.5)
+        res[sm] = G.linear_fwd(x, w, None, gelu=True)
+    for a, b in zip(res[0], res[2]):
+        assert _rel(a, b) < 1e-2
+
+
+def test_split_tail_conv_stats(gpu_ext, split_mode, any_shape):
+    from fluxmpi_amd.ops import gemm_nt as G
+    torch.manual_seed(5)
+    nimg, h, w_, c, co = 64, 14, 14, 256, 256  # 196 output tiles: every CU shares the tail
+    x = _uni(nimg, c, h, w_).contiguous(memory_format=torch.channels_last)
+    wt = _uni(co, c, 3, 3, scale=(9 * c) ** -0.5)
+    ref = torch.nn.functional.conv2d(x.float(), wt.float(), padding=1).permute(0, 2, 3, 1).reshape(-1, co)
+    taps = wt.permute(0, 2, 3, 1).reshape(co, 9 * c).contiguous()
+    for sm in (0, 8, 2):
+        split_mode(sm)
+        y = torch.empty(nimg * h * w_, co, device="cuda", dtype=torch.bfloat16)
+        st = torch.zeros(64, 2, co, device="cuda")
+        G.conv3x3(x, taps, y, st)
+        assert _rel(y, ref) < 5e-3, sm
+        s = st.sum(0)
+        torch.testing.assert_close(s[0], y.float().sum(0), rtol=2e-3, atol=0.5)
+        torch.testing.assert_close(s[1], (y.float() ** 2).sum(0), rtol=2e-3, atol=0.5)
