@@ -245,6 +245,12 @@ void gemm_nt(const void* a, const void* b, void* c, void* c2, const void* bias, 
 // x [nimg][H][W][C] (C % 64 == 0), B = w [Cout][3][3][C]; y [nimg*H*W][Cout]; epi 0 or 3 (statistics)
 void gemm_nt_conv(const void* x, const void* w, void* y, float* stats, int64_t nimg, int H, int W, int C,
                   int64_t Cout, int epi, hipStream_t stream);
+// Narrow-channel 3x3 / stride 1 / pad 1 convolution (conv3x3n.hip): C = Cout in {64, 128}, the
+// input halo staged once per 256-pixel workgroup; x [pixels][C] NHWC, w [Cout][9][C], y [pixels][Cout];
+// epi 0 or 3 (BatchNorm statistics into stats[64][2][Cout])
+bool conv3x3n_supported(int64_t pixels, int C, int Cout, int H, int W);
+void conv3x3n(const void* x, const void* w, void* y, float* stats, int64_t pixels, int H, int W, int C, int Cout,
+              int epi, hipStream_t stream);
 // dst[c][r] = src[r][c], bf16 (rows, cols, leading dims multiples of 8)
 void transpose_bf16(const void* src, void* dst, int64_t rows, int64_t cols, int64_t lds, int64_t ldd,
                     hipStream_t stream);

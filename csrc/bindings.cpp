@@ -309,6 +309,12 @@ PYBIND11_MODULE(_C, m) {
     gemm_nt(reinterpret_cast<const void*>(a), reinterpret_cast<const void*>(b), reinterpret_cast<void*>(c), nullptr,
             nullptr, 0, nullptr, nullptr, reinterpret_cast<float*>(stats), lda, ldb, ldc, M, N, K, 3, S(stream));
   });
+  m.def("conv3x3n_supported", &conv3x3n_supported);
+  m.def("conv3x3n", [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, int64_t pixels, int H, int W, int C,
+                       int Cout, int epi, uintptr_t stream) {
+    conv3x3n(reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(w), reinterpret_cast<void*>(y),
+             reinterpret_cast<float*>(stats), pixels, H, W, C, Cout, epi, S(stream));
+  });
   m.def("gemm_nt_conv_supported", &gemm_nt_conv_supported);
   m.def("gemm_nt_conv", [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, int64_t nimg, int H, int W, int C,
                            int64_t Cout, int epi, uintptr_t stream) {

@@ -739,14 +739,8 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_dx_dual_kernel(
   }
 }
 
-// vectors per lane per iteration of the elementwise BN kernels (FLUXMPI_BN_UNROLL: 2 or 4)
-int bn_unroll() {
-  static const int u = [] {
-    const char* e = std::getenv("FLUXMPI_BN_UNROLL");
-    return (e != nullptr && std::atoi(e) == 4) ? 4 : 2;
-  }();
-  return u;
-}
+// vectors per lane per iteration of the elementwise BN kernels: 2 (4 measured equal, round 4:
+// profiles/rd4ak_bench_bn_unroll_ab.jsonl — the passes run at 4.4-5.8 TB/s either way)
 
 // one full round of resident workgroups (or fewer if the tensor is small)
 int elementwise_grid(const void* kernel, size_t smem, int64_t nvec) {
@@ -793,7 +787,7 @@ void norm_t(const void* x, void* y, const void* res, const float* w, const float
 #define LAUNCH(RELU, RES, FX)                                                                                   \
   {                                                                                                            \
     const size_t sm = FX ? 0 : 2 * C * sizeof(float);                                                          \
-    auto k = bn_unroll() == 4 ? bn_norm_kernel<T, RELU, RES, FX, 4> : bn_norm_kernel<T, RELU, RES, FX, 2>;   \
+    auto k = bn_norm_kernel<T, RELU, RES, FX, 2>;   \
     k<<<elementwise_grid(reinterpret_cast<const void*>(k), sm, nvec), kThreads, sm, s>>>(                      \
         xr, yr, rr, w, b, mean, stat2, (int)C, eps, train, nvec, mask);                                        \
   }
@@ -858,7 +852,7 @@ void bwd_t(const void* dy, const void* x, const void* y, const uint8_t* mask, co
 #define LAUNCH(RM, DRES, FX)                                                                                    \
   {                                                                                                            \
     const size_t lds = FX ? 0 : C * sizeof(DxCoef);                                                            \
-    auto k = bn_unroll() == 4 ? bn_bwd_dx_kernel<T, RM, DRES, FX, 4> : bn_bwd_dx_kernel<T, RM, DRES, FX, 2>;   \
+    auto k = bn_bwd_dx_kernel<T, RM, DRES, FX, 2>;   \
     k<<<elementwise_grid(reinterpret_cast<const void*>(k), lds, nvec), kThreads, lds, s>>>(                    \
         dyr, xr, yr, mask, w, b, sm, si, dw, db, dxr, drr, rows, (int)C, nvec);                                \
   }

@@ -735,14 +735,8 @@ void gemm_bf16(const GemmProblem& g, hipStream_t stream) {
 #undef DISPATCH
 }
 
-// FLUXMPI_COLREDUCE=0: always the multi-launch tree (A/B)
-static bool colreduce_on() {
-  static const bool on = [] {
-    const char* e = std::getenv("FLUXMPI_COLREDUCE");
-    return e == nullptr || e[0] != '0';
-  }();
-  return on;
-}
+// the one-launch column reduce wherever it applies (the multi-launch tree otherwise)
+static bool colreduce_on() { return true; }
 
 namespace {
 template <typename TO>

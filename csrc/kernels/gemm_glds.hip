@@ -820,13 +820,6 @@ __global__ __launch_bounds__(kThreads) void xpose_taps_kernel(XposeArgs a) {
 }
 }  // namespace
 
-static bool narrow_k64() {
-  static const bool on = [] {
-    const char* e = std::getenv("FLUXMPI_NARROW_K64");
-    return e != nullptr && e[0] == '1';
-  }();
-  return on;
-}
 
 bool gemm_glds_supported(const GemmProblem& g) {
   const int64_t aff_c = g.conv_h > 0 ? g.conv_c : g.K;
@@ -892,10 +885,9 @@ void gemm_glds(const GemmProblem& g, hipStream_t stream) {
     return;
   }
   // narrow channel counts (C % 32 != 0: per-chunk taps, e.g. the 48-channel DEQ cell, K = 432)
-  // may take 64-deep K steps too (7 instead of 14 K iterations) with FLUXMPI_NARROW_K64=1: measured
-  // slower on the DEQ cell's 28x28x48 input gradient (34.1 vs 31.3 us per call), so off by default
-  const bool narrow = conv && g.conv_c % 32 != 0;
-  const bool k64ok = !conv || g.conv_c % 64 == 0 || (narrow && !aff && narrow_k64());
+  // stay on 32-deep K steps: 64-deep ones measured slower on the DEQ cell's 28x28x48 input
+  // gradient (34.1 vs 31.3 us per call, round 3)
+  const bool k64ok = !conv || g.conv_c % 64 == 0;
   // K <= 64 (two 32-deep steps: all in flight after one wait anyway): a 2-stage ring, whose
   // smaller LDS footprint (the C staging tile sets it) fits a 4th workgroup per CU — measured
   // 153 -> 116 us on ResNet-50's 56x56 64->256 forward (scripts/bench_gemm_bw.py)

@@ -248,7 +248,7 @@ void for_each_group(const std::vector<uintptr_t>& p, const std::vector<uintptr_t
   flush();
 }
 
-#define FLUXMPI_OPT_COMBOS(X)            \
+#define OPT_DTYPE_COMBOS(X)            \
   X(float, float, float, false)          \
   X(float, bf16, float, false)           \
   X(bf16, bf16, bf16, false)             \
@@ -283,7 +283,7 @@ void mt_adam(const std::vector<uintptr_t>& param, const std::vector<uintptr_t>& 
     mt_adam_kernel<P, G, S, M><<<blocks, kThreads, 0, stream>>>(a, h);                           \
     done = true;                                                                                 \
   }
-    FLUXMPI_OPT_COMBOS(X)
+    OPT_DTYPE_COMBOS(X)
 #undef X
     if (!done)
       throw std::runtime_error("mt_adam: unsupported dtype combination p=" + std::to_string(p_dtype) +
@@ -313,7 +313,7 @@ void mt_sgd(const std::vector<uintptr_t>& param, const std::vector<uintptr_t>& g
     mt_sgd_kernel<P, G, S, M><<<blocks, kThreads, 0, stream>>>(a, h);                            \
     done = true;                                                                                 \
   }
-    FLUXMPI_OPT_COMBOS(X)
+    OPT_DTYPE_COMBOS(X)
 #undef X
     if (!done) throw std::runtime_error("mt_sgd: unsupported dtype combination");
     FLUXMPI_HIP_CHECK(hipGetLastError());

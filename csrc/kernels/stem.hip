@@ -291,7 +291,7 @@ __device__ __forceinline__ Item item_of(int r, int wave, int slot) {
 // Pipelined: while the MFMA phase of row pair `it` runs, the DMA of row pair it + 1's image
 // halo and pooled-gradient rows (into the other stage) and this lane's conv-output loads for
 // it + 1 (registers) are in flight. One workgroup per CU (LDS: two stages + the dz / x tiles).
-// MODE (bottleneck experiments, FLUXMPI_STEM_BWD_MODE): 0 = normal, 1 = no MFMA phase,
+// MODE (round-3 bottleneck experiments, rebuilt by hand): 0 = normal, 1 = no MFMA phase,
 // 2 = no element-phase gather (dz = 0), 3 = no next-iteration loads (stale stages)
 template <int MODE>
 __global__ __launch_bounds__(kBT, 2) void stem_bwd_kernel(StemBwdArgs p) {
@@ -657,14 +657,7 @@ void stem_bwd(const void* x, const void* c, const void* dp, const uint8_t* idx, 
   const int total = static_cast<int>(n * kPH);
   StemBwdArgs a{static_cast<const bf16*>(x), static_cast<const bf16*>(c), static_cast<const bf16*>(dp), idx, mean, inv,
                 part, stats, (total + blocks - 1) / blocks, total};
-  static const int mode = [] {
-    const char* e = std::getenv("FLUXMPI_STEM_BWD_MODE");
-    return e != nullptr ? std::atoi(e) : 0;
-  }();
-  if (mode == 1) stem_bwd_kernel<1><<<static_cast<unsigned>(blocks), kBT, kBSmem, s>>>(a);
-  else if (mode == 2) stem_bwd_kernel<2><<<static_cast<unsigned>(blocks), kBT, kBSmem, s>>>(a);
-  else if (mode == 3) stem_bwd_kernel<3><<<static_cast<unsigned>(blocks), kBT, kBSmem, s>>>(a);
-  else stem_bwd_kernel<0><<<static_cast<unsigned>(blocks), kBT, kBSmem, s>>>(a);
+  stem_bwd_kernel<0><<<static_cast<unsigned>(blocks), kBT, kBSmem, s>>>(a);
   FLUXMPI_HIP_CHECK(hipGetLastError());
   bn_finalize_bwd(stats, kCo, dw_bn, db_bn, s);
   stem_wgrad_combine_kernel<<<kKk, kCT, 0, s>>>(part, blocks, w, mean, inv, dw_bn, db_bn,

@@ -30,18 +30,18 @@ from ..ops.batchnorm import FusedBatchNorm2d, GradLink
 from ..ops.groupnorm import FusedGroupNorm, fp32_affine_cache, skip_param_grads
 from ..ops.groupnorm import native_ok as gn_native_ok
 
-# Convergence tests read a device value back LAG iterations late (FLUXMPI_DEQ_CHECK_LAG,
+# Convergence tests read a device value back LAG iterations late (CHECK_LAG,
 # default 2 on the GPU): the host never drains the queue, so the GPU always has LAG
 # iterations of work in flight while the host waits for an old flag; the price is at most
 # LAG extra (harmless, still-contracting) iterations after convergence. 0 = test every
 # iteration synchronously (the round-1 behaviour: ~11 % of the step idle, profiles/r1_deq_s63).
-CHECK_LAG = int(os.environ.get("FLUXMPI_DEQ_CHECK_LAG", "2"))
-# FLUXMPI_DEQ_MANUAL_VJP=0: the adjoint's VJPs through autograd.grad (A/B runs)
-MANUAL_VJP = os.environ.get("FLUXMPI_DEQ_MANUAL_VJP", "1") != "0"
-# FLUXMPI_DEQ_GRAPH=0: no solver graphs (every iteration launched from the host; A/B runs);
-# FLUXMPI_DEQ_GRAPH_CHUNK: adjoint iterations per graph replay
-GRAPHS = os.environ.get("FLUXMPI_DEQ_GRAPH", "1") != "0"
-GRAPH_CHUNK = int(os.environ.get("FLUXMPI_DEQ_GRAPH_CHUNK", "5"))
+CHECK_LAG = 2
+# False: the adjoint's VJPs through autograd.grad (A/B runs, tests)
+MANUAL_VJP = True
+# GRAPHS False: no solver graphs (every iteration launched from the host; A/B runs);
+# GRAPH_CHUNK: adjoint iterations per graph replay
+GRAPHS = True
+GRAPH_CHUNK = 5
 # DEQ-CIFAR solver settings (bench.py --deq-solver overrides): relative-residual tolerances the
 # Anderson forward and the adjoint fixed point reach before their iteration caps
 DEQ_CIFAR_SOLVER = {"max_iter": 30, "tol": 1e-4, "bwd_iter": 30, "bwd_tol": 1e-4}

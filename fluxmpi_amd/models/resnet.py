@@ -140,22 +140,15 @@ class Bottleneck(nn.Module):
                     link = fb.GradLink(masked=fb.masked_links_ok()) if needs else None
                 else:
                     link = fb.SideGradLink() if (needs and fused_ds) else None
-                prev = getattr(x, "_fluxmpi_bnlink", None) if (link is not None and self.downsample is None) else None
-                bnl = grad and fb.BN_LINK
-                # bn3-only mode: downsample blocks keep their dual BatchNorm (which hands no link)
-                out_link = fb.BNStatsLink() if (bnl and not (fb.BN_LINK_BN3_ONLY and self.downsample is not None)) \
-                    else None
-                bnl = bnl and not fb.BN_LINK_BN3_ONLY  # the in-block links (bn1 -> conv2, bn2 -> conv3)
-                bl1 = None
+                # (BatchNorm-backward reductions in the dgrad epilogues — fused_block.BNStatsLink —
+                # measured a loss in every form on MI355X, round 4: not linked here)
                 if self.hybrid:
-                    # bn1 -> conv2 (its only consumer): conv2's dgrad epilogue reduces bn1's backward
-                    bl1 = fb.BNStatsLink() if (bnl and fb.conv3x3_supported(x, self.conv2)) else None
                     o1 = fb.conv1x1_forward_is_ours(x, self.conv1.weight)
-                    c1 = fb.conv1x1_hybrid(x, self.conv1.weight, link, prev, ours_stats=o1)
-                    a1 = fb.bn_from_stats(c1, self.bn1, relu=True, stats_ready=True, bnlink=bl1) if o1 else \
-                        self.bn1(c1, relu=True, bnlink=bl1)
+                    c1 = fb.conv1x1_hybrid(x, self.conv1.weight, link, ours_stats=o1)
+                    a1 = fb.bn_from_stats(c1, self.bn1, relu=True, stats_ready=True) if o1 else \
+                        self.bn1(c1, relu=True)
                 else:
-                    c1 = fb.conv1x1_stats(x, self.conv1.weight, link, prev)  # + bn1 statistics (GEMM epilogue)
+                    c1 = fb.conv1x1_stats(x, self.conv1.weight, link)  # + bn1 statistics (GEMM epilogue)
                     a1 = fb.bn_from_stats(c1, self.bn1, relu=True)
                 # the downsample branch is built AFTER conv1: autograd runs ready nodes newest-first
                 # and conv1's backward becomes ready last, so the downsample conv's backward (which
@@ -167,7 +160,7 @@ class Bottleneck(nn.Module):
                     identity = x
                 elif fused_ds:
                     ds = self.downsample
-                    dual = out_link is None and fb.dual_bn_ok(x, ds[0].out_channels, self.bn3, ds[1])
+                    dual = fb.dual_bn_ok(x, ds[0].out_channels, self.bn3, ds[1])
                     # our GEMM (+ the downsample BN's sums in its epilogue) where measured faster
                     ds_stats = dual and fb.ds_forward_is_ours(x, ds[0].weight, ds[0].stride[0])
                     identity = fb.conv1x1_downsample(x, ds[0].weight, ds[0].stride[0],
@@ -179,30 +172,23 @@ class Bottleneck(nn.Module):
                         identity = ds[1](identity)
                 else:
                     identity = self.downsample(x)
-                fold = False
                 if self.hybrid:
-                    bl2 = fb.BNStatsLink() if bnl else None  # bn2 -> conv3 (its only consumer)
                     if fb.conv3x3_supported(a1, self.conv2):
                         # implicit-GEMM conv2 (input gradient always; forward where measured faster,
                         # then bn2's statistics come from its epilogue)
                         ours = fb.conv3x3_forward_is_ours(a1, self.conv2.weight)
-                        c2 = fb.conv3x3(a1, self.conv2.weight, with_stats=True, bnlink=bl1)
-                        fold = bl2 is None and fb.bn2_fold_ok(c2, self.bn2, self.conv3.weight)
-                        if fold:  # bn2 + ReLU in conv3's A load; c3's sums pending from its epilogue
-                            c3, o3 = fb.bn_relu_conv1x1(c2, self.bn2, self.conv3.weight, stats_ready=ours), True
-                        else:
-                            a2 = fb.bn_from_stats(c2, self.bn2, relu=True, stats_ready=ours, bnlink=bl2)
+                        c2 = fb.conv3x3(a1, self.conv2.weight, with_stats=True)
+                        a2 = fb.bn_from_stats(c2, self.bn2, relu=True, stats_ready=ours)
                     elif fb.conv3x3_s2_supported(a1, self.conv2):
                         # stride-2 conv2: forward where measured faster on our implicit GEMM (+ bn2's
                         # sums from its epilogue), weight gradient autotuned (fused_block._Conv3x3S2)
                         ours = fb.conv3x3_s2_forward_is_ours(a1, self.conv2.weight)
                         c2 = fb.conv3x3_s2(a1, self.conv2.weight, with_stats=ours)
-                        a2 = fb.bn_from_stats(c2, self.bn2, relu=True, stats_ready=ours, bnlink=bl2)
+                        a2 = fb.bn_from_stats(c2, self.bn2, relu=True, stats_ready=ours)
                     else:
-                        a2 = self.bn2(self.conv2(a1), relu=True, bnlink=bl2)
-                    if not fold:
-                        o3 = fb.conv1x1_forward_is_ours(a2, self.conv3.weight)
-                        c3 = fb.conv1x1_hybrid(a2, self.conv3.weight, None, bl2, ours_stats=o3)
+                        a2 = self.bn2(self.conv2(a1), relu=True)
+                    o3 = fb.conv1x1_forward_is_ours(a2, self.conv3.weight)
+                    c3 = fb.conv1x1_hybrid(a2, self.conv3.weight, None, ours_stats=o3)
                 else:
                     c2 = fb.conv3x3(a1, self.conv2.weight) if fb.conv3x3_supported(a1, self.conv2) else self.conv2(a1)
                     c3 = fb.bn_relu_conv1x1(c2, self.bn2, self.conv3.weight)  # bn2+relu fused into the A load
@@ -210,16 +196,13 @@ class Bottleneck(nn.Module):
                     out = fb.dual_bn_relu(c3, self.bn3, cds, self.downsample[1],
                                           stats_ready=o3 if self.hybrid else True, ds_stats_ready=ds_stats)
                 elif self.hybrid and not o3:
-                    out = self.bn3(c3, relu=True, residual=identity, link=link if self.downsample is None else None,
-                                   bnlink=out_link)
+                    out = self.bn3(c3, relu=True, residual=identity, link=link if self.downsample is None else None)
                 elif self.hybrid:
                     out = fb.bn_from_stats(c3, self.bn3, relu=True, residual=identity, stats_ready=True,
-                                           link=link if self.downsample is None else None, bnlink=out_link)
+                                           link=link if self.downsample is None else None)
                 else:
                     out = fb.bn_from_stats(c3, self.bn3, relu=True, residual=identity,
-                                           link=link if self.downsample is None else None, bnlink=out_link)
-                if out_link is not None:
-                    out._fluxmpi_bnlink = out_link  # for the next block's conv1 (used iff it is an identity block)
+                                           link=link if self.downsample is None else None)
                 return out
         identity = x if self.downsample is None else self.downsample(x)
         if self.fused:

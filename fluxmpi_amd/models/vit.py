@@ -25,11 +25,11 @@ from ..ops.gelu import GeluLink, gelu, linear_gelu
 from ..ops.layernorm import linear_add_layer_norm
 from ..ops.linear import Linear
 
-# FLUXMPI_VIT_FUSED_GELU=0: autograd's GELU backward + separate bias reduction (A/B runs)
-_FUSED_GELU = os.environ.get("FLUXMPI_VIT_FUSED_GELU", "1") != "0"
-_FUSED_PROJ_LN = os.environ.get("FLUXMPI_VIT_FUSED_PROJ_LN", "1") != "0"
-# FLUXMPI_VIT_CLS_ONLY=0: the last block's MLP over every token (A/B runs; same result)
-_CLS_ONLY = os.environ.get("FLUXMPI_VIT_CLS_ONLY", "1") != "0"
+# False: autograd's GELU backward + separate bias reduction (A/B runs)
+_FUSED_GELU = True
+_FUSED_PROJ_LN = True
+# False: the last block's MLP over every token (A/B runs; same result)
+_CLS_ONLY = True
 
 
 class PatchEmbed(nn.Module):

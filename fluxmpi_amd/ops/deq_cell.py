@@ -8,7 +8,7 @@ is 5 launches and ~5 full-tensor HBM round trips per evaluation; the DEQ solver 
 evaluations per training step. Same state format, same numerics (bf16 activations, fp32
 statistics); the reference example this serves is the FastDEQ model of the reference README.
 
-``FLUXMPI_DEQ_FUSED_CELL=0`` keeps the unfused path (A/B runs).
+``ENABLED = False`` keeps the unfused path (A/B runs).
 """
 from __future__ import annotations
 
@@ -18,7 +18,7 @@ import torch
 
 from . import _ext
 
-ENABLED = os.environ.get("FLUXMPI_DEQ_FUSED_CELL", "1") != "0"
+ENABLED = True  # False: the unfused 5-launch cell (A/B, scripts/diag_deq_graphs.py)
 
 
 def _ptr(t) -> int:

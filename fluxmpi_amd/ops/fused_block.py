@@ -40,41 +40,28 @@ from .gemm import conv1x1_dgrad, conv1x1_wgrad, conv3x3_dgrad, conv3x3_fwd, gemm
 from .multi_tensor import DTYPE_CODE
 
 
-# BNStatsLink: off by default. Measured on MI355X (ResNet-50 bs256, hybrid): the epilogue's
-# extra read of the BN input makes the dgrad GEMMs +1.4 ms/step slower while the removed
-# reduce passes save 1.05 ms — a net loss until the GEMM epilogue streams as well as the
-# BN kernels do. FLUXMPI_BN_LINK=1 enables it for every link (numerics covered by tests either way);
-# "bn3" only for the previous block's bn3 -> an identity block's conv1 (whose dgrad runs on the
-# LDS-DMA kernel with the residual epilogue anyway: the 3x3 input gradients stay on gemm_nt)
-_BN_LINK_ENV = os.environ.get("FLUXMPI_BN_LINK", "0")
-BN_LINK = _BN_LINK_ENV in ("1", "bn3")
-BN_LINK_BN3_ONLY = _BN_LINK_ENV == "bn3"
 # 3x3 / stride-1 convolutions of the bottlenecks: "ours" = forward (+ the next BatchNorm's
 # statistics in the epilogue) and input gradient on the implicit-GEMM MFMA kernel, weight
 # gradient on MIOpen; "dgrad" = only the input gradient ours; "miopen" = all MIOpen
-CONV3X3 = os.environ.get("FLUXMPI_CONV3X3", "ours")
+CONV3X3 = "ours"
 # 1x1 forward of the bottlenecks: "ours" = our GEMM + statistics epilogue where measured faster
 # than MIOpen + the statistics pass; "miopen" = always MIOpen
-CONV1X1 = os.environ.get("FLUXMPI_CONV1X1", "ours")
+CONV1X1 = "ours"
 # weight gradients of the bottleneck convolutions: "auto" = the fastest (measured once per
 # shape) of MIOpen and our split-K transposed-operand kernel in a few configurations
-WGRAD = os.environ.get("FLUXMPI_WGRAD", "auto")
+WGRAD = "auto"
 # downsample blocks: bn3 and the downsample branch's BatchNorm as one dual kernel pair
 # (relu(bn3(c3) + bn_ds(c_ds)) without materialising bn_ds(c_ds); see dual_bn_relu)
-DUAL_BN = os.environ.get("FLUXMPI_DUAL_BN", "1") == "1"
+DUAL_BN = True
 # downsample 1x1 forward: "ours" = our GEMM (stride 2 gathers the even pixels in the A staging)
 # with the downsample BatchNorm's sums in its epilogue where measured faster than MIOpen + the
 # statistics pass (dual-BN blocks only); "force" = ours wherever supported; "miopen" = always MIOpen
-DS_FWD = os.environ.get("FLUXMPI_DS_FWD", "ours")
+DS_FWD = "ours"
 # weight gradients of the downsample 1x1 and the stride-2 3x3 convolutions: MIOpen vs our split-K
 # kernel (stride-2 B-row gather / implicit stride-2 im2col), measured per shape
-# (FLUXMPI_DS_WGRAD=0: always MIOpen)
-DS_WGRAD = os.environ.get("FLUXMPI_DS_WGRAD", "1") == "1"
-# bottleneck bn2 -> conv3: BatchNorm + ReLU applied in conv3's A-operand load (bn_relu_conv1x1: no bn2
-# output pass, bn2's backward reductions in conv3's dgrad epilogue) instead of a bn2 pass + conv3
-BN2_FOLD = os.environ.get("FLUXMPI_BN2_FOLD", "0") == "1"
+DS_WGRAD = True
 # stride-2 3x3 forward: our implicit GEMM (+ statistics epilogue) where measured faster (0: MIOpen)
-S2_FWD = os.environ.get("FLUXMPI_S2_FWD", "1") == "1"
+S2_FWD = True
 
 
 def _stream(t):
@@ -768,7 +755,7 @@ _WG_CONFIGS = ((2, 512), (2, 768), (2, 1024), (2, 384))  # (variant, target work
 
 
 def _w256_ok(co: int, ci: int, dc: torch.Tensor) -> bool:
-    if os.environ.get("FLUXMPI_WGRAD256", "1") == "0" or dc.dtype != torch.bfloat16:
+    if dc.dtype != torch.bfloat16:
         return False
     C = _ext.get(required=True)
     k = dc.numel() // co
@@ -939,16 +926,6 @@ def bn_relu_conv1x1(c2, bn, weight, stats_ready=False):
     mom, nbt = bn_counter(bn)
     return _BNReluConv1x1.apply(c2, bn.weight, bn.bias, bn.running_mean, bn.running_var, weight, mom, bn.eps, nbt,
                                 stats_ready)
-
-
-def bn2_fold_ok(c2, bn, weight) -> bool:
-    """:func:`bn_relu_conv1x1` takes this BatchNorm -> 1x1 pair (``FLUXMPI_BN2_FOLD``): the A-prologue
-    affine holds <= 512 channels, the kernel wants bf16 NHWC with channel counts % 32."""
-    from .batchnorm import FusedBatchNorm2d
-    ch = c2.shape[1]
-    return (BN2_FOLD and G.ENGINE != 1 and c2.is_cuda and c2.dtype == torch.bfloat16 and ch % 32 == 0 and ch <= 512
-            and weight.shape[0] % 32 == 0 and isinstance(bn, FusedBatchNorm2d) and bn.training and bn.affine
-            and bn.track_running_stats)
 
 
 def supported(x: torch.Tensor, *channels: int) -> bool:

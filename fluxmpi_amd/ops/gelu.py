@@ -23,7 +23,7 @@ FORM = os.environ.get("FLUXMPI_GELU", "tanh").lower()
 if FORM not in ("tanh", "erf"):
     raise ValueError(f"FLUXMPI_GELU must be 'tanh' or 'erf' (got {FORM!r})")
 _synced = [None]  # form last pushed to the extension
-_FWD_NATIVE = os.environ.get("FLUXMPI_GELU_FWD", "hip") != "torch"  # A/B: "torch" = F.gelu
+_FWD_NATIVE = True  # False: F.gelu (the pre-round-3 path; tests)
 
 
 def set_form(form: str) -> None:

@@ -21,7 +21,7 @@ from . import graddst
 
 SHARDS = 64  # == kShards in csrc/kernels/{batchnorm,gemm}.hip
 # LDS buffering of the GEMM main loop: 0 = per-shape choice in the kernel launcher, 1 or 2 forces it
-NBUF = int(os.environ.get("FLUXMPI_GEMM_NBUF", "0"))
+NBUF = 0
 # GEMM kernel: 0 = launcher's choice, 1 = register-staged (gemm.hip), 2 = LDS-DMA pipelined (gemm_glds.hip)
 ENGINE = int(os.environ.get("FLUXMPI_GEMM_ENGINE", "0"))
 def _stream(t):
@@ -161,6 +161,27 @@ def filter_t(w: torch.Tensor) -> torch.Tensor:
     return e[1]
 
 
+def conv_n_ok(pixels: int, c: int, co: int, h: int, w: int, *tensors: torch.Tensor) -> bool:
+    """The narrow-channel 3x3 kernel (``conv3x3n.hip``: C = Cout in {64, 128}, ResNet-50 stages
+    1-2) takes this stride-1 convolution (16-B aligned bf16 operands)."""
+    if not tensors[0].is_cuda or any(t.dtype != torch.bfloat16 or t.data_ptr() % 16 for t in tensors):
+        return False
+    C = _ext.get(required=False)
+    return C is not None and hasattr(C, "conv3x3n") and bool(C.conv3x3n_supported(pixels, c, co, h, w))
+
+
+def conv3x3n(x: torch.Tensor, w_taps: torch.Tensor, y: torch.Tensor, pixels: int, h: int, w: int,
+             stats: torch.Tensor | None = None) -> torch.Tensor:
+    """``y [pixels, Cout] = conv3x3(x)`` on the narrow-channel kernel: ``x`` NHWC memory, ``w_taps``
+    [Cout][3][3][C] (tap-major), ``stats``: BatchNorm shards [64][2][Cout] (sum / sum of squares of
+    the rounded output)."""
+    C = _ext.get(required=True)
+    c, co = x.shape[1], w_taps.shape[0]
+    C.conv3x3n(x.data_ptr(), w_taps.data_ptr(), y.data_ptr(), stats.data_ptr() if stats is not None else 0,
+               pixels, h, w, c, co, 3 if stats is not None else 0, _stream(x))
+    return y
+
+
 def conv3x3_fwd(x: torch.Tensor, w: torch.Tensor, in_affine=None, stats: torch.Tensor | None = None,
                 out: torch.Tensor | None = None, engine: int | None = None) -> torch.Tensor:
     """3x3 / stride 1 / pad 1 convolution as an implicit GEMM on the MFMA kernel.
@@ -179,6 +200,9 @@ def conv3x3_fwd(x: torch.Tensor, w: torch.Tensor, in_affine=None, stats: torch.T
     note_filter(w)
     y = out if out is not None else torch.empty(n, h, wd, co, device=x.device, dtype=x.dtype).permute(0, 3, 1, 2)
     M = n * h * wd
+    if (in_affine is None and not engine and y.is_contiguous(memory_format=torch.channels_last)
+            and conv_n_ok(M, c, co, h, wd, xs, w2, y)):
+        return conv3x3n(xs, w2, y, M, h, wd, stats)  # narrow channels: the halo staged once per tile
     if (in_affine is None and not engine and y.is_contiguous(memory_format=torch.channels_last)
             and _NT.conv_ok(M, c, co, xs, w2)):
         return _NT.conv3x3(xs, w2.view(co, 9 * c), y, stats)  # 256x256 persistent implicit GEMM
@@ -219,6 +243,9 @@ def conv3x3_dgrad(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = 
     dx = out if out is not None else torch.empty(n, h, wd, ci, device=dy.device, dtype=dy.dtype).permute(0, 3, 1, 2)
     if bn_bwd is not None:
         assert stats is not None and bn_bwd[0].shape == (n * h * wd, ci) and ENGINE != 1
+    if (bn_bwd is None and residual is None and ENGINE != 1 and dx.is_contiguous(memory_format=torch.channels_last)
+            and conv_n_ok(n * h * wd, co, ci, h, wd, dys, wt, dx)):
+        return conv3x3n(dys, wt, dx, n * h * wd, h, wd)  # the flipped transpose [ci][3][3][co] as the filter
     if (bn_bwd is None and residual is None and ENGINE != 1 and dx.is_contiguous(memory_format=torch.channels_last)
             and _NT.conv_ok(n * h * wd, co, ci, dys, wt)):
         return _NT.conv3x3(dys, wt, dx)  # the flipped transpose [ci][3][3][co] as B
@@ -286,7 +313,7 @@ def conv1x1_wgrad(dy2d: torch.Tensor, x2d: torch.Tensor, in_affine=None, out: to
 
 # ---- weight gradients on the LDS-DMA transposed-operand kernel --------------------------------
 # workgroups the weight-gradient split-K aims at (one round of the 3-per-CU kernel on 256 CUs)
-WGRAD_TARGET_WG = int(os.environ.get("FLUXMPI_WGRAD_TARGET_WG", "768"))
+WGRAD_TARGET_WG = 768
 
 
 def _wgrad_splits_v2(M: int, N: int, K: int) -> int:
@@ -312,9 +339,9 @@ def _actual_splits_v2(K: int, splits: int) -> int:
 
 
 # weight-gradient kernel variant: 1 = 32-deep K-step / 3 stages, 2 = 64-deep / 2 stages
-WGRAD_VARIANT = int(os.environ.get("FLUXMPI_WGRAD_VARIANT", "1"))
+WGRAD_VARIANT = 1
 # 1 (default): XCD-aware (split, tile) block order in the weight-gradient grid; 0: dispatch order
-WGRAD_REMAP = os.environ.get("FLUXMPI_WGRAD_REMAP", "1") == "1"
+WGRAD_REMAP = True
 
 
 def conv1x1_wgrad_v2(dy2d: torch.Tensor, x2d: torch.Tensor, out_dtype=torch.bfloat16, splits: int | None = None):

@@ -144,8 +144,8 @@ def linear_dgrad(dy2: torch.Tensor, weight: torch.Tensor, gelu_d: torch.Tensor |
 CONV = os.environ.get("FLUXMPI_GEMM_NT_CONV", "1") != "0"
 
 
-MIN_TILES = int(os.environ.get("FLUXMPI_GEMM_NT_MIN_TILES", "160"))
-MIN_K = int(os.environ.get("FLUXMPI_GEMM_NT_MIN_K", "1024"))
+MIN_TILES = 160
+MIN_K = 1024
 
 
 def _worth(rows: int, n_out: int, k: int) -> bool:

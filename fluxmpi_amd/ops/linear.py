@@ -12,7 +12,7 @@ reads; 0.91-0.98 PF/s on the ViT shapes) when both widths are multiples of 256, 
 ``scripts/bench_vit_gemm.py``. The bias gradient is the
 ``colsum`` HIP kernel (one read of dy at HBM rate) instead of autograd's generic reduction.
 
-``FLUXMPI_LINEAR_WGRAD=torch`` keeps hipBLASLt for the weight gradient (A/B runs).
+``WGRAD_MODE = "torch"`` keeps hipBLASLt for the weight gradient (A/B runs).
 """
 from __future__ import annotations
 
@@ -29,8 +29,12 @@ from .multi_tensor import DTYPE_CODE
 _SPLITS = {(2304, 768): 16, (768, 768): 16, (3072, 768): 8, (768, 3072): 4}
 
 
+# "ours": the split-K 256x256 weight-gradient kernel where it applies; "torch": hipBLASLt (A/B, tests)
+WGRAD_MODE = "ours"
+
+
 def _wgrad_mode() -> str:
-    return os.environ.get("FLUXMPI_LINEAR_WGRAD", "ours")
+    return WGRAD_MODE
 
 
 def native_ok(x2: torch.Tensor, dy2: torch.Tensor) -> bool:
@@ -42,7 +46,7 @@ def native_ok(x2: torch.Tensor, dy2: torch.Tensor) -> bool:
 
 
 # workgroups the 256x256 kernel's split-K aims at (one per CU: 128 KiB of LDS each)
-WG256_TARGET = int(os.environ.get("FLUXMPI_WGRAD256_WG", "256"))
+WG256_TARGET = 256
 
 
 def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype, splits: int | None = None) -> torch.Tensor:
@@ -54,7 +58,7 @@ def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype, spl
     K, n_out = dy2.shape
     n_in = x2.shape[1]
     C = _ext.get(required=True)
-    if os.environ.get("FLUXMPI_WGRAD256", "1") != "0" and C.wgrad256_supported(n_out, n_in, K, dy2.stride(0),
+    if C.wgrad256_supported(n_out, n_in, K, dy2.stride(0),
                                                                                   x2.stride(0)):
         tiles = (n_out // 256) * (n_in // 256)
         # exactly one round of workgroups (floor, not ceil: a second, partial round costs a whole

@@ -23,18 +23,14 @@ def _models(impl="fused"):
     return ref, fus
 
 
-@pytest.mark.parametrize("impl", ["fused", "hybrid", "fused+bnlink", "hybrid+bnlink", "hybrid+bn2fold", "hybrid+bnlink3"])
-def test_fused_resnet_matches_unfused(gpu_ext, impl, monkeypatch):
+@pytest.mark.parametrize("impl", ["fused", "hybrid"])
+def test_fused_resnet_matches_unfused(gpu_ext, impl):
     """Both bf16 pipelines are compared with an fp32 model holding the same (bf16-rounded)
     weights: the fused pipeline must be about as accurate as the unfused one. Layer 1 has an
-    identity block, so the GradLink residual-gradient hand-off is exercised. ``+bn2fold``: bn2 +
-    ReLU applied in conv3's A load (``FLUXMPI_BN2_FOLD``)."""
+    identity block, so the GradLink residual-gradient hand-off is exercised; "fused" applies bn2 +
+    ReLU in conv3's A load (bn_relu_conv1x1)."""
     from fluxmpi_amd.models.resnet import ResNet
-    from fluxmpi_amd.ops import fused_block as fb
-    monkeypatch.setattr(fb, "BN_LINK", impl.endswith("+bnlink") or impl.endswith("+bnlink3"))
-    monkeypatch.setattr(fb, "BN_LINK_BN3_ONLY", impl.endswith("+bnlink3"))
-    monkeypatch.setattr(fb, "BN2_FOLD", impl.endswith("+bn2fold"))
-    ref, fus = _models(impl.split("+")[0])
+    ref, fus = _models(impl)
     f32 = ResNet((2, 1, 1, 1), 10, conv_impl="miopen", norm="fused").cuda().to(memory_format=torch.channels_last)
     f32.load_state_dict({k: v.float() if v.is_floating_point() else v for k, v in ref.state_dict().items()})
     x = torch.randn(8, 3, 64, 64, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
