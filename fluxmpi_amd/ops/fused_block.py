@@ -26,8 +26,6 @@ recomputed in the backward match the forward bit for bit.
 """
 from __future__ import annotations
 
-import os
-
 import torch
 
 from . import _ext
@@ -36,6 +34,10 @@ from .batchnorm import BNStatsLink, GradLink, SideGradLink, _dual_workspace, _li
 from . import gemm as G
 from . import gemm_nt as _NT
 from . import groupnorm as _GN
+from .conv_choice import (_DGRAD_CHOICE, _DS_CHOICE, _FWD1_CHOICE, _FWD_CHOICE, _FWD_ENGINE, _S2_CHOICE,  # noqa: F401
+                          _WG_CHOICE, FWD_ENGINES, choices_frozen, dump_choices, freeze_choices,
+                          load_choice_lines, load_choices, no_measure as _no_measure, stats_choice,
+                          time_us as _time_us, w256_ok as _w256_ok, wgrad_best)
 from .gemm import conv1x1_dgrad, conv1x1_wgrad, conv3x3_dgrad, conv3x3_fwd, gemm, note_filter
 from .multi_tensor import DTYPE_CODE
 
@@ -47,9 +49,6 @@ CONV3X3 = "ours"
 # 1x1 forward of the bottlenecks: "ours" = our GEMM + statistics epilogue where measured faster
 # than MIOpen + the statistics pass; "miopen" = always MIOpen
 CONV1X1 = "ours"
-# weight gradients of the bottleneck convolutions: "auto" = the fastest (measured once per
-# shape) of MIOpen and our split-K transposed-operand kernel in a few configurations
-WGRAD = "auto"
 # downsample blocks: bn3 and the downsample branch's BatchNorm as one dual kernel pair
 # (relu(bn3(c3) + bn_ds(c_ds)) without materialising bn_ds(c_ds); see dual_bn_relu)
 DUAL_BN = True
@@ -246,9 +245,6 @@ def ds_forward_supported(x, weight, stride) -> bool:
             and weight.shape[0] % 8 == 0 and x.numel() // x.shape[1] < 2 ** 31)
 
 
-_DS_CHOICE: dict = {}
-
-
 def ds_forward_is_ours(x, weight, stride) -> bool:
     """Per-shape choice of the downsample forward, measured once: our GEMM with the statistics
     epilogue vs MIOpen plus the statistics pass its BatchNorm then needs (one read of the output
@@ -257,24 +253,13 @@ def ds_forward_is_ours(x, weight, stride) -> bool:
         return False
     if DS_FWD == "force":
         return True
-    key = (tuple(x.shape), weight.shape[0], stride)
-    hit = _DS_CHOICE.get(key)
-    if hit is not None:
-        return hit
-    if _no_measure():
-        return True
-    with torch.no_grad():
-        xs = x.detach().contiguous(memory_format=torch.channels_last)
-        w = weight.detach()
+    def make():
+        xs, w = x.detach().contiguous(memory_format=torch.channels_last), weight.detach()
+        n, _, h, wd = x.shape
         ws = torch.zeros_like(_workspace(xs))
-        ours = _time_us(lambda: _ds_fwd_ours(xs, w, stride, ws))
-        theirs = _time_us(lambda: torch.nn.functional.conv2d(xs, w, None, stride))
-    n, _, h, wd = x.shape
-    stats_pass_us = n * ((h + stride - 1) // stride) * ((wd + stride - 1) // stride) * weight.shape[0] * \
-        x.element_size() / 5e12 * 1e6
-    choice = ours <= theirs + stats_pass_us
-    _DS_CHOICE[key] = choice
-    return choice
+        return (lambda: _ds_fwd_ours(xs, w, stride, ws), lambda: torch.nn.functional.conv2d(xs, w, None, stride),
+                n * ((h + stride - 1) // stride) * ((wd + stride - 1) // stride) * w.shape[0] * x.element_size())
+    return stats_choice(_DS_CHOICE, (tuple(x.shape), weight.shape[0], stride), make)
 
 
 class _Conv1x1Downsample(torch.autograd.Function):
@@ -613,9 +598,6 @@ class _Conv3x3(torch.autograd.Function):
         return dx, dw, None, None, None, None
 
 
-_DGRAD_CHOICE: dict = {}
-
-
 def _dgrad_is_ours(dy, weight, x_shape) -> bool:
     """Input gradient on our implicit GEMM, or MIOpen. Channel counts that are multiples of 32
     (ResNet-50) always take ours; narrower ones (e.g. the 48-channel DEQ cell, whose K tiles
@@ -678,31 +660,18 @@ def conv3x3_s2_supported(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
             and x.numel() // x.shape[1] < 2 ** 31)
 
 
-_S2_CHOICE: dict = {}
-
-
 def conv3x3_s2_forward_is_ours(x, weight) -> bool:
     """Per-shape choice of the stride-2 3x3 forward, measured once: our implicit GEMM with the
     statistics epilogue vs MIOpen plus the statistics pass (one read of the output at 5 TB/s)."""
     if CONV3X3 != "ours" or not S2_FWD or x.shape[1] % 32 != 0:
         return False
-    key = (tuple(x.shape), weight.shape[0])
-    hit = _S2_CHOICE.get(key)
-    if hit is not None:
-        return hit
-    if _no_measure():
-        return True
-    with torch.no_grad():
-        xs = x.detach().contiguous(memory_format=torch.channels_last)
-        w = weight.detach()
+    def make():
+        xs, w = x.detach().contiguous(memory_format=torch.channels_last), weight.detach()
+        n, _, h, wd = x.shape
         ws = torch.zeros_like(_workspace(xs))
-        ours = _time_us(lambda: G.conv3x3_s2_fwd(xs, w, stats=ws))
-        theirs = _time_us(lambda: torch.nn.functional.conv2d(xs, w, None, 2, 1))
-    n, _, h, wd = x.shape
-    stats_pass_us = n * ((h + 1) // 2) * ((wd + 1) // 2) * weight.shape[0] * x.element_size() / 5e12 * 1e6
-    choice = ours <= theirs + stats_pass_us
-    _S2_CHOICE[key] = choice
-    return choice
+        return (lambda: G.conv3x3_s2_fwd(xs, w, stats=ws), lambda: torch.nn.functional.conv2d(xs, w, None, 2, 1),
+                n * ((h + 1) // 2) * ((wd + 1) // 2) * w.shape[0] * x.element_size())
+    return stats_choice(_S2_CHOICE, (tuple(x.shape), weight.shape[0]), make)
 
 
 def conv3x3_s2(x, weight, with_stats=False):
@@ -717,90 +686,6 @@ def conv3x3_supported(x: torch.Tensor, conv: torch.nn.Conv2d) -> bool:
             and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None
             and conv.in_channels % 8 == 0 and conv.out_channels % 8 == 0 and conv.weight.dtype == torch.bfloat16
             and x.numel() // x.shape[1] < 2 ** 31)
-
-
-_FWD_CHOICE: dict = {}  # (N, C, H, W, Co) -> True: our forward (+ statistics epilogue) is faster
-_FWD_ENGINE: dict = {}  # (N, C, H, W, Co) -> the fastest of _FWD_ENGINES for our forward
-_FWD_ENGINES = (0, 8, 7)  # 0: auto (128x128 tiles); 8 / 7: 256x128 tiles, 64- / 32-deep K-steps
-
-
-_FROZEN = False  # freeze_choices(): no more measurements (rank-consistent tables at N > 1)
-
-
-def _no_measure() -> bool:
-    """Take the default instead of timing: inside a HIP-graph capture, or once frozen."""
-    return _FROZEN or torch.cuda.is_current_stream_capturing()
-
-
-def _time_us(fn, iters=10, repeats=3):
-    """Best of ``repeats`` timings of ``iters`` back-to-back calls (autotune: choices flip on
-    single-sample noise otherwise)."""
-    for _ in range(2):
-        fn()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    best = float("inf")
-    for _ in range(repeats):
-        s.record()
-        for _ in range(iters):
-            fn()
-        e.record()
-        e.synchronize()
-        best = min(best, s.elapsed_time(e) * 1e3 / iters)
-    return best
-
-
-_WG_CHOICE: dict = {}
-# our weight-gradient kernel configurations tried by the autotune: (variant, target workgroups)
-_WG_CONFIGS = ((2, 512), (2, 768), (2, 1024), (2, 384))  # (variant, target workgroups); s44 sweep
-
-
-def _w256_ok(co: int, ci: int, dc: torch.Tensor) -> bool:
-    if dc.dtype != torch.bfloat16:
-        return False
-    C = _ext.get(required=True)
-    k = dc.numel() // co
-    return bool(C.wgrad256_supported(co, ci, k, co, ci)) and k >= 4096
-
-
-def wgrad_best(key, impls: dict, param=None):
-    """Run the fastest weight-gradient implementation for ``key`` (measured on first use, like
-    cudnn.benchmark: MIOpen vs our kernel in each of ``_WG_CONFIGS``) and return its result.
-    ``param``: the weight, whose DDP bucket slice (if any) receives the returned gradient
-    (``graddst``; never during the measurements)."""
-    choice = _WG_CHOICE.get(key)
-    if choice is None:
-        if WGRAD == "miopen" or _no_measure():
-            choice = ("miopen", None)
-        elif WGRAD == "ours":
-            choice = ("ours", _WG_CONFIGS[0])
-        else:
-            best = (_time_us(impls["miopen"]), ("miopen", None))
-            saved = G.WGRAD_VARIANT, G.WGRAD_TARGET_WG
-            try:
-                for cfg in _WG_CONFIGS:
-                    G.WGRAD_VARIANT, G.WGRAD_TARGET_WG = cfg
-                    t = _time_us(impls["ours"])
-                    if t < best[0]:
-                        best = (t, ("ours", cfg))
-            finally:
-                G.WGRAD_VARIANT, G.WGRAD_TARGET_WG = saved
-            if "w256" in impls:  # 256x256-tile kernel (wgrad256.hip) where both widths allow it
-                t = _time_us(impls["w256"])
-                if t < best[0]:
-                    best = (t, ("w256", None))
-            choice = best[1]
-        _WG_CHOICE[key] = choice
-    name, cfg = choice
-    if cfg is None:
-        with graddst.into(param):
-            return impls[name]()
-    saved = G.WGRAD_VARIANT, G.WGRAD_TARGET_WG
-    G.WGRAD_VARIANT, G.WGRAD_TARGET_WG = cfg
-    try:
-        with graddst.into(param):
-            return impls[name]()
-    finally:
-        G.WGRAD_VARIANT, G.WGRAD_TARGET_WG = saved
 
 
 def conv3x3_forward_is_ours(x, weight) -> bool:
@@ -823,7 +708,7 @@ def conv3x3_forward_is_ours(x, weight) -> bool:
         # our tile configurations: the default 128x128 and the 256x128 ones (fewer, larger tiles:
         # less wave quantization on e.g. 14x14x256, 1.5 rounds of 128x128 tiles)
         best = None
-        for eng in (_FWD_ENGINES if G.ENGINE == 0 else (0,)):
+        for eng in (FWD_ENGINES if G.ENGINE == 0 else (0,)):
             t = _time_us(lambda: conv3x3_fwd(xs, w, stats=ws, engine=eng))
             if best is None or t < best[0]:
                 best = (t, eng)
@@ -879,33 +764,19 @@ def conv1x1_stats(x, weight, link=None, bnlink=None):
     return _Conv1x1Stats.apply(x, weight, link, bnlink)
 
 
-_FWD1_CHOICE: dict = {}
-
-
 def conv1x1_forward_is_ours(x, weight) -> bool:
     """Per-shape choice of a 1x1 forward, measured once: our GEMM with the statistics epilogue
     vs MIOpen plus the statistics pass the next BatchNorm then needs (one read of the output
     at 5 TB/s)."""
     if CONV1X1 != "ours":
         return False
-    key = (tuple(x.shape), weight.shape[0])
-    hit = _FWD1_CHOICE.get(key)
-    if hit is not None:
-        return hit
-    if _no_measure():
-        return True
-    with torch.no_grad():
-        xs = x.detach().contiguous(memory_format=torch.channels_last)
-        w = weight.detach()
-        n, ci, h, wd = xs.shape
-        co = w.shape[0]
+    def make():
+        xs, w = x.detach().contiguous(memory_format=torch.channels_last), weight.detach()
+        n, _, h, wd = xs.shape
         ws = torch.zeros_like(_workspace(xs))
-        ours = _time_us(lambda: _fwd1x1_stats(xs, w, ws))  # what the forward runs
-        theirs = _time_us(lambda: torch.nn.functional.conv2d(xs, w))
-    stats_pass_us = n * h * wd * co * xs.element_size() / 5e12 * 1e6
-    choice = ours <= theirs + stats_pass_us
-    _FWD1_CHOICE[key] = choice
-    return choice
+        return (lambda: _fwd1x1_stats(xs, w, ws), lambda: torch.nn.functional.conv2d(xs, w),
+                n * h * wd * w.shape[0] * xs.element_size())
+    return stats_choice(_FWD1_CHOICE, (tuple(x.shape), weight.shape[0]), make)
 
 
 def conv1x1_hybrid(x, weight, link=None, bnlink=None, ours_stats=False):
@@ -932,63 +803,3 @@ def supported(x: torch.Tensor, *channels: int) -> bool:
     """Shapes the fused path handles (bf16 NHWC on GPU, channels % 32 == 0, <= 2048)."""
     return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4
             and all(c % 32 == 0 and 32 <= c <= 2048 for c in channels))
-
-
-# ---- shipped per-shape kernel choices (the analogue of MIOpen's find-db) -----------------------
-_CHOICE_TABLES = {"fwd1x1_ours": "_FWD1_CHOICE", "fwd3x3_ours": "_FWD_CHOICE", "wgrad": "_WG_CHOICE",
-                  "fwd_ds_ours": "_DS_CHOICE", "fwd3x3s2_ours": "_S2_CHOICE", "fwd3x3_engine": "_FWD_ENGINE",
-                  "dgrad3x3_ours": "_DGRAD_CHOICE"}
-
-
-def dump_choices():
-    """The per-shape choices measured so far, as JSON-lines records (``scripts/show_choices.py``)."""
-    import json
-    g = globals()
-    out = []
-    for kind, name in _CHOICE_TABLES.items():
-        for k, v in g[name].items():
-            out.append(json.dumps({"kind": kind, "key": str(k), "choice": str(v)}))
-    return out
-
-
-def load_choice_lines(lines) -> int:
-    """Pre-populate the per-shape kernel choices from JSON-lines records (``dump_choices``):
-    those shapes skip the first-step measurement (no autotune time, no run-to-run flips of
-    marginal shapes); others are still measured (unless frozen). Returns the entries loaded."""
-    import ast
-    import json
-    g = globals()
-    n = 0
-    for line in lines:
-        line = line.strip()
-        if not line:
-            continue
-        rec = json.loads(line)
-        name = _CHOICE_TABLES.get(rec["kind"])
-        if name is None:
-            continue
-        g[name][ast.literal_eval(rec["key"])] = ast.literal_eval(rec["choice"])
-        n += 1
-    return n
-
-
-def load_choices(path: str) -> int:
-    """:func:`load_choice_lines` from a file."""
-    with open(path) as f:
-        return load_choice_lines(f.readlines())
-
-
-def freeze_choices(frozen: bool = True) -> None:
-    """Stop measuring: a shape missing from the tables takes the deterministic default (what a
-    HIP-graph capture takes) instead of a timing that could differ between ranks
-    (``parallel/autotune.calibrate``)."""
-    global _FROZEN
-    _FROZEN = frozen
-
-
-def choices_frozen() -> bool:
-    return _FROZEN
-
-
-if os.environ.get("FLUXMPI_KERNEL_CHOICES"):
-    load_choices(os.environ["FLUXMPI_KERNEL_CHOICES"])

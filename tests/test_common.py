@@ -48,7 +48,7 @@ def test_kernel_choice_table_roundtrip(tmp_path):
     dictionaries and dumps back to the same records."""
     import json
     import os
-    from fluxmpi_amd.ops import fused_block as fb
+    from fluxmpi_amd.ops import conv_choice as fb
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     path = os.path.join(root, "tuning", "kernel_choices", "resnet50_bs256.jsonl")
     saved = {name: dict(getattr(fb, name)) for name in fb._CHOICE_TABLES.values()}

@@ -175,9 +175,9 @@ def test_hybrid_resnet_weight_gradient_kernels(gpu_ext, wgrad, monkeypatch):
     """The hybrid ResNet with every bottleneck weight gradient forced onto our split-K kernel
     (or MIOpen) matches the fp32 model as closely as the unfused bf16 pipeline does."""
     from fluxmpi_amd.models.resnet import ResNet
-    from fluxmpi_amd.ops import fused_block as fb
-    monkeypatch.setattr(fb, "WGRAD", wgrad)
-    monkeypatch.setattr(fb, "_WG_CHOICE", {})
+    from fluxmpi_amd.ops import conv_choice as CC
+    monkeypatch.setattr(CC, "WGRAD", wgrad)
+    monkeypatch.setattr(CC, "_WG_CHOICE", {})
     ref, fus = _models("hybrid")
     f32 = ResNet((2, 1, 1, 1), 10, conv_impl="miopen", norm="fused").cuda().to(memory_format=torch.channels_last)
     f32.load_state_dict({k: v.float() if v.is_floating_point() else v for k, v in ref.state_dict().items()})
@@ -186,7 +186,7 @@ def test_hybrid_resnet_weight_gradient_kernels(gpu_ext, wgrad, monkeypatch):
     g = torch.randn_like(yc)
     for y in (ya, yb, yc):
         (y.float() * g).sum().backward()
-    assert fb._WG_CHOICE and all(c[0] == wgrad for c in fb._WG_CHOICE.values())
+    assert CC._WG_CHOICE and all(c[0] == wgrad for c in CC._WG_CHOICE.values())
     for (n, pa), pb, pc in zip(ref.named_parameters(), fus.parameters(), f32.parameters()):
         ea, eb = _rel(pa.grad, pc.grad), _rel(pb.grad, pc.grad)
         assert eb < 2 * ea + 2e-2, f"{n}: {wgrad} {eb:.3e} vs unfused {ea:.3e}"
