@@ -295,7 +295,7 @@ def main():
         loss.backward()
         ddp.step()
         if deq is not None:
-            iters.append((deq.last_iters, deq.last_bwd_iters))
+            iters.append((deq.last_iters, deq.last_bwd_iters, deq.last_res))
         return loss
 
     calibrated = False
@@ -395,7 +395,9 @@ def main():
                        **({"deq_solver": {k: getattr(deq, k) for k in ("max_iter", "tol", "bwd_iter", "bwd_tol")}}
                           if deq is not None else {}),
                        **({"deq_fwd_iters_per_step": round(sum(i[0] for i in timed_iters) / len(timed_iters), 2),
-                           "deq_bwd_iters_per_step": round(sum(i[1] for i in timed_iters) / len(timed_iters), 2)}
+                           "deq_bwd_iters_per_step": round(sum(i[1] for i in timed_iters) / len(timed_iters), 2),
+                           "deq_fwd_residual_max": max([float(i[2]) for i in timed_iters if i[2] is not None],
+                                                       default=None)}
                           if timed_iters else {})},
         }
         print(json.dumps(rec), flush=True)

@@ -759,8 +759,10 @@ int cus() {
   return n;
 }
 
-// FLUXMPI_GEMM_NT_SPLIT: the fewest k-tiles of a workgroup's share of the split tail (default 8;
-// 0: no split). Shapes with an odd k-tile count or fewer than 16 k-tiles are never split.
+// FLUXMPI_GEMM_NT_SPLIT: the fewest k-tiles of a workgroup's share of the split tail (0: no split,
+// the default — measured slower end to end: ResNet-50 20.85 vs 20.32 ms/step, ViT-B/16 per-GEMM
+// -7..+5 %, profiles/rd5d_*; 8 / 16: the tested settings). Shapes with an odd k-tile count or
+// fewer than 16 k-tiles are never split.
 int g_split_min = -1;  // < 0: not yet read from the environment
 
 int split_norm(int x) { return x <= 0 ? 0 : (x < 2 ? 2 : x + (x & 1)); }
@@ -768,7 +770,7 @@ int split_norm(int x) { return x <= 0 ? 0 : (x < 2 ? 2 : x + (x & 1)); }
 int split_min() {
   if (g_split_min < 0) {
     const char* e = std::getenv("FLUXMPI_GEMM_NT_SPLIT");
-    g_split_min = split_norm(e != nullptr ? std::atoi(e) : 8);
+    g_split_min = split_norm(e != nullptr ? std::atoi(e) : 0);
   }
   return g_split_min;
 }

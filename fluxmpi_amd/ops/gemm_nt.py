@@ -72,7 +72,7 @@ def supported(rows: int, n_out: int, k: int, *tensors: torch.Tensor, fused: bool
 
 
 def set_split(min_ktiles: int) -> None:
-    """The split-K tail of the persistent kernel (``FLUXMPI_GEMM_NT_SPLIT``, default 8): the last,
+    """The split-K tail of the persistent kernel (``FLUXMPI_GEMM_NT_SPLIT``, default 0 = off: measured slower end to end, profiles/rd5d_*): the last,
     partial round of each XCD's tiles is cut into even k-tile ranges of at least ``min_ktiles``
     spread over all its workgroups (pieces summed by the last arriving workgroup, in piece order:
     deterministic); ``0`` runs the last round tile-granular."""

@@ -2,7 +2,7 @@
 """gemm_nt.hip (ping-pong 8-wave 256x256 NT GEMM) vs hipBLASLt (torch), TFLOP/s on
 uniform [-1, 1) bf16 operands (cdna_hip_programming.md rule 25), interleaved rounds in one process.
 
-Split-K tail arms: nt_s<k> = the default kernel with FLUXMPI_GEMM_NT_SPLIT = k (0: off; nt = 8).
+Split-K tail arms: nt_s<k> = the default kernel with FLUXMPI_GEMM_NT_SPLIT = k (0: off, the default; nt = the current setting).
 
 Shapes: 4096^3 and the ViT-B/16 Linears at batch 256 (M = 50432 tokens), forward (x W^T),
 input gradient (dy W, ours on W^T), fc1 forward + bias + GELU (EPI 1), fc2 input gradient +
