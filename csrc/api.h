@@ -72,8 +72,6 @@ void bn_bwd(const void* dy, const void* x, const void* y, const uint8_t* relu_ma
             const float* save_mean, const float* save_invstd, void* dx, void* dres,
             float* dweight, float* dbias, float* workspace, int64_t rows, int64_t C, int relu,
             int dtype, hipStream_t stream, int stats_ready = 0);
-// every BatchNorm workspace: bn_workspace_floats() zeroed floats ([64][2][2048] shards + the
-// backward reduction's last-arriver ticket at a fixed offset; left zeroed after each call)
 size_t bn_workspace_floats(int64_t rows, int64_t C);
 // Split forward for producer/consumer fusion with the GEMM:
 // bn_stats_finalize: [stats pass over x unless stats_ready (a GEMM epilogue already

@@ -13,9 +13,8 @@
 // Reductions: a workgroup accumulates fp32 per-channel partials over its rows
 // in registers, reduces the lanes that share a channel vector through LDS and
 // adds its partial to one of 64 shards of a [64][2][C] fp32 accumulator with
-// global float atomics. A tiny finalize kernel (forward statistics; or, in the
-// backward reductions, the reduce kernel's last workgroup) sums the shards into
-// the per-channel statistics (and re-zeroes them, so the persistent workspace
+// global float atomics. A tiny finalize kernel sums the shards into the
+// per-channel statistics (and re-zeroes them, so the persistent workspace
 // needs no memset per call); the consumer kernels derive their per-channel
 // coefficients from those statistics (registers, or LDS when C/8 does not divide
 // the workgroup). Grids are one full round of resident workgroups (occupancy x CUs).
@@ -206,55 +205,17 @@ __global__ __launch_bounds__(kFinCh * kFinGroups) void bn_finalize_bwd_kernel(fl
   dw[c] = q;  // sum(dy_eff * xhat)
 }
 
-// Last-arriver finalize of the backward row reductions (no finalize launch of their own: one
-// kernel fewer per BatchNorm backward). Every workgroup's shard atomics are released at agent
-// scope before it takes a ticket; the workgroup with the last ticket sums the kRedShards shards
-// of each channel in shard order (bit-identical to take_shards over a 16-shard workspace), reads
-// them with agent-scope atomic loads (coherent across the XCDs' L2s), re-zeroes them and resets
-// the ticket for the next launch. The ticket lives in the workspace's slack (kTicketOff).
-constexpr int64_t kTicketOff = static_cast<int64_t>(kShards) * 2 * kMaxC;
-
-__device__ __forceinline__ bool last_arriver(int* __restrict__ ticket) {
-  __shared__ int s_last;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  __syncthreads();
-  if (threadIdx.x == 0)
-    s_last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
-             static_cast<int>(gridDim.x) - 1;
-  __syncthreads();
-  if (!s_last) return false;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  return true;
-}
-
-__device__ __forceinline__ void take_red_shards(float* __restrict__ acc, int C, float* __restrict__ out_s,
-                                                float* __restrict__ out_q) {
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float va[kRedShards], vb[kRedShards];
-#pragma unroll
-    for (int k = 0; k < kRedShards; ++k) {
-      va[k] = __hip_atomic_load(acc + static_cast<size_t>(k) * 2 * C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      vb[k] = __hip_atomic_load(acc + static_cast<size_t>(k) * 2 * C + C + c, __ATOMIC_RELAXED,
-                                __HIP_MEMORY_SCOPE_AGENT);
-    }
-    float a = 0.f, b = 0.f;
-#pragma unroll
-    for (int k = 0; k < kRedShards; ++k) {
-      a += va[k];
-      b += vb[k];
-    }
-#pragma unroll
-    for (int k = 0; k < kRedShards; ++k) {
-      __hip_atomic_store(acc + static_cast<size_t>(k) * 2 * C + c, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(acc + static_cast<size_t>(k) * 2 * C + C + c, 0.f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    out_s[c] = a;
-    out_q[c] = b;
-  }
-}
-
-__device__ __forceinline__ void reset_ticket(int* __restrict__ ticket) {
-  if (threadIdx.x == 0) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// the dual (bn3 + downsample) backward's two finalizes in one launch: blockIdx.y picks the workspace
+__global__ __launch_bounds__(kFinCh * kFinGroups) void bn_finalize_bwd2_kernel(float* __restrict__ acc, float* __restrict__ acc2,
+                                                                               int C, float* __restrict__ dw,
+                                                                               float* __restrict__ db, float* __restrict__ dw2,
+                                                                               float* __restrict__ db2) {
+  float s, q;
+  int c;
+  const bool second = blockIdx.y != 0;
+  if (!take_shards(second ? acc2 : acc, C, s, q, c)) return;
+  (second ? db2 : db)[c] = s;
+  (second ? dw2 : dw)[c] = q;
 }
 
 // ---------------------------------------------------------------- forward
@@ -403,8 +364,7 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const T* __rest
                                                                  const float* __restrict__ b,
                                                                  const float* __restrict__ smean,
                                                                  const float* __restrict__ sinv, int64_t rows, int C,
-                                                                 Geo g, float* __restrict__ acc,
-                                                                 float* __restrict__ dw, float* __restrict__ db) {
+                                                                 Geo g, float* __restrict__ acc) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int t = threadIdx.x;
   const int r0 = t / g.cv, c8 = t % g.cv;
@@ -468,10 +428,6 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_kernel(const T* __rest
     }
   }
   block_reduce_atomic(s, q, g.cv, g.rpi, C, acc, smem);
-  int* ticket = reinterpret_cast<int*>(acc + kTicketOff);
-  if (!last_arriver(ticket)) return;
-  take_red_shards(acc, C, db, dw);  // db = sum(dy_eff), dw = sum(dy_eff * xhat)
-  reset_ticket(ticket);
 }
 
 // dx = w*invstd * (dy_eff - sum_dy/R - xhat * sum_dy_xhat/R); dres = dy_eff
@@ -654,8 +610,7 @@ template <typename T>
 __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_dual_kernel(
     const T* __restrict__ dy, const uint8_t* __restrict__ mask, const T* __restrict__ x, const T* __restrict__ x2,
     const float* __restrict__ mean, const float* __restrict__ inv, const float* __restrict__ mean2,
-    const float* __restrict__ inv2, int64_t rows, int C, Geo g, float* __restrict__ acc, float* __restrict__ acc2,
-    float* __restrict__ dw, float* __restrict__ db, float* __restrict__ dw2, float* __restrict__ db2) {
+    const float* __restrict__ inv2, int64_t rows, int C, Geo g, float* __restrict__ acc, float* __restrict__ acc2) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int t = threadIdx.x;
   const int r0 = t / g.cv, c8 = t % g.cv;
@@ -711,11 +666,6 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_reduce_dual_kernel(
   block_reduce_atomic(s, q, g.cv, g.rpi, C, acc, smem);
   __syncthreads();  // the LDS staging is reused
   block_reduce_atomic(s, q2, g.cv, g.rpi, C, acc2, smem);
-  int* ticket = reinterpret_cast<int*>(acc + kTicketOff);
-  if (!last_arriver(ticket)) return;
-  take_red_shards(acc, C, db, dw);
-  take_red_shards(acc2, C, db2, dw2);
-  reset_ticket(ticket);
 }
 
 // dx = A*dy_eff + B*x + D, dx2 = A2*dy_eff + B2*x2 + D2 (coefficients as in bn_bwd_dx_kernel)
@@ -882,17 +832,18 @@ void bwd_t(const void* dy, const void* x, const void* y, const uint8_t* mask, co
   {                                                                                                             \
     const Geo g = reduce_geometry(reinterpret_cast<const void*>(bn_bwd_reduce_kernel<T, RM>), rows, C);          \
     bn_bwd_reduce_kernel<T, RM><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(dyr, xr, yr, mask, w, b, sm, si,   \
-                                                                              rows, (int)C, g, ws, dw, db);     \
+                                                                              rows, (int)C, g, ws);             \
   }
   // stats_ready: the reductions were accumulated into ws by the producer of dy (the GEMM's
-  // BN-backward epilogue), so the reduce pass over (dy, x) is skipped and only the finalize
-  // runs; otherwise the reduce kernel's last workgroup finalizes
-  if (stats_ready) bn_finalize_bwd_kernel<<<finalize_blocks(C), kFinCh * kFinGroups, 0, s>>>(ws, (int)C, dw, db);
+  // BN-backward epilogue), so the reduce pass over (dy, x) is skipped
+  if (stats_ready) {}
   else if (rm == 0) RED(0)
   else if (rm == 1) RED(1)
   else if (rm == 2) RED(2)
   else RED(3)
 #undef RED
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+  bn_finalize_bwd_kernel<<<finalize_blocks(C), kFinCh * kFinGroups, 0, s>>>(ws, (int)C, dw, db);
   FLUXMPI_HIP_CHECK(hipGetLastError());
   const int64_t nvec = rows * C / 8;
   T* dxr = static_cast<T*>(dx);
@@ -941,7 +892,10 @@ void bwd_dual_t(const void* dy, const uint8_t* mask, const void* x, const void* 
   const T* x2r = static_cast<const T*>(x2);
   const Geo g = reduce_geometry(reinterpret_cast<const void*>(bn_bwd_reduce_dual_kernel<T>), rows, C);
   bn_bwd_reduce_dual_kernel<T><<<g.blocks, kThreads, reduce_smem(g, C), s>>>(dyr, mask, xr, x2r, sm, si, sm2, si2,
-                                                                             rows, (int)C, g, ws, ws2, dw, db, dw2, db2);
+                                                                             rows, (int)C, g, ws, ws2);
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+  bn_finalize_bwd2_kernel<<<dim3(finalize_blocks(C), 2), kFinCh * kFinGroups, 0, s>>>(ws, ws2, (int)C, dw, db, dw2,
+                                                                                      db2);
   FLUXMPI_HIP_CHECK(hipGetLastError());
   const int64_t nvec = rows * C / 8;
   auto k = bn_bwd_dx_dual_kernel<T>;
@@ -989,8 +943,7 @@ void bn_bwd_dual(const void* dy, const uint8_t* mask, const void* x, const void*
 
 size_t bn_workspace_floats(int64_t rows, int64_t C) {
   (void)rows;
-  (void)C;
-  return static_cast<size_t>(kTicketOff) + 64;  // shards at any C <= kMaxC + the reductions' ticket
+  return static_cast<size_t>(kShards) * 2 * static_cast<size_t>(C);
 }
 
 void bn_fwd_train(const void* x, void* y, const void* residual, const float* weight, const float* bias,
