@@ -60,8 +60,9 @@ def parse():
     ap.add_argument("--deq-solver", default="",
                     help="DEQ models: solver settings as k=v pairs, e.g. 'tol=1e-2,bwd_tol=1e-2,max_iter=30'")
     ap.add_argument("--overlap-opt", type=int, default=None, choices=[0, 1],
-                    help="per-bucket optimiser overlap (default: FLUXMPI_OVERLAP_OPT): each bucket's fused "
-                         "update is enqueued during backward as soon as its gradient is reduced")
+                    help="per-bucket optimiser overlap: each bucket's fused update is enqueued during "
+                         "backward behind its allreduce (default: on when the step communicates — N>1 or "
+                         "--force-comm — and not --graph; the bench loop is backward -> step())")
     ap.add_argument("--api", default="ddp", choices=["ddp", "functional"],
                     help="ddp: the DDP engine (hooks, buckets born in the comm buffers, fused optimiser); "
                          "functional: the reference's API shape (src/optimizer.jl:45-65) — the nested "
@@ -275,8 +276,11 @@ def main():
             return 2
         ddp = Functional(FluxMPI, O, model, rule)
     else:
+        ovo = args.overlap_opt
+        if ovo is None:  # the engine's contract (every backward followed by step()) holds here
+            ovo = int((world > 1 or args.force_comm) and not args.graph and not args.no_overlap)
         ddp = DDP(model, rule, average=True, overlap=not args.no_overlap, force_comm=args.force_comm,
-                  overlap_opt=None if args.overlap_opt is None else bool(args.overlap_opt))
+                  overlap_opt=bool(ovo))
 
     B = args.batch
     gx = torch.Generator(device=dev).manual_seed(rank)
