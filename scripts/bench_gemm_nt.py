@@ -12,6 +12,7 @@ matmul of the same bf16 operands before it is timed.
 usage: python scripts/bench_gemm_nt.py [--quick]  -> JSON lines
 """
 import json
+import os
 import sys
 
 import torch
@@ -62,6 +63,9 @@ def checks_only(C, st, name, m, n, k):
               k, k, n, m, n, k, 1, st)
     torch.cuda.synchronize()
     check(f"{name}_epi1_g", c2, torch.nn.functional.gelu((ref + bias).bfloat16().float(), approximate="tanh"))
+
+
+SPLITS = tuple(int(v) for v in os.environ.get("BENCH_NT_SPLITS", "0,8,16,24,32").split(","))
 
 
 def main():
@@ -123,11 +127,11 @@ def main():
         for rnd in range(3):
             best.setdefault("blas", []).append(t_us(lambda: torch.matmul(a, wt)))
             best.setdefault("blas_bias", []).append(t_us(lambda: torch.nn.functional.linear(a, w, bias.bfloat16())))
-            for sm in (0, 4, 16):  # the split-K tail's minimum share (0: the last round tile-granular)
+            for sm in SPLITS:  # the split-K tail's minimum share (0: the last round tile-granular)
                 C.gemm_nt_set_split(sm)
                 best.setdefault(f"nt_s{sm}", []).append(t_us(lambda: ours()))
                 best.setdefault(f"nt_epi2_s{sm}", []).append(t_us(lambda: ours(2, h=h, part=part)))
-            C.gemm_nt_set_split(8)
+            C.gemm_nt_set_split(0)
             best.setdefault("nt", []).append(t_us(lambda: ours()))
             best.setdefault("nt_bias", []).append(t_us(lambda: ours(0, bias_=bias)))
             best.setdefault("nt_gelu", []).append(t_us(lambda: ours(1, bias_=bias)))
