@@ -256,19 +256,20 @@ void transpose_bf16(const void* src, void* dst, int64_t rows, int64_t cols, int6
                     hipStream_t stream);
 
 // ---- Anderson-acceleration solver (DEQ) --------------------------------------------
-// X, F: fp32 histories [bsz][m rows of row_stride][d] (batch_stride between batches).
+// X: fp32 history, F: fp32 or bf16 history, [bsz][m rows of row_stride][d] (batch_stride between batches).
 // anderson_gram: partials[b][chunk][37]: the upper-triangle pair sums of G G^T (G = F - X over
 // rows < n; pair (i, j>=i) at index i*n - i*(i-1)/2 + (j-i)) and |F[last]|^2 at [36];
 // sum over chunks on the host side. anderson_gram_chunks: the chunk count to allocate for.
 int anderson_gram_chunks(int64_t bsz, int64_t d);
 // G (nullable): stored G = F - X rows (same layout); rows with their bit set in `fresh` are
 // recomputed from F - X and written to G, the others are read from G.
-void anderson_gram(const float* X, const float* F, float* G, unsigned fresh, float* partials, int64_t bsz, int64_t d,
-                   int64_t row_stride, int64_t batch_stride, int n, int last, int chunks, hipStream_t stream);
+// F: fp32 or bf16 (f_dtype), same element layout as X.
+void anderson_gram(const float* X, const void* F, int f_dtype, float* G, unsigned fresh, float* partials, int64_t bsz,
+                   int64_t d, int64_t row_stride, int64_t batch_stride, int n, int last, int chunks, hipStream_t stream);
 // X[b, slot] = beta * sum_i alpha[b][i] F[b, i] + (1 - beta) * sum_i alpha[b][i] X[b, i] (i < n);
 // z (nullable, [bsz][d], dtype z_dtype): the new iterate cast to the model dtype.
-void anderson_mix(float* X, const float* F, const float* alpha, void* z, int z_dtype, int64_t bsz, int64_t d,
-                  int64_t row_stride, int64_t batch_stride, int n, int slot, float beta, hipStream_t stream);
+void anderson_mix(float* X, const void* F, int f_dtype, const float* alpha, void* z, int z_dtype, int64_t bsz,
+                  int64_t d, int64_t row_stride, int64_t batch_stride, int n, int slot, float beta, hipStream_t stream);
 // anderson_solve: from anderson_gram's partials, alpha[b][0..n) of the regularised Anderson system
 // [[0, 1^T], [1, G G^T + lam I]] a = e_0 (a[1..n]) per batch element (bsz <= 1024, one launch),
 // and (res nullable) the relative residual of row `last` into res[0].
@@ -294,14 +295,14 @@ void groupnorm_nhwc_bwd(const void* dy, const void* h, const float* mean, const 
 // ---- the DEQ cell in one kernel per evaluation (kernels/deq_cell.hip) ----------------------
 // f(z, x) = GN3(relu(z + GN2(x + conv2(GN1(relu(conv1 z)))))) on NHWC bf16 [N][H*W][48]; one
 // workgroup per sample, everything LDS-resident. w1 / w2: [C][9C] bf16 with k = tap * C + ci.
-// gn_w / gn_b: 3 fp32 vectors each (nullable). out (bf16) and/or out32 (fp32, sample stride
-// out32_stride elements); h[3] (the GroupNorm inputs) and mean / rstd[3] ([N][G]) nullable.
+// gn_w / gn_b: 3 fp32 vectors each (nullable). out (bf16, sample stride out_stride elements, 0 =
+// dense) and/or out32 (fp32, sample stride out32_stride elements); h[3] (the GroupNorm inputs) and mean / rstd[3] ([N][G]) nullable.
 // vjp: J_f(z)^T u from that state; w2t / w1t are the transposed tap-flipped filters (k = tap * C + co).
 bool deq_cell_supported(int64_t H, int64_t W, int64_t C, int64_t G);
 void deq_cell_fwd(const void* z, const void* x, const void* w1, const void* w2, const float* const* gn_w,
                   const float* const* gn_b, void* out, float* out32, int64_t out32_stride, void* const* h,
                   float* const* mean, float* const* rstd, int64_t N, int64_t H, int64_t W, int64_t C, int64_t G,
-                  float eps, hipStream_t stream);
+                  float eps, hipStream_t stream, int64_t out_stride = 0);
 // grad / ss_part (nullable together): the adjoint update fused in, out = bf16(J^T u + grad) and
 // ss_part[N] the per-sample sum of (out - u)^2; deq_adjoint_check sums them (ss_out) and tests
 // flag = (sum <= *thresh2) in one tiny launch.

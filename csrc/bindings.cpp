@@ -193,9 +193,10 @@ PYBIND11_MODULE(_C, m) {
 
   // ---- Anderson solver (DEQ) ---------------------------------------------------
   m.def("anderson_gram_chunks", &anderson_gram_chunks);
-  m.def("anderson_gram", [](uintptr_t X, uintptr_t F, uintptr_t G, unsigned fresh, uintptr_t part, int64_t bsz,
-                            int64_t d, int64_t rs, int64_t bs, int n, int last, int chunks, uintptr_t stream) {
-    anderson_gram(reinterpret_cast<const float*>(X), reinterpret_cast<const float*>(F), reinterpret_cast<float*>(G),
+  m.def("anderson_gram", [](uintptr_t X, uintptr_t F, int fdt, uintptr_t G, unsigned fresh, uintptr_t part,
+                            int64_t bsz, int64_t d, int64_t rs, int64_t bs, int n, int last, int chunks,
+                            uintptr_t stream) {
+    anderson_gram(reinterpret_cast<const float*>(X), reinterpret_cast<const void*>(F), fdt, reinterpret_cast<float*>(G),
                   fresh, reinterpret_cast<float*>(part), bsz, d, rs, bs, n, last, chunks, S(stream));
   });
   m.def("adjoint_step_blocks", &adjoint_step_blocks);
@@ -210,9 +211,9 @@ PYBIND11_MODULE(_C, m) {
     anderson_solve(reinterpret_cast<const float*>(part), chunks, bsz, n, last, lam, reinterpret_cast<float*>(alpha),
                    reinterpret_cast<float*>(res), S(stream));
   });
-  m.def("anderson_mix", [](uintptr_t X, uintptr_t F, uintptr_t alpha, uintptr_t z, int zdt, int64_t bsz, int64_t d,
-                           int64_t rs, int64_t bs, int n, int slot, float beta, uintptr_t stream) {
-    anderson_mix(reinterpret_cast<float*>(X), reinterpret_cast<const float*>(F), reinterpret_cast<const float*>(alpha),
+  m.def("anderson_mix", [](uintptr_t X, uintptr_t F, int fdt, uintptr_t alpha, uintptr_t z, int zdt, int64_t bsz,
+                           int64_t d, int64_t rs, int64_t bs, int n, int slot, float beta, uintptr_t stream) {
+    anderson_mix(reinterpret_cast<float*>(X), reinterpret_cast<const void*>(F), fdt, reinterpret_cast<const float*>(alpha),
                  reinterpret_cast<void*>(z), zdt, bsz, d, rs, bs, n, slot, beta, S(stream));
   });
 
@@ -239,7 +240,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("deq_cell_fwd", [](uintptr_t z, uintptr_t x, uintptr_t w1, uintptr_t w2, std::array<uintptr_t, 3> gw,
                            std::array<uintptr_t, 3> gb, uintptr_t out, uintptr_t out32, int64_t out32_stride,
                            std::array<uintptr_t, 3> h, std::array<uintptr_t, 3> mean, std::array<uintptr_t, 3> rstd,
-                           int64_t N, int64_t H, int64_t W, int64_t C, int64_t G, float eps, uintptr_t stream) {
+                           int64_t N, int64_t H, int64_t W, int64_t C, int64_t G, float eps, uintptr_t stream,
+                           int64_t out_stride) {
     const float* gwp[3];
     const float* gbp[3];
     void* hp[3];
@@ -254,7 +256,7 @@ PYBIND11_MODULE(_C, m) {
     }
     deq_cell_fwd(reinterpret_cast<const void*>(z), reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(w1),
                  reinterpret_cast<const void*>(w2), gwp, gbp, reinterpret_cast<void*>(out),
-                 reinterpret_cast<float*>(out32), out32_stride, hp, mp, rp, N, H, W, C, G, eps, S(stream));
+                 reinterpret_cast<float*>(out32), out32_stride, hp, mp, rp, N, H, W, C, G, eps, S(stream), out_stride);
   });
   m.def("deq_cell_vjp", [](uintptr_t u, std::array<uintptr_t, 3> h, uintptr_t w2t, uintptr_t w1t,
                            std::array<uintptr_t, 3> gw, std::array<uintptr_t, 3> mean, std::array<uintptr_t, 3> rstd,

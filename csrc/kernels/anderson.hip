@@ -1,6 +1,7 @@
 // Anderson-acceleration solver kernels for the Deep Equilibrium Model — gfx950.
 //
-// The solver keeps a history of m iterates X[b, i, :] and their images F[b, i, :] (fp32,
+// The solver keeps a history of m iterates X[b, i, :] (fp32) and their images F[b, i, :] (fp32,
+// or bf16 when the model computes in bf16 — the cell's outputs are bf16 values either way),
 // row length d = C*H*W, e.g. 48*28*28 = 37632) and, every iteration, needs
 //   gram[b]  = G G^T  with G = F[b, :n] - X[b, :n]         (n <= m <= 8 rows)
 //   X[b, s]  = beta * alpha[b] F[b, :n] + (1 - beta) * alpha[b] X[b, :n]
@@ -35,21 +36,37 @@ __device__ __forceinline__ float dot4(const float4& a, const float4& b) {
   return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
 }
 
+// 4 consecutive elements of an F history row at element offset e, widened to fp32. F is bf16 when
+// the model computes in bf16: its values are the cell's bf16 outputs either way, so the narrower
+// history is exact and halves the bytes of the mix's N-row read.
+template <typename FT>
+__device__ __forceinline__ float4 ldf4(const FT* __restrict__ p, int64_t e) {
+  if constexpr (sizeof(FT) == 4) {
+    return *reinterpret_cast<const float4*>(p + e);
+  } else {
+    const uint2 u = *reinterpret_cast<const uint2*>(p + e);
+    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                       __uint_as_float(u.y & 0xffff0000u));
+  }
+}
+
 // grid (chunks, bsz). part[b][chunk][kOut]
-// G (nullable): stored differences, same layout as X / F. With G, rows whose bit is set in
-// `fresh` are formed from F - X and written back to G; the other rows are read from G
-// (k > 2: one fresh row, so 2 + (n-1) rows are read instead of 2n).
-template <int N>
-__global__ __launch_bounds__(kThreads) void gram_kernel(const float* __restrict__ X, const float* __restrict__ F,
+// ONE = false: every row's G = F - X is formed from the history (and written to G when G is
+// given). ONE = true (the steady state): only row `fr` is new; it is formed from F - X and
+// written to G, the other rows are read from G. Every load is unconditional from a
+// wave-uniformly chosen address (a load under a branch is waited for at the join: N serial
+// memory latencies per iteration otherwise): with ONE, row fr's G load re-reads its X line (a
+// cache hit) instead of a stale G line. |F[last]|^2 needs last == fr with ONE (host-checked).
+template <int N, bool ONE, typename FT>
+__global__ __launch_bounds__(kThreads) void gram_kernel(const float* __restrict__ X, const FT* __restrict__ F,
                                                         float* __restrict__ G, float* __restrict__ part, int64_t d4,
                                                         int64_t row_stride, int64_t batch_stride, int64_t chunk4,
-                                                        int last, unsigned fresh) {
+                                                        int last, int fr) {
   const int b = blockIdx.y;
   const int c = blockIdx.x;
-  const float4* xb = reinterpret_cast<const float4*>(X + b * batch_stride);
-  const float4* fb = reinterpret_cast<const float4*>(F + b * batch_stride);
-  float4* gb = G != nullptr ? reinterpret_cast<float4*>(G + b * batch_stride) : nullptr;
-  const int64_t rs4 = row_stride / 4;
+  const float* xb = X + b * batch_stride;
+  const FT* fb = F + b * batch_stride;
+  float* gb = G != nullptr ? G + b * batch_stride : nullptr;
   float acc[kPairs];
   float fn = 0.f;
 #pragma unroll
@@ -57,33 +74,32 @@ __global__ __launch_bounds__(kThreads) void gram_kernel(const float* __restrict_
   const int64_t v0 = static_cast<int64_t>(c) * chunk4;
   int64_t v1 = v0 + chunk4;
   if (v1 > d4) v1 = d4;
-  // Per row, two UNCONDITIONAL loads from wave-uniformly chosen sources (a load under a
-  // branch is waited for at the join: N serial memory latencies per iteration otherwise):
-  //   fresh row (g = f - x):     A = f, B = x
-  //   stored row, the last one:  A = g, B = f   (|f_last|^2)
-  //   stored row:                A = g, B = g   (a cache hit)
-  const float4* gsrc = gb != nullptr ? gb : fb;
   for (int64_t v = v0 + threadIdx.x; v < v1; v += kThreads) {
-    float4 av[N], bv[N];
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const bool fr = gb == nullptr || ((fresh >> i) & 1u);
-      av[i] = (fr ? fb : gsrc)[i * rs4 + v];
-      bv[i] = (fr ? xb : (i == last ? fb : gsrc))[i * rs4 + v];
-    }
+    const int64_t e = 4 * v;
     float4 g[N];
+    if constexpr (ONE) {
+      const float4 f = ldf4(fb, fr * row_stride + e);
+      const float4 x = *reinterpret_cast<const float4*>(xb + fr * row_stride + e);
 #pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const bool fr = gb == nullptr || ((fresh >> i) & 1u);
-      if (fr) {
-        g[i] = make_float4(av[i].x - bv[i].x, av[i].y - bv[i].y, av[i].z - bv[i].z, av[i].w - bv[i].w);
-        if (gb != nullptr) gb[i * rs4 + v] = g[i];
-      } else {
-        g[i] = av[i];
+      for (int i = 0; i < N; ++i) g[i] = *reinterpret_cast<const float4*>((i == fr ? xb : gb) + i * row_stride + e);
+      const float4 gn = make_float4(f.x - x.x, f.y - x.y, f.z - x.z, f.w - x.w);
+#pragma unroll
+      for (int i = 0; i < N; ++i)
+        if (i == fr) g[i] = gn;
+      *reinterpret_cast<float4*>(gb + fr * row_stride + e) = gn;
+      fn += dot4(f, f);
+    } else {
+      float4 f[N], x[N];
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        f[i] = ldf4(fb, i * row_stride + e);
+        x[i] = *reinterpret_cast<const float4*>(xb + i * row_stride + e);
       }
-      if (i == last) {
-        const float4 f = fr ? av[i] : bv[i];
-        fn += dot4(f, f);
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        g[i] = make_float4(f[i].x - x[i].x, f[i].y - x[i].y, f[i].z - x[i].z, f[i].w - x[i].w);
+        if (gb != nullptr) *reinterpret_cast<float4*>(gb + i * row_stride + e) = g[i];
+        if (i == last) fn += dot4(f[i], f[i]);
       }
     }
     int p = 0;
@@ -119,26 +135,28 @@ __global__ __launch_bounds__(kThreads) void gram_kernel(const float* __restrict_
 }
 
 // grid (ceil(d4 / kThreads), bsz): X[b, slot] = beta * sum_i a_i F[b,i] + (1-beta) * sum_i a_i X[b,i]
-template <int N, bool MIXX, typename Z>
-__global__ __launch_bounds__(kThreads) void mix_kernel(float* __restrict__ X, const float* __restrict__ F,
+template <int N, bool MIXX, typename Z, typename FT>
+__global__ __launch_bounds__(kThreads) void mix_kernel(float* __restrict__ X, const FT* __restrict__ F,
                                                        const float* __restrict__ alpha, Z* __restrict__ z, int64_t d4,
                                                        int64_t row_stride, int64_t batch_stride, int slot, float beta) {
   const int b = blockIdx.y;
   const int64_t v = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
   if (v >= d4) return;
-  const int64_t rs4 = row_stride / 4;
-  float4* xb = reinterpret_cast<float4*>(X + b * batch_stride);
-  const float4* fb = reinterpret_cast<const float4*>(F + b * batch_stride);
+  const int64_t e = 4 * v;
+  float* xb = X + b * batch_stride;
+  const FT* fb = F + b * batch_stride;
   float a[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) a[i] = alpha[b * N + i];
   float4 sf = make_float4(0.f, 0.f, 0.f, 0.f), sx = sf;
+  float4 fv[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) fv[i] = ldf4(fb, i * row_stride + e);
 #pragma unroll
   for (int i = 0; i < N; ++i) {
-    const float4 f = fb[i * rs4 + v];
-    sf.x += a[i] * f.x; sf.y += a[i] * f.y; sf.z += a[i] * f.z; sf.w += a[i] * f.w;
+    sf.x += a[i] * fv[i].x; sf.y += a[i] * fv[i].y; sf.z += a[i] * fv[i].z; sf.w += a[i] * fv[i].w;
     if (MIXX) {
-      const float4 x = xb[i * rs4 + v];
+      const float4 x = *reinterpret_cast<const float4*>(xb + i * row_stride + e);
       sx.x += a[i] * x.x; sx.y += a[i] * x.y; sx.z += a[i] * x.z; sx.w += a[i] * x.w;
     }
   }
@@ -147,9 +165,9 @@ __global__ __launch_bounds__(kThreads) void mix_kernel(float* __restrict__ X, co
     const float c = 1.f - beta;
     o = make_float4(beta * sf.x + c * sx.x, beta * sf.y + c * sx.y, beta * sf.z + c * sx.z, beta * sf.w + c * sx.w);
   }
-  xb[slot * rs4 + v] = o;
+  *reinterpret_cast<float4*>(xb + slot * row_stride + e) = o;
   if (z != nullptr) {
-    Z* zp = z + (static_cast<int64_t>(b) * d4 + v) * 4;
+    Z* zp = z + static_cast<int64_t>(b) * d4 * 4 + e;
     zp[0] = static_cast<Z>(o.x);
     zp[1] = static_cast<Z>(o.y);
     zp[2] = static_cast<Z>(o.z);
@@ -303,10 +321,11 @@ __global__ __launch_bounds__(kThreads) void adjoint_step_kernel(const T* __restr
   }
 }
 
+// X (fp32) and F (fp32 or bf16) share one element layout: [bsz][rows of row_stride][d]
 void check_layout(const void* X, const void* F, int64_t d, int64_t row_stride, int64_t batch_stride, int n) {
   if (n < 1 || n > kMaxRows) throw std::runtime_error("anderson: need 1 <= n <= 8 (got " + std::to_string(n) + ")");
   if (d % 4 != 0 || row_stride % 4 != 0 || batch_stride % 4 != 0 || row_stride < d)
-    throw std::runtime_error("anderson: d and strides must be multiples of 4 floats");
+    throw std::runtime_error("anderson: d and strides must be multiples of 4 elements");
   if (((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(F)) & 15u) != 0)
     throw std::runtime_error("anderson: X and F must be 16-byte aligned");
 }
@@ -323,9 +342,21 @@ int anderson_gram_chunks(int64_t bsz, int64_t d) {
   return static_cast<int>(chunks);
 }
 
-void anderson_gram(const float* X, const float* F, float* G, unsigned fresh, float* partials, int64_t bsz, int64_t d,
-                   int64_t row_stride, int64_t batch_stride, int n, int last, int chunks, hipStream_t stream) {
+template <int N, bool ONE>
+void gram_launch(const float* X, const void* F, int fdt, float* G, float* part, dim3 grid, int64_t d4, int64_t rs,
+                 int64_t bs, int64_t chunk4, int last, int fr, hipStream_t s) {
+  if (fdt == kBF16)
+    gram_kernel<N, ONE, bf16><<<grid, kThreads, 0, s>>>(X, static_cast<const bf16*>(F), G, part, d4, rs, bs, chunk4,
+                                                        last, fr);
+  else
+    gram_kernel<N, ONE, float><<<grid, kThreads, 0, s>>>(X, static_cast<const float*>(F), G, part, d4, rs, bs, chunk4,
+                                                         last, fr);
+}
+
+void anderson_gram(const float* X, const void* F, int f_dtype, float* G, unsigned fresh, float* partials, int64_t bsz,
+                   int64_t d, int64_t row_stride, int64_t batch_stride, int n, int last, int chunks, hipStream_t stream) {
   check_layout(X, F, d, row_stride, batch_stride, n);
+  if (f_dtype != kF32 && f_dtype != kBF16) throw std::runtime_error("anderson_gram: F must be fp32 or bf16");
   if (G != nullptr && (reinterpret_cast<uintptr_t>(G) & 15u) != 0)
     throw std::runtime_error("anderson_gram: G must be 16-byte aligned");
   if (last < 0 || last >= n) throw std::runtime_error("anderson_gram: last row out of range");
@@ -333,10 +364,14 @@ void anderson_gram(const float* X, const float* F, float* G, unsigned fresh, flo
   const int64_t d4 = d / 4;
   const int64_t chunk4 = (d4 + chunks - 1) / chunks;
   dim3 grid(chunks, static_cast<unsigned>(bsz));
-#define GRAM_CASE(NN)                                                                                   \
-  case NN:                                                                                              \
-    gram_kernel<NN><<<grid, kThreads, 0, stream>>>(X, F, G, partials, d4, row_stride, batch_stride, chunk4, \
-                                                   last, fresh);                                           \
+  // one new row (the steady state): the others come from G; otherwise every row from F - X
+  const bool one = G != nullptr && fresh == (1u << last);
+#define GRAM_CASE(NN)                                                                                              \
+  case NN:                                                                                                         \
+    if (one) gram_launch<NN, true>(X, F, f_dtype, G, partials, grid, d4, row_stride, batch_stride, chunk4, last,  \
+                                   last, stream);                                                                  \
+    else gram_launch<NN, false>(X, F, f_dtype, G, partials, grid, d4, row_stride, batch_stride, chunk4, last, 0,  \
+                                stream);                                                                           \
     break;
   switch (n) {
     GRAM_CASE(1) GRAM_CASE(2) GRAM_CASE(3) GRAM_CASE(4) GRAM_CASE(5) GRAM_CASE(6) GRAM_CASE(7) GRAM_CASE(8)
@@ -345,21 +380,22 @@ void anderson_gram(const float* X, const float* F, float* G, unsigned fresh, flo
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
 
-template <int N, bool MIXX>
-void mix_launch(float* X, const float* F, const float* alpha, void* z, int zdt, int64_t bsz, int64_t d4,
-                int64_t rs, int64_t bs, int slot, float beta, hipStream_t s) {
+template <int N, bool MIXX, typename FT>
+void mix_launch(float* X, const FT* F, const float* alpha, void* z, int zdt, int64_t bsz, int64_t d4, int64_t rs,
+                int64_t bs, int slot, float beta, hipStream_t s) {
   dim3 grid(static_cast<unsigned>((d4 + kThreads - 1) / kThreads), static_cast<unsigned>(bsz));
   switch (zdt) {
-    case kBF16: mix_kernel<N, MIXX, bf16><<<grid, kThreads, 0, s>>>(X, F, alpha, static_cast<bf16*>(z), d4, rs, bs, slot, beta); break;
-    case kF16: mix_kernel<N, MIXX, f16><<<grid, kThreads, 0, s>>>(X, F, alpha, static_cast<f16*>(z), d4, rs, bs, slot, beta); break;
-    case kF32: mix_kernel<N, MIXX, float><<<grid, kThreads, 0, s>>>(X, F, alpha, static_cast<float*>(z), d4, rs, bs, slot, beta); break;
+    case kBF16: mix_kernel<N, MIXX, bf16, FT><<<grid, kThreads, 0, s>>>(X, F, alpha, static_cast<bf16*>(z), d4, rs, bs, slot, beta); break;
+    case kF16: mix_kernel<N, MIXX, f16, FT><<<grid, kThreads, 0, s>>>(X, F, alpha, static_cast<f16*>(z), d4, rs, bs, slot, beta); break;
+    case kF32: mix_kernel<N, MIXX, float, FT><<<grid, kThreads, 0, s>>>(X, F, alpha, static_cast<float*>(z), d4, rs, bs, slot, beta); break;
     default: throw std::runtime_error("anderson_mix: unsupported z dtype");
   }
 }
 
-void anderson_mix(float* X, const float* F, const float* alpha, void* z, int z_dtype, int64_t bsz, int64_t d,
-                  int64_t row_stride, int64_t batch_stride, int n, int slot, float beta, hipStream_t stream) {
+void anderson_mix(float* X, const void* F, int f_dtype, const float* alpha, void* z, int z_dtype, int64_t bsz,
+                  int64_t d, int64_t row_stride, int64_t batch_stride, int n, int slot, float beta, hipStream_t stream) {
   check_layout(X, F, d, row_stride, batch_stride, n);
+  if (f_dtype != kF32 && f_dtype != kBF16) throw std::runtime_error("anderson_mix: F must be fp32 or bf16");
   if (slot < 0 || slot * row_stride + d > batch_stride) throw std::runtime_error("anderson_mix: slot out of range");
   if (bsz > 65535) throw std::runtime_error("anderson_mix: bsz > 65535");
   if (z != nullptr && (reinterpret_cast<uintptr_t>(z) & 7u) != 0)
@@ -367,10 +403,17 @@ void anderson_mix(float* X, const float* F, const float* alpha, void* z, int z_d
   const int64_t d4 = d / 4;
   const bool mixx = beta != 1.f;
   const int zdt = z != nullptr ? z_dtype : kF32;
-#define MIX_CASE(NN)                                                                                 \
-  case NN:                                                                                           \
-    if (mixx) mix_launch<NN, true>(X, F, alpha, z, zdt, bsz, d4, row_stride, batch_stride, slot, beta, stream); \
-    else mix_launch<NN, false>(X, F, alpha, z, zdt, bsz, d4, row_stride, batch_stride, slot, beta, stream);    \
+  const bf16* fh = static_cast<const bf16*>(F);
+  const float* ff = static_cast<const float*>(F);
+#define MIX_CASE(NN)                                                                                              \
+  case NN:                                                                                                        \
+    if (f_dtype == kBF16) {                                                                                       \
+      if (mixx) mix_launch<NN, true>(X, fh, alpha, z, zdt, bsz, d4, row_stride, batch_stride, slot, beta, stream); \
+      else mix_launch<NN, false>(X, fh, alpha, z, zdt, bsz, d4, row_stride, batch_stride, slot, beta, stream);    \
+    } else {                                                                                                      \
+      if (mixx) mix_launch<NN, true>(X, ff, alpha, z, zdt, bsz, d4, row_stride, batch_stride, slot, beta, stream); \
+      else mix_launch<NN, false>(X, ff, alpha, z, zdt, bsz, d4, row_stride, batch_stride, slot, beta, stream);    \
+    }                                                                                                             \
     break;
   switch (n) {
     MIX_CASE(1) MIX_CASE(2) MIX_CASE(3) MIX_CASE(4) MIX_CASE(5) MIX_CASE(6) MIX_CASE(7) MIX_CASE(8)

@@ -400,9 +400,10 @@ struct FwdArgs {
   const bf16* w1;  // [C][9C], k = tap * C + ci
   const bf16* w2;
   CellGN gn;
-  bf16* out;            // nullable
+  bf16* out;            // nullable, sample stride out_stride (an Anderson bf16 history slot, or dense)
   float* out32;         // nullable: fp32 copy of the output, sample stride out32_stride
   int64_t out32_stride;
+  int64_t out_stride;
   bf16* h[3];           // nullable: the GroupNorm inputs (the VJP's state)
   CellStats st;         // mean / rstd pointers nullable
 };
@@ -463,7 +464,7 @@ __global__ __launch_bounds__(kThreads) void deq_cell_fwd_kernel(FwdArgs a, CellS
   }
   if (a.h[2] != nullptr) store_lane(a.h[2] + so, v, L);
   gn_forward(v, a.gn.w[2], a.gn.b[2], part, red, coef, L, s, a.st.mean[2], a.st.rstd[2], n);
-  if (a.out != nullptr) store_lane(a.out + so, v, L);
+  if (a.out != nullptr) store_lane(a.out + static_cast<int64_t>(n) * a.out_stride, v, L);
   if (a.out32 != nullptr) {
     float* o = a.out32 + static_cast<int64_t>(n) * a.out32_stride;
 #pragma unroll
@@ -622,13 +623,15 @@ bool deq_cell_supported(int64_t H, int64_t W, int64_t C, int64_t G) {
 void deq_cell_fwd(const void* z, const void* x, const void* w1, const void* w2, const float* const* gn_w,
                   const float* const* gn_b, void* out, float* out32, int64_t out32_stride, void* const* h,
                   float* const* mean, float* const* rstd, int64_t N, int64_t H, int64_t W, int64_t C, int64_t G,
-                  float eps, hipStream_t stream) {
+                  float eps, hipStream_t stream, int64_t out_stride) {
   const CellShape s = cell_shape(N, H, W, C, G, eps);
   check16({z, x, w1, w2, out, out32, h[0], h[1], h[2]});
   if (out == nullptr && out32 == nullptr) throw std::runtime_error("deq_cell_fwd: no output");
   if (out32 != nullptr && out32_stride % 4 != 0) throw std::runtime_error("deq_cell_fwd: out32 stride % 4");
+  if (out_stride == 0) out_stride = H * W * C;
+  if (out_stride % 8 != 0 || out_stride < H * W * C) throw std::runtime_error("deq_cell_fwd: out stride");
   FwdArgs a{static_cast<const bf16*>(z), static_cast<const bf16*>(x), static_cast<const bf16*>(w1),
-            static_cast<const bf16*>(w2), {}, static_cast<bf16*>(out), out32, out32_stride, {}, {}};
+            static_cast<const bf16*>(w2), {}, static_cast<bf16*>(out), out32, out32_stride, out_stride, {}, {}};
   for (int i = 0; i < 3; ++i) {
     a.gn.w[i] = gn_w[i];
     a.gn.b[i] = gn_b[i];

@@ -87,6 +87,12 @@ class LaggedFlags:
         return i, float(self.buf[i])
 
 
+def _f_hist_dtype(dt: torch.dtype, like: torch.Tensor) -> torch.dtype:
+    """dtype of the Anderson F history: bf16 for a bf16 model on the GPU (f's outputs are bf16
+    values, so the narrower history is exact), fp32 otherwise."""
+    return torch.bfloat16 if (dt == torch.bfloat16 and like.is_cuda) else torch.float32
+
+
 def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0, check_lag: int | None = None,
              graphs: "SolverGraphs | None" = None):
     """Anderson acceleration for ``x = f(x)`` over batch-flattened tensors. Returns (x, iters, rel_residual).
@@ -110,13 +116,15 @@ def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0, check_lag: i
     bsz = x0.shape[0]
     shape, dt = x0.shape, x0.dtype
     d = x0[0].numel()
-    # the solver history and the small (m+1)^2 systems are kept in fp32 whatever the model
-    # dtype (bf16 has no batched LU, and 8-bit mantissas would stall the extrapolation)
+    # the iterates X, the differences G = F - X and the small (m+1)^2 systems are fp32 whatever
+    # the model dtype (bf16 has no batched LU, and 8-bit mantissas in X or G would stall the
+    # extrapolation); the images F are f's outputs, so in a bf16 model they are bf16 values and
+    # their history is kept in bf16 on the GPU (exact; the mix reads n rows of it per iteration)
     if graphs is not None:
         X, Fv, Gs = graphs.history(m)
     else:
         X = torch.zeros(bsz, m, d, dtype=torch.float32, device=x0.device)
-        Fv = torch.zeros_like(X)
+        Fv = torch.zeros_like(X, dtype=_f_hist_dtype(dt, x0))
         Gs = torch.zeros_like(X)
 
     # flatten in MEMORY order: a channels_last iterate stays channels_last through f (views,
@@ -194,7 +202,7 @@ def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0, check_lag: i
     if not converged:
         k = max(k - 1, 1)  # the last completed iteration
         s = k % m
-        res_t = (Fv[:, s] - X[:, s]).norm() / (1e-5 + Fv[:, s].norm())
+        res_t = (Fv[:, s].float() - X[:, s]).norm() / (1e-5 + Fv[:, s].float().norm())
         res = res_t if flags is not None else float(res_t)
     return unflat(X[:, k % m].contiguous()).to(dt), k, res
 
@@ -216,7 +224,10 @@ class _CellEval:
         from ..ops import deq_cell
         if not (hasattr(self.cell, "conv1") and deq_cell.supported(self.cell, z)):
             return False
-        deq_cell.cell_forward(self.cell, z, self.x, out32=dst, want_out=False)
+        if dst.dtype == torch.bfloat16:
+            deq_cell.cell_forward(self.cell, z, self.x, out_slot=dst)
+        else:
+            deq_cell.cell_forward(self.cell, z, self.x, out32=dst, want_out=False)
         return True
 
 
@@ -263,7 +274,7 @@ class SolverGraphs:
         bsz, d = self.x.shape[0], self.x[0].numel()
         if self._hist is None or self._hist[0].shape[1] != m:
             X = torch.zeros(bsz, m, d, dtype=torch.float32, device=self.x.device)
-            self._hist = (X, torch.zeros_like(X), torch.zeros_like(X))
+            self._hist = (X, torch.zeros_like(X, dtype=_f_hist_dtype(self.x.dtype, self.x)), torch.zeros_like(X))
             self.g_fwd = None
         return self._hist
 

@@ -37,12 +37,14 @@ def _stream(t):
 def _native(X: torch.Tensor, F: torch.Tensor, n: int) -> bool:
     if not (X.is_cuda and F.is_cuda):
         return False
-    ok = (X.dtype == F.dtype == torch.float32 and X.dim() == F.dim() == 3 and X.shape == F.shape
+    ok = (X.dtype == torch.float32 and F.dtype in (torch.float32, torch.bfloat16) and X.dim() == F.dim() == 3
+          and X.shape == F.shape
           and X.stride() == F.stride() and X.stride(2) == 1 and X.shape[2] % 4 == 0 and X.stride(1) % 4 == 0
           and X.stride(0) % 4 == 0 and 1 <= n <= min(_MAX_ROWS, X.shape[1]) and X.shape[0] <= 65535
           and X.data_ptr() % 16 == 0 and F.data_ptr() % 16 == 0)
     if not ok:
-        raise ValueError("anderson ops: need fp32 [bsz<=65535, m, d%4==0] histories with matching strides, n<=8")
+        raise ValueError("anderson ops: need an fp32 X and an fp32 / bf16 F history [bsz<=65535, m, d%4==0] with "
+                         "matching strides, n<=8")
     return True
 
 
@@ -59,7 +61,7 @@ def gram(X: torch.Tensor, F: torch.Tensor, n: int, last: int, G: torch.Tensor | 
             Gn = G[:, :n]
         else:
             Gn = F[:, :n] - X[:, :n]
-        return torch.bmm(Gn, Gn.transpose(1, 2)), F[:, last].pow(2).sum(1)
+        return torch.bmm(Gn, Gn.transpose(1, 2)), F[:, last].float().pow(2).sum(1)
     C = _ext.get(required=True)
     bsz, _, d = X.shape
     chunks = C.anderson_gram_chunks(bsz, d)
@@ -70,8 +72,8 @@ def gram(X: torch.Tensor, F: torch.Tensor, n: int, last: int, G: torch.Tensor | 
             raise ValueError("anderson gram: G must match X's shape, strides and dtype")
         for i in fresh:
             mask |= 1 << int(i)
-    C.anderson_gram(X.data_ptr(), F.data_ptr(), G.data_ptr() if G is not None else 0, mask, part.data_ptr(), bsz, d,
-                    X.stride(1), X.stride(0), n, last, chunks, _stream(X))
+    C.anderson_gram(X.data_ptr(), F.data_ptr(), DTYPE_CODE[F.dtype], G.data_ptr() if G is not None else 0, mask,
+                    part.data_ptr(), bsz, d, X.stride(1), X.stride(0), n, last, chunks, _stream(X))
     tot = part.sum(1)
     # one gather (cached symmetric index) instead of building the index and two scatters
     H = tot.index_select(1, _sym_index(n, X.device)).view(bsz, n, n)
@@ -105,8 +107,8 @@ def gram_solve(X: torch.Tensor, F: torch.Tensor, n: int, last: int, G: torch.Ten
     for i in fresh:
         mask |= 1 << int(i)
     stream = _stream(X)
-    C.anderson_gram(X.data_ptr(), F.data_ptr(), G.data_ptr(), mask, part.data_ptr(), bsz, d, X.stride(1),
-                    X.stride(0), n, last, chunks, stream)
+    C.anderson_gram(X.data_ptr(), F.data_ptr(), DTYPE_CODE[F.dtype], G.data_ptr(), mask, part.data_ptr(), bsz, d,
+                    X.stride(1), X.stride(0), n, last, chunks, stream)
     alpha = torch.empty(bsz, n, device=X.device, dtype=torch.float32)
     res = torch.empty((), device=X.device, dtype=torch.float32) if want_res else None
     C.anderson_solve(part.data_ptr(), chunks, bsz, n, last, float(lam), alpha.data_ptr(),
@@ -122,7 +124,7 @@ def mix(X: torch.Tensor, F: torch.Tensor, alpha: torch.Tensor, slot: int, beta: 
     the ``X[:, slot]`` view otherwise)."""
     n = alpha.shape[1]
     if not _native(X, F, n):
-        new = beta * torch.bmm(alpha[:, None], F[:, :n])[:, 0]
+        new = beta * torch.bmm(alpha[:, None], F[:, :n].float())[:, 0]
         if beta != 1.0:
             new = new + (1 - beta) * torch.bmm(alpha[:, None], X[:, :n])[:, 0]
         X[:, slot] = new
@@ -133,7 +135,7 @@ def mix(X: torch.Tensor, F: torch.Tensor, alpha: torch.Tensor, slot: int, beta: 
     z = None
     if z_dtype not in (None, torch.float32):
         z = torch.empty(bsz, d, device=X.device, dtype=z_dtype)
-    C.anderson_mix(X.data_ptr(), F.data_ptr(), a.data_ptr(), z.data_ptr() if z is not None else 0,
+    C.anderson_mix(X.data_ptr(), F.data_ptr(), DTYPE_CODE[F.dtype], a.data_ptr(), z.data_ptr() if z is not None else 0,
                    DTYPE_CODE[z_dtype] if z is not None else 7, bsz, d, X.stride(1), X.stride(0), n, slot, float(beta),
                    _stream(X))
     return z if z is not None else X[:, slot]

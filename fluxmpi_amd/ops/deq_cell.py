@@ -59,10 +59,12 @@ def _filter_k(w: torch.Tensor) -> torch.Tensor:
 
 
 def cell_forward(cell, z: torch.Tensor, x: torch.Tensor, keep: bool = False, out32: torch.Tensor | None = None,
-                 want_out: bool = True):
+                 want_out: bool = True, out_slot: torch.Tensor | None = None):
     """``f(z, x)`` in one launch. ``keep``: also return the VJP state of ``ResidualCell.forward_state``
     (``(shape, (h1, mean1, rstd1, w1), (h2, ...), (h3, ...))``). ``out32`` ([N, H*W*C] fp32 rows,
-    any row stride): the output is also written there in fp32 (an Anderson history slot)."""
+    any row stride): the output is also written there in fp32 (an Anderson history slot).
+    ``out_slot`` ([N, H*W*C] bf16 rows, any row stride): the bf16 output goes there instead of a
+    fresh tensor (an Anderson bf16 history slot; returned)."""
     from .gemm import note_filter
     from .groupnorm import _f32
     C = _ext.get(required=True)
@@ -77,7 +79,12 @@ def cell_forward(cell, z: torch.Tensor, x: torch.Tensor, keep: bool = False, out
     norms = (cell.n1, cell.n2, cell.n3)
     gw = [_f32(m.weight) for m in norms]
     gb = [_f32(m.bias) for m in norms]
-    out = torch.empty_like(z, memory_format=torch.channels_last) if want_out or out32 is None else None
+    out_stride = 0
+    if out_slot is not None:
+        assert out_slot.dtype == torch.bfloat16 and out_slot.shape == (n, ch * h * wd) and out_slot.stride(1) == 1
+        out, out_stride = out_slot, out_slot.stride(0)
+    else:
+        out = torch.empty_like(z, memory_format=torch.channels_last) if want_out or out32 is None else None
     hs = [torch.empty_like(z, memory_format=torch.channels_last) for _ in range(3)] if keep else [None] * 3
     st = [torch.empty(n, G, device=z.device, dtype=torch.float32) for _ in range(6)] if keep else [None] * 6
     if out32 is not None:
@@ -85,7 +92,7 @@ def cell_forward(cell, z: torch.Tensor, x: torch.Tensor, keep: bool = False, out
     C.deq_cell_fwd(z.data_ptr(), x.data_ptr(), w1.data_ptr(), w2.data_ptr(), [_ptr(t) for t in gw],
                    [_ptr(t) for t in gb], _ptr(out), _ptr(out32), out32.stride(0) if out32 is not None else 0,
                    [_ptr(t) for t in hs], [_ptr(t) for t in st[0::2]], [_ptr(t) for t in st[1::2]],
-                   n, h, wd, ch, G, float(cell.n1.eps), _stream(z))
+                   n, h, wd, ch, G, float(cell.n1.eps), _stream(z), out_stride)
     if not keep:
         return out
     state = (tuple(z.shape), (hs[0], st[0], st[1], gw[0]), (hs[1], st[2], st[3], gw[1]), (hs[2], st[4], st[5], gw[2]))

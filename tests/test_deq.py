@@ -86,32 +86,35 @@ def test_deq_train_step_cpu():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fdt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("n", [1, 2, 3, 5, 8])
 @pytest.mark.parametrize("bsz,d", [(3, 36), (64, 4100), (256, 37632)])
-def test_anderson_gram_gpu(n, bsz, d):
+def test_anderson_gram_gpu(n, bsz, d, fdt):
+    """fdt bf16: the F history of a bf16 model (the reference reads the same bf16 values)."""
     torch.manual_seed(n)
     m = max(n, 5)
     X = torch.randn(bsz, m, d, device="cuda")
-    Fv = torch.randn(bsz, m, d, device="cuda")
+    Fv = torch.randn(bsz, m, d, device="cuda").to(fdt)
     last = n - 1
     H, fn = AO.gram(X, Fv, n, last)
-    Hr, fr = _ref_gram(X, Fv, n, last)
+    Hr, fr = _ref_gram(X, Fv.float(), n, last)
     torch.testing.assert_close(H.double(), Hr, rtol=1e-4, atol=1e-3 * d ** 0.5)
     torch.testing.assert_close(fn.double(), fr, rtol=1e-4, atol=1e-3)
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fdt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("n,beta", [(1, 1.0), (3, 1.0), (5, 1.0), (5, 0.8), (8, 0.5)])
 @pytest.mark.parametrize("zdt", [None, torch.bfloat16, torch.float16])
-def test_anderson_mix_gpu(n, beta, zdt):
+def test_anderson_mix_gpu(n, beta, zdt, fdt):
     torch.manual_seed(10 + n)
     bsz, m, d = 37, 8, 4100
     X = torch.randn(bsz, m, d, device="cuda")
-    Fv = torch.randn(bsz, m, d, device="cuda")
+    Fv = torch.randn(bsz, m, d, device="cuda").to(fdt)
     alpha = torch.randn(bsz, n, device="cuda")
     slot = (n + 2) % m
     keep = X.clone()
-    want = _ref_mix(X, Fv, alpha, beta)
+    want = _ref_mix(X, Fv.float(), alpha, beta)
     z = AO.mix(X, Fv, alpha, slot, beta, zdt)
     torch.testing.assert_close(X[:, slot].double(), want, rtol=1e-5, atol=1e-4)
     others = [i for i in range(m) if i != slot]
@@ -260,23 +263,31 @@ def test_deq_train_step_gpu_param_grads():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("fdt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("n", [2, 5, 8])
-def test_anderson_gram_stored_g_gpu(n):
+def test_anderson_gram_stored_g_gpu(n, fdt):
     torch.manual_seed(20 + n)
     bsz, m, d = 64, 8, 4100
     X = torch.randn(bsz, m, d, device="cuda")
-    Fv = torch.randn(bsz, m, d, device="cuda")
+    Fv = torch.randn(bsz, m, d, device="cuda").to(fdt)
     G = torch.zeros_like(X)
     H0, _ = AO.gram(X, Fv, n, n - 1, G, tuple(range(n)))  # all rows fresh: fills G
-    torch.testing.assert_close(G[:, :n], Fv[:, :n] - X[:, :n])
-    s = n // 2  # one row changes: only it is recomputed, the others come from G
+    torch.testing.assert_close(G[:, :n], Fv[:, :n].float() - X[:, :n])
+    s = n // 2  # one row changes (the newest, `last`): only it is recomputed, the others come from G
     X[:, s].normal_()
     Fv[:, s].normal_()
     H, fn = AO.gram(X, Fv, n, s, G, (s,))
-    Hr, fr = _ref_gram(X, Fv, n, s)
+    Hr, fr = _ref_gram(X, Fv.float(), n, s)
     torch.testing.assert_close(H.double(), Hr, rtol=1e-4, atol=1e-3 * d ** 0.5)
     torch.testing.assert_close(fn.double(), fr, rtol=1e-4, atol=1e-3)
-    torch.testing.assert_close(G[:, s], Fv[:, s] - X[:, s])
+    torch.testing.assert_close(G[:, s], Fv[:, s].float() - X[:, s])
+    # a fresh row that is not `last`: every row is recomputed from F - X (same result)
+    t = (s + 1) % n
+    X[:, t].normal_()
+    H2, fn2 = AO.gram(X, Fv, n, s, G, (t,))
+    Hr2, fr2 = _ref_gram(X, Fv.float(), n, s)
+    torch.testing.assert_close(H2.double(), Hr2, rtol=1e-4, atol=1e-3 * d ** 0.5)
+    torch.testing.assert_close(fn2.double(), fr2, rtol=1e-4, atol=1e-3)
 
 
 @pytest.mark.gpu
@@ -528,6 +539,12 @@ def test_deq_fused_cell_forward(gpu_ext, monkeypatch):
     deq_cell.cell_forward(cell, z, x, out32=hist[:, 1], want_out=False)
     torch.testing.assert_close(hist[:, 1], out_f.permute(0, 2, 3, 1).reshape(n, -1).float(), rtol=0, atol=0)
     assert torch.isnan(hist[:, 0]).all() and torch.isnan(hist[:, 2]).all()
+    # bf16 output straight into a strided bf16 history slot (the bf16 F history)
+    histb = torch.full((n, 3, z[0].numel()), float("nan"), device="cuda", dtype=torch.bfloat16)
+    ob = deq_cell.cell_forward(cell, z, x, out_slot=histb[:, 1])
+    assert ob.data_ptr() == histb[:, 1].data_ptr()
+    torch.testing.assert_close(histb[:, 1], out_f.permute(0, 2, 3, 1).reshape(n, -1), rtol=0, atol=0)
+    assert torch.isnan(histb[:, 0].float()).all() and torch.isnan(histb[:, 2].float()).all()
 
 
 @pytest.mark.gpu
