@@ -242,9 +242,10 @@ void gemm_nt(const void* a, const void* b, void* c, void* c2, const void* bias, 
              float* colpart, float* stats, int64_t lda, int64_t ldb, int64_t ldc, int64_t M, int64_t N, int64_t K,
              int epi, hipStream_t stream);
 // 3x3 / stride 1 / pad 1 convolution on the same kernel: A = the implicit im2col of the NHWC image
-// x [nimg][H][W][C] (C % 64 == 0), B = w [Cout][3][3][C]; y [nimg*H*W][Cout]; epi 0 or 3 (statistics)
+// x [nimg][H][W][C] (C % 64 == 0), B = w [Cout][3][3][C]; y [nimg*H*W][Cout]; epi 0, 3 (statistics)
+// or 4 (y = bf16(bf16(conv) + residual), residual laid out as y)
 void gemm_nt_conv(const void* x, const void* w, void* y, float* stats, int64_t nimg, int H, int W, int C,
-                  int64_t Cout, int epi, hipStream_t stream);
+                  int64_t Cout, int epi, hipStream_t stream, const void* residual = nullptr);
 // Narrow-channel 3x3 / stride 1 / pad 1 convolution (conv3x3n.hip): C = Cout in {64, 128}, the
 // input halo staged once per 256-pixel workgroup; x [pixels][C] NHWC, w [Cout][9][C], y [pixels][Cout];
 // epi 0 or 3 (BatchNorm statistics into stats[64][2][Cout])

@@ -319,9 +319,10 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("gemm_nt_conv_supported", &gemm_nt_conv_supported);
   m.def("gemm_nt_conv", [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, int64_t nimg, int H, int W, int C,
-                           int64_t Cout, int epi, uintptr_t stream) {
+                           int64_t Cout, int epi, uintptr_t stream, uintptr_t residual) {
     gemm_nt_conv(reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(w), reinterpret_cast<void*>(y),
-                 reinterpret_cast<float*>(stats), nimg, H, W, C, Cout, epi, S(stream));
+                 reinterpret_cast<float*>(stats), nimg, H, W, C, Cout, epi, S(stream),
+                 reinterpret_cast<const void*>(residual));
   });
   m.def("transpose_bf16", [](uintptr_t src, uintptr_t dst, int64_t rows, int64_t cols, int64_t lds, int64_t ldd,
                              uintptr_t stream) {

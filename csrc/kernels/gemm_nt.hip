@@ -233,7 +233,7 @@ template <int EPI, int BIAS, bool CONV, int GF = 1>  // GF (EPI 1 / 2): 1 tanh G
 __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
   __shared__ __attribute__((aligned(1024))) char smem[kSmem];
   // vector-memory instructions per wave in an epilogue (lower bound: unconditional ones)
-  constexpr int kEpiVm = EPI == 1 || EPI == 2 ? 32 : 16;
+  constexpr int kEpiVm = EPI == 1 || EPI == 2 || EPI == 4 ? 32 : 16;
   const int G = gridDim.x;
   const int nk = p.nk;  // >= 2
   const int tiles = p.tiles_m * p.tiles_n;
@@ -590,7 +590,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
     const __amdgpu_buffer_rsrc_t crs = tile_rsrc(p.c);
     i32x4 hv[4][2][2];  // EPI 2: every GELU derivative of the tile's lane issued before the first use (one round trip)
 #ifndef GNT_DBG_HVLATE
-    if (EPI == 2) {
+    if (EPI == 2 || EPI == 4) {
       const __amdgpu_buffer_rsrc_t hrs = tile_rsrc(p.h);
 #pragma unroll
       for (int ph = 0; ph < 4; ++ph)
@@ -603,7 +603,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
 #pragma unroll
     for (int ph = 0; ph < 4; ++ph) {
 #ifdef GNT_DBG_HVLATE
-      if (EPI == 2) {
+      if (EPI == 2 || EPI == 4) {
         const __amdgpu_buffer_rsrc_t hrs = tile_rsrc(p.h);
 #pragma unroll
         for (int ii = 0; ii < 2; ++ii)
@@ -672,6 +672,14 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt_kernel(NTArgs p) {
               oo[e] = static_cast<bf16>(static_cast<float>(v8[e]) * static_cast<float>(dd[e]));
               cs[q][e] += static_cast<float>(oo[e]);  // the bias gradient of the rounded dh
             }
+            __builtin_memcpy(&out, oo, 16);
+          } else if (EPI == 4) {
+            // y = bf16(bf16(acc) + r): the residual summand of the input's gradient (a second
+            // consumer's share), added to the rounded product in the exchanged 8-column layout
+            bf16 rr[8], oo[8];
+            __builtin_memcpy(rr, &hv[ph][ii][q], 16);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) oo[e] = static_cast<bf16>(static_cast<float>(v8[e]) + static_cast<float>(rr[e]));
             __builtin_memcpy(&out, oo, 16);
           }
           __builtin_amdgcn_raw_buffer_store_b128(out, crs, vo + 64 * q, rowblk(ph, ii), 0);
@@ -915,24 +923,29 @@ void gemm_nt(const void* a, const void* b, void* c, void* c2, const void* bias, 
 }
 
 void gemm_nt_conv(const void* x, const void* w, void* y, float* stats, int64_t nimg, int H, int W, int C,
-                  int64_t Cout, int epi, hipStream_t stream) {
+                  int64_t Cout, int epi, hipStream_t stream, const void* residual) {
   const int64_t pixels = nimg * H * W;
   if (!gemm_nt_conv_supported(pixels, C, Cout))
     throw std::runtime_error("gemm_nt_conv: unsupported shape (pixels, Cout multiples of 256, C of 64; pixels=" +
                              std::to_string(pixels) + " C=" + std::to_string(C) + " Cout=" + std::to_string(Cout) + ")");
   if (((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(y)) & 15u) != 0)
     throw std::runtime_error("gemm_nt_conv: operands must be 16-byte aligned");
-  if (epi != 0 && epi != 3) throw std::runtime_error("gemm_nt_conv: epilogue 0 (plain) or 3 (statistics)");
+  if (epi != 0 && epi != 3 && epi != 4)
+    throw std::runtime_error("gemm_nt_conv: epilogue 0 (plain), 3 (statistics) or 4 (+ residual)");
   if (epi == 3 && stats == nullptr) throw std::runtime_error("gemm_nt_conv: the statistics epilogue needs the shards");
+  if (epi == 4 && (residual == nullptr || (reinterpret_cast<uintptr_t>(residual) & 15u) != 0))
+    throw std::runtime_error("gemm_nt_conv: the residual epilogue needs a 16-byte aligned residual");
   NTArgs p{};
   p.a = static_cast<const bf16*>(x), p.b = static_cast<const bf16*>(w), p.c = static_cast<bf16*>(y);
   p.stats = stats, p.lda = 9 * C, p.ldb = 9 * C, p.ldc = Cout, p.N = Cout;
+  p.h = static_cast<const bf16*>(residual);  // EPI 4: the residual, laid out as y
   p.nk = 9 * C / kBK, p.tiles_m = static_cast<int>(pixels / kT), p.tiles_n = static_cast<int>(Cout / kT);
   p.gelu_tanh = 0;
   p.conv_h = H, p.conv_w = W, p.conv_c = C, p.conv_cpt = C / kBK;
   p.conv_inv_cpt = 1.f / static_cast<float>(C / kBK);
   p.a_bytes = static_cast<uint32_t>(pixels * C * 2);
   if (epi == 3) launch<3, 0, true>(p, stream);
+  else if (epi == 4) launch<4, 0, true>(p, stream);
   else launch<0, 0, true>(p, stream);
 }
 

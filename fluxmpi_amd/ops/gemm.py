@@ -246,13 +246,14 @@ def conv3x3_dgrad(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = 
     if (bn_bwd is None and residual is None and ENGINE != 1 and dx.is_contiguous(memory_format=torch.channels_last)
             and conv_n_ok(n * h * wd, co, ci, h, wd, dys, wt, dx)):
         return conv3x3n(dys, wt, dx, n * h * wd, h, wd)  # the flipped transpose [ci][3][3][co] as the filter
-    if (bn_bwd is None and residual is None and ENGINE != 1 and dx.is_contiguous(memory_format=torch.channels_last)
-            and _NT.conv_ok(n * h * wd, co, ci, dys, wt)):
-        return _NT.conv3x3(dys, wt, dx)  # the flipped transpose [ci][3][3][co] as B
     r2 = None
     if residual is not None:
         assert residual.shape == dx.shape and residual.dtype == dy.dtype and bn_bwd is None
         r2 = residual.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(-1, ci)
+    if (bn_bwd is None and ENGINE != 1 and dx.is_contiguous(memory_format=torch.channels_last)
+            and _NT.conv_ok(n * h * wd, co, ci, dys, wt, *(() if r2 is None else (r2,)))):
+        # the flipped transpose [ci][3][3][co] as B; the residual (if any) added in the epilogue
+        return _NT.conv3x3(dys, wt, dx, residual=r2)
     gemm(dys, wt, dx, M=n * h * wd, N=ci, K=9 * co, lda=co, ldb=9 * co, ldc=ci, conv=(h, wd, co),
          mode=1 if bn_bwd is not None else 0, stats=stats, bn_bwd=bn_bwd, residual=r2)
     return dx

@@ -173,17 +173,21 @@ def gemm_ok(rows: int, n_out: int, k: int, *tensors: torch.Tensor) -> bool:
     return C is not None and hasattr(C, "gemm_nt_stats") and bool(C.gemm_nt_supported(rows, n_out, k, k, k, n_out))
 
 
-def conv3x3(x: torch.Tensor, w_taps: torch.Tensor, y: torch.Tensor, stats: torch.Tensor | None = None) -> torch.Tensor:
+def conv3x3(x: torch.Tensor, w_taps: torch.Tensor, y: torch.Tensor, stats: torch.Tensor | None = None,
+            residual: torch.Tensor | None = None) -> torch.Tensor:
     """``y [N*H*W, Cout] = conv3x3(x)``: ``x`` NHWC [N, H, W, C] memory (a channels_last tensor),
     ``w_taps`` [Cout, 9*C] (tap-major, channel-fastest: a channels_last filter, or the flipped
     transpose of the input-gradient), ``stats``: the BatchNorm shards [64, 2, Cout] receive the
-    output's per-channel sum / sum of squares (EPI 3)."""
+    output's per-channel sum / sum of squares (EPI 3); ``residual`` (laid out as ``y``, 16-B
+    aligned): ``y = bf16(bf16(conv) + residual)`` (EPI 4; not with ``stats``)."""
     C = _ext.get(required=True)
     n, c, h, wd = x.shape
     cout = w_taps.shape[0]
     s = _stream(x)
+    assert stats is None or residual is None
+    epi = 3 if stats is not None else (4 if residual is not None else 0)
     C.gemm_nt_conv(x.data_ptr(), w_taps.data_ptr(), y.data_ptr(), stats.data_ptr() if stats is not None else 0,
-                   n, h, wd, c, cout, 3 if stats is not None else 0, s)
+                   n, h, wd, c, cout, epi, s, residual.data_ptr() if residual is not None else 0)
     return y
 
 

@@ -161,6 +161,11 @@ def test_conv3x3_fwd_stats_and_dgrad(gpu_ext, any_shape, nimg, h, w, c, co):
         dx = GM.conv3x3_dgrad(dy, wt)
         dref = torch.nn.grad.conv2d_input(x.shape, wt.float(), dy.float(), padding=1)
         assert _rel(dx, dref) < 5e-3
+        # + a residual summand in the epilogue (EPI 4): exactly bf16(bf16(conv) + r)
+        res = _uni(nimg, c, h, w).contiguous(memory_format=torch.channels_last)
+        dxr = GM.conv3x3_dgrad(dy, wt, residual=res)
+        torch.testing.assert_close(dxr, (dx.float() + res.float()).bfloat16(), rtol=0, atol=0)
+        assert _rel(dxr, dref + res.float()) < 5e-3
 
 
 @pytest.mark.parametrize("m,n,k", [(50176, 1024, 256), (12544, 512, 2048), (802816 // 4, 256, 64 * 2)])
