@@ -286,9 +286,10 @@ void adjoint_step(const void* vjp, const void* grad, const void* u, void* u_new,
 // forward: h = [relu](x [+ add]) (stored when h != nullptr); y = GN(h) * w + b (w/b fp32, nullable);
 // mean / rstd [N][G] fp32 saved. backward: dh = d(GN)/dh [* (h > 0) when relu], the gradient of
 // both x and add; partials[N][2][C] = per-sample (dw, db).
+// y_stride: y's sample stride in elements (0: HW * C, dense) — y can be an Anderson history slot.
 void groupnorm_nhwc_fwd(const void* x, const void* add, void* h, void* y, const float* w, const float* b, float* mean,
                         float* rstd, int64_t N, int64_t HW, int64_t C, int64_t G, bool relu, float eps, int dtype,
-                        hipStream_t stream);
+                        hipStream_t stream, int64_t y_stride = 0);
 void groupnorm_nhwc_bwd(const void* dy, const void* h, const float* mean, const float* rstd, const float* w, void* dh,
                         float* partials, int64_t N, int64_t HW, int64_t C, int64_t G, bool relu, int dtype,
                         hipStream_t stream);

@@ -220,11 +220,11 @@ PYBIND11_MODULE(_C, m) {
   // ---- fused NHWC GroupNorm ------------------------------------------------------
   m.def("groupnorm_nhwc_fwd", [](uintptr_t x, uintptr_t a, uintptr_t h, uintptr_t y, uintptr_t w, uintptr_t b,
                                  uintptr_t mean, uintptr_t rstd, int64_t N, int64_t HW, int64_t C, int64_t G, bool relu,
-                                 float eps, int dtype, uintptr_t stream) {
+                                 float eps, int dtype, uintptr_t stream, int64_t y_stride) {
     groupnorm_nhwc_fwd(reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(a), reinterpret_cast<void*>(h),
                        reinterpret_cast<void*>(y), reinterpret_cast<const float*>(w), reinterpret_cast<const float*>(b),
                        reinterpret_cast<float*>(mean), reinterpret_cast<float*>(rstd), N, HW, C, G, relu, eps, dtype,
-                       S(stream));
+                       S(stream), y_stride);
   });
   m.def("groupnorm_nhwc_bwd", [](uintptr_t dy, uintptr_t h, uintptr_t mean, uintptr_t rstd, uintptr_t w, uintptr_t dh,
                                  uintptr_t part, int64_t N, int64_t HW, int64_t C, int64_t G, bool relu, int dtype,

@@ -70,7 +70,7 @@ __global__ __launch_bounds__(kMaxThreads) void gn_fwd_kernel(const T* __restrict
                                                              T* __restrict__ h, T* __restrict__ y,
                                                              const float* __restrict__ w, const float* __restrict__ b,
                                                              float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                             GnShape s, float eps) {
+                                                             GnShape s, float eps, int64_t y_stride) {
   extern __shared__ float lds[];
   float* red = lds;
   float* chan = red + 2 * s.PL * s.C;
@@ -78,6 +78,7 @@ __global__ __launch_bounds__(kMaxThreads) void gn_fwd_kernel(const T* __restrict
   const int n = blockIdx.x;
   const int cv = threadIdx.x % s.CV, pl = threadIdx.x / s.CV;
   const int64_t base = static_cast<int64_t>(n) * s.HW * s.C + cv * 8;
+  y += static_cast<int64_t>(n) * (y_stride - static_cast<int64_t>(s.HW) * s.C);  // y's sample n at n * y_stride
   const bool active = threadIdx.x < s.T;
   float sum[8], sq[8];
 #pragma unroll
@@ -289,7 +290,7 @@ size_t gn_lds(const GnShape& s) { return sizeof(float) * (2 * s.PL * s.C + 2 * s
 
 template <typename T>
 void fwd_dispatch(const void* x, const void* a, void* h, void* y, const float* w, const float* b, float* mean,
-                  float* rstd, int64_t N, const GnShape& s, bool relu, float eps, hipStream_t st) {
+                  float* rstd, int64_t N, const GnShape& s, bool relu, float eps, hipStream_t st, int64_t ys) {
   const T* xp = static_cast<const T*>(x);
   const T* ap = static_cast<const T*>(a);
   T* hp = static_cast<T*>(h);
@@ -297,7 +298,8 @@ void fwd_dispatch(const void* x, const void* a, void* h, void* y, const float* w
   const size_t lds = gn_lds(s);
   const dim3 grid(static_cast<unsigned>(N));
   const bool add = a != nullptr, saveh = h != nullptr;
-#define GN_FWD(A, R, H) gn_fwd_kernel<T, A, R, H><<<grid, kMaxThreads, lds, st>>>(xp, ap, hp, yp, w, b, mean, rstd, s, eps)
+#define GN_FWD(A, R, H) \
+  gn_fwd_kernel<T, A, R, H><<<grid, kMaxThreads, lds, st>>>(xp, ap, hp, yp, w, b, mean, rstd, s, eps, ys)
   if (add && relu) { if (saveh) GN_FWD(true, true, true); else GN_FWD(true, true, false); }
   else if (add) { if (saveh) GN_FWD(true, false, true); else GN_FWD(true, false, false); }
   else if (relu) { if (saveh) GN_FWD(false, true, true); else GN_FWD(false, true, false); }
@@ -328,14 +330,16 @@ void check_ptrs(std::initializer_list<const void*> ps) {
 
 void groupnorm_nhwc_fwd(const void* x, const void* add, void* h, void* y, const float* w, const float* b, float* mean,
                         float* rstd, int64_t N, int64_t HW, int64_t C, int64_t G, bool relu, float eps, int dtype,
-                        hipStream_t stream) {
+                        hipStream_t stream, int64_t y_stride) {
   const GnShape s = gn_shape(HW, C, G);
   check_ptrs({x, add, h, y});
   if (N < 1 || N > 2147483647LL) throw std::runtime_error("fused groupnorm: bad N");
+  if (y_stride == 0) y_stride = HW * C;
+  if (y_stride < HW * C || y_stride % 8 != 0) throw std::runtime_error("fused groupnorm: bad output sample stride");
   switch (dtype) {
-    case kBF16: fwd_dispatch<bf16>(x, add, h, y, w, b, mean, rstd, N, s, relu, eps, stream); break;
-    case kF16: fwd_dispatch<f16>(x, add, h, y, w, b, mean, rstd, N, s, relu, eps, stream); break;
-    case kF32: fwd_dispatch<float>(x, add, h, y, w, b, mean, rstd, N, s, relu, eps, stream); break;
+    case kBF16: fwd_dispatch<bf16>(x, add, h, y, w, b, mean, rstd, N, s, relu, eps, stream, y_stride); break;
+    case kF16: fwd_dispatch<f16>(x, add, h, y, w, b, mean, rstd, N, s, relu, eps, stream, y_stride); break;
+    case kF32: fwd_dispatch<float>(x, add, h, y, w, b, mean, rstd, N, s, relu, eps, stream, y_stride); break;
     default: throw std::runtime_error("fused groupnorm: unsupported dtype");
   }
   FLUXMPI_HIP_CHECK(hipGetLastError());

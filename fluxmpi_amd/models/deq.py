@@ -219,11 +219,15 @@ class _CellEval:
         return self.cell.forward_raw(z, self.x) if self.raw else self.cell(z, self.x)
 
     def write_into(self, z, dst) -> bool:
-        if not self.raw or dst.stride(-1) != 1:
+        if not self.raw or dst.stride(-1) != 1 or not hasattr(self.cell, "conv1"):
             return False
         from ..ops import deq_cell
-        if not (hasattr(self.cell, "conv1") and deq_cell.supported(self.cell, z)):
-            return False
+        if not deq_cell.supported(self.cell, z):
+            if dst.dtype != z.dtype or not hasattr(self.cell, "forward_state"):
+                return False
+            # the last GroupNorm writes the model-dtype history slot itself (no copy pass)
+            self.cell.forward_state(z, self.x, keep=False, out_slot=dst)
+            return True
         if dst.dtype == torch.bfloat16:
             deq_cell.cell_forward(self.cell, z, self.x, out_slot=dst)
         else:
@@ -522,19 +526,22 @@ class ResidualCell(nn.Module):
         return self.forward_state(z, x, keep=False)
 
     @torch.no_grad()
-    def forward_state(self, z, x, keep: bool = True):
+    def forward_state(self, z, x, keep: bool = True, out_slot=None):
         """``f(z, x)`` without autograd, keeping what :meth:`vjp` needs (GPU fused path): one
-        LDS-resident kernel per evaluation where it applies (ops/deq_cell.py), else 5 launches."""
+        LDS-resident kernel per evaluation where it applies (ops/deq_cell.py), else 5 launches.
+        ``out_slot`` ([N, C*H*W] model-dtype rows, e.g. an Anderson history slot): the output is
+        written there (returned as that tensor)."""
         from ..ops import deq_cell
         from ..ops.fused_block import conv3x3_fwd_raw
         from ..ops.groupnorm import gn_fwd_raw
         if deq_cell.supported(self, z):
-            return deq_cell.cell_forward(self, z, x, keep=keep)
+            return deq_cell.cell_forward(self, z, x, keep=keep, out_slot=out_slot)
         c1 = conv3x3_fwd_raw(z, self.conv1.weight)
         a1, h1, m1, r1, w1 = gn_fwd_raw(c1, None, self.n1.weight, self.n1.bias, self.n1.num_groups, self.n1.eps, True)
         c2 = conv3x3_fwd_raw(a1, self.conv2.weight)
         a2, h2, m2, r2, w2 = gn_fwd_raw(c2, x, self.n2.weight, self.n2.bias, self.n2.num_groups, self.n2.eps, False)
-        out, h3, m3, r3, w3 = gn_fwd_raw(z, a2, self.n3.weight, self.n3.bias, self.n3.num_groups, self.n3.eps, True)
+        out, h3, m3, r3, w3 = gn_fwd_raw(z, a2, self.n3.weight, self.n3.bias, self.n3.num_groups, self.n3.eps, True,
+                                         out=out_slot)
         if not keep:
             return out
         return out, (tuple(z.shape), (h1, m1, r1, w1), (h2, m2, r2, w2), (h3, m3, r3, w3))

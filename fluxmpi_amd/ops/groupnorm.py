@@ -101,22 +101,28 @@ def supported(x: torch.Tensor, groups: int) -> bool:
             and x.is_contiguous(memory_format=torch.channels_last))
 
 
-def gn_fwd_raw(x, add, weight, bias, groups, eps, relu):
+def gn_fwd_raw(x, add, weight, bias, groups, eps, relu, out=None):
     """``GN(relu(x + add))`` on the fused kernel, no autograd: returns ``(y, saved, mean, rstd, w32)``
-    where ``saved`` is what the backward reads (the GroupNorm input ``relu(x + add)``, or ``x``)."""
+    where ``saved`` is what the backward reads (the GroupNorm input ``relu(x + add)``, or ``x``).
+    ``out`` ([N, H*W*C] rows of x's dtype, any row stride, e.g. an Anderson history slot): y is
+    written there (and returned as that tensor)."""
     C = _ext.get(required=True)
     N, Ch, H, W = x.shape
     if add is not None:
         add = add.contiguous(memory_format=torch.channels_last)
     w32, b32 = _f32(weight), _f32(bias)
-    y = torch.empty_like(x, memory_format=torch.channels_last)
+    if out is not None:
+        assert out.dtype == x.dtype and out.shape == (N, Ch * H * W) and out.stride(1) == 1
+        y, ys = out, out.stride(0)
+    else:
+        y, ys = torch.empty_like(x, memory_format=torch.channels_last), 0
     h = torch.empty_like(y) if (add is not None or relu) else None
     mean = torch.empty(N, groups, device=x.device, dtype=torch.float32)
     rstd = torch.empty_like(mean)
     C.groupnorm_nhwc_fwd(x.data_ptr(), add.data_ptr() if add is not None else 0, h.data_ptr() if h is not None else 0,
                          y.data_ptr(), w32.data_ptr() if w32 is not None else 0,
                          b32.data_ptr() if b32 is not None else 0, mean.data_ptr(), rstd.data_ptr(), N, H * W, Ch,
-                         groups, bool(relu), float(eps), DTYPE_CODE[x.dtype], _stream(x))
+                         groups, bool(relu), float(eps), DTYPE_CODE[x.dtype], _stream(x), ys)
     return y, (h if h is not None else x), mean, rstd, w32
 
 

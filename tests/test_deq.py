@@ -227,6 +227,26 @@ def test_fused_groupnorm_gpu(add, relu, dtype, shape, groups):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_groupnorm_out_slot_gpu(gpu_ext, dtype):
+    """gn_fwd_raw writing straight into strided history rows (the DEQ-CIFAR cell's last GroupNorm
+    into its Anderson F slot): the dense output's values, the other rows untouched."""
+    from fluxmpi_amd.ops.groupnorm import gn_fwd_raw
+    torch.manual_seed(8)
+    cl = torch.channels_last
+    N, C, H, W = 4, 64, 9, 7
+    x = torch.randn(N, C, H, W, device="cuda").to(dtype).contiguous(memory_format=cl)
+    a = torch.randn(N, C, H, W, device="cuda").to(dtype).contiguous(memory_format=cl)
+    w, b = torch.randn(C, device="cuda"), torch.randn(C, device="cuda")
+    y, *_ = gn_fwd_raw(x, a, w, b, 16, 1e-5, True)
+    hist = torch.full((N, 3, C * H * W), float("nan"), device="cuda", dtype=dtype)
+    ys, *_ = gn_fwd_raw(x, a, w, b, 16, 1e-5, True, out=hist[:, 1])
+    assert ys.data_ptr() == hist[:, 1].data_ptr()
+    torch.testing.assert_close(hist[:, 1], y.permute(0, 2, 3, 1).reshape(N, -1), rtol=0, atol=0)
+    assert torch.isnan(hist[:, 0].float()).all() and torch.isnan(hist[:, 2].float()).all()
+
+
+@pytest.mark.gpu
 def test_deq_cell_fused_path_gpu():
     """The DEQ cell on channels_last bf16 takes the HIP GroupNorm path and matches the fp32 composition."""
     from fluxmpi_amd.models.deq import ResidualCell
