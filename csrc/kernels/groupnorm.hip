@@ -6,7 +6,8 @@
 // workgroup owns one sample (HW x C contiguous in NHWC):
 //   forward   h = [relu](x [+ a]);  y = (h - mean_g) * rstd_g * w_c + b_c
 //             pass 1 per-channel sum / sumsq in registers (each lane keeps ONE fixed 8-channel
-//             vector: blockDim = (256 / (C/8)) * (C/8) lanes, so a lane's channels never change),
+//             vector: blockDim = PL * (C/8) lanes, PL pixel lanes (up to 1024 lanes, the reduction
+//             scratch within 64 KB of LDS), so a lane's channels never change),
 //             LDS reduce -> group stats; pass 2 (L2-hot re-read) applies and writes y [and h].
 //   backward  per-channel sums of dy and dy*h in one pass give db_c, dw_c and the two group
 //             terms; pass 2 writes dh = rstd (dy w - s1/M - xhat s2/M) [* (h > 0)], which is the
@@ -20,7 +21,13 @@
 namespace fluxmpi {
 namespace {
 
-constexpr int kMaxThreads = 256;
+// lanes per workgroup (one workgroup per sample: with a batch of 256 and 256 CUs, the lanes of
+// ONE workgroup are all the memory parallelism a CU gets); GN_THREADS: A/B builds only
+#ifndef GN_THREADS
+#define GN_THREADS 1024
+#endif
+constexpr int kMaxThreads = GN_THREADS;
+constexpr int kLdsBudget = 64 * 1024;  // dynamic LDS without a per-kernel attribute
 constexpr int kMaxG = 64;
 // pixels per lane whose loads are issued together (one workgroup per sample: at one pixel per
 // iteration every pass was a chain of dependent memory round trips, ~2.6 TB/s on the DEQ cell)
@@ -38,7 +45,11 @@ GnShape gn_shape(int64_t HW, int64_t C, int64_t G) {
   s.C = static_cast<int>(C);
   s.G = static_cast<int>(G);
   s.CV = s.C / 8;
-  s.PL = kMaxThreads / s.CV;
+  // pixel lanes: as many as fit the workgroup and the reduction's LDS (red[2][PL][C] floats plus
+  // chan[2][C] and grp[2][G])
+  const int by_lds = (kLdsBudget / 4 - 2 * s.C - 2 * s.G) / (2 * s.C);
+  s.PL = kMaxThreads / s.CV < by_lds ? kMaxThreads / s.CV : by_lds;
+  if (s.PL < 1) s.PL = 1;
   s.T = s.PL * s.CV;
   return s;
 }
@@ -286,6 +297,8 @@ __global__ __launch_bounds__(kMaxThreads) void gn_bwd_kernel(const T* __restrict
   }
 }
 
+unsigned block_of(const GnShape& s) { return static_cast<unsigned>((s.T + 63) / 64 * 64); }
+
 size_t gn_lds(const GnShape& s) { return sizeof(float) * (2 * s.PL * s.C + 2 * s.C + 2 * s.G); }
 
 template <typename T>
@@ -299,7 +312,7 @@ void fwd_dispatch(const void* x, const void* a, void* h, void* y, const float* w
   const dim3 grid(static_cast<unsigned>(N));
   const bool add = a != nullptr, saveh = h != nullptr;
 #define GN_FWD(A, R, H) \
-  gn_fwd_kernel<T, A, R, H><<<grid, kMaxThreads, lds, st>>>(xp, ap, hp, yp, w, b, mean, rstd, s, eps, ys)
+  gn_fwd_kernel<T, A, R, H><<<grid, block_of(s), lds, st>>>(xp, ap, hp, yp, w, b, mean, rstd, s, eps, ys)
   if (add && relu) { if (saveh) GN_FWD(true, true, true); else GN_FWD(true, true, false); }
   else if (add) { if (saveh) GN_FWD(true, false, true); else GN_FWD(true, false, false); }
   else if (relu) { if (saveh) GN_FWD(false, true, true); else GN_FWD(false, true, false); }
@@ -313,10 +326,10 @@ void bwd_dispatch(const void* dy, const void* h, const float* mean, const float*
   const size_t lds = gn_lds(s);
   const dim3 grid(static_cast<unsigned>(N));
   if (relu)
-    gn_bwd_kernel<T, true><<<grid, kMaxThreads, lds, st>>>(static_cast<const T*>(dy), static_cast<const T*>(h), mean,
+    gn_bwd_kernel<T, true><<<grid, block_of(s), lds, st>>>(static_cast<const T*>(dy), static_cast<const T*>(h), mean,
                                                           rstd, w, static_cast<T*>(dh), part, s);
   else
-    gn_bwd_kernel<T, false><<<grid, kMaxThreads, lds, st>>>(static_cast<const T*>(dy), static_cast<const T*>(h), mean,
+    gn_bwd_kernel<T, false><<<grid, block_of(s), lds, st>>>(static_cast<const T*>(dy), static_cast<const T*>(h), mean,
                                                            rstd, w, static_cast<T*>(dh), part, s);
 }
 
