@@ -375,7 +375,9 @@ def test_deq_manual_vjp_matches_autograd(gpu_ext):
     out, state = cell.forward_state(z, x)
     z0 = z.clone().requires_grad_()
     f0 = cell(z0, x)
-    assert (out.float() - f0.detach().float()).abs().max() < 1e-2
+    # the fused cell kernel and the module path reduce the GroupNorm statistics in different
+    # orders: equal to within one bf16 rounding of the output (2^-8 relative)
+    torch.testing.assert_close(out.float(), f0.detach().float(), rtol=8e-3, atol=1e-2)
     for _ in range(2):
         u = torch.randn_like(z)
         with skip_param_grads():
