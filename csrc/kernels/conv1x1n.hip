@@ -8,8 +8,8 @@
 // without the statistics (profiles/rd5g_roofline_resnet50.md).
 //
 // Persistent: one workgroup per CU owns one 256-column slice of the output (its filter slice,
-// 256 x K, is DMA'd into LDS once) and walks 128-row tiles of x, the next tile's DMA in flight
-// during this tile's MFMAs and stores. 8 waves: 4 row groups of 32 rows x 2 column halves of 128;
+// 256 x K, is DMA'd into LDS once) and walks 128-row tiles of x, the next tile's loads in flight
+// (into registers) during this tile's MFMAs and stores. 8 waves: 4 row groups of 32 rows x 2 column halves of 128;
 // per 32-channel k-step a wave reads 2 activation and 8 filter fragments (ds_read_b128, 128-B
 // rows with chunk slot q ^ (row & 7): conflict-free) for 16 v_mfma_f32_16x16x32_bf16. The
 // statistics accumulate in registers over ALL of the workgroup's tiles and meet in LDS once at
@@ -47,9 +47,11 @@ struct C1Args {
   uint32_t x_bytes;
 };
 
-// __restrict__: the reads get alias scopes, so the waitcnt pass does not put a vmcnt(0) for the
-// in-flight tile DMA (and the stores queued behind it) in front of them
-__device__ __forceinline__ bf16x8 frag(const char* __restrict__ p) { return *reinterpret_cast<const bf16x8*>(p); }
+// LDS reads through an address-space-3 pointer with alias scopes (__restrict__): otherwise the
+// waitcnt pass puts a vmcnt(0) for the in-flight tile DMA — and the stores queued behind it — in
+// front of them
+typedef __attribute__((address_space(3))) const bf16x8 lds_bf16x8;
+__device__ __forceinline__ bf16x8 frag(const char* __restrict__ p) { return *(lds_bf16x8*)(p); }
 
 template <int K, int EPI>
 __global__ __launch_bounds__(kThreads, 1) void conv1x1n_kernel(C1Args p) {
@@ -59,7 +61,11 @@ __global__ __launch_bounds__(kThreads, 1) void conv1x1n_kernel(C1Args p) {
   constexpr int kAPlane = kBM * 128;         // activation plane bytes (one buffer)
   constexpr int kABuf = NPL * kAPlane;
   __shared__ __attribute__((aligned(1024))) char wl[NPL * kWPlane];
-  __shared__ __attribute__((aligned(1024))) char al[2 * kABuf];
+  // two separate tile buffers (not halves of one array): the LDS reads of one and the DMA into the
+  // other are then provably disjoint, so the waitcnt pass does not drain the DMA (and the stores
+  // queued behind it) before the reads
+  __shared__ __attribute__((aligned(1024))) char al0[kABuf];
+  __shared__ __attribute__((aligned(1024))) char al1[kABuf];
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int lrow = lane >> 3, lslot = lane & 7;
@@ -81,17 +87,34 @@ __global__ __launch_bounds__(kThreads, 1) void conv1x1n_kernel(C1Args p) {
     const uint32_t off = static_cast<uint32_t>((slice * kBN + co) * (K * 2) + pl * 128 + ((lslot ^ (co & 7)) << 4));
     __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_char*)(wl + pl * kWPlane + rg * 1024), 16, off, 0, 0, 0);
   }
-  auto issue_a = [&](int t, int buf) {  // one tile of x: NPL * kBM / 8 DMA instructions
-    for (int i = wave; i < NPL * (kBM / 8); i += kWaves) {
+  // x tiles: prefetched into registers one tile ahead (global_load_dwordx4, 16 B per lane), then
+  // written to LDS after this tile's stores; the compiler's own vmcnt accounting then covers the
+  // stores queued between (an LDS-DMA ring made it drain them before every tile's reads)
+  constexpr int kAL = NPL * (kBM / 8) / kWaves;  // 16-B loads per lane per tile
+  uint4 pre[kAL];
+  auto load_a = [&](int t) {
+#pragma unroll
+    for (int j = 0; j < kAL; ++j) {
+      const int i = j * kWaves + wave;
       const int pl = i / (kBM / 8), rg = i - pl * (kBM / 8);
       const int row = rg * 8 + lrow;
-      const uint32_t off =
-          static_cast<uint32_t>((t * kBM + row) * (K * 2) + pl * 128 + ((lslot ^ (row & 7)) << 4));
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_char*)(al + buf * kABuf + pl * kAPlane + rg * 1024), 16, off,
-                                               0, 0, 0);
+      const uint32_t off = static_cast<uint32_t>((t * kBM + row) * (K * 2) + pl * 128 + (lslot << 4));
+      pre[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
     }
   };
-  if (first < p.tiles) issue_a(first, 0);
+  auto store_a = [&](char* dst) {
+#pragma unroll
+    for (int j = 0; j < kAL; ++j) {
+      const int i = j * kWaves + wave;
+      const int pl = i / (kBM / 8), rg = i - pl * (kBM / 8);
+      const int row = rg * 8 + lrow;
+      *reinterpret_cast<uint4*>(dst + pl * kAPlane + row * 128 + ((lslot ^ (row & 7)) << 4)) = pre[j];
+    }
+  };
+  if (first < p.tiles) {
+    load_a(first);
+    store_a(al0);
+  }
 
   float cs[8][4], cq[8][4];  // EPI 3: the lane's column partial sums over every tile it stores
 #pragma unroll
@@ -99,15 +122,15 @@ __global__ __launch_bounds__(kThreads, 1) void conv1x1n_kernel(C1Args p) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) cs[nb][r] = cq[nb][r] = 0.f;
 
-  int buf = 0;
-  for (int t = first; t < p.tiles; t += step, buf ^= 1) {
-    // this wave's DMAs of tile t (and of the filter) have landed; vmcnt counts in issue order and
-    // the previous tile's 16 stores were issued after those DMAs, so they may stay in flight
-    if (t == first) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // everyone's; buffer buf ^ 1 is free again
-    if (t + step < p.tiles) issue_a(t + step, buf ^ 1);
-    const char* ab = al + buf * kABuf;
+  // one tile: wait for `cur`, prefetch the next tile into registers, MFMAs, stores, then `nxt`
+  auto do_tile = [&](int t, const char* __restrict__ cur, char* __restrict__ nxt) {
+    // tile t is in `cur` (every wave's ds_writes, and the filter DMA on the first tile, done);
+    // `nxt` was last read during the previous tile
+    if (t == first) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const bool more = t + step < p.tiles;
+    if (more) load_a(t + step);
     f32x4 acc[2][8];
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb)
@@ -125,7 +148,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv1x1n_kernel(C1Args p) {
 #pragma unroll
       for (int mb = 0; mb < 2; ++mb) {
         const int row = wr * 32 + mb * 16 + fr;
-        fa[mb] = frag(ab + pl * kAPlane + row * 128 + ((ch ^ (row & 7)) << 4));
+        fa[mb] = frag(cur + pl * kAPlane + row * 128 + ((ch ^ (row & 7)) << 4));
       }
 #pragma unroll
       for (int mb = 0; mb < 2; ++mb)
@@ -154,13 +177,19 @@ __global__ __launch_bounds__(kThreads, 1) void conv1x1n_kernel(C1Args p) {
         *reinterpret_cast<uint2*>(yrow + nb * 16) = v;
       }
     }
+    if (more) store_a(nxt);
+  };
+  // the tile loop unrolled by two: each half's buffers are compile-time known (see al0 / al1)
+  for (int t = first; t < p.tiles; t += 2 * step) {
+    do_tile(t, al0, al1);
+    if (t + step < p.tiles) do_tile(t + step, al1, al0);
   }
   if constexpr (EPI == 3) {
     // per column: the wave's 16 row lanes, then the 4 row-group waves through LDS (the tile
     // buffers are free once every wave is past its last tile), one atomic per column and moment
     // per workgroup into the shard blockIdx % kShards
     __syncthreads();
-    float* red = reinterpret_cast<float*>(al);  // [4 row groups][2][kBN]
+    float* red = reinterpret_cast<float*>(al0);  // [4 row groups][2][kBN]
 #pragma unroll
     for (int nb = 0; nb < 8; ++nb)
 #pragma unroll
