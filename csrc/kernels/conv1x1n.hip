@@ -131,6 +131,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv1x1n_kernel(C1Args p) {
     __builtin_amdgcn_s_barrier();
     const bool more = t + step < p.tiles;
     if (more) load_a(t + step);
+    __builtin_amdgcn_sched_barrier(0);  // keep the loads at the top: their latency hides under this tile
     f32x4 acc[2][8];
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb)

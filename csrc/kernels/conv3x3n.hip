@@ -18,7 +18,7 @@
 //     row (a tap shifts the rows by (dr + 1) W + dc + 1), is bank-conflict free for
 //     ds_read_b128's lane groups (model: scripts/lds_banks.py);
 //   * the filter streams one tap (Cout x C) at a time through a double-buffered LDS slot, the
-//     next tap's DMA in flight during this tap's MFMAs;
+//     next tap's loads in flight (into registers) during this tap's MFMAs;
 //   * a tap that falls outside the image (row / column / image boundary in flattened order)
 //     redirects the lane's fragment read to a zero row: one address select per read, no data
 //     masking.
@@ -114,6 +114,31 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 4 : 2) void conv3x3n_kernel(CNA
     }
   };
   issue_b(0, 0);
+  // taps 1..8 are prefetched through registers (global loads during the previous tap's MFMAs,
+  // ds_write after them): an LDS-DMA of the next tap made the waitcnt pass drain it with a
+  // vmcnt(0) in front of the current tap's reads, so nothing overlapped
+  constexpr int kBL = NPL * CO * 8 / kThreads;  // 16-B pieces per lane per tap
+  static_assert(kBL >= 1 && NPL * CO * 8 % kThreads == 0, "tap staging");
+  uint4 bpre[kBL];
+  auto load_b = [&](int tap) {
+#pragma unroll
+    for (int j = 0; j < kBL; ++j) {
+      const int idx = j * kThreads + threadIdx.x;          // (plane, co, chunk)
+      const int pl = idx / (CO * 8), rem = idx - pl * CO * 8;
+      const int co = rem >> 3, q = rem & 7;
+      const uint32_t off = static_cast<uint32_t>((co * 9 + tap) * (C * 2) + pl * 128 + (q << 4));
+      bpre[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, 0));
+    }
+  };
+  auto store_b = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < kBL; ++j) {
+      const int idx = j * kThreads + threadIdx.x;
+      const int pl = idx / (CO * 8), rem = idx - pl * CO * 8;
+      const int co = rem >> 3, q = rem & 7;
+      *reinterpret_cast<uint4*>(bbuf + buf * kBBytes + pl * CO * 128 + co * 128 + ((q ^ (co & 7)) << 4)) = bpre[j];
+    }
+  };
 
   // ---- the lane's rows: local row lr = 32 wave + 16 mb + (lane & 15); in-image taps as 9-bit masks
   const int fr = lane & 15, fg = lane >> 4;
@@ -136,7 +161,8 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 4 : 2) void conv3x3n_kernel(CNA
   __syncthreads();
 
   for (int tap = 0; tap < 9; ++tap) {
-    if (tap < 8) issue_b(tap + 1, (tap + 1) & 1);  // that slot was last read in tap - 1 (barrier since)
+    if (tap < 8) load_b(tap + 1);
+    __builtin_amdgcn_sched_barrier(0);  // keep the loads at the top: their latency hides under this tap
     const int dr = tap / 3, dc = tap - 3 * dr;     // 0..2
     const char* bb = bbuf + (tap & 1) * kBBytes;
     int arow[2];
@@ -161,7 +187,7 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 4 : 2) void conv3x3n_kernel(CNA
         for (int nb = 0; nb < NB; ++nb)
           acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[nb], fa[mb], acc[mb][nb], 0, 0, 0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next tap's filter has landed (this wave's part)
+    if (tap < 8) store_b((tap + 1) & 1);  // that slot was last read in tap - 1 (barrier since)
     __syncthreads();
   }
 
