@@ -7,7 +7,8 @@ C="--model deq_cifar --force-comm --steps 20 --warmup 10"
 B="--steps 20 --warmup 10"
 step pytest 600 0 python -u -m pytest tests/test_deq.py tests/test_conv1x1n_gpu.py tests/test_conv3x3n_gpu.py tests/test_fused_block_gpu.py -m gpu \
   -x -q --timeout 120 --timeout-method thread
-step bench_c1 240 0 python scripts/bench_conv1x1n.py && python scripts/bench_conv3x3n.py
+step bench_c1 240 0 python scripts/bench_conv1x1n.py
+step bench_c3 240 0 python scripts/bench_conv3x3n.py
 step cifar_gn256 300 0 env FLUXMPI_C_VARIANT=exp/variants/_C_gn256.so python scripts/diag/bench_variant.py $C
 step cifar_gn1024 300 0 python bench.py $C
 step r50_off 300 0 python scripts/diag/bench_no_conv1x1n.py $B
