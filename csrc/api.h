@@ -249,11 +249,6 @@ void gemm_nt_conv(const void* x, const void* w, void* y, float* stats, int64_t n
 // Narrow-channel 3x3 / stride 1 / pad 1 convolution (conv3x3n.hip): C = Cout in {64, 128}, the
 // input halo staged once per 256-pixel workgroup; x [pixels][C] NHWC, w [Cout][9][C], y [pixels][Cout];
 // epi 0 or 3 (BatchNorm statistics into stats[64][2][Cout])
-// Narrow-K 1x1 forward (conv1x1n.hip): y[M][N] = x[M][K] W[N][K]^T for K in {64, 128}, N % 256 == 0,
-// M % 128 == 0; epi 0 or 3 (BatchNorm statistics into stats[64][2][N])
-bool conv1x1n_supported(int64_t M, int64_t K, int64_t N);
-void conv1x1n(const void* x, const void* w, void* y, float* stats, int64_t M, int64_t K, int64_t N, int epi,
-              hipStream_t stream);
 bool conv3x3n_supported(int64_t pixels, int C, int Cout, int H, int W);
 void conv3x3n(const void* x, const void* w, void* y, float* stats, int64_t pixels, int H, int W, int C, int Cout,
               int epi, hipStream_t stream);

@@ -311,12 +311,6 @@ PYBIND11_MODULE(_C, m) {
     gemm_nt(reinterpret_cast<const void*>(a), reinterpret_cast<const void*>(b), reinterpret_cast<void*>(c), nullptr,
             nullptr, 0, nullptr, nullptr, reinterpret_cast<float*>(stats), lda, ldb, ldc, M, N, K, 3, S(stream));
   });
-  m.def("conv1x1n_supported", &conv1x1n_supported);
-  m.def("conv1x1n", [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, int64_t M, int64_t K, int64_t N, int epi,
-                       uintptr_t stream) {
-    conv1x1n(reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(w), reinterpret_cast<void*>(y),
-             reinterpret_cast<float*>(stats), M, K, N, epi, S(stream));
-  });
   m.def("conv3x3n_supported", &conv3x3n_supported);
   m.def("conv3x3n", [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, int64_t pixels, int H, int W, int C,
                        int Cout, int epi, uintptr_t stream) {

@@ -98,9 +98,7 @@ def _fwd1x1_stats(x, weight, stats):
     co = weight.shape[0]
     c = _empty_nhwc(n, co, h, w, x)
     x2, w2 = _nhwc2d(x), weight.reshape(co, ci)
-    if G.conv1x1n_ok(n * h * w, ci, co, x2, w2):  # K = 64 / 128 expansions (stages 1-2)
-        G.conv1x1n(x2, w2.contiguous(), _nhwc2d(c), stats)
-    elif G.ENGINE != 1 and _NT.gemm_ok(n * h * w, co, ci, x2, w2):
+    if G.ENGINE != 1 and _NT.gemm_ok(n * h * w, co, ci, x2, w2):
         _NT.gemm_plain(x2, w2, _nhwc2d(c), stats)
     else:
         gemm(x2, w2, c, M=n * h * w, N=co, K=ci, lda=ci, ldb=ci, ldc=co, a_kmajor=True, b_kmajor=True, mode=1,
@@ -236,9 +234,6 @@ def _ds_fwd_ours(x, weight, stride, stats):
     co = weight.shape[0]
     ho, wo = (h + stride - 1) // stride, (w + stride - 1) // stride
     c = _empty_nhwc(n, co, ho, wo, x)
-    if stride == 1 and G.conv1x1n_ok(n * h * w, ci, co, x):  # the stage-1 downsample (64 -> 256)
-        G.conv1x1n(_nhwc2d(x), weight.reshape(co, ci).contiguous(), _nhwc2d(c), stats)
-        return c
     gemm(_nhwc2d(x), weight.reshape(co, ci), c, M=n * ho * wo, N=co, K=ci, lda=ci, ldb=ci, ldc=co, mode=1,
          stats=stats, a_sub=(h, w) if stride == 2 else None)
     return c

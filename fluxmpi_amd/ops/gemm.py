@@ -170,27 +170,6 @@ def conv_n_ok(pixels: int, c: int, co: int, h: int, w: int, *tensors: torch.Tens
     return C is not None and hasattr(C, "conv3x3n") and bool(C.conv3x3n_supported(pixels, c, co, h, w))
 
 
-def conv1x1n_ok(m: int, k: int, n: int, *tensors: torch.Tensor) -> bool:
-    """The narrow-K 1x1 forward kernel (``conv1x1n.hip``: K in {64, 128}, N % 256 == 0, M % 128 == 0;
-    ResNet-50's stage-1/2 expansions) takes this GEMM (16-B aligned bf16 operands)."""
-    if ENGINE == 1 or not tensors[0].is_cuda or any(t.dtype != torch.bfloat16 or t.data_ptr() % 16 for t in tensors):
-        return False
-    C = _ext.get(required=False)
-    return C is not None and hasattr(C, "conv1x1n") and bool(C.conv1x1n_supported(m, k, n))
-
-
-def conv1x1n(x2: torch.Tensor, w2: torch.Tensor, y2: torch.Tensor, stats: torch.Tensor | None = None) -> torch.Tensor:
-    """``y2 [M, N] = x2 [M, K] @ w2 [N, K]^T`` on the narrow-K kernel (dense rows); ``stats``:
-    BatchNorm shards [64][2][N] (sum / sum of squares of the rounded output)."""
-    C = _ext.get(required=True)
-    m, k = x2.shape
-    n = w2.shape[0]
-    assert x2.is_contiguous() and w2.is_contiguous() and y2.is_contiguous()
-    C.conv1x1n(x2.data_ptr(), w2.data_ptr(), y2.data_ptr(), stats.data_ptr() if stats is not None else 0, m, k, n,
-               3 if stats is not None else 0, _stream(x2))
-    return y2
-
-
 def conv3x3n(x: torch.Tensor, w_taps: torch.Tensor, y: torch.Tensor, pixels: int, h: int, w: int,
              stats: torch.Tensor | None = None) -> torch.Tensor:
     """``y [pixels, Cout] = conv3x3(x)`` on the narrow-channel kernel: ``x`` NHWC memory, ``w_taps``
