@@ -6,7 +6,7 @@
 // workgroup owns one sample (HW x C contiguous in NHWC):
 //   forward   h = [relu](x [+ a]);  y = (h - mean_g) * rstd_g * w_c + b_c
 //             pass 1 per-channel sum / sumsq in registers (each lane keeps ONE fixed 8-channel
-//             vector: blockDim = PL * (C/8) lanes, PL pixel lanes (up to 1024 lanes, the reduction
+//             vector: blockDim = PL * (C/8) lanes, PL pixel lanes (up to 256 lanes, the reduction
 //             scratch within 64 KB of LDS), so a lane's channels never change),
 //             LDS reduce -> group stats; pass 2 (L2-hot re-read) applies and writes y [and h].
 //   backward  per-channel sums of dy and dy*h in one pass give db_c, dw_c and the two group
@@ -21,10 +21,10 @@
 namespace fluxmpi {
 namespace {
 
-// lanes per workgroup (one workgroup per sample: with a batch of 256 and 256 CUs, the lanes of
-// ONE workgroup are all the memory parallelism a CU gets); GN_THREADS: A/B builds only
+// lanes per workgroup, one workgroup per sample. 1024 lanes (GN_THREADS=1024, A/B builds only)
+// measured 4-8 % slower than 256 at the DEQ shapes (profiles/rd5l_bench_gn.jsonl)
 #ifndef GN_THREADS
-#define GN_THREADS 1024
+#define GN_THREADS 256
 #endif
 constexpr int kMaxThreads = GN_THREADS;
 constexpr int kLdsBudget = 64 * 1024;  // dynamic LDS without a per-kernel attribute
