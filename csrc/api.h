@@ -252,6 +252,15 @@ void gemm_nt_conv(const void* x, const void* w, void* y, float* stats, int64_t n
 bool conv3x3n_supported(int64_t pixels, int C, int Cout, int H, int W);
 void conv3x3n(const void* x, const void* w, void* y, float* stats, int64_t pixels, int H, int W, int C, int Cout,
               int epi, hipStream_t stream);
+// Weight gradient of the narrow-channel 3x3 / stride 1 / pad 1 convolution (wgrad3x3n.hip): dy
+// [N][H][W][Cout], x [N][H][W][C] (C in {64, 128}); ws[split][Cout][9 C] fp32 partials (reduce with
+// gemm_splitk_reduce; the actual split count is wgrad3x3n_splits). variant bit 0: 8 waves (else 4).
+// A workgroup owns 64 Cout x all nine taps (C = 64) or x one filter row of three taps (C = 128).
+bool wgrad3x3n_supported(int64_t N, int H, int W, int C, int Cout);
+int wgrad3x3n_splits(int64_t N, int H, int splits);
+int wgrad3x3n_groups(int C, int Cout, int variant);
+void wgrad3x3n(const void* dy, const void* x, float* ws, int64_t N, int H, int W, int C, int Cout, int splits,
+               int variant, hipStream_t stream);
 // dst[c][r] = src[r][c], bf16 (rows, cols, leading dims multiples of 8)
 void transpose_bf16(const void* src, void* dst, int64_t rows, int64_t cols, int64_t lds, int64_t ldd,
                     hipStream_t stream);

@@ -317,6 +317,14 @@ PYBIND11_MODULE(_C, m) {
     conv3x3n(reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(w), reinterpret_cast<void*>(y),
              reinterpret_cast<float*>(stats), pixels, H, W, C, Cout, epi, S(stream));
   });
+  m.def("wgrad3x3n_supported", &wgrad3x3n_supported);
+  m.def("wgrad3x3n_splits", &wgrad3x3n_splits);
+  m.def("wgrad3x3n_groups", &wgrad3x3n_groups);
+  m.def("wgrad3x3n", [](uintptr_t dy, uintptr_t x, uintptr_t ws, int64_t N, int H, int W, int C, int Cout, int splits,
+                        int variant, uintptr_t stream) {
+    wgrad3x3n(reinterpret_cast<const void*>(dy), reinterpret_cast<const void*>(x), reinterpret_cast<float*>(ws), N, H,
+              W, C, Cout, splits, variant, S(stream));
+  });
   m.def("gemm_nt_conv_supported", &gemm_nt_conv_supported);
   m.def("gemm_nt_conv", [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, int64_t nimg, int H, int W, int C,
                            int64_t Cout, int epi, uintptr_t stream, uintptr_t residual) {

@@ -1,0 +1,314 @@
+// Weight gradient of the narrow-channel 3x3 / stride 1 / pad 1 convolution, NHWC bf16 — gfx950.
+//
+//   dW[co][tap][ci] = sum over pixels p of dY[p][co] * X[p + shift(tap)][ci],  tap = 3 (dr + 1) + (ds + 1)
+//
+// ResNet-50's stage-1 (C = 64, 56 x 56) and stage-2 (C = 128, 28 x 28) 3x3 weight gradients ran at
+// 18 / 25 % of the bf16 peak on the split-K LDS-DMA kernel (profiles/rd5g_roofline_resnet50.md):
+// its B operand is the implicit im2col, so each input pixel crosses L2 -> LDS once per tap and dY
+// once per 128-column tile (~1.5 GB of L2 -> LDS traffic for 0.2 GB of operands). Here a workgroup
+// walks blocks of kR image rows:
+//   * the block's dY rows and the kR + 2 input rows around them (zeros outside the image) are
+//     staged ONCE into LDS, the input in a layout with zero columns either side of each row, so the
+//     nine taps are nine constant offsets into one image: no masks, no per-tap loads;
+//   * both MFMA operands run along pixels (the GEMM's k) and are read with ds_read_b64_tr_b16. A
+//     read's 32-lane half takes two runs of 4 consecutive pixels, and pixel slots lie C * 2 + 32
+//     bytes apart (an odd multiple of 8 banks): the 8 rows of a half land on 8 disjoint 8-bank
+//     windows whatever the tap offset, provided the second run starts 4 slots (mod 8) after the
+//     first — true inside an image row, and across rows once the row pitch P == W (mod 8);
+//   * the next block's rows are loaded into registers during this block's MFMAs (ds_write after a
+//     barrier: an LDS-DMA ring makes the waitcnt pass drain it in front of the reads, conv3x3n.hip).
+// The workgroup's output is 64 co x TG taps x C ci. Its 4 or 8 waves split the columns (and with 8
+// the co rows in halves) and keep fp32 sums in registers across all blocks of their K-split;
+// partials [splits][Cout][9 C] go through the shared split-K reduce (gemm_splitk_reduce).
+// Reference: /root/reference has no kernels — this is the compute under the per-step gradient work
+// of the ResNet-50 DDP configuration (BASELINE.json, src/optimizer.jl:20-23).
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+#include "../api.h"
+#include "common.h"
+
+namespace fluxmpi {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short short4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) short4v lds_short4v;
+
+constexpr int kR = 4;       // image rows per block
+constexpr int kCOB = 64;    // output channels per workgroup
+constexpr int kSA = 160;    // dY slot stride (64 channels + 32 B): 40 banks
+constexpr uint32_t kOOB = 0x80000000u;  // a buffer offset past every operand: the load returns zeros
+
+template <int C> struct Geo3 {
+  static constexpr int kW = C == 64 ? 56 : 28;            // widest supported image row
+  static constexpr int kP = kW % 8 == 0 ? kW + 2 : kW + 8;  // its padded row pitch
+  static constexpr int kSB = C * 2 + 32;                  // input slot stride: 40 / 72 banks
+  static constexpr int kXBytes = (kR + 2) * kP * kSB;
+  static constexpr int kDBytes = kR * kW * kSA;
+  static constexpr int kBytes = kXBytes + kDBytes + kSA;  // + one zero dY slot
+};
+
+__host__ __device__ constexpr int pitch_of(int W) { return W % 8 == 0 ? W + 2 : W + 8; }
+
+struct W3Args {
+  const bf16* dy;  // [N][H][W][CO]
+  const bf16* x;   // [N][H][W][C]
+  float* ws;       // [splits][CO][9 C]
+  uint32_t dy_bytes, x_bytes;
+  int H, W, CO;
+  int nblocks;     // N * H / kR
+  int per_split;   // blocks per K-split
+  int groups;      // (CO / 64) * (9 / TG) output blocks per split
+};
+
+__device__ __forceinline__ short4v tr_read(const char* lds, int byte) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(lds + byte));
+}
+
+__device__ __forceinline__ bf16x8 join(short4v lo, short4v hi) {
+  bf16x8 out;
+  __builtin_memcpy(&out, &lo, 8);
+  __builtin_memcpy(reinterpret_cast<char*>(&out) + 8, &hi, 8);
+  return out;
+}
+
+template <int C, int TG, int NWM>
+__global__ __launch_bounds__(256 * NWM, 1) void wgrad3x3n_kernel(W3Args p) {
+  using G = Geo3<C>;
+  constexpr int NT = 256 * NWM;
+  constexpr int CW = kCOB / NWM;             // co rows per wave
+  constexpr int FI = CW / 16;                // A fragments per wave
+  constexpr int CF = C / 16;                 // 16-column fragments per tap
+  constexpr int NF = TG * CF / 4;            // B fragments per wave
+  static_assert(TG * CF % 4 == 0, "tap group split");
+  constexpr int kXP = (kR + 2) * G::kW * C / 8;  // 16-B input pieces of a block (widest row)
+  constexpr int kDP = kR * G::kW * kCOB / 8;     // 16-B dY pieces
+  constexpr int JX = (kXP + NT - 1) / NT, JD = (kDP + NT - 1) / NT;
+  constexpr int DB = G::kXBytes, ZB = G::kXBytes + G::kDBytes;
+  __shared__ __attribute__((aligned(1024))) char lds[G::kBytes];
+
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int wm = wave / 4, wn = wave % 4;
+  const int H = p.H, W = p.W, P = pitch_of(W), CO = p.CO;
+  const int hb = H / kR;
+  // (split, group) of this workgroup; XCD-aware: the workgroups of one XCD take a contiguous range,
+  // so the groups of one split (same pixels, other output columns) share that XCD's L2
+  int lid = blockIdx.x;
+  const int total = static_cast<int>(gridDim.x);
+  if (total >= 8) {
+    const int q = total / 8, r = total % 8, xcd = lid % 8, pos = lid / 8;
+    lid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+  }
+  lid = __builtin_amdgcn_readfirstlane(lid);
+  const int split = lid / p.groups, grp = lid - split * p.groups;
+  constexpr int NTG = 9 / TG;
+  const int co0 = (grp / NTG) * kCOB, t0 = (grp % NTG) * TG;
+  const int b0 = split * p.per_split;
+  const int b1 = b0 + p.per_split < p.nblocks ? b0 + p.per_split : p.nblocks;
+
+  // ---- zero the pad columns of the input rows and the zero dY slot (never written again)
+  {
+    constexpr int SP = G::kSB / 16;  // 16-B pieces per input slot
+    const int padc = P - W;          // pad slots per row: column 0 and W + 1 .. P - 1
+    const int npad = (kR + 2) * padc * SP;
+    for (int i = tid; i < npad + kSA / 16; i += NT) {
+      int off;
+      if (i < npad) {
+        const int s = i / SP, piece = i - s * SP;
+        const int rr = s / padc, k = s - rr * padc;
+        off = (rr * P + (k == 0 ? 0 : W + k)) * G::kSB + piece * 16;
+      } else {
+        off = ZB + (i - npad) * 16;
+      }
+      *reinterpret_cast<uint4*>(lds + off) = uint4{0, 0, 0, 0};
+    }
+  }
+
+  // ---- staging: this thread's 16-B pieces (the same LDS places for every block)
+  const int NX = (kR + 2) * W * C / 8, ND = kR * W * kCOB / 8;
+  int xl[JX];
+#pragma unroll
+  for (int j = 0; j < JX; ++j) {
+    const int i = j * NT + tid;
+    const int pi = i / (C / 8), c = i - pi * (C / 8);
+    const int rr = pi / W, w = pi - rr * W;
+    xl[j] = (rr * P + w + 1) * G::kSB + c * 16;
+  }
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(p.x), 0, p.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(p.dy), 0, p.dy_bytes, 0x00020000);
+  uint4 xv[JX], dv[JD];
+  auto load = [&](int b) {
+    const int n = b / hb, h0 = (b - n * hb) * kR;
+    const int64_t xbase = (static_cast<int64_t>(n) * H + h0 - 1) * W * C * 2;
+    const int lo = h0 == 0 ? W * C / 8 : 0;
+    const int hi = h0 + kR == H ? (kR + 1) * W * C / 8 : NX;
+#pragma unroll
+    for (int j = 0; j < JX; ++j) {
+      const int i = j * NT + tid;
+      const uint32_t off = i >= lo && i < hi ? static_cast<uint32_t>(xbase + i * 16) : kOOB;
+      xv[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
+    }
+    const int64_t dbase = (static_cast<int64_t>(n) * H + h0) * W * CO * 2 + co0 * 2;
+#pragma unroll
+    for (int j = 0; j < JD; ++j) {
+      const int i = j * NT + tid;
+      const uint32_t off = i < ND ? static_cast<uint32_t>(dbase + (i >> 3) * CO * 2 + (i & 7) * 16) : kOOB;
+      dv[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(dr, off, 0, 0));
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int j = 0; j < JX; ++j)
+      if (j * NT + tid < NX) *reinterpret_cast<uint4*>(lds + xl[j]) = xv[j];
+#pragma unroll
+    for (int j = 0; j < JD; ++j) {
+      const int i = j * NT + tid;
+      if (i < ND) *reinterpret_cast<uint4*>(lds + DB + (i >> 3) * kSA + (i & 7) * 16) = dv[j];
+    }
+  };
+
+  // ---- the lane's pixels: read r of step s takes pixel 32 s + 8 r + c0 of the block for MFMA row
+  // k = 8 g + 4 r + q (g = lane / 16, q = (lane / 4) % 4): each 32-lane half reads two runs of 4
+  // consecutive pixels; pc = lane % 4 picks the 4 columns of the 16 that the lane fetches
+  const int g = lane >> 4, q = (lane >> 2) & 3, pc = lane & 3;
+  const int c0 = 16 * (g >> 1) + 4 * (g & 1) + q;
+  const int RW = kR * W, nstep = (RW + 31) / 32;
+  int row0[2], col0[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    row0[r] = (8 * r + c0) / W;
+    col0[r] = 8 * r + c0 - row0[r] * W;
+  }
+  // B fragments: wave wn takes the 16-channel blocks wn + 4 j of every tap of the group, so a
+  // fragment's offset from the wave's base is (filter row) x P + (filter column) slots + 128 j bytes:
+  // compile-time except the row term (P is the runtime pitch), one base per filter row
+  constexpr int TR = TG / 3;  // filter rows per workgroup (the tap group is whole rows)
+  constexpr int JB = CF / 4;  // channel blocks per wave and tap
+  const int bwave = __builtin_amdgcn_readfirstlane((t0 / 3) * P * G::kSB + wn * 32);
+  f32x4 acc[FI][NF];
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int f = 0; f < NF; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (b0 < b1) {
+    load(b0);
+    store();
+  }
+  __syncthreads();
+  for (int b = b0; b < b1; ++b) {
+    const bool more = b + 1 < b1;
+    if (more) load(b + 1);
+    __builtin_amdgcn_sched_barrier(0);  // keep the loads at the top: their latency hides under the MFMAs
+    int row[2] = {row0[0], row0[1]}, col[2] = {col0[0], col0[1]};
+    for (int s = 0; s < nstep; ++s) {
+      int aa[2], bb[2][TR];
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const bool ok = row[r] < kR;  // a partial last step reads zero dY rows (and finite input)
+        aa[r] = (ok ? DB + (row[r] * W + col[r]) * kSA : ZB) + wm * CW * 2 + pc * 8;
+        const int base = (ok ? (row[r] * P + col[r]) * G::kSB : 0) + bwave + pc * 8;
+#pragma unroll
+        for (int d = 0; d < TR; ++d) bb[r][d] = base + d * P * G::kSB;
+        col[r] += 32;
+        while (col[r] >= W) {
+          col[r] -= W;
+          ++row[r];
+        }
+      }
+      bf16x8 fa[FI], fb[NF];
+#pragma unroll
+      for (int i = 0; i < FI; ++i) fa[i] = join(tr_read(lds, aa[0] + i * 32), tr_read(lds, aa[1] + i * 32));
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        const int tl = f / JB, j = f % JB;
+        const int off = (tl % 3) * G::kSB + j * 128;
+        fb[f] = join(tr_read(lds, bb[0][tl / 3] + off), tr_read(lds, bb[1][tl / 3] + off));
+      }
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+          acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[f], acc[i][f], 0, 0, 0);
+    }
+    if (more) {
+      __syncthreads();  // every wave is done reading this block
+      store();
+    }
+    __syncthreads();
+  }
+
+  // ---- fp32 partials: acc[i][f][r] = dW[co0 + wm CW + 16 i + 4 g + r][(t0 + tl) C + 16 (wn + 4 j) + lane % 16]
+  float* out = p.ws + static_cast<int64_t>(split) * CO * 9 * C;
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const int tl = f / JB, j = f % JB;
+      const int col = (t0 + tl) * C + 16 * (wn + 4 * j) + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wm * CW + 16 * i + 4 * g + r;
+        out[static_cast<int64_t>(co) * 9 * C + col] = acc[i][f][r];
+      }
+    }
+}
+
+template <int C, int TG, int NWM>
+void launch3(const W3Args& a, int splits, hipStream_t s) {
+  wgrad3x3n_kernel<C, TG, NWM><<<splits * a.groups, 256 * NWM, 0, s>>>(a);
+  FLUXMPI_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace
+
+bool wgrad3x3n_supported(int64_t N, int H, int W, int C, int Cout) {
+  if (C != 64 && C != 128) return false;
+  const int maxw = C == 64 ? Geo3<64>::kW : Geo3<128>::kW;
+  const int maxp = C == 64 ? Geo3<64>::kP : Geo3<128>::kP;
+  return N >= 1 && H >= kR && H % kR == 0 && W >= 4 && W % 4 == 0 && W <= maxw && pitch_of(W) <= maxp &&
+         Cout >= kCOB && Cout % kCOB == 0 && N * H * W * static_cast<int64_t>(C > Cout ? C : Cout) * 2 < (int64_t(1) << 31);
+}
+
+int wgrad3x3n_splits(int64_t N, int H, int splits) {
+  const int64_t nb = N * (H / kR);
+  const int64_t s = splits < 1 ? 1 : (splits > nb ? nb : splits);
+  const int64_t per = (nb + s - 1) / s;
+  return static_cast<int>((nb + per - 1) / per);
+}
+
+int wgrad3x3n_groups(int C, int Cout, int variant) {
+  (void)variant;
+  return (Cout / kCOB) * (C == 64 ? 1 : 3);
+}
+
+void wgrad3x3n(const void* dy, const void* x, float* ws, int64_t N, int H, int W, int C, int Cout, int splits,
+               int variant, hipStream_t stream) {
+  if (!wgrad3x3n_supported(N, H, W, C, Cout))
+    throw std::runtime_error("wgrad3x3n: unsupported shape (C in {64, 128}, Cout % 64 == 0, H % 4 == 0, W % 4 == 0, "
+                             "W <= 56 / 28; N=" + std::to_string(N) + " H=" + std::to_string(H) + " W=" +
+                             std::to_string(W) + " C=" + std::to_string(C) + " Cout=" + std::to_string(Cout) + ")");
+  if (((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(ws)) & 15u) != 0)
+    throw std::runtime_error("wgrad3x3n: operands must be 16-byte aligned");
+  W3Args a{};
+  a.dy = static_cast<const bf16*>(dy), a.x = static_cast<const bf16*>(x), a.ws = ws;
+  a.dy_bytes = static_cast<uint32_t>(N * H * W * Cout * 2);
+  a.x_bytes = static_cast<uint32_t>(N * H * W * C * 2);
+  a.H = H, a.W = W, a.CO = Cout;
+  a.nblocks = static_cast<int>(N * (H / kR));
+  const int sp = wgrad3x3n_splits(N, H, splits);
+  a.per_split = (a.nblocks + sp - 1) / sp;
+  a.groups = wgrad3x3n_groups(C, Cout, variant);
+  const bool w8 = variant & 1;
+  if (C == 64) {
+    if (w8) launch3<64, 9, 2>(a, sp, stream); else launch3<64, 9, 1>(a, sp, stream);
+  } else {
+    if (w8) launch3<128, 3, 2>(a, sp, stream); else launch3<128, 3, 1>(a, sp, stream);
+  }
+}
+
+}  // namespace fluxmpi

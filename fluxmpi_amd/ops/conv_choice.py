@@ -12,7 +12,7 @@ the same kernels):
 ``_S2_CHOICE``    3x3 / s2 forward: ours + statistics epilogue (True) or MIOpen
 ``_DS_CHOICE``    downsample 1x1 forward: ours + statistics epilogue (True) or MIOpen
 ``_DGRAD_CHOICE`` 3x3 / s1 input gradient with narrow channels: ours (True) or MIOpen
-``_WG_CHOICE``    weight gradients: ("miopen" | "ours" | "w256", our kernel config)
+``_WG_CHOICE``    weight gradients: ("miopen" | "ours" | "w256" | "w3n", our kernel config)
 ================  ================================================================
 
 Frozen (``freeze_choices``) or inside a HIP-graph capture, a missing shape takes the
@@ -35,6 +35,8 @@ WGRAD = "auto"
 FWD_ENGINES = (0, 8, 7)
 # our weight-gradient kernel configurations tried by the autotune: (variant, target workgroups); s44 sweep
 _WG_CONFIGS = ((2, 512), (2, 768), (2, 1024), (2, 384))
+# the narrow 3x3 weight-gradient kernel (wgrad3x3n.hip) configurations: (variant, target workgroups)
+_W3N_CONFIGS = ((1, 256), (1, 512), (0, 256), (0, 512))
 # the statistics pass a MIOpen forward then needs is priced at one read of the output at this rate
 _STATS_PASS_BPS = 5e12
 
@@ -111,7 +113,8 @@ def _with_cfg(cfg, fn):
 
 def wgrad_best(key, impls: dict, param=None):
     """Run the fastest weight-gradient implementation for ``key`` (measured on first use: MIOpen
-    vs our kernel in each of ``_WG_CONFIGS``, and "w256" when offered) and return its result.
+    vs our kernel in each of ``_WG_CONFIGS``, "w256" when offered, and "w3n" — a callable taking one
+    of ``_W3N_CONFIGS`` — when offered) and return its result.
     ``param``: the weight, whose DDP bucket slice (if any) receives the returned gradient
     (``graddst``; never during the measurements)."""
     choice = _WG_CHOICE.get(key)
@@ -130,10 +133,17 @@ def wgrad_best(key, impls: dict, param=None):
                 t = time_us(impls["w256"])
                 if t < best[0]:
                     best = (t, ("w256", None))
+            if "w3n" in impls:
+                for cfg in _W3N_CONFIGS:
+                    t = time_us(lambda: impls["w3n"](cfg))
+                    if t < best[0]:
+                        best = (t, ("w3n", cfg))
             choice = best[1]
         _WG_CHOICE[key] = choice
     name, cfg = choice
     with graddst.into(param):
+        if name == "w3n":
+            return impls[name](cfg)
         return impls[name]() if cfg is None else _with_cfg(cfg, impls[name])
 
 

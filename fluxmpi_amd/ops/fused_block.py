@@ -566,10 +566,13 @@ class _Conv3x3(torch.autograd.Function):
         # (inside groupnorm.skip_param_grads — the DEQ adjoint's VJPs w.r.t. activations only — the
         # filter gradient is not wanted although needs_input_grad, fixed at forward time, says so)
         if ctx.needs_input_grad[1] and not _GN._SKIP_PARAM_GRADS:
-            dw = wgrad_best(("3x3", tuple(x.shape), weight.shape[0]), {
+            impls = {
                 "miopen": lambda: torch.ops.aten.convolution_backward(dy, x, weight, None, [1, 1], [1, 1], [1, 1], False,
                                                                       [0, 0], 1, [False, True, False])[1],
-                "ours": lambda: G.conv3x3_wgrad(dy, x)}, param=weight)
+                "ours": lambda: G.conv3x3_wgrad(dy, x)}
+            if x.dtype == torch.bfloat16 and G.wgrad3x3n_ok(tuple(x.shape), weight.shape[0]):
+                impls["w3n"] = lambda cfg: G.conv3x3_wgrad_n(dy, x, *cfg)  # narrow channels: rows staged once
+            dw = wgrad_best(("3x3", tuple(x.shape), weight.shape[0]), impls, param=weight)
         dx = None
         if ctx.needs_input_grad[0]:
             bl = ctx.bnlink

@@ -394,6 +394,34 @@ def conv3x3_wgrad_s2(dy: torch.Tensor, x: torch.Tensor, splits: int | None = Non
     return dw.permute(0, 3, 1, 2)
 
 
+def wgrad3x3n_ok(x_shape, co: int) -> bool:
+    """The narrow-channel 3x3 weight-gradient kernel (``wgrad3x3n.hip``: C in {64, 128}, Cout % 64
+    == 0, H % 4 == 0, W % 4 == 0 up to 56 / 28 — ResNet-50 stages 1-2) takes this shape."""
+    C = _ext.get()
+    n, c, h, w = x_shape
+    return C is not None and hasattr(C, "wgrad3x3n") and bool(C.wgrad3x3n_supported(n, h, w, c, co))
+
+
+def conv3x3_wgrad_n(dy: torch.Tensor, x: torch.Tensor, variant: int = 1, target_wg: int = 256) -> torch.Tensor:
+    """Weight gradient of the 3x3/s1/p1 convolution on ``wgrad3x3n.hip`` (input rows staged once
+    per block of 4 image rows, the nine taps as offsets into them; variant 1: 8 waves, 0: 4):
+    fp32 partials over ~``target_wg`` workgroups, then the split-K reduce. Returns [Co, Ci, 3, 3]
+    in channels_last, like ``conv3x3_wgrad``."""
+    n, co, h, wd = dy.shape
+    ci = x.shape[1]
+    dys = dy if dy.is_contiguous(memory_format=torch.channels_last) else dy.contiguous(
+        memory_format=torch.channels_last)
+    xs = x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
+    C = _ext.get(required=True)
+    groups = C.wgrad3x3n_groups(ci, co, variant)
+    s = C.wgrad3x3n_splits(n, h, max(1, target_wg // groups))
+    ws = torch.empty(s, co, 9 * ci, device=dy.device, dtype=torch.float32)
+    C.wgrad3x3n(dys.data_ptr(), xs.data_ptr(), ws.data_ptr(), n, h, wd, ci, co, s, variant, _stream(dy))
+    dw = graddst.empty((co, 3, 3, ci), dy.dtype, dy.device)
+    _wgrad_reduce(ws, s, dw)
+    return dw.permute(0, 3, 1, 2)
+
+
 def conv3x3_wgrad(dy: torch.Tensor, x: torch.Tensor, splits: int | None = None) -> torch.Tensor:
     """Weight gradient of the 3x3/s1/p1 convolution: dW[co][(r, s, ci)] = sum over pixels of
     dY[pix][co] * X[pix + (r-1)*W + (s-1)][ci] — the implicit im2col is the B operand. Returns
