@@ -16,7 +16,8 @@
 //     windows whatever the tap offset, provided the second run starts 4 slots (mod 8) after the
 //     first — true inside an image row, and across rows once the row pitch P == W (mod 8);
 //   * the next block's rows are loaded into registers during this block's MFMAs (ds_write after a
-//     barrier: an LDS-DMA ring makes the waitcnt pass drain it in front of the reads, conv3x3n.hip).
+//     barrier: an LDS-DMA ring makes the waitcnt pass drain it in front of the reads, conv3x3n.hip);
+//     DEPTH 2 keeps the next two blocks in flight in two register sets.
 // The workgroup's output is 64 co x TG taps x C ci. Its 4 or 8 waves split the columns (and with 8
 // the co rows in halves) and keep fp32 sums in registers across all blocks of their K-split;
 // partials [splits][Cout][9 C] go through the shared split-K reduce (gemm_splitk_reduce).
@@ -75,7 +76,18 @@ __device__ __forceinline__ bf16x8 join(short4v lo, short4v hi) {
   return out;
 }
 
-template <int C, int TG, int NWM>
+// scheduling pattern for one k-step: MFMA i is followed by DS reads floor((i+1) NR / NM) - floor(i NR / NM)
+template <int I, int NM, int NR>
+__device__ __forceinline__ void interleave_mfma_ds() {
+  if constexpr (I < NM) {
+    constexpr int nr = (I + 1) * NR / NM - I * NR / NM;
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    if constexpr (nr > 0) __builtin_amdgcn_sched_group_barrier(0x100, nr, 0);
+    interleave_mfma_ds<I + 1, NM, NR>();
+  }
+}
+
+template <int C, int TG, int NWM, int DEPTH>
 __global__ __launch_bounds__(256 * NWM, 1) void wgrad3x3n_kernel(W3Args p) {
   using G = Geo3<C>;
   constexpr int NT = 256 * NWM;
@@ -140,27 +152,42 @@ __global__ __launch_bounds__(256 * NWM, 1) void wgrad3x3n_kernel(W3Args p) {
   }
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(p.x), 0, p.x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(p.dy), 0, p.dy_bytes, 0x00020000);
-  uint4 xv[JX], dv[JD];
-  auto load = [&](int b) {
+  using XV = uint4[JX];
+  using DV = uint4[JD];
+  XV xa, xb;
+  DV da, db;
+  auto load = [&](int b, XV& xv, DV& dv) {
     const int n = b / hb, h0 = (b - n * hb) * kR;
     const int64_t xbase = (static_cast<int64_t>(n) * H + h0 - 1) * W * C * 2;
+#if W3N_DIAG_NOHALO  // diagnostics: the halo rows not loaded (wrong results; their traffic's price)
+    const int lo = W * C / 8, hi = (kR + 1) * W * C / 8;
+#else
     const int lo = h0 == 0 ? W * C / 8 : 0;
     const int hi = h0 + kR == H ? (kR + 1) * W * C / 8 : NX;
+#endif
 #pragma unroll
     for (int j = 0; j < JX; ++j) {
       const int i = j * NT + tid;
+#if W3N_DIAG_NOLOAD  // diagnostics: every load out of bounds (no memory traffic)
+      const uint32_t off = i > (1 << 30) ? static_cast<uint32_t>(xbase + i * 16 + lo + hi) : kOOB;
+#else
       const uint32_t off = i >= lo && i < hi ? static_cast<uint32_t>(xbase + i * 16) : kOOB;
+#endif
       xv[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0));
     }
     const int64_t dbase = (static_cast<int64_t>(n) * H + h0) * W * CO * 2 + co0 * 2;
 #pragma unroll
     for (int j = 0; j < JD; ++j) {
       const int i = j * NT + tid;
+#if W3N_DIAG_NOLOAD
+      const uint32_t off = i > (1 << 30) ? static_cast<uint32_t>(dbase) : kOOB;
+#else
       const uint32_t off = i < ND ? static_cast<uint32_t>(dbase + (i >> 3) * CO * 2 + (i & 7) * 16) : kOOB;
+#endif
       dv[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(dr, off, 0, 0));
     }
   };
-  auto store = [&]() {
+  auto store = [&](const XV& xv, const DV& dv) {
 #pragma unroll
     for (int j = 0; j < JX; ++j)
       if (j * NT + tid < NX) *reinterpret_cast<uint4*>(lds + xl[j]) = xv[j];
@@ -176,13 +203,14 @@ __global__ __launch_bounds__(256 * NWM, 1) void wgrad3x3n_kernel(W3Args p) {
   // consecutive pixels; pc = lane % 4 picks the 4 columns of the 16 that the lane fetches
   const int g = lane >> 4, q = (lane >> 2) & 3, pc = lane & 3;
   const int c0 = 16 * (g >> 1) + 4 * (g & 1) + q;
+#if W3N_DIAG_NOCOMPUTE  // diagnostics: no k-steps (the staging alone)
+  const int RW = kR * W, nstep = W < 0 ? 1 : 0;
+#else
   const int RW = kR * W, nstep = (RW + 31) / 32;
-  int row0[2], col0[2];
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    row0[r] = (8 * r + c0) / W;
-    col0[r] = 8 * r + c0 - row0[r] * W;
-  }
+#endif
+  // pixel px -> (row, column) without a divide: px < 2^9 and W <= 56, so px * ceil(2^20 / W) >> 20
+  // is exact
+  const uint32_t invw = ((1u << 20) + W - 1) / W;
   // B fragments: wave wn takes the 16-channel blocks wn + 4 j of every tap of the group, so a
   // fragment's offset from the wave's base is (filter row) x P + (filter column) slots + 128 j bytes:
   // compile-time except the row term (P is the runtime pitch), one base per filter row
@@ -195,55 +223,102 @@ __global__ __launch_bounds__(256 * NWM, 1) void wgrad3x3n_kernel(W3Args p) {
 #pragma unroll
     for (int f = 0; f < NF; ++f) acc[i][f] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // the fragments of step s (issue only: the waitcnt pass waits for them at their first MFMA)
+  auto read = [&](int s, bf16x8 (&fa)[FI], bf16x8 (&fb)[NF]) {
+    int aa[2], bb[2][TR];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int px = 32 * s + 8 * r + c0;
+      const int row = static_cast<int>((static_cast<uint32_t>(px) * invw) >> 20), col = px - row * W;
+      const bool ok = px < RW;  // a partial last step reads zero dY rows (and finite input)
+      aa[r] = (ok ? DB + px * kSA : ZB) + wm * CW * 2 + pc * 8;
+      const int base = (ok ? (row * P + col) * G::kSB : 0) + bwave + pc * 8;
+#pragma unroll
+      for (int d = 0; d < TR; ++d) bb[r][d] = base + d * P * G::kSB;
+    }
+#pragma unroll
+    for (int i = 0; i < FI; ++i) fa[i] = join(tr_read(lds, aa[0] + i * 32), tr_read(lds, aa[1] + i * 32));
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const int tl = f / JB, j = f % JB;
+      const int off = (tl % 3) * G::kSB + j * 128;
+      fb[f] = join(tr_read(lds, bb[0][tl / 3] + off), tr_read(lds, bb[1][tl / 3] + off));
+    }
+  };
+  auto mma = [&](const bf16x8 (&fa)[FI], const bf16x8 (&fb)[NF]) {
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+      for (int f = 0; f < NF; ++f)
+        acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[f], acc[i][f], 0, 0, 0);
+  };
+  // software-pipelined k-steps: step s + 1's fragment reads are interleaved with step s's MFMAs
+  // (two fragment sets), so the LDS latency hides under the matrix work and fewer than 16 reads
+  // are ever outstanding (lgkmcnt's range: a burst of all 2 (FI + NF) reads made the waitcnt pass
+  // drain most of the next step's reads before this step's first MFMA). The tail step re-reads the
+  // last one into the spare set (harmless) to keep the loop body free of branches.
+  auto compute = [&]() {
+    bf16x8 fa0[FI], fb0[NF], fa1[FI], fb1[NF];
+    read(0, fa0, fb0);
+    int s = 0;
+    for (; s + 1 < nstep; s += 2) {
+      read(s + 1, fa1, fb1);
+      mma(fa0, fb0);
+      interleave_mfma_ds<0, FI * NF, 2 * (FI + NF)>();
+      read(s + 2 < nstep ? s + 2 : nstep - 1, fa0, fb0);
+      mma(fa1, fb1);
+      interleave_mfma_ds<0, FI * NF, 2 * (FI + NF)>();
+    }
+    if (s < nstep) mma(fa0, fb0);
+  };
+
+  // the next block's rows are in flight during this block's MFMAs (DEPTH 1), or the next two blocks'
+  // (DEPTH 2: two register sets, so a load has two blocks' time to arrive)
   if (b0 < b1) {
-    load(b0);
-    store();
+    load(b0, xa, da);
+    store(xa, da);
   }
+  if (DEPTH == 2 && b0 + 1 < b1) load(b0 + 1, xb, db);
   __syncthreads();
-  for (int b = b0; b < b1; ++b) {
-    const bool more = b + 1 < b1;
-    if (more) load(b + 1);
-    __builtin_amdgcn_sched_barrier(0);  // keep the loads at the top: their latency hides under the MFMAs
-    int row[2] = {row0[0], row0[1]}, col[2] = {col0[0], col0[1]};
-    for (int s = 0; s < nstep; ++s) {
-      int aa[2], bb[2][TR];
-#pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        const bool ok = row[r] < kR;  // a partial last step reads zero dY rows (and finite input)
-        aa[r] = (ok ? DB + (row[r] * W + col[r]) * kSA : ZB) + wm * CW * 2 + pc * 8;
-        const int base = (ok ? (row[r] * P + col[r]) * G::kSB : 0) + bwave + pc * 8;
-#pragma unroll
-        for (int d = 0; d < TR; ++d) bb[r][d] = base + d * P * G::kSB;
-        col[r] += 32;
-        while (col[r] >= W) {
-          col[r] -= W;
-          ++row[r];
-        }
+  if constexpr (DEPTH == 1) {
+    for (int b = b0; b < b1; ++b) {
+      const bool more = b + 1 < b1;
+      if (more) load(b + 1, xa, da);
+      __builtin_amdgcn_sched_barrier(0);  // keep the loads at the top: their latency hides under the MFMAs
+      compute();
+      if (more) {
+        __syncthreads();  // every wave is done reading this block
+        store(xa, da);
       }
-      bf16x8 fa[FI], fb[NF];
-#pragma unroll
-      for (int i = 0; i < FI; ++i) fa[i] = join(tr_read(lds, aa[0] + i * 32), tr_read(lds, aa[1] + i * 32));
-#pragma unroll
-      for (int f = 0; f < NF; ++f) {
-        const int tl = f / JB, j = f % JB;
-        const int off = (tl % 3) * G::kSB + j * 128;
-        fb[f] = join(tr_read(lds, bb[0][tl / 3] + off), tr_read(lds, bb[1][tl / 3] + off));
+      __syncthreads();
+    }
+  } else {
+    for (int b = b0; b < b1; b += 2) {
+      if (b + 2 < b1) load(b + 2, xa, da);  // set b holds block b + 1
+      __builtin_amdgcn_sched_barrier(0);
+      compute();
+      if (b + 1 < b1) {
+        __syncthreads();
+        store(xb, db);
       }
-#pragma unroll
-      for (int i = 0; i < FI; ++i)
-#pragma unroll
-        for (int f = 0; f < NF; ++f)
-          acc[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[f], acc[i][f], 0, 0, 0);
+      __syncthreads();
+      if (b + 1 >= b1) break;
+      if (b + 3 < b1) load(b + 3, xb, db);  // set a holds block b + 2
+      __builtin_amdgcn_sched_barrier(0);
+      compute();
+      if (b + 2 < b1) {
+        __syncthreads();
+        store(xa, da);
+      }
+      __syncthreads();
     }
-    if (more) {
-      __syncthreads();  // every wave is done reading this block
-      store();
-    }
-    __syncthreads();
   }
 
   // ---- fp32 partials: acc[i][f][r] = dW[co0 + wm CW + 16 i + 4 g + r][(t0 + tl) C + 16 (wn + 4 j) + lane % 16]
   float* out = p.ws + static_cast<int64_t>(split) * CO * 9 * C;
+#if W3N_DIAG_NOSTORE  // diagnostics: only split 0 stores its partials (the partial traffic's price)
+  if (split != 0) return;
+#endif
 #pragma unroll
   for (int i = 0; i < FI; ++i)
 #pragma unroll
@@ -258,9 +333,9 @@ __global__ __launch_bounds__(256 * NWM, 1) void wgrad3x3n_kernel(W3Args p) {
     }
 }
 
-template <int C, int TG, int NWM>
+template <int C, int TG, int NWM, int DEPTH>
 void launch3(const W3Args& a, int splits, hipStream_t s) {
-  wgrad3x3n_kernel<C, TG, NWM><<<splits * a.groups, 256 * NWM, 0, s>>>(a);
+  wgrad3x3n_kernel<C, TG, NWM, DEPTH><<<splits * a.groups, 256 * NWM, 0, s>>>(a);
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
 
@@ -303,11 +378,13 @@ void wgrad3x3n(const void* dy, const void* x, float* ws, int64_t N, int H, int W
   const int sp = wgrad3x3n_splits(N, H, splits);
   a.per_split = (a.nblocks + sp - 1) / sp;
   a.groups = wgrad3x3n_groups(C, Cout, variant);
-  const bool w8 = variant & 1;
+  const bool w8 = variant & 1, d2 = variant & 2;
   if (C == 64) {
-    if (w8) launch3<64, 9, 2>(a, sp, stream); else launch3<64, 9, 1>(a, sp, stream);
+    if (w8) launch3<64, 9, 2, 1>(a, sp, stream);  // (8 waves with two register sets spill)
+    else { if (d2) launch3<64, 9, 1, 2>(a, sp, stream); else launch3<64, 9, 1, 1>(a, sp, stream); }
   } else {
-    if (w8) launch3<128, 3, 2>(a, sp, stream); else launch3<128, 3, 1>(a, sp, stream);
+    if (w8) launch3<128, 3, 2, 1>(a, sp, stream);
+    else { if (d2) launch3<128, 3, 1, 2>(a, sp, stream); else launch3<128, 3, 1, 1>(a, sp, stream); }
   }
 }
 

@@ -35,8 +35,9 @@ WGRAD = "auto"
 FWD_ENGINES = (0, 8, 7)
 # our weight-gradient kernel configurations tried by the autotune: (variant, target workgroups); s44 sweep
 _WG_CONFIGS = ((2, 512), (2, 768), (2, 1024), (2, 384))
-# the narrow 3x3 weight-gradient kernel (wgrad3x3n.hip) configurations: (variant, target workgroups)
-_W3N_CONFIGS = ((1, 256), (1, 512), (0, 256), (0, 512))
+# the narrow 3x3 weight-gradient kernel (wgrad3x3n.hip) configurations: (variant, target workgroups);
+# variant bit 0: 8 waves (else 4), bit 1 (4 waves only): the next two blocks in flight (else one)
+_W3N_CONFIGS = ((1, 256), (2, 256), (0, 256), (1, 512))
 # the statistics pass a MIOpen forward then needs is priced at one read of the output at this rate
 _STATS_PASS_BPS = 5e12
 

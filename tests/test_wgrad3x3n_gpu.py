@@ -30,7 +30,7 @@ def _ref(x, dy, co):
 
 
 @pytest.mark.parametrize("N,C,CO,H,W", SHAPES)
-@pytest.mark.parametrize("cfg", [(1, 256), (0, 256), (1, 512), (0, 7)])
+@pytest.mark.parametrize("cfg", [(1, 256), (0, 256), (1, 512), (0, 7), (2, 256), (2, 7), (2, 5), (1, 5)])
 def test_wgrad3x3n_matches_fp32(gpu_ext, N, C, CO, H, W, cfg):
     from fluxmpi_amd.ops import gemm as G
     torch.manual_seed(0)
