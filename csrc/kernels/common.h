@@ -123,6 +123,20 @@ __device__ __forceinline__ float wave_sum_dpp(float v) {
           __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48)));
 }
 
+// Scheduling pattern for a software-pipelined MFMA block: MFMA i is followed by
+// floor((i + 1) NR / NM) - floor(i NR / NM) of the next k-step's DS reads, so the reads stream in
+// under the matrix work (and fewer than lgkmcnt's 16 are ever outstanding) instead of following it
+// in a burst. Call right after the reads and MFMAs it orders, in the same basic block.
+template <int I, int NM, int NR>
+__device__ __forceinline__ void interleave_mfma_ds() {
+  if constexpr (I < NM) {
+    constexpr int nr = (I + 1) * NR / NM - I * NR / NM;
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    if constexpr (nr > 0) __builtin_amdgcn_sched_group_barrier(0x100, nr, 0);
+    interleave_mfma_ds<I + 1, NM, NR>();
+  }
+}
+
 // 8 elements per lane: 16 B for 2-byte types, 2 x 16 B for fp32, 4 x 16 B for fp64.
 template <typename T> struct Vec8 {
   T v[8];

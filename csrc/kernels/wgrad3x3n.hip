@@ -76,17 +76,6 @@ __device__ __forceinline__ bf16x8 join(short4v lo, short4v hi) {
   return out;
 }
 
-// scheduling pattern for one k-step: MFMA i is followed by DS reads floor((i+1) NR / NM) - floor(i NR / NM)
-template <int I, int NM, int NR>
-__device__ __forceinline__ void interleave_mfma_ds() {
-  if constexpr (I < NM) {
-    constexpr int nr = (I + 1) * NR / NM - I * NR / NM;
-    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-    if constexpr (nr > 0) __builtin_amdgcn_sched_group_barrier(0x100, nr, 0);
-    interleave_mfma_ds<I + 1, NM, NR>();
-  }
-}
-
 template <int C, int TG, int NWM, int DEPTH>
 __global__ __launch_bounds__(256 * NWM, 1) void wgrad3x3n_kernel(W3Args p) {
   using G = Geo3<C>;
