@@ -273,13 +273,15 @@ void transpose_bf16(const void* src, void* dst, int64_t rows, int64_t cols, int6
 int anderson_gram_chunks(int64_t bsz, int64_t d);
 // G (nullable): stored G = F - X rows (same layout); rows with their bit set in `fresh` are
 // recomputed from F - X and written to G, the others are read from G.
-// F: fp32 or bf16 (f_dtype), same element layout as X.
-void anderson_gram(const float* X, const void* F, int f_dtype, float* G, unsigned fresh, float* partials, int64_t bsz,
-                   int64_t d, int64_t row_stride, int64_t batch_stride, int n, int last, int chunks, hipStream_t stream);
+// F: fp32 or bf16 (f_dtype), same element layout as X; X and G: h_dtype (fp32 or bf16).
+void anderson_gram(const void* X, const void* F, int f_dtype, void* G, unsigned fresh, float* partials, int64_t bsz,
+                   int64_t d, int64_t row_stride, int64_t batch_stride, int n, int last, int chunks, hipStream_t stream,
+                   int h_dtype = 7);
 // X[b, slot] = beta * sum_i alpha[b][i] F[b, i] + (1 - beta) * sum_i alpha[b][i] X[b, i] (i < n);
 // z (nullable, [bsz][d], dtype z_dtype): the new iterate cast to the model dtype.
-void anderson_mix(float* X, const void* F, int f_dtype, const float* alpha, void* z, int z_dtype, int64_t bsz,
-                  int64_t d, int64_t row_stride, int64_t batch_stride, int n, int slot, float beta, hipStream_t stream);
+void anderson_mix(void* X, const void* F, int f_dtype, const float* alpha, void* z, int z_dtype, int64_t bsz,
+                  int64_t d, int64_t row_stride, int64_t batch_stride, int n, int slot, float beta, hipStream_t stream,
+                  int h_dtype = 7);
 // anderson_solve: from anderson_gram's partials, alpha[b][0..n) of the regularised Anderson system
 // [[0, 1^T], [1, G G^T + lam I]] a = e_0 (a[1..n]) per batch element (bsz <= 1024, one launch),
 // and (res nullable) the relative residual of row `last` into res[0].

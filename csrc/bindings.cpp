@@ -195,10 +195,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("anderson_gram_chunks", &anderson_gram_chunks);
   m.def("anderson_gram", [](uintptr_t X, uintptr_t F, int fdt, uintptr_t G, unsigned fresh, uintptr_t part,
                             int64_t bsz, int64_t d, int64_t rs, int64_t bs, int n, int last, int chunks,
-                            uintptr_t stream) {
-    anderson_gram(reinterpret_cast<const float*>(X), reinterpret_cast<const void*>(F), fdt, reinterpret_cast<float*>(G),
-                  fresh, reinterpret_cast<float*>(part), bsz, d, rs, bs, n, last, chunks, S(stream));
-  });
+                            uintptr_t stream, int hdt) {
+    anderson_gram(reinterpret_cast<const void*>(X), reinterpret_cast<const void*>(F), fdt, reinterpret_cast<void*>(G),
+                  fresh, reinterpret_cast<float*>(part), bsz, d, rs, bs, n, last, chunks, S(stream), hdt);
+  }, py::arg("X"), py::arg("F"), py::arg("fdt"), py::arg("G"), py::arg("fresh"), py::arg("part"), py::arg("bsz"),
+     py::arg("d"), py::arg("rs"), py::arg("bs"), py::arg("n"), py::arg("last"), py::arg("chunks"), py::arg("stream"),
+     py::arg("hdt") = 7);
   m.def("adjoint_step_blocks", &adjoint_step_blocks);
   m.def("adjoint_step", [](uintptr_t vjp, uintptr_t grad, uintptr_t u, uintptr_t u_new, uintptr_t part, int blocks,
                            int64_t n, int dtype, uintptr_t stream) {
@@ -212,10 +214,12 @@ PYBIND11_MODULE(_C, m) {
                    reinterpret_cast<float*>(res), S(stream));
   });
   m.def("anderson_mix", [](uintptr_t X, uintptr_t F, int fdt, uintptr_t alpha, uintptr_t z, int zdt, int64_t bsz,
-                           int64_t d, int64_t rs, int64_t bs, int n, int slot, float beta, uintptr_t stream) {
-    anderson_mix(reinterpret_cast<float*>(X), reinterpret_cast<const void*>(F), fdt, reinterpret_cast<const float*>(alpha),
-                 reinterpret_cast<void*>(z), zdt, bsz, d, rs, bs, n, slot, beta, S(stream));
-  });
+                           int64_t d, int64_t rs, int64_t bs, int n, int slot, float beta, uintptr_t stream, int hdt) {
+    anderson_mix(reinterpret_cast<void*>(X), reinterpret_cast<const void*>(F), fdt, reinterpret_cast<const float*>(alpha),
+                 reinterpret_cast<void*>(z), zdt, bsz, d, rs, bs, n, slot, beta, S(stream), hdt);
+  }, py::arg("X"), py::arg("F"), py::arg("fdt"), py::arg("alpha"), py::arg("z"), py::arg("zdt"), py::arg("bsz"),
+     py::arg("d"), py::arg("rs"), py::arg("bs"), py::arg("n"), py::arg("slot"), py::arg("beta"), py::arg("stream"),
+     py::arg("hdt") = 7);
 
   // ---- fused NHWC GroupNorm ------------------------------------------------------
   m.def("groupnorm_nhwc_fwd", [](uintptr_t x, uintptr_t a, uintptr_t h, uintptr_t y, uintptr_t w, uintptr_t b,

@@ -50,6 +50,19 @@ __device__ __forceinline__ float4 ldf4(const FT* __restrict__ p, int64_t e) {
   }
 }
 
+// 4 elements to a history row (fp32, or bf16 rounded to nearest even)
+template <typename HT>
+__device__ __forceinline__ void st4(HT* __restrict__ p, int64_t e, const float4& v) {
+  if constexpr (sizeof(HT) == 4) {
+    *reinterpret_cast<float4*>(p + e) = v;
+  } else {
+    const bf16 h[4] = {static_cast<bf16>(v.x), static_cast<bf16>(v.y), static_cast<bf16>(v.z), static_cast<bf16>(v.w)};
+    uint2 u;
+    __builtin_memcpy(&u, h, 8);
+    *reinterpret_cast<uint2*>(p + e) = u;
+  }
+}
+
 // grid (chunks, bsz). part[b][chunk][kOut]
 // ONE = false: every row's G = F - X is formed from the history (and written to G when G is
 // given). ONE = true (the steady state): only row `fr` is new; it is formed from F - X and
@@ -57,16 +70,16 @@ __device__ __forceinline__ float4 ldf4(const FT* __restrict__ p, int64_t e) {
 // wave-uniformly chosen address (a load under a branch is waited for at the join: N serial
 // memory latencies per iteration otherwise): with ONE, row fr's G load re-reads its X line (a
 // cache hit) instead of a stale G line. |F[last]|^2 needs last == fr with ONE (host-checked).
-template <int N, bool ONE, typename FT>
-__global__ __launch_bounds__(kThreads) void gram_kernel(const float* __restrict__ X, const FT* __restrict__ F,
-                                                        float* __restrict__ G, float* __restrict__ part, int64_t d4,
+template <int N, bool ONE, typename FT, typename HT>
+__global__ __launch_bounds__(kThreads) void gram_kernel(const HT* __restrict__ X, const FT* __restrict__ F,
+                                                        HT* __restrict__ G, float* __restrict__ part, int64_t d4,
                                                         int64_t row_stride, int64_t batch_stride, int64_t chunk4,
                                                         int last, int fr) {
   const int b = blockIdx.y;
   const int c = blockIdx.x;
-  const float* xb = X + b * batch_stride;
+  const HT* xb = X + b * batch_stride;
   const FT* fb = F + b * batch_stride;
-  float* gb = G != nullptr ? G + b * batch_stride : nullptr;
+  HT* gb = G != nullptr ? G + b * batch_stride : nullptr;
   float acc[kPairs];
   float fn = 0.f;
 #pragma unroll
@@ -79,26 +92,26 @@ __global__ __launch_bounds__(kThreads) void gram_kernel(const float* __restrict_
     float4 g[N];
     if constexpr (ONE) {
       const float4 f = ldf4(fb, fr * row_stride + e);
-      const float4 x = *reinterpret_cast<const float4*>(xb + fr * row_stride + e);
+      const float4 x = ldf4(xb, fr * row_stride + e);
 #pragma unroll
-      for (int i = 0; i < N; ++i) g[i] = *reinterpret_cast<const float4*>((i == fr ? xb : gb) + i * row_stride + e);
+      for (int i = 0; i < N; ++i) g[i] = ldf4((i == fr ? xb : static_cast<const HT*>(gb)), i * row_stride + e);
       const float4 gn = make_float4(f.x - x.x, f.y - x.y, f.z - x.z, f.w - x.w);
 #pragma unroll
       for (int i = 0; i < N; ++i)
         if (i == fr) g[i] = gn;
-      *reinterpret_cast<float4*>(gb + fr * row_stride + e) = gn;
+      st4(gb, fr * row_stride + e, gn);
       fn += dot4(f, f);
     } else {
       float4 f[N], x[N];
 #pragma unroll
       for (int i = 0; i < N; ++i) {
         f[i] = ldf4(fb, i * row_stride + e);
-        x[i] = *reinterpret_cast<const float4*>(xb + i * row_stride + e);
+        x[i] = ldf4(xb, i * row_stride + e);
       }
 #pragma unroll
       for (int i = 0; i < N; ++i) {
         g[i] = make_float4(f[i].x - x[i].x, f[i].y - x[i].y, f[i].z - x[i].z, f[i].w - x[i].w);
-        if (gb != nullptr) *reinterpret_cast<float4*>(gb + i * row_stride + e) = g[i];
+        if (gb != nullptr) st4(gb, i * row_stride + e, g[i]);
         if (i == last) fn += dot4(f[i], f[i]);
       }
     }
@@ -135,15 +148,15 @@ __global__ __launch_bounds__(kThreads) void gram_kernel(const float* __restrict_
 }
 
 // grid (ceil(d4 / kThreads), bsz): X[b, slot] = beta * sum_i a_i F[b,i] + (1-beta) * sum_i a_i X[b,i]
-template <int N, bool MIXX, typename Z, typename FT>
-__global__ __launch_bounds__(kThreads) void mix_kernel(float* __restrict__ X, const FT* __restrict__ F,
+template <int N, bool MIXX, typename Z, typename FT, typename HT>
+__global__ __launch_bounds__(kThreads) void mix_kernel(HT* __restrict__ X, const FT* __restrict__ F,
                                                        const float* __restrict__ alpha, Z* __restrict__ z, int64_t d4,
                                                        int64_t row_stride, int64_t batch_stride, int slot, float beta) {
   const int b = blockIdx.y;
   const int64_t v = static_cast<int64_t>(blockIdx.x) * kThreads + threadIdx.x;
   if (v >= d4) return;
   const int64_t e = 4 * v;
-  float* xb = X + b * batch_stride;
+  HT* xb = X + b * batch_stride;
   const FT* fb = F + b * batch_stride;
   float a[N];
 #pragma unroll
@@ -156,7 +169,7 @@ __global__ __launch_bounds__(kThreads) void mix_kernel(float* __restrict__ X, co
   for (int i = 0; i < N; ++i) {
     sf.x += a[i] * fv[i].x; sf.y += a[i] * fv[i].y; sf.z += a[i] * fv[i].z; sf.w += a[i] * fv[i].w;
     if (MIXX) {
-      const float4 x = *reinterpret_cast<const float4*>(xb + i * row_stride + e);
+      const float4 x = ldf4(static_cast<const HT*>(xb), i * row_stride + e);
       sx.x += a[i] * x.x; sx.y += a[i] * x.y; sx.z += a[i] * x.z; sx.w += a[i] * x.w;
     }
   }
@@ -165,7 +178,7 @@ __global__ __launch_bounds__(kThreads) void mix_kernel(float* __restrict__ X, co
     const float c = 1.f - beta;
     o = make_float4(beta * sf.x + c * sx.x, beta * sf.y + c * sx.y, beta * sf.z + c * sx.z, beta * sf.w + c * sx.w);
   }
-  *reinterpret_cast<float4*>(xb + slot * row_stride + e) = o;
+  st4(xb, slot * row_stride + e, o);
   if (z != nullptr) {
     Z* zp = z + static_cast<int64_t>(b) * d4 * 4 + e;
     zp[0] = static_cast<Z>(o.x);
@@ -321,7 +334,7 @@ __global__ __launch_bounds__(kThreads) void adjoint_step_kernel(const T* __restr
   }
 }
 
-// X (fp32) and F (fp32 or bf16) share one element layout: [bsz][rows of row_stride][d]
+// X / G (fp32 or bf16) and F (fp32 or bf16) share one element layout: [bsz][rows of row_stride][d]
 void check_layout(const void* X, const void* F, int64_t d, int64_t row_stride, int64_t batch_stride, int n) {
   if (n < 1 || n > kMaxRows) throw std::runtime_error("anderson: need 1 <= n <= 8 (got " + std::to_string(n) + ")");
   if (d % 4 != 0 || row_stride % 4 != 0 || batch_stride % 4 != 0 || row_stride < d)
@@ -342,30 +355,20 @@ int anderson_gram_chunks(int64_t bsz, int64_t d) {
   return static_cast<int>(chunks);
 }
 
-template <int N, bool ONE>
-void gram_launch(const float* X, const void* F, int fdt, float* G, float* part, dim3 grid, int64_t d4, int64_t rs,
+template <int N, bool ONE, typename HT>
+void gram_launch(const HT* X, const void* F, int fdt, HT* G, float* part, dim3 grid, int64_t d4, int64_t rs,
                  int64_t bs, int64_t chunk4, int last, int fr, hipStream_t s) {
   if (fdt == kBF16)
-    gram_kernel<N, ONE, bf16><<<grid, kThreads, 0, s>>>(X, static_cast<const bf16*>(F), G, part, d4, rs, bs, chunk4,
-                                                        last, fr);
+    gram_kernel<N, ONE, bf16, HT><<<grid, kThreads, 0, s>>>(X, static_cast<const bf16*>(F), G, part, d4, rs, bs, chunk4,
+                                                            last, fr);
   else
-    gram_kernel<N, ONE, float><<<grid, kThreads, 0, s>>>(X, static_cast<const float*>(F), G, part, d4, rs, bs, chunk4,
-                                                         last, fr);
+    gram_kernel<N, ONE, float, HT><<<grid, kThreads, 0, s>>>(X, static_cast<const float*>(F), G, part, d4, rs, bs,
+                                                             chunk4, last, fr);
 }
 
-void anderson_gram(const float* X, const void* F, int f_dtype, float* G, unsigned fresh, float* partials, int64_t bsz,
-                   int64_t d, int64_t row_stride, int64_t batch_stride, int n, int last, int chunks, hipStream_t stream) {
-  check_layout(X, F, d, row_stride, batch_stride, n);
-  if (f_dtype != kF32 && f_dtype != kBF16) throw std::runtime_error("anderson_gram: F must be fp32 or bf16");
-  if (G != nullptr && (reinterpret_cast<uintptr_t>(G) & 15u) != 0)
-    throw std::runtime_error("anderson_gram: G must be 16-byte aligned");
-  if (last < 0 || last >= n) throw std::runtime_error("anderson_gram: last row out of range");
-  if (bsz > 65535) throw std::runtime_error("anderson_gram: bsz > 65535");
-  const int64_t d4 = d / 4;
-  const int64_t chunk4 = (d4 + chunks - 1) / chunks;
-  dim3 grid(chunks, static_cast<unsigned>(bsz));
-  // one new row (the steady state): the others come from G; otherwise every row from F - X
-  const bool one = G != nullptr && fresh == (1u << last);
+template <typename HT>
+void gram_dispatch(const HT* X, const void* F, int f_dtype, HT* G, bool one, float* partials, dim3 grid, int64_t d4,
+                   int64_t row_stride, int64_t batch_stride, int64_t chunk4, int n, int last, hipStream_t stream) {
 #define GRAM_CASE(NN)                                                                                              \
   case NN:                                                                                                         \
     if (one) gram_launch<NN, true>(X, F, f_dtype, G, partials, grid, d4, row_stride, batch_stride, chunk4, last,  \
@@ -377,32 +380,48 @@ void anderson_gram(const float* X, const void* F, int f_dtype, float* G, unsigne
     GRAM_CASE(1) GRAM_CASE(2) GRAM_CASE(3) GRAM_CASE(4) GRAM_CASE(5) GRAM_CASE(6) GRAM_CASE(7) GRAM_CASE(8)
   }
 #undef GRAM_CASE
+}
+
+void anderson_gram(const void* X, const void* F, int f_dtype, void* G, unsigned fresh, float* partials, int64_t bsz,
+                   int64_t d, int64_t row_stride, int64_t batch_stride, int n, int last, int chunks, hipStream_t stream,
+                   int h_dtype) {
+  check_layout(X, F, d, row_stride, batch_stride, n);
+  if (f_dtype != kF32 && f_dtype != kBF16) throw std::runtime_error("anderson_gram: F must be fp32 or bf16");
+  if (h_dtype != kF32 && h_dtype != kBF16) throw std::runtime_error("anderson_gram: X / G must be fp32 or bf16");
+  if (G != nullptr && (reinterpret_cast<uintptr_t>(G) & 15u) != 0)
+    throw std::runtime_error("anderson_gram: G must be 16-byte aligned");
+  if (last < 0 || last >= n) throw std::runtime_error("anderson_gram: last row out of range");
+  if (bsz > 65535) throw std::runtime_error("anderson_gram: bsz > 65535");
+  const int64_t d4 = d / 4;
+  const int64_t chunk4 = (d4 + chunks - 1) / chunks;
+  dim3 grid(chunks, static_cast<unsigned>(bsz));
+  // one new row (the steady state): the others come from G; otherwise every row from F - X
+  const bool one = G != nullptr && fresh == (1u << last);
+  if (h_dtype == kBF16)
+    gram_dispatch(static_cast<const bf16*>(X), F, f_dtype, static_cast<bf16*>(G), one, partials, grid, d4, row_stride,
+                  batch_stride, chunk4, n, last, stream);
+  else
+    gram_dispatch(static_cast<const float*>(X), F, f_dtype, static_cast<float*>(G), one, partials, grid, d4,
+                  row_stride, batch_stride, chunk4, n, last, stream);
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
 
-template <int N, bool MIXX, typename FT>
-void mix_launch(float* X, const FT* F, const float* alpha, void* z, int zdt, int64_t bsz, int64_t d4, int64_t rs,
+template <int N, bool MIXX, typename FT, typename HT>
+void mix_launch(HT* X, const FT* F, const float* alpha, void* z, int zdt, int64_t bsz, int64_t d4, int64_t rs,
                 int64_t bs, int slot, float beta, hipStream_t s) {
   dim3 grid(static_cast<unsigned>((d4 + kThreads - 1) / kThreads), static_cast<unsigned>(bsz));
   switch (zdt) {
-    case kBF16: mix_kernel<N, MIXX, bf16, FT><<<grid, kThreads, 0, s>>>(X, F, alpha, static_cast<bf16*>(z), d4, rs, bs, slot, beta); break;
-    case kF16: mix_kernel<N, MIXX, f16, FT><<<grid, kThreads, 0, s>>>(X, F, alpha, static_cast<f16*>(z), d4, rs, bs, slot, beta); break;
-    case kF32: mix_kernel<N, MIXX, float, FT><<<grid, kThreads, 0, s>>>(X, F, alpha, static_cast<float*>(z), d4, rs, bs, slot, beta); break;
+    case kBF16: mix_kernel<N, MIXX, bf16, FT, HT><<<grid, kThreads, 0, s>>>(X, F, alpha, static_cast<bf16*>(z), d4, rs, bs, slot, beta); break;
+    case kF16: mix_kernel<N, MIXX, f16, FT, HT><<<grid, kThreads, 0, s>>>(X, F, alpha, static_cast<f16*>(z), d4, rs, bs, slot, beta); break;
+    case kF32: mix_kernel<N, MIXX, float, FT, HT><<<grid, kThreads, 0, s>>>(X, F, alpha, static_cast<float*>(z), d4, rs, bs, slot, beta); break;
     default: throw std::runtime_error("anderson_mix: unsupported z dtype");
   }
 }
 
-void anderson_mix(float* X, const void* F, int f_dtype, const float* alpha, void* z, int z_dtype, int64_t bsz,
-                  int64_t d, int64_t row_stride, int64_t batch_stride, int n, int slot, float beta, hipStream_t stream) {
-  check_layout(X, F, d, row_stride, batch_stride, n);
-  if (f_dtype != kF32 && f_dtype != kBF16) throw std::runtime_error("anderson_mix: F must be fp32 or bf16");
-  if (slot < 0 || slot * row_stride + d > batch_stride) throw std::runtime_error("anderson_mix: slot out of range");
-  if (bsz > 65535) throw std::runtime_error("anderson_mix: bsz > 65535");
-  if (z != nullptr && (reinterpret_cast<uintptr_t>(z) & 7u) != 0)
-    throw std::runtime_error("anderson_mix: z must be 8-byte aligned");
-  const int64_t d4 = d / 4;
+template <typename HT>
+void mix_dispatch(HT* X, const void* F, int f_dtype, const float* alpha, void* z, int zdt, int64_t bsz, int64_t d4,
+                  int64_t row_stride, int64_t batch_stride, int n, int slot, float beta, hipStream_t stream) {
   const bool mixx = beta != 1.f;
-  const int zdt = z != nullptr ? z_dtype : kF32;
   const bf16* fh = static_cast<const bf16*>(F);
   const float* ff = static_cast<const float*>(F);
 #define MIX_CASE(NN)                                                                                              \
@@ -419,6 +438,26 @@ void anderson_mix(float* X, const void* F, int f_dtype, const float* alpha, void
     MIX_CASE(1) MIX_CASE(2) MIX_CASE(3) MIX_CASE(4) MIX_CASE(5) MIX_CASE(6) MIX_CASE(7) MIX_CASE(8)
   }
 #undef MIX_CASE
+}
+
+void anderson_mix(void* X, const void* F, int f_dtype, const float* alpha, void* z, int z_dtype, int64_t bsz,
+                  int64_t d, int64_t row_stride, int64_t batch_stride, int n, int slot, float beta, hipStream_t stream,
+                  int h_dtype) {
+  check_layout(X, F, d, row_stride, batch_stride, n);
+  if (f_dtype != kF32 && f_dtype != kBF16) throw std::runtime_error("anderson_mix: F must be fp32 or bf16");
+  if (h_dtype != kF32 && h_dtype != kBF16) throw std::runtime_error("anderson_mix: X must be fp32 or bf16");
+  if (slot < 0 || slot * row_stride + d > batch_stride) throw std::runtime_error("anderson_mix: slot out of range");
+  if (bsz > 65535) throw std::runtime_error("anderson_mix: bsz > 65535");
+  if (z != nullptr && (reinterpret_cast<uintptr_t>(z) & 7u) != 0)
+    throw std::runtime_error("anderson_mix: z must be 8-byte aligned");
+  const int64_t d4 = d / 4;
+  const int zdt = z != nullptr ? z_dtype : kF32;
+  if (h_dtype == kBF16)
+    mix_dispatch(static_cast<bf16*>(X), F, f_dtype, alpha, z, zdt, bsz, d4, row_stride, batch_stride, n, slot, beta,
+                 stream);
+  else
+    mix_dispatch(static_cast<float*>(X), F, f_dtype, alpha, z, zdt, bsz, d4, row_stride, batch_stride, n, slot, beta,
+                 stream);
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
 

@@ -93,6 +93,19 @@ def _f_hist_dtype(dt: torch.dtype, like: torch.Tensor) -> torch.dtype:
     return torch.bfloat16 if (dt == torch.bfloat16 and like.is_cuda) else torch.float32
 
 
+# FLUXMPI_DEQ_HIST: dtype of the iterate (X) and difference (G = F - X) histories of a bf16 model on
+# the GPU — "bf16" (default: the iterates the model evaluates are bf16-rounded anyway; the Gram
+# sums and the (n+1)^2 solve stay fp32; residual-vs-iteration curves of both models equal to the
+# fp32 histories', profiles/rd5x_deq_hist_residual.jsonl; the Gram pass reads 14 instead of 26
+# bytes per element) or "fp32"
+HIST = os.environ.get("FLUXMPI_DEQ_HIST", "bf16")
+
+
+def _x_hist_dtype(dt: torch.dtype, like: torch.Tensor) -> torch.dtype:
+    """dtype of the Anderson X and G histories (see :data:`HIST`)."""
+    return torch.bfloat16 if (HIST == "bf16" and dt == torch.bfloat16 and like.is_cuda) else torch.float32
+
+
 def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0, check_lag: int | None = None,
              graphs: "SolverGraphs | None" = None):
     """Anderson acceleration for ``x = f(x)`` over batch-flattened tensors. Returns (x, iters, rel_residual).
@@ -116,14 +129,14 @@ def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0, check_lag: i
     bsz = x0.shape[0]
     shape, dt = x0.shape, x0.dtype
     d = x0[0].numel()
-    # the iterates X, the differences G = F - X and the small (m+1)^2 systems are fp32 whatever
-    # the model dtype (bf16 has no batched LU, and 8-bit mantissas in X or G would stall the
-    # extrapolation); the images F are f's outputs, so in a bf16 model they are bf16 values and
-    # their history is kept in bf16 on the GPU (exact; the mix reads n rows of it per iteration)
+    # the small (m+1)^2 systems and every Gram sum are fp32 whatever the model dtype (bf16 has no
+    # batched LU); the images F are f's outputs, so in a bf16 model they are bf16 values and their
+    # history is kept in bf16 on the GPU (exact); the iterates X and the differences G = F - X are
+    # bf16 there too (:data:`HIST`: the model only ever evaluates bf16-rounded iterates)
     if graphs is not None:
         X, Fv, Gs = graphs.history(m)
     else:
-        X = torch.zeros(bsz, m, d, dtype=torch.float32, device=x0.device)
+        X = torch.zeros(bsz, m, d, dtype=_x_hist_dtype(dt, x0), device=x0.device)
         Fv = torch.zeros_like(X, dtype=_f_hist_dtype(dt, x0))
         Gs = torch.zeros_like(X)
 
@@ -202,7 +215,7 @@ def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0, check_lag: i
     if not converged:
         k = max(k - 1, 1)  # the last completed iteration
         s = k % m
-        res_t = (Fv[:, s].float() - X[:, s]).norm() / (1e-5 + Fv[:, s].float().norm())
+        res_t = (Fv[:, s].float() - X[:, s].float()).norm() / (1e-5 + Fv[:, s].float().norm())
         res = res_t if flags is not None else float(res_t)
     return unflat(X[:, k % m].contiguous()).to(dt), k, res
 
@@ -277,7 +290,7 @@ class SolverGraphs:
     def history(self, m: int):
         bsz, d = self.x.shape[0], self.x[0].numel()
         if self._hist is None or self._hist[0].shape[1] != m:
-            X = torch.zeros(bsz, m, d, dtype=torch.float32, device=self.x.device)
+            X = torch.zeros(bsz, m, d, dtype=_x_hist_dtype(self.x.dtype, self.x), device=self.x.device)
             self._hist = (X, torch.zeros_like(X, dtype=_f_hist_dtype(self.x.dtype, self.x)), torch.zeros_like(X))
             self.g_fwd = None
         return self._hist

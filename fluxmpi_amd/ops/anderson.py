@@ -37,13 +37,14 @@ def _stream(t):
 def _native(X: torch.Tensor, F: torch.Tensor, n: int) -> bool:
     if not (X.is_cuda and F.is_cuda):
         return False
-    ok = (X.dtype == torch.float32 and F.dtype in (torch.float32, torch.bfloat16) and X.dim() == F.dim() == 3
+    ok = (X.dtype in (torch.float32, torch.bfloat16) and F.dtype in (torch.float32, torch.bfloat16)
+          and X.dim() == F.dim() == 3
           and X.shape == F.shape
           and X.stride() == F.stride() and X.stride(2) == 1 and X.shape[2] % 4 == 0 and X.stride(1) % 4 == 0
           and X.stride(0) % 4 == 0 and 1 <= n <= min(_MAX_ROWS, X.shape[1]) and X.shape[0] <= 65535
           and X.data_ptr() % 16 == 0 and F.data_ptr() % 16 == 0)
     if not ok:
-        raise ValueError("anderson ops: need an fp32 X and an fp32 / bf16 F history [bsz<=65535, m, d%4==0] with "
+        raise ValueError("anderson ops: need fp32 / bf16 X and F histories [bsz<=65535, m, d%4==0] with "
                          "matching strides, n<=8")
     return True
 
@@ -57,10 +58,10 @@ def gram(X: torch.Tensor, F: torch.Tensor, n: int, last: int, G: torch.Tensor | 
     if not _native(X, F, n):
         if G is not None:
             for i in fresh:
-                G[:, i] = F[:, i] - X[:, i]
-            Gn = G[:, :n]
+                G[:, i] = F[:, i].float() - X[:, i].float()
+            Gn = G[:, :n].float()
         else:
-            Gn = F[:, :n] - X[:, :n]
+            Gn = F[:, :n].float() - X[:, :n].float()
         return torch.bmm(Gn, Gn.transpose(1, 2)), F[:, last].float().pow(2).sum(1)
     C = _ext.get(required=True)
     bsz, _, d = X.shape
@@ -68,12 +69,12 @@ def gram(X: torch.Tensor, F: torch.Tensor, n: int, last: int, G: torch.Tensor | 
     part = torch.empty(bsz, chunks, 37, device=X.device, dtype=torch.float32)
     mask = 0
     if G is not None:
-        if G.shape != X.shape or G.stride() != X.stride() or G.dtype != torch.float32 or G.data_ptr() % 16:
+        if G.shape != X.shape or G.stride() != X.stride() or G.dtype != X.dtype or G.data_ptr() % 16:
             raise ValueError("anderson gram: G must match X's shape, strides and dtype")
         for i in fresh:
             mask |= 1 << int(i)
     C.anderson_gram(X.data_ptr(), F.data_ptr(), DTYPE_CODE[F.dtype], G.data_ptr() if G is not None else 0, mask,
-                    part.data_ptr(), bsz, d, X.stride(1), X.stride(0), n, last, chunks, _stream(X))
+                    part.data_ptr(), bsz, d, X.stride(1), X.stride(0), n, last, chunks, _stream(X), DTYPE_CODE[X.dtype])
     tot = part.sum(1)
     # one gather (cached symmetric index) instead of building the index and two scatters
     H = tot.index_select(1, _sym_index(n, X.device)).view(bsz, n, n)
@@ -101,14 +102,14 @@ def gram_solve(X: torch.Tensor, F: torch.Tensor, n: int, last: int, G: torch.Ten
     d = X.shape[2]
     chunks = C.anderson_gram_chunks(bsz, d)
     part = torch.empty(bsz, chunks, 37, device=X.device, dtype=torch.float32)
-    if G.shape != X.shape or G.stride() != X.stride() or G.dtype != torch.float32 or G.data_ptr() % 16:
+    if G.shape != X.shape or G.stride() != X.stride() or G.dtype != X.dtype or G.data_ptr() % 16:
         raise ValueError("anderson gram: G must match X's shape, strides and dtype")
     mask = 0
     for i in fresh:
         mask |= 1 << int(i)
     stream = _stream(X)
     C.anderson_gram(X.data_ptr(), F.data_ptr(), DTYPE_CODE[F.dtype], G.data_ptr(), mask, part.data_ptr(), bsz, d,
-                    X.stride(1), X.stride(0), n, last, chunks, stream)
+                    X.stride(1), X.stride(0), n, last, chunks, stream, DTYPE_CODE[X.dtype])
     alpha = torch.empty(bsz, n, device=X.device, dtype=torch.float32)
     res = torch.empty((), device=X.device, dtype=torch.float32) if want_res else None
     C.anderson_solve(part.data_ptr(), chunks, bsz, n, last, float(lam), alpha.data_ptr(),
@@ -126,9 +127,9 @@ def mix(X: torch.Tensor, F: torch.Tensor, alpha: torch.Tensor, slot: int, beta: 
     if not _native(X, F, n):
         new = beta * torch.bmm(alpha[:, None], F[:, :n].float())[:, 0]
         if beta != 1.0:
-            new = new + (1 - beta) * torch.bmm(alpha[:, None], X[:, :n])[:, 0]
+            new = new + (1 - beta) * torch.bmm(alpha[:, None], X[:, :n].float())[:, 0]
         X[:, slot] = new
-        return X[:, slot] if z_dtype in (None, torch.float32) else X[:, slot].to(z_dtype)
+        return X[:, slot] if z_dtype in (None, X.dtype) else new.to(z_dtype)
     C = _ext.get(required=True)
     bsz, _, d = X.shape
     a = alpha.float().contiguous()
@@ -137,7 +138,7 @@ def mix(X: torch.Tensor, F: torch.Tensor, alpha: torch.Tensor, slot: int, beta: 
         z = torch.empty(bsz, d, device=X.device, dtype=z_dtype)
     C.anderson_mix(X.data_ptr(), F.data_ptr(), DTYPE_CODE[F.dtype], a.data_ptr(), z.data_ptr() if z is not None else 0,
                    DTYPE_CODE[z_dtype] if z is not None else 7, bsz, d, X.stride(1), X.stride(0), n, slot, float(beta),
-                   _stream(X))
+                   _stream(X), DTYPE_CODE[X.dtype])
     return z if z is not None else X[:, slot]
 
 
