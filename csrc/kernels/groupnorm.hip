@@ -31,7 +31,12 @@ constexpr int kLdsBudget = 64 * 1024;  // dynamic LDS without a per-kernel attri
 constexpr int kMaxG = 64;
 // pixels per lane whose loads are issued together (one workgroup per sample: at one pixel per
 // iteration every pass was a chain of dependent memory round trips, ~2.6 TB/s on the DEQ cell)
-constexpr int kU = 4;
+// (GN_KU = 8 / 16, A/B builds only: equal or slower at the DEQ shapes, profiles/rd5y_bench_gn_ku.jsonl —
+// the forward is at ~4.4 TB/s of algorithmic traffic already)
+#ifndef GN_KU
+#define GN_KU 4
+#endif
+constexpr int kU = GN_KU;
 
 struct GnShape {
   int HW, C, G, CV, PL, T;  // CV = C/8 channel vectors per pixel, PL pixel lanes, T = PL*CV lanes
