@@ -254,8 +254,9 @@ void conv3x3n(const void* x, const void* w, void* y, float* stats, int64_t pixel
               int epi, hipStream_t stream);
 // Weight gradient of the narrow-channel 3x3 / stride 1 / pad 1 convolution (wgrad3x3n.hip): dy
 // [N][H][W][Cout], x [N][H][W][C] (C in {64, 128}); ws[split][Cout][9 C] fp32 partials (reduce with
-// gemm_splitk_reduce; the actual split count is wgrad3x3n_splits). variant bit 0: 8 waves (else 4).
-// A workgroup owns 64 Cout x all nine taps (C = 64) or x one filter row of three taps (C = 128).
+// gemm_splitk_reduce; the actual split count is wgrad3x3n_splits). variant bit 0: 8 waves (else 4),
+// bit 1: two register sets of prefetched rows (4 waves), bit 2 (C = 128): 128 Cout per workgroup.
+// A workgroup owns 64 / 128 Cout x all nine taps (C = 64) or x one filter row of three taps (C = 128).
 bool wgrad3x3n_supported(int64_t N, int H, int W, int C, int Cout);
 int wgrad3x3n_splits(int64_t N, int H, int splits);
 int wgrad3x3n_groups(int C, int Cout, int variant);

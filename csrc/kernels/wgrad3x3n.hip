@@ -18,7 +18,7 @@
 //   * the next block's rows are loaded into registers during this block's MFMAs (ds_write after a
 //     barrier: an LDS-DMA ring makes the waitcnt pass drain it in front of the reads, conv3x3n.hip);
 //     DEPTH 2 keeps the next two blocks in flight in two register sets.
-// The workgroup's output is 64 co x TG taps x C ci. Its 4 or 8 waves split the columns (and with 8
+// The workgroup's output is COB (64 / 128) co x TG taps x C ci. Its 4 or 8 waves split the columns (and with 8
 // the co rows in halves) and keep fp32 sums in registers across all blocks of their K-split;
 // partials [splits][Cout][9 C] go through the shared split-K reduce (gemm_splitk_reduce).
 // Reference: /root/reference has no kernels — this is the compute under the per-step gradient work
@@ -39,14 +39,15 @@ typedef short short4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) short4v lds_short4v;
 
 constexpr int kR = 4;       // image rows per block
-constexpr int kCOB = 64;    // output channels per workgroup
-constexpr int kSA = 160;    // dY slot stride (64 channels + 32 B): 40 banks
 constexpr uint32_t kOOB = 0x80000000u;  // a buffer offset past every operand: the load returns zeros
 
-template <int C> struct Geo3 {
+// COB: output channels per workgroup (64, or 128 for the 128-channel layers: half the input
+// re-reads of two 64-channel workgroups)
+template <int C, int COB> struct Geo3 {
   static constexpr int kW = C == 64 ? 56 : 28;            // widest supported image row
   static constexpr int kP = kW % 8 == 0 ? kW + 2 : kW + 8;  // its padded row pitch
   static constexpr int kSB = C * 2 + 32;                  // input slot stride: 40 / 72 banks
+  static constexpr int kSA = COB * 2 + 32;                // dY slot stride: 40 / 72 banks
   static constexpr int kXBytes = (kR + 2) * kP * kSB;
   static constexpr int kDBytes = kR * kW * kSA;
   static constexpr int kBytes = kXBytes + kDBytes + kSA;  // + one zero dY slot
@@ -62,7 +63,7 @@ struct W3Args {
   int H, W, CO;
   int nblocks;     // N * H / kR
   int per_split;   // blocks per K-split
-  int groups;      // (CO / 64) * (9 / TG) output blocks per split
+  int groups;      // (CO / COB) * (9 / TG) output blocks per split
 };
 
 __device__ __forceinline__ short4v tr_read(const char* lds, int byte) {
@@ -76,17 +77,19 @@ __device__ __forceinline__ bf16x8 join(short4v lo, short4v hi) {
   return out;
 }
 
-template <int C, int TG, int NWM, int DEPTH>
+template <int C, int TG, int NWM, int DEPTH, int COB>
 __global__ __launch_bounds__(256 * NWM, 1) void wgrad3x3n_kernel(W3Args p) {
-  using G = Geo3<C>;
+  using G = Geo3<C, COB>;
+  constexpr int kSA = G::kSA;
+  constexpr int DPP = COB / 8;               // 16-B dY pieces per pixel
   constexpr int NT = 256 * NWM;
-  constexpr int CW = kCOB / NWM;             // co rows per wave
+  constexpr int CW = COB / NWM;              // co rows per wave
   constexpr int FI = CW / 16;                // A fragments per wave
   constexpr int CF = C / 16;                 // 16-column fragments per tap
   constexpr int NF = TG * CF / 4;            // B fragments per wave
   static_assert(TG * CF % 4 == 0, "tap group split");
   constexpr int kXP = (kR + 2) * G::kW * C / 8;  // 16-B input pieces of a block (widest row)
-  constexpr int kDP = kR * G::kW * kCOB / 8;     // 16-B dY pieces
+  constexpr int kDP = kR * G::kW * COB / 8;      // 16-B dY pieces
   constexpr int JX = (kXP + NT - 1) / NT, JD = (kDP + NT - 1) / NT;
   constexpr int DB = G::kXBytes, ZB = G::kXBytes + G::kDBytes;
   __shared__ __attribute__((aligned(1024))) char lds[G::kBytes];
@@ -107,7 +110,7 @@ __global__ __launch_bounds__(256 * NWM, 1) void wgrad3x3n_kernel(W3Args p) {
   lid = __builtin_amdgcn_readfirstlane(lid);
   const int split = lid / p.groups, grp = lid - split * p.groups;
   constexpr int NTG = 9 / TG;
-  const int co0 = (grp / NTG) * kCOB, t0 = (grp % NTG) * TG;
+  const int co0 = (grp / NTG) * COB, t0 = (grp % NTG) * TG;
   const int b0 = split * p.per_split;
   const int b1 = b0 + p.per_split < p.nblocks ? b0 + p.per_split : p.nblocks;
 
@@ -130,7 +133,7 @@ __global__ __launch_bounds__(256 * NWM, 1) void wgrad3x3n_kernel(W3Args p) {
   }
 
   // ---- staging: this thread's 16-B pieces (the same LDS places for every block)
-  const int NX = (kR + 2) * W * C / 8, ND = kR * W * kCOB / 8;
+  const int NX = (kR + 2) * W * C / 8, ND = kR * W * COB / 8;
   int xl[JX];
 #pragma unroll
   for (int j = 0; j < JX; ++j) {
@@ -171,7 +174,7 @@ __global__ __launch_bounds__(256 * NWM, 1) void wgrad3x3n_kernel(W3Args p) {
 #if W3N_DIAG_NOLOAD
       const uint32_t off = i > (1 << 30) ? static_cast<uint32_t>(dbase) : kOOB;
 #else
-      const uint32_t off = i < ND ? static_cast<uint32_t>(dbase + (i >> 3) * CO * 2 + (i & 7) * 16) : kOOB;
+      const uint32_t off = i < ND ? static_cast<uint32_t>(dbase + (i / DPP) * CO * 2 + (i % DPP) * 16) : kOOB;
 #endif
       dv[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(dr, off, 0, 0));
     }
@@ -183,7 +186,7 @@ __global__ __launch_bounds__(256 * NWM, 1) void wgrad3x3n_kernel(W3Args p) {
 #pragma unroll
     for (int j = 0; j < JD; ++j) {
       const int i = j * NT + tid;
-      if (i < ND) *reinterpret_cast<uint4*>(lds + DB + (i >> 3) * kSA + (i & 7) * 16) = dv[j];
+      if (i < ND) *reinterpret_cast<uint4*>(lds + DB + (i / DPP) * kSA + (i % DPP) * 16) = dv[j];
     }
   };
 
@@ -322,9 +325,9 @@ __global__ __launch_bounds__(256 * NWM, 1) void wgrad3x3n_kernel(W3Args p) {
     }
 }
 
-template <int C, int TG, int NWM, int DEPTH>
+template <int C, int TG, int NWM, int DEPTH, int COB = 64>
 void launch3(const W3Args& a, int splits, hipStream_t s) {
-  wgrad3x3n_kernel<C, TG, NWM, DEPTH><<<splits * a.groups, 256 * NWM, 0, s>>>(a);
+  wgrad3x3n_kernel<C, TG, NWM, DEPTH, COB><<<splits * a.groups, 256 * NWM, 0, s>>>(a);
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
 
@@ -332,10 +335,10 @@ void launch3(const W3Args& a, int splits, hipStream_t s) {
 
 bool wgrad3x3n_supported(int64_t N, int H, int W, int C, int Cout) {
   if (C != 64 && C != 128) return false;
-  const int maxw = C == 64 ? Geo3<64>::kW : Geo3<128>::kW;
-  const int maxp = C == 64 ? Geo3<64>::kP : Geo3<128>::kP;
+  const int maxw = C == 64 ? Geo3<64, 64>::kW : Geo3<128, 64>::kW;
+  const int maxp = C == 64 ? Geo3<64, 64>::kP : Geo3<128, 64>::kP;
   return N >= 1 && H >= kR && H % kR == 0 && W >= 4 && W % 4 == 0 && W <= maxw && pitch_of(W) <= maxp &&
-         Cout >= kCOB && Cout % kCOB == 0 && N * H * W * static_cast<int64_t>(C > Cout ? C : Cout) * 2 < (int64_t(1) << 31);
+         Cout >= 64 && Cout % 64 == 0 && N * H * W * static_cast<int64_t>(C > Cout ? C : Cout) * 2 < (int64_t(1) << 31);
 }
 
 int wgrad3x3n_splits(int64_t N, int H, int splits) {
@@ -345,9 +348,11 @@ int wgrad3x3n_splits(int64_t N, int H, int splits) {
   return static_cast<int>((nb + per - 1) / per);
 }
 
+// variant bit 2 (C = 128, Cout % 128 == 0): 128 output channels per workgroup
+static int cob_of(int C, int Cout, int variant) { return C == 128 && (variant & 4) && Cout % 128 == 0 ? 128 : 64; }
+
 int wgrad3x3n_groups(int C, int Cout, int variant) {
-  (void)variant;
-  return (Cout / kCOB) * (C == 64 ? 1 : 3);
+  return (Cout / cob_of(C, Cout, variant)) * (C == 64 ? 1 : 3);
 }
 
 void wgrad3x3n(const void* dy, const void* x, float* ws, int64_t N, int H, int W, int C, int Cout, int splits,
@@ -371,6 +376,8 @@ void wgrad3x3n(const void* dy, const void* x, float* ws, int64_t N, int H, int W
   if (C == 64) {
     if (w8) launch3<64, 9, 2, 1>(a, sp, stream);  // (8 waves with two register sets spill)
     else { if (d2) launch3<64, 9, 1, 2>(a, sp, stream); else launch3<64, 9, 1, 1>(a, sp, stream); }
+  } else if (cob_of(C, Cout, variant) == 128) {
+    if (w8) launch3<128, 3, 2, 1, 128>(a, sp, stream); else launch3<128, 3, 1, 1, 128>(a, sp, stream);
   } else {
     if (w8) launch3<128, 3, 2, 1>(a, sp, stream);
     else { if (d2) launch3<128, 3, 1, 2>(a, sp, stream); else launch3<128, 3, 1, 1>(a, sp, stream); }

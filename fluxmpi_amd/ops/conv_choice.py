@@ -38,6 +38,13 @@ _WG_CONFIGS = ((2, 512), (2, 768), (2, 1024), (2, 384))
 # the narrow 3x3 weight-gradient kernel (wgrad3x3n.hip) configurations: (variant, target workgroups);
 # variant bit 0: 8 waves (else 4), bit 1 (4 waves only): the next two blocks in flight (else one)
 _W3N_CONFIGS = ((1, 256), (2, 256), (0, 256), (1, 512))
+# ... for the 128-channel layers (bit 2: 128 output channels per workgroup)
+_W3N_CONFIGS_128 = ((5, 256), (4, 256), (1, 256), (5, 512))
+
+
+def w3n_configs(ci: int):
+    """The wgrad3x3n configurations the autotune times for ``ci`` input channels."""
+    return _W3N_CONFIGS_128 if ci == 128 else _W3N_CONFIGS
 # the statistics pass a MIOpen forward then needs is priced at one read of the output at this rate
 _STATS_PASS_BPS = 5e12
 
@@ -135,7 +142,7 @@ def wgrad_best(key, impls: dict, param=None):
                 if t < best[0]:
                     best = (t, ("w256", None))
             if "w3n" in impls:
-                for cfg in _W3N_CONFIGS:
+                for cfg in impls.get("w3n_cfgs", _W3N_CONFIGS):
                     t = time_us(lambda: impls["w3n"](cfg))
                     if t < best[0]:
                         best = (t, ("w3n", cfg))

@@ -37,7 +37,7 @@ from . import groupnorm as _GN
 from .conv_choice import (_DGRAD_CHOICE, _DS_CHOICE, _FWD1_CHOICE, _FWD_CHOICE, _FWD_ENGINE, _S2_CHOICE,  # noqa: F401
                           _WG_CHOICE, FWD_ENGINES, choices_frozen, dump_choices, freeze_choices,
                           load_choice_lines, load_choices, no_measure as _no_measure, stats_choice,
-                          time_us as _time_us, w256_ok as _w256_ok, wgrad_best)
+                          time_us as _time_us, w256_ok as _w256_ok, w3n_configs, wgrad_best)
 from .gemm import conv1x1_dgrad, conv1x1_wgrad, conv3x3_dgrad, conv3x3_fwd, gemm, note_filter
 from .multi_tensor import DTYPE_CODE
 
@@ -572,6 +572,7 @@ class _Conv3x3(torch.autograd.Function):
                 "ours": lambda: G.conv3x3_wgrad(dy, x)}
             if x.dtype == torch.bfloat16 and G.wgrad3x3n_ok(tuple(x.shape), weight.shape[0]):
                 impls["w3n"] = lambda cfg: G.conv3x3_wgrad_n(dy, x, *cfg)  # narrow channels: rows staged once
+                impls["w3n_cfgs"] = w3n_configs(x.shape[1])
             dw = wgrad_best(("3x3", tuple(x.shape), weight.shape[0]), impls, param=weight)
         dx = None
         if ctx.needs_input_grad[0]:

@@ -33,12 +33,12 @@ def main():
         wt = torch.zeros(c, c, 3, 3, device="cuda", dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
         ref = G.conv3x3_wgrad(dy, x).float()
         errs = {}
-        for cfg in CC._W3N_CONFIGS:
+        for cfg in CC.w3n_configs(c):
             d = G.conv3x3_wgrad_n(dy, x, *cfg).float()
             errs[str(cfg)] = round(float((d - ref).norm() / ref.norm()), 5)
             assert errs[str(cfg)] < 5e-3, errs
         fl = 2.0 * n * h * w * c * 9 * c
-        arms = {f"w3n_{v}_{t}": (lambda v=v, t=t: G.conv3x3_wgrad_n(dy, x, v, t)) for v, t in CC._W3N_CONFIGS}
+        arms = {f"w3n_{v}_{t}": (lambda v=v, t=t: G.conv3x3_wgrad_n(dy, x, v, t)) for v, t in CC.w3n_configs(c)}
         for v, t in CC._WG_CONFIGS:
             arms[f"im2col_{v}_{t}"] = lambda v=v, t=t: CC._with_cfg((v, t), lambda: G.conv3x3_wgrad(dy, x))
         arms["miopen"] = lambda: torch.ops.aten.convolution_backward(dy, x, wt, None, [1, 1], [1, 1], [1, 1], False,

@@ -2,7 +2,8 @@
 rows staged once per block of 4 image rows — against PyTorch fp32 (the filter gradient of
 F.conv2d on the same bf16 operands): every variant and split count, the ResNet-50 stage 1 / 2
 shapes, rows whose width leaves a partial last k-step (W % 8 == 4), several output-channel
-groups (Cout > 64), and the autotuned route through the fused 3x3 block."""
+groups (Cout > 64; variant bit 2: 128-channel groups where Cout % 128 == 0, else 64), and the
+autotuned route through the fused 3x3 block."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -30,7 +31,8 @@ def _ref(x, dy, co):
 
 
 @pytest.mark.parametrize("N,C,CO,H,W", SHAPES)
-@pytest.mark.parametrize("cfg", [(1, 256), (0, 256), (1, 512), (0, 7), (2, 256), (2, 7), (2, 5), (1, 5)])
+@pytest.mark.parametrize("cfg", [(1, 256), (0, 256), (1, 512), (0, 7), (2, 256), (2, 7), (2, 5), (1, 5), (5, 256),
+                                 (4, 256), (5, 7), (4, 5)])
 def test_wgrad3x3n_matches_fp32(gpu_ext, N, C, CO, H, W, cfg):
     from fluxmpi_amd.ops import gemm as G
     torch.manual_seed(0)
