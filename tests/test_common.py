@@ -68,3 +68,22 @@ def test_kernel_choice_table_roundtrip(tmp_path):
         for name, d in saved.items():
             getattr(fb, name).clear()
             getattr(fb, name).update(d)
+
+
+def test_kernel_choice_w3n_record_roundtrip():
+    """A weight-gradient choice of the narrow 3x3 kernel (name + (variant, target workgroups))
+    survives dump_choices / load_choice_lines — the form rank 0's table is broadcast in."""
+    from fluxmpi_amd.ops import conv_choice as fb
+    key = ("3x3", (256, 64, 56, 56), 64)
+    saved = dict(fb._WG_CHOICE)
+    try:
+        fb._WG_CHOICE.clear()
+        fb._WG_CHOICE[key] = ("w3n", (1, 256))
+        lines = fb.dump_choices()
+        fb._WG_CHOICE.clear()
+        assert fb.load_choice_lines(lines) == 1
+        assert fb._WG_CHOICE[key] == ("w3n", (1, 256))
+        assert fb.w3n_configs(128) != fb.w3n_configs(64)
+    finally:
+        fb._WG_CHOICE.clear()
+        fb._WG_CHOICE.update(saved)
