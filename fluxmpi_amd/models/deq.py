@@ -169,11 +169,12 @@ def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0, check_lag: i
     lag = (CHECK_LAG if check_lag is None else int(check_lag)) if x0.is_cuda else 0
     flags = LaggedFlags(lag, max_iter) if lag > 0 else None
 
-    def solve_step(k):
+    def solve_step(k, res_out=None):
         # stored G = F - X: only the row(s) changed since the last Gram are recomputed; on the GPU
-        # the residual and the (n+1)^2 solve are ONE launch after the Gram pass (AO.gram_solve)
+        # the residual and the (n+1)^2 solve are ONE launch after the Gram pass (AO.gram_solve);
+        # res_out: a static slot the residual is written into (the graph replay's buffer)
         last = (k - 1) % m
-        return AO.gram_solve(X, Fv, min(k, m), last, Gs, (0, 1) if k == 2 else (last,), lam, k > 2)
+        return AO.gram_solve(X, Fv, min(k, m), last, Gs, (0, 1) if k == 2 else (last,), lam, k > 2, res_out)
 
     def mix_step(k, alpha):
         fx_into(AO.mix(X, Fv, alpha, k % m, beta, dt), k % m)
@@ -304,10 +305,11 @@ class SolverGraphs:
             g = torch.cuda.CUDAGraph()
             with torch.no_grad(), _capture(g):
                 for i in range(m):
-                    alpha, res_t = solve_step(k0 + i)
-                    self.rbuf[i].copy_(res_t)
+                    alpha, res_t = solve_step(k0 + i, self.rbuf[i])
+                    if res_t is not None and res_t.data_ptr() != self.rbuf[i].data_ptr():
+                        self.rbuf[i].copy_(res_t)
                     mix_step(k0 + i, alpha)
-                self.rmin.copy_(self.rbuf.min())
+                torch.amin(self.rbuf, dim=0, out=self.rmin)
             self.g_fwd = g
         self.g_fwd.replay()
         return self.rmin
@@ -333,9 +335,12 @@ class SolverGraphs:
             with _capture(g):
                 u = self.u
                 for i in range(chunk):
-                    u, _ = cell.adjoint_step(self.state, u, self.grad, self.thresh2, self.done[i:i + 1])
-                self.u.copy_(u)
-                self.dmax.copy_(self.done.max())
+                    # the chunk's last iterate straight into the static u (its input is another buffer)
+                    out = self.u if (i == chunk - 1 and chunk > 1) else None
+                    u, _ = cell.adjoint_step(self.state, u, self.grad, self.thresh2, self.done[i:i + 1], out=out)
+                if u.data_ptr() != self.u.data_ptr():
+                    self.u.copy_(u)
+                torch.amax(self.done, dim=0, out=self.dmax)
             self.g_adj = g
             self.chunk = chunk
 
@@ -576,16 +581,18 @@ class ResidualCell(nn.Module):
         return conv3x3_dgrad_raw(d1, self.conv1.weight, zs, residual=d3)   # + n3's direct path to z
 
     @torch.no_grad()
-    def adjoint_step(self, state, u, grad, thresh2=None, flag=None):
+    def adjoint_step(self, state, u, grad, thresh2=None, flag=None, out=None):
         """One adjoint iteration ``u_new = J_f(z)^T u + grad`` with ``ss = |u_new - u|^2`` (0-d fp32
         device tensor); with ``thresh2`` / ``flag`` also ``flag = ss <= thresh2`` on the device.
-        One-kernel cell: the update is fused into the VJP kernel (2 launches per iteration)."""
+        One-kernel cell: the update is fused into the VJP kernel (2 launches per iteration).
+        ``out``: write ``u_new`` there when possible (not ``u`` itself)."""
         from ..ops import deq_cell
         if deq_cell.supported(self, u):
-            u_new, part = deq_cell.cell_vjp(self, state, u, grad=grad)
+            u_new, part = deq_cell.cell_vjp(self, state, u, grad=grad, out=out)
             t2 = None if thresh2 is None else thresh2.float()
             return u_new, deq_cell.adjoint_check(part, t2, flag)
-        u_new, ss = AO.adjoint_step(self.vjp(state, u), grad, u)
+        u_new, ss = AO.adjoint_step(self.vjp(state, u), grad, u,
+                                    out=out if (out is not None and out.data_ptr() != u.data_ptr()) else None)
         if flag is not None:
             flag.copy_((ss <= thresh2).float().reshape(flag.shape))
         return u_new, ss

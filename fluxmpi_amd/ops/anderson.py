@@ -82,16 +82,21 @@ def gram(X: torch.Tensor, F: torch.Tensor, n: int, last: int, G: torch.Tensor | 
 
 
 def gram_solve(X: torch.Tensor, F: torch.Tensor, n: int, last: int, G: torch.Tensor, fresh, lam: float,
-               want_res: bool):
+               want_res: bool, res_out: torch.Tensor | None = None):
     """``(alpha [bsz, n], res)`` of one Anderson step: the Gram pass (:func:`gram`, stored ``G``)
     then ONE launch (``anderson_solve``) for the chunk sums, the relative residual of row ``last``
     (a 0-d device tensor, or None without ``want_res``) and the batched pivoted solve of
     ``[[0, 1^T], [1, G G^T + lam I]] a = e_0``, ``alpha = a[1:]``. CPU tensors (and batches over
-    1024) use the PyTorch composition: :func:`gram`, ``torch.linalg.solve_ex``."""
+    1024) use the PyTorch composition: :func:`gram`, ``torch.linalg.solve_ex``.
+    ``res_out`` (0-d fp32 device tensor, with ``want_res``): the residual is written there (no copy
+    of a fresh scalar into the caller's buffer)."""
     bsz = X.shape[0]
     if not (_native(X, F, n) and bsz <= 1024):
         H, fn2 = gram(X, F, n, last, G, fresh)
         res = (H[:, last, last].sum().sqrt() / (1e-5 + fn2.sum().sqrt())) if want_res else None
+        if res is not None and res_out is not None:
+            res_out.copy_(res)
+            res = res_out
         A = torch.zeros(bsz, n + 1, n + 1, dtype=torch.float32, device=X.device)
         A[:, 0, 1:] = A[:, 1:, 0] = 1
         A[:, 1:, 1:] = H + lam * torch.eye(n, dtype=torch.float32, device=X.device)
@@ -111,7 +116,8 @@ def gram_solve(X: torch.Tensor, F: torch.Tensor, n: int, last: int, G: torch.Ten
     C.anderson_gram(X.data_ptr(), F.data_ptr(), DTYPE_CODE[F.dtype], G.data_ptr(), mask, part.data_ptr(), bsz, d,
                     X.stride(1), X.stride(0), n, last, chunks, stream, DTYPE_CODE[X.dtype])
     alpha = torch.empty(bsz, n, device=X.device, dtype=torch.float32)
-    res = torch.empty((), device=X.device, dtype=torch.float32) if want_res else None
+    res = (res_out if res_out is not None else torch.empty((), device=X.device, dtype=torch.float32)) \
+        if want_res else None
     C.anderson_solve(part.data_ptr(), chunks, bsz, n, last, float(lam), alpha.data_ptr(),
                      res.data_ptr() if res is not None else 0, stream)
     return alpha, res
@@ -142,22 +148,25 @@ def mix(X: torch.Tensor, F: torch.Tensor, alpha: torch.Tensor, slot: int, beta: 
     return z if z is not None else X[:, slot]
 
 
-def adjoint_step(vjp: torch.Tensor, grad: torch.Tensor, u: torch.Tensor):
+def adjoint_step(vjp: torch.Tensor, grad: torch.Tensor, u: torch.Tensor, out: torch.Tensor | None = None):
     """``(u_new, ss)``: ``u_new = vjp + grad`` and ``ss = |u_new - u|^2`` (0-d fp32 device tensor)
     in one pass on the GPU (``adjoint_step`` + one partial-sum reduce); the DEQ adjoint solve's
-    update and convergence test. Other layouts / CPU: the PyTorch composition."""
+    update and convergence test. ``out`` (optional, like ``vjp``, not ``u``): written instead of a
+    new tensor. Other layouts / CPU: the PyTorch composition."""
     same = (vjp.shape == grad.shape == u.shape and vjp.dtype == grad.dtype == u.dtype
             and vjp.stride() == grad.stride() == u.stride())
     dense = same and vjp.numel() % 8 == 0 and (vjp.is_contiguous() or (vjp.dim() == 4 and vjp.is_contiguous(
         memory_format=torch.channels_last)))
     if not (vjp.is_cuda and dense and vjp.dtype in DTYPE_CODE and vjp.numel() > 0
             and (vjp.data_ptr() | grad.data_ptr() | u.data_ptr()) % 16 == 0):
-        u_new = vjp + grad
+        u_new = torch.add(vjp, grad, out=out) if out is not None else vjp + grad
         return u_new, (u_new - u).float().pow(2).sum()
     C = _ext.get(required=True)
     n = vjp.numel()
     blocks = C.adjoint_step_blocks(n)
-    u_new = torch.empty_like(vjp)  # same strides (dense), so the flat element order matches
+    # same strides (dense), so the flat element order matches
+    u_new = out if (out is not None and out.stride() == vjp.stride() and out.dtype == vjp.dtype) else \
+        torch.empty_like(vjp)
     part = torch.empty(blocks, device=vjp.device, dtype=torch.float32)
     ss = torch.empty((), device=vjp.device, dtype=torch.float32)
     stream = _stream(vjp)

@@ -99,12 +99,13 @@ def cell_forward(cell, z: torch.Tensor, x: torch.Tensor, keep: bool = False, out
     return out, state
 
 
-def cell_vjp(cell, state, u: torch.Tensor, grad: torch.Tensor | None = None):
+def cell_vjp(cell, state, u: torch.Tensor, grad: torch.Tensor | None = None, out: torch.Tensor | None = None):
     """``J_f(z)^T u`` in one launch from a ``forward_state`` state (fused or unfused producer).
 
     ``grad``: the adjoint iteration's update is fused in — returns ``(u_new, part)`` with
     ``u_new = bf16(J^T u + grad)`` and ``part[n]`` the per-sample ``sum (u_new - u)^2`` (sum them
-    with :func:`adjoint_check`): one launch instead of the VJP + ``adjoint_step`` pair."""
+    with :func:`adjoint_check`): one launch instead of the VJP + ``adjoint_step`` pair. ``out``
+    (channels_last bf16 like ``u``, not ``u`` itself): written instead of a new tensor."""
     from .gemm import filter_t
     C = _ext.get(required=True)
     zs, (h1, m1, r1, w1), (h2, m2, r2, w2), (h3, m3, r3, w3) = state
@@ -117,7 +118,9 @@ def cell_vjp(cell, state, u: torch.Tensor, grad: torch.Tensor | None = None):
             t.shape != (n, G) or t.dtype != torch.float32 for t in (m1, r1, m2, r2, m3, r3)):
         raise ValueError("deq_cell.cell_vjp: state does not match the gradient's shape")
     w2t, w1t = filter_t(cell.conv2.weight), filter_t(cell.conv1.weight)  # [ci][tap * co], taps flipped
-    out = torch.empty_like(u, memory_format=torch.channels_last)
+    if out is None or out.shape != u.shape or out.dtype != torch.bfloat16 or not _cl(out) or \
+            out.data_ptr() == u.data_ptr():
+        out = torch.empty_like(u, memory_format=torch.channels_last)
     part = None
     if grad is not None:
         if not _cl(grad) or grad.dtype != torch.bfloat16:
