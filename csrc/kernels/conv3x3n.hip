@@ -27,6 +27,7 @@
 // Reference: /root/reference has no kernels — this is the compute under the per-step gradient
 // work of the ResNet-50 DDP configuration (BASELINE.json, src/optimizer.jl:20-23).
 #include <cstdint>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -61,6 +62,9 @@ struct CNArgs {
   float* stats;    // EPI 3: [kShards][2][Cout]
   int H, W;
   int tiles;
+  int m_base;      // pixel of tile 0
+  int ncob;        // output-channel blocks of CO per tile (workgroup b: tile b / ncob, block b % ncob)
+  int ldy;         // output channels of y (and of the statistics) = ncob * CO
   uint32_t x_bytes;
 };
 
@@ -79,11 +83,12 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 4 : 2) void conv3x3n_kernel(CNA
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   // XCD-aware tile order: the workgroups of one XCD (b % 8) take a contiguous range of tiles, so
   // neighbouring tiles' shared halo rows meet in that XCD's L2 (speed only)
-  int tile = blockIdx.x;
-  if (p.tiles % 8 == 0) tile = (blockIdx.x % 8) * (p.tiles / 8) + blockIdx.x / 8;
+  int tile = blockIdx.x / p.ncob;
+  const int co0 = (blockIdx.x - tile * p.ncob) * CO;  // first output channel of this workgroup
+  if (p.ncob == 1 && p.tiles % 8 == 0) tile = (blockIdx.x % 8) * (p.tiles / 8) + blockIdx.x / 8;
   tile = __builtin_amdgcn_readfirstlane(tile);
   const int W = p.W, H = p.H;
-  const int m0 = tile * kTM;
+  const int m0 = p.m_base + tile * kTM;
   const int hb = m0 - W - 1;  // global pixel of halo row 0
   const int hrows = kTM + 2 * W + 2;
 
@@ -93,7 +98,8 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 4 : 2) void conv3x3n_kernel(CNA
     *reinterpret_cast<uint4*>(halo + pl * G::kPlaneBytes + G::kZeroRow * 128 + q * 16) = uint4{0, 0, 0, 0};
   }
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(p.x), 0, p.x_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(p.w), 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16*>(p.w) + static_cast<int64_t>(co0) * 9 * C, 0,
+                                                                   0x7fffffff, 0x00020000);
   const int lrow = lane >> 3, lslot = lane & 7;
   {
     const int groups = (hrows + 7) / 8;  // DMA instructions per plane (8 rows each)
@@ -199,7 +205,7 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 4 : 2) void conv3x3n_kernel(CNA
     for (int r = 0; r < 4; ++r) cs[nb][r] = cq[nb][r] = 0.f;
 #pragma unroll
   for (int mb = 0; mb < 2; ++mb) {
-    bf16* yrow = p.y + static_cast<int64_t>(m0 + wave * 32 + mb * 16 + fr) * CO + 4 * fg;
+    bf16* yrow = p.y + static_cast<int64_t>(m0 + wave * 32 + mb * 16 + fr) * p.ldy + co0 + 4 * fg;
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
       bf16 o[4];
@@ -238,16 +244,38 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 4 : 2) void conv3x3n_kernel(CNA
       float t = 0.f;
 #pragma unroll
       for (int wv = 0; wv < kWaves; ++wv) t += red[(wv * 2 + mom) * CO + col];
-      atomicAdd(p.stats + (static_cast<int64_t>(tile % kShards) * 2 + mom) * CO + col, t);
+      atomicAdd(p.stats + (static_cast<int64_t>(tile % kShards) * 2 + mom) * p.ldy + co0 + col, t);
     }
   }
 }
 
 template <int C, int CO>
 void launch(const CNArgs& p, int epi, hipStream_t s) {
-  if (epi == 3) conv3x3n_kernel<C, CO, 3><<<p.tiles, kThreads, 0, s>>>(p);
-  else conv3x3n_kernel<C, CO, 0><<<p.tiles, kThreads, 0, s>>>(p);
+  const int grid = p.tiles * p.ncob;
+  if (epi == 3) conv3x3n_kernel<C, CO, 3><<<grid, kThreads, 0, s>>>(p);
+  else conv3x3n_kernel<C, CO, 0><<<grid, kThreads, 0, s>>>(p);
   FLUXMPI_HIP_CHECK(hipGetLastError());
+}
+
+// The 128-channel kernel holds one workgroup per CU (150 KB of LDS): ResNet-50's 28 x 28 x 128
+// layers at batch 256 are 784 tiles = 3 rounds of 256 + 16, and that last round cost ~20 % of the
+// call (profiles/rd5ah_conv3x3n_tail.jsonl: 85.0 us vs 66.5 at 735 tiles). Its tiles run as 32
+// output channels per workgroup instead: four times the workgroups, a quarter of each wave's MFMAs
+// (64-pixel tiles of a 2-wave kernel kept each wave's work and saved only 2 us, rd5ai).
+void launch128(CNArgs p, int epi, hipStream_t s) {
+  static const int slots = std::getenv("FLUXMPI_CONV3X3N_NOTAIL")
+                               ? 0
+                               : resident_blocks(reinterpret_cast<const void*>(&conv3x3n_kernel<128, 128, 3>), kThreads, 0);
+  const int full = slots > 0 ? p.tiles / slots * slots : 0, rem = p.tiles - full;
+  if (full == 0 || rem == 0 || rem * 4 > slots) {
+    launch<128, 128>(p, epi, s);
+    return;
+  }
+  CNArgs t = p;
+  p.tiles = full;
+  launch<128, 128>(p, epi, s);
+  t.m_base = full * kTM, t.tiles = rem, t.ncob = 4;
+  launch<128, 32>(t, epi, s);
 }
 
 }  // namespace
@@ -272,8 +300,9 @@ void conv3x3n(const void* x, const void* w, void* y, float* stats, int64_t pixel
   p.x = static_cast<const bf16*>(x), p.w = static_cast<const bf16*>(w), p.y = static_cast<bf16*>(y);
   p.stats = stats, p.H = H, p.W = W, p.tiles = static_cast<int>(pixels / kTM);
   p.x_bytes = static_cast<uint32_t>(pixels * C * 2);
+  p.m_base = 0, p.ncob = 1, p.ldy = Cout;
   if (C == 64) launch<64, 64>(p, epi, stream);
-  else launch<128, 128>(p, epi, stream);
+  else launch128(p, epi, stream);
 }
 
 }  // namespace fluxmpi
