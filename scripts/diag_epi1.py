@@ -4,11 +4,18 @@ import sys
 import torch
 
 sys.path.insert(0, __file__.rsplit("/scripts/", 1)[0])
+sys.path.insert(0, __file__.rsplit("/", 1)[0] + "/diag")
+import load_variant  # noqa: E402  (FLUXMPI_C_VARIANT=<.so>: e.g. gemm_nt.hip built with SLP vectorisation)
+
+load_variant.install()
 from fluxmpi_amd.ops import gelu as GL  # noqa: E402
 from fluxmpi_amd.ops import gemm_nt as G  # noqa: E402
 
-GL.set_form("tanh")
-for m, n, k in ((512, 512, 128), (50432, 2304, 768)):
+print("library:", sys.modules["fluxmpi_amd._C"].__file__ if "fluxmpi_amd._C" in sys.modules else "package default")
+for form, m, n, k in (("tanh", 512, 512, 128), ("tanh", 50432, 2304, 768), ("tanh", 50432, 3072, 768),
+                      ("erf", 50432, 3072, 768)):
+    GL.set_form(form)
+    print("form", form)
     torch.manual_seed(0)
     x = ((torch.rand(m, k, device="cuda") * 2 - 1)).bfloat16()
     w = ((torch.rand(n, k, device="cuda") * 2 - 1) * k ** -0.5).bfloat16()

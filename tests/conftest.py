@@ -21,6 +21,11 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an AMD Instinct GPU (MI355X)")
     config.addinivalue_line("markers", "slow: long-running test")
+    if os.environ.get("FLUXMPI_C_VARIANT"):  # run the suite against a variant build of the library
+        sys.path.insert(0, os.path.join(ROOT, "scripts", "diag"))
+        import load_variant
+
+        load_variant.install()
 
 
 def run_spmd(target: str, nprocs: int | None = None, env: dict | None = None, timeout: float = 300.0):
