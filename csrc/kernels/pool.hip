@@ -14,6 +14,7 @@
 //             and feeds the plain BatchNorm backward.
 // Layout NHWC, 8 channels (16 B) per lane; consecutive lanes walk channels, then
 // output columns, so a wave reads whole contiguous pixel rows.
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -32,7 +33,9 @@ struct PoolGeo {
 
 // One workgroup per output row (n, oh); lanes walk (ow, channel vector) of the row with
 // 32-bit index math (64-bit division per element made the first version ALU-bound).
-template <typename T>
+// KK > 0: the window size at compile time; every in-image tap's load is issued before the first
+// compare (the generic loop's branches kept one 16-B load in flight per lane at a time).
+template <typename T, int KK = 0>
 __global__ __launch_bounds__(1024) void bn_relu_maxpool_fwd_kernel(const T* __restrict__ x,
                                                                        const float* __restrict__ scale,
                                                                        const float* __restrict__ shift,
@@ -58,7 +61,29 @@ __global__ __launch_bounds__(1024) void bn_relu_maxpool_fwd_kernel(const T* __re
       best[j] = -INFINITY;
       arg[j] = 0;
     }
-    for (int kh = 0; kh < g.K; ++kh) {
+    if constexpr (KK > 0) {
+      T raw[KK * KK][8];
+      bool ok[KK * KK];
+#pragma unroll
+      for (int k = 0; k < KK * KK; ++k) {
+        const int h = h0 + k / KK, w = w0 + k % KK;
+        ok[k] = h >= 0 && h < g.H && w >= 0 && w < g.W;
+        load8(xn + (static_cast<int64_t>(ok[k] ? h : 0) * g.W + (ok[k] ? w : 0)) * g.C + c0, raw[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < KK * KK; ++k) {
+        if (!ok[k]) continue;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float z = fmaf(static_cast<float>(raw[k][j]), sc[j], sh[j]);  // as below
+          if (z > best[j]) {
+            best[j] = z;
+            arg[j] = k;
+          }
+        }
+      }
+    }
+    for (int kh = 0; KK == 0 && kh < g.K; ++kh) {
       const int h = h0 + kh;
       if (h < 0 || h >= g.H) continue;
       for (int kw = 0; kw < g.K; ++kw) {
@@ -233,8 +258,12 @@ void bn_relu_maxpool_fwd(const void* x, const float* scale, const float* shift, 
   const int thr = per_row <= 1024 ? static_cast<int>((per_row + 63) / 64 * 64) : kThreads;
   switch (dtype) {
     case kBF16:
-      bn_relu_maxpool_fwd_kernel<bf16><<<nb, thr, 0, s>>>(static_cast<const bf16*>(x), scale, shift,
-                                                               static_cast<bf16*>(y), idx, g);
+      if (g.K == 3 && !std::getenv("FLUXMPI_POOL_GENERIC"))
+        bn_relu_maxpool_fwd_kernel<bf16, 3><<<nb, thr, 0, s>>>(static_cast<const bf16*>(x), scale, shift,
+                                                                  static_cast<bf16*>(y), idx, g);
+      else
+        bn_relu_maxpool_fwd_kernel<bf16><<<nb, thr, 0, s>>>(static_cast<const bf16*>(x), scale, shift,
+                                                                 static_cast<bf16*>(y), idx, g);
       break;
     case kF16:
       bn_relu_maxpool_fwd_kernel<f16><<<nb, thr, 0, s>>>(static_cast<const f16*>(x), scale, shift,
