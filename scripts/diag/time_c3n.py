@@ -40,4 +40,6 @@ for (n, c, h, w) in [(256, 64, 56, 56), (256, 128, 28, 28), (240, 128, 28, 28)]:
     ref = torch.nn.functional.conv2d(x.float(), w2.permute(0, 3, 1, 2).float(), padding=1)
     rec[f"{n}x{c}x{h}_rel"] = round(float((y.float() - ref).norm() / ref.norm()), 5)
     rec[f"{n}x{c}x{h}"] = round(t_us(lambda: G.conv3x3n(x, w2, y, M, h, w, stats)), 1)
+    if os.environ.get("C3N_EPI0"):
+        rec[f"{n}x{c}x{h}_epi0"] = round(t_us(lambda: G.conv3x3n(x, w2, y, M, h, w, None)), 1)
 print(json.dumps(rec), flush=True)
