@@ -42,8 +42,14 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) char lds_char;
 
 constexpr int kTM = 256;     // output pixels per workgroup
-constexpr int kWaves = 8;
-constexpr int kThreads = 64 * kWaves;
+#ifndef C3N_W128
+#define C3N_W128 16
+#endif
+// waves per workgroup: 8 x 32 rows; the 128-channel kernel (one workgroup per CU: 150 KB of LDS)
+// runs 16, two per 32-row block, each on half of the output channels: 4 waves per SIMD instead of
+// 2 (104 VGPRs), 77.5 vs 81.2 us per call at 28 x 28 x 128 x 256 images, 64.7 vs 69.0 at 240
+// (profiles/rd5ax_conv3x3n_16waves_ab.jsonl)
+template <int CO> constexpr int waves_of() { return CO == 128 ? C3N_W128 : 8; }
 constexpr int kShards = 64;  // BatchNorm statistics shards (== batchnorm.hip)
 
 // halo rows for the widest image each channel count supports (LDS sizing)
@@ -71,11 +77,13 @@ struct CNArgs {
 __device__ __forceinline__ bf16x8 frag(const char* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
 template <int C, int CO, int EPI>
-__global__ __launch_bounds__(kThreads, C == 64 ? 4 : 2) void conv3x3n_kernel(CNArgs p) {
+__global__ __launch_bounds__(64 * waves_of<CO>(), C == 64 ? 4 : (waves_of<CO>() == 16 ? 4 : 2)) void conv3x3n_kernel(CNArgs p) {
   using G = Geo<C>;
+  constexpr int kWaves = waves_of<CO>(), kThreads = 64 * kWaves;
   constexpr int NPL = G::kPlanes;
   constexpr int KS = C / 32;               // 32-channel k-steps per tap
-  constexpr int NB = CO / 16;              // N-blocks
+  constexpr int WN = kWaves / 8, WM = 8;   // wave grid: 8 row blocks of 32 x WN column blocks
+  constexpr int NB = CO / WN / 16;         // 16-column blocks per wave
   constexpr int kBBytes = NPL * CO * 128;  // one tap of the filter
   __shared__ __attribute__((aligned(1024))) char halo[NPL * G::kPlaneBytes];
   __shared__ __attribute__((aligned(1024))) char bbuf[2 * kBBytes];
@@ -148,10 +156,11 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 4 : 2) void conv3x3n_kernel(CNA
 
   // ---- the lane's rows: local row lr = 32 wave + 16 mb + (lane & 15); in-image taps as 9-bit masks
   const int fr = lane & 15, fg = lane >> 4;
+  const int wm = wave % WM, wn = wave / WM;  // the wave's 32-row block and column block
   uint32_t vmask[2];
 #pragma unroll
   for (int mb = 0; mb < 2; ++mb) {
-    const int m = m0 + wave * 32 + mb * 16 + fr;
+    const int m = m0 + wm * 32 + mb * 16 + fr;
     const int hw = m % (H * W), h = hw / W, w = hw - h * W;
     const uint32_t rm = (h > 0 ? 1u : 0u) | 2u | (h < H - 1 ? 4u : 0u);
     const uint32_t cm = (w > 0 ? 1u : 0u) | 2u | (w < W - 1 ? 4u : 0u);
@@ -174,14 +183,14 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 4 : 2) void conv3x3n_kernel(CNA
     int arow[2];
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb)
-      arow[mb] = (vmask[mb] >> tap) & 1u ? wave * 32 + mb * 16 + fr + dr * W + dc : G::kZeroRow;
+      arow[mb] = (vmask[mb] >> tap) & 1u ? wm * 32 + mb * 16 + fr + dr * W + dc : G::kZeroRow;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int pl = ks / 2, ch = (ks & 1) * 4 + fg;  // plane, 16-B chunk within its 128-B row
       bf16x8 fb[NB], fa[2];
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) {
-        const int co = nb * 16 + fr;
+        const int co = wn * (NB * 16) + nb * 16 + fr;
         fb[nb] = frag(bb + pl * CO * 128 + co * 128 + ((ch ^ (co & 7)) << 4));
       }
 #pragma unroll
@@ -205,7 +214,7 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 4 : 2) void conv3x3n_kernel(CNA
     for (int r = 0; r < 4; ++r) cs[nb][r] = cq[nb][r] = 0.f;
 #pragma unroll
   for (int mb = 0; mb < 2; ++mb) {
-    bf16* yrow = p.y + static_cast<int64_t>(m0 + wave * 32 + mb * 16 + fr) * p.ldy + co0 + 4 * fg;
+    bf16* yrow = p.y + static_cast<int64_t>(m0 + wm * 32 + mb * 16 + fr) * p.ldy + co0 + wn * (NB * 16) + 4 * fg;
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
       bf16 o[4];
@@ -234,8 +243,8 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 4 : 2) void conv3x3n_kernel(CNA
       for (int r = 0; r < 4; ++r) {
         const float s = row_sum16(cs[nb][r]), q = row_sum16(cq[nb][r]);
         if (fr == 0) {
-          red[(wave * 2 + 0) * CO + nb * 16 + 4 * fg + r] = s;
-          red[(wave * 2 + 1) * CO + nb * 16 + 4 * fg + r] = q;
+          red[(wm * 2 + 0) * CO + wn * (NB * 16) + nb * 16 + 4 * fg + r] = s;
+          red[(wm * 2 + 1) * CO + wn * (NB * 16) + nb * 16 + 4 * fg + r] = q;
         }
       }
     __syncthreads();
@@ -243,7 +252,7 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 4 : 2) void conv3x3n_kernel(CNA
       const int mom = threadIdx.x / CO, col = threadIdx.x - mom * CO;
       float t = 0.f;
 #pragma unroll
-      for (int wv = 0; wv < kWaves; ++wv) t += red[(wv * 2 + mom) * CO + col];
+      for (int wv = 0; wv < WM; ++wv) t += red[(wv * 2 + mom) * CO + col];
       atomicAdd(p.stats + (static_cast<int64_t>(tile % kShards) * 2 + mom) * p.ldy + co0 + col, t);
     }
   }
@@ -252,8 +261,8 @@ __global__ __launch_bounds__(kThreads, C == 64 ? 4 : 2) void conv3x3n_kernel(CNA
 template <int C, int CO>
 void launch(const CNArgs& p, int epi, hipStream_t s) {
   const int grid = p.tiles * p.ncob;
-  if (epi == 3) conv3x3n_kernel<C, CO, 3><<<grid, kThreads, 0, s>>>(p);
-  else conv3x3n_kernel<C, CO, 0><<<grid, kThreads, 0, s>>>(p);
+  if (epi == 3) conv3x3n_kernel<C, CO, 3><<<grid, 64 * waves_of<CO>(), 0, s>>>(p);
+  else conv3x3n_kernel<C, CO, 0><<<grid, 64 * waves_of<CO>(), 0, s>>>(p);
   FLUXMPI_HIP_CHECK(hipGetLastError());
 }
 
@@ -265,7 +274,8 @@ void launch(const CNArgs& p, int epi, hipStream_t s) {
 void launch128(CNArgs p, int epi, hipStream_t s) {
   static const int slots = std::getenv("FLUXMPI_CONV3X3N_NOTAIL")
                                ? 0
-                               : resident_blocks(reinterpret_cast<const void*>(&conv3x3n_kernel<128, 128, 3>), kThreads, 0);
+                               : resident_blocks(reinterpret_cast<const void*>(&conv3x3n_kernel<128, 128, 3>),
+                                                 64 * waves_of<128>(), 0);
   const int full = slots > 0 ? p.tiles / slots * slots : 0, rem = p.tiles - full;
   if (full == 0 || rem == 0 || rem * 4 > slots) {
     launch<128, 128>(p, epi, s);
