@@ -22,8 +22,10 @@
 //   * a tap that falls outside the image (row / column / image boundary in flattened order)
 //     redirects the lane's fragment read to a zero row: one address select per read, no data
 //     masking.
-// 8 waves x 32 rows: per tap and 32-channel k-step a wave reads Cout / 16 filter fragments and 2
-// activation fragments (ds_read_b128) for 2 Cout / 16 MFMAs (v_mfma_f32_16x16x32_bf16).
+// 8 waves x 32 rows (64 channels; 128 channels: 16 waves, two per 32-row block on half of the
+// output channels each): per tap and 32-channel k-step a wave reads one filter fragment per 16 of
+// its output channels and 2 activation fragments (ds_read_b128) for two MFMAs per filter fragment
+// (v_mfma_f32_16x16x32_bf16).
 // Reference: /root/reference has no kernels — this is the compute under the per-step gradient
 // work of the ResNet-50 DDP configuration (BASELINE.json, src/optimizer.jl:20-23).
 #include <cstdint>
