@@ -44,6 +44,9 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) char lds_char;
 
 constexpr int kTM = 256;     // output pixels per workgroup
+#ifndef C3N_TAIL_CO
+#define C3N_TAIL_CO 16
+#endif
 #ifndef C3N_W128
 #define C3N_W128 16
 #endif
@@ -133,8 +136,10 @@ __global__ __launch_bounds__(64 * waves_of<CO>(), C == 64 ? 4 : (waves_of<CO>() 
   // taps 1..8 are prefetched through registers (global loads during the previous tap's MFMAs,
   // ds_write after them): an LDS-DMA of the next tap made the waitcnt pass drain it with a
   // vmcnt(0) in front of the current tap's reads, so nothing overlapped
-  constexpr int kBL = NPL * CO * 8 / kThreads;  // 16-B pieces per lane per tap
-  static_assert(kBL >= 1 && NPL * CO * 8 % kThreads == 0, "tap staging");
+  constexpr int kPieces = NPL * CO * 8;  // 16-B pieces of one tap
+  constexpr int kBL = (kPieces + kThreads - 1) / kThreads;  // per lane
+  static_assert(kPieces % kThreads == 0 || kPieces < kThreads, "tap staging");
+  constexpr bool kAll = kPieces % kThreads == 0;  // else (16-channel tail blocks) lanes >= kPieces idle
   uint4 bpre[kBL];
   auto load_b = [&](int tap) {
 #pragma unroll
@@ -143,7 +148,7 @@ __global__ __launch_bounds__(64 * waves_of<CO>(), C == 64 ? 4 : (waves_of<CO>() 
       const int pl = idx / (CO * 8), rem = idx - pl * CO * 8;
       const int co = rem >> 3, q = rem & 7;
       const uint32_t off = static_cast<uint32_t>((co * 9 + tap) * (C * 2) + pl * 128 + (q << 4));
-      bpre[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, 0));
+      if (kAll || idx < kPieces) bpre[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, 0));
     }
   };
   auto store_b = [&](int buf) {
@@ -152,7 +157,8 @@ __global__ __launch_bounds__(64 * waves_of<CO>(), C == 64 ? 4 : (waves_of<CO>() 
       const int idx = j * kThreads + threadIdx.x;
       const int pl = idx / (CO * 8), rem = idx - pl * CO * 8;
       const int co = rem >> 3, q = rem & 7;
-      *reinterpret_cast<uint4*>(bbuf + buf * kBBytes + pl * CO * 128 + co * 128 + ((q ^ (co & 7)) << 4)) = bpre[j];
+      if (kAll || idx < kPieces)
+        *reinterpret_cast<uint4*>(bbuf + buf * kBBytes + pl * CO * 128 + co * 128 + ((q ^ (co & 7)) << 4)) = bpre[j];
     }
   };
 
@@ -270,24 +276,28 @@ void launch(const CNArgs& p, int epi, hipStream_t s) {
 
 // The 128-channel kernel holds one workgroup per CU (150 KB of LDS): ResNet-50's 28 x 28 x 128
 // layers at batch 256 are 784 tiles = 3 rounds of 256 + 16, and that last round cost ~20 % of the
-// call (profiles/rd5ah_conv3x3n_tail.jsonl: 85.0 us vs 66.5 at 735 tiles). Its tiles run as 32
-// output channels per workgroup instead: four times the workgroups, a quarter of each wave's MFMAs
-// (64-pixel tiles of a 2-wave kernel kept each wave's work and saved only 2 us, rd5ai).
+// call (profiles/rd5ah_conv3x3n_tail.jsonl: 85.0 us vs 66.5 at 735 tiles). Its tiles run as 16
+// (or, for more than 32 leftover tiles, 32) output channels per workgroup instead: eight (four)
+// times the workgroups, an eighth (a quarter) of each wave's MFMAs; 16 vs 32 measured 75.1-77.8
+// vs 77.6-77.9 us per call (rd5az). 64-pixel tiles of a 2-wave kernel kept each wave's work and
+// saved only 2 us (rd5ai).
 void launch128(CNArgs p, int epi, hipStream_t s) {
   static const int slots = std::getenv("FLUXMPI_CONV3X3N_NOTAIL")
                                ? 0
                                : resident_blocks(reinterpret_cast<const void*>(&conv3x3n_kernel<128, 128, 3>),
                                                  64 * waves_of<128>(), 0);
   const int full = slots > 0 ? p.tiles / slots * slots : 0, rem = p.tiles - full;
-  if (full == 0 || rem == 0 || rem * 4 > slots) {
+  const int ncob = rem * 8 <= slots && C3N_TAIL_CO == 16 ? 8 : (rem * 4 <= slots ? 4 : 1);
+  if (full == 0 || rem == 0 || ncob == 1) {
     launch<128, 128>(p, epi, s);
     return;
   }
   CNArgs t = p;
   p.tiles = full;
   launch<128, 128>(p, epi, s);
-  t.m_base = full * kTM, t.tiles = rem, t.ncob = 4;
-  launch<128, 32>(t, epi, s);
+  t.m_base = full * kTM, t.tiles = rem, t.ncob = ncob;
+  if (ncob == 8) launch<128, 16>(t, epi, s);  // 16 output channels per workgroup: an eighth of the MFMAs
+  else launch<128, 32>(t, epi, s);
 }
 
 }  // namespace
