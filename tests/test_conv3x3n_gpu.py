@@ -10,8 +10,8 @@ pytestmark = pytest.mark.gpu
 
 SHAPES = [(4, 64, 56, 56), (16, 128, 28, 28), (4, 64, 8, 8), (2, 64, 16, 24), (3, 128, 16, 16), (1, 64, 64, 64),
           (2, 128, 32, 32), (16, 64, 7, 16),
-          # more 256-pixel tiles than the 128-channel kernel's resident slots: the leftover tiles run
-          # as 64-pixel tiles of the 2-wave tail kernel
+          # more 256-pixel tiles than the 128-channel kernel's 256 resident slots: the leftover tiles
+          # run as 32-output-channel workgroups (294 tiles: 38 left) or 16-channel ones (272: 16 left)
           (96, 128, 28, 28), (272, 128, 16, 16)]
 
 
