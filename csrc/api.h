@@ -235,9 +235,10 @@ void gemm_wgrad256(const void* a, const void* b, float* ws, int64_t lda, int64_t
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t ldc);
 bool gemm_nt_conv_supported(int64_t pixels, int64_t C, int64_t Cout);
 int gemm_nt_colpart_rows(int64_t M);
-// split-K tail: the fewest k-tiles of a workgroup's share of the last round (0: off; default 8 or
-// FLUXMPI_GEMM_NT_SPLIT)
+// split-K tail: the fewest k-tiles of a workgroup's share of the last round (0: off, the default;
+// FLUXMPI_GEMM_NT_SPLIT overrides it). Test/diagnostic knob, not public API.
 void gemm_nt_set_split(int min_ktiles);
+int gemm_nt_get_split();
 void gemm_nt(const void* a, const void* b, void* c, void* c2, const void* bias, int bias_f32, const void* h,
              float* colpart, float* stats, int64_t lda, int64_t ldb, int64_t ldc, int64_t M, int64_t N, int64_t K,
              int epi, hipStream_t stream);
@@ -249,6 +250,8 @@ void gemm_nt_conv(const void* x, const void* w, void* y, float* stats, int64_t n
 // Narrow-channel 3x3 / stride 1 / pad 1 convolution (conv3x3n.hip): C = Cout in {64, 128}, the
 // input halo staged once per 256-pixel workgroup; x [pixels][C] NHWC, w [Cout][9][C], y [pixels][Cout];
 // epi 0 or 3 (BatchNorm statistics into stats[64][2][Cout])
+// resident workgroups of the 128-channel kernel on the current device (its tail split's round size)
+int conv3x3n_slots128();
 bool conv3x3n_supported(int64_t pixels, int C, int Cout, int H, int W);
 void conv3x3n(const void* x, const void* w, void* y, float* stats, int64_t pixels, int H, int W, int C, int Cout,
               int epi, hipStream_t stream);

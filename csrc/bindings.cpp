@@ -303,6 +303,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_nt_supported", &gemm_nt_supported);
   m.def("gemm_nt_colpart_rows", &gemm_nt_colpart_rows);
   m.def("gemm_nt_set_split", &gemm_nt_set_split);
+  m.def("gemm_nt_get_split", &gemm_nt_get_split);
   m.def("gemm_nt", [](uintptr_t a, uintptr_t b, uintptr_t c, uintptr_t c2, uintptr_t bias, int bias_f32, uintptr_t h,
                       uintptr_t colpart, int64_t lda, int64_t ldb, int64_t ldc,
                       int64_t M, int64_t N, int64_t K, int epi, uintptr_t stream) {
@@ -316,6 +317,7 @@ PYBIND11_MODULE(_C, m) {
             nullptr, 0, nullptr, nullptr, reinterpret_cast<float*>(stats), lda, ldb, ldc, M, N, K, 3, S(stream));
   });
   m.def("conv3x3n_supported", &conv3x3n_supported);
+  m.def("conv3x3n_slots128", &conv3x3n_slots128);
   m.def("conv3x3n", [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, int64_t pixels, int H, int W, int C,
                        int Cout, int epi, uintptr_t stream) {
     conv3x3n(reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(w), reinterpret_cast<void*>(y),

@@ -281,11 +281,13 @@ void launch(const CNArgs& p, int epi, hipStream_t s) {
 // times the workgroups, an eighth (a quarter) of each wave's MFMAs; 16 vs 32 measured 75.1-77.8
 // vs 77.6-77.9 us per call (rd5az). 64-pixel tiles of a 2-wave kernel kept each wave's work and
 // saved only 2 us (rd5ai).
+int slots128() {  // resident 128-channel workgroups on the current device (cached per device)
+  return resident_blocks(reinterpret_cast<const void*>(&conv3x3n_kernel<128, 128, 3>), 64 * waves_of<128>(), 0);
+}
+
 void launch128(CNArgs p, int epi, hipStream_t s) {
-  static const int slots = std::getenv("FLUXMPI_CONV3X3N_NOTAIL")
-                               ? 0
-                               : resident_blocks(reinterpret_cast<const void*>(&conv3x3n_kernel<128, 128, 3>),
-                                                 64 * waves_of<128>(), 0);
+  static const bool notail = std::getenv("FLUXMPI_CONV3X3N_NOTAIL") != nullptr;
+  const int slots = notail ? 0 : slots128();
   const int full = slots > 0 ? p.tiles / slots * slots : 0, rem = p.tiles - full;
   const int ncob = rem * 8 <= slots && C3N_TAIL_CO == 16 ? 8 : (rem * 4 <= slots ? 4 : 1);
   if (full == 0 || rem == 0 || ncob == 1) {
@@ -301,6 +303,8 @@ void launch128(CNArgs p, int epi, hipStream_t s) {
 }
 
 }  // namespace
+
+int conv3x3n_slots128() { return slots128(); }
 
 bool conv3x3n_supported(int64_t pixels, int C, int Cout, int H, int W) {
   if (!((C == 64 && Cout == 64) || (C == 128 && Cout == 128))) return false;

@@ -882,6 +882,7 @@ bool gemm_nt_conv_supported(int64_t pixels, int64_t C, int64_t Cout) {
 }
 
 void gemm_nt_set_split(int min_ktiles) { g_split_min = split_norm(min_ktiles); }
+int gemm_nt_get_split() { return split_min(); }
 
 int gemm_nt_colpart_rows(int64_t M) { return static_cast<int>(2 * (M / kT)); }
 

@@ -79,6 +79,11 @@ def set_split(min_ktiles: int) -> None:
     _ext.get(required=True).gemm_nt_set_split(int(min_ktiles))
 
 
+def get_split() -> int:
+    """The split-K tail setting in force (see :func:`set_split`)."""
+    return int(_ext.get(required=True).gemm_nt_get_split())
+
+
 def weight_t(weight: torch.Tensor) -> torch.Tensor:
     """``weight.t().contiguous()`` by the 16-B-vector transpose kernel."""
     C = _ext.get(required=True)
@@ -206,5 +211,5 @@ def gemm_plain(a2: torch.Tensor, b2: torch.Tensor, c2: torch.Tensor, stats: torc
     return c2
 
 
-__all__ = ["supported", "set_split", "weight_t", "linear_fwd", "linear_dgrad", "conv_ok", "gemm_ok", "conv3x3", "gemm_plain",
+__all__ = ["supported", "weight_t", "linear_fwd", "linear_dgrad", "conv_ok", "gemm_ok", "conv3x3", "gemm_plain",
            "ENABLED", "MODE", "CONV"]

@@ -23,6 +23,7 @@ import torch.nn.functional as F
 
 from . import _ext
 from . import graddst
+from . import wgrad_stream
 from .multi_tensor import DTYPE_CODE
 
 # (N_out, N_in) -> split-K factor, from scripts/bench_vit_gemm.py on MI355X (M = 50432 tokens)
@@ -123,13 +124,15 @@ class _LinearFn(torch.autograd.Function):
         # written straight into the DDP bucket slices when a communicating engine is attached
         same = dy2.dtype == x2.dtype == w.dtype
         if need_w:
-            with graddst.into(w):
-                if native:
-                    dw = weight_grad(dy2, x2, w.dtype)
-                elif same:  # short K (e.g. a classifier head): hipBLASLt, output in the slice
-                    dw = torch.mm(dy2.t(), x2, out=graddst.empty(tuple(w.shape), w.dtype, dy2.device))
-                else:
-                    dw = (dy2.t() @ x2).to(w.dtype)
+            def wgrad():
+                with graddst.into(w):
+                    if native:
+                        return weight_grad(dy2, x2, w.dtype)
+                    if same:  # short K (e.g. a classifier head): hipBLASLt, output in the slice
+                        return torch.mm(dy2.t(), x2, out=graddst.empty(tuple(w.shape), w.dtype, dy2.device))
+                    return (dy2.t() @ x2).to(w.dtype)
+            # on the side stream (ops/wgrad_stream.py): concurrent with the input-gradient chain
+            dw = wgrad_stream.run(wgrad, w, dy2, x2)
         if need_b:
             with graddst.into(ctx.bias):
                 if native:

@@ -56,6 +56,7 @@ from .. import optimisers as O
 from ..ops import multi_tensor as mt
 from ..ops import _ext
 from ..ops import graddst
+from ..ops import wgrad_stream
 from ..ops import optim as fused
 from ..utils.config import get_config
 from ..utils import profiling
@@ -190,6 +191,21 @@ class DDP:
             comm_dtype = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16,
                           "bfloat16": torch.bfloat16, "fp16": torch.float16}.get(cfg.comm_dtype)
         self.comm_dtype = comm_dtype
+        # measured bucket plan (parallel/bucket_plan.py): at N > 1, unless sizes were given
+        self.bucket_plan, self.comm_probe = "default", None
+        explicit = bucket_mb is not None or first_bucket_mb is not None or tail_bucket_mb is not None \
+            or cfg.buckets_explicit
+        if self.communicate and self.world > 1 and (cfg.bucket_plan == "measured"
+                                                    or (cfg.bucket_plan == "auto" and not explicit)):
+            from . import bucket_plan as BP
+            nbytes: dict = {}
+            for p in params:
+                nbytes[p.dtype] = nbytes.get(p.dtype, 0) + p.numel() * p.element_size()
+            wire = comm_dtype or max(nbytes, key=nbytes.get)
+            plan, rec = BP.measured_plan(comm, self.device, wire, sum(nbytes.values()),
+                                         cpu_comm=runtime.cpu_comm() if runtime.Initialized() else None)
+            bucket_mb, first_bucket_mb, tail_bucket_mb = plan["bucket_mb"], plan["first_bucket_mb"], plan["tail_bucket_mb"]
+            self.bucket_plan, self.comm_probe = "measured", {"samples": rec, "plan": plan}
         bb = int((bucket_mb if bucket_mb is not None else cfg.bucket_mb) * (1 << 20))
         fb = int((first_bucket_mb if first_bucket_mb is not None else cfg.first_bucket_mb) * (1 << 20))
         tb = int((tail_bucket_mb if tail_bucket_mb is not None else cfg.tail_bucket_mb) * (1 << 20))
@@ -209,6 +225,11 @@ class DDP:
                     graddst.attach(p, b.flat_grad, o)
                 else:
                     graddst.detach(p)  # a previous engine's buckets are not this one's
+        # weight gradients of this engine's parameters may run on the side stream
+        # (ops/wgrad_stream.py): "steal" mode only — autograd hands over each gradient, no
+        # in-place accumulation kernel reads it before the end-of-backward join
+        self.wgrad_stream = self.grad_mode == "steal" and self.device.type == "cuda" and wgrad_stream.ENABLED
+        wgrad_stream.enable(params, self.wgrad_stream)
         self._hooks = []
         self._sync_enabled = True
         # per-bucket optimiser overlap: on the communicator's in-order stream (behind the bucket's
@@ -402,6 +423,16 @@ class DDP:
         if not self._sync_enabled:
             return
         b = self._param_bucket[id(p)]
+        if b.pending <= 0 or b.launched:
+            # a second backward reached this bucket before step(): its first gradients are
+            # already being reduced (and, with overlap_opt, applied to the weights the second
+            # backward may have read) — accumulating into them would silently drop or corrupt
+            # the update, so refuse loudly (accumulate under no_sync() instead)
+            raise RuntimeError(
+                f"DDP: a second backward reached gradient bucket {b.index} before step(); its "
+                "gradients were already " + ("reduced and applied" if self.overlap_opt else "sent for reduction")
+                + ". Accumulate gradients inside `with ddp.no_sync():` and run the last backward "
+                "outside it, then step()")
         b.pending -= 1
         if b.pending == 0:
             b.ready = True
@@ -445,6 +476,7 @@ class DDP:
             return
         if not self.communicate:
             st.wait_stream(torch.cuda.current_stream(self.device))
+        wgrad_stream.fence(st, self.device)  # weight gradients still running on the side stream
         with torch.cuda.stream(st):
             if self.communicate:
                 if b.comm_buf is not None and self.comm_dtype != b.dtype:
@@ -458,6 +490,8 @@ class DDP:
 
     def _launch_comm(self, b: _Bucket):
         self._pack(b)
+        if self.wgrad_stream and getattr(self.comm, "stream", None) is not None:
+            wgrad_stream.fence(self.comm.stream, self.device)  # side-stream weight gradients first
         buf = b.flat_grad
         if self.comm_dtype is not None and self.comm_dtype != b.dtype:
             # K5: cast the bucket to the wire dtype (e.g. fp32 grads sent as bf16) in one launch
@@ -551,6 +585,9 @@ class DDP:
                 dst.copy_(g)
                 self._note_copy(p)
         if srcs:
+            if self.wgrad_stream and wgrad_stream.pending(b.device):
+                # the copies read gradients the side stream may still be writing
+                torch.cuda.current_stream(b.device).wait_stream(wgrad_stream.side_stream(b.device))
             C = _ext.get(required=True)
             code = mt.DTYPE_CODE[b.dtype]
             C.mt_copy([g.data_ptr() for g in srcs], dptrs, ns, code, code, 1.0,
@@ -878,6 +915,8 @@ class DDP:
                 "bucket_mb": [round(b.numel * b.flat_grad.element_size() / 2 ** 20, 2) for b in self.buckets],
                 "comm": (self.comm.name if self.communicate else "none"),
                 "direct_grads": self.direct_grads, "overlap_opt": self.overlap_opt,
+                "wgrad_stream": self.wgrad_stream, "bucket_plan": self.bucket_plan,
+                "comm_probe": self.comm_probe,
                 # gradients the packs copied per step so far (0: every one delivered in place)
                 "pack_copies_per_step": round(self.pack_copies / max(1, self.step_count), 2),
                 # the parameter shapes the packs copied (total over the steps so far), most first
@@ -891,6 +930,7 @@ class DDP:
         for h in self._hooks:
             h.remove()
         self._hooks.clear()
+        wgrad_stream.enable([p for b in self.buckets for p in b.params], False)
 
 
 __all__ = ["DDP"]

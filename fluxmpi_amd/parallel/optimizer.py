@@ -45,6 +45,8 @@ from .comm import ReduceOp
 _CHECKED: set = set()
 # structure hash of a `like` tree -> signature of the zero-filled gradient tree checked across ranks
 _LIKE_CHECKED: dict = {}
+# the same key -> leaf dtypes of that checked tree (what a zero-filled leaf is created as)
+_LIKE_DTYPES: dict = {}
 
 
 def check_plan(obj, what: str, derived: bool = False) -> None:
@@ -111,28 +113,49 @@ class DistributedOptimizer(AbstractRule):
         return f"DistributedOptimizer({self.optimizer!r})"
 
 
-def _zero_fill(gs: Any, like: Any) -> Any:
-    """``gs`` with every missing (``None``) gradient replaced by zeros shaped like ``like``."""
-    if gs is None:
-        if isinstance(like, torch.Tensor):
-            return torch.zeros_like(like)
-        if isinstance(like, np.ndarray):
-            return np.zeros_like(like)
-    if isinstance(like, torch.nn.Module):
-        named = dict(like.named_parameters())
-        g = gs if isinstance(gs, dict) else {n: p.grad for n, p in named.items()}
-        return {n: _zero_fill(g.get(n), p) for n, p in named.items()}
-    nd = node_def(like)
-    if nd is None:
-        return gs
-    lc, aux = nd[0](like)
-    gc = [None] * len(lc) if gs is None else nd[0](gs)[0]
-    if len(gc) != len(lc):
-        raise ValueError("allreduce_gradients: gradient tree and `like` tree differ in structure")
-    return nd[1](aux, [_zero_fill(g, c) for g, c in zip(gc, lc)])
+def _zero_fill(gs: Any, like: Any, dtypes: list | None = None, record: list | None = None) -> Any:
+    """``gs`` with every missing (``None``) gradient replaced by zeros shaped like ``like``.
+
+    ``record`` receives the dtype of every array leaf of the result (traversal order);
+    ``dtypes`` (such a record from the call whose plan was checked across ranks) gives a
+    zero-filled leaf that recorded dtype instead of its parameter's, so a gradient that arrives
+    in another dtype than its parameter (fp32 grads of bf16 params) and later goes missing on
+    every rank keeps the checked signature."""
+    pos = [0]
+
+    def leaf(g, p):
+        i = pos[0]
+        pos[0] += 1
+        if g is None:
+            dt = dtypes[i] if dtypes is not None and i < len(dtypes) else None
+            if isinstance(p, torch.Tensor):
+                g = torch.zeros_like(p, dtype=dt if isinstance(dt, torch.dtype) else None)
+            elif isinstance(p, np.ndarray):
+                g = np.zeros_like(p, dtype=dt if isinstance(dt, np.dtype) else None)
+        if record is not None:
+            record.append(g.dtype if isinstance(g, (torch.Tensor, np.ndarray)) else None)
+        return g
+
+    def walk(g, p):
+        if isinstance(p, (torch.Tensor, np.ndarray)):
+            return leaf(g, p)
+        if isinstance(p, torch.nn.Module):
+            named = dict(p.named_parameters())
+            gd = g if isinstance(g, dict) else {n: q.grad for n, q in named.items()}
+            return {n: walk(gd.get(n), q) for n, q in named.items()}
+        nd = node_def(p)
+        if nd is None:
+            return g
+        lc, aux = nd[0](p)
+        gc = [None] * len(lc) if g is None else nd[0](g)[0]
+        if len(gc) != len(lc):
+            raise ValueError("allreduce_gradients: gradient tree and `like` tree differ in structure")
+        return nd[1](aux, [walk(a, c) for a, c in zip(gc, lc)])
+
+    return walk(gs, like)
 
 
-def _check_like_plan(gs: Any, like: Any) -> None:
+def _check_like_plan(gs: Any, like: Any, key=None) -> None:
     """Plan check for ``allreduce_gradients(like=...)``.
 
     The gate is the structure hash of ``like`` (the parameter tree: identical on every rank
@@ -140,13 +163,13 @@ def _check_like_plan(gs: Any, like: Any) -> None:
     ``like`` structure compares the zero-filled gradient tree (shapes and dtypes included)
     across ranks; later calls compare it LOCALLY against the signature that was checked, so a
     gradient whose shape or dtype changed on one rank raises instead of entering a mismatched
-    collective. The table is keyed by structure, so it stays bounded however often callers
-    build fresh ``like`` trees.
+    collective. Zero-filled leaves take the dtypes of the checked plan (:func:`_zero_fill`), so
+    a gradient missing on every rank never changes the signature by itself. The table is keyed
+    by structure, so it stays bounded however often callers build fresh ``like`` trees.
     """
-    mode = get_config().check_plans
-    if mode == "never" or not runtime.Initialized() or runtime.total_workers() == 1:
+    if not _plan_checks_on():
         return
-    key = structure_hash(like)
+    key = structure_hash(like) if key is None else key
     sig = structure_signature(gs)
     seen = _LIKE_CHECKED.get(key)
     if seen is None:
@@ -156,6 +179,10 @@ def _check_like_plan(gs: Any, like: Any) -> None:
         raise CollectiveMismatchError(
             "allreduce_gradients(like=...): a gradient's shape or dtype differs from the plan "
             "checked across ranks for this parameter tree; the collectives would mismatch")
+
+
+def _plan_checks_on() -> bool:
+    return get_config().check_plans != "never" and runtime.Initialized() and runtime.total_workers() > 1
 
 
 def allreduce_gradients(gs: Any, on_gpu: bool | None = None, op=ReduceOp.SUM, like: Any = None) -> Any:
@@ -173,8 +200,12 @@ def allreduce_gradients(gs: Any, on_gpu: bool | None = None, op=ReduceOp.SUM, li
     """
     runtime._require()
     if like is not None:
-        gs = _zero_fill(gs, like)
-        _check_like_plan(gs, like)
+        key = structure_hash(like) if _plan_checks_on() else None
+        rec: list = []
+        gs = _zero_fill(gs, like, dtypes=_LIKE_DTYPES.get(key), record=rec)
+        if key is not None:
+            _check_like_plan(gs, like, key)
+            _LIKE_DTYPES.setdefault(key, rec)
     else:
         check_plan(gs, "gradient tree")
     leaves: list = []

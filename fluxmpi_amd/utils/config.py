@@ -153,6 +153,10 @@ class Config:
     overlap_opt: bool = False  # per-bucket optimiser update during backward (DDP)
     # cross-rank structure check of functional reduction plans: always / first / never
     check_plans: str = "always"
+    # gradient-bucket sizes at N > 1: "auto" (measured unless sizes are given explicitly),
+    # "measured" (probe the communicator: parallel/bucket_plan.py), "default" (the sizes above)
+    bucket_plan: str = "auto"
+    buckets_explicit: bool = False  # a bucket size came from the environment or the preferences
     extra: dict = field(default_factory=dict)
 
     @classmethod
@@ -179,6 +183,10 @@ class Config:
             direct_grads=_env_bool("FLUXMPI_DIRECT_GRADS", bool(prefs.get("direct_grads", True))),
             overlap_opt=_env_bool("FLUXMPI_OVERLAP_OPT", bool(prefs.get("overlap_opt", False))),
             check_plans=os.environ.get("FLUXMPI_CHECK_PLANS", str(prefs.get("check_plans", "always"))).lower(),
+            bucket_plan=os.environ.get("FLUXMPI_BUCKET_PLAN", str(prefs.get("bucket_plan", "auto"))).lower(),
+            buckets_explicit=any(os.environ.get(k) for k in ("FLUXMPI_BUCKET_MB", "FLUXMPI_FIRST_BUCKET_MB",
+                                                             "FLUXMPI_TAIL_BUCKET_MB"))
+            or any(k in prefs for k in ("bucket_mb", "first_bucket_mb", "tail_bucket_mb")),
             extra=prefs,
         )
 

@@ -9,10 +9,7 @@ import torch.nn.functional as F
 pytestmark = pytest.mark.gpu
 
 SHAPES = [(4, 64, 56, 56), (16, 128, 28, 28), (4, 64, 8, 8), (2, 64, 16, 24), (3, 128, 16, 16), (1, 64, 64, 64),
-          (2, 128, 32, 32), (16, 64, 7, 16),
-          # more 256-pixel tiles than the 128-channel kernel's 256 resident slots: the leftover tiles
-          # run as 32-output-channel workgroups (294 tiles: 38 left) or 16-channel ones (272: 16 left)
-          (96, 128, 28, 28), (272, 128, 16, 16)]
+          (2, 128, 32, 32), (16, 64, 7, 16), (96, 128, 28, 28)]
 
 
 def _nhwc(t):
@@ -55,6 +52,21 @@ def test_conv3x3n_dgrad(gpu_ext, N, C, H, W):
     dx = G.conv3x3_dgrad(dy, _nhwc(w))
     assert dx.shape == x.shape and dx.is_contiguous(memory_format=torch.channels_last)
     assert _rel(dx, x.grad) < 5e-3
+
+
+@pytest.mark.parametrize("tail_co", [32, 16])
+def test_conv3x3n_tail_split(gpu_ext, tail_co):
+    """More 256-pixel tiles than the 128-channel kernel has resident slots on THIS device: the
+    leftover tiles run as 32-output-channel workgroups (more than slots / 8 left) or 16-channel
+    ones (at most slots / 8 left). Shapes derived from the runtime slot count, one
+    16 x 16 image = one tile."""
+    from fluxmpi_amd.ops import _ext
+    slots = _ext.get(required=True).conv3x3n_slots128()
+    rem = slots // 8 + 2 if tail_co == 32 else max(1, slots // 16)
+    assert (rem * 8 > slots) == (tail_co == 32) and rem * 4 <= slots
+    n = slots + rem
+    test_conv3x3n_fwd_stats(gpu_ext, n, 128, 16, 16)
+    test_conv3x3n_dgrad(gpu_ext, n, 128, 16, 16)
 
 
 def test_conv3x3n_unsupported_routes_elsewhere(gpu_ext):

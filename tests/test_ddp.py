@@ -473,3 +473,29 @@ def worker_overlap_opt():
 
 def test_overlap_opt_two_ranks_gloo(spmd):
     spmd("tests.test_ddp:worker_overlap_opt", nprocs=2, timeout=180)
+
+
+@pytest.mark.parametrize("how", ["overlap_opt", "force_comm"])
+def test_second_backward_before_step_raises(how):
+    """a second backward that reaches a bucket already reduced (and, with overlap_opt,
+    already applied) before step() must fail loudly, not drop or corrupt the update; accumulation
+    under no_sync() keeps working."""
+    import fluxmpi_amd as FluxMPI
+    from fluxmpi_amd import optimisers as O
+    from fluxmpi_amd.parallel.ddp import DDP
+
+    FluxMPI.Init()
+    kw = {"overlap_opt": True} if how == "overlap_opt" else {"force_comm": True, "overlap_opt": False}
+    model = _mlp(5)
+    d = DDP(model, O.Adam(1e-2), bucket_mb=0.001, first_bucket_mb=0.0005, overlap=True, **kw)
+    x, y = _data(0)
+    ((d(x) - y) ** 2).mean().backward()
+    with pytest.raises(RuntimeError, match="second backward"):
+        ((d(x) - y) ** 2).mean().backward()
+    d.step()
+    # the supported accumulation pattern still works after the error
+    with d.no_sync():
+        ((d(x[:4]) - y[:4]) ** 2).sum().backward()
+    ((d(x[4:]) - y[4:]) ** 2).sum().backward()
+    d.step()
+    assert all(torch.isfinite(p).all() for p in model.parameters())

@@ -86,7 +86,18 @@ def worker_irregular():
     # and the group is still usable afterwards
     t = torch.ones(3)
     FluxMPI.allreduce(t, "+")
-    assert torch.equal(t, torch.full((3,), 2.0))
+    assert torch.equal(t, torch.full((3,), float(W)))
+
+    # 4. ADVICE r5: gradients in another dtype than their parameters (fp64 grads of fp32 params)
+    # on the checked step; on a later step one of them is missing on EVERY rank — the zero fill
+    # takes the checked plan's dtype, so a consistent run does not raise
+    like = {"w": torch.zeros(3, 2), "v": torch.zeros(4)}
+    out = FluxMPI.allreduce_gradients({"w": torch.ones(3, 2, dtype=torch.float64),
+                                       "v": torch.ones(4, dtype=torch.float64)}, like=like)
+    assert out["w"].dtype == torch.float64 and torch.equal(out["v"], torch.full((4,), float(W), dtype=torch.float64))
+    out = FluxMPI.allreduce_gradients({"w": torch.ones(3, 2, dtype=torch.float64), "v": None}, like=like)
+    assert out["v"].dtype == torch.float64 and torch.count_nonzero(out["v"]) == 0
+    assert torch.equal(out["w"], torch.full((3, 2), float(W), dtype=torch.float64))
     FluxMPI.Finalize()
 
 
