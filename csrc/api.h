@@ -247,6 +247,16 @@ void gemm_nt(const void* a, const void* b, void* c, void* c2, const void* bias, 
 // or 4 (y = bf16(bf16(conv) + residual), residual laid out as y)
 void gemm_nt_conv(const void* x, const void* w, void* y, float* stats, int64_t nimg, int H, int W, int C,
                   int64_t Cout, int epi, hipStream_t stream, const void* residual = nullptr);
+// 3x3 / pad 1 / stride 1-2 convolution over a 3-channel NHWC bf16 image (conv_c3.hip), Cout % 128 == 0:
+// forward y [pixels][Cout] from w_pairs [Cout][14] (the channels_last filter's 27 taps x channels as
+// packed bf16 pairs, the 28th element 0); filter gradient as fp32 partials [blocks][Cout][27]
+// (reduce with gemm_splitk_reduce into the [Cout][3][3][3] channels_last filter order)
+bool conv_c3_supported(int64_t N, int H, int W, int stride, int Cout);
+int64_t conv_c3_wgrad_blocks(int64_t N, int H, int W, int stride);
+void conv_c3_fwd(const void* x, const void* w_pairs, void* y, int64_t N, int H, int W, int stride, int Cout,
+                 hipStream_t stream);
+void conv_c3_wgrad(const void* x, const void* dy, float* part, int64_t N, int H, int W, int stride, int Cout,
+                   hipStream_t stream);
 // Narrow-channel 3x3 / stride 1 / pad 1 convolution (conv3x3n.hip): C = Cout in {64, 128}, the
 // input halo staged once per 256-pixel workgroup; x [pixels][C] NHWC, w [Cout][9][C], y [pixels][Cout];
 // epi 0 or 3 (BatchNorm statistics into stats[64][2][Cout])

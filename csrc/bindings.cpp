@@ -316,6 +316,18 @@ PYBIND11_MODULE(_C, m) {
     gemm_nt(reinterpret_cast<const void*>(a), reinterpret_cast<const void*>(b), reinterpret_cast<void*>(c), nullptr,
             nullptr, 0, nullptr, nullptr, reinterpret_cast<float*>(stats), lda, ldb, ldc, M, N, K, 3, S(stream));
   });
+  m.def("conv_c3_supported", &conv_c3_supported);
+  m.def("conv_c3_wgrad_blocks", &conv_c3_wgrad_blocks);
+  m.def("conv_c3_fwd", [](uintptr_t x, uintptr_t w, uintptr_t y, int64_t N, int H, int W, int stride, int Cout,
+                          uintptr_t stream) {
+    conv_c3_fwd(reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(w), reinterpret_cast<void*>(y), N, H,
+                W, stride, Cout, S(stream));
+  });
+  m.def("conv_c3_wgrad", [](uintptr_t x, uintptr_t dy, uintptr_t part, int64_t N, int H, int W, int stride, int Cout,
+                            uintptr_t stream) {
+    conv_c3_wgrad(reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(dy), reinterpret_cast<float*>(part),
+                  N, H, W, stride, Cout, S(stream));
+  });
   m.def("conv3x3n_supported", &conv3x3n_supported);
   m.def("conv3x3n_slots128", &conv3x3n_slots128);
   m.def("conv3x3n", [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, int64_t pixels, int H, int W, int C,

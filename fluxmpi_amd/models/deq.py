@@ -50,6 +50,11 @@ GRAPH_CHUNK = 5
 # (fp32 alike, Anderson m = 5 / 8 alike: 3e-2 at 10, 1e-2 at ~22). With the solver graphs the
 # test runs on each 5-iteration period's best residual, read one period late, so a solve stops
 # 5-9 iterations after the iterate that met the tolerance.
+# Keeping the trained cell contractive (ResidualCell.constrain_, run before every training
+# forward): "conv" = max-norm projection of each conv output channel's filter onto the ball of
+# its expected init norm; "conv+gn" also clamps n3's GroupNorm gain (it multiplies the whole
+# Jacobian) to [-1, 1]; "none" = off.
+CONSTRAIN = os.environ.get("FLUXMPI_DEQ_CONSTRAIN", "none")
 DEQ_MNIST_SOLVER = {"max_iter": 30, "tol": 1e-3, "bwd_iter": 30, "bwd_tol": 1e-3}
 DEQ_CIFAR_SOLVER = {"max_iter": 30, "tol": 2e-2, "bwd_iter": 30, "bwd_tol": 1e-2}
 
@@ -408,6 +413,8 @@ class DEQFixedPoint(nn.Module):
         return gs
 
     def forward(self, x):
+        if self.training and CONSTRAIN != "none" and hasattr(self.f, "constrain_"):
+            self.f.constrain_(CONSTRAIN)
         gs = self._graphs_for(x)
         # the cell's GroupNorm parameters cast to fp32 once for the ~30 calls below (into the
         # graphs' static buffers when the solver loops replay graphs)
@@ -515,6 +522,21 @@ class ResidualCell(nn.Module):
         self.n1, self.n2, self.n3 = (FusedGroupNorm(groups, ch) for _ in range(3))
         for c in (self.conv1, self.conv2):
             nn.init.normal_(c.weight, 0, 0.01)
+        # expected per-output-channel filter norm at init (the max-norm radius of constrain_)
+        self.max_norm = 0.01 * (9 * ch) ** 0.5
+
+    @torch.no_grad()
+    def constrain_(self, mode: str = "conv") -> None:
+        """Project the cell back into a contractive set after an optimiser step: each conv output
+        channel's filter onto the ball of radius ``max_norm`` (in place; a no-op for channels
+        inside it), and with ``"conv+gn"`` n3's gain into [-1, 1]. In-place edits bump the
+        parameters' versions, so a DDP engine re-reads its fp32 masters from them."""
+        for c in (self.conv1, self.conv2):
+            w = c.weight
+            n = w.float().square().sum((1, 2, 3), keepdim=True).sqrt_()
+            w.mul_((self.max_norm / n.clamp_min(1e-12)).clamp_(max=1.0).to(w.dtype))
+        if mode == "conv+gn" and self.n3.weight is not None:
+            self.n3.weight.clamp_(-1.0, 1.0)
 
     def _conv(self, conv, t, link=None):
         # bf16 channels_last on the GPU: the implicit-GEMM MFMA kernels (ops/fused_block.conv3x3,

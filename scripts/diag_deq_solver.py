@@ -1,0 +1,82 @@
+#!/usr/bin/env python
+"""Why does the trained DEQ cell's forward solve stop at its cap? Trains the bench loop for --train
+steps, then solves the trained cell's fixed point for the bench batch with no early stop and prints
+the final relative residual after k iterations for: Anderson m = 5 (the bench), m = 8 / 12, damping
+beta = 0.8, plain fixed-point iteration (m = 1), and the same cell in fp32 (PyTorch ops). A curve that
+keeps falling = a slow contraction; one that flattens = the evaluation-noise floor.
+    python scripts/diag_deq_solver.py --model deq --train 40"""
+import argparse
+import copy
+import json
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="deq")
+    ap.add_argument("--train", type=int, default=40)
+    ap.add_argument("--batch", type=int, default=256)
+    a = ap.parse_args()
+    import fluxmpi_amd as FluxMPI
+    from fluxmpi_amd import optimisers as O
+    from fluxmpi_amd.models import build_model
+    from fluxmpi_amd.models import deq as D
+    from fluxmpi_amd.parallel.ddp import DDP
+    FluxMPI.Init()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(1234)
+    model = build_model(a.model).to(dev, memory_format=torch.channels_last)
+    for m in model.modules():
+        if not (isinstance(m, torch.nn.modules.batchnorm._BatchNorm) or type(m).__name__ == "FusedBatchNorm2d"):
+            for p in m.parameters(recurse=False):
+                p.data = p.data.to(torch.bfloat16)
+    ddp = DDP(model, O.Adam(1e-3), average=True)
+    cin, img = {"deq": (1, 28), "deq_cifar": (3, 32)}[a.model]
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(a.batch, cin, img, img, device=dev, generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (a.batch,), device=dev, generator=g)
+    for s in range(a.train + 1):
+        if s in (0, a.train):
+            # the injected input of the implicit layer, as the bench's forward computes it
+            with torch.no_grad():
+                captured = {}
+                h = model.deq.register_forward_pre_hook(lambda mod, args: captured.setdefault("x", args[0].detach().clone()))
+                model(x)
+                h.remove()
+            xin = captured["x"]
+            cell = model.deq.f
+            runs = [("m5", 5, 1.0, cell, xin), ("m8", 8, 1.0, cell, xin), ("m12", 12, 1.0, cell, xin),
+                    ("m5_beta0.8", 5, 0.8, cell, xin), ("picard", 1, 1.0, cell, xin)]
+            c32 = copy.deepcopy(cell).float()
+            runs.append(("m5_fp32", 5, 1.0, c32, xin.float()))
+            for name, mm, beta, c, xi in runs:
+                raw = D.MANUAL_VJP and c.manual_ok(xi)
+                fz = D._CellEval(c, xi, raw)
+                curve = {}
+                for k in (5, 10, 15, 20, 30, 45, 60, 80):
+                    with torch.no_grad(), D.fp32_affine_cache(c):
+                        if mm == 1:
+                            z = torch.zeros_like(xi)
+                            for _ in range(k):
+                                fzv = fz(z)
+                                r = float((fzv.float() - z.float()).norm() / (1e-5 + fzv.float().norm()))
+                                z = fzv
+                            res = r
+                        else:
+                            _, _, res = D.anderson(fz, torch.zeros_like(xi), m=mm, max_iter=k, tol=0.0, beta=beta,
+                                                   check_lag=0)
+                    curve[k] = float(res)
+                print(json.dumps({"model": a.model, "trained_steps": s, "solver": name, "res_at_iter": curve}), flush=True)
+        if s < a.train:
+            F.cross_entropy(ddp(x).float(), y).backward()
+            ddp.step()
+
+
+if __name__ == "__main__":
+    main()

@@ -3,10 +3,12 @@
 * ``@pytest.mark.gpu`` marks tests that need an MI355X (run on the GPU box
   with ``pytest -m gpu``); everything else runs on CPU.
 * :func:`run_spmd` mirrors the reference's test driver (``test/runtests.jl``):
-  a test body is an SPMD program executed by N ranks (default
-  ``FLUXMPI_TEST_NPROCS`` = 2, like ``clamp(CPU_THREADS, 2, 4)``) over the gloo
-  backend; assertions run inside every rank and the parent checks the exit
-  codes.
+  a test body is an SPMD program executed by N ranks over the gloo backend
+  (default ``FLUXMPI_TEST_NPROCS``, else ``clamp(cpu_count, 2, 4)`` exactly as the
+  reference's driver, ``/root/reference/test/runtests.jl:3-4``: 4 on CI machines);
+  assertions run inside every rank and the parent checks the exit codes. Tests
+  that need a specific world (3-rank uneven shards, 8-rank wire sums, GPU
+  rehearsals) pass ``nprocs`` explicitly.
 """
 import os
 import sys
@@ -28,10 +30,16 @@ def pytest_configure(config):
         load_variant.install()
 
 
+def default_nprocs() -> int:
+    """``FLUXMPI_TEST_NPROCS`` or ``clamp(cpu_count, 2, 4)`` (the reference's ``runtests.jl:4``)."""
+    v = os.environ.get("FLUXMPI_TEST_NPROCS")
+    return int(v) if v else max(2, min(4, os.cpu_count() or 2))
+
+
 def run_spmd(target: str, nprocs: int | None = None, env: dict | None = None, timeout: float = 300.0):
     from fluxmpi_amd.launch import launch
 
-    n = nprocs or int(os.environ.get("FLUXMPI_TEST_NPROCS", "2"))
+    n = nprocs or default_nprocs()
     e = {
         "PYTHONPATH": ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""),
         "FLUXMPI_BACKEND": "gloo",

@@ -30,7 +30,7 @@ def worker_checks():
 
 
 def test_replica_and_structure_checks(spmd):
-    spmd("tests.test_aux:worker_checks", nprocs=2)
+    spmd("tests.test_aux:worker_checks")
 
 
 def test_watchdog_detects_async_error():
@@ -220,4 +220,4 @@ def worker_calibrate_cpu():
 
 
 def test_calibrate_cpu(spmd):
-    spmd("tests.test_aux:worker_calibrate_cpu", nprocs=2, timeout=120)
+    spmd("tests.test_aux:worker_calibrate_cpu", timeout=120)

@@ -26,11 +26,12 @@ def worker():
     assert math.isclose(float(total), float(data.double().sum()), rel_tol=1e-6)
     # list-of-samples datasets + fancy indexing
     ds = DistributedDataContainer(list(range(10)))
-    assert ds[0] == ds.idxs[0] and ds[[0, 1]] == [ds.idxs[0], ds.idxs[1]]
+    j = len(ds) - 1
+    assert ds[0] == ds.idxs[0] and ds[[0, j]] == [ds.idxs[0], ds.idxs[j]]
     FluxMPI.Finalize()
 
 
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 4])
 def test_data(spmd, n):
     spmd("tests.test_data:worker", nprocs=n)
 

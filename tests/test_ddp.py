@@ -80,7 +80,8 @@ def _ddp_checks(grad_mode):
             for p in ref.parameters():
                 p -= 0.1 * p.grad
     for p, q in zip(model.parameters(), ref.parameters()):
-        torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-5, atol=1e-6)
+        # the reference's tolerance (test/test_optimizer.jl:20-26): W-rank fp32 sums in another order
+        torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-5, atol=1e-5)
     # ranks hold identical parameters
     for p in model.parameters():
         g = FluxMPI.allgather(p.detach().clone())
@@ -110,7 +111,7 @@ def _ddp_checks(grad_mode):
 
 
 def test_ddp_gloo(spmd):
-    spmd("tests.test_ddp:worker_ddp", nprocs=2)
+    spmd("tests.test_ddp:worker_ddp")
 
 
 def worker_ddp_resnet():
@@ -149,7 +150,7 @@ def worker_ddp_resnet():
 
 
 def test_ddp_resnet_gloo(spmd):
-    spmd("tests.test_ddp:worker_ddp_resnet", nprocs=2)
+    spmd("tests.test_ddp:worker_ddp_resnet")
 
 
 def test_bucket_launch_order_mixed_dtypes():
@@ -260,7 +261,7 @@ def worker_ddp_no_zero_grad():
 
 
 def test_ddp_no_zero_grad_gloo(spmd):
-    spmd("tests.test_ddp:worker_ddp_no_zero_grad", nprocs=2, timeout=120)
+    spmd("tests.test_ddp:worker_ddp_no_zero_grad", timeout=120)
 
 
 def test_ddp_master_follows_outside_param_changes(tmp_path):
@@ -386,7 +387,7 @@ def worker_ddp_master_sync():
 
 
 def test_ddp_master_sync_gloo(spmd):
-    spmd("tests.test_ddp:worker_ddp_master_sync", nprocs=2, timeout=120)
+    spmd("tests.test_ddp:worker_ddp_master_sync", timeout=120)
 
 
 def worker_ddp_frozen_param_sync():
@@ -412,7 +413,7 @@ def worker_ddp_frozen_param_sync():
 
 
 def test_ddp_frozen_param_sync_gloo(spmd):
-    spmd("tests.test_ddp:worker_ddp_frozen_param_sync", nprocs=2, timeout=120)
+    spmd("tests.test_ddp:worker_ddp_frozen_param_sync", timeout=120)
 
 
 def test_engine_registry_does_not_keep_engines_alive():
@@ -472,7 +473,7 @@ def worker_overlap_opt():
 
 
 def test_overlap_opt_two_ranks_gloo(spmd):
-    spmd("tests.test_ddp:worker_overlap_opt", nprocs=2, timeout=180)
+    spmd("tests.test_ddp:worker_overlap_opt", timeout=180)
 
 
 @pytest.mark.parametrize("how", ["overlap_opt", "force_comm"])

@@ -681,7 +681,7 @@ def worker_deq_cifar_functional():
 
 
 def test_deq_cifar_functional_gloo(spmd):
-    spmd("tests.test_deq:worker_deq_cifar_functional", nprocs=2, timeout=300)
+    spmd("tests.test_deq:worker_deq_cifar_functional", timeout=300)
 
 
 def worker_functional_bf16_masters():
@@ -739,4 +739,4 @@ def worker_functional_bf16_masters():
 
 
 def test_functional_bf16_masters_gloo(spmd):
-    spmd("tests.test_deq:worker_functional_bf16_masters", nprocs=2, timeout=300)
+    spmd("tests.test_deq:worker_functional_bf16_masters", timeout=300)

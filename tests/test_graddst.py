@@ -120,7 +120,7 @@ def worker_graddst():
             assert ddp.pack_copies - before == (1 if shared else 0)
         ref = _reference(shared, W, 3, 0.1)
         for p, q in zip(model.parameters(), ref.parameters()):
-            torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-5, atol=1e-6)
+            torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-5, atol=1e-5)
         # gradient accumulation: two half batches under no_sync == one full batch
         with ddp.no_sync():
             ((ddp(x[:4]) - y[:4]) ** 2).sum().backward()
@@ -153,12 +153,12 @@ def worker_graddst():
             for p, g0 in zip(ref.parameters(), grads[0]):
                 p -= 0.1 * (g0 if len(grads) == 1 else p.grad + g0)
     for p, q in zip(model.parameters(), ref.parameters()):
-        torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-5, atol=1e-5)
     FluxMPI.Finalize()
 
 
 def test_graddst_gloo(spmd):
-    spmd("tests.test_graddst:worker_graddst", nprocs=2, timeout=120)
+    spmd("tests.test_graddst:worker_graddst", timeout=120)
 
 
 def test_no_attachment_without_communication():

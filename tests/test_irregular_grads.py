@@ -25,7 +25,6 @@ def worker_irregular():
 
     FluxMPI.Init()
     r, W = FluxMPI.local_rank(), FluxMPI.total_workers()
-    assert W == 2
 
     # 1. DistributedOptimizer: rank 1 has no gradient for "b" (DEQ-style irregular tree)
     ps = _params()
@@ -46,7 +45,7 @@ def worker_irregular():
     if r == 0:
         grads["c"] = None
     st, ps = O.update_(st, ps, grads)
-    total_c = _grad(1, "c")
+    total_c = sum(_grad(k, "c") for k in range(1, W))
     torch.testing.assert_close(ps["c"], _params()["c"] - 0.1 * total_c)
 
     # 2. allreduce_gradients with the parameter tree: zero-filled sum
@@ -54,15 +53,15 @@ def worker_irregular():
     if r == 1:
         grads["a"] = None
     out = FluxMPI.allreduce_gradients(grads, like=_params())
-    torch.testing.assert_close(out["a"], _grad(0, "a"))
-    torch.testing.assert_close(out["b"], _grad(0, "b") + _grad(1, "b"))
+    torch.testing.assert_close(out["a"], sum(_grad(k, "a") for k in range(W) if k != 1))
+    torch.testing.assert_close(out["b"], sum(_grad(k, "b") for k in range(W)))
     # a fresh `like` tree of the same structure (new object every step) skips the cross-rank
     # check on every rank; a gradient whose shape changed on one rank raises there instead of
     # entering a mismatched collective (the others are not sent into the collective either:
     # the same step raises the same way on the rank that differs, and we stop here)
     grads = {n: _grad(r, n) for n in ps}
     out = FluxMPI.allreduce_gradients(grads, like=_params())
-    torch.testing.assert_close(out["c"], _grad(0, "c") + _grad(1, "c"))
+    torch.testing.assert_close(out["c"], sum(_grad(k, "c") for k in range(W)))
     grads = {n: _grad(r, n) for n in ps}
     grads["c"] = torch.zeros(4) if r == 1 else grads["c"]
     if r == 1:
@@ -102,7 +101,7 @@ def worker_irregular():
 
 
 def test_irregular_gradient_trees(spmd):
-    spmd("tests.test_irregular_grads:worker_irregular", nprocs=2, timeout=120)
+    spmd("tests.test_irregular_grads:worker_irregular", timeout=120)
 
 
 def test_zero_fill_only_for_collective_rules():

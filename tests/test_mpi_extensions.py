@@ -204,4 +204,4 @@ def worker_bench_selfcheck():
 
 
 def test_bench_comm_selfcheck_cpu(spmd):
-    spmd("tests.test_mpi_extensions:worker_bench_selfcheck", nprocs=2, timeout=120)
+    spmd("tests.test_mpi_extensions:worker_bench_selfcheck", timeout=120)
