@@ -194,7 +194,11 @@ struct GemmProblem {
   // stride-2 1x1 convolution without the strided copy of its input. Plain K-major A only.
   int a_sub_h = 0, a_sub_w = 0;
   // LDS-DMA kernel, implicit conv: conv_s == 2 — a 3x3 / stride 2 / pad 1 convolution over the
-  // NHWC image [M/(Ho*Wo)][conv_h][conv_w][conv_c] (conv_h / conv_w the INPUT size, Ho = ceil(H/2))
+  // NHWC image [M/(Ho*Wo)][conv_h][conv_w][conv_c] (conv_h / conv_w the INPUT size, Ho = ceil(H/2));
+  // conv_s == 16 + (2 py + px) — parity class (py, px) of that convolution's INPUT gradient: A = dY
+  // [M/(Ho*Wo)][conv_h = Ho][conv_w = Wo][conv_c = Cout], B = the flipped transposed filter
+  // [N = Cin][3][3][Cout] (ldb >= 9 Cout), K = taps * Cout (1, 2, 2, 4 taps), C row (img, a, b) =
+  // dX pixel (img, 2a + py, 2b + px) of [.][2 Ho][2 Wo] (even input sizes)
   int conv_s = 1;
 };
 void gemm_bf16(const GemmProblem& g, hipStream_t stream);
@@ -247,6 +251,14 @@ void gemm_nt(const void* a, const void* b, void* c, void* c2, const void* bias, 
 // or 4 (y = bf16(bf16(conv) + residual), residual laid out as y)
 void gemm_nt_conv(const void* x, const void* w, void* y, float* stats, int64_t nimg, int H, int W, int C,
                   int64_t Cout, int epi, hipStream_t stream, const void* residual = nullptr);
+// A token-major Linear's input and weight gradients in one launch (linbwd.hip): dx [M][K] =
+// dy [M][N] W [N][K] (bf16, nullptr: skip) and the weight gradient's fp32 split-K partials
+// ws [s][N][K] of dy^T x (nullptr: skip; s = linear_bwd_splits(M, N, K, splits), sum them with
+// gemm_splitk_reduce). M, N, K multiples of 256.
+bool linear_bwd_supported(int64_t M, int64_t N, int64_t K, int64_t ldy, int64_t ldx, int64_t ldw, int64_t lddx);
+int linear_bwd_splits(int64_t M, int64_t N, int64_t K, int splits);
+void linear_bwd(const void* dy, const void* x, const void* w, void* dx, float* ws, int64_t M, int64_t N, int64_t K,
+                int64_t ldy, int64_t ldx, int64_t ldw, int64_t lddx, int splits, int dg_first, hipStream_t stream);
 // 3x3 / pad 1 / stride 1-2 convolution over a 3-channel NHWC bf16 image (conv_c3.hip), Cout % 128 == 0:
 // forward y [pixels][Cout] from w_pairs [Cout][14] (the channels_last filter's 27 taps x channels as
 // packed bf16 pairs, the 28th element 0); filter gradient as fp32 partials [blocks][Cout][27]

@@ -316,6 +316,15 @@ PYBIND11_MODULE(_C, m) {
     gemm_nt(reinterpret_cast<const void*>(a), reinterpret_cast<const void*>(b), reinterpret_cast<void*>(c), nullptr,
             nullptr, 0, nullptr, nullptr, reinterpret_cast<float*>(stats), lda, ldb, ldc, M, N, K, 3, S(stream));
   });
+  m.def("linear_bwd_supported", &linear_bwd_supported);
+  m.def("linear_bwd_splits", &linear_bwd_splits);
+  m.def("linear_bwd", [](uintptr_t dy, uintptr_t x, uintptr_t w, uintptr_t dx, uintptr_t ws, int64_t M, int64_t N,
+                         int64_t K, int64_t ldy, int64_t ldx, int64_t ldw, int64_t lddx, int splits, int dg_first,
+                         uintptr_t stream) {
+    linear_bwd(reinterpret_cast<const void*>(dy), reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(w),
+               reinterpret_cast<void*>(dx), reinterpret_cast<float*>(ws), M, N, K, ldy, ldx, ldw, lddx, splits, dg_first,
+               S(stream));
+  });
   m.def("conv_c3_supported", &conv_c3_supported);
   m.def("conv_c3_wgrad_blocks", &conv_c3_wgrad_blocks);
   m.def("conv_c3_fwd", [](uintptr_t x, uintptr_t w, uintptr_t y, int64_t N, int H, int W, int stride, int Cout,

@@ -642,7 +642,7 @@ void gemm_bf16(const GemmProblem& g, hipStream_t stream) {
   // engine 0 (auto): the LDS-DMA pipelined kernel for every problem it covers
   // (not for a prologue affine: its per-fragment transform costs the LDS-DMA kernel 1.3-2.3x —
   // measured — while register staging applies it on the way to LDS; engine 2 forces it)
-  const bool glds_only = g.res_mask != nullptr || g.res_sub_h > 0 || g.a_sub_h > 0 || g.conv_s == 2;
+  const bool glds_only = g.res_mask != nullptr || g.res_sub_h > 0 || g.a_sub_h > 0 || g.conv_s == 2 || g.conv_s >= 16;
   if (glds_only && !gemm_glds_supported(g))
     throw std::runtime_error("gemm_bf16: a masked / subsampled residual or a subsampled A needs the LDS-DMA kernel");
   if (g.engine >= 2 || glds_only || (g.engine == 0 && g.a_scale == nullptr && gemm_glds_supported(g))) {

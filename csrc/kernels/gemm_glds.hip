@@ -76,8 +76,18 @@ struct GldsArgs {
   const float* a_shift;
   int aff_c;             // channels of the affine (C for the implicit conv, K for a 1x1)
   int a_sub_h, a_sub_w;  // > 0: A row (n, ho, wo) is image row (n, 2ho, 2wo) of [.][a_sub_h][a_sub_w] (see api.h)
-  int conv_s;            // CONV: 1, or 2 (stride-2 3x3 over the [.][conv_h][conv_w] input; rows = output pixels)
+  int conv_s;            // CONV: 1, or 2 (stride-2 3x3 over the [.][conv_h][conv_w] input; rows = output pixels),
+                         // or 16 + (py * 2 + px): one parity class of a stride-2 3x3 INPUT gradient (rows =
+                         // the dY pixels [.][conv_h][conv_w] = the class's dX pixels (2a + py, 2b + px))
 };
+
+// dX row of class row m = (img, a, b) of the [.][Ho][Wo] dY grid: pixel (img, 2a + py, 2b + px)
+// of the [.][2 Ho][2 Wo] input (32-bit math: M < 2^31 host-checked)
+__device__ __forceinline__ int64_t dx_row(int64_t m, int Ho, int Wo, int cls) {
+  const unsigned mm = static_cast<unsigned>(m), hw = static_cast<unsigned>(Ho) * Wo;
+  const unsigned img = mm / hw, r = mm - img * hw, a = r / Wo, b = r - a * Wo;
+  return (static_cast<int64_t>(img) * (2 * Ho) + 2 * a + (cls >> 1)) * (2 * Wo) + 2 * b + (cls & 1);
+}
 
 // s_waitcnt vmcnt(N) with expcnt / lgkmcnt left alone (gfx9 encoding)
 template <int N>
@@ -114,17 +124,34 @@ template <int ROWS, int BK, bool CONV, bool PAD = false>
 __device__ __forceinline__ void issue_tile(bf16* lds_tile, const bf16* __restrict__ g, int64_t ld,
                                            int64_t rows, int64_t r0, int64_t k0, int64_t kend,
                                            const int* ph, const int* pw, int H, int W, int C,
-                                           const int64_t* srow = nullptr, const int* pbase = nullptr) {
+                                           const int64_t* srow = nullptr, const int* pbase = nullptr,
+                                           int tapcls = -1) {
   constexpr int CPR = BK / 8, RPP = 64 / CPR;
   constexpr int PPW = ROWS * BK / 2048;  // 1 KiB pieces per wave
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int dr = 0, ds = 0, c0 = 0;
   const bool tile_tap = !CONV || C % BK == 0;  // kernel-uniform
+  int64_t bk = k0;  // tap class (plain B operand): the column of the flipped [ci][3][3][co] filter
   if (CONV && tile_tap) {
     const int tap = static_cast<int>(k0 / C);
     c0 = static_cast<int>(k0 - static_cast<int64_t>(tap) * C);
-    dr = tap / 3 - 1;
-    ds = tap % 3 - 1;
+    if (tapcls >= 0) {
+      // stride-2 input-gradient parity class (py, px) = (tapcls >> 1, tapcls & 1): its taps in
+      // (row tap, column tap) order, row taps kh = 1 (py = 0) or kh = 0, 2 (py = 1) reading dY
+      // rows a + 1 and a (dr = +1, 0); columns likewise
+      const int px = tapcls & 1, nc = px ? 2 : 1;
+      const int tr = tap / nc, tc = tap - tr * nc;
+      dr = (tapcls >> 1) && tr == 0 ? 1 : 0;
+      ds = px && tc == 0 ? 1 : 0;
+    } else {
+      dr = tap / 3 - 1;
+      ds = tap % 3 - 1;
+    }
+  } else if (!CONV && tapcls >= 0) {
+    const int px = tapcls & 1, nc = px ? 2 : 1;
+    const int tap = static_cast<int>(k0 / C), tr = tap / nc, tc = tap - tr * nc;
+    const int kh = (tapcls >> 1) ? (tr == 0 ? 0 : 2) : 1, kw = px ? (tc == 0 ? 0 : 2) : 1;
+    bk = static_cast<int64_t>(8 - (kh * 3 + kw)) * C + (k0 - static_cast<int64_t>(tap) * C);
   }
 #pragma unroll
   for (int j = 0; j < PPW; ++j) {
@@ -148,7 +175,7 @@ __device__ __forceinline__ void issue_tile(bf16* lds_tile, const bf16* __restric
           static_cast<unsigned>(pw[j] + cds) < static_cast<unsigned>(W))
         src = g + (static_cast<int64_t>(pbase[j]) + cdr * W + cds) * C + cc;
     } else {
-      if (grow < rows && k0 + q * 8 < kend) src = g + (srow != nullptr ? srow[j] : grow) * ld + k0 + q * 8;
+      if (grow < rows && k0 + q * 8 < kend) src = g + (srow != nullptr ? srow[j] : grow) * ld + bk + q * 8;
     }
     typedef __attribute__((address_space(3))) char lds_char;
     typedef __attribute__((address_space(1))) void gl_void;
@@ -217,6 +244,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_glds_kernel(GldsArgs p) {
   const int64_t m0 = static_cast<int64_t>(tm) * BM, n0 = static_cast<int64_t>(tn) * BN;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int wm = wave >> 1, wn = wave & 1;
+  const int tapcls = CONV && p.conv_s >= 16 ? p.conv_s - 16 : -1;  // stride-2 input-gradient parity class
 
   // CONV: image position of each A row this lane stages (fixed over K)
   constexpr int PPWA = BM * kBK / 2048, RPPA = 512 / kBK;
@@ -256,8 +284,9 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_glds_kernel(GldsArgs p) {
   }
   auto issue = [&](int s, int64_t k0) {
     issue_tile<BM, kBK, CONV, AFF>(sa(s), p.a, p.lda, p.M, m0, k0, p.K, ph, pw, p.conv_h, p.conv_w, p.conv_c,
-                                   CONV ? nullptr : arow, CONV ? pbase : nullptr);
-    issue_tile<BN, kBK, false>(sb(s), p.b, p.ldb, p.N, n0, k0, p.K, nullptr, nullptr, 0, 0, 0);
+                                   CONV ? nullptr : arow, CONV ? pbase : nullptr, tapcls);
+    issue_tile<BN, kBK, false>(sb(s), p.b, p.ldb, p.N, n0, k0, p.K, nullptr, nullptr, 0, 0, p.conv_c, nullptr,
+                               nullptr, tapcls);
   };
   float* st_lds = reinterpret_cast<float*>(smem + kRingOrC);
   if (AFF) {  // stage the affine pairs once (read back with ds_read_b128 per fragment)
@@ -436,7 +465,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_glds_kernel(GldsArgs p) {
         }
         __builtin_memcpy(&v, e8, 16);
       }
-      *reinterpret_cast<uint4*>(p.c + m * p.ldc + n) = v;
+      *reinterpret_cast<uint4*>(p.c + (tapcls >= 0 ? dx_row(m, p.conv_h, p.conv_w, tapcls) : m) * p.ldc + n) = v;
       if (BNB && bnb) {
         bf16 x8[8];
         __builtin_memcpy(x8, &ecur.xv[u], 16);
@@ -821,6 +850,8 @@ __global__ __launch_bounds__(kThreads) void xpose_taps_kernel(XposeArgs a) {
 }  // namespace
 
 
+int64_t s2_class_taps(int cls) { return static_cast<int64_t>(((cls >> 1) ? 2 : 1) * ((cls & 1) ? 2 : 1)); }
+
 bool gemm_glds_supported(const GemmProblem& g) {
   const int64_t aff_c = g.conv_h > 0 ? g.conv_c : g.K;
   return g.a_kmajor && g.b_kmajor && g.mode <= 1 && (g.splits <= 1) &&
@@ -832,7 +863,13 @@ bool gemm_glds_supported(const GemmProblem& g) {
          // implicit 3x3 conv: C % 32 == 0 (a K tile inside one tap), or C % 8 == 0 with per-chunk taps
          // (no A affine then: its per-tile channel base assumes one tap per tile)
          (g.conv_h == 0 || ((g.conv_c % 32 == 0 || (g.conv_c % 8 == 0 && g.a_scale == nullptr && g.conv_c <= 8192)) &&
-                            g.K == 9LL * g.conv_c && g.M < (1LL << 31))) &&
+                            g.K == (g.conv_s >= 16 ? s2_class_taps(g.conv_s - 16) : 9LL) * g.conv_c &&
+                            g.M < (1LL << 31))) &&
+         // stride-2 input-gradient class: plain epilogue, C % 32 == 0 (a K tile inside one tap), K-major
+         // flipped-transposed filter [N][9][conv_c] as B
+         (g.conv_s < 16 || (g.conv_s < 20 && g.conv_h > 0 && g.conv_c % 32 == 0 && g.mode == 0 && g.res == nullptr &&
+                            g.a_scale == nullptr && g.bnb_x == nullptr && g.ldb >= 9LL * g.conv_c &&
+                            g.M % (static_cast<int64_t>(g.conv_h) * g.conv_w) == 0)) &&
          (g.conv_s != 2 || (g.conv_h > 0 && g.M % (static_cast<int64_t>((g.conv_h + 1) / 2) * ((g.conv_w + 1) / 2)) == 0)) &&
          (g.a_sub_h == 0 || (g.conv_h == 0 && g.a_kmajor && g.a_sub_w > 0 && g.M < (1LL << 31) &&
                              g.M % (static_cast<int64_t>((g.a_sub_h + 1) / 2) * ((g.a_sub_w + 1) / 2)) == 0)) &&
@@ -859,7 +896,7 @@ void gemm_glds(const GemmProblem& g, hipStream_t stream) {
   a.res_mask = g.res_mask;
   a.res_sub_h = g.res_sub_h; a.res_sub_w = g.res_sub_w;
   a.a_sub_h = g.a_sub_h; a.a_sub_w = g.a_sub_w;
-  a.conv_s = g.conv_s == 2 ? 2 : 1;
+  a.conv_s = g.conv_s == 2 || (g.conv_s >= 16 && g.conv_s < 20) ? g.conv_s : 1;
   a.aff_c = static_cast<int>(g.conv_h > 0 ? g.conv_c : g.K);
   const bool aff = g.a_scale != nullptr;
   const bool bnb = g.bnb_x != nullptr;

@@ -71,7 +71,7 @@ def _obj_for(src: str) -> str:
 # clean: profiles/rd5c_gemm_nt_store_hazard.md). The memory-bound elementwise kernels keep it.
 _NO_SLP = ["-fno-slp-vectorize"]
 EXTRA_FLAGS = {f: _NO_SLP for f in ("gemm_nt.hip", "attention.hip", "gemm_glds.hip", "gemm.hip", "conv3x3n.hip",
-                                        "wgrad3x3n.hip")}
+                                        "wgrad3x3n.hip", "linbwd.hip")}
 
 
 def _compile_cmd(src: str, obj: str) -> list[str]:

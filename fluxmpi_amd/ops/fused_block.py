@@ -628,13 +628,16 @@ def _dgrad_is_ours(dy, weight, x_shape) -> bool:
 class _Conv3x3S2(torch.autograd.Function):
     """3x3 / stride 2 / pad 1 convolution (the first conv2 of ResNet stages 2-4). Forward: MIOpen,
     or (``with_stats``) our implicit GEMM over the output pixels with the next BatchNorm's sums in
-    its epilogue; input gradient on MIOpen; weight gradient measured per shape between MIOpen and
+    its epilogue; input gradient on the four parity-class implicit GEMMs (``gemm.conv3x3_s2_dgrad``,
+    even input sizes; MIOpen otherwise); weight gradient measured per shape between MIOpen and
     our split-K kernel over the stride-2 implicit im2col (``gemm.conv3x3_wgrad_s2``)."""
 
     @staticmethod
     def forward(ctx, x, weight, with_stats=False):
         x = x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
         ctx.save_for_backward(x, weight)
+        if G.S2_DGRAD:
+            note_filter(weight)  # the input gradient reads the batched transposed-filter cache
         if with_stats:
             return G.conv3x3_s2_fwd(x, weight, stats=_workspace(x))
         return torch.nn.functional.conv2d(x, weight, None, 2, 1)
@@ -651,8 +654,11 @@ class _Conv3x3S2(torch.autograd.Function):
                                                                       [0, 0], 1, [False, True, False])[1],
                 "ours": lambda: G.conv3x3_wgrad_s2(dy, x)}, param=weight)
         if ctx.needs_input_grad[0]:
-            dx = torch.ops.aten.convolution_backward(dy, x, weight, None, [2, 2], [1, 1], [1, 1], False, [0, 0], 1,
-                                                     [True, False, False])[0]
+            if G.s2_dgrad_ok(dy, weight, x.shape):
+                dx = G.conv3x3_s2_dgrad(dy, weight, x.shape)  # four parity-class implicit GEMMs
+            else:
+                dx = torch.ops.aten.convolution_backward(dy, x, weight, None, [2, 2], [1, 1], [1, 1], False, [0, 0],
+                                                         1, [True, False, False])[0]
         return dx, dw, None
 
 

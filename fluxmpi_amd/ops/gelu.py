@@ -174,10 +174,18 @@ class _LinearGeluFn(torch.autograd.Function):
         n = h.shape[-1]
         dh2 = dh.reshape(-1, n)
         x2 = x.reshape(-1, x.shape[-1])
-        from .linear import _wgrad_mode, dgrad, native_ok, weight_grad
-        dx = dgrad(dh2, w).reshape(x.shape) if ctx.needs_input_grad[0] else None
-        dw = None
-        if ctx.needs_input_grad[1]:
+        from .linear import _wgrad_mode, dgrad, dgrad_wgrad, linbwd_ok, native_ok, weight_grad
+        dx = dw = None
+        if (ctx.needs_input_grad[0] and ctx.needs_input_grad[1] and _wgrad_mode() == "ours" and native_ok(x2, dh2)
+                and linbwd_ok(dh2, x2, w)):
+            # input and weight gradient in one launch (linbwd.hip)
+            from . import graddst
+            with graddst.into(ctx.weight):
+                dx, dw = dgrad_wgrad(dh2, x2, w, w.dtype)
+            dx = dx.reshape(x.shape)
+        elif ctx.needs_input_grad[0]:
+            dx = dgrad(dh2, w).reshape(x.shape)
+        if ctx.needs_input_grad[1] and dw is None:
             # long-K weight gradient on the split-K HIP kernel (ops/linear.py)
             from . import graddst
             with graddst.into(ctx.weight):  # the DDP bucket slice when one is attached

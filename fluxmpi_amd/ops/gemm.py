@@ -225,6 +225,47 @@ def conv3x3_s2_fwd(x: torch.Tensor, w: torch.Tensor, stats: torch.Tensor | None 
     return y
 
 
+# stride-2 3x3 input gradients on the parity-class implicit GEMM (conv3x3_s2_dgrad); "0": MIOpen
+S2_DGRAD = os.environ.get("FLUXMPI_S2_DGRAD", "1") != "0"
+
+
+def s2_dgrad_ok(dy: torch.Tensor, w: torch.Tensor, x_shape) -> bool:
+    """Shapes :func:`conv3x3_s2_dgrad` takes: even input sizes (each parity class is the dY grid),
+    Cout % 32 == 0 (a K tile inside one tap), Cin % 8 == 0, bf16."""
+    if not (S2_DGRAD and ENGINE != 1 and dy.is_cuda and dy.dtype == w.dtype == torch.bfloat16):
+        return False
+    n, co, ho, wo = dy.shape
+    ci = w.shape[1]
+    h, wd = x_shape[2], x_shape[3]
+    return (tuple(w.shape[2:]) == (3, 3) and h == 2 * ho and wd == 2 * wo and co % 32 == 0 and ci % 8 == 0
+            and n * h * wd < 2 ** 31)
+
+
+def conv3x3_s2_dgrad(dy: torch.Tensor, w: torch.Tensor, x_shape) -> torch.Tensor:
+    """Input gradient of the 3x3 / stride 2 / pad 1 convolution (even input sizes) as four
+    implicit GEMMs, one per output parity class (py, px): dX pixel (2a + py, 2b + px) only
+    receives the taps kh = 1 (py = 0) or kh = 0, 2 (py = 1) — dY rows a, and a + 1 / a — and
+    likewise in columns, so the classes take 1, 2, 2 and 4 taps: exactly the convolution's
+    9 Cout-deep products per 2 x 2 input block, no zero-inserted dY, no atomics, every dX element
+    written once. A = the dY grid itself (rows = class pixels), B = the flipped transposed filter
+    (the batched ``filter_t`` cache; each class indexes its taps), epilogue rows remapped to the
+    class's dX pixels (``gemm_glds.hip``, ``conv_s = 16 + 2 py + px``). Replaces MIOpen's
+    backward-data kernels (ResNet-50: 2 x 112 + 106 us per step plus a 28 us output fill each,
+    ``profiles/rd5ba_resnet50_steady.md``)."""
+    n, co, ho, wo = dy.shape
+    ci = w.shape[1]
+    h, wd = x_shape[2], x_shape[3]
+    dys = dy if dy.is_contiguous(memory_format=torch.channels_last) else dy.contiguous(
+        memory_format=torch.channels_last)
+    wt = filter_t(w)  # [ci][3][3][co] flipped: original tap (kh, kw) at column block 8 - (3 kh + kw)
+    dx = torch.empty(n, h, wd, ci, device=dy.device, dtype=dy.dtype).permute(0, 3, 1, 2)
+    for cls in range(4):
+        taps = (2 if cls >> 1 else 1) * (2 if cls & 1 else 1)
+        gemm(dys, wt, dx, M=n * ho * wo, N=ci, K=taps * co, lda=co, ldb=9 * co, ldc=ci, conv=(ho, wo, co),
+             conv_stride=16 + cls)
+    return dx
+
+
 def conv3x3_dgrad(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None, bn_bwd=None,
                   stats: torch.Tensor | None = None, residual: torch.Tensor | None = None) -> torch.Tensor:
     """Input gradient of the 3x3/s1/p1 convolution: the same implicit GEMM over dY with the

@@ -188,10 +188,10 @@ class _LinearAddLayerNormFn(torch.autograd.Function):
         n_out, n_in = weight.shape
         g2 = dx.reshape(-1, n_out)
         a2 = a.reshape(-1, n_in)
-        da = None
+        da = dw = None
         if ctx.needs_input_grad[0]:
             from . import gemm_nt
-            from .linear import dgrad
+            from .linear import dgrad, dgrad_wgrad, linbwd_ok
             link = ctx.gelu_link
             if (link is not None and link.h is not None and link.deriv and link.h.shape == a.shape
                     and gemm_nt.supported(g2.shape[0], n_in, n_out, g2, weight, link.h, fused="dgrad")):
@@ -200,10 +200,14 @@ class _LinearAddLayerNormFn(torch.autograd.Function):
                 link.dh, link.db = gemm_nt.linear_dgrad(g2, weight, gelu_d=link.h, bias_dtype=link.bias_dtype,
                                                         bias_param=link.bias)
                 da = torch.zeros((), device=a.device, dtype=a.dtype).expand(a.shape)  # placeholder, never read
+            elif ctx.needs_input_grad[1] and native_ok(a2, g2) and linbwd_ok(g2, a2, weight):
+                # input and weight gradient in one launch (linbwd.hip)
+                with graddst.into(ctx.weight):
+                    da, dw = dgrad_wgrad(g2, a2, weight, weight.dtype)
+                da = da.reshape(a.shape)
             else:
                 da = dgrad(g2, weight).reshape(a.shape)
-        dw = None
-        if ctx.needs_input_grad[1]:
+        if ctx.needs_input_grad[1] and dw is None:
             with graddst.into(ctx.weight):  # the DDP bucket slice when one is attached
                 if native_ok(a2, g2):
                     dw = weight_grad(g2, a2, weight.dtype)

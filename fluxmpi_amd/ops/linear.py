@@ -77,6 +77,64 @@ def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype, spl
     return conv1x1_wgrad_v2(dy2, x2, out_dtype=out_dtype, splits=splits or _SPLITS.get((n_out, n_in)))
 
 
+# One launch for a Linear's input AND weight gradient (csrc/kernels/linbwd.hip); "0": the two
+# separate calls (dgrad below + weight_grad)
+LINBWD = os.environ.get("FLUXMPI_LINBWD", "1") != "0"
+
+
+def linbwd_plan(M: int, N: int, K: int, cus: int = 256) -> tuple[int, int]:
+    """(split count, dg_first) for :func:`dgrad_wgrad`: as many weight-gradient jobs as about HALF
+    the CUs (``round(cus / 2 / tiles)`` splits), listed before the input-gradient tiles. Measured
+    on MI355X at the ViT-B/16 shapes (M = 50432; ``profiles/rd6d_bench_linbwd.jsonl``, sweep of
+    4-32 splits x both orders): the best points were 108-144 weight-gradient jobs, weight
+    gradient first — qkv 4 splits 334 us, proj 16 splits 128 us, fc1 4 splits 434 us, against
+    363 / 148 / 444 us for hipBLASLt's input gradient + wgrad256 (one round of 256 split-K
+    workgroups). More splits move more fp32 partials than the finer tail saves; the
+    input-gradient tiles first leave the long weight-gradient jobs as the tail."""
+    tiles = max(1, (N // 256) * (K // 256))
+    C = _ext.get(required=False)
+    sp = max(1, min(64, round(cus / 2 / tiles)))
+    if C is not None and hasattr(C, "linear_bwd_splits"):
+        sp = C.linear_bwd_splits(M, N, K, sp)
+    return sp, 0
+
+
+def linbwd_ok(dy2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor) -> bool:
+    if not (LINBWD and dy2.is_cuda and dy2.dtype == x2.dtype == w.dtype == torch.bfloat16):
+        return False
+    if not (dy2.is_contiguous() and x2.is_contiguous() and w.is_contiguous()):
+        return False
+    if any(t.data_ptr() % 16 for t in (dy2, x2, w)):
+        return False
+    C = _ext.get(required=False)
+    if C is None or not hasattr(C, "linear_bwd"):
+        return False
+    M, N = dy2.shape
+    K = x2.shape[1]
+    return tuple(w.shape) == (N, K) and bool(C.linear_bwd_supported(M, N, K, N, K, K, K))
+
+
+def dgrad_wgrad(dy2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, out_dtype: torch.dtype):
+    """``(dy2 @ w, dy2^T @ x2)`` — a Linear's input and weight gradients — in ONE launch of
+    ``linbwd.hip`` (fp32 accumulation; the weight gradient's split-K partials reduced into
+    ``out_dtype``, into the weight's DDP bucket slice when the caller binds it with
+    ``graddst.into``). Callers check :func:`linbwd_ok` first."""
+    C = _ext.get(required=True)
+    M, N = dy2.shape
+    K = x2.shape[1]
+    cus = torch.cuda.get_device_properties(dy2.device).multi_processor_count
+    sp, first = linbwd_plan(M, N, K, cus)
+    dx = torch.empty(M, K, device=dy2.device, dtype=dy2.dtype)
+    ws = torch.empty(sp, N, K, device=dy2.device, dtype=torch.float32)
+    stream = torch.cuda.current_stream(dy2.device).cuda_stream
+    C.linear_bwd(dy2.data_ptr(), x2.data_ptr(), w.data_ptr(), dx.data_ptr(), ws.data_ptr(), M, N, K, N, K, K, K, sp,
+                 first, stream)
+    odt = out_dtype if out_dtype in (torch.float32, torch.bfloat16) else torch.float32
+    dw = graddst.empty((N, K), odt, dy2.device)
+    C.gemm_splitk_reduce(ws.data_ptr(), sp, dw.numel(), dw.data_ptr(), DTYPE_CODE[odt], stream)
+    return dx, dw.to(out_dtype)
+
+
 def bias_grad(dy2: torch.Tensor, out_dtype: torch.dtype) -> torch.Tensor:
     """Column sums of ``dy2`` [rows, N] -> [N] (fp32 accumulation, cast to ``out_dtype``)."""
     if not (dy2.is_cuda and dy2.dtype in DTYPE_CODE and dy2.is_contiguous() and dy2.shape[1] % 8 == 0
@@ -123,6 +181,14 @@ class _LinearFn(torch.autograd.Function):
 
         # written straight into the DDP bucket slices when a communicating engine is attached
         same = dy2.dtype == x2.dtype == w.dtype
+        dx = None
+        if need_w and ctx.needs_input_grad[0] and native and linbwd_ok(dy2, x2, w):
+            # both GEMMs in one launch (linbwd.hip): the weight gradient's jobs fill the input
+            # gradient's partial last round
+            with graddst.into(w):
+                dx, dw = dgrad_wgrad(dy2, x2, w, w.dtype)
+            dx = dx.reshape(x.shape)
+            need_w = False
         if need_w:
             def wgrad():
                 with graddst.into(w):
@@ -141,7 +207,8 @@ class _LinearFn(torch.autograd.Function):
                     db = torch.sum(dy2, 0, out=graddst.empty((n_out,), ctx.bias_dtype, dy2.device))
                 else:
                     db = dy2.sum(0).to(ctx.bias_dtype)
-        dx = dgrad(dy2, w).reshape(x.shape) if ctx.needs_input_grad[0] else None
+        if dx is None and ctx.needs_input_grad[0]:
+            dx = dgrad(dy2, w).reshape(x.shape)
         return dx, dw, db
 
 
@@ -178,4 +245,4 @@ class Linear(torch.nn.Linear):
         return linear(x, self.weight, self.bias)
 
 
-__all__ = ["linear", "Linear", "weight_grad", "bias_grad", "native_ok", "fwd", "dgrad"]
+__all__ = ["linear", "Linear", "weight_grad", "bias_grad", "native_ok", "fwd", "dgrad", "dgrad_wgrad", "linbwd_ok"]

