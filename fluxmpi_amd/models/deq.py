@@ -55,6 +55,29 @@ GRAPH_CHUNK = 5
 # its expected init norm; "conv+gn" also clamps n3's GroupNorm gain (it multiplies the whole
 # Jacobian) to [-1, 1]; "none" = off.
 CONSTRAIN = os.environ.get("FLUXMPI_DEQ_CONSTRAIN", "none")
+# Jacobian regularisation (Bai, Koltun, Kolter 2021, "Stabilizing Equilibrium Models by Jacobian
+# Regularization"; DeepEquilibriumNetworks.jl's `jacobian_regularization`): loss += gamma * ||J_f||_F^2 / d
+# at the fixed point, estimated each training step by a finite difference along one random
+# direction, ||f(z* + s e) - f(z*)||^2 / (s^2 ||e||^2) (two extra cell evaluations with autograd, no
+# double backward: the fused kernels' backward is first-order). "gamma,sigma"; empty = off.
+JAC_REG = os.environ.get("FLUXMPI_DEQ_JR", "")
+
+
+class _AddPenaltyGrad(torch.autograd.Function):
+    """Identity on ``z``; in the backward ``penalty`` receives gradient ``weight``: the same
+    parameter gradients as adding ``weight * penalty`` to the loss, without changing the loss the
+    caller computes (the bench loop, user code)."""
+
+    @staticmethod
+    def forward(ctx, z, penalty, weight):
+        ctx.weight = float(weight)
+        ctx.pmeta = (penalty.dtype, penalty.device)
+        return z.view_as(z)
+
+    @staticmethod
+    def backward(ctx, g):
+        dt, dev = ctx.pmeta
+        return g, torch.full((), ctx.weight, dtype=dt, device=dev), None
 DEQ_MNIST_SOLVER = {"max_iter": 30, "tol": 1e-3, "bwd_iter": 30, "bwd_tol": 1e-3}
 DEQ_CIFAR_SOLVER = {"max_iter": 30, "tol": 2e-2, "bwd_iter": 30, "bwd_tol": 1e-2}
 
@@ -386,9 +409,14 @@ class SolverGraphs:
 
 
 class DEQFixedPoint(nn.Module):
-    def __init__(self, f: nn.Module, max_iter=30, tol=1e-4, bwd_iter=30, bwd_tol=1e-4, check_lag: int | None = None):
+    def __init__(self, f: nn.Module, max_iter=30, tol=1e-4, bwd_iter=30, bwd_tol=1e-4, check_lag: int | None = None,
+                 jac_reg: float | None = None, jac_sigma: float | None = None):
         super().__init__()
         self.f = f
+        env = [float(v) for v in JAC_REG.split(",")] if JAC_REG else []
+        self.jac_reg = float(jac_reg if jac_reg is not None else (env[0] if env else 0.0))
+        self.jac_sigma = float(jac_sigma if jac_sigma is not None else (env[1] if len(env) > 1 else 0.05))
+        self.last_jr = None  # the last training step's ||J||_F^2 / d estimate (0-d device tensor)
         self.max_iter, self.tol, self.bwd_iter, self.bwd_tol = max_iter, tol, bwd_iter, bwd_tol
         self.check_lag = check_lag
         self.last_iters = 0
@@ -419,7 +447,25 @@ class DEQFixedPoint(nn.Module):
         # the cell's GroupNorm parameters cast to fp32 once for the ~30 calls below (into the
         # graphs' static buffers when the solver loops replay graphs)
         with fp32_affine_cache(self.f, buffers=gs.aff if gs is not None else None):
-            return self._forward(x, gs)
+            out = self._forward(x, gs)
+        if self.jac_reg > 0 and self.training and torch.is_grad_enabled() and out.requires_grad:
+            out = self._jacobian_penalty(out, x)
+        return out
+
+    def _jacobian_penalty(self, out, x):
+        """``out`` carrying the gradient of ``jac_reg * ||J_f(z*)||_F^2 / d`` (module constant
+        :data:`JAC_REG`): two differentiable cell evaluations at the solution and at a random
+        perturbation of it, separate from the implicit-differentiation step (whose output gradient
+        the adjoint solve replaces)."""
+        z0 = self._z_star
+        e = torch.randn_like(z0)
+        s = self.jac_sigma
+        with fp32_affine_cache(self.f):
+            f1 = self.f(z0, x)
+            f2 = self.f(z0 + s * e, x)
+        jr = (f2.float() - f1.float()).square().sum() / (s * s * e.float().square().sum())
+        self.last_jr = jr.detach()
+        return _AddPenaltyGrad.apply(out, jr, self.jac_reg)
 
     def _forward(self, x, gs: SolverGraphs | None = None):
         # the solver's ~30 evaluations by direct kernel calls when the cell allows (no autograd
@@ -430,6 +476,7 @@ class DEQFixedPoint(nn.Module):
         with torch.no_grad():
             z, self.last_iters, self.last_res = anderson(fz, torch.zeros_like(x), max_iter=self.max_iter,
                                              tol=self.tol, check_lag=self.check_lag, graphs=gs)
+        self._z_star = z.detach()
         # one differentiable step re-engages autograd at z*; its GroupNorms save fresh fp32 affine
         # copies, not the graphs' static buffers (a later forward at this shape rewrites those in
         # place before this one's backward)

@@ -13,6 +13,7 @@ the same kernels):
 ``_DS_CHOICE``    downsample 1x1 forward: ours + statistics epilogue (True) or MIOpen
 ``_DGRAD_CHOICE`` 3x3 / s1 input gradient with narrow channels: ours (True) or MIOpen
 ``_WG_CHOICE``    weight gradients: ("miopen" | "ours" | "w256" | "w3n", our kernel config)
+``_LB_CHOICE``    token-major Linear backward in one launch (linbwd.hip): split count
 ================  ================================================================
 
 Frozen (``freeze_choices``) or inside a HIP-graph capture, a missing shape takes the
@@ -55,7 +56,8 @@ _S2_CHOICE: dict = {}
 _DS_CHOICE: dict = {}
 _DGRAD_CHOICE: dict = {}
 _WG_CHOICE: dict = {}
-_CHOICE_TABLES = {"fwd1x1_ours": "_FWD1_CHOICE", "fwd3x3_ours": "_FWD_CHOICE", "wgrad": "_WG_CHOICE",
+_LB_CHOICE: dict = {}
+_CHOICE_TABLES = {"linbwd_splits": "_LB_CHOICE", "fwd1x1_ours": "_FWD1_CHOICE", "fwd3x3_ours": "_FWD_CHOICE", "wgrad": "_WG_CHOICE",
                   "fwd_ds_ours": "_DS_CHOICE", "fwd3x3s2_ours": "_S2_CHOICE", "fwd3x3_engine": "_FWD_ENGINE",
                   "dgrad3x3_ours": "_DGRAD_CHOICE"}
 
@@ -81,6 +83,21 @@ def time_us(fn, iters=10, repeats=3):
         e.record()
         e.synchronize()
         best = min(best, s.elapsed_time(e) * 1e3 / iters)
+    return best
+
+
+def linbwd_choice(key, candidates, default: int, run) -> int:
+    """The split count of a Linear's one-launch backward (``ops/linear.dgrad_wgrad``) for ``key``:
+    the fastest of ``candidates`` (``run(splits)`` launches the kernel into scratch buffers),
+    measured once per shape; ``default`` when frozen / capturing."""
+    hit = _LB_CHOICE.get(key)
+    if hit is not None:
+        return hit
+    if no_measure():
+        return default
+    with torch.no_grad():
+        best = min(candidates, key=lambda sp: time_us(lambda: run(sp), iters=5, repeats=3))
+    _LB_CHOICE[key] = best
     return best
 
 

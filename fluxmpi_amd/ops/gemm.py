@@ -225,8 +225,13 @@ def conv3x3_s2_fwd(x: torch.Tensor, w: torch.Tensor, stats: torch.Tensor | None 
     return y
 
 
-# stride-2 3x3 input gradients on the parity-class implicit GEMM (conv3x3_s2_dgrad); "0": MIOpen
-S2_DGRAD = os.environ.get("FLUXMPI_S2_DGRAD", "1") != "0"
+# stride-2 3x3 input gradients on the parity-class implicit GEMM (conv3x3_s2_dgrad): OFF by
+# default ("1" turns it on) — measured slower than MIOpen on ResNet-50: the four class GEMMs re-read
+# dY once per tap (9x per layer) and took 141 / 156 / 193 us for the 7x7x512 / 14x14x256 / 28x28x128
+# layers against ~140 us each for MIOpen's igemm_bwd + its output fill; ResNet-50 12.74k / 12.72k vs
+# 12.80k / 12.76k img/s (profiles/rd6e_s2_dgrad_ab.jsonl). A one-pass kernel (each dY tile staged once
+# for the 2 x 2 output parities, conv3x3n-style) is the form that would win.
+S2_DGRAD = os.environ.get("FLUXMPI_S2_DGRAD", "0") == "1"
 
 
 def s2_dgrad_ok(dy: torch.Tensor, w: torch.Tensor, x_shape) -> bool:

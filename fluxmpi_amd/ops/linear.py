@@ -82,21 +82,15 @@ def weight_grad(dy2: torch.Tensor, x2: torch.Tensor, out_dtype: torch.dtype, spl
 LINBWD = os.environ.get("FLUXMPI_LINBWD", "1") != "0"
 
 
-def linbwd_plan(M: int, N: int, K: int, cus: int = 256) -> tuple[int, int]:
-    """(split count, dg_first) for :func:`dgrad_wgrad`: as many weight-gradient jobs as about HALF
-    the CUs (``round(cus / 2 / tiles)`` splits), listed before the input-gradient tiles. Measured
-    on MI355X at the ViT-B/16 shapes (M = 50432; ``profiles/rd6d_bench_linbwd.jsonl``, sweep of
-    4-32 splits x both orders): the best points were 108-144 weight-gradient jobs, weight
-    gradient first — qkv 4 splits 334 us, proj 16 splits 128 us, fc1 4 splits 434 us, against
-    363 / 148 / 444 us for hipBLASLt's input gradient + wgrad256 (one round of 256 split-K
-    workgroups). More splits move more fp32 partials than the finer tail saves; the
-    input-gradient tiles first leave the long weight-gradient jobs as the tail."""
+def linbwd_candidates(M: int, N: int, K: int, cus: int) -> tuple[list, int]:
+    """Split counts the one-launch backward is timed at (weight-gradient jobs between a quarter
+    and all of the CUs' worth, four geometric steps) and the untimed default (about half)."""
+    C = _ext.get(required=True)
     tiles = max(1, (N // 256) * (K // 256))
-    C = _ext.get(required=False)
-    sp = max(1, min(64, round(cus / 2 / tiles)))
-    if C is not None and hasattr(C, "linear_bwd_splits"):
-        sp = C.linear_bwd_splits(M, N, K, sp)
-    return sp, 0
+    lo, hi = max(1, cus // 4 // tiles), max(1, cus // tiles)
+    raw = {max(1, round(lo * (hi / lo) ** (i / 3))) for i in range(4)} if hi > lo else {lo}
+    cands = sorted({C.linear_bwd_splits(M, N, K, min(64, sp)) for sp in raw})
+    return cands, C.linear_bwd_splits(M, N, K, max(1, min(64, cus // 2 // tiles)))
 
 
 def linbwd_ok(dy2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor) -> bool:
@@ -114,21 +108,45 @@ def linbwd_ok(dy2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor) -> bool:
     return tuple(w.shape) == (N, K) and bool(C.linear_bwd_supported(M, N, K, N, K, K, K))
 
 
+def _lb_known():
+    from .conv_choice import _LB_CHOICE
+    return _LB_CHOICE
+
+
 def dgrad_wgrad(dy2: torch.Tensor, x2: torch.Tensor, w: torch.Tensor, out_dtype: torch.dtype):
     """``(dy2 @ w, dy2^T @ x2)`` — a Linear's input and weight gradients — in ONE launch of
     ``linbwd.hip`` (fp32 accumulation; the weight gradient's split-K partials reduced into
     ``out_dtype``, into the weight's DDP bucket slice when the caller binds it with
-    ``graddst.into``). Callers check :func:`linbwd_ok` first."""
+    ``graddst.into``). The split count is measured once per shape among
+    :func:`linbwd_candidates` (``ops/conv_choice.linbwd_choice``: rank-consistent through
+    ``parallel/autotune.calibrate``); on the ViT-B/16 shapes the best points lie at 108-144
+    weight-gradient jobs, weight gradient first: qkv 334-341 us, proj 128-131, fc1 434-451
+    against 363 / 148 / 444-450 for hipBLASLt's input gradient + wgrad256, and the cost is not
+    smooth in the split count (qkv 5 splits 364 us), so it is timed, not modelled. Callers check
+    :func:`linbwd_ok` first."""
+    from .conv_choice import linbwd_choice
     C = _ext.get(required=True)
     M, N = dy2.shape
     K = x2.shape[1]
     cus = torch.cuda.get_device_properties(dy2.device).multi_processor_count
-    sp, first = linbwd_plan(M, N, K, cus)
-    dx = torch.empty(M, K, device=dy2.device, dtype=dy2.dtype)
-    ws = torch.empty(sp, N, K, device=dy2.device, dtype=torch.float32)
     stream = torch.cuda.current_stream(dy2.device).cuda_stream
+    dx = torch.empty(M, K, device=dy2.device, dtype=dy2.dtype)
+    cands, default = linbwd_candidates(M, N, K, cus)
+
+    def trial(sp):  # into scratch: a measured launch never touches the real outputs
+        C.linear_bwd(dy2.data_ptr(), x2.data_ptr(), w.data_ptr(), dx.data_ptr(), scratch.data_ptr(), M, N, K, N, K,
+                     K, K, sp, 0, stream)
+
+    scratch = None
+    if (M, N, K, cus) not in _lb_known():
+        scratch = torch.empty(max(cands + [default]), N, K, device=dy2.device, dtype=torch.float32)
+    sp = linbwd_choice((M, N, K, cus), cands, default, trial)
+    del scratch
+    ws = torch.empty(sp, N, K, device=dy2.device, dtype=torch.float32)
+    # weight-gradient jobs first (the longer jobs; the input-gradient tiles fill the tail):
+    # measured 8-25 % faster than the other order at every split count (profiles/rd6d_bench_linbwd.jsonl)
     C.linear_bwd(dy2.data_ptr(), x2.data_ptr(), w.data_ptr(), dx.data_ptr(), ws.data_ptr(), M, N, K, N, K, K, K, sp,
-                 first, stream)
+                 0, stream)
     odt = out_dtype if out_dtype in (torch.float32, torch.bfloat16) else torch.float32
     dw = graddst.empty((N, K), odt, dy2.device)
     C.gemm_splitk_reduce(ws.data_ptr(), sp, dw.numel(), dw.data_ptr(), DTYPE_CODE[odt], stream)

@@ -39,14 +39,30 @@ def test_linbwd_matches_fp32(gpu_ext, M, N, K, splits, first):
 
 
 def test_linbwd_vit_shape(gpu_ext):
-    """The ViT-B/16 qkv backward at batch 256 (M = 50432 tokens) with the planned split / order."""
-    from fluxmpi_amd.ops.linear import linbwd_plan
-    s, first = linbwd_plan(50432, 2304, 768)
-    dx, dw, rdx, rdw = _run(50432, 2304, 768, s, first, seed=1)
+    """The ViT-B/16 qkv backward at batch 256 (M = 50432 tokens) at each timed split count."""
+    from fluxmpi_amd.ops.linear import linbwd_candidates
+    cands, default = linbwd_candidates(50432, 2304, 768, 256)
+    assert default in range(1, 65) and all(1 <= c <= 64 for c in cands)
+    dx, dw, rdx, rdw = _run(50432, 2304, 768, cands[-1], 0, seed=1)
     assert _rel(dx, rdx) < 5e-3 and _rel(dw, rdw) < 2e-3
 
 
 @pytest.mark.parametrize("N,K", [(768, 768), (2304, 768)])
+def test_dgrad_wgrad_measures_once_and_matches(gpu_ext):
+    from fluxmpi_amd.ops import conv_choice
+    from fluxmpi_amd.ops.linear import dgrad_wgrad
+    torch.manual_seed(3)
+    M, N, K = 4096, 768, 768
+    dy = (torch.randn(M, N, device="cuda") * 0.5).bfloat16()
+    x = torch.randn(M, K, device="cuda").bfloat16()
+    w = (torch.randn(N, K, device="cuda") * N ** -0.5).bfloat16()
+    conv_choice._LB_CHOICE.clear()
+    dx, dw = dgrad_wgrad(dy, x, w, torch.bfloat16)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    assert (M, N, K, cus) in conv_choice._LB_CHOICE
+    assert _rel(dx, dy.float() @ w.float()) < 5e-3 and _rel(dw, dy.float().t() @ x.float()) < 5e-3
+
+
 def test_linear_module_routes_to_linbwd(gpu_ext, N, K):
     from fluxmpi_amd.ops import graddst
     from fluxmpi_amd.ops.linear import Linear, linbwd_ok
