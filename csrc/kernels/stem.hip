@@ -40,6 +40,7 @@
 //     operand straight from the halo by transposed reads too (a lane's 8-B piece is one pixel's
 //     4 channels; halo pitch 118 chunks keeps a 32-lane read on 64 distinct banks); G3 by
 //     v_dot2c_f32_bf16 against ones on the B fragments.
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -657,7 +658,14 @@ void stem_bwd(const void* x, const void* c, const void* dp, const uint8_t* idx, 
   const int total = static_cast<int>(n * kPH);
   StemBwdArgs a{static_cast<const bf16*>(x), static_cast<const bf16*>(c), static_cast<const bf16*>(dp), idx, mean, inv,
                 part, stats, (total + blocks - 1) / blocks, total};
-  stem_bwd_kernel<0><<<static_cast<unsigned>(blocks), kBT, kBSmem, s>>>(a);
+  // FLUXMPI_STEM_BWD_DIAG=1/2/3: the MODE builds (time split of the phases; results are wrong)
+  static const int mode = [] {
+    const char* e = std::getenv("FLUXMPI_STEM_BWD_DIAG");
+    const int v = e != nullptr ? std::atoi(e) : 0;
+    return v >= 0 && v <= 3 ? v : 0;
+  }();
+  auto kern = mode == 1 ? stem_bwd_kernel<1> : mode == 2 ? stem_bwd_kernel<2> : mode == 3 ? stem_bwd_kernel<3> : stem_bwd_kernel<0>;
+  kern<<<static_cast<unsigned>(blocks), kBT, kBSmem, s>>>(a);
   FLUXMPI_HIP_CHECK(hipGetLastError());
   bn_finalize_bwd(stats, kCo, dw_bn, db_bn, s);
   stem_wgrad_combine_kernel<<<kKk, kCT, 0, s>>>(part, blocks, w, mean, inv, dw_bn, db_bn,

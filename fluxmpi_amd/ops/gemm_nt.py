@@ -20,7 +20,8 @@ GELU forward (EPI 1: gelu(h) and gelu'(h) from one tanh evaluation; the derivati
 pre-activation as what the backward saves) and fc2's input gradient times that derivative +
 fc1's bias-gradient partials (EPI 2: no GELU math left in the backward); ``all`` also every
 plain forward / input gradient (at parity with hipBLASLt on qkv / proj, 1-5 % behind on the
-K = 3072 / N = 3072 ones); ``0`` never. Measured: profiles/rd4i_bench_gemm_nt.jsonl (the hipBLASLt
+K = 3072 / N = 3072 ones); ``fwd`` the fused calls and every plain forward (the input gradients of
+the plain Linears go to ``linbwd.hip`` either way, ``ops/linear.py``); ``0`` never. Measured: profiles/rd4i_bench_gemm_nt.jsonl (the hipBLASLt
 columns are the roofline baseline per shape).
 
 Convolutions (ops/gemm.py routes here, ``FLUXMPI_GEMM_NT_CONV``, default on): the stride-1 3x3
@@ -58,11 +59,13 @@ def supported(rows: int, n_out: int, k: int, *tensors: torch.Tensor, fused: bool
     weight transpose of an input gradient) under the current mode. ``fused``: the call carries an
     epilogue fusion — ``"fwd"`` (fc1 bias + GELU) or ``"dgrad"`` (GELU backward), taken in modes
     fused / all (the pair works together: the backward multiplies by the derivative the forward
-    stored), ``True`` (either: shape checks of the kernel itself)."""
+    stored), ``True`` (either: shape checks of the kernel itself), ``"plain_fwd"`` (a plain Linear
+forward: taken in modes fwd / all)."""
     if not ENABLED or not tensors or not tensors[0].is_cuda:
         return False
     if MODE not in ("all", "1"):
-        ok = fused is True or (fused in ("fwd", "dgrad") and MODE in ("fused", "dgrad"))
+        ok = (fused is True or (fused in ("fwd", "dgrad") and MODE in ("fused", "dgrad", "fwd"))
+              or (fused == "plain_fwd" and MODE == "fwd"))
         if not ok:
             return False
     if any(t.dtype != torch.bfloat16 for t in tensors) or not _aligned(*tensors):

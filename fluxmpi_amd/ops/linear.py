@@ -235,7 +235,7 @@ def fwd(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None) -> tor
     from . import gemm_nt
     n_out, n_in = weight.shape
     rows = x.numel() // n_in if n_in else 0
-    if x.is_contiguous() and gemm_nt.supported(rows, n_out, n_in, x, weight):
+    if x.is_contiguous() and gemm_nt.supported(rows, n_out, n_in, x, weight, fused="plain_fwd"):
         return gemm_nt.linear_fwd(x.view(rows, n_in), weight, bias).view(*x.shape[:-1], n_out)
     return F.linear(x, weight, bias)
 
