@@ -74,8 +74,9 @@ forward: taken in modes fwd / all)."""
     return C is not None and hasattr(C, "gemm_nt") and bool(C.gemm_nt_supported(rows, n_out, k, k, k, n_out))
 
 
-def set_split(min_ktiles: int) -> None:
-    """The split-K tail of the persistent kernel (``FLUXMPI_GEMM_NT_SPLIT``, default 0 = off: measured slower end to end, profiles/rd5d_*): the last,
+def _set_split(min_ktiles: int) -> None:
+    """TEST / DIAGNOSTIC knob, not public API (its EPI 2 fix-up path needed the epilogue store guard,
+    root cause not pinned: profiles/rd6_store_hazard_scan.md). The split-K tail of the persistent kernel (``FLUXMPI_GEMM_NT_SPLIT``, default 0 = off: measured slower end to end, profiles/rd5d_*): the last,
     partial round of each XCD's tiles is cut into even k-tile ranges of at least ``min_ktiles``
     spread over all its workgroups (pieces summed by the last arriving workgroup, in piece order:
     deterministic); ``0`` runs the last round tile-granular."""
@@ -83,7 +84,7 @@ def set_split(min_ktiles: int) -> None:
 
 
 def get_split() -> int:
-    """The split-K tail setting in force (see :func:`set_split`)."""
+    """The split-K tail setting in force (see :func:`_set_split`)."""
     return int(_ext.get(required=True).gemm_nt_get_split())
 
 

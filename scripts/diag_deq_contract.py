@@ -20,6 +20,10 @@ def main():
     ap.add_argument("--model", default="deq")
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--labels", default="random", choices=["random", "teacher"],
+                    help="teacher: labels from a fixed random linear teacher on the 4x4-pooled input "
+                         "(a learnable synthetic task) instead of independent random labels")
+    ap.add_argument("--batches", type=int, default=1, help="distinct synthetic batches, cycled")
     a = ap.parse_args()
     import fluxmpi_amd as FluxMPI
     from fluxmpi_amd import optimisers as O
@@ -37,16 +41,24 @@ def main():
     ddp = DDP(model, O.Adam(1e-3), average=True)
     cin, img = {"deq": (1, 28), "deq_cifar": (3, 32)}[a.model]
     g = torch.Generator(device=dev).manual_seed(0)
-    x = torch.randn(a.batch, cin, img, img, device=dev, generator=g).bfloat16().contiguous(memory_format=torch.channels_last)
-    y = torch.randint(0, 10, (a.batch,), device=dev, generator=g)
+    data = []
+    teacher = torch.randn(cin * (img // 4) ** 2, 10, device=dev, generator=g)
+    for _ in range(a.batches):
+        xb = torch.randn(a.batch, cin, img, img, device=dev, generator=g)
+        if a.labels == "teacher":
+            yb = (F.avg_pool2d(xb, 4).flatten(1) @ teacher).argmax(1)
+        else:
+            yb = torch.randint(0, 10, (a.batch,), device=dev, generator=g)
+        data.append((xb.bfloat16().contiguous(memory_format=torch.channels_last), yb))
     cell = model.deq.f
     for s in range(a.steps):
+        x, y = data[s % len(data)]
         loss = F.cross_entropy(ddp(x).float(), y)
         loss.backward()
         ddp.step()
         torch.cuda.synchronize()
         wn = max(float(c.weight.float().square().sum((1, 2, 3)).sqrt().max()) for c in (cell.conv1, cell.conv2))
-        rec = {"model": a.model, "constrain": D.CONSTRAIN, "step": s, "loss": round(float(loss), 4),
+        rec = {"model": a.model, "labels": a.labels, "batches": a.batches, "constrain": D.CONSTRAIN, "step": s, "loss": round(float(loss), 4),
                "jac_reg": model.deq.jac_reg, "jr": float(model.deq.last_jr) if model.deq.last_jr is not None else None,
                "fwd_iters": model.deq.last_iters, "fwd_res": float(model.deq.last_res),
                "bwd_iters": model.deq.last_bwd_iters, "conv_norm_max": round(wn, 4), "max_norm": round(cell.max_norm, 4),

@@ -205,8 +205,8 @@ SPLIT_SHAPES = [(M_VIT, 768, 3072), (M_VIT, 768, 2304), (256 * 300, 512, 1024), 
 def split_mode():
     from fluxmpi_amd.ops import gemm_nt as G
     prev = G.get_split()  # the production default (0 = off) unless FLUXMPI_GEMM_NT_SPLIT says otherwise
-    yield G.set_split
-    G.set_split(prev)
+    yield G._set_split
+    G._set_split(prev)
     assert G.get_split() == prev
 
 
