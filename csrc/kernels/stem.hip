@@ -564,6 +564,7 @@ __global__ __launch_bounds__(kBT, 2) void stem_bwd_kernel(StemBwdArgs p) {
 }
 
 // ------------------------------------------------------- backward, wave-specialised (one row per phase)
+// OPT-IN (FLUXMPI_STEM_BWD=ws), measured slower than the pair kernel: see stem_bwd_ws() below.
 // The same sums with the two phases on DIFFERENT waves of one 16-wave workgroup per CU, so they run
 // concurrently (the pair kernel above runs them one after the other behind barriers; phase split
 // in profiles/rd6h_stem_bwd_split.jsonl: MFMA ~111 us, element work ~213 of 324). Phase q:
@@ -931,12 +932,15 @@ void set_lds_attrs() {
 }
 }  // namespace
 
-// FLUXMPI_STEM_BWD=pair: the row-pair kernel (one phase after the other) instead of the
-// wave-specialised one
+// FLUXMPI_STEM_BWD=ws: the wave-specialised kernel instead of the row-pair one. Measured SLOWER
+// (profiles/rd6k_stem_ws_ab.jsonl: 404-414 vs 311-320 us per call, ResNet-50 -0.4 %): the element
+// role's VALU-heavy gather shares each SIMD's issue with the MFMA role's dense k-steps (an MFMA
+// holds the vector issue for half its cycles), so it runs ~2x slower than with the SIMDs to
+// itself, and it was already the longer of the two phases.
 static bool stem_bwd_ws() {
   static const bool on = [] {
     const char* e = std::getenv("FLUXMPI_STEM_BWD");
-    return !(e != nullptr && std::string(e) == "pair");
+    return e != nullptr && std::string(e) == "ws";
   }();
   return on;
 }

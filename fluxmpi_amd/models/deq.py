@@ -78,8 +78,16 @@ class _AddPenaltyGrad(torch.autograd.Function):
     def backward(ctx, g):
         dt, dev = ctx.pmeta
         return g, torch.full((), ctx.weight, dtype=dt, device=dev), None
-DEQ_MNIST_SOLVER = {"max_iter": 30, "tol": 1e-3, "bwd_iter": 30, "bwd_tol": 1e-3}
-DEQ_CIFAR_SOLVER = {"max_iter": 30, "tol": 2e-2, "bwd_iter": 30, "bwd_tol": 1e-2}
+# Round 6: the caps are set so that the solves END BY TOLERANCE under training, not at the cap.
+# The trained cells contract slowly (residual curves after 40 Adam steps, fp32 alike:
+# profiles/rd6e_deq_solver_curves.jsonl; Jacobian regularisation, a max-norm constraint and
+# learnable synthetic labels did not change that, rd6h / rd6i), so the round-5 presets (30
+# iterations, MNIST tolerance 1e-3) measured iteration caps. Measured with these presets
+# (profiles/rd6k_bench_deq_presets.jsonl): MNIST 27.25 forward iterations of 60, final residual
+# <= 9.8e-3, 56 adjoint iterations; CIFAR 29 of 60, residual <= 1.9e-2, 10.25 adjoint iterations.
+# The MNIST adjoint gets 80 iterations of headroom (it needed 56 on average at tolerance 2e-2).
+DEQ_MNIST_SOLVER = {"max_iter": 60, "tol": 1e-2, "bwd_iter": 80, "bwd_tol": 2e-2}
+DEQ_CIFAR_SOLVER = {"max_iter": 60, "tol": 2e-2, "bwd_iter": 60, "bwd_tol": 1e-2}
 
 
 # host seconds spent blocked on convergence flags (LaggedFlags.pop_ready), cumulative: bench.py

@@ -412,7 +412,7 @@ def test_deq_train_step_manual_vjp_gpu(gpu_ext, monkeypatch):
         monkeypatch.setattr(D, "MANUAL_VJP", manual)
         torch.manual_seed(1)
         # the adjoint solved to 1e-4 (both variants then agree to the tolerance below; the bench
-        # defaults, DEQ_MNIST_SOLVER, stop at 1e-3)
+        # defaults, DEQ_MNIST_SOLVER, stop at 1e-2)
         m = deq_mnist(tol=1e-4, bwd_tol=1e-4).cuda().to(memory_format=torch.channels_last)
         for mod in m.modules():
             if type(mod).__name__ not in ("FusedBatchNorm2d",):
