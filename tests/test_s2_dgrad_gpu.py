@@ -7,6 +7,14 @@ import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True)
+def _s2_dgrad_on(monkeypatch):
+    """The parity-class path is opt-in (FLUXMPI_S2_DGRAD=1: measured slower than MIOpen on the
+    ResNet-50 shapes, profiles/rd6e_s2_dgrad_ab.jsonl); these tests switch it on."""
+    from fluxmpi_amd.ops import gemm as G
+    monkeypatch.setattr(G, "S2_DGRAD", True)
+
 SHAPES = [(4, 128, 56, 56, 128), (4, 256, 28, 28, 256), (4, 512, 14, 14, 512), (3, 128, 32, 32, 512),
           (2, 64, 10, 6, 96), (1, 32, 2, 2, 64)]
 
