@@ -24,6 +24,8 @@ def main():
                     help="teacher: labels from a fixed random linear teacher on the 4x4-pooled input "
                          "(a learnable synthetic task) instead of independent random labels")
     ap.add_argument("--batches", type=int, default=1, help="distinct synthetic batches, cycled")
+    ap.add_argument("--lr", type=float, default=1e-3, help="Adam learning rate")
+    ap.add_argument("--solver", default="", help="DEQ solver overrides, k=v pairs (bench.py --deq-solver)")
     a = ap.parse_args()
     import fluxmpi_amd as FluxMPI
     from fluxmpi_amd import optimisers as O
@@ -33,12 +35,16 @@ def main():
     FluxMPI.Init()
     dev = torch.device("cuda", 0)
     torch.manual_seed(1234)
-    model = build_model(a.model).to(dev, memory_format=torch.channels_last)
+    solver = {}
+    for kv in filter(None, a.solver.split(",")):
+        k, v = kv.split("=")
+        solver[k.strip()] = int(v) if k.strip() in ("max_iter", "bwd_iter") else float(v)
+    model = build_model(a.model, **solver).to(dev, memory_format=torch.channels_last)
     for m in model.modules():
         if not (isinstance(m, torch.nn.modules.batchnorm._BatchNorm) or type(m).__name__ == "FusedBatchNorm2d"):
             for p in m.parameters(recurse=False):
                 p.data = p.data.to(torch.bfloat16)
-    ddp = DDP(model, O.Adam(1e-3), average=True)
+    ddp = DDP(model, O.Adam(a.lr), average=True)
     cin, img = {"deq": (1, 28), "deq_cifar": (3, 32)}[a.model]
     g = torch.Generator(device=dev).manual_seed(0)
     data = []
@@ -58,7 +64,7 @@ def main():
         ddp.step()
         torch.cuda.synchronize()
         wn = max(float(c.weight.float().square().sum((1, 2, 3)).sqrt().max()) for c in (cell.conv1, cell.conv2))
-        rec = {"model": a.model, "labels": a.labels, "batches": a.batches, "constrain": D.CONSTRAIN, "step": s, "loss": round(float(loss), 4),
+        rec = {"model": a.model, "lr": a.lr, "labels": a.labels, "batches": a.batches, "constrain": D.CONSTRAIN, "step": s, "loss": round(float(loss), 4),
                "jac_reg": model.deq.jac_reg, "jr": float(model.deq.last_jr) if model.deq.last_jr is not None else None,
                "fwd_iters": model.deq.last_iters, "fwd_res": float(model.deq.last_res),
                "bwd_iters": model.deq.last_bwd_iters, "conv_norm_max": round(wn, 4), "max_norm": round(cell.max_norm, 4),
