@@ -244,9 +244,8 @@ struct StemBwdArgs {
   const float* inv;
   float* part;          // [gridDim.x][kPart]
   float* stats;         // BN backward sums: [kShards][2][64] (sum dz, sum dz * xhat)
-  int iters_per_block;  // row pairs (pair kernel) / rows (wave-specialised kernel) per workgroup
-  int total_iters;      // N * 56 / N * 112
-  int nimg;             // N
+  int iters_per_block;  // row pairs per workgroup
+  int total_iters;      // N * 56
 };
 
 // __restrict__: gives the transposed reads alias scopes; without them the waitcnt pass assumes they
@@ -563,318 +562,6 @@ __global__ __launch_bounds__(kBT, 2) void stem_bwd_kernel(StemBwdArgs p) {
   }
 }
 
-// ------------------------------------------------------- backward, wave-specialised (one row per phase)
-// OPT-IN (FLUXMPI_STEM_BWD=ws), measured slower than the pair kernel: see stem_bwd_ws() below.
-// The same sums with the two phases on DIFFERENT waves of one 16-wave workgroup per CU, so they run
-// concurrently (the pair kernel above runs them one after the other behind barriers; phase split
-// in profiles/rd6h_stem_bwd_split.jsonl: MFMA ~111 us, element work ~213 of 324). Phase q:
-//   waves 8-15 (element role): pool-gradient gather of conv row q from pool stage q & 1 (+ the
-//     conv-output registers loaded during phase q - 1), BN sums, dz / x tiles into tile buffer
-//     q & 1; then row q + 1's conv-output loads;
-//   waves 0-7 (MFMA role): LDS-DMA of row q + 1's pooled gradient into pool stage (q + 1) & 1,
-//     then row q - 1's 4 k-steps from tile buffer (q - 1) & 1 and halo buffer (q - 1) & 1; before
-//     the next phase's first barrier they wait for their DMA and issue row q + 1's image halo into
-//     halo buffer (q + 1) & 1 (its last reader was row q - 1's MFMA work, finished by then).
-// Only the MFMA waves issue LDS-DMA: their fragment reads carry alias scopes (tr_frag), and the
-// element waves' gather never has a DMA of its own in flight (the waitcnt pass would drain it before
-// every LDS read). Two barriers per phase, executed by all 16 waves: B1 (the stages a phase reads
-// are complete) and B2 (this phase's tiles written, its MFMA reads done). Rows are 112 pixels padded
-// to 128 (4 k-steps): the padded rows of the tiles are zero (written once), their halo reads land
-// in zero slack, G3 skips them. 16 waves per CU: each role's registers fit in 128.
-constexpr int kWT = 1024;
-constexpr int kWPix = 128;
-constexpr int kWTile = kWPix * kCo * 2;                     // 16384: one operand tile of one row
-constexpr int kWHaloRows = 8;                               // image rows 2 oy - 4 .. 2 oy + 3
-constexpr int kWHaloChunks = kWHaloRows * kBPitch;          // 944
-constexpr int kWHaloPer = 2;                                // DMA instructions per MFMA wave (1024 slots)
-constexpr int kWHalo = kWHaloPer * 512 * 16;                // 16384 (chunks 944.. zero slack)
-constexpr int kWPoolPer = 3;                                // 1536 slots >= kPoolChunks
-constexpr int kWPool = kWPoolPer * 512 * 16;                // 24576
-constexpr int kWTilesOff = 0;                               // [2 buffers][dz, x][kWTile]
-constexpr int kWHaloOff = 4 * kWTile;                       // [2 buffers][kWHalo]
-constexpr int kWPoolOff = kWHaloOff + 2 * kWHalo;           // [2 buffers][kWPool]
-constexpr int kWSmiOff = kWPoolOff + 2 * kWPool;
-constexpr int kWRedOff = kWSmiOff + 3 * kCo * 4;            // element role's BN sums [8][2][64]
-constexpr int kWSmem = kWRedOff + 8 * 2 * kCo * 4;          // 152320
-static_assert(kWHaloChunks <= kWHaloPer * 512 && kPoolChunks <= kWPoolPer * 512, "staging slots");
-static_assert((7 * kBPitch + (kWPix - 1) + 3) * 16 + 16 <= kWHalo, "halo slack covers the padded pixels");
-static_assert(kWSmem <= 160 * 1024, "LDS");
-
-__global__ __launch_bounds__(kWT) void stem_bwd_ws_kernel(StemBwdArgs p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
-  const int lane = threadIdx.x & 63;
-  float* smi = reinterpret_cast<float*>(smem + kWSmiOff);
-  float* sred = reinterpret_cast<float*>(smem + kWRedOff);  // [8][2][64]
-  if (threadIdx.x < kCo) {
-    const float m = p.mean[threadIdx.x], v = p.inv[threadIdx.x];
-    smi[threadIdx.x] = m;
-    smi[kCo + threadIdx.x] = v;
-    smi[2 * kCo + threadIdx.x] = -m * v;
-  }
-  if (threadIdx.x < 512) {  // padded pixels 112..127 of the 4 tiles, once
-    const int t = threadIdx.x >> 7, P = 112 + ((threadIdx.x >> 3) & 15), q = threadIdx.x & 7;
-    *reinterpret_cast<uint4*>(smem + kWTilesOff + t * kWTile + tile_off(P, q)) = uint4{0, 0, 0, 0};
-  } else if (threadIdx.x < 512 + 8 * 2 * kCo / 4) {
-    reinterpret_cast<float4*>(sred)[threadIdx.x - 512] = float4{0.f, 0.f, 0.f, 0.f};
-  }
-  const int it0 = blockIdx.x * p.iters_per_block;
-  const int it1 = it0 + p.iters_per_block < p.total_iters ? it0 + p.iters_per_block : p.total_iters;
-  const int n = it1 > it0 ? it1 - it0 : 0;
-
-  if (wave >= 8) {
-    // ================================================================ element role
-    const int ew = wave - 8;
-    const int cg = lane & 7, slot = lane >> 3;
-    auto item = [&](int r, bool& on, int& par, int& m) {
-      const int G = r * 8 + ew;
-      on = G < 14;
-      par = G / 7;
-      m = 8 * (G - 7 * par) + slot;
-    };
-    // unconditional loads from a valid address (a branch around a load waits for it at the join)
-    auto load_x = [&](int it, uint4 (&xr)[2]) {
-      const int img = it / kOH, oy = it - img * kOH;
-      const bf16* cb = p.c + (static_cast<int64_t>(img) * kOH + oy) * kOW * kCo + cg * 8;
-#pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        bool on;
-        int par, m;
-        item(r, on, par, m);
-        xr[r] = *reinterpret_cast<const uint4*>(cb + (on ? 2 * m + par : 0) * kCo);
-      }
-    };
-    uint4 xr[2];
-    if (n > 0) load_x(it0, xr);
-    __syncthreads();  // A: smi, zero rows, sred; row 0's stages (issued by the MFMA role)
-    for (int ph = 0; ph <= n; ++ph) {
-      __builtin_amdgcn_s_barrier();  // B1
-      if (ph < n) {
-        const int oy = (it0 + ph) % kOH;
-        const bool odd = oy & 1;
-        const bool second_prow = (oy >> 1) + 1 < kPH;
-        const int kya = odd ? 2 : 1;
-        const char* spd = smem + kWPoolOff + (ph & 1) * kWPool;  // pooled gradient [2][56][64] bf16
-        const char* spi = spd + kPoolDpBytes;                      // window index [2][56][64] u8
-        char* tdz = smem + kWTilesOff + (ph & 1) * 2 * kWTile;
-        char* tx = tdz + kWTile;
-        float s1[8], sx[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) s1[e] = sx[e] = 0.f;
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-          bool on;
-          int par, m;
-          item(r, on, par, m);
-          if (on) {
-            const int kxa = par ? 2 : 1;
-            const bool two_w = par && m + 1 < kPW;
-            const bool two_h = odd && second_prow;
-            const int e00 = m * kCo + cg * 8;
-            float dz[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-            auto visit = [&](int e0, int kk) {
-              const uint4 dv = *reinterpret_cast<const uint4*>(spd + e0 * 2);
-              const uint2 iv2 = *reinterpret_cast<const uint2*>(spi + e0);
-              bf16 d8[8];
-              uint8_t a8[8];
-              __builtin_memcpy(d8, &dv, 16);
-              __builtin_memcpy(a8, &iv2, 8);
-#pragma unroll
-              for (int e = 0; e < 8; ++e)
-                if (static_cast<int>(a8[e]) == kk) dz[e] += static_cast<float>(d8[e]);
-            };
-            visit(e00, kya * 3 + kxa);
-            if (two_w) visit(e00 + kCo, kya * 3);
-            if (two_h) {
-              visit(e00 + kPW * kCo, kxa);
-              if (two_w) visit(e00 + kPW * kCo + kCo, 0);
-            }
-            bf16 x8[8], z8[8];
-            __builtin_memcpy(x8, &xr[r], 16);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              z8[e] = static_cast<bf16>(dz[e]);
-              s1[e] += dz[e];
-              sx[e] = fmaf(dz[e], static_cast<float>(x8[e]), sx[e]);
-            }
-            uint4 zv;
-            __builtin_memcpy(&zv, z8, 16);
-            const int o = tile_off(2 * m + par, cg);
-            *reinterpret_cast<uint4*>(tdz + o) = zv;
-            *reinterpret_cast<uint4*>(tx + o) = xr[r];
-          }
-        }
-        if (ph + 1 < n) load_x(it0 + ph + 1, xr);
-        // BN sums per (element wave, channel), flushed once per row: sum(dz) and
-        // sum(dz * xhat) = inv * sum(dz * x) + (-mean * inv) * sum(dz) over the row's items
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          s1[e] = butterfly_from<8>(s1[e]);
-          sx[e] = butterfly_from<8>(sx[e]);
-        }
-        if (lane < 8) {
-          float iv[8], nm[8];
-          __builtin_memcpy(iv, smi + kCo + lane * 8, 32);
-          __builtin_memcpy(nm, smi + 2 * kCo + lane * 8, 32);
-          float* r0 = sred + (ew * 2) * kCo + lane * 8;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            r0[e] += s1[e];
-            r0[kCo + e] += fmaf(iv[e], sx[e], nm[e] * s1[e]);
-          }
-        }
-      }
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): tile writes done; conv-output loads in flight
-      __builtin_amdgcn_s_barrier();         // B2
-    }
-    wait_vm0();
-    __syncthreads();  // E
-    __syncthreads();  // F
-    if (threadIdx.x - 512 < 2 * kCo) {
-      const int t = threadIdx.x - 512, which = t >> 6, c = t & 63;
-      float s = 0.f;
-#pragma unroll
-      for (int w2 = 0; w2 < 8; ++w2) s += sred[(w2 * 2 + which) * kCo + c];
-      atomicAdd(p.stats + static_cast<size_t>(blockIdx.x % kShards) * 2 * kCo + which * kCo + c, s);
-    }
-  } else {
-    // ================================================================ MFMA role (+ the stage DMA)
-    // DMA pieces of this lane: slot L = (i * 8 + wave) * 64 + lane of a stage
-    // Stage DMA through buffer resources: wave-uniform bases in SGPRs, one 32-bit lane offset per
-    // piece, and out-of-range offsets (padding pixels, rows outside the image, unused slots, the
-    // pooled row past the last image) read as zeros — few VGPRs in this role's loop (128 budget).
-    auto issue_pool = [&](int it, int buf) {
-      const int img = it / kOH, oy = it - img * kOH;
-      const int64_t pimg = (static_cast<int64_t>(img) * kPH + (oy >> 1)) * kPW * kCo;
-      const int64_t rest = static_cast<int64_t>(p.nimg) * kPH * kPW * kCo - pimg;  // elements from the row on
-      const __amdgpu_buffer_rsrc_t rdp = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<bf16*>(p.dp) + pimg, 0, static_cast<int>(rest * 2 < 0x7fffffff ? rest * 2 : 0x7fffffff), 0x00020000);
-      const __amdgpu_buffer_rsrc_t rix = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<uint8_t*>(p.idx) + pimg, 0, static_cast<int>(rest < 0x7fffffff ? rest : 0x7fffffff), 0x00020000);
-      char* dst = smem + kWPoolOff + buf * kWPool;
-#pragma unroll
-      for (int i = 0; i < kWPoolPer; ++i) {
-        const int L0 = (i * 8 + wave) * 64;  // wave-uniform: the dp / idx / unused boundaries are multiples of 64
-        const bool is_dp = L0 < kPoolDpBytes / 16;
-        const uint32_t off = L0 < kPoolChunks ? static_cast<uint32_t>((is_dp ? L0 : L0 - kPoolDpBytes / 16) + lane) * 16
-                                              : 0x80000000u;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(is_dp ? rdp : rix, (lds_char*)(dst + (i * 8 + wave) * 1024), 16,
-                                                 static_cast<int>(off), 0, 0, 0);
-      }
-    };
-    uint32_t lofs[kWHaloPer];  // this lane's halo chunk: byte offset from its image row, or out of range
-#pragma unroll
-    for (int i = 0; i < kWHaloPer; ++i) {
-      const int L = (i * 8 + wave) * 64 + lane;
-      const int hr = L / kBPitch, j = L - hr * kBPitch;
-      const bool ok = L < kWHaloChunks && j >= 2 && j <= kIW / 2 + 1;
-      lofs[i] = ok ? static_cast<uint32_t>(hr * kIW * 8 + (2 * j - 4) * 8) : 0x80000000u;
-    }
-    auto issue_halo = [&](int it, int buf) {
-      const int img = it / kOH, oy = it - img * kOH;
-      const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<bf16*>(p.x) + static_cast<int64_t>(img) * kIH * kIW * 4, 0, kIH * kIW * 8, 0x00020000);
-      const int rowterm = (2 * oy - 4) * kIW * 8;  // may be negative: rows above the image wrap out of range
-      char* dst = smem + kWHaloOff + buf * kWHalo;
-#pragma unroll
-      for (int i = 0; i < kWHaloPer; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_char*)(dst + (i * 8 + wave) * 1024), 16,
-                                                 static_cast<int>(lofs[i] + static_cast<uint32_t>(rowterm)), 0, 0, 0);
-    };
-    const int g = lane >> 4, li = lane & 15, q4 = li >> 2, pp = li & 3;
-    const bool gx = wave >= 4;
-    const int wn = wave & 3;
-    f32x4 acc[4][4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int nn = 0; nn < 4; ++nn) acc[t][nn] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float g3[4] = {0.f, 0.f, 0.f, 0.f};
-    const int P0 = 8 * g + q4;
-    int a_lo[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-      a_lo[t] = kWTilesOff + (gx ? kWTile : 0) + tile_off(P0, 2 * t + (pp >> 1)) + (pp & 1) * 8;
-    int b_lo[4];
-#pragma unroll
-    for (int nn = 0; nn < 4; ++nn) {
-      const int kc = 2 * (4 * wn + nn) + (pp >> 1);
-      const int ay = kc & 3, ax = (kc >> 2) & 3, by = kc >> 4;
-      b_lo[nn] = kWHaloOff + (2 * ay + by) * (kBPitch * 16) + ax * 16 + (pp & 1) * 8 + P0 * 16;
-    }
-    if (n > 0) issue_pool(it0, 0);
-    wait_vm0();
-    __syncthreads();  // A
-    for (int ph = 0; ph <= n; ++ph) {
-      __builtin_amdgcn_s_barrier();  // B1: pool stage ph & 1 (row ph) and halo buffer (ph - 1) & 1 complete
-      // row ph + 1's pool stage (its buffer's last reader: row ph - 1's gather) and row ph's halo
-      // (its buffer's last reader: row ph - 2's MFMA work), both waited for before B2
-      if (ph + 1 < n) issue_pool(it0 + ph + 1, (ph + 1) & 1);
-      if (ph < n) issue_halo(it0 + ph, ph & 1);
-      if (ph >= 1) {
-        const int buf = (ph - 1) & 1;
-        const int ta = buf * 2 * kWTile, hb = buf * kWHalo;
-#pragma unroll
-        for (int ks = 0; ks < kWPix / 32; ++ks) {
-          bf16x8 fa[4];
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const char* lo = smem + a_lo[t] + ta + ks * 4096;
-            fa[t] = tr_frag(lo, lo + 512);
-          }
-          // column sums over the real pixels (k-step 3: lane groups 0-1), the k-steps split between the
-          // two wave groups; branch-free (a divergent branch here cost registers: spills)
-          const bool colsum = gx == static_cast<bool>(ks & 1) && (ks < 3 || g < 2);
-          const bf16 one = static_cast<bf16>(colsum ? 1.f : 0.f);
-          const bf16x2 w1 = {one, one};
-#pragma unroll
-          for (int nn = 0; nn < 4; ++nn) {
-            const char* lo = smem + b_lo[nn] + hb + ks * 512;
-            const bf16x8 fb = tr_frag(lo, lo + 64);
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-              acc[t][nn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[t], fb, acc[t][nn], 0, 0, 0);
-            {
-              bf16x2 h2[4];
-              __builtin_memcpy(h2, &fb, 16);
-#pragma unroll
-              for (int j = 0; j < 4; ++j) g3[nn] = __builtin_amdgcn_fdot2_f32_bf16(h2[j], w1, g3[nn], false);
-            }
-            __builtin_amdgcn_sched_barrier(0);  // one B fragment live at a time (128-VGPR budget)
-          }
-        }
-      }
-      __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0): this wave's DMA landed, fragment reads done
-      __builtin_amdgcn_s_barrier();         // B2
-    }
-    __syncthreads();  // E
-    float* part = p.part + static_cast<size_t>(blockIdx.x) * kPart;
-    float* gp = part + (gx ? kKk * kCo : 0);
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int nn = 0; nn < 4; ++nn) {
-        const int k = 16 * (4 * wn + nn) + li;
-        *reinterpret_cast<f32x4*>(gp + k * kCo + 16 * t + 4 * g) = acc[t][nn];
-      }
-#pragma unroll
-    for (int nn = 0; nn < 4; ++nn) g3[nn] = butterfly_from<16>(g3[nn]);
-    float* red3 = reinterpret_cast<float*>(smem);  // [256] (the tiles are free after E)
-    if (gx && g == 0) {
-#pragma unroll
-      for (int nn = 0; nn < 4; ++nn) red3[16 * (4 * wn + nn) + li] = g3[nn];
-    }
-    __syncthreads();  // F
-    if (!gx && g == 0) {
-#pragma unroll
-      for (int nn = 0; nn < 4; ++nn) {
-        const int k = 16 * (4 * wn + nn) + li;
-        part[2 * kKk * kCo + k] = g3[nn] + red3[k];
-      }
-    }
-  }
-}
-
 // dW'[c][k] = a_c G1[k][c] + b_c G2[k][c] + d_c G3[k] summed over the partials: one workgroup per k,
 // 4 groups of 64 lanes (channels) split the partials, LDS sum. a, b, d as in bn_bwd_dx_kernel.
 constexpr int kCT = 256;
@@ -926,33 +613,17 @@ void set_lds_attrs() {
   for (const void* k : {reinterpret_cast<const void*>(&stem_bwd_kernel<0>), reinterpret_cast<const void*>(&stem_bwd_kernel<1>),
                         reinterpret_cast<const void*>(&stem_bwd_kernel<2>), reinterpret_cast<const void*>(&stem_bwd_kernel<3>)})
     FLUXMPI_HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kBSmem));
-  FLUXMPI_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&stem_bwd_ws_kernel),
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, kWSmem));
   done = true;
 }
 }  // namespace
 
-// FLUXMPI_STEM_BWD=ws: the wave-specialised kernel instead of the row-pair one. Measured SLOWER
-// (profiles/rd6k_stem_ws_ab.jsonl: 404-414 vs 311-320 us per call, ResNet-50 -0.4 %): the element
-// role's VALU-heavy gather shares each SIMD's issue with the MFMA role's dense k-steps (an MFMA
-// holds the vector issue for half its cycles), so it runs ~2x slower than with the SIMDs to
-// itself, and it was already the longer of the two phases.
-static bool stem_bwd_ws() {
-  static const bool on = [] {
-    const char* e = std::getenv("FLUXMPI_STEM_BWD");
-    return e != nullptr && std::string(e) == "ws";
-  }();
-  return on;
-}
-
 int stem_bwd_blocks(int64_t n) {
   static int b = [] {
     set_lds_attrs();
-    const int r = stem_bwd_ws() ? resident_blocks(reinterpret_cast<const void*>(&stem_bwd_ws_kernel), kWT, kWSmem)
-                                : resident_blocks(reinterpret_cast<const void*>(&stem_bwd_kernel<0>), kBT, kBSmem);
-    return r > 0 ? r : 256;
+    const int r = resident_blocks(reinterpret_cast<const void*>(&stem_bwd_kernel<0>), kBT, kBSmem);
+    return r > 0 ? r : 512;
   }();
-  const int64_t iters = n * (stem_bwd_ws() ? kOH : kPH);
+  const int64_t iters = n * kPH;
   return static_cast<int>(iters < b ? iters : b);
 }
 
@@ -990,16 +661,11 @@ void stem_bwd(const void* x, const void* c, const void* dp, const uint8_t* idx, 
     const int v = e != nullptr ? std::atoi(e) : 0;
     return v >= 0 && v <= 3 ? v : 0;
   }();
-  const bool ws = stem_bwd_ws() && mode == 0;
-  const int total = static_cast<int>(n * (ws ? kOH : kPH));
+  const int total = static_cast<int>(n * kPH);
   StemBwdArgs a{static_cast<const bf16*>(x), static_cast<const bf16*>(c), static_cast<const bf16*>(dp), idx, mean, inv,
-                part, stats, (total + blocks - 1) / blocks, total, static_cast<int>(n)};
-  if (ws) {
-    stem_bwd_ws_kernel<<<static_cast<unsigned>(blocks), kWT, kWSmem, s>>>(a);
-  } else {
-    auto kern = mode == 1 ? stem_bwd_kernel<1> : mode == 2 ? stem_bwd_kernel<2> : mode == 3 ? stem_bwd_kernel<3> : stem_bwd_kernel<0>;
-    kern<<<static_cast<unsigned>(blocks), kBT, kBSmem, s>>>(a);
-  }
+                part, stats, (total + blocks - 1) / blocks, total};
+  auto kern = mode == 1 ? stem_bwd_kernel<1> : mode == 2 ? stem_bwd_kernel<2> : mode == 3 ? stem_bwd_kernel<3> : stem_bwd_kernel<0>;
+  kern<<<static_cast<unsigned>(blocks), kBT, kBSmem, s>>>(a);
   FLUXMPI_HIP_CHECK(hipGetLastError());
   bn_finalize_bwd(stats, kCo, dw_bn, db_bn, s);
   stem_wgrad_combine_kernel<<<kKk, kCT, 0, s>>>(part, blocks, w, mean, inv, dw_bn, db_bn,

@@ -23,7 +23,6 @@ import torch.nn.functional as F
 
 from . import _ext
 from . import graddst
-from . import wgrad_stream
 from .multi_tensor import DTYPE_CODE
 
 # (N_out, N_in) -> split-K factor, from scripts/bench_vit_gemm.py on MI355X (M = 50432 tokens)
@@ -215,8 +214,7 @@ class _LinearFn(torch.autograd.Function):
                     if same:  # short K (e.g. a classifier head): hipBLASLt, output in the slice
                         return torch.mm(dy2.t(), x2, out=graddst.empty(tuple(w.shape), w.dtype, dy2.device))
                     return (dy2.t() @ x2).to(w.dtype)
-            # on the side stream (ops/wgrad_stream.py): concurrent with the input-gradient chain
-            dw = wgrad_stream.run(wgrad, w, dy2, x2)
+            dw = wgrad()
         if need_b:
             with graddst.into(ctx.bias):
                 if native:

@@ -56,7 +56,6 @@ from .. import optimisers as O
 from ..ops import multi_tensor as mt
 from ..ops import _ext
 from ..ops import graddst
-from ..ops import wgrad_stream
 from ..ops import optim as fused
 from ..utils.config import get_config
 from ..utils import profiling
@@ -225,11 +224,6 @@ class DDP:
                     graddst.attach(p, b.flat_grad, o)
                 else:
                     graddst.detach(p)  # a previous engine's buckets are not this one's
-        # weight gradients of this engine's parameters may run on the side stream
-        # (ops/wgrad_stream.py): "steal" mode only — autograd hands over each gradient, no
-        # in-place accumulation kernel reads it before the end-of-backward join
-        self.wgrad_stream = self.grad_mode == "steal" and self.device.type == "cuda" and wgrad_stream.ENABLED
-        wgrad_stream.enable(params, self.wgrad_stream)
         self._hooks = []
         self._sync_enabled = True
         # per-bucket optimiser overlap: on the communicator's in-order stream (behind the bucket's
@@ -476,7 +470,6 @@ class DDP:
             return
         if not self.communicate:
             st.wait_stream(torch.cuda.current_stream(self.device))
-        wgrad_stream.fence(st, self.device)  # weight gradients still running on the side stream
         with torch.cuda.stream(st):
             if self.communicate:
                 if b.comm_buf is not None and self.comm_dtype != b.dtype:
@@ -490,8 +483,6 @@ class DDP:
 
     def _launch_comm(self, b: _Bucket):
         self._pack(b)
-        if self.wgrad_stream and getattr(self.comm, "stream", None) is not None:
-            wgrad_stream.fence(self.comm.stream, self.device)  # side-stream weight gradients first
         buf = b.flat_grad
         if self.comm_dtype is not None and self.comm_dtype != b.dtype:
             # K5: cast the bucket to the wire dtype (e.g. fp32 grads sent as bf16) in one launch
@@ -585,9 +576,6 @@ class DDP:
                 dst.copy_(g)
                 self._note_copy(p)
         if srcs:
-            if self.wgrad_stream and wgrad_stream.pending(b.device):
-                # the copies read gradients the side stream may still be writing
-                torch.cuda.current_stream(b.device).wait_stream(wgrad_stream.side_stream(b.device))
             C = _ext.get(required=True)
             code = mt.DTYPE_CODE[b.dtype]
             C.mt_copy([g.data_ptr() for g in srcs], dptrs, ns, code, code, 1.0,
@@ -915,7 +903,7 @@ class DDP:
                 "bucket_mb": [round(b.numel * b.flat_grad.element_size() / 2 ** 20, 2) for b in self.buckets],
                 "comm": (self.comm.name if self.communicate else "none"),
                 "direct_grads": self.direct_grads, "overlap_opt": self.overlap_opt,
-                "wgrad_stream": self.wgrad_stream, "bucket_plan": self.bucket_plan,
+                "bucket_plan": self.bucket_plan,
                 "comm_probe": self.comm_probe,
                 # gradients the packs copied per step so far (0: every one delivered in place)
                 "pack_copies_per_step": round(self.pack_copies / max(1, self.step_count), 2),
@@ -930,7 +918,6 @@ class DDP:
         for h in self._hooks:
             h.remove()
         self._hooks.clear()
-        wgrad_stream.enable([p for b in self.buckets for p in b.params], False)
 
 
 __all__ = ["DDP"]

@@ -107,36 +107,3 @@ def test_overlap_opt_bitwise_gpu(gpu_ext, force_comm):
         outs.append([p.detach().clone() for p in m.parameters()] + [b.master.clone() for b in d.buckets])
     for a, b in zip(*outs):
         assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("force_comm", [False, True])
-def test_wgrad_stream_bitwise_gpu(gpu_ext, force_comm, monkeypatch):
-    """Weight gradients on the side stream (``ops/wgrad_stream.py``, opt-in): the same Linear
-    kernels on another stream, joined at the end of backward / fenced before each allreduce, give
-    bit-identical parameters to the single-stream run (token-major bf16 Linears on the HIP wgrad
-    path, several buckets, a parameter used twice so the accumulation join is exercised)."""
-    import fluxmpi_amd as FluxMPI
-    from fluxmpi_amd import optimisers as O
-    from fluxmpi_amd.ops import wgrad_stream
-    from fluxmpi_amd.ops.linear import Linear
-    from fluxmpi_amd.parallel.ddp import DDP
-    FluxMPI.Init()
-    x = torch.randn(2048, 256, device="cuda").bfloat16()
-    outs = []
-    for on in (False, True):
-        monkeypatch.setattr(wgrad_stream, "ENABLED", on)
-        torch.manual_seed(4)
-        m = torch.nn.Sequential(Linear(256, 512), torch.nn.GELU(), Linear(512, 256)).cuda().bfloat16()
-        d = DDP(m, O.Adam(1e-2), bucket_mb=0.2, first_bucket_mb=0.1, force_comm=force_comm)
-        assert d.wgrad_stream == on
-        n0 = wgrad_stream.launches
-        for _ in range(3):
-            h = d(x)
-            (d(h) - h).float().square().mean().backward()  # every Linear used twice
-            d.step()
-        torch.cuda.synchronize()
-        assert (wgrad_stream.launches > n0) == on
-        outs.append([p.detach().clone() for p in m.parameters()])
-        d.remove_hooks()
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)

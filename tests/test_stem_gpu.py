@@ -90,16 +90,3 @@ def test_stem_bwd_deterministic():
         outs.append(conv.weight.grad.clone())
     assert torch.equal(outs[0], outs[1]) or _rel(outs[0], outs[1]) < 1e-5
 
-
-def test_stem_bwd_wave_specialised_variant():
-    """The opt-in wave-specialised backward (FLUXMPI_STEM_BWD=ws, read once per process by the
-    native library) passes the same reference checks, in a child process."""
-    import os
-    import subprocess
-    import sys
-    env = dict(os.environ, FLUXMPI_STEM_BWD="ws")
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider",
-                        os.path.join(root, "tests", "test_stem_gpu.py"), "-k", "matches_reference or deterministic"],
-                       env=env, cwd=root, capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
