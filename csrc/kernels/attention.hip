@@ -920,6 +920,173 @@ __global__ __launch_bounds__(1024) void attn_bwd_dkv_res_kernel(AttnBwdArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Fused backward, one workgroup per (batch, head), one wave per 16 keys / 16 queries (NT waves):
+//   phase 1  the dK / dV sweep of attn_bwd_dkv_res (each wave: its 16 keys against every query in
+//            k-steps of 32: S = Q K^T, dP = dO V^T, P, dS = P (dP - D), dV^T += dO^T P,
+//            dK^T += Q^T dS) that ALSO writes dS into an LDS image [query][key] (bf16);
+//   phase 2  with K staged into the Q image's slot: dQ^T = K^T dS^T per wave of 16 queries (A = K^T
+//            by transposed reads of the K image, B = dS^T from two 8-B reads of a dS row, in the
+//            accumulator-pair k order of img_tr).
+// S, P, dP and dS are computed ONCE (the dq / dkv pair computes S and dP in both kernels), Q, K, V,
+// dO and O are read once, and D = rowsum(dO * O) is formed in the prologue (no stats round trip).
+// LDS: Q (then K) and dO images 2 x TV x 128 B, the dS image 16 NT x 464 B, lse / D 2 x TV floats:
+// 152 KB at T = 197, one workgroup of NT = 13 waves per CU (the pair holds 2 x 7).
+// dS rows are 464 B (116 dwords = 4 x 29 mod 64: a 32-lane half of the phase-2 ds_read_b64 pair
+// touches 16 rows x 2 groups on distinct 4-dword bank slots); keys >= 16 NT are zero columns (their
+// K rows are zero, and 0 * uninitialised could be NaN).
+constexpr int kDsRow = 464;
+
+template <int NT>
+__global__ __launch_bounds__(1024) void attn_bwd_fused_kernel(AttnBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int TV = ((16 * NT + 31) / 32) * 32;  // key / query rows of the images (224 at NT = 13)
+  constexpr int NQ = 16 * NT;                      // dS rows = queries the waves own (208)
+  constexpr int KS = TV / 32;
+  char* qimg = smem;               // phase 1: Q image; phase 2: K image
+  char* gimg = smem + TV * 128;    // dO image
+  char* dsimg = smem + 2 * TV * 128;
+  float* sL = reinterpret_cast<float*>(dsimg + NQ * kDsRow);
+  float* sD = sL + TV;
+  int part, h, b;
+  res_coords(a, b, h, part);  // a.nblk == 1
+  stage_rows<false>(qimg, a.q + b * a.sq_b + h * DH, a.sq_t, TV, a.T);
+  stage_rows<false>(gimg, a.dout + b * a.sg_b + h * DH, a.sg_t, TV, a.T);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, col = lane & 15, g = lane >> 4;
+  // zero dS columns NQ .. TV - 1 of every row (32 B per row: two 16-B pieces)
+  for (int i = threadIdx.x; i < NQ * 2; i += blockDim.x)
+    *reinterpret_cast<uint4*>(dsimg + (i >> 1) * kDsRow + NQ * 2 + (i & 1) * 16) = uint4{0, 0, 0, 0};
+  // phase-1 keys of this wave
+  const int k0 = 16 * w, ki = k0 + col;
+  const bool kok = ki < a.T;
+  const int64_t koff = b * a.sq_b + static_cast<int64_t>(ki) * a.sq_t + h * DH;
+  bf16x8 kf[2] = {}, vf[2] = {};
+  if (kok) {
+    kf[0] = ld8(a.k + koff + 8 * g);
+    kf[1] = ld8(a.k + koff + 32 + 8 * g);
+    vf[0] = ld8(a.v + koff + 8 * g);
+    vf[1] = ld8(a.v + koff + 32 + 8 * g);
+  }
+  // phase-2 queries of this wave: D = rowsum(dO * O) and lse into LDS for every query
+  const int q0 = 16 * w, qi = q0 + col;
+  const bool qok = qi < a.T;
+  const int64_t qoff = b * a.sq_b + static_cast<int64_t>(qi) * a.sq_t + h * DH;
+  bf16x8 gf[2] = {}, o0 = {}, o1 = {};
+  float lse = kInf;
+  if (qok) {
+    const bf16* gp = a.dout + b * a.sg_b + static_cast<int64_t>(qi) * a.sg_t + h * DH;
+    gf[0] = ld8(gp + 8 * g);
+    gf[1] = ld8(gp + 32 + 8 * g);
+    const bf16* op = a.o + b * a.so_b + static_cast<int64_t>(qi) * a.so_t + h * a.so_h;
+    o0 = ld8(op + 8 * g);
+    o1 = ld8(op + 32 + 8 * g);
+    lse = a.stats[((static_cast<int64_t>(b) * a.H + h) * a.T + qi) * 2];
+  }
+  float dsum = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dsum += (float)gf[0][j] * (float)o0[j] + (float)gf[1][j] * (float)o1[j];
+  dsum = butterfly_from<16>(dsum);  // over the 4 lane groups of the query
+  if (g == 0) {
+    sL[qi] = lse;
+    sD[qi] = qok ? dsum : 0.f;
+  }
+  for (int qq = NQ + threadIdx.x; qq < TV; qq += blockDim.x) {
+    sL[qq] = kInf;
+    sD[qq] = 0.f;
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+
+  // ---- phase 1: dK^T, dV^T of this wave's keys; dS into the image
+  const float c2 = a.scale * kLog2e;
+  f32x4 accK[4] = {}, accV[4] = {};
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    f32x4 p[2], dsv[2];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int row = 32 * ks + 16 * half + col;  // query row of the A fragment
+      f32x4 sv = {}, dp = {};
+      sv = mfma(img_row(qimg, row, g), kf[0], sv);
+      sv = mfma(img_row(qimg, row, 4 + g), kf[1], sv);
+      dp = mfma(img_row(gimg, row, g), vf[0], dp);
+      dp = mfma(img_row(gimg, row, 4 + g), vf[1], dp);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qq = 32 * ks + 16 * half + 4 * g + r;
+        const float pv = fast_exp2(fmaf(sv[r], c2, -sL[qq]));  // padded query: lse = +inf -> 0
+        p[half][r] = pv;
+        dsv[half][r] = pv * (dp[r] - sD[qq]);
+      }
+      if (32 * ks + 16 * half < NQ) {  // compile-time: rows past the waves' queries are not in the image
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          *reinterpret_cast<bf16*>(dsimg + (32 * ks + 16 * half + 4 * g + r) * kDsRow + (k0 + col) * 2) =
+              static_cast<bf16>(dsv[half][r]);
+      }
+    }
+    const bf16x8 pb = pack(p[0], p[1]), db = pack(dsv[0], dsv[1]);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      accV[dt] = mfma(img_tr(gimg, 32 * ks, 16 * dt), pb, accV[dt]);
+      accK[dt] = mfma(img_tr(qimg, 32 * ks, 16 * dt), db, accK[dt]);
+    }
+  }
+  if (kok) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const bf16x4 v = {(bf16)accV[dt][0], (bf16)accV[dt][1], (bf16)accV[dt][2], (bf16)accV[dt][3]};
+      const bf16x4 k = {(bf16)(accK[dt][0] * a.scale), (bf16)(accK[dt][1] * a.scale),
+                        (bf16)(accK[dt][2] * a.scale), (bf16)(accK[dt][3] * a.scale)};
+      *reinterpret_cast<bf16x4*>(a.dv + koff + dt * 16 + 4 * g) = v;
+      *reinterpret_cast<bf16x4*>(a.dk + koff + dt * 16 + 4 * g) = k;
+    }
+  }
+  if (a.colpart != nullptr) {
+    colpart_store(colpart_row(a, b, h, 0, w, 1), accK, a.scale, kok);
+    colpart_store(colpart_row(a, b, h, 0, w, 2), accV, 1.f, kok);
+  }
+  __syncthreads();  // dS complete, the Q image's last reads done
+  stage_rows<false>(qimg, a.k + b * a.sq_b + h * DH, a.sq_t, TV, a.T);  // the K image
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+
+  // ---- phase 2: dQ^T[d][q] = sum over keys of K^T[d][key] dS^T[key][q], this wave's 16 queries
+  f32x4 acc[4] = {};
+  const char* drow = dsimg + qi * kDsRow;  // qi < NQ always (16 NT rows)
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const bf16x4 lo = *reinterpret_cast<const bf16x4*>(drow + (32 * ks + 4 * g) * 2);
+    const bf16x4 hi = *reinterpret_cast<const bf16x4*>(drow + (32 * ks + 16 + 4 * g) * 2);
+    const bf16x8 bop = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) acc[dt] = mfma(img_tr(qimg, 32 * ks, 16 * dt), bop, acc[dt]);
+  }
+  if (qok) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const bf16x4 o = {(bf16)(acc[dt][0] * a.scale), (bf16)(acc[dt][1] * a.scale), (bf16)(acc[dt][2] * a.scale),
+                        (bf16)(acc[dt][3] * a.scale)};
+      *reinterpret_cast<bf16x4*>(a.dq + qoff + dt * 16 + 4 * g) = o;
+    }
+  }
+  if (a.colpart != nullptr) colpart_store(colpart_row(a, b, h, 0, w, 0), acc, a.scale, qok);
+}
+
+constexpr size_t fused_lds(int nt) {
+  return static_cast<size_t>(2 * (((16 * nt + 31) / 32) * 32) * 128 + 16 * nt * kDsRow +
+                             2 * (((16 * nt + 31) / 32) * 32) * 4);
+}
+
+// FLUXMPI_ATTN_BWD=fused: the one-kernel backward (T 193..208, i.e. 13 key / query tiles)
+bool attn_fused_env() {
+  static const bool on = [] {
+    const char* e = std::getenv("FLUXMPI_ATTN_BWD");
+    return e != nullptr && std::string(e) == "fused";
+  }();
+  return on;
+}
+
 // FLUXMPI_ATTN_GENERIC=1: the runtime-tile-count kernels for every T (A/B of the NT = 13 instances)
 // explicitly pipelined dkv k-steps for the compile-time-tile-count kernel (FLUXMPI_ATTN_DKV_PIPE=0: off)
 bool dkv_pipe() {
@@ -966,6 +1133,7 @@ int attn_bwd_colpart_rows(int B, int T, int H, int64_t sq_t, int64_t sg_t) {
   // the resident dq / dkv pair writes the column-sum partials; every other variant does not
   if (blocked_env("FLUXMPI_ATTN_BWD") || T > kResMaxT || T <= 0 || (sq_t % 8) != 0 || (sg_t % 8) != 0) return 0;
   const int tiles = (T + 15) / 16;
+  if (attn_fused_env() && tiles == 13) return B * tiles;  // the fused kernel: one part of 13 waves
   const int nblk = res_parts(tiles);
   const int waves = (tiles + nblk - 1) / nblk;
   (void)H;
@@ -989,6 +1157,22 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* o, const 
   static const bool resident = !blocked_env("FLUXMPI_ATTN_BWD");
   if (resident && T <= kResMaxT && (sq_t % 8) == 0 && (sg_t % 8) == 0) {
     const int tiles = (T + 15) / 16;
+    if (attn_fused_env() && tiles == 13 && !attn_generic()) {
+      a.nblk = 1;
+      const int64_t bh = static_cast<int64_t>(B) * H;
+      if (bh > 0x7fffffff) throw std::runtime_error("attn_bwd: grid too large");
+      a.colpart = colpart;  // [B * 13][3 * H * 64] (attn_bwd_colpart_rows), or nullptr
+      static const bool attr = [] {
+        FLUXMPI_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_fused_kernel<13>),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              static_cast<int>(fused_lds(13))));
+        return true;
+      }();
+      (void)attr;
+      attn_bwd_fused_kernel<13><<<static_cast<unsigned>(bh), 13 * 64, fused_lds(13), s>>>(a);
+      FLUXMPI_HIP_CHECK(hipGetLastError());
+      return;
+    }
     a.nblk = res_parts(tiles);
     const int64_t bh = static_cast<int64_t>(B) * H * a.nblk;
     if (bh > 0x7fffffff) throw std::runtime_error("attn_bwd: grid too large");

@@ -105,3 +105,43 @@ def test_attn_bwd_colsum_partials(gpu_ext, b, t, heads):
     dqkv2 = attn_bwd_packed(xb, out, g, heads, stats)
     dqkv2.add_(1.0)
     assert take_colpart(dqkv2.view(b * t, -1)) is None
+
+
+@pytest.mark.gpu
+def test_attn_bwd_fused_variant(gpu_ext):
+    """The one-kernel backward (FLUXMPI_ATTN_BWD=fused, read once per process by the native
+    library; taken for 13 key tiles, T 193..208): the fp32-reference and column-sum tests of this
+    file, in a child process with the variant on."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, FLUXMPI_ATTN_BWD="fused")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider",
+                        os.path.join(root, "tests", "test_attention_gpu.py"), "-k",
+                        "attn_bwd_vs_fp32 or colsum_partials or fused_matches_pair"],
+                       env=env, cwd=root, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+@pytest.mark.gpu
+def test_attn_bwd_fused_matches_pair(gpu_ext):
+    """Run by the child process of test_attn_bwd_fused_variant (a no-op comparison otherwise): at
+    the ViT shape the fused kernel's dQKV and column sums agree with the fp32 reference."""
+    from fluxmpi_amd.ops.attention import attn_bwd_packed, attn_fwd_packed, take_colpart
+    torch.manual_seed(5)
+    b, t, heads = 4, 197, 12
+    xb = (torch.randn(b, t, 3 * heads * 64, device="cuda") * 1.5).to(torch.bfloat16)
+    xr = xb.float().requires_grad_()
+    yr = _ref(xr, heads)
+    g = torch.randn_like(yr)
+    yr.backward(g)
+    out, stats = attn_fwd_packed(xb, heads)
+    dqkv = attn_bwd_packed(xb, out, g.to(torch.bfloat16), heads, stats)
+    assert torch.isfinite(dqkv).all()
+    for i in range(3):
+        assert _rel(dqkv.view(b, t, 3, -1)[:, :, i], xr.grad.view(b, t, 3, -1)[:, :, i]) < 2e-2, i
+    part = take_colpart(dqkv.view(b * t, -1))
+    assert part is not None
+    ref = dqkv.float().sum((0, 1))
+    torch.testing.assert_close(part.sum(0), ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item() / 10 + 1e-3)
