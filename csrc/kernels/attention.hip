@@ -1078,11 +1078,14 @@ constexpr size_t fused_lds(int nt) {
                              2 * (((16 * nt + 31) / 32) * 32) * 4);
 }
 
-// FLUXMPI_ATTN_BWD=fused: the one-kernel backward (T 193..208, i.e. 13 key / query tiles)
+// the one-kernel backward for 13 key / query tiles (T 193..208: ViT's 197), default; measured 286-289
+// vs 340-343 us per call for the dq / dkv pair, ViT-B/16 7698 / 7694 vs 7549 / 7588 img/s on one box
+// (profiles/rd6o_attn_fused_ab.jsonl). FLUXMPI_ATTN_BWD=pair keeps the pair (A/B), =blocked the
+// non-resident kernels.
 bool attn_fused_env() {
   static const bool on = [] {
     const char* e = std::getenv("FLUXMPI_ATTN_BWD");
-    return e != nullptr && std::string(e) == "fused";
+    return e == nullptr || (std::string(e) != "pair" && std::string(e) != "blocked");
   }();
   return on;
 }
@@ -1133,7 +1136,7 @@ int attn_bwd_colpart_rows(int B, int T, int H, int64_t sq_t, int64_t sg_t) {
   // the resident dq / dkv pair writes the column-sum partials; every other variant does not
   if (blocked_env("FLUXMPI_ATTN_BWD") || T > kResMaxT || T <= 0 || (sq_t % 8) != 0 || (sg_t % 8) != 0) return 0;
   const int tiles = (T + 15) / 16;
-  if (attn_fused_env() && tiles == 13) return B * tiles;  // the fused kernel: one part of 13 waves
+  if (attn_fused_env() && tiles == 13 && !attn_generic()) return B * tiles;  // the fused kernel: one part of 13 waves
   const int nblk = res_parts(tiles);
   const int waves = (tiles + nblk - 1) / nblk;
   (void)H;

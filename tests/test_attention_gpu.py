@@ -108,14 +108,14 @@ def test_attn_bwd_colsum_partials(gpu_ext, b, t, heads):
 
 
 @pytest.mark.gpu
-def test_attn_bwd_fused_variant(gpu_ext):
-    """The one-kernel backward (FLUXMPI_ATTN_BWD=fused, read once per process by the native
-    library; taken for 13 key tiles, T 193..208): the fp32-reference and column-sum tests of this
-    file, in a child process with the variant on."""
+def test_attn_bwd_pair_variant(gpu_ext):
+    """The dq / dkv pair (FLUXMPI_ATTN_BWD=pair, read once per process by the native library; the
+    default for 13 key tiles, T 193..208, is the fused kernel): the fp32-reference and column-sum
+    tests of this file, in a child process with the pair."""
     import os
     import subprocess
     import sys
-    env = dict(os.environ, FLUXMPI_ATTN_BWD="fused")
+    env = dict(os.environ, FLUXMPI_ATTN_BWD="pair")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider",
                         os.path.join(root, "tests", "test_attention_gpu.py"), "-k",
@@ -126,8 +126,8 @@ def test_attn_bwd_fused_variant(gpu_ext):
 
 @pytest.mark.gpu
 def test_attn_bwd_fused_matches_pair(gpu_ext):
-    """Run by the child process of test_attn_bwd_fused_variant (a no-op comparison otherwise): at
-    the ViT shape the fused kernel's dQKV and column sums agree with the fp32 reference."""
+    """At the ViT shape (the fused kernel by default; the pair in test_attn_bwd_pair_variant's
+    child process) dQKV and its column sums agree with the fp32 reference."""
     from fluxmpi_amd.ops.attention import attn_bwd_packed, attn_fwd_packed, take_colpart
     torch.manual_seed(5)
     b, t, heads = 4, 197, 12
