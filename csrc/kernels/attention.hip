@@ -422,49 +422,10 @@ __device__ __forceinline__ bf16x8 img_tr(const char* img, int r0, int c0) {
   return out;
 }
 
-// the same reads through restrict pointers (alias scopes): the fused backward stages the K image
-// into the Q slot's first rows while its phase 1 still reads the last ones, and without scopes the
-// waitcnt pass drains that LDS-DMA (vmcnt(0)) before every read
-__device__ __forceinline__ bf16x8 img_row_r(const char* __restrict__ img, int row, int ch) {
-  return *reinterpret_cast<const bf16x8*>(img + row * 128 + ((ch ^ swz_b(row)) << 4));
-}
-__device__ __forceinline__ bf16x8 img_tr_r(const char* __restrict__ img, int r0, int c0) {
-  const int l = threadIdx.x & 63, g = l >> 4, q = (l >> 2) & 3, p = l & 3;
-  const int ra = r0 + 4 * g + q, rb = ra + 16;
-  const int ch = (c0 >> 3) + (p >> 1);
-  const char* a0 = img + ra * 128 + ((ch ^ swz_b(ra)) << 4) + (p & 1) * 8;
-  const char* a1 = img + rb * 128 + ((ch ^ swz_b(rb)) << 4) + (p & 1) * 8;
-  typedef short short4v __attribute__((ext_vector_type(4)));
-  typedef __attribute__((address_space(3))) short4v lds_short4v;
-  short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(a0));
-  short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)(a1));
-  bf16x8 out;
-  __builtin_memcpy(&out, &lo, 8);
-  __builtin_memcpy(reinterpret_cast<char*>(&out) + 8, &hi, 8);
-  return out;
-}
-__device__ __forceinline__ float lds_f32_r(const float* __restrict__ p, int i) { return p[i]; }
-__device__ __forceinline__ void lds_bf16_store_r(char* __restrict__ p, bf16 v) { *reinterpret_cast<bf16*>(p) = v; }
-
 __device__ __attribute__((aligned(16))) uint4 g_attn_zero[4];
 
 // LDS-DMA of rows [0, rows) of a [T][64] head operand (row stride st) into a swizzled 128-B-row
 // image; rows >= T read a zero line. Pieces are spread over the workgroup's waves.
-// rows [r0, r1) only (r0, r1 multiples of 8): the fused backward's K image in two parts
-__device__ __forceinline__ void stage_rows_range(char* img, const bf16* __restrict__ base, int64_t st, int r0, int r1,
-                                                 int T) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
-  for (int pc = r0 / 8 + wave; pc < r1 / 8; pc += nw) {
-    const int row = 8 * pc + (lane >> 3);
-    const int chunk = (lane & 7) ^ swz_k(row);
-    const void* src = row < T ? static_cast<const void*>(base + static_cast<int64_t>(row) * st + chunk * 8)
-                              : static_cast<const void*>(g_attn_zero);
-    typedef __attribute__((address_space(3))) char lds_char;
-    typedef __attribute__((address_space(1))) void gl_void;
-    __builtin_amdgcn_global_load_lds((gl_void*)(src), (lds_char*)(img + pc * 1024), 16, 0, 0);
-  }
-}
-
 template <bool V>
 __device__ __forceinline__ void stage_rows(char* img, const bf16* __restrict__ base, int64_t st, int rows, int T) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
@@ -976,8 +937,7 @@ __global__ __launch_bounds__(1024) void attn_bwd_dkv_res_kernel(AttnBwdArgs a) {
 // K rows are zero, and 0 * uninitialised could be NaN).
 constexpr int kDsRow = 464;
 
-// MID: the K image's first half is staged mid-phase-1 (into Q rows phase 1 is done with)
-template <int NT, bool MID>
+template <int NT>
 __global__ __launch_bounds__(1024) void attn_bwd_fused_kernel(AttnBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TV = ((16 * NT + 31) / 32) * 32;  // key / query rows of the images (224 at NT = 13)
@@ -1040,42 +1000,36 @@ __global__ __launch_bounds__(1024) void attn_bwd_fused_kernel(AttnBwdArgs a) {
   // ---- phase 1: dK^T, dV^T of this wave's keys; dS into the image
   const float c2 = a.scale * kLog2e;
   f32x4 accK[4] = {}, accV[4] = {};
-  constexpr int KMID = MID ? KS / 2 : 0;  // after k-step KMID - 1 the Q rows [0, 32 KMID) are free: K goes there
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
-    if (MID && ks == KMID) {
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only: no LDS-DMA is in flight here
-      __builtin_amdgcn_s_barrier();        // every wave is past its reads of those rows
-      stage_rows_range(qimg, a.k + b * a.sq_b + h * DH, a.sq_t, 0, 32 * KMID, a.T);
-    }
     f32x4 p[2], dsv[2];
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       const int row = 32 * ks + 16 * half + col;  // query row of the A fragment
       f32x4 sv = {}, dp = {};
-      sv = mfma(img_row_r(qimg, row, g), kf[0], sv);
-      sv = mfma(img_row_r(qimg, row, 4 + g), kf[1], sv);
-      dp = mfma(img_row_r(gimg, row, g), vf[0], dp);
-      dp = mfma(img_row_r(gimg, row, 4 + g), vf[1], dp);
+      sv = mfma(img_row(qimg, row, g), kf[0], sv);
+      sv = mfma(img_row(qimg, row, 4 + g), kf[1], sv);
+      dp = mfma(img_row(gimg, row, g), vf[0], dp);
+      dp = mfma(img_row(gimg, row, 4 + g), vf[1], dp);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int qq = 32 * ks + 16 * half + 4 * g + r;
-        const float pv = fast_exp2(fmaf(sv[r], c2, -lds_f32_r(sL, qq)));  // padded query: lse = +inf -> 0
+        const float pv = fast_exp2(fmaf(sv[r], c2, -sL[qq]));  // padded query: lse = +inf -> 0
         p[half][r] = pv;
-        dsv[half][r] = pv * (dp[r] - lds_f32_r(sD, qq));
+        dsv[half][r] = pv * (dp[r] - sD[qq]);
       }
       if (32 * ks + 16 * half < NQ) {  // compile-time: rows past the waves' queries are not in the image
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          lds_bf16_store_r(dsimg + (32 * ks + 16 * half + 4 * g + r) * kDsRow + (k0 + col) * 2,
-                           static_cast<bf16>(dsv[half][r]));
+          *reinterpret_cast<bf16*>(dsimg + (32 * ks + 16 * half + 4 * g + r) * kDsRow + (k0 + col) * 2) =
+              static_cast<bf16>(dsv[half][r]);
       }
     }
     const bf16x8 pb = pack(p[0], p[1]), db = pack(dsv[0], dsv[1]);
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) {
-      accV[dt] = mfma(img_tr_r(gimg, 32 * ks, 16 * dt), pb, accV[dt]);
-      accK[dt] = mfma(img_tr_r(qimg, 32 * ks, 16 * dt), db, accK[dt]);
+      accV[dt] = mfma(img_tr(gimg, 32 * ks, 16 * dt), pb, accV[dt]);
+      accK[dt] = mfma(img_tr(qimg, 32 * ks, 16 * dt), db, accK[dt]);
     }
   }
   if (kok) {
@@ -1092,9 +1046,8 @@ __global__ __launch_bounds__(1024) void attn_bwd_fused_kernel(AttnBwdArgs a) {
     colpart_store(colpart_row(a, b, h, 0, w, 1), accK, a.scale, kok);
     colpart_store(colpart_row(a, b, h, 0, w, 2), accV, 1.f, kok);
   }
-  __builtin_amdgcn_s_waitcnt(0xC07F);
-  __builtin_amdgcn_s_barrier();  // dS complete, the Q image's last reads done
-  stage_rows_range(qimg, a.k + b * a.sq_b + h * DH, a.sq_t, 32 * KMID, TV, a.T);  // the K image's rest
+  __syncthreads();  // dS complete, the Q image's last reads done
+  stage_rows<false>(qimg, a.k + b * a.sq_b + h * DH, a.sq_t, TV, a.T);  // the K image
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
 
@@ -1212,21 +1165,14 @@ void attn_bwd(const void* q, const void* k, const void* v, const void* o, const 
       const int64_t bh = static_cast<int64_t>(B) * H;
       if (bh > 0x7fffffff) throw std::runtime_error("attn_bwd: grid too large");
       a.colpart = colpart;  // [B * 13][3 * H * 64] (attn_bwd_colpart_rows), or nullptr
-      // FLUXMPI_ATTN_FUSED_MID=0: the whole K image staged after phase 1 (A/B)
-      static const bool mid = [] {
-        const char* e = std::getenv("FLUXMPI_ATTN_FUSED_MID");
-        return e == nullptr || e[0] != '0';
-      }();
       static const bool attr = [] {
-        for (const void* k : {reinterpret_cast<const void*>(&attn_bwd_fused_kernel<13, true>),
-                              reinterpret_cast<const void*>(&attn_bwd_fused_kernel<13, false>)})
-          FLUXMPI_HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                static_cast<int>(fused_lds(13))));
+        FLUXMPI_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_fused_kernel<13>),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              static_cast<int>(fused_lds(13))));
         return true;
       }();
       (void)attr;
-      auto kf = mid ? attn_bwd_fused_kernel<13, true> : attn_bwd_fused_kernel<13, false>;
-      kf<<<static_cast<unsigned>(bh), 13 * 64, fused_lds(13), s>>>(a);
+      attn_bwd_fused_kernel<13><<<static_cast<unsigned>(bh), 13 * 64, fused_lds(13), s>>>(a);
       FLUXMPI_HIP_CHECK(hipGetLastError());
       return;
     }
