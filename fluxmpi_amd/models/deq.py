@@ -87,7 +87,8 @@ class _AddPenaltyGrad(torch.autograd.Function):
 # <= 9.8e-3, 56 adjoint iterations; CIFAR 29 of 60, residual <= 1.9e-2, 10.25 adjoint iterations.
 # Caps of 80 leave headroom for the slow steps (a 60-iteration MNIST solve ended at 1.004e-2 against
 # 1e-2 in rd6q, a DEQ-CIFAR one at 0.024 in rd6m): an easy step still stops at its tolerance, so the
-# cap only costs time on the steps that need it.
+# cap only costs time on the steps that need it (profiles/rd6r_bench_deq_caps80.jsonl: all four 1-GPU
+# lines end by tolerance; the 2-rank rehearsals did not).
 DEQ_MNIST_SOLVER = {"max_iter": 80, "tol": 1e-2, "bwd_iter": 80, "bwd_tol": 2e-2}
 DEQ_CIFAR_SOLVER = {"max_iter": 80, "tol": 2e-2, "bwd_iter": 80, "bwd_tol": 1e-2}
 
