@@ -420,10 +420,23 @@ class SolverGraphs:
 
 
 class DEQFixedPoint(nn.Module):
+    """``z* = f(z*, x)`` by Anderson acceleration, implicit (adjoint fixed-point) backward.
+
+    ``skip`` (channels, > 0: on): the Skip DEQ of FastDEQ.jl (the reference's DEQ example library,
+    /root/reference/README.md:76): an explicit 3x3 convolution of the injection predicts the fixed
+    point and the solve starts there instead of at zero; it is trained towards z* by an auxiliary
+    loss ``skip_reg * ||skip(x) - z*||^2 / ||z*||^2`` whose gradient reaches only the skip
+    convolution (the solver's initial guess does not change z* nor its implicit gradient)."""
+
     def __init__(self, f: nn.Module, max_iter=30, tol=1e-4, bwd_iter=30, bwd_tol=1e-4, check_lag: int | None = None,
-                 jac_reg: float | None = None, jac_sigma: float | None = None):
+                 jac_reg: float | None = None, jac_sigma: float | None = None, skip: int = 0, skip_reg: float = 1.0):
         super().__init__()
         self.f = f
+        self.skip = nn.Conv2d(int(skip), int(skip), 3, padding=1, bias=False) if skip else None
+        if self.skip is not None:
+            nn.init.zeros_(self.skip.weight)  # starts at the zero guess of the plain solve
+        self.skip_reg = float(skip_reg)
+        self.last_skip_res = None  # the last training step's ||skip(x) - z*|| / ||z*|| (0-d device tensor)
         env = [float(v) for v in JAC_REG.split(",")] if JAC_REG else []
         self.jac_reg = float(jac_reg if jac_reg is not None else (env[0] if env else 0.0))
         self.jac_sigma = float(jac_sigma if jac_sigma is not None else (env[1] if len(env) > 1 else 0.05))
@@ -457,10 +470,19 @@ class DEQFixedPoint(nn.Module):
         gs = self._graphs_for(x)
         # the cell's GroupNorm parameters cast to fp32 once for the ~30 calls below (into the
         # graphs' static buffers when the solver loops replay graphs)
+        z_pred = self.skip(x) if self.skip is not None else None
+        x0 = z_pred.detach().contiguous(memory_format=torch.channels_last) if z_pred is not None and \
+            x.is_contiguous(memory_format=torch.channels_last) else (z_pred.detach() if z_pred is not None else None)
         with fp32_affine_cache(self.f, buffers=gs.aff if gs is not None else None):
-            out = self._forward(x, gs)
-        if self.jac_reg > 0 and self.training and torch.is_grad_enabled() and out.requires_grad:
+            out = self._forward(x, gs, x0)
+        training = self.training and torch.is_grad_enabled() and out.requires_grad
+        if self.jac_reg > 0 and training:
             out = self._jacobian_penalty(out, x)
+        if z_pred is not None and training and z_pred.requires_grad:
+            zs = self._z_star.float()
+            err = (z_pred.float() - zs).square().sum() / zs.square().sum().clamp_min(1e-12)
+            self.last_skip_res = err.detach().sqrt()
+            out = _AddPenaltyGrad.apply(out, err, self.skip_reg)
         return out
 
     def _jacobian_penalty(self, out, x):
@@ -478,14 +500,15 @@ class DEQFixedPoint(nn.Module):
         self.last_jr = jr.detach()
         return _AddPenaltyGrad.apply(out, jr, self.jac_reg)
 
-    def _forward(self, x, gs: SolverGraphs | None = None):
+    def _forward(self, x, gs: SolverGraphs | None = None, x0: torch.Tensor | None = None):
         # the solver's ~30 evaluations by direct kernel calls when the cell allows (no autograd
         # Function objects per call: the DEQ step is host-bound, profiles/rd3h_ab_deq.jsonl)
         raw = MANUAL_VJP and hasattr(self.f, "manual_ok") and self.f.manual_ok(x)
         xs = gs.x if gs is not None else x  # the solve reads the graphs' static copy
         fz = _CellEval(self.f, xs, raw)
         with torch.no_grad():
-            z, self.last_iters, self.last_res = anderson(fz, torch.zeros_like(x), max_iter=self.max_iter,
+            z, self.last_iters, self.last_res = anderson(fz, x0 if x0 is not None else torch.zeros_like(x),
+                                                         max_iter=self.max_iter,
                                              tol=self.tol, check_lag=self.check_lag, graphs=gs)
         self._z_star = z.detach()
         # one differentiable step re-engages autograd at z*; its GroupNorms save fresh fp32 affine
@@ -695,6 +718,8 @@ class DEQClassifier(nn.Module):
         # our NHWC BatchNorm kernels (ops/batchnorm.py) instead of MIOpen's (nn.BatchNorm2d API,
         # same parameters / state dict)
         self.inj_norm = FusedBatchNorm2d(ch)
+        if solver.get("skip"):
+            solver["skip"] = ch
         self.deq = DEQFixedPoint(ResidualCell(ch), **solver)
         self.out_norm = FusedBatchNorm2d(ch)
         self.head = nn.Linear(ch * 4 * 4, num_classes)
@@ -731,6 +756,8 @@ class DEQCifar(nn.Module):
         self.inj_norm = FusedBatchNorm2d(ch)
         for k, v in DEQ_CIFAR_SOLVER.items():
             solver.setdefault(k, v)
+        if solver.get("skip"):
+            solver["skip"] = ch
         self.deq = DEQFixedPoint(ResidualCell(ch, groups), **solver)
         self.out_norm = FusedBatchNorm2d(ch)
         self.head = Linear(ch, num_classes)  # ops.linear.Linear: dW / db born in their bucket slices

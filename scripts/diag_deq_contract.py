@@ -65,6 +65,7 @@ def main():
         torch.cuda.synchronize()
         wn = max(float(c.weight.float().square().sum((1, 2, 3)).sqrt().max()) for c in (cell.conv1, cell.conv2))
         rec = {"model": a.model, "lr": a.lr, "labels": a.labels, "batches": a.batches, "constrain": D.CONSTRAIN, "step": s, "loss": round(float(loss), 4),
+               "skip_res": float(model.deq.last_skip_res) if getattr(model.deq, "last_skip_res", None) is not None else None,
                "jac_reg": model.deq.jac_reg, "jr": float(model.deq.last_jr) if model.deq.last_jr is not None else None,
                "fwd_iters": model.deq.last_iters, "fwd_res": float(model.deq.last_res),
                "bwd_iters": model.deq.last_bwd_iters, "conv_norm_max": round(wn, 4), "max_norm": round(cell.max_norm, 4),

@@ -740,3 +740,29 @@ def worker_functional_bf16_masters():
 
 def test_functional_bf16_masters_gloo(spmd):
     spmd("tests.test_deq:worker_functional_bf16_masters", timeout=300)
+
+
+def test_skip_deq_initial_guess_and_aux_gradient_cpu():
+    """Skip DEQ (FastDEQ.jl's explicit initial-guess network): the solve starts at skip(x), the
+    skip convolution is trained by the auxiliary loss only, and the classifier's loss gradient is
+    unchanged by it (same fixed point up to the solver tolerance)."""
+    torch.manual_seed(0)
+    m = deq_mnist(tol=1e-5, max_iter=60, bwd_tol=1e-5, bwd_iter=60, skip=1, skip_reg=1.0)
+    assert m.deq.skip is not None and m.deq.skip.weight.shape == (48, 48, 3, 3)
+    assert float(m.deq.skip.weight.detach().abs().sum()) == 0.0  # zero init: the first solve starts at 0
+    x = torch.randn(2, 1, 28, 28)
+    y = torch.randint(0, 10, (2,))
+    F.cross_entropy(m(x), y).backward()
+    g = m.deq.skip.weight.grad
+    assert g is not None and torch.isfinite(g).all() and float(g.abs().sum()) > 0
+    assert m.deq.last_skip_res is not None and abs(float(m.deq.last_skip_res) - 1.0) < 1e-4  # 0 vs z*
+    # a trained-looking guess: the fixed point and the head gradient do not depend on it
+    m2 = deq_mnist(tol=1e-5, max_iter=60, bwd_tol=1e-5, bwd_iter=60)
+    m2.load_state_dict({k: v for k, v in m.state_dict().items() if not k.startswith("deq.skip")})
+    with torch.no_grad():
+        m.deq.skip.weight.normal_(0, 0.05)
+    m.zero_grad()
+    m2.zero_grad()
+    F.cross_entropy(m(x), y).backward()
+    F.cross_entropy(m2(x), y).backward()
+    torch.testing.assert_close(m.head.weight.grad, m2.head.weight.grad, rtol=1e-3, atol=1e-5)
