@@ -293,6 +293,51 @@ def _capture(graph: "torch.cuda.CUDAGraph"):
     return torch.cuda.graph(graph, capture_error_mode="thread_local")
 
 
+def _rms_rows(t: torch.Tensor) -> torch.Tensor:
+    """Per-sample root-mean-square of ``t`` (fp32 [N], floored): the adjoint's right-hand side is
+    divided by it before an Anderson solve, whose Gram regulariser ``lam`` is absolute (the loss
+    gradient reaching the DEQ is ~1e-4 per element: unscaled, ``lam`` would swamp ``G G^T``), and
+    multiplied back after (the adjoint is linear in its right-hand side)."""
+    return t.float().reshape(t.shape[0], -1).square().mean(1).sqrt_().clamp_min_(1e-30)
+
+
+class _AndersonGraph:
+    """One Anderson solve's static history and its captured period (``m`` iterations, slots
+    ``k % m``): what :func:`anderson` takes as ``graphs``. ``like``: the iterate's shape, dtype and
+    device."""
+
+    def __init__(self, like: torch.Tensor):
+        self.like = like
+        self._hist = None
+        self.g = self.rbuf = self.rmin = None
+
+    def history(self, m: int):
+        bsz, d = self.like.shape[0], self.like[0].numel()
+        if self._hist is None or self._hist[0].shape[1] != m:
+            X = torch.zeros(bsz, m, d, dtype=_x_hist_dtype(self.like.dtype, self.like), device=self.like.device)
+            self._hist = (X, torch.zeros_like(X, dtype=_f_hist_dtype(self.like.dtype, self.like)), torch.zeros_like(X))
+            self.g = None
+        return self._hist
+
+    def anderson_period(self, k0: int, m: int, solve_step, mix_step) -> torch.Tensor:
+        """Replay iterations ``k0 .. k0 + m - 1`` (capturing them on first use); returns the
+        smallest residual of the period (0-d device tensor, static)."""
+        if self.g is None:
+            self.rbuf = torch.zeros(m, dtype=torch.float32, device=self.like.device)
+            self.rmin = torch.zeros((), dtype=torch.float32, device=self.like.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.no_grad(), _capture(g):
+                for i in range(m):
+                    alpha, res_t = solve_step(k0 + i, self.rbuf[i])
+                    if res_t is not None and res_t.data_ptr() != self.rbuf[i].data_ptr():
+                        self.rbuf[i].copy_(res_t)
+                    mix_step(k0 + i, alpha)
+                torch.amin(self.rbuf, dim=0, out=self.rmin)
+            self.g = g
+        self.g.replay()
+        return self.rmin
+
+
 class SolverGraphs:
     """HIP graphs of one :class:`DEQFixedPoint`'s two solver loops at one input shape.
 
@@ -320,38 +365,22 @@ class SolverGraphs:
         self.x = torch.empty_like(x)  # the solve's injection, same strides (channels_last stays)
         self.x.copy_(x)
         self.aff: dict = {}
-        self._hist = None
-        self.rbuf = self.rmin = None
-        self.g_fwd = self.g_state = self.g_adj = None
+        self.fwd = _AndersonGraph(self.x)  # the forward solve's history + period graph
+        self.adj = None                    # the Anderson adjoint's (bwd_m > 0), made on first use
+        self.g_state = self.g_adj = None
         self.state = self.z0 = self.grad = self.u = self.thresh2 = self.dmax = self.done = None
         self.gen = 0  # forward_state calls so far (a hook whose generation is stale goes eager)
         self.chunk = 0
 
+    @property
+    def g_fwd(self):
+        return self.fwd.g
+
     def history(self, m: int):
-        bsz, d = self.x.shape[0], self.x[0].numel()
-        if self._hist is None or self._hist[0].shape[1] != m:
-            X = torch.zeros(bsz, m, d, dtype=_x_hist_dtype(self.x.dtype, self.x), device=self.x.device)
-            self._hist = (X, torch.zeros_like(X, dtype=_f_hist_dtype(self.x.dtype, self.x)), torch.zeros_like(X))
-            self.g_fwd = None
-        return self._hist
+        return self.fwd.history(m)
 
     def anderson_period(self, k0: int, m: int, solve_step, mix_step) -> torch.Tensor:
-        """Replay iterations ``k0 .. k0 + m - 1`` (capturing them on first use); returns the
-        smallest residual of the period (0-d device tensor, static)."""
-        if self.g_fwd is None:
-            self.rbuf = torch.zeros(m, dtype=torch.float32, device=self.x.device)
-            self.rmin = torch.zeros((), dtype=torch.float32, device=self.x.device)
-            g = torch.cuda.CUDAGraph()
-            with torch.no_grad(), _capture(g):
-                for i in range(m):
-                    alpha, res_t = solve_step(k0 + i, self.rbuf[i])
-                    if res_t is not None and res_t.data_ptr() != self.rbuf[i].data_ptr():
-                        self.rbuf[i].copy_(res_t)
-                    mix_step(k0 + i, alpha)
-                torch.amin(self.rbuf, dim=0, out=self.rmin)
-            self.g_fwd = g
-        self.g_fwd.replay()
-        return self.rmin
+        return self.fwd.anderson_period(k0, m, solve_step, mix_step)
 
     def capture_adjoint(self, cell, z: torch.Tensor, chunk: int) -> None:
         """Capture ``forward_state`` at a static ``z0`` and ``chunk`` adjoint iterations."""
@@ -418,6 +447,20 @@ class SolverGraphs:
             it += 1
         return u, it
 
+    def adjoint_anderson(self, cell, grad: torch.Tensor, tol: float, max_iter: int, m: int, lag: int):
+        """Solve ``u = J^T u + grad`` by Anderson(``m``) on the static state: the right-hand side
+        is normalised per sample (:func:`_rms_rows`) into the static ``grad`` buffer, the solve's
+        history and period graph are this object's second :class:`_AndersonGraph`; returns
+        ``(u, iterations)``."""
+        s = _rms_rows(grad).view(-1, *([1] * (grad.dim() - 1)))
+        self.grad.copy_(grad.float() / s)
+        cell.refresh_filters()  # the optimiser may have changed the weights since the capture
+        if self.adj is None:
+            self.adj = _AndersonGraph(self.grad)
+        step = lambda u: cell.adjoint_step(self.state, u, self.grad)[0]  # noqa: E731
+        u, it, _ = anderson(step, self.grad, m=m, max_iter=max_iter, tol=tol, check_lag=lag, graphs=self.adj)
+        return (u.float() * s).to(grad.dtype), it
+
 
 class DEQFixedPoint(nn.Module):
     """``z* = f(z*, x)`` by Anderson acceleration, implicit (adjoint fixed-point) backward.
@@ -429,9 +472,12 @@ class DEQFixedPoint(nn.Module):
     convolution (the solver's initial guess does not change z* nor its implicit gradient)."""
 
     def __init__(self, f: nn.Module, max_iter=30, tol=1e-4, bwd_iter=30, bwd_tol=1e-4, check_lag: int | None = None,
-                 jac_reg: float | None = None, jac_sigma: float | None = None, skip: int = 0, skip_reg: float = 1.0):
+                 jac_reg: float | None = None, jac_sigma: float | None = None, skip: int = 0, skip_reg: float = 1.0,
+                 m: int = 5, bwd_m: int = 0):
         super().__init__()
         self.f = f
+        self.m = int(m)          # Anderson memory of the forward solve (<= 8: anderson.hip)
+        self.bwd_m = int(bwd_m)  # > 0: the adjoint solve by Anderson(bwd_m) too; 0: fixed-point iteration
         self.skip = nn.Conv2d(int(skip), int(skip), 3, padding=1, bias=False) if skip else None
         if self.skip is not None:
             nn.init.zeros_(self.skip.weight)  # starts at the zero guess of the plain solve
@@ -508,7 +554,7 @@ class DEQFixedPoint(nn.Module):
         fz = _CellEval(self.f, xs, raw)
         with torch.no_grad():
             z, self.last_iters, self.last_res = anderson(fz, x0 if x0 is not None else torch.zeros_like(x),
-                                                         max_iter=self.max_iter,
+                                                         m=self.m, max_iter=self.max_iter,
                                              tol=self.tol, check_lag=self.check_lag, graphs=gs)
         self._z_star = z.detach()
         # one differentiable step re-engages autograd at z*; its GroupNorms save fresh fp32 affine
@@ -532,6 +578,10 @@ class DEQFixedPoint(nn.Module):
                     _, state = self.f.forward_state(z_star, x_in)
                     return self._adjoint_loop(grad, lambda u, g: self.f.adjoint_step(state, u, g), z_star)
                 lag = CHECK_LAG if self.check_lag is None else int(self.check_lag)
+                if self.bwd_m > 0:
+                    u, self.last_bwd_iters = gs.adjoint_anderson(self.f, grad, self.bwd_tol, self.bwd_iter,
+                                                                 self.bwd_m, lag)
+                    return u
                 u, self.last_bwd_iters = gs.adjoint(self.f, grad, self.bwd_tol, self.bwd_iter, lag)
                 return u
 
@@ -567,13 +617,21 @@ class DEQFixedPoint(nn.Module):
     def _adjoint_loop(self, grad, step, z0):
         """Eager adjoint fixed point ``u = J^T u + grad`` (``step(u, grad) -> (u_new, |u_new - u|^2)``)."""
         lag = (CHECK_LAG if self.check_lag is None else int(self.check_lag)) if grad.is_cuda else 0
-        flags = LaggedFlags(lag, self.bwd_iter) if lag > 0 else None
-        thresh = self.bwd_tol * (grad.norm() + 1e-9)  # device scalar, computed once
-        thresh2 = thresh * thresh
         if z0.dim() == 4 and z0.is_contiguous(memory_format=torch.channels_last):
             # the incoming gradient (from the BatchNorm after the DEQ) may be NCHW: one layout
             # copy here instead of one per iteration in the cell's NHWC GroupNorm backward
             grad = grad.contiguous(memory_format=torch.channels_last)
+        if self.bwd_m > 0:
+            # Anderson(bwd_m) on the per-sample normalised right-hand side; its test is the
+            # relative residual |h(u) - u| / |h(u)| of h(u) = J^T u + g (the forward's test)
+            s = _rms_rows(grad).view(-1, *([1] * (grad.dim() - 1)))
+            gn = (grad.float() / s).to(grad.dtype)
+            u, self.last_bwd_iters, _ = anderson(lambda v: step(v, gn)[0], gn, m=self.bwd_m, max_iter=self.bwd_iter,
+                                                 tol=self.bwd_tol, check_lag=lag)
+            return (u.float() * s).to(grad.dtype)
+        flags = LaggedFlags(lag, self.bwd_iter) if lag > 0 else None
+        thresh = self.bwd_tol * (grad.norm() + 1e-9)  # device scalar, computed once
+        thresh2 = thresh * thresh
         u = grad
         it = 0
         for it in range(self.bwd_iter):  # u = J^T u + grad

@@ -484,6 +484,43 @@ def test_deq_solver_graphs_match_eager(gpu_ext):
 
 
 @pytest.mark.gpu
+def test_deq_anderson_adjoint_graphs_match_eager(gpu_ext):
+    """The Anderson adjoint (bwd_m = 5) through its own history and period graph
+    (SolverGraphs.adjoint_anderson) replays the eager Anderson adjoint: same iteration counts,
+    outputs and gradients over four training steps (eager, capture, replay, replay)."""
+    eager, graphed = _graphed_vs_eager(4, max_iter=13, tol=0.0, bwd_iter=17, bwd_tol=0.0, bwd_m=5)
+    for s, ((oa, ga, ia, ba), (ob, gb, ib, bb)) in enumerate(zip(eager, graphed)):
+        assert (ia, ba) == (ib, bb) and ba >= 15, (s, ia, ba, ib, bb)
+        torch.testing.assert_close(ob, oa, rtol=2e-2, atol=2e-2)
+        for a, b in zip(ga, gb):
+            rel = float((b - a).norm() / a.norm().clamp_min(1e-12))
+            assert rel < 2e-2, (s, rel)
+
+
+@pytest.mark.gpu
+def test_deq_anderson_adjoint_gpu_matches_fixed_point(gpu_ext):
+    """bf16 DEQ on the fused GPU path: gradients from the Anderson adjoint (bwd_tol 1e-3) agree
+    with the fixed-point adjoint solved to 1e-4 within the bf16 fixed-point spread of
+    test_deq_train_step_manual_vjp_gpu, in fewer iterations."""
+    torch.manual_seed(5)
+    x = torch.randn(32, 1, 28, 28, device="cuda").bfloat16().contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (32,), device="cuda")
+    grads, iters = [], []
+    for bwd_m, bwd_tol in ((0, 1e-4), (5, 1e-3)):
+        torch.manual_seed(3)
+        m = _deq_bf16(tol=1e-4, max_iter=60, bwd_tol=bwd_tol, bwd_iter=120, bwd_m=bwd_m)
+        for _ in range(3):  # eager, capture, replay: the last step's gradients are compared
+            for p in m.parameters():
+                p.grad = None
+            F.cross_entropy(m(x).float(), y).backward()
+        grads.append([p.grad.float().clone() for p in m.parameters()])
+        iters.append(m.deq.last_bwd_iters)
+    rels = [float((b - a).norm() / a.norm().clamp_min(1e-12)) for a, b in zip(*grads)]
+    assert max(rels) < 1e-1 and sorted(rels)[len(rels) // 2] < 6e-2, rels
+    assert iters[1] < iters[0], iters
+
+
+@pytest.mark.gpu
 def test_deq_solver_graphs_two_forwards_one_backward(gpu_ext):
     """loss = f(x1) + f(x2) at one shape: the second graphed forward overwrites the solver graphs'
     static state before the first call's adjoint runs, so that adjoint must run on its own state
@@ -766,3 +803,25 @@ def test_skip_deq_initial_guess_and_aux_gradient_cpu():
     F.cross_entropy(m(x), y).backward()
     F.cross_entropy(m2(x), y).backward()
     torch.testing.assert_close(m.head.weight.grad, m2.head.weight.grad, rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("bwd_m", [3, 5])
+def test_anderson_adjoint_matches_fixed_point_adjoint_cpu(bwd_m):
+    """The adjoint solve by Anderson(bwd_m) (per-sample normalised right-hand side) gives the
+    parameter gradients of a tightly converged fixed-point adjoint, in a fraction of its
+    iterations (its residual test is relative to h(u) = J^T u + g, the forward's kind of test)."""
+    torch.manual_seed(0)
+    x = torch.randn(3, 1, 28, 28)
+    y = torch.randint(0, 10, (3,))
+    grads, iters = [], []
+    for m_, tol in ((0, 1e-6), (bwd_m, 1e-3)):
+        torch.manual_seed(1)
+        m = deq_mnist(tol=1e-6, max_iter=60, bwd_tol=tol, bwd_iter=200, bwd_m=m_)
+        F.cross_entropy(m(x), y).backward()
+        grads.append({k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None})
+        iters.append(m.deq.last_bwd_iters)
+    ref, got = grads
+    assert ref.keys() == got.keys()
+    err = sum((got[k] - ref[k]).square().sum() for k in ref).sqrt() / sum(ref[k].square().sum() for k in ref).sqrt()
+    assert float(err) < 5e-3, float(err)
+    assert iters[1] * 3 < iters[0], iters
