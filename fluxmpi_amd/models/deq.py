@@ -90,7 +90,13 @@ class _AddPenaltyGrad(torch.autograd.Function):
 # cap only costs time on the steps that need it (profiles/rd6r_bench_deq_caps80.jsonl: all four 1-GPU
 # lines end by tolerance; the 2-rank rehearsals did not).
 DEQ_MNIST_SOLVER = {"max_iter": 80, "tol": 1e-2, "bwd_iter": 80, "bwd_tol": 2e-2}
-DEQ_CIFAR_SOLVER = {"max_iter": 80, "tol": 2e-2, "bwd_iter": 80, "bwd_tol": 1e-2}
+# DEQ-CIFAR runs as a Skip DEQ (FastDEQ.jl's explicit initial-guess network, DEQFixedPoint ``skip``):
+# with it every line ends its solves by tolerance, the 2-rank rehearsal included (28 forward
+# iterations at 0.019976 against 0.02, 45 adjoint; without it 56 at 0.034 and the adjoint at its
+# cap, 2294 vs 3798 img/s: profiles/rd6t_skip_deq_comm.jsonl), and the 1-GPU line is faster (14 vs
+# 19-29 forward iterations, 9.0k vs 8.8k img/s: rd6s_skip_deq.jsonl, rd6u_deq_anderson_adjoint.jsonl).
+# MNIST stays without it: there the skip measured mixed (rd6s, rd6t).
+DEQ_CIFAR_SOLVER = {"max_iter": 80, "tol": 2e-2, "bwd_iter": 80, "bwd_tol": 1e-2, "skip": 1}
 
 
 # host seconds spent blocked on convergence flags (LaggedFlags.pop_ready), cumulative: bench.py
@@ -468,8 +474,11 @@ class DEQFixedPoint(nn.Module):
     ``skip`` (channels, > 0: on): the Skip DEQ of FastDEQ.jl (the reference's DEQ example library,
     /root/reference/README.md:76): an explicit 3x3 convolution of the injection predicts the fixed
     point and the solve starts there instead of at zero; it is trained towards z* by an auxiliary
-    loss ``skip_reg * ||skip(x) - z*||^2 / ||z*||^2`` whose gradient reaches only the skip
-    convolution (the solver's initial guess does not change z* nor its implicit gradient)."""
+    loss ``skip_reg * ||skip(x) - z*||^2 / ||z*||^2`` (z* a constant: the cell gets none of its
+    gradient; the skip convolution and, through the injection x, the layers before the DEQ do).
+    The solver's initial guess changes neither z* (up to the tolerance) nor its implicit gradient.
+    ``m`` / ``bwd_m``: Anderson memory of the forward / adjoint solve (``bwd_m`` 0: the adjoint by
+    fixed-point iteration ``u <- J^T u + g``)."""
 
     def __init__(self, f: nn.Module, max_iter=30, tol=1e-4, bwd_iter=30, bwd_tol=1e-4, check_lag: int | None = None,
                  jac_reg: float | None = None, jac_sigma: float | None = None, skip: int = 0, skip_reg: float = 1.0,
@@ -516,7 +525,9 @@ class DEQFixedPoint(nn.Module):
         gs = self._graphs_for(x)
         # the cell's GroupNorm parameters cast to fp32 once for the ~30 calls below (into the
         # graphs' static buffers when the solver loops replay graphs)
-        z_pred = self.skip(x) if self.skip is not None else None
+        z_pred = None
+        if self.skip is not None:  # bf16 channels_last on the GPU: our implicit-GEMM 3x3 kernels
+            z_pred = conv3x3(x, self.skip.weight) if conv3x3_supported(x, self.skip) else self.skip(x)
         x0 = z_pred.detach().contiguous(memory_format=torch.channels_last) if z_pred is not None and \
             x.is_contiguous(memory_format=torch.channels_last) else (z_pred.detach() if z_pred is not None else None)
         with fp32_affine_cache(self.f, buffers=gs.aff if gs is not None else None):
