@@ -481,16 +481,19 @@ __device__ __forceinline__ void colpart_zero(float* row) {
 
 // NT > 0: the head's key-tile count (TP / 16) at compile time — loops without runtime guards are
 // straight-line code the scheduler can pipeline (LDS reads ahead of the MFMAs); 0: any T <= 256
+// LDS: the V image's TP rows, then the K image's TP rows (2 TP x 128 B: 53,248 B at T = 197, so
+// three workgroups fit a CU's 160 KB). The P V k-steps read V rows up to TV - 1 >= TP: those rows
+// are the K image's first TV - TP (0 or 16) rows, finite values multiplied by P = 0 (keys >= TP).
 template <int NT>
 __global__ __launch_bounds__(1024) void attn_fwd_res_kernel(AttnBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int TP = (a.T + 15) & ~15, TV = (a.T + 31) & ~31;
-  char* kimg = smem;
-  char* vimg = smem + TP * 128;
+  char* vimg = smem;
+  char* kimg = smem + TP * 128;
   int part, h, b;
   res_coords(a, b, h, part);
   stage_rows<false>(kimg, a.k + b * a.sq_b + h * DH, a.sq_t, TP, a.T);
-  stage_rows<true>(vimg, a.v + b * a.sq_b + h * DH, a.sq_t, TV, a.T);
+  stage_rows<true>(vimg, a.v + b * a.sq_b + h * DH, a.sq_t, TP, a.T);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, col = lane & 15, g = lane >> 4;
   const int q0 = 16 * (part * (blockDim.x >> 6) + w);
   const int qi = q0 + col;
@@ -1122,6 +1125,18 @@ int res_parts(int tiles) {
   return parts < tiles ? parts : tiles;
 }
 
+// workgroups per (b, h) of the resident forward (FLUXMPI_ATTN_FWD_PARTS, default 2). At 53 KB of
+// LDS three fit a CU, but three parts measured slower than two (101-102 vs 94-95 us per call at
+// the ViT-B/16 shape, one part 103, four 110-111; ViT-B/16 equal: profiles/rd6w_attn_fwd_parts.jsonl)
+int fwd_parts(int tiles) {
+  static const int parts = [] {
+    const char* e = std::getenv("FLUXMPI_ATTN_FWD_PARTS");
+    const int v = e != nullptr ? std::atoi(e) : 2;
+    return v < 1 ? 1 : (v > 16 ? 16 : v);
+  }();
+  return parts < tiles ? parts : tiles;
+}
+
 }  // namespace
 
 namespace {
@@ -1226,13 +1241,13 @@ void attn_fwd(const void* q, const void* k, const void* v, void* o, float* stats
   a.scale = scale;
   static const bool resident = !blocked_env("FLUXMPI_ATTN_FWD");
   if (resident && T <= kResMaxT && (sq_t % 8) == 0) {
-    // whole head resident in LDS: res_parts() workgroups per (b, h), one wave per 16 queries
+    // whole head resident in LDS: fwd_parts() workgroups per (b, h), one wave per 16 queries
     const int tiles = (T + 15) / 16;
-    a.nblk = res_parts(tiles);
+    a.nblk = fwd_parts(tiles);
     const int64_t total = static_cast<int64_t>(B) * H * a.nblk;
     if (total > 0x7fffffff) throw std::runtime_error("attn_fwd: grid too large");
     const int waves = (tiles + a.nblk - 1) / a.nblk;
-    const size_t lds = static_cast<size_t>(((T + 15) & ~15) + ((T + 31) & ~31)) * 128;
+    const size_t lds = static_cast<size_t>(2 * ((T + 15) & ~15)) * 128;
     auto kf = (tiles == 13 && !attn_generic()) ? attn_fwd_res_kernel<13> : attn_fwd_res_kernel<0>;
     kf<<<static_cast<unsigned>(total), waves * 64, lds, s>>>(a);
     FLUXMPI_HIP_CHECK(hipGetLastError());

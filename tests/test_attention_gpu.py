@@ -30,7 +30,7 @@ SHAPES = [(4, 197, 12), (2, 50, 4), (1, 7, 2), (2, 64, 3), (1, 1, 1), (3, 300, 2
 @pytest.mark.gpu
 @pytest.mark.parametrize("b,t,heads", SHAPES + [(64, 197, 12)])
 def test_attn_fwd_vs_fp32(gpu_ext, b, t, heads):
-    """The resident forward (two workgroups per head) vs fp32."""
+    """The resident forward (two workgroups per head; FLUXMPI_ATTN_FWD_PARTS) vs fp32."""
     from fluxmpi_amd.ops.attention import attn_fwd_packed
     torch.manual_seed(0)
     xb = (torch.randn(b, t, 3 * heads * 64, device="cuda") * 1.5).to(torch.bfloat16)
