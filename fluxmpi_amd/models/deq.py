@@ -763,11 +763,9 @@ class ResidualCell(nn.Module):
             u_new, part = deq_cell.cell_vjp(self, state, u, grad=grad, out=out)
             t2 = None if thresh2 is None else thresh2.float()
             return u_new, deq_cell.adjoint_check(part, t2, flag)
-        u_new, ss = AO.adjoint_step(self.vjp(state, u), grad, u,
-                                    out=out if (out is not None and out.data_ptr() != u.data_ptr()) else None)
-        if flag is not None:
-            flag.copy_((ss <= thresh2).float().reshape(flag.shape))
-        return u_new, ss
+        return AO.adjoint_step(self.vjp(state, u), grad, u,
+                               out=out if (out is not None and out.data_ptr() != u.data_ptr()) else None,
+                               thresh2=None if flag is None else thresh2.float(), flag=flag)
 
     def forward(self, z, x):
         # z feeds conv1 and n3's add: n3's backward hands its gradient of z to conv1's dgrad

@@ -148,11 +148,14 @@ def mix(X: torch.Tensor, F: torch.Tensor, alpha: torch.Tensor, slot: int, beta: 
     return z if z is not None else X[:, slot]
 
 
-def adjoint_step(vjp: torch.Tensor, grad: torch.Tensor, u: torch.Tensor, out: torch.Tensor | None = None):
+def adjoint_step(vjp: torch.Tensor, grad: torch.Tensor, u: torch.Tensor, out: torch.Tensor | None = None,
+                 thresh2: torch.Tensor | None = None, flag: torch.Tensor | None = None):
     """``(u_new, ss)``: ``u_new = vjp + grad`` and ``ss = |u_new - u|^2`` (0-d fp32 device tensor)
     in one pass on the GPU (``adjoint_step`` + one partial-sum reduce); the DEQ adjoint solve's
     update and convergence test. ``out`` (optional, like ``vjp``, not ``u``): written instead of a
-    new tensor. Other layouts / CPU: the PyTorch composition."""
+    new tensor. ``thresh2`` / ``flag`` (fp32 device scalar / one fp32 element): also
+    ``flag = ss <= thresh2``, in the reduce's launch on the GPU (no compare / cast / copy kernels per
+    iteration). Other layouts / CPU: the PyTorch composition."""
     same = (vjp.shape == grad.shape == u.shape and vjp.dtype == grad.dtype == u.dtype
             and vjp.stride() == grad.stride() == u.stride())
     dense = same and vjp.numel() % 8 == 0 and (vjp.is_contiguous() or (vjp.dim() == 4 and vjp.is_contiguous(
@@ -160,7 +163,10 @@ def adjoint_step(vjp: torch.Tensor, grad: torch.Tensor, u: torch.Tensor, out: to
     if not (vjp.is_cuda and dense and vjp.dtype in DTYPE_CODE and vjp.numel() > 0
             and (vjp.data_ptr() | grad.data_ptr() | u.data_ptr()) % 16 == 0):
         u_new = torch.add(vjp, grad, out=out) if out is not None else vjp + grad
-        return u_new, (u_new - u).float().pow(2).sum()
+        ss = (u_new - u).float().pow(2).sum()
+        if flag is not None:
+            flag.copy_((ss <= thresh2).float().reshape(flag.shape))
+        return u_new, ss
     C = _ext.get(required=True)
     n = vjp.numel()
     blocks = C.adjoint_step_blocks(n)
@@ -172,5 +178,11 @@ def adjoint_step(vjp: torch.Tensor, grad: torch.Tensor, u: torch.Tensor, out: to
     stream = _stream(vjp)
     C.adjoint_step(vjp.data_ptr(), grad.data_ptr(), u.data_ptr(), u_new.data_ptr(), part.data_ptr(), blocks, n,
                    DTYPE_CODE[vjp.dtype], stream)
-    C.gemm_splitk_reduce(part.data_ptr(), blocks, 1, ss.data_ptr(), DTYPE_CODE[torch.float32], stream)
+    if flag is not None:
+        if not (thresh2 is not None and thresh2.dtype == flag.dtype == torch.float32 and flag.is_contiguous()
+                and thresh2.is_cuda and flag.is_cuda and flag.numel() == 1):
+            raise ValueError("adjoint_step: flag needs a one-element fp32 flag and an fp32 device thresh2")
+        C.deq_adjoint_check(part.data_ptr(), blocks, thresh2.data_ptr(), ss.data_ptr(), flag.data_ptr(), stream)
+    else:
+        C.gemm_splitk_reduce(part.data_ptr(), blocks, 1, ss.data_ptr(), DTYPE_CODE[torch.float32], stream)
     return u_new, ss

@@ -179,6 +179,14 @@ def test_adjoint_step_gpu(dtype, cl):
     torch.testing.assert_close(u_new, want, rtol=0, atol=0)
     ref = (want.float() - u.float()).pow(2).sum()
     torch.testing.assert_close(ss, ref, rtol=1e-4, atol=1e-3)
+    # the convergence flag in the reduce's launch: flag = ss <= thresh2
+    for scale, want_flag in ((1.01, 1.0), (0.99, 0.0)):
+        flag = torch.full((1,), -1.0, device="cuda")
+        t2 = (ref * scale).float()
+        u2, ss2 = AO.adjoint_step(v, g, u, thresh2=t2, flag=flag)
+        torch.testing.assert_close(u2, want, rtol=0, atol=0)
+        torch.testing.assert_close(ss2, ref, rtol=1e-4, atol=1e-3)
+        assert float(flag) == want_flag, (scale, float(flag))
 
 
 @pytest.mark.gpu
