@@ -42,6 +42,12 @@ from .multi_tensor import DTYPE_CODE
 
 MODE = os.environ.get("FLUXMPI_GEMM_NT", "fused").lower()
 ENABLED = MODE != "0"
+# In the default ("fused") mode a plain Linear forward also runs here when its K is at most this
+# (ViT-B/16's qkv and proj at 1024). Default 0 (none), by measurement: qkv + proj on gemm_nt take
+# the same kernel time as hipBLASLt (2.98 vs ~2.95 ms/step, profiles/rd6z_vit_b16_steady.md) and
+# cut hipBLASLt to fc2 (2.75 ms), but ViT-B/16 measured -0.4 % in three interleaved pairs
+# (profiles/rd6z_vit_plain_fwd_ab.jsonl); plain forward GEMMs stay on the vendor library.
+PLAIN_FWD_MAX_K = int(os.environ.get("FLUXMPI_GEMM_NT_PLAIN_FWD_MAX_K", "0"))
 
 
 def _stream(t):
@@ -60,12 +66,12 @@ def supported(rows: int, n_out: int, k: int, *tensors: torch.Tensor, fused: bool
     epilogue fusion — ``"fwd"`` (fc1 bias + GELU) or ``"dgrad"`` (GELU backward), taken in modes
     fused / all (the pair works together: the backward multiplies by the derivative the forward
     stored), ``True`` (either: shape checks of the kernel itself), ``"plain_fwd"`` (a plain Linear
-forward: taken in modes fwd / all)."""
+forward: taken in modes fwd / all, and in the default mode up to :data:`PLAIN_FWD_MAX_K`)."""
     if not ENABLED or not tensors or not tensors[0].is_cuda:
         return False
     if MODE not in ("all", "1"):
         ok = (fused is True or (fused in ("fwd", "dgrad") and MODE in ("fused", "dgrad", "fwd"))
-              or (fused == "plain_fwd" and MODE == "fwd"))
+              or (fused == "plain_fwd" and (MODE == "fwd" or (MODE == "fused" and k <= PLAIN_FWD_MAX_K))))
         if not ok:
             return False
     if any(t.dtype != torch.bfloat16 for t in tensors) or not _aligned(*tensors):
