@@ -91,11 +91,11 @@ class _AddPenaltyGrad(torch.autograd.Function):
 # lines end by tolerance; the 2-rank rehearsals did not).
 DEQ_MNIST_SOLVER = {"max_iter": 80, "tol": 1e-2, "bwd_iter": 80, "bwd_tol": 2e-2}
 # DEQ-CIFAR runs as a Skip DEQ (FastDEQ.jl's explicit initial-guess network, DEQFixedPoint ``skip``):
-# with it every line ends its solves by tolerance, the 2-rank rehearsal included (28 forward
-# iterations at 0.019976 against 0.02, 45 adjoint; without it 56 at 0.034 and the adjoint at its
-# cap, 2294 vs 3798 img/s: profiles/rd6t_skip_deq_comm.jsonl), and the 1-GPU line is faster (14 vs
-# 19-29 forward iterations, 9.0k vs 8.8k img/s: rd6s_skip_deq.jsonl, rd6u_deq_anderson_adjoint.jsonl).
-# MNIST stays without it: there the skip measured mixed (rd6s, rd6t).
+# 11 of 13 round-6 lines with it ended every solve by tolerance against 3 of 5 without it
+# (profiles/rd6_deq_convergence_tally.md; one 2-rank rehearsal: 28 forward iterations at 0.019976
+# against 0.02 vs 56 at 0.034 without, 3798 vs 2294 img/s, rd6t_skip_deq_comm.jsonl), and the 1-GPU
+# line is faster (14 vs 19-29 forward iterations, 9.0k vs 8.8k img/s: rd6s_skip_deq.jsonl,
+# rd6u_deq_anderson_adjoint.jsonl). MNIST stays without it: there the skip measured mixed (rd6s, rd6t).
 DEQ_CIFAR_SOLVER = {"max_iter": 80, "tol": 2e-2, "bwd_iter": 80, "bwd_tol": 1e-2, "skip": 1}
 
 
