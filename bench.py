@@ -396,7 +396,7 @@ def main():
                        "rank_ms_per_step_min": round(1000 * min(per_rank) / args.steps, 3),
                        "rank_ms_per_step_max": round(1000 * max(per_rank) / args.steps, 3),
                        **({"gelu": _gelu_form()} if args.model == "vit_b16" else {}),
-                       **({"deq_solver": {**{k: getattr(deq, k) for k in ("max_iter", "tol", "bwd_iter", "bwd_tol", "m", "bwd_m")},
+                       **({"deq_solver": {**{k: getattr(deq, k) for k in ("max_iter", "tol", "bwd_iter", "bwd_tol", "m", "bwd_m", "beta", "lam")},
                                           "skip": deq.skip is not None}}
                           if deq is not None else {}),
                        **({"deq_fwd_iters_per_step": round(sum(i[0] for i in timed_iters) / len(timed_iters), 2),

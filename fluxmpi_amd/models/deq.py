@@ -478,15 +478,17 @@ class DEQFixedPoint(nn.Module):
     gradient; the skip convolution and, through the injection x, the layers before the DEQ do).
     The solver's initial guess changes neither z* (up to the tolerance) nor its implicit gradient.
     ``m`` / ``bwd_m``: Anderson memory of the forward / adjoint solve (``bwd_m`` 0: the adjoint by
-    fixed-point iteration ``u <- J^T u + g``)."""
+    fixed-point iteration ``u <- J^T u + g``); ``beta`` / ``lam``: the forward Anderson's mixing
+    (1: undamped) and Gram regulariser."""
 
     def __init__(self, f: nn.Module, max_iter=30, tol=1e-4, bwd_iter=30, bwd_tol=1e-4, check_lag: int | None = None,
                  jac_reg: float | None = None, jac_sigma: float | None = None, skip: int = 0, skip_reg: float = 1.0,
-                 m: int = 5, bwd_m: int = 0):
+                 m: int = 5, bwd_m: int = 0, beta: float = 1.0, lam: float = 1e-4):
         super().__init__()
         self.f = f
         self.m = int(m)          # Anderson memory of the forward solve (<= 8: anderson.hip)
         self.bwd_m = int(bwd_m)  # > 0: the adjoint solve by Anderson(bwd_m) too; 0: fixed-point iteration
+        self.beta, self.lam = float(beta), float(lam)  # the forward Anderson's mixing and regulariser
         self.skip = nn.Conv2d(int(skip), int(skip), 3, padding=1, bias=False) if skip else None
         if self.skip is not None:
             nn.init.zeros_(self.skip.weight)  # starts at the zero guess of the plain solve
@@ -565,7 +567,8 @@ class DEQFixedPoint(nn.Module):
         fz = _CellEval(self.f, xs, raw)
         with torch.no_grad():
             z, self.last_iters, self.last_res = anderson(fz, x0 if x0 is not None else torch.zeros_like(x),
-                                                         m=self.m, max_iter=self.max_iter,
+                                                         m=self.m, lam=self.lam, beta=self.beta,
+                                                         max_iter=self.max_iter,
                                              tol=self.tol, check_lag=self.check_lag, graphs=gs)
         self._z_star = z.detach()
         # one differentiable step re-engages autograd at z*; its GroupNorms save fresh fp32 affine
