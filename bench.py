@@ -249,7 +249,7 @@ def main():
     solver = {}
     for kv in filter(None, args.deq_solver.split(",")):
         k, v = kv.split("=")
-        solver[k.strip()] = int(v) if k.strip() in ("max_iter", "bwd_iter", "check_lag", "m", "bwd_m", "skip") else float(v)
+        solver[k.strip()] = int(v) if k.strip() in ("max_iter", "bwd_iter", "check_lag", "m", "bwd_m", "skip", "restart") else float(v)
     model = build_model(args.model, conv_impl=args.conv, norm=args.norm, **solver)
     memfmt = {"channels_last": torch.channels_last, "contiguous": torch.contiguous_format}.get(
         args.memory_format, getattr(model, "memory_format", torch.channels_last))
@@ -396,7 +396,7 @@ def main():
                        "rank_ms_per_step_min": round(1000 * min(per_rank) / args.steps, 3),
                        "rank_ms_per_step_max": round(1000 * max(per_rank) / args.steps, 3),
                        **({"gelu": _gelu_form()} if args.model == "vit_b16" else {}),
-                       **({"deq_solver": {**{k: getattr(deq, k) for k in ("max_iter", "tol", "bwd_iter", "bwd_tol", "m", "bwd_m", "beta", "lam")},
+                       **({"deq_solver": {**{k: getattr(deq, k) for k in ("max_iter", "tol", "bwd_iter", "bwd_tol", "m", "bwd_m", "beta", "lam", "restart")},
                                           "skip": deq.skip is not None}}
                           if deq is not None else {}),
                        **({"deq_fwd_iters_per_step": round(sum(i[0] for i in timed_iters) / len(timed_iters), 2),

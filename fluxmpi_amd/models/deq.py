@@ -152,7 +152,7 @@ def _x_hist_dtype(dt: torch.dtype, like: torch.Tensor) -> torch.dtype:
 
 
 def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0, check_lag: int | None = None,
-             graphs: "SolverGraphs | None" = None):
+             graphs: "SolverGraphs | None" = None, restart: int = 0):
     """Anderson acceleration for ``x = f(x)`` over batch-flattened tensors. Returns (x, iters, rel_residual).
 
     The history Gram matrix and the mix run as single-pass HIP kernels on the GPU
@@ -168,6 +168,12 @@ def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0, check_lag: i
     the iteration is periodic (k >= m: slot k % m, all m rows in the Gram), whole periods of m
     iterations replay one captured HIP graph; the test then runs per period on the period's
     smallest residual (read back one period late).
+
+    ``restart`` (> 0): restart the history from the newest iterate when the last ``restart``
+    residual tests (periods with graphs, iterations without) improved on the best before them by
+    less than 10 % — Anderson on a slowly contracting, non-normal map can stall with a history
+    whose least-squares problem no longer finds a descent direction. The iteration count and the
+    cap include every restart's iterations.
     """
     from ..ops import anderson as AO
 
@@ -225,22 +231,47 @@ def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0, check_lag: i
         fx_into(AO.mix(X, Fv, alpha, k % m, beta, dt), k % m)
 
     res = float("inf")
-    k, converged = 2, False
-    while k < max_iter:
-        if graphs is not None and k >= max(m, 3) and k % m == 0 and k + m <= max_iter:
+    # k: iterations of the current history segment (slot arithmetic); base: iterations of the
+    # segments before the last restart (k + base counts every f evaluation)
+    k, base, converged = 2, 0, False
+    tests: list = []  # residual tests read back since the last restart (floats)
+
+    def stalled() -> bool:
+        if restart <= 0 or len(tests) < restart + 2:
+            return False
+        return min(tests[-restart:]) > 0.9 * min(tests[:-restart])
+
+    def restart_from_newest() -> None:
+        nonlocal k, base
+        s_new = (k - 1) % m  # newest iterate and its image: the new segment's first pair
+        if s_new != 0:
+            X[:, 0] = X[:, s_new]
+            Fv[:, 0] = Fv[:, s_new]
+        X[:, 1] = Fv[:, 0]
+        fx_into(Fv[:, 0], 1)
+        base += k - 1
+        k = 2
+        tests.clear()
+
+    while base + k < max_iter:
+        if graphs is not None and k >= max(m, 3) and k % m == 0 and base + k + m <= max_iter:
             # iterations k .. k + m - 1 in one replay; iterate k - 1 + m is then complete
             rmin = graphs.anderson_period(k, m, solve_step, mix_step)
             k += m
             if flags is None:
                 res = float(rmin)
                 converged = res < tol
+                tests.append(res)
             else:
-                flags.push(k - 1, rmin)
+                flags.push(base + k - 1, rmin)
                 while not converged and (hit := flags.pop_ready(lag=1)) is not None:
                     res, converged = hit[1], hit[1] < tol
+                    tests.append(res)
             if converged:
                 k -= 1
                 break
+            if stalled() and base + k + 1 < max_iter:
+                restart_from_newest()
             continue
         alpha, res_t = solve_step(k)
         if k > 2:  # residual of the iterate produced by the previous iteration
@@ -249,21 +280,26 @@ def anderson(f, x0, m=5, lam=1e-4, max_iter=30, tol=1e-4, beta=1.0, check_lag: i
                 if res < tol:
                     k, converged = k - 1, True
                     break
+                tests.append(res)
             else:
-                flags.push(k, res_t)
+                flags.push(base + k, res_t)
                 hit = flags.pop_ready()
                 if hit is not None and hit[1] < tol:
                     # iterate hit[0] - 1 converged; the newest one (iteration k - 1) is at least as good
                     res, k, converged = hit[1], k - 1, True
                     break
+                if hit is not None:
+                    tests.append(hit[1])
         mix_step(k, alpha)
         k += 1
+        if stalled() and base + k + 1 < max_iter:
+            restart_from_newest()
     if not converged:
         k = max(k - 1, 1)  # the last completed iteration
         s = k % m
         res_t = (Fv[:, s].float() - X[:, s].float()).norm() / (1e-5 + Fv[:, s].float().norm())
         res = res_t if flags is not None else float(res_t)
-    return unflat(X[:, k % m].contiguous()).to(dt), k, res
+    return unflat(X[:, k % m].contiguous()).to(dt), base + k, res
 
 
 class _CellEval:
@@ -479,16 +515,17 @@ class DEQFixedPoint(nn.Module):
     The solver's initial guess changes neither z* (up to the tolerance) nor its implicit gradient.
     ``m`` / ``bwd_m``: Anderson memory of the forward / adjoint solve (``bwd_m`` 0: the adjoint by
     fixed-point iteration ``u <- J^T u + g``); ``beta`` / ``lam``: the forward Anderson's mixing
-    (1: undamped) and Gram regulariser."""
+    (1: undamped) and Gram regulariser; ``restart``: see :func:`anderson`."""
 
     def __init__(self, f: nn.Module, max_iter=30, tol=1e-4, bwd_iter=30, bwd_tol=1e-4, check_lag: int | None = None,
                  jac_reg: float | None = None, jac_sigma: float | None = None, skip: int = 0, skip_reg: float = 1.0,
-                 m: int = 5, bwd_m: int = 0, beta: float = 1.0, lam: float = 1e-4):
+                 m: int = 5, bwd_m: int = 0, beta: float = 1.0, lam: float = 1e-4, restart: int = 0):
         super().__init__()
         self.f = f
         self.m = int(m)          # Anderson memory of the forward solve (<= 8: anderson.hip)
         self.bwd_m = int(bwd_m)  # > 0: the adjoint solve by Anderson(bwd_m) too; 0: fixed-point iteration
         self.beta, self.lam = float(beta), float(lam)  # the forward Anderson's mixing and regulariser
+        self.restart = int(restart)  # > 0: the forward solve restarts its history on a stall (anderson)
         self.skip = nn.Conv2d(int(skip), int(skip), 3, padding=1, bias=False) if skip else None
         if self.skip is not None:
             nn.init.zeros_(self.skip.weight)  # starts at the zero guess of the plain solve
@@ -568,7 +605,7 @@ class DEQFixedPoint(nn.Module):
         with torch.no_grad():
             z, self.last_iters, self.last_res = anderson(fz, x0 if x0 is not None else torch.zeros_like(x),
                                                          m=self.m, lam=self.lam, beta=self.beta,
-                                                         max_iter=self.max_iter,
+                                                         restart=self.restart, max_iter=self.max_iter,
                                              tol=self.tol, check_lag=self.check_lag, graphs=gs)
         self._z_star = z.detach()
         # one differentiable step re-engages autograd at z*; its GroupNorms save fresh fp32 affine

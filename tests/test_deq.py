@@ -833,3 +833,35 @@ def test_anderson_adjoint_matches_fixed_point_adjoint_cpu(bwd_m):
     err = sum((got[k] - ref[k]).square().sum() for k in ref).sqrt() / sum(ref[k].square().sum() for k in ref).sqrt()
     assert float(err) < 5e-3, float(err)
     assert iters[1] * 3 < iters[0], iters
+
+
+def test_anderson_restart_same_fixed_point_cpu():
+    """anderson(restart=r): a history restart from the newest iterate on a stall keeps the fixed
+    point and the iteration accounting (every segment's evaluations count against max_iter)."""
+    torch.manual_seed(0)
+    d = 64
+    A = torch.randn(4, d, d) / d ** 0.5
+    A = 0.97 * A / torch.linalg.matrix_norm(A, ord=2).view(-1, 1, 1)  # slowly contracting
+    b = torch.randn(4, d)
+    calls = []
+
+    def f(z):
+        calls.append(1)
+        return torch.einsum("bij,bj->bi", A, z) + b
+
+    ref = torch.linalg.solve(torch.eye(d) - A, b)
+    for r in (0, 1, 2):
+        calls.clear()
+        z, it, res = anderson(f, torch.zeros(4, d), m=3, max_iter=200, tol=1e-6, restart=r)
+        torch.testing.assert_close(z, ref, rtol=1e-4, atol=1e-4)
+        assert it <= 200 and len(calls) == it + 1, (r, it, len(calls))
+    # a map without a fixed point (residual ~ 1 / k): the stall test fires, the restarted solve
+    # takes a different path, and the evaluations still match the reported count
+    outs = []
+    for r in (0, 1):
+        calls.clear()
+        z, it, res = anderson(lambda v: (calls.append(1), v + 1.0)[1], torch.zeros(2, 16), m=3, max_iter=40,
+                              tol=0.0, restart=r)
+        assert it == 39 and len(calls) == 40, (r, it, len(calls))
+        outs.append(float(res))
+    assert outs[0] != outs[1], outs
