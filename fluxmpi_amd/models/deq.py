@@ -89,7 +89,11 @@ class _AddPenaltyGrad(torch.autograd.Function):
 # 1e-2 in rd6q, a DEQ-CIFAR one at 0.024 in rd6m): an easy step still stops at its tolerance, so the
 # cap only costs time on the steps that need it (profiles/rd6r_bench_deq_caps80.jsonl: all four 1-GPU
 # lines end by tolerance; the 2-rank rehearsals did not).
-DEQ_MNIST_SOLVER = {"max_iter": 80, "tol": 1e-2, "bwd_iter": 80, "bwd_tol": 2e-2}
+# MNIST restarts its Anderson history when two period tests in a row improve on the best by < 10 %
+# (anderson(restart=2)): the trained cell's solves stall near a 1e-2 residual, and with restarts 5 of
+# 9 lines met every condition against 1 of 9 without, 28.5k vs 24.9k img/s mean (interleaved, one box:
+# profiles/rd6ae_deq_restart.jsonl).
+DEQ_MNIST_SOLVER = {"max_iter": 80, "tol": 1e-2, "bwd_iter": 80, "bwd_tol": 2e-2, "restart": 2}
 # DEQ-CIFAR runs as a Skip DEQ (FastDEQ.jl's explicit initial-guess network, DEQFixedPoint ``skip``):
 # 11 of 13 round-6 lines with it ended every solve by tolerance against 3 of 5 without it
 # (profiles/rd6_deq_convergence_tally.md; one 2-rank rehearsal: 28 forward iterations at 0.019976

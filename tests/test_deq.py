@@ -360,7 +360,7 @@ def test_deq_lagged_matches_sync():
     torch.backends.cudnn.deterministic = True  # MIOpen's default solvers vary run to run
     torch.manual_seed(0)
     # tight tolerances: both solves converge, so the lagged run's extra iterations change little
-    kw = dict(max_iter=80, tol=1e-6, bwd_iter=80, bwd_tol=1e-6)
+    kw = dict(max_iter=80, tol=1e-6, bwd_iter=80, bwd_tol=1e-6, restart=0)  # restarts depend on when a test is read
     m0 = deq_mnist(check_lag=0, **kw).cuda()
     m2 = deq_mnist(check_lag=2, **kw).cuda()
     m2.load_state_dict(m0.state_dict())
@@ -438,6 +438,7 @@ def test_deq_train_step_manual_vjp_gpu(gpu_ext, monkeypatch):
 
 
 def _deq_bf16(**kw):
+    kw.setdefault("restart", 0)  # exact eager / graphed comparisons: no stall-dependent restarts
     m = deq_mnist(**kw).cuda().to(memory_format=torch.channels_last)
     for mod in m.modules():
         if type(mod).__name__ not in ("FusedBatchNorm2d",):
