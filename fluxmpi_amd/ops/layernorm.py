@@ -49,6 +49,17 @@ def _const(d: int, device, value: float) -> torch.Tensor:
     return t
 
 
+def _zero(device, dtype) -> torch.Tensor:
+    """A cached 0-d zero (expanded into the never-read placeholder gradient of a linked GELU output:
+    a fresh ``torch.zeros(())`` launched one fill kernel per block per step)."""
+    key = ("zero", str(device), dtype)
+    t = _AFFINE.get(key)
+    if t is None:
+        t = torch.zeros((), device=device, dtype=dtype)
+        _AFFINE[key] = t
+    return t
+
+
 def _affine(x, weight, bias):
     """The (w, b) the kernels read: the parameters themselves when both are present in the
     activation dtype (the kernels convert on load), else fp32 copies / cached ones-zeros."""
@@ -199,7 +210,7 @@ class _LinearAddLayerNormFn(torch.autograd.Function):
                 # gradient come out of this input-gradient GEMM's epilogue (gemm_nt.hip EPI 2)
                 link.dh, link.db = gemm_nt.linear_dgrad(g2, weight, gelu_d=link.h, bias_dtype=link.bias_dtype,
                                                         bias_param=link.bias)
-                da = torch.zeros((), device=a.device, dtype=a.dtype).expand(a.shape)  # placeholder, never read
+                da = _zero(a.device, a.dtype).expand(a.shape)  # placeholder, never read
             elif ctx.needs_input_grad[1] and native_ok(a2, g2) and linbwd_ok(g2, a2, weight):
                 # input and weight gradient in one launch (linbwd.hip)
                 with graddst.into(ctx.weight):
