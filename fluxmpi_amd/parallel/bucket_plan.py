@@ -115,28 +115,34 @@ def choose(model: CommModel, total_bytes: int | None = None, max_buckets: int = 
 
 
 def probe(comm, device: torch.device, dtype: torch.dtype = torch.bfloat16, sizes=LADDER, iters: int = 5,
-          warmup: int = 2, cpu_comm=None) -> list[tuple[int, float]]:
+          warmup: int = 2, cpu_comm=None, passes: int = 2) -> list[tuple[int, float]]:
     """Time ``comm.allreduce`` over the ``sizes`` ladder (bytes) of ``dtype``; returns
     ``[(bytes, us)]`` with each time the MAXIMUM over ranks (identical on every rank). Host wall
     time around ``iters`` back-to-back collectives, the device synchronised at both ends (the
-    collective's own stream included)."""
+    collective's own stream included); the ladder runs ``passes`` times and each size keeps its
+    fastest pass (a rank arriving late at the first timed size inflated it ~6x in the gloo
+    rehearsals, profiles/rd6ai_rehearsals.jsonl)."""
     esz = torch.empty((), dtype=dtype).element_size()
     buf = torch.zeros(max(sizes) // esz, dtype=dtype, device=device)
     cuda = device.type == "cuda"
-    out = []
-    for nb in sizes:
-        t = buf[: max(1, nb // esz)]
-        for _ in range(warmup):
-            comm.allreduce(t)
-        if cuda:
-            torch.cuda.synchronize(device)
-        comm.barrier()
-        t0 = time.perf_counter()
-        for _ in range(iters):
-            comm.allreduce(t)
-        if cuda:
-            torch.cuda.synchronize(device)
-        out.append((t.numel() * esz, (time.perf_counter() - t0) / iters * 1e6))
+    best: dict = {}
+    for _ in range(max(1, passes)):
+        for nb in sizes:
+            t = buf[: max(1, nb // esz)]
+            for _ in range(warmup):
+                comm.allreduce(t)
+            if cuda:
+                torch.cuda.synchronize(device)
+            comm.barrier()
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                comm.allreduce(t)
+            if cuda:
+                torch.cuda.synchronize(device)
+            us = (time.perf_counter() - t0) / iters * 1e6
+            key = t.numel() * esz
+            best[key] = min(us, best.get(key, float("inf")))
+    out = list(best.items())
     del buf
     times = torch.tensor([us for _, us in out], dtype=torch.float64)
     if cpu_comm is not None and cpu_comm.size > 1:
