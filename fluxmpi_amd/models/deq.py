@@ -95,7 +95,7 @@ class _AddPenaltyGrad(torch.autograd.Function):
 # profiles/rd6ae_deq_restart.jsonl).
 DEQ_MNIST_SOLVER = {"max_iter": 80, "tol": 1e-2, "bwd_iter": 80, "bwd_tol": 2e-2, "restart": 2}
 # DEQ-CIFAR runs as a Skip DEQ (FastDEQ.jl's explicit initial-guess network, DEQFixedPoint ``skip``):
-# 13 of 17 round-6 lines with it ended every solve by tolerance against 3 of 5 without it
+# 13 of 18 round-6 lines with it ended every solve by tolerance against 3 of 5 without it
 # (profiles/rd6_deq_convergence_tally.md; one 2-rank rehearsal: 28 forward iterations at 0.019976
 # against 0.02 vs 56 at 0.034 without, 3798 vs 2294 img/s, rd6t_skip_deq_comm.jsonl), and the 1-GPU
 # line is faster (14 vs 19-29 forward iterations, 9.0k vs 8.8k img/s: rd6s_skip_deq.jsonl,
