@@ -249,7 +249,7 @@ def main():
     solver = {}
     for kv in filter(None, args.deq_solver.split(",")):
         k, v = kv.split("=")
-        solver[k.strip()] = int(v) if k.strip() in ("max_iter", "bwd_iter", "check_lag", "m", "bwd_m", "skip", "restart") else float(v)
+        solver[k.strip()] = int(v) if k.strip() in ("max_iter", "bwd_iter", "check_lag", "m", "bwd_m", "skip", "restart", "skip_detach") else float(v)
     model = build_model(args.model, conv_impl=args.conv, norm=args.norm, **solver)
     memfmt = {"channels_last": torch.channels_last, "contiguous": torch.contiguous_format}.get(
         args.memory_format, getattr(model, "memory_format", torch.channels_last))

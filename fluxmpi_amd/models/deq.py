@@ -523,7 +523,8 @@ class DEQFixedPoint(nn.Module):
 
     def __init__(self, f: nn.Module, max_iter=30, tol=1e-4, bwd_iter=30, bwd_tol=1e-4, check_lag: int | None = None,
                  jac_reg: float | None = None, jac_sigma: float | None = None, skip: int = 0, skip_reg: float = 1.0,
-                 m: int = 5, bwd_m: int = 0, beta: float = 1.0, lam: float = 1e-4, restart: int = 0):
+                 m: int = 5, bwd_m: int = 0, beta: float = 1.0, lam: float = 1e-4, restart: int = 0,
+                 skip_detach: int = 0):
         super().__init__()
         self.f = f
         self.m = int(m)          # Anderson memory of the forward solve (<= 8: anderson.hip)
@@ -534,6 +535,7 @@ class DEQFixedPoint(nn.Module):
         if self.skip is not None:
             nn.init.zeros_(self.skip.weight)  # starts at the zero guess of the plain solve
         self.skip_reg = float(skip_reg)
+        self.skip_detach = bool(skip_detach)  # the skip convolution reads a detached injection
         self.last_skip_res = None  # the last training step's ||skip(x) - z*|| / ||z*|| (0-d device tensor)
         env = [float(v) for v in JAC_REG.split(",")] if JAC_REG else []
         self.jac_reg = float(jac_reg if jac_reg is not None else (env[0] if env else 0.0))
@@ -570,7 +572,8 @@ class DEQFixedPoint(nn.Module):
         # graphs' static buffers when the solver loops replay graphs)
         z_pred = None
         if self.skip is not None:  # bf16 channels_last on the GPU: our implicit-GEMM 3x3 kernels
-            z_pred = conv3x3(x, self.skip.weight) if conv3x3_supported(x, self.skip) else self.skip(x)
+            xs = x.detach() if self.skip_detach else x  # skip_detach: the auxiliary loss stops at the skip
+            z_pred = conv3x3(xs, self.skip.weight) if conv3x3_supported(xs, self.skip) else self.skip(xs)
         x0 = z_pred.detach().contiguous(memory_format=torch.channels_last) if z_pred is not None and \
             x.is_contiguous(memory_format=torch.channels_last) else (z_pred.detach() if z_pred is not None else None)
         with fp32_affine_cache(self.f, buffers=gs.aff if gs is not None else None):

@@ -38,7 +38,7 @@ def main():
     solver = {}
     for kv in filter(None, a.solver.split(",")):
         k, v = kv.split("=")
-        solver[k.strip()] = int(v) if k.strip() in ("max_iter", "bwd_iter", "check_lag", "m", "bwd_m", "skip", "restart") else float(v)
+        solver[k.strip()] = int(v) if k.strip() in ("max_iter", "bwd_iter", "check_lag", "m", "bwd_m", "skip", "restart", "skip_detach") else float(v)
     model = build_model(a.model, **solver).to(dev, memory_format=torch.channels_last)
     for m in model.modules():
         if not (isinstance(m, torch.nn.modules.batchnorm._BatchNorm) or type(m).__name__ == "FusedBatchNorm2d"):
