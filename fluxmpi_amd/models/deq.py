@@ -517,6 +517,8 @@ class DEQFixedPoint(nn.Module):
     loss ``skip_reg * ||skip(x) - z*||^2 / ||z*||^2`` (z* a constant: the cell gets none of its
     gradient; the skip convolution and, through the injection x, the layers before the DEQ do).
     The solver's initial guess changes neither z* (up to the tolerance) nor its implicit gradient.
+    ``skip_detach``: the skip convolution reads a detached injection (measured less stable:
+    profiles/rd6ak_deq_skip_detach.jsonl).
     ``m`` / ``bwd_m``: Anderson memory of the forward / adjoint solve (``bwd_m`` 0: the adjoint by
     fixed-point iteration ``u <- J^T u + g``); ``beta`` / ``lam``: the forward Anderson's mixing
     (1: undamped) and Gram regulariser; ``restart``: see :func:`anderson`."""
