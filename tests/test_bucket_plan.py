@@ -95,3 +95,31 @@ def worker_measured_plan():
 
 def test_measured_plan_gloo(spmd):
     spmd("tests.test_bucket_plan:worker_measured_plan", timeout=180)
+
+
+def test_probe_keeps_the_fastest_pass():
+    """probe(): every ladder size keeps its fastest pass — a slow first pass (a rank arriving late at
+    the first timed size, connection setup) does not reach the fit."""
+    import time
+
+    from fluxmpi_amd.parallel.bucket_plan import probe
+
+    class SlowFirstPass:
+        size = 1
+
+        def __init__(self):
+            self.calls = 0
+
+        def allreduce(self, t):
+            self.calls += 1
+            # 2 warm-up + 3 timed calls per size and pass; the first pass's timed calls are slow
+            if self.calls <= 2 * 5 and (self.calls - 1) % 5 >= 2:
+                time.sleep(0.02)
+
+        def barrier(self):
+            pass
+
+    sizes = (1 << 10, 1 << 12)
+    out = probe(SlowFirstPass(), torch.device("cpu"), torch.float32, sizes=sizes, iters=3, warmup=2, passes=2)
+    assert [n for n, _ in out] == list(sizes)
+    assert all(us < 10_000 for _, us in out), out  # the 20 ms first-pass calls were dropped
